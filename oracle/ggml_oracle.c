@@ -1,0 +1,545 @@
+/*
+ * ggml_oracle.c -- TEST INFRASTRUCTURE ONLY (see ggml_oracle.h).
+ *
+ * Plain-C restatement of the reference CPU ggml semantics on the Llama
+ * token-generation path.  Each function cites the reference file:line it follows.
+ * Never linked into the product library; imported only by tests/, smoke() and the
+ * cpu_baseline leg of bench.py.
+ */
+#include "ggml_oracle.h"
+#include "../include/kcpp_synth.h"
+
+#include <immintrin.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <omp.h>
+
+#define QK_K 256
+
+typedef struct { uint16_t d; uint8_t qs[16]; } blk_q4_0;                  /* ggml-common.h:144 */
+typedef struct { uint16_t d; int8_t qs[32]; } blk_q8_0;                   /* ggml-common.h:186 */
+typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qs[128]; } blk_q4_K;   /* :286 */
+typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qh[32]; uint8_t qs[128]; } blk_q5_K; /* :303 */
+typedef struct { uint8_t ql[128]; uint8_t qh[64]; int8_t scales[16]; uint16_t d; } blk_q6_K;       /* :321 */
+typedef struct { float d; int8_t qs[256]; int16_t bsums[16]; } blk_q8_K;  /* :330 */
+
+_Static_assert(sizeof(blk_q4_0) == 18, "q4_0");
+_Static_assert(sizeof(blk_q8_0) == 34, "q8_0");
+_Static_assert(sizeof(blk_q4_K) == 144, "q4_K");
+_Static_assert(sizeof(blk_q5_K) == 176, "q5_K");
+_Static_assert(sizeof(blk_q6_K) == 210, "q6_K");
+_Static_assert(sizeof(blk_q8_K) == 292, "q8_K");
+
+float orc_fp16_to_fp32(uint16_t h) { return _cvtsh_ss(h); }
+uint16_t orc_fp32_to_fp16(float f) { return _cvtss_sh(f, 0); }
+#define H2F orc_fp16_to_fp32
+#define F2H orc_fp32_to_fp16
+
+/* get_scale_min_k4, ggml-quants.c:1899-1906 */
+static inline void scale_min_k4(int j, const uint8_t *q, uint8_t *d, uint8_t *m) {
+    if (j < 4) { *d = q[j] & 63; *m = q[j + 4] & 63; }
+    else {
+        *d = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+        *m = (q[j + 4] >> 4) | ((q[j - 0] >> 6) << 4);
+    }
+}
+
+int64_t orc_row_bytes(int type, int64_t k) {
+    return k / ks_block_elems(type) * ks_block_bytes(type);
+}
+
+void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
+    switch (type) {
+    case KT_F32: memcpy(y, vx, k * 4); return;
+    case KT_F16: { const uint16_t *x = vx; for (int64_t i = 0; i < k; ++i) y[i] = H2F(x[i]); } return;
+    case KT_Q4_0: {                                   /* ggml-quants.c:1523-1540 */
+        const blk_q4_0 *x = vx;
+        for (int64_t i = 0; i < k / 32; ++i) {
+            const float d = H2F(x[i].d);
+            for (int j = 0; j < 16; ++j) {
+                y[i * 32 + j] = ((x[i].qs[j] & 0x0F) - 8) * d;
+                y[i * 32 + j + 16] = ((x[i].qs[j] >> 4) - 8) * d;
+            }
+        }
+    } return;
+    case KT_Q8_0: {                                   /* ggml-quants.c:1617-1631 */
+        const blk_q8_0 *x = vx;
+        for (int64_t i = 0; i < k / 32; ++i) {
+            const float d = H2F(x[i].d);
+            for (int j = 0; j < 32; ++j) y[i * 32 + j] = x[i].qs[j] * d;
+        }
+    } return;
+    case KT_Q4_K: {                                   /* ggml-quants.c:2556-2578 */
+        const blk_q4_K *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const uint8_t *q = x[i].qs;
+            const float d = H2F(x[i].d), min = H2F(x[i].dmin);
+            int is = 0; uint8_t sc, m;
+            for (int j = 0; j < QK_K; j += 64) {
+                scale_min_k4(is + 0, x[i].scales, &sc, &m);
+                const float d1 = d * sc, m1 = min * m;
+                scale_min_k4(is + 1, x[i].scales, &sc, &m);
+                const float d2 = d * sc, m2 = min * m;
+                for (int l = 0; l < 32; ++l) *y++ = d1 * (q[l] & 0xF) - m1;
+                for (int l = 0; l < 32; ++l) *y++ = d2 * (q[l] >> 4) - m2;
+                q += 32; is += 2;
+            }
+        }
+    } return;
+    case KT_Q5_K: {                                   /* ggml-quants.c:2764-2790 */
+        const blk_q5_K *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const uint8_t *ql = x[i].qs, *qh = x[i].qh;
+            const float d = H2F(x[i].d), min = H2F(x[i].dmin);
+            int is = 0; uint8_t sc, m, u1 = 1, u2 = 2;
+            for (int j = 0; j < QK_K; j += 64) {
+                scale_min_k4(is + 0, x[i].scales, &sc, &m);
+                const float d1 = d * sc, m1 = min * m;
+                scale_min_k4(is + 1, x[i].scales, &sc, &m);
+                const float d2 = d * sc, m2 = min * m;
+                for (int l = 0; l < 32; ++l) *y++ = d1 * ((ql[l] & 0xF) + (qh[l] & u1 ? 16 : 0)) - m1;
+                for (int l = 0; l < 32; ++l) *y++ = d2 * ((ql[l] >> 4) + (qh[l] & u2 ? 16 : 0)) - m2;
+                ql += 32; is += 2; u1 <<= 2; u2 <<= 2;
+            }
+        }
+    } return;
+    case KT_Q6_K: {                                   /* ggml-quants.c:2978-3006 */
+        const blk_q6_K *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const float d = H2F(x[i].d);
+            const uint8_t *ql = x[i].ql, *qh = x[i].qh;
+            const int8_t *sc = x[i].scales;
+            for (int n = 0; n < QK_K; n += 128) {
+                for (int l = 0; l < 32; ++l) {
+                    int is = l / 16;
+                    const int8_t q1 = (int8_t)((ql[l + 0] & 0xF) | (((qh[l] >> 0) & 3) << 4)) - 32;
+                    const int8_t q2 = (int8_t)((ql[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4)) - 32;
+                    const int8_t q3 = (int8_t)((ql[l + 0] >> 4) | (((qh[l] >> 4) & 3) << 4)) - 32;
+                    const int8_t q4 = (int8_t)((ql[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4)) - 32;
+                    y[l + 0] = d * sc[is + 0] * q1;
+                    y[l + 32] = d * sc[is + 2] * q2;
+                    y[l + 64] = d * sc[is + 4] * q3;
+                    y[l + 96] = d * sc[is + 6] * q4;
+                }
+                y += 128; ql += 64; qh += 32; sc += 8;
+            }
+        }
+    } return;
+    default: abort();
+    }
+}
+
+/* type_traits[..].vec_dot_type, ggml.c:793-959 */
+int orc_vec_dot_type(int wtype) {
+    switch (wtype) {
+        case KT_Q4_0: case KT_Q8_0: return KT_Q8_0;
+        case KT_Q4_K: case KT_Q5_K: case KT_Q6_K: return KT_Q8_K;
+        case KT_F16: return KT_F16;
+        default: return KT_F32;
+    }
+}
+
+/* nearest_int, ggml-quants.c:1640-1645 */
+static inline int nearest_int(float fval) {
+    float val = fval + 12582912.f;
+    int i; memcpy(&i, &val, sizeof(int));
+    return (i & 0x007fffff) - 0x00400000;
+}
+
+/* quantize_row_q8_K_ref, ggml-quants.c:3786-3823 */
+void orc_quantize_row_q8_K(const float *x, void *vy, int64_t k) {
+    blk_q8_K *y = vy;
+    for (int64_t i = 0; i < k / QK_K; ++i) {
+        float max = 0, amax = 0;
+        for (int j = 0; j < QK_K; ++j) {
+            float ax = fabsf(x[j]);
+            if (ax > amax) { amax = ax; max = x[j]; }
+        }
+        if (!amax) {
+            y[i].d = 0; memset(y[i].qs, 0, QK_K); memset(y[i].bsums, 0, sizeof(y[i].bsums));
+            x += QK_K; continue;
+        }
+        const float iscale = -127.f / max;
+        for (int j = 0; j < QK_K; ++j) {
+            int v = nearest_int(iscale * x[j]);
+            y[i].qs[j] = v < 127 ? v : 127;
+        }
+        for (int j = 0; j < QK_K / 16; ++j) {
+            int sum = 0;
+            for (int ii = 0; ii < 16; ++ii) sum += y[i].qs[j * 16 + ii];
+            y[i].bsums[j] = sum;
+        }
+        y[i].d = 1 / iscale;
+        x += QK_K;
+    }
+}
+
+/* quantize_row_q8_0, AVX2 branch ggml-quants.c:940-1000 */
+void orc_quantize_row_q8_0(const float *x, void *vy, int64_t k) {
+    blk_q8_0 *y = vy;
+    for (int64_t i = 0; i < k / 32; ++i) {
+        float amax = 0;
+        for (int j = 0; j < 32; ++j) { float a = fabsf(x[i * 32 + j]); amax = a > amax ? a : amax; }
+        const float d = amax / 127.f;
+        y[i].d = F2H(d);
+        const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
+        for (int j = 0; j < 32; ++j) {
+            float v = nearbyintf(x[i * 32 + j] * id);   /* _MM_ROUND_NEAREST: half-to-even */
+            int iv = (int)v;
+            y[i].qs[j] = (int8_t)(iv > 127 ? 127 : (iv < -128 ? -128 : iv));
+        }
+    }
+}
+
+void orc_quantize_row(int vtype, const float *x, void *y, int64_t k) {
+    switch (vtype) {
+        case KT_Q8_K: orc_quantize_row_q8_K(x, y, k); break;
+        case KT_Q8_0: orc_quantize_row_q8_0(x, y, k); break;
+        case KT_F16: { uint16_t *h = y; for (int64_t i = 0; i < k; ++i) h[i] = F2H(x[i]); } break;
+        case KT_F32: memcpy(y, x, k * 4); break;
+        default: abort();
+    }
+}
+
+/* ---------------- dot products (scalar restatement of ggml-quants.c) ---------------- */
+
+static float dot_q4_K(int n, const blk_q4_K *x, const blk_q8_K *y) {       /* :7714, scalar :8223 */
+    float sumf = 0;
+    for (int i = 0; i < n / QK_K; ++i) {
+        int sumi = 0, summ = 0;
+        for (int j = 0; j < 8; ++j) {
+            uint8_t sc, m;
+            scale_min_k4(j, x[i].scales, &sc, &m);
+            const uint8_t *q4 = x[i].qs + 32 * (j / 2);
+            const int8_t *q8 = y[i].qs + 32 * j;
+            int dot = 0;
+            for (int l = 0; l < 32; ++l) dot += ((j & 1) ? (q4[l] >> 4) : (q4[l] & 0xF)) * q8[l];
+            sumi += sc * dot;
+            summ += m * (y[i].bsums[2 * j] + y[i].bsums[2 * j + 1]);
+        }
+        const float d = y[i].d * H2F(x[i].d);
+        const float dmin = y[i].d * H2F(x[i].dmin);
+        sumf += d * (float)sumi;
+        sumf -= dmin * (float)summ;
+    }
+    return sumf;
+}
+
+static float dot_q5_K(int n, const blk_q5_K *x, const blk_q8_K *y) {       /* :8282 */
+    float sumf = 0;
+    for (int i = 0; i < n / QK_K; ++i) {
+        int sumi = 0, summ = 0;
+        for (int j = 0; j < 8; ++j) {
+            uint8_t sc, m;
+            scale_min_k4(j, x[i].scales, &sc, &m);
+            const uint8_t *q4 = x[i].qs + 32 * (j / 2);
+            const int8_t *q8 = y[i].qs + 32 * j;
+            int dot = 0;
+            for (int l = 0; l < 32; ++l) {
+                int v = ((j & 1) ? (q4[l] >> 4) : (q4[l] & 0xF)) + ((x[i].qh[l] >> j) & 1) * 16;
+                dot += v * q8[l];
+            }
+            sumi += sc * dot;
+            summ += m * (y[i].bsums[2 * j] + y[i].bsums[2 * j + 1]);
+        }
+        const float d = y[i].d * H2F(x[i].d);
+        const float dmin = y[i].d * H2F(x[i].dmin);
+        sumf += d * (float)sumi;
+        sumf -= dmin * (float)summ;
+    }
+    return sumf;
+}
+
+static float dot_q6_K(int n, const blk_q6_K *x, const blk_q8_K *y) {       /* :8919, scalar ~:9530 */
+    float sumf = 0;
+    for (int i = 0; i < n / QK_K; ++i) {
+        int8_t a[QK_K];
+        const uint8_t *q4 = x[i].ql, *qh = x[i].qh;
+        int8_t *pa = a;
+        for (int j = 0; j < QK_K; j += 128) {
+            for (int l = 0; l < 32; ++l) {
+                pa[l + 0] = (int8_t)((q4[l + 0] & 0xF) | (((qh[l] >> 0) & 3) << 4)) - 32;
+                pa[l + 32] = (int8_t)((q4[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4)) - 32;
+                pa[l + 64] = (int8_t)((q4[l + 0] >> 4) | (((qh[l] >> 4) & 3) << 4)) - 32;
+                pa[l + 96] = (int8_t)((q4[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4)) - 32;
+            }
+            pa += 128; q4 += 64; qh += 32;
+        }
+        int sumi = 0;
+        for (int g = 0; g < 16; ++g) {
+            int dot = 0;
+            for (int l = 0; l < 16; ++l) dot += a[g * 16 + l] * y[i].qs[g * 16 + l];
+            sumi += x[i].scales[g] * dot;
+        }
+        sumf += H2F(x[i].d) * y[i].d * (float)sumi;
+    }
+    return sumf;
+}
+
+static float dot_q4_0(int n, const blk_q4_0 *x, const blk_q8_0 *y) {       /* :3922, scalar tail */
+    float sumf = 0;
+    for (int ib = 0; ib < n / 32; ++ib) {
+        int s0 = 0, s1 = 0;
+        for (int j = 0; j < 16; ++j) {
+            s0 += ((x[ib].qs[j] & 0x0F) - 8) * y[ib].qs[j];
+            s1 += ((x[ib].qs[j] >> 4) - 8) * y[ib].qs[j + 16];
+        }
+        sumf += (s0 + s1) * (H2F(x[ib].d) * H2F(y[ib].d));
+    }
+    return sumf;
+}
+
+static float dot_q8_0(int n, const blk_q8_0 *x, const blk_q8_0 *y) {       /* :5519, scalar tail */
+    float sumf = 0;
+    for (int ib = 0; ib < n / 32; ++ib) {
+        int s = 0;
+        for (int j = 0; j < 32; ++j) s += x[ib].qs[j] * y[ib].qs[j];
+        sumf += s * (H2F(x[ib].d) * H2F(y[ib].d));
+    }
+    return sumf;
+}
+
+static float dot_f16(int n, const uint16_t *x, const uint16_t *y) {        /* ggml.c:2258 */
+    double s = 0;
+    for (int i = 0; i < n; ++i) s += (double)(H2F(x[i]) * H2F(y[i]));
+    return (float)s;
+}
+
+float orc_vec_dot(int wtype, int n, const void *w, const void *a) {
+    switch (wtype) {
+        case KT_Q4_K: return dot_q4_K(n, w, a);
+        case KT_Q5_K: return dot_q5_K(n, w, a);
+        case KT_Q6_K: return dot_q6_K(n, w, a);
+        case KT_Q4_0: return dot_q4_0(n, w, a);
+        case KT_Q8_0: return dot_q8_0(n, w, a);
+        case KT_F16: return dot_f16(n, w, a);
+        case KT_F32: { const float *x = w, *y = a; double s = 0; for (int i = 0; i < n; ++i) s += x[i] * y[i]; return (float)s; }
+        default: abort();
+    }
+}
+
+/* ggml_compute_forward_mul_mat, ggml.c:12486-12707: src1 rows -> vec_dot_type, then row dots */
+void orc_mul_mat(int wtype, const void *W, int64_t K, int64_t N, const float *X, int64_t M,
+                 float *dst, int nthreads) {
+    const int vt = orc_vec_dot_type(wtype);
+    const int64_t abytes = orc_row_bytes(vt, K), wbytes = orc_row_bytes(wtype, K);
+    uint8_t *qa = malloc(abytes * M);
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+    #pragma omp parallel for num_threads(nthreads) schedule(static)
+    for (int64_t m = 0; m < M; ++m) orc_quantize_row(vt, X + m * K, qa + m * abytes, K);
+    const int64_t NB = 16;
+    #pragma omp parallel for num_threads(nthreads) schedule(dynamic, 4) collapse(2)
+    for (int64_t nb = 0; nb < (N + NB - 1) / NB; ++nb)
+        for (int64_t m = 0; m < M; ++m)
+            for (int64_t n = nb * NB; n < (nb + 1) * NB && n < N; ++n)
+                dst[m * N + n] = orc_vec_dot(wtype, (int)K, (const uint8_t *)W + n * wbytes, qa + m * abytes);
+    free(qa);
+}
+
+/* ggml_compute_forward_rms_norm_f32 (ggml.c:12059-12103) then ggml_mul by w */
+void orc_rms_norm(const float *x, const float *w, float *y, int64_t ne0, int64_t nrows, float eps) {
+    for (int64_t r = 0; r < nrows; ++r) {
+        const float *xr = x + r * ne0;
+        float *yr = y + r * ne0;
+        double sum = 0.0;
+        for (int64_t i = 0; i < ne0; ++i) sum += (double)(xr[i] * xr[i]);
+        const float mean = (float)(sum / ne0);
+        const float scale = 1.0f / sqrtf(mean + eps);
+        for (int64_t i = 0; i < ne0; ++i) yr[i] = xr[i] * scale;
+        if (w) for (int64_t i = 0; i < ne0; ++i) yr[i] = yr[i] * w[i];
+    }
+}
+
+/* rope helpers, ggml.c:14216-14270 */
+static float rope_yarn_ramp(const float low, const float high, const int i0) {
+    const float y = (i0 / 2 - low) / fmaxf(0.001f, high - low);
+    return 1 - fminf(1, fmaxf(0, y));
+}
+static float rope_corr_dim(int n_dims, int n_ctx_orig, float n_rot, float base) {
+    return n_dims * logf(n_ctx_orig / (n_rot * 2 * (float)M_PI)) / (2 * logf(base));
+}
+
+void orc_rope(const float *x, float *y, int64_t head_dim, int64_t n_heads, int64_t n_tokens,
+              const int32_t *pos, int n_dims, float freq_base, float freq_scale,
+              const float *freq_factors, float ext_factor, float attn_factor,
+              float beta_fast, float beta_slow, int n_ctx_orig) {
+    const float theta_scale = powf(freq_base, -2.0f / n_dims);
+    float corr[2];
+    {
+        float start = floorf(rope_corr_dim(n_dims, n_ctx_orig, beta_fast, freq_base));
+        float end = ceilf(rope_corr_dim(n_dims, n_ctx_orig, beta_slow, freq_base));
+        corr[0] = fmaxf(0, start); corr[1] = fminf(n_dims - 1, end);
+    }
+    float *cache = malloc(sizeof(float) * head_dim);
+    for (int64_t t = 0; t < n_tokens; ++t) {
+        float theta = (float)pos[t];
+        for (int64_t i0 = 0; i0 < head_dim; i0 += 2) {           /* ggml_rope_cache_init */
+            const float ff = freq_factors ? freq_factors[i0 / 2] : 1.0f;
+            float theta_extrap = theta / ff;
+            float theta_interp = freq_scale * theta_extrap;
+            float th = theta_interp, mscale = attn_factor;
+            if (ext_factor != 0.0f) {
+                float ramp_mix = rope_yarn_ramp(corr[0], corr[1], (int)i0) * ext_factor;
+                th = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
+                mscale *= 1.0f + 0.1f * logf(1.0f / freq_scale);
+            }
+            cache[i0] = cosf(th) * mscale;
+            cache[i0 + 1] = sinf(th) * mscale;
+            theta *= theta_scale;
+        }
+        for (int64_t h = 0; h < n_heads; ++h) {
+            const float *src = x + (t * n_heads + h) * head_dim;
+            float *dst = y + (t * n_heads + h) * head_dim;
+            for (int64_t i0 = 0; i0 < n_dims; i0 += 2) {
+                const float c = cache[i0], s = cache[i0 + 1];
+                const float x0 = src[i0], x1 = src[i0 + 1];
+                dst[i0] = x0 * c - x1 * s;
+                dst[i0 + 1] = x0 * s + x1 * c;
+            }
+            for (int64_t i0 = n_dims; i0 < head_dim; ++i0) dst[i0] = src[i0];
+        }
+    }
+    free(cache);
+}
+
+/* ggml_compute_forward_flash_attn_ext_f16, F16 K/V branch (ggml.c:15667-15875) */
+void orc_flash_attn_ext(const float *q, const uint16_t *k, const uint16_t *v, int64_t kv_stride,
+                        const uint16_t *mask, float *out, int D, int n_q, int n_head,
+                        int n_kv, int n_head_kv, float scale, int nthreads) {
+    const int rk = n_head / n_head_kv;
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+    #pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+    for (int ir = 0; ir < n_q * n_head; ++ir) {
+        const int iq1 = ir / n_head, h = ir % n_head;   /* row order irrelevant */
+        const int hk = h / rk;
+        uint16_t qh[512];
+        uint16_t vkq16[512];
+        float vkq32[512];
+        const float *pq = q + ((int64_t)iq1 * n_head + h) * D;
+        for (int d = 0; d < D; ++d) { qh[d] = F2H(pq[d]); vkq16[d] = 0; }
+        float S = 0.0f, M = -INFINITY;
+        for (int ic = 0; ic < n_kv; ++ic) {
+            const float mv = mask ? H2F(mask[(int64_t)iq1 * n_kv + ic]) : 0.0f;
+            if (mv == -INFINITY) continue;
+            const uint16_t *kr = k + (int64_t)ic * kv_stride + (int64_t)hk * D;
+            float s = dot_f16(D, kr, qh);
+            s = s * scale;
+            s += mv;
+            const float Mold = M;
+            float ms = 1.0f, vs = 1.0f;
+            const uint16_t *vr = v + (int64_t)ic * kv_stride + (int64_t)hk * D;
+            if (s > M) {
+                M = s;
+                ms = expf(Mold - M);
+                for (int d = 0; d < D; ++d) vkq16[d] = F2H(H2F(vkq16[d]) * ms);   /* ggml_vec_scale_f16 */
+            } else {
+                vs = expf(s - M);
+            }
+            for (int d = 0; d < D; ++d) vkq16[d] = F2H(fmaf(H2F(vr[d]), vs, H2F(vkq16[d])));  /* ggml_vec_mad_f16 */
+            S = S * ms + vs;
+        }
+        for (int d = 0; d < D; ++d) vkq32[d] = H2F(vkq16[d]);
+        const float S_inv = 1.0f / S;
+        float *po = out + ((int64_t)iq1 * n_head + h) * D;
+        for (int d = 0; d < D; ++d) po[d] = vkq32[d] * S_inv;
+    }
+}
+
+/* ======================= Llama forward (build_llama) ======================= */
+struct orc_llama {
+    orc_hparams hp;
+    const void *const *w;
+    const int *t;
+    int nthreads;
+    uint16_t *kc, *vc;     /* [n_layer][n_ctx][n_head_kv*D] f16 */
+    float *last_hidden;
+};
+
+orc_llama *orc_llama_create(const orc_hparams *hp, const void *const *data, const int *types, int nthreads) {
+    orc_llama *m = calloc(1, sizeof(*m));
+    m->hp = *hp;
+    int nw = 3 + 9 * hp->n_layer;
+    void **w = malloc(sizeof(void *) * nw);
+    int *t = malloc(sizeof(int) * nw);
+    memcpy(w, data, sizeof(void *) * nw);
+    memcpy(t, types, sizeof(int) * nw);
+    m->w = (const void *const *)w; m->t = t;
+    m->nthreads = nthreads > 0 ? nthreads : omp_get_max_threads();
+    const int64_t D = hp->n_embd / hp->n_head;
+    const int64_t kvsz = (int64_t)hp->n_layer * hp->n_ctx * hp->n_head_kv * D;
+    m->kc = calloc(kvsz, 2);
+    m->vc = calloc(kvsz, 2);
+    m->last_hidden = calloc(hp->n_embd, 4);
+    return m;
+}
+
+void orc_llama_free(orc_llama *m) {
+    if (!m) return;
+    free((void *)m->w); free((void *)m->t); free(m->kc); free(m->vc); free(m->last_hidden); free(m);
+}
+
+void orc_llama_last_hidden(orc_llama *m, float *out) { memcpy(out, m->last_hidden, 4 * m->hp.n_embd); }
+
+static void add_inplace(float *a, const float *b, int64_t n) { for (int64_t i = 0; i < n; ++i) a[i] += b[i]; }
+
+int orc_llama_eval(orc_llama *m, const int32_t *tokens, int T, int n_past, float *logits) {
+    const orc_hparams *hp = &m->hp;
+    const int E = hp->n_embd, H = hp->n_head, HKV = hp->n_head_kv, D = E / H, F = hp->n_ff;
+    const int EKV = HKV * D;
+    const int NT = m->nthreads;
+    if (n_past + T > hp->n_ctx) return -1;
+    float *x = malloc(sizeof(float) * T * E), *cur = malloc(sizeof(float) * T * E);
+    float *q = malloc(sizeof(float) * T * E), *kk = malloc(sizeof(float) * T * EKV), *vv = malloc(sizeof(float) * T * EKV);
+    float *attn = malloc(sizeof(float) * T * E), *tmp = malloc(sizeof(float) * T * E);
+    float *g = malloc(sizeof(float) * T * F), *u = malloc(sizeof(float) * T * F);
+    int32_t *pos = malloc(sizeof(int32_t) * T);
+    for (int t = 0; t < T; ++t) pos[t] = n_past + t;
+    /* token embeddings: get_rows (dequantize one row) */
+    const int64_t erow = orc_row_bytes(m->t[0], E);
+    for (int t = 0; t < T; ++t) orc_dequantize_row(m->t[0], (const uint8_t *)m->w[0] + (int64_t)tokens[t] * erow, x + (int64_t)t * E, E);
+    const int n_kv = n_past + T;
+    uint16_t *mask = malloc(sizeof(uint16_t) * (int64_t)T * n_kv);
+    for (int t = 0; t < T; ++t)
+        for (int j = 0; j < n_kv; ++j)
+            mask[(int64_t)t * n_kv + j] = (j <= n_past + t) ? 0 : 0xFC00; /* -inf */
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    for (int il = 0; il < hp->n_layer; ++il) {
+        const void *const *lw = m->w + 3 + 9 * il;
+        const int *lt = m->t + 3 + 9 * il;
+        orc_rms_norm(x, (const float *)lw[0], cur, E, T, hp->eps);
+        orc_mul_mat(lt[1], lw[1], E, E, cur, T, q, NT);
+        orc_mul_mat(lt[2], lw[2], E, EKV, cur, T, kk, NT);
+        orc_mul_mat(lt[3], lw[3], E, EKV, cur, T, vv, NT);
+        orc_rope(q, q, D, H, T, pos, D, hp->rope_base, hp->rope_freq_scale, NULL, 0.0f, 1.0f, 32.0f, 1.0f, hp->n_ctx);
+        orc_rope(kk, kk, D, HKV, T, pos, D, hp->rope_base, hp->rope_freq_scale, NULL, 0.0f, 1.0f, 32.0f, 1.0f, hp->n_ctx);
+        uint16_t *kl = m->kc + (int64_t)il * hp->n_ctx * EKV, *vl = m->vc + (int64_t)il * hp->n_ctx * EKV;
+        for (int t = 0; t < T; ++t)
+            for (int i = 0; i < EKV; ++i) {           /* ggml_cpy f32 -> f16 into the cache */
+                kl[(int64_t)(n_past + t) * EKV + i] = F2H(kk[(int64_t)t * EKV + i]);
+                vl[(int64_t)(n_past + t) * EKV + i] = F2H(vv[(int64_t)t * EKV + i]);
+            }
+        orc_flash_attn_ext(q, kl, vl, EKV, mask, attn, D, T, H, n_kv, HKV, kq_scale, NT);
+        orc_mul_mat(lt[4], lw[4], E, E, attn, T, tmp, NT);
+        add_inplace(tmp, x, (int64_t)T * E);             /* ffn_inp = attn_out + inpSA */
+        memcpy(x, tmp, sizeof(float) * T * E);
+        orc_rms_norm(x, (const float *)lw[5], cur, E, T, hp->eps);
+        orc_mul_mat(lt[6], lw[6], E, F, cur, T, g, NT);
+        orc_mul_mat(lt[7], lw[7], E, F, cur, T, u, NT);
+        for (int64_t i = 0; i < (int64_t)T * F; ++i) g[i] = (g[i] / (1.0f + expf(-g[i]))) * u[i];  /* silu(gate)*up */
+        orc_mul_mat(lt[8], lw[8], F, E, g, T, tmp, NT);
+        add_inplace(x, tmp, (int64_t)T * E);             /* l_out = ffn_out + ffn_inp */
+    }
+    memcpy(m->last_hidden, x + (int64_t)(T - 1) * E, sizeof(float) * E);
+    orc_rms_norm(x + (int64_t)(T - 1) * E, (const float *)m->w[1], cur, E, 1, hp->eps);
+    orc_mul_mat(m->t[2], m->w[2], E, hp->n_vocab, cur, 1, logits, NT);
+    free(x); free(cur); free(q); free(kk); free(vv); free(attn); free(tmp); free(g); free(u); free(pos); free(mask);
+    return 0;
+}
+
+/* deterministic synthetic tensors (same generator as the product; used by tests) */
+void orc_synth_fill(int type, uint64_t seed, uint64_t tid, int64_t nblocks, void *dst) {
+    const int bb = ks_block_bytes(type);
+    #pragma omp parallel for schedule(static)
+    for (int64_t b = 0; b < nblocks; ++b) ks_fill_block(type, seed, tid, (uint64_t)b, (uint8_t *)dst + b * bb);
+}

@@ -1,0 +1,217 @@
+"""TEST INFRASTRUCTURE: ctypes access to the C restatement (oracle/liboracle.so) and a
+driver for the reference-ggml harness (oracle/_ref/ref_llama).  Only tests/, smoke() and
+bench.py's cpu_baseline leg use this module."""
+import ctypes
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+REF_BIN = os.path.join(ROOT, "oracle", "_ref", "ref_llama")
+
+# ggml_type ids (ggml/include/ggml.h:364-399)
+F32, F16, Q4_0, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 8, 12, 13, 14, 15
+BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q8_0: (32, 34), Q4_K: (256, 144),
+         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292)}
+
+
+def row_bytes(t, k):
+    e, b = BLOCK[t]
+    return k // e * b
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_SO):
+            subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "all"])
+        L = ctypes.CDLL(ORACLE_SO)
+        P, I, I64, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+        L.orc_dequantize_row.argtypes = [I, P, P, I64]
+        L.orc_quantize_row.argtypes = [I, P, P, I64]
+        L.orc_vec_dot.argtypes = [I, I, P, P]
+        L.orc_vec_dot.restype = F
+        L.orc_vec_dot_type.argtypes = [I]
+        L.orc_mul_mat.argtypes = [I, P, I64, I64, P, I64, P, I]
+        L.orc_rms_norm.argtypes = [P, P, P, I64, I64, F]
+        L.orc_rope.argtypes = [P, P, I64, I64, I64, P, I, F, F, P, F, F, F, F, I]
+        L.orc_flash_attn_ext.argtypes = [P, P, P, I64, P, P, I, I, I, I, I, F, I]
+        L.orc_synth_fill.argtypes = [I, ctypes.c_uint64, ctypes.c_uint64, I64, P]
+        L.orc_llama_create.argtypes = [P, P, P, I]
+        L.orc_llama_create.restype = P
+        L.orc_llama_free.argtypes = [P]
+        L.orc_llama_eval.argtypes = [P, P, I, I, P]
+        L.orc_llama_last_hidden.argtypes = [P, P]
+        _lib = L
+    return _lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def synth(t, seed, tid, k, n):
+    """Synthetic tensor bytes [n rows x k elems] of ggml type t (include/kcpp_synth.h)."""
+    e, b = BLOCK[t]
+    nbl = (k // e) * n
+    out = np.empty(nbl * b, dtype=np.uint8)
+    lib().orc_synth_fill(t, seed, tid, nbl, ptr(out))
+    return out
+
+
+def dequant(t, data, k):
+    y = np.empty(k, dtype=np.float32)
+    lib().orc_dequantize_row(t, ptr(np.ascontiguousarray(data)), ptr(y), k)
+    return y
+
+
+def quantize(vt, x):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    out = np.empty(row_bytes(vt, x.size), dtype=np.uint8)
+    lib().orc_quantize_row(vt, ptr(x), ptr(out), x.size)
+    return out
+
+
+def mul_mat(t, w, K, N, X, nthreads=0):
+    X = np.ascontiguousarray(X, dtype=np.float32).reshape(-1, K)
+    M = X.shape[0]
+    dst = np.empty((M, N), dtype=np.float32)
+    lib().orc_mul_mat(t, ptr(np.ascontiguousarray(w)), K, N, ptr(X), M, ptr(dst), nthreads)
+    return dst
+
+
+def rms_norm(x, w, eps):
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    y = np.empty_like(x)
+    n = x.shape[-1]
+    lib().orc_rms_norm(ptr(x), ptr(np.ascontiguousarray(w, dtype=np.float32)) if w is not None else None,
+                       ptr(y), n, x.size // n, eps)
+    return y
+
+
+def rope(x, pos, base, freq_scale=1.0):
+    """x [T][H][D] f32, NORM mode (adjacent pairs)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    T, H, D = x.shape
+    y = np.empty_like(x)
+    pos = np.ascontiguousarray(pos, dtype=np.int32)
+    lib().orc_rope(ptr(x), ptr(y), D, H, T, ptr(pos), D, base, freq_scale, None, 0.0, 1.0, 32.0, 1.0, 4096)
+    return y
+
+
+def flash_attn(q, k, v, mask, nthreads=0):
+    """q [T][H][D] f32; k,v [n_kv][HKV][D] f16 (uint16 view ok); mask [T][n_kv] f16 or None."""
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    T, H, D = q.shape
+    k = np.ascontiguousarray(k).view(np.uint16)
+    v = np.ascontiguousarray(v).view(np.uint16)
+    n_kv, HKV, _ = k.shape
+    out = np.empty_like(q)
+    m = ptr(np.ascontiguousarray(mask).view(np.uint16)) if mask is not None else None
+    lib().orc_flash_attn_ext(ptr(q), ptr(k), ptr(v), HKV * D, m, ptr(out), D, T, H, n_kv, HKV,
+                             1.0 / np.sqrt(D), nthreads)
+    return out
+
+
+class HParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")] + \
+               [(n, ctypes.c_float) for n in ("eps", "rope_base", "rope_freq_scale")]
+
+
+def weight_shapes(hp):
+    """(K, N) per canonical weight index: tok_embd, output_norm, output, then 9 per layer."""
+    E, F, V = hp["n_embd"], hp["n_ff"], hp["n_vocab"]
+    EKV = hp["n_head_kv"] * (E // hp["n_head"])
+    s = [(E, V), (E, 1), (E, V)]
+    for _ in range(hp["n_layer"]):
+        s += [(E, 1), (E, E), (E, EKV), (E, EKV), (E, E), (E, 1), (E, F), (E, F), (F, E)]
+    return s
+
+
+class OracleLlama:
+    def __init__(self, hp, types, seed, nthreads=0):
+        self.hp = hp
+        self.bufs = [synth(t, seed, i, k, n) for i, ((k, n), t) in enumerate(zip(weight_shapes(hp), types))]
+        arr = (ctypes.c_void_p * len(self.bufs))(*[b.ctypes.data for b in self.bufs])
+        tarr = (ctypes.c_int * len(types))(*types)
+        h = HParams(*[hp[n] for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")],
+                    hp["eps"], hp["rope_base"], hp.get("rope_freq_scale", 1.0))
+        self._arr, self._tarr, self._h = arr, tarr, h
+        self.m = lib().orc_llama_create(ctypes.byref(h), arr, tarr, nthreads)
+
+    def eval(self, tokens, n_past):
+        tok = np.ascontiguousarray(tokens, dtype=np.int32)
+        logits = np.empty(self.hp["n_vocab"], dtype=np.float32)
+        rc = lib().orc_llama_eval(self.m, ptr(tok), len(tok), n_past, ptr(logits))
+        assert rc == 0
+        return logits
+
+    def __del__(self):
+        if getattr(self, "m", None):
+            lib().orc_llama_free(self.m)
+            self.m = None
+
+
+def ref_available():
+    return os.path.exists(REF_BIN)
+
+
+def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeout=600):
+    """Run the reference ggml graph; returns (logits [1+n_gen, V], info dict)."""
+    import json
+    with tempfile.TemporaryDirectory() as td:
+        cfg = os.path.join(td, "cfg.txt")
+        out = os.path.join(td, "logits.bin")
+        with open(cfg, "w") as f:
+            f.write(" ".join(str(hp[n]) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")))
+            f.write(" %r %r %r %d\n" % (float(hp["eps"]), float(hp["rope_base"]), float(hp.get("rope_freq_scale", 1.0)), seed))
+            f.write(" ".join(map(str, types)) + "\n")
+            f.write("%d %d %d %d\n" % (nthreads, len(prompt), n_gen, ubatch))
+            f.write(" ".join(map(str, prompt)) + "\n" + out + "\n")
+        r = subprocess.run([REF_BIN, "llama", cfg], capture_output=True, text=True, timeout=timeout,
+                           env=dict(os.environ, OMP_NUM_THREADS=str(nthreads)))
+        if r.returncode != 0:
+            raise RuntimeError("ref_llama failed: %s %s" % (r.returncode, r.stderr))
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        logits = np.fromfile(out, dtype=np.float32).reshape(-1, hp["n_vocab"])
+        return logits, info
+
+
+def run_ref_op(op, inp_bytes, out_count, args, nthreads=4):
+    with tempfile.TemporaryDirectory() as td:
+        fi, fo = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
+        with open(fi, "wb") as f:
+            f.write(inp_bytes)
+        r = subprocess.run([REF_BIN, "op", op, fi, fo] + [str(a) for a in args], capture_output=True, text=True,
+                           env=dict(os.environ, REF_THREADS=str(nthreads)))
+        if r.returncode != 0:
+            raise RuntimeError("ref op %s failed rc=%s %s" % (op, r.returncode, r.stderr))
+        return np.fromfile(fo, dtype=np.float32)[:out_count]
+
+
+TINY = dict(n_vocab=512, n_embd=512, n_head=4, n_head_kv=1, n_layer=2, n_ff=1024, n_ctx=256,
+            eps=1e-5, rope_base=500000.0)
+
+
+def q4_k_m_types(n_layer, tok=Q4_K, out=Q6_K):
+    """Q4_K_M per-tensor policy (src/llama.cpp:17986-18157): Q6_K for attn_v/ffn_down on 'more bits'
+    layers (i<L/8, i>=7L/8, (i-L/8)%3==2), output Q6_K, everything else Q4_K."""
+    types = [tok, F32, out]
+    for i in range(n_layer):
+        more = i < n_layer // 8 or i >= 7 * n_layer // 8 or (i - n_layer // 8) % 3 == 2
+        v = Q6_K if more else Q4_K
+        types += [F32, Q4_K, Q4_K, v, Q4_K, F32, Q4_K, Q4_K, v]
+    return types
+
+
+def uniform_types(n_layer, t, out=None):
+    types = [t, F32, out if out is not None else t]
+    for _ in range(n_layer):
+        types += [F32, t, t, t, t, F32, t, t, t]
+    return types
