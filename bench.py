@@ -1,0 +1,181 @@
+"""Benchmark: Llama-3-8B Q4_K_M (synthetic weights), 4k context, koboldcpp --benchmark semantics.
+
+Workload (BASELINE.json configs[1]): prompt of 3840 tokens prefilled in
+ubatches of 512, then greedy decode at positions 3840..4095.  A "step" is one decode token
+(one pass of the token-generation hot path); `value` = decode tokens/s.  Prefill tok/s is reported
+beside it.  Multi-GPU (N>1, torchrun): layer split across ranks (tensor_split 1,1,...), the hidden
+state handed off rank->rank with RCCL send/recv; value = tokens/s of the whole pipeline.
+
+Adds:
+  roofline     -- dominant decode kernel (Q4_K gate|up mat-vec, 4096 x 2*14336), HIP-event timed
+  cpu_baseline -- the REFERENCE ggml CPU path (oracle/_ref/ref_llama, built from the reference
+                  sources) on the same synthetic 8B weights, bounded sample, rank 0 only.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+LLAMA3_8B = dict(n_vocab=128256, n_embd=4096, n_head=32, n_head_kv=8, n_layer=32, n_ff=14336, n_ctx=4096,
+                 eps=1e-5, rope_base=500000.0)
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
+
+
+def q4_k_m_types(n_layer):
+    import refharness as R
+    return R.q4_k_m_types(n_layer)
+
+
+def weight_bytes(hp, types):
+    import refharness as R
+    return sum(R.row_bytes(t, k) * n for (k, n), t in zip(R.weight_shapes(hp), types))
+
+
+def measure_roofline(K, torch, iters=50):
+    """Time the dominant decode kernel: Q4_K GLU mat-vec (ffn_gate|ffn_up, 4096 -> 14336)."""
+    Kd, N = 4096, 14336
+    wbytes = Kd // 256 * 144 * N
+    w = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
+    w2 = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    K.call("kcpp_weight_synth", 12, 1, 1, w.data_ptr(), Kd, N, s)
+    K.call("kcpp_weight_synth", 12, 1, 2, w2.data_ptr(), Kd, N, s)
+    x = torch.randn(Kd, device="cuda")
+    act = torch.empty(K.act_bytes(12, Kd, 1), dtype=torch.uint8, device="cuda")
+    K.call("kcpp_quantize_act", 15, x.data_ptr(), Kd, act.data_ptr(), Kd, 1, s)
+    y = torch.empty(N, device="cuda")
+    args = (12, w.data_ptr(), w2.data_ptr(), Kd, N, act.data_ptr(), 1, y.data_ptr(), N, None, 0, 1, s)
+    for _ in range(5):
+        K.call("kcpp_gemv", *args)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # rotate over 4 weight pairs so the 66 MB working set is not L3-resident (>256 MiB total)
+    ws = [(w, w2)]
+    for i in range(3):
+        a = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
+        b = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
+        K.call("kcpp_weight_synth", 12, 1, 10 + 2 * i, a.data_ptr(), Kd, N, s)
+        K.call("kcpp_weight_synth", 12, 1, 11 + 2 * i, b.data_ptr(), Kd, N, s)
+        ws.append((a, b))
+    torch.cuda.synchronize()
+    e0.record()
+    for i in range(iters):
+        a, b = ws[i % len(ws)]
+        K.call("kcpp_gemv", 12, a.data_ptr(), b.data_ptr(), Kd, N, act.data_ptr(), 1, y.data_ptr(), N, None, 0, 1, s)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    alg = 2 * wbytes + K.act_bytes(12, Kd, 1) + N * 4          # weights + activation + output
+    gbs = alg / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "k_gemv<Q4_K,GLU> 4096x(2x14336)", "bytes_per_launch": alg, "avg_us": round(ms * 1e3, 2)}
+
+
+def cpu_baseline(hp, types, threads, n_prompt=32, n_gen=4):
+    import refharness as R
+    if not R.ref_available():
+        return None
+    prompt = [16 + (i % 2) for i in range(n_prompt)]     # " 1" style repeated ids
+    hp2 = dict(hp)
+    hp2["n_ctx"] = n_prompt + n_gen + 8
+    _, info = R.run_ref_llama(hp2, types, 1234, prompt, n_gen, nthreads=threads, ubatch=512, timeout=900)
+    return {"value": round(n_gen / info["decode_s"], 3), "unit": "tok/s (decode)", "cores": threads,
+            "kind": "reference",
+            "prefill_tok_s": round(n_prompt / info["prefill_s"], 3),
+            "sample": "reference ggml CPU (oracle/_ref/ref_llama) on the same synthetic Llama-3-8B Q4_K_M: "
+                      "%d-token prefill + %d greedy decode tokens, %d threads" % (n_prompt, n_gen, threads)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--prompt", type=int, default=3840)
+    ap.add_argument("--ubatch", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--layers", type=int, default=None, help="override n_layer (debug only; invalidates metric)")
+    args = ap.parse_args()
+
+    import torch
+    import koboldcpp_amd.lib as K
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        from koboldcpp_amd import pipeline
+        return pipeline.bench_main(args, world, rank, local)
+
+    torch.cuda.set_device(0)
+    hp = dict(LLAMA3_8B)
+    if args.layers:
+        hp["n_layer"] = args.layers
+    types = q4_k_m_types(hp["n_layer"])
+    m = K.Model(hp, types, max_ubatch=args.ubatch)
+    m.synth(1234)
+    prompt = [16 + (i % 2) for i in range(args.prompt)]
+    # warm-up prefill on a short prompt (JIT-free, but first-touch of buffers / graph capture)
+    m.decode(prompt[:64], 0, want_logits=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m.decode(prompt, 0, want_logits=False)
+    torch.cuda.synchronize()
+    t_pp = time.perf_counter() - t0
+    tok = m.argmax()
+    n_past = len(prompt)
+    for _ in range(args.warmup):
+        m.decode([tok], n_past, want_logits=False)
+        tok = m.argmax()
+        n_past += 1
+    steps = min(args.steps, hp["n_ctx"] - n_past)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.decode([tok], n_past, want_logits=False)
+        tok = m.argmax()
+        n_past += 1
+    torch.cuda.synchronize()
+    t_tg = time.perf_counter() - t0
+    wb = m.weight_bytes()
+    m.close()
+    dec = steps / t_tg
+    pre = args.prompt / t_pp
+    ms_step = t_tg / steps * 1e3
+    # decode roofline over the whole token: weights + KV at the mean position
+    kv_bytes = 2 * hp["n_layer"] * hp["n_head_kv"] * (hp["n_embd"] // hp["n_head"]) * 2 * (n_past - steps / 2)
+    token_gbs = (wb + kv_bytes) / (ms_step * 1e-3) / 1e9
+    roof = measure_roofline(K, torch)
+    out = {
+        "metric": "decode tok/s (Llama-3-8B Q4_K_M, 4k ctx); prefill tok/s in prefill_tok_s",
+        "value": round(dec, 2), "unit": "tok/s", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+        "dtype": "q4_K/q6_K weights x q8_K activations (int8 dot, f32 accum); f16 KV", "data": "synthetic",
+        "config": {"workload": "llama3-8b-q4_k_m ctx4096: prefill %d (ubatch %d) + greedy decode" % (args.prompt, args.ubatch),
+                   "model": "Llama-3-8B-shape Q4_K_M random-init", "n_layer": hp["n_layer"],
+                   "prompt_tokens": args.prompt, "gen_positions": [args.prompt + args.warmup, n_past],
+                   "parallelism": "single GPU"},
+        "prefill_tok_s": round(pre, 1), "prefill_s": round(t_pp, 4),
+        "decode_effective_GBps": round(token_gbs, 1), "decode_hbm_frac": round(token_gbs / HBM_PEAK_GBS, 4),
+        "weight_bytes": wb,
+        "roofline": roof,
+    }
+    if not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(hp, types, args.cpu_threads)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"error": str(e)[:300]}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,114 @@
+/*
+ * kcpp_mi355x.h -- C ABI of koboldcpp_amd/koboldcpp_hipblas.so (MI355X / gfx950 ggml backend).
+ *
+ * Plain pointers and sizes only.  Device pointers are HIP device addresses; `stream` is a
+ * hipStream_t (NULL = default stream).  Every function returns 0 on success, <0 on error
+ * (never aborts across the ABI: mirrors the reference's "return failure, never throw" rule,
+ * SURVEY.md §8b b2).
+ *
+ * Three layers:
+ *   1. kernel entry points (what ggml_cuda_compute_forward dispatches to in the reference,
+ *      ggml/src/ggml-cuda.cu:2145-2349) -- used by the parity tests;
+ *   2. the Llama runtime (the part of src/llama.cpp + ggml-backend scheduling this backend
+ *      executes on the device: build_llama :10453, llama_decode_internal :17114);
+ *   3. the koboldcpp drop-in ABI (expose.cpp/expose.h) -- declared in include/kcpp_expose.h.
+ *
+ * Tensor data layouts: weights live in the "kcpp layout" (same byte count as ggml; Q6_K, Q4_0,
+ * Q8_0 are split into structure-of-arrays streams -- koboldcpp_amd/csrc/kcpp_common.h);
+ * activations, KV caches and outputs follow ggml's row-major order.
+ */
+#ifndef KCPP_MI355X_H
+#define KCPP_MI355X_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------- 1. kernels ---------- */
+
+/* ggml layout <-> kcpp layout (to_ggml=0: ggml->kcpp).  Replaces ggml_backend_cuda_buffer_set_tensor /
+ * get_tensor byte copies (ggml/src/ggml-cuda.cu:471-484) for quantized weights. */
+int kcpp_weight_repack(int type, const void *src, void *dst, int64_t K, int64_t N, int to_ggml, void *stream);
+/* deterministic synthetic weights (include/kcpp_synth.h) written directly in kcpp layout */
+int kcpp_weight_synth(int type, uint64_t seed, uint64_t tid, void *dst, int64_t K, int64_t N, void *stream);
+/* dequantize a whole kcpp-layout tensor to f32 [N][K] (ggml_get_to_fp32_cuda, convert.cu) */
+int kcpp_dequantize(int type, const void *w, float *y, int64_t K, int64_t N, void *stream);
+/* get_rows of a quantized table (k_get_rows, getrows.cu:5): y[t] = dequant(W[ids[t]]) */
+int kcpp_get_rows(int type, const void *w, int64_t K, int64_t N, const int32_t *ids, int64_t T, float *y,
+                  int64_t ldy, void *stream);
+
+/* activation quantization to the CPU vec_dot_type of the weight (Q8_K or Q8_0), bit-exact with
+ * quantize_row_q8_K_ref / quantize_row_q8_0 (ggml-quants.c:3786,940).  Replaces quantize_q8_1
+ * (ggml/src/ggml-cuda/quantize.cu:4-38). */
+int64_t kcpp_act_bytes(int wtype, int64_t K, int64_t M);
+int kcpp_vec_dot_type(int wtype);
+int kcpp_quantize_act(int vtype, const float *x, int64_t ldx, void *out, int64_t K, int64_t M, void *stream);
+
+/* Quantized mat-vec for M <= 8 columns (replaces mul_mat_vec_q, mmvq.cu:50-202):
+ *   mode 0: Y[c][n] = W[n].x[c] (+ res[c][n])     mode 1: Y[c][n] = silu(W[n].x[c]) * (W2[n].x[c]) */
+int kcpp_gemv(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
+              int64_t ldy, const float *res, int64_t ldr, int mode, void *stream);
+
+/* Batched quantized mat-mul on MFMA for M > 8 (replaces mul_mat_q / the hipBLAS dequant path,
+ * mmq.cuh:2572-2905, ggml-cuda.cu:1186-1284).  act from kcpp_quantize_act (mode 0/1 as gemv). */
+int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M);
+int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
+              int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream);
+
+/* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */
+int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,
+                  int64_t nrows, float eps, void *stream);
+/* host-side table of (cos, sin) per [pos][D/2], exactly as ggml_rope_cache_init (ggml.c:14246) */
+int kcpp_rope_table(float *tab_host, int n_pos, int n_dims, float freq_base, float freq_scale, const float *freq_factors,
+                    float ext_factor, float attn_factor, float beta_fast, float beta_slow, int n_ctx_orig);
+/* rope(q), rope(k) (NORM mode) + f16 store of K and V into the caches at positions pos.. */
+int kcpp_rope_kv(const float *qkv, int64_t ldqkv, float *q_out, uint16_t *q16, uint16_t *kc, uint16_t *vc, int T,
+                 int H, int HKV, int D, int n_past, const int32_t *pos_dev, const void *rope_tab, void *stream);
+/* flash attention over the f16 cache (ggml_cuda_flash_attn_ext, fattn.cu:298-345) */
+int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max);
+int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qout, void *ws,
+                    int T, int H, int HKV, int D, int n_past, const int32_t *n_past_dev, int n_kv_max, float scale,
+                    int force_path, void *stream);
+int kcpp_add(float *y, const float *a, const float *b, int64_t n, void *stream);
+int kcpp_silu_mul(float *y, const float *g, const float *u, int64_t n, void *stream);
+
+/* ---------- 2. Llama runtime ---------- */
+typedef struct kcpp_hparams {
+    int n_vocab, n_embd, n_head, n_head_kv, n_layer, n_ff, n_ctx;
+    float eps, rope_base, rope_freq_scale;
+} kcpp_hparams;
+
+typedef struct kcpp_model kcpp_model;
+
+/* Layer range [il0, il1) lives on `device`; embed/output flags say whether this stage owns the
+ * token embedding / output head (layer split, src/llama.cpp:7000-7036).  types[] has 3+9*n_layer
+ * entries in canonical order: tok_embd, output_norm, output, then per layer attn_norm, wq, wk,
+ * wv, wo, ffn_norm, ffn_gate, ffn_up, ffn_down. */
+kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *types, int device, int il0, int il1, int has_embed,
+                              int has_output, int max_ubatch);
+/* weights: synthetic (seed) or uploaded from host ggml-layout bytes (tensor index = canonical order) */
+int kcpp_model_synth_weights(kcpp_model *m, uint64_t seed);
+int kcpp_model_set_tensor(kcpp_model *m, int index, const void *ggml_bytes, int64_t nbytes);
+void kcpp_model_free(kcpp_model *m);
+
+/* One llama_decode of T tokens at n_past (T may exceed the ubatch: split internally).
+ * If the stage has the embedding, `tokens` are used; otherwise the stage's input hidden state
+ * must have been placed with kcpp_model_hidden_in.  If the stage has the output head, the last
+ * token's logits are copied to logits_host (may be NULL). */
+int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, int n_past, float *logits_host);
+/* device pointers of this stage's residual stream [max_ubatch][n_embd] f32 (pipeline handoff) */
+float *kcpp_model_hidden(kcpp_model *m);
+void *kcpp_model_stream(kcpp_model *m);
+/* per-stage step without embedding/out: run layers on the hidden buffer for T tokens */
+int kcpp_model_forward_hidden(kcpp_model *m, int T, int n_past);
+/* greedy argmax of the last logits on device (avoids the 0.5 MB logits copy) */
+int kcpp_model_argmax(kcpp_model *m, int32_t *token_out);
+/* enable/disable hipGraph replay for single-token decode (default on) */
+int kcpp_model_set_graphs(kcpp_model *m, int enable);
+int64_t kcpp_model_weight_bytes(kcpp_model *m);
+const char *kcpp_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,353 @@
+// attn.hip -- flash attention over the F16 KV cache (GGML_OP_FLASH_ATTN_EXT).
+//
+// Semantics: ggml_compute_forward_flash_attn_ext_f16 (reference ggml/src/ggml.c:15667-15875):
+// Q is rounded to f16 (q_to_vec_dot), s = (q16 . k16) * scale + mask, softmax over the
+// causal window, V-weighted sum.  The CPU accumulates V in f16 (ggml_vec_mad_f16); we keep
+// f32 accumulators (strictly more accurate; parity within the f16 rounding of the CPU path).
+// The reference GPU path (ggml/src/ggml-cuda/fattn-vec-f16.cuh:4-299) is a 32-lane vector
+// kernel with half accumulators; this is a wave64 split-KV design instead:
+//   decode  : k_fa_decode  grid (chunks of 256 keys, kv-head, query) -> partial (O, m, l)
+//             k_fa_combine one 256-thread block per (query, head pair) -> f32 out (+Q8_K quant)
+//   prefill : k_fa_prefill tiled 64 queries x 64 keys per step, online softmax.
+#include "kcpp_common.h"
+#include "kcpp_internal.h"
+
+#define FA_CHUNK 256
+#define FA_MAXG 8
+
+// K/V cache layout: [pos][HKV][D] f16, row stride EKV = HKV*D elements.
+// Query layout: q16 [T][H][D] f16.  Query t sits at absolute position n_past + t.
+template <int D, int G>
+__global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
+                                                   const uint16_t *__restrict__ vc, float *__restrict__ part_o,
+                                                   float2 *__restrict__ part_ml, int H, int HKV, int n_past_arg,
+                                                   const int32_t *__restrict__ n_past_dev, int n_chunks, float scale) {
+    static_assert(D == 128, "head dim 128");
+    const int c = blockIdx.x, hk = blockIdx.y, t = blockIdx.z;
+    const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
+    if (c * FA_CHUNK > n_past + t) return;               // chunk unused by this query (graph-static grid)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int qpos = n_past + t;
+    const int p0 = c * FA_CHUNK;
+    const int p1 = min(p0 + FA_CHUNK, qpos + 1);          // exclusive
+    const int64_t EKV = (int64_t)HKV * D;
+    __shared__ float s_sc[FA_MAXG][FA_CHUNK];
+    __shared__ float s_red[4][FA_MAXG][D];
+    __shared__ float s_m[FA_MAXG], s_l[FA_MAXG];
+
+    // --- scores: 16 lanes per key, 8 dims per lane
+    const int sub = lane & 15, kq = lane >> 4;
+    float qv[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint4 qq = *(const uint4 *)(q16 + ((int64_t)t * H + hk * G + g) * D + sub * 8);
+        const uint32_t w4[4] = {qq.x, qq.y, qq.z, qq.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            qv[g][2 * i] = h2f(w4[i] & 0xFFFF);
+            qv[g][2 * i + 1] = h2f(w4[i] >> 16);
+        }
+    }
+    for (int p = p0 + wave * 4 + kq; p < p0 + FA_CHUNK; p += 16) {
+        float kf[8];
+        const bool valid = p < p1;
+        if (valid) {
+            const uint4 kk = *(const uint4 *)(kc + (int64_t)p * EKV + hk * D + sub * 8);
+            const uint32_t w4[4] = {kk.x, kk.y, kk.z, kk.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { kf[2 * i] = h2f(w4[i] & 0xFFFF); kf[2 * i + 1] = h2f(w4[i] >> 16); }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float s = 0.0f;
+            if (valid) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) s = fmaf(qv[g][i], kf[i], s);
+            }
+            s = group_sum<16>(s);
+            if (sub == 0) s_sc[g][p - p0] = valid ? s * scale : -INFINITY;
+        }
+    }
+    __syncthreads();
+    // --- softmax statistics per head (one wave per head)
+    for (int g = wave; g < G; g += 4) {
+        float m = -INFINITY;
+        for (int i = lane; i < FA_CHUNK; i += 64) m = fmaxf(m, s_sc[g][i]);
+        m = wave_max(m);
+        float l = 0.0f;
+        for (int i = lane; i < FA_CHUNK; i += 64) {
+            const float e = (s_sc[g][i] == -INFINITY) ? 0.0f : expf(s_sc[g][i] - m);
+            s_sc[g][i] = e;
+            l += e;
+        }
+        l = wave_sum(l);
+        if (lane == 0) { s_m[g] = m; s_l[g] = l; }
+    }
+    __syncthreads();
+    // --- P.V: each lane owns dims 2*lane, 2*lane+1; wave w takes keys w, w+4, ...
+    float acc[G][2];
+#pragma unroll
+    for (int g = 0; g < G; ++g) acc[g][0] = acc[g][1] = 0.0f;
+    for (int p = p0 + wave; p < p1; p += 4) {
+        const uint32_t vv = *(const uint32_t *)(vc + (int64_t)p * EKV + hk * D + 2 * lane);
+        const float v0 = h2f(vv & 0xFFFF), v1 = h2f(vv >> 16);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float pr = s_sc[g][p - p0];
+            acc[g][0] = fmaf(pr, v0, acc[g][0]);
+            acc[g][1] = fmaf(pr, v1, acc[g][1]);
+        }
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) { s_red[wave][g][2 * lane] = acc[g][0]; s_red[wave][g][2 * lane + 1] = acc[g][1]; }
+    __syncthreads();
+    for (int i = threadIdx.x; i < G * D; i += 256) {
+        const int g = i / D, d = i % D;
+        const float o = s_red[0][g][d] + s_red[1][g][d] + s_red[2][g][d] + s_red[3][g][d];
+        const int h = hk * G + g;
+        part_o[(((int64_t)t * H + h) * n_chunks + c) * D + d] = o;
+    }
+    if (threadIdx.x < G) {
+        const int h = hk * G + threadIdx.x;
+        part_ml[((int64_t)t * H + h) * n_chunks + c] = make_float2(s_m[threadIdx.x], s_l[threadIdx.x]);
+    }
+}
+
+// combine split-KV partials; one 256-thread block covers two heads (= one Q8_K block of 256)
+__device__ void q8k_quant_block_attn(const float4 v, int lane, int8_t *qs, float *dptr, int16_t *bs);
+
+template <bool QUANT>
+__global__ void __launch_bounds__(256) k_fa_combine(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
+                                                    float *__restrict__ out, uint8_t *__restrict__ qout, int T, int H,
+                                                    int D, int n_past_arg, const int32_t *__restrict__ n_past_dev,
+                                                    int n_chunks_alloc) {
+    const int t = blockIdx.y;
+    const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
+    const int pair = blockIdx.x;                       // heads 2*pair, 2*pair+1
+    const int tid = threadIdx.x;
+    const int h = 2 * pair + tid / 128, d = tid % 128;
+    const int nch = (n_past + t) / FA_CHUNK + 1;       // chunks this query actually used
+    const float2 *ml = part_ml + ((int64_t)t * H + h) * n_chunks_alloc;
+    float M = -INFINITY;
+    for (int c = 0; c < nch; ++c) M = fmaxf(M, ml[c].x);
+    float L = 0.0f, O = 0.0f;
+    for (int c = 0; c < nch; ++c) {
+        const float w = ml[c].x == -INFINITY ? 0.0f : expf(ml[c].x - M);
+        L = fmaf(w, ml[c].y, L);
+        O = fmaf(w, part_o[(((int64_t)t * H + h) * n_chunks_alloc + c) * 128 + d], O);
+    }
+    const float r = O / L;
+    const int64_t e = (int64_t)t * H * 128 + (int64_t)h * 128 + d;
+    if (out) out[e] = r;
+    if constexpr (QUANT) {
+        // regroup: lane l of wave w needs elements 4*(64*w + l) .. +3 of the 256-block
+        __shared__ float s_v[256];
+        s_v[tid] = r;
+        __syncthreads();
+        if (tid < 64) {
+            const float4 v = make_float4(s_v[4 * tid], s_v[4 * tid + 1], s_v[4 * tid + 2], s_v[4 * tid + 3]);
+            const int64_t E = (int64_t)H * 128;
+            const int64_t nsb = E / 256;
+            int8_t *qs = (int8_t *)qout + (int64_t)t * E + pair * 256;
+            float *dp = (float *)(qout + (int64_t)T * E) + (int64_t)t * nsb + pair;
+            int16_t *bs = (int16_t *)(qout + (int64_t)T * E + (int64_t)T * nsb * 4) + (int64_t)t * (E / 16) + pair * 16;
+            q8k_quant_block_attn(v, tid, qs, dp, bs);
+        }
+    }
+}
+
+__device__ __forceinline__ void q8k_quant_block_attn(const float4 v, int lane, int8_t *qs, float *dptr, int16_t *bs) {
+    float xs[4] = {v.x, v.y, v.z, v.w};
+    float am = -1.0f; int ai = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { float a = fabsf(xs[e]); if (a > am) { am = a; ai = lane * 4 + e; } }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float am2 = __shfl_xor(am, o, 64);
+        int ai2 = __shfl_xor(ai, o, 64);
+        if (am2 > am || (am2 == am && ai2 < ai)) { am = am2; ai = ai2; }
+    }
+    const int ae = ai & 3;
+    const float mine = ae == 0 ? xs[0] : (ae == 1 ? xs[1] : (ae == 2 ? xs[2] : xs[3]));
+    const float mx = __shfl(mine, ai >> 2, 64);
+    int q[4];
+    if (am == 0.0f) {
+        q[0] = q[1] = q[2] = q[3] = 0;
+        if (lane == 0) *dptr = 0.0f;
+    } else {
+        const float iscale = -127.f / mx;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { int tq = nearest_int_mul(iscale, xs[e]); q[e] = tq < 127 ? tq : 127; }
+        if (lane == 0) *dptr = 1.0f / iscale;
+    }
+    ((int *)qs)[lane] = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
+    int s = q[0] + q[1] + q[2] + q[3];
+    s = group_sum<4>(s);
+    if ((lane & 3) == 0) bs[lane >> 2] = (int16_t)s;
+}
+
+// ---------------------------------------------------------------- prefill (tiled, online softmax)
+// grid (ceil(T/64), H), block 256.  Thread (ty = tid/16, tx = tid%16): query rows 4*ty..4*ty+3,
+// S columns tx + 16*j (j<4) and O dims tx*8 .. tx*8+7 (8 dims).
+#define FP_BQ 64
+#define FP_BK 64
+template <int D>
+__global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
+                                                    const uint16_t *__restrict__ vc, float *__restrict__ out, int T,
+                                                    int H, int HKV, int n_past, float scale) {
+    const int qt = blockIdx.x, h = blockIdx.y;
+    const int G = H / HKV, hk = h / G;
+    const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+    const int64_t EKV = (int64_t)HKV * D;
+    __shared__ float sQ[FP_BQ][D + 1];
+    __shared__ float sK[FP_BK][D + 1];
+    __shared__ float sV[FP_BK][D];
+    const int q0 = qt * FP_BQ;
+    for (int i = tid; i < FP_BQ * D; i += 256) {
+        const int r = i / D, d = i % D;
+        sQ[r][d] = (q0 + r < T) ? h2f(q16[((int64_t)(q0 + r) * H + h) * D + d]) : 0.0f;
+    }
+    float m[4], l[4], o[4][8];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        m[r] = -INFINITY; l[r] = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[r][j] = 0.0f;
+    }
+    const int last_q = min(q0 + FP_BQ, T) - 1;
+    const int kend = n_past + last_q + 1;                 // keys needed by this tile (exclusive)
+    for (int k0 = 0; k0 < kend; k0 += FP_BK) {
+        __syncthreads();
+        for (int i = tid; i < FP_BK * D / 2; i += 256) {
+            const int r = i / (D / 2), d2 = i % (D / 2);
+            const int p = k0 + r;
+            uint32_t kk = 0, vv = 0;
+            if (p < kend) {
+                kk = *(const uint32_t *)(kc + (int64_t)p * EKV + hk * D + 2 * d2);
+                vv = *(const uint32_t *)(vc + (int64_t)p * EKV + hk * D + 2 * d2);
+            }
+            sK[r][2 * d2] = h2f(kk & 0xFFFF); sK[r][2 * d2 + 1] = h2f(kk >> 16);
+            sV[r][2 * d2] = h2f(vv & 0xFFFF); sV[r][2 * d2 + 1] = h2f(vv >> 16);
+        }
+        __syncthreads();
+        float s[4][4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s[r][j] = 0.0f;
+        for (int d = 0; d < D; ++d) {
+            float qd[4], kd[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) qd[r] = sQ[4 * ty + r][d];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) kd[j] = sK[tx + 16 * j][d];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) s[r][j] = fmaf(qd[r], kd[j], s[r][j]);
+        }
+        // online softmax per query row; the 16 threads of a row-group (same ty) share rows
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int qi = q0 + 4 * ty + r;
+            const int qpos = n_past + qi;
+            float mx = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int p = k0 + tx + 16 * j;
+                s[r][j] = (qi < T && p <= qpos) ? s[r][j] * scale : -INFINITY;
+                mx = fmaxf(mx, s[r][j]);
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 1, 64)); mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 4, 64)); mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
+            const float mnew = fmaxf(m[r], mx);
+            const float alpha = (mnew == -INFINITY) ? 1.0f : expf(m[r] - mnew);
+            float ls = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                s[r][j] = (s[r][j] == -INFINITY) ? 0.0f : expf(s[r][j] - mnew);
+                ls += s[r][j];
+            }
+            ls += __shfl_xor(ls, 1, 64); ls += __shfl_xor(ls, 2, 64);
+            ls += __shfl_xor(ls, 4, 64); ls += __shfl_xor(ls, 8, 64);
+            l[r] = l[r] * alpha + ls;
+            m[r] = mnew;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[r][j] *= alpha;
+        }
+        // O += P V : P row r lives across the 16 tx-threads of the group (4 cols each)
+        for (int src = 0; src < 16; ++src) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kr = src + 16 * j;
+                float vr[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) vr[e] = sV[kr][tx * 8 + e];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float pr = __shfl(s[r][j], ((16 * ty) & 63) + src, 64);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) o[r][e] = fmaf(pr, vr[e], o[r][e]);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int qi = q0 + 4 * ty + r;
+        if (qi < T) {
+            const float inv = 1.0f / l[r];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) out[((int64_t)qi * H + h) * D + tx * 8 + e] = o[r][e] * inv;
+        }
+    }
+}
+
+extern "C" {
+
+int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max) {
+    const int64_t nch = (n_kv_max + FA_CHUNK - 1) / FA_CHUNK;
+    return (int64_t)T * H * nch * (128 * 4 + 8) + 256;
+}
+
+// out f32 [T][H][D] (may be null), qout Q8_K act [T][H*D] (may be null), ws from kcpp_fa_workspace_bytes
+// n_past_dev (optional): device-resident n_past (graph-replayable decode); then n_kv_max
+// bounds the grid and the kernels read the real n_past from memory.
+int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qout, void *ws,
+                    int T, int H, int HKV, int D, int n_past, const int32_t *n_past_dev, int n_kv_max, float scale,
+                    int force_path, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (D != 128 || H % HKV || H / HKV > FA_MAXG || (H % 2)) return -1;
+    const bool use_decode = force_path == 1 || (force_path == 0 && T <= 16);
+    if (use_decode) {
+        const int nkv = n_past_dev ? n_kv_max : n_past + T;
+        const int nch = (nkv + FA_CHUNK - 1) / FA_CHUNK;
+        float *po = (float *)ws;
+        float2 *pml = (float2 *)(po + (int64_t)T * H * nch * 128);
+        const dim3 grid(nch, HKV, T);
+        switch (H / HKV) {
+        case 1: hipLaunchKernelGGL((k_fa_decode<128, 1>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, HKV, n_past, n_past_dev, nch, scale); break;
+        case 2: hipLaunchKernelGGL((k_fa_decode<128, 2>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, HKV, n_past, n_past_dev, nch, scale); break;
+        case 4: hipLaunchKernelGGL((k_fa_decode<128, 4>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, HKV, n_past, n_past_dev, nch, scale); break;
+        case 8: hipLaunchKernelGGL((k_fa_decode<128, 8>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, HKV, n_past, n_past_dev, nch, scale); break;
+        default: return -3;
+        }
+        KCPP_CHECK(hipGetLastError());
+        if (qout)
+            hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, T), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, T, H,
+                               D, n_past, n_past_dev, nch);
+        else
+            hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, T), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, T,
+                               H, D, n_past, n_past_dev, nch);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
+    if (!out) return -2;
+    hipLaunchKernelGGL(k_fa_prefill<128>, dim3((T + FP_BQ - 1) / FP_BQ, H), dim3(256), 0, s, q16, kc, vc, out, T, H, HKV,
+                       n_past, scale);
+    KCPP_CHECK(hipGetLastError());
+    if (qout) return kcpp_quantize_act(KT_Q8_K, out, (int64_t)H * D, qout, (int64_t)H * D, T, stream);
+    return 0;
+}
+
+}  // extern "C"

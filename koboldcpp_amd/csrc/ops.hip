@@ -1,0 +1,186 @@
+// ops.hip -- norm / rope / KV-store / elementwise / embedding kernels.
+//
+// Semantics follow the CPU ops (reference ggml/src/ggml.c):
+//   rms_norm  ggml_compute_forward_rms_norm_f32  :12059  (double accumulation of float x*x)
+//   rope      ggml_compute_forward_rope_f32      :14272  (NORM mode, iterated theta *= theta_scale)
+//   KV store  ggml_cpy f32->f16 (RNE)            src/llama.cpp:9180-9202
+//   silu      x/(1+exp(-x)), then * up           src/llama.cpp:9289-9414
+// Fusions (MI355X-first, one launch instead of 2-4 ggml nodes): rms_norm * w -> Q8_K quantize;
+// rope(q) + rope(k) + f16 store of K/V into the cache.
+#include "kcpp_common.h"
+#include "kcpp_internal.h"
+
+// ---------------------------------------------------------------- rms_norm (+ weight, + quantize)
+// one 256-thread block per row; each wave owns super-blocks sb = wave, wave+4, ... (<= 8 per wave)
+__device__ void q8k_quant_block_dev(const float4 v, int lane, int8_t *qs, float *dptr, int16_t *bs);
+
+template <bool QUANT>
+__global__ void __launch_bounds__(256) k_rms_norm(const float *__restrict__ x, int64_t ldx, const float *__restrict__ w,
+                                                  float *__restrict__ y, int64_t ldy, uint8_t *__restrict__ qout,
+                                                  int64_t ne0, int64_t nrows, float eps) {
+    const int64_t r = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nsb = (int)(ne0 / 256);
+    const float *xr = x + r * ldx;
+    float4 v[8];
+    double ss = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int sb = wave + 4 * i;
+        if (sb < nsb) {
+            v[i] = *(const float4 *)(xr + sb * 256 + lane * 4);
+            ss += (double)__fmul_rn(v[i].x, v[i].x);
+            ss += (double)__fmul_rn(v[i].y, v[i].y);
+            ss += (double)__fmul_rn(v[i].z, v[i].z);
+            ss += (double)__fmul_rn(v[i].w, v[i].w);
+        }
+    }
+    ss = wave_sum(ss);
+    __shared__ double red[4];
+    if (lane == 0) red[wave] = ss;
+    __syncthreads();
+    const double sum = red[0] + red[1] + red[2] + red[3];
+    const float mean = (float)(sum / (double)ne0);
+    const float scale = 1.0f / sqrtf(mean + eps);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int sb = wave + 4 * i;
+        if (sb < nsb) {
+            const int64_t e = sb * 256 + lane * 4;
+            float4 o;
+            o.x = __fmul_rn(v[i].x, scale); o.y = __fmul_rn(v[i].y, scale);
+            o.z = __fmul_rn(v[i].z, scale); o.w = __fmul_rn(v[i].w, scale);
+            if (w) {
+                const float4 ww = *(const float4 *)(w + e);
+                o.x = __fmul_rn(o.x, ww.x); o.y = __fmul_rn(o.y, ww.y);
+                o.z = __fmul_rn(o.z, ww.z); o.w = __fmul_rn(o.w, ww.w);
+            }
+            if (y) *(float4 *)(y + r * ldy + e) = o;
+            if constexpr (QUANT) {
+                int8_t *qs = (int8_t *)qout + r * ne0 + sb * 256;
+                float *d = (float *)(qout + nrows * ne0) + r * nsb + sb;
+                int16_t *bs = (int16_t *)(qout + nrows * ne0 + nrows * nsb * 4) + r * (ne0 / 16) + sb * 16;
+                q8k_quant_block_dev(o, lane, qs, d, bs);
+            }
+        }
+    }
+}
+
+// identical to quant.hip's q8k_quant_block (kept in this TU so the fused kernel inlines it)
+__device__ __forceinline__ void q8k_quant_block_dev(const float4 v, int lane, int8_t *qs, float *dptr, int16_t *bs) {
+    float xs[4] = {v.x, v.y, v.z, v.w};
+    float am = -1.0f; int ai = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { float a = fabsf(xs[e]); if (a > am) { am = a; ai = lane * 4 + e; } }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float am2 = __shfl_xor(am, o, 64);
+        int ai2 = __shfl_xor(ai, o, 64);
+        if (am2 > am || (am2 == am && ai2 < ai)) { am = am2; ai = ai2; }
+    }
+    const int ae = ai & 3;
+    const float mine = ae == 0 ? xs[0] : (ae == 1 ? xs[1] : (ae == 2 ? xs[2] : xs[3]));
+    const float mx = __shfl(mine, ai >> 2, 64);
+    int q[4];
+    if (am == 0.0f) {
+        q[0] = q[1] = q[2] = q[3] = 0;
+        if (lane == 0) *dptr = 0.0f;
+    } else {
+        const float iscale = -127.f / mx;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { int t = nearest_int_mul(iscale, xs[e]); q[e] = t < 127 ? t : 127; }
+        if (lane == 0) *dptr = 1.0f / iscale;
+    }
+    ((int *)qs)[lane] = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
+    int s = q[0] + q[1] + q[2] + q[3];
+    s = group_sum<4>(s);
+    if ((lane & 3) == 0) bs[lane >> 2] = (int16_t)s;
+}
+
+// ---------------------------------------------------------------- rope + KV store
+// qkv row layout per token: q [H*D] | k [HKV*D] | v [HKV*D] at stride ldqkv.
+// Outputs: q_out f32 [T][H][D] (roped), q16 f16 copy (FA operand), K/V caches f16 [pos][HKV*D].
+// rope_tab [pos][D/2] (cos, sin) is built on the host exactly as ggml_rope_cache_init
+// (ggml.c:14246) computes it, so the rotation is bit-identical to the CPU op.
+__global__ void k_rope_kv(const float *__restrict__ qkv, int64_t ldqkv, float *__restrict__ q_out,
+                          uint16_t *__restrict__ q16, uint16_t *__restrict__ kc, uint16_t *__restrict__ vc,
+                          int H, int HKV, int D, int n_past, const int32_t *__restrict__ pos_dev,
+                          const float2 *__restrict__ rope_tab) {
+    const int t = blockIdx.x;
+    const int p = pos_dev ? pos_dev[t] : n_past + t;
+    const int half = D / 2;
+    const int npairs_q = H * half, npairs_k = HKV * half;
+    const float *row = qkv + (int64_t)t * ldqkv;
+    const int64_t EKV = (int64_t)HKV * D;
+    for (int i = threadIdx.x; i < npairs_q + npairs_k + (int)EKV; i += blockDim.x) {
+        if (i < npairs_q + npairs_k) {
+            const bool isq = i < npairs_q;
+            const int pi = isq ? i : i - npairs_q;
+            const int hh = pi / half, ip = pi % half;
+            const float2 cs = rope_tab[(int64_t)p * half + ip];
+            const float c = cs.x, s = cs.y;
+            const float *src = isq ? row + (int64_t)hh * D + 2 * ip : row + (int64_t)H * D + (int64_t)hh * D + 2 * ip;
+            const float x0 = src[0], x1 = src[1];
+            const float o0 = __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s));
+            const float o1 = __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c));
+            if (isq) {
+                const int64_t o = ((int64_t)t * H + hh) * D + 2 * ip;
+                if (q_out) { q_out[o] = o0; q_out[o + 1] = o1; }
+                if (q16) { q16[o] = f2h(o0); q16[o + 1] = f2h(o1); }
+            } else {
+                const int64_t o = (int64_t)p * EKV + (int64_t)hh * D + 2 * ip;
+                kc[o] = f2h(o0); kc[o + 1] = f2h(o1);
+            }
+        } else {
+            const int e = i - npairs_q - npairs_k;
+            vc[(int64_t)p * EKV + e] = f2h(row[(int64_t)(H + HKV) * D + e]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- elementwise / embedding
+__global__ void k_add(float *__restrict__ y, const float *__restrict__ a, const float *__restrict__ b, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = __fadd_rn(a[i], b[i]);
+}
+__global__ void k_silu_mul(float *__restrict__ y, const float *__restrict__ g, const float *__restrict__ u, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { const float x = g[i]; y[i] = (x / (1.0f + expf(-x))) * u[i]; }
+}
+
+
+extern "C" {
+
+int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,
+                  int64_t nrows, float eps, void *stream) {
+    if (ne0 % 256 || ne0 > 8192) return -1;
+    if (q8k_out)
+        hipLaunchKernelGGL(k_rms_norm<true>, dim3((unsigned)nrows), dim3(256), 0, (hipStream_t)stream, x, ldx, w, y, ldy,
+                           (uint8_t *)q8k_out, ne0, nrows, eps);
+    else
+        hipLaunchKernelGGL(k_rms_norm<false>, dim3((unsigned)nrows), dim3(256), 0, (hipStream_t)stream, x, ldx, w, y, ldy,
+                           (uint8_t *)nullptr, ne0, nrows, eps);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_rope_kv(const float *qkv, int64_t ldqkv, float *q_out, uint16_t *q16, uint16_t *kc, uint16_t *vc, int T, int H,
+                 int HKV, int D, int n_past, const int32_t *pos_dev, const void *rope_tab, void *stream) {
+    hipLaunchKernelGGL(k_rope_kv, dim3((unsigned)T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, q_out, q16, kc, vc, H,
+                       HKV, D, n_past, pos_dev, (const float2 *)rope_tab);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_add(float *y, const float *a, const float *b, int64_t n, void *stream) {
+    hipLaunchKernelGGL(k_add, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, y, a, b, n);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+int kcpp_silu_mul(float *y, const float *g, const float *u, int64_t n, void *stream) {
+    hipLaunchKernelGGL(k_silu_mul, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, y, g, u, n);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

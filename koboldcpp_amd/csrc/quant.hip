@@ -1,0 +1,305 @@
+// quant.hip -- weight layout (repack / synth / dequant) and activation quantization kernels.
+//
+// Activation quantization mirrors the CPU vec_dot_type conversion bit-for-bit:
+//   Q8_K: quantize_row_q8_K_ref   (reference ggml/src/ggml-quants.c:3786-3823)
+//   Q8_0: quantize_row_q8_0 AVX2  (reference ggml/src/ggml-quants.c:940-1000)
+// Dequantization mirrors dequantize_row_* (ggml-quants.c:1523,1617,2556,2764,2978).
+#include "kcpp_common.h"
+#include "kcpp_internal.h"
+
+// ---------------------------------------------------------------- weight layout
+// place one ggml-layout block (src) into the kcpp GPU layout at block index b
+__device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uint8_t *dst, int64_t b, int64_t nb) {
+    switch (type) {
+    case KT_Q6_K: {
+        uint8_t *q = dst + b * 192, *sc = dst + nb * 192 + b * 16, *d = dst + nb * 208 + b * 2;
+        for (int i = 0; i < 192; ++i) q[i] = src[i];
+        for (int i = 0; i < 16; ++i) sc[i] = src[192 + i];
+        d[0] = src[208]; d[1] = src[209];
+    } break;
+    case KT_Q4_0: {
+        uint8_t *q = dst + b * 16, *d = dst + nb * 16 + b * 2;
+        d[0] = src[0]; d[1] = src[1];
+        for (int i = 0; i < 16; ++i) q[i] = src[2 + i];
+    } break;
+    case KT_Q8_0: {
+        uint8_t *q = dst + b * 32, *d = dst + nb * 32 + b * 2;
+        d[0] = src[0]; d[1] = src[1];
+        for (int i = 0; i < 32; ++i) q[i] = src[2 + i];
+    } break;
+    default: {
+        const int bb = ks_block_bytes(type);
+        for (int i = 0; i < bb; ++i) dst[b * bb + i] = src[i];
+    }
+    }
+}
+__device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint8_t *blk, int64_t b, int64_t nb) {
+    switch (type) {
+    case KT_Q6_K: {
+        const uint8_t *q = src + b * 192, *sc = src + nb * 192 + b * 16, *d = src + nb * 208 + b * 2;
+        for (int i = 0; i < 192; ++i) blk[i] = q[i];
+        for (int i = 0; i < 16; ++i) blk[192 + i] = sc[i];
+        blk[208] = d[0]; blk[209] = d[1];
+    } break;
+    case KT_Q4_0: {
+        const uint8_t *q = src + b * 16, *d = src + nb * 16 + b * 2;
+        blk[0] = d[0]; blk[1] = d[1];
+        for (int i = 0; i < 16; ++i) blk[2 + i] = q[i];
+    } break;
+    case KT_Q8_0: {
+        const uint8_t *q = src + b * 32, *d = src + nb * 32 + b * 2;
+        blk[0] = d[0]; blk[1] = d[1];
+        for (int i = 0; i < 32; ++i) blk[2 + i] = q[i];
+    } break;
+    default: {
+        const int bb = ks_block_bytes(type);
+        for (int i = 0; i < bb; ++i) blk[i] = src[b * bb + i];
+    }
+    }
+}
+
+__global__ void k_repack(int type, const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int64_t nb, int dir) {
+    int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    uint8_t blk[256];
+    const int bb = ks_block_bytes(type);
+    if (dir == 0) {                    // ggml -> kcpp
+        for (int i = 0; i < bb; ++i) blk[i] = src[b * bb + i];
+        kl_store_block(type, blk, dst, b, nb);
+    } else {                           // kcpp -> ggml
+        kl_load_block(type, src, blk, b, nb);
+        for (int i = 0; i < bb; ++i) dst[b * bb + i] = blk[i];
+    }
+}
+
+__global__ void k_synth(int type, uint64_t seed, uint64_t tid, uint8_t *__restrict__ dst, int64_t nb) {
+    int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    uint8_t blk[256];
+    ks_fill_block(type, seed, tid, (uint64_t)b, blk);
+    kl_store_block(type, blk, dst, b, nb);
+}
+
+__device__ __forceinline__ void scale_min_k4(int j, const uint8_t *q, int &d, int &m) {
+    if (j < 4) { d = q[j] & 63; m = q[j + 4] & 63; }
+    else {
+        d = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+        m = (q[j + 4] >> 4) | ((q[j - 0] >> 6) << 4);
+    }
+}
+
+// dequantize block b of a kcpp-layout tensor (nb blocks total) into o[0..block_elems)
+__device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t b, float *o) {
+    uint8_t blk[256];
+    kl_load_block(type, src, blk, b, nb);
+    switch (type) {
+    case KT_F32: o[0] = *(const float *)blk; break;
+    case KT_F16: o[0] = h2f(*(const uint16_t *)blk); break;
+    case KT_Q4_0: {
+        float d = h2f(blk[0] | (blk[1] << 8));
+        for (int j = 0; j < 16; ++j) {
+            o[j] = ((blk[2 + j] & 0x0F) - 8) * d;
+            o[j + 16] = ((blk[2 + j] >> 4) - 8) * d;
+        }
+    } break;
+    case KT_Q8_0: {
+        float d = h2f(blk[0] | (blk[1] << 8));
+        for (int j = 0; j < 32; ++j) o[j] = (int8_t)blk[2 + j] * d;
+    } break;
+    case KT_Q4_K: case KT_Q5_K: {
+        const bool five = type == KT_Q5_K;
+        const float d = h2f(blk[0] | (blk[1] << 8)), mn = h2f(blk[2] | (blk[3] << 8));
+        const uint8_t *sc = blk + 4, *qh = blk + 16, *q = blk + (five ? 48 : 16);
+        for (int c = 0; c < 4; ++c) {
+            int s1, m1, s2, m2;
+            scale_min_k4(2 * c, sc, s1, m1);
+            scale_min_k4(2 * c + 1, sc, s2, m2);
+            const float d1 = d * s1, mm1 = mn * m1, d2 = d * s2, mm2 = mn * m2;
+            for (int l = 0; l < 32; ++l) {
+                int lo = q[32 * c + l] & 0xF, hi = q[32 * c + l] >> 4;
+                if (five) { lo += ((qh[l] >> (2 * c)) & 1) << 4; hi += ((qh[l] >> (2 * c + 1)) & 1) << 4; }
+                o[64 * c + l] = __fsub_rn(__fmul_rn(d1, (float)lo), mm1);
+                o[64 * c + 32 + l] = __fsub_rn(__fmul_rn(d2, (float)hi), mm2);
+            }
+        }
+    } break;
+    case KT_Q6_K: {
+        const float d = h2f(blk[208] | (blk[209] << 8));
+        const uint8_t *ql = blk, *qh = blk + 128;
+        const int8_t *sc = (const int8_t *)(blk + 192);
+        for (int n = 0; n < 2; ++n) {
+            for (int l = 0; l < 32; ++l) {
+                int is = l / 16;
+                int q1 = ((ql[l] & 0xF) | (((qh[l] >> 0) & 3) << 4)) - 32;
+                int q2 = ((ql[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4)) - 32;
+                int q3 = ((ql[l] >> 4) | (((qh[l] >> 4) & 3) << 4)) - 32;
+                int q4 = ((ql[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4)) - 32;
+                o[l + 0] = __fmul_rn(__fmul_rn(d, (float)sc[is + 0]), (float)q1);
+                o[l + 32] = __fmul_rn(__fmul_rn(d, (float)sc[is + 2]), (float)q2);
+                o[l + 64] = __fmul_rn(__fmul_rn(d, (float)sc[is + 4]), (float)q3);
+                o[l + 96] = __fmul_rn(__fmul_rn(d, (float)sc[is + 6]), (float)q4);
+            }
+            o += 128; ql += 64; qh += 32; sc += 8;
+        }
+    } break;
+    }
+}
+
+// one thread per block: dequantize into y (row-major [N][K])
+__global__ void k_dequant(int type, const uint8_t *__restrict__ src, float *__restrict__ y, int64_t nb) {
+    int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    deq_block(type, src, nb, b, y + b * ks_block_elems(type));
+}
+
+// get_rows: one workgroup per token, threads over the row's blocks (embedding lookup)
+__global__ void k_get_rows(int type, const uint8_t *__restrict__ src, int64_t K, int64_t N,
+                           const int32_t *__restrict__ ids, float *__restrict__ y, int64_t ldy) {
+    const int64_t t = blockIdx.x;
+    const int64_t r = ids[t];
+    const int64_t bpr = K / ks_block_elems(type), nb = bpr * N;
+    for (int64_t i = threadIdx.x; i < bpr; i += blockDim.x)
+        deq_block(type, src, nb, r * bpr + i, y + t * ldy + i * ks_block_elems(type));
+}
+
+// ---------------------------------------------------------------- activation quantization
+// Q8_K: one wave per 256-element super-block, 4 elements per lane.
+__device__ __forceinline__ void q8k_quant_block(const float4 v, int lane, int8_t *qs, float *dptr, int16_t *bs) {
+    float xs[4] = {v.x, v.y, v.z, v.w};
+    // arg-max |x| with the first index winning ties (ggml-quants.c:3794-3799)
+    float am = -1.0f; int ai = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { float a = fabsf(xs[e]); if (a > am) { am = a; ai = lane * 4 + e; } }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float am2 = __shfl_xor(am, o, 64);
+        int ai2 = __shfl_xor(ai, o, 64);
+        if (am2 > am || (am2 == am && ai2 < ai)) { am = am2; ai = ai2; }
+    }
+    const int ae = ai & 3;
+    const float mine = ae == 0 ? xs[0] : (ae == 1 ? xs[1] : (ae == 2 ? xs[2] : xs[3]));
+    const float mx = __shfl(mine, ai >> 2, 64);
+    int q[4];
+    if (am == 0.0f) {
+        q[0] = q[1] = q[2] = q[3] = 0;
+        if (lane == 0) *dptr = 0.0f;
+    } else {
+        const float iscale = -127.f / mx;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { int t = nearest_int_mul(iscale, xs[e]); q[e] = t < 127 ? t : 127; }
+        if (lane == 0) *dptr = 1.0f / iscale;
+    }
+    const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
+    ((int *)qs)[lane] = packed;
+    int s = q[0] + q[1] + q[2] + q[3];
+    s = group_sum<4>(s);
+    if ((lane & 3) == 0) bs[lane >> 2] = (int16_t)s;
+}
+
+__global__ void k_quant_q8k(const float *__restrict__ x, int64_t ldx, uint8_t *__restrict__ out, int64_t K, int64_t M) {
+    const int lane = threadIdx.x & 63;
+    const int64_t g = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);  // global super-block
+    const int64_t nsb = K / 256;
+    if (g >= nsb * M) return;
+    const int64_t m = g / nsb, sb = g % nsb;
+    const float4 v = *(const float4 *)(x + m * ldx + sb * 256 + lane * 4);
+    int8_t *qs = (int8_t *)out + m * K + sb * 256;
+    float *d = (float *)(out + M * K) + m * nsb + sb;
+    int16_t *bs = (int16_t *)(out + M * K + M * nsb * 4) + m * (K / 16) + sb * 16;
+    q8k_quant_block(v, lane, qs, d, bs);
+}
+
+// Q8_0 (AVX2 semantics): 8 lanes per 32-block, 4 elements per lane.
+__global__ void k_quant_q80(const float *__restrict__ x, int64_t ldx, uint8_t *__restrict__ out, int64_t K, int64_t M) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nb = K / 32;
+    const int64_t blk = t >> 3;
+    const int sub = t & 7;
+    const bool valid = blk < nb * M;
+    const int64_t m = valid ? blk / nb : 0, ib = valid ? blk % nb : 0;
+    float4 v = valid ? *(const float4 *)(x + m * ldx + ib * 32 + sub * 4) : make_float4(0, 0, 0, 0);
+    float am = fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w)));
+    am = fmaxf(am, __shfl_xor(am, 1, 64));
+    am = fmaxf(am, __shfl_xor(am, 2, 64));
+    am = fmaxf(am, __shfl_xor(am, 4, 64));
+    const float d = am / 127.f;
+    const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+    float xs[4] = {v.x, v.y, v.z, v.w};
+    int q[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+        float r = rintf(__fmul_rn(xs[e], id));
+        int iv = (int)r;
+        q[e] = iv > 127 ? 127 : (iv < -128 ? -128 : iv);
+    }
+    int s = q[0] + q[1] + q[2] + q[3];
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if (!valid) return;
+    const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
+    ((int *)((int8_t *)out + m * K + ib * 32))[sub] = packed;
+    if (sub == 0) {
+        ((float *)(out + M * K))[m * nb + ib] = h2f(f2h(d));        // the dot uses GGML_FP16_TO_FP32(y.d)
+        ((int16_t *)(out + M * K + M * nb * 4))[m * nb + ib] = (int16_t)s;
+    }
+}
+
+// ---------------------------------------------------------------- host launchers
+extern "C" {
+
+int kcpp_weight_repack(int type, const void *src_ggml, void *dst_kcpp, int64_t K, int64_t N, int to_ggml, void *stream) {
+    const int64_t nb = kl_nblocks(type, K, N);
+    if (nb <= 0) return 0;
+    hipLaunchKernelGGL(k_repack, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, type,
+                       (const uint8_t *)src_ggml, (uint8_t *)dst_kcpp, nb, to_ggml);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_weight_synth(int type, uint64_t seed, uint64_t tid, void *dst, int64_t K, int64_t N, void *stream) {
+    const int64_t nb = kl_nblocks(type, K, N);
+    hipLaunchKernelGGL(k_synth, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, type, seed, tid,
+                       (uint8_t *)dst, nb);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_dequantize(int type, const void *w, float *y, int64_t K, int64_t N, void *stream) {
+    const int64_t nb = kl_nblocks(type, K, N);
+    hipLaunchKernelGGL(k_dequant, dim3((unsigned)((nb + 127) / 128)), dim3(128), 0, (hipStream_t)stream, type,
+                       (const uint8_t *)w, y, nb);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_quantize_act(int vtype, const float *x, int64_t ldx, void *out, int64_t K, int64_t M, void *stream) {
+    if (vtype == KT_Q8_K) {
+        if (K % 256) return -1;
+        const int64_t nsb = K / 256 * M;
+        hipLaunchKernelGGL(k_quant_q8k, dim3((unsigned)((nsb + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, ldx,
+                           (uint8_t *)out, K, M);
+    } else if (vtype == KT_Q8_0) {
+        if (K % 32) return -1;
+        const int64_t nthreads = K / 32 * M * 8;
+        hipLaunchKernelGGL(k_quant_q80, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                           ldx, (uint8_t *)out, K, M);
+    } else {
+        return -2;
+    }
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_get_rows(int type, const void *w, int64_t K, int64_t N, const int32_t *ids, int64_t T, float *y, int64_t ldy,
+                  void *stream) {
+    hipLaunchKernelGGL(k_get_rows, dim3((unsigned)T), dim3(64), 0, (hipStream_t)stream, type, (const uint8_t *)w, K, N,
+                       ids, y, ldy);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int64_t kcpp_act_bytes(int wtype, int64_t K, int64_t M) { return act_bytes(vec_dot_type(wtype), K, M); }
+int kcpp_vec_dot_type(int wtype) { return vec_dot_type(wtype); }
+
+}  // extern "C"

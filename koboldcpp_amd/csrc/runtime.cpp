@@ -1,0 +1,419 @@
+// runtime.cpp -- Llama forward on one MI355X (one pipeline stage of the layer split).
+//
+// The reference executes build_llama (src/llama.cpp:10453-10620) as a ggml graph through
+// ggml_backend_sched -> ggml_backend_cuda_graph_compute (ggml-cuda.cu:2508), one kernel per
+// node with host dispatch per node (CUDA graphs are compiled out on HIP, common.cuh:580-582).
+// Here the same computation is a fixed, fused launch sequence per layer:
+//   rms_norm*w -> Q8_K           (1 launch)
+//   wq | wk | wv  mat-vec        (3 launches into one packed qkv row)
+//   rope(q,k) + K/V f16 store    (1)
+//   flash-attn split-KV + combine(+Q8_K quant)  (2)
+//   wo mat-vec + residual add    (1)
+//   rms_norm*w -> Q8_K           (1)
+//   gate|up mat-vec + silu*mul   (1)
+//   quantize -> down + residual  (2)
+// and single-token decode is captured once into a hipGraph and replayed (n_past and the token
+// id are read from device memory, so one graph serves every position).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/kcpp_mi355x.h"
+#include "../../include/kcpp_synth.h"
+
+static thread_local std::string g_err;
+extern "C" const char *kcpp_last_error(void) { return g_err.c_str(); }
+
+#define RT_CHECK(expr)                                                                                 \
+    do {                                                                                               \
+        hipError_t _e = (expr);                                                                        \
+        if (_e != hipSuccess) {                                                                        \
+            char _b[512];                                                                              \
+            snprintf(_b, sizeof _b, "HIP %s at %s:%d (%s)", hipGetErrorName(_e), __FILE__, __LINE__, #expr); \
+            g_err = _b;                                                                                \
+            fprintf(stderr, "[kcpp] %s\n", _b);                                                        \
+            return -1;                                                                                 \
+        }                                                                                              \
+    } while (0)
+#define RC(expr)                                                                                       \
+    do {                                                                                               \
+        int _r = (expr);                                                                               \
+        if (_r != 0) {                                                                                 \
+            char _b[512];                                                                              \
+            snprintf(_b, sizeof _b, "rc=%d at %s:%d (%s)", _r, __FILE__, __LINE__, #expr);             \
+            g_err = _b;                                                                                \
+            fprintf(stderr, "[kcpp] %s\n", _b);                                                        \
+            return _r;                                                                                 \
+        }                                                                                              \
+    } while (0)
+
+struct KTensor {
+    int type = KT_F32;
+    int64_t K = 0, N = 0;
+    void *d = nullptr;
+    size_t bytes = 0;
+};
+
+struct KLayer {
+    KTensor t[9];   // attn_norm, wq, wk, wv, wo, ffn_norm, gate, up, down
+    uint16_t *kc = nullptr, *vc = nullptr;
+};
+
+struct kcpp_model {
+    kcpp_hparams hp;
+    std::vector<int> types;
+    int device = 0, il0 = 0, il1 = 0, has_embed = 1, has_output = 1, ub = 512;
+    hipStream_t stream = nullptr;
+    KTensor tok_embd, output_norm, output;
+    std::vector<KLayer> layers;      // only [il0, il1)
+    // workspace
+    float *x = nullptr, *qkv = nullptr, *attn = nullptr, *h = nullptr, *logits = nullptr;
+    uint16_t *q16 = nullptr;
+    void *act = nullptr, *act2 = nullptr, *fa_ws = nullptr, *gemm_ws = nullptr;
+    size_t act_sz = 0, gemm_ws_sz = 0;
+    int32_t *tok_dev = nullptr, *pos_dev = nullptr, *argmax_dev = nullptr;
+    float2 *rope_tab = nullptr;
+    int32_t *pin = nullptr;          // pinned host {token, n_past}
+    float *logits_pin = nullptr;
+    bool use_graphs = true;
+    hipGraphExec_t g_exec = nullptr;
+    int64_t weight_bytes = 0;
+};
+
+static int64_t tensor_bytes(int type, int64_t K, int64_t N) {
+    return K / ks_block_elems(type) * N * ks_block_bytes(type);
+}
+
+static void shape_of(const kcpp_hparams &hp, int idx, int64_t &K, int64_t &N) {
+    const int64_t E = hp.n_embd, F = hp.n_ff, V = hp.n_vocab, EKV = (int64_t)hp.n_head_kv * (E / hp.n_head);
+    if (idx == 0) { K = E; N = V; return; }
+    if (idx == 1) { K = E; N = 1; return; }
+    if (idx == 2) { K = E; N = V; return; }
+    switch ((idx - 3) % 9) {
+    case 0: K = E; N = 1; return;
+    case 1: K = E; N = E; return;
+    case 2: K = E; N = EKV; return;
+    case 3: K = E; N = EKV; return;
+    case 4: K = E; N = E; return;
+    case 5: K = E; N = 1; return;
+    case 6: K = E; N = F; return;
+    case 7: K = E; N = F; return;
+    default: K = F; N = E; return;
+    }
+}
+
+static KTensor *tensor_at(kcpp_model *m, int idx) {
+    if (idx == 0) return m->has_embed ? &m->tok_embd : nullptr;
+    if (idx == 1) return m->has_output ? &m->output_norm : nullptr;
+    if (idx == 2) return m->has_output ? &m->output : nullptr;
+    const int il = (idx - 3) / 9, j = (idx - 3) % 9;
+    if (il < m->il0 || il >= m->il1) return nullptr;
+    return &m->layers[il - m->il0].t[j];
+}
+
+static int alloc_tensor(kcpp_model *m, KTensor &t, int type, int64_t K, int64_t N) {
+    t.type = type; t.K = K; t.N = N;
+    t.bytes = (size_t)tensor_bytes(type, K, N);
+    RT_CHECK(hipMalloc(&t.d, (t.bytes + 255) & ~(size_t)255));
+    m->weight_bytes += t.bytes;
+    return 0;
+}
+
+extern "C" int kcpp_rope_table(float *tab, int n_pos, int n_dims, float freq_base, float freq_scale,
+                               const float *freq_factors, float ext_factor, float attn_factor, float beta_fast,
+                               float beta_slow, int n_ctx_orig) {
+    // ggml_rope_cache_init + rope_yarn (ggml.c:14216-14260); n_dims == head dim for Llama
+    const float theta_scale = powf(freq_base, -2.0f / n_dims);
+    auto corr_dim = [&](float n_rot) { return n_dims * logf(n_ctx_orig / (n_rot * 2 * (float)M_PI)) / (2 * logf(freq_base)); };
+    float corr0 = fmaxf(0, floorf(corr_dim(beta_fast))), corr1 = fminf(n_dims - 1, ceilf(corr_dim(beta_slow)));
+    for (int p = 0; p < n_pos; ++p) {
+        float theta = (float)p;
+        for (int i0 = 0; i0 < n_dims; i0 += 2) {
+            const float ff = freq_factors ? freq_factors[i0 / 2] : 1.0f;
+            const float theta_extrap = theta / ff;
+            const float theta_interp = freq_scale * theta_extrap;
+            float th = theta_interp, mscale = attn_factor;
+            if (ext_factor != 0.0f) {
+                const float y = (i0 / 2 - corr0) / fmaxf(0.001f, corr1 - corr0);
+                const float ramp_mix = (1 - fminf(1, fmaxf(0, y))) * ext_factor;
+                th = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
+                mscale *= 1.0f + 0.1f * logf(1.0f / freq_scale);
+            }
+            tab[((int64_t)p * (n_dims / 2) + i0 / 2) * 2 + 0] = cosf(th) * mscale;
+            tab[((int64_t)p * (n_dims / 2) + i0 / 2) * 2 + 1] = sinf(th) * mscale;
+            theta *= theta_scale;
+        }
+    }
+    return 0;
+}
+
+extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *types, int device, int il0, int il1,
+                                         int has_embed, int has_output, int max_ubatch) {
+    if (hipSetDevice(device) != hipSuccess) { g_err = "hipSetDevice failed"; return nullptr; }
+    kcpp_model *m = new kcpp_model();
+    m->hp = *hp;
+    m->types.assign(types, types + 3 + 9 * hp->n_layer);
+    m->device = device; m->il0 = il0; m->il1 = il1; m->has_embed = has_embed; m->has_output = has_output;
+    m->ub = max_ubatch > 0 ? max_ubatch : 512;
+    auto fail = [&](const char *what) { g_err = what; kcpp_model_free(m); return (kcpp_model *)nullptr; };
+    if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
+    const int64_t E = hp->n_embd, F = hp->n_ff, H = hp->n_head, HKV = hp->n_head_kv, D = E / H, EKV = HKV * D;
+    const int64_t UB = m->ub;
+    m->layers.resize(il1 - il0);
+    for (int idx = 0; idx < 3 + 9 * hp->n_layer; ++idx) {
+        KTensor *t = tensor_at(m, idx);
+        if (!t) continue;
+        int64_t K, N;
+        shape_of(*hp, idx, K, N);
+        if (alloc_tensor(m, *t, types[idx], K, N)) return fail("weight alloc");
+    }
+    for (auto &L : m->layers) {
+        const size_t kvb = (size_t)hp->n_ctx * EKV * 2;
+        if (hipMalloc(&L.kc, kvb) != hipSuccess || hipMalloc(&L.vc, kvb) != hipSuccess) return fail("kv alloc");
+        hipMemset(L.kc, 0, kvb); hipMemset(L.vc, 0, kvb);
+    }
+    // activation buffers sized for the widest vec_dot input (K = F) at UB columns
+    m->act_sz = (size_t)std::max(kcpp_act_bytes(KT_Q4_K, std::max(E, F), UB), kcpp_act_bytes(KT_Q8_0, std::max(E, F), UB));
+    m->gemm_ws_sz = 0;
+    for (int idx = 0; idx < 3 + 9 * hp->n_layer; ++idx) {
+        int64_t K, N; shape_of(*hp, idx, K, N);
+        if (types[idx] == KT_F32) continue;
+        m->gemm_ws_sz = std::max<size_t>(m->gemm_ws_sz, (size_t)kcpp_gemm_workspace_bytes(types[idx], K, N, UB));
+    }
+    bool ok = hipMalloc(&m->x, UB * E * 4) == hipSuccess && hipMalloc(&m->qkv, UB * (E + 2 * EKV) * 4) == hipSuccess &&
+              hipMalloc(&m->attn, UB * E * 4) == hipSuccess && hipMalloc(&m->h, UB * F * 4) == hipSuccess &&
+              hipMalloc(&m->q16, UB * E * 2) == hipSuccess && hipMalloc(&m->act, m->act_sz) == hipSuccess &&
+              hipMalloc(&m->act2, m->act_sz) == hipSuccess &&
+              hipMalloc(&m->fa_ws, kcpp_fa_workspace_bytes(std::max<int>(16, 1), H, hp->n_ctx)) == hipSuccess &&
+              hipMalloc(&m->tok_dev, UB * 4) == hipSuccess && hipMalloc(&m->pos_dev, 64) == hipSuccess &&
+              hipMalloc(&m->argmax_dev, 64) == hipSuccess &&
+              hipMalloc(&m->rope_tab, (size_t)hp->n_ctx * D / 2 * sizeof(float2)) == hipSuccess &&
+              hipHostMalloc((void **)&m->pin, 64, hipHostMallocDefault) == hipSuccess &&
+              (m->gemm_ws_sz == 0 || hipMalloc(&m->gemm_ws, m->gemm_ws_sz) == hipSuccess);
+    if (!ok) return fail("workspace alloc");
+    if (has_output) {
+        if (hipMalloc(&m->logits, (size_t)hp->n_vocab * 4) != hipSuccess) return fail("logits alloc");
+        if (hipHostMalloc((void **)&m->logits_pin, (size_t)hp->n_vocab * 4, hipHostMallocDefault) != hipSuccess)
+            return fail("logits pin");
+    }
+    std::vector<float> tab((size_t)hp->n_ctx * D);
+    kcpp_rope_table(tab.data(), hp->n_ctx, (int)D, hp->rope_base, hp->rope_freq_scale, nullptr, 0.0f, 1.0f, 32.0f, 1.0f,
+                    hp->n_ctx);
+    if (hipMemcpy(m->rope_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess) return fail("rope tab");
+    return m;
+}
+
+extern "C" void kcpp_model_free(kcpp_model *m) {
+    if (!m) return;
+    hipSetDevice(m->device);
+    if (m->g_exec) hipGraphExecDestroy(m->g_exec);
+    auto F = [](void *p) { if (p) hipFree(p); };
+    F(m->tok_embd.d); F(m->output_norm.d); F(m->output.d);
+    for (auto &L : m->layers) { for (auto &t : L.t) F(t.d); F(L.kc); F(L.vc); }
+    F(m->x); F(m->qkv); F(m->attn); F(m->h); F(m->logits); F(m->q16); F(m->act); F(m->act2); F(m->fa_ws);
+    F(m->gemm_ws); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->rope_tab);
+    if (m->pin) hipHostFree(m->pin);
+    if (m->logits_pin) hipHostFree(m->logits_pin);
+    if (m->stream) hipStreamDestroy(m->stream);
+    delete m;
+}
+
+extern "C" int kcpp_model_synth_weights(kcpp_model *m, uint64_t seed) {
+    RT_CHECK(hipSetDevice(m->device));
+    for (int idx = 0; idx < 3 + 9 * m->hp.n_layer; ++idx) {
+        KTensor *t = tensor_at(m, idx);
+        if (!t) continue;
+        RC(kcpp_weight_synth(t->type, seed, (uint64_t)idx, t->d, t->K, t->N, m->stream));
+    }
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    return 0;
+}
+
+extern "C" int kcpp_model_set_tensor(kcpp_model *m, int idx, const void *src, int64_t nbytes) {
+    KTensor *t = tensor_at(m, idx);
+    if (!t) return 0;                      // not on this stage
+    if ((size_t)nbytes != t->bytes) { g_err = "set_tensor: size mismatch"; return -2; }
+    RT_CHECK(hipSetDevice(m->device));
+    if (t->type == KT_Q6_K || t->type == KT_Q4_0 || t->type == KT_Q8_0) {
+        void *stage = nullptr;
+        RT_CHECK(hipMalloc(&stage, t->bytes));
+        RT_CHECK(hipMemcpyAsync(stage, src, t->bytes, hipMemcpyHostToDevice, m->stream));
+        RC(kcpp_weight_repack(t->type, stage, t->d, t->K, t->N, 0, m->stream));
+        RT_CHECK(hipStreamSynchronize(m->stream));
+        RT_CHECK(hipFree(stage));
+    } else {
+        RT_CHECK(hipMemcpyAsync(t->d, src, t->bytes, hipMemcpyHostToDevice, m->stream));
+        RT_CHECK(hipStreamSynchronize(m->stream));
+    }
+    return 0;
+}
+
+extern "C" float *kcpp_model_hidden(kcpp_model *m) { return m->x; }
+extern "C" void *kcpp_model_stream(kcpp_model *m) { return m->stream; }
+extern "C" int64_t kcpp_model_weight_bytes(kcpp_model *m) { return m->weight_bytes; }
+extern "C" int kcpp_model_set_graphs(kcpp_model *m, int enable) {
+    m->use_graphs = enable != 0;
+    return 0;
+}
+
+// y[c][n] = W . act  (+res) for M columns: mat-vec for M <= 8, MFMA GEMM above
+static int matmul(kcpp_model *m, const KTensor &W, const KTensor *W2, const void *act, int64_t M, float *Y, int64_t ldy,
+                  const float *res, int64_t ldr, int mode) {
+    if (M <= 8)
+        return kcpp_gemv(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, m->stream);
+    return kcpp_gemm(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, m->gemm_ws, m->stream);
+}
+
+// run layers [il0, il1) on m->x for T tokens (T <= ub).  n_past via pos_dev when graph-replayed.
+static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
+    const kcpp_hparams &hp = m->hp;
+    const int64_t E = hp.n_embd, F = hp.n_ff, H = hp.n_head, HKV = hp.n_head_kv, D = E / H, EKV = HKV * D;
+    const int64_t LQ = E + 2 * EKV;
+    hipStream_t s = m->stream;
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    const int32_t *posp = dev_pos ? m->pos_dev : nullptr;
+    for (int il = m->il0; il < m->il1; ++il) {
+        KLayer &L = m->layers[il - m->il0];
+        const KTensor *t = L.t;
+        const bool kq = kcpp_vec_dot_type(t[1].type) == KT_Q8_K;
+        // attn_norm -> act (Q8_K fused, or f32 then Q8_0)
+        if (kq && kcpp_vec_dot_type(t[2].type) == KT_Q8_K && kcpp_vec_dot_type(t[3].type) == KT_Q8_K) {
+            RC(kcpp_rms_norm(m->x, E, (const float *)t[0].d, nullptr, E, m->act, E, T, hp.eps, s));
+            RC(matmul(m, t[1], nullptr, m->act, T, m->qkv, LQ, nullptr, 0, 0));
+            RC(matmul(m, t[2], nullptr, m->act, T, m->qkv + E, LQ, nullptr, 0, 0));
+            RC(matmul(m, t[3], nullptr, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0));
+        } else {
+            RC(kcpp_rms_norm(m->x, E, (const float *)t[0].d, m->attn, E, nullptr, E, T, hp.eps, s));
+            for (int j = 1; j <= 3; ++j) {
+                RC(kcpp_quantize_act(kcpp_vec_dot_type(t[j].type), m->attn, E, m->act, E, T, s));
+                const int64_t off = j == 1 ? 0 : (j == 2 ? E : E + EKV);
+                RC(matmul(m, t[j], nullptr, m->act, T, m->qkv + off, LQ, nullptr, 0, 0));
+            }
+        }
+        RC(kcpp_rope_kv(m->qkv, LQ, nullptr, m->q16, L.kc, L.vc, T, (int)H, (int)HKV, (int)D, n_past, posp, m->rope_tab, s));
+        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K;
+        RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, (woq && T <= 16) ? m->act : nullptr, m->fa_ws, T, (int)H,
+                           (int)HKV, (int)D, n_past, posp, hp.n_ctx, kq_scale, 0, s));
+        if (!(woq && T <= 16)) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, T, s));
+        RC(matmul(m, t[4], nullptr, m->act, T, m->x, E, m->x, E, 0));                    // x += wo . attn
+        const bool gq = kcpp_vec_dot_type(t[6].type) == KT_Q8_K && kcpp_vec_dot_type(t[7].type) == KT_Q8_K;
+        if (gq) {
+            RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, nullptr, E, m->act, E, T, hp.eps, s));
+        } else {
+            RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, T, hp.eps, s));
+            RC(kcpp_quantize_act(kcpp_vec_dot_type(t[6].type), m->attn, E, m->act, E, T, s));
+        }
+        if (t[6].type == t[7].type) {
+            RC(matmul(m, t[6], &t[7], m->act, T, m->h, F, nullptr, 0, 1));              // h = silu(g) * u
+        } else {
+            RC(matmul(m, t[6], nullptr, m->act, T, m->h, F, nullptr, 0, 0));
+            RC(matmul(m, t[7], nullptr, m->act, T, m->qkv, F, nullptr, 0, 0));
+            RC(kcpp_silu_mul(m->h, m->h, m->qkv, (int64_t)T * F, s));
+        }
+        RC(kcpp_quantize_act(kcpp_vec_dot_type(t[8].type), m->h, F, m->act2, F, T, s));
+        RC(matmul(m, t[8], nullptr, m->act2, T, m->x, E, m->x, E, 0));                   // x += down . h
+    }
+    return 0;
+}
+
+static int head(kcpp_model *m, int T) {
+    const kcpp_hparams &hp = m->hp;
+    const int64_t E = hp.n_embd;
+    const float *last = m->x + (int64_t)(T - 1) * E;
+    if (kcpp_vec_dot_type(m->output.type) == KT_Q8_K) {
+        RC(kcpp_rms_norm(last, E, (const float *)m->output_norm.d, nullptr, E, m->act, E, 1, hp.eps, m->stream));
+    } else {
+        RC(kcpp_rms_norm(last, E, (const float *)m->output_norm.d, m->attn, E, nullptr, E, 1, hp.eps, m->stream));
+        RC(kcpp_quantize_act(kcpp_vec_dot_type(m->output.type), m->attn, E, m->act, E, 1, m->stream));
+    }
+    RC(kcpp_gemv(m->output.type, m->output.d, nullptr, E, hp.n_vocab, m->act, 1, m->logits, hp.n_vocab, nullptr, 0, 0,
+                 m->stream));
+    return 0;
+}
+
+// full single-token step with the inputs read from device memory (graph-capturable)
+static int decode_step_dev(kcpp_model *m) {
+    const kcpp_hparams &hp = m->hp;
+    if (m->has_embed)
+        RC(kcpp_get_rows(m->tok_embd.type, m->tok_embd.d, hp.n_embd, hp.n_vocab, m->tok_dev, 1, m->x, hp.n_embd,
+                         m->stream));
+    RC(forward_layers(m, 1, 0, true));
+    if (m->has_output) RC(head(m, 1));
+    return 0;
+}
+
+extern "C" int kcpp_model_forward_hidden(kcpp_model *m, int T, int n_past) {
+    RT_CHECK(hipSetDevice(m->device));
+    return forward_layers(m, T, n_past, false);
+}
+
+extern "C" int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, int n_past, float *logits_host) {
+    RT_CHECK(hipSetDevice(m->device));
+    const kcpp_hparams &hp = m->hp;
+    if (T < 1 || n_past + T > hp.n_ctx) { g_err = "context overflow"; return -2; }
+    if (T == 1 && m->use_graphs) {
+        m->pin[0] = m->has_embed ? tokens[0] : 0;
+        m->pin[1] = n_past;
+        if (!m->g_exec) {
+            hipGraph_t g;
+            RT_CHECK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
+            hipMemcpyAsync(m->tok_dev, &m->pin[0], 4, hipMemcpyHostToDevice, m->stream);
+            hipMemcpyAsync(m->pos_dev, &m->pin[1], 4, hipMemcpyHostToDevice, m->stream);
+            int rc = decode_step_dev(m);
+            hipError_t e = hipStreamEndCapture(m->stream, &g);
+            if (rc || e != hipSuccess) { g_err = "graph capture failed"; return rc ? rc : -3; }
+            RT_CHECK(hipGraphInstantiate(&m->g_exec, g, nullptr, nullptr, 0));
+            hipGraphDestroy(g);
+        }
+        RT_CHECK(hipGraphLaunch(m->g_exec, m->stream));
+    } else {
+        // split into ubatches (llama_decode_internal, src/llama.cpp:17187-17201)
+        for (int i = 0; i < T; i += m->ub) {
+            const int t = std::min(m->ub, T - i);
+            if (m->has_embed) {
+                RT_CHECK(hipMemcpyAsync(m->tok_dev, tokens + i, (size_t)t * 4, hipMemcpyHostToDevice, m->stream));
+                RC(kcpp_get_rows(m->tok_embd.type, m->tok_embd.d, hp.n_embd, hp.n_vocab, m->tok_dev, t, m->x, hp.n_embd,
+                                 m->stream));
+            }
+            RC(forward_layers(m, t, n_past + i, false));
+            if (m->has_output && i + t == T) RC(head(m, t));
+        }
+    }
+    if (m->has_output && logits_host) {
+        RT_CHECK(hipMemcpyAsync(logits_host, m->logits, (size_t)hp.n_vocab * 4, hipMemcpyDeviceToHost, m->stream));
+    }
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    return 0;
+}
+
+__global__ void k_argmax(const float *__restrict__ x, int n, int32_t *out) {
+    __shared__ float sv[256];
+    __shared__ int si[256];
+    float bv = -INFINITY; int bi = 0;
+    for (int i = threadIdx.x; i < n; i += 256) if (x[i] > bv) { bv = x[i]; bi = i; }
+    sv[threadIdx.x] = bv; si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            const float v2 = sv[threadIdx.x + o]; const int i2 = si[threadIdx.x + o];
+            if (v2 > sv[threadIdx.x] || (v2 == sv[threadIdx.x] && i2 < si[threadIdx.x])) { sv[threadIdx.x] = v2; si[threadIdx.x] = i2; }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = si[0];
+}
+
+extern "C" int kcpp_model_argmax(kcpp_model *m, int32_t *token_out) {
+    if (!m->has_output) return -1;
+    RT_CHECK(hipSetDevice(m->device));
+    hipLaunchKernelGGL(k_argmax, dim3(1), dim3(256), 0, m->stream, m->logits, m->hp.n_vocab, m->argmax_dev);
+    RT_CHECK(hipMemcpyAsync(token_out, m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    return 0;
+}

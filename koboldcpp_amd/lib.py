@@ -1,0 +1,164 @@
+"""ctypes binding of koboldcpp_hipblas.so (include/kcpp_mi355x.h).
+
+Host-side mirror of the reference's operator interface for this path: the same ggml type ids,
+the same op semantics (mul_mat / rms_norm / rope_ext / flash_attn_ext) and the same error
+behaviour (a non-zero return is raised as KcppError instead of aborting the process).
+Fails loudly when the native library is absent -- there is no Python/CPU fallback.
+"""
+import ctypes
+import os
+
+from . import LIB_PATH
+
+F32, F16, Q4_0, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 8, 12, 13, 14, 15
+BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q8_0: (32, 34), Q4_K: (256, 144),
+         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292)}
+
+
+class KcppError(RuntimeError):
+    pass
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError("native library missing: %s (run __graft_entry__.build())" % LIB_PATH)
+
+_L = ctypes.CDLL(LIB_PATH)
+P, I, I64, U64, Fl = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float
+
+_SIGS = {
+    "kcpp_weight_repack": [I, P, P, I64, I64, I, P],
+    "kcpp_weight_synth": [I, U64, U64, P, I64, I64, P],
+    "kcpp_dequantize": [I, P, P, I64, I64, P],
+    "kcpp_get_rows": [I, P, I64, I64, P, I64, P, I64, P],
+    "kcpp_quantize_act": [I, P, I64, P, I64, I64, P],
+    "kcpp_gemv": [I, P, P, I64, I64, P, I64, P, I64, P, I64, I, P],
+    "kcpp_gemm": [I, P, P, I64, I64, P, I64, P, I64, P, I64, I, P, P],
+    "kcpp_rms_norm": [P, I64, P, P, I64, P, I64, I64, Fl, P],
+    "kcpp_rope_table": [P, I, I, Fl, Fl, P, Fl, Fl, Fl, Fl, I],
+    "kcpp_rope_kv": [P, I64, P, P, P, P, I, I, I, I, I, P, P, P],
+    "kcpp_flash_attn": [P, P, P, P, P, P, I, I, I, I, I, P, I, Fl, I, P],
+    "kcpp_add": [P, P, P, I64, P],
+    "kcpp_silu_mul": [P, P, P, I64, P],
+    "kcpp_model_create": [P, P, I, I, I, I, I, I],
+    "kcpp_model_synth_weights": [P, U64],
+    "kcpp_model_set_tensor": [P, I, P, I64],
+    "kcpp_model_free": [P],
+    "kcpp_model_decode": [P, P, I, I, P],
+    "kcpp_model_hidden": [P],
+    "kcpp_model_stream": [P],
+    "kcpp_model_forward_hidden": [P, I, I],
+    "kcpp_model_argmax": [P, P],
+    "kcpp_model_set_graphs": [P, I],
+    "kcpp_model_weight_bytes": [P],
+}
+_RES = {"kcpp_act_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
+        "kcpp_model_create": P, "kcpp_model_hidden": P, "kcpp_model_stream": P, "kcpp_model_weight_bytes": I64,
+        "kcpp_last_error": ctypes.c_char_p, "kcpp_model_free": None}
+_L.kcpp_act_bytes.argtypes = [I, I64, I64]
+_L.kcpp_fa_workspace_bytes.argtypes = [I, I, I]
+_L.kcpp_gemm_workspace_bytes.argtypes = [I, I64, I64, I64]
+_L.kcpp_vec_dot_type.argtypes = [I]
+for _n, _a in _SIGS.items():
+    getattr(_L, _n).argtypes = _a
+for _n, _r in _RES.items():
+    getattr(_L, _n).restype = _r
+
+
+def exported_symbols():
+    return sorted(set(_SIGS) | set(_RES) | {"kcpp_vec_dot_type"})
+
+
+def raw():
+    return _L
+
+
+def _chk(rc, name):
+    if rc != 0:
+        raise KcppError("%s failed rc=%d: %s" % (name, rc, (_L.kcpp_last_error() or b"").decode()))
+
+
+def call(name, *args):
+    _chk(getattr(_L, name)(*args), name)
+
+
+def row_bytes(t, k):
+    e, b = BLOCK[t]
+    return k // e * b
+
+
+def act_bytes(wtype, K, M):
+    return int(_L.kcpp_act_bytes(wtype, K, M))
+
+
+def vec_dot_type(wtype):
+    return int(_L.kcpp_vec_dot_type(wtype))
+
+
+def fa_workspace_bytes(T, H, n_kv):
+    return int(_L.kcpp_fa_workspace_bytes(T, H, n_kv))
+
+
+class HParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")] + \
+               [(n, ctypes.c_float) for n in ("eps", "rope_base", "rope_freq_scale")]
+
+
+def hparams(hp):
+    return HParams(*[int(hp[n]) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")],
+                   float(hp["eps"]), float(hp["rope_base"]), float(hp.get("rope_freq_scale", 1.0)))
+
+
+class Model:
+    """One pipeline stage of a Llama model on one GPU (kcpp_model_*)."""
+
+    def __init__(self, hp, types, device=0, il0=0, il1=None, has_embed=True, has_output=True, max_ubatch=512):
+        self.hp = dict(hp)
+        self._h = hparams(hp)
+        self._t = (ctypes.c_int * len(types))(*types)
+        il1 = hp["n_layer"] if il1 is None else il1
+        self.m = _L.kcpp_model_create(ctypes.byref(self._h), self._t, device, il0, il1, int(has_embed),
+                                      int(has_output), max_ubatch)
+        if not self.m:
+            raise KcppError("kcpp_model_create failed: %s" % (_L.kcpp_last_error() or b"").decode())
+
+    def synth(self, seed):
+        _chk(_L.kcpp_model_synth_weights(self.m, seed), "synth")
+
+    def set_tensor(self, idx, arr):
+        _chk(_L.kcpp_model_set_tensor(self.m, idx, arr.ctypes.data_as(P), arr.nbytes), "set_tensor")
+
+    def decode(self, tokens, n_past, want_logits=True):
+        import numpy as np
+        tok = np.ascontiguousarray(tokens, dtype=np.int32)
+        logits = np.empty(self.hp["n_vocab"], np.float32) if want_logits else None
+        _chk(_L.kcpp_model_decode(self.m, tok.ctypes.data_as(P), len(tok), n_past,
+                                  logits.ctypes.data_as(P) if want_logits else None), "decode")
+        return logits
+
+    def argmax(self):
+        v = ctypes.c_int32(0)
+        _chk(_L.kcpp_model_argmax(self.m, ctypes.byref(v)), "argmax")
+        return v.value
+
+    def forward_hidden(self, T, n_past):
+        _chk(_L.kcpp_model_forward_hidden(self.m, T, n_past), "forward_hidden")
+
+    def hidden_ptr(self):
+        return _L.kcpp_model_hidden(self.m)
+
+    def stream(self):
+        return _L.kcpp_model_stream(self.m)
+
+    def set_graphs(self, on):
+        _L.kcpp_model_set_graphs(self.m, int(on))
+
+    def weight_bytes(self):
+        return int(_L.kcpp_model_weight_bytes(self.m))
+
+    def close(self):
+        if getattr(self, "m", None):
+            _L.kcpp_model_free(self.m)
+            self.m = None
+
+    def __del__(self):
+        self.close()

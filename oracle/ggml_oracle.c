@@ -403,6 +403,11 @@ void orc_rope(const float *x, float *y, int64_t head_dim, int64_t n_heads, int64
     free(cache);
 }
 
+/* Diagnostic switch (not reference behaviour): accumulate V in f32 instead of the reference's
+ * f16 VKQ16 accumulator, to separate f16-accumulation noise from real discrepancies. */
+static int g_fa_f32_accum = 0;
+void orc_set_fa_f32_accum(int on) { g_fa_f32_accum = on; }
+
 /* ggml_compute_forward_flash_attn_ext_f16, F16 K/V branch (ggml.c:15667-15875) */
 void orc_flash_attn_ext(const float *q, const uint16_t *k, const uint16_t *v, int64_t kv_stride,
                         const uint16_t *mask, float *out, int D, int n_q, int n_head,
@@ -417,7 +422,7 @@ void orc_flash_attn_ext(const float *q, const uint16_t *k, const uint16_t *v, in
         uint16_t vkq16[512];
         float vkq32[512];
         const float *pq = q + ((int64_t)iq1 * n_head + h) * D;
-        for (int d = 0; d < D; ++d) { qh[d] = F2H(pq[d]); vkq16[d] = 0; }
+        for (int d = 0; d < D; ++d) { qh[d] = F2H(pq[d]); vkq16[d] = 0; vkq32[d] = 0.0f; }
         float S = 0.0f, M = -INFINITY;
         for (int ic = 0; ic < n_kv; ++ic) {
             const float mv = mask ? H2F(mask[(int64_t)iq1 * n_kv + ic]) : 0.0f;
@@ -432,14 +437,16 @@ void orc_flash_attn_ext(const float *q, const uint16_t *k, const uint16_t *v, in
             if (s > M) {
                 M = s;
                 ms = expf(Mold - M);
-                for (int d = 0; d < D; ++d) vkq16[d] = F2H(H2F(vkq16[d]) * ms);   /* ggml_vec_scale_f16 */
+                if (g_fa_f32_accum) for (int d = 0; d < D; ++d) vkq32[d] *= ms;
+                else for (int d = 0; d < D; ++d) vkq16[d] = F2H(H2F(vkq16[d]) * ms);   /* ggml_vec_scale_f16 */
             } else {
                 vs = expf(s - M);
             }
-            for (int d = 0; d < D; ++d) vkq16[d] = F2H(fmaf(H2F(vr[d]), vs, H2F(vkq16[d])));  /* ggml_vec_mad_f16 */
+            if (g_fa_f32_accum) for (int d = 0; d < D; ++d) vkq32[d] = fmaf(H2F(vr[d]), vs, vkq32[d]);
+            else for (int d = 0; d < D; ++d) vkq16[d] = F2H(fmaf(H2F(vr[d]), vs, H2F(vkq16[d])));  /* ggml_vec_mad_f16 */
             S = S * ms + vs;
         }
-        for (int d = 0; d < D; ++d) vkq32[d] = H2F(vkq16[d]);
+        if (!g_fa_f32_accum) for (int d = 0; d < D; ++d) vkq32[d] = H2F(vkq16[d]);
         const float S_inv = 1.0f / S;
         float *po = out + ((int64_t)iq1 * n_head + h) * D;
         for (int d = 0; d < D; ++d) po[d] = vkq32[d] * S_inv;

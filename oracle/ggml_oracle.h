@@ -57,6 +57,9 @@ void orc_flash_attn_ext(const float *q, const uint16_t *k, const uint16_t *v, in
                         const uint16_t *mask, float *out, int D, int n_q, int n_head,
                         int n_kv, int n_head_kv, float scale, int nthreads);
 
+/* diagnostic: 1 = accumulate V in f32 in orc_flash_attn_ext (NOT the reference's f16 VKQ16) */
+void orc_set_fa_f32_accum(int on);
+
 /* ---------------- Llama forward (build_llama, src/llama.cpp:10453-10620) ---------------- */
 typedef struct {
     int n_vocab, n_embd, n_head, n_head_kv, n_layer, n_ff, n_ctx;

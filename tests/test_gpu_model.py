@@ -1,0 +1,115 @@
+"""End-to-end GPU parity: the Llama runtime (kcpp_model_*) vs the reference ggml graph's golden
+logits (tests/golden/e2e_tiny.npz, from oracle/_ref/ref_llama) and vs the C restatement."""
+import numpy as np
+import pytest
+
+import refharness as R
+
+pytestmark = pytest.mark.gpu
+
+# Parity bar (DESIGN.md "parity bar"):
+#  * vs the C restatement with f32 V-accumulation in attention (same math as the HIP path): tight.
+#  * vs the reference itself: the reference CPU accumulates attention V in f16 (ggml.c:15788,
+#    ggml_vec_mad_f16), the HIP path in f32; on this tiny random model that alone moves logits by
+#    ~0.3% (median) -- measured identically between the restatement-f32 and the reference -- and the
+#    reference's own AVX2 vs scalar builds differ by up to ~0.02.  Teacher-forced comparison.
+TOL_MAX = 0.05
+TOL_MEDIAN_REF = 6e-3
+TOL_MEDIAN_F32 = 1e-4
+
+
+@pytest.fixture(scope="module")
+def K():
+    import torch
+    assert torch.cuda.is_available()
+    import koboldcpp_amd.lib as K
+    return K
+
+
+def run_gpu(K, types, prompt, n_gen, ub=512, graphs=True, hp=R.TINY):
+    m = K.Model(hp, types, max_ubatch=ub)
+    m.set_graphs(graphs)
+    m.synth(1234)
+    out = [m.decode(prompt, 0)]
+    n = len(prompt)
+    for _ in range(n_gen):
+        tok = int(np.argmax(out[-1]))
+        assert m.argmax() == tok
+        out.append(m.decode([tok], n))
+        n += 1
+    m.close()
+    return np.array(out)
+
+
+def run_gpu_forced(K, types, prompt, forced, hp=R.TINY):
+    """prefill, then decode the given tokens (teacher forcing) -> logits per step"""
+    m = K.Model(hp, types)
+    m.synth(1234)
+    out = [m.decode(prompt, 0)]
+    n = len(prompt)
+    for tok in forced:
+        out.append(m.decode([int(tok)], n))
+        n += 1
+    m.close()
+    return np.array(out)
+
+
+def oracle_forced(types, prompt, forced, f32_accum, hp=R.TINY):
+    R.lib().orc_set_fa_f32_accum(int(f32_accum))
+    try:
+        o = R.OracleLlama(hp, types, 1234)
+        out = [o.eval(prompt, 0)]
+        n = len(prompt)
+        for tok in forced:
+            out.append(o.eval([int(tok)], n))
+            n += 1
+    finally:
+        R.lib().orc_set_fa_f32_accum(0)
+    return np.array(out)
+
+
+@pytest.mark.parametrize("tag", ["q4km", "q8_0"])
+def test_e2e_vs_reference_golden(K, golden_e2e, tag):
+    types = [int(t) for t in golden_e2e[tag + "_types"]]
+    prompt = golden_e2e[tag + "_prompt"]
+    L = golden_e2e[tag + "_logits"]
+    forced = golden_e2e[tag + "_tokens"][:-1]          # the reference's own greedy tokens
+    got = run_gpu_forced(K, types, prompt, forced)
+    d = np.abs(got - L)
+    assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_REF, (d.max(), np.median(d))
+    # the same comparison for the restatement with f32 attention accumulation shows the same spread
+    orc32 = oracle_forced(types, prompt, forced, True)
+    d32 = np.abs(orc32 - L)
+    assert np.median(d) < 2 * np.median(d32) + 1e-4
+    # and the HIP path equals that restatement up to fp32 summation order
+    e = np.abs(got - orc32)
+    assert np.median(e) < TOL_MEDIAN_F32 and e.max() < TOL_MAX, (np.median(e), e.max())
+
+
+def test_graph_replay_matches_eager(K):
+    types = R.q4_k_m_types(R.TINY["n_layer"])
+    prompt = list(range(3, 20))
+    a = run_gpu(K, types, prompt, 6, graphs=True)
+    b = run_gpu(K, types, prompt, 6, graphs=False)
+    assert np.array_equal(a, b)
+
+
+def test_ubatch_split_matches_single_batch(K):
+    types = R.q4_k_m_types(R.TINY["n_layer"])
+    prompt = [int(v) for v in np.random.default_rng(2).integers(1, 500, size=150)]
+    a = run_gpu(K, types, prompt, 2, ub=512)
+    b = run_gpu(K, types, prompt, 2, ub=64)
+    np.testing.assert_allclose(a, b, rtol=0, atol=TOL_MAX)
+
+
+@pytest.mark.parametrize("types_fn", [lambda n: R.uniform_types(n, R.Q4_0, R.Q6_K),
+                                      lambda n: R.uniform_types(n, R.Q5_K, R.Q8_0)])
+def test_e2e_vs_oracle_other_types(K, types_fn):
+    hp = dict(R.TINY)
+    types = types_fn(hp["n_layer"])
+    prompt = [int(v) for v in np.random.default_rng(7).integers(1, 500, size=45)]
+    got = run_gpu(K, types, prompt, 4)
+    forced = np.argmax(got, axis=1)[:-1]
+    orc32 = oracle_forced(types, prompt, forced, True)
+    d = np.abs(got - orc32)
+    assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_F32, (d.max(), np.median(d))
