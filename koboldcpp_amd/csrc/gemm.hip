@@ -1,21 +1,388 @@
-// gemm.hip -- batched (prefill) quantized mat-mul.
+// gemm.hip -- batched (prefill / ubatch) quantized mat-mul on CDNA4 matrix cores.
+//
+// Replaces the reference's batched paths -- mul_mat_q (ggml/src/ggml-cuda/mmq.cuh:2572-2905, DP4A
+// on AMD, no MFMA) and the default ROCm "dequantize the whole weight to F16 + hipblasGemmEx with
+// FP16 compute" path (ggml-cuda.cu:1186-1284) -- while computing exactly what the CPU vec_dot does
+// (ggml-quants.c:3922,5519,7714,8282,8919): weights x CPU-quantized activations (Q8_K / Q8_0) as
+// exact integer block dots, scaled per super-block (or per 32-block) in fp32.
+//
+// How the integer dot stays exact on f16 MFMA (v_mfma_f32_32x32x16_f16, fp32 accumulate):
+//   * activations are int8 values -> exact in f16;
+//   * the weight operand is the *integer* sub-block product sc*q (Q4_K <= 945, Q5_K <= 1953:
+//     exact in f16), or for Q6_K sc*(q-32) split as 8*(sc>>3)*(q-32) + (sc&7)*(q-32), both
+//     exact, accumulated into the same fp32 accumulator by two MFMAs;
+//   * products are exact and partial sums stay < 2^24, so the fp32 accumulator holds the same
+//     integer as the CPU's int32 `sumi`; Q4_K/Q5_K mins use a 16-deep MFMA over the Q8_K bsums.
+// Dequantization to those f16 integers costs 2 VALU ops per pair of weights (v_perm_b32 builds
+// 1024+q halves, v_pk_fma_f16 scales and removes the 1024 bias exactly).
+//
+// Tiling: workgroup = 4 waves = 128 tokens x 64 weight rows, K step 256.  The 64x256 weight tile
+// is dequantized once per workgroup into LDS in MFMA-fragment order (ds_read_b128 per lane,
+// conflict-free); each wave owns 32 tokens x 64 rows (two 32x32 MFMA tiles).
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
-int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, int64_t Mtot,
-              int64_t c0, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *stream);
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+typedef float f16acc __attribute__((ext_vector_type(16)));
+
+#define GB_M 128
+#define GB_N 64
+#define GB_K 256
+
+// ---------------------------------------------------------------- activation -> f16 operand
+// a16 [Mp][K] f16 (int8 values), dy [Mp][K/G] f32 (copied), bs16 [Mp][K/16] f16 (Q8_K bsums)
+__global__ void k_act_to_f16(const uint8_t *__restrict__ act, int vt, int64_t K, int64_t M, int64_t Mp,
+                             _Float16 *__restrict__ a16, float *__restrict__ dy, _Float16 *__restrict__ bs16) {
+    const int64_t m = blockIdx.y;
+    const int64_t G = vt == KT_Q8_K ? 256 : 32;
+    const bool valid = m < M;
+    const int8_t *qs = (const int8_t *)act + m * K;
+    for (int64_t i = (int64_t)threadIdx.x * 4 + (int64_t)blockIdx.x * 1024; i < K && i < ((int64_t)blockIdx.x + 1) * 1024;
+         i += (int64_t)blockDim.x * 4) {
+        const int v = valid ? *(const int *)(qs + i) : 0;
+        a16[m * K + i + 0] = (_Float16)(int8_t)(v & 0xFF);
+        a16[m * K + i + 1] = (_Float16)(int8_t)((v >> 8) & 0xFF);
+        a16[m * K + i + 2] = (_Float16)(int8_t)((v >> 16) & 0xFF);
+        a16[m * K + i + 3] = (_Float16)(int8_t)((v >> 24) & 0xFF);
+    }
+    if (blockIdx.x == 0) {
+        const float *d = (const float *)(act + M * K) + m * (K / G);
+        for (int64_t i = threadIdx.x; i < K / G; i += blockDim.x) dy[m * (K / G) + i] = valid ? d[i] : 0.0f;
+        if (vt == KT_Q8_K) {
+            const int16_t *bs = (const int16_t *)(act + M * K + M * (K / 256) * 4) + m * (K / 16);
+            for (int64_t i = threadIdx.x; i < K / 16; i += blockDim.x) bs16[m * (K / 16) + i] = valid ? (_Float16)bs[i] : (_Float16)0;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- dequant helpers
+// 4 bytes b0..b3 (each < 256 - 1024 offset trick requires b < 1024) -> two h2v holding 1024+b
+__device__ __forceinline__ h2v bias_lo(uint32_t t) { return __builtin_bit_cast(h2v, __builtin_amdgcn_perm(t, 0x64646464u, 0x0c050c04u)); }
+__device__ __forceinline__ h2v bias_hi(uint32_t t) { return __builtin_bit_cast(h2v, __builtin_amdgcn_perm(t, 0x64646464u, 0x0c070c06u)); }
+
+// (1024 + q) * s - (1024 + off) * s  ==  (q - off) * s   exactly (single rounding of an exact value)
+__device__ __forceinline__ h2v scale2(h2v x, _Float16 s, _Float16 bias) {
+    const h2v sv = {s, s};
+    const h2v bv = {bias, bias};
+    return __builtin_elementwise_fma(x, sv, bv);
+}
+// 8 weights (two dwords of bytes) -> fragment of 8 halves, (byte - off) * s
+__device__ __forceinline__ h8v frag8(uint32_t t0, uint32_t t1, float s, float off) {
+    const _Float16 sh = (_Float16)s;
+    const _Float16 bh = (_Float16)(-(1024.0f + off) * s);
+    const h2v a = scale2(bias_lo(t0), sh, bh), b = scale2(bias_hi(t0), sh, bh);
+    const h2v c = scale2(bias_lo(t1), sh, bh), d = scale2(bias_hi(t1), sh, bh);
+    h8v r;
+    r[0] = a[0]; r[1] = a[1]; r[2] = b[0]; r[3] = b[1]; r[4] = c[0]; r[5] = c[1]; r[6] = d[0]; r[7] = d[1];
+    return r;
+}
+
+// Q6_K variant: (byte - off) exactly first (small ints), then * s (exact: |8*(sc>>3)*(q-32)| <= 4096,
+// a multiple of 8; |(sc&7)*(q-32)| <= 224).  A single fma would need a bias beyond the f16 range.
+__device__ __forceinline__ h8v frag8_sub(uint32_t t0, uint32_t t1, float s, float off) {
+    const h2v sv = {(_Float16)s, (_Float16)s};
+    const h2v bv = {(_Float16)(-(1024.0f + off)), (_Float16)(-(1024.0f + off))};
+    const h2v a = (bias_lo(t0) + bv) * sv, b = (bias_hi(t0) + bv) * sv;
+    const h2v c = (bias_lo(t1) + bv) * sv, d = (bias_hi(t1) + bv) * sv;
+    h8v r;
+    r[0] = a[0]; r[1] = a[1]; r[2] = b[0]; r[3] = b[1]; r[4] = c[0]; r[5] = c[1]; r[6] = d[0]; r[7] = d[1];
+    return r;
+}
+
+// get_scale_min_k4 (ggml-quants.c:1899) on the 12 scale bytes held in hdr.y/z/w (registers only)
+__device__ __forceinline__ void k4_sm(const uint4 &hdr, int j, int &d, int &m) {
+    auto b = [&](int k) -> int {
+        const uint32_t w = k < 4 ? hdr.y : (k < 8 ? hdr.z : hdr.w);
+        return (w >> (8 * (k & 3))) & 0xFF;
+    };
+    if (j < 4) { d = b(j) & 63; m = b(j + 4) & 63; }
+    else { d = (b(j + 4) & 0xF) | ((b(j - 4) >> 6) << 4); m = (b(j + 4) >> 4) | ((b(j) >> 6) << 4); }
+}
+
+// fragment slot for element k (0..255) of weight row nl (0..63): (tile, step, lane); 16 B per slot
+__device__ __forceinline__ int bslot(int nl, int k) {
+    const int tile = nl >> 5, s = k >> 4, h = (k >> 3) & 1;
+    return ((tile * 16 + s) * 64 + h * 32 + (nl & 31));
+}
+
+template <int TYPE> struct GemmTraits {
+    static constexpr int NB = 1;            // B fragment planes (Q6_K: 2)
+    static constexpr bool MINS = false;     // Q8_K bsum x mins term
+    static constexpr bool SB = true;        // per-256 scaling (K-quants) vs per-32 (Q4_0/Q8_0)
+};
+template <> struct GemmTraits<KT_Q4_K> { static constexpr int NB = 1; static constexpr bool MINS = true; static constexpr bool SB = true; };
+template <> struct GemmTraits<KT_Q5_K> { static constexpr int NB = 1; static constexpr bool MINS = true; static constexpr bool SB = true; };
+template <> struct GemmTraits<KT_Q6_K> { static constexpr int NB = 2; static constexpr bool MINS = false; static constexpr bool SB = true; };
+template <> struct GemmTraits<KT_Q4_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
+template <> struct GemmTraits<KT_Q8_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
+
+template <int NB> struct GemmSmem {
+    h8v bf[NB][2 * 16 * 64];      // [plane][tile*16*64 + step*64 + lane]
+    h8v bm[2 * 64];               // mins fragment [tile*64 + lane]
+    float wd[GB_N][8];            // K-quants: [0]=d, [1]=dmin ; Q4_0/Q8_0: d per 32-block
+    float dy[GB_M][8];            // K-quants: [0]=dy of this super-block ; Q4_0/Q8_0: per 32-block
+};
+
+// dequantize the 64 x 256 weight tile of super-block `sb` into LDS (thread t: row t>>2, chunk t&3)
+template <int TYPE, typename SM>
+__device__ __forceinline__ void stage_weights(SM &S, const uint8_t *__restrict__ W, int64_t K, int64_t N,
+                                              int64_t n0, int64_t sb) {
+    const int t = threadIdx.x, nl = t >> 2, c = t & 3;
+    const int64_t n = min(n0 + nl, N - 1);
+    const int64_t bpr = K / ks_block_elems(TYPE);
+    const int64_t nbt = bpr * N;
+    if constexpr (TYPE == KT_Q4_K || TYPE == KT_Q5_K) {
+        const int BB = TYPE == KT_Q4_K ? 144 : 176;
+        const uint8_t *blk = W + (n * bpr + sb) * BB;
+        const uint4 hdr = *(const uint4 *)blk;
+        const uint4 q0 = *(const uint4 *)(blk + (TYPE == KT_Q4_K ? 16 : 48) + 32 * c);
+        const uint4 q1 = *(const uint4 *)(blk + (TYPE == KT_Q4_K ? 32 : 64) + 32 * c);
+        uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0;
+        if constexpr (TYPE == KT_Q5_K) { h0 = *(const uint4 *)(blk + 16); h1 = *(const uint4 *)(blk + 32); }
+        int s0, m0, s1, m1;
+        k4_sm(hdr, 2 * c, s0, m0);
+        k4_sm(hdr, 2 * c + 1, s1, m1);
+        const uint32_t qd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        const uint32_t hd[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t lo0 = qd[2 * i] & 0x0F0F0F0Fu, lo1 = qd[2 * i + 1] & 0x0F0F0F0Fu;
+            uint32_t hi0 = (qd[2 * i] >> 4) & 0x0F0F0F0Fu, hi1 = (qd[2 * i + 1] >> 4) & 0x0F0F0F0Fu;
+            if constexpr (TYPE == KT_Q5_K) {
+                lo0 |= ((hd[2 * i] >> (2 * c)) & 0x01010101u) << 4;
+                lo1 |= ((hd[2 * i + 1] >> (2 * c)) & 0x01010101u) << 4;
+                hi0 |= ((hd[2 * i] >> (2 * c + 1)) & 0x01010101u) << 4;
+                hi1 |= ((hd[2 * i + 1] >> (2 * c + 1)) & 0x01010101u) << 4;
+            }
+            S.bf[0][bslot(nl, 64 * c + 8 * i)] = frag8(lo0, lo1, (float)s0, 0.0f);
+            S.bf[0][bslot(nl, 64 * c + 32 + 8 * i)] = frag8(hi0, hi1, (float)s1, 0.0f);
+        }
+        // mins fragment: k = g (0..15) holds m_{g/2}; this thread owns g = 4c..4c+3
+        _Float16 *bm = (_Float16 *)&S.bm[(nl >> 5) * 64 + (c >> 1) * 32 + (nl & 31)] + 4 * (c & 1);
+        bm[0] = (_Float16)m0; bm[1] = (_Float16)m0; bm[2] = (_Float16)m1; bm[3] = (_Float16)m1;
+        if (c == 0) {
+            S.wd[nl][0] = h2f((uint16_t)(hdr.x & 0xFFFF));
+            S.wd[nl][1] = h2f((uint16_t)(hdr.x >> 16));
+        }
+    } else if constexpr (TYPE == KT_Q6_K) {
+        const int64_t b = n * bpr + sb;
+        const uint8_t *q = W + b * 192;
+        const int8_t *scp = (const int8_t *)(W + nbt * 192 + b * 16);
+        const int hh = c >> 1;                   // 128-element half
+        const int pb = 2 * (c & 1);              // planes pb, pb+1
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+            const int p = pb + pp;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint2 ql = *(const uint2 *)(q + 64 * hh + 32 * (p & 1) + 8 * i);
+                const uint2 qh = *(const uint2 *)(q + 128 + 32 * hh + 8 * i);
+                const int sh4 = 4 * (p >> 1);
+                const uint32_t v0 = ((ql.x >> sh4) & 0x0F0F0F0Fu) | (((qh.x >> (2 * p)) & 0x03030303u) << 4);
+                const uint32_t v1 = ((ql.y >> sh4) & 0x0F0F0F0Fu) | (((qh.y >> (2 * p)) & 0x03030303u) << 4);
+                const int scv = scp[8 * hh + (i >> 1) + 2 * p];
+                const int shi = scv >> 3, slo = scv & 7;
+                const int k = 128 * hh + 32 * p + 8 * i;
+                S.bf[0][bslot(nl, k)] = frag8_sub(v0, v1, (float)(8 * shi), 32.0f);
+                S.bf[1][bslot(nl, k)] = frag8_sub(v0, v1, (float)slo, 32.0f);
+            }
+        }
+        if (c == 0) S.wd[nl][0] = h2f(*(const uint16_t *)(W + nbt * 208 + b * 2));
+    } else if constexpr (TYPE == KT_Q4_0) {
+        // this thread: 32-blocks 2c, 2c+1 of the 8 in the super-step
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int jb = 2 * c + bb;
+            const int64_t b = n * bpr + sb * 8 + jb;
+            const uint4 qv = *(const uint4 *)(W + b * 16);
+            const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
+            S.bf[0][bslot(nl, 32 * jb + 0)] = frag8(qd[0] & 0x0F0F0F0Fu, qd[1] & 0x0F0F0F0Fu, 1.0f, 8.0f);
+            S.bf[0][bslot(nl, 32 * jb + 8)] = frag8(qd[2] & 0x0F0F0F0Fu, qd[3] & 0x0F0F0F0Fu, 1.0f, 8.0f);
+            S.bf[0][bslot(nl, 32 * jb + 16)] = frag8((qd[0] >> 4) & 0x0F0F0F0Fu, (qd[1] >> 4) & 0x0F0F0F0Fu, 1.0f, 8.0f);
+            S.bf[0][bslot(nl, 32 * jb + 24)] = frag8((qd[2] >> 4) & 0x0F0F0F0Fu, (qd[3] >> 4) & 0x0F0F0F0Fu, 1.0f, 8.0f);
+            S.wd[nl][jb] = h2f(*(const uint16_t *)(W + nbt * 16 + b * 2));
+        }
+    } else {   // Q8_0: int8 -> (q ^ 0x80) = q + 128 as a byte
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int jb = 2 * c + bb;
+            const int64_t b = n * bpr + sb * 8 + jb;
+            const uint4 q0 = *(const uint4 *)(W + b * 32), q1 = *(const uint4 *)(W + b * 32 + 16);
+            const uint32_t qd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                S.bf[0][bslot(nl, 32 * jb + 8 * i)] = frag8(qd[2 * i] ^ 0x80808080u, qd[2 * i + 1] ^ 0x80808080u, 1.0f, 128.0f);
+            S.wd[nl][jb] = h2f(*(const uint16_t *)(W + nbt * 32 + b * 2));
+        }
+    }
+}
+
+template <int TYPE>
+__global__ void __launch_bounds__(256) k_gemm(const uint8_t *__restrict__ W, int64_t K, int64_t N,
+                                              const _Float16 *__restrict__ a16, const float *__restrict__ dyg,
+                                              const _Float16 *__restrict__ bs16, int64_t M, float *__restrict__ Y,
+                                              int64_t ldy, const float *res, int64_t ldr) {
+    using T = GemmTraits<TYPE>;
+    __shared__ GemmSmem<T::NB> S;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t n0 = (int64_t)blockIdx.x * GB_N, m0 = (int64_t)blockIdx.y * GB_M;
+    const int64_t nsb = K / GB_K;
+    const int64_t G = T::SB ? 256 : 32;
+    const int lr = lane & 31, lh = lane >> 5;
+    const int64_t arow = m0 + 32 * wave + lr;                  // token row this lane feeds into A
+    const _Float16 *ap = a16 + arow * K + 8 * lh;
+    f16acc tot[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { tot[0][i] = 0.0f; tot[1][i] = 0.0f; }
+
+    for (int64_t sb = 0; sb < nsb; ++sb) {
+        __syncthreads();                                        // previous step done with LDS
+        stage_weights<TYPE>(S, W, K, N, n0, sb);
+        if (threadIdx.x < GB_M) {
+            if constexpr (T::SB) S.dy[threadIdx.x][0] = dyg[(m0 + threadIdx.x) * (K / 256) + sb];
+            else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) S.dy[threadIdx.x][j] = dyg[(m0 + threadIdx.x) * (K / 32) + sb * 8 + j];
+            }
+        }
+        __syncthreads();
+        if constexpr (T::SB) {
+            f16acc acc[2], accm[2];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { acc[0][i] = acc[1][i] = 0.0f; accm[0][i] = accm[1][i] = 0.0f; }
+#pragma unroll 4
+            for (int s = 0; s < 16; ++s) {
+                const h8v a = *(const h8v *)(ap + sb * GB_K + 16 * s);
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl) {
+                    acc[tl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, S.bf[0][(tl * 16 + s) * 64 + lane], acc[tl], 0, 0, 0);
+                    if constexpr (T::NB == 2)
+                        acc[tl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, S.bf[T::NB - 1][(tl * 16 + s) * 64 + lane], acc[tl], 0, 0, 0);
+                }
+            }
+            if constexpr (T::MINS) {
+                const h8v am = *(const h8v *)(bs16 + arow * (K / 16) + sb * 16 + 8 * lh);
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl)
+                    accm[tl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, S.bm[tl * 64 + lane], accm[tl], 0, 0, 0);
+            }
+            // epilogue: tot += dy*d*sumi - dy*dmin*summ  (ggml_vec_dot_q4_K_q8_K, ggml-quants.c:7796-7859)
+#pragma unroll
+            for (int tl = 0; tl < 2; ++tl) {
+                const float dw = S.wd[tl * 32 + lr][0];
+                const float dm = T::MINS ? S.wd[tl * 32 + lr][1] : 0.0f;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int tk = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                    const float dy = S.dy[tk][0];
+                    float v = __fmul_rn(__fmul_rn(dy, dw), acc[tl][r]);
+                    if constexpr (T::MINS) v = __fsub_rn(v, __fmul_rn(__fmul_rn(dy, dm), accm[tl][r]));
+                    tot[tl][r] = __fadd_rn(tot[tl][r], v);
+                }
+            }
+        } else {
+#pragma unroll 2
+            for (int jb = 0; jb < 8; ++jb) {
+                f16acc acc[2];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[0][i] = acc[1][i] = 0.0f;
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    const int s = 2 * jb + ss;
+                    const h8v a = *(const h8v *)(ap + sb * GB_K + 16 * s);
+#pragma unroll
+                    for (int tl = 0; tl < 2; ++tl)
+                        acc[tl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, S.bf[0][(tl * 16 + s) * 64 + lane], acc[tl], 0, 0, 0);
+                }
+                // tot += sumi * (d_w * d_a)   (ggml_vec_dot_q8_0_q8_0 scalar tail, ggml-quants.c:5519)
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl) {
+                    const float dw = S.wd[tl * 32 + lr][jb];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const int tk = 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                        tot[tl][r] = __fadd_rn(tot[tl][r], __fmul_rn(acc[tl][r], __fmul_rn(dw, S.dy[tk][jb])));
+                    }
+                }
+            }
+        }
+    }
+    // store (+ residual)
+#pragma unroll
+    for (int tl = 0; tl < 2; ++tl) {
+        const int64_t n = n0 + tl * 32 + lr;
+        if (n >= N) continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t t = m0 + 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[tl][r], res[t * ldr + n]) : tot[tl][r];
+        }
+    }
+}
+
+__global__ void k_silu_mul_strided(float *__restrict__ y, int64_t ldy, const float *__restrict__ u, int64_t N, int64_t M) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N * M) return;
+    const int64_t m = i / N, n = i % N;
+    const float g = y[m * ldy + n];
+    y[m * ldy + n] = (g / (1.0f + expf(-g))) * u[i];
+}
+
+static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a16, int64_t &o_dy, int64_t &o_bs, int64_t &o_up) {
+    const int64_t Mp = (M + GB_M - 1) / GB_M * GB_M;
+    const int64_t G = (type == KT_Q4_0 || type == KT_Q8_0) ? 32 : 256;
+    int64_t off = 0;
+    o_a16 = off; off += (Mp * K * 2 + 255) & ~255LL;
+    o_dy = off; off += (Mp * (K / G) * 4 + 255) & ~255LL;
+    o_bs = off; off += (Mp * (K / 16) * 2 + 255) & ~255LL;
+    o_up = off; off += (M * N * 4 + 255) & ~255LL;
+    return off;
+}
 
 extern "C" {
 
-int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M) { return 0; }
+int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M) {
+    int64_t a, b, c, d;
+    return ws_layout(type, K, N, M, a, b, c, d);
+}
 
 int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream) {
-    for (int64_t c0 = 0; c0 < M; c0 += 8) {
-        const int64_t mc = M - c0 < 8 ? M - c0 : 8;
-        int rc = gemv_cols(type, W, W2, K, N, act, mc, M, c0, Y, ldy, res, ldr, mode, stream);
-        if (rc) return rc;
-    }
+    hipStream_t s = (hipStream_t)stream;
+    if (K % GB_K) return -1;
+    if (!ws) return -2;
+    int64_t o_a16, o_dy, o_bs, o_up;
+    ws_layout(type, K, N, M, o_a16, o_dy, o_bs, o_up);
+    const int64_t Mp = (M + GB_M - 1) / GB_M * GB_M;
+    uint8_t *w8 = (uint8_t *)ws;
+    _Float16 *a16 = (_Float16 *)(w8 + o_a16);
+    float *dy = (float *)(w8 + o_dy);
+    _Float16 *bs16 = (_Float16 *)(w8 + o_bs);
+    float *up = (float *)(w8 + o_up);
+    const int vt = vec_dot_type(type);
+    hipLaunchKernelGGL(k_act_to_f16, dim3((unsigned)((K + 1023) / 1024), (unsigned)Mp), dim3(256), 0, s,
+                       (const uint8_t *)act, vt, K, M, Mp, a16, dy, bs16);
+    KCPP_CHECK(hipGetLastError());
+    const dim3 grid((unsigned)((N + GB_N - 1) / GB_N), (unsigned)(Mp / GB_M));
+    auto launch = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
+        switch (type) {
+        case KT_Q4_K: hipLaunchKernelGGL(k_gemm<KT_Q4_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
+        case KT_Q5_K: hipLaunchKernelGGL(k_gemm<KT_Q5_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
+        case KT_Q6_K: hipLaunchKernelGGL(k_gemm<KT_Q6_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
+        case KT_Q4_0: hipLaunchKernelGGL(k_gemm<KT_Q4_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
+        case KT_Q8_0: hipLaunchKernelGGL(k_gemm<KT_Q8_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
+        default: return -3;
+        }
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    };
+    int rc = launch(W, Y, ldy, mode == 1 ? nullptr : res, ldr);
+    if (rc || mode != 1) return rc;
+    rc = launch(W2, up, N, nullptr, 0);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_silu_mul_strided, dim3((unsigned)((N * M + 255) / 256)), dim3(256), 0, s, Y, ldy, up, N, M);
+    KCPP_CHECK(hipGetLastError());
     return 0;
 }
 
