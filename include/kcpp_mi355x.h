@@ -98,6 +98,8 @@ void kcpp_model_free(kcpp_model *m);
 int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, int n_past, float *logits_host);
 /* device pointers of this stage's residual stream [max_ubatch][n_embd] f32 (pipeline handoff) */
 float *kcpp_model_hidden(kcpp_model *m);
+/* copy n floats of the residual stream starting at float offset (debug / pipeline host path) */
+int kcpp_model_read_hidden(kcpp_model *m, float *host, int64_t n_floats, int64_t offset);
 void *kcpp_model_stream(kcpp_model *m);
 /* per-stage step without embedding/out: run layers on the hidden buffer for T tokens */
 int kcpp_model_forward_hidden(kcpp_model *m, int T, int n_past);

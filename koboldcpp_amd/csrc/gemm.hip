@@ -57,9 +57,10 @@ __global__ void k_act_to_f16(const uint8_t *__restrict__ act, int vt, int64_t K,
 }
 
 // ---------------------------------------------------------------- dequant helpers
-// 4 bytes b0..b3 (each < 256 - 1024 offset trick requires b < 1024) -> two h2v holding 1024+b
-__device__ __forceinline__ h2v bias_lo(uint32_t t) { return __builtin_bit_cast(h2v, __builtin_amdgcn_perm(t, 0x64646464u, 0x0c050c04u)); }
-__device__ __forceinline__ h2v bias_hi(uint32_t t) { return __builtin_bit_cast(h2v, __builtin_amdgcn_perm(t, 0x64646464u, 0x0c070c06u)); }
+// v_perm_b32 byte selects: 4..7 = bytes of src0 (t), 0..3 = bytes of src1 (0x64 each):
+// bytes (b0,0x64,b1,0x64) are the f16 halves 1024+b0, 1024+b1 (exact for b < 1024)
+__device__ __forceinline__ h2v bias_lo(uint32_t t) { return __builtin_bit_cast(h2v, __builtin_amdgcn_perm(t, 0x64646464u, 0x00050004u)); }
+__device__ __forceinline__ h2v bias_hi(uint32_t t) { return __builtin_bit_cast(h2v, __builtin_amdgcn_perm(t, 0x64646464u, 0x00070006u)); }
 
 // (1024 + q) * s - (1024 + off) * s  ==  (q - off) * s   exactly (single rounding of an exact value)
 __device__ __forceinline__ h2v scale2(h2v x, _Float16 s, _Float16 bias) {

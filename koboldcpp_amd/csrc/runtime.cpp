@@ -255,6 +255,12 @@ extern "C" int kcpp_model_set_tensor(kcpp_model *m, int idx, const void *src, in
 }
 
 extern "C" float *kcpp_model_hidden(kcpp_model *m) { return m->x; }
+extern "C" int kcpp_model_read_hidden(kcpp_model *m, float *host, int64_t n_floats, int64_t offset) {
+    RT_CHECK(hipSetDevice(m->device));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    RT_CHECK(hipMemcpy(host, m->x + offset, (size_t)n_floats * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
 extern "C" void *kcpp_model_stream(kcpp_model *m) { return m->stream; }
 extern "C" int64_t kcpp_model_weight_bytes(kcpp_model *m) { return m->weight_bytes; }
 extern "C" int kcpp_model_set_graphs(kcpp_model *m, int enable) {
@@ -298,8 +304,9 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
         }
         RC(kcpp_rope_kv(m->qkv, LQ, nullptr, m->q16, L.kc, L.vc, T, (int)H, (int)HKV, (int)D, n_past, posp, m->rope_tab, s));
         const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K;
+        static const int fa_force = getenv("KCPP_FA_PATH") ? atoi(getenv("KCPP_FA_PATH")) : 0;
         RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, (woq && T <= 16) ? m->act : nullptr, m->fa_ws, T, (int)H,
-                           (int)HKV, (int)D, n_past, posp, hp.n_ctx, kq_scale, 0, s));
+                           (int)HKV, (int)D, n_past, posp, hp.n_ctx, kq_scale, fa_force, s));
         if (!(woq && T <= 16)) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, T, s));
         RC(matmul(m, t[4], nullptr, m->act, T, m->x, E, m->x, E, 0));                    // x += wo . attn
         const bool gq = kcpp_vec_dot_type(t[6].type) == KT_Q8_K && kcpp_vec_dot_type(t[7].type) == KT_Q8_K;

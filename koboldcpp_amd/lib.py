@@ -45,6 +45,7 @@ _SIGS = {
     "kcpp_model_free": [P],
     "kcpp_model_decode": [P, P, I, I, P],
     "kcpp_model_hidden": [P],
+    "kcpp_model_read_hidden": [P, P, I64, I64],
     "kcpp_model_stream": [P],
     "kcpp_model_forward_hidden": [P, I, I],
     "kcpp_model_argmax": [P, P],
@@ -142,6 +143,12 @@ class Model:
 
     def forward_hidden(self, T, n_past):
         _chk(_L.kcpp_model_forward_hidden(self.m, T, n_past), "forward_hidden")
+
+    def read_hidden(self, n, offset=0):
+        import numpy as np
+        out = np.empty(n, np.float32)
+        _chk(_L.kcpp_model_read_hidden(self.m, out.ctypes.data_as(P), n, offset), "read_hidden")
+        return out
 
     def hidden_ptr(self):
         return _L.kcpp_model_hidden(self.m)

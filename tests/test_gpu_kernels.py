@@ -269,3 +269,52 @@ def test_flash_attn_golden(env, golden_ops, key):
     K.call("kcpp_flash_attn", qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), None, ws.data_ptr(), T, H,
            HKV, D, n_past, None, n_kv, 1.0 / np.sqrt(D), 0, sptr(torch))
     np.testing.assert_allclose(host(torch, out, np.float32).reshape(q.shape), golden_ops[key + "_y"], rtol=4e-3, atol=4e-3)
+
+
+@pytest.mark.parametrize("T,n_past,path", [(1, 0, 1), (1, 1000, 1), (5, 295, 1), (16, 300, 1), (16, 300, 2),
+                                           (17, 0, 2), (37, 0, 2), (40, 0, 2), (70, 130, 2), (200, 60, 2)])
+def test_flash_attn_vs_oracle_f32_accum(env, T, n_past, path):
+    """Same math as the HIP kernels (f32 V accumulation): must agree to fp32 rounding."""
+    torch, K = env
+    H, HKV, D = 32, 8, 128
+    n_ctx = 1024
+    rng = np.random.default_rng(T * 7 + n_past)
+    n_kv = n_past + T
+    q = rng.standard_normal((T, H, D)).astype(np.float32)
+    kcache = (rng.standard_normal((n_ctx, HKV, D)) * 0.5).astype(np.float16)
+    vcache = rng.standard_normal((n_ctx, HKV, D)).astype(np.float16)
+    mask = np.zeros((T, n_kv), np.float16)
+    for t in range(T):
+        mask[t, n_past + t + 1:] = -np.inf
+    R.lib().orc_set_fa_f32_accum(1)
+    try:
+        want = R.flash_attn(q, kcache[:n_kv], vcache[:n_kv], mask)
+    finally:
+        R.lib().orc_set_fa_f32_accum(0)
+    q16 = dev(torch, q.astype(np.float16))
+    kd, vd = dev(torch, kcache), dev(torch, vcache)
+    out = torch.empty((T, H, D), dtype=torch.float32, device="cuda")
+    ws = empty(torch, K.fa_workspace_bytes(max(T, 16), H, n_ctx))
+    K.call("kcpp_flash_attn", q16.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), None, ws.data_ptr(), T, H,
+           HKV, D, n_past, None, n_ctx, 1.0 / np.sqrt(D), path, sptr(torch))
+    got = host(torch, out, np.float32).reshape(T, H, D)
+    np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("t", TYPES)
+@pytest.mark.parametrize("Kd,N", [(512, 128), (512, 512), (512, 1024), (1024, 512)])
+@pytest.mark.parametrize("M", [17, 37])
+def test_gemm_small_shapes(env, t, Kd, N, M):
+    torch, K = env
+    rng = np.random.default_rng(Kd + N + M + t)
+    w = R.synth(t, 3, 500 + t, Kd, N)
+    w2 = R.synth(t, 3, 600 + t, Kd, N)
+    X = rng.standard_normal((M, Kd)).astype(np.float32)
+    res = rng.standard_normal((M, N)).astype(np.float32)
+    a = R.mul_mat(t, w, Kd, N, X)
+    b = R.mul_mat(t, w2, Kd, N, X)
+    tol = 3e-6 * max(1.0, np.abs(a).max())
+    np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X), a, rtol=0, atol=tol)
+    np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, res=res), a + res, rtol=0, atol=tol + 1e-6)
+    glu = (a / (1 + np.exp(-a))) * b
+    np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, mode=1, w2=w2), glu, rtol=1e-5, atol=tol)
