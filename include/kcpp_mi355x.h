@@ -55,6 +55,12 @@ int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M);
 int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream);
 
+/* Fused single-token mat-vec (koboldcpp_amd/csrc/gemv_dec.hip): args points at a DecArgs struct
+ * (koboldcpp_amd/csrc/kcpp_internal.h, size kcpp_gemv_dec_args_size()).  mode 0 plain(+res),
+ * 1 silu-GLU, 2 RoPE + K/V-cache store; pro 0 act given, 1 rms_norm+quantize prologue, 2 quantize. */
+int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream);
+int64_t kcpp_gemv_dec_args_size(void);
+
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,
                   int64_t nrows, float eps, void *stream);
@@ -107,6 +113,8 @@ int kcpp_model_forward_hidden(kcpp_model *m, int T, int n_past);
 int kcpp_model_argmax(kcpp_model *m, int32_t *token_out);
 /* enable/disable hipGraph replay for single-token decode (default on) */
 int kcpp_model_set_graphs(kcpp_model *m, int enable);
+/* single-token decode through the fused mat-vec path (default on); off = one kernel per op */
+int kcpp_model_set_fused_decode(kcpp_model *m, int enable);
 int64_t kcpp_model_weight_bytes(kcpp_model *m);
 const char *kcpp_last_error(void);
 

@@ -12,11 +12,14 @@
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
-#define FA_CHUNK 256
+#define FA_CHUNK 64
 #define FA_MAXG 8
 
 // K/V cache layout: [pos][HKV][D] f16, row stride EKV = HKV*D elements.
 // Query layout: q16 [T][H][D] f16.  Query t sits at absolute position n_past + t.
+// One workgroup = (64-key chunk, kv head, query); its G = H/HKV query heads share every K/V row
+// (GQA).  Wave w owns keys 16w..16w+15; 16 lanes x 16 B cover one 256-B K or V row, so each
+// wave-instruction moves 4 rows and every load is a coalesced dwordx4.
 template <int D, int G>
 __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
                                                    const uint16_t *__restrict__ vc, float *__restrict__ part_o,
@@ -31,11 +34,10 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
     const int p0 = c * FA_CHUNK;
     const int p1 = min(p0 + FA_CHUNK, qpos + 1);          // exclusive
     const int64_t EKV = (int64_t)HKV * D;
-    __shared__ float s_sc[FA_MAXG][FA_CHUNK];
-    __shared__ float s_red[4][FA_MAXG][D];
-    __shared__ float s_m[FA_MAXG], s_l[FA_MAXG];
+    __shared__ float s_sc[G][FA_CHUNK];
+    __shared__ float s_red[4][G][D];
+    __shared__ float s_m[G], s_l[G];
 
-    // --- scores: 16 lanes per key, 8 dims per lane
     const int sub = lane & 15, kq = lane >> 4;
     float qv[G][8];
 #pragma unroll
@@ -43,63 +45,84 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
         const uint4 qq = *(const uint4 *)(q16 + ((int64_t)t * H + hk * G + g) * D + sub * 8);
         const uint32_t w4[4] = {qq.x, qq.y, qq.z, qq.w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            qv[g][2 * i] = h2f(w4[i] & 0xFFFF);
-            qv[g][2 * i + 1] = h2f(w4[i] >> 16);
-        }
+        for (int i = 0; i < 4; ++i) { qv[g][2 * i] = h2f(w4[i] & 0xFFFF); qv[g][2 * i + 1] = h2f(w4[i] >> 16); }
     }
-    for (int p = p0 + wave * 4 + kq; p < p0 + FA_CHUNK; p += 16) {
-        float kf[8];
-        const bool valid = p < p1;
-        if (valid) {
-            const uint4 kk = *(const uint4 *)(kc + (int64_t)p * EKV + hk * D + sub * 8);
-            const uint32_t w4[4] = {kk.x, kk.y, kk.z, kk.w};
+    // ---- scores (issue all 4 K loads first)
+    uint4 kk[4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) { kf[2 * i] = h2f(w4[i] & 0xFFFF); kf[2 * i + 1] = h2f(w4[i] >> 16); }
-        }
+    for (int i = 0; i < 4; ++i) {
+        const int p = p0 + 16 * wave + 4 * i + kq;
+        kk[i] = p < p1 ? *(const uint4 *)(kc + (int64_t)p * EKV + hk * D + sub * 8) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int p = p0 + 16 * wave + 4 * i + kq;
+        const uint32_t w4[4] = {kk[i].x, kk[i].y, kk[i].z, kk[i].w};
+        float kf[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { kf[2 * e] = h2f(w4[e] & 0xFFFF); kf[2 * e + 1] = h2f(w4[e] >> 16); }
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            float s = 0.0f;
-            if (valid) {
+            float sc = 0.0f;
 #pragma unroll
-                for (int i = 0; i < 8; ++i) s = fmaf(qv[g][i], kf[i], s);
-            }
-            s = group_sum<16>(s);
-            if (sub == 0) s_sc[g][p - p0] = valid ? s * scale : -INFINITY;
+            for (int e = 0; e < 8; ++e) sc = fmaf(qv[g][e], kf[e], sc);
+            sc = group_sum<16>(sc);
+            if (sub == 0) s_sc[g][p - p0] = p < p1 ? sc * scale : -INFINITY;
         }
     }
+    // issue the V loads before the softmax barrier (independent of the scores)
+    uint4 vv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int p = p0 + 16 * wave + 4 * i + kq;
+        vv[i] = p < p1 ? *(const uint4 *)(vc + (int64_t)p * EKV + hk * D + sub * 8) : make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
-    // --- softmax statistics per head (one wave per head)
+    // ---- softmax statistics of the chunk, one wave per head (lane = key)
     for (int g = wave; g < G; g += 4) {
-        float m = -INFINITY;
-        for (int i = lane; i < FA_CHUNK; i += 64) m = fmaxf(m, s_sc[g][i]);
-        m = wave_max(m);
-        float l = 0.0f;
-        for (int i = lane; i < FA_CHUNK; i += 64) {
-            const float e = (s_sc[g][i] == -INFINITY) ? 0.0f : expf(s_sc[g][i] - m);
-            s_sc[g][i] = e;
-            l += e;
-        }
-        l = wave_sum(l);
+        const float sv = s_sc[g][lane];
+        const float m = wave_max(sv);
+        const float e = (sv == -INFINITY) ? 0.0f : expf(sv - m);
+        s_sc[g][lane] = e;
+        const float l = wave_sum(e);
         if (lane == 0) { s_m[g] = m; s_l[g] = l; }
     }
     __syncthreads();
-    // --- P.V: each lane owns dims 2*lane, 2*lane+1; wave w takes keys w, w+4, ...
-    float acc[G][2];
+    // ---- P.V: lane owns dims 8*sub..+7 for keys 16w + 4i + kq
+    float acc[G][8];
 #pragma unroll
-    for (int g = 0; g < G; ++g) acc[g][0] = acc[g][1] = 0.0f;
-    for (int p = p0 + wave; p < p1; p += 4) {
-        const uint32_t vv = *(const uint32_t *)(vc + (int64_t)p * EKV + hk * D + 2 * lane);
-        const float v0 = h2f(vv & 0xFFFF), v1 = h2f(vv >> 16);
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[g][e] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int kl = 16 * wave + 4 * i + kq;
+        const uint32_t w4[4] = {vv[i].x, vv[i].y, vv[i].z, vv[i].w};
+        float vf[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { vf[2 * e] = h2f(w4[e] & 0xFFFF); vf[2 * e + 1] = h2f(w4[e] >> 16); }
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const float pr = s_sc[g][p - p0];
-            acc[g][0] = fmaf(pr, v0, acc[g][0]);
-            acc[g][1] = fmaf(pr, v1, acc[g][1]);
+            const float pr = s_sc[g][kl];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(pr, vf[e], acc[g][e]);
         }
     }
 #pragma unroll
-    for (int g = 0; g < G; ++g) { s_red[wave][g][2 * lane] = acc[g][0]; s_red[wave][g][2 * lane + 1] = acc[g][1]; }
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float v = acc[g][e];
+            v += __shfl_xor(v, 16, 64);
+            v += __shfl_xor(v, 32, 64);
+            acc[g][e] = v;
+        }
+    if (kq == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s_red[wave][g][sub * 8 + e] = acc[g][e];
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < G * D; i += 256) {
         const int g = i / D, d = i % D;
@@ -113,77 +136,69 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
     }
 }
 
-// combine split-KV partials; one 256-thread block covers two heads (= one Q8_K block of 256)
-__device__ void q8k_quant_block_attn(const float4 v, int lane, int8_t *qs, float *dptr, int16_t *bs);
-
+// combine split-KV partials; one 256-thread workgroup covers two heads (= one Q8_K block of 256).
+// Per head one wave turns the chunk maxima into weights exp(m_c - M) (lane = chunk, <= 64 per
+// pass), then every thread sums its dim over the chunks with independent loads.
 template <bool QUANT>
 __global__ void __launch_bounds__(256) k_fa_combine(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
                                                     float *__restrict__ out, uint8_t *__restrict__ qout, int T, int H,
                                                     int D, int n_past_arg, const int32_t *__restrict__ n_past_dev,
                                                     int n_chunks_alloc) {
     const int t = blockIdx.y;
-    const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
     const int pair = blockIdx.x;                       // heads 2*pair, 2*pair+1
-    const int tid = threadIdx.x;
-    const int h = 2 * pair + tid / 128, d = tid % 128;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
     const int nch = (n_past + t) / FA_CHUNK + 1;       // chunks this query actually used
-    const float2 *ml = part_ml + ((int64_t)t * H + h) * n_chunks_alloc;
-    float M = -INFINITY;
-    for (int c = 0; c < nch; ++c) M = fmaxf(M, ml[c].x);
-    float L = 0.0f, O = 0.0f;
-    for (int c = 0; c < nch; ++c) {
-        const float w = ml[c].x == -INFINITY ? 0.0f : expf(ml[c].x - M);
-        L = fmaf(w, ml[c].y, L);
-        O = fmaf(w, part_o[(((int64_t)t * H + h) * n_chunks_alloc + c) * 128 + d], O);
+    __shared__ float s_w[2][4096 / FA_CHUNK * 4];
+    __shared__ float s_inv[2];
+    if (wave < 2) {
+        const int h = 2 * pair + wave;
+        const float2 *ml = part_ml + ((int64_t)t * H + h) * n_chunks_alloc;
+        float M = -INFINITY;
+        for (int c = lane; c < nch; c += 64) M = fmaxf(M, ml[c].x);
+        M = wave_max(M);
+        float L = 0.0f;
+        for (int c = lane; c < nch; c += 64) {
+            const float2 v = ml[c];
+            const float wgt = v.x == -INFINITY ? 0.0f : expf(v.x - M);
+            s_w[wave][c] = wgt;
+            L = fmaf(wgt, v.y, L);
+        }
+        L = wave_sum(L);
+        if (lane == 0) s_inv[wave] = L;
     }
-    const float r = O / L;
+    __syncthreads();
+    const int hl = tid >> 7, d = tid & 127, h = 2 * pair + hl;
+    const float *po = part_o + ((int64_t)t * H + h) * n_chunks_alloc * 128 + d;
+    float O0 = 0.0f, O1 = 0.0f, O2 = 0.0f, O3 = 0.0f;
+    int c = 0;
+    for (; c + 4 <= nch; c += 4) {
+        O0 = fmaf(s_w[hl][c], po[(int64_t)c * 128], O0);
+        O1 = fmaf(s_w[hl][c + 1], po[(int64_t)(c + 1) * 128], O1);
+        O2 = fmaf(s_w[hl][c + 2], po[(int64_t)(c + 2) * 128], O2);
+        O3 = fmaf(s_w[hl][c + 3], po[(int64_t)(c + 3) * 128], O3);
+    }
+    for (; c < nch; ++c) O0 = fmaf(s_w[hl][c], po[(int64_t)c * 128], O0);
+    const float r = ((O0 + O1) + (O2 + O3)) / s_inv[hl];
     const int64_t e = (int64_t)t * H * 128 + (int64_t)h * 128 + d;
     if (out) out[e] = r;
     if constexpr (QUANT) {
-        // regroup: lane l of wave w needs elements 4*(64*w + l) .. +3 of the 256-block
+        // regroup so that lane j of the 16-lane group holds elements 16j..16j+15 of the block
         __shared__ float s_v[256];
         s_v[tid] = r;
         __syncthreads();
-        if (tid < 64) {
-            const float4 v = make_float4(s_v[4 * tid], s_v[4 * tid + 1], s_v[4 * tid + 2], s_v[4 * tid + 3]);
+        if (tid < 16) {
+            float v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = s_v[16 * tid + k];
             const int64_t E = (int64_t)H * 128;
             const int64_t nsb = E / 256;
             int8_t *qs = (int8_t *)qout + (int64_t)t * E + pair * 256;
             float *dp = (float *)(qout + (int64_t)T * E) + (int64_t)t * nsb + pair;
             int16_t *bs = (int16_t *)(qout + (int64_t)T * E + (int64_t)T * nsb * 4) + (int64_t)t * (E / 16) + pair * 16;
-            q8k_quant_block_attn(v, tid, qs, dp, bs);
+            q8k_quant16(v, tid, qs, dp, bs);
         }
     }
-}
-
-__device__ __forceinline__ void q8k_quant_block_attn(const float4 v, int lane, int8_t *qs, float *dptr, int16_t *bs) {
-    float xs[4] = {v.x, v.y, v.z, v.w};
-    float am = -1.0f; int ai = 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { float a = fabsf(xs[e]); if (a > am) { am = a; ai = lane * 4 + e; } }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        float am2 = __shfl_xor(am, o, 64);
-        int ai2 = __shfl_xor(ai, o, 64);
-        if (am2 > am || (am2 == am && ai2 < ai)) { am = am2; ai = ai2; }
-    }
-    const int ae = ai & 3;
-    const float mine = ae == 0 ? xs[0] : (ae == 1 ? xs[1] : (ae == 2 ? xs[2] : xs[3]));
-    const float mx = __shfl(mine, ai >> 2, 64);
-    int q[4];
-    if (am == 0.0f) {
-        q[0] = q[1] = q[2] = q[3] = 0;
-        if (lane == 0) *dptr = 0.0f;
-    } else {
-        const float iscale = -127.f / mx;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { int tq = nearest_int_mul(iscale, xs[e]); q[e] = tq < 127 ? tq : 127; }
-        if (lane == 0) *dptr = 1.0f / iscale;
-    }
-    ((int *)qs)[lane] = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
-    int s = q[0] + q[1] + q[2] + q[3];
-    s = group_sum<4>(s);
-    if ((lane & 3) == 0) bs[lane >> 2] = (int16_t)s;
 }
 
 // ---------------------------------------------------------------- prefill (tiled, online softmax)
@@ -322,6 +337,7 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     if (use_decode) {
         const int nkv = n_past_dev ? n_kv_max : n_past + T;
         const int nch = (nkv + FA_CHUNK - 1) / FA_CHUNK;
+        if (nch > 4096 / FA_CHUNK * 4) return -4;       // combine's chunk-weight table (16k context)
         float *po = (float *)ws;
         float2 *pml = (float2 *)(po + (int64_t)T * H * nch * 128);
         const dim3 grid(nch, HKV, T);

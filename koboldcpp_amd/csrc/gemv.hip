@@ -13,252 +13,7 @@
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-// streamed-once weight loads: nontemporal (MI355X_MICROARCH.md "nt-weights")
-__device__ __forceinline__ uint4 ld_nt(const void *p) {
-    const v4u v = __builtin_nontemporal_load((const v4u *)p);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-template <int TYPE> struct Unit;
-
-// ---- Q4_K: unit = (super-block sb, 64-elem chunk j): 32 B of nibbles + 16 B header
-template <> struct Unit<KT_Q4_K> {
-    static constexpr int ELEMS = 64;
-    uint4 hdr, q0, q1;
-    __device__ __forceinline__ void load(const uint8_t *row, int64_t nblk_total, int u) {
-        const uint8_t *blk = row + (int64_t)(u >> 2) * 144;
-        const int j = u & 3;
-        hdr = ld_nt((const void *)blk);
-        q0 = ld_nt((const void *)(blk + 16 + 32 * j));
-        q1 = ld_nt((const void *)(blk + 32 + 32 * j));
-    }
-};
-// ---- Q5_K: like Q4_K plus 32 B of high bits per super-block
-template <> struct Unit<KT_Q5_K> {
-    static constexpr int ELEMS = 64;
-    uint4 hdr, q0, q1, h0, h1;
-    __device__ __forceinline__ void load(const uint8_t *row, int64_t, int u) {
-        const uint8_t *blk = row + (int64_t)(u >> 2) * 176;
-        const int j = u & 3;
-        hdr = ld_nt((const void *)blk);
-        h0 = *(const uint4 *)(blk + 16);
-        h1 = *(const uint4 *)(blk + 32);
-        q0 = ld_nt((const void *)(blk + 48 + 32 * j));
-        q1 = ld_nt((const void *)(blk + 64 + 32 * j));
-    }
-};
-// ---- Q6_K (SoA): unit = (sb, half h, l-quarter lq): ql 2x16 B, qh 16 B, 16 B scales, d
-template <> struct Unit<KT_Q6_K> {
-    static constexpr int ELEMS = 64;
-    uint4 qa, qb, qh, sc;
-    uint16_t d;
-    __device__ __forceinline__ void load(const uint8_t *base, int64_t nb, int64_t b0, int u) {
-        const int64_t b = b0 + (u >> 2);
-        const int h = (u >> 1) & 1, lq = u & 1;
-        const uint8_t *q = base + b * 192;
-        qa = ld_nt((const void *)(q + 64 * h + 16 * lq));
-        qb = ld_nt((const void *)(q + 64 * h + 32 + 16 * lq));
-        qh = ld_nt((const void *)(q + 128 + 32 * h + 16 * lq));
-        sc = *(const uint4 *)(base + nb * 192 + b * 16);
-        d = *(const uint16_t *)(base + nb * 208 + b * 2);
-    }
-};
-// ---- Q4_0 (SoA): unit = one 32-elem block: 16 B nibbles + fp16 d
-template <> struct Unit<KT_Q4_0> {
-    static constexpr int ELEMS = 32;
-    uint4 q;
-    uint16_t d;
-    __device__ __forceinline__ void load(const uint8_t *base, int64_t nb, int64_t b0, int u) {
-        const int64_t b = b0 + u;
-        q = ld_nt((const void *)(base + b * 16));
-        d = *(const uint16_t *)(base + nb * 16 + b * 2);
-    }
-};
-// ---- Q8_0 (SoA): unit = one 32-elem block: 32 B int8 + fp16 d
-template <> struct Unit<KT_Q8_0> {
-    static constexpr int ELEMS = 32;
-    uint4 q0, q1;
-    uint16_t d;
-    __device__ __forceinline__ void load(const uint8_t *base, int64_t nb, int64_t b0, int u) {
-        const int64_t b = b0 + u;
-        q0 = ld_nt((const void *)(base + b * 32));
-        q1 = ld_nt((const void *)(base + b * 32 + 16));
-        d = *(const uint16_t *)(base + nb * 32 + b * 2);
-    }
-};
-
-__device__ __forceinline__ int byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xFF; }
-__device__ __forceinline__ uint32_t u4(const uint4 &v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w)); }
-
-// scale/min of sub-block `is` from the 12 packed bytes (get_scale_min_k4, ggml-quants.c:1899)
-__device__ __forceinline__ void k4_scale_min(const uint4 &hdr, int is, int &sc, int &m) {
-    // bytes s[0..11] live in hdr.y (0-3), hdr.z (4-7), hdr.w (8-11)
-    auto s = [&](int k) -> int { return k < 4 ? byte_of(hdr.y, k) : (k < 8 ? byte_of(hdr.z, k - 4) : byte_of(hdr.w, k - 8)); };
-    if (is < 4) { sc = s(is) & 63; m = s(is + 4) & 63; }
-    else {
-        sc = (s(is + 4) & 0xF) | ((s(is - 4) >> 6) << 4);
-        m = (s(is + 4) >> 4) | ((s(is) >> 6) << 4);
-    }
-}
-
-// Activation unit for K-quants: 64 int8 + d + 4 bsums (sub-groups of 16)
-struct ActK {
-    int4 a[4];
-    float d;
-    int bs[4];
-};
-__device__ __forceinline__ void load_actk(const ActView &av, int u, ActK &x) {
-    const int64_t e0 = (int64_t)u * 64;
-    const int4 *p = (const int4 *)(av.qs + e0);
-    x.a[0] = p[0]; x.a[1] = p[1]; x.a[2] = p[2]; x.a[3] = p[3];
-    x.d = av.d[e0 >> 8];
-    const int2 b = *(const int2 *)(av.bs + (e0 >> 4));
-    x.bs[0] = (int16_t)(b.x & 0xFFFF); x.bs[1] = (int16_t)(b.x >> 16);
-    x.bs[2] = (int16_t)(b.y & 0xFFFF); x.bs[3] = (int16_t)(b.y >> 16);
-}
-__device__ __forceinline__ int ai(const ActK &x, int i) {   // dword i (0..15) of the 64 int8
-    const int4 &v = x.a[i >> 2];
-    const int k = i & 3;
-    return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
-}
-// Activation unit for Q8_0-type: 32 int8 + d + asum
-struct Act0 {
-    int4 a[2];
-    float d;
-    int s;
-};
-__device__ __forceinline__ void load_act0(const ActView &av, int u, Act0 &x) {
-    const int4 *p = (const int4 *)(av.qs + (int64_t)u * 32);
-    x.a[0] = p[0]; x.a[1] = p[1];
-    x.d = av.d[u];
-    x.s = av.bs[u];
-}
-
-template <int TYPE> struct ActOf { typedef ActK T; };
-template <> struct ActOf<KT_Q4_0> { typedef Act0 T; };
-template <> struct ActOf<KT_Q8_0> { typedef Act0 T; };
-
-__device__ __forceinline__ void load_act(const ActView &av, int u, ActK &x) { load_actk(av, u, x); }
-__device__ __forceinline__ void load_act(const ActView &av, int u, Act0 &x) { load_act0(av, u, x); }
-
-// ---------------------------------------------------------------- per-unit dot products
-__device__ __forceinline__ float unit_dot(const Unit<KT_Q4_K> &w, int u, const ActK &x) {
-    const int j = u & 3;
-    int sc0, m0, sc1, m1;
-    k4_scale_min(w.hdr, 2 * j, sc0, m0);
-    k4_scale_min(w.hdr, 2 * j + 1, sc1, m1);
-    int dlo = 0, dhi = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t q = i < 4 ? u4(w.q0, i) : u4(w.q1, i - 4);
-        dlo = sdot4((int)(q & 0x0F0F0F0Fu), ai(x, i), dlo);
-        dhi = sdot4((int)((q >> 4) & 0x0F0F0F0Fu), ai(x, 8 + i), dhi);
-    }
-    const int sumi = sc0 * dlo + sc1 * dhi;
-    const int summ = m0 * (x.bs[0] + x.bs[1]) + m1 * (x.bs[2] + x.bs[3]);
-    const float d = __fmul_rn(x.d, h2f((uint16_t)(w.hdr.x & 0xFFFF)));
-    const float dmin = __fmul_rn(x.d, h2f((uint16_t)(w.hdr.x >> 16)));
-    return __fsub_rn(__fmul_rn(d, (float)sumi), __fmul_rn(dmin, (float)summ));
-}
-
-__device__ __forceinline__ float unit_dot(const Unit<KT_Q5_K> &w, int u, const ActK &x) {
-    const int j = u & 3;
-    int sc0, m0, sc1, m1;
-    k4_scale_min(w.hdr, 2 * j, sc0, m0);
-    k4_scale_min(w.hdr, 2 * j + 1, sc1, m1);
-    int dlo = 0, dhi = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint32_t q = i < 4 ? u4(w.q0, i) : u4(w.q1, i - 4);
-        const uint32_t h = i < 4 ? u4(w.h0, i) : u4(w.h1, i - 4);
-        const uint32_t lo = (q & 0x0F0F0F0Fu) | (((h >> (2 * j)) & 0x01010101u) << 4);
-        const uint32_t hi = ((q >> 4) & 0x0F0F0F0Fu) | (((h >> (2 * j + 1)) & 0x01010101u) << 4);
-        dlo = sdot4((int)lo, ai(x, i), dlo);
-        dhi = sdot4((int)hi, ai(x, 8 + i), dhi);
-    }
-    const int sumi = sc0 * dlo + sc1 * dhi;
-    const int summ = m0 * (x.bs[0] + x.bs[1]) + m1 * (x.bs[2] + x.bs[3]);
-    const float d = __fmul_rn(x.d, h2f((uint16_t)(w.hdr.x & 0xFFFF)));
-    const float dmin = __fmul_rn(x.d, h2f((uint16_t)(w.hdr.x >> 16)));
-    return __fsub_rn(__fmul_rn(d, (float)sumi), __fmul_rn(dmin, (float)summ));
-}
-
-// Q6_K activation unit is not contiguous: 4 planes of 16 elements at stride 32
-struct Act6 {
-    int4 a[4];
-    float d;
-    int bs[4];
-};
-__device__ __forceinline__ void load_act6(const ActView &av, int u, Act6 &x) {
-    const int64_t sb = u >> 2;
-    const int h = (u >> 1) & 1, lq = u & 1;
-    const int64_t e0 = sb * 256 + 128 * h + 16 * lq;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) x.a[p] = *(const int4 *)(av.qs + e0 + 32 * p);
-    x.d = av.d[sb];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) x.bs[p] = av.bs[(e0 + 32 * p) >> 4];
-}
-template <> struct ActOf<KT_Q6_K> { typedef Act6 T; };
-__device__ __forceinline__ void load_act(const ActView &av, int u, Act6 &x) { load_act6(av, u, x); }
-
-__device__ __forceinline__ float unit_dot(const Unit<KT_Q6_K> &w, int u, const Act6 &x) {
-    const int h = (u >> 1) & 1, lq = u & 1;
-    int dp[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t la = u4(w.qa, i), lb = u4(w.qb, i), hh = u4(w.qh, i);
-        const uint32_t p0 = (la & 0x0F0F0F0Fu) | ((hh << 4) & 0x30303030u);
-        const uint32_t p1 = (lb & 0x0F0F0F0Fu) | ((hh << 2) & 0x30303030u);
-        const uint32_t p2 = ((la >> 4) & 0x0F0F0F0Fu) | (hh & 0x30303030u);
-        const uint32_t p3 = ((lb >> 4) & 0x0F0F0F0Fu) | ((hh >> 2) & 0x30303030u);
-        dp[0] = sdot4((int)p0, u4(*(const uint4 *)&x.a[0], i), dp[0]);
-        dp[1] = sdot4((int)p1, u4(*(const uint4 *)&x.a[1], i), dp[1]);
-        dp[2] = sdot4((int)p2, u4(*(const uint4 *)&x.a[2], i), dp[2]);
-        dp[3] = sdot4((int)p3, u4(*(const uint4 *)&x.a[3], i), dp[3]);
-    }
-    // scales: is = lq + 2p + 8h  (dequantize_row_q6_K: sc[is + 0/2/4/6], ggml-quants.c:2997)
-    int sumi = 0;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        const int is = lq + 2 * p + 8 * h;
-        const int s = (int8_t)byte_of(u4(w.sc, is >> 2), is & 3);
-        sumi += s * (dp[p] - 32 * x.bs[p]);
-    }
-    return __fmul_rn(__fmul_rn(h2f(w.d), x.d), (float)sumi);
-}
-
-__device__ __forceinline__ float unit_dot(const Unit<KT_Q4_0> &w, int, const Act0 &x) {
-    int s = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const uint32_t q = u4(w.q, i);
-        s = sdot4((int)(q & 0x0F0F0F0Fu), u4(*(const uint4 *)&x.a[0], i), s);
-        s = sdot4((int)((q >> 4) & 0x0F0F0F0Fu), u4(*(const uint4 *)&x.a[1], i), s);
-    }
-    s -= 8 * x.s;
-    return __fmul_rn((float)s, __fmul_rn(h2f(w.d), x.d));
-}
-
-__device__ __forceinline__ float unit_dot(const Unit<KT_Q8_0> &w, int, const Act0 &x) {
-    int s = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        s = sdot4((int)u4(w.q0, i), u4(*(const uint4 *)&x.a[0], i), s);
-        s = sdot4((int)u4(w.q1, i), u4(*(const uint4 *)&x.a[1], i), s);
-    }
-    return __fmul_rn((float)s, __fmul_rn(h2f(w.d), x.d));
-}
-
-// uniform unit loader: native-layout types index by row pointer, SoA types by block index
-template <int TYPE>
-__device__ __forceinline__ void load_unit(Unit<TYPE> &w, const uint8_t *W, int64_t nb, int64_t row, int64_t units_per_row, int u) {
-    if constexpr (TYPE == KT_Q4_K) w.load(W + row * (units_per_row / 4) * 144, nb, u);
-    else if constexpr (TYPE == KT_Q5_K) w.load(W + row * (units_per_row / 4) * 176, nb, u);
-    else if constexpr (TYPE == KT_Q6_K) w.load(W, nb, row * (units_per_row / 4), u);
-    else w.load(W, nb, row * units_per_row, u);
-}
+#include "gemv_units.h"
 
 // ---------------------------------------------------------------- kernel
 // mode 0: Y[c][n] = dot (+ res[c][n] if res)      mode 1 (GLU): Y[c][n] = silu(dot(W,n)) * dot(W2,n)

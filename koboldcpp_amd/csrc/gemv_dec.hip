@@ -1,0 +1,20 @@
+// gemv_dec.hip -- C entry of the fused single-token mat-vec (gemv_dec_impl.h, one TU per type).
+#include "kcpp_internal.h"
+#include "kcpp_common.h"
+
+template <int TYPE> int dispatch_mode(const DecArgs &a, int mode, int pro, int rows_per_wave, hipStream_t s);
+
+extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream) {
+    const DecArgs &a = *(const DecArgs *)args;
+    hipStream_t s = (hipStream_t)stream;
+    switch (type) {
+    case KT_Q4_K: return dispatch_mode<KT_Q4_K>(a, mode, pro, rows_per_wave, s);
+    case KT_Q5_K: return dispatch_mode<KT_Q5_K>(a, mode, pro, rows_per_wave, s);
+    case KT_Q6_K: return dispatch_mode<KT_Q6_K>(a, mode, pro, rows_per_wave, s);
+    case KT_Q4_0: return dispatch_mode<KT_Q4_0>(a, mode, pro, rows_per_wave, s);
+    case KT_Q8_0: return dispatch_mode<KT_Q8_0>(a, mode, pro, rows_per_wave, s);
+    default: return -3;
+    }
+}
+
+extern "C" int64_t kcpp_gemv_dec_args_size(void) { return (int64_t)sizeof(DecArgs); }

@@ -96,3 +96,99 @@ __host__ __device__ inline ActView act_view(int vtype, const void *buf, int64_t 
 inline int vec_dot_type(int wtype) {
     return (wtype == KT_Q4_0 || wtype == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;
 }
+
+// ---------------------------------------------------------------------------------
+// DPP (VALU, no LDS round trip) all-reduce over aligned 16-lane groups:
+// quad_perm xor1 (0xB1), quad_perm xor2 (0x4E), row_half_mirror (0x141), row_mirror (0x140).
+// After the 4 steps every lane of the group holds the group result (max / int sum exact;
+// float sums may differ in rounding between lanes -- read one lane when that matters).
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false)); }
+
+__device__ __forceinline__ int sum16_i(int v) {
+    v += dpp_i<0xB1>(v); v += dpp_i<0x4E>(v); v += dpp_i<0x141>(v); v += dpp_i<0x140>(v);
+    return v;
+}
+__device__ __forceinline__ float max16_f(float v) {
+    v = fmaxf(v, dpp_f<0xB1>(v)); v = fmaxf(v, dpp_f<0x4E>(v));
+    v = fmaxf(v, dpp_f<0x141>(v)); v = fmaxf(v, dpp_f<0x140>(v));
+    return v;
+}
+// (|x|, index, x) arg-max with the smallest index winning ties (commutative + associative,
+// so the DPP pairing order does not matter).
+template <int CTRL>
+__device__ __forceinline__ void amax_step(float &a, int &i, float &x) {
+    const float a2 = dpp_f<CTRL>(a), x2 = dpp_f<CTRL>(x);
+    const int i2 = dpp_i<CTRL>(i);
+    const bool take = a2 > a || (a2 == a && i2 < i);
+    a = take ? a2 : a; i = take ? i2 : i; x = take ? x2 : x;
+}
+
+// quantize_row_q8_K_ref (ggml-quants.c:3786-3823) of one 256-element super-block held by an
+// aligned 16-lane group, lane j holding elements 16j..16j+15 (so bsums[j] is lane-local).
+// qs/d/bs point at the super-block's output; l16 = lane & 15.
+__device__ __forceinline__ void q8k_quant16(const float (&v)[16], int l16, int8_t *qs, float *d, int16_t *bs) {
+    float am = -1.0f, mx = 0.0f;
+    int ai = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+        const float a = fabsf(v[e]);
+        if (a > am) { am = a; ai = 16 * l16 + e; mx = v[e]; }
+    }
+    amax_step<0xB1>(am, ai, mx);
+    amax_step<0x4E>(am, ai, mx);
+    amax_step<0x141>(am, ai, mx);
+    amax_step<0x140>(am, ai, mx);
+    int q[16];
+    if (am == 0.0f) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) q[e] = 0;
+        if (l16 == 0) *d = 0.0f;
+    } else {
+        const float iscale = -127.f / mx;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) { const int t = nearest_int_mul(iscale, v[e]); q[e] = t < 127 ? t : 127; }
+        if (l16 == 0) *d = 1.0f / iscale;
+    }
+    int s = 0;
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        w[k] = (uint32_t)(q[4 * k] & 0xFF) | ((uint32_t)(q[4 * k + 1] & 0xFF) << 8) |
+               ((uint32_t)(q[4 * k + 2] & 0xFF) << 16) | ((uint32_t)(q[4 * k + 3] & 0xFF) << 24);
+        s += q[4 * k] + q[4 * k + 1] + q[4 * k + 2] + q[4 * k + 3];
+    }
+    *(uint4 *)(qs + 16 * l16) = make_uint4(w[0], w[1], w[2], w[3]);
+    bs[l16] = (int16_t)s;
+}
+
+// 64-lane all-reduce of a double: DPP within rows of 16 (two 32-bit halves per step), then two
+// cross-row exchanges.  The summation tree differs from a sequential CPU sum only below 1 ulp of
+// double, which is invisible after the (float) rounding the rms_norm callers apply.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xFFFFFFFFll), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+    v += dpp_d<0xB1>(v); v += dpp_d<0x4E>(v); v += dpp_d<0x141>(v); v += dpp_d<0x140>(v);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    return v;
+}
+__device__ __forceinline__ float wave_max_dpp(float v) {
+    v = max16_f(v);
+    v = fmaxf(v, __shfl_xor(v, 16, 64));
+    v = fmaxf(v, __shfl_xor(v, 32, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_sum_f(float v) {
+    v += dpp_f<0xB1>(v); v += dpp_f<0x4E>(v); v += dpp_f<0x141>(v); v += dpp_f<0x140>(v);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    return v;
+}

@@ -11,3 +11,27 @@ int64_t kcpp_act_bytes(int wtype, int64_t K, int64_t M);
 int kcpp_vec_dot_type(int wtype);
 }
 #include "../../include/kcpp_mi355x.h"
+#include <hip/hip_runtime.h>
+
+// arguments of the fused decode mat-vec (gemv_dec.hip)
+struct DecArgs {
+    const uint8_t *W[3];
+    float *Y[3];
+    int64_t N[3];
+    int role[3];          // MODE 2: 0 = q, 1 = k, 2 = v
+    int nseg;
+    const uint8_t *W2;    // MODE 1: up weight
+    int64_t K;
+    const uint8_t *act;   // PRO 0
+    const float *x;       // PRO 1/2 input row
+    const float *nw;      // PRO 1 norm weight
+    float eps;
+    const float *res;     // MODE 0 residual (indexed like Y[0])
+    uint16_t *q16, *kc, *vc;
+    int64_t ekv;
+    int D;
+    const int32_t *pos;
+    const float2 *rope_tab;
+};
+extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream);
+

@@ -11,90 +11,60 @@
 #include "kcpp_internal.h"
 
 // ---------------------------------------------------------------- rms_norm (+ weight, + quantize)
-// one 256-thread block per row; each wave owns super-blocks sb = wave, wave+4, ... (<= 8 per wave)
-__device__ void q8k_quant_block_dev(const float4 v, int lane, int8_t *qs, float *dptr, int16_t *bs);
-
-template <bool QUANT>
-__global__ void __launch_bounds__(256) k_rms_norm(const float *__restrict__ x, int64_t ldx, const float *__restrict__ w,
-                                                  float *__restrict__ y, int64_t ldy, uint8_t *__restrict__ qout,
-                                                  int64_t ne0, int64_t nrows, float eps) {
+// One workgroup per row, ne0/16 threads, 16 consecutive elements per thread: an aligned 16-lane
+// group is exactly one Q8_K super-block, so the fused quantization needs only DPP steps.
+__global__ void __launch_bounds__(1024) k_rms_norm(const float *__restrict__ x, int64_t ldx, const float *__restrict__ w,
+                                                   float *__restrict__ y, int64_t ldy, uint8_t *__restrict__ qout,
+                                                   int64_t ne0, int64_t nrows, float eps) {
     const int64_t r = blockIdx.x;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nsb = (int)(ne0 / 256);
-    const float *xr = x + r * ldx;
-    float4 v[8];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (blockDim.x + 63) >> 6;
+    const int64_t e0 = (int64_t)tid * 16;
+    const bool active = e0 < ne0;                    // block is >= 64 threads even for small rows
+    float v[16];
+    const float4 *src = (const float4 *)(x + r * ldx + e0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float4 f = active ? src[k] : make_float4(0, 0, 0, 0);
+        v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
+    }
     double ss = 0.0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int sb = wave + 4 * i;
-        if (sb < nsb) {
-            v[i] = *(const float4 *)(xr + sb * 256 + lane * 4);
-            ss += (double)__fmul_rn(v[i].x, v[i].x);
-            ss += (double)__fmul_rn(v[i].y, v[i].y);
-            ss += (double)__fmul_rn(v[i].z, v[i].z);
-            ss += (double)__fmul_rn(v[i].w, v[i].w);
-        }
-    }
+    for (int e = 0; e < 16; ++e) ss += (double)__fmul_rn(v[e], v[e]);
     ss = wave_sum(ss);
-    __shared__ double red[4];
+    __shared__ double red[16];
     if (lane == 0) red[wave] = ss;
     __syncthreads();
-    const double sum = red[0] + red[1] + red[2] + red[3];
+    double sum = 0.0;
+    for (int i = 0; i < nw; ++i) sum += red[i];
     const float mean = (float)(sum / (double)ne0);
     const float scale = 1.0f / sqrtf(mean + eps);
+    if (!active) return;
+    float wv[16];
+    if (w) {
+        const float4 *wp = (const float4 *)(w + e0);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int sb = wave + 4 * i;
-        if (sb < nsb) {
-            const int64_t e = sb * 256 + lane * 4;
-            float4 o;
-            o.x = __fmul_rn(v[i].x, scale); o.y = __fmul_rn(v[i].y, scale);
-            o.z = __fmul_rn(v[i].z, scale); o.w = __fmul_rn(v[i].w, scale);
-            if (w) {
-                const float4 ww = *(const float4 *)(w + e);
-                o.x = __fmul_rn(o.x, ww.x); o.y = __fmul_rn(o.y, ww.y);
-                o.z = __fmul_rn(o.z, ww.z); o.w = __fmul_rn(o.w, ww.w);
-            }
-            if (y) *(float4 *)(y + r * ldy + e) = o;
-            if constexpr (QUANT) {
-                int8_t *qs = (int8_t *)qout + r * ne0 + sb * 256;
-                float *d = (float *)(qout + nrows * ne0) + r * nsb + sb;
-                int16_t *bs = (int16_t *)(qout + nrows * ne0 + nrows * nsb * 4) + r * (ne0 / 16) + sb * 16;
-                q8k_quant_block_dev(o, lane, qs, d, bs);
-            }
+        for (int k = 0; k < 4; ++k) {
+            const float4 f = wp[k];
+            wv[4 * k] = f.x; wv[4 * k + 1] = f.y; wv[4 * k + 2] = f.z; wv[4 * k + 3] = f.w;
         }
     }
-}
-
-// identical to quant.hip's q8k_quant_block (kept in this TU so the fused kernel inlines it)
-__device__ __forceinline__ void q8k_quant_block_dev(const float4 v, int lane, int8_t *qs, float *dptr, int16_t *bs) {
-    float xs[4] = {v.x, v.y, v.z, v.w};
-    float am = -1.0f; int ai = 0;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) { float a = fabsf(xs[e]); if (a > am) { am = a; ai = lane * 4 + e; } }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        float am2 = __shfl_xor(am, o, 64);
-        int ai2 = __shfl_xor(ai, o, 64);
-        if (am2 > am || (am2 == am && ai2 < ai)) { am = am2; ai = ai2; }
+    for (int e = 0; e < 16; ++e) {
+        v[e] = __fmul_rn(v[e], scale);
+        if (w) v[e] = __fmul_rn(v[e], wv[e]);
     }
-    const int ae = ai & 3;
-    const float mine = ae == 0 ? xs[0] : (ae == 1 ? xs[1] : (ae == 2 ? xs[2] : xs[3]));
-    const float mx = __shfl(mine, ai >> 2, 64);
-    int q[4];
-    if (am == 0.0f) {
-        q[0] = q[1] = q[2] = q[3] = 0;
-        if (lane == 0) *dptr = 0.0f;
-    } else {
-        const float iscale = -127.f / mx;
+    if (y) {
+        float4 *dst = (float4 *)(y + r * ldy + e0);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { int t = nearest_int_mul(iscale, xs[e]); q[e] = t < 127 ? t : 127; }
-        if (lane == 0) *dptr = 1.0f / iscale;
+        for (int k = 0; k < 4; ++k) dst[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
     }
-    ((int *)qs)[lane] = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
-    int s = q[0] + q[1] + q[2] + q[3];
-    s = group_sum<4>(s);
-    if ((lane & 3) == 0) bs[lane >> 2] = (int16_t)s;
+    if (qout) {
+        const int64_t nsb = ne0 / 256, sb = tid >> 4;
+        int8_t *qs = (int8_t *)qout + r * ne0 + sb * 256;
+        float *d = (float *)(qout + nrows * ne0) + r * nsb + sb;
+        int16_t *bs = (int16_t *)(qout + nrows * ne0 + nrows * nsb * 4) + r * (ne0 / 16) + sb * 16;
+        q8k_quant16(v, tid & 15, qs, d, bs);
+    }
 }
 
 // ---------------------------------------------------------------- rope + KV store
@@ -112,7 +82,7 @@ __global__ void k_rope_kv(const float *__restrict__ qkv, int64_t ldqkv, float *_
     const int npairs_q = H * half, npairs_k = HKV * half;
     const float *row = qkv + (int64_t)t * ldqkv;
     const int64_t EKV = (int64_t)HKV * D;
-    for (int i = threadIdx.x; i < npairs_q + npairs_k + (int)EKV; i += blockDim.x) {
+    for (int i = blockIdx.y * blockDim.x + threadIdx.x; i < npairs_q + npairs_k + (int)EKV; i += gridDim.y * blockDim.x) {
         if (i < npairs_q + npairs_k) {
             const bool isq = i < npairs_q;
             const int pi = isq ? i : i - npairs_q;
@@ -153,21 +123,19 @@ extern "C" {
 
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,
                   int64_t nrows, float eps, void *stream) {
-    if (ne0 % 256 || ne0 > 8192) return -1;
-    if (q8k_out)
-        hipLaunchKernelGGL(k_rms_norm<true>, dim3((unsigned)nrows), dim3(256), 0, (hipStream_t)stream, x, ldx, w, y, ldy,
-                           (uint8_t *)q8k_out, ne0, nrows, eps);
-    else
-        hipLaunchKernelGGL(k_rms_norm<false>, dim3((unsigned)nrows), dim3(256), 0, (hipStream_t)stream, x, ldx, w, y, ldy,
-                           (uint8_t *)nullptr, ne0, nrows, eps);
+    if (ne0 % 256 || ne0 > 16384) return -1;
+    const unsigned nthr = (unsigned)(ne0 / 16 < 64 ? 64 : ne0 / 16);
+    hipLaunchKernelGGL(k_rms_norm, dim3((unsigned)nrows), dim3(nthr), 0, (hipStream_t)stream, x, ldx, w, y,
+                       ldy, (uint8_t *)q8k_out, ne0, nrows, eps);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }
 
 int kcpp_rope_kv(const float *qkv, int64_t ldqkv, float *q_out, uint16_t *q16, uint16_t *kc, uint16_t *vc, int T, int H,
                  int HKV, int D, int n_past, const int32_t *pos_dev, const void *rope_tab, void *stream) {
-    hipLaunchKernelGGL(k_rope_kv, dim3((unsigned)T), dim3(256), 0, (hipStream_t)stream, qkv, ldqkv, q_out, q16, kc, vc, H,
-                       HKV, D, n_past, pos_dev, (const float2 *)rope_tab);
+    const int items = H * D / 2 + HKV * D / 2 + HKV * D;
+    hipLaunchKernelGGL(k_rope_kv, dim3((unsigned)T, (unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)stream, qkv,
+                       ldqkv, q_out, q16, kc, vc, H, HKV, D, n_past, pos_dev, (const float2 *)rope_tab);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

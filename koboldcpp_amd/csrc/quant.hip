@@ -152,61 +152,74 @@ __global__ void k_dequant(int type, const uint8_t *__restrict__ src, float *__re
     deq_block(type, src, nb, b, y + b * ks_block_elems(type));
 }
 
-// get_rows: one workgroup per token, threads over the row's blocks (embedding lookup)
+// get_rows: one workgroup per token; thread i dequantizes element chunks of 8 of the selected row.
+// K-quant element e of super-block sb uses the same formulas as deq_block (ggml-quants.c:2556-3006).
+__device__ __forceinline__ float deq_elem(int type, const uint8_t *src, int64_t nb, int64_t b, int e) {
+    switch (type) {
+    case KT_F32: return ((const float *)src)[b];
+    case KT_F16: return h2f(((const uint16_t *)src)[b]);
+    case KT_Q4_0: {
+        const float d = h2f(*(const uint16_t *)(src + nb * 16 + b * 2));
+        const uint8_t q = src[b * 16 + (e & 15)];
+        return ((e < 16 ? (q & 0xF) : (q >> 4)) - 8) * d;
+    }
+    case KT_Q8_0: return (int8_t)src[b * 32 + e] * h2f(*(const uint16_t *)(src + nb * 32 + b * 2));
+    case KT_Q4_K: case KT_Q5_K: {
+        const bool five = type == KT_Q5_K;
+        const uint8_t *blk = src + b * (five ? 176 : 144);
+        const float d = h2f(blk[0] | (blk[1] << 8)), mn = h2f(blk[2] | (blk[3] << 8));
+        const int c = e >> 6, l = e & 31, hi = (e >> 5) & 1;
+        int sc, m;
+        scale_min_k4(2 * c + hi, blk + 4, sc, m);
+        const uint8_t qb = blk[(five ? 48 : 16) + 32 * c + l];
+        int q = hi ? (qb >> 4) : (qb & 0xF);
+        if (five) q += ((blk[16 + l] >> (2 * c + hi)) & 1) << 4;
+        return __fsub_rn(__fmul_rn(d * sc, (float)q), mn * m);
+    }
+    case KT_Q6_K: {
+        const uint8_t *q6 = src + b * 192;
+        const int8_t *scp = (const int8_t *)(src + nb * 192 + b * 16);
+        const float d = h2f(*(const uint16_t *)(src + nb * 208 + b * 2));
+        const int n = e >> 7, r = e & 127, p = r >> 5, l = r & 31;
+        const uint8_t ql = q6[64 * n + l + 32 * (p & 1)], qh = q6[128 + 32 * n + l];
+        const int q = (((p >> 1) ? (ql >> 4) : (ql & 0xF)) | (((qh >> (2 * p)) & 3) << 4)) - 32;
+        return __fmul_rn(__fmul_rn(d, (float)scp[8 * n + l / 16 + 2 * p]), (float)q);
+    }
+    }
+    return 0.0f;
+}
+
 __global__ void k_get_rows(int type, const uint8_t *__restrict__ src, int64_t K, int64_t N,
                            const int32_t *__restrict__ ids, float *__restrict__ y, int64_t ldy) {
-    const int64_t t = blockIdx.x;
+    const int64_t t = blockIdx.y;
     const int64_t r = ids[t];
-    const int64_t bpr = K / ks_block_elems(type), nb = bpr * N;
-    for (int64_t i = threadIdx.x; i < bpr; i += blockDim.x)
-        deq_block(type, src, nb, r * bpr + i, y + t * ldy + i * ks_block_elems(type));
+    const int be = ks_block_elems(type);
+    const int64_t bpr = K / be, nb = bpr * N;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += (int64_t)gridDim.x * blockDim.x)
+        y[t * ldy + k] = deq_elem(type, src, nb, r * bpr + k / be, (int)(k % be));
 }
 
 // ---------------------------------------------------------------- activation quantization
-// Q8_K: one wave per 256-element super-block, 4 elements per lane.
-__device__ __forceinline__ void q8k_quant_block(const float4 v, int lane, int8_t *qs, float *dptr, int16_t *bs) {
-    float xs[4] = {v.x, v.y, v.z, v.w};
-    // arg-max |x| with the first index winning ties (ggml-quants.c:3794-3799)
-    float am = -1.0f; int ai = 0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { float a = fabsf(xs[e]); if (a > am) { am = a; ai = lane * 4 + e; } }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        float am2 = __shfl_xor(am, o, 64);
-        int ai2 = __shfl_xor(ai, o, 64);
-        if (am2 > am || (am2 == am && ai2 < ai)) { am = am2; ai = ai2; }
-    }
-    const int ae = ai & 3;
-    const float mine = ae == 0 ? xs[0] : (ae == 1 ? xs[1] : (ae == 2 ? xs[2] : xs[3]));
-    const float mx = __shfl(mine, ai >> 2, 64);
-    int q[4];
-    if (am == 0.0f) {
-        q[0] = q[1] = q[2] = q[3] = 0;
-        if (lane == 0) *dptr = 0.0f;
-    } else {
-        const float iscale = -127.f / mx;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { int t = nearest_int_mul(iscale, xs[e]); q[e] = t < 127 ? t : 127; }
-        if (lane == 0) *dptr = 1.0f / iscale;
-    }
-    const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
-    ((int *)qs)[lane] = packed;
-    int s = q[0] + q[1] + q[2] + q[3];
-    s = group_sum<4>(s);
-    if ((lane & 3) == 0) bs[lane >> 2] = (int16_t)s;
-}
-
-__global__ void k_quant_q8k(const float *__restrict__ x, int64_t ldx, uint8_t *__restrict__ out, int64_t K, int64_t M) {
-    const int lane = threadIdx.x & 63;
-    const int64_t g = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);  // global super-block
+// one aligned 16-lane group per super-block, 16 elements per lane
+__global__ void __launch_bounds__(256) k_quant_q8k(const float *__restrict__ x, int64_t ldx, uint8_t *__restrict__ out,
+                                                   int64_t K, int64_t M) {
+    const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nsb = K / 256;
-    if (g >= nsb * M) return;
-    const int64_t m = g / nsb, sb = g % nsb;
-    const float4 v = *(const float4 *)(x + m * ldx + sb * 256 + lane * 4);
+    const int64_t g = gt >> 4;                        // global super-block
+    const int l16 = threadIdx.x & 15;
+    const bool valid = g < nsb * M;
+    const int64_t m = valid ? g / nsb : 0, sb = valid ? g % nsb : 0;
+    float v[16];
+    const float4 *src = (const float4 *)(x + m * ldx + sb * 256 + 16 * l16);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float4 f = valid ? src[k] : make_float4(0, 0, 0, 0);
+        v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
+    }
     int8_t *qs = (int8_t *)out + m * K + sb * 256;
     float *d = (float *)(out + M * K) + m * nsb + sb;
     int16_t *bs = (int16_t *)(out + M * K + M * nsb * 4) + m * (K / 16) + sb * 16;
-    q8k_quant_block(v, lane, qs, d, bs);
+    if (valid) q8k_quant16(v, l16, qs, d, bs);
 }
 
 // Q8_0 (AVX2 semantics): 8 lanes per 32-block, 4 elements per lane.
@@ -276,8 +289,8 @@ int kcpp_dequantize(int type, const void *w, float *y, int64_t K, int64_t N, voi
 int kcpp_quantize_act(int vtype, const float *x, int64_t ldx, void *out, int64_t K, int64_t M, void *stream) {
     if (vtype == KT_Q8_K) {
         if (K % 256) return -1;
-        const int64_t nsb = K / 256 * M;
-        hipLaunchKernelGGL(k_quant_q8k, dim3((unsigned)((nsb + 3) / 4)), dim3(256), 0, (hipStream_t)stream, x, ldx,
+        const int64_t nthr = K / 16 * M;
+        hipLaunchKernelGGL(k_quant_q8k, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, ldx,
                            (uint8_t *)out, K, M);
     } else if (vtype == KT_Q8_0) {
         if (K % 32) return -1;
@@ -293,8 +306,8 @@ int kcpp_quantize_act(int vtype, const float *x, int64_t ldx, void *out, int64_t
 
 int kcpp_get_rows(int type, const void *w, int64_t K, int64_t N, const int32_t *ids, int64_t T, float *y, int64_t ldy,
                   void *stream) {
-    hipLaunchKernelGGL(k_get_rows, dim3((unsigned)T), dim3(64), 0, (hipStream_t)stream, type, (const uint8_t *)w, K, N,
-                       ids, y, ldy);
+    hipLaunchKernelGGL(k_get_rows, dim3((unsigned)((K + 255) / 256), (unsigned)T), dim3(256), 0, (hipStream_t)stream, type,
+                       (const uint8_t *)w, K, N, ids, y, ldy);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

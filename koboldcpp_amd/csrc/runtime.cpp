@@ -26,6 +26,7 @@
 
 #include "../../include/kcpp_mi355x.h"
 #include "../../include/kcpp_synth.h"
+#include "kcpp_internal.h"
 
 static thread_local std::string g_err;
 extern "C" const char *kcpp_last_error(void) { return g_err.c_str(); }
@@ -82,6 +83,7 @@ struct kcpp_model {
     int32_t *pin = nullptr;          // pinned host {token, n_past}
     float *logits_pin = nullptr;
     bool use_graphs = true;
+    bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
     hipGraphExec_t g_exec = nullptr;
     int64_t weight_bytes = 0;
 };
@@ -267,6 +269,11 @@ extern "C" int kcpp_model_set_graphs(kcpp_model *m, int enable) {
     m->use_graphs = enable != 0;
     return 0;
 }
+extern "C" int kcpp_model_set_fused_decode(kcpp_model *m, int enable) {
+    m->fused_decode = enable != 0;
+    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    return 0;
+}
 
 // y[c][n] = W . act  (+res) for M columns: mat-vec for M <= 8, MFMA GEMM above
 static int matmul(kcpp_model *m, const KTensor &W, const KTensor *W2, const void *act, int64_t M, float *Y, int64_t ldy,
@@ -274,6 +281,91 @@ static int matmul(kcpp_model *m, const KTensor &W, const KTensor *W2, const void
     if (M <= 8)
         return kcpp_gemv(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, m->stream);
     return kcpp_gemm(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, m->gemm_ws, m->stream);
+}
+
+static int rows_per_wave(int64_t N, int mode) {
+    static const int r0 = getenv("KCPP_R0") ? atoi(getenv("KCPP_R0")) : 0;
+    static const int r1 = getenv("KCPP_R1") ? atoi(getenv("KCPP_R1")) : 0;
+    if (mode == 1) return r1 ? r1 : 1;
+    if (r0) return r0;
+    return N > 16384 ? 4 : (N > 4096 ? 2 : 1);
+}
+
+// single-token layer step, 6-7 launches (gemv_dec.hip fusions); position read from m->pos_dev
+static int forward_layers_dec(kcpp_model *m) {
+    const kcpp_hparams &hp = m->hp;
+    const int64_t E = hp.n_embd, F = hp.n_ff, H = hp.n_head, HKV = hp.n_head_kv, D = E / H, EKV = HKV * D;
+    hipStream_t s = m->stream;
+    const float kq_scale = 1.0f / sqrtf((float)D);
+    for (int il = m->il0; il < m->il1; ++il) {
+        KLayer &L = m->layers[il - m->il0];
+        const KTensor *t = L.t;
+        // --- attn_norm + q|k|v + rope + K/V cache store (one launch per quant type present)
+        for (int j = 1; j <= 3;) {
+            DecArgs a;
+            memset(&a, 0, sizeof a);
+            a.K = E; a.x = m->x; a.nw = (const float *)t[0].d; a.eps = hp.eps;
+            a.q16 = m->q16; a.kc = L.kc; a.vc = L.vc; a.ekv = EKV; a.D = (int)D; a.pos = m->pos_dev;
+            a.rope_tab = m->rope_tab;
+            const int ty = t[j].type;
+            while (j <= 3 && t[j].type == ty) {
+                a.W[a.nseg] = (const uint8_t *)t[j].d; a.N[a.nseg] = t[j].N; a.role[a.nseg] = j - 1;
+                ++a.nseg; ++j;
+            }
+            RC(kcpp_gemv_dec(ty, &a, 2, 1, 2, s));
+        }
+        // --- attention over the cache, combine + Q8_K quantize for wo
+        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K;
+        RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, woq ? m->act : nullptr, m->fa_ws, 1, (int)H, (int)HKV, (int)D, 0,
+                           m->pos_dev, hp.n_ctx, kq_scale, 1, s));
+        if (!woq) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, 1, s));
+        {   // x += wo . attn
+            DecArgs a;
+            memset(&a, 0, sizeof a);
+            a.K = E; a.act = (const uint8_t *)m->act; a.nseg = 1;
+            a.W[0] = (const uint8_t *)t[4].d; a.N[0] = t[4].N; a.Y[0] = m->x; a.res = m->x;
+            RC(kcpp_gemv_dec(t[4].type, &a, 0, 0, rows_per_wave(t[4].N, 0), s));
+        }
+        // --- ffn_norm + gate|up + silu*mul
+        if (t[6].type == t[7].type) {
+            DecArgs a;
+            memset(&a, 0, sizeof a);
+            a.K = E; a.x = m->x; a.nw = (const float *)t[5].d; a.eps = hp.eps; a.nseg = 1;
+            a.W[0] = (const uint8_t *)t[6].d; a.W2 = (const uint8_t *)t[7].d; a.N[0] = F; a.Y[0] = m->h;
+            RC(kcpp_gemv_dec(t[6].type, &a, 1, 1, rows_per_wave(F, 1), s));
+        } else {
+            for (int j = 6; j <= 7; ++j) {
+                DecArgs a;
+                memset(&a, 0, sizeof a);
+                a.K = E; a.x = m->x; a.nw = (const float *)t[5].d; a.eps = hp.eps; a.nseg = 1;
+                a.W[0] = (const uint8_t *)t[j].d; a.N[0] = F; a.Y[0] = j == 6 ? m->h : m->qkv;
+                RC(kcpp_gemv_dec(t[j].type, &a, 0, 1, rows_per_wave(F, 0), s));
+            }
+            RC(kcpp_silu_mul(m->h, m->h, m->qkv, F, s));
+        }
+        {   // x += down . quant(h)
+            DecArgs a;
+            memset(&a, 0, sizeof a);
+            a.K = F; a.x = m->h; a.nseg = 1;
+            a.W[0] = (const uint8_t *)t[8].d; a.N[0] = E; a.Y[0] = m->x; a.res = m->x;
+            const int rc = kcpp_gemv_dec(t[8].type, &a, 0, 2, rows_per_wave(E, 0), s);
+            if (rc == -8) {   // K-slices beyond the fused kernel's register budget (very large n_ff)
+                RC(kcpp_quantize_act(kcpp_vec_dot_type(t[8].type), m->h, F, m->act2, F, 1, s));
+                RC(kcpp_gemv(t[8].type, t[8].d, nullptr, F, E, m->act2, 1, m->x, E, m->x, E, 0, s));
+            } else if (rc) {
+                RC(rc);
+            }
+        }
+    }
+    return 0;
+}
+
+static int head_dec(kcpp_model *m) {
+    DecArgs a;
+    memset(&a, 0, sizeof a);
+    a.K = m->hp.n_embd; a.x = m->x; a.nw = (const float *)m->output_norm.d; a.eps = m->hp.eps; a.nseg = 1;
+    a.W[0] = (const uint8_t *)m->output.d; a.N[0] = m->hp.n_vocab; a.Y[0] = m->logits;
+    return kcpp_gemv_dec(m->output.type, &a, 0, 1, rows_per_wave(m->hp.n_vocab, 0), m->stream);
 }
 
 // run layers [il0, il1) on m->x for T tokens (T <= ub).  n_past via pos_dev when graph-replayed.
@@ -350,8 +442,13 @@ static int decode_step_dev(kcpp_model *m) {
     if (m->has_embed)
         RC(kcpp_get_rows(m->tok_embd.type, m->tok_embd.d, hp.n_embd, hp.n_vocab, m->tok_dev, 1, m->x, hp.n_embd,
                          m->stream));
-    RC(forward_layers(m, 1, 0, true));
-    if (m->has_output) RC(head(m, 1));
+    if (m->fused_decode) {
+        RC(forward_layers_dec(m));
+        if (m->has_output) RC(head_dec(m));
+    } else {
+        RC(forward_layers(m, 1, 0, true));
+        if (m->has_output) RC(head(m, 1));
+    }
     return 0;
 }
 
@@ -379,6 +476,12 @@ extern "C" int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, in
             hipGraphDestroy(g);
         }
         RT_CHECK(hipGraphLaunch(m->g_exec, m->stream));
+    } else if (T == 1) {
+        m->pin[0] = m->has_embed ? tokens[0] : 0;
+        m->pin[1] = n_past;
+        RT_CHECK(hipMemcpyAsync(m->tok_dev, &m->pin[0], 4, hipMemcpyHostToDevice, m->stream));
+        RT_CHECK(hipMemcpyAsync(m->pos_dev, &m->pin[1], 4, hipMemcpyHostToDevice, m->stream));
+        RC(decode_step_dev(m));
     } else {
         // split into ubatches (llama_decode_internal, src/llama.cpp:17187-17201)
         for (int i = 0; i < T; i += m->ub) {

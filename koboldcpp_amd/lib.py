@@ -50,6 +50,7 @@ _SIGS = {
     "kcpp_model_forward_hidden": [P, I, I],
     "kcpp_model_argmax": [P, P],
     "kcpp_model_set_graphs": [P, I],
+    "kcpp_model_set_fused_decode": [P, I],
     "kcpp_model_weight_bytes": [P],
 }
 _RES = {"kcpp_act_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
@@ -59,6 +60,8 @@ _L.kcpp_act_bytes.argtypes = [I, I64, I64]
 _L.kcpp_fa_workspace_bytes.argtypes = [I, I, I]
 _L.kcpp_gemm_workspace_bytes.argtypes = [I, I64, I64, I64]
 _L.kcpp_vec_dot_type.argtypes = [I]
+_L.kcpp_gemv_dec.argtypes = [I, P, I, I, I, P]
+_L.kcpp_gemv_dec_args_size.restype = I64
 for _n, _a in _SIGS.items():
     getattr(_L, _n).argtypes = _a
 for _n, _r in _RES.items():
@@ -66,7 +69,7 @@ for _n, _r in _RES.items():
 
 
 def exported_symbols():
-    return sorted(set(_SIGS) | set(_RES) | {"kcpp_vec_dot_type"})
+    return sorted(set(_SIGS) | set(_RES) | {"kcpp_vec_dot_type", "kcpp_gemv_dec", "kcpp_gemv_dec_args_size"})
 
 
 def raw():
@@ -155,6 +158,9 @@ class Model:
 
     def stream(self):
         return _L.kcpp_model_stream(self.m)
+
+    def set_fused_decode(self, on):
+        _L.kcpp_model_set_fused_decode(self.m, int(on))
 
     def set_graphs(self, on):
         _L.kcpp_model_set_graphs(self.m, int(on))

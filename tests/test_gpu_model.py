@@ -116,3 +116,25 @@ def test_e2e_vs_oracle_other_types(K, types_fn):
     orc32 = oracle_forced(types, prompt, forced, True)
     d = np.abs(got - orc32)
     assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_F32, (d.max(), np.median(d))
+
+
+@pytest.mark.parametrize("types_fn", [lambda n: R.q4_k_m_types(n), lambda n: R.uniform_types(n, R.Q8_0),
+                                      lambda n: R.uniform_types(n, R.Q4_0, R.Q5_K)])
+def test_fused_decode_matches_unfused(K, types_fn):
+    """gemv_dec fusions (norm/quant prologue, RoPE/KV epilogue) vs one-kernel-per-op decode."""
+    types = types_fn(R.TINY["n_layer"])
+    prompt = list(range(5, 30))
+    outs = []
+    for fused in (True, False):
+        m = K.Model(R.TINY, types)
+        m.set_fused_decode(fused)
+        m.synth(1234)
+        lg = [m.decode(prompt, 0)]
+        n = len(prompt)
+        for tok in (7, 100, 3, 250):
+            lg.append(m.decode([tok], n))
+            n += 1
+        m.close()
+        outs.append(np.array(lg))
+    d = np.abs(outs[0] - outs[1])
+    assert d.max() < TOL_MAX and np.median(d) < 1e-5, (d.max(), np.median(d))
