@@ -12,23 +12,32 @@
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
+#include <cstdlib>
+
 #define FA_CHUNK 64
 #define FA_MAXG 8
 
 // K/V cache layout: [pos][HKV][D] f16, row stride EKV = HKV*D elements.
 // Query layout: q16 [T][H][D] f16.  Query t sits at absolute position n_past + t.
-// One workgroup = (64-key chunk, kv head, query); its G = H/HKV query heads share every K/V row
-// (GQA).  Wave w owns keys 16w..16w+15; 16 lanes x 16 B cover one 256-B K or V row, so each
-// wave-instruction moves 4 rows and every load is a coalesced dwordx4.
-template <int D, int G>
+// One workgroup = (128-key chunk, kv head, query); its G = H/HKV query heads share every K/V row
+// (GQA).  Wave w owns keys 32w..32w+31.  Scores: 16 lanes x 16 B per K row; P.V: lane owns two
+// dims and reads one dword of each V row (no cross-lane reduction).  The last workgroup of a
+// (query, kv head) to finish -- an agent-scope release/acquire ticket (cdna_hip_programming.md
+// Guideline 16) -- merges the chunk partials and, for G >= 2, quantizes the heads' output to
+// Q8_K for wo (replaces the reference's separate flash_attn_combine_results launch,
+// ggml/src/ggml-cuda/fattn-common.cuh:523).
+template <int D, int G, bool FUSED>
 __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
                                                    const uint16_t *__restrict__ vc, float *__restrict__ part_o,
-                                                   float2 *__restrict__ part_ml, int H, int HKV, int n_past_arg,
-                                                   const int32_t *__restrict__ n_past_dev, int n_chunks, float scale) {
+                                                   float2 *__restrict__ part_ml, int *__restrict__ tickets,
+                                                   float *__restrict__ out, uint8_t *__restrict__ qout, int T, int H,
+                                                   int HKV, int n_past_arg, const int32_t *__restrict__ n_past_dev,
+                                                   int n_chunks, float scale) {
     static_assert(D == 128, "head dim 128");
     const int c = blockIdx.x, hk = blockIdx.y, t = blockIdx.z;
     const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
     if (c * FA_CHUNK > n_past + t) return;               // chunk unused by this query (graph-static grid)
+    const int nused = (n_past + t) / FA_CHUNK + 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int qpos = n_past + t;
     const int p0 = c * FA_CHUNK;
@@ -37,6 +46,7 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
     __shared__ float s_sc[G][FA_CHUNK];
     __shared__ float s_red[4][G][D];
     __shared__ float s_m[G], s_l[G];
+    __shared__ int s_last;
 
     const int sub = lane & 15, kq = lane >> 4;
     float qv[G][8];
@@ -47,16 +57,22 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
 #pragma unroll
         for (int i = 0; i < 4; ++i) { qv[g][2 * i] = h2f(w4[i] & 0xFFFF); qv[g][2 * i + 1] = h2f(w4[i] >> 16); }
     }
-    // ---- scores (issue all 4 K loads first)
-    uint4 kk[4];
+    constexpr int KPW = FA_CHUNK / 4;                    // keys per wave
+    uint4 kk[KPW / 4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int p = p0 + 16 * wave + 4 * i + kq;
+    for (int i = 0; i < KPW / 4; ++i) {
+        const int p = p0 + KPW * wave + 4 * i + kq;
         kk[i] = p < p1 ? *(const uint4 *)(kc + (int64_t)p * EKV + hk * D + sub * 8) : make_uint4(0, 0, 0, 0);
     }
+    uint32_t vv[KPW];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int p = p0 + 16 * wave + 4 * i + kq;
+    for (int i = 0; i < KPW; ++i) {
+        const int p = p0 + KPW * wave + i;
+        vv[i] = p < p1 ? *(const uint32_t *)(vc + (int64_t)p * EKV + hk * D + 2 * lane) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < KPW / 4; ++i) {
+        const int p = p0 + KPW * wave + 4 * i + kq;
         const uint32_t w4[4] = {kk[i].x, kk[i].y, kk[i].z, kk[i].w};
         float kf[8];
 #pragma unroll
@@ -66,73 +82,116 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
             float sc = 0.0f;
 #pragma unroll
             for (int e = 0; e < 8; ++e) sc = fmaf(qv[g][e], kf[e], sc);
-            sc = group_sum<16>(sc);
+            sc += dpp_f<0xB1>(sc); sc += dpp_f<0x4E>(sc); sc += dpp_f<0x141>(sc); sc += dpp_f<0x140>(sc);
             if (sub == 0) s_sc[g][p - p0] = p < p1 ? sc * scale : -INFINITY;
         }
     }
-    // issue the V loads before the softmax barrier (independent of the scores)
-    uint4 vv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int p = p0 + 16 * wave + 4 * i + kq;
-        vv[i] = p < p1 ? *(const uint4 *)(vc + (int64_t)p * EKV + hk * D + sub * 8) : make_uint4(0, 0, 0, 0);
-    }
     __syncthreads();
-    // ---- softmax statistics of the chunk, one wave per head (lane = key)
+    // softmax statistics of the chunk, one wave per head (lanes cover FA_CHUNK keys)
     for (int g = wave; g < G; g += 4) {
-        const float sv = s_sc[g][lane];
-        const float m = wave_max(sv);
-        const float e = (sv == -INFINITY) ? 0.0f : expf(sv - m);
-        s_sc[g][lane] = e;
-        const float l = wave_sum(e);
+        float m = -INFINITY;
+        for (int i = lane; i < FA_CHUNK; i += 64) m = fmaxf(m, s_sc[g][i]);
+        m = wave_max_dpp(m);
+        float l = 0.0f;
+        for (int i = lane; i < FA_CHUNK; i += 64) {
+            const float sv = s_sc[g][i];
+            const float e = (sv == -INFINITY) ? 0.0f : expf(sv - m);
+            s_sc[g][i] = e;
+            l += e;
+        }
+        l = wave_sum_f(l);
         if (lane == 0) { s_m[g] = m; s_l[g] = l; }
     }
     __syncthreads();
-    // ---- P.V: lane owns dims 8*sub..+7 for keys 16w + 4i + kq
-    float acc[G][8];
+    float acc[G][2];
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+    for (int g = 0; g < G; ++g) acc[g][0] = acc[g][1] = 0.0f;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[g][e] = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int kl = 16 * wave + 4 * i + kq;
-        const uint32_t w4[4] = {vv[i].x, vv[i].y, vv[i].z, vv[i].w};
-        float vf[8];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { vf[2 * e] = h2f(w4[e] & 0xFFFF); vf[2 * e + 1] = h2f(w4[e] >> 16); }
+    for (int i = 0; i < KPW; ++i) {
+        const float v0 = h2f(vv[i] & 0xFFFF), v1 = h2f(vv[i] >> 16);
 #pragma unroll
         for (int g = 0; g < G; ++g) {
-            const float pr = s_sc[g][kl];
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(pr, vf[e], acc[g][e]);
+            const float pr = s_sc[g][KPW * wave + i];
+            acc[g][0] = fmaf(pr, v0, acc[g][0]);
+            acc[g][1] = fmaf(pr, v1, acc[g][1]);
         }
     }
 #pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            float v = acc[g][e];
-            v += __shfl_xor(v, 16, 64);
-            v += __shfl_xor(v, 32, 64);
-            acc[g][e] = v;
-        }
-    if (kq == 0) {
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int e = 0; e < 8; ++e) s_red[wave][g][sub * 8 + e] = acc[g][e];
-    }
+    for (int g = 0; g < G; ++g) { s_red[wave][g][2 * lane] = acc[g][0]; s_red[wave][g][2 * lane + 1] = acc[g][1]; }
     __syncthreads();
     for (int i = threadIdx.x; i < G * D; i += 256) {
         const int g = i / D, d = i % D;
         const float o = s_red[0][g][d] + s_red[1][g][d] + s_red[2][g][d] + s_red[3][g][d];
-        const int h = hk * G + g;
-        part_o[(((int64_t)t * H + h) * n_chunks + c) * D + d] = o;
+        part_o[(((int64_t)t * H + hk * G + g) * n_chunks + c) * D + d] = o;
     }
-    if (threadIdx.x < G) {
-        const int h = hk * G + threadIdx.x;
-        part_ml[((int64_t)t * H + h) * n_chunks + c] = make_float2(s_m[threadIdx.x], s_l[threadIdx.x]);
+    if (threadIdx.x < G) part_ml[((int64_t)t * H + hk * G + threadIdx.x) * n_chunks + c] = make_float2(s_m[threadIdx.x], s_l[threadIdx.x]);
+    if constexpr (!FUSED) return;
+    // ---- ticket: the last chunk of (t, hk) to finish merges the partials
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int prev = __hip_atomic_fetch_add(&tickets[t * HKV + hk], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == nused - 1;
+        if (s_last) {
+            __hip_atomic_store(&tickets[t * HKV + hk], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // chunk weights exp(m_c - M) per head; the denominators
+    __shared__ float s_w[G][4096 / FA_CHUNK * 4];
+    for (int g = wave; g < G; g += 4) {
+        const float2 *ml = part_ml + ((int64_t)t * H + hk * G + g) * n_chunks;
+        float M = -INFINITY;
+        for (int cc = lane; cc < nused; cc += 64) M = fmaxf(M, ml[cc].x);
+        M = wave_max_dpp(M);
+        float L = 0.0f;
+        for (int cc = lane; cc < nused; cc += 64) {
+            const float2 v = ml[cc];
+            const float wgt = v.x == -INFINITY ? 0.0f : expf(v.x - M);
+            s_w[g][cc] = wgt;
+            L = fmaf(wgt, v.y, L);
+        }
+        L = wave_sum_f(L);
+        if (lane == 0) s_l[g] = L;
+    }
+    __syncthreads();
+    float *s_out = &s_red[0][0][0];                        // reuse: G*D floats
+    for (int i = threadIdx.x; i < G * D; i += 256) {
+        const int g = i / D, d = i % D;
+        const float *po = part_o + ((int64_t)t * H + hk * G + g) * n_chunks * D + d;
+        float O0 = 0.0f, O1 = 0.0f, O2 = 0.0f, O3 = 0.0f;
+        int cc = 0;
+        for (; cc + 4 <= nused; cc += 4) {
+            O0 = fmaf(s_w[g][cc], po[(int64_t)cc * D], O0);
+            O1 = fmaf(s_w[g][cc + 1], po[(int64_t)(cc + 1) * D], O1);
+            O2 = fmaf(s_w[g][cc + 2], po[(int64_t)(cc + 2) * D], O2);
+            O3 = fmaf(s_w[g][cc + 3], po[(int64_t)(cc + 3) * D], O3);
+        }
+        for (; cc < nused; ++cc) O0 = fmaf(s_w[g][cc], po[(int64_t)cc * D], O0);
+        const float r = ((O0 + O1) + (O2 + O3)) / s_l[g];
+        s_out[i] = r;
+        if (out) out[(int64_t)t * H * D + (int64_t)(hk * G + g) * D + d] = r;
+    }
+    if (qout == nullptr || G * D < 256) return;
+    __syncthreads();
+    // quantize the G*D outputs (G*D/256 Q8_K super-blocks of this kv head's query heads)
+    const int nsbk = G * D / 256;
+    if ((int)threadIdx.x < nsbk * 16) {
+        const int sbl = threadIdx.x >> 4, l16 = threadIdx.x & 15;
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = s_out[sbl * 256 + 16 * l16 + k];
+        const int64_t E = (int64_t)H * D, nsb = E / 256;
+        const int64_t sbg = (int64_t)hk * nsbk + sbl;      // super-block index within the row
+        int8_t *qs = (int8_t *)qout + (int64_t)t * E + sbg * 256;
+        float *dp = (float *)(qout + (int64_t)T * E) + (int64_t)t * nsb + sbg;
+        int16_t *bs = (int16_t *)(qout + (int64_t)T * E + (int64_t)T * nsb * 4) + (int64_t)t * (E / 16) + sbg * 16;
+        q8k_quant16(v, l16, qs, dp, bs);
     }
 }
 
@@ -320,9 +379,11 @@ __global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__
 
 extern "C" {
 
+// partial O + (m, l) per (query, head, chunk) + one ticket per (query, kv head).  The tickets must be
+// zero before first use (allocate zeroed); the merging workgroup resets its ticket.
 int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max) {
     const int64_t nch = (n_kv_max + FA_CHUNK - 1) / FA_CHUNK;
-    return (int64_t)T * H * nch * (128 * 4 + 8) + 256;
+    return (int64_t)T * H * nch * (128 * 4 + 8) + (int64_t)T * H * 4 + 256;
 }
 
 // out f32 [T][H][D] (may be null), qout Q8_K act [T][H*D] (may be null), ws from kcpp_fa_workspace_bytes
@@ -341,20 +402,36 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
         float *po = (float *)ws;
         float2 *pml = (float2 *)(po + (int64_t)T * H * nch * 128);
         const dim3 grid(nch, HKV, T);
-        switch (H / HKV) {
-        case 1: hipLaunchKernelGGL((k_fa_decode<128, 1>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, HKV, n_past, n_past_dev, nch, scale); break;
-        case 2: hipLaunchKernelGGL((k_fa_decode<128, 2>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, HKV, n_past, n_past_dev, nch, scale); break;
-        case 4: hipLaunchKernelGGL((k_fa_decode<128, 4>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, HKV, n_past, n_past_dev, nch, scale); break;
-        case 8: hipLaunchKernelGGL((k_fa_decode<128, 8>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, HKV, n_past, n_past_dev, nch, scale); break;
+        int *tickets = (int *)(pml + (int64_t)T * H * nch);
+        const int G = H / HKV;
+        static const int fuse_env = getenv("KCPP_FA_FUSED") ? atoi(getenv("KCPP_FA_FUSED")) : 0;
+        const bool fused = fuse_env && G >= 2;           // one kv head's outputs must fill Q8_K blocks
+#define KCPP_FA_CASE(GG)                                                                                       \
+    case GG:                                                                                                   \
+        if (fused)                                                                                             \
+            hipLaunchKernelGGL((k_fa_decode<128, GG, true>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, \
+                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale);             \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_fa_decode<128, GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, \
+                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale);             \
+        break;
+        switch (G) {
+            KCPP_FA_CASE(1)
+            KCPP_FA_CASE(2)
+            KCPP_FA_CASE(4)
+            KCPP_FA_CASE(8)
         default: return -3;
         }
+#undef KCPP_FA_CASE
         KCPP_CHECK(hipGetLastError());
-        if (qout)
-            hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, T), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, T, H,
-                               D, n_past, n_past_dev, nch);
-        else
-            hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, T), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, T,
-                               H, D, n_past, n_past_dev, nch);
+        if (!fused) {
+            if (qout)
+                hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, T), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, T,
+                                   H, D, n_past, n_past_dev, nch);
+            else
+                hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, T), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr,
+                                   T, H, D, n_past, n_past_dev, nch);
+        }
         KCPP_CHECK(hipGetLastError());
         return 0;
     }

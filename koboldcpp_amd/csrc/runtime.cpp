@@ -199,6 +199,8 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
               hipHostMalloc((void **)&m->pin, 64, hipHostMallocDefault) == hipSuccess &&
               (m->gemm_ws_sz == 0 || hipMalloc(&m->gemm_ws, m->gemm_ws_sz) == hipSuccess);
     if (!ok) return fail("workspace alloc");
+    // flash-attention tickets must start at zero (the merging workgroup resets its own)
+    if (hipMemset(m->fa_ws, 0, kcpp_fa_workspace_bytes(16, H, hp->n_ctx)) != hipSuccess) return fail("fa ws memset");
     if (has_output) {
         if (hipMalloc(&m->logits, (size_t)hp->n_vocab * 4) != hipSuccess) return fail("logits alloc");
         if (hipHostMalloc((void **)&m->logits_pin, (size_t)hp->n_vocab * 4, hipHostMallocDefault) != hipSuccess)

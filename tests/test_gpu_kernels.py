@@ -248,7 +248,7 @@ def test_flash_attn_vs_oracle(env, T, n_past, path):
     q16 = dev(torch, q.astype(np.float16))
     kd, vd = dev(torch, kcache), dev(torch, vcache)
     out = torch.empty((T, H, D), dtype=torch.float32, device="cuda")
-    ws = empty(torch, K.fa_workspace_bytes(max(T, 16), H, n_ctx))
+    ws = torch.zeros(K.fa_workspace_bytes(max(T, 16), H, n_ctx), dtype=torch.uint8, device="cuda")
     K.call("kcpp_flash_attn", q16.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), None, ws.data_ptr(), T, H,
            HKV, D, n_past, None, n_ctx, 1.0 / np.sqrt(D), path, sptr(torch))
     got = host(torch, out, np.float32).reshape(T, H, D)
@@ -264,7 +264,7 @@ def test_flash_attn_golden(env, golden_ops, key):
     n_kv, HKV, _ = k.shape
     n_past = n_kv - T
     out = torch.empty((T, H, D), dtype=torch.float32, device="cuda")
-    ws = empty(torch, K.fa_workspace_bytes(16, H, n_kv))
+    ws = torch.zeros(K.fa_workspace_bytes(16, H, n_kv), dtype=torch.uint8, device="cuda")
     qd, kd, vd = dev(torch, q.astype(np.float16)), dev(torch, k), dev(torch, v)   # keep alive across the call
     K.call("kcpp_flash_attn", qd.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), None, ws.data_ptr(), T, H,
            HKV, D, n_past, None, n_kv, 1.0 / np.sqrt(D), 0, sptr(torch))
@@ -294,7 +294,7 @@ def test_flash_attn_vs_oracle_f32_accum(env, T, n_past, path):
     q16 = dev(torch, q.astype(np.float16))
     kd, vd = dev(torch, kcache), dev(torch, vcache)
     out = torch.empty((T, H, D), dtype=torch.float32, device="cuda")
-    ws = empty(torch, K.fa_workspace_bytes(max(T, 16), H, n_ctx))
+    ws = torch.zeros(K.fa_workspace_bytes(max(T, 16), H, n_ctx), dtype=torch.uint8, device="cuda")
     K.call("kcpp_flash_attn", q16.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), None, ws.data_ptr(), T, H,
            HKV, D, n_past, None, n_ctx, 1.0 / np.sqrt(D), path, sptr(torch))
     got = host(torch, out, np.float32).reshape(T, H, D)
@@ -318,3 +318,34 @@ def test_gemm_small_shapes(env, t, Kd, N, M):
     np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, res=res), a + res, rtol=0, atol=tol + 1e-6)
     glu = (a / (1 + np.exp(-a))) * b
     np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, mode=1, w2=w2), glu, rtol=1e-5, atol=tol)
+
+
+@pytest.mark.parametrize("H,HKV", [(32, 8), (8, 8), (64, 8), (16, 8)])
+def test_flash_attn_decode_fused_quant(env, H, HKV):
+    """decode FA with the ticketed in-kernel combine (+Q8_K of the output) vs oracle and vs the
+    separate quantizer; repeated calls reuse the self-resetting tickets."""
+    torch, K = env
+    D, n_ctx = 128, 1024
+    rng = np.random.default_rng(H)
+    kcache = (rng.standard_normal((n_ctx, HKV, D)) * 0.5).astype(np.float16)
+    vcache = rng.standard_normal((n_ctx, HKV, D)).astype(np.float16)
+    kd, vd = dev(torch, kcache), dev(torch, vcache)
+    ws = torch.zeros(K.fa_workspace_bytes(16, H, n_ctx), dtype=torch.uint8, device="cuda")
+    for n_past in (0, 127, 128, 700):
+        q = rng.standard_normal((1, H, D)).astype(np.float32)
+        q16 = dev(torch, q.astype(np.float16))
+        out = torch.empty((1, H, D), dtype=torch.float32, device="cuda")
+        qa = empty(torch, K.act_bytes(R.Q4_K, H * D, 1))
+        K.call("kcpp_flash_attn", q16.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), qa.data_ptr(),
+               ws.data_ptr(), 1, H, HKV, D, n_past, None, n_ctx, 1.0 / np.sqrt(D), 1, sptr(torch))
+        got = host(torch, out, np.float32).reshape(1, H, D)
+        n_kv = n_past + 1
+        R.lib().orc_set_fa_f32_accum(1)
+        try:
+            want = R.flash_attn(q, kcache[:n_kv], vcache[:n_kv], None)
+        finally:
+            R.lib().orc_set_fa_f32_accum(0)
+        np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
+        ref = R.quantize(R.Q8_K, got.ravel()).reshape(-1, 292)
+        gq = host(torch, qa, np.uint8)
+        assert np.array_equal(gq[:H * D].reshape(-1, 256), ref[:, 4:260])

@@ -51,7 +51,7 @@ def main():
     for (T, n_past) in [(512, 0), (512, 3328), (1, 4095), (1, 1024)]:
         q = torch.randn(T, H, D, device="cuda").half()
         o = torch.empty(T, H, D, device="cuda")
-        ws = torch.empty(K.fa_workspace_bytes(max(T, 16), H, n_ctx), dtype=torch.uint8, device="cuda")
+        ws = torch.zeros(K.fa_workspace_bytes(max(T, 16), H, n_ctx), dtype=torch.uint8, device="cuda")
         f = lambda: K.call("kcpp_flash_attn", q.data_ptr(), kc.data_ptr(), vc.data_ptr(), o.data_ptr(), None, ws.data_ptr(),
                            T, H, HKV, D, n_past, None, n_ctx, 1 / np.sqrt(D), 0, s)
         ms = timeit(f)
