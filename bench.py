@@ -39,44 +39,48 @@ def weight_bytes(hp, types):
     return sum(R.row_bytes(t, k) * n for (k, n), t in zip(R.weight_shapes(hp), types))
 
 
-def measure_roofline(K, torch, iters=50):
-    """Time the dominant decode kernel: Q4_K GLU mat-vec (ffn_gate|ffn_up, 4096 -> 14336)."""
+def measure_roofline(K, torch, iters=48):
+    """Time the dominant decode kernel as the decode path launches it: the fused Q4_K gate|up
+    mat-vec with rms_norm+Q8_K prologue and SiLU-GLU epilogue (k_gemv_dec<Q4_K, mode 1, pro 1>,
+    4096 -> 2 x 14336), HIP events on the launch stream.  Algorithmic bytes per launch =
+    both weight matrices + x + norm weight + output row ("roofline")."""
     Kd, N = 4096, 14336
     wbytes = Kd // 256 * 144 * N
-    w = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
-    w2 = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
-    s = torch.cuda.current_stream().cuda_stream
-    K.call("kcpp_weight_synth", 12, 1, 1, w.data_ptr(), Kd, N, s)
-    K.call("kcpp_weight_synth", 12, 1, 2, w2.data_ptr(), Kd, N, s)
-    x = torch.randn(Kd, device="cuda")
-    act = torch.empty(K.act_bytes(12, Kd, 1), dtype=torch.uint8, device="cuda")
-    K.call("kcpp_quantize_act", 15, x.data_ptr(), Kd, act.data_ptr(), Kd, 1, s)
-    y = torch.empty(N, device="cuda")
-    args = (12, w.data_ptr(), w2.data_ptr(), Kd, N, act.data_ptr(), 1, y.data_ptr(), N, None, 0, 1, s)
-    for _ in range(5):
-        K.call("kcpp_gemv", *args)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    # rotate over 4 weight pairs so the 66 MB working set is not L3-resident (>256 MiB total)
-    ws = [(w, w2)]
-    for i in range(3):
+    s = torch.cuda.current_stream()
+    sp = s.cuda_stream
+    # 4 weight pairs (264 MB) so consecutive launches do not hit the 256 MiB Infinity Cache
+    ws = []
+    for i in range(4):
         a = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
         b = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
-        K.call("kcpp_weight_synth", 12, 1, 10 + 2 * i, a.data_ptr(), Kd, N, s)
-        K.call("kcpp_weight_synth", 12, 1, 11 + 2 * i, b.data_ptr(), Kd, N, s)
+        K.call("kcpp_weight_synth", 12, 1, 10 + 2 * i, a.data_ptr(), Kd, N, sp)
+        K.call("kcpp_weight_synth", 12, 1, 11 + 2 * i, b.data_ptr(), Kd, N, sp)
         ws.append((a, b))
+    x = torch.randn(Kd, device="cuda")
+    nw = torch.ones(Kd, device="cuda")
+    y = torch.empty(N, device="cuda")
+    args = []
+    for a, b in ws:
+        d = K.DecArgs()
+        d.K, d.x, d.nw, d.eps, d.nseg = Kd, x.data_ptr(), nw.data_ptr(), 1e-5, 1
+        d.W[0], d.W2, d.N[0], d.Y[0] = a.data_ptr(), b.data_ptr(), N, y.data_ptr()
+        args.append(d)
+    for i in range(8):
+        assert K.gemv_dec(12, args[i % 4], 1, 1, 1, sp) == 0
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
-    e0.record()
+    e0.record(s)
     for i in range(iters):
-        a, b = ws[i % len(ws)]
-        K.call("kcpp_gemv", 12, a.data_ptr(), b.data_ptr(), Kd, N, act.data_ptr(), 1, y.data_ptr(), N, None, 0, 1, s)
-    e1.record()
+        K.gemv_dec(12, args[i % 4], 1, 1, 1, sp)
+    e1.record(s)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
-    alg = 2 * wbytes + K.act_bytes(12, Kd, 1) + N * 4          # weights + activation + output
+    alg = 2 * wbytes + 2 * Kd * 4 + N * 4
     gbs = alg / (ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "k_gemv<Q4_K,GLU> 4096x(2x14336)", "bytes_per_launch": alg, "avg_us": round(ms * 1e3, 2)}
+            "kernel": "k_gemv_dec<Q4_K,GLU,norm+quant prologue> 4096x(2x14336)", "bytes_per_launch": alg,
+            "avg_us": round(ms * 1e3, 2)}
 
 
 def cpu_baseline(hp, types, threads, n_prompt=32, n_gen=4):
@@ -87,7 +91,14 @@ def cpu_baseline(hp, types, threads, n_prompt=32, n_gen=4):
     hp2 = dict(hp)
     hp2["n_ctx"] = n_prompt + n_gen + 8
     _, info = R.run_ref_llama(hp2, types, 1234, prompt, n_gen, nthreads=threads, ubatch=512, timeout=900)
+    cpu = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu = next(l.split(":", 1)[1].strip() for l in f if l.startswith("model name"))
+    except Exception:
+        pass
     return {"value": round(n_gen / info["decode_s"], 3), "unit": "tok/s (decode)", "cores": threads,
+            "cpu_model": cpu, "host_cpus": os.cpu_count(),
             "kind": "reference",
             "prefill_tok_s": round(n_prompt / info["prefill_s"], 3),
             "sample": "reference ggml CPU (oracle/_ref/ref_llama) on the same synthetic Llama-3-8B Q4_K_M: "

@@ -107,6 +107,12 @@ float *kcpp_model_hidden(kcpp_model *m);
 /* copy n floats of the residual stream starting at float offset (debug / pipeline host path) */
 int kcpp_model_read_hidden(kcpp_model *m, float *host, int64_t n_floats, int64_t offset);
 void *kcpp_model_stream(kcpp_model *m);
+/* stream-ordered copy of n_floats of the residual stream at float offset to/from buf (device or host
+ * memory): dir 0 = buf -> stage input, 1 = stage output -> buf.  Pipeline handoff (replaces
+ * ggml_backend_cuda_cpy_tensor_async, ggml/src/ggml-cuda.cu:2392-2445). */
+int kcpp_model_hidden_io(kcpp_model *m, void *buf, int64_t n_floats, int64_t offset, int dir);
+/* wait for all work queued on the stage's stream */
+int kcpp_model_sync(kcpp_model *m);
 /* per-stage step without embedding/out: run layers on the hidden buffer for T tokens */
 int kcpp_model_forward_hidden(kcpp_model *m, int T, int n_past);
 /* greedy argmax of the last logits on device (avoids the 0.5 MB logits copy) */

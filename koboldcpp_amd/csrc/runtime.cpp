@@ -265,6 +265,22 @@ extern "C" int kcpp_model_read_hidden(kcpp_model *m, float *host, int64_t n_floa
     RT_CHECK(hipMemcpy(host, m->x + offset, (size_t)n_floats * 4, hipMemcpyDeviceToHost));
     return 0;
 }
+// stream-ordered copy between the residual stream and a caller buffer (device or pinned/pageable
+// host; hipMemcpyDefault infers the direction).  dir 0: buf -> stage input, 1: stage output -> buf.
+// Pipeline handoff replacing ggml_backend_cuda_cpy_tensor_async (ggml-cuda.cu:2392-2445).
+extern "C" int kcpp_model_hidden_io(kcpp_model *m, void *buf, int64_t n_floats, int64_t offset, int dir) {
+    RT_CHECK(hipSetDevice(m->device));
+    if (n_floats < 0 || offset < 0 || offset + n_floats > (int64_t)m->ub * m->hp.n_embd) { g_err = "hidden_io: range"; return -2; }
+    float *x = m->x + offset;
+    RT_CHECK(hipMemcpyAsync(dir ? buf : (void *)x, dir ? (const void *)x : buf, (size_t)n_floats * 4, hipMemcpyDefault,
+                            m->stream));
+    return 0;
+}
+extern "C" int kcpp_model_sync(kcpp_model *m) {
+    RT_CHECK(hipSetDevice(m->device));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    return 0;
+}
 extern "C" void *kcpp_model_stream(kcpp_model *m) { return m->stream; }
 extern "C" int64_t kcpp_model_weight_bytes(kcpp_model *m) { return m->weight_bytes; }
 extern "C" int kcpp_model_set_graphs(kcpp_model *m, int enable) {
@@ -463,6 +479,7 @@ extern "C" int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, in
     RT_CHECK(hipSetDevice(m->device));
     const kcpp_hparams &hp = m->hp;
     if (T < 1 || n_past + T > hp.n_ctx) { g_err = "context overflow"; return -2; }
+    if (m->has_embed && !tokens) { g_err = "decode: stage owns the embedding but tokens == NULL"; return -2; }
     if (T == 1 && m->use_graphs) {
         m->pin[0] = m->has_embed ? tokens[0] : 0;
         m->pin[1] = n_past;

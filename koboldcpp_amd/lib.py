@@ -47,6 +47,8 @@ _SIGS = {
     "kcpp_model_hidden": [P],
     "kcpp_model_read_hidden": [P, P, I64, I64],
     "kcpp_model_stream": [P],
+    "kcpp_model_hidden_io": [P, P, I64, I64, I],
+    "kcpp_model_sync": [P],
     "kcpp_model_forward_hidden": [P, I, I],
     "kcpp_model_argmax": [P, P],
     "kcpp_model_set_graphs": [P, I],
@@ -102,6 +104,23 @@ def fa_workspace_bytes(T, H, n_kv):
     return int(_L.kcpp_fa_workspace_bytes(T, H, n_kv))
 
 
+class DecArgs(ctypes.Structure):
+    """mirror of struct DecArgs (koboldcpp_amd/csrc/kcpp_internal.h), checked against
+    kcpp_gemv_dec_args_size() at import"""
+    _fields_ = [("W", P * 3), ("Y", P * 3), ("N", I64 * 3), ("role", I * 3), ("nseg", I), ("W2", P), ("K", I64),
+                ("act", P), ("x", P), ("nw", P), ("eps", Fl), ("res", P), ("q16", P), ("kc", P), ("vc", P),
+                ("ekv", I64), ("D", I), ("pos", P), ("rope_tab", P)]
+
+
+if ctypes.sizeof(DecArgs) != _L.kcpp_gemv_dec_args_size():
+    raise ImportError("DecArgs layout mismatch: %d vs %d" % (ctypes.sizeof(DecArgs), _L.kcpp_gemv_dec_args_size()))
+
+
+def gemv_dec(wtype, args, mode, pro, rows_per_wave, stream):
+    """fused single-token mat-vec; returns the native rc (-8 = K too large for the fused kernel)"""
+    return int(_L.kcpp_gemv_dec(wtype, ctypes.byref(args), mode, pro, rows_per_wave, stream))
+
+
 class HParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")] + \
                [(n, ctypes.c_float) for n in ("eps", "rope_base", "rope_freq_scale")]
@@ -131,11 +150,17 @@ class Model:
     def set_tensor(self, idx, arr):
         _chk(_L.kcpp_model_set_tensor(self.m, idx, arr.ctypes.data_as(P), arr.nbytes), "set_tensor")
 
-    def decode(self, tokens, n_past, want_logits=True):
+    def decode(self, tokens, n_past, want_logits=True, n_tokens=None):
+        """llama_decode of len(tokens) tokens at n_past.  A stage without the embedding takes
+        tokens=None and n_tokens=T: its input is the residual stream placed with hidden_io."""
         import numpy as np
-        tok = np.ascontiguousarray(tokens, dtype=np.int32)
+        if tokens is None:
+            tok, T = None, int(n_tokens)
+        else:
+            tok = np.ascontiguousarray(tokens, dtype=np.int32)
+            T = len(tok)
         logits = np.empty(self.hp["n_vocab"], np.float32) if want_logits else None
-        _chk(_L.kcpp_model_decode(self.m, tok.ctypes.data_as(P), len(tok), n_past,
+        _chk(_L.kcpp_model_decode(self.m, tok.ctypes.data_as(P) if tok is not None else None, T, n_past,
                                   logits.ctypes.data_as(P) if want_logits else None), "decode")
         return logits
 
@@ -152,6 +177,13 @@ class Model:
         out = np.empty(n, np.float32)
         _chk(_L.kcpp_model_read_hidden(self.m, out.ctypes.data_as(P), n, offset), "read_hidden")
         return out
+
+    def hidden_io(self, ptr, n, offset=0, to_buf=False):
+        """stream-ordered copy between the residual stream and ptr (device or host address)"""
+        _chk(_L.kcpp_model_hidden_io(self.m, ptr, n, offset, int(to_buf)), "hidden_io")
+
+    def sync(self):
+        _chk(_L.kcpp_model_sync(self.m), "sync")
 
     def hidden_ptr(self):
         return _L.kcpp_model_hidden(self.m)
