@@ -114,6 +114,8 @@ def main():
     ap.add_argument("--ubatch", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="only the dominant-kernel timing (for the rocprofv3 --pmc passes in profiles/)")
     ap.add_argument("--layers", type=int, default=None, help="override n_layer (debug only; invalidates metric)")
     args = ap.parse_args()
 
@@ -128,6 +130,9 @@ def main():
         return pipeline.bench_main(args, world, rank, local)
 
     torch.cuda.set_device(0)
+    if args.roofline_only:
+        print(json.dumps({"roofline": measure_roofline(K, torch)}))
+        return
     hp = dict(LLAMA3_8B)
     if args.layers:
         hp["n_layer"] = args.layers

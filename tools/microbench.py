@@ -1,5 +1,8 @@
 """Kernel micro-benchmarks (HIP-event timed) for the hot path: mat-vec (decode), MFMA GEMM (prefill),
 flash attention.  Prints one JSON line per kernel.  Not part of the driver contract."""
+import os
+import sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import json
 import sys
 

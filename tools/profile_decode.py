@@ -1,4 +1,7 @@
 """Decode-step workload for rocprofv3 (kernel trace): Llama-3-8B Q4_K_M synthetic, context ~4k."""
+import os
+import sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import sys
 import torch
 import koboldcpp_amd.lib as K
