@@ -147,18 +147,16 @@ def main():
     m.decode(prompt, 0, want_logits=False)
     torch.cuda.synchronize()
     t_pp = time.perf_counter() - t0
-    tok = m.argmax()
+    tok = m.argmax()                      # first generated token; stays on device for the next step
     n_past = len(prompt)
     for _ in range(args.warmup):
-        m.decode([tok], n_past, want_logits=False)
-        tok = m.argmax()
+        tok = m.decode_greedy(n_past)
         n_past += 1
     steps = min(args.steps, hp["n_ctx"] - n_past)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(steps):
-        m.decode([tok], n_past, want_logits=False)
-        tok = m.argmax()
+    for _ in range(steps):                # greedy generation: graph replay + on-device argmax per token
+        tok = m.decode_greedy(n_past)
         n_past += 1
     torch.cuda.synchronize()
     t_tg = time.perf_counter() - t0

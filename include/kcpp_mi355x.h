@@ -60,6 +60,9 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
  * 1 silu-GLU, 2 RoPE + K/V-cache store; pro 0 act given, 1 rms_norm+quantize prologue, 2 quantize. */
 int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream);
 int64_t kcpp_gemv_dec_args_size(void);
+/* the coalesced-streaming Q4_K variant kcpp_gemv_dec dispatches to (koboldcpp_amd/csrc/gemv_stream.hip);
+ * returns -3 when the type/shape/mode is not covered.  Exposed for the parity tests and tools. */
+int kcpp_gemv_stream(int type, const void *args, int mode, int pro, void *stream);
 
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,
@@ -115,8 +118,13 @@ int kcpp_model_hidden_io(kcpp_model *m, void *buf, int64_t n_floats, int64_t off
 int kcpp_model_sync(kcpp_model *m);
 /* per-stage step without embedding/out: run layers on the hidden buffer for T tokens */
 int kcpp_model_forward_hidden(kcpp_model *m, int T, int n_past);
-/* greedy argmax of the last logits on device (avoids the 0.5 MB logits copy) */
+/* greedy argmax of the last logits on device (avoids the 0.5 MB logits copy); also becomes the
+ * next decode_greedy step's input token */
 int kcpp_model_argmax(kcpp_model *m, int32_t *token_out);
+/* one greedy generation step at n_past: input = the previous argmax (device-resident), the step's
+ * own argmax computed in the same graph replay and returned (one host sync per token).
+ * Requires a stage owning both the embedding and the output head. */
+int kcpp_model_decode_greedy(kcpp_model *m, int n_past, int32_t *token_out);
 /* enable/disable hipGraph replay for single-token decode (default on) */
 int kcpp_model_set_graphs(kcpp_model *m, int enable);
 /* single-token decode through the fused mat-vec path (default on); off = one kernel per op */

@@ -195,61 +195,82 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
     }
 }
 
-// combine split-KV partials; one 256-thread workgroup covers two heads (= one Q8_K block of 256).
-// Per head one wave turns the chunk maxima into weights exp(m_c - M) (lane = chunk, <= 64 per
-// pass), then every thread sums its dim over the chunks with independent loads.
+// combine split-KV partials; one 1024-thread workgroup covers two heads (= one Q8_K block of 256).
+// Latency-bound (a few hundred KB from L2), so it is built for memory-level parallelism: every
+// thread issues its 16 partial-O loads (4 threads per output dim split the chunks) together with
+// the chunk (m, l) loads, then the chunk weights exp(m_c - M) are formed in LDS and applied.
 template <bool QUANT>
-__global__ void __launch_bounds__(256) k_fa_combine(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
-                                                    float *__restrict__ out, uint8_t *__restrict__ qout, int T, int H,
-                                                    int D, int n_past_arg, const int32_t *__restrict__ n_past_dev,
-                                                    int n_chunks_alloc) {
+__global__ void __launch_bounds__(1024) k_fa_combine(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
+                                                     float *__restrict__ out, uint8_t *__restrict__ qout, int T, int H,
+                                                     int D, int n_past_arg, const int32_t *__restrict__ n_past_dev,
+                                                     int n_chunks_alloc) {
+    constexpr int MAXCH = 4096 / FA_CHUNK * 4;         // 16k context
     const int t = blockIdx.y;
     const int pair = blockIdx.x;                       // heads 2*pair, 2*pair+1
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int hl = tid >> 9, r = tid & 511, d = r & 127, cg = r >> 7;
+    const int h = 2 * pair + hl;
     const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
     const int nch = (n_past + t) / FA_CHUNK + 1;       // chunks this query actually used
-    __shared__ float s_w[2][4096 / FA_CHUNK * 4];
-    __shared__ float s_inv[2];
-    if (wave < 2) {
-        const int h = 2 * pair + wave;
-        const float2 *ml = part_ml + ((int64_t)t * H + h) * n_chunks_alloc;
-        float M = -INFINITY;
-        for (int c = lane; c < nch; c += 64) M = fmaxf(M, ml[c].x);
-        M = wave_max(M);
-        float L = 0.0f;
-        for (int c = lane; c < nch; c += 64) {
-            const float2 v = ml[c];
-            const float wgt = v.x == -INFINITY ? 0.0f : expf(v.x - M);
-            s_w[wave][c] = wgt;
-            L = fmaf(wgt, v.y, L);
-        }
-        L = wave_sum(L);
-        if (lane == 0) s_inv[wave] = L;
-    }
-    __syncthreads();
-    const int hl = tid >> 7, d = tid & 127, h = 2 * pair + hl;
+    __shared__ float s_w[2][MAXCH];
+    __shared__ float s_red[16];
+    __shared__ float s_sum[2][4][128];
+    const float2 *ml = part_ml + ((int64_t)t * H + h) * n_chunks_alloc;
     const float *po = part_o + ((int64_t)t * H + h) * n_chunks_alloc * 128 + d;
-    float O0 = 0.0f, O1 = 0.0f, O2 = 0.0f, O3 = 0.0f;
-    int c = 0;
-    for (; c + 4 <= nch; c += 4) {
-        O0 = fmaf(s_w[hl][c], po[(int64_t)c * 128], O0);
-        O1 = fmaf(s_w[hl][c + 1], po[(int64_t)(c + 1) * 128], O1);
-        O2 = fmaf(s_w[hl][c + 2], po[(int64_t)(c + 2) * 128], O2);
-        O3 = fmaf(s_w[hl][c + 3], po[(int64_t)(c + 3) * 128], O3);
+    // (m, l) of chunk r (r < nch), and this thread's first 16 O partials, all in flight together
+    const float2 mlv = r < nch ? ml[r] : make_float2(-INFINITY, 0.0f);
+    float ov[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int c = cg + 4 * k;
+        ov[k] = c < nch ? po[(int64_t)c * 128] : 0.0f;
     }
-    for (; c < nch; ++c) O0 = fmaf(s_w[hl][c], po[(int64_t)c * 128], O0);
-    const float r = ((O0 + O1) + (O2 + O3)) / s_inv[hl];
-    const int64_t e = (int64_t)t * H * 128 + (int64_t)h * 128 + d;
-    if (out) out[e] = r;
+    // M = max_c m_c per head: waves 0-7 hold head 0's chunks, 8-15 head 1's
+    float M = wave_max(mlv.x);
+    if (lane == 0) s_red[wave] = M;
+    __syncthreads();
+    M = s_red[8 * hl];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) M = fmaxf(M, s_red[8 * hl + w]);
+    const float wgt = mlv.x == -INFINITY ? 0.0f : expf(mlv.x - M);
+    if (r < MAXCH) s_w[hl][r] = wgt;
+    float L = wave_sum(wgt * mlv.y);
+    __syncthreads();                                   // s_red reuse + s_w visible
+    if (lane == 0) s_red[wave] = L;
+    __syncthreads();
+    L = 0.0f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) L += s_red[8 * hl + w];
+    float O = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int c = cg + 4 * k;
+        if (c < nch) O = fmaf(s_w[hl][c], ov[k], O);
+    }
+    for (int c0 = 64; c0 < nch; c0 += 64) {            // contexts beyond 64 chunks
+#pragma unroll 4
+        for (int k = 0; k < 16; ++k) {
+            const int c = c0 + cg + 4 * k;
+            if (c < nch) O = fmaf(s_w[hl][c], po[(int64_t)c * 128], O);
+        }
+    }
+    s_sum[hl][cg][d] = O;
+    __syncthreads();
+    if (cg == 0) {
+        const float res = ((s_sum[hl][0][d] + s_sum[hl][1][d]) + (s_sum[hl][2][d] + s_sum[hl][3][d])) / L;
+        const int64_t e = (int64_t)t * H * 128 + (int64_t)h * 128 + d;
+        if (out) out[e] = res;
+        s_sum[hl][0][d] = res;
+    }
     if constexpr (QUANT) {
-        // regroup so that lane j of the 16-lane group holds elements 16j..16j+15 of the block
-        __shared__ float s_v[256];
-        s_v[tid] = r;
         __syncthreads();
-        if (tid < 16) {
+        if (tid < 16) {                                // lane j holds elements 16j..16j+15 of the block
             float v[16];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = s_v[16 * tid + k];
+            for (int k = 0; k < 16; ++k) {
+                const int e = 16 * tid + k;
+                v[k] = s_sum[e >> 7][0][e & 127];
+            }
             const int64_t E = (int64_t)H * 128;
             const int64_t nsb = E / 256;
             int8_t *qs = (int8_t *)qout + (int64_t)t * E + pair * 256;
@@ -426,10 +447,10 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
         KCPP_CHECK(hipGetLastError());
         if (!fused) {
             if (qout)
-                hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, T), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, T,
+                hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, T), dim3(1024), 0, s, po, pml, out, (uint8_t *)qout, T,
                                    H, D, n_past, n_past_dev, nch);
             else
-                hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, T), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr,
+                hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, T), dim3(1024), 0, s, po, pml, out, (uint8_t *)nullptr,
                                    T, H, D, n_past, n_past_dev, nch);
         }
         KCPP_CHECK(hipGetLastError());

@@ -2,11 +2,19 @@
 #include "kcpp_internal.h"
 #include "kcpp_common.h"
 
+#include <cstdlib>
+
 template <int TYPE> int dispatch_mode(const DecArgs &a, int mode, int pro, int rows_per_wave, hipStream_t s);
 
 extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream) {
     const DecArgs &a = *(const DecArgs *)args;
     hipStream_t s = (hipStream_t)stream;
+    // coalesced-streaming kernel where it covers the type/shape (gemv_stream.hip), else unit-per-lane
+    static const int use_stream = getenv("KCPP_STREAM") ? atoi(getenv("KCPP_STREAM")) : 1;
+    if (use_stream) {
+        const int rc = kcpp_gemv_stream(type, args, mode, pro, stream);
+        if (rc != -3) return rc;
+    }
     switch (type) {
     case KT_Q4_K: return dispatch_mode<KT_Q4_K>(a, mode, pro, rows_per_wave, s);
     case KT_Q5_K: return dispatch_mode<KT_Q5_K>(a, mode, pro, rows_per_wave, s);

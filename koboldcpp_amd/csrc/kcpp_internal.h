@@ -34,4 +34,6 @@ struct DecArgs {
     const float2 *rope_tab;
 };
 extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream);
+// coalesced Q4_K variant (gemv_stream.hip); -3 = not covered
+extern "C" int kcpp_gemv_stream(int type, const void *args, int mode, int pro, void *stream);
 

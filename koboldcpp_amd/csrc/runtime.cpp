@@ -79,6 +79,7 @@ struct kcpp_model {
     void *act = nullptr, *act2 = nullptr, *fa_ws = nullptr, *gemm_ws = nullptr;
     size_t act_sz = 0, gemm_ws_sz = 0;
     int32_t *tok_dev = nullptr, *pos_dev = nullptr, *argmax_dev = nullptr;
+    void *argmax_ws = nullptr;       // ARGMAX_BLOCKS (value, index) partials
     float2 *rope_tab = nullptr;
     int32_t *pin = nullptr;          // pinned host {token, n_past}
     float *logits_pin = nullptr;
@@ -87,6 +88,9 @@ struct kcpp_model {
     hipGraphExec_t g_exec = nullptr;
     int64_t weight_bytes = 0;
 };
+
+static int ensure_graph(kcpp_model *m);
+static int launch_argmax(kcpp_model *m);
 
 static int64_t tensor_bytes(int type, int64_t K, int64_t N) {
     return K / ks_block_elems(type) * N * ks_block_bytes(type);
@@ -194,7 +198,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
               hipMalloc(&m->act2, m->act_sz) == hipSuccess &&
               hipMalloc(&m->fa_ws, kcpp_fa_workspace_bytes(std::max<int>(16, 1), H, hp->n_ctx)) == hipSuccess &&
               hipMalloc(&m->tok_dev, UB * 4) == hipSuccess && hipMalloc(&m->pos_dev, 64) == hipSuccess &&
-              hipMalloc(&m->argmax_dev, 64) == hipSuccess &&
+              hipMalloc(&m->argmax_dev, 64) == hipSuccess && hipMalloc(&m->argmax_ws, 256 * 8) == hipSuccess &&
               hipMalloc(&m->rope_tab, (size_t)hp->n_ctx * D / 2 * sizeof(float2)) == hipSuccess &&
               hipHostMalloc((void **)&m->pin, 64, hipHostMallocDefault) == hipSuccess &&
               (m->gemm_ws_sz == 0 || hipMalloc(&m->gemm_ws, m->gemm_ws_sz) == hipSuccess);
@@ -221,7 +225,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     F(m->tok_embd.d); F(m->output_norm.d); F(m->output.d);
     for (auto &L : m->layers) { for (auto &t : L.t) F(t.d); F(L.kc); F(L.vc); }
     F(m->x); F(m->qkv); F(m->attn); F(m->h); F(m->logits); F(m->q16); F(m->act); F(m->act2); F(m->fa_ws);
-    F(m->gemm_ws); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->rope_tab);
+    F(m->gemm_ws); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
     if (m->pin) hipHostFree(m->pin);
     if (m->logits_pin) hipHostFree(m->logits_pin);
     if (m->stream) hipStreamDestroy(m->stream);
@@ -467,6 +471,21 @@ static int decode_step_dev(kcpp_model *m) {
         RC(forward_layers(m, 1, 0, true));
         if (m->has_output) RC(head(m, 1));
     }
+    if (m->has_output) RC(launch_argmax(m));      // greedy token on device (tok_dev for the next step)
+    return 0;
+}
+
+// single-token graph: pos_dev <- pin[1] (read at replay time), embedding of tok_dev, layers, head, argmax
+static int ensure_graph(kcpp_model *m) {
+    if (m->g_exec) return 0;
+    hipGraph_t g;
+    RT_CHECK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
+    hipMemcpyAsync(m->pos_dev, &m->pin[1], 4, hipMemcpyHostToDevice, m->stream);
+    int rc = decode_step_dev(m);
+    hipError_t e = hipStreamEndCapture(m->stream, &g);
+    if (rc || e != hipSuccess) { g_err = "graph capture failed"; return rc ? rc : -3; }
+    RT_CHECK(hipGraphInstantiate(&m->g_exec, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
     return 0;
 }
 
@@ -483,17 +502,8 @@ extern "C" int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, in
     if (T == 1 && m->use_graphs) {
         m->pin[0] = m->has_embed ? tokens[0] : 0;
         m->pin[1] = n_past;
-        if (!m->g_exec) {
-            hipGraph_t g;
-            RT_CHECK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
-            hipMemcpyAsync(m->tok_dev, &m->pin[0], 4, hipMemcpyHostToDevice, m->stream);
-            hipMemcpyAsync(m->pos_dev, &m->pin[1], 4, hipMemcpyHostToDevice, m->stream);
-            int rc = decode_step_dev(m);
-            hipError_t e = hipStreamEndCapture(m->stream, &g);
-            if (rc || e != hipSuccess) { g_err = "graph capture failed"; return rc ? rc : -3; }
-            RT_CHECK(hipGraphInstantiate(&m->g_exec, g, nullptr, nullptr, 0));
-            hipGraphDestroy(g);
-        }
+        if (m->has_embed) RT_CHECK(hipMemcpyAsync(m->tok_dev, &m->pin[0], 4, hipMemcpyHostToDevice, m->stream));
+        RC(ensure_graph(m));
         RT_CHECK(hipGraphLaunch(m->g_exec, m->stream));
     } else if (T == 1) {
         m->pin[0] = m->has_embed ? tokens[0] : 0;
@@ -521,28 +531,70 @@ extern "C" int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, in
     return 0;
 }
 
-__global__ void k_argmax(const float *__restrict__ x, int n, int32_t *out) {
-    __shared__ float sv[256];
-    __shared__ int si[256];
-    float bv = -INFINITY; int bi = 0;
-    for (int i = threadIdx.x; i < n; i += 256) if (x[i] > bv) { bv = x[i]; bi = i; }
-    sv[threadIdx.x] = bv; si[threadIdx.x] = bi;
+// greedy argmax over the logits (first index wins ties, like the CPU sampler's top-1):
+// stage 1, ARGMAX_BLOCKS workgroups reduce strided slices to (value, index) pairs; stage 2, one
+// workgroup reduces those and writes the token to out[0] (and to tok[0] when given: the next
+// decode step's embedding input, so a greedy loop never round-trips the token through the host).
+#define ARGMAX_BLOCKS 256
+__device__ __forceinline__ void amax_merge(float &v, int &i, float v2, int i2) {
+    if (v2 > v || (v2 == v && i2 < i)) { v = v2; i = i2; }
+}
+__device__ __forceinline__ void amax_block(float &v, int &i) {
+    for (int o = 32; o > 0; o >>= 1) amax_merge(v, i, __shfl_xor(v, o, 64), __shfl_xor(i, o, 64));
+    __shared__ float sv[4];
+    __shared__ int si[4];
+    if ((threadIdx.x & 63) == 0) { sv[threadIdx.x >> 6] = v; si[threadIdx.x >> 6] = i; }
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (threadIdx.x < o) {
-            const float v2 = sv[threadIdx.x + o]; const int i2 = si[threadIdx.x + o];
-            if (v2 > sv[threadIdx.x] || (v2 == sv[threadIdx.x] && i2 < si[threadIdx.x])) { sv[threadIdx.x] = v2; si[threadIdx.x] = i2; }
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) *out = si[0];
+    v = sv[0]; i = si[0];
+    for (int w = 1; w < 4; ++w) amax_merge(v, i, sv[w], si[w]);
+}
+__global__ void __launch_bounds__(256) k_argmax_part(const float *__restrict__ x, int n, float2 *part) {
+    float v = -INFINITY; int i = 0x7fffffff;
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += ARGMAX_BLOCKS * 256) amax_merge(v, i, x[j], j);
+    amax_block(v, i);
+    if (threadIdx.x == 0) part[blockIdx.x] = make_float2(v, __int_as_float(i));
+}
+__global__ void __launch_bounds__(256) k_argmax_final(const float2 *__restrict__ part, int32_t *out, int32_t *tok) {
+    const float2 p = part[threadIdx.x];
+    float v = p.x; int i = __float_as_int(p.y);
+    amax_block(v, i);
+    if (threadIdx.x == 0) { out[0] = i; if (tok) tok[0] = i; }
+}
+static int launch_argmax(kcpp_model *m) {
+    hipLaunchKernelGGL(k_argmax_part, dim3(ARGMAX_BLOCKS), dim3(256), 0, m->stream, m->logits, m->hp.n_vocab,
+                       (float2 *)m->argmax_ws);
+    hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, m->stream, (const float2 *)m->argmax_ws, m->argmax_dev,
+                       m->has_embed ? m->tok_dev : nullptr);
+    RT_CHECK(hipGetLastError());
+    return 0;
 }
 
 extern "C" int kcpp_model_argmax(kcpp_model *m, int32_t *token_out) {
     if (!m->has_output) return -1;
     RT_CHECK(hipSetDevice(m->device));
-    hipLaunchKernelGGL(k_argmax, dim3(1), dim3(256), 0, m->stream, m->logits, m->hp.n_vocab, m->argmax_dev);
-    RT_CHECK(hipMemcpyAsync(token_out, m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
+    RC(launch_argmax(m));
+    RT_CHECK(hipMemcpyAsync(&m->pin[2], m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
     RT_CHECK(hipStreamSynchronize(m->stream));
+    *token_out = m->pin[2];
+    return 0;
+}
+
+// One greedy step: the input token is the previous argmax (already in tok_dev), the step's own
+// argmax is computed inside the same graph replay and returned.  One host sync per token.
+extern "C" int kcpp_model_decode_greedy(kcpp_model *m, int n_past, int32_t *token_out) {
+    if (!m->has_embed || !m->has_output) { g_err = "decode_greedy needs embedding and output on this stage"; return -2; }
+    if (n_past + 1 > m->hp.n_ctx) { g_err = "context overflow"; return -2; }
+    RT_CHECK(hipSetDevice(m->device));
+    m->pin[1] = n_past;
+    if (m->use_graphs) {
+        RC(ensure_graph(m));
+        RT_CHECK(hipGraphLaunch(m->g_exec, m->stream));
+    } else {
+        RT_CHECK(hipMemcpyAsync(m->pos_dev, &m->pin[1], 4, hipMemcpyHostToDevice, m->stream));
+        RC(decode_step_dev(m));
+    }
+    RT_CHECK(hipMemcpyAsync(&m->pin[2], m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    *token_out = m->pin[2];
     return 0;
 }

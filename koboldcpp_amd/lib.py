@@ -51,6 +51,7 @@ _SIGS = {
     "kcpp_model_sync": [P],
     "kcpp_model_forward_hidden": [P, I, I],
     "kcpp_model_argmax": [P, P],
+    "kcpp_model_decode_greedy": [P, I, P],
     "kcpp_model_set_graphs": [P, I],
     "kcpp_model_set_fused_decode": [P, I],
     "kcpp_model_weight_bytes": [P],
@@ -64,6 +65,7 @@ _L.kcpp_gemm_workspace_bytes.argtypes = [I, I64, I64, I64]
 _L.kcpp_vec_dot_type.argtypes = [I]
 _L.kcpp_gemv_dec.argtypes = [I, P, I, I, I, P]
 _L.kcpp_gemv_dec_args_size.restype = I64
+_L.kcpp_gemv_stream.argtypes = [I, P, I, I, P]
 for _n, _a in _SIGS.items():
     getattr(_L, _n).argtypes = _a
 for _n, _r in _RES.items():
@@ -71,7 +73,8 @@ for _n, _r in _RES.items():
 
 
 def exported_symbols():
-    return sorted(set(_SIGS) | set(_RES) | {"kcpp_vec_dot_type", "kcpp_gemv_dec", "kcpp_gemv_dec_args_size"})
+    return sorted(set(_SIGS) | set(_RES) | {"kcpp_vec_dot_type", "kcpp_gemv_dec", "kcpp_gemv_dec_args_size",
+                                             "kcpp_gemv_stream"})
 
 
 def raw():
@@ -167,6 +170,12 @@ class Model:
     def argmax(self):
         v = ctypes.c_int32(0)
         _chk(_L.kcpp_model_argmax(self.m, ctypes.byref(v)), "argmax")
+        return v.value
+
+    def decode_greedy(self, n_past):
+        """one greedy step on the device-resident previous argmax; returns this step's token"""
+        v = ctypes.c_int32(0)
+        _chk(_L.kcpp_model_decode_greedy(self.m, n_past, ctypes.byref(v)), "decode_greedy")
         return v.value
 
     def forward_hidden(self, T, n_past):

@@ -138,3 +138,30 @@ def test_fused_decode_matches_unfused(K, types_fn):
         outs.append(np.array(lg))
     d = np.abs(outs[0] - outs[1])
     assert d.max() < TOL_MAX and np.median(d) < 1e-5, (d.max(), np.median(d))
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_decode_greedy_matches_host_loop(K, graphs):
+    """kcpp_model_decode_greedy (token fed back on device) == decode([tok]) + argmax on the host"""
+    types = R.q4_k_m_types(R.TINY["n_layer"])
+    prompt = [(5 * i + 1) % R.TINY["n_vocab"] for i in range(21)]
+
+    def run(greedy):
+        m = K.Model(R.TINY, types)
+        m.set_graphs(graphs)
+        m.synth(1234)
+        m.decode(prompt, 0, want_logits=False)
+        tok = m.argmax()
+        toks, n = [tok], len(prompt)
+        for _ in range(12):
+            if greedy:
+                tok = m.decode_greedy(n)
+            else:
+                logits = m.decode([tok], n)
+                tok = m.argmax()
+                assert tok == int(np.argmax(logits))
+            toks.append(tok)
+            n += 1
+        m.close()
+        return toks
+    assert run(True) == run(False)

@@ -22,6 +22,40 @@ __global__ void __launch_bounds__(256) k_stream(const v4u *__restrict__ p, int64
     if (acc == 0x9e3779b9u) sink[0] = acc;
 }
 
+// Q4_K mat-vec ACCESS PATTERN only (hdr 16 B + 2 x 16 B nibbles per lane per 64-element unit, rows
+// of 2304 B, one row per wave-iteration, U rows in flight per wave), trivial compute.
+template <int U>
+__global__ void __launch_bounds__(256) k_q4k_pattern(const uint8_t *__restrict__ W, int nrows, unsigned *sink) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int nw = gridDim.x * 4;
+    const uint32_t o = (uint32_t)(lane >> 2) * 144u, j = (uint32_t)(lane & 3);
+    unsigned acc = 0;
+    for (int r0 = wave; r0 < nrows; r0 += U * nw) {
+        v4u h[U], a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = min(r0 + u * nw, nrows - 1);
+            const uint8_t *rp = W + (int64_t)r * 2304;
+            h[u] = __builtin_nontemporal_load((const v4u *)(rp + o));
+            a[u] = __builtin_nontemporal_load((const v4u *)(rp + o + 16u + 32u * j));
+            b[u] = __builtin_nontemporal_load((const v4u *)(rp + o + 32u + 32u * j));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= h[u].x ^ a[u].y ^ b[u].z ^ a[u].w ^ b[u].x;
+    }
+    if (acc == 0x9e3779b9u) sink[0] = acc;
+}
+
+extern "C" int probe_q4k(const void *W, int nrows, int blocks, int unroll, unsigned *sink, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (unroll == 1) hipLaunchKernelGGL(k_q4k_pattern<1>, dim3(blocks), dim3(256), 0, s, (const uint8_t *)W, nrows, sink);
+    else if (unroll == 2) hipLaunchKernelGGL(k_q4k_pattern<2>, dim3(blocks), dim3(256), 0, s, (const uint8_t *)W, nrows, sink);
+    else if (unroll == 4) hipLaunchKernelGGL(k_q4k_pattern<4>, dim3(blocks), dim3(256), 0, s, (const uint8_t *)W, nrows, sink);
+    else hipLaunchKernelGGL(k_q4k_pattern<8>, dim3(blocks), dim3(256), 0, s, (const uint8_t *)W, nrows, sink);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 __global__ void k_empty(unsigned *sink) {
     if (threadIdx.x == 1023) sink[0] = 1;
 }

@@ -23,6 +23,7 @@ def lib():
     P, I, I64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64
     L.probe_stream.argtypes = [P, I64, I, I, I, P, P]
     L.probe_empty.argtypes = [I, P, P]
+    L.probe_q4k.argtypes = [P, I, I, I, P, P]
     return L
 
 
@@ -73,6 +74,20 @@ def stream(L):
         print(json.dumps(dict(best, probe="stream-best")))
 
 
+def q4k_pattern(L):
+    pool = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    sink = torch.zeros(4, dtype=torch.int32, device="cuda")
+    for nrows in (4096, 14336, 28672):
+        size = nrows * 2304
+        nslot = (1 << 30) // size
+        for blocks in (256, 512, 1024, 2048):
+            for unroll in (1, 2, 4, 8):
+                us = timed(lambda i, sp: L.probe_q4k(pool.data_ptr() + (i % nslot) * size, nrows, blocks, unroll,
+                                                     sink.data_ptr(), sp), 40)
+                print(json.dumps({"probe": "q4k-pattern", "rows": nrows, "bytes": size, "blocks": blocks,
+                                  "unroll": unroll, "us": round(us, 2), "GBps": round(size / us / 1e3, 1)}))
+
+
 def dec():
     import koboldcpp_amd.lib as K
     sp = torch.cuda.current_stream().cuda_stream
@@ -86,6 +101,11 @@ def dec():
         ("down q4k pro0", 12, F, E, 0, 0, 1),
         ("down q6k pro0", 14, F, E, 0, 0, 1),
         ("head q6k pro1", 14, E, 128256, 0, 1, 4),
+        ("glu q4k pro1 r2", 12, E, F, 1, 1, 2),
+        ("glu q4k pro0", 12, E, F, 1, 0, 1),
+        ("wo q4k pro0 r2", 12, E, E, 0, 0, 2),
+        ("wo q4k pro0 r4", 12, E, E, 0, 0, 4),
+        ("down q4k pro0 r2", 12, F, E, 0, 0, 2),
     ]
     x = torch.randn(F, device="cuda")
     nw = torch.ones(F, device="cuda")
@@ -95,7 +115,10 @@ def dec():
     vc = torch.zeros(4096 * 1024, dtype=torch.int16, device="cuda")
     pos = torch.tensor([100], dtype=torch.int32, device="cuda")
     tab = torch.zeros(4096 * 64 * 2, device="cuda")
+    only = os.environ.get("PROBE_CASE")
     for name, t, Kd, N, mode, pro, rpw in cases:
+        if only and name != only:
+            continue
         rb = K.row_bytes(t, Kd)
         wb = rb * N
         nmat = 2 if mode == 1 else 1
@@ -126,7 +149,9 @@ def dec():
                     d.W2 = mats[1].data_ptr()
             args.append(d)
         rc = K.gemv_dec(t, args[0], mode, pro, rpw, sp)
-        assert rc == 0, (name, rc)
+        if rc != 0:
+            print(json.dumps({"probe": "dec", "case": name, "rc": rc}))
+            continue
         us = timed(lambda i, sp: K.gemv_dec(t, args[i % len(args)], mode, pro, rpw, sp), 40)
         print(json.dumps({"probe": "dec", "case": name, "bytes": wb * nmat, "us": round(us, 2),
                           "GBps": round(wb * nmat / us / 1e3, 1), "blocks_env": os.environ.get("KCPP_DEC_BLOCKS")}))
@@ -138,5 +163,7 @@ if __name__ == "__main__":
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what in ("stream", "all"):
         stream(lib())
+    if what in ("pattern", "all"):
+        q4k_pattern(lib())
     if what in ("dec", "all"):
         dec()
