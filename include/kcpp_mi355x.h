@@ -63,6 +63,9 @@ int64_t kcpp_gemv_dec_args_size(void);
 /* the coalesced-streaming Q4_K variant kcpp_gemv_dec dispatches to (koboldcpp_amd/csrc/gemv_stream.hip);
  * returns -3 when the type/shape/mode is not covered.  Exposed for the parity tests and tools. */
 int kcpp_gemv_stream(int type, const void *args, int mode, int pro, void *stream);
+/* the VALU-lean unit-per-lane Q4_K variant (koboldcpp_amd/csrc/gemv_q4k.hip), tried first for Q4_K;
+ * -3 when not covered */
+int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream);
 
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,

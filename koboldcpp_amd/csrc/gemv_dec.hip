@@ -10,6 +10,11 @@ extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int 
     const DecArgs &a = *(const DecArgs *)args;
     hipStream_t s = (hipStream_t)stream;
     // coalesced-streaming kernel where it covers the type/shape (gemv_stream.hip), else unit-per-lane
+    static const int use_q4k = getenv("KCPP_Q4K") ? atoi(getenv("KCPP_Q4K")) : 1;
+    if (use_q4k && type == KT_Q4_K) {
+        const int rc = kcpp_gemv_q4k(args, mode, pro, stream);
+        if (rc != -3) return rc;
+    }
     static const int use_stream = getenv("KCPP_STREAM") ? atoi(getenv("KCPP_STREAM")) : 1;
     if (use_stream) {
         const int rc = kcpp_gemv_stream(type, args, mode, pro, stream);

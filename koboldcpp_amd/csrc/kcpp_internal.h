@@ -36,4 +36,6 @@ struct DecArgs {
 extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream);
 // coalesced Q4_K variant (gemv_stream.hip); -3 = not covered
 extern "C" int kcpp_gemv_stream(int type, const void *args, int mode, int pro, void *stream);
+// VALU-lean unit-per-lane Q4_K variant (gemv_q4k.hip); -3 = not covered
+extern "C" int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream);
 

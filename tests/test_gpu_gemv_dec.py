@@ -69,7 +69,7 @@ CASES = [  # name, type, K, N, mode, pro
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-@pytest.mark.parametrize("entry", ["dec", "stream"])
+@pytest.mark.parametrize("entry", ["dec", "stream", "q4k"])
 def test_gemv_dec_vs_unfused(env, case, entry):
     torch, K = env
     name, t, Kd, N, mode, pro = case
@@ -93,6 +93,12 @@ def test_gemv_dec_vs_unfused(env, case, entry):
         rc = int(K.raw().kcpp_gemv_stream(t, __import__("ctypes").byref(a), mode, pro, s))
         if rc == -3:
             pytest.skip("shape/type not covered by the streaming kernel")
+    elif entry == "q4k":
+        if t != R.Q4_K:
+            pytest.skip("Q4_K kernel")
+        rc = int(K.raw().kcpp_gemv_q4k(__import__("ctypes").byref(a), mode, pro, s))
+        if rc == -3:
+            pytest.skip("shape not covered by the Q4_K kernel")
     else:
         rc = K.gemv_dec(t, a, mode, pro, 1, s)
     assert rc == 0
@@ -100,7 +106,7 @@ def test_gemv_dec_vs_unfused(env, case, entry):
     _close(y.cpu().numpy(), yref.cpu().numpy())
 
 
-@pytest.mark.parametrize("entry", ["dec", "stream"])
+@pytest.mark.parametrize("entry", ["dec", "stream", "q4k"])
 @pytest.mark.parametrize("pos", [0, 77, 4000])
 def test_gemv_dec_qkv_rope_kv(env, entry, pos):
     """mode 2: q|k|v mat-vec + RoPE + f16 stores, vs kcpp_gemv + kcpp_rope_kv"""
@@ -134,6 +140,10 @@ def test_gemv_dec_qkv_rope_kv(env, entry, pos):
               ekv=EKV, D=D, pos=posd.data_ptr(), rope_tab=tab_d.data_ptr())
     if entry == "stream":
         rc = int(K.raw().kcpp_gemv_stream(t, ctypes.byref(a), 2, 1, s))
+        if rc == -3:
+            pytest.skip("shape/type not covered by the streaming kernel")
+    elif entry == "q4k":
+        rc = int(K.raw().kcpp_gemv_q4k(ctypes.byref(a), 2, 1, s))
     else:
         rc = K.gemv_dec(t, a, 2, 1, 2, s)
     assert rc == 0
