@@ -77,10 +77,14 @@ int kcpp_rope_table(float *tab_host, int n_pos, int n_dims, float freq_base, flo
 int kcpp_rope_kv(const float *qkv, int64_t ldqkv, float *q_out, uint16_t *q16, uint16_t *kc, uint16_t *vc, int T,
                  int H, int HKV, int D, int n_past, const int32_t *pos_dev, const void *rope_tab, void *stream);
 /* flash attention over the f16 cache (ggml_cuda_flash_attn_ext, fattn.cu:298-345) */
+/* force_path: 0 auto, 1 split-KV decode, 2 FMA-tiled prefill, 3 MFMA prefill (D = 128, H = 4 HKV) */
 int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max);
 int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qout, void *ws,
                     int T, int H, int HKV, int D, int n_past, const int32_t *n_past_dev, int n_kv_max, float scale,
                     int force_path, void *stream);
+/* the MFMA prefill kernel alone (koboldcpp_amd/csrc/attn_mfma.hip); -3 when the shape is not covered */
+int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, int T, int H,
+                                 int HKV, int D, int n_past, float scale, void *stream);
 int kcpp_add(float *y, const float *a, const float *b, int64_t n, void *stream);
 int kcpp_silu_mul(float *y, const float *g, const float *u, int64_t n, void *stream);
 

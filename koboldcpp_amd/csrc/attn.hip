@@ -457,8 +457,17 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
         return 0;
     }
     if (!out) return -2;
-    hipLaunchKernelGGL(k_fa_prefill<128>, dim3((T + FP_BQ - 1) / FP_BQ, H), dim3(256), 0, s, q16, kc, vc, out, T, H, HKV,
-                       n_past, scale);
+    // prefill: MFMA kernel (attn_mfma.hip) for GQA groups of 4 (force_path 3, or auto), else FMA tiles (2)
+    static const int mfma_env = getenv("KCPP_FA_MFMA") ? atoi(getenv("KCPP_FA_MFMA")) : 1;
+    int rc = -3;
+    if (force_path == 3 || (force_path == 0 && mfma_env))
+        rc = kcpp_flash_attn_prefill_mfma(q16, kc, vc, out, T, H, HKV, D, n_past, scale, stream);
+    if (rc == -3 && force_path == 3) return -3;
+    if (rc == -3)
+        hipLaunchKernelGGL(k_fa_prefill<128>, dim3((T + FP_BQ - 1) / FP_BQ, H), dim3(256), 0, s, q16, kc, vc, out, T, H, HKV,
+                           n_past, scale);
+    else if (rc)
+        return rc;
     KCPP_CHECK(hipGetLastError());
     if (qout) return kcpp_quantize_act(KT_Q8_K, out, (int64_t)H * D, qout, (int64_t)H * D, T, stream);
     return 0;

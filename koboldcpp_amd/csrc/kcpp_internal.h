@@ -39,3 +39,7 @@ extern "C" int kcpp_gemv_stream(int type, const void *args, int mode, int pro, v
 // VALU-lean unit-per-lane Q4_K variant (gemv_q4k.hip); -3 = not covered
 extern "C" int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream);
 
+
+// MFMA prefill flash attention (attn_mfma.hip); -3 = shape not covered (needs D = 128, H = 4 * HKV)
+extern "C" int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out,
+                                            int T, int H, int HKV, int D, int n_past, float scale, void *stream);

@@ -37,6 +37,7 @@ _SIGS = {
     "kcpp_rope_table": [P, I, I, Fl, Fl, P, Fl, Fl, Fl, Fl, I],
     "kcpp_rope_kv": [P, I64, P, P, P, P, I, I, I, I, I, P, P, P],
     "kcpp_flash_attn": [P, P, P, P, P, P, I, I, I, I, I, P, I, Fl, I, P],
+    "kcpp_flash_attn_prefill_mfma": [P, P, P, P, I, I, I, I, I, Fl, P],
     "kcpp_add": [P, P, P, I64, P],
     "kcpp_silu_mul": [P, P, P, I64, P],
     "kcpp_model_create": [P, P, I, I, I, I, I, I],

@@ -231,7 +231,8 @@ def test_rope_kv(env, golden_ops):
 
 
 @pytest.mark.parametrize("T,n_past,path", [(1, 0, 1), (1, 255, 1), (1, 1000, 1), (3, 700, 1), (5, 295, 1),
-                                           (40, 0, 2), (70, 130, 2), (16, 300, 2)])
+                                           (40, 0, 2), (70, 130, 2), (16, 300, 2),
+                                           (40, 0, 3), (70, 130, 3), (16, 300, 3), (200, 700, 3), (1, 5, 3)])
 def test_flash_attn_vs_oracle(env, T, n_past, path):
     torch, K = env
     H, HKV, D = 32, 8, 128
@@ -272,9 +273,11 @@ def test_flash_attn_golden(env, golden_ops, key):
 
 
 @pytest.mark.parametrize("T,n_past,path", [(1, 0, 1), (1, 1000, 1), (5, 295, 1), (16, 300, 1), (16, 300, 2),
-                                           (17, 0, 2), (37, 0, 2), (40, 0, 2), (70, 130, 2), (200, 60, 2)])
+                                           (17, 0, 2), (37, 0, 2), (40, 0, 2), (70, 130, 2), (200, 60, 2),
+                                           (17, 0, 3), (37, 0, 3), (70, 130, 3), (200, 60, 3), (512, 300, 3)])
 def test_flash_attn_vs_oracle_f32_accum(env, T, n_past, path):
-    """Same math as the HIP kernels (f32 V accumulation): must agree to fp32 rounding."""
+    """Same math as the HIP kernels (f32 V accumulation): must agree to fp32 rounding.  Path 3 (MFMA
+    prefill) rounds the probabilities to f16 for the P.V product: a 2^-11 relative error per weight."""
     torch, K = env
     H, HKV, D = 32, 8, 128
     n_ctx = 1024
@@ -298,7 +301,10 @@ def test_flash_attn_vs_oracle_f32_accum(env, T, n_past, path):
     K.call("kcpp_flash_attn", q16.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), None, ws.data_ptr(), T, H,
            HKV, D, n_past, None, n_ctx, 1.0 / np.sqrt(D), path, sptr(torch))
     got = host(torch, out, np.float32).reshape(T, H, D)
-    np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
+    if path == 3:
+        np.testing.assert_allclose(got, want, rtol=2e-3, atol=2e-3)
+    else:
+        np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
 
 
 @pytest.mark.parametrize("t", TYPES)
