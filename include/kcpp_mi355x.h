@@ -121,6 +121,8 @@ void *kcpp_model_stream(kcpp_model *m);
  * memory): dir 0 = buf -> stage input, 1 = stage output -> buf.  Pipeline handoff (replaces
  * ggml_backend_cuda_cpy_tensor_async, ggml/src/ggml-cuda.cu:2392-2445). */
 int kcpp_model_hidden_io(kcpp_model *m, void *buf, int64_t n_floats, int64_t offset, int dir);
+/* copy the last decode's logits [n_vocab] f32 to host memory (stage with the output head) */
+int kcpp_model_read_logits(kcpp_model *m, float *host);
 /* wait for all work queued on the stage's stream */
 int kcpp_model_sync(kcpp_model *m);
 /* per-stage step without embedding/out: run layers on the hidden buffer for T tokens */

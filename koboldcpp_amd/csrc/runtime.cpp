@@ -286,6 +286,14 @@ extern "C" int kcpp_model_sync(kcpp_model *m) {
     return 0;
 }
 extern "C" void *kcpp_model_stream(kcpp_model *m) { return m->stream; }
+extern "C" int kcpp_model_read_logits(kcpp_model *m, float *host) {
+    if (!m->has_output) { g_err = "read_logits: stage has no output head"; return -2; }
+    RT_CHECK(hipSetDevice(m->device));
+    RT_CHECK(hipMemcpyAsync(m->logits_pin, m->logits, (size_t)m->hp.n_vocab * 4, hipMemcpyDeviceToHost, m->stream));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    memcpy(host, m->logits_pin, (size_t)m->hp.n_vocab * 4);
+    return 0;
+}
 extern "C" int64_t kcpp_model_weight_bytes(kcpp_model *m) { return m->weight_bytes; }
 extern "C" int kcpp_model_set_graphs(kcpp_model *m, int enable) {
     m->use_graphs = enable != 0;

@@ -50,6 +50,7 @@ _SIGS = {
     "kcpp_model_stream": [P],
     "kcpp_model_hidden_io": [P, P, I64, I64, I],
     "kcpp_model_sync": [P],
+    "kcpp_model_read_logits": [P, P],
     "kcpp_model_forward_hidden": [P, I, I],
     "kcpp_model_argmax": [P, P],
     "kcpp_model_decode_greedy": [P, I, P],
