@@ -12,7 +12,9 @@ import refharness as R
 
 pytestmark = pytest.mark.gpu
 
-WORDS = ["▁hello", "▁world", "▁the", "he", "llo", "▁a", "▁b", "ab", "▁of", "▁to"]
+# SentencePiece merges only through pieces that exist: give every word its whole prefix chain
+WORDS = ["▁h", "▁he", "▁hel", "▁hell", "▁hello", "▁w", "▁wo", "▁wor", "▁worl", "▁world", "▁t", "▁th", "▁the",
+         "a", "b", "ab", "▁a", "▁b", "▁of", "▁to"]
 
 
 def piece(toks, types, t):
@@ -50,9 +52,9 @@ def test_token_count_spm(model):
     r = h.token_count(b"hello world the", True)
     ids = [r.ids[i] for i in range(r.count)]
     assert ids == [1, toks.index("▁hello"), toks.index("▁world"), toks.index("▁the")]
-    r = h.token_count(b"hellab", False)        # "▁hello" wins over "he"+"llo"; "ab" merges
+    r = h.token_count(b"hellab", False)        # merges stop at "▁hell" ("▁hella" is no piece)
     ids = [r.ids[i] for i in range(r.count)]
-    assert ids == [toks.index("▁hello"), toks.index("ab")]
+    assert ids == [toks.index("▁hell"), toks.index("ab")]
     r = h.token_count("zé".encode(), False)  # no pieces: byte fallback for every byte
     ids = [r.ids[i] for i in range(r.count)]
     assert [toks[i] for i in ids] == ["<0xE2>", "<0x96>", "<0x81>", "<0x7A>", "<0xC3>", "<0xA9>"]
