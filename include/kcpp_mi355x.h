@@ -66,6 +66,8 @@ int kcpp_gemv_stream(int type, const void *args, int mode, int pro, void *stream
 /* the VALU-lean unit-per-lane Q4_K variant (koboldcpp_amd/csrc/gemv_q4k.hip), tried first for Q4_K;
  * -3 when not covered */
 int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream);
+/* the VALU-lean Q6_K variant (koboldcpp_amd/csrc/gemv_q6k.hip), tried first for Q6_K; -3 when not covered */
+int kcpp_gemv_q6k(const void *args, int mode, int pro, void *stream);
 
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,

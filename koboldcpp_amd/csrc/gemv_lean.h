@@ -1,0 +1,125 @@
+// gemv_lean.h -- shared parts of the VALU-lean decode mat-vec kernels (gemv_q4k.hip, gemv_q6k.hip):
+// the activation prologue (rms_norm * w -> Q8_K in LDS, or an already-quantized activation copied to
+// LDS) with its global loads issued before the first weight loads, and the epilogue that stores the
+// per-lane parked results (residual add / SiLU-GLU / RoPE + f16 K/V cache stores).
+#pragma once
+#include "gemv_units.h"
+#include "kcpp_internal.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace lean {
+
+template <int PRO, int MAXC>
+struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_impl.h); loads first
+    float v[MAXC][16];
+    float w[PRO == 1 ? MAXC : 1][16];
+    __device__ __forceinline__ void load(const DecArgs &a) {
+        const int tid = threadIdx.x, nchunk = (int)(a.K / 16);
+#pragma unroll
+        for (int i = 0; i < MAXC; ++i) {
+            const int c = min(tid + 256 * i, nchunk - 1);
+            const float4 *p = (const float4 *)(a.x + 16 * (int64_t)c);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 f = p[k];
+                v[i][4 * k] = f.x; v[i][4 * k + 1] = f.y; v[i][4 * k + 2] = f.z; v[i][4 * k + 3] = f.w;
+            }
+            if constexpr (PRO == 1) {
+                const float4 *q = (const float4 *)(a.nw + 16 * (int64_t)c);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float4 f = q[k];
+                    w[i][4 * k] = f.x; w[i][4 * k + 1] = f.y; w[i][4 * k + 2] = f.z; w[i][4 * k + 3] = f.w;
+                }
+            }
+        }
+    }
+    __device__ __forceinline__ void compute(const DecArgs &a, uint8_t *lds) {
+        const int tid = threadIdx.x;
+        const int64_t K = a.K;
+        const int nchunk = (int)(K / 16);
+        if constexpr (PRO == 1) {
+            double ss = 0.0;
+#pragma unroll
+            for (int i = 0; i < MAXC; ++i)
+                if (tid + 256 * i < nchunk) {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) ss += (double)__fmul_rn(v[i][e], v[i][e]);
+                }
+            ss = wave_sum_d(ss);
+            __shared__ double red[4];
+            if ((tid & 63) == 0) red[tid >> 6] = ss;
+            __syncthreads();
+            const double sum = red[0] + red[1] + red[2] + red[3];
+            const float scale = 1.0f / sqrtf((float)(sum / (double)K) + a.eps);   // ggml.c:12089
+#pragma unroll
+            for (int i = 0; i < MAXC; ++i)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) v[i][e] = __fmul_rn(__fmul_rn(v[i][e], scale), w[i][e]);
+        }
+        int8_t *qs = (int8_t *)lds;
+        float *d = (float *)(lds + K);
+        int16_t *bs = (int16_t *)(lds + K + K / 256 * 4);
+#pragma unroll
+        for (int i = 0; i < MAXC; ++i) {
+            const int c = tid + 256 * i;
+            if (c < nchunk) q8k_quant16(v[i], c & 15, qs + (c >> 4) * 256, d + (c >> 4), bs + (c >> 4) * 16);
+        }
+        __syncthreads();
+    }
+};
+
+
+// quantized activation (M = 1, <= 20 KB, multiple of 16 B) -> LDS through registers
+struct ActCopy {
+    uint4 r[5];
+    __device__ __forceinline__ void load(const uint8_t *act, int abytes) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const int o = min(((int)threadIdx.x + 256 * i) * 16, abytes - 16);
+            r[i] = *(const uint4 *)(act + o);
+        }
+    }
+    __device__ __forceinline__ void store(uint8_t *lds, int abytes) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            const int o = ((int)threadIdx.x + 256 * i) * 16;
+            if (o < abytes) *(uint4 *)(lds + o) = r[i];
+        }
+        __syncthreads();
+    }
+};
+
+// store R parked results of group slot_g (rows row0.. of segment seg)
+template <int R, int MODE>
+__device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0, const float (&slot)[R]) {
+    if constexpr (MODE != 2) {
+        float *Y = seg == 0 ? a.Y[0] : (seg == 1 ? a.Y[1] : a.Y[2]);
+#pragma unroll
+        for (int r = 0; r < R; ++r) Y[row0 + r] = (MODE == 0 && a.res) ? __fadd_rn(slot[r], a.res[row0 + r]) : slot[r];
+    } else {
+        const int role = seg == 0 ? a.role[0] : (seg == 1 ? a.role[1] : a.role[2]);
+        const int p = a.pos[0];
+        if (role == 2) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) a.vc[(int64_t)p * a.ekv + row0 + r] = f2h(slot[r]);
+        } else {
+            const int hd = a.D / 2;
+#pragma unroll
+            for (int r = 0; r < R; r += 2) {          // rows (2i, 2i+1): a RoPE pair (NORM mode)
+                const int row = row0 + r;
+                const float2 cs = a.rope_tab[(int64_t)p * hd + (row % a.D) / 2];
+                const float x0 = slot[r], x1 = slot[r + 1];
+                const float o0 = __fsub_rn(__fmul_rn(x0, cs.x), __fmul_rn(x1, cs.y));
+                const float o1 = __fadd_rn(__fmul_rn(x0, cs.y), __fmul_rn(x1, cs.x));
+                const uint32_t pk = (uint32_t)f2h(o0) | ((uint32_t)f2h(o1) << 16);
+                if (role == 0) *(uint32_t *)(a.q16 + row) = pk;
+                else *(uint32_t *)(a.kc + (int64_t)p * a.ekv + row) = pk;
+            }
+        }
+    }
+}
+
+}  // namespace lean

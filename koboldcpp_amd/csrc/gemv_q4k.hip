@@ -16,8 +16,7 @@
 //     after the loop (no stores in flight while weights stream).
 // The float accumulation order differs from the CPU (per 64-element unit instead of per
 // super-block); parity is the same tolerance class as every GPU mat-vec here.
-#include "gemv_units.h"
-#include "kcpp_internal.h"
+#include "gemv_lean.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -82,69 +81,11 @@ __device__ __forceinline__ float q4k_unit(const uint4 &hdr, const uint4 &q0, con
     return x.d * fmaf(dw, (float)sumi, -dmw * (float)summ);
 }
 
-template <int PRO, int MAXC>
-struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_impl.h); loads first
-    float v[MAXC][16];
-    float w[PRO == 1 ? MAXC : 1][16];
-    __device__ __forceinline__ void load(const DecArgs &a) {
-        const int tid = threadIdx.x, nchunk = (int)(a.K / 16);
-#pragma unroll
-        for (int i = 0; i < MAXC; ++i) {
-            const int c = min(tid + 256 * i, nchunk - 1);
-            const float4 *p = (const float4 *)(a.x + 16 * (int64_t)c);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float4 f = p[k];
-                v[i][4 * k] = f.x; v[i][4 * k + 1] = f.y; v[i][4 * k + 2] = f.z; v[i][4 * k + 3] = f.w;
-            }
-            if constexpr (PRO == 1) {
-                const float4 *q = (const float4 *)(a.nw + 16 * (int64_t)c);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    const float4 f = q[k];
-                    w[i][4 * k] = f.x; w[i][4 * k + 1] = f.y; w[i][4 * k + 2] = f.z; w[i][4 * k + 3] = f.w;
-                }
-            }
-        }
-    }
-    __device__ __forceinline__ void compute(const DecArgs &a, uint8_t *lds) {
-        const int tid = threadIdx.x;
-        const int64_t K = a.K;
-        const int nchunk = (int)(K / 16);
-        if constexpr (PRO == 1) {
-            double ss = 0.0;
-#pragma unroll
-            for (int i = 0; i < MAXC; ++i)
-                if (tid + 256 * i < nchunk) {
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) ss += (double)__fmul_rn(v[i][e], v[i][e]);
-                }
-            ss = wave_sum_d(ss);
-            __shared__ double red[4];
-            if ((tid & 63) == 0) red[tid >> 6] = ss;
-            __syncthreads();
-            const double sum = red[0] + red[1] + red[2] + red[3];
-            const float scale = 1.0f / sqrtf((float)(sum / (double)K) + a.eps);   // ggml.c:12089
-#pragma unroll
-            for (int i = 0; i < MAXC; ++i)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) v[i][e] = __fmul_rn(__fmul_rn(v[i][e], scale), w[i][e]);
-        }
-        int8_t *qs = (int8_t *)lds;
-        float *d = (float *)(lds + K);
-        int16_t *bs = (int16_t *)(lds + K + K / 256 * 4);
-#pragma unroll
-        for (int i = 0; i < MAXC; ++i) {
-            const int c = tid + 256 * i;
-            if (c < nchunk) q8k_quant16(v[i], c & 15, qs + (c >> 4) * 256, d + (c >> 4), bs + (c >> 4) * 16);
-        }
-        __syncthreads();
-    }
-};
-
 }  // namespace
 
-template <int IT, int R, int MODE, int PRO, int MC>
+// PF: prefetch the next group's weights while computing this one (two register buffers); only worth
+// its registers when a wave streams several groups (gate|up, output head), not at one group per wave.
+template <int IT, int R, int MODE, int PRO, int MC, int PF>
 __global__ void __launch_bounds__(256) k_gemv_q4k(const DecArgs a) {
     constexpr int RR = MODE == 1 ? 2 * R : R;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -190,24 +131,15 @@ __global__ void __launch_bounds__(256) k_gemv_q4k(const DecArgs a) {
     Buf ba, bb;
     const int g0 = min(wid, ngroups - 1);
     if constexpr (PRO != 0) {
-        ActPro<PRO, MC> pro;
+        lean::ActPro<PRO, MC> pro;
         pro.load(a);
         issue(g0, ba);
         pro.compute(a, lds);
     } else {
-        uint4 r[5];
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const int o = min(((int)threadIdx.x + 256 * i) * 16, abytes - 16);
-            r[i] = *(const uint4 *)(a.act + o);
-        }
+        lean::ActCopy cp;
+        cp.load(a.act, abytes);
         issue(g0, ba);
-#pragma unroll
-        for (int i = 0; i < 5; ++i) {
-            const int o = ((int)threadIdx.x + 256 * i) * 16;
-            if (o < abytes) *(uint4 *)(lds + o) = r[i];
-        }
-        __syncthreads();
+        cp.store(lds, abytes);
     }
     // K = 4096: the activation unit of this lane is constant for the launch
     ActU xr;
@@ -246,47 +178,30 @@ __global__ void __launch_bounds__(256) k_gemv_q4k(const DecArgs a) {
         slot_g = mine ? g : slot_g;
     };
     int k = 0;
-    for (int g = wid; g < ngroups; g += 2 * nw, k += 2) {
-        const int g1 = g + nw, g2 = g + 2 * nw;
-        issue(min(g1, ngroups - 1), bb);
-        compute(g, ba, k);
-        if (g1 >= ngroups) break;
-        issue(min(g2, ngroups - 1), ba);
-        compute(g1, bb, k + 1);
+    if constexpr (PF) {
+        for (int g = wid; g < ngroups; g += 2 * nw, k += 2) {
+            const int g1 = g + nw, g2 = g + 2 * nw;
+            issue(min(g1, ngroups - 1), bb);
+            compute(g, ba, k);
+            if (g1 >= ngroups) break;
+            issue(min(g2, ngroups - 1), ba);
+            compute(g1, bb, k + 1);
+        }
+    } else {
+        for (int g = wid; g < ngroups; g += nw, ++k) {
+            if (k) issue(g, ba);
+            compute(g, ba, k);
+        }
     }
     // epilogue stores (one group per lane)
     if (slot_g < 0) return;
     int seg, row0;
     group_rows(slot_g, seg, row0);
-    if constexpr (MODE != 2) {
-        float *Y = seg == 0 ? a.Y[0] : (seg == 1 ? a.Y[1] : a.Y[2]);
-#pragma unroll
-        for (int r = 0; r < R; ++r) Y[row0 + r] = (MODE == 0 && a.res) ? __fadd_rn(slot[r], a.res[row0 + r]) : slot[r];
-    } else {
-        const int role = seg == 0 ? a.role[0] : (seg == 1 ? a.role[1] : a.role[2]);
-        const int p = a.pos[0];
-        if (role == 2) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) a.vc[(int64_t)p * a.ekv + row0 + r] = f2h(slot[r]);
-        } else {
-            const int hd = a.D / 2;
-#pragma unroll
-            for (int r = 0; r < R; r += 2) {          // rows (2i, 2i+1): a RoPE pair (NORM mode)
-                const int row = row0 + r;
-                const float2 cs = a.rope_tab[(int64_t)p * hd + (row % a.D) / 2];
-                const float x0 = slot[r], x1 = slot[r + 1];
-                const float o0 = __fsub_rn(__fmul_rn(x0, cs.x), __fmul_rn(x1, cs.y));
-                const float o1 = __fadd_rn(__fmul_rn(x0, cs.y), __fmul_rn(x1, cs.x));
-                const uint32_t pk = (uint32_t)f2h(o0) | ((uint32_t)f2h(o1) << 16);
-                if (role == 0) *(uint32_t *)(a.q16 + row) = pk;
-                else *(uint32_t *)(a.kc + (int64_t)p * a.ekv + row) = pk;
-            }
-        }
-    }
+    lean::store_group<R, MODE>(a, seg, row0, slot);
 }
 
 namespace {
-template <int IT, int R, int MODE, int PRO, int MC>
+template <int IT, int R, int MODE, int PRO, int MC, int PF>
 int launch_q4k(const DecArgs &a, hipStream_t s) {
     int64_t ntot = 0;
     for (int i = 0; i < a.nseg; ++i) {
@@ -298,7 +213,7 @@ int launch_q4k(const DecArgs &a, hipStream_t s) {
     int64_t nblk = std::min<int64_t>((groups + 3) / 4, max_blocks);
     nblk = std::max<int64_t>(nblk, (groups + 255) / 256);    // <= 64 groups per wave (result slots)
     const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
-    hipLaunchKernelGGL((k_gemv_q4k<IT, R, MODE, PRO, MC>), dim3((unsigned)nblk), dim3(256), (size_t)abytes + 16, s, a);
+    hipLaunchKernelGGL((k_gemv_q4k<IT, R, MODE, PRO, MC, PF>), dim3((unsigned)nblk), dim3(256), (size_t)abytes + 16, s, a);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }
@@ -313,12 +228,12 @@ extern "C" int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream) 
     // gate|up (mode 1) stays on gemv_dec_impl.h by default: measured 21.3 vs 22.7 us there
     static const int glu = getenv("KCPP_Q4K_GLU") ? atoi(getenv("KCPP_Q4K_GLU")) : 0;
     if (a.K == 4096) {
-        if (mode == 1 && pro == 1 && glu) return r_env == 2 ? launch_q4k<1, 2, 1, 1, 1>(a, s) : launch_q4k<1, 1, 1, 1, 1>(a, s);
-        if (mode == 2 && pro == 1) return launch_q4k<1, 2, 2, 1, 1>(a, s);
-        if (mode == 0 && pro == 0) return r_env == 2 ? launch_q4k<1, 2, 0, 0, 1>(a, s) : launch_q4k<1, 1, 0, 0, 1>(a, s);
-        if (mode == 0 && pro == 1) return launch_q4k<1, 2, 0, 1, 1>(a, s);
+        if (mode == 1 && pro == 1 && glu) return r_env == 2 ? launch_q4k<1, 2, 1, 1, 1, 1>(a, s) : launch_q4k<1, 1, 1, 1, 1, 1>(a, s);
+        if (mode == 2 && pro == 1) return launch_q4k<1, 2, 2, 1, 1, 0>(a, s);
+        if (mode == 0 && pro == 0) return r_env == 2 ? launch_q4k<1, 2, 0, 0, 1, 0>(a, s) : launch_q4k<1, 1, 0, 0, 1, 0>(a, s);
+        if (mode == 0 && pro == 1) return launch_q4k<1, 2, 0, 1, 1, 1>(a, s);
         return -3;
     }
-    if (a.K == 14336 && mode == 0 && pro == 2) return launch_q4k<4, 1, 0, 2, 4>(a, s);
+    if (a.K == 14336 && mode == 0 && pro == 2) return launch_q4k<4, 1, 0, 2, 4, 0>(a, s);
     return -3;
 }

@@ -69,6 +69,7 @@ _L.kcpp_gemv_dec.argtypes = [I, P, I, I, I, P]
 _L.kcpp_gemv_dec_args_size.restype = I64
 _L.kcpp_gemv_stream.argtypes = [I, P, I, I, P]
 _L.kcpp_gemv_q4k.argtypes = [P, I, I, P]
+_L.kcpp_gemv_q6k.argtypes = [P, I, I, P]
 for _n, _a in _SIGS.items():
     getattr(_L, _n).argtypes = _a
 for _n, _r in _RES.items():
@@ -77,7 +78,7 @@ for _n, _r in _RES.items():
 
 def exported_symbols():
     return sorted(set(_SIGS) | set(_RES) | {"kcpp_vec_dot_type", "kcpp_gemv_dec", "kcpp_gemv_dec_args_size",
-                                             "kcpp_gemv_stream", "kcpp_gemv_q4k"})
+                                             "kcpp_gemv_stream", "kcpp_gemv_q4k", "kcpp_gemv_q6k"})
 
 
 def raw():

@@ -65,11 +65,13 @@ CASES = [  # name, type, K, N, mode, pro
     ("head_q4k", R.Q4_K, 4096, 8192, 0, 1),
     ("head_q6k", R.Q6_K, 4096, 8192, 0, 1),
     ("glu_q80", R.Q8_0, 4096, 2048, 1, 1),
+    ("glu_q6k", R.Q6_K, 4096, 2048, 1, 1),
+    ("head_q6k_big", R.Q6_K, 4096, 128256, 0, 1),
 ]
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-@pytest.mark.parametrize("entry", ["dec", "stream", "q4k"])
+@pytest.mark.parametrize("entry", ["dec", "stream", "q4k", "q6k"])
 def test_gemv_dec_vs_unfused(env, case, entry):
     torch, K = env
     name, t, Kd, N, mode, pro = case
@@ -93,12 +95,13 @@ def test_gemv_dec_vs_unfused(env, case, entry):
         rc = int(K.raw().kcpp_gemv_stream(t, __import__("ctypes").byref(a), mode, pro, s))
         if rc == -3:
             pytest.skip("shape/type not covered by the streaming kernel")
-    elif entry == "q4k":
-        if t != R.Q4_K:
-            pytest.skip("Q4_K kernel")
-        rc = int(K.raw().kcpp_gemv_q4k(__import__("ctypes").byref(a), mode, pro, s))
+    elif entry in ("q4k", "q6k"):
+        if t != (R.Q4_K if entry == "q4k" else R.Q6_K):
+            pytest.skip("type-specific kernel")
+        fn = K.raw().kcpp_gemv_q4k if entry == "q4k" else K.raw().kcpp_gemv_q6k
+        rc = int(fn(__import__("ctypes").byref(a), mode, pro, s))
         if rc == -3:
-            pytest.skip("shape not covered by the Q4_K kernel")
+            pytest.skip("shape not covered")
     else:
         rc = K.gemv_dec(t, a, mode, pro, 1, s)
     assert rc == 0
