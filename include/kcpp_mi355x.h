@@ -43,6 +43,8 @@ int kcpp_get_rows(int type, const void *w, int64_t K, int64_t N, const int32_t *
 int64_t kcpp_act_bytes(int wtype, int64_t K, int64_t M);
 int kcpp_vec_dot_type(int wtype);
 int kcpp_quantize_act(int vtype, const float *x, int64_t ldx, void *out, int64_t K, int64_t M, void *stream);
+/* Q8_K of silu(g) * u with g = x[m][i], u = x[m][uoff + i] (fused gate|up GEMM output; = k_silu_mul + quantize) */
+int kcpp_quantize_act_glu(const float *x, int64_t ldx, int64_t uoff, void *out, int64_t K, int64_t M, void *stream);
 
 /* Quantized mat-vec for M <= 8 columns (replaces mul_mat_vec_q, mmvq.cu:50-202):
  *   mode 0: Y[c][n] = W[n].x[c] (+ res[c][n])     mode 1: Y[c][n] = silu(W[n].x[c]) * (W2[n].x[c]) */

@@ -201,8 +201,11 @@ __global__ void k_get_rows(int type, const uint8_t *__restrict__ src, int64_t K,
 
 // ---------------------------------------------------------------- activation quantization
 // one aligned 16-lane group per super-block, 16 elements per lane
+// GLU: the input element is silu(x[i]) * x[i + uoff] (gate | up halves of one fused GEMM output row),
+// the same expression as k_silu_mul, so quantize(silu(g)*u) is bit-identical to the unfused pair.
+template <bool GLU>
 __global__ void __launch_bounds__(256) k_quant_q8k(const float *__restrict__ x, int64_t ldx, uint8_t *__restrict__ out,
-                                                   int64_t K, int64_t M) {
+                                                   int64_t K, int64_t M, int64_t uoff) {
     const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nsb = K / 256;
     const int64_t g = gt >> 4;                        // global super-block
@@ -215,6 +218,16 @@ __global__ void __launch_bounds__(256) k_quant_q8k(const float *__restrict__ x, 
     for (int k = 0; k < 4; ++k) {
         const float4 f = valid ? src[k] : make_float4(0, 0, 0, 0);
         v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
+    }
+    if constexpr (GLU) {
+        const float4 *usrc = (const float4 *)(x + m * ldx + uoff + sb * 256 + 16 * l16);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 f = valid ? usrc[k] : make_float4(0, 0, 0, 0);
+            const float u4v[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { const float g = v[4 * k + e]; v[4 * k + e] = (g / (1.0f + expf(-g))) * u4v[e]; }
+        }
     }
     int8_t *qs = (int8_t *)out + m * K + sb * 256;
     float *d = (float *)(out + M * K) + m * nsb + sb;
@@ -290,8 +303,8 @@ int kcpp_quantize_act(int vtype, const float *x, int64_t ldx, void *out, int64_t
     if (vtype == KT_Q8_K) {
         if (K % 256) return -1;
         const int64_t nthr = K / 16 * M;
-        hipLaunchKernelGGL(k_quant_q8k, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, ldx,
-                           (uint8_t *)out, K, M);
+        hipLaunchKernelGGL(k_quant_q8k<false>, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                           ldx, (uint8_t *)out, K, M, (int64_t)0);
     } else if (vtype == KT_Q8_0) {
         if (K % 32) return -1;
         const int64_t nthreads = K / 32 * M * 8;
@@ -300,6 +313,15 @@ int kcpp_quantize_act(int vtype, const float *x, int64_t ldx, void *out, int64_t
     } else {
         return -2;
     }
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_quantize_act_glu(const float *x, int64_t ldx, int64_t uoff, void *out, int64_t K, int64_t M, void *stream) {
+    if (K % 256) return -1;
+    const int64_t nthr = K / 16 * M;
+    hipLaunchKernelGGL(k_quant_q8k<true>, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, ldx,
+                       (uint8_t *)out, K, M, uoff);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

@@ -59,11 +59,18 @@ struct KTensor {
     int64_t K = 0, N = 0;
     void *d = nullptr;
     size_t bytes = 0;
+    bool owned = true;               // false: a slice of a fused group allocation
 };
 
 struct KLayer {
     KTensor t[9];   // attn_norm, wq, wk, wv, wo, ffn_norm, gate, up, down
     uint16_t *kc = nullptr, *vc = nullptr;
+    // prefill fusion: same-type row-major (Q4_K/Q5_K) weights sharing one input are stored back to back,
+    // so q|k(|v) and gate|up each run as ONE GEMM over the concatenated rows (one activation conversion,
+    // 6x/2x more workgroups for the narrow k/v shapes)
+    void *qkv_base = nullptr, *glu_base = nullptr;
+    int nqkv = 0;                    // 2: q|k contiguous, 3: q|k|v contiguous
+    bool glu_fused = false;
 };
 
 struct kcpp_model {
@@ -75,6 +82,7 @@ struct kcpp_model {
     std::vector<KLayer> layers;      // only [il0, il1)
     // workspace
     float *x = nullptr, *qkv = nullptr, *attn = nullptr, *h = nullptr, *logits = nullptr;
+    float *hglu = nullptr;           // [ubatch][2 n_ff] fused gate|up GEMM output (prefill)
     uint16_t *q16 = nullptr;
     void *act = nullptr, *act2 = nullptr, *fa_ws = nullptr, *gemm_ws = nullptr;
     size_t act_sz = 0, gemm_ws_sz = 0;
@@ -172,9 +180,38 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     const int64_t E = hp->n_embd, F = hp->n_ff, H = hp->n_head, HKV = hp->n_head_kv, D = E / H, EKV = HKV * D;
     const int64_t UB = m->ub;
     m->layers.resize(il1 - il0);
+    static const int fuse_env = getenv("KCPP_PREFILL_FUSE") ? atoi(getenv("KCPP_PREFILL_FUSE")) : 1;
+    auto rowmajor = [](int t) { return t == KT_Q4_K || t == KT_Q5_K; };
+    auto alloc_group = [&](void *&base, int idx0, int n) -> int {
+        size_t tot = 0;
+        for (int j = 0; j < n; ++j) { int64_t K, N; shape_of(*hp, idx0 + j, K, N); tot += (size_t)tensor_bytes(types[idx0 + j], K, N); }
+        if (hipMalloc(&base, (tot + 255) & ~(size_t)255) != hipSuccess) return -1;
+        size_t off = 0;
+        for (int j = 0; j < n; ++j) {
+            KTensor &t = *tensor_at(m, idx0 + j);
+            int64_t K, N; shape_of(*hp, idx0 + j, K, N);
+            t.type = types[idx0 + j]; t.K = K; t.N = N; t.bytes = (size_t)tensor_bytes(t.type, K, N);
+            t.d = (uint8_t *)base + off; t.owned = false;
+            off += t.bytes;
+            m->weight_bytes += t.bytes;
+        }
+        return 0;
+    };
+    for (int il = il0; il < il1 && fuse_env; ++il) {
+        KLayer &L = m->layers[il - il0];
+        const int b = 3 + 9 * il;
+        if (rowmajor(types[b + 1]) && types[b + 2] == types[b + 1]) {
+            L.nqkv = types[b + 3] == types[b + 1] ? 3 : 2;
+            if (alloc_group(L.qkv_base, b + 1, L.nqkv)) return fail("qkv alloc");
+        }
+        if (rowmajor(types[b + 6]) && types[b + 7] == types[b + 6]) {
+            L.glu_fused = true;
+            if (alloc_group(L.glu_base, b + 6, 2)) return fail("glu alloc");
+        }
+    }
     for (int idx = 0; idx < 3 + 9 * hp->n_layer; ++idx) {
         KTensor *t = tensor_at(m, idx);
-        if (!t) continue;
+        if (!t || t->d) continue;
         int64_t K, N;
         shape_of(*hp, idx, K, N);
         if (alloc_tensor(m, *t, types[idx], K, N)) return fail("weight alloc");
@@ -191,9 +228,13 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
         int64_t K, N; shape_of(*hp, idx, K, N);
         if (types[idx] == KT_F32) continue;
         m->gemm_ws_sz = std::max<size_t>(m->gemm_ws_sz, (size_t)kcpp_gemm_workspace_bytes(types[idx], K, N, UB));
+        // fused shapes (q|k|v: N = E + 2 EKV; gate|up: N = 2 F)
+        m->gemm_ws_sz = std::max<size_t>(m->gemm_ws_sz, (size_t)kcpp_gemm_workspace_bytes(types[idx], E, E + 2 * EKV, UB));
+        m->gemm_ws_sz = std::max<size_t>(m->gemm_ws_sz, (size_t)kcpp_gemm_workspace_bytes(types[idx], E, 2 * F, UB));
     }
     bool ok = hipMalloc(&m->x, UB * E * 4) == hipSuccess && hipMalloc(&m->qkv, UB * (E + 2 * EKV) * 4) == hipSuccess &&
               hipMalloc(&m->attn, UB * E * 4) == hipSuccess && hipMalloc(&m->h, UB * F * 4) == hipSuccess &&
+              hipMalloc(&m->hglu, UB * 2 * F * 4) == hipSuccess &&
               hipMalloc(&m->q16, UB * E * 2) == hipSuccess && hipMalloc(&m->act, m->act_sz) == hipSuccess &&
               hipMalloc(&m->act2, m->act_sz) == hipSuccess &&
               hipMalloc(&m->fa_ws, kcpp_fa_workspace_bytes(std::max<int>(16, 1), H, hp->n_ctx)) == hipSuccess &&
@@ -223,7 +264,11 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     if (m->g_exec) hipGraphExecDestroy(m->g_exec);
     auto F = [](void *p) { if (p) hipFree(p); };
     F(m->tok_embd.d); F(m->output_norm.d); F(m->output.d);
-    for (auto &L : m->layers) { for (auto &t : L.t) F(t.d); F(L.kc); F(L.vc); }
+    for (auto &L : m->layers) {
+        for (auto &t : L.t) if (t.owned) F(t.d);
+        F(L.qkv_base); F(L.glu_base); F(L.kc); F(L.vc);
+    }
+    F(m->hglu);
     F(m->x); F(m->qkv); F(m->attn); F(m->h); F(m->logits); F(m->q16); F(m->act); F(m->act2); F(m->fa_ws);
     F(m->gemm_ws); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
     if (m->pin) hipHostFree(m->pin);
@@ -413,9 +458,16 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
         // attn_norm -> act (Q8_K fused, or f32 then Q8_0)
         if (kq && kcpp_vec_dot_type(t[2].type) == KT_Q8_K && kcpp_vec_dot_type(t[3].type) == KT_Q8_K) {
             RC(kcpp_rms_norm(m->x, E, (const float *)t[0].d, nullptr, E, m->act, E, T, hp.eps, s));
-            RC(matmul(m, t[1], nullptr, m->act, T, m->qkv, LQ, nullptr, 0, 0));
-            RC(matmul(m, t[2], nullptr, m->act, T, m->qkv + E, LQ, nullptr, 0, 0));
-            RC(matmul(m, t[3], nullptr, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0));
+            if (L.nqkv >= 2) {                       // q|k(|v) rows back to back: one GEMM
+                KTensor f = t[1];
+                f.N = E + (L.nqkv - 1) * EKV;
+                RC(matmul(m, f, nullptr, m->act, T, m->qkv, LQ, nullptr, 0, 0));
+                if (L.nqkv == 2) RC(matmul(m, t[3], nullptr, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0));
+            } else {
+                RC(matmul(m, t[1], nullptr, m->act, T, m->qkv, LQ, nullptr, 0, 0));
+                RC(matmul(m, t[2], nullptr, m->act, T, m->qkv + E, LQ, nullptr, 0, 0));
+                RC(matmul(m, t[3], nullptr, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0));
+            }
         } else {
             RC(kcpp_rms_norm(m->x, E, (const float *)t[0].d, m->attn, E, nullptr, E, T, hp.eps, s));
             for (int j = 1; j <= 3; ++j) {
@@ -438,14 +490,21 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, T, hp.eps, s));
             RC(kcpp_quantize_act(kcpp_vec_dot_type(t[6].type), m->attn, E, m->act, E, T, s));
         }
-        if (t[6].type == t[7].type) {
-            RC(matmul(m, t[6], &t[7], m->act, T, m->h, F, nullptr, 0, 1));              // h = silu(g) * u
+        if (L.glu_fused && kcpp_vec_dot_type(t[8].type) == KT_Q8_K) {
+            KTensor f = t[6];                          // gate|up rows back to back: one GEMM, then
+            f.N = 2 * F;                               // silu(g)*u fused into the Q8_K quantization
+            RC(matmul(m, f, nullptr, m->act, T, m->hglu, 2 * F, nullptr, 0, 0));
+            RC(kcpp_quantize_act_glu(m->hglu, 2 * F, F, m->act2, F, T, s));
         } else {
-            RC(matmul(m, t[6], nullptr, m->act, T, m->h, F, nullptr, 0, 0));
-            RC(matmul(m, t[7], nullptr, m->act, T, m->qkv, F, nullptr, 0, 0));
-            RC(kcpp_silu_mul(m->h, m->h, m->qkv, (int64_t)T * F, s));
+            if (t[6].type == t[7].type) {
+                RC(matmul(m, t[6], &t[7], m->act, T, m->h, F, nullptr, 0, 1));          // h = silu(g) * u
+            } else {
+                RC(matmul(m, t[6], nullptr, m->act, T, m->h, F, nullptr, 0, 0));
+                RC(matmul(m, t[7], nullptr, m->act, T, m->hglu, F, nullptr, 0, 0));
+                RC(kcpp_silu_mul(m->h, m->h, m->hglu, (int64_t)T * F, s));
+            }
+            RC(kcpp_quantize_act(kcpp_vec_dot_type(t[8].type), m->h, F, m->act2, F, T, s));
         }
-        RC(kcpp_quantize_act(kcpp_vec_dot_type(t[8].type), m->h, F, m->act2, F, T, s));
         RC(matmul(m, t[8], nullptr, m->act2, T, m->x, E, m->x, E, 0));                   // x += down . h
     }
     return 0;

@@ -31,6 +31,7 @@ _SIGS = {
     "kcpp_dequantize": [I, P, P, I64, I64, P],
     "kcpp_get_rows": [I, P, I64, I64, P, I64, P, I64, P],
     "kcpp_quantize_act": [I, P, I64, P, I64, I64, P],
+    "kcpp_quantize_act_glu": [P, I64, I64, P, I64, I64, P],
     "kcpp_gemv": [I, P, P, I64, I64, P, I64, P, I64, P, I64, I, P],
     "kcpp_gemm": [I, P, P, I64, I64, P, I64, P, I64, P, I64, I, P, P],
     "kcpp_rms_norm": [P, I64, P, P, I64, P, I64, I64, Fl, P],

@@ -28,8 +28,12 @@ def timeit(fn, iters=20, warm=3):
 def main():
     s = torch.cuda.current_stream().cuda_stream
     out = []
-    for (t, Kd, N, M) in [(12, 4096, 14336, 512), (12, 4096, 4096, 512), (14, 14336, 4096, 512), (12, 14336, 4096, 512),
-                          (8, 4096, 14336, 32), (8, 4096, 4096, 512), (2, 4096, 4096, 512), (13, 4096, 4096, 512)]:
+    shapes = [(12, 4096, 14336, 512), (12, 4096, 4096, 512), (12, 4096, 1024, 512), (14, 4096, 1024, 512),
+              (12, 4096, 6144, 512), (12, 4096, 28672, 512), (14, 14336, 4096, 512), (12, 14336, 4096, 512),
+              (8, 4096, 14336, 32), (8, 4096, 4096, 512), (2, 4096, 4096, 512), (13, 4096, 4096, 512)]
+    if os.environ.get("MB_SHAPES") == "prefill":
+        shapes = shapes[:8]
+    for (t, Kd, N, M) in shapes:
         wb = Kd // K.BLOCK[t][0] * K.BLOCK[t][1] * N
         w = torch.empty(wb, dtype=torch.uint8, device="cuda")
         K.call("kcpp_weight_synth", t, 1, 1, w.data_ptr(), Kd, N, s)
