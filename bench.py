@@ -79,7 +79,7 @@ def measure_roofline(K, torch, iters=48):
     gbs = alg / (ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "k_gemv_dec<Q4_K,GLU,norm+quant prologue> 4096x(2x14336)", "bytes_per_launch": alg,
+            "kernel": "kcpp_gemv_dec -> k_gemv_q4k<IT1,R2,GLU,norm+quant prologue> 4096x(2x14336)", "bytes_per_launch": alg,
             "avg_us": round(ms * 1e3, 2)}
 
 

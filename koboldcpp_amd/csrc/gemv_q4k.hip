@@ -209,9 +209,14 @@ int launch_q4k(const DecArgs &a, hipStream_t s) {
         ntot += a.N[i];
     }
     const int64_t groups = ntot / R;
-    static const int max_blocks = getenv("KCPP_Q4K_BLOCKS") ? atoi(getenv("KCPP_Q4K_BLOCKS")) : 1024;
+    // measured (tools/stream_probe.py sweep): 512 workgroups (2 per CU) for every shape, 256 for gate|up with
+    // R = 2 -- fewer prologues (each workgroup re-derives the activation) and less queueing than 1024
+    static const int env_blocks = getenv("KCPP_Q4K_BLOCKS") ? atoi(getenv("KCPP_Q4K_BLOCKS")) : 0;
+    const int max_blocks = env_blocks ? env_blocks : (MODE == 1 && R == 2 ? 256 : 512);
+    static const int min_gpw = getenv("KCPP_Q4K_ONEPASS") ? atoi(getenv("KCPP_Q4K_ONEPASS")) : 0;
     int64_t nblk = std::min<int64_t>((groups + 3) / 4, max_blocks);
     nblk = std::max<int64_t>(nblk, (groups + 255) / 256);    // <= 64 groups per wave (result slots)
+    if (min_gpw) nblk = (groups + 3) / 4;                     // experiment: one group per wave
     const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
     hipLaunchKernelGGL((k_gemv_q4k<IT, R, MODE, PRO, MC, PF>), dim3((unsigned)nblk), dim3(256), (size_t)abytes + 16, s, a);
     KCPP_CHECK(hipGetLastError());
@@ -225,12 +230,16 @@ extern "C" int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream) 
     hipStream_t s = (hipStream_t)stream;
     if (a.nseg < 1 || a.nseg > 3) return -3;
     static const int r_env = getenv("KCPP_Q4K_R") ? atoi(getenv("KCPP_Q4K_R")) : 0;
-    // gate|up (mode 1) stays on gemv_dec_impl.h by default: measured 21.3 vs 22.7 us there
-    static const int glu = getenv("KCPP_Q4K_GLU") ? atoi(getenv("KCPP_Q4K_GLU")) : 0;
+    // gate|up: R = 2 with prefetch at 256 workgroups (17.5 us vs 21.1 us for gemv_dec_impl.h)
+    static const int glu = getenv("KCPP_Q4K_GLU") ? atoi(getenv("KCPP_Q4K_GLU")) : 1;
     if (a.K == 4096) {
-        if (mode == 1 && pro == 1 && glu) return r_env == 2 ? launch_q4k<1, 2, 1, 1, 1, 1>(a, s) : launch_q4k<1, 1, 1, 1, 1, 1>(a, s);
+        static const int pf_env = getenv("KCPP_Q4K_PF") ? atoi(getenv("KCPP_Q4K_PF")) : 1;
+        if (mode == 1 && pro == 1 && glu) {
+            if (!pf_env) return launch_q4k<1, 1, 1, 1, 1, 0>(a, s);
+            return r_env == 1 ? launch_q4k<1, 1, 1, 1, 1, 1>(a, s) : launch_q4k<1, 2, 1, 1, 1, 1>(a, s);
+        }
         if (mode == 2 && pro == 1) return launch_q4k<1, 2, 2, 1, 1, 0>(a, s);
-        if (mode == 0 && pro == 0) return r_env == 2 ? launch_q4k<1, 2, 0, 0, 1, 0>(a, s) : launch_q4k<1, 1, 0, 0, 1, 0>(a, s);
+        if (mode == 0 && pro == 0) return launch_q4k<1, 1, 0, 0, 1, 0>(a, s);
         if (mode == 0 && pro == 1) return launch_q4k<1, 2, 0, 1, 1, 1>(a, s);
         return -3;
     }
