@@ -178,7 +178,21 @@ __global__ void __launch_bounds__(256) k_gemv_q4k(const DecArgs a) {
         slot_g = mine ? g : slot_g;
     };
     int k = 0;
-    if constexpr (PF) {
+    if constexpr (PF == 2) {                          // three buffers: two groups in flight while computing
+        Buf bc;
+        issue(min(wid + nw, ngroups - 1), bb);
+        for (int g = wid; g < ngroups; g += 3 * nw, k += 3) {
+            const int g1 = g + nw, g2 = g + 2 * nw, g3 = g + 3 * nw, g4 = g + 4 * nw;
+            issue(min(g2, ngroups - 1), bc);
+            compute(g, ba, k);
+            if (g1 >= ngroups) break;
+            issue(min(g3, ngroups - 1), ba);
+            compute(g1, bb, k + 1);
+            if (g2 >= ngroups) break;
+            issue(min(g4, ngroups - 1), bb);
+            compute(g2, bc, k + 2);
+        }
+    } else if constexpr (PF) {
         for (int g = wid; g < ngroups; g += 2 * nw, k += 2) {
             const int g1 = g + nw, g2 = g + 2 * nw;
             issue(min(g1, ngroups - 1), bb);
@@ -236,6 +250,7 @@ extern "C" int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream) 
         static const int pf_env = getenv("KCPP_Q4K_PF") ? atoi(getenv("KCPP_Q4K_PF")) : 1;
         if (mode == 1 && pro == 1 && glu) {
             if (!pf_env) return launch_q4k<1, 1, 1, 1, 1, 0>(a, s);
+            if (pf_env == 2) return launch_q4k<1, 2, 1, 1, 1, 2>(a, s);
             return r_env == 1 ? launch_q4k<1, 1, 1, 1, 1, 1>(a, s) : launch_q4k<1, 2, 1, 1, 1, 1>(a, s);
         }
         if (mode == 2 && pro == 1) return launch_q4k<1, 2, 2, 1, 1, 0>(a, s);
