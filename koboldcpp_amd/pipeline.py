@@ -182,8 +182,14 @@ def bench_main(args, world, rank, local):
     import torch.distributed as dist
     import bench as B
 
-    torch.cuda.set_device(local)
     backend = os.environ.get("KCPP_PIPE_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        # rehearsal on fewer GPUs than ranks (host-staged gloo transport only; RCCL needs distinct GPUs)
+        if os.environ.get("KCPP_PIPE_SHARE_GPU") != "1" or backend == "nccl":
+            raise RuntimeError("local rank %d but only %d GPU(s) visible" % (local, ndev))
+        local = local % ndev
+    torch.cuda.set_device(local)
     dist.init_process_group(backend=backend, init_method="env://", world_size=world, rank=rank)
     hp = dict(B.LLAMA3_8B)
     if args.layers:
