@@ -466,7 +466,7 @@ struct orc_llama {
 orc_llama *orc_llama_create(const orc_hparams *hp, const void *const *data, const int *types, int nthreads) {
     orc_llama *m = calloc(1, sizeof(*m));
     m->hp = *hp;
-    int nw = 3 + 9 * hp->n_layer;
+    int nw = 3 + (hp->n_expert ? 10 : 9) * hp->n_layer;
     void **w = malloc(sizeof(void *) * nw);
     int *t = malloc(sizeof(int) * nw);
     memcpy(w, data, sizeof(void *) * nw);
@@ -490,6 +490,50 @@ void orc_llama_last_hidden(orc_llama *m, float *out) { memcpy(out, m->last_hidde
 
 static void add_inplace(float *a, const float *b, int64_t n) { for (int64_t i = 0; i < n; ++i) a[i] += b[i]; }
 
+/* llm_build_moe_ffn (src/llama.cpp:9416-9520) for the llama architecture: router mul_mat, soft_max
+ * (ggml.c:13909, ggml_float sum), top_k = argsort descending (the exchange sort of
+ * ggml_compute_forward_argsort_f32), normalized weights (sum_rows + div), per selected expert
+ * up / silu(gate) mul_mat_id, down mul_mat_id, weighted, summed in top-k order.  Writes moe[T][E]. */
+static void moe_ffn(const orc_hparams *hp, const void *const *lw, const int *lt, const float *cur, int T, float *moe, int NT) {
+    const int E = hp->n_embd, F = hp->n_ff, NE = hp->n_expert, NU = hp->n_expert_used;
+    float *lg = malloc(sizeof(float) * T * NE);
+    orc_mul_mat(lt[9], lw[9], E, NE, cur, T, lg, NT);
+    const int64_t rg = orc_row_bytes(lt[6], E) * F, ru = orc_row_bytes(lt[7], E) * F, rd = orc_row_bytes(lt[8], F) * E;
+    float *g = malloc(sizeof(float) * F), *u = malloc(sizeof(float) * F), *o = malloc(sizeof(float) * E);
+    for (int t = 0; t < T; ++t) {
+        float *p = lg + (int64_t)t * NE;
+        float mx = -INFINITY;
+        for (int e = 0; e < NE; ++e) mx = fmaxf(mx, p[e]);
+        double sum = 0.0;
+        for (int e = 0; e < NE; ++e) { const float v = expf(p[e] - mx); sum += (double)v; p[e] = v; }
+        const float inv = (float)(1.0 / sum);
+        for (int e = 0; e < NE; ++e) p[e] *= inv;
+        int idx[64];
+        for (int e = 0; e < NE; ++e) idx[e] = e;
+        for (int j = 0; j < NE; ++j)
+            for (int k = j + 1; k < NE; ++k)
+                if (p[idx[j]] < p[idx[k]]) { const int tmp = idx[j]; idx[j] = idx[k]; idx[k] = tmp; }
+        double ws = 0.0;
+        for (int j = 0; j < NU; ++j) ws += (double)p[idx[j]];
+        const float wsum = (float)ws;
+        float *mo = moe + (int64_t)t * E;
+        for (int j = 0; j < NU; ++j) {
+            const int e = idx[j];
+            const float w = p[e] / wsum;
+            const float *ct = cur + (int64_t)t * E;
+            orc_mul_mat(lt[6], (const uint8_t *)lw[6] + e * rg, E, F, ct, 1, g, 1);
+            orc_mul_mat(lt[7], (const uint8_t *)lw[7] + e * ru, E, F, ct, 1, u, 1);
+            for (int i = 0; i < F; ++i) g[i] = u[i] * (g[i] / (1.0f + expf(-g[i])));   /* up * silu(gate) */
+            orc_mul_mat(lt[8], (const uint8_t *)lw[8] + e * rd, F, E, g, 1, o, 1);
+            for (int i = 0; i < E; ++i) {
+                const float v = o[i] * w;
+                mo[i] = j == 0 ? v : mo[i] + v;
+            }
+        }
+    }
+    free(lg); free(g); free(u); free(o);
+}
+
 int orc_llama_eval(orc_llama *m, const int32_t *tokens, int T, int n_past, float *logits) {
     const orc_hparams *hp = &m->hp;
     const int E = hp->n_embd, H = hp->n_head, HKV = hp->n_head_kv, D = E / H, F = hp->n_ff;
@@ -511,9 +555,10 @@ int orc_llama_eval(orc_llama *m, const int32_t *tokens, int T, int n_past, float
         for (int j = 0; j < n_kv; ++j)
             mask[(int64_t)t * n_kv + j] = (j <= n_past + t) ? 0 : 0xFC00; /* -inf */
     const float kq_scale = 1.0f / sqrtf((float)D);
+    const int LW = hp->n_expert ? 10 : 9;
     for (int il = 0; il < hp->n_layer; ++il) {
-        const void *const *lw = m->w + 3 + 9 * il;
-        const int *lt = m->t + 3 + 9 * il;
+        const void *const *lw = m->w + 3 + LW * il;
+        const int *lt = m->t + 3 + LW * il;
         orc_rms_norm(x, (const float *)lw[0], cur, E, T, hp->eps);
         orc_mul_mat(lt[1], lw[1], E, E, cur, T, q, NT);
         orc_mul_mat(lt[2], lw[2], E, EKV, cur, T, kk, NT);
@@ -531,6 +576,11 @@ int orc_llama_eval(orc_llama *m, const int32_t *tokens, int T, int n_past, float
         add_inplace(tmp, x, (int64_t)T * E);             /* ffn_inp = attn_out + inpSA */
         memcpy(x, tmp, sizeof(float) * T * E);
         orc_rms_norm(x, (const float *)lw[5], cur, E, T, hp->eps);
+        if (hp->n_expert) {
+            moe_ffn(hp, lw, lt, cur, T, tmp, NT);
+            for (int64_t i = 0; i < (int64_t)T * E; ++i) x[i] = tmp[i] + x[i];   /* ggml_add(moe_out, ffn_inp) */
+            continue;
+        }
         orc_mul_mat(lt[6], lw[6], E, F, cur, T, g, NT);
         orc_mul_mat(lt[7], lw[7], E, F, cur, T, u, NT);
         for (int64_t i = 0; i < (int64_t)T * F; ++i) g[i] = (g[i] / (1.0f + expf(-g[i]))) * u[i];  /* silu(gate)*up */

@@ -64,11 +64,14 @@ void orc_set_fa_f32_accum(int on);
 typedef struct {
     int n_vocab, n_embd, n_head, n_head_kv, n_layer, n_ff, n_ctx;
     float eps, rope_base, rope_freq_scale;
+    int n_expert, n_expert_used;     /* 0 = dense FFN; else mixture of experts (llm_build_moe_ffn) */
 } orc_hparams;
 
-/* weights: 3 + 9*n_layer entries in this order:
+/* weights: 3 + LW*n_layer entries (LW = 9 dense, 10 MoE) in this order:
  *   tok_embd, output_norm, output, then per layer
- *   attn_norm, wq, wk, wv, wo, ffn_norm, ffn_gate, ffn_up, ffn_down */
+ *   attn_norm, wq, wk, wv, wo, ffn_norm, ffn_gate, ffn_up, ffn_down (, ffn_gate_inp)
+ * MoE: ffn_gate/up/down hold n_expert consecutive [K][N] slices (ggml's [K, N, n_expert] _exps
+ * tensors); ffn_gate_inp is the [n_embd, n_expert] router. */
 typedef struct orc_llama orc_llama;
 orc_llama *orc_llama_create(const orc_hparams *hp, const void *const *data, const int *types, int nthreads);
 void       orc_llama_free(orc_llama *m);

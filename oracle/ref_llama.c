@@ -32,7 +32,8 @@ typedef struct {
     int n_vocab, n_embd, n_head, n_head_kv, n_layer, n_ff, n_ctx;
     float eps, rope_base, rope_freq_scale;
     unsigned long long seed;
-    int *types;            /* 3 + 9*n_layer */
+    int n_expert, n_expert_used;   /* MoE (llm_build_moe_ffn) when n_expert > 0 */
+    int *types;            /* 3 + LW*n_layer, LW = 9 dense / 10 MoE (+ ffn_gate_inp) */
     int nthreads;
     int n_prompt, n_gen, ubatch;
     int *prompt;
@@ -42,11 +43,11 @@ typedef struct {
 static int read_cfg(const char *path, cfg_t *c) {
     FILE *f = fopen(path, "r");
     if (!f) return -1;
-    int ok = fscanf(f, "%d %d %d %d %d %d %d %f %f %f %llu", &c->n_vocab, &c->n_embd, &c->n_head,
+    int ok = fscanf(f, "%d %d %d %d %d %d %d %f %f %f %llu %d %d", &c->n_vocab, &c->n_embd, &c->n_head,
                     &c->n_head_kv, &c->n_layer, &c->n_ff, &c->n_ctx, &c->eps, &c->rope_base,
-                    &c->rope_freq_scale, &c->seed);
-    if (ok != 11) { fclose(f); return -2; }
-    int nw = 3 + 9 * c->n_layer;
+                    &c->rope_freq_scale, &c->seed, &c->n_expert, &c->n_expert_used);
+    if (ok != 13) { fclose(f); return -2; }
+    int nw = 3 + (c->n_expert ? 10 : 9) * c->n_layer;
     c->types = malloc(sizeof(int) * nw);
     for (int i = 0; i < nw; ++i) if (fscanf(f, "%d", &c->types[i]) != 1) { fclose(f); return -3; }
     if (fscanf(f, "%d %d %d %d", &c->nthreads, &c->n_prompt, &c->n_gen, &c->ubatch) != 4) { fclose(f); return -4; }
@@ -75,14 +76,17 @@ static void fill_tensor(struct ggml_tensor *t, int type, unsigned long long seed
 static int load_model(model_t *m) {
     cfg_t *c = &m->c;
     const int E = c->n_embd, D = E / c->n_head, EKV = c->n_head_kv * D, F = c->n_ff, V = c->n_vocab;
-    const int nw = 3 + 9 * c->n_layer;
+    const int LW = c->n_expert ? 10 : 9;
+    const int nw = 3 + LW * c->n_layer;
+    const int NE = c->n_expert ? c->n_expert : 1;
     size_t total = 0;
-    int64_t shapes[3 + 9 * 256][2];
+    int64_t shapes[3 + 10 * 256][3];
+    for (int i = 0; i < nw; ++i) shapes[i][2] = 1;
     shapes[0][0] = E; shapes[0][1] = V;
     shapes[1][0] = E; shapes[1][1] = 1;
     shapes[2][0] = E; shapes[2][1] = V;
     for (int il = 0; il < c->n_layer; ++il) {
-        int64_t (*s)[2] = shapes + 3 + 9 * il;
+        int64_t (*s)[3] = shapes + 3 + LW * il;
         s[0][0] = E; s[0][1] = 1;
         s[1][0] = E; s[1][1] = E;
         s[2][0] = E; s[2][1] = EKV;
@@ -92,9 +96,13 @@ static int load_model(model_t *m) {
         s[6][0] = E; s[6][1] = F;
         s[7][0] = E; s[7][1] = F;
         s[8][0] = F; s[8][1] = E;
+        if (c->n_expert) {
+            s[6][2] = s[7][2] = s[8][2] = NE;          /* _exps tensors [K, N, n_expert] */
+            s[9][0] = E; s[9][1] = NE; s[9][2] = 1;    /* ffn_gate_inp */
+        }
     }
     for (int i = 0; i < nw; ++i)
-        total += ggml_row_size((enum ggml_type)c->types[i], shapes[i][0]) * shapes[i][1] + 256;
+        total += ggml_row_size((enum ggml_type)c->types[i], shapes[i][0]) * shapes[i][1] * shapes[i][2] + 256;
     total += (size_t)2 * c->n_layer * ((size_t)EKV * c->n_ctx * 2 + 256);
     total += (size_t)(nw + 2 * c->n_layer + 16) * ggml_tensor_overhead();
     struct ggml_init_params ip = { total, NULL, false };
@@ -102,8 +110,21 @@ static int load_model(model_t *m) {
     if (!m->wctx) return -1;
     m->w = malloc(sizeof(*m->w) * nw);
     for (int i = 0; i < nw; ++i) {
-        m->w[i] = ggml_new_tensor_2d(m->wctx, (enum ggml_type)c->types[i], shapes[i][0], shapes[i][1]);
-        fill_tensor(m->w[i], c->types[i], c->seed, i);
+        if (shapes[i][2] > 1) {
+            /* expert e of tensor i: synthetic tid = i * 256 + e (the convention of tests/refharness.py) */
+            m->w[i] = ggml_new_tensor_3d(m->wctx, (enum ggml_type)c->types[i], shapes[i][0], shapes[i][1], shapes[i][2]);
+            const size_t slice = ggml_row_size((enum ggml_type)c->types[i], shapes[i][0]) * shapes[i][1];
+            const int bb = ks_block_bytes(c->types[i]);
+            for (int64_t e = 0; e < shapes[i][2]; ++e) {
+                uint8_t *p = (uint8_t *)m->w[i]->data + e * slice;
+                const int64_t nbl = slice / bb;
+                #pragma omp parallel for
+                for (int64_t b = 0; b < nbl; ++b) ks_fill_block(c->types[i], c->seed, (uint64_t)(i * 256 + e), (uint64_t)b, p + b * bb);
+            }
+        } else {
+            m->w[i] = ggml_new_tensor_2d(m->wctx, (enum ggml_type)c->types[i], shapes[i][0], shapes[i][1]);
+            fill_tensor(m->w[i], c->types[i], c->seed, i);
+        }
     }
     m->kc = malloc(sizeof(*m->kc) * c->n_layer);
     m->vc = malloc(sizeof(*m->vc) * c->n_layer);
@@ -125,7 +146,9 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits)
     size_t mem = (size_t)T * c->n_layer * ((size_t)E * 16 + (size_t)F * 4 + (size_t)EKV * 6) * sizeof(float)
                + (size_t)n_kv * T_pad * 2 + (size_t)c->n_vocab * 8 + (size_t)T * 16
                + (size_t)(c->n_layer * 64 + 64) * ggml_tensor_overhead() + ggml_graph_overhead_custom(8192, false)
-               + (size_t)64 * 1024 * 1024 + (size_t)T * F * 8 + (size_t)T * E * 8;
+               + (size_t)64 * 1024 * 1024 + (size_t)T * F * 8 + (size_t)T * E * 8
+               + (c->n_expert ? (size_t)T * c->n_layer * ((size_t)F * 4 + (size_t)E * 3 + 64) * c->n_expert_used * sizeof(float)
+                                + (size_t)c->n_layer * 64 * ggml_tensor_overhead() : 0);
     struct ggml_init_params ip = { mem, NULL, false };
     struct ggml_context *ctx = ggml_init(ip);
     if (!ctx) return -1;
@@ -146,7 +169,7 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits)
     const float kq_scale = 1.0f / sqrtf((float)D);
     struct ggml_tensor *inpL = ggml_get_rows(ctx, m->w[0], inp_tokens);   /* llm_build_inp_embd */
     for (int il = 0; il < c->n_layer; ++il) {
-        struct ggml_tensor **lw = m->w + 3 + 9 * il;
+        struct ggml_tensor **lw = m->w + 3 + (c->n_expert ? 10 : 9) * il;
         struct ggml_tensor *inpSA = inpL;
         struct ggml_tensor *cur = ggml_mul(ctx, ggml_rms_norm(ctx, inpL, c->eps), lw[0]);
         struct ggml_tensor *Qcur = ggml_mul_mat(ctx, lw[1], cur);
@@ -177,10 +200,32 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits)
         }
         struct ggml_tensor *ffn_inp = ggml_add(ctx, cur, inpSA);
         cur = ggml_mul(ctx, ggml_rms_norm(ctx, ffn_inp, c->eps), lw[5]);
-        struct ggml_tensor *up = ggml_mul_mat(ctx, lw[7], cur);
-        struct ggml_tensor *gate = ggml_mul_mat(ctx, lw[6], cur);
-        cur = ggml_mul(ctx, ggml_silu(ctx, gate), up);
-        cur = ggml_mul_mat(ctx, lw[8], cur);
+        if (c->n_expert) {
+            /* mixture of experts as llm_build_moe_ffn (src/llama.cpp:9416), llama arch: norm_w = true */
+            const int NE = c->n_expert, NU = c->n_expert_used;
+            const int64_t T = cur->ne[1];                  /* 1 in the last layer (out_ids) */
+            struct ggml_tensor *logits = ggml_mul_mat(ctx, lw[9], cur);                 /* [NE, T] */
+            struct ggml_tensor *probs = ggml_soft_max(ctx, logits);
+            struct ggml_tensor *sel = ggml_top_k(ctx, probs, NU);                        /* [NU, T] */
+            struct ggml_tensor *wts = ggml_get_rows(ctx, ggml_reshape_3d(ctx, probs, 1, NE, T), sel);
+            wts = ggml_reshape_2d(ctx, wts, NU, T);
+            wts = ggml_div(ctx, wts, ggml_sum_rows(ctx, wts));
+            wts = ggml_reshape_3d(ctx, wts, 1, NU, T);
+            struct ggml_tensor *cur3 = ggml_reshape_3d(ctx, cur, E, 1, T);
+            struct ggml_tensor *up = ggml_mul_mat_id(ctx, lw[7], cur3, sel);             /* [F, NU, T] */
+            struct ggml_tensor *gate = ggml_mul_mat_id(ctx, lw[6], cur3, sel);
+            struct ggml_tensor *par = ggml_mul(ctx, up, ggml_silu(ctx, gate));
+            struct ggml_tensor *ex = ggml_mul_mat_id(ctx, lw[8], par, sel);              /* [E, NU, T] */
+            ex = ggml_mul(ctx, ex, wts);
+            struct ggml_tensor *moe = ggml_view_2d(ctx, ex, E, T, ex->nb[2], 0);
+            for (int i = 1; i < NU; ++i) moe = ggml_add(ctx, moe, ggml_view_2d(ctx, ex, E, T, ex->nb[2], i * ex->nb[1]));
+            cur = moe;
+        } else {
+            struct ggml_tensor *up = ggml_mul_mat(ctx, lw[7], cur);
+            struct ggml_tensor *gate = ggml_mul_mat(ctx, lw[6], cur);
+            cur = ggml_mul(ctx, ggml_silu(ctx, gate), up);
+            cur = ggml_mul_mat(ctx, lw[8], cur);
+        }
         inpL = ggml_add(ctx, cur, ffn_inp);
     }
     struct ggml_tensor *cur = ggml_mul(ctx, ggml_rms_norm(ctx, inpL, c->eps), m->w[1]);

@@ -112,5 +112,22 @@ def main():
     print("wrote", sorted(os.listdir(HERE)))
 
 
+def moe():
+    """tiny Mixtral-style model (TINY_MOE: 4 experts, top-2, Q5_K_M-like types): reference logits for
+    prefill + 8 greedy steps; written to e2e_moe.npz (make_golden.py --moe)"""
+    rng = np.random.default_rng(20241017)
+    hp = R.TINY_MOE
+    types = R.moe_types(hp["n_layer"])
+    prompt = [int(v) for v in rng.integers(1, hp["n_vocab"], size=29)]
+    L, _ = R.run_ref_llama(hp, types, 1234, prompt, 8)
+    np.savez_compressed(os.path.join(HERE, "e2e_moe.npz"), types=np.array(types, np.int32),
+                        prompt=np.array(prompt, np.int32), logits=L, tokens=np.argmax(L, axis=1).astype(np.int32))
+    print("wrote e2e_moe.npz")
+
+
 if __name__ == "__main__":
-    main()
+    import sys
+    if "--moe" in sys.argv:
+        moe()
+    else:
+        main()

@@ -121,27 +121,52 @@ def flash_attn(q, k, v, mask, nthreads=0):
 
 class HParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")] + \
-               [(n, ctypes.c_float) for n in ("eps", "rope_base", "rope_freq_scale")]
+               [(n, ctypes.c_float) for n in ("eps", "rope_base", "rope_freq_scale")] + \
+               [(n, ctypes.c_int) for n in ("n_expert", "n_expert_used")]
+
+
+def per_layer(hp):
+    return 10 if hp.get("n_expert", 0) else 9
 
 
 def weight_shapes(hp):
-    """(K, N) per canonical weight index: tok_embd, output_norm, output, then 9 per layer."""
+    """(K, N) per canonical weight index: tok_embd, output_norm, output, then 9 per layer (10 with MoE:
+    + ffn_gate_inp [n_embd, n_expert]; the expert tensors' (K, N) is per expert slice)."""
     E, F, V = hp["n_embd"], hp["n_ff"], hp["n_vocab"]
     EKV = hp["n_head_kv"] * (E // hp["n_head"])
     s = [(E, V), (E, 1), (E, V)]
     for _ in range(hp["n_layer"]):
         s += [(E, 1), (E, E), (E, EKV), (E, EKV), (E, E), (E, 1), (E, F), (E, F), (F, E)]
+        if hp.get("n_expert", 0):
+            s += [(E, hp["n_expert"])]
     return s
+
+
+def n_slices(hp, idx):
+    """experts per tensor index (1 for dense tensors)"""
+    if idx < 3 or not hp.get("n_expert", 0):
+        return 1
+    return hp["n_expert"] if (idx - 3) % 10 in (6, 7, 8) else 1
+
+
+def synth_tensor(hp, t, seed, idx):
+    """bytes of canonical tensor idx; expert e of an _exps tensor uses tid idx * 256 + e"""
+    k, n = weight_shapes(hp)[idx]
+    ns = n_slices(hp, idx)
+    if ns == 1:
+        return synth(t, seed, idx, k, n)
+    return np.concatenate([synth(t, seed, idx * 256 + e, k, n) for e in range(ns)])
 
 
 class OracleLlama:
     def __init__(self, hp, types, seed, nthreads=0):
         self.hp = hp
-        self.bufs = [synth(t, seed, i, k, n) for i, ((k, n), t) in enumerate(zip(weight_shapes(hp), types))]
+        self.bufs = [synth_tensor(hp, t, seed, i) for i, t in enumerate(types)]
         arr = (ctypes.c_void_p * len(self.bufs))(*[b.ctypes.data for b in self.bufs])
         tarr = (ctypes.c_int * len(types))(*types)
         h = HParams(*[hp[n] for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")],
-                    hp["eps"], hp["rope_base"], hp.get("rope_freq_scale", 1.0))
+                    hp["eps"], hp["rope_base"], hp.get("rope_freq_scale", 1.0), hp.get("n_expert", 0),
+                    hp.get("n_expert_used", 0))
         self._arr, self._tarr, self._h = arr, tarr, h
         self.m = lib().orc_llama_create(ctypes.byref(h), arr, tarr, nthreads)
 
@@ -170,7 +195,8 @@ def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeou
         out = os.path.join(td, "logits.bin")
         with open(cfg, "w") as f:
             f.write(" ".join(str(hp[n]) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")))
-            f.write(" %r %r %r %d\n" % (float(hp["eps"]), float(hp["rope_base"]), float(hp.get("rope_freq_scale", 1.0)), seed))
+            f.write(" %r %r %r %d %d %d\n" % (float(hp["eps"]), float(hp["rope_base"]), float(hp.get("rope_freq_scale", 1.0)),
+                                             seed, hp.get("n_expert", 0), hp.get("n_expert_used", 0)))
             f.write(" ".join(map(str, types)) + "\n")
             f.write("%d %d %d %d\n" % (nthreads, len(prompt), n_gen, ubatch))
             f.write(" ".join(map(str, prompt)) + "\n" + out + "\n")
@@ -197,6 +223,17 @@ def run_ref_op(op, inp_bytes, out_count, args, nthreads=4):
 
 TINY = dict(n_vocab=512, n_embd=512, n_head=4, n_head_kv=1, n_layer=2, n_ff=1024, n_ctx=256,
             eps=1e-5, rope_base=500000.0)
+# Mixtral-style tiny MoE (4 experts, top-2): BASELINE config 5's structure at test size
+TINY_MOE = dict(TINY, n_expert=4, n_expert_used=2)
+
+
+def moe_types(n_layer, t=Q5_K, router=F16):
+    """Q5_K_M-like MoE mix: Q5_K everywhere, Q6_K ffn_down_exps on the 'more bits' layers, F16 router"""
+    ty = [Q4_K, F32, Q6_K]
+    for il in range(n_layer):
+        more = il < n_layer // 8 or il >= 7 * n_layer // 8 or (il - n_layer // 8) % 3 == 2
+        ty += [F32, t, t, t, t, F32, t, t, Q6_K if more else t, router]
+    return ty
 
 
 def q4_k_m_types(n_layer, tok=Q4_K, out=Q6_K):
