@@ -89,6 +89,18 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
 /* the MFMA prefill kernel alone (koboldcpp_amd/csrc/attn_mfma.hip); -3 when the shape is not covered */
 int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, int T, int H,
                                  int HKV, int D, int n_past, float scale, void *stream);
+/* MoE router (llm_build_moe_ffn, src/llama.cpp:9435-9460): logits = W_router . x (W F16 -> x rounded
+ * to f16 like the CPU vec_dot_f16, or F32), softmax, top-k (argsort descending), weights normalized to
+ * sum 1; ids/weights [T][k] */
+int kcpp_moe_route(const float *x, int64_t ldx, const void *w_router, int wtype, int64_t K, int n_expert, int k,
+                   int32_t *ids, float *weights, int T, void *stream);
+/* MoE helpers: dst[i] = src[rows[i]] (row gather); dst[rows[i]] = w[i] * src[i] (weighted scatter into
+ * the token's top-k slot row); combine: x[i] = ((slots[0][i] + slots[1][i]) + ...) + x[i] over k slots
+ * spaced slot_stride floats (the ggml_add chain of llm_build_moe_ffn, src/llama.cpp:9500-9515) */
+int kcpp_moe_gather(const float *src, int64_t lds, const int32_t *rows, int n, int64_t E, float *dst, void *stream);
+int kcpp_moe_scatter(float *dst, int64_t ldd, const float *src, const int32_t *rows, const float *w, int n, int64_t E,
+                     void *stream);
+int kcpp_moe_combine(float *x, const float *slots, int64_t slot_stride, int k, int64_t n, void *stream);
 int kcpp_add(float *y, const float *a, const float *b, int64_t n, void *stream);
 int kcpp_silu_mul(float *y, const float *g, const float *u, int64_t n, void *stream);
 
@@ -96,14 +108,17 @@ int kcpp_silu_mul(float *y, const float *g, const float *u, int64_t n, void *str
 typedef struct kcpp_hparams {
     int n_vocab, n_embd, n_head, n_head_kv, n_layer, n_ff, n_ctx;
     float eps, rope_base, rope_freq_scale;
+    int n_expert, n_expert_used;     /* 0 = dense FFN; else Mixtral-style MoE (llm_build_moe_ffn) */
 } kcpp_hparams;
 
 typedef struct kcpp_model kcpp_model;
 
 /* Layer range [il0, il1) lives on `device`; embed/output flags say whether this stage owns the
- * token embedding / output head (layer split, src/llama.cpp:7000-7036).  types[] has 3+9*n_layer
- * entries in canonical order: tok_embd, output_norm, output, then per layer attn_norm, wq, wk,
- * wv, wo, ffn_norm, ffn_gate, ffn_up, ffn_down. */
+ * token embedding / output head (layer split, src/llama.cpp:7000-7036).  types[] has 3+LW*n_layer
+ * entries (LW = 9 dense, 10 MoE) in canonical order: tok_embd, output_norm, output, then per layer
+ * attn_norm, wq, wk, wv, wo, ffn_norm, ffn_gate, ffn_up, ffn_down (, ffn_gate_inp).  With MoE the
+ * ffn_gate/up/down entries are the [K, N, n_expert] _exps tensors (n_expert consecutive [K, N]
+ * slices, synthetic tid = index * 256 + expert) and ffn_gate_inp is the F16/F32 router. */
 kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *types, int device, int il0, int il1, int has_embed,
                               int has_output, int max_ubatch);
 /* weights: synthetic (seed) or uploaded from host ggml-layout bytes (tensor index = canonical order) */

@@ -156,6 +156,9 @@ __global__ void __launch_bounds__(256) k_gemv_dec(const DecArgs a) {
     const int64_t ngroups = ntot / R;
     const int64_t nw = (int64_t)gridDim.x * 4;
     const int64_t wid = (int64_t)blockIdx.x * 4 + wave;
+    // MoE: this launch's expert slice (index read on the device, wave-uniform)
+    const int64_t eoff = a.eid ? (int64_t)__builtin_amdgcn_readfirstlane(a.eid[0]) * a.ebytes : 0;
+    const float escale = a.escale ? a.escale[0] : 1.0f;
 
     auto group_rows = [&](int64_t g, int &seg, int64_t &row0) {
         int64_t r = g * R;
@@ -174,8 +177,8 @@ __global__ void __launch_bounds__(256) k_gemv_dec(const DecArgs a) {
             if (u < upr) {
 #pragma unroll
                 for (int r = 0; r < RR; ++r) {
-                    if constexpr (MODE == 1) load_unit<TYPE>(w[it][r], r < R ? a.W[seg] : a.W2, nb, row0 + (r % R), upr, u);
-                    else load_unit<TYPE>(w[it][r], a.W[seg], nb, row0 + r, upr, u);
+                    if constexpr (MODE == 1) load_unit<TYPE>(w[it][r], (r < R ? a.W[seg] : a.W2) + eoff, nb, row0 + (r % R), upr, u);
+                    else load_unit<TYPE>(w[it][r], a.W[seg] + eoff, nb, row0 + r, upr, u);
                 }
             }
         }
@@ -189,7 +192,10 @@ __global__ void __launch_bounds__(256) k_gemv_dec(const DecArgs a) {
         float *Y = a.Y[seg];
         if constexpr (MODE == 0) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) Y[row0 + r] = a.res ? __fadd_rn(acc[r], a.res[row0 + r]) : acc[r];
+            for (int r = 0; r < R; ++r) {
+                const float v = a.escale ? __fmul_rn(acc[r], escale) : acc[r];
+                Y[row0 + r] = a.res ? __fadd_rn(v, a.res[row0 + r]) : v;
+            }
         } else if constexpr (MODE == 1) {
 #pragma unroll
             for (int r = 0; r < R; ++r) {

@@ -98,7 +98,10 @@ __device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0,
     if constexpr (MODE != 2) {
         float *Y = seg == 0 ? a.Y[0] : (seg == 1 ? a.Y[1] : a.Y[2]);
 #pragma unroll
-        for (int r = 0; r < R; ++r) Y[row0 + r] = (MODE == 0 && a.res) ? __fadd_rn(slot[r], a.res[row0 + r]) : slot[r];
+        for (int r = 0; r < R; ++r) {
+            const float v = (MODE == 0 && a.escale) ? __fmul_rn(slot[r], a.escale[0]) : slot[r];
+            Y[row0 + r] = (MODE == 0 && a.res) ? __fadd_rn(v, a.res[row0 + r]) : v;
+        }
     } else {
         const int role = seg == 0 ? a.role[0] : (seg == 1 ? a.role[1] : a.role[2]);
         const int p = a.pos[0];

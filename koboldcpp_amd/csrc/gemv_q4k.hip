@@ -96,6 +96,7 @@ __global__ void __launch_bounds__(256) k_gemv_q4k(const DecArgs a) {
     const int ngroups = (N0 + N1 + N2) / R;
     const int nw = (int)gridDim.x * 4;
     const int wid = (int)blockIdx.x * 4 + wave;
+    const int64_t eoff = a.eid ? (int64_t)__builtin_amdgcn_readfirstlane(a.eid[0]) * a.ebytes : 0;   // MoE slice
     const int abytes = K + K / 256 * 4 + K / 16 * 2;
     const ScaleSel ss = scale_sel(lane & 3);
     // per-lane byte offsets of the unit (it) inside a row: super-block (u >> 2), chunk j = lane & 3
@@ -114,10 +115,10 @@ __global__ void __launch_bounds__(256) k_gemv_q4k(const DecArgs a) {
     auto issue = [&](int g, Buf &b) {
         int seg, row0;
         group_rows(g, seg, row0);
-        const uint8_t *W = seg == 0 ? a.W[0] : (seg == 1 ? a.W[1] : a.W[2]);
+        const uint8_t *W = (seg == 0 ? a.W[0] : (seg == 1 ? a.W[1] : a.W[2])) + eoff;
 #pragma unroll
         for (int r = 0; r < RR; ++r) {
-            const uint8_t *rp = (MODE == 1 && r >= R ? a.W2 : W) + (int64_t)(row0 + (r % R)) * RB;
+            const uint8_t *rp = (MODE == 1 && r >= R ? a.W2 + eoff : W) + (int64_t)(row0 + (r % R)) * RB;
 #pragma unroll
             for (int it = 0; it < IT; ++it) {
                 const uint32_t o = unit_off(it);

@@ -74,6 +74,7 @@ __global__ void __launch_bounds__(256) k_gemv_q6k(const DecArgs a) {
     const int ngroups = (N0 + N1 + N2) / R;
     const int nw = (int)gridDim.x * 4;
     const int wid = (int)blockIdx.x * 4 + wave;
+    const int64_t eoff = a.eid ? (int64_t)__builtin_amdgcn_readfirstlane(a.eid[0]) * a.ebytes : 0;   // MoE slice
     const int abytes = K + K / 256 * 4 + K / 16 * 2;
     const int h = (lane >> 1) & 1, lq = lane & 1;
     const uint32_t oq = 64u * h + 16u * lq, oh = 128u + 32u * h + 16u * lq, os = 8u * h;
@@ -87,11 +88,11 @@ __global__ void __launch_bounds__(256) k_gemv_q6k(const DecArgs a) {
     auto issue = [&](int g, Buf &b) {
         int seg, row0;
         group_rows(g, seg, row0);
-        const uint8_t *W = seg == 0 ? a.W[0] : (seg == 1 ? a.W[1] : a.W[2]);
+        const uint8_t *W = (seg == 0 ? a.W[0] : (seg == 1 ? a.W[1] : a.W[2])) + eoff;
         const int64_t NB = (int64_t)nsb * (seg == 0 ? N0 : (seg == 1 ? N1 : N2));   // blocks of the tensor
 #pragma unroll
         for (int r = 0; r < RR; ++r) {
-            const uint8_t *T = (MODE == 1 && r >= R) ? a.W2 : W;
+            const uint8_t *T = (MODE == 1 && r >= R) ? a.W2 + eoff : W;
             const int64_t b0 = (int64_t)(row0 + (r % R)) * nsb;
             const uint8_t *qp = T + b0 * 192, *sp = T + NB * 192 + b0 * 16, *dp = T + NB * 208 + b0 * 2;
 #pragma unroll

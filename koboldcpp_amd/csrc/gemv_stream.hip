@@ -321,7 +321,7 @@ int launch_stream(const DecArgs &a, hipStream_t s) {
 extern "C" int kcpp_gemv_stream(int type, const void *args, int mode, int pro, void *stream) {
     const DecArgs &a = *(const DecArgs *)args;
     hipStream_t s = (hipStream_t)stream;
-    if (type != KT_Q4_K || a.K % 256 || a.nseg < 1 || a.nseg > 3) return -3;
+    if (type != KT_Q4_K || a.K % 256 || a.nseg < 1 || a.nseg > 3 || a.eid) return -3;
     static const int lpr_env = getenv("KCPP_STREAM_LPR") ? atoi(getenv("KCPP_STREAM_LPR")) : 0;
     const int64_t K = a.K, NC = K / 256 * 9;
     // measured (tools/stream_probe.py): only the K = 14336 quantize-prologue shape (ffn_down) beats the

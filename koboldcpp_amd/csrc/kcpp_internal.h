@@ -32,6 +32,11 @@ struct DecArgs {
     int D;
     const int32_t *pos;
     const float2 *rope_tab;
+    // mixture of experts (mul_mat_id at batch 1): W, W2 are expert 0 of [n_expert] equal slices of
+    // `ebytes`; the expert index is read on the device (eid[0]); MODE 0 scales the product by escale[0]
+    const int32_t *eid;
+    int64_t ebytes;
+    const float *escale;
 };
 extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream);
 // coalesced Q4_K variant (gemv_stream.hip); -3 = not covered

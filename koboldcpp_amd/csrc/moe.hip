@@ -1,0 +1,134 @@
+// moe.hip -- mixture-of-experts pieces around the expert mat-vecs / GEMMs (GGML_OP_MUL_MAT_ID path).
+//
+// Reference: llm_build_moe_ffn (src/llama.cpp:9416-9520) and its CUDA execution ggml_cuda_mul_mat_id
+// (ggml/src/ggml-cuda.cu:2003-2139), which copies the expert ids to the host and synchronizes on every
+// MoE mat-mul.  Here:
+//   * k_moe_route: router logits (F16 weights: the activation rounded to f16 first, as the CPU's
+//     vec_dot_f16 does; or F32), softmax (ggml_float sum), top-k by the CPU argsort's exchange order,
+//     weights normalized by their sum -- one workgroup per token, results stay on the device;
+//   * decode reads the expert id inside the expert mat-vec kernels (DecArgs.eid), so a whole token
+//     remains one hipGraph replay with no host round trip;
+//   * prefill groups tokens per expert on the host (one sync per layer, like the reference) and runs
+//     each expert as a dense GEMM over its gathered rows; k_moe_scatter writes w * out into the token's
+//     top-k slot, and k_moe_combine sums the slots in top-k order and adds the residual
+//     (ggml_add chain over the weighted experts view, then ggml_add(moe_out, ffn_inp)).
+#include "kcpp_common.h"
+#include "kcpp_internal.h"
+
+#define MOE_MAX_EXPERT 64
+
+template <int WT>
+__global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, int64_t ldx, const void *__restrict__ w,
+                                                   int K, int NE, int NU, int32_t *__restrict__ ids,
+                                                   float *__restrict__ wts) {
+    const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const float *xr = x + (int64_t)t * ldx;
+    __shared__ float s_part[4][MOE_MAX_EXPERT];
+    __shared__ float s_logit[MOE_MAX_EXPERT];
+    for (int e = 0; e < NE; ++e) {
+        float acc = 0.0f;
+        for (int i = tid; i < K; i += 256) {
+            float xv = xr[i], wv;
+            if constexpr (WT == KT_F16) {
+                xv = h2f(f2h(xv));                      // ggml converts src1 to the F16 vec_dot_type
+                wv = h2f(((const uint16_t *)w)[(int64_t)e * K + i]);
+            } else {
+                wv = ((const float *)w)[(int64_t)e * K + i];
+            }
+            acc = fmaf(xv, wv, acc);
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) s_part[wave][e] = acc;
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    float p[MOE_MAX_EXPERT];
+    float mx = -INFINITY;
+    for (int e = 0; e < NE; ++e) {
+        p[e] = (s_part[0][e] + s_part[1][e]) + (s_part[2][e] + s_part[3][e]);
+        mx = fmaxf(mx, p[e]);
+    }
+    double sum = 0.0;                                    // ggml_vec_soft_max_f32: ggml_float sum
+    for (int e = 0; e < NE; ++e) { p[e] = expf(p[e] - mx); sum += (double)p[e]; }
+    const float inv = (float)(1.0 / sum);
+    for (int e = 0; e < NE; ++e) p[e] *= inv;
+    int idx[MOE_MAX_EXPERT];
+    for (int e = 0; e < NE; ++e) idx[e] = e;
+    for (int j = 0; j < NU; ++j)                         // argsort descending (exchange order), first NU
+        for (int k = j + 1; k < NE; ++k)
+            if (p[idx[j]] < p[idx[k]]) { const int tmp = idx[j]; idx[j] = idx[k]; idx[k] = tmp; }
+    double ws = 0.0;
+    for (int j = 0; j < NU; ++j) ws += (double)p[idx[j]];
+    const float wsum = (float)ws;
+    for (int j = 0; j < NU; ++j) {
+        ids[t * NU + j] = idx[j];
+        wts[t * NU + j] = p[idx[j]] / wsum;
+    }
+}
+
+__global__ void k_moe_gather(const float *__restrict__ src, int64_t lds, const int32_t *__restrict__ rows, int n,
+                             int64_t E, float *__restrict__ dst) {
+    const int i = blockIdx.y;
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && c < E) dst[(int64_t)i * E + c] = src[(int64_t)rows[i] * lds + c];
+}
+
+__global__ void k_moe_scatter(float *__restrict__ dst, int64_t ldd, const float *__restrict__ src,
+                              const int32_t *__restrict__ rows, const float *__restrict__ w, int n, int64_t E) {
+    const int i = blockIdx.y;
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && c < E) dst[(int64_t)rows[i] * ldd + c] = __fmul_rn(src[(int64_t)i * E + c], w[i]);
+}
+
+// x[t] = ((slot0[t] + slot1[t]) + ...) + x[t]
+__global__ void k_moe_combine(float *__restrict__ x, const float *__restrict__ slots, int64_t slot_stride, int nu,
+                              int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float acc = slots[i];
+    for (int j = 1; j < nu; ++j) acc = __fadd_rn(acc, slots[j * slot_stride + i]);
+    x[i] = __fadd_rn(acc, x[i]);
+}
+
+extern "C" {
+
+int kcpp_moe_route(const float *x, int64_t ldx, const void *w_router, int wtype, int64_t K, int n_expert, int k,
+                   int32_t *ids, float *weights, int T, void *stream) {
+    if (n_expert < 1 || n_expert > MOE_MAX_EXPERT || k < 1 || k > n_expert) return -1;
+    hipStream_t s = (hipStream_t)stream;
+    if (wtype == KT_F16)
+        hipLaunchKernelGGL(k_moe_route<KT_F16>, dim3(T), dim3(256), 0, s, x, ldx, w_router, (int)K, n_expert, k, ids, weights);
+    else if (wtype == KT_F32)
+        hipLaunchKernelGGL(k_moe_route<KT_F32>, dim3(T), dim3(256), 0, s, x, ldx, w_router, (int)K, n_expert, k, ids, weights);
+    else
+        return -3;
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_moe_gather(const float *src, int64_t lds, const int32_t *rows, int n, int64_t E, float *dst, void *stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_moe_gather, dim3((unsigned)((E + 255) / 256), n), dim3(256), 0, (hipStream_t)stream, src, lds,
+                       rows, n, E, dst);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_moe_scatter(float *dst, int64_t ldd, const float *src, const int32_t *rows, const float *w, int n, int64_t E,
+                     void *stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_moe_scatter, dim3((unsigned)((E + 255) / 256), n), dim3(256), 0, (hipStream_t)stream, dst, ldd,
+                       src, rows, w, n, E);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_moe_combine(float *x, const float *slots, int64_t slot_stride, int k, int64_t n, void *stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_moe_combine, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, slots,
+                       slot_stride, k, n);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

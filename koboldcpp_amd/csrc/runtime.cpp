@@ -60,10 +60,12 @@ struct KTensor {
     void *d = nullptr;
     size_t bytes = 0;
     bool owned = true;               // false: a slice of a fused group allocation
+    int slices = 1;                  // MoE _exps tensors: n_expert consecutive [K][N] slices
+    size_t slice_bytes = 0;
 };
 
 struct KLayer {
-    KTensor t[9];   // attn_norm, wq, wk, wv, wo, ffn_norm, gate, up, down
+    KTensor t[10];  // attn_norm, wq, wk, wv, wo, ffn_norm, gate, up, down (, ffn_gate_inp for MoE)
     uint16_t *kc = nullptr, *vc = nullptr;
     // prefill fusion: same-type row-major (Q4_K/Q5_K) weights sharing one input are stored back to back,
     // so q|k(|v) and gate|up each run as ONE GEMM over the concatenated rows (one activation conversion,
@@ -88,6 +90,15 @@ struct kcpp_model {
     size_t act_sz = 0, gemm_ws_sz = 0;
     int32_t *tok_dev = nullptr, *pos_dev = nullptr, *argmax_dev = nullptr;
     void *argmax_ws = nullptr;       // ARGMAX_BLOCKS (value, index) partials
+    int32_t *moe_ids = nullptr;      // [ubatch][n_expert_used] selected experts (device)
+    float *moe_w = nullptr;          // [ubatch][n_expert_used] normalized weights (device)
+    int32_t *moe_rows = nullptr;     // prefill, grouped by expert: [ubatch*k] token rows ++ [ubatch*k] slot rows
+    float *moe_rw = nullptr;         // [ubatch*k] routing weight of each grouped entry
+    float *moe_slots = nullptr;      // [k][ubatch][n_embd] weighted expert outputs, summed in top-k order
+    int32_t *moe_ids_h = nullptr;    // pinned host copies (prefill routing)
+    float *moe_w_h = nullptr;
+    int32_t *moe_rows_h = nullptr;
+    float *moe_rw_h = nullptr;
     float2 *rope_tab = nullptr;
     int32_t *pin = nullptr;          // pinned host {token, n_past}
     float *logits_pin = nullptr;
@@ -104,12 +115,20 @@ static int64_t tensor_bytes(int type, int64_t K, int64_t N) {
     return K / ks_block_elems(type) * N * ks_block_bytes(type);
 }
 
+static int per_layer(const kcpp_hparams &hp) { return hp.n_expert > 0 ? 10 : 9; }
+static int n_tensors(const kcpp_hparams &hp) { return 3 + per_layer(hp) * hp.n_layer; }
+static int n_slices(const kcpp_hparams &hp, int idx) {
+    if (idx < 3 || hp.n_expert <= 0) return 1;
+    const int j = (idx - 3) % 10;
+    return (j >= 6 && j <= 8) ? hp.n_expert : 1;
+}
+
 static void shape_of(const kcpp_hparams &hp, int idx, int64_t &K, int64_t &N) {
     const int64_t E = hp.n_embd, F = hp.n_ff, V = hp.n_vocab, EKV = (int64_t)hp.n_head_kv * (E / hp.n_head);
     if (idx == 0) { K = E; N = V; return; }
     if (idx == 1) { K = E; N = 1; return; }
     if (idx == 2) { K = E; N = V; return; }
-    switch ((idx - 3) % 9) {
+    switch ((idx - 3) % per_layer(hp)) {
     case 0: K = E; N = 1; return;
     case 1: K = E; N = E; return;
     case 2: K = E; N = EKV; return;
@@ -118,7 +137,8 @@ static void shape_of(const kcpp_hparams &hp, int idx, int64_t &K, int64_t &N) {
     case 5: K = E; N = 1; return;
     case 6: K = E; N = F; return;
     case 7: K = E; N = F; return;
-    default: K = F; N = E; return;
+    case 8: K = F; N = E; return;
+    default: K = E; N = hp.n_expert; return;    // ffn_gate_inp (router)
     }
 }
 
@@ -126,14 +146,17 @@ static KTensor *tensor_at(kcpp_model *m, int idx) {
     if (idx == 0) return m->has_embed ? &m->tok_embd : nullptr;
     if (idx == 1) return m->has_output ? &m->output_norm : nullptr;
     if (idx == 2) return m->has_output ? &m->output : nullptr;
-    const int il = (idx - 3) / 9, j = (idx - 3) % 9;
+    const int LW = per_layer(m->hp);
+    const int il = (idx - 3) / LW, j = (idx - 3) % LW;
     if (il < m->il0 || il >= m->il1) return nullptr;
     return &m->layers[il - m->il0].t[j];
 }
 
-static int alloc_tensor(kcpp_model *m, KTensor &t, int type, int64_t K, int64_t N) {
+static int alloc_tensor(kcpp_model *m, KTensor &t, int type, int64_t K, int64_t N, int slices = 1) {
     t.type = type; t.K = K; t.N = N;
-    t.bytes = (size_t)tensor_bytes(type, K, N);
+    t.slices = slices;
+    t.slice_bytes = (size_t)tensor_bytes(type, K, N);
+    t.bytes = t.slice_bytes * slices;
     RT_CHECK(hipMalloc(&t.d, (t.bytes + 255) & ~(size_t)255));
     m->weight_bytes += t.bytes;
     return 0;
@@ -172,7 +195,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     if (hipSetDevice(device) != hipSuccess) { g_err = "hipSetDevice failed"; return nullptr; }
     kcpp_model *m = new kcpp_model();
     m->hp = *hp;
-    m->types.assign(types, types + 3 + 9 * hp->n_layer);
+    m->types.assign(types, types + n_tensors(*hp));
     m->device = device; m->il0 = il0; m->il1 = il1; m->has_embed = has_embed; m->has_output = has_output;
     m->ub = max_ubatch > 0 ? max_ubatch : 512;
     auto fail = [&](const char *what) { g_err = what; kcpp_model_free(m); return (kcpp_model *)nullptr; };
@@ -199,22 +222,22 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     };
     for (int il = il0; il < il1 && fuse_env; ++il) {
         KLayer &L = m->layers[il - il0];
-        const int b = 3 + 9 * il;
+        const int b = 3 + per_layer(*hp) * il;
         if (rowmajor(types[b + 1]) && types[b + 2] == types[b + 1]) {
             L.nqkv = types[b + 3] == types[b + 1] ? 3 : 2;
             if (alloc_group(L.qkv_base, b + 1, L.nqkv)) return fail("qkv alloc");
         }
-        if (rowmajor(types[b + 6]) && types[b + 7] == types[b + 6]) {
+        if (hp->n_expert <= 0 && rowmajor(types[b + 6]) && types[b + 7] == types[b + 6]) {
             L.glu_fused = true;
             if (alloc_group(L.glu_base, b + 6, 2)) return fail("glu alloc");
         }
     }
-    for (int idx = 0; idx < 3 + 9 * hp->n_layer; ++idx) {
+    for (int idx = 0; idx < n_tensors(*hp); ++idx) {
         KTensor *t = tensor_at(m, idx);
         if (!t || t->d) continue;
         int64_t K, N;
         shape_of(*hp, idx, K, N);
-        if (alloc_tensor(m, *t, types[idx], K, N)) return fail("weight alloc");
+        if (alloc_tensor(m, *t, types[idx], K, N, n_slices(*hp, idx))) return fail("weight alloc");
     }
     for (auto &L : m->layers) {
         const size_t kvb = (size_t)hp->n_ctx * EKV * 2;
@@ -224,9 +247,9 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     // activation buffers sized for the widest vec_dot input (K = F) at UB columns
     m->act_sz = (size_t)std::max(kcpp_act_bytes(KT_Q4_K, std::max(E, F), UB), kcpp_act_bytes(KT_Q8_0, std::max(E, F), UB));
     m->gemm_ws_sz = 0;
-    for (int idx = 0; idx < 3 + 9 * hp->n_layer; ++idx) {
+    for (int idx = 0; idx < n_tensors(*hp); ++idx) {
         int64_t K, N; shape_of(*hp, idx, K, N);
-        if (types[idx] == KT_F32) continue;
+        if (types[idx] == KT_F32 || types[idx] == KT_F16) continue;
         m->gemm_ws_sz = std::max<size_t>(m->gemm_ws_sz, (size_t)kcpp_gemm_workspace_bytes(types[idx], K, N, UB));
         // fused shapes (q|k|v: N = E + 2 EKV; gate|up: N = 2 F)
         m->gemm_ws_sz = std::max<size_t>(m->gemm_ws_sz, (size_t)kcpp_gemm_workspace_bytes(types[idx], E, E + 2 * EKV, UB));
@@ -244,6 +267,18 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
               hipHostMalloc((void **)&m->pin, 64, hipHostMallocDefault) == hipSuccess &&
               (m->gemm_ws_sz == 0 || hipMalloc(&m->gemm_ws, m->gemm_ws_sz) == hipSuccess);
     if (!ok) return fail("workspace alloc");
+    if (hp->n_expert > 0) {
+        const int NU = hp->n_expert_used;
+        if (NU < 1 || NU > hp->n_expert || hp->n_expert > 64) return fail("bad n_expert / n_expert_used");
+        if (hipMalloc(&m->moe_ids, UB * NU * 4) != hipSuccess || hipMalloc(&m->moe_w, UB * NU * 4) != hipSuccess ||
+            hipMalloc(&m->moe_rows, 2 * UB * NU * 4) != hipSuccess || hipMalloc(&m->moe_rw, UB * NU * 4) != hipSuccess ||
+            hipMalloc(&m->moe_slots, NU * UB * E * 4) != hipSuccess ||
+            hipHostMalloc((void **)&m->moe_ids_h, UB * NU * 4, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&m->moe_w_h, UB * NU * 4, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&m->moe_rows_h, 2 * UB * NU * 4, hipHostMallocDefault) != hipSuccess ||
+            hipHostMalloc((void **)&m->moe_rw_h, UB * NU * 4, hipHostMallocDefault) != hipSuccess)
+            return fail("moe workspace alloc");
+    }
     // flash-attention tickets must start at zero (the merging workgroup resets its own)
     if (hipMemset(m->fa_ws, 0, kcpp_fa_workspace_bytes(16, H, hp->n_ctx)) != hipSuccess) return fail("fa ws memset");
     if (has_output) {
@@ -268,7 +303,9 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
         for (auto &t : L.t) if (t.owned) F(t.d);
         F(L.qkv_base); F(L.glu_base); F(L.kc); F(L.vc);
     }
-    F(m->hglu);
+    F(m->hglu); F(m->moe_ids); F(m->moe_w); F(m->moe_rows); F(m->moe_rw); F(m->moe_slots);
+    for (void *p : {(void *)m->moe_ids_h, (void *)m->moe_w_h, (void *)m->moe_rows_h, (void *)m->moe_rw_h})
+        if (p) hipHostFree(p);
     F(m->x); F(m->qkv); F(m->attn); F(m->h); F(m->logits); F(m->q16); F(m->act); F(m->act2); F(m->fa_ws);
     F(m->gemm_ws); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
     if (m->pin) hipHostFree(m->pin);
@@ -279,10 +316,16 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
 
 extern "C" int kcpp_model_synth_weights(kcpp_model *m, uint64_t seed) {
     RT_CHECK(hipSetDevice(m->device));
-    for (int idx = 0; idx < 3 + 9 * m->hp.n_layer; ++idx) {
+    for (int idx = 0; idx < n_tensors(m->hp); ++idx) {
         KTensor *t = tensor_at(m, idx);
         if (!t) continue;
-        RC(kcpp_weight_synth(t->type, seed, (uint64_t)idx, t->d, t->K, t->N, m->stream));
+        if (t->slices == 1) {
+            RC(kcpp_weight_synth(t->type, seed, (uint64_t)idx, t->d, t->K, t->N, m->stream));
+        } else {                               // expert e: tid = idx * 256 + e (tests/refharness.py)
+            for (int e = 0; e < t->slices; ++e)
+                RC(kcpp_weight_synth(t->type, seed, (uint64_t)idx * 256 + e, (uint8_t *)t->d + e * t->slice_bytes, t->K,
+                                     t->N, m->stream));
+        }
     }
     RT_CHECK(hipStreamSynchronize(m->stream));
     return 0;
@@ -297,7 +340,9 @@ extern "C" int kcpp_model_set_tensor(kcpp_model *m, int idx, const void *src, in
         void *stage = nullptr;
         RT_CHECK(hipMalloc(&stage, t->bytes));
         RT_CHECK(hipMemcpyAsync(stage, src, t->bytes, hipMemcpyHostToDevice, m->stream));
-        RC(kcpp_weight_repack(t->type, stage, t->d, t->K, t->N, 0, m->stream));
+        for (int e = 0; e < t->slices; ++e)         // structure-of-arrays layout per expert slice
+            RC(kcpp_weight_repack(t->type, (uint8_t *)stage + e * t->slice_bytes, (uint8_t *)t->d + e * t->slice_bytes,
+                                  t->K, t->N, 0, m->stream));
         RT_CHECK(hipStreamSynchronize(m->stream));
         RT_CHECK(hipFree(stage));
     } else {
@@ -366,6 +411,109 @@ static int rows_per_wave(int64_t N, int mode) {
     return N > 16384 ? 4 : (N > 4096 ? 2 : 1);
 }
 
+// MoE FFN for one token (llm_build_moe_ffn, src/llama.cpp:9416-9514), entirely on the device:
+// ffn_norm -> router/softmax/top-k on the GPU (moe_ids, moe_w), then per top-k slot j the expert's
+// gate|up and down mat-vecs read their expert index from moe_ids[j] (DecArgs.eid) and down writes
+// w_j * out into slot j; the combine sums the slots in top-k order and adds the residual.
+static int moe_dec(kcpp_model *m, const KLayer &L) {
+    const kcpp_hparams &hp = m->hp;
+    const int64_t E = hp.n_embd, F = hp.n_ff;
+    const int NU = hp.n_expert_used;
+    const KTensor *t = L.t;
+    hipStream_t s = m->stream;
+    RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, 1, hp.eps, s));
+    RC(kcpp_moe_route(m->attn, E, t[9].d, t[9].type, E, hp.n_expert, NU, m->moe_ids, m->moe_w, 1, s));
+    for (int j = 0; j < NU; ++j) {
+        if (t[6].type == t[7].type) {
+            DecArgs a;
+            memset(&a, 0, sizeof a);
+            a.K = E; a.x = m->x; a.nw = (const float *)t[5].d; a.eps = hp.eps; a.nseg = 1;
+            a.W[0] = (const uint8_t *)t[6].d; a.W2 = (const uint8_t *)t[7].d; a.N[0] = F; a.Y[0] = m->h;
+            a.eid = m->moe_ids + j; a.ebytes = (int64_t)t[6].slice_bytes;
+            RC(kcpp_gemv_dec(t[6].type, &a, 1, 1, rows_per_wave(F, 1), s));
+        } else {
+            for (int i = 6; i <= 7; ++i) {
+                DecArgs a;
+                memset(&a, 0, sizeof a);
+                a.K = E; a.x = m->x; a.nw = (const float *)t[5].d; a.eps = hp.eps; a.nseg = 1;
+                a.W[0] = (const uint8_t *)t[i].d; a.N[0] = F; a.Y[0] = i == 6 ? m->h : m->qkv;
+                a.eid = m->moe_ids + j; a.ebytes = (int64_t)t[i].slice_bytes;
+                RC(kcpp_gemv_dec(t[i].type, &a, 0, 1, rows_per_wave(F, 0), s));
+            }
+            RC(kcpp_silu_mul(m->h, m->h, m->qkv, F, s));
+        }
+        DecArgs a;
+        memset(&a, 0, sizeof a);
+        a.K = F; a.x = m->h; a.nseg = 1;
+        a.W[0] = (const uint8_t *)t[8].d; a.N[0] = E; a.Y[0] = m->moe_slots + j * E;
+        a.eid = m->moe_ids + j; a.ebytes = (int64_t)t[8].slice_bytes; a.escale = m->moe_w + j;
+        const int rc = kcpp_gemv_dec(t[8].type, &a, 0, 2, rows_per_wave(E, 0), s);
+        if (rc == -8) { g_err = "MoE down projection: n_ff beyond the fused mat-vec's K budget"; return rc; }
+        RC(rc);
+    }
+    return kcpp_moe_combine(m->x, m->moe_slots, E, NU, E, s);
+}
+
+// MoE FFN for a ubatch of T tokens: routing on the GPU, one host sync to group the tokens by expert
+// (ggml_cuda_mul_mat_id does the same, ggml-cuda.cu:2003-2139), then per expert with tokens: gather
+// the normalized rows, gate|up GEMM with silu*up, down GEMM, weighted scatter into the top-k slots.
+static int moe_prefill(kcpp_model *m, const KLayer &L, int T) {
+    const kcpp_hparams &hp = m->hp;
+    const int64_t E = hp.n_embd, F = hp.n_ff, UB = m->ub;
+    const int NU = hp.n_expert_used, NE = hp.n_expert;
+    const KTensor *t = L.t;
+    hipStream_t s = m->stream;
+    RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, T, hp.eps, s));
+    RC(kcpp_moe_route(m->attn, E, t[9].d, t[9].type, E, NE, NU, m->moe_ids, m->moe_w, T, s));
+    RT_CHECK(hipMemcpyAsync(m->moe_ids_h, m->moe_ids, (size_t)T * NU * 4, hipMemcpyDeviceToHost, s));
+    RT_CHECK(hipMemcpyAsync(m->moe_w_h, m->moe_w, (size_t)T * NU * 4, hipMemcpyDeviceToHost, s));
+    RT_CHECK(hipStreamSynchronize(s));
+    int cnt[64] = {0}, off[65];
+    for (int i = 0; i < T * NU; ++i) {
+        const int e = m->moe_ids_h[i];
+        if (e < 0 || e >= NE) { g_err = "MoE router produced an invalid expert id"; return -5; }
+        ++cnt[e];
+    }
+    off[0] = 0;
+    for (int e = 0; e < NE; ++e) off[e + 1] = off[e] + cnt[e];
+    int fill[64];
+    memcpy(fill, off, sizeof fill);
+    int32_t *src_rows = m->moe_rows_h, *dst_rows = m->moe_rows_h + UB * NU;
+    for (int tk = 0; tk < T; ++tk)
+        for (int j = 0; j < NU; ++j) {
+            const int e = m->moe_ids_h[tk * NU + j], p = fill[e]++;
+            src_rows[p] = tk;
+            dst_rows[p] = j * T + tk;                        // slot j, token tk
+            m->moe_rw_h[p] = m->moe_w_h[tk * NU + j];
+        }
+    RT_CHECK(hipMemcpyAsync(m->moe_rows, m->moe_rows_h, (size_t)2 * UB * NU * 4, hipMemcpyHostToDevice, s));
+    RT_CHECK(hipMemcpyAsync(m->moe_rw, m->moe_rw_h, (size_t)T * NU * 4, hipMemcpyHostToDevice, s));
+    float *xg = m->qkv, *eo = m->hglu;
+    for (int e = 0; e < NE; ++e) {
+        const int n = cnt[e];
+        if (!n) continue;
+        RC(kcpp_moe_gather(m->attn, E, m->moe_rows + off[e], n, E, xg, s));
+        KTensor g = t[6], u = t[7], d = t[8];
+        g.d = (uint8_t *)t[6].d + e * t[6].slice_bytes;
+        u.d = (uint8_t *)t[7].d + e * t[7].slice_bytes;
+        d.d = (uint8_t *)t[8].d + e * t[8].slice_bytes;
+        RC(kcpp_quantize_act(kcpp_vec_dot_type(g.type), xg, E, m->act, E, n, s));
+        if (g.type == u.type) {
+            RC(matmul(m, g, &u, m->act, n, m->h, F, nullptr, 0, 1));           // h = silu(g) * u
+        } else {
+            RC(matmul(m, g, nullptr, m->act, n, m->h, F, nullptr, 0, 0));
+            if (kcpp_vec_dot_type(u.type) != kcpp_vec_dot_type(g.type))
+                RC(kcpp_quantize_act(kcpp_vec_dot_type(u.type), xg, E, m->act, E, n, s));
+            RC(matmul(m, u, nullptr, m->act, n, eo, F, nullptr, 0, 0));
+            RC(kcpp_silu_mul(m->h, m->h, eo, (int64_t)n * F, s));
+        }
+        RC(kcpp_quantize_act(kcpp_vec_dot_type(d.type), m->h, F, m->act2, F, n, s));
+        RC(matmul(m, d, nullptr, m->act2, n, eo, E, nullptr, 0, 0));
+        RC(kcpp_moe_scatter(m->moe_slots, E, eo, m->moe_rows + UB * NU + off[e], m->moe_rw + off[e], n, E, s));
+    }
+    return kcpp_moe_combine(m->x, m->moe_slots, (int64_t)T * E, NU, (int64_t)T * E, s);
+}
+
 // single-token layer step, 6-7 launches (gemv_dec.hip fusions); position read from m->pos_dev
 static int forward_layers_dec(kcpp_model *m) {
     const kcpp_hparams &hp = m->hp;
@@ -401,6 +549,7 @@ static int forward_layers_dec(kcpp_model *m) {
             a.W[0] = (const uint8_t *)t[4].d; a.N[0] = t[4].N; a.Y[0] = m->x; a.res = m->x;
             RC(kcpp_gemv_dec(t[4].type, &a, 0, 0, rows_per_wave(t[4].N, 0), s));
         }
+        if (hp.n_expert > 0) { RC(moe_dec(m, L)); continue; }
         // --- ffn_norm + gate|up + silu*mul
         if (t[6].type == t[7].type) {
             DecArgs a;
@@ -483,6 +632,7 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
                            (int)HKV, (int)D, n_past, posp, hp.n_ctx, kq_scale, fa_force, s));
         if (!(woq && T <= 16)) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, T, s));
         RC(matmul(m, t[4], nullptr, m->act, T, m->x, E, m->x, E, 0));                    // x += wo . attn
+        if (hp.n_expert > 0) { RC(T == 1 ? moe_dec(m, L) : moe_prefill(m, L, T)); continue; }   // T == 1: no host sync (graphs)
         const bool gq = kcpp_vec_dot_type(t[6].type) == KT_Q8_K && kcpp_vec_dot_type(t[7].type) == KT_Q8_K;
         if (gq) {
             RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, nullptr, E, m->act, E, T, hp.eps, s));

@@ -41,6 +41,10 @@ _SIGS = {
     "kcpp_flash_attn_prefill_mfma": [P, P, P, P, I, I, I, I, I, Fl, P],
     "kcpp_add": [P, P, P, I64, P],
     "kcpp_silu_mul": [P, P, P, I64, P],
+    "kcpp_moe_route": [P, I64, P, I, I64, I, I, P, P, I, P],
+    "kcpp_moe_gather": [P, I64, P, I, I64, P, P],
+    "kcpp_moe_scatter": [P, I64, P, P, P, I, I64, P],
+    "kcpp_moe_combine": [P, P, I64, I, I64, P],
     "kcpp_model_create": [P, P, I, I, I, I, I, I],
     "kcpp_model_synth_weights": [P, U64],
     "kcpp_model_set_tensor": [P, I, P, I64],
@@ -117,7 +121,7 @@ class DecArgs(ctypes.Structure):
     kcpp_gemv_dec_args_size() at import"""
     _fields_ = [("W", P * 3), ("Y", P * 3), ("N", I64 * 3), ("role", I * 3), ("nseg", I), ("W2", P), ("K", I64),
                 ("act", P), ("x", P), ("nw", P), ("eps", Fl), ("res", P), ("q16", P), ("kc", P), ("vc", P),
-                ("ekv", I64), ("D", I), ("pos", P), ("rope_tab", P)]
+                ("ekv", I64), ("D", I), ("pos", P), ("rope_tab", P), ("eid", P), ("ebytes", I64), ("escale", P)]
 
 
 if ctypes.sizeof(DecArgs) != _L.kcpp_gemv_dec_args_size():
@@ -131,12 +135,14 @@ def gemv_dec(wtype, args, mode, pro, rows_per_wave, stream):
 
 class HParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")] + \
-               [(n, ctypes.c_float) for n in ("eps", "rope_base", "rope_freq_scale")]
+               [(n, ctypes.c_float) for n in ("eps", "rope_base", "rope_freq_scale")] + \
+               [(n, ctypes.c_int) for n in ("n_expert", "n_expert_used")]
 
 
 def hparams(hp):
     return HParams(*[int(hp[n]) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")],
-                   float(hp["eps"]), float(hp["rope_base"]), float(hp.get("rope_freq_scale", 1.0)))
+                   float(hp["eps"]), float(hp["rope_base"]), float(hp.get("rope_freq_scale", 1.0)),
+                   int(hp.get("n_expert", 0)), int(hp.get("n_expert_used", 0)))
 
 
 class Model:

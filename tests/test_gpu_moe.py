@@ -1,0 +1,231 @@
+"""Mixture-of-experts FFN on the GPU (GGML_OP_MUL_MAT_ID as used by
+llm_build_moe_ffn, src/llama.cpp:9416-9514; BASELINE config 5, Mixtral-style top-2).
+
+* router kernel (kcpp_moe_route) vs a numpy restatement of the reference's router math
+  (F16 mul_mat with src1 rounded to f16, ggml_vec_soft_max_f32 with a ggml_float sum, argsort
+  descending, weights / sum_rows): ids exact, weights to fp32 summation order;
+* expert-indexed mat-vecs (DecArgs.eid / escale: the expert id read on the device) are bit-identical
+  to the same kernel run on that expert's slice, times the routing weight;
+* the whole model (TINY_MOE: 4 experts, top-2, Q5_K_M-like mix, F16 router) vs the reference graph's
+  golden logits (tests/golden/e2e_moe.npz, oracle/_ref/ref_llama) and vs the C restatement; graph
+  replay vs eager; ubatch split; fused vs unfused decode."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import refharness as R
+from test_gpu_model import TOL_MAX, TOL_MEDIAN_F32, TOL_MEDIAN_REF, oracle_forced, run_gpu, run_gpu_forced
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+    assert torch.cuda.is_available()
+    import koboldcpp_amd.lib as K
+    return torch, K
+
+
+def _route_ref(x, w, wtype, k):
+    """llm_build_moe_ffn router (src/llama.cpp:9435-9470) for one token, in the reference's precision"""
+    if wtype == R.F16:
+        lg = (x.astype(np.float16).astype(np.float64) @ w.astype(np.float64).T)
+    else:
+        lg = x.astype(np.float64) @ w.astype(np.float64).T
+    lg = lg.astype(np.float32)
+    out_ids, out_w, gaps = [], [], []
+    for p in lg:
+        e = np.exp((p - p.max()).astype(np.float32)).astype(np.float32)
+        pr = (e * np.float32(1.0 / e.astype(np.float64).sum())).astype(np.float32)
+        order = sorted(range(len(pr)), key=lambda i: (-pr[i], i))
+        sel = order[:k]
+        srt = np.sort(pr)[::-1]
+        gaps.append(srt[k - 1] - srt[k] if k < len(pr) else 1.0)
+        ws = np.float32(pr[sel].astype(np.float64).sum())
+        out_ids.append(sel)
+        out_w.append(pr[sel] / ws)
+    return np.array(out_ids), np.array(out_w, np.float32), np.array(gaps)
+
+
+@pytest.mark.parametrize("wtype", [R.F16, R.F32])
+@pytest.mark.parametrize("NE,k", [(8, 2), (4, 2), (16, 4), (64, 6)])
+def test_router_vs_restatement(env, wtype, NE, k):
+    torch, K = env
+    E, T = 512, 37
+    rng = np.random.default_rng(NE * 10 + k)
+    x = rng.standard_normal((T, E)).astype(np.float32)
+    w = (0.05 * rng.standard_normal((NE, E))).astype(np.float16 if wtype == R.F16 else np.float32)
+    xd, wd = torch.from_numpy(x).cuda(), torch.from_numpy(w.view(np.uint8).copy()).cuda()
+    ids = torch.full((T, k), -1, dtype=torch.int32, device="cuda")
+    wts = torch.zeros((T, k), device="cuda")
+    K.call("kcpp_moe_route", xd.data_ptr(), E, wd.data_ptr(), wtype, E, NE, k, ids.data_ptr(), wts.data_ptr(), T,
+           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rid, rw, gaps = _route_ref(x, w, wtype, k)
+    gid, gw = ids.cpu().numpy(), wts.cpu().numpy()
+    clear = gaps > 1e-5                          # near-ties may legitimately swap under fp32 sum order
+    assert clear.sum() > T // 2
+    np.testing.assert_array_equal(gid[clear], rid[clear])
+    np.testing.assert_allclose(gw[clear], rw[clear], rtol=2e-5, atol=1e-6)
+    np.testing.assert_allclose(gw.sum(1), 1.0, atol=1e-5)
+
+
+def test_router_rejects_bad_shapes(env):
+    torch, K = env
+    rc = K.raw().kcpp_moe_route(None, 512, None, R.F16, 512, 65, 2, None, None, 1, None)
+    assert rc != 0
+    rc = K.raw().kcpp_moe_route(None, 512, None, R.F16, 512, 8, 9, None, None, 1, None)
+    assert rc != 0
+
+
+EXPERT_CASES = [  # type, K, N, mode, pro
+    (R.Q4_K, 4096, 2048, 1, 1),      # gate|up + silu (lean Q4_K GLU kernel)
+    (R.Q5_K, 4096, 2048, 1, 1),
+    (R.Q4_K, 14336, 4096, 0, 2),     # down, quantizing the f32 input in the prologue
+    (R.Q5_K, 14336, 4096, 0, 2),
+    (R.Q6_K, 14336, 4096, 0, 2),
+    (R.Q8_0, 4096, 1024, 1, 1),
+    (R.Q4_0, 4096, 1024, 0, 2),
+]
+
+
+@pytest.mark.parametrize("case", EXPERT_CASES, ids=lambda c: "t%d_%dx%d_m%d" % c[:4])
+def test_expert_indexed_matvec_bit_identical(env, case):
+    torch, K = env
+    t, Kd, N, mode, pro = case
+    NE = 4
+    s = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(Kd, generator=g).cuda()
+    nw = (1 + 0.01 * torch.randn(Kd, generator=g)).cuda()
+    sb = K.row_bytes(t, Kd) * N
+    W = torch.empty(NE * sb, dtype=torch.uint8, device="cuda")
+    W2 = torch.empty(NE * sb, dtype=torch.uint8, device="cuda")
+    for e in range(NE):
+        K.call("kcpp_weight_synth", t, 9, 100 + e, W[e * sb:].data_ptr(), Kd, N, s)
+        K.call("kcpp_weight_synth", t, 9, 200 + e, W2[e * sb:].data_ptr(), Kd, N, s)
+    for e in (2, 0, 3):
+        eid = torch.tensor([e], dtype=torch.int32, device="cuda")
+        wt = torch.tensor([0.3125 + 0.1 * e], dtype=torch.float32, device="cuda")
+        y0 = torch.full((N,), float("nan"), device="cuda")
+        y1 = torch.full((N,), float("nan"), device="cuda")
+        a0 = K.DecArgs()
+        a1 = K.DecArgs()
+        for a, y, wp, w2p in ((a0, y0, W[e * sb:].data_ptr(), W2[e * sb:].data_ptr()),
+                              (a1, y1, W.data_ptr(), W2.data_ptr())):
+            a.K, a.nseg, a.x, a.nw, a.eps = Kd, 1, x.data_ptr(), nw.data_ptr(), 1e-5
+            a.N[0], a.Y[0], a.W[0] = N, y.data_ptr(), wp
+            if mode == 1:
+                a.W2 = w2p
+        a1.eid, a1.ebytes = eid.data_ptr(), sb
+        if mode == 0:
+            a1.escale = wt.data_ptr()
+        assert K.gemv_dec(t, a0, mode, pro, 1, s) == 0
+        assert K.gemv_dec(t, a1, mode, pro, 1, s) == 0
+        torch.cuda.synchronize()
+        ref = y0.cpu().numpy()
+        if mode == 0:
+            ref = (ref * np.float32(wt.item())).astype(np.float32)
+        got = y1.cpu().numpy()
+        assert np.isfinite(got).all()
+        assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)), (t, e, np.abs(got - ref).max())
+
+
+def test_scatter_combine_order(env):
+    """x = ((s0 + s1) + s2) + x, slots written as w * out (ggml_mul then the ggml_add chain)"""
+    torch, K = env
+    s = torch.cuda.current_stream().cuda_stream
+    T, E, k = 5, 256, 3
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((T, E)).astype(np.float32)
+    outs = rng.standard_normal((T * k, E)).astype(np.float32)
+    w = rng.random(T * k).astype(np.float32)
+    rows = rng.permutation(T * k).astype(np.int32)       # entry i -> slot row rows[i] (= j * T + t)
+    slots = torch.zeros(k * T * E, device="cuda")
+    xd = torch.from_numpy(x.copy()).cuda()
+    od, wd, rd = torch.from_numpy(outs).cuda(), torch.from_numpy(w).cuda(), torch.from_numpy(rows).cuda()
+    K.call("kcpp_moe_scatter", slots.data_ptr(), E, od.data_ptr(), rd.data_ptr(), wd.data_ptr(), T * k, E, s)
+    K.call("kcpp_moe_combine", xd.data_ptr(), slots.data_ptr(), T * E, k, T * E, s)
+    torch.cuda.synchronize()
+    sl = np.zeros((k * T, E), np.float32)
+    sl[rows] = outs * w[:, None]
+    sl = sl.reshape(k, T, E)
+    acc = sl[0].copy()
+    for j in range(1, k):
+        acc = acc + sl[j]
+    want = acc + x
+    assert np.array_equal(xd.cpu().numpy(), want)
+    # gather
+    src = torch.from_numpy(x).cuda()
+    g = torch.zeros((3, E), device="cuda")
+    idx = torch.tensor([4, 0, 2], dtype=torch.int32, device="cuda")
+    K.call("kcpp_moe_gather", src.data_ptr(), E, idx.data_ptr(), 3, E, g.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert np.array_equal(g.cpu().numpy(), x[[4, 0, 2]])
+
+
+@pytest.fixture(scope="module")
+def golden_moe():
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "e2e_moe.npz"))
+
+
+def test_moe_e2e_vs_reference_golden(env, golden_moe):
+    """teacher-forced on the reference's own greedy tokens, same bar as the dense model"""
+    torch, K = env
+    types = [int(t) for t in golden_moe["types"]]
+    prompt = golden_moe["prompt"]
+    L = golden_moe["logits"]
+    forced = golden_moe["tokens"][:-1]
+    got = run_gpu_forced(K, types, prompt, forced, hp=R.TINY_MOE)
+    d = np.abs(got - L)
+    assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_REF, (d.max(), np.median(d))
+    orc32 = oracle_forced(types, prompt, forced, True, hp=R.TINY_MOE)
+    e = np.abs(got - orc32)
+    assert np.median(e) < TOL_MEDIAN_F32 and e.max() < TOL_MAX, (np.median(e), e.max())
+
+
+@pytest.mark.parametrize("t", [R.Q4_K, R.Q8_0])
+def test_moe_e2e_vs_oracle_other_types(env, t):
+    torch, K = env
+    hp = R.TINY_MOE
+    types = R.moe_types(hp["n_layer"], t=t, router=R.F32 if t == R.Q8_0 else R.F16)
+    prompt = [int(v) for v in np.random.default_rng(7).integers(1, 500, size=45)]
+    got = run_gpu(K, types, prompt, 4, hp=hp)
+    forced = np.argmax(got, axis=1)[:-1]
+    orc32 = oracle_forced(types, prompt, forced, True, hp=hp)
+    d = np.abs(got - orc32)
+    assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_F32, (d.max(), np.median(d))
+
+
+def test_moe_graph_replay_and_ubatch(env):
+    torch, K = env
+    types = R.moe_types(R.TINY_MOE["n_layer"])
+    prompt = [int(v) for v in np.random.default_rng(2).integers(1, 500, size=150)]
+    a = run_gpu(K, types, prompt, 5, graphs=True, hp=R.TINY_MOE)
+    b = run_gpu(K, types, prompt, 5, graphs=False, hp=R.TINY_MOE)
+    assert np.array_equal(a, b)
+    c = run_gpu(K, types, prompt, 2, ub=64, hp=R.TINY_MOE)
+    np.testing.assert_allclose(a[:3], c, rtol=0, atol=TOL_MAX)
+
+
+def test_moe_fused_decode_matches_unfused(env):
+    torch, K = env
+    types = R.moe_types(R.TINY_MOE["n_layer"])
+    prompt = list(range(5, 30))
+    outs = []
+    for fused in (True, False):
+        m = K.Model(R.TINY_MOE, types)
+        m.set_fused_decode(fused)
+        m.synth(1234)
+        lg = [m.decode(prompt, 0)]
+        n = len(prompt)
+        for tok in (7, 100, 3, 250):
+            lg.append(m.decode([tok], n))
+            n += 1
+        m.close()
+        outs.append(np.array(lg))
+    d = np.abs(outs[0] - outs[1])
+    assert d.max() < TOL_MAX and np.median(d) < 1e-5, (d.max(), np.median(d))
