@@ -63,7 +63,7 @@ const char *tname(int il, int j) {
 }
 
 bool supported_type(int t) {
-    return t == KT_F32 || t == KT_Q4_0 || t == KT_Q8_0 || t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K;
+    return t == KT_F32 || t == KT_F16 || t == KT_Q4_0 || t == KT_Q8_0 || t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K;
 }
 
 // layer -> device (src/llama.cpp:7010-7036, all layers offloaded)
@@ -189,22 +189,67 @@ bool load_model(const load_model_inputs inputs) {
         fprintf(stderr, "[kcpp] load_model: need head_dim 128 (got n_embd %d / n_head %d)\n", hp.n_embd, hp.n_head);
         return false;
     }
-    // canonical tensor order: tok_embd, output_norm, output, layers x 9
-    std::vector<const gguf::Tensor *> ts(3 + 9 * hp.n_layer, nullptr);
-    ts[0] = emb;
-    ts[1] = f.tensor("output_norm.weight");
-    ts[2] = f.tensor("output.weight");
-    if (!ts[2]) ts[2] = emb;                       // tied embeddings
-    for (int il = 0; il < hp.n_layer; ++il)
-        for (int j = 0; j < 9; ++j) ts[3 + 9 * il + j] = f.tensor("blk." + std::to_string(il) + "." + tname(il, j) + ".weight");
+    // mixture of experts (llm_load_hparams / llm_load_tensors, src/llama.cpp:5444-5445, 7176-7215)
+    hp.n_expert = (int)f.get_i("llama.expert_count", 0);
+    hp.n_expert_used = (int)f.get_i("llama.expert_used_count", 0);
+    if (hp.n_expert > 0 && (hp.n_expert_used < 1 || hp.n_expert_used > hp.n_expert || hp.n_expert > 64)) {
+        fprintf(stderr, "[kcpp] load_model: unsupported expert_count %d / expert_used_count %d\n", hp.n_expert,
+                hp.n_expert_used);
+        return false;
+    }
+    const int LW = hp.n_expert > 0 ? 10 : 9;
+    // canonical tensor order: tok_embd, output_norm, output, layers x LW (+ ffn_gate_inp for MoE);
+    // MoE gate/up/down are the 3-D *_exps tensors, or the older per-expert tensors concatenated
+    struct Src { const gguf::Tensor *t = nullptr; int type = 0; int64_t bytes = 0; const uint8_t *data = nullptr; };
+    std::vector<Src> ts(3 + LW * hp.n_layer);
+    std::vector<std::vector<uint8_t>> merged;       // concatenated split experts (kept until upload)
+    merged.reserve(3 * hp.n_layer);
+    auto rbytes = [](const gguf::Tensor *t) {
+        return t->ne[0] / ks_block_elems(t->type) * ks_block_bytes(t->type) * t->ne[1] * t->ne[2] * t->ne[3];
+    };
+    auto set = [&](int k, const gguf::Tensor *t) {
+        if (t) { ts[k].t = t; ts[k].type = t->type; ts[k].bytes = rbytes(t); ts[k].data = t->data; }
+    };
+    set(0, emb);
+    set(1, f.tensor("output_norm.weight"));
+    set(2, f.tensor("output.weight"));
+    if (!ts[2].t) set(2, emb);                     // tied embeddings
+    static const char *exps[3] = {"ffn_gate_exps", "ffn_up_exps", "ffn_down_exps"};
+    static const char *exp1[3] = {"ffn_gate", "ffn_up", "ffn_down"};
+    for (int il = 0; il < hp.n_layer; ++il) {
+        const std::string b = "blk." + std::to_string(il) + ".";
+        for (int j = 0; j < 9; ++j) {
+            const int k = 3 + LW * il + j;
+            if (hp.n_expert == 0 || j < 6) { set(k, f.tensor(b + tname(il, j) + ".weight")); continue; }
+            set(k, f.tensor(b + exps[j - 6] + ".weight"));
+            if (ts[k].t) {
+                if (ts[k].t->ne[2] != hp.n_expert) { fprintf(stderr, "[kcpp] load_model: %s: expert dim\n", ts[k].t->name.c_str()); return false; }
+                continue;
+            }
+            std::vector<uint8_t> buf;                // blk.N.ffn_gate.E.weight, E = 0..n_expert-1
+            for (int x = 0; x < hp.n_expert; ++x) {
+                const gguf::Tensor *t = f.tensor(b + exp1[j - 6] + "." + std::to_string(x) + ".weight");
+                if (!t || (x > 0 && t->type != ts[k].type)) { ts[k] = Src(); break; }
+                if (x == 0) set(k, t);
+                const int64_t nb = rbytes(t);
+                buf.insert(buf.end(), t->data, t->data + nb);
+            }
+            if (ts[k].t) {
+                merged.push_back(std::move(buf));
+                ts[k].data = merged.back().data();
+                ts[k].bytes = (int64_t)merged.back().size();
+            }
+        }
+        if (LW == 10) set(3 + LW * il + 9, f.tensor(b + "ffn_gate_inp.weight"));
+    }
     e->types.resize(ts.size());
     for (size_t k = 0; k < ts.size(); ++k) {
-        if (!ts[k]) { fprintf(stderr, "[kcpp] load_model: missing tensor #%zu\n", k); return false; }
-        if (!supported_type(ts[k]->type)) {
-            fprintf(stderr, "[kcpp] load_model: tensor %s has unsupported type %d\n", ts[k]->name.c_str(), ts[k]->type);
+        if (!ts[k].t) { fprintf(stderr, "[kcpp] load_model: missing tensor #%zu\n", k); return false; }
+        if (!supported_type(ts[k].type)) {
+            fprintf(stderr, "[kcpp] load_model: tensor %s has unsupported type %d\n", ts[k].t->name.c_str(), ts[k].type);
             return false;
         }
-        e->types[k] = ts[k]->type;
+        e->types[k] = ts[k].type;
     }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) { fprintf(stderr, "[kcpp] load_model: no GPU\n"); return false; }
@@ -233,10 +278,9 @@ bool load_model(const load_model_inputs inputs) {
         if (last) break;
     }
     for (size_t k = 0; k < ts.size(); ++k) {
-        const int64_t bytes = ts[k]->ne[0] / ks_block_elems(ts[k]->type) * ks_block_bytes(ts[k]->type) * ts[k]->ne[1];
         for (kcpp_model *m : e->stages)
-            if (kcpp_model_set_tensor(m, (int)k, ts[k]->data, bytes)) {
-                fprintf(stderr, "[kcpp] load_model: upload %s: %s\n", ts[k]->name.c_str(), kcpp_last_error());
+            if (kcpp_model_set_tensor(m, (int)k, ts[k].data, ts[k].bytes)) {
+                fprintf(stderr, "[kcpp] load_model: upload %s: %s\n", ts[k].t->name.c_str(), kcpp_last_error());
                 return false;
             }
     }

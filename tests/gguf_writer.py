@@ -81,7 +81,10 @@ def spm_vocab(n_vocab, words):
 LAYER_NAMES = ["attn_norm", "attn_q", "attn_k", "attn_v", "attn_output", "ffn_norm", "ffn_gate", "ffn_up", "ffn_down"]
 
 
-def llama_gguf(path, hp, types, seed, words):
+def llama_gguf(path, hp, types, seed, words, split_experts=False):
+    """Llama GGUF with the runtime's synthetic weights.  MoE (hp["n_expert"]): gate/up/down as 3-D
+    blk.N.ffn_*_exps tensors [k, n, n_expert] plus blk.N.ffn_gate_inp, or with split_experts the older
+    per-expert blk.N.ffn_gate.E tensors (both accepted by llm_load_tensors, src/llama.cpp:7176-7215)."""
     import refharness as R
     toks, scores, ttypes = spm_vocab(hp["n_vocab"], words)
     kv = {
@@ -102,13 +105,32 @@ def llama_gguf(path, hp, types, seed, words):
         "tokenizer.ggml.bos_token_id": 1,
         "tokenizer.ggml.eos_token_id": 2,
     }
+    ne_ = int(hp.get("n_expert", 0))
+    if ne_:
+        kv["llama.expert_count"] = ne_
+        kv["llama.expert_used_count"] = int(hp["n_expert_used"])
     names = ["token_embd.weight", "output_norm.weight", "output.weight"]
     for il in range(hp["n_layer"]):
-        names += ["blk.%d.%s.weight" % (il, n) for n in LAYER_NAMES]
+        if ne_:
+            names += ["blk.%d.%s.weight" % (il, n) for n in LAYER_NAMES[:6]]
+            names += ["blk.%d.%s_exps.weight" % (il, n) for n in LAYER_NAMES[6:]]
+            names += ["blk.%d.ffn_gate_inp.weight" % il]
+        else:
+            names += ["blk.%d.%s.weight" % (il, n) for n in LAYER_NAMES]
     tensors = []
     for idx, ((k, n), t) in enumerate(zip(R.weight_shapes(hp), types)):
-        data = R.synth(t, seed, idx, k, n)
-        ne = [k] if n == 1 else [k, n]
-        tensors.append((names[idx], t, ne, np.ascontiguousarray(data).tobytes()))
+        ns = R.n_slices(hp, idx)
+        if ns == 1:
+            data = R.synth(t, seed, idx, k, n)
+            ne = [k] if n == 1 else [k, n]
+            tensors.append((names[idx], t, ne, np.ascontiguousarray(data).tobytes()))
+        elif split_experts:
+            base = names[idx].replace("_exps.weight", "")
+            for e in range(ns):
+                data = R.synth(t, seed, idx * 256 + e, k, n)
+                tensors.append(("%s.%d.weight" % (base, e), t, [k, n], np.ascontiguousarray(data).tobytes()))
+        else:
+            data = R.synth_tensor(hp, t, seed, idx)
+            tensors.append((names[idx], t, [k, n, ns], np.ascontiguousarray(data).tobytes()))
     write(path, kv, tensors)
     return toks

@@ -121,3 +121,48 @@ def test_generate_stop_sequence_and_sampling(model):
         gi.stop_sequence[0] = stop
         o = h.generate(gi)
         assert o.stopreason == 2 and o.text == full[:full.find(stop)]
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_moe_gguf_generate_matches_runtime(model, tmp_path, split):
+    """Mixtral-style GGUF (expert_count / expert_used_count, ffn_*_exps or per-expert tensors,
+    ffn_gate_inp) through load_model + greedy generate == the in-process runtime.  Runs last: it
+    replaces the module's loaded model."""
+    import koboldcpp_amd.lib as K
+    h, X, _, _, _ = model
+    hp = dict(R.TINY_MOE, n_ctx=256)
+    types = R.moe_types(hp["n_layer"])
+    path = str(tmp_path / "moe.gguf")
+    toks = GW.llama_gguf(path, hp, types, 99, WORDS, split_experts=split)
+    li = X.load_model_inputs()
+    li.model_filename = path.encode()
+    li.max_context_length = 248
+    li.blasbatchsize = 512
+    li.gpulayers = 999
+    li.rope_freq_base = 10000.0
+    li.rope_freq_scale = 1.0
+    assert h.load_model(li)
+    _, _, ttypes = GW.spm_vocab(hp["n_vocab"], WORDS)
+    prompt = b"hello world the a b of to the"
+    r = h.token_count(prompt, True)
+    ids = [r.ids[i] for i in range(r.count)]
+    gi = X.generation_inputs()
+    gi.prompt = prompt
+    gi.max_context_length = 248
+    gi.max_length = 10
+    gi.temperature = 0.0
+    gi.top_k = 1
+    gi.rep_pen = 1.0
+    gi.bypass_eos_token = True
+    out = h.generate(gi)
+    assert out.status == 1
+    m = K.Model(hp, types)
+    m.synth(99)
+    m.decode(ids, 0, want_logits=False)
+    want = [m.argmax()]
+    n = len(ids)
+    for _ in range(9):
+        want.append(m.decode_greedy(n))
+        n += 1
+    m.close()
+    assert out.text == b"".join(piece(toks, ttypes, t) for t in want)
