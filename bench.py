@@ -39,6 +39,20 @@ def weight_bytes(hp, types):
     return sum(R.row_bytes(t, k) * n for (k, n), t in zip(R.weight_shapes(hp), types))
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the newest committed PMC summary
+    (profiles/rNN_roofline_pmc.json, written by tools/profile_round.sh + tools/roofline_summary.py:
+    separate FETCH_SIZE and WRITE_SIZE passes over `bench.py --roofline-only`, FETCH_SIZE doubled per
+    the gfx950 correction).  None when no summary exists."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_roofline_pmc.json")))
+    if not fs:
+        return None, None
+    with open(fs[-1]) as f:
+        d = json.load(f)
+    return d.get("traffic_bytes_per_launch"), os.path.relpath(fs[-1], ROOT)
+
+
 def measure_roofline(K, torch, iters=48):
     """Time the dominant decode kernel as the decode path launches it: the fused Q4_K gate|up
     mat-vec with rms_norm+Q8_K prologue and SiLU-GLU epilogue (k_gemv_dec<Q4_K, mode 1, pro 1>,
@@ -77,8 +91,9 @@ def measure_roofline(K, torch, iters=48):
     ms = e0.elapsed_time(e1) / iters
     alg = 2 * wbytes + 2 * Kd * 4 + N * 4
     gbs = alg / (ms * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic()
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
             "kernel": "kcpp_gemv_dec -> k_gemv_q4k<IT1,R2,GLU,norm+quant prologue> 4096x(2x14336)", "bytes_per_launch": alg,
             "avg_us": round(ms * 1e3, 2)}
 
