@@ -104,6 +104,48 @@ int kcpp_moe_combine(float *x, const float *slots, int64_t slot_stride, int k, i
 int kcpp_add(float *y, const float *a, const float *b, int64_t n, void *stream);
 int kcpp_silu_mul(float *y, const float *g, const float *u, int64_t n, void *stream);
 
+/* ---------- 1b. general-layout ggml node kernels (the b1 backend, csrc/ggml_backend_kcpp.cpp) ----------
+ * A tensor is described by its ggml shape and byte strides (ggml_tensor.ne / .nb); data pointers are
+ * device pointers.  Each entry follows the reference CPU op named in csrc/ggml_ops.hip. */
+typedef struct kcpp_tdesc {
+    int64_t ne[4];
+    int64_t nb[4];
+} kcpp_tdesc;
+enum { KCPP_BIN_ADD = 0, KCPP_BIN_SUB = 1, KCPP_BIN_MUL = 2, KCPP_BIN_DIV = 3 };
+enum { KCPP_UN_SILU = 0, KCPP_UN_SCALE = 1, KCPP_UN_NEG = 2, KCPP_UN_RELU = 3 };
+/* d = a (op) b, b broadcast over d's shape by modulo (ggml_can_repeat) */
+int kcpp_ggml_binary(int op, const void *a, const kcpp_tdesc *ta, const void *b, const kcpp_tdesc *tb, void *d,
+                     const kcpp_tdesc *td, void *stream);
+/* d = f(a); KCPP_UN_SCALE multiplies by param */
+int kcpp_ggml_unary(int op, const void *a, const kcpp_tdesc *ta, void *d, const kcpp_tdesc *td, float param,
+                    void *stream);
+/* element-order copy with conversion (KT_F32 / KT_F16 each side); shapes may differ, counts equal */
+int kcpp_ggml_cpy(int stype, const void *src, const kcpp_tdesc *ts, int dtype, void *dst, const kcpp_tdesc *td,
+                  void *stream);
+int kcpp_ggml_rms_norm(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdesc *ty, float eps, void *stream);
+/* GGML_OP_ROPE f32, mode 0 (NORM) or 2 (NEOX); pos int32 [ne2]; freq_factors may be null */
+int kcpp_ggml_rope(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdesc *ty, const int32_t *pos,
+                   const float *freq_factors, int n_dims, int mode, int n_ctx_orig, float freq_base, float freq_scale,
+                   float ext_factor, float attn_factor, float beta_fast, float beta_slow, void *stream);
+/* softmax(x * scale + mask[row % mask_rows]) per row; mask KT_F16 / KT_F32 or null */
+int kcpp_ggml_soft_max(const void *x, const kcpp_tdesc *tx, const void *mask, int mask_type, int64_t mask_ld,
+                       int64_t mask_rows, void *y, const kcpp_tdesc *ty, float scale, void *stream);
+int kcpp_ggml_argsort(const void *x, const kcpp_tdesc *tx, int32_t *d, int64_t ld, int desc, void *stream);
+int kcpp_ggml_sum_rows(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdesc *ty, void *stream);
+/* dst[:, i10, i11, i12] = src[:, ids[i10, i11, i12], i11, i12] for KT_F32 / KT_F16 sources */
+int kcpp_ggml_get_rows(int stype, const void *src, const kcpp_tdesc *ts, const int32_t *ids, const kcpp_tdesc *ti,
+                       void *dst, const kcpp_tdesc *td, void *stream);
+/* mul_mat with a KT_F16 (src1 rounded to f16, vec_dot_f16) or KT_F32 weight, any strides, batched */
+int kcpp_ggml_mul_mat_f(int wtype, const void *w, const kcpp_tdesc *tw, const float *x, const kcpp_tdesc *tx, float *d,
+                        const kcpp_tdesc *td, void *stream);
+/* GGML_OP_FLASH_ATTN_EXT in the graph's own form: q f32 (byte strides q_nb1 per query, q_nb2 per head), K/V f16
+ * cache views [n_kv][HKV][128], optional f16 mask [T][n_kv] (row stride mask_ld; -inf keys skipped), out f32
+ * [T][H][128]; ws of kcpp_fa_ext_workspace_bytes */
+int64_t kcpp_fa_ext_workspace_bytes(int T, int H, int n_kv, int D);
+int kcpp_flash_attn_ext(const float *q, int64_t q_nb1, int64_t q_nb2, const uint16_t *kc, const uint16_t *vc,
+                        const uint16_t *mask, int64_t mask_ld, float *out, void *ws, int T, int H, int HKV, int D,
+                        int n_kv, float scale, void *stream);
+
 /* ---------- 2. Llama runtime ---------- */
 typedef struct kcpp_hparams {
     int n_vocab, n_embd, n_head, n_head_kv, n_layer, n_ff, n_ctx;

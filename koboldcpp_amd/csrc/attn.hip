@@ -32,16 +32,20 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
                                                    float2 *__restrict__ part_ml, int *__restrict__ tickets,
                                                    float *__restrict__ out, uint8_t *__restrict__ qout, int T, int H,
                                                    int HKV, int n_past_arg, const int32_t *__restrict__ n_past_dev,
-                                                   int n_chunks, float scale) {
+                                                   int n_chunks, float scale, const uint16_t *__restrict__ mask,
+                                                   int64_t mask_ld) {
     static_assert(D == 128, "head dim 128");
     const int c = blockIdx.x, hk = blockIdx.y, t = blockIdx.z;
     const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
-    if (c * FA_CHUNK > n_past + t) return;               // chunk unused by this query (graph-static grid)
-    const int nused = (n_past + t) / FA_CHUNK + 1;
+    // implicit causal window [0, n_past + t] (mask_ld < 0), or the ggml op's explicit form: all n_kv
+    // (= n_past_arg) keys under the mask (none if mask is null)
+    const int kend = mask_ld >= 0 ? n_past_arg : n_past + t + 1;   // exclusive
+    if (c * FA_CHUNK >= kend) return;                    // chunk unused by this query (graph-static grid)
+    const int nused = (kend - 1) / FA_CHUNK + 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int qpos = n_past + t;
     const int p0 = c * FA_CHUNK;
-    const int p1 = min(p0 + FA_CHUNK, qpos + 1);          // exclusive
+    const int p1 = min(p0 + FA_CHUNK, kend);              // exclusive
+    const uint16_t *mrow = mask ? mask + (int64_t)t * mask_ld : nullptr;
     const int64_t EKV = (int64_t)HKV * D;
     __shared__ float s_sc[G][FA_CHUNK];
     __shared__ float s_red[4][G][D];
@@ -68,7 +72,9 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
 #pragma unroll
     for (int i = 0; i < KPW; ++i) {
         const int p = p0 + KPW * wave + i;
-        vv[i] = p < p1 ? *(const uint32_t *)(vc + (int64_t)p * EKV + hk * D + 2 * lane) : 0u;
+        // masked keys are skipped like the CPU does (their V never enters the sum, even if not finite)
+        const bool use = p < p1 && !(mrow && mrow[p] == 0xFC00);
+        vv[i] = use ? *(const uint32_t *)(vc + (int64_t)p * EKV + hk * D + 2 * lane) : 0u;
     }
 #pragma unroll
     for (int i = 0; i < KPW / 4; ++i) {
@@ -83,7 +89,11 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
 #pragma unroll
             for (int e = 0; e < 8; ++e) sc = fmaf(qv[g][e], kf[e], sc);
             sc += dpp_f<0xB1>(sc); sc += dpp_f<0x4E>(sc); sc += dpp_f<0x141>(sc); sc += dpp_f<0x140>(sc);
-            if (sub == 0) s_sc[g][p - p0] = p < p1 ? sc * scale : -INFINITY;
+            if (sub == 0) {
+                float sv = -INFINITY;
+                if (p < p1) sv = mrow ? (mrow[p] == 0xFC00 ? -INFINITY : sc * scale + h2f(mrow[p])) : sc * scale;
+                s_sc[g][p - p0] = sv;
+            }
         }
     }
     __syncthreads();
@@ -203,7 +213,7 @@ template <bool QUANT>
 __global__ void __launch_bounds__(1024) k_fa_combine(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
                                                      float *__restrict__ out, uint8_t *__restrict__ qout, int T, int H,
                                                      int D, int n_past_arg, const int32_t *__restrict__ n_past_dev,
-                                                     int n_chunks_alloc) {
+                                                     int n_chunks_alloc, int masked) {
     constexpr int MAXCH = 4096 / FA_CHUNK * 4;         // 16k context
     const int t = blockIdx.y;
     const int pair = blockIdx.x;                       // heads 2*pair, 2*pair+1
@@ -211,7 +221,8 @@ __global__ void __launch_bounds__(1024) k_fa_combine(const float *__restrict__ p
     const int hl = tid >> 9, r = tid & 511, d = r & 127, cg = r >> 7;
     const int h = 2 * pair + hl;
     const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
-    const int nch = (n_past + t) / FA_CHUNK + 1;       // chunks this query actually used
+    const int nch = masked ? (n_past_arg - 1) / FA_CHUNK + 1    // explicit mask: all n_kv keys
+                           : (n_past + t) / FA_CHUNK + 1;     // chunks this query actually used
     __shared__ float s_w[2][MAXCH];
     __shared__ float s_red[16];
     __shared__ float s_sum[2][4][128];
@@ -289,7 +300,8 @@ __global__ void __launch_bounds__(1024) k_fa_combine(const float *__restrict__ p
 template <int D>
 __global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
                                                     const uint16_t *__restrict__ vc, float *__restrict__ out, int T,
-                                                    int H, int HKV, int n_past, float scale) {
+                                                    int H, int HKV, int n_past, float scale,
+                                                    const uint16_t *__restrict__ mask, int64_t mask_ld, int n_kv) {
     const int qt = blockIdx.x, h = blockIdx.y;
     const int G = H / HKV, hk = h / G;
     const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
@@ -310,8 +322,17 @@ __global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__
         for (int j = 0; j < 8; ++j) o[r][j] = 0.0f;
     }
     const int last_q = min(q0 + FP_BQ, T) - 1;
-    const int kend = n_past + last_q + 1;                 // keys needed by this tile (exclusive)
+    const bool expl = mask_ld >= 0;                       // explicit ggml mask form (mask may be null)
+    const int kend = expl ? n_kv : n_past + last_q + 1;   // keys needed by this tile (exclusive)
+    __shared__ int s_dead[FP_BK];
     for (int k0 = 0; k0 < kend; k0 += FP_BK) {
+        __syncthreads();
+        if (expl && mask && tid < FP_BK) {               // keys masked for every query of the tile are skipped
+            int dead = 1;                                // (their V may be anything, as on the CPU)
+            const int p = k0 + tid;
+            for (int qi = q0; qi <= last_q && dead && p < kend; ++qi) dead = mask[(int64_t)qi * mask_ld + p] == 0xFC00;
+            s_dead[tid] = dead;
+        }
         __syncthreads();
         for (int i = tid; i < FP_BK * D / 2; i += 256) {
             const int r = i / (D / 2), d2 = i % (D / 2);
@@ -319,7 +340,7 @@ __global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__
             uint32_t kk = 0, vv = 0;
             if (p < kend) {
                 kk = *(const uint32_t *)(kc + (int64_t)p * EKV + hk * D + 2 * d2);
-                vv = *(const uint32_t *)(vc + (int64_t)p * EKV + hk * D + 2 * d2);
+                if (!(expl && mask && s_dead[r])) vv = *(const uint32_t *)(vc + (int64_t)p * EKV + hk * D + 2 * d2);
             }
             sK[r][2 * d2] = h2f(kk & 0xFFFF); sK[r][2 * d2 + 1] = h2f(kk >> 16);
             sV[r][2 * d2] = h2f(vv & 0xFFFF); sV[r][2 * d2 + 1] = h2f(vv >> 16);
@@ -350,7 +371,13 @@ __global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int p = k0 + tx + 16 * j;
-                s[r][j] = (qi < T && p <= qpos) ? s[r][j] * scale : -INFINITY;
+                if (expl) {
+                    const uint16_t mv = (qi < T && p < kend) ? (mask ? mask[(int64_t)qi * mask_ld + p] : (uint16_t)0)
+                                                             : (uint16_t)0xFC00;
+                    s[r][j] = mv == 0xFC00 ? -INFINITY : s[r][j] * scale + h2f(mv);
+                } else {
+                    s[r][j] = (qi < T && p <= qpos) ? s[r][j] * scale : -INFINITY;
+                }
                 mx = fmaxf(mx, s[r][j]);
             }
             mx = fmaxf(mx, __shfl_xor(mx, 1, 64)); mx = fmaxf(mx, __shfl_xor(mx, 2, 64));
@@ -431,10 +458,10 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     case GG:                                                                                                   \
         if (fused)                                                                                             \
             hipLaunchKernelGGL((k_fa_decode<128, GG, true>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, \
-                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale);             \
+                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale, nullptr, -1); \
         else                                                                                                   \
             hipLaunchKernelGGL((k_fa_decode<128, GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, \
-                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale);             \
+                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale, nullptr, -1); \
         break;
         switch (G) {
             KCPP_FA_CASE(1)
@@ -448,10 +475,10 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
         if (!fused) {
             if (qout)
                 hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, T), dim3(1024), 0, s, po, pml, out, (uint8_t *)qout, T,
-                                   H, D, n_past, n_past_dev, nch);
+                                   H, D, n_past, n_past_dev, nch, 0);
             else
                 hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, T), dim3(1024), 0, s, po, pml, out, (uint8_t *)nullptr,
-                                   T, H, D, n_past, n_past_dev, nch);
+                                   T, H, D, n_past, n_past_dev, nch, 0);
         }
         KCPP_CHECK(hipGetLastError());
         return 0;
@@ -465,11 +492,67 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     if (rc == -3 && force_path == 3) return -3;
     if (rc == -3)
         hipLaunchKernelGGL(k_fa_prefill<128>, dim3((T + FP_BQ - 1) / FP_BQ, H), dim3(256), 0, s, q16, kc, vc, out, T, H, HKV,
-                           n_past, scale);
+                           n_past, scale, nullptr, -1, 0);
     else if (rc)
         return rc;
     KCPP_CHECK(hipGetLastError());
     if (qout) return kcpp_quantize_act(KT_Q8_K, out, (int64_t)H * D, qout, (int64_t)H * D, T, stream);
+    return 0;
+}
+
+// GGML_OP_FLASH_ATTN_EXT as the ggml graph states it (the b1 backend path): q f32 [D][T][H] with byte
+// strides (q_nb1 between queries, q_nb2 between heads), K/V f16 cache views [n_kv][HKV][D] (row stride
+// HKV*D), mask f16 [T_pad][n_kv] (row stride mask_ld elements, 0 / -inf, may be null = no mask), out f32
+// [T][H][D].  Q is rounded to f16 first (q_to_vec_dot of ggml_compute_forward_flash_attn_ext_f16,
+// ggml.c:15667); keys whose mask is -inf are skipped.  ws: kcpp_fa_workspace_bytes(T, H, n_kv) + T*H*D*2.
+int64_t kcpp_fa_ext_workspace_bytes(int T, int H, int n_kv, int D) {
+    return ((kcpp_fa_workspace_bytes(T, H, n_kv) + 255) & ~(int64_t)255) + (int64_t)T * H * D * 2 + 256;
+}
+
+__global__ void k_q_to_f16(const char *__restrict__ q, int64_t nb1, int64_t nb2, int T, int H, int D,
+                           uint16_t *__restrict__ q16) {
+    const int t = blockIdx.x, h = blockIdx.y;
+    for (int d = threadIdx.x; d < D; d += blockDim.x)
+        q16[((int64_t)t * H + h) * D + d] = f2h(((const float *)(q + t * nb1 + h * nb2))[d]);
+}
+
+int kcpp_flash_attn_ext(const float *q, int64_t q_nb1, int64_t q_nb2, const uint16_t *kc, const uint16_t *vc,
+                        const uint16_t *mask, int64_t mask_ld, float *out, void *ws, int T, int H, int HKV, int D,
+                        int n_kv, float scale, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (D != 128 || H % HKV || H / HKV > FA_MAXG || (H % 2) || n_kv < 1) return -1;
+    uint16_t *q16 = (uint16_t *)((uint8_t *)ws + ((kcpp_fa_workspace_bytes(T, H, n_kv) + 255) & ~(int64_t)255));
+    hipLaunchKernelGGL(k_q_to_f16, dim3(T, H), dim3(128), 0, s, (const char *)q, q_nb1, q_nb2, T, H, D, q16);
+    KCPP_CHECK(hipGetLastError());
+    if (mask_ld < 0) mask_ld = 0;
+    if (T <= 16) {
+        const int nch = (n_kv + FA_CHUNK - 1) / FA_CHUNK;
+        if (nch > 4096 / FA_CHUNK * 4) return -4;
+        float *po = (float *)ws;
+        float2 *pml = (float2 *)(po + (int64_t)T * H * nch * 128);
+        int *tickets = (int *)(pml + (int64_t)T * H * nch);
+        const dim3 grid(nch, HKV, T);
+#define KCPP_FA_CASE(GG)                                                                                          \
+    case GG:                                                                                                      \
+        hipLaunchKernelGGL((k_fa_decode<128, GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, \
+                           (uint8_t *)nullptr, T, H, HKV, n_kv, nullptr, nch, scale, mask, mask_ld);              \
+        break;
+        switch (H / HKV) {
+            KCPP_FA_CASE(1)
+            KCPP_FA_CASE(2)
+            KCPP_FA_CASE(4)
+            KCPP_FA_CASE(8)
+        default: return -3;
+        }
+#undef KCPP_FA_CASE
+        KCPP_CHECK(hipGetLastError());
+        hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, T), dim3(1024), 0, s, po, pml, out, (uint8_t *)nullptr, T, H,
+                           D, n_kv, nullptr, nch, 1);
+    } else {
+        hipLaunchKernelGGL(k_fa_prefill<128>, dim3((T + FP_BQ - 1) / FP_BQ, H), dim3(256), 0, s, q16, kc, vc, out, T, H,
+                           HKV, 0, scale, mask, mask_ld, n_kv);
+    }
+    KCPP_CHECK(hipGetLastError());
     return 0;
 }
 

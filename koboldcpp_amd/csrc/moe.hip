@@ -77,7 +77,10 @@ __global__ void k_moe_scatter(float *__restrict__ dst, int64_t ldd, const float 
                               const int32_t *__restrict__ rows, const float *__restrict__ w, int n, int64_t E) {
     const int i = blockIdx.y;
     const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n && c < E) dst[(int64_t)rows[i] * ldd + c] = __fmul_rn(src[(int64_t)i * E + c], w[i]);
+    if (i < n && c < E) {
+        const float v = src[(int64_t)i * E + c];
+        dst[(int64_t)rows[i] * ldd + c] = w ? __fmul_rn(v, w[i]) : v;          // w null: plain row scatter
+    }
 }
 
 // x[t] = ((slot0[t] + slot1[t]) + ...) + x[t]

@@ -45,6 +45,17 @@ _SIGS = {
     "kcpp_moe_gather": [P, I64, P, I, I64, P, P],
     "kcpp_moe_scatter": [P, I64, P, P, P, I, I64, P],
     "kcpp_moe_combine": [P, P, I64, I, I64, P],
+    "kcpp_ggml_binary": [I, P, P, P, P, P, P, P],
+    "kcpp_ggml_unary": [I, P, P, P, P, Fl, P],
+    "kcpp_ggml_cpy": [I, P, P, I, P, P, P],
+    "kcpp_ggml_rms_norm": [P, P, P, P, Fl, P],
+    "kcpp_ggml_rope": [P, P, P, P, P, P, I, I, I, Fl, Fl, Fl, Fl, Fl, Fl, P],
+    "kcpp_ggml_soft_max": [P, P, P, I, I64, I64, P, P, Fl, P],
+    "kcpp_ggml_argsort": [P, P, P, I64, I, P],
+    "kcpp_ggml_sum_rows": [P, P, P, P, P],
+    "kcpp_ggml_get_rows": [I, P, P, P, P, P, P, P],
+    "kcpp_ggml_mul_mat_f": [I, P, P, P, P, P, P, P],
+    "kcpp_flash_attn_ext": [P, I64, I64, P, P, P, I64, P, P, I, I, I, I, I, Fl, P],
     "kcpp_model_create": [P, P, I, I, I, I, I, I],
     "kcpp_model_synth_weights": [P, U64],
     "kcpp_model_set_tensor": [P, I, P, I64],
@@ -63,11 +74,12 @@ _SIGS = {
     "kcpp_model_set_fused_decode": [P, I],
     "kcpp_model_weight_bytes": [P],
 }
-_RES = {"kcpp_act_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
+_RES = {"kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
         "kcpp_model_create": P, "kcpp_model_hidden": P, "kcpp_model_stream": P, "kcpp_model_weight_bytes": I64,
         "kcpp_last_error": ctypes.c_char_p, "kcpp_model_free": None}
 _L.kcpp_act_bytes.argtypes = [I, I64, I64]
 _L.kcpp_fa_workspace_bytes.argtypes = [I, I, I]
+_L.kcpp_fa_ext_workspace_bytes.argtypes = [I, I, I, I]
 _L.kcpp_gemm_workspace_bytes.argtypes = [I, I64, I64, I64]
 _L.kcpp_vec_dot_type.argtypes = [I]
 _L.kcpp_gemv_dec.argtypes = [I, P, I, I, I, P]
@@ -114,6 +126,27 @@ def vec_dot_type(wtype):
 
 def fa_workspace_bytes(T, H, n_kv):
     return int(_L.kcpp_fa_workspace_bytes(T, H, n_kv))
+
+
+class TDesc(ctypes.Structure):
+    """struct kcpp_tdesc: ggml shape ne[4] and byte strides nb[4] (innermost first)"""
+    _fields_ = [("ne", I64 * 4), ("nb", I64 * 4)]
+
+
+def tdesc(t):
+    """kcpp_tdesc of a torch tensor (any strides): ne/nb are the reversed shape/strides, in bytes"""
+    shape, strides = list(t.shape)[::-1], [s * t.element_size() for s in t.stride()][::-1]
+    while len(shape) < 4:
+        shape.append(1)
+        strides.append(strides[-1] * shape[-2] if strides else t.element_size())
+    d = TDesc()
+    for i in range(4):
+        d.ne[i], d.nb[i] = int(shape[i]), int(strides[i])
+    return d
+
+
+def fa_ext_workspace_bytes(T, H, n_kv, D=128):
+    return int(_L.kcpp_fa_ext_workspace_bytes(T, H, n_kv, D))
 
 
 class DecArgs(ctypes.Structure):
