@@ -265,7 +265,7 @@ static int launch_dec_it(const DecArgs &a, hipStream_t s) {
         if (a.N[i] % R) return -5;
         ntot += a.N[i];
     }
-    if (a.K > 4096 * MC) return -6;
+    if (PRO != 0 && a.K > 4096 * MC) return -6;
     // 1024 workgroups for K = n_embd shapes (the output head prefers more), 512 for the K = n_ff
     // quantize-prologue shape (ffn_down: 20.6 vs 26.8 us measured)
     static const int env_blocks = getenv("KCPP_DEC_BLOCKS") ? atoi(getenv("KCPP_DEC_BLOCKS")) : 0;

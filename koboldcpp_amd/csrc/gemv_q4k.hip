@@ -142,9 +142,11 @@ __global__ void __launch_bounds__(256) k_gemv_q4k(const DecArgs a) {
         issue(g0, ba);
         cp.store(lds, abytes);
     }
-    // K = 4096: the activation unit of this lane is constant for the launch
-    ActU xr;
-    if constexpr (IT == 1) act_unit(lds, K, lane, xr);
+    // the lane's activation units (u = lane + 64 it) are the same for every row: held in registers for the
+    // whole launch (LDS re-reads at a 64-B lane stride were bank-conflict bound at K = 14336)
+    ActU xr[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) act_unit(lds, K, min(lane + 64 * it, upr - 1), xr[it]);
 
     float slot[R];
 #pragma unroll
@@ -157,12 +159,9 @@ __global__ void __launch_bounds__(256) k_gemv_q4k(const DecArgs a) {
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
             const int u0 = lane + 64 * it;
-            ActU x;
-            if constexpr (IT == 1) x = xr;
-            else act_unit(lds, K, min(u0, upr - 1), x);
 #pragma unroll
             for (int r = 0; r < RR; ++r) {
-                const float p = q4k_unit(b.h[it][r], b.q0[it][r], b.q1[it][r], x, ss);
+                const float p = q4k_unit(b.h[it][r], b.q0[it][r], b.q1[it][r], xr[it], ss);
                 acc[r] += (IT == 1 || u0 < upr) ? p : 0.0f;
             }
         }
@@ -259,6 +258,22 @@ extern "C" int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream) 
         if (mode == 0 && pro == 1) return launch_q4k<1, 2, 0, 1, 1, 1>(a, s);
         return -3;
     }
-    if (a.K == 14336 && mode == 0 && pro == 2) return launch_q4k<4, 1, 0, 2, 4, 0>(a, s);
+    static const int down_v = getenv("KCPP_Q4K_DOWN") ? atoi(getenv("KCPP_Q4K_DOWN")) : 0;
+    if (a.K == 14336 && mode == 0 && pro == 2) {
+        switch (down_v) {
+        case 1: return launch_q4k<4, 2, 0, 2, 4, 0>(a, s);
+        case 2: return launch_q4k<4, 1, 0, 2, 4, 1>(a, s);
+        case 3: return launch_q4k<4, 2, 0, 2, 4, 1>(a, s);
+        default: return launch_q4k<4, 1, 0, 2, 4, 0>(a, s);
+        }
+    }
+    if (a.K == 14336 && mode == 0 && pro == 0) {
+        switch (down_v) {
+        case 1: return launch_q4k<4, 2, 0, 0, 4, 0>(a, s);
+        case 2: return launch_q4k<4, 1, 0, 0, 4, 1>(a, s);
+        case 3: return launch_q4k<4, 2, 0, 0, 4, 1>(a, s);
+        default: return launch_q4k<4, 1, 0, 0, 4, 0>(a, s);
+        }
+    }
     return -3;
 }
