@@ -12,6 +12,7 @@
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 #define FA_CHUNK 64
@@ -201,6 +202,234 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
         int8_t *qs = (int8_t *)qout + (int64_t)t * E + sbg * 256;
         float *dp = (float *)(qout + (int64_t)T * E) + (int64_t)t * nsb + sbg;
         int16_t *bs = (int16_t *)(qout + (int64_t)T * E + (int64_t)T * nsb * 4) + (int64_t)t * (E / 16) + sbg * 16;
+        q8k_quant16(v, l16, qs, dp, bs);
+    }
+}
+
+// ---------------------------------------------------------------- decode v2: split-KV + in-launch merge
+// One token (T = 1).  Grid (NS splits, kv head), 512 threads, one workgroup per CU at NS = 32 x 8 kv heads.
+// Split sp owns keys [p0, p1) of the causal window [0, n_past]; it streams them in 128-key sub-chunks, the
+// next one's loads issued before the current one is used (wave w: keys 16w + 4i + (lane >> 4), i < 4; a 16-lane row holds one K row and one V row, 8 dims per
+// lane), keeps an online softmax per wave, merges its 4 waves in LDS and publishes (m, l, O) of its G
+// heads WRITE-THROUGH (sc1 stores), then adds to the kv head's ticket.  The split whose add comes last
+// merges all NS partials with sc1 loads (MI355X_MICROARCH.md, visibility table row 1: one lane per storing
+// workgroup adds to one unsharded counter after every storing wave's vmcnt(0) + barrier; the last adder
+// loads), writes the f32 output and the Q8_K activation of wo, and resets the ticket.  Replaces the
+// reference's flash_attn_vec_ext + flash_attn_combine_results pair (fattn-vec-f16.cuh:4-299,
+// fattn-common.cuh:523) and this file's k_fa_decode + k_fa_combine pair (two launches, 1 MB of partials).
+typedef unsigned long long fa_u64;
+__device__ __forceinline__ void st_sc1_f2(float2 *p, float2 v) {
+    __hip_atomic_store((fa_u64 *)p, ((fa_u64)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 ld_sc1_f2(const float2 *p) {
+    const fa_u64 x = __hip_atomic_load((fa_u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return make_float2(__uint_as_float((uint32_t)x), __uint_as_float((uint32_t)(x >> 32)));
+}
+
+#define FA2_NS 32
+// FA2_W waves per workgroup (16 FA2_W-key sub-chunks): 8, or 4 at G = 8 (register budget)
+template <int G, int FA2_W = (G == 8 ? 4 : 8)>
+__global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
+                                                 const uint16_t *__restrict__ vc, float *__restrict__ part_o,
+                                                 float2 *__restrict__ part_ml, unsigned *__restrict__ tickets,
+                                                 float *__restrict__ out, uint8_t *__restrict__ qout, int H, int HKV,
+                                                 int n_past_arg, const int32_t *__restrict__ n_past_dev, float scale) {
+    constexpr int D = 128;
+    const int sp = blockIdx.x, NS = gridDim.x, hk = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = lane & 15, kq = lane >> 4;
+    const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
+    const int nkv = n_past + 1;
+    const int per = ((nkv + NS - 1) / NS + 3) & ~3;
+    const int p0 = min(sp * per, nkv), p1 = min(p0 + per, nkv);
+    const int64_t EKV = (int64_t)HKV * D;
+    __shared__ float s_o[FA2_W][G][D];
+    __shared__ float s_m[FA2_W][G], s_l[FA2_W][G];
+    __shared__ int s_last;
+
+    float qv[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint4 qq = *(const uint4 *)(q16 + (int64_t)(hk * G + g) * D + sub * 8);
+        const uint32_t w4[4] = {qq.x, qq.y, qq.z, qq.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { qv[g][2 * i] = h2f(w4[i] & 0xFFFF); qv[g][2 * i + 1] = h2f(w4[i] >> 16); }
+    }
+    float m[G], l[G], acc[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        m[g] = -INFINITY; l[g] = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[g][e] = 0.0f;
+    }
+    const uint16_t *kb = kc + hk * D + sub * 8, *vb = vc + hk * D + sub * 8;
+    uint4 kk[4], vv[4];
+    auto load_kv = [&](int c0, uint4 (&kr)[4], uint4 (&vr)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int p = c0 + 16 * wave + 4 * i + kq;
+            kr[i] = p < p1 ? *(const uint4 *)(kb + (int64_t)p * EKV) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int p = c0 + 16 * wave + 4 * i + kq;
+            vr[i] = p < p1 ? *(const uint4 *)(vb + (int64_t)p * EKV) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    constexpr bool PF = true;                                       // register budget of the prefetch
+    if (PF && p0 < p1) load_kv(p0, kk, vv);
+    for (int c0 = p0; c0 < p1; c0 += 16 * FA2_W) {
+        uint4 kn[4], vn[4];
+        const bool nxt = PF && c0 + 16 * FA2_W < p1;
+        if (nxt) load_kv(c0 + 16 * FA2_W, kn, vn);
+        if (!PF) load_kv(c0, kk, vv);
+        float sc[G][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t w4[4] = {kk[i].x, kk[i].y, kk[i].z, kk[i].w};
+            float kf[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { kf[2 * e] = h2f(w4[e] & 0xFFFF); kf[2 * e + 1] = h2f(w4[e] >> 16); }
+            const bool valid = c0 + 16 * wave + 4 * i + kq < p1;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                float s = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) s = fmaf(qv[g][e], kf[e], s);
+                s += dpp_f<0xB1>(s); s += dpp_f<0x4E>(s); s += dpp_f<0x141>(s); s += dpp_f<0x140>(s);
+                sc[g][i] = valid ? s * scale : -INFINITY;
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float cm = fmaxf(fmaxf(sc[g][0], sc[g][1]), fmaxf(sc[g][2], sc[g][3]));
+            cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+            cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+            const float mn = fmaxf(m[g], cm);
+            if (mn == -INFINITY) continue;                          // nothing valid yet (wave-uniform)
+            const float alpha = m[g] == -INFINITY ? 0.0f : expf(m[g] - mn);
+            m[g] = mn;
+            float pr[4];
+            float ls = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { pr[i] = sc[g][i] == -INFINITY ? 0.0f : expf(sc[g][i] - mn); ls += pr[i]; }
+            l[g] = fmaf(l[g], alpha, ls);                           // lane-partial over its own keys
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[g][e] *= alpha;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t w4[4] = {vv[i].x, vv[i].y, vv[i].z, vv[i].w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    acc[g][2 * e] = fmaf(pr[i], h2f(w4[e] & 0xFFFF), acc[g][2 * e]);
+                    acc[g][2 * e + 1] = fmaf(pr[i], h2f(w4[e] >> 16), acc[g][2 * e + 1]);
+                }
+            }
+        }
+        if (nxt) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) { kk[i] = kn[i]; vv[i] = vn[i]; }
+        }
+    }
+    // wave merge over its 4 key rows (kq): m is wave-uniform, l and acc are per row
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        l[g] += __shfl_xor(l[g], 16, 64);
+        l[g] += __shfl_xor(l[g], 32, 64);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            acc[g][e] += __shfl_xor(acc[g][e], 16, 64);
+            acc[g][e] += __shfl_xor(acc[g][e], 32, 64);
+        }
+        if (kq == 0) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) s_o[wave][g][sub * 8 + e] = acc[g][e];
+        }
+        if (lane == 0) { s_m[wave][g] = m[g]; s_l[wave][g] = l[g]; }
+    }
+    __syncthreads();
+    // workgroup merge of the 4 waves -> this split's partial, published write-through
+    float2 *pml = part_ml + ((int64_t)hk * NS + sp) * G;
+    float *po = part_o + ((int64_t)hk * NS + sp) * G * D;
+    for (int j = tid; j < G * D / 2; j += 64 * FA2_W) {
+        const int g = (2 * j) / D, d = (2 * j) % D;
+        float M = s_m[0][g];
+#pragma unroll
+        for (int w = 1; w < FA2_W; ++w) M = fmaxf(M, s_m[w][g]);
+        float o0 = 0.0f, o1 = 0.0f;
+        if (M != -INFINITY) {
+#pragma unroll
+            for (int w = 0; w < FA2_W; ++w) {
+                const float wt = s_m[w][g] == -INFINITY ? 0.0f : expf(s_m[w][g] - M);
+                o0 = fmaf(wt, s_o[w][g][d], o0);
+                o1 = fmaf(wt, s_o[w][g][d + 1], o1);
+            }
+        }
+        st_sc1_f2((float2 *)(po + g * D + d), make_float2(o0, o1));
+    }
+    if (tid < G) {
+        const int g = tid;
+        float M = s_m[0][g];
+#pragma unroll
+        for (int w = 1; w < FA2_W; ++w) M = fmaxf(M, s_m[w][g]);
+        float L = 0.0f;
+        if (M != -INFINITY) {
+#pragma unroll
+            for (int w = 0; w < FA2_W; ++w) L = fmaf(s_m[w][g] == -INFINITY ? 0.0f : expf(s_m[w][g] - M), s_l[w][g], L);
+        }
+        st_sc1_f2(pml + g, make_float2(M, L));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(&tickets[hk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == (unsigned)(NS - 1);
+        if (s_last) __hip_atomic_store(&tickets[hk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // ---- last split of this kv head: merge the NS partials (sc1 loads only)
+    float *s_res = &s_o[0][0][0];                                  // reuse: G*D floats
+    for (int j = tid; j < G * D / 2; j += 64 * FA2_W) {
+        const int g = (2 * j) / D, d = (2 * j) % D;
+        const float2 *mlb = part_ml + (int64_t)hk * NS * G + g;
+        const float *ob = part_o + (int64_t)hk * NS * G * D + g * D + d;
+        float2 ml[FA2_NS], ov[FA2_NS];
+#pragma unroll
+        for (int s2 = 0; s2 < FA2_NS; ++s2) {
+            ml[s2] = s2 < NS ? ld_sc1_f2(mlb + s2 * G) : make_float2(-INFINITY, 0.0f);
+            ov[s2] = s2 < NS ? ld_sc1_f2((const float2 *)(ob + (int64_t)s2 * G * D)) : make_float2(0.0f, 0.0f);
+        }
+        float M = -INFINITY;
+#pragma unroll
+        for (int s2 = 0; s2 < FA2_NS; ++s2) M = fmaxf(M, ml[s2].x);
+        float L = 0.0f, o0 = 0.0f, o1 = 0.0f;
+#pragma unroll
+        for (int s2 = 0; s2 < FA2_NS; ++s2) {
+            const float wt = ml[s2].x == -INFINITY ? 0.0f : expf(ml[s2].x - M);
+            L = fmaf(wt, ml[s2].y, L);
+            o0 = fmaf(wt, ov[s2].x, o0);
+            o1 = fmaf(wt, ov[s2].y, o1);
+        }
+        const float r0 = o0 / L, r1 = o1 / L;
+        s_res[g * D + d] = r0;
+        s_res[g * D + d + 1] = r1;
+        if (out) *(float2 *)(out + (int64_t)(hk * G + g) * D + d) = make_float2(r0, r1);
+    }
+    if (qout == nullptr || G * D < 256) return;
+    __syncthreads();
+    const int nsbk = G * D / 256;
+    if (tid < nsbk * 16) {
+        const int sbl = tid >> 4, l16 = tid & 15;
+        float v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) v[k] = s_res[sbl * 256 + 16 * l16 + k];
+        const int64_t E = (int64_t)H * D, nsb = E / 256;
+        const int64_t sbg = (int64_t)hk * nsbk + sbl;
+        int8_t *qs = (int8_t *)qout + sbg * 256;
+        float *dp = (float *)(qout + E) + sbg;
+        int16_t *bs = (int16_t *)(qout + E + nsb * 4) + sbg * 16;
         q8k_quant16(v, l16, qs, dp, bs);
     }
 }
@@ -431,8 +660,10 @@ extern "C" {
 // zero before first use (allocate zeroed); the merging workgroup resets its ticket.
 int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max) {
     const int64_t nch = (n_kv_max + FA_CHUNK - 1) / FA_CHUNK;
-    return (int64_t)T * H * nch * (128 * 4 + 8) + (int64_t)T * H * 4 + 256;
+    return 256 + (int64_t)T * H * nch * (128 * 4 + 8) + (int64_t)T * H * 4 + 256;
 }
+// the first 256 B of the workspace are the decode-v2 tickets (one per kv head, zero between launches)
+#define FA_WS_TICKETS 256
 
 // out f32 [T][H][D] (may be null), qout Q8_K act [T][H*D] (may be null), ws from kcpp_fa_workspace_bytes
 // n_past_dev (optional): device-resident n_past (graph-replayable decode); then n_kv_max
@@ -442,8 +673,27 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
                     int force_path, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     if (D != 128 || H % HKV || H / HKV > FA_MAXG || (H % 2)) return -1;
-    const bool use_decode = force_path == 1 || (force_path == 0 && T <= 16);
+    const bool use_decode = force_path == 1 || force_path == 4 || (force_path == 0 && T <= 16);
+    static const int v2_env = getenv("KCPP_FA_V2") ? atoi(getenv("KCPP_FA_V2")) : 0;   // in-launch merge: slower end to end (422 vs 443 tok/s)
+    const int G0 = H / HKV;
+    if (use_decode && T == 1 && (v2_env || force_path == 4) && HKV <= 64 && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) && (qout == nullptr || G0 >= 2)) {
+        const int nkv = n_past_dev ? n_kv_max : n_past + 1;
+        const int NS = std::max(1, std::min(FA2_NS, (nkv + 127) / 128));   // >= 1 sub-chunk of 128 keys per split
+        unsigned *tickets = (unsigned *)ws;
+        float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
+        float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
+        const dim3 grid(NS, HKV);
+        switch (G0) {
+        case 1: hipLaunchKernelGGL(k_fa_dec2<1>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale); break;
+        case 2: hipLaunchKernelGGL(k_fa_dec2<2>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale); break;
+        case 4: hipLaunchKernelGGL(k_fa_dec2<4>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale); break;
+        default: hipLaunchKernelGGL(k_fa_dec2<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale); break;
+        }
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
     if (use_decode) {
+        ws = (uint8_t *)ws + FA_WS_TICKETS;
         const int nkv = n_past_dev ? n_kv_max : n_past + T;
         const int nch = (nkv + FA_CHUNK - 1) / FA_CHUNK;
         if (nch > 4096 / FA_CHUNK * 4) return -4;       // combine's chunk-weight table (16k context)
@@ -528,7 +778,7 @@ int kcpp_flash_attn_ext(const float *q, int64_t q_nb1, int64_t q_nb2, const uint
     if (T <= 16) {
         const int nch = (n_kv + FA_CHUNK - 1) / FA_CHUNK;
         if (nch > 4096 / FA_CHUNK * 4) return -4;
-        float *po = (float *)ws;
+        float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
         float2 *pml = (float2 *)(po + (int64_t)T * H * nch * 128);
         int *tickets = (int *)(pml + (int64_t)T * H * nch);
         const dim3 grid(nch, HKV, T);

@@ -22,6 +22,8 @@
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
+#include <cstdlib>
+
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f16acc __attribute__((ext_vector_type(16)));
@@ -322,6 +324,325 @@ __global__ void __launch_bounds__(256) k_gemm(const uint8_t *__restrict__ W, int
     }
 }
 
+
+__device__ __forceinline__ uint4 ldg16(const void *p) { return *(const uint4 *)p; }
+
+// ================================================================ K-quant GEMM v2 (Q4_K / Q5_K / Q6_K)
+// Same exact-integer MFMA formulation as k_gemm, restructured for throughput:
+//   * the activation operand is converted once into MFMA fragment order (k_act_frag): every wave-load
+//     of A is one contiguous 1 KiB (16 B per lane), read straight from L2 into registers, two half
+//     super-blocks in flight (the next one issued while the current one is multiplied);
+//   * the dequantized weight tile (64 rows x 256, f16 sc*q integers) is double-buffered in LDS: the
+//     raw bytes of super-block sb+1 are loaded into registers before the MFMAs of sb are issued and
+//     dequantized into the other buffer after them -- one barrier per super-block;
+//   * XCD-aware tile order: the workgroups of one token tile sit on the same XCD (blockIdx % 8 under
+//     round-robin dispatch; speed only), so each XCD's L2 holds one activation slice instead of all.
+// Epilogue per super-block: tot += dy * (d * S - dmin * Mn)  (S, Mn exact integers; CPU:
+// ggml_vec_dot_q4_K_q8_K, ggml-quants.c:7796-7859 -- same value, fp32 combination order differs).
+
+// A fragment order: af[(mt*(K/16) + s16)*64 + lane] = 8 halves of token 32mt + (lane&31),
+// k = 16 s16 + 8 (lane>>5) .. +7.  bsf[(mt*(K/256) + sb)*64 + lane] = Q8_K bsums g = 8 (lane>>5)..+7.
+__global__ void k_act_frag(const uint8_t *__restrict__ act, int64_t K, int64_t M, int64_t Mp, h8v *__restrict__ af,
+                           float *__restrict__ dy, h8v *__restrict__ bsf) {
+    const int64_t nA = Mp * K / 8, nS = (Mp / 32) * (K / 256) * 64, nD = Mp * (K / 256);
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int8_t *qs = (const int8_t *)act;
+    const float *d = (const float *)(act + M * K);
+    const int16_t *bs = (const int16_t *)(act + M * K + M * (K / 256) * 4);
+    if (i < nA) {
+        const int lane = (int)(i & 63);
+        const int64_t s16 = (i >> 6) % (K / 16), mt = (i >> 6) / (K / 16);
+        const int64_t m = 32 * mt + (lane & 31), k0 = 16 * s16 + 8 * (lane >> 5);
+        uint2 v = make_uint2(0, 0);
+        if (m < M) v = *(const uint2 *)(qs + m * K + k0);
+        const uint32_t w[2] = {v.x, v.y};
+        h8v r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r[e] = (_Float16)(int8_t)((w[e >> 2] >> (8 * (e & 3))) & 0xFF);
+        af[i] = r;
+    } else if (i < nA + nS) {
+        const int64_t j = i - nA;
+        const int lane = (int)(j & 63);
+        const int64_t sb = (j >> 6) % (K / 256), mt = (j >> 6) / (K / 256);
+        const int64_t m = 32 * mt + (lane & 31);
+        h8v r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r[e] = m < M ? (_Float16)bs[m * (K / 16) + sb * 16 + 8 * (lane >> 5) + e] : (_Float16)0;
+        bsf[j] = r;
+    } else if (i < nA + nS + nD) {
+        const int64_t j = i - nA - nS;
+        const int64_t m = j / (K / 256);
+        dy[j] = m < M ? d[j] : 0.0f;
+    }
+}
+
+template <int TYPE> struct KqRaw;
+template <> struct KqRaw<KT_Q4_K> { uint4 h, q0, q1; };
+template <> struct KqRaw<KT_Q5_K> { uint4 h, q0, q1, qh0, qh1; };
+template <> struct KqRaw<KT_Q6_K> { uint4 ql[4], qh[2]; uint32_t sc; uint32_t d; };
+
+// raw bytes of unit (row n, chunk c) of super-block sb; the kcpp layout (kcpp_common.h)
+template <int TYPE>
+__device__ __forceinline__ void kq_load(KqRaw<TYPE> &r, const uint8_t *__restrict__ W, int64_t bpr, int64_t nbt,
+                                        int64_t n, int c, int64_t sb) {
+    const int64_t b = n * bpr + sb;
+    if constexpr (TYPE == KT_Q4_K) {
+        const uint8_t *blk = W + b * 144;
+        r.h = ldg16(blk);
+        r.q0 = ldg16(blk + 16 + 32 * c);
+        r.q1 = ldg16(blk + 32 + 32 * c);
+    } else if constexpr (TYPE == KT_Q5_K) {
+        const uint8_t *blk = W + b * 176;
+        r.h = ldg16(blk);
+        r.qh0 = ldg16(blk + 16);
+        r.qh1 = ldg16(blk + 32);
+        r.q0 = ldg16(blk + 48 + 32 * c);
+        r.q1 = ldg16(blk + 64 + 32 * c);
+    } else {
+        const int hh = c >> 1, pb = 2 * (c & 1);
+        const uint8_t *q = W + b * 192;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r.ql[i] = ldg16(q + 64 * hh + 16 * i);
+        r.qh[0] = ldg16(q + 128 + 32 * hh);
+        r.qh[1] = ldg16(q + 128 + 32 * hh + 16);
+        r.sc = *(const uint32_t *)(W + nbt * 192 + b * 16 + 8 * hh + 2 * pb);
+        r.d = *(const uint16_t *)(W + nbt * 208 + b * 2);
+    }
+}
+
+template <int NB> struct KqSmem {
+    h8v bf[2][NB][2 * 16 * 64];   // [buf][plane][tile*16*64 + step*64 + lane]
+    h8v bm[2][2 * 64];            // mins fragment [buf][tile*64 + lane]
+    float wd[2][GB_N][2];         // d, dmin per row
+};
+
+// dequantize the raw unit into LDS buffer `buf` (fragment order; thread: row nl, chunk c)
+template <int TYPE, typename SM>
+__device__ __forceinline__ void kq_stage(SM &S, int buf, const KqRaw<TYPE> &r, int nl, int c) {
+    if constexpr (TYPE == KT_Q4_K || TYPE == KT_Q5_K) {
+        int s0, m0, s1, m1;
+        k4_sm(r.h, 2 * c, s0, m0);
+        k4_sm(r.h, 2 * c + 1, s1, m1);
+        const uint32_t qd[8] = {r.q0.x, r.q0.y, r.q0.z, r.q0.w, r.q1.x, r.q1.y, r.q1.z, r.q1.w};
+        uint32_t hd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if constexpr (TYPE == KT_Q5_K) {
+            hd[0] = r.qh0.x; hd[1] = r.qh0.y; hd[2] = r.qh0.z; hd[3] = r.qh0.w;
+            hd[4] = r.qh1.x; hd[5] = r.qh1.y; hd[6] = r.qh1.z; hd[7] = r.qh1.w;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t lo0 = qd[2 * i] & 0x0F0F0F0Fu, lo1 = qd[2 * i + 1] & 0x0F0F0F0Fu;
+            uint32_t hi0 = (qd[2 * i] >> 4) & 0x0F0F0F0Fu, hi1 = (qd[2 * i + 1] >> 4) & 0x0F0F0F0Fu;
+            if constexpr (TYPE == KT_Q5_K) {
+                lo0 |= ((hd[2 * i] >> (2 * c)) & 0x01010101u) << 4;
+                lo1 |= ((hd[2 * i + 1] >> (2 * c)) & 0x01010101u) << 4;
+                hi0 |= ((hd[2 * i] >> (2 * c + 1)) & 0x01010101u) << 4;
+                hi1 |= ((hd[2 * i + 1] >> (2 * c + 1)) & 0x01010101u) << 4;
+            }
+            S.bf[buf][0][bslot(nl, 64 * c + 8 * i)] = frag8(lo0, lo1, (float)s0, 0.0f);
+            S.bf[buf][0][bslot(nl, 64 * c + 32 + 8 * i)] = frag8(hi0, hi1, (float)s1, 0.0f);
+        }
+        _Float16 *bm = (_Float16 *)&S.bm[buf][(nl >> 5) * 64 + (c >> 1) * 32 + (nl & 31)] + 4 * (c & 1);
+        bm[0] = (_Float16)m0; bm[1] = (_Float16)m0; bm[2] = (_Float16)m1; bm[3] = (_Float16)m1;
+        if (c == 0) {
+            S.wd[buf][nl][0] = h2f((uint16_t)(r.h.x & 0xFFFF));
+            S.wd[buf][nl][1] = h2f((uint16_t)(r.h.x >> 16));
+        }
+    } else {
+        const int hh = c >> 1, pb = 2 * (c & 1);
+        const uint32_t qlw[16] = {r.ql[0].x, r.ql[0].y, r.ql[0].z, r.ql[0].w, r.ql[1].x, r.ql[1].y, r.ql[1].z, r.ql[1].w,
+                                  r.ql[2].x, r.ql[2].y, r.ql[2].z, r.ql[2].w, r.ql[3].x, r.ql[3].y, r.ql[3].z, r.ql[3].w};
+        const uint32_t qhw[8] = {r.qh[0].x, r.qh[0].y, r.qh[0].z, r.qh[0].w, r.qh[1].x, r.qh[1].y, r.qh[1].z, r.qh[1].w};
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+            const int p = pb + pp;
+            const int sh4 = 4 * (p >> 1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                // ql bytes 32*(p&1) + 8i .. +7 ; qh bytes 8i .. +7
+                const uint32_t l0 = qlw[8 * (p & 1) + 2 * i], l1 = qlw[8 * (p & 1) + 2 * i + 1];
+                const uint32_t h0 = qhw[2 * i], h1 = qhw[2 * i + 1];
+                const uint32_t v0 = ((l0 >> sh4) & 0x0F0F0F0Fu) | (((h0 >> (2 * p)) & 0x03030303u) << 4);
+                const uint32_t v1 = ((l1 >> sh4) & 0x0F0F0F0Fu) | (((h1 >> (2 * p)) & 0x03030303u) << 4);
+                const int scv = (int)(int8_t)((r.sc >> (8 * ((i >> 1) + 2 * pp))) & 0xFF);
+                const int shi = scv >> 3, slo = scv & 7;
+                const int k = 128 * hh + 32 * p + 8 * i;
+                S.bf[buf][0][bslot(nl, k)] = frag8_sub(v0, v1, (float)(8 * shi), 32.0f);
+                S.bf[buf][1][bslot(nl, k)] = frag8_sub(v0, v1, (float)slo, 32.0f);
+            }
+        }
+        if (c == 0) S.wd[buf][nl][0] = h2f((uint16_t)r.d);
+    }
+}
+
+// grid: (Mp / (128 TM)) * ceil(N / 64) workgroups, 256 threads; wave w: tokens [32 TM w, 32 TM (w+1)) of the
+// tile x 64 rows (TM x 2 MFMA tiles; every LDS weight fragment feeds TM MFMAs)
+template <int TYPE, int TM>
+__global__ void __launch_bounds__(256, TM == 1 ? 2 : 1) k_gemm_kq(const uint8_t *__restrict__ W, int64_t K, int64_t N,
+                                                    const h8v *__restrict__ af, const float *__restrict__ dyg,
+                                                    const h8v *__restrict__ bsf, int64_t M, int MT, float *__restrict__ Y,
+                                                    int64_t ldy, const float *res, int64_t ldr) {
+    constexpr int NB = TYPE == KT_Q6_K ? 2 : 1;
+    constexpr bool MINS = TYPE != KT_Q6_K;
+    constexpr int BM = GB_M * TM;
+    __shared__ KqSmem<NB> S;
+    __shared__ float sdy[2][BM];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 31, lh = lane >> 5;
+    // XCD-aware tile order: workgroup id -> (token tile, row tile) so that ids with equal id % 8 (one XCD
+    // under round-robin dispatch) share a token tile whenever MT divides 8
+    const int64_t id = blockIdx.x, nwg = gridDim.x;
+    int64_t mt, nt;
+    if (8 % MT == 0 && nwg % 8 == 0) {
+        const int64_t x = id & 7, j = id >> 3;
+        mt = x % MT;
+        nt = j * (8 / MT) + x / MT;
+    } else {
+        mt = id % MT;
+        nt = id / MT;
+    }
+    const int64_t n0 = nt * GB_N;
+    const int64_t m0 = mt * BM;
+    const int64_t nsb = K / 256, bpr = K / 256, nbt = bpr * N;
+    const int nl = tid >> 2, c = tid & 3;
+    const int64_t nrow = min(n0 + nl, N - 1);
+    const int64_t wt0 = (m0 >> 5) + TM * wave;                 // this wave's first 32-token tile
+    const h8v *ap = af + wt0 * (K / 16) * 64 + lane;           // token tile j: + j * (K/16) * 64
+    const h8v *bp = bsf + wt0 * nsb * 64 + lane;               // token tile j: + j * nsb * 64
+    const int64_t tstride = (K / 16) * 64;
+
+    f16acc tot[TM][2];
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { tot[j][0][i] = 0.0f; tot[j][1][i] = 0.0f; }
+
+    KqRaw<TYPE> raw;
+    kq_load<TYPE>(raw, W, bpr, nbt, nrow, c, 0);
+    float dyn[TM];
+#pragma unroll
+    for (int j = 0; j < TM; ++j) dyn[j] = dyg[(m0 + j * 128 + (tid & 127)) * nsb];
+    h8v a0[TM][8], a1[TM][8];
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+        for (int s = 0; s < 8; ++s) a0[j][s] = ap[j * tstride + s * 64];
+    kq_stage<TYPE>(S, 0, raw, nl, c);
+    if (tid < 128) {
+#pragma unroll
+        for (int j = 0; j < TM; ++j) sdy[0][j * 128 + tid] = dyn[j];
+    }
+    __syncthreads();
+
+    for (int64_t sb = 0; sb < nsb; ++sb) {
+        const int buf = (int)(sb & 1);
+        const bool more = sb + 1 < nsb;
+        if (more) {
+            kq_load<TYPE>(raw, W, bpr, nbt, nrow, c, sb + 1);
+#pragma unroll
+            for (int j = 0; j < TM; ++j) dyn[j] = dyg[(m0 + j * 128 + (tid & 127)) * nsb + sb + 1];
+        }
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int s = 0; s < 8; ++s) a1[j][s] = ap[j * tstride + (sb * 16 + 8 + s) * 64];
+        // per-token dy of this super-block for the accumulator rows of every token tile
+        float dyv[TM][16];
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = *(const float4 *)&sdy[buf][32 * (TM * wave + j) + 8 * q + 4 * lh];
+                dyv[j][4 * q] = v.x; dyv[j][4 * q + 1] = v.y; dyv[j][4 * q + 2] = v.z; dyv[j][4 * q + 3] = v.w;
+            }
+        // mins term first (tot -= dy * dmin * sum_j m_j bsum_j), so its accumulators are free before the main loop
+        if constexpr (MINS) {
+#pragma unroll
+            for (int j = 0; j < TM; ++j) {
+                const h8v am = bp[j * nsb * 64 + sb * 64];
+#pragma unroll
+                for (int tl = 0; tl < 2; ++tl) {
+                    f16acc accm;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) accm[i] = 0.0f;
+                    accm = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, S.bm[buf][tl * 64 + lane], accm, 0, 0, 0);
+                    const float dm = S.wd[buf][tl * 32 + lr][1];
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) tot[j][tl][r] = fmaf(-__fmul_rn(dyv[j][r], dm), accm[r], tot[j][tl][r]);
+                }
+            }
+        }
+        f16acc acc[TM][2];
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) { acc[j][0][i] = 0.0f; acc[j][1][i] = 0.0f; }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+#pragma unroll
+            for (int tl = 0; tl < 2; ++tl) {
+                const h8v b0 = S.bf[buf][0][(tl * 16 + s) * 64 + lane];
+#pragma unroll
+                for (int j = 0; j < TM; ++j) acc[j][tl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[j][s], b0, acc[j][tl], 0, 0, 0);
+                if constexpr (NB == 2) {
+                    const h8v b1 = S.bf[buf][1][(tl * 16 + s) * 64 + lane];
+#pragma unroll
+                    for (int j = 0; j < TM; ++j) acc[j][tl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[j][s], b1, acc[j][tl], 0, 0, 0);
+                }
+            }
+        }
+        if (more) {
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+#pragma unroll
+                for (int s = 0; s < 8; ++s) a0[j][s] = ap[j * tstride + ((sb + 1) * 16 + s) * 64];
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+#pragma unroll
+            for (int tl = 0; tl < 2; ++tl) {
+                const h8v b0 = S.bf[buf][0][(tl * 16 + 8 + s) * 64 + lane];
+#pragma unroll
+                for (int j = 0; j < TM; ++j) acc[j][tl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[j][s], b0, acc[j][tl], 0, 0, 0);
+                if constexpr (NB == 2) {
+                    const h8v b1 = S.bf[buf][1][(tl * 16 + 8 + s) * 64 + lane];
+#pragma unroll
+                    for (int j = 0; j < TM; ++j) acc[j][tl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[j][s], b1, acc[j][tl], 0, 0, 0);
+                }
+            }
+        }
+        // tot += dy * d * S
+#pragma unroll
+        for (int tl = 0; tl < 2; ++tl) {
+            const float dw = S.wd[buf][tl * 32 + lr][0];
+#pragma unroll
+            for (int j = 0; j < TM; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) tot[j][tl][r] = fmaf(dyv[j][r], __fmul_rn(dw, acc[j][tl][r]), tot[j][tl][r]);
+        }
+        if (more) {
+            kq_stage<TYPE>(S, buf ^ 1, raw, nl, c);
+            if (tid < 128) {
+#pragma unroll
+                for (int j = 0; j < TM; ++j) sdy[buf ^ 1][j * 128 + tid] = dyn[j];
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int tl = 0; tl < 2; ++tl) {
+        const int64_t n = n0 + tl * 32 + lr;
+        if (n >= N) continue;
+#pragma unroll
+        for (int j = 0; j < TM; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int64_t t = m0 + 32 * (TM * wave + j) + (r & 3) + 8 * (r >> 2) + 4 * lh;
+                if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][tl][r], res[t * ldr + n]) : tot[j][tl][r];
+            }
+    }
+}
+
 __global__ void k_silu_mul_strided(float *__restrict__ y, int64_t ldy, const float *__restrict__ u, int64_t N, int64_t M) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N * M) return;
@@ -362,6 +683,38 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     _Float16 *bs16 = (_Float16 *)(w8 + o_bs);
     float *up = (float *)(w8 + o_up);
     const int vt = vec_dot_type(type);
+    static const int v1 = getenv("KCPP_GEMM_V1") ? atoi(getenv("KCPP_GEMM_V1")) : 0;
+    if (!v1 && (type == KT_Q4_K || type == KT_Q5_K || type == KT_Q6_K)) {
+        const int64_t nth = Mp * K / 8 + (Mp / 32) * (K / 256) * 64 + Mp * (K / 256);
+        hipLaunchKernelGGL(k_act_frag, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
+                           (h8v *)a16, dy, (h8v *)bs16);
+        KCPP_CHECK(hipGetLastError());
+        static const int tm_env = getenv("KCPP_GEMM_TM") ? atoi(getenv("KCPP_GEMM_TM")) : 0;
+        const int TMv = type != KT_Q4_K ? 1 : (tm_env ? tm_env : ((Mp % 256 == 0 && N >= 8192) ? 2 : 1));
+        if (TMv == 2 && Mp % 256) return -5;
+        const int MT = (int)(Mp / (GB_M * TMv));
+        const unsigned nwg = (unsigned)(MT * ((N + GB_N - 1) / GB_N));
+        auto launch2 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
+            switch (type) {
+            case KT_Q4_K: if (TMv == 2) hipLaunchKernelGGL((k_gemm_kq<KT_Q4_K, 2>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+                else hipLaunchKernelGGL((k_gemm_kq<KT_Q4_K, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+                break;
+            case KT_Q5_K: hipLaunchKernelGGL((k_gemm_kq<KT_Q5_K, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+                break;
+            default: hipLaunchKernelGGL((k_gemm_kq<KT_Q6_K, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+                break;
+            }
+            KCPP_CHECK(hipGetLastError());
+            return 0;
+        };
+        int rc = launch2(W, Y, ldy, mode == 1 ? nullptr : res, ldr);
+        if (rc || mode != 1) return rc;
+        rc = launch2(W2, up, N, nullptr, 0);
+        if (rc) return rc;
+        hipLaunchKernelGGL(k_silu_mul_strided, dim3((unsigned)((N * M + 255) / 256)), dim3(256), 0, s, Y, ldy, up, N, M);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
     hipLaunchKernelGGL(k_act_to_f16, dim3((unsigned)((K + 1023) / 1024), (unsigned)Mp), dim3(256), 0, s,
                        (const uint8_t *)act, vt, K, M, Mp, a16, dy, bs16);
     KCPP_CHECK(hipGetLastError());

@@ -307,6 +307,35 @@ def test_flash_attn_vs_oracle_f32_accum(env, T, n_past, path):
         np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("path", [1, 4])
+@pytest.mark.parametrize("n_past", [63, 2047, 4095])
+def test_flash_attn_decode_long_ctx(env, n_past, path):
+    """decode (1: split-KV + combine; 4: v2, 32 splits x kv heads, in-launch merge) at 4k context, graph-style device n_past, vs the
+    f32-accumulation oracle; twice in a row so the self-resetting tickets are exercised."""
+    torch, K = env
+    H, HKV, D, n_ctx = 32, 8, 128, 4096
+    rng = np.random.default_rng(n_past)
+    n_kv = n_past + 1
+    kcache = (rng.standard_normal((n_ctx, HKV, D)) * 0.5).astype(np.float16)
+    vcache = rng.standard_normal((n_ctx, HKV, D)).astype(np.float16)
+    kd, vd = dev(torch, kcache), dev(torch, vcache)
+    ws = torch.zeros(K.fa_workspace_bytes(16, H, n_ctx), dtype=torch.uint8, device="cuda")
+    npd = dev(torch, np.array([n_past], np.int32))
+    for rep in range(2):
+        q = rng.standard_normal((1, H, D)).astype(np.float32)
+        q16 = dev(torch, q.astype(np.float16))
+        out = torch.empty((1, H, D), dtype=torch.float32, device="cuda")
+        K.call("kcpp_flash_attn", q16.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), None, ws.data_ptr(), 1, H,
+               HKV, D, 0, npd.data_ptr(), n_ctx, 1.0 / np.sqrt(D), path, sptr(torch))
+        got = host(torch, out, np.float32).reshape(1, H, D)
+        R.lib().orc_set_fa_f32_accum(1)
+        try:
+            want = R.flash_attn(q, kcache[:n_kv], vcache[:n_kv], np.zeros((1, n_kv), np.float16))
+        finally:
+            R.lib().orc_set_fa_f32_accum(0)
+        np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
+
+
 @pytest.mark.parametrize("t", TYPES)
 @pytest.mark.parametrize("Kd,N", [(512, 128), (512, 512), (512, 1024), (1024, 512)])
 @pytest.mark.parametrize("M", [17, 37])
