@@ -55,8 +55,8 @@ def pmc_traffic():
 
 def measure_roofline(K, torch, iters=48):
     """Time the dominant decode kernel as the decode path launches it: the fused Q4_K gate|up
-    mat-vec with rms_norm+Q8_K prologue and SiLU-GLU epilogue (k_gemv_dec<Q4_K, mode 1, pro 1>,
-    4096 -> 2 x 14336), HIP events on the launch stream.  Algorithmic bytes per launch =
+    mat-vec over the row-major decode layout with rms_norm+Q8_K prologue and SiLU-GLU epilogue
+    (kcpp_gemv_dec(Q4_K_RS, mode 1, pro 1) -> k_gemv_rs, 4096 -> 2 x 14336), HIP events on the launch stream.  Algorithmic bytes per launch =
     both weight matrices + x + norm weight + output row ("roofline")."""
     Kd, N = 4096, 14336
     wbytes = Kd // 256 * 144 * N
@@ -67,8 +67,8 @@ def measure_roofline(K, torch, iters=48):
     for i in range(4):
         a = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
         b = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
-        K.call("kcpp_weight_synth", 12, 1, 10 + 2 * i, a.data_ptr(), Kd, N, sp)
-        K.call("kcpp_weight_synth", 12, 1, 11 + 2 * i, b.data_ptr(), Kd, N, sp)
+        K.call("kcpp_weight_synth", K.Q4_K_RS, 1, 10 + 2 * i, a.data_ptr(), Kd, N, sp)
+        K.call("kcpp_weight_synth", K.Q4_K_RS, 1, 11 + 2 * i, b.data_ptr(), Kd, N, sp)
         ws.append((a, b))
     x = torch.randn(Kd, device="cuda")
     nw = torch.ones(Kd, device="cuda")
@@ -80,12 +80,12 @@ def measure_roofline(K, torch, iters=48):
         d.W[0], d.W2, d.N[0], d.Y[0] = a.data_ptr(), b.data_ptr(), N, y.data_ptr()
         args.append(d)
     for i in range(8):
-        assert K.gemv_dec(12, args[i % 4], 1, 1, 1, sp) == 0
+        assert K.gemv_dec(K.Q4_K_RS, args[i % 4], 1, 1, 1, sp) == 0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record(s)
     for i in range(iters):
-        K.gemv_dec(12, args[i % 4], 1, 1, 1, sp)
+        K.gemv_dec(K.Q4_K_RS, args[i % 4], 1, 1, 1, sp)
     e1.record(s)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
@@ -94,7 +94,7 @@ def measure_roofline(K, torch, iters=48):
     traffic, tsrc = pmc_traffic()
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-            "kernel": "kcpp_gemv_dec -> k_gemv_q4k<IT1,R2,GLU,norm+quant prologue> 4096x(2x14336)", "bytes_per_launch": alg,
+            "kernel": "kcpp_gemv_dec -> k_gemv_rs<Q4_K_RS,NI2,R1,GLU,norm+quant prologue,PF> 4096x(2x14336)", "bytes_per_launch": alg,
             "avg_us": round(ms * 1e3, 2)}
 
 

@@ -70,6 +70,11 @@ int kcpp_gemv_stream(int type, const void *args, int mode, int pro, void *stream
 int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream);
 /* the VALU-lean Q6_K variant (koboldcpp_amd/csrc/gemv_q6k.hip), tried first for Q6_K; -3 when not covered */
 int kcpp_gemv_q6k(const void *args, int mode, int pro, void *stream);
+/* single-token mat-vec over the row-major decode layouts KT_Q4_K_RS / KT_Q6_K_RS (type ids 112 / 114,
+ * koboldcpp_amd/csrc/gemv_rs.hip); kcpp_gemv_dec dispatches these types here.  kcpp_rs_supported(type, K)
+ * says whether a [K x N] weight of Q4_K / Q6_K (or its RS id) can be held in the RS layout. */
+int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
+int kcpp_rs_supported(int type, int64_t K);
 
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,

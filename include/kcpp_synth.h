@@ -29,8 +29,17 @@
 enum kcpp_type {
     KT_F32 = 0, KT_F16 = 1, KT_Q4_0 = 2, KT_Q4_1 = 3, KT_Q5_0 = 6, KT_Q5_1 = 7,
     KT_Q8_0 = 8, KT_Q8_1 = 9, KT_Q2_K = 10, KT_Q3_K = 11, KT_Q4_K = 12,
-    KT_Q5_K = 13, KT_Q6_K = 14, KT_Q8_K = 15, KT_BF16 = 30
+    KT_Q5_K = 13, KT_Q6_K = 14, KT_Q8_K = 15, KT_BF16 = 30,
+    /* GPU-internal row-major decode layouts of Q4_K / Q6_K (same bytes per row, re-arranged inside
+       each row so the single-token mat-vec reads 1 KiB-contiguous wave loads; csrc/kcpp_common.h).
+       Not ggml ids: they never leave the device library. */
+    KT_Q4_K_RS = 112, KT_Q6_K_RS = 114
 };
+
+/* the ggml type whose blocks a layout holds */
+KS_FN int ks_base_type(int type) {
+    return type == KT_Q4_K_RS ? KT_Q4_K : (type == KT_Q6_K_RS ? KT_Q6_K : type);
+}
 
 KS_FN uint64_t ks_mix(uint64_t z) {          /* splitmix64 finalizer */
     z += 0x9E3779B97F4A7C15ull;
@@ -80,9 +89,9 @@ KS_FN int ks_block_bytes(int type) {
         case KT_F16: return 2;
         case KT_Q4_0: return 18;
         case KT_Q8_0: return 34;
-        case KT_Q4_K: return 144;
+        case KT_Q4_K: case KT_Q4_K_RS: return 144;
         case KT_Q5_K: return 176;
-        case KT_Q6_K: return 210;
+        case KT_Q6_K: case KT_Q6_K_RS: return 210;
         case KT_Q8_K: return 292;
         default: return 0;
     }
@@ -90,6 +99,7 @@ KS_FN int ks_block_bytes(int type) {
 
 /* Fill one block (ggml on-disk layout) of tensor `tid` at block index `b`. */
 KS_FN void ks_fill_block(int type, uint64_t seed, uint64_t tid, uint64_t b, uint8_t *dst) {
+    type = ks_base_type(type);
     uint64_t base = ks_mix(seed ^ (tid * 0xD1B54A32D192ED03ull)) ^ (b * 0x9E3779B97F4A7C15ull);
     int nb = ks_block_bytes(type);
     /* random payload, 8 bytes per hash */

@@ -381,12 +381,34 @@ template <> struct KqRaw<KT_Q4_K> { uint4 h, q0, q1; };
 template <> struct KqRaw<KT_Q5_K> { uint4 h, q0, q1, qh0, qh1; };
 template <> struct KqRaw<KT_Q6_K> { uint4 ql[4], qh[2]; uint32_t sc; uint32_t d; };
 
-// raw bytes of unit (row n, chunk c) of super-block sb; the kcpp layout (kcpp_common.h)
-template <int TYPE>
+// raw bytes of unit (row n, chunk c) of super-block sb; LAY 0: the kcpp layout, 1: the row-major decode
+// layouts KT_Q4_K_RS / KT_Q6_K_RS (kcpp_common.h; same raw unit, gathered from the row's planes)
+template <int TYPE, int LAY>
 __device__ __forceinline__ void kq_load(KqRaw<TYPE> &r, const uint8_t *__restrict__ W, int64_t bpr, int64_t nbt,
                                         int64_t n, int c, int64_t sb) {
     const int64_t b = n * bpr + sb;
-    if constexpr (TYPE == KT_Q4_K) {
+    if constexpr (LAY == 1 && TYPE == KT_Q4_K) {
+        const uint8_t *row = W + n * 144 * bpr;
+        r.h = ldg16(row + 16 * sb);
+        r.q0 = ldg16(row + 16 * bpr + 128 * sb + 32 * c);
+        r.q1 = ldg16(row + 16 * bpr + 128 * sb + 32 * c + 16);
+    } else if constexpr (LAY == 1 && TYPE == KT_Q6_K) {
+        const int hh = c >> 1, pb = 2 * (c & 1);
+        const uint8_t *row = W + n * 210 * bpr;
+        const int64_t U0 = 4 * sb + 2 * hh;                     // units (hh, lh = 0) and (hh, lh = 1)
+        r.ql[0] = ldg16(row + 16 * U0);
+        r.ql[1] = ldg16(row + 16 * U0 + 16);
+        r.ql[2] = ldg16(row + 64 * bpr + 16 * U0);
+        r.ql[3] = ldg16(row + 64 * bpr + 16 * U0 + 16);
+        r.qh[0] = ldg16(row + 128 * bpr + 16 * U0);
+        r.qh[1] = ldg16(row + 128 * bpr + 16 * U0 + 16);
+        // unit (hh, lh) holds sc[8 hh + lh + 2 g], g = 0..3; the stage wants sc[8 hh + pb + 0..3]
+        const uint32_t s0 = *(const uint32_t *)(row + 192 * bpr + 4 * U0), s1 = *(const uint32_t *)(row + 192 * bpr + 4 * U0 + 4);
+        const int k0 = pb / 2 * 2;
+        r.sc = ((s0 >> (8 * k0)) & 0xFF) | (((s1 >> (8 * k0)) & 0xFF) << 8) | (((s0 >> (8 * k0 + 8)) & 0xFF) << 16) |
+               (((s1 >> (8 * k0 + 8)) & 0xFF) << 24);
+        r.d = *(const uint16_t *)(row + 208 * bpr + 2 * sb);
+    } else if constexpr (TYPE == KT_Q4_K) {
         const uint8_t *blk = W + b * 144;
         r.h = ldg16(blk);
         r.q0 = ldg16(blk + 16 + 32 * c);
@@ -477,7 +499,7 @@ __device__ __forceinline__ void kq_stage(SM &S, int buf, const KqRaw<TYPE> &r, i
 
 // grid: (Mp / (128 TM)) * ceil(N / 64) workgroups, 256 threads; wave w: tokens [32 TM w, 32 TM (w+1)) of the
 // tile x 64 rows (TM x 2 MFMA tiles; every LDS weight fragment feeds TM MFMAs)
-template <int TYPE, int TM>
+template <int TYPE, int TM, int LAY>
 __global__ void __launch_bounds__(256, TM == 1 ? 2 : 1) k_gemm_kq(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                                     const h8v *__restrict__ af, const float *__restrict__ dyg,
                                                     const h8v *__restrict__ bsf, int64_t M, int MT, float *__restrict__ Y,
@@ -518,7 +540,7 @@ __global__ void __launch_bounds__(256, TM == 1 ? 2 : 1) k_gemm_kq(const uint8_t 
         for (int i = 0; i < 16; ++i) { tot[j][0][i] = 0.0f; tot[j][1][i] = 0.0f; }
 
     KqRaw<TYPE> raw;
-    kq_load<TYPE>(raw, W, bpr, nbt, nrow, c, 0);
+    kq_load<TYPE, LAY>(raw, W, bpr, nbt, nrow, c, 0);
     float dyn[TM];
 #pragma unroll
     for (int j = 0; j < TM; ++j) dyn[j] = dyg[(m0 + j * 128 + (tid & 127)) * nsb];
@@ -538,7 +560,7 @@ __global__ void __launch_bounds__(256, TM == 1 ? 2 : 1) k_gemm_kq(const uint8_t 
         const int buf = (int)(sb & 1);
         const bool more = sb + 1 < nsb;
         if (more) {
-            kq_load<TYPE>(raw, W, bpr, nbt, nrow, c, sb + 1);
+            kq_load<TYPE, LAY>(raw, W, bpr, nbt, nrow, c, sb + 1);
 #pragma unroll
             for (int j = 0; j < TM; ++j) dyn[j] = dyg[(m0 + j * 128 + (tid & 127)) * nsb + sb + 1];
         }
@@ -684,24 +706,30 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     float *up = (float *)(w8 + o_up);
     const int vt = vec_dot_type(type);
     static const int v1 = getenv("KCPP_GEMM_V1") ? atoi(getenv("KCPP_GEMM_V1")) : 0;
-    if (!v1 && (type == KT_Q4_K || type == KT_Q5_K || type == KT_Q6_K)) {
+    const bool rs = type == KT_Q4_K_RS || type == KT_Q6_K_RS;       // decode layouts: v2 only
+    if (rs || (!v1 && (type == KT_Q4_K || type == KT_Q5_K || type == KT_Q6_K))) {
         const int64_t nth = Mp * K / 8 + (Mp / 32) * (K / 256) * 64 + Mp * (K / 256);
         hipLaunchKernelGGL(k_act_frag, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
                            (h8v *)a16, dy, (h8v *)bs16);
         KCPP_CHECK(hipGetLastError());
         static const int tm_env = getenv("KCPP_GEMM_TM") ? atoi(getenv("KCPP_GEMM_TM")) : 0;
-        const int TMv = type != KT_Q4_K ? 1 : (tm_env ? tm_env : ((Mp % 256 == 0 && N >= 8192) ? 2 : 1));
+        const int TMv = (type != KT_Q4_K && type != KT_Q4_K_RS) ? 1 : (tm_env ? tm_env : ((Mp % 256 == 0 && N >= 8192) ? 2 : 1));
         if (TMv == 2 && Mp % 256) return -5;
         const int MT = (int)(Mp / (GB_M * TMv));
         const unsigned nwg = (unsigned)(MT * ((N + GB_N - 1) / GB_N));
         auto launch2 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
             switch (type) {
-            case KT_Q4_K: if (TMv == 2) hipLaunchKernelGGL((k_gemm_kq<KT_Q4_K, 2>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
-                else hipLaunchKernelGGL((k_gemm_kq<KT_Q4_K, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+            case KT_Q4_K: if (TMv == 2) hipLaunchKernelGGL((k_gemm_kq<KT_Q4_K, 2, 0>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+                else hipLaunchKernelGGL((k_gemm_kq<KT_Q4_K, 1, 0>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
                 break;
-            case KT_Q5_K: hipLaunchKernelGGL((k_gemm_kq<KT_Q5_K, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+            case KT_Q5_K: hipLaunchKernelGGL((k_gemm_kq<KT_Q5_K, 1, 0>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
                 break;
-            default: hipLaunchKernelGGL((k_gemm_kq<KT_Q6_K, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+            case KT_Q6_K: hipLaunchKernelGGL((k_gemm_kq<KT_Q6_K, 1, 0>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+                break;
+            case KT_Q4_K_RS: if (TMv == 2) hipLaunchKernelGGL((k_gemm_kq<KT_Q4_K, 2, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+                else hipLaunchKernelGGL((k_gemm_kq<KT_Q4_K, 1, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+                break;
+            default: hipLaunchKernelGGL((k_gemm_kq<KT_Q6_K, 1, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
                 break;
             }
             KCPP_CHECK(hipGetLastError());

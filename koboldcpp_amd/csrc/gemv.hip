@@ -13,6 +13,8 @@
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
+#include <cstring>
+
 #include "gemv_units.h"
 
 // ---------------------------------------------------------------- kernel
@@ -103,6 +105,18 @@ int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, con
               int64_t c0, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     if (M < 1 || M > 8) return -1;
+    if (type == KT_Q4_K_RS || type == KT_Q6_K_RS) {   // decode layouts: one RS mat-vec launch per column
+        for (int64_t c = 0; c < M; ++c) {
+            DecArgs a;
+            memset(&a, 0, sizeof a);
+            a.K = K; a.nseg = 1; a.W[0] = (const uint8_t *)W; a.W2 = (const uint8_t *)W2; a.N[0] = N;
+            a.Y[0] = Y + c * ldy; a.res = res ? res + c * ldr : nullptr;
+            a.act = (const uint8_t *)act; a.act_mtot = Mtot; a.act_col = c0 + c;
+            const int rc = kcpp_gemv_rs(type, &a, mode, 0, stream);
+            if (rc) return rc;
+        }
+        return 0;
+    }
     const int64_t E = (type == KT_Q4_0 || type == KT_Q8_0) ? 32 : 64;
     if (K % (type == KT_Q4_0 || type == KT_Q8_0 ? 32 : 256) || K / E < 1) return -2;
 #define KCPP_T(T)                                                                   \

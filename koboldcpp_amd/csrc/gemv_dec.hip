@@ -9,6 +9,8 @@ template <int TYPE> int dispatch_mode(const DecArgs &a, int mode, int pro, int r
 extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream) {
     const DecArgs &a = *(const DecArgs *)args;
     hipStream_t s = (hipStream_t)stream;
+    // row-major decode layouts: only the RS kernels read them (gemv_rs.hip)
+    if (type == KT_Q4_K_RS || type == KT_Q6_K_RS) return kcpp_gemv_rs(type, args, mode, pro, stream);
     // coalesced-streaming kernel where it covers the type/shape (gemv_stream.hip), else unit-per-lane
     static const int use_q4k = getenv("KCPP_Q4K") ? atoi(getenv("KCPP_Q4K")) : 1;
     if (use_q4k && type == KT_Q4_K) {

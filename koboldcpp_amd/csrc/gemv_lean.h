@@ -92,6 +92,36 @@ struct ActCopy {
     }
 };
 
+// column c of a Q8_K activation buffer with Mt columns (qs [Mt][K] ++ d [Mt][K/256] ++ bsums [Mt][K/16]) ->
+// the single-column LDS image qs[K] ++ d[K/256] ++ bsums[K/16]; K <= 16384
+struct ActCopyCol {
+    uint4 q[4];
+    uint32_t s[2];
+    __device__ __forceinline__ void load(const uint8_t *act, int K, int64_t Mt, int64_t c) {
+        const int tid = threadIdx.x, nq = K / 16, ns = K / 256 + K / 32;
+        const uint8_t *qs = act + c * K;
+        const uint32_t *d = (const uint32_t *)(act + Mt * K) + c * (K / 256);
+        const uint32_t *bs = (const uint32_t *)(act + Mt * K + Mt * (K / 256) * 4) + c * (K / 32);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = *(const uint4 *)(qs + 16 * min(tid + 256 * i, nq - 1));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int j = min(tid + 256 * i, ns - 1);
+            s[i] = j < K / 256 ? d[j] : bs[j - K / 256];
+        }
+    }
+    __device__ __forceinline__ void store(uint8_t *lds, int K) {
+        const int tid = threadIdx.x, nq = K / 16, ns = K / 256 + K / 32;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (tid + 256 * i < nq) *(uint4 *)(lds + 16 * (tid + 256 * i)) = q[i];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            if (tid + 256 * i < ns) ((uint32_t *)(lds + K))[tid + 256 * i] = s[i];
+        __syncthreads();
+    }
+};
+
 // store R parked results of group slot_g (rows row0.. of segment seg)
 template <int R, int MODE>
 __device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0, const float (&slot)[R]) {

@@ -1,0 +1,363 @@
+// gemv_rs.hip -- single-token mat-vec (decode) over the row-major decode layouts KT_Q4_K_RS / KT_Q6_K_RS.
+//
+// Why a layout of its own: in the ggml block order (block_q4_K, ggml-common.h:286: 16-B header + 128 B
+// of nibbles, repeated) a lane that owns a 64-element unit reads three 16-B pieces at a 144-B stride,
+// so every wave-wide load instruction touches ~18 cache lines for 1 KiB of data -- the address
+// pattern alone capped a 66 MB gate|up read at 15 us against 11.3 us for a contiguous stream
+// (tools/stream_probe.py).  The RS layouts keep each row's bytes together but split them into planes
+// (kcpp_common.h):
+//   Q4_K_RS row: [nsb][16] headers ++ [nsb][128] nibbles
+//   Q6_K_RS row: [4 nsb][16] ql-lo ++ [4 nsb][16] ql-hi ++ [4 nsb][16] qh ++ [4 nsb][4] scales ++ [nsb] f16 d
+// so lane l's data piece i is the 16 B at plane + 16 (l + 64 i): one wave load = 1 KiB contiguous.
+//
+// Work split: lane l owns the same piece positions of every row, so its Q8_K activation slices (from
+// the LDS prologue: rms_norm * w -> Q8_K, quantize only, or a copy) live in registers for the whole
+// launch; a wave owns R rows per group (x2 for gate|up), groups stride over a persistent grid, the
+// next group's loads are in flight while the current one is reduced (PF), and the per-row results are
+// parked per lane and stored once after the streaming loop (lean::store_group: residual, SiLU-GLU,
+// RoPE + f16 K/V cache stores).
+//
+// Integer parts are exact (v_dot4_i32_i8 on the 4/6-bit weights and the Q8_K int8 activation, bsums
+// for the min / -32 offsets) as in ggml_vec_dot_q4_K_q8_K / ggml_vec_dot_q6_K_q8_K
+// (ggml-quants.c:7714, 8919); only the fp32 combination order differs (per 32/64 elements).
+#include "gemv_lean.h"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace {
+
+// ---------------------------------------------------------------- Q4_K_RS
+// piece c = l + 64 i of the nibble plane: super-block sb = c >> 3, pair j = (c >> 1) & 3, half hh = c & 1:
+// low nibbles = elements 64 j + 16 hh + 0..15 (sub-block 2j), high nibbles = the same + 32 (sub-block 2j+1)
+struct Q4Sel {
+    bool hi;
+    int sh, offh, shm;
+};
+__device__ __forceinline__ Q4Sel q4_sel(int j) {
+    Q4Sel s;
+    s.hi = j >= 2;
+    s.sh = 16 * (j & 1);
+    s.offh = s.hi ? 6 : 4;
+    s.shm = s.hi ? s.sh + 4 : s.sh;
+    return s;
+}
+// get_scale_min_k4 (ggml-quants.c:1899) for sub-blocks 2j, 2j+1 from header dwords y, z, w (scales[12])
+__device__ __forceinline__ void q4_scales(const uint4 &h, const Q4Sel &s, int &sc0, int &m0, int &sc1, int &m1) {
+    const uint32_t lo_sc = s.hi ? h.w : h.y, lo_m = s.hi ? h.w : h.z;
+    sc0 = (int)(__builtin_amdgcn_ubfe(lo_sc, s.sh, 4) | (__builtin_amdgcn_ubfe(h.y, s.sh + s.offh, 2) << 4));
+    sc1 = (int)(__builtin_amdgcn_ubfe(lo_sc, s.sh + 8, 4) | (__builtin_amdgcn_ubfe(h.y, s.sh + 8 + s.offh, 2) << 4));
+    m0 = (int)(__builtin_amdgcn_ubfe(lo_m, s.shm, 4) | (__builtin_amdgcn_ubfe(h.z, s.sh + s.offh, 2) << 4));
+    m1 = (int)(__builtin_amdgcn_ubfe(lo_m, s.shm + 8, 4) | (__builtin_amdgcn_ubfe(h.z, s.sh + 8 + s.offh, 2) << 4));
+}
+
+template <int TYPE> struct RS;
+
+template <> struct RS<KT_Q4_K_RS> {
+    static constexpr int BYTES = 144;
+    static constexpr int PIECES_PER_SB = 8;
+    struct Act { int4 lo, hi; float d; int bslo, bshi; };
+    struct W { uint4 h, q; };
+    struct Lane { Q4Sel s; int j, hh; };
+    static __device__ __forceinline__ Lane lane_consts(int lane) {
+        Lane c;
+        c.j = (lane >> 1) & 3; c.hh = lane & 1; c.s = q4_sel(c.j);
+        return c;
+    }
+    static __device__ __forceinline__ int sb_of(int lane, int i) { return (lane >> 3) + 8 * i; }
+    static __device__ __forceinline__ void act(const uint8_t *lds, int K, int sb, const Lane &c, Act &x) {
+        const int e0 = 256 * sb + 64 * c.j + 16 * c.hh;
+        x.lo = *(const int4 *)(lds + e0);
+        x.hi = *(const int4 *)(lds + e0 + 32);
+        x.d = ((const float *)(lds + K))[sb];
+        const int16_t *bs = (const int16_t *)(lds + K + (K / 256) * 4);
+        x.bslo = bs[e0 >> 4];
+        x.bshi = bs[(e0 >> 4) + 2];
+    }
+    // piece p (clamped to the row) of row `rp` with nsb super-blocks
+    static __device__ __forceinline__ void load(const uint8_t *rp, int nsb, int p, W &w) {
+        w.h = ld_nt(rp + 16 * (p >> 3));
+        w.q = ld_nt(rp + 16 * nsb + 16 * p);
+    }
+    static __device__ __forceinline__ float dot(const W &w, const Act &x, const Lane &c) {
+        int sc0, m0, sc1, m1;
+        q4_scales(w.h, c.s, sc0, m0, sc1, m1);
+        const uint32_t q[4] = {w.q.x, w.q.y, w.q.z, w.q.w};
+        const int al[4] = {x.lo.x, x.lo.y, x.lo.z, x.lo.w}, ah[4] = {x.hi.x, x.hi.y, x.hi.z, x.hi.w};
+        int dlo = 0, dhi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            dlo = sdot4((int)(q[k] & 0x0F0F0F0Fu), al[k], dlo);
+            dhi = sdot4((int)((q[k] >> 4) & 0x0F0F0F0Fu), ah[k], dhi);
+        }
+        const int sumi = __mul24(sc0, dlo) + __mul24(sc1, dhi);
+        const int summ = __mul24(m0, x.bslo) + __mul24(m1, x.bshi);
+        const float dw = h2f((uint16_t)(w.h.x & 0xFFFF)), dmw = h2f((uint16_t)(w.h.x >> 16));
+        return x.d * fmaf(dw, (float)sumi, -dmw * (float)summ);
+    }
+};
+
+// ---------------------------------------------------------------- Q6_K_RS
+// unit U = l + 64 i = 4 sb + u, u = (half h = u >> 1, 16-lane half lh = u & 1); its 64 elements are
+// 256 sb + 128 h + 16 lh + 32 g + 0..15 for g = 0..3 (dequantize_row_q6_K, ggml-quants.c:2978):
+//   g0: ql-lo & 15 | qh >> 0 & 3,  g1: ql-hi & 15 | qh >> 2 & 3,  g2: ql-lo >> 4 | qh >> 4 & 3,
+//   g3: ql-hi >> 4 | qh >> 6 & 3;  scales sc[8 h + lh + 2 g] (one int8 per 16 elements).
+template <> struct RS<KT_Q6_K_RS> {
+    static constexpr int BYTES = 210;
+    static constexpr int PIECES_PER_SB = 4;
+    struct Act { int4 a[4]; float d; int bs[4]; };
+    struct W { uint4 A, B, C; uint32_t sc; uint32_t d; };
+    struct Lane { int h, lh; };
+    static __device__ __forceinline__ Lane lane_consts(int lane) {
+        Lane c;
+        c.h = (lane >> 1) & 1; c.lh = lane & 1;
+        return c;
+    }
+    static __device__ __forceinline__ int sb_of(int lane, int i) { return (lane >> 2) + 16 * i; }
+    static __device__ __forceinline__ void act(const uint8_t *lds, int K, int sb, const Lane &c, Act &x) {
+        const int e0 = 256 * sb + 128 * c.h + 16 * c.lh;
+        const int16_t *bs = (const int16_t *)(lds + K + (K / 256) * 4);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            x.a[g] = *(const int4 *)(lds + e0 + 32 * g);
+            x.bs[g] = bs[(e0 >> 4) + 2 * g];
+        }
+        x.d = ((const float *)(lds + K))[sb];
+    }
+    static __device__ __forceinline__ void load(const uint8_t *rp, int nsb, int p, W &w) {
+        w.A = ld_nt(rp + 16 * p);
+        w.B = ld_nt(rp + 64 * nsb + 16 * p);
+        w.C = ld_nt(rp + 128 * nsb + 16 * p);
+        w.sc = __builtin_nontemporal_load((const uint32_t *)(rp + 192 * nsb + 4 * p));
+        w.d = __builtin_nontemporal_load((const uint16_t *)(rp + 208 * nsb + 2 * (p >> 2)));
+    }
+    static __device__ __forceinline__ float dot(const W &w, const Act &x, const Lane &) {
+        const uint32_t A[4] = {w.A.x, w.A.y, w.A.z, w.A.w}, B[4] = {w.B.x, w.B.y, w.B.z, w.B.w};
+        const uint32_t C[4] = {w.C.x, w.C.y, w.C.z, w.C.w};
+        int dg[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t q0 = (A[k] & 0x0F0F0F0Fu) | ((C[k] << 4) & 0x30303030u);
+            const uint32_t q1 = (B[k] & 0x0F0F0F0Fu) | ((C[k] << 2) & 0x30303030u);
+            const uint32_t q2 = ((A[k] >> 4) & 0x0F0F0F0Fu) | (C[k] & 0x30303030u);
+            const uint32_t q3 = ((B[k] >> 4) & 0x0F0F0F0Fu) | ((C[k] >> 2) & 0x30303030u);
+            const int av[4] = {k == 0 ? x.a[0].x : k == 1 ? x.a[0].y : k == 2 ? x.a[0].z : x.a[0].w,
+                               k == 0 ? x.a[1].x : k == 1 ? x.a[1].y : k == 2 ? x.a[1].z : x.a[1].w,
+                               k == 0 ? x.a[2].x : k == 1 ? x.a[2].y : k == 2 ? x.a[2].z : x.a[2].w,
+                               k == 0 ? x.a[3].x : k == 1 ? x.a[3].y : k == 2 ? x.a[3].z : x.a[3].w};
+            dg[0] = sdot4((int)q0, av[0], dg[0]);
+            dg[1] = sdot4((int)q1, av[1], dg[1]);
+            dg[2] = sdot4((int)q2, av[2], dg[2]);
+            dg[3] = sdot4((int)q3, av[3], dg[3]);
+        }
+        int isum = 0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int sc = (int)(int8_t)((w.sc >> (8 * g)) & 0xFF);
+            isum += sc * (dg[g] - 32 * x.bs[g]);
+        }
+        return x.d * (h2f((uint16_t)w.d) * (float)isum);
+    }
+};
+
+}  // namespace
+
+// NI = pieces per lane per row (ceil(nsb * PIECES_PER_SB / 64)); R rows per group (x2 for gate|up);
+// PRO 0: act copy, 1: rms_norm * w -> Q8_K, 2: quantize only; MC = ceil(K / 4096) prologue chunks;
+// PF: issue the next group's loads before reducing the current one.
+template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF>
+__global__ void __launch_bounds__(256) k_gemv_rs(const DecArgs a) {
+    using T = RS<TYPE>;
+    constexpr int RR = MODE == 1 ? 2 * R : R;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int K = (int)a.K, nsb = K / 256, RB = nsb * T::BYTES;
+    const int npieces = nsb * T::PIECES_PER_SB;
+    const int N0 = (int)a.N[0], N1 = a.nseg > 1 ? (int)a.N[1] : 0, N2 = a.nseg > 2 ? (int)a.N[2] : 0;
+    const int ngroups = (N0 + N1 + N2) / R;
+    const int nw = (int)gridDim.x * 4;
+    const int wid = (int)blockIdx.x * 4 + wave;
+    const int64_t eoff = a.eid ? (int64_t)__builtin_amdgcn_readfirstlane(a.eid[0]) * a.ebytes : 0;   // MoE slice
+    const int abytes = K + K / 256 * 4 + K / 16 * 2;
+    const typename T::Lane lc = T::lane_consts(lane);
+
+    auto group_rows = [&](int g, int &seg, int &row0) {
+        const int r = g * R;
+        seg = r < N0 ? 0 : (r < N0 + N1 ? 1 : 2);
+        row0 = seg == 0 ? r : (seg == 1 ? r - N0 : r - N0 - N1);
+    };
+    struct Buf { typename T::W w[NI][RR]; };
+    auto issue = [&](int g, Buf &b) {
+        int seg, row0;
+        group_rows(g, seg, row0);
+        const uint8_t *W = (seg == 0 ? a.W[0] : (seg == 1 ? a.W[1] : a.W[2])) + eoff;
+#pragma unroll
+        for (int r = 0; r < RR; ++r) {
+            const uint8_t *rp = (MODE == 1 && r >= R ? a.W2 + eoff : W) + (int64_t)(row0 + (r % R)) * RB;
+#pragma unroll
+            for (int i = 0; i < NI; ++i) T::load(rp, nsb, min(lane + 64 * i, npieces - 1), b.w[i][r]);
+        }
+    };
+
+    Buf ba, bb;
+    const int g0 = min(wid, ngroups - 1);
+    if constexpr (PRO != 0) {
+        lean::ActPro<PRO, MC> pro;
+        pro.load(a);
+        issue(g0, ba);
+        pro.compute(a, lds);
+    } else {
+        lean::ActCopyCol cp;
+        cp.load(a.act, K, a.act_mtot > 0 ? a.act_mtot : 1, a.act_col);
+        issue(g0, ba);
+        cp.store(lds, K);
+    }
+    typename T::Act xr[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) T::act(lds, K, min(T::sb_of(lane, i), nsb - 1), lc, xr[i]);
+
+    float slot[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) slot[r] = 0.0f;
+    int slot_g = -1;
+    auto compute = [&](int g, const Buf &b, int k) {
+        float acc[RR];
+#pragma unroll
+        for (int r = 0; r < RR; ++r) acc[r] = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const bool ok = (NI * 64 == npieces) || lane + 64 * i < npieces;
+#pragma unroll
+            for (int r = 0; r < RR; ++r) {
+                const float p = T::dot(b.w[i][r], xr[i], lc);
+                acc[r] += ok ? p : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < RR; ++r) acc[r] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_sum_f(acc[r]))));
+        const bool mine = lane == k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            float v;
+            if constexpr (MODE == 1) v = (acc[r] / (1.0f + expf(-acc[r]))) * acc[R + r];
+            else v = acc[r];
+            slot[r] = mine ? v : slot[r];
+        }
+        slot_g = mine ? g : slot_g;
+    };
+    int k = 0;
+    if constexpr (PF) {
+        for (int g = wid; g < ngroups; g += 2 * nw, k += 2) {
+            const int g1 = g + nw, g2 = g + 2 * nw;
+            issue(min(g1, ngroups - 1), bb);
+            compute(g, ba, k);
+            if (g1 >= ngroups) break;
+            issue(min(g2, ngroups - 1), ba);
+            compute(g1, bb, k + 1);
+        }
+    } else {
+        for (int g = wid; g < ngroups; g += nw, ++k) {
+            if (k) issue(g, ba);
+            compute(g, ba, k);
+        }
+    }
+    if (slot_g < 0) return;
+    int seg, row0;
+    group_rows(slot_g, seg, row0);
+    lean::store_group<R, MODE>(a, seg, row0, slot);
+}
+
+namespace {
+template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF>
+int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
+    int64_t ntot = 0;
+    for (int i = 0; i < a.nseg; ++i) {
+        if (a.N[i] % R) return -5;
+        ntot += a.N[i];
+    }
+    const int64_t groups = ntot / R;
+    int64_t nblk = std::min<int64_t>((groups + 3) / 4, max_blocks);
+    nblk = std::max<int64_t>(nblk, (groups + 255) / 256);    // <= 64 groups per wave (result slots)
+    const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
+    hipLaunchKernelGGL((k_gemv_rs<TYPE, NI, R, MODE, PRO, MC, PF>), dim3((unsigned)nblk), dim3(256), (size_t)abytes + 16, s,
+                       a);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// rows per group, prefetch and grid per shape, from the launch sweep (tools/sweep_rs.sh, MI355X):
+//   gate|up (mode 1)  : R 1, PF, 512 workgroups     14.8 us / 66 MB
+//   q|k|v (mode 2)    : R 2, 512                     7.0 us / 14 MB
+//   head (N > 16384)  : R 2, 512                    69.4 us / 431 MB (6.2 TB/s)
+//   down (K > 8192)   : R 1, PF, 256 (Q4_K) / 512 (Q6_K)   12.5 / 15.0 us
+//   other (wo, ...)   : R 1, 1024                    4.9 us / 9.4 MB
+// KCPP_RS_R / KCPP_RS_PF / KCPP_RS_BLOCKS override (sweeps)
+template <int TYPE, int NI, int MC>
+int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
+    static const int r_env = getenv("KCPP_RS_R") ? atoi(getenv("KCPP_RS_R")) : 0;
+    static const int pf_env = getenv("KCPP_RS_PF") ? atoi(getenv("KCPP_RS_PF")) : -1;
+    static const int b_env = getenv("KCPP_RS_BLOCKS") ? atoi(getenv("KCPP_RS_BLOCKS")) : 0;
+    const int64_t ntot = a.N[0] + (a.nseg > 1 ? a.N[1] : 0) + (a.nseg > 2 ? a.N[2] : 0);
+    int R = 1, PF = 0, B = 1024;
+    if (mode == 1) { PF = 1; B = 512; }
+    else if (mode == 2) { R = 2; B = 512; }
+    else if (ntot > 16384) { R = 2; B = 512; }
+    else if (a.K > 8192) { PF = TYPE == KT_Q4_K_RS; B = TYPE == KT_Q4_K_RS ? 256 : 512; }
+    if (r_env && mode == 0) R = r_env;
+    if (pf_env >= 0) PF = pf_env;
+    if (b_env) B = b_env;
+#define KCPP_RS_P(PRO_)                                                                                             \
+    if (pro == PRO_) {                                                                                              \
+        if (mode == 1) return PF ? launch_rs<TYPE, NI, 1, 1, PRO_, MC, 1>(a, B, s) : launch_rs<TYPE, NI, 1, 1, PRO_, MC, 0>(a, B, s); \
+        if (mode == 2) return launch_rs<TYPE, NI, 2, 2, PRO_, MC, 0>(a, B, s);                                                \
+        if (R == 2) return PF ? launch_rs<TYPE, NI, 2, 0, PRO_, MC, 1>(a, B, s) : launch_rs<TYPE, NI, 2, 0, PRO_, MC, 0>(a, B, s); \
+        return PF ? launch_rs<TYPE, NI, 1, 0, PRO_, MC, 1>(a, B, s) : launch_rs<TYPE, NI, 1, 0, PRO_, MC, 0>(a, B, s);             \
+    }
+    KCPP_RS_P(0)
+    KCPP_RS_P(1)
+    KCPP_RS_P(2)
+#undef KCPP_RS_P
+    return -3;
+}
+}  // namespace
+
+// K coverage of the RS kernels (the runtime picks an RS layout only where this holds)
+extern "C" int kcpp_rs_supported(int type, int64_t K) {
+    if (K % 256 || K < 256) return 0;
+    const int64_t nsb = K / 256;
+    if (type == KT_Q4_K_RS || type == KT_Q4_K) return nsb <= 56;
+    if (type == KT_Q6_K_RS || type == KT_Q6_K) return nsb % 8 == 0 && nsb <= 64;
+    return 0;
+}
+
+// -3 = not covered
+extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream) {
+    const DecArgs &a = *(const DecArgs *)args;
+    hipStream_t s = (hipStream_t)stream;
+    if (a.nseg < 1 || a.nseg > 3 || !kcpp_rs_supported(type, a.K)) return -3;
+    if (mode == 1 && a.nseg != 1) return -3;
+    const int nsb = (int)(a.K / 256);
+    if (type == KT_Q4_K_RS) {
+        const int ni = (nsb * 8 + 63) / 64, mc = (int)((a.K + 4095) / 4096);
+        switch (ni) {
+        case 1: return pick_rs<KT_Q4_K_RS, 1, 1>(a, mode, pro, s);
+        case 2: return pick_rs<KT_Q4_K_RS, 2, 1>(a, mode, pro, s);
+        case 3: return pick_rs<KT_Q4_K_RS, 3, 2>(a, mode, pro, s);
+        case 4: return pick_rs<KT_Q4_K_RS, 4, 2>(a, mode, pro, s);
+        case 5: return pick_rs<KT_Q4_K_RS, 5, 3>(a, mode, pro, s);
+        case 6: return pick_rs<KT_Q4_K_RS, 6, 3>(a, mode, pro, s);
+        default: return mc <= 4 ? pick_rs<KT_Q4_K_RS, 7, 4>(a, mode, pro, s) : -3;
+        }
+    }
+    if (type == KT_Q6_K_RS) {
+        const int ni = (nsb * 4 + 63) / 64;
+        switch (ni) {
+        case 1: return pick_rs<KT_Q6_K_RS, 1, 1>(a, mode, pro, s);
+        case 2: return pick_rs<KT_Q6_K_RS, 2, 2>(a, mode, pro, s);
+        case 3: return pick_rs<KT_Q6_K_RS, 3, 3>(a, mode, pro, s);
+        default: return pick_rs<KT_Q6_K_RS, 4, 4>(a, mode, pro, s);
+        }
+    }
+    return -3;
+}

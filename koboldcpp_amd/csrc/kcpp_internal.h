@@ -37,6 +37,8 @@ struct DecArgs {
     const int32_t *eid;
     int64_t ebytes;
     const float *escale;
+    // PRO 0 in the RS kernels: column act_col of an activation buffer holding act_mtot (0 = 1) columns
+    int64_t act_mtot, act_col;
 };
 extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream);
 // coalesced Q4_K variant (gemv_stream.hip); -3 = not covered
@@ -49,3 +51,6 @@ extern "C" int kcpp_gemv_q6k(const void *args, int mode, int pro, void *stream);
 // MFMA prefill flash attention (attn_mfma.hip); -3 = shape not covered (needs D = 128, H = 4 * HKV)
 extern "C" int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out,
                                             int T, int H, int HKV, int D, int n_past, float scale, void *stream);
+// decode mat-vec over the row-major RS layouts (gemv_rs.hip); -3 = not covered
+extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
+extern "C" int kcpp_rs_supported(int type, int64_t K);

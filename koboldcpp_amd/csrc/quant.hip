@@ -8,8 +8,9 @@
 #include "kcpp_internal.h"
 
 // ---------------------------------------------------------------- weight layout
-// place one ggml-layout block (src) into the kcpp GPU layout at block index b
-__device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uint8_t *dst, int64_t b, int64_t nb) {
+// place one ggml-layout block (src) into the kcpp GPU layout at block index b (bpr blocks per row)
+__device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uint8_t *dst, int64_t b, int64_t nb,
+                                               int64_t bpr) {
     switch (type) {
     case KT_Q6_K: {
         uint8_t *q = dst + b * 192, *sc = dst + nb * 192 + b * 16, *d = dst + nb * 208 + b * 2;
@@ -27,13 +28,35 @@ __device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uin
         d[0] = src[0]; d[1] = src[1];
         for (int i = 0; i < 32; ++i) q[i] = src[2 + i];
     } break;
+    case KT_Q4_K_RS: {
+        const int64_t n = b / bpr, sb = b % bpr;
+        uint8_t *row = dst + n * 144 * bpr;
+        for (int i = 0; i < 16; ++i) row[16 * sb + i] = src[i];
+        for (int i = 0; i < 128; ++i) row[16 * bpr + 128 * sb + i] = src[16 + i];
+    } break;
+    case KT_Q6_K_RS: {
+        const int64_t n = b / bpr, sb = b % bpr;
+        uint8_t *row = dst + n * 210 * bpr;
+        for (int u = 0; u < 4; ++u) {
+            const int h = u >> 1, lh = u & 1;
+            const int64_t U = 4 * sb + u;
+            for (int i = 0; i < 16; ++i) {
+                row[16 * U + i] = src[64 * h + 16 * lh + i];
+                row[64 * bpr + 16 * U + i] = src[64 * h + 32 + 16 * lh + i];
+                row[128 * bpr + 16 * U + i] = src[128 + 32 * h + 16 * lh + i];
+            }
+            for (int g = 0; g < 4; ++g) row[192 * bpr + 4 * U + g] = src[192 + 8 * h + lh + 2 * g];
+        }
+        row[208 * bpr + 2 * sb] = src[208]; row[208 * bpr + 2 * sb + 1] = src[209];
+    } break;
     default: {
         const int bb = ks_block_bytes(type);
         for (int i = 0; i < bb; ++i) dst[b * bb + i] = src[i];
     }
     }
 }
-__device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint8_t *blk, int64_t b, int64_t nb) {
+__device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint8_t *blk, int64_t b, int64_t nb,
+                                              int64_t bpr) {
     switch (type) {
     case KT_Q6_K: {
         const uint8_t *q = src + b * 192, *sc = src + nb * 192 + b * 16, *d = src + nb * 208 + b * 2;
@@ -51,6 +74,27 @@ __device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint
         blk[0] = d[0]; blk[1] = d[1];
         for (int i = 0; i < 32; ++i) blk[2 + i] = q[i];
     } break;
+    case KT_Q4_K_RS: {
+        const int64_t n = b / bpr, sb = b % bpr;
+        const uint8_t *row = src + n * 144 * bpr;
+        for (int i = 0; i < 16; ++i) blk[i] = row[16 * sb + i];
+        for (int i = 0; i < 128; ++i) blk[16 + i] = row[16 * bpr + 128 * sb + i];
+    } break;
+    case KT_Q6_K_RS: {
+        const int64_t n = b / bpr, sb = b % bpr;
+        const uint8_t *row = src + n * 210 * bpr;
+        for (int u = 0; u < 4; ++u) {
+            const int h = u >> 1, lh = u & 1;
+            const int64_t U = 4 * sb + u;
+            for (int i = 0; i < 16; ++i) {
+                blk[64 * h + 16 * lh + i] = row[16 * U + i];
+                blk[64 * h + 32 + 16 * lh + i] = row[64 * bpr + 16 * U + i];
+                blk[128 + 32 * h + 16 * lh + i] = row[128 * bpr + 16 * U + i];
+            }
+            for (int g = 0; g < 4; ++g) blk[192 + 8 * h + lh + 2 * g] = row[192 * bpr + 4 * U + g];
+        }
+        blk[208] = row[208 * bpr + 2 * sb]; blk[209] = row[208 * bpr + 2 * sb + 1];
+    } break;
     default: {
         const int bb = ks_block_bytes(type);
         for (int i = 0; i < bb; ++i) blk[i] = src[b * bb + i];
@@ -58,26 +102,27 @@ __device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint
     }
 }
 
-__global__ void k_repack(int type, const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int64_t nb, int dir) {
+__global__ void k_repack(int type, const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int64_t nb, int64_t bpr,
+                         int dir) {
     int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     uint8_t blk[256];
     const int bb = ks_block_bytes(type);
     if (dir == 0) {                    // ggml -> kcpp
         for (int i = 0; i < bb; ++i) blk[i] = src[b * bb + i];
-        kl_store_block(type, blk, dst, b, nb);
+        kl_store_block(type, blk, dst, b, nb, bpr);
     } else {                           // kcpp -> ggml
-        kl_load_block(type, src, blk, b, nb);
+        kl_load_block(type, src, blk, b, nb, bpr);
         for (int i = 0; i < bb; ++i) dst[b * bb + i] = blk[i];
     }
 }
 
-__global__ void k_synth(int type, uint64_t seed, uint64_t tid, uint8_t *__restrict__ dst, int64_t nb) {
+__global__ void k_synth(int type, uint64_t seed, uint64_t tid, uint8_t *__restrict__ dst, int64_t nb, int64_t bpr) {
     int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     uint8_t blk[256];
     ks_fill_block(type, seed, tid, (uint64_t)b, blk);
-    kl_store_block(type, blk, dst, b, nb);
+    kl_store_block(type, blk, dst, b, nb, bpr);
 }
 
 __device__ __forceinline__ void scale_min_k4(int j, const uint8_t *q, int &d, int &m) {
@@ -89,10 +134,10 @@ __device__ __forceinline__ void scale_min_k4(int j, const uint8_t *q, int &d, in
 }
 
 // dequantize block b of a kcpp-layout tensor (nb blocks total) into o[0..block_elems)
-__device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t b, float *o) {
+__device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t bpr, int64_t b, float *o) {
     uint8_t blk[256];
-    kl_load_block(type, src, blk, b, nb);
-    switch (type) {
+    kl_load_block(type, src, blk, b, nb, bpr);
+    switch (ks_base_type(type)) {
     case KT_F32: o[0] = *(const float *)blk; break;
     case KT_F16: o[0] = h2f(*(const uint16_t *)blk); break;
     case KT_Q4_0: {
@@ -146,10 +191,10 @@ __device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t b, f
 }
 
 // one thread per block: dequantize into y (row-major [N][K])
-__global__ void k_dequant(int type, const uint8_t *__restrict__ src, float *__restrict__ y, int64_t nb) {
+__global__ void k_dequant(int type, const uint8_t *__restrict__ src, float *__restrict__ y, int64_t nb, int64_t bpr) {
     int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
-    deq_block(type, src, nb, b, y + b * ks_block_elems(type));
+    deq_block(type, src, nb, bpr, b, y + b * ks_block_elems(type));
 }
 
 // get_rows: one workgroup per token; thread i dequantizes element chunks of 8 of the selected row.
@@ -176,6 +221,7 @@ __device__ __forceinline__ float deq_elem(int type, const uint8_t *src, int64_t 
         if (five) q += ((blk[16 + l] >> (2 * c + hi)) & 1) << 4;
         return __fsub_rn(__fmul_rn(d * sc, (float)q), mn * m);
     }
+    case KT_Q4_K_RS: case KT_Q6_K_RS: return 0.0f;      // row gathers of decode layouts are not used
     case KT_Q6_K: {
         const uint8_t *q6 = src + b * 192;
         const int8_t *scp = (const int8_t *)(src + nb * 192 + b * 16);
@@ -278,7 +324,7 @@ int kcpp_weight_repack(int type, const void *src_ggml, void *dst_kcpp, int64_t K
     const int64_t nb = kl_nblocks(type, K, N);
     if (nb <= 0) return 0;
     hipLaunchKernelGGL(k_repack, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, type,
-                       (const uint8_t *)src_ggml, (uint8_t *)dst_kcpp, nb, to_ggml);
+                       (const uint8_t *)src_ggml, (uint8_t *)dst_kcpp, nb, K / ks_block_elems(type), to_ggml);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }
@@ -286,7 +332,7 @@ int kcpp_weight_repack(int type, const void *src_ggml, void *dst_kcpp, int64_t K
 int kcpp_weight_synth(int type, uint64_t seed, uint64_t tid, void *dst, int64_t K, int64_t N, void *stream) {
     const int64_t nb = kl_nblocks(type, K, N);
     hipLaunchKernelGGL(k_synth, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, type, seed, tid,
-                       (uint8_t *)dst, nb);
+                       (uint8_t *)dst, nb, K / ks_block_elems(type));
     KCPP_CHECK(hipGetLastError());
     return 0;
 }
@@ -294,7 +340,7 @@ int kcpp_weight_synth(int type, uint64_t seed, uint64_t tid, void *dst, int64_t 
 int kcpp_dequantize(int type, const void *w, float *y, int64_t K, int64_t N, void *stream) {
     const int64_t nb = kl_nblocks(type, K, N);
     hipLaunchKernelGGL(k_dequant, dim3((unsigned)((nb + 127) / 128)), dim3(128), 0, (hipStream_t)stream, type,
-                       (const uint8_t *)w, y, nb);
+                       (const uint8_t *)w, y, nb, K / ks_block_elems(type));
     KCPP_CHECK(hipGetLastError());
     return 0;
 }
@@ -328,6 +374,7 @@ int kcpp_quantize_act_glu(const float *x, int64_t ldx, int64_t uoff, void *out, 
 
 int kcpp_get_rows(int type, const void *w, int64_t K, int64_t N, const int32_t *ids, int64_t T, float *y, int64_t ldy,
                   void *stream) {
+    if (type == KT_Q4_K_RS || type == KT_Q6_K_RS) return -2;
     hipLaunchKernelGGL(k_get_rows, dim3((unsigned)((K + 255) / 256), (unsigned)T), dim3(256), 0, (hipStream_t)stream, type,
                        (const uint8_t *)w, K, N, ids, y, ldy);
     KCPP_CHECK(hipGetLastError());

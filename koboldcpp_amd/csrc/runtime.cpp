@@ -195,7 +195,21 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     if (hipSetDevice(device) != hipSuccess) { g_err = "hipSetDevice failed"; return nullptr; }
     kcpp_model *m = new kcpp_model();
     m->hp = *hp;
-    m->types.assign(types, types + n_tensors(*hp));
+    // on-device layout per tensor: dense Q4_K / Q6_K mat-mul weights whose K the RS kernels cover are held in
+    // the row-major decode layouts (KT_Q4_K_RS / KT_Q6_K_RS, gemv_rs.hip); the token embedding (row
+    // gathers), expert slices and everything else keep the kcpp layout.  KCPP_RS=0 disables (A/B runs).
+    static const int rs_env = getenv("KCPP_RS") ? atoi(getenv("KCPP_RS")) : 1;
+    m->types.resize(n_tensors(*hp));
+    for (int idx = 0; idx < n_tensors(*hp); ++idx) {
+        int t = types[idx];
+        int64_t K, N;
+        shape_of(*hp, idx, K, N);
+        const bool dense = idx >= 2 && n_slices(*hp, idx) == 1 && N > 1 && (idx == 2 || (idx - 3) % per_layer(*hp) <= 8);
+        if (rs_env && dense && (t == KT_Q4_K || t == KT_Q6_K) && kcpp_rs_supported(t, K))
+            t = t == KT_Q4_K ? KT_Q4_K_RS : KT_Q6_K_RS;
+        m->types[idx] = t;
+    }
+    types = m->types.data();
     m->device = device; m->il0 = il0; m->il1 = il1; m->has_embed = has_embed; m->has_output = has_output;
     m->ub = max_ubatch > 0 ? max_ubatch : 512;
     auto fail = [&](const char *what) { g_err = what; kcpp_model_free(m); return (kcpp_model *)nullptr; };
@@ -204,7 +218,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     const int64_t UB = m->ub;
     m->layers.resize(il1 - il0);
     static const int fuse_env = getenv("KCPP_PREFILL_FUSE") ? atoi(getenv("KCPP_PREFILL_FUSE")) : 1;
-    auto rowmajor = [](int t) { return t == KT_Q4_K || t == KT_Q5_K; };
+    auto rowmajor = [](int t) { return t == KT_Q4_K || t == KT_Q5_K || t == KT_Q4_K_RS || t == KT_Q6_K_RS; };
     auto alloc_group = [&](void *&base, int idx0, int n) -> int {
         size_t tot = 0;
         for (int j = 0; j < n; ++j) { int64_t K, N; shape_of(*hp, idx0 + j, K, N); tot += (size_t)tensor_bytes(types[idx0 + j], K, N); }
@@ -336,7 +350,7 @@ extern "C" int kcpp_model_set_tensor(kcpp_model *m, int idx, const void *src, in
     if (!t) return 0;                      // not on this stage
     if ((size_t)nbytes != t->bytes) { g_err = "set_tensor: size mismatch"; return -2; }
     RT_CHECK(hipSetDevice(m->device));
-    if (t->type == KT_Q6_K || t->type == KT_Q4_0 || t->type == KT_Q8_0) {
+    if (t->type == KT_Q6_K || t->type == KT_Q4_0 || t->type == KT_Q8_0 || t->type == KT_Q4_K_RS || t->type == KT_Q6_K_RS) {
         void *stage = nullptr;
         RT_CHECK(hipMalloc(&stage, t->bytes));
         RT_CHECK(hipMemcpyAsync(stage, src, t->bytes, hipMemcpyHostToDevice, m->stream));

@@ -11,8 +11,10 @@ import os
 from . import LIB_PATH
 
 F32, F16, Q4_0, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 8, 12, 13, 14, 15
+# device-internal row-major decode layouts of Q4_K / Q6_K (include/kcpp_synth.h; never ggml ids)
+Q4_K_RS, Q6_K_RS = 112, 114
 BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q8_0: (32, 34), Q4_K: (256, 144),
-         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292)}
+         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292), Q4_K_RS: (256, 144), Q6_K_RS: (256, 210)}
 
 
 class KcppError(RuntimeError):
@@ -87,6 +89,8 @@ _L.kcpp_gemv_dec_args_size.restype = I64
 _L.kcpp_gemv_stream.argtypes = [I, P, I, I, P]
 _L.kcpp_gemv_q4k.argtypes = [P, I, I, P]
 _L.kcpp_gemv_q6k.argtypes = [P, I, I, P]
+_L.kcpp_gemv_rs.argtypes = [I, P, I, I, P]
+_L.kcpp_rs_supported.argtypes = [I, I64]
 for _n, _a in _SIGS.items():
     getattr(_L, _n).argtypes = _a
 for _n, _r in _RES.items():
@@ -95,7 +99,8 @@ for _n, _r in _RES.items():
 
 def exported_symbols():
     return sorted(set(_SIGS) | set(_RES) | {"kcpp_vec_dot_type", "kcpp_gemv_dec", "kcpp_gemv_dec_args_size",
-                                             "kcpp_gemv_stream", "kcpp_gemv_q4k", "kcpp_gemv_q6k"})
+                                             "kcpp_gemv_stream", "kcpp_gemv_q4k", "kcpp_gemv_q6k",
+                                             "kcpp_gemv_rs", "kcpp_rs_supported"})
 
 
 def raw():
@@ -154,7 +159,8 @@ class DecArgs(ctypes.Structure):
     kcpp_gemv_dec_args_size() at import"""
     _fields_ = [("W", P * 3), ("Y", P * 3), ("N", I64 * 3), ("role", I * 3), ("nseg", I), ("W2", P), ("K", I64),
                 ("act", P), ("x", P), ("nw", P), ("eps", Fl), ("res", P), ("q16", P), ("kc", P), ("vc", P),
-                ("ekv", I64), ("D", I), ("pos", P), ("rope_tab", P), ("eid", P), ("ebytes", I64), ("escale", P)]
+                ("ekv", I64), ("D", I), ("pos", P), ("rope_tab", P), ("eid", P), ("ebytes", I64), ("escale", P),
+                ("act_mtot", I64), ("act_col", I64)]
 
 
 if ctypes.sizeof(DecArgs) != _L.kcpp_gemv_dec_args_size():

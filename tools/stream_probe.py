@@ -106,7 +106,16 @@ def dec():
         ("wo q4k pro0 r2", 12, E, E, 0, 0, 2),
         ("wo q4k pro0 r4", 12, E, E, 0, 0, 4),
         ("down q4k pro0 r2", 12, F, E, 0, 0, 2),
+        ("rs wo q4k pro0", 112, E, E, 0, 0, 1),
+        ("rs qkv q4k pro1 rope", 112, E, E + 2048, 2, 1, 2),
+        ("rs glu q4k pro1", 112, E, F, 1, 1, 1),
+        ("rs down q4k pro2", 112, F, E, 0, 2, 1),
+        ("rs down q6k pro2", 114, F, E, 0, 2, 1),
+        ("rs v q6k pro1", 114, E, 1024, 0, 1, 1),
+        ("rs head q6k pro1", 114, E, 128256, 0, 1, 1),
     ]
+    if os.environ.get("PROBE_RS_ONLY"):
+        cases = [c for c in cases if c[0].startswith("rs ")]
     x = torch.randn(F, device="cuda")
     nw = torch.ones(F, device="cuda")
     y = torch.empty(128256 * 2, device="cuda")
