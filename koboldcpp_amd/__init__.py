@@ -8,4 +8,4 @@ benchmark and Python callers.  There is no CPU fallback: if the library is missi
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "koboldcpp_hipblas.so")
+LIB_PATH = os.environ.get("KCPP_LIB") or os.path.join(PKG_DIR, "koboldcpp_hipblas.so")   # KCPP_LIB: A/B builds

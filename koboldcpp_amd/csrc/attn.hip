@@ -218,6 +218,7 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
 // reference's flash_attn_vec_ext + flash_attn_combine_results pair (fattn-vec-f16.cuh:4-299,
 // fattn-common.cuh:523) and this file's k_fa_decode + k_fa_combine pair (two launches, 1 MB of partials).
 typedef unsigned long long fa_u64;
+typedef unsigned int fa_v4u __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_sc1_f2(float2 *p, float2 v) {
     __hip_atomic_store((fa_u64 *)p, ((fa_u64)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -234,7 +235,8 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
                                                  const uint16_t *__restrict__ vc, float *__restrict__ part_o,
                                                  float2 *__restrict__ part_ml, unsigned *__restrict__ tickets,
                                                  float *__restrict__ out, uint8_t *__restrict__ qout, int H, int HKV,
-                                                 int n_past_arg, const int32_t *__restrict__ n_past_dev, float scale) {
+                                                 int n_past_arg, const int32_t *__restrict__ n_past_dev, float scale,
+                                                 int probe) {
     constexpr int D = 128;
     const int sp = blockIdx.x, NS = gridDim.x, hk = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -349,24 +351,25 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
         if (lane == 0) { s_m[wave][g] = m[g]; s_l[wave][g] = l[g]; }
     }
     __syncthreads();
-    // workgroup merge of the 4 waves -> this split's partial, published write-through
+    // workgroup merge of the waves -> this split's partial, published write-through (16-B sc1 stores)
     float2 *pml = part_ml + ((int64_t)hk * NS + sp) * G;
-    float *po = part_o + ((int64_t)hk * NS + sp) * G * D;
-    for (int j = tid; j < G * D / 2; j += 64 * FA2_W) {
-        const int g = (2 * j) / D, d = (2 * j) % D;
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(part_o, 0, 0x7FFFFFFF, 0x00020000);
+    for (int j = tid; j < G * D / 4; j += 64 * FA2_W) {
+        const int g = (4 * j) / D, d = (4 * j) % D;
         float M = s_m[0][g];
 #pragma unroll
         for (int w = 1; w < FA2_W; ++w) M = fmaxf(M, s_m[w][g]);
-        float o0 = 0.0f, o1 = 0.0f;
+        float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
         if (M != -INFINITY) {
 #pragma unroll
             for (int w = 0; w < FA2_W; ++w) {
                 const float wt = s_m[w][g] == -INFINITY ? 0.0f : expf(s_m[w][g] - M);
-                o0 = fmaf(wt, s_o[w][g][d], o0);
-                o1 = fmaf(wt, s_o[w][g][d + 1], o1);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = fmaf(wt, s_o[w][g][d + e], o[e]);
             }
         }
-        st_sc1_f2((float2 *)(po + g * D + d), make_float2(o0, o1));
+        const fa_v4u v = {__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])};
+        __builtin_amdgcn_raw_buffer_store_b128(v, prs, (int)((((int64_t)hk * NS + sp) * G * D + g * D + d) * 4), 0, 16);
     }
     if (tid < G) {
         const int g = tid;
@@ -380,7 +383,8 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
         }
         st_sc1_f2(pml + g, make_float2(M, L));
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tickets == nullptr) return;                                 // probe: partials only (tools/microbench.py)
+    if (probe != 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
         const unsigned prev = __hip_atomic_fetch_add(&tickets[hk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -388,34 +392,51 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
         if (s_last) __hip_atomic_store(&tickets[hk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (!s_last) return;
-    // ---- last split of this kv head: merge the NS partials (sc1 loads only)
+    if (!s_last || probe == 3) return;
+    // ---- last split of this kv head: merge the NS partials (sc1 loads only).  SS adjacent lanes share one
+    // 4-dim quad of one head, each loading every SS-th split (16-B loads, all issued before use), then
+    // reduce over the SS lanes: every thread of the workgroup has <= PER partials in flight.
     float *s_res = &s_o[0][0][0];                                  // reuse: G*D floats
-    for (int j = tid; j < G * D / 2; j += 64 * FA2_W) {
-        const int g = (2 * j) / D, d = (2 * j) % D;
-        const float2 *mlb = part_ml + (int64_t)hk * NS * G + g;
-        const float *ob = part_o + (int64_t)hk * NS * G * D + g * D + d;
-        float2 ml[FA2_NS], ov[FA2_NS];
+    {
+        constexpr int NQ = G * D / 4, NT = 64 * FA2_W;
+        constexpr int SS = NT / NQ >= 1 ? NT / NQ : 1, PER = (FA2_NS + SS - 1) / SS;
+        if (tid < NQ * SS) {
+            const int q = tid / SS, sub = tid % SS;
+            const int g = q / (D / 4), d = 4 * (q % (D / 4));
+            float2 ml[PER];
+            fa_v4u ov[PER];
 #pragma unroll
-        for (int s2 = 0; s2 < FA2_NS; ++s2) {
-            ml[s2] = s2 < NS ? ld_sc1_f2(mlb + s2 * G) : make_float2(-INFINITY, 0.0f);
-            ov[s2] = s2 < NS ? ld_sc1_f2((const float2 *)(ob + (int64_t)s2 * G * D)) : make_float2(0.0f, 0.0f);
+            for (int k = 0; k < PER; ++k) {
+                const int s2 = sub + SS * k;
+                ml[k] = s2 < NS ? ld_sc1_f2(part_ml + ((int64_t)hk * NS + s2) * G + g) : make_float2(-INFINITY, 0.0f);
+                ov[k] = s2 < NS ? __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)hk * NS + s2) * G * D + g * D + d) * 4), 0, 16)
+                                : fa_v4u{0u, 0u, 0u, 0u};
+            }
+            float M = -INFINITY;
+#pragma unroll
+            for (int k = 0; k < PER; ++k) M = fmaxf(M, ml[k].x);
+#pragma unroll
+            for (int o_ = 1; o_ < SS; o_ <<= 1) M = fmaxf(M, __shfl_xor(M, o_, 64));
+            float L = 0.0f, o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int k = 0; k < PER; ++k) {
+                const float wt = ml[k].x == -INFINITY ? 0.0f : expf(ml[k].x - M);
+                L = fmaf(wt, ml[k].y, L);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = fmaf(wt, __uint_as_float(ov[k][e]), o[e]);
+            }
+#pragma unroll
+            for (int o_ = 1; o_ < SS; o_ <<= 1) {
+                L += __shfl_xor(L, o_, 64);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] += __shfl_xor(o[e], o_, 64);
+            }
+            if (sub == 0) {
+                const float4 r = make_float4(o[0] / L, o[1] / L, o[2] / L, o[3] / L);
+                *(float4 *)&s_res[g * D + d] = r;
+                if (out) *(float4 *)(out + (int64_t)(hk * G + g) * D + d) = r;
+            }
         }
-        float M = -INFINITY;
-#pragma unroll
-        for (int s2 = 0; s2 < FA2_NS; ++s2) M = fmaxf(M, ml[s2].x);
-        float L = 0.0f, o0 = 0.0f, o1 = 0.0f;
-#pragma unroll
-        for (int s2 = 0; s2 < FA2_NS; ++s2) {
-            const float wt = ml[s2].x == -INFINITY ? 0.0f : expf(ml[s2].x - M);
-            L = fmaf(wt, ml[s2].y, L);
-            o0 = fmaf(wt, ov[s2].x, o0);
-            o1 = fmaf(wt, ov[s2].y, o1);
-        }
-        const float r0 = o0 / L, r1 = o1 / L;
-        s_res[g * D + d] = r0;
-        s_res[g * D + d + 1] = r1;
-        if (out) *(float2 *)(out + (int64_t)(hk * G + g) * D + d) = make_float2(r0, r1);
     }
     if (qout == nullptr || G * D < 256) return;
     __syncthreads();
@@ -431,6 +452,63 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
         float *dp = (float *)(qout + E) + sbg;
         int16_t *bs = (int16_t *)(qout + E + nsb * 4) + sbg * 16;
         q8k_quant16(v, l16, qs, dp, bs);
+    }
+}
+
+// combine of k_fa_dec2's partials (decode v3 = k_fa_dec2 without tickets + this): one 256-thread workgroup
+// per head pair (= one Q8_K block of 256); 4 adjacent lanes share a 4-dim quad of one head and each loads
+// every 4th split (<= 8 x 16-B O loads + 8 x 8-B (m, l) loads per thread, all issued before use), then
+// reduce over the 4 lanes.  One barrier, before the Q8_K quantization of the pair's 256 outputs.
+template <int G, bool QUANT>
+__global__ void __launch_bounds__(256) k_fa_combine2(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
+                                                    float *__restrict__ out, uint8_t *__restrict__ qout, int H, int NS) {
+    constexpr int D = 128, SS = 4, PER = FA2_NS / SS;
+    const int pair = blockIdx.x, tid = threadIdx.x;
+    const int hl = tid >> 7, r = tid & 127, q = r >> 2, sub = r & 3;
+    const int h = 2 * pair + hl, hk = h / G, g = h % G, d = 4 * q;
+    __shared__ float s_res[2 * D];
+    float2 ml[PER];
+    float4 ov[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int s2 = sub + SS * k;
+        ml[k] = s2 < NS ? part_ml[((int64_t)hk * NS + s2) * G + g] : make_float2(-INFINITY, 0.0f);
+        ov[k] = s2 < NS ? *(const float4 *)(part_o + (((int64_t)hk * NS + s2) * G + g) * D + d) : make_float4(0, 0, 0, 0);
+    }
+    float M = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) M = fmaxf(M, ml[k].x);
+    M = fmaxf(M, __shfl_xor(M, 1, 64));
+    M = fmaxf(M, __shfl_xor(M, 2, 64));
+    float L = 0.0f, o0 = 0.0f, o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const float wt = ml[k].x == -INFINITY ? 0.0f : expf(ml[k].x - M);
+        L = fmaf(wt, ml[k].y, L);
+        o0 = fmaf(wt, ov[k].x, o0); o1 = fmaf(wt, ov[k].y, o1);
+        o2 = fmaf(wt, ov[k].z, o2); o3 = fmaf(wt, ov[k].w, o3);
+    }
+#pragma unroll
+    for (int x = 1; x <= 2; x <<= 1) {
+        L += __shfl_xor(L, x, 64);
+        o0 += __shfl_xor(o0, x, 64); o1 += __shfl_xor(o1, x, 64);
+        o2 += __shfl_xor(o2, x, 64); o3 += __shfl_xor(o3, x, 64);
+    }
+    if (sub == 0) {
+        const float4 res = make_float4(o0 / L, o1 / L, o2 / L, o3 / L);
+        *(float4 *)&s_res[hl * D + d] = res;
+        if (out) *(float4 *)(out + (int64_t)h * D + d) = res;
+    }
+    if constexpr (QUANT) {
+        __syncthreads();
+        if (tid < 16) {
+            float v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = s_res[16 * tid + k];
+            const int64_t E = (int64_t)H * D, nsb = E / 256;
+            q8k_quant16(v, tid, (int8_t *)qout + pair * 256, (float *)(qout + E) + pair,
+                        (int16_t *)(qout + E + nsb * 4) + pair * 16);
+        }
     }
 }
 
@@ -673,23 +751,37 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
                     int force_path, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     if (D != 128 || H % HKV || H / HKV > FA_MAXG || (H % 2)) return -1;
-    const bool use_decode = force_path == 1 || force_path == 4 || (force_path == 0 && T <= 16);
+    const bool use_decode = force_path == 1 || force_path == 4 || force_path == 5 || (force_path == 0 && T <= 16);
     static const int v2_env = getenv("KCPP_FA_V2") ? atoi(getenv("KCPP_FA_V2")) : 0;   // in-launch merge: slower end to end (422 vs 443 tok/s)
     const int G0 = H / HKV;
-    if (use_decode && T == 1 && (v2_env || force_path == 4) && HKV <= 64 && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) && (qout == nullptr || G0 >= 2)) {
+    static const int v3_env = getenv("KCPP_FA_V3") ? atoi(getenv("KCPP_FA_V3")) : 0;
+    const bool v3 = (v3_env || force_path == 5) && !(force_path == 4);
+    if (use_decode && T == 1 && (v2_env || v3 || force_path == 4) && HKV <= 64 && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) && (qout == nullptr || G0 >= 2)) {
         const int nkv = n_past_dev ? n_kv_max : n_past + 1;
         const int NS = std::max(1, std::min(FA2_NS, (nkv + 127) / 128));   // >= 1 sub-chunk of 128 keys per split
-        unsigned *tickets = (unsigned *)ws;
+        static const int nomerge_env = getenv("KCPP_FA2_NOMERGE") ? atoi(getenv("KCPP_FA2_NOMERGE")) : 0;
+        const int nomerge = v3 ? 1 : nomerge_env;
+        unsigned *tickets = nomerge == 1 ? nullptr : (unsigned *)ws;
         float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
         float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
         const dim3 grid(NS, HKV);
         switch (G0) {
-        case 1: hipLaunchKernelGGL(k_fa_dec2<1>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale); break;
-        case 2: hipLaunchKernelGGL(k_fa_dec2<2>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale); break;
-        case 4: hipLaunchKernelGGL(k_fa_dec2<4>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale); break;
-        default: hipLaunchKernelGGL(k_fa_dec2<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale); break;
+        case 1: hipLaunchKernelGGL(k_fa_dec2<1>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge); break;
+        case 2: hipLaunchKernelGGL(k_fa_dec2<2>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge); break;
+        case 4: hipLaunchKernelGGL(k_fa_dec2<4>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge); break;
+        default: hipLaunchKernelGGL(k_fa_dec2<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge); break;
         }
         KCPP_CHECK(hipGetLastError());
+        if (v3) {
+#define KCPP_FA_C2(GG)                                                                                                     \
+    case GG:                                                                                                               \
+        if (qout) hipLaunchKernelGGL((k_fa_combine2<GG, true>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS); \
+        else hipLaunchKernelGGL((k_fa_combine2<GG, false>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS);    \
+        break;
+            switch (G0) { KCPP_FA_C2(1) KCPP_FA_C2(2) KCPP_FA_C2(4) KCPP_FA_C2(8) }
+#undef KCPP_FA_C2
+            KCPP_CHECK(hipGetLastError());
+        }
         return 0;
     }
     if (use_decode) {

@@ -198,3 +198,4 @@ def test_rs_columns_and_gemm(env, base, M):
             assert np.array_equal(a_.view(np.uint32), b_.view(np.uint32))
         else:
             _close(b_, a_)
+

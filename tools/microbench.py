@@ -33,6 +33,8 @@ def main():
               (8, 4096, 14336, 32), (8, 4096, 4096, 512), (2, 4096, 4096, 512), (13, 4096, 4096, 512)]
     if os.environ.get("MB_SHAPES") == "prefill":
         shapes = shapes[:8]
+    if os.environ.get("MB_SHAPES") == "fa":
+        shapes = []
     for (t, Kd, N, M) in shapes:
         wb = Kd // K.BLOCK[t][0] * K.BLOCK[t][1] * N
         w = torch.empty(wb, dtype=torch.uint8, device="cuda")
