@@ -12,7 +12,7 @@ import shutil
 import sys
 
 tag = sys.argv[1]
-sub = sys.argv[2] if len(sys.argv) > 2 else "k_gemv_q4k"
+sub = sys.argv[2] if len(sys.argv) > 2 else "k_gemv_rs"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = os.path.join(root, "gpurun_out", "prof_" + tag)
 

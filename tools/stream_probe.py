@@ -113,6 +113,10 @@ def dec():
         ("rs down q6k pro2", 114, F, E, 0, 2, 1),
         ("rs v q6k pro1", 114, E, 1024, 0, 1, 1),
         ("rs head q6k pro1", 114, E, 128256, 0, 1, 1),
+        ("rs glu q4k pro0", 112, E, F, 1, 0, 1),
+        ("rs down q4k pro0", 112, F, E, 0, 0, 1),
+        ("rs down q6k pro0", 114, F, E, 0, 0, 1),
+        ("rs qkv q4k pro0 rope", 112, E, E + 2048, 2, 0, 2),
     ]
     if os.environ.get("PROBE_RS_ONLY"):
         cases = [c for c in cases if c[0].startswith("rs ")]
