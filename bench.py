@@ -26,6 +26,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 LLAMA3_8B = dict(n_vocab=128256, n_embd=4096, n_head=32, n_head_kv=8, n_layer=32, n_ff=14336, n_ctx=4096,
                  eps=1e-5, rope_base=500000.0)
+MIXTRAL_8X7B = dict(n_vocab=32000, n_embd=4096, n_head=32, n_head_kv=8, n_layer=32, n_ff=14336, n_ctx=4096,
+                    eps=1e-5, rope_base=1000000.0, n_expert=8, n_expert_used=2)
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
 
 
@@ -120,6 +122,89 @@ def cpu_baseline(hp, types, threads, n_prompt=32, n_gen=4):
                       "%d-token prefill + %d greedy decode tokens, %d threads" % (n_prompt, n_gen, threads)}
 
 
+def run_model(K, torch, hp, types, n_prompt, ubatch, steps, warmup):
+    """koboldcpp --benchmark semantics on one GPU: prefill n_prompt ids (" 1" pattern) in ubatches, then
+    greedy decode (graph replay + on-device argmax per token).  Weights and inputs resident before timing."""
+    m = K.Model(hp, types, max_ubatch=ubatch)
+    m.synth(1234)
+    prompt = [16 + (i % 2) for i in range(n_prompt)]
+    # warm-up prefill on a short prompt (first touch of buffers / graph capture)
+    m.decode(prompt[:64], 0, want_logits=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m.decode(prompt, 0, want_logits=False)
+    torch.cuda.synchronize()
+    t_pp = time.perf_counter() - t0
+    m.argmax()                            # first generated token; stays on device for the next step
+    n_past = len(prompt)
+    for _ in range(warmup):
+        m.decode_greedy(n_past)
+        n_past += 1
+    steps = min(steps, hp["n_ctx"] - n_past)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m.decode_greedy(n_past)
+        n_past += 1
+    torch.cuda.synchronize()
+    t_tg = time.perf_counter() - t0
+    wb = m.weight_bytes()
+    m.close()
+    return {"dec": steps / t_tg, "pre": n_prompt / t_pp, "t_pp": t_pp, "ms_step": t_tg / steps * 1e3, "steps": steps,
+            "n_past": n_past, "wb": wb}
+
+
+def other_config(args, K, torch):
+    """BASELINE configs[2] (Llama-3-8B all-Q8_0, prefill in ubatches of 32: the batched MFMA mat-mul path,
+    HBM-bound at 32 tokens) and configs[4] (Mixtral-8x7B-shape Q5_K_M, 8 experts top-2:
+    expert-routed decode mat-vecs).  Parity-tested at small sizes in tests/; these are their measurements."""
+    import refharness as R
+    if args.config == "llama3-8b-q8_0-b32":
+        hp = dict(LLAMA3_8B)
+        types = R.uniform_types(hp["n_layer"], R.Q8_0)
+        n_prompt, ub = (args.prompt if args.prompt != 3840 else 1024), 32
+        r = run_model(K, torch, hp, types, n_prompt, ub, min(args.steps, 64), args.warmup)
+        # bytes per ubatch: every layer weight once (the Q8_0 output head runs once per llama_decode call)
+        shapes = R.weight_shapes(hp)
+        layer_bytes = sum(R.row_bytes(t, k) * n for i, ((k, n), t) in enumerate(zip(shapes, types)) if i >= 3)
+        n_ub = -(-n_prompt // ub)
+        t_ub = r["t_pp"] / n_ub
+        gbs = layer_bytes / t_ub / 1e9
+        flops = 2 * sum(k * n for i, (k, n) in enumerate(shapes) if i >= 3 and n > 1) * ub
+        return {"metric": "prefill tok/s at ubatch 32 (Llama-3-8B Q8_0)", "value": round(r["pre"], 1), "unit": "tok/s",
+                "n_gpus": 1, "higher_is_better": True,
+                "dtype": "q8_0 weights x q8_0 activations (exact int dot on f16 MFMA, f32 accum)", "data": "synthetic",
+                "config": {"workload": "llama3-8b-q8_0 prefill %d tokens in ubatches of %d" % (n_prompt, ub),
+                           "model": "Llama-3-8B-shape Q8_0 random-init", "parallelism": "single GPU"},
+                "ms_per_ubatch": round(t_ub * 1e3, 3), "decode_tok_s": round(r["dec"], 2),
+                "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_ubatch": layer_bytes,
+                             "mfma_TFLOPs": round(flops / t_ub / 1e12, 1), "scope": "whole ubatch (all layers)"}}
+    if args.config == "mixtral-8x7b-q5_k_m":
+        hp = dict(MIXTRAL_8X7B)
+        types = R.mixtral_q5_k_m_types(hp["n_layer"])
+        n_prompt = args.prompt if args.prompt != 3840 else 512
+        r = run_model(K, torch, hp, types, n_prompt, args.ubatch, args.steps, args.warmup)
+        shapes = R.weight_shapes(hp)
+        tok_bytes = 0
+        for i, ((k, n), t) in enumerate(zip(shapes, types)):
+            if i == 0:
+                continue                   # token embedding: one row gathered
+            b = R.row_bytes(t, k) * n
+            tok_bytes += b * (hp["n_expert_used"] if R.n_slices(hp, i) > 1 else 1)
+        kv = 2 * hp["n_layer"] * hp["n_head_kv"] * (hp["n_embd"] // hp["n_head"]) * 2 * (r["n_past"] - r["steps"] / 2)
+        gbs = (tok_bytes + kv) / (r["ms_step"] * 1e-3) / 1e9
+        return {"metric": "decode tok/s (Mixtral-8x7B Q5_K_M, top-2 of 8 experts)", "value": round(r["dec"], 2),
+                "unit": "tok/s", "n_gpus": 1, "steps": r["steps"], "warmup": args.warmup,
+                "ms_per_step": round(r["ms_step"], 4), "higher_is_better": True,
+                "dtype": "q5_K/q6_K/q8_0 weights x q8_K/q8_0 activations; f16 KV", "data": "synthetic",
+                "config": {"workload": "mixtral-8x7b-q5_k_m: prefill %d + greedy decode" % n_prompt,
+                           "model": "Mixtral-8x7B-shape Q5_K_M random-init", "parallelism": "single GPU"},
+                "prefill_tok_s": round(r["pre"], 1), "weight_bytes": r["wb"], "bytes_per_token": tok_bytes,
+                "decode_effective_GBps": round(gbs, 1), "decode_hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+    raise SystemExit("unknown --config %s" % args.config)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -131,6 +216,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the dominant-kernel timing (for the rocprofv3 --pmc passes in profiles/)")
+    ap.add_argument("--config", default="llama3-8b-q4_k_m",
+                    choices=["llama3-8b-q4_k_m", "llama3-8b-q8_0-b32", "mixtral-8x7b-q5_k_m"],
+                    help="BASELINE configs[1] (default: the driver's line), configs[2], configs[4]")
     ap.add_argument("--layers", type=int, default=None, help="override n_layer (debug only; invalidates metric)")
     args = ap.parse_args()
 
@@ -148,38 +236,15 @@ def main():
     if args.roofline_only:
         print(json.dumps({"roofline": measure_roofline(K, torch)}))
         return
+    if args.config != "llama3-8b-q4_k_m":
+        print(json.dumps(other_config(args, K, torch)))
+        return
     hp = dict(LLAMA3_8B)
     if args.layers:
         hp["n_layer"] = args.layers
     types = q4_k_m_types(hp["n_layer"])
-    m = K.Model(hp, types, max_ubatch=args.ubatch)
-    m.synth(1234)
-    prompt = [16 + (i % 2) for i in range(args.prompt)]
-    # warm-up prefill on a short prompt (JIT-free, but first-touch of buffers / graph capture)
-    m.decode(prompt[:64], 0, want_logits=False)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    m.decode(prompt, 0, want_logits=False)
-    torch.cuda.synchronize()
-    t_pp = time.perf_counter() - t0
-    tok = m.argmax()                      # first generated token; stays on device for the next step
-    n_past = len(prompt)
-    for _ in range(args.warmup):
-        tok = m.decode_greedy(n_past)
-        n_past += 1
-    steps = min(args.steps, hp["n_ctx"] - n_past)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):                # greedy generation: graph replay + on-device argmax per token
-        tok = m.decode_greedy(n_past)
-        n_past += 1
-    torch.cuda.synchronize()
-    t_tg = time.perf_counter() - t0
-    wb = m.weight_bytes()
-    m.close()
-    dec = steps / t_tg
-    pre = args.prompt / t_pp
-    ms_step = t_tg / steps * 1e3
+    r = run_model(K, torch, hp, types, args.prompt, args.ubatch, args.steps, args.warmup)
+    dec, pre, ms_step, steps, n_past, wb, t_pp = r["dec"], r["pre"], r["ms_step"], r["steps"], r["n_past"], r["wb"], r["t_pp"]
     # decode roofline over the whole token: weights + KV at the mean position
     kv_bytes = 2 * hp["n_layer"] * hp["n_head_kv"] * (hp["n_embd"] // hp["n_head"]) * 2 * (n_past - steps / 2)
     token_gbs = (wb + kv_bytes) / (ms_step * 1e-3) / 1e9

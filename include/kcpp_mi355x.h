@@ -56,6 +56,10 @@ int kcpp_gemv(int type, const void *W, const void *W2, int64_t K, int64_t N, con
 int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M);
 int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream);
+/* Q4_K GEMM kernel generation for later kcpp_gemm calls: 3 = 128x128 tiles, LDS-DMA activation,
+ * register-dequantized weights; 2 = 128(256)x64 tiles, LDS weights; 0 (default; env KCPP_GEMM_V) = 3 when
+ * the grid has >= 384 workgroups, else 2.  Same results bit for bit.  Returns the previous value. */
+int kcpp_gemm_set_variant(int v);
 
 /* Fused single-token mat-vec (koboldcpp_amd/csrc/gemv_dec.hip): args points at a DecArgs struct
  * (koboldcpp_amd/csrc/kcpp_internal.h, size kcpp_gemv_dec_args_size()).  mode 0 plain(+res),

@@ -22,6 +22,7 @@
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
@@ -665,6 +666,318 @@ __global__ void __launch_bounds__(256, TM == 1 ? 2 : 1) k_gemm_kq(const uint8_t 
     }
 }
 
+// ================================================================ Q4_K GEMM v3
+// Same exact-integer formulation and per-super-block epilogue as k_gemm_kq (bit-identical results: every
+// integer partial sum is exact in fp32), re-tiled so the activation is read from L2 once per 128 weight
+// rows instead of once per 64 and the weights never pass through LDS:
+//   * workgroup = 128 tokens x 128 weight rows; wave w = rows [32w, 32w+32) x all 128 tokens (4 MFMA
+//     32x32x16 tiles);
+//   * A (activation, f16 integers) staged in LDS by global_load_lds (16 B per lane; the fragment images
+//     are lane-linear, so the LDS-DMA writes them as they are read), two buffers: super-block sb+1's copy
+//     is in flight while sb is multiplied, one barrier per super-block;
+//   * B: each lane dequantizes its own weight row straight into MFMA fragments from raw Q4_K bytes
+//     loaded one super-block ahead.  The k order inside a sub-block pair is permuted so that a lane's 8
+//     k-values are the low and high nibbles of 4 consecutive qs bytes (one dword -> one fragment):
+//       MFMA step s = 4p + st (p = sub-block pair, st = 0..3), lane half kg = lane >> 5, half e:
+//       e < 4 : k = 64p + 16kg + 4st + e        (sub-block 2p, low nibble of qs byte 32p + 16kg + 4st + e)
+//       e >= 4: k = 64p + 32 + 16kg + 4st + e-4 (sub-block 2p+1, high nibble of the same byte)
+//     and k_act_frag3 writes A in the same order.
+// k_act_frag3: af as k_act_frag with the permuted k order; dyT[sb][Mp] (transposed, so one super-block's
+// 128 token scales are one contiguous 512 B LDS-DMA); bsf as k_act_frag.
+__global__ void k_act_frag3(const uint8_t *__restrict__ act, int64_t K, int64_t M, int64_t Mp, h8v *__restrict__ af,
+                            float *__restrict__ dyT, h8v *__restrict__ bsf) {
+    const int64_t nA = Mp * K / 8, nS = (Mp / 32) * (K / 256) * 64, nD = Mp * (K / 256);
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int8_t *qs = (const int8_t *)act;
+    const float *d = (const float *)(act + M * K);
+    const int16_t *bs = (const int16_t *)(act + M * K + M * (K / 256) * 4);
+    if (i < nA) {
+        const int lane = (int)(i & 63), kg = lane >> 5;
+        const int64_t s16 = (i >> 6) % (K / 16), mt = (i >> 6) / (K / 16);
+        const int64_t m = 32 * mt + (lane & 31);
+        const int p = (int)((s16 >> 2) & 3), st = (int)(s16 & 3);
+        const int64_t k0 = 256 * (s16 >> 4) + 64 * p + 16 * kg + 4 * st;
+        uint32_t lo = 0, hi = 0;
+        if (m < M) {
+            lo = *(const uint32_t *)(qs + m * K + k0);
+            hi = *(const uint32_t *)(qs + m * K + k0 + 32);
+        }
+        h8v r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            r[e] = (_Float16)(int8_t)((lo >> (8 * e)) & 0xFF);
+            r[4 + e] = (_Float16)(int8_t)((hi >> (8 * e)) & 0xFF);
+        }
+        af[i] = r;
+    } else if (i < nA + nS) {
+        const int64_t j = i - nA;
+        const int lane = (int)(j & 63);
+        const int64_t sb = (j >> 6) % (K / 256), mt = (j >> 6) / (K / 256);
+        const int64_t m = 32 * mt + (lane & 31);
+        h8v r;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r[e] = m < M ? (_Float16)bs[m * (K / 16) + sb * 16 + 8 * (lane >> 5) + e] : (_Float16)0;
+        bsf[j] = r;
+    } else if (i < nA + nS + nD) {
+        const int64_t j = i - nA - nS;
+        const int64_t sb = j / Mp, m = j % Mp;
+        dyT[j] = m < M ? d[m * (K / 256) + sb] : 0.0f;
+    }
+}
+
+struct Q4v3Smem {
+    h8v a[2][4][16 * 64];     // activation fragments [buf][token tile][step * 64 + lane]   (64 KiB per buffer)
+    h8v bs[2][4][64];         // Q8_K bsum fragments  [buf][token tile][lane]
+    float dy[2][128];         // activation scale of the super-block per token [buf][token]
+};
+
+// 16 B global -> LDS per lane (LDS address = wave-uniform base + 16 * lane)
+__device__ __forceinline__ void glds16(const void *g, void *lds_base) {
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(g),
+                                     (__attribute__((address_space(3))) void *)(lds_base), 16, 0, 0);
+}
+
+// one qs dword (4 bytes of a sub-block pair) -> fragment: 4 low nibbles * s0, 4 high nibbles * s1 (exact)
+__device__ __forceinline__ h8v frag_q4v3(uint32_t w, float s0, float s1) {
+    const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+    const _Float16 a = (_Float16)s0, ab = (_Float16)(-1024.0f * s0);
+    const _Float16 b = (_Float16)s1, bb = (_Float16)(-1024.0f * s1);
+    const h2v x0 = scale2(bias_lo(lo), a, ab), x1 = scale2(bias_hi(lo), a, ab);
+    const h2v x2 = scale2(bias_lo(hi), b, bb), x3 = scale2(bias_hi(hi), b, bb);
+    h8v r;
+    r[0] = x0[0]; r[1] = x0[1]; r[2] = x1[0]; r[3] = x1[1]; r[4] = x2[0]; r[5] = x2[1]; r[6] = x3[0]; r[7] = x3[1];
+    return r;
+}
+
+__device__ __forceinline__ uint32_t u4c(const uint4 &v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w)); }
+
+// grid: MT * ceil(N / 128) workgroups (MT = Mp / 128), 256 threads, one workgroup per CU (137 KiB LDS).
+// Wave w owns weight rows [32w, 32w+32) of the tile against all 128 tokens (4 MFMA tiles): its B fragments
+// are dequantized once per workgroup (no two waves share a row) and feed 4 MFMAs each.
+template <int LAY>
+__global__ void __launch_bounds__(256, 1) k_gemm_q4v3(const uint8_t *__restrict__ W, int64_t K, int64_t N,
+                                                     const h8v *__restrict__ af, const float *__restrict__ dyT,
+                                                     const h8v *__restrict__ bsf, int64_t M, int64_t Mp, int MT,
+                                                     float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr) {
+    __shared__ Q4v3Smem S;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, kg = lane >> 5;
+    // XCD-aware tile order (as k_gemm_kq): ids with equal id % 8 share a token tile when MT divides 8
+    const int64_t id = blockIdx.x, nwg = gridDim.x;
+    int64_t mt, nt;
+    if (8 % MT == 0 && nwg % 8 == 0) {
+        const int64_t x = id & 7, j = id >> 3;
+        mt = x % MT;
+        nt = j * (8 / MT) + x / MT;
+    } else {
+        mt = id % MT;
+        nt = id / MT;
+    }
+    const int64_t m0 = mt * 128, n0 = nt * 128;
+    const int64_t nsb = K / 256, bpr = nsb;
+    // this lane's weight row; clamped at N (its results are not stored)
+    const int64_t nrow = min(n0 + 32 * wave + lr, N - 1);
+    const uint8_t *hp, *qp;
+    if constexpr (LAY == 1) {
+        hp = W + nrow * 144 * bpr;
+        qp = hp + 16 * bpr + 16 * kg;
+    } else {
+        hp = W + nrow * bpr * 144;
+        qp = hp + 16 + 16 * kg;
+    }
+    constexpr int64_t HS = LAY == 1 ? 16 : 144, QS = LAY == 1 ? 128 : 144;   // bytes per super-block
+    // LDS-DMA sources: wave w copies token tile w (A: 16 KiB, bsums: 1 KiB); wave 0, lanes < 32: dy (512 B)
+    const h8v *asrc = af + (m0 / 32 + wave) * (K / 16) * 64 + lane;
+    const h8v *bsrc = bsf + (m0 / 32 + wave) * nsb * 64 + lane;
+    const float *dsrc = dyT + m0 + 4 * lane;
+    auto stage = [&](int buf, int64_t sb) {
+#pragma unroll
+        for (int st = 0; st < 16; ++st) glds16(asrc + (16 * sb + st) * 64, &S.a[buf][wave][st * 64]);
+        glds16(bsrc + sb * 64, &S.bs[buf][wave][0]);
+        if (wave == 0 && lane < 32) glds16(dsrc + sb * Mp, &S.dy[buf][0]);
+    };
+    uint4 hn, qn[4];
+    auto load_raw = [&](int64_t sb) {
+        hn = ldg16(hp + HS * sb);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) qn[p] = ldg16(qp + QS * sb + 32 * p);
+    };
+
+    f16acc tot[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tot[j][i] = 0.0f;
+    stage(0, 0);
+    load_raw(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    for (int64_t sb = 0; sb < nsb; ++sb) {
+        const int buf = (int)(sb & 1);
+        const uint4 hc = hn;
+        uint4 qc[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) qc[p] = qn[p];
+        if (sb + 1 < nsb) {
+            stage(buf ^ 1, sb + 1);
+            load_raw(sb + 1);
+        }
+        f16acc acc[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[j][i] = 0.0f;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            int s0, s1, m_;
+            k4_sm(hc, 2 * p, s0, m_);
+            k4_sm(hc, 2 * p + 1, s1, m_);
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const h8v b = frag_q4v3(u4c(qc[p], st), (float)s0, (float)s1);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(S.a[buf][j][(4 * p + st) * 64 + lane], b, acc[j], 0, 0, 0);
+            }
+        }
+        // epilogue: tot -= dy * dmin * (sum_j m_j bsum_j), then tot += dy * (d * S)  (k_gemm_kq's order)
+        h8v bm;                                   // mins of sub-blocks 4kg .. 4kg+3, each for its two 16-groups
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            int sc_, mn_;
+            k4_sm(hc, 4 * kg + e, sc_, mn_);
+            bm[2 * e] = (_Float16)mn_;
+            bm[2 * e + 1] = (_Float16)mn_;
+        }
+        const float dw = h2f((uint16_t)(hc.x & 0xFFFF)), dm = h2f((uint16_t)(hc.x >> 16));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            float dyv[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = *(const float4 *)&S.dy[buf][32 * j + 8 * q + 4 * kg];
+                dyv[4 * q] = v.x; dyv[4 * q + 1] = v.y; dyv[4 * q + 2] = v.z; dyv[4 * q + 3] = v.w;
+            }
+            f16acc accm;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) accm[i] = 0.0f;
+            accm = __builtin_amdgcn_mfma_f32_32x32x16_f16(S.bs[buf][j][lane], bm, accm, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) tot[j][r] = fmaf(-__fmul_rn(dyv[r], dm), accm[r], tot[j][r]);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) tot[j][r] = fmaf(dyv[r], __fmul_rn(dw, acc[j][r]), tot[j][r]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    const int64_t n = n0 + 32 * wave + lr;
+    if (n >= N) return;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t t = m0 + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * kg;
+            if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
+        }
+}
+
+// ================================================================ Q8_0 small-batch GEMM (M <= 32)
+// BASELINE config 3 (Llama-3-8B Q8_0, ubatch 32) is HBM-bound: the weights must stream at full bandwidth while
+// only 32 tokens use them.  One v_mfma_i32_32x32x32_i8 per 32-block computes the exact integer block dot of
+// ggml_vec_dot_q8_0_q8_0 (ggml-quants.c:5519) straight from the raw int8 weight and activation bytes (no
+// dequantization, no LDS operand staging); the block result is scaled sumi * (d_w * d_x) in fp32 as the
+// scalar CPU path does.  Workgroup = 128 weight rows (wave: 32 rows x the 32 tokens) x one K range; S K ranges
+// per row tile give >= ~384 workgroups, their fp32 partials [S][32][N] are summed in split order by
+// k_q80s_reduce (deterministic), which also applies the residual or silu(g) * u.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+#define Q80S_UNROLL 8
+
+static int q80s_splits(int64_t K, int64_t N) {
+    const int64_t nt = (N + 127) / 128, nb = K / 32;
+    int64_t S = (384 + nt - 1) / nt;
+    S = std::min<int64_t>(S, std::max<int64_t>(1, nb / (2 * Q80S_UNROLL)));
+    return (int)std::max<int64_t>(S, 1);
+}
+
+// grid (ceil(N / 128), S), 256 threads; dynamic LDS: bps * 32 floats (the activation scales of the K range)
+__global__ void __launch_bounds__(256) k_gemm_q80s(const uint8_t *__restrict__ W, int64_t K, int64_t N,
+                                                  const uint8_t *__restrict__ act, int64_t M, float *__restrict__ part) {
+    extern __shared__ float sdx[];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int lr = lane & 31, kg = lane >> 5;
+    const int64_t nb = K / 32, S = gridDim.y;
+    const int64_t bps = (nb + S - 1) / S, b0 = (int64_t)blockIdx.y * bps, b1 = std::min<int64_t>(nb, b0 + bps);
+    const int64_t n = (int64_t)blockIdx.x * 128 + 32 * wave + lr;
+    const int64_t nrow = std::min<int64_t>(n, N - 1), trow = std::min<int64_t>(lr, M - 1);
+    const int8_t *qx = (const int8_t *)act + trow * K + 16 * kg;                 // A: token lr, bytes 16kg..+15
+    const float *dx = (const float *)(act + M * K);                               // [M][nb]
+    const uint8_t *qw = W + nrow * nb * 32 + 16 * kg;                             // B: row nrow
+    const uint16_t *dw = (const uint16_t *)(W + N * nb * 32) + nrow * nb;
+    for (int64_t i = tid; i < (b1 - b0) * 32; i += 256) {
+        const int64_t b = i >> 5, t = i & 31;
+        sdx[i] = t < M ? dx[t * nb + b0 + b] : 0.0f;
+    }
+    __syncthreads();
+    float tot[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tot[r] = 0.0f;
+    for (int64_t bb = b0; bb < b1; bb += Q80S_UNROLL) {
+        i32x4 a[Q80S_UNROLL], w[Q80S_UNROLL];
+        float dwv[Q80S_UNROLL];
+#pragma unroll
+        for (int u = 0; u < Q80S_UNROLL; ++u) {
+            const int64_t b = std::min<int64_t>(bb + u, b1 - 1);
+            a[u] = *(const i32x4 *)(qx + b * 32);
+            w[u] = *(const i32x4 *)(qw + b * 32);
+            dwv[u] = h2f(dw[b]);
+        }
+#pragma unroll
+        for (int u = 0; u < Q80S_UNROLL; ++u) {
+            if (bb + u >= b1) break;
+            i32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0;
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[u], w[u], acc, 0, 0, 0);
+            const float *sd = sdx + (bb + u - b0) * 32;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 d4 = *(const float4 *)(sd + 8 * q + 4 * kg);
+                const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    tot[4 * q + e] = __fadd_rn(tot[4 * q + e], __fmul_rn((float)acc[4 * q + e], __fmul_rn(dwv[u], dv[e])));
+            }
+        }
+    }
+    if (n >= N) return;
+    float *pp = part + (int64_t)blockIdx.y * 32 * N + n;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int t = (r & 3) + 8 * (r >> 2) + 4 * kg;
+        pp[(int64_t)t * N] = tot[r];
+    }
+}
+
+// Y[t][n] = sum_s part[s][t][n] (+ res), or silu(sum_s g) * (sum_s u) with u partials in part2
+__global__ void k_q80s_reduce(const float *__restrict__ part, const float *__restrict__ part2, int S, int64_t M,
+                              int64_t N, float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M * N) return;
+    const int64_t t = i / N, n = i % N;
+    float g = part[t * N + n];
+    for (int s = 1; s < S; ++s) g = __fadd_rn(g, part[((int64_t)s * 32 + t) * N + n]);
+    if (part2) {
+        float u = part2[t * N + n];
+        for (int s = 1; s < S; ++s) u = __fadd_rn(u, part2[((int64_t)s * 32 + t) * N + n]);
+        Y[t * ldy + n] = (g / (1.0f + expf(-g))) * u;
+    } else {
+        Y[t * ldy + n] = res ? __fadd_rn(g, res[t * ldr + n]) : g;
+    }
+}
+
 __global__ void k_silu_mul_strided(float *__restrict__ y, int64_t ldy, const float *__restrict__ u, int64_t N, int64_t M) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N * M) return;
@@ -681,10 +994,23 @@ static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a
     o_dy = off; off += (Mp * (K / G) * 4 + 255) & ~255LL;
     o_bs = off; off += (Mp * (K / 16) * 2 + 255) & ~255LL;
     o_up = off; off += (M * N * 4 + 255) & ~255LL;
+    if (type == KT_Q8_0) off += 2 * (int64_t)q80s_splits(K, N) * 32 * N * 4;   // small-M split-K partials (g, u)
     return off;
 }
 
+static int g_gemm_variant = -1;
+static int gemm_variant() {
+    if (g_gemm_variant < 0) g_gemm_variant = getenv("KCPP_GEMM_V") ? atoi(getenv("KCPP_GEMM_V")) : 0;
+    return g_gemm_variant;
+}
+
 extern "C" {
+
+int kcpp_gemm_set_variant(int v) {
+    const int old = gemm_variant();
+    g_gemm_variant = v;
+    return old;
+}
 
 int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M) {
     int64_t a, b, c, d;
@@ -705,6 +1031,53 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     _Float16 *bs16 = (_Float16 *)(w8 + o_bs);
     float *up = (float *)(w8 + o_up);
     const int vt = vec_dot_type(type);
+    if (type == KT_Q8_0 && M <= 32 && K % 32 == 0) {
+        const int S = q80s_splits(K, N);
+        float *part = (float *)(w8 + o_up + ((M * N * 4 + 255) & ~255LL));
+        float *part2 = part + (int64_t)S * 32 * N;
+        const int64_t nb = K / 32, bps = (nb + S - 1) / S;
+        const dim3 grid((unsigned)((N + 127) / 128), (unsigned)S);
+        hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 32 * 4, s, (const uint8_t *)W, K, N, (const uint8_t *)act,
+                           M, part);
+        KCPP_CHECK(hipGetLastError());
+        if (mode == 1) {
+            hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 32 * 4, s, (const uint8_t *)W2, K, N,
+                               (const uint8_t *)act, M, part2);
+            KCPP_CHECK(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, mode == 1 ? part2 : nullptr,
+                           S, M, N, Y, ldy, mode == 1 ? nullptr : res, ldr);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
+    // v3 where its 128-row tiles still give >= 1.5 workgroups per CU (measured, tools/gemm_ab.py at M = 512:
+    // gate|up 4096 x 28672 251 vs 301 us; wo / qkv / down with 128-256 workgroups are faster on v2)
+    const int gv = gemm_variant();
+    const bool v3 = gv == 3 || (gv == 0 && Mp / 128 * ((N + 127) / 128) >= 384);
+    if ((type == KT_Q4_K || type == KT_Q4_K_RS) && v3) {
+        const int64_t nth = Mp * K / 8 + (Mp / 32) * (K / 256) * 64 + Mp * (K / 256);
+        hipLaunchKernelGGL(k_act_frag3, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
+                           (h8v *)a16, dy, (h8v *)bs16);
+        KCPP_CHECK(hipGetLastError());
+        const int MT = (int)(Mp / 128);
+        const unsigned nwg = (unsigned)(MT * ((N + 127) / 128));
+        auto launch3 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
+            if (type == KT_Q4_K_RS)
+                hipLaunchKernelGGL(k_gemm_q4v3<1>, dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy,
+                                   (const h8v *)bs16, M, Mp, MT, y, ly, r, lr);
+            else
+                hipLaunchKernelGGL(k_gemm_q4v3<0>, dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy,
+                                   (const h8v *)bs16, M, Mp, MT, y, ly, r, lr);
+            KCPP_CHECK(hipGetLastError());
+            return 0;
+        };
+        int rc = launch3(W, Y, ldy, mode == 1 ? nullptr : res, ldr);
+        if (rc || mode != 1) return rc;
+        if ((rc = launch3(W2, up, N, nullptr, 0))) return rc;
+        hipLaunchKernelGGL(k_silu_mul_strided, dim3((unsigned)((N * M + 255) / 256)), dim3(256), 0, s, Y, ldy, up, N, M);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
     static const int v1 = getenv("KCPP_GEMM_V1") ? atoi(getenv("KCPP_GEMM_V1")) : 0;
     const bool rs = type == KT_Q4_K_RS || type == KT_Q6_K_RS;       // decode layouts: v2 only
     if (rs || (!v1 && (type == KT_Q4_K || type == KT_Q5_K || type == KT_Q6_K))) {

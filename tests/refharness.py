@@ -236,6 +236,17 @@ def moe_types(n_layer, t=Q5_K, router=F16):
     return ty
 
 
+def mixtral_q5_k_m_types(n_layer):
+    """Q5_K_M policy for an 8-expert model (src/llama.cpp:17986-18157): Q5_K default (token_embd too),
+    Q8_0 attn_k / attn_v (n_expert == 8), Q6_K ffn_down_exps on the 'more bits' layers, Q6_K output,
+    F32 router (ffn_gate_inp is never quantized)"""
+    ty = [Q5_K, F32, Q6_K]
+    for il in range(n_layer):
+        more = il < n_layer // 8 or il >= 7 * n_layer // 8 or (il - n_layer // 8) % 3 == 2
+        ty += [F32, Q5_K, Q8_0, Q8_0, Q5_K, F32, Q5_K, Q5_K, Q6_K if more else Q5_K, F32]
+    return ty
+
+
 def q4_k_m_types(n_layer, tok=Q4_K, out=Q6_K):
     """Q4_K_M per-tensor policy (src/llama.cpp:17986-18157): Q6_K for attn_v/ffn_down on 'more bits'
     layers (i<L/8, i>=7L/8, (i-L/8)%3==2), output Q6_K, everything else Q4_K."""

@@ -384,3 +384,23 @@ def test_flash_attn_decode_fused_quant(env, H, HKV):
         ref = R.quantize(R.Q8_K, got.ravel()).reshape(-1, 292)
         gq = host(torch, qa, np.uint8)
         assert np.array_equal(gq[:H * D].reshape(-1, 256), ref[:, 4:260])
+
+
+@pytest.mark.parametrize("Kd,N,M", [(4096, 1024, 32), (14336, 256, 32), (4096, 4096, 9), (2048, 300, 31)])
+def test_gemm_q8_0_small_batch(env, Kd, N, M):
+    """BASELINE config 3's batched Q8_0 path (M <= 32: int8 MFMA block dots, split-K, ordered reduction)
+    vs the C restatement of ggml_vec_dot_q8_0_q8_0 (plain, + residual, silu GLU)"""
+    torch, K = env
+    t = R.Q8_0
+    rng = np.random.default_rng(Kd + N + M)
+    w = R.synth(t, 5, 700, Kd, N)
+    w2 = R.synth(t, 5, 701, Kd, N)
+    X = rng.standard_normal((M, Kd)).astype(np.float32)
+    res = rng.standard_normal((M, N)).astype(np.float32)
+    a = R.mul_mat(t, w, Kd, N, X)
+    b = R.mul_mat(t, w2, Kd, N, X)
+    tol = 3e-6 * max(1.0, np.abs(a).max())
+    np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X), a, rtol=0, atol=tol)
+    np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, res=res), a + res, rtol=0, atol=tol + 1e-6)
+    glu = (a / (1 + np.exp(-a))) * b
+    np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, mode=1, w2=w2), glu, rtol=1e-5, atol=tol)

@@ -118,6 +118,18 @@ def test_e2e_vs_oracle_other_types(K, types_fn):
     assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_F32, (d.max(), np.median(d))
 
 
+def test_q8_0_batch32_prefill_vs_oracle(K):
+    """BASELINE config 3 at test size: all-Q8_0 weights, prompt prefilled in ubatches of 32 tokens (the
+    batched Q8_0 GEMM path at M = 32, plus a ragged last ubatch), teacher-forced vs the restatement"""
+    types = R.uniform_types(R.TINY["n_layer"], R.Q8_0)
+    prompt = [int(v) for v in np.random.default_rng(5).integers(1, 500, size=77)]
+    got = run_gpu(K, types, prompt, 3, ub=32)
+    forced = np.argmax(got, axis=1)[:-1]
+    orc32 = oracle_forced(types, prompt, forced, True)
+    d = np.abs(got - orc32)
+    assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_F32, (d.max(), np.median(d))
+
+
 @pytest.mark.parametrize("types_fn", [lambda n: R.q4_k_m_types(n), lambda n: R.uniform_types(n, R.Q8_0),
                                       lambda n: R.uniform_types(n, R.Q4_0, R.Q5_K)])
 def test_fused_decode_matches_unfused(K, types_fn):

@@ -229,3 +229,18 @@ def test_moe_fused_decode_matches_unfused(env):
         outs.append(np.array(lg))
     d = np.abs(outs[0] - outs[1])
     assert d.max() < TOL_MAX and np.median(d) < 1e-5, (d.max(), np.median(d))
+
+
+@pytest.mark.gpu
+def test_moe_mixtral_q5_k_m_policy_vs_oracle(env):
+    """BASELINE config 5's exact type mix (Q5_K, Q8_0 attn_k/attn_v, Q6_K down on more-bits layers, F32
+    router, Q6_K output) on the tiny MoE shape, teacher-forced vs the f32-accumulation restatement"""
+    torch, K = env
+    hp = R.TINY_MOE                     # 2 layers: layer 1 is a "more bits" layer (Q6_K ffn_down_exps)
+    types = R.mixtral_q5_k_m_types(hp["n_layer"])
+    prompt = [int(v) for v in np.random.default_rng(11).integers(1, 500, size=37)]
+    got = run_gpu(K, types, prompt, 4, hp=hp)
+    forced = np.argmax(got, axis=1)[:-1]
+    orc32 = oracle_forced(types, prompt, forced, True, hp=hp)
+    d = np.abs(got - orc32)
+    assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_F32, (d.max(), np.median(d))

@@ -199,3 +199,36 @@ def test_rs_columns_and_gemm(env, base, M):
         else:
             _close(b_, a_)
 
+
+
+@pytest.mark.parametrize("base", [R.Q4_K, "rs"])
+@pytest.mark.parametrize("Kd,N,M", [(4096, 512, 37), (4096, 640, 128), (2048, 1024, 300), (14336, 256, 512),
+                                    (4096, 192, 17)])
+def test_gemm_v3_matches_v2_bitwise(env, base, Kd, N, M):
+    """Q4_K GEMM v3 (128x128 tiles, LDS-DMA activation, register-dequantized weights, permuted k order)
+    against v2 (LDS weight tiles, natural k order): every integer partial sum is exact in fp32, so the two
+    must agree bit for bit, for both layouts, plain+residual and GLU modes, ragged M and N"""
+    torch, K = env
+    t = RS[R.Q4_K] if base == "rs" else R.Q4_K
+    s = sptr(torch)
+    X = torch.randn(M, Kd, generator=torch.Generator(device="cpu").manual_seed(M + Kd)).cuda()
+    act = torch.zeros(K.act_bytes(R.Q4_K, Kd, M), dtype=torch.uint8, device="cuda")
+    K.call("kcpp_quantize_act", K.vec_dot_type(R.Q4_K), X.data_ptr(), Kd, act.data_ptr(), Kd, M, s)
+    res = torch.randn(M, N).cuda()
+    W, W2 = _synth(torch, K, t, Kd, N, 3), _synth(torch, K, t, Kd, N, 4)
+    ws = torch.empty(K.raw().kcpp_gemm_workspace_bytes(t, Kd, N, M), dtype=torch.uint8, device="cuda")
+    outs = {}
+    try:
+        for v in (2, 3):
+            K.raw().kcpp_gemm_set_variant(v)
+            for mode in (0, 1):
+                Y = torch.full((M, N), float("nan"), device="cuda")
+                K.call("kcpp_gemm", t, W.data_ptr(), W2.data_ptr() if mode == 1 else None, Kd, N, act.data_ptr(), M,
+                       Y.data_ptr(), N, res.data_ptr() if mode == 0 else None, N, mode, ws.data_ptr(), s)
+                torch.cuda.synchronize()
+                outs[v, mode] = Y.cpu().numpy()
+    finally:
+        K.raw().kcpp_gemm_set_variant(0)
+    for mode in (0, 1):
+        assert np.isfinite(outs[3, mode]).all()
+        assert np.array_equal(outs[2, mode].view(np.uint32), outs[3, mode].view(np.uint32)), mode
