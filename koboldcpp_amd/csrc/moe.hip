@@ -5,7 +5,8 @@
 // MoE mat-mul.  Here:
 //   * k_moe_route: router logits (F16 weights: the activation rounded to f16 first, as the CPU's
 //     vec_dot_f16 does; or F32), softmax (ggml_float sum), top-k by the CPU argsort's exchange order,
-//     weights normalized by their sum -- one workgroup per token, results stay on the device;
+//     weights normalized by their sum -- one workgroup per token (wave w: experts w, w+4, ..., all loads of
+//     an expert in flight at once), results stay on the device;
 //   * decode reads the expert id inside the expert mat-vec kernels (DecArgs.eid), so a whole token
 //     remains one hipGraph replay with no host round trip;
 //   * prefill groups tokens per expert on the host (one sync per layer, like the reference) and runs
@@ -23,29 +24,40 @@ __global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, 
                                                    float *__restrict__ wts) {
     const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const float *xr = x + (int64_t)t * ldx;
-    __shared__ float s_part[4][MOE_MAX_EXPERT];
     __shared__ float s_logit[MOE_MAX_EXPERT];
-    for (int e = 0; e < NE; ++e) {
-        float acc = 0.0f;
-        for (int i = tid; i < K; i += 256) {
-            float xv = xr[i], wv;
-            if constexpr (WT == KT_F16) {
-                xv = h2f(f2h(xv));                      // ggml converts src1 to the F16 vec_dot_type
-                wv = h2f(((const uint16_t *)w)[(int64_t)e * K + i]);
-            } else {
-                wv = ((const float *)w)[(int64_t)e * K + i];
+    // wave w: experts w, w+4, ...; lane: 4 consecutive elements per 256-element step, 4 steps in flight
+    for (int e = wave; e < NE; e += 4) {
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int i0 = 4 * lane; i0 < K; i0 += 1024) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + 256 * u;
+                if (i >= K) break;
+                float4 xv = *(const float4 *)(xr + i);
+                float4 wv;
+                if constexpr (WT == KT_F16) {
+                    // ggml converts src1 to the F16 vec_dot_type
+                    xv = make_float4(h2f(f2h(xv.x)), h2f(f2h(xv.y)), h2f(f2h(xv.z)), h2f(f2h(xv.w)));
+                    const uint2 h = *(const uint2 *)((const uint16_t *)w + (int64_t)e * K + i);
+                    wv = make_float4(h2f(h.x & 0xFFFF), h2f(h.x >> 16), h2f(h.y & 0xFFFF), h2f(h.y >> 16));
+                } else {
+                    wv = *(const float4 *)((const float *)w + (int64_t)e * K + i);
+                }
+                acc[u] = fmaf(xv.x, wv.x, acc[u]);
+                acc[u] = fmaf(xv.y, wv.y, acc[u]);
+                acc[u] = fmaf(xv.z, wv.z, acc[u]);
+                acc[u] = fmaf(xv.w, wv.w, acc[u]);
             }
-            acc = fmaf(xv, wv, acc);
         }
-        acc = wave_sum(acc);
-        if (lane == 0) s_part[wave][e] = acc;
+        const float a = wave_sum((acc[0] + acc[1]) + (acc[2] + acc[3]));
+        if (lane == 0) s_logit[e] = a;
     }
     __syncthreads();
     if (tid != 0) return;
     float p[MOE_MAX_EXPERT];
     float mx = -INFINITY;
     for (int e = 0; e < NE; ++e) {
-        p[e] = (s_part[0][e] + s_part[1][e]) + (s_part[2][e] + s_part[3][e]);
+        p[e] = s_logit[e];
         mx = fmaxf(mx, p[e]);
     }
     double sum = 0.0;                                    // ggml_vec_soft_max_f32: ggml_float sum
@@ -98,6 +110,7 @@ extern "C" {
 int kcpp_moe_route(const float *x, int64_t ldx, const void *w_router, int wtype, int64_t K, int n_expert, int k,
                    int32_t *ids, float *weights, int T, void *stream) {
     if (n_expert < 1 || n_expert > MOE_MAX_EXPERT || k < 1 || k > n_expert) return -1;
+    if (K % 4 || ldx % 4) return -1;                    // float4 / 4-half loads
     hipStream_t s = (hipStream_t)stream;
     if (wtype == KT_F16)
         hipLaunchKernelGGL(k_moe_route<KT_F16>, dim3(T), dim3(256), 0, s, x, ldx, w_router, (int)K, n_expert, k, ids, weights);
