@@ -751,17 +751,22 @@ __device__ __forceinline__ h8v frag_q4v3(uint32_t w, float s0, float s1) {
 
 __device__ __forceinline__ uint32_t u4c(const uint4 &v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w)); }
 
-// grid: MT * ceil(N / 128) workgroups (MT = Mp / 128), 256 threads, one workgroup per CU (137 KiB LDS).
-// Wave w owns weight rows [32w, 32w+32) of the tile against all 128 tokens (4 MFMA tiles): its B fragments
-// are dequantized once per workgroup (no two waves share a row) and feed 4 MFMAs each.
-template <int LAY>
-__global__ void __launch_bounds__(256, 1) k_gemm_q4v3(const uint8_t *__restrict__ W, int64_t K, int64_t N,
-                                                     const h8v *__restrict__ af, const float *__restrict__ dyT,
-                                                     const h8v *__restrict__ bsf, int64_t M, int64_t Mp, int MT,
-                                                     float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr) {
+// grid: MT * ceil(N / 128) workgroups (MT = Mp / 128), 64 NW threads, one workgroup per CU (137 KiB LDS).
+// Wave w owns weight rows [32 (w % 4), +32) of the tile against the TPW = 16 / NW token tiles
+// [TPW (w / 4), +TPW): NW = 4 dequantizes every B fragment once per workgroup and feeds it to 4 MFMAs; NW = 8
+// (two waves per SIMD, so one wave's LDS reads and dequantization hide under the other's MFMAs) dequantizes
+// each row twice.
+template <int LAY, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restrict__ W, int64_t K, int64_t N,
+                                                         const h8v *__restrict__ af, const float *__restrict__ dyT,
+                                                         const h8v *__restrict__ bsf, int64_t M, int64_t Mp, int MT,
+                                                         float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr) {
+    constexpr int TPW = 16 / NW;              // token tiles per wave
+    constexpr int SPW = 16 * 4 / NW;          // A staging: LDS-DMA steps per wave and super-block
     __shared__ Q4v3Smem S;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave & 3, wt = wave >> 2;
     const int lr = lane & 31, kg = lane >> 5;
     // XCD-aware tile order (as k_gemm_kq): ids with equal id % 8 share a token tile when MT divides 8
     const int64_t id = blockIdx.x, nwg = gridDim.x;
@@ -777,7 +782,7 @@ __global__ void __launch_bounds__(256, 1) k_gemm_q4v3(const uint8_t *__restrict_
     const int64_t m0 = mt * 128, n0 = nt * 128;
     const int64_t nsb = K / 256, bpr = nsb;
     // this lane's weight row; clamped at N (its results are not stored)
-    const int64_t nrow = min(n0 + 32 * wave + lr, N - 1);
+    const int64_t nrow = min(n0 + 32 * wr + lr, N - 1);
     const uint8_t *hp, *qp;
     if constexpr (LAY == 1) {
         hp = W + nrow * 144 * bpr;
@@ -787,14 +792,16 @@ __global__ void __launch_bounds__(256, 1) k_gemm_q4v3(const uint8_t *__restrict_
         qp = hp + 16 + 16 * kg;
     }
     constexpr int64_t HS = LAY == 1 ? 16 : 144, QS = LAY == 1 ? 128 : 144;   // bytes per super-block
-    // LDS-DMA sources: wave w copies token tile w (A: 16 KiB, bsums: 1 KiB); wave 0, lanes < 32: dy (512 B)
-    const h8v *asrc = af + (m0 / 32 + wave) * (K / 16) * 64 + lane;
-    const h8v *bsrc = bsf + (m0 / 32 + wave) * nsb * 64 + lane;
+    // LDS-DMA: wave w copies steps [SPW (w / 4), +SPW) of token tile w % 4 (16 KiB per tile and super-block);
+    // waves 0-3 the bsum fragments of tile w; wave 0, lanes < 32: dy (512 B)
+    const int st0 = SPW * (wave >> 2);
+    const h8v *asrc = af + (m0 / 32 + wr) * (K / 16) * 64 + lane;
+    const h8v *bsrc = bsf + (m0 / 32 + wr) * nsb * 64 + lane;
     const float *dsrc = dyT + m0 + 4 * lane;
     auto stage = [&](int buf, int64_t sb) {
 #pragma unroll
-        for (int st = 0; st < 16; ++st) glds16(asrc + (16 * sb + st) * 64, &S.a[buf][wave][st * 64]);
-        glds16(bsrc + sb * 64, &S.bs[buf][wave][0]);
+        for (int st = 0; st < SPW; ++st) glds16(asrc + (16 * sb + st0 + st) * 64, &S.a[buf][wr][(st0 + st) * 64]);
+        if (wave < 4) glds16(bsrc + sb * 64, &S.bs[buf][wr][0]);
         if (wave == 0 && lane < 32) glds16(dsrc + sb * Mp, &S.dy[buf][0]);
     };
     uint4 hn, qn[4];
@@ -804,9 +811,9 @@ __global__ void __launch_bounds__(256, 1) k_gemm_q4v3(const uint8_t *__restrict_
         for (int p = 0; p < 4; ++p) qn[p] = ldg16(qp + QS * sb + 32 * p);
     };
 
-    f16acc tot[4];
+    f16acc tot[TPW];
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < TPW; ++j)
 #pragma unroll
         for (int i = 0; i < 16; ++i) tot[j][i] = 0.0f;
     stage(0, 0);
@@ -824,23 +831,35 @@ __global__ void __launch_bounds__(256, 1) k_gemm_q4v3(const uint8_t *__restrict_
             stage(buf ^ 1, sb + 1);
             load_raw(sb + 1);
         }
-        f16acc acc[4];
+        f16acc acc[TPW];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < TPW; ++j)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[j][i] = 0.0f;
+        // 16 MFMA steps; the A fragments of step s+1 are read from LDS before step s's MFMAs are issued
+        const h8v *abase = &S.a[buf][TPW * wt][lane];
+        h8v an[TPW];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            int s0, s1, m_;
-            k4_sm(hc, 2 * p, s0, m_);
-            k4_sm(hc, 2 * p + 1, s1, m_);
+        for (int j = 0; j < TPW; ++j) an[j] = abase[j * 1024];
+        int s0 = 0, s1 = 0;
 #pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                const h8v b = frag_q4v3(u4c(qc[p], st), (float)s0, (float)s1);
+        for (int s = 0; s < 16; ++s) {
+            h8v ac[TPW];
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(S.a[buf][j][(4 * p + st) * 64 + lane], b, acc[j], 0, 0, 0);
+            for (int j = 0; j < TPW; ++j) ac[j] = an[j];
+            if (s + 1 < 16) {
+#pragma unroll
+                for (int j = 0; j < TPW; ++j) an[j] = abase[j * 1024 + (s + 1) * 64];
             }
+            const int p = s >> 2, st = s & 3;
+            if (st == 0) {
+                int m_;
+                k4_sm(hc, 2 * p, s0, m_);
+                k4_sm(hc, 2 * p + 1, s1, m_);
+            }
+            const h8v b = frag_q4v3(u4c(qc[p], st), (float)s0, (float)s1);
+#pragma unroll
+            for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac[j], b, acc[j], 0, 0, 0);
         }
         // epilogue: tot -= dy * dmin * (sum_j m_j bsum_j), then tot += dy * (d * S)  (k_gemm_kq's order)
         h8v bm;                                   // mins of sub-blocks 4kg .. 4kg+3, each for its two 16-groups
@@ -853,17 +872,18 @@ __global__ void __launch_bounds__(256, 1) k_gemm_q4v3(const uint8_t *__restrict_
         }
         const float dw = h2f((uint16_t)(hc.x & 0xFFFF)), dm = h2f((uint16_t)(hc.x >> 16));
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < TPW; ++j) {
+            const int tt = TPW * wt + j;
             float dyv[16];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const float4 v = *(const float4 *)&S.dy[buf][32 * j + 8 * q + 4 * kg];
+                const float4 v = *(const float4 *)&S.dy[buf][32 * tt + 8 * q + 4 * kg];
                 dyv[4 * q] = v.x; dyv[4 * q + 1] = v.y; dyv[4 * q + 2] = v.z; dyv[4 * q + 3] = v.w;
             }
             f16acc accm;
 #pragma unroll
             for (int i = 0; i < 16; ++i) accm[i] = 0.0f;
-            accm = __builtin_amdgcn_mfma_f32_32x32x16_f16(S.bs[buf][j][lane], bm, accm, 0, 0, 0);
+            accm = __builtin_amdgcn_mfma_f32_32x32x16_f16(S.bs[buf][tt][lane], bm, accm, 0, 0, 0);
 #pragma unroll
             for (int r = 0; r < 16; ++r) tot[j][r] = fmaf(-__fmul_rn(dyv[r], dm), accm[r], tot[j][r]);
 #pragma unroll
@@ -872,13 +892,13 @@ __global__ void __launch_bounds__(256, 1) k_gemm_q4v3(const uint8_t *__restrict_
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
     }
-    const int64_t n = n0 + 32 * wave + lr;
+    const int64_t n = n0 + 32 * wr + lr;
     if (n >= N) return;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < TPW; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int64_t t = m0 + 32 * j + (r & 3) + 8 * (r >> 2) + 4 * kg;
+            const int64_t t = m0 + 32 * (TPW * wt + j) + (r & 3) + 8 * (r >> 2) + 4 * kg;
             if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
         }
 }
@@ -1061,13 +1081,14 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         KCPP_CHECK(hipGetLastError());
         const int MT = (int)(Mp / 128);
         const unsigned nwg = (unsigned)(MT * ((N + 127) / 128));
+        static const int nw_env = getenv("KCPP_GEMM_V3_WAVES") ? atoi(getenv("KCPP_GEMM_V3_WAVES")) : 8;
         auto launch3 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
-            if (type == KT_Q4_K_RS)
-                hipLaunchKernelGGL(k_gemm_q4v3<1>, dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy,
-                                   (const h8v *)bs16, M, Mp, MT, y, ly, r, lr);
-            else
-                hipLaunchKernelGGL(k_gemm_q4v3<0>, dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy,
-                                   (const h8v *)bs16, M, Mp, MT, y, ly, r, lr);
+#define KCPP_V3(L_, NW_)                                                                                                    \
+    hipLaunchKernelGGL((k_gemm_q4v3<L_, NW_>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, \
+                       (const h8v *)bs16, M, Mp, MT, y, ly, r, lr)
+            if (type == KT_Q4_K_RS) { if (nw_env == 4) KCPP_V3(1, 4); else KCPP_V3(1, 8); }
+            else { if (nw_env == 4) KCPP_V3(0, 4); else KCPP_V3(0, 8); }
+#undef KCPP_V3
             KCPP_CHECK(hipGetLastError());
             return 0;
         };
