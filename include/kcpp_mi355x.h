@@ -98,6 +98,9 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
 /* the MFMA prefill kernel alone (koboldcpp_amd/csrc/attn_mfma.hip); -3 when the shape is not covered */
 int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, int T, int H,
                                  int HKV, int D, int n_past, float scale, void *stream);
+/* MFMA prefill kernel generation: 2 (default; env KCPP_FA_MFMA_V) = next tile prefetched, V read through the
+ * LDS transpose; 1 = the first version; 0 = the default.  Bit-identical outputs.  Returns the previous value. */
+int kcpp_fa_prefill_set_variant(int v);
 /* MoE router (llm_build_moe_ffn, src/llama.cpp:9435-9460): logits = W_router . x (W F16 -> x rounded
  * to f16 like the CPU vec_dot_f16, or F32), softmax, top-k (argsort descending), weights normalized to
  * sum 1; ids/weights [T][k] */

@@ -404,3 +404,29 @@ def test_gemm_q8_0_small_batch(env, Kd, N, M):
     np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, res=res), a + res, rtol=0, atol=tol + 1e-6)
     glu = (a / (1 + np.exp(-a))) * b
     np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, mode=1, w2=w2), glu, rtol=1e-5, atol=tol)
+
+
+@pytest.mark.parametrize("T,n_past", [(16, 0), (37, 0), (200, 60), (512, 300), (512, 3328), (70, 130)])
+def test_flash_attn_prefill_mfma_v2_bitwise(env, T, n_past):
+    """MFMA prefill v2 (next-tile prefetch, V through ds_read_b64_tr_b16) keeps v1's key order and summation
+    order: outputs must be identical bit for bit"""
+    torch, K = env
+    H, HKV, D = 32, 8, 128
+    n_ctx = n_past + T + 64
+    rng = np.random.default_rng(T + 7 * n_past)
+    q = rng.standard_normal((T, H, D)).astype(np.float16)
+    kcache = (rng.standard_normal((n_ctx, HKV, D)) * 0.5).astype(np.float16)
+    vcache = rng.standard_normal((n_ctx, HKV, D)).astype(np.float16)
+    q16, kd, vd = dev(torch, q), dev(torch, kcache), dev(torch, vcache)
+    outs = []
+    try:
+        for v in (1, 2):
+            K.raw().kcpp_fa_prefill_set_variant(v)
+            out = torch.full((T, H, D), float("nan"), dtype=torch.float32, device="cuda")
+            K.call("kcpp_flash_attn_prefill_mfma", q16.data_ptr(), kd.data_ptr(), vd.data_ptr(), out.data_ptr(), T, H, HKV,
+                   D, n_past, float(1.0 / np.sqrt(D)), sptr(torch))
+            outs.append(host(torch, out, np.float32))
+    finally:
+        K.raw().kcpp_fa_prefill_set_variant(0)
+    assert np.isfinite(outs[1]).all()
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
