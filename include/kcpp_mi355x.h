@@ -60,6 +60,11 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
  * register-dequantized weights; 2 = 128(256)x64 tiles, LDS weights; 0 (default; env KCPP_GEMM_V) = 3 when
  * the grid has >= 384 workgroups, else 2.  Same results bit for bit.  Returns the previous value. */
 int kcpp_gemm_set_variant(int v);
+/* Q8_0 at M <= 32 over nseg <= 3 weights whose outputs sit back to back in Y's columns (q|k|v of one layer,
+ * one activation quantization and one launch instead of three); every N_i but the last a multiple of 128;
+ * ws from kcpp_gemm_workspace_bytes(KT_Q8_0, K, sum N_i, M) */
+int kcpp_gemm_q80_segs(const void *const *W, const int64_t *N, int nseg, int64_t K, const void *act, int64_t M, float *Y,
+                       int64_t ldy, void *ws, void *stream);
 
 /* Fused single-token mat-vec (koboldcpp_amd/csrc/gemv_dec.hip): args points at a DecArgs struct
  * (koboldcpp_amd/csrc/kcpp_internal.h, size kcpp_gemv_dec_args_size()).  mode 0 plain(+res),

@@ -922,8 +922,15 @@ static int q80s_splits(int64_t K, int64_t N) {
     return (int)std::max<int64_t>(S, 1);
 }
 
-// grid (ceil(N / 128), S), 256 threads; dynamic LDS: bps * 32 floats (the activation scales of the K range)
-__global__ void __launch_bounds__(256) k_gemm_q80s(const uint8_t *__restrict__ W, int64_t K, int64_t N,
+// up to 3 weight segments back to back in the output columns (q|k|v); segment boundaries multiples of 128
+struct Q80Segs {
+    const uint8_t *W[3];
+    int64_t N[3];
+    int nseg;
+};
+
+// grid (ceil(Ntot / 128), S), 256 threads; dynamic LDS: bps * 32 floats (the activation scales of the K range)
+__global__ void __launch_bounds__(256) k_gemm_q80s(const Q80Segs sg, int64_t K, int64_t N,
                                                   const uint8_t *__restrict__ act, int64_t M, float *__restrict__ part) {
     extern __shared__ float sdx[];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -931,11 +938,17 @@ __global__ void __launch_bounds__(256) k_gemm_q80s(const uint8_t *__restrict__ W
     const int64_t nb = K / 32, S = gridDim.y;
     const int64_t bps = (nb + S - 1) / S, b0 = (int64_t)blockIdx.y * bps, b1 = std::min<int64_t>(nb, b0 + bps);
     const int64_t n = (int64_t)blockIdx.x * 128 + 32 * wave + lr;
-    const int64_t nrow = std::min<int64_t>(n, N - 1), trow = std::min<int64_t>(lr, M - 1);
+    // this tile's segment (uniform: boundaries are multiples of 128)
+    const int64_t nt0 = (int64_t)blockIdx.x * 128;
+    const int seg = (sg.nseg > 1 && nt0 >= sg.N[0]) ? ((sg.nseg > 2 && nt0 >= sg.N[0] + sg.N[1]) ? 2 : 1) : 0;
+    const int64_t soff = seg == 0 ? 0 : (seg == 1 ? sg.N[0] : sg.N[0] + sg.N[1]);
+    const int64_t Ns = seg == 0 ? sg.N[0] : (seg == 1 ? sg.N[1] : sg.N[2]);
+    const uint8_t *W = seg == 0 ? sg.W[0] : (seg == 1 ? sg.W[1] : sg.W[2]);
+    const int64_t nrow = std::min<int64_t>(n - soff, Ns - 1), trow = std::min<int64_t>(lr, M - 1);
     const int8_t *qx = (const int8_t *)act + trow * K + 16 * kg;                 // A: token lr, bytes 16kg..+15
     const float *dx = (const float *)(act + M * K);                               // [M][nb]
     const uint8_t *qw = W + nrow * nb * 32 + 16 * kg;                             // B: row nrow
-    const uint16_t *dw = (const uint16_t *)(W + N * nb * 32) + nrow * nb;
+    const uint16_t *dw = (const uint16_t *)(W + Ns * nb * 32) + nrow * nb;
     for (int64_t i = tid; i < (b1 - b0) * 32; i += 256) {
         const int64_t b = i >> 5, t = i & 31;
         sdx[i] = t < M ? dx[t * nb + b0 + b] : 0.0f;
@@ -1032,6 +1045,34 @@ int kcpp_gemm_set_variant(int v) {
     return old;
 }
 
+// q|k|v style: nseg <= 3 Q8_0 weights [K][N_i] whose outputs sit back to back in Y's columns, M <= 32,
+// every N_i a multiple of 128; ws from kcpp_gemm_workspace_bytes(KT_Q8_0, K, sum N_i, M)
+int kcpp_gemm_q80_segs(const void *const *W, const int64_t *N, int nseg, int64_t K, const void *act, int64_t M, float *Y,
+                       int64_t ldy, void *ws, void *stream) {
+    if (nseg < 1 || nseg > 3 || M < 1 || M > 32 || K % 32 || !ws) return -1;
+    Q80Segs sg = {{nullptr, nullptr, nullptr}, {0, 0, 0}, nseg};
+    int64_t Ntot = 0;
+    for (int i = 0; i < nseg; ++i) {
+        if (N[i] <= 0 || (N[i] % 128 && i + 1 < nseg)) return -1;
+        sg.W[i] = (const uint8_t *)W[i];
+        sg.N[i] = N[i];
+        Ntot += N[i];
+    }
+    int64_t o_a16, o_dy, o_bs, o_up;
+    ws_layout(KT_Q8_0, K, Ntot, M, o_a16, o_dy, o_bs, o_up);
+    float *part = (float *)((uint8_t *)ws + o_up + ((M * Ntot * 4 + 255) & ~255LL));
+    const int S = q80s_splits(K, Ntot);
+    const int64_t nb = K / 32, bps = (nb + S - 1) / S;
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_gemm_q80s, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), (size_t)bps * 32 * 4, s, sg, K,
+                       Ntot, (const uint8_t *)act, M, part);
+    KCPP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * Ntot + 255) / 256)), dim3(256), 0, s, part, nullptr, S, M, Ntot, Y, ldy,
+                       nullptr, 0);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
 int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M) {
     int64_t a, b, c, d;
     return ws_layout(type, K, N, M, a, b, c, d);
@@ -1057,12 +1098,12 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         float *part2 = part + (int64_t)S * 32 * N;
         const int64_t nb = K / 32, bps = (nb + S - 1) / S;
         const dim3 grid((unsigned)((N + 127) / 128), (unsigned)S);
-        hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 32 * 4, s, (const uint8_t *)W, K, N, (const uint8_t *)act,
-                           M, part);
+        Q80Segs sg = {{(const uint8_t *)W, nullptr, nullptr}, {N, 0, 0}, 1};
+        hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 32 * 4, s, sg, K, N, (const uint8_t *)act, M, part);
         KCPP_CHECK(hipGetLastError());
         if (mode == 1) {
-            hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 32 * 4, s, (const uint8_t *)W2, K, N,
-                               (const uint8_t *)act, M, part2);
+            sg.W[0] = (const uint8_t *)W2;
+            hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 32 * 4, s, sg, K, N, (const uint8_t *)act, M, part2);
             KCPP_CHECK(hipGetLastError());
         }
         hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, mode == 1 ? part2 : nullptr,

@@ -28,6 +28,7 @@ __global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, 
     // wave w: experts w, w+4, ...; lane: 4 consecutive elements per 256-element step, 4 steps in flight
     for (int e = wave; e < NE; e += 4) {
         float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll 4
         for (int i0 = 4 * lane; i0 < K; i0 += 1024) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {

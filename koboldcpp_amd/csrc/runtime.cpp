@@ -656,6 +656,13 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
                 RC(matmul(m, t[2], nullptr, m->act, T, m->qkv + E, LQ, nullptr, 0, 0));
                 RC(matmul(m, t[3], nullptr, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0));
             }
+        } else if (T > 8 && T <= 32 && t[1].type == KT_Q8_0 && t[2].type == KT_Q8_0 && t[3].type == KT_Q8_0 && E % 128 == 0 &&
+                   EKV % 128 == 0) {                 // small-batch Q8_0: one quantization, one q|k|v launch
+            RC(kcpp_rms_norm(m->x, E, (const float *)t[0].d, m->attn, E, nullptr, E, T, hp.eps, s));
+            RC(kcpp_quantize_act(KT_Q8_0, m->attn, E, m->act, E, T, s));
+            const void *Wq[3] = {t[1].d, t[2].d, t[3].d};
+            const int64_t Nq[3] = {E, EKV, EKV};
+            RC(kcpp_gemm_q80_segs(Wq, Nq, 3, E, m->act, T, m->qkv, LQ, m->gemm_ws, s));
         } else {
             RC(kcpp_rms_norm(m->x, E, (const float *)t[0].d, m->attn, E, nullptr, E, T, hp.eps, s));
             for (int j = 1; j <= 3; ++j) {
