@@ -919,6 +919,7 @@ static int q80s_splits(int64_t K, int64_t N) {
     const int64_t nt = (N + 127) / 128, nb = K / 32;
     int64_t S = (384 + nt - 1) / nt;
     S = std::min<int64_t>(S, std::max<int64_t>(1, nb / (2 * Q80S_UNROLL)));
+    S = std::max<int64_t>(S, (nb + 47) / 48);          // <= 48 blocks per split: <= 54 KiB of dynamic LDS
     return (int)std::max<int64_t>(S, 1);
 }
 
@@ -929,11 +930,12 @@ struct Q80Segs {
     int nseg;
 };
 
-// grid (ceil(Ntot / 128), S), 256 threads; dynamic LDS: bps * 32 floats (the activation scales of the K range)
+// grid (ceil(Ntot / 128), S), 256 threads; dynamic LDS bps * 1152 B: the K range's activation fragments + scales
 __global__ void __launch_bounds__(256) k_gemm_q80s(const Q80Segs sg, int64_t K, int64_t N,
                                                   const uint8_t *__restrict__ act, int64_t M, float *__restrict__ part) {
-    extern __shared__ float sdx[];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    extern __shared__ __attribute__((aligned(16))) uint8_t q80_lds[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lr = lane & 31, kg = lane >> 5;
     const int64_t nb = K / 32, S = gridDim.y;
     const int64_t bps = (nb + S - 1) / S, b0 = (int64_t)blockIdx.y * bps, b1 = std::min<int64_t>(nb, b0 + bps);
@@ -949,31 +951,44 @@ __global__ void __launch_bounds__(256) k_gemm_q80s(const Q80Segs sg, int64_t K, 
     const float *dx = (const float *)(act + M * K);                               // [M][nb]
     const uint8_t *qw = W + nrow * nb * 32 + 16 * kg;                             // B: row nrow
     const uint16_t *dw = (const uint16_t *)(W + Ns * nb * 32) + nrow * nb;
+    // the workgroup's activation K range in LDS once (LDS-DMA, 1 KiB fragment image per block) + its scales
+    i32x4 *sA = (i32x4 *)q80_lds;                                                // [bps][64 lanes]
+    float *sdx = (float *)(q80_lds + bps * 1024);                                // [bps][32 tokens]
+    for (int64_t b = wave; b < b1 - b0; b += 4) glds16(qx + (b0 + b) * 32, &sA[b * 64]);
     for (int64_t i = tid; i < (b1 - b0) * 32; i += 256) {
         const int64_t b = i >> 5, t = i & 31;
         sdx[i] = t < M ? dx[t * nb + b0 + b] : 0.0f;
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     float tot[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) tot[r] = 0.0f;
-    for (int64_t bb = b0; bb < b1; bb += Q80S_UNROLL) {
-        i32x4 a[Q80S_UNROLL], w[Q80S_UNROLL];
-        float dwv[Q80S_UNROLL];
+    // weights: the next group of blocks is in flight while the current one is multiplied
+    i32x4 wn[Q80S_UNROLL];
+    float dn[Q80S_UNROLL];
+    auto loadw = [&](int64_t bb) {
 #pragma unroll
         for (int u = 0; u < Q80S_UNROLL; ++u) {
             const int64_t b = std::min<int64_t>(bb + u, b1 - 1);
-            a[u] = *(const i32x4 *)(qx + b * 32);
-            w[u] = *(const i32x4 *)(qw + b * 32);
-            dwv[u] = h2f(dw[b]);
+            wn[u] = *(const i32x4 *)(qw + b * 32);
+            dn[u] = h2f(dw[b]);
         }
+    };
+    loadw(b0);
+    for (int64_t bb = b0; bb < b1; bb += Q80S_UNROLL) {
+        i32x4 wc[Q80S_UNROLL];
+        float dc[Q80S_UNROLL];
+#pragma unroll
+        for (int u = 0; u < Q80S_UNROLL; ++u) { wc[u] = wn[u]; dc[u] = dn[u]; }
+        if (bb + Q80S_UNROLL < b1) loadw(bb + Q80S_UNROLL);
 #pragma unroll
         for (int u = 0; u < Q80S_UNROLL; ++u) {
             if (bb + u >= b1) break;
             i32x16 acc;
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = 0;
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[u], w[u], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(sA[(bb + u - b0) * 64 + lane], wc[u], acc, 0, 0, 0);
             const float *sd = sdx + (bb + u - b0) * 32;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -981,7 +996,7 @@ __global__ void __launch_bounds__(256) k_gemm_q80s(const Q80Segs sg, int64_t K, 
                 const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    tot[4 * q + e] = __fadd_rn(tot[4 * q + e], __fmul_rn((float)acc[4 * q + e], __fmul_rn(dwv[u], dv[e])));
+                    tot[4 * q + e] = __fadd_rn(tot[4 * q + e], __fmul_rn((float)acc[4 * q + e], __fmul_rn(dc[u], dv[e])));
             }
         }
     }
@@ -1064,7 +1079,7 @@ int kcpp_gemm_q80_segs(const void *const *W, const int64_t *N, int nseg, int64_t
     const int S = q80s_splits(K, Ntot);
     const int64_t nb = K / 32, bps = (nb + S - 1) / S;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_gemm_q80s, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), (size_t)bps * 32 * 4, s, sg, K,
+    hipLaunchKernelGGL(k_gemm_q80s, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), (size_t)bps * 1152, s, sg, K,
                        Ntot, (const uint8_t *)act, M, part);
     KCPP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * Ntot + 255) / 256)), dim3(256), 0, s, part, nullptr, S, M, Ntot, Y, ldy,
@@ -1099,11 +1114,11 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         const int64_t nb = K / 32, bps = (nb + S - 1) / S;
         const dim3 grid((unsigned)((N + 127) / 128), (unsigned)S);
         Q80Segs sg = {{(const uint8_t *)W, nullptr, nullptr}, {N, 0, 0}, 1};
-        hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 32 * 4, s, sg, K, N, (const uint8_t *)act, M, part);
+        hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 1152, s, sg, K, N, (const uint8_t *)act, M, part);
         KCPP_CHECK(hipGetLastError());
         if (mode == 1) {
             sg.W[0] = (const uint8_t *)W2;
-            hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 32 * 4, s, sg, K, N, (const uint8_t *)act, M, part2);
+            hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 1152, s, sg, K, N, (const uint8_t *)act, M, part2);
             KCPP_CHECK(hipGetLastError());
         }
         hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, mode == 1 ? part2 : nullptr,
