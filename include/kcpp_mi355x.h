@@ -56,9 +56,9 @@ int kcpp_gemv(int type, const void *W, const void *W2, int64_t K, int64_t N, con
 int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M);
 int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream);
-/* Q4_K GEMM kernel generation for later kcpp_gemm calls: 3 = 128x128 tiles, LDS-DMA activation,
- * register-dequantized weights; 2 = 128(256)x64 tiles, LDS weights; 0 (default; env KCPP_GEMM_V) = 3 when
- * the grid has >= 384 workgroups, else 2.  Same results bit for bit.  Returns the previous value. */
+/* Q4_K GEMM kernel generation for later kcpp_gemm calls: 3 (= 0, the default; env KCPP_GEMM_V) = 128(64) x 128
+ * tiles, LDS-DMA activation, register-dequantized weights; 2 = 128(256) x 64 tiles, LDS weights.  Same results
+ * bit for bit.  Returns the previous value. */
 int kcpp_gemm_set_variant(int v);
 /* Q8_0 at M <= 32 over nseg <= 3 weights whose outputs sit back to back in Y's columns (q|k|v of one layer,
  * one activation quantization and one launch instead of three); every N_i but the last a multiple of 128;

@@ -725,10 +725,10 @@ __global__ void k_act_frag3(const uint8_t *__restrict__ act, int64_t K, int64_t 
     }
 }
 
-struct Q4v3Smem {
-    h8v a[2][4][16 * 64];     // activation fragments [buf][token tile][step * 64 + lane]   (64 KiB per buffer)
-    h8v bs[2][4][64];         // Q8_K bsum fragments  [buf][token tile][lane]
-    float dy[2][128];         // activation scale of the super-block per token [buf][token]
+template <int BMT> struct Q4v3Smem {
+    h8v a[2][BMT][16 * 64];   // activation fragments [buf][token tile][step * 64 + lane]   (16 KiB per tile)
+    h8v bs[2][BMT][64];       // Q8_K bsum fragments  [buf][token tile][lane]
+    float dy[2][32 * BMT];    // activation scale of the super-block per token [buf][token]
 };
 
 // 16 B global -> LDS per lane (LDS address = wave-uniform base + 16 * lane)
@@ -751,19 +751,20 @@ __device__ __forceinline__ h8v frag_q4v3(uint32_t w, float s0, float s1) {
 
 __device__ __forceinline__ uint32_t u4c(const uint4 &v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w)); }
 
-// grid: MT * ceil(N / 128) workgroups (MT = Mp / 128), 64 NW threads, one workgroup per CU (137 KiB LDS).
-// Wave w owns weight rows [32 (w % 4), +32) of the tile against the TPW = 16 / NW token tiles
-// [TPW (w / 4), +TPW): NW = 4 dequantizes every B fragment once per workgroup and feeds it to 4 MFMAs; NW = 8
-// (two waves per SIMD, so one wave's LDS reads and dequantization hide under the other's MFMAs) dequantizes
-// each row twice.
-template <int LAY, int NW>
+// grid: MT * ceil(N / 128) workgroups (MT = Mp / (32 BMT)), 64 NW threads, one workgroup per CU.
+// Workgroup = 32 BMT tokens x 128 weight rows.  Wave w owns weight rows [32 (w % 4), +32) against the
+// TPW = 4 BMT / NW token tiles [TPW (w / 4), +TPW): NW = 4 dequantizes every B fragment once per workgroup and
+// feeds it to TPW MFMAs; NW = 8 (two waves per SIMD, so one wave's LDS reads and dequantization hide under the
+// other's MFMAs) dequantizes each row twice.  BMT = 2 doubles the grid of small-N shapes (wo, q|k|v, down).
+template <int LAY, int NW, int BMT>
 __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                                          const h8v *__restrict__ af, const float *__restrict__ dyT,
                                                          const h8v *__restrict__ bsf, int64_t M, int64_t Mp, int MT,
                                                          float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr) {
-    constexpr int TPW = 16 / NW;              // token tiles per wave
-    constexpr int SPW = 16 * 4 / NW;          // A staging: LDS-DMA steps per wave and super-block
-    __shared__ Q4v3Smem S;
+    constexpr int TPW = 4 * BMT / NW;         // token tiles per wave
+    constexpr int SPW = 16 * BMT / NW;        // A staging: LDS-DMA steps per wave and super-block
+    static_assert(TPW >= 1 && SPW >= 1, "tile shape");
+    __shared__ Q4v3Smem<BMT> S;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave & 3, wt = wave >> 2;
@@ -779,7 +780,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
         mt = id % MT;
         nt = id / MT;
     }
-    const int64_t m0 = mt * 128, n0 = nt * 128;
+    const int64_t m0 = mt * 32 * BMT, n0 = nt * 128;
     const int64_t nsb = K / 256, bpr = nsb;
     // this lane's weight row; clamped at N (its results are not stored)
     const int64_t nrow = min(n0 + 32 * wr + lr, N - 1);
@@ -792,17 +793,17 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
         qp = hp + 16 + 16 * kg;
     }
     constexpr int64_t HS = LAY == 1 ? 16 : 144, QS = LAY == 1 ? 128 : 144;   // bytes per super-block
-    // LDS-DMA: wave w copies steps [SPW (w / 4), +SPW) of token tile w % 4 (16 KiB per tile and super-block);
-    // waves 0-3 the bsum fragments of tile w; wave 0, lanes < 32: dy (512 B)
-    const int st0 = SPW * (wave >> 2);
-    const h8v *asrc = af + (m0 / 32 + wr) * (K / 16) * 64 + lane;
-    const h8v *bsrc = bsf + (m0 / 32 + wr) * nsb * 64 + lane;
+    // LDS-DMA: wave w copies steps [SPW (w / BMT), +SPW) of token tile w % BMT (16 KiB per tile and
+    // super-block); waves < BMT the bsum fragments of tile w; wave 0: dy (128 BMT bytes)
+    const int stt = wave % BMT, st0 = SPW * (wave / BMT);
+    const h8v *asrc = af + (m0 / 32 + stt) * (K / 16) * 64 + lane;
+    const h8v *bsrc = bsf + (m0 / 32 + stt) * nsb * 64 + lane;
     const float *dsrc = dyT + m0 + 4 * lane;
     auto stage = [&](int buf, int64_t sb) {
 #pragma unroll
-        for (int st = 0; st < SPW; ++st) glds16(asrc + (16 * sb + st0 + st) * 64, &S.a[buf][wr][(st0 + st) * 64]);
-        if (wave < 4) glds16(bsrc + sb * 64, &S.bs[buf][wr][0]);
-        if (wave == 0 && lane < 32) glds16(dsrc + sb * Mp, &S.dy[buf][0]);
+        for (int st = 0; st < SPW; ++st) glds16(asrc + (16 * sb + st0 + st) * 64, &S.a[buf][stt][(st0 + st) * 64]);
+        if (wave < BMT) glds16(bsrc + sb * 64, &S.bs[buf][stt][0]);
+        if (wave == 0 && lane < 8 * BMT) glds16(dsrc + sb * Mp, &S.dy[buf][0]);
     };
     uint4 hn, qn[4];
     auto load_raw = [&](int64_t sb) {
@@ -1126,24 +1127,33 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         KCPP_CHECK(hipGetLastError());
         return 0;
     }
-    // v3 where its 128-row tiles still give >= 1.5 workgroups per CU (measured, tools/gemm_ab.py at M = 512:
-    // gate|up 4096 x 28672 251 vs 301 us; wo / qkv / down with 128-256 workgroups are faster on v2)
+    // v3: 128 tokens x 128 rows per workgroup when that gives >= 384 workgroups, else 64 x 128 (BMT = 2);
+    // KCPP_GEMM_V / kcpp_gemm_set_variant: 2 forces v2, 3 forces v3
     const int gv = gemm_variant();
-    const bool v3 = gv == 3 || (gv == 0 && Mp / 128 * ((N + 127) / 128) >= 384);
+    const bool v3 = gv == 3 || gv == 0;
     if ((type == KT_Q4_K || type == KT_Q4_K_RS) && v3) {
         const int64_t nth = Mp * K / 8 + (Mp / 32) * (K / 256) * 64 + Mp * (K / 256);
         hipLaunchKernelGGL(k_act_frag3, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
                            (h8v *)a16, dy, (h8v *)bs16);
         KCPP_CHECK(hipGetLastError());
-        const int MT = (int)(Mp / 128);
-        const unsigned nwg = (unsigned)(MT * ((N + 127) / 128));
-        static const int nw_env = getenv("KCPP_GEMM_V3_WAVES") ? atoi(getenv("KCPP_GEMM_V3_WAVES")) : 8;
+        // measured at M = 512 (tools/gemm_ab.py): 128 x 128 tiles with 8 waves for gate|up (247 vs v2 301 us),
+        // 64 x 128 tiles with 4 waves for the 128-192-tile shapes (wo 44.7 vs 46.7, down 131.5 vs 137.2 us)
+        static const int nw_env = getenv("KCPP_GEMM_V3_WAVES") ? atoi(getenv("KCPP_GEMM_V3_WAVES")) : 0;
+        static const int bmt_env = getenv("KCPP_GEMM_V3_BMT") ? atoi(getenv("KCPP_GEMM_V3_BMT")) : 0;
+        const int64_t nt = (N + 127) / 128;
+        const bool big = Mp / 128 * nt >= 384;
+        const int BMT = bmt_env ? bmt_env : (big ? 4 : 2);
+        const int NWv = nw_env ? nw_env : (big ? 8 : 4);
+        const int MT = (int)(Mp / (32 * BMT));
+        const unsigned nwg = (unsigned)(MT * nt);
         auto launch3 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
-#define KCPP_V3(L_, NW_)                                                                                                    \
-    hipLaunchKernelGGL((k_gemm_q4v3<L_, NW_>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, \
-                       (const h8v *)bs16, M, Mp, MT, y, ly, r, lr)
-            if (type == KT_Q4_K_RS) { if (nw_env == 4) KCPP_V3(1, 4); else KCPP_V3(1, 8); }
-            else { if (nw_env == 4) KCPP_V3(0, 4); else KCPP_V3(0, 8); }
+#define KCPP_V3(L_, NW_, B_)                                                                                                 \
+    hipLaunchKernelGGL((k_gemm_q4v3<L_, NW_, B_>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, \
+                       dy, (const h8v *)bs16, M, Mp, MT, y, ly, r, lr)
+#define KCPP_V3B(L_, B_) { if (NWv == 4) KCPP_V3(L_, 4, B_); else KCPP_V3(L_, 8, B_); }
+            if (type == KT_Q4_K_RS) { if (BMT == 2) KCPP_V3B(1, 2) else KCPP_V3B(1, 4) }
+            else { if (BMT == 2) KCPP_V3B(0, 2) else KCPP_V3B(0, 4) }
+#undef KCPP_V3B
 #undef KCPP_V3
             KCPP_CHECK(hipGetLastError());
             return 0;
