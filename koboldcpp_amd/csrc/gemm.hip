@@ -904,6 +904,178 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
         }
 }
 
+// ================================================================ Q6_K GEMM v3 (row-major decode layout Q6_K_RS)
+// k_gemm_q4v3's structure for Q6_K: activation by LDS-DMA, each wave dequantizes its own 32 rows into MFMA
+// fragments, exact integer weights sc*(q-32) split as 8*(sc>>3)*(q-32) + (sc&7)*(q-32) into two MFMAs (as v2).
+// k order: MFMA step s = 4u + g (u = RS unit (h = u >> 1, lh = u & 1), g = 0..3), lane half kg, half e:
+//   k = 128 h + 16 lh + 32 g + 8 kg + e    -- one 16-element sub-block per fragment (one scale), the lane's
+// bytes 8kg..8kg+7 of the unit's ql-lo / ql-hi / qh planes (dequantize_row_q6_K, ggml-quants.c:2978).
+__global__ void k_act_frag6(const uint8_t *__restrict__ act, int64_t K, int64_t M, int64_t Mp, h8v *__restrict__ af,
+                            float *__restrict__ dyT) {
+    const int64_t nA = Mp * K / 8, nD = Mp * (K / 256);
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int8_t *qs = (const int8_t *)act;
+    const float *d = (const float *)(act + M * K);
+    if (i < nA) {
+        const int lane = (int)(i & 63), kg = lane >> 5;
+        const int64_t s16 = (i >> 6) % (K / 16), mt = (i >> 6) / (K / 16);
+        const int64_t m = 32 * mt + (lane & 31);
+        const int u = (int)((s16 >> 2) & 3), g = (int)(s16 & 3);
+        const int64_t k0 = 256 * (s16 >> 4) + 128 * (u >> 1) + 16 * (u & 1) + 32 * g + 8 * kg;
+        uint2 v = make_uint2(0, 0);
+        if (m < M) v = *(const uint2 *)(qs + m * K + k0);
+        h8v r;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            r[e] = (_Float16)(int8_t)((v.x >> (8 * e)) & 0xFF);
+            r[4 + e] = (_Float16)(int8_t)((v.y >> (8 * e)) & 0xFF);
+        }
+        af[i] = r;
+    } else if (i < nA + nD) {
+        const int64_t j = i - nA;
+        const int64_t sb = j / Mp, m = j % Mp;
+        dyT[j] = m < M ? d[m * (K / 256) + sb] : 0.0f;
+    }
+}
+
+template <int BMT> struct Q6v3Smem {
+    h8v a[2][BMT][16 * 64];
+    float dy[2][32 * BMT];
+};
+
+template <int NW, int BMT>
+__global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6v3(const uint8_t *__restrict__ W, int64_t K, int64_t N,
+                                                         const h8v *__restrict__ af, const float *__restrict__ dyT,
+                                                         int64_t M, int64_t Mp, int MT, float *__restrict__ Y, int64_t ldy,
+                                                         const float *res, int64_t ldr) {
+    constexpr int TPW = 4 * BMT / NW;
+    constexpr int SPW = 16 * BMT / NW;
+    static_assert(TPW >= 1 && SPW >= 1, "tile shape");
+    __shared__ Q6v3Smem<BMT> S;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave & 3, wt = wave >> 2;
+    const int lr = lane & 31, kg = lane >> 5;
+    const int64_t id = blockIdx.x, nwg = gridDim.x;
+    int64_t mt, nt;
+    if (8 % MT == 0 && nwg % 8 == 0) {
+        const int64_t x = id & 7, j = id >> 3;
+        mt = x % MT;
+        nt = j * (8 / MT) + x / MT;
+    } else {
+        mt = id % MT;
+        nt = id / MT;
+    }
+    const int64_t m0 = mt * 32 * BMT, n0 = nt * 128;
+    const int64_t nsb = K / 256, bpr = nsb;
+    const int64_t nrow = min(n0 + 32 * wr + lr, N - 1);
+    const uint8_t *row = W + nrow * 210 * bpr;
+    const uint8_t *plo = row + 8 * kg, *phi = row + 64 * bpr + 8 * kg, *pqh = row + 128 * bpr + 8 * kg;
+    const uint8_t *psc = row + 192 * bpr;
+    const uint16_t *pd = (const uint16_t *)(row + 208 * bpr);
+    const int stt = wave % BMT, st0 = SPW * (wave / BMT);
+    const h8v *asrc = af + (m0 / 32 + stt) * (K / 16) * 64 + lane;
+    const float *dsrc = dyT + m0 + 4 * lane;
+    auto stage = [&](int buf, int64_t sb) {
+#pragma unroll
+        for (int st = 0; st < SPW; ++st) glds16(asrc + (16 * sb + st0 + st) * 64, &S.a[buf][stt][(st0 + st) * 64]);
+        if (wave == 0 && lane < 8 * BMT) glds16(dsrc + sb * Mp, &S.dy[buf][0]);
+    };
+    uint2 nlo[4], nhi[4], nqh[4];
+    uint4 nsc;
+    uint16_t nd;
+    auto load_raw = [&](int64_t sb) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t U = 4 * sb + u;
+            nlo[u] = *(const uint2 *)(plo + 16 * U);
+            nhi[u] = *(const uint2 *)(phi + 16 * U);
+            nqh[u] = *(const uint2 *)(pqh + 16 * U);
+        }
+        nsc = ldg16(psc + 16 * sb);
+        nd = pd[sb];
+    };
+
+    f16acc tot[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tot[j][i] = 0.0f;
+    stage(0, 0);
+    load_raw(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    for (int64_t sb = 0; sb < nsb; ++sb) {
+        const int buf = (int)(sb & 1);
+        uint2 clo[4], chi[4], cqh[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { clo[u] = nlo[u]; chi[u] = nhi[u]; cqh[u] = nqh[u]; }
+        const uint4 csc = nsc;
+        const uint16_t cd = nd;
+        if (sb + 1 < nsb) {
+            stage(buf ^ 1, sb + 1);
+            load_raw(sb + 1);
+        }
+        f16acc acc[TPW];
+#pragma unroll
+        for (int j = 0; j < TPW; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[j][i] = 0.0f;
+        const h8v *abase = &S.a[buf][TPW * wt][lane];
+        h8v an[TPW];
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) an[j] = abase[j * 1024];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            h8v ac[TPW];
+#pragma unroll
+            for (int j = 0; j < TPW; ++j) ac[j] = an[j];
+            if (s + 1 < 16) {
+#pragma unroll
+                for (int j = 0; j < TPW; ++j) an[j] = abase[j * 1024 + (s + 1) * 64];
+            }
+            const int u = s >> 2, g = s & 3;
+            const uint2 P = (g & 1) ? chi[u] : clo[u];
+            const uint2 Hq = cqh[u];
+            const uint32_t v0 = ((P.x >> (4 * (g >> 1))) & 0x0F0F0F0Fu) | (((Hq.x >> (2 * g)) & 0x03030303u) << 4);
+            const uint32_t v1 = ((P.y >> (4 * (g >> 1))) & 0x0F0F0F0Fu) | (((Hq.y >> (2 * g)) & 0x03030303u) << 4);
+            const int scv = (int)(int8_t)((u4c(csc, u) >> (8 * g)) & 0xFF);
+            const h8v bh = frag8_sub(v0, v1, (float)(8 * (scv >> 3)), 32.0f);
+            const h8v bl = frag8_sub(v0, v1, (float)(scv & 7), 32.0f);
+#pragma unroll
+            for (int j = 0; j < TPW; ++j) {
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac[j], bh, acc[j], 0, 0, 0);
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac[j], bl, acc[j], 0, 0, 0);
+            }
+        }
+        const float dw = h2f(cd);
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+            const int tt = TPW * wt + j;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = *(const float4 *)&S.dy[buf][32 * tt + 8 * q + 4 * kg];
+                const float dv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    tot[j][4 * q + e] = fmaf(dv[e], __fmul_rn(dw, acc[j][4 * q + e]), tot[j][4 * q + e]);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    const int64_t n = n0 + 32 * wr + lr;
+    if (n >= N) return;
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t t = m0 + 32 * (TPW * wt + j) + (r & 3) + 8 * (r >> 2) + 4 * kg;
+            if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
+        }
+}
+
 // ================================================================ Q8_0 small-batch GEMM (M <= 32)
 // BASELINE config 3 (Llama-3-8B Q8_0, ubatch 32) is HBM-bound: the weights must stream at full bandwidth while
 // only 32 tokens use them.  One v_mfma_i32_32x32x32_i8 per 32-block computes the exact integer block dot of
@@ -1161,6 +1333,36 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         int rc = launch3(W, Y, ldy, mode == 1 ? nullptr : res, ldr);
         if (rc || mode != 1) return rc;
         if ((rc = launch3(W2, up, N, nullptr, 0))) return rc;
+        hipLaunchKernelGGL(k_silu_mul_strided, dim3((unsigned)((N * M + 255) / 256)), dim3(256), 0, s, Y, ldy, up, N, M);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
+    if (type == KT_Q6_K_RS && v3) {
+        const int64_t nth = Mp * K / 8 + Mp * (K / 256);
+        hipLaunchKernelGGL(k_act_frag6, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
+                           (h8v *)a16, dy);
+        KCPP_CHECK(hipGetLastError());
+        static const int nw6_env = getenv("KCPP_GEMM_V3_WAVES") ? atoi(getenv("KCPP_GEMM_V3_WAVES")) : 0;
+        static const int bmt6_env = getenv("KCPP_GEMM_V3_BMT") ? atoi(getenv("KCPP_GEMM_V3_BMT")) : 0;
+        const int64_t nt = (N + 127) / 128;
+        const bool big = Mp / 128 * nt >= 384;
+        const int BMT = bmt6_env ? bmt6_env : (big ? 4 : 2);
+        const int NWv = nw6_env ? nw6_env : (big ? 8 : 4);
+        const int MT = (int)(Mp / (32 * BMT));
+        const unsigned nwg = (unsigned)(MT * nt);
+        auto launch6 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
+#define KCPP_V6(NW_, B_)                                                                                                   \
+    hipLaunchKernelGGL((k_gemm_q6v3<NW_, B_>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, \
+                       M, Mp, MT, y, ly, r, lr)
+            if (BMT == 2) { if (NWv == 4) KCPP_V6(4, 2); else KCPP_V6(8, 2); }
+            else { if (NWv == 4) KCPP_V6(4, 4); else KCPP_V6(8, 4); }
+#undef KCPP_V6
+            KCPP_CHECK(hipGetLastError());
+            return 0;
+        };
+        int rc = launch6(W, Y, ldy, mode == 1 ? nullptr : res, ldr);
+        if (rc || mode != 1) return rc;
+        if ((rc = launch6(W2, up, N, nullptr, 0))) return rc;
         hipLaunchKernelGGL(k_silu_mul_strided, dim3((unsigned)((N * M + 255) / 256)), dim3(256), 0, s, Y, ldy, up, N, M);
         KCPP_CHECK(hipGetLastError());
         return 0;

@@ -201,7 +201,7 @@ def test_rs_columns_and_gemm(env, base, M):
 
 
 
-@pytest.mark.parametrize("base", [R.Q4_K, "rs"])
+@pytest.mark.parametrize("base", [R.Q4_K, "rs", "rs6"])
 @pytest.mark.parametrize("Kd,N,M", [(4096, 512, 37), (4096, 640, 128), (2048, 1024, 300), (14336, 256, 512),
                                     (4096, 192, 17)])
 def test_gemm_v3_matches_v2_bitwise(env, base, Kd, N, M):
@@ -209,7 +209,7 @@ def test_gemm_v3_matches_v2_bitwise(env, base, Kd, N, M):
     against v2 (LDS weight tiles, natural k order): every integer partial sum is exact in fp32, so the two
     must agree bit for bit, for both layouts, plain+residual and GLU modes, ragged M and N"""
     torch, K = env
-    t = RS[R.Q4_K] if base == "rs" else R.Q4_K
+    t = {"rs": RS[R.Q4_K], "rs6": RS[R.Q6_K]}.get(base, R.Q4_K)
     s = sptr(torch)
     X = torch.randn(M, Kd, generator=torch.Generator(device="cpu").manual_seed(M + Kd)).cuda()
     act = torch.zeros(K.act_bytes(R.Q4_K, Kd, M), dtype=torch.uint8, device="cuda")

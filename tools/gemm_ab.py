@@ -17,11 +17,12 @@ def main():
     s = torch.cuda.current_stream()
     sp = s.cuda_stream
     M = int(os.environ.get("GEMM_M", "512"))
-    t = K.Q4_K_RS
-    for name, Kd, N, mode in [("gate|up", 4096, 28672, 0), ("qkv", 4096, 6144, 0), ("wo", 4096, 4096, 0),
-                              ("down", 14336, 4096, 0), ("glu2", 4096, 14336, 1)]:
+    for name, t, Kd, N, mode in [("gate|up", K.Q4_K_RS, 4096, 28672, 0), ("qkv", K.Q4_K_RS, 4096, 6144, 0),
+                                 ("wo", K.Q4_K_RS, 4096, 4096, 0), ("down", K.Q4_K_RS, 14336, 4096, 0),
+                                 ("glu2", K.Q4_K_RS, 4096, 14336, 1), ("down6", K.Q6_K_RS, 14336, 4096, 0),
+                                 ("v6", K.Q6_K_RS, 4096, 1024, 0)]:
         nrot = 3
-        ws_ = [torch.empty(K.row_bytes(12, Kd) * N, dtype=torch.uint8, device="cuda") for _ in range(nrot)]
+        ws_ = [torch.empty(K.row_bytes(t, Kd) * N, dtype=torch.uint8, device="cuda") for _ in range(nrot)]
         for i, w in enumerate(ws_):
             K.call("kcpp_weight_synth", t, 1, 40 + i, w.data_ptr(), Kd, N, sp)
         X = torch.randn(M, Kd, device="cuda")
@@ -45,7 +46,7 @@ def main():
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / it * 1e3
             fl = 2.0 * M * N * Kd * (2 if mode else 1)
-            print(json.dumps({"shape": name, "M": M, "K": Kd, "N": N, "variant": v, "us": round(us, 1),
+            print(json.dumps({"shape": name, "type": t, "M": M, "K": Kd, "N": N, "variant": v, "us": round(us, 1),
                               "TFLOPs": round(fl / us / 1e6, 1)}), flush=True)
     K.raw().kcpp_gemm_set_variant(0)
 
