@@ -92,6 +92,13 @@ int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t
 int kcpp_rope_table(float *tab_host, int n_pos, int n_dims, float freq_base, float freq_scale, const float *freq_factors,
                     float ext_factor, float attn_factor, float beta_fast, float beta_slow, int n_ctx_orig);
 /* rope(q), rope(k) (NORM mode) + f16 store of K and V into the caches at positions pos.. */
+/* one position's (cos, sin) pairs of the table above; p may be negative (a K-shift distance) */
+int kcpp_rope_row(float *row_host, int p, int n_dims, float freq_base, float freq_scale, float ext_factor,
+                  float attn_factor, float beta_fast, float beta_slow, int n_ctx_orig);
+/* K-shift of cache rows: ks = f16(rope(f32(kc), cs)) per adjacent pair (ggml_compute_forward_rope_f16, NORM),
+ * vs = vc; rows x D f16 each, cs = D floats (cos, sin per pair, device) */
+int kcpp_kv_shift_rows(const uint16_t *kc, const uint16_t *vc, uint16_t *ks, uint16_t *vs, int64_t rows, int D,
+                       const float *cs, void *stream);
 int kcpp_rope_kv(const float *qkv, int64_t ldqkv, float *q_out, uint16_t *q16, uint16_t *kc, uint16_t *vc, int T,
                  int H, int HKV, int D, int n_past, const int32_t *pos_dev, const void *rope_tab, void *stream);
 /* flash attention over the f16 cache (ggml_cuda_flash_attn_ext, fattn.cu:298-345) */
@@ -212,6 +219,10 @@ int kcpp_model_argmax(kcpp_model *m, int32_t *token_out);
  * own argmax computed in the same graph replay and returned (one host sync per token).
  * Requires a stage owning both the embedding and the output head. */
 int kcpp_model_decode_greedy(kcpp_model *m, int n_past, int32_t *token_out);
+/* context shift (koboldcpp PurgeMissingTokens, gpttype_adapter.cpp:1504-1571: llama_kv_cache_seq_rm(p0, p0+diff)
+ * + seq_add(p0+diff, n_past, -diff) + the K-shift of build_k_shift): cache rows [p0+diff, n_past) move to
+ * [p0, n_past-diff) and K is re-rotated by position -diff (rope f16, mode NORM).  Synchronous. */
+int kcpp_model_kv_shift(kcpp_model *m, int p0, int diff, int n_past);
 /* enable/disable hipGraph replay for single-token decode (default on) */
 int kcpp_model_set_graphs(kcpp_model *m, int enable);
 /* single-token decode through the fused mat-vec path (default on); off = one kernel per op */

@@ -4,8 +4,9 @@
 //   load_model  -> GGUF (general.architecture "llama"), layer split over the visible GPUs by
 //                  tensor_split exactly like llm_load_tensors (src/llama.cpp:7000-7036), weights uploaded
 //                  from the mmap'd file in ggml block layout (repacked on the device).
-//   generate    -> memory + prompt tokenized (BOS per the vocab), truncated to keep the newest tokens
-//                  (max_context_length - max_length), the KV prefix shared with the previous request reused
+//   generate    -> prompt and memory tokenized (BOS per the vocab) and assembled as gpttype_adapter.cpp:2794-2887
+//                  (prompt cut from the front, memory kept), context shifting when enabled (PurgeMissingTokens,
+//                  :1504-1571: a removed middle span leaves the KV cache by a K-shift), the KV prefix shared with the previous request reused
 //                  ("fast forward", gpttype_adapter.cpp:2929-2945), prefill in ubatches, sampling, streaming
 //                  text through new_token()/get_pending_output(), stop on EOS / stop sequences / max_length /
 //                  abort; last_process_time / last_eval_time in ms per token (gpttype_adapter.cpp:3513-3526).
@@ -41,6 +42,7 @@ struct Engine {
     std::vector<kcpp_model *> stages;
     std::vector<float *> hidden;            // per stage residual stream (device)
     int ub = 512;
+    bool use_contextshift = false;
     std::vector<int> ctx;                   // tokens whose K/V are in the caches
     std::vector<float> logits;
     ~Engine() { for (auto *m : stages) kcpp_model_free(m); }
@@ -156,6 +158,78 @@ int sample(Engine &e, const generation_inputs &in, const std::vector<int> &recen
     return idx[keep - 1];
 }
 
+
+// ---- context shifting (restatement of model_adapter.cpp:337-430 and gpttype_adapter.cpp:1504-1571)
+bool arr_start_with(const std::vector<int> &t, const std::vector<int> &q) {
+    if (t.size() < q.size()) return false;
+    for (size_t i = 0; i < q.size(); ++i)
+        if (t[i] != q[i]) return false;
+    return true;
+}
+int arr_find_index_of(const std::vector<int> &t, const std::vector<int> &q) {
+    const int ss = (int)q.size(), tas = (int)t.size();
+    if (tas < ss) return -1;
+    for (int i = 0; i < tas; ++i) {
+        bool fail = false;
+        for (int k = 0; k < ss; ++k)
+            if (i + k >= tas || t[i + k] != q[k]) { fail = true; break; }
+        if (!fail) return i;
+    }
+    return -1;
+}
+// longest common contiguous run, first maximum in (i, j) order as the reference's full-table scan finds it;
+// two rolling rows instead of the (m+1) x (n+1) table
+std::vector<int> longest_common_subseq(const std::vector<int> &x, const std::vector<int> &y) {
+    const int m = (int)x.size(), n = (int)y.size();
+    std::vector<int> prev(n + 1, 0), cur(n + 1, 0);
+    int best = 0, best_i = 0;
+    for (int i = 1; i <= m; ++i) {
+        cur[0] = 0;
+        for (int j = 1; j <= n; ++j) {
+            cur[j] = x[i - 1] == y[j - 1] ? prev[j - 1] + 1 : 0;
+            if (cur[j] > best) { best = cur[j]; best_i = i; }
+        }
+        std::swap(prev, cur);
+    }
+    return std::vector<int>(x.begin() + (best_i - best), x.begin() + best_i);
+}
+// PurgeMissingTokens: when the new prompt is the old context with a middle span removed (the front end
+// trimmed it to fit), erase that span from the KV cache (rows move down, K re-rotated) instead of
+// re-processing everything after it.  Returns the number of erased positions.
+int purge_missing_tokens(Engine &e, std::vector<int> &cur, const std::vector<int> &inp, int genamt, int nctx) {
+    const int ShortfallThreshold = 200 + std::min(nctx / 30, 140);
+    const int SlackAllowance = 60 + std::min(nctx / 60, 70);
+    const int new_len = (int)inp.size();
+    if (new_len == 0) return 0;
+    int trimstart = 0;
+    bool purgeneeded = true;
+    for (int i = 0; i < (int)cur.size(); ++i) {
+        if (cur[i] == inp[i]) trimstart += 1;
+        else break;
+        if (i + 2 >= new_len) { purgeneeded = false; break; }
+    }
+    if (!purgeneeded || new_len < 6 || cur.size() < 6 || new_len - trimstart < ShortfallThreshold) return 0;
+    const int LCSTokThreshold = std::max(std::min((new_len - trimstart) - (genamt + SlackAllowance), (int)(nctx * 0.45)),
+                                         ShortfallThreshold - SlackAllowance);
+    const std::vector<int> cur_wo(cur.begin() + trimstart, cur.end()), new_wo(inp.begin() + trimstart, inp.end());
+    const std::vector<int> shared = longest_common_subseq(cur_wo, new_wo);
+    if ((int)shared.size() <= LCSTokThreshold || !arr_start_with(new_wo, shared)) return 0;
+    const int found = arr_find_index_of(cur, shared);
+    if (found < 0 || found <= trimstart) return 0;
+    const int diff = found - trimstart;
+    for (kcpp_model *m : e.stages)
+        if (kcpp_model_kv_shift(m, trimstart, diff, (int)cur.size())) {
+            fprintf(stderr, "[kcpp] context shift failed: %s\n", kcpp_last_error());
+            cur.resize(trimstart);                 // KV beyond trimstart is no longer trusted: recompute it
+            return 0;
+        }
+    // as the reference: the moved tail excludes the last token (it is re-evaluated by the fast forward)
+    for (size_t i = trimstart + diff; i + 1 < cur.size(); ++i) cur[i - diff] = cur[i];
+    cur.resize(cur.size() - diff);
+    fprintf(stderr, "[kcpp] Context Shifting: Erased %d tokens at position %d\n", diff, trimstart + 1);
+    return diff;
+}
+
 }  // namespace
 
 extern "C" {
@@ -255,6 +329,7 @@ bool load_model(const load_model_inputs inputs) {
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) { fprintf(stderr, "[kcpp] load_model: no GPU\n"); return false; }
     const std::vector<int> ldev = split_layers(hp.n_layer, std::min(ndev, KCPP_TENSOR_SPLIT_MAX), inputs.tensor_split);
     e->ub = inputs.blasbatchsize > 0 ? std::min(inputs.blasbatchsize, 512) : 512;
+    e->use_contextshift = inputs.use_contextshift;
     int il = 0;
     while (il < hp.n_layer || e->stages.empty()) {
         const int d = il < hp.n_layer ? ldev[il] : ldev[hp.n_layer];
@@ -302,12 +377,34 @@ generation_outputs generate(const generation_inputs in) {
     }
     g_finished = false;
     g_abort = false;
-    std::string text = std::string(in.memory ? in.memory : "") + std::string(in.prompt ? in.prompt : "");
-    std::vector<int> toks = e->tok.encode(text, true);
     const int max_ctx = std::min(in.max_context_length > 0 ? in.max_context_length : e->hp.n_ctx - 8, e->hp.n_ctx - 8);
     const int max_len = std::max(1, std::min(in.max_length > 0 ? in.max_length : 64, max_ctx - 1));
-    if ((int)toks.size() > max_ctx - max_len) toks.erase(toks.begin(), toks.end() - (max_ctx - max_len));
+    // prompt assembly as gpttype_adapter.cpp:2794-2887: the prompt is cut from the front (BOS kept first) to
+    // leave room for max_length, the memory is kept whole (cut from its front only if it alone does not fit)
+    // and the prompt makes room for it
+    std::vector<int> toks = e->tok.encode(in.prompt ? in.prompt : "", true);
+    const std::vector<int> bosv = e->tok.encode("", true);
+    if ((int)toks.size() + max_len > max_ctx) {
+        toks.erase(toks.begin(), toks.begin() + ((int)toks.size() - max_ctx + max_len));
+        if (!bosv.empty() && !toks.empty()) toks[0] = bosv[0];
+    }
+    if (in.memory && in.memory[0]) {
+        std::vector<int> mem = e->tok.encode(in.memory, true);
+        if (!bosv.empty() && !toks.empty() && toks[0] == bosv[0]) toks.erase(toks.begin());
+        if ((int)mem.size() + max_len + 4 > max_ctx) {
+            mem.erase(mem.begin(), mem.begin() + ((int)mem.size() - max_ctx + max_len + 4));
+            if (!bosv.empty() && !mem.empty()) mem[0] = bosv[0];
+        }
+        const int total = (int)(mem.size() + toks.size()) + max_len;
+        if (total > max_ctx) {
+            const int excess = total - max_ctx;
+            if ((int)toks.size() >= excess) toks.erase(toks.begin(), toks.begin() + excess);
+            else toks.clear();
+        }
+        toks.insert(toks.begin(), mem.begin(), mem.end());
+    }
     if (toks.empty()) toks.push_back(e->tok.bos());
+    if (e->use_contextshift) purge_missing_tokens(*e, e->ctx, toks, max_len, max_ctx);
     // fast forward over the shared prefix (recompute at least the last prompt token for its logits)
     size_t keep = 0;
     while (keep < toks.size() && keep < e->ctx.size() && e->ctx[keep] == toks[keep]) ++keep;

@@ -119,6 +119,22 @@ __global__ void k_silu_mul(float *__restrict__ y, const float *__restrict__ g, c
 }
 
 
+// K-shift of a layer's cache rows (llama.cpp build_k_shift + ggml_compute_forward_rope_f16, mode NORM; koboldcpp
+// context shifting, gpttype_adapter.cpp:1504-1571): ks = f16(rope_f32(f32(kc), cs)) per adjacent pair, vs = vc.
+// rows = positions x n_head_kv, D elements each; cs = (cos, sin) per pair for the shift distance.
+__global__ void k_kv_shift(const uint32_t *__restrict__ kc, const uint32_t *__restrict__ vc, uint32_t *__restrict__ ks,
+                           uint32_t *__restrict__ vs, int64_t npairs, int half_d, const float2 *__restrict__ cs) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npairs) return;
+    const uint32_t kk = kc[i];
+    const float2 c = cs[i % half_d];
+    const float x0 = h2f((uint16_t)(kk & 0xFFFF)), x1 = h2f((uint16_t)(kk >> 16));
+    const uint16_t y0 = f2h(__fsub_rn(__fmul_rn(x0, c.x), __fmul_rn(x1, c.y)));
+    const uint16_t y1 = f2h(__fadd_rn(__fmul_rn(x0, c.y), __fmul_rn(x1, c.x)));
+    ks[i] = (uint32_t)y0 | ((uint32_t)y1 << 16);
+    vs[i] = vc[i];
+}
+
 extern "C" {
 
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,
@@ -136,6 +152,17 @@ int kcpp_rope_kv(const float *qkv, int64_t ldqkv, float *q_out, uint16_t *q16, u
     const int items = H * D / 2 + HKV * D / 2 + HKV * D;
     hipLaunchKernelGGL(k_rope_kv, dim3((unsigned)T, (unsigned)((items + 255) / 256)), dim3(256), 0, (hipStream_t)stream, qkv,
                        ldqkv, q_out, q16, kc, vc, H, HKV, D, n_past, pos_dev, (const float2 *)rope_tab);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_kv_shift_rows(const uint16_t *kc, const uint16_t *vc, uint16_t *ks, uint16_t *vs, int64_t rows, int D,
+                       const float *cs, void *stream) {
+    if (D % 2 || rows < 0) return -1;
+    const int64_t np = rows * D / 2;
+    if (np == 0) return 0;
+    hipLaunchKernelGGL(k_kv_shift, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, (hipStream_t)stream, (const uint32_t *)kc,
+                       (const uint32_t *)vc, (uint32_t *)ks, (uint32_t *)vs, np, D / 2, (const float2 *)cs);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

@@ -100,6 +100,8 @@ struct kcpp_model {
     int32_t *moe_rows_h = nullptr;
     float *moe_rw_h = nullptr;
     float2 *rope_tab = nullptr;
+    void *kv_scratch = nullptr;             // context shift: moved K/V rows (n_ctx x EKV x 2 f16, lazily)
+    float *shift_cs = nullptr;              // context shift: (cos, sin) pairs of the shift distance
     int32_t *pin = nullptr;          // pinned host {token, n_past}
     float *logits_pin = nullptr;
     bool use_graphs = true;
@@ -164,31 +166,73 @@ static int alloc_tensor(kcpp_model *m, KTensor &t, int type, int64_t K, int64_t 
     return 0;
 }
 
-extern "C" int kcpp_rope_table(float *tab, int n_pos, int n_dims, float freq_base, float freq_scale,
-                               const float *freq_factors, float ext_factor, float attn_factor, float beta_fast,
-                               float beta_slow, int n_ctx_orig) {
-    // ggml_rope_cache_init + rope_yarn (ggml.c:14216-14260); n_dims == head dim for Llama
+// one position's (cos, sin) pairs: ggml_rope_cache_init + rope_yarn (ggml.c:14216-14260); p may be negative
+// (a K-shift distance), n_dims == head dim for Llama
+static void rope_row(float *row, float p, int n_dims, float freq_base, float freq_scale, const float *freq_factors,
+                     float ext_factor, float attn_factor, float beta_fast, float beta_slow, int n_ctx_orig) {
     const float theta_scale = powf(freq_base, -2.0f / n_dims);
     auto corr_dim = [&](float n_rot) { return n_dims * logf(n_ctx_orig / (n_rot * 2 * (float)M_PI)) / (2 * logf(freq_base)); };
     float corr0 = fmaxf(0, floorf(corr_dim(beta_fast))), corr1 = fminf(n_dims - 1, ceilf(corr_dim(beta_slow)));
-    for (int p = 0; p < n_pos; ++p) {
-        float theta = (float)p;
-        for (int i0 = 0; i0 < n_dims; i0 += 2) {
-            const float ff = freq_factors ? freq_factors[i0 / 2] : 1.0f;
-            const float theta_extrap = theta / ff;
-            const float theta_interp = freq_scale * theta_extrap;
-            float th = theta_interp, mscale = attn_factor;
-            if (ext_factor != 0.0f) {
-                const float y = (i0 / 2 - corr0) / fmaxf(0.001f, corr1 - corr0);
-                const float ramp_mix = (1 - fminf(1, fmaxf(0, y))) * ext_factor;
-                th = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
-                mscale *= 1.0f + 0.1f * logf(1.0f / freq_scale);
-            }
-            tab[((int64_t)p * (n_dims / 2) + i0 / 2) * 2 + 0] = cosf(th) * mscale;
-            tab[((int64_t)p * (n_dims / 2) + i0 / 2) * 2 + 1] = sinf(th) * mscale;
-            theta *= theta_scale;
+    float theta = p;
+    for (int i0 = 0; i0 < n_dims; i0 += 2) {
+        const float ff = freq_factors ? freq_factors[i0 / 2] : 1.0f;
+        const float theta_extrap = theta / ff;
+        const float theta_interp = freq_scale * theta_extrap;
+        float th = theta_interp, mscale = attn_factor;
+        if (ext_factor != 0.0f) {
+            const float y = (i0 / 2 - corr0) / fmaxf(0.001f, corr1 - corr0);
+            const float ramp_mix = (1 - fminf(1, fmaxf(0, y))) * ext_factor;
+            th = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
+            mscale *= 1.0f + 0.1f * logf(1.0f / freq_scale);
         }
+        row[i0 + 0] = cosf(th) * mscale;
+        row[i0 + 1] = sinf(th) * mscale;
+        theta *= theta_scale;
     }
+}
+
+extern "C" int kcpp_rope_table(float *tab, int n_pos, int n_dims, float freq_base, float freq_scale,
+                               const float *freq_factors, float ext_factor, float attn_factor, float beta_fast,
+                               float beta_slow, int n_ctx_orig) {
+    for (int p = 0; p < n_pos; ++p)
+        rope_row(tab + (int64_t)p * n_dims, (float)p, n_dims, freq_base, freq_scale, freq_factors, ext_factor, attn_factor,
+                 beta_fast, beta_slow, n_ctx_orig);
+    return 0;
+}
+
+extern "C" int kcpp_rope_row(float *row, int p, int n_dims, float freq_base, float freq_scale, float ext_factor,
+                             float attn_factor, float beta_fast, float beta_slow, int n_ctx_orig) {
+    rope_row(row, (float)p, n_dims, freq_base, freq_scale, nullptr, ext_factor, attn_factor, beta_fast, beta_slow, n_ctx_orig);
+    return 0;
+}
+
+// Context shift (koboldcpp PurgeMissingTokens: llama_kv_cache_seq_rm(p0, p0 + diff) +
+// llama_kv_cache_seq_add(p0 + diff, n_past, -diff), then the K-shift of build_k_shift on the next decode):
+// cache rows [p0 + diff, n_past) move to [p0, n_past - diff), K re-rotated by position -diff.  The caches are
+// position-indexed here, so the rows move (through a scratch copy) instead of the cells being relabelled.
+extern "C" int kcpp_model_kv_shift(kcpp_model *m, int p0, int diff, int n_past) {
+    if (!m || p0 < 0 || diff <= 0 || p0 + diff > n_past || n_past > m->hp.n_ctx) { g_err = "kv_shift: bad range"; return -1; }
+    hipSetDevice(m->device);
+    const int64_t E = m->hp.n_embd, H = m->hp.n_head, HKV = m->hp.n_head_kv, D = E / H, EKV = HKV * D;
+    const int64_t count = n_past - p0 - diff;
+    if (count == 0) return 0;
+    if (!m->kv_scratch && hipMalloc(&m->kv_scratch, (size_t)m->hp.n_ctx * EKV * 2 * 2) != hipSuccess) {
+        g_err = "kv_shift scratch";
+        return -2;
+    }
+    if (!m->shift_cs && hipMalloc(&m->shift_cs, (size_t)D * 4) != hipSuccess) { g_err = "kv_shift cs"; return -2; }
+    std::vector<float> row((size_t)D);
+    rope_row(row.data(), (float)-diff, (int)D, m->hp.rope_base, m->hp.rope_freq_scale, nullptr, 0.0f, 1.0f, 32.0f, 1.0f,
+             m->hp.n_ctx);
+    RT_CHECK(hipMemcpyAsync(m->shift_cs, row.data(), (size_t)D * 4, hipMemcpyHostToDevice, m->stream));
+    uint16_t *ks = (uint16_t *)m->kv_scratch, *vs = ks + (size_t)m->hp.n_ctx * EKV;
+    for (auto &L : m->layers) {
+        RC(kcpp_kv_shift_rows(L.kc + (p0 + diff) * EKV, L.vc + (p0 + diff) * EKV, ks, vs, count * HKV, (int)D, m->shift_cs,
+                              m->stream));
+        RT_CHECK(hipMemcpyAsync(L.kc + p0 * EKV, ks, (size_t)count * EKV * 2, hipMemcpyDeviceToDevice, m->stream));
+        RT_CHECK(hipMemcpyAsync(L.vc + p0 * EKV, vs, (size_t)count * EKV * 2, hipMemcpyDeviceToDevice, m->stream));
+    }
+    RT_CHECK(hipStreamSynchronize(m->stream));     // the host row above must outlive its copy
     return 0;
 }
 
@@ -328,6 +372,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
         if (p) hipHostFree(p);
     F(m->x); F(m->qkv); F(m->attn); F(m->h); F(m->logits); F(m->q16); F(m->act); F(m->act2); F(m->fa_ws);
     F(m->gemm_ws); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
+    F(m->kv_scratch); F(m->shift_cs);
     if (m->pin) hipHostFree(m->pin);
     if (m->logits_pin) hipHostFree(m->logits_pin);
     if (m->stream) hipStreamDestroy(m->stream);

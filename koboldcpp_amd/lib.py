@@ -38,6 +38,9 @@ _SIGS = {
     "kcpp_gemm": [I, P, P, I64, I64, P, I64, P, I64, P, I64, I, P, P],
     "kcpp_rms_norm": [P, I64, P, P, I64, P, I64, I64, Fl, P],
     "kcpp_rope_table": [P, I, I, Fl, Fl, P, Fl, Fl, Fl, Fl, I],
+    "kcpp_rope_row": [P, I, I, Fl, Fl, Fl, Fl, Fl, Fl, I],
+    "kcpp_kv_shift_rows": [P, P, P, P, I64, I, P, P],
+    "kcpp_model_kv_shift": [P, I, I, I],
     "kcpp_rope_kv": [P, I64, P, P, P, P, I, I, I, I, I, P, P, P],
     "kcpp_flash_attn": [P, P, P, P, P, P, I, I, I, I, I, P, I, Fl, I, P],
     "kcpp_flash_attn_prefill_mfma": [P, P, P, P, I, I, I, I, I, Fl, P],
@@ -196,6 +199,10 @@ class Model:
                                       int(has_output), max_ubatch)
         if not self.m:
             raise KcppError("kcpp_model_create failed: %s" % (_L.kcpp_last_error() or b"").decode())
+
+    def kv_shift(self, p0, diff, n_past):
+        """context shift: cache rows [p0+diff, n_past) -> [p0, n_past-diff), K re-rotated by -diff"""
+        _chk(_L.kcpp_model_kv_shift(self.m, p0, diff, n_past), "kv_shift")
 
     def synth(self, seed):
         _chk(_L.kcpp_model_synth_weights(self.m, seed), "synth")
