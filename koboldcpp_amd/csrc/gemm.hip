@@ -104,6 +104,15 @@ __device__ __forceinline__ void k4_sm(const uint4 &hdr, int j, int &d, int &m) {
     else { d = (b(j + 4) & 0xF) | ((b(j - 4) >> 6) << 4); m = (b(j + 4) >> 4) | ((b(j) >> 6) << 4); }
 }
 
+// get_scale_min_k4 for all 8 sub-blocks at once, four 6-bit values per dword: byte j of sc_lo / m_lo is
+// sub-block j, byte j of sc_hi / m_hi sub-block 4 + j (scales bytes 0-3 = hdr.y, 4-7 = hdr.z, 8-11 = hdr.w)
+__device__ __forceinline__ void k4_all(const uint4 &h, uint32_t &sc_lo, uint32_t &sc_hi, uint32_t &m_lo, uint32_t &m_hi) {
+    sc_lo = h.y & 0x3F3F3F3Fu;
+    m_lo = h.z & 0x3F3F3F3Fu;
+    sc_hi = (h.w & 0x0F0F0F0Fu) | ((h.y >> 2) & 0x30303030u);
+    m_hi = ((h.w >> 4) & 0x0F0F0F0Fu) | ((h.z >> 2) & 0x30303030u);
+}
+
 // fragment slot for element k (0..255) of weight row nl (0..63): (tile, step, lane); 16 B per slot
 __device__ __forceinline__ int bslot(int nl, int k) {
     const int tile = nl >> 5, s = k >> 4, h = (k >> 3) & 1;
@@ -825,6 +834,8 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
     for (int64_t sb = 0; sb < nsb; ++sb) {
         const int buf = (int)(sb & 1);
         const uint4 hc = hn;
+        uint32_t sc_lo, sc_hi, m_lo, m_hi;
+        k4_all(hc, sc_lo, sc_hi, m_lo, m_hi);
         uint4 qc[4];
 #pragma unroll
         for (int p = 0; p < 4; ++p) qc[p] = qn[p];
@@ -853,10 +864,10 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
                 for (int j = 0; j < TPW; ++j) an[j] = abase[j * 1024 + (s + 1) * 64];
             }
             const int p = s >> 2, st = s & 3;
-            if (st == 0) {
-                int m_;
-                k4_sm(hc, 2 * p, s0, m_);
-                k4_sm(hc, 2 * p + 1, s1, m_);
+            if (st == 0) {                        // sub-blocks 2p, 2p+1: bytes 2(p&1), +1 of the low / high dword
+                const uint32_t sdw = p < 2 ? sc_lo : sc_hi;
+                s0 = (int)((sdw >> (16 * (p & 1))) & 0xFF);
+                s1 = (int)((sdw >> (16 * (p & 1) + 8)) & 0xFF);
             }
             const h8v b = frag_q4v3(u4c(qc[p], st), (float)s0, (float)s1);
 #pragma unroll
@@ -864,12 +875,12 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
         }
         // epilogue: tot -= dy * dmin * (sum_j m_j bsum_j), then tot += dy * (d * S)  (k_gemm_kq's order)
         h8v bm;                                   // mins of sub-blocks 4kg .. 4kg+3, each for its two 16-groups
+        const uint32_t mdw = kg ? m_hi : m_lo;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-            int sc_, mn_;
-            k4_sm(hc, 4 * kg + e, sc_, mn_);
-            bm[2 * e] = (_Float16)mn_;
-            bm[2 * e + 1] = (_Float16)mn_;
+            const _Float16 mn = (_Float16)(float)((mdw >> (8 * e)) & 0xFF);
+            bm[2 * e] = mn;
+            bm[2 * e + 1] = mn;
         }
         const float dw = h2f((uint16_t)(hc.x & 0xFFFF)), dm = h2f((uint16_t)(hc.x >> 16));
 #pragma unroll

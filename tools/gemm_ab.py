@@ -21,6 +21,8 @@ def main():
                                  ("wo", K.Q4_K_RS, 4096, 4096, 0), ("down", K.Q4_K_RS, 14336, 4096, 0),
                                  ("glu2", K.Q4_K_RS, 4096, 14336, 1), ("down6", K.Q6_K_RS, 14336, 4096, 0),
                                  ("v6", K.Q6_K_RS, 4096, 1024, 0)]:
+        if os.environ.get("GEMM_ONLY") and name != os.environ["GEMM_ONLY"]:
+            continue
         nrot = 3
         ws_ = [torch.empty(K.row_bytes(t, Kd) * N, dtype=torch.uint8, device="cuda") for _ in range(nrot)]
         for i, w in enumerate(ws_):
