@@ -1,0 +1,101 @@
+"""Full-size properties (BASELINE configs[1]: Llama-3-8B-shape Q4_K_M, synthetic weights), where the oracle would
+take minutes per token: size-independent invariants of the GPU path.
+
+* ubatch invariance: prefilling 1024 tokens as 2 x 512 or 4 x 256 gives bit-identical last-token logits -- every
+  kernel is per token (RMS norm, Q8_K, integer GEMM dots with a fixed epilogue order) or processes keys in
+  absolute 64-key tiles (flash attention), so how the prompt is cut must not matter;
+* graph replay: the hipGraph decode step equals the eagerly launched one bit for bit at ~1.1k context;
+* decode vs prefill (full width, 2 layers): the single-token path (mat-vecs, split-KV attention with f32 P.V) and
+  the prefill path (MFMA GEMMs, MFMA attention with P rounded to f16) agree on the next token's logits within
+  max 0.15 / median 0.02 (logit std ~1.35; measured 0.042 / 0.0063).  With more layers the random synthetic
+  weights amplify such differences chaotically (measured median 0.07 at 8 layers, 0.24 at 32), so depth is
+  covered by the bit-exact invariants instead;
+* greedy decode on the device (on-device argmax feeding the next step) equals the host argmax loop."""
+import numpy as np
+import pytest
+
+import refharness as R
+
+pytestmark = pytest.mark.gpu
+
+LLAMA3_8B = dict(n_vocab=128256, n_embd=4096, n_head=32, n_head_kv=8, n_layer=32, n_ff=14336, n_ctx=2048,
+                 eps=1e-5, rope_base=500000.0)
+
+
+@pytest.fixture(scope="module")
+def K():
+    import torch
+    assert torch.cuda.is_available()
+    import koboldcpp_amd.lib as K
+    return K
+
+
+def prompt(n):
+    return [int(v) for v in np.random.default_rng(8).integers(1, 128000, size=n)]
+
+
+def test_fullsize_ubatch_invariance(K):
+    types = R.q4_k_m_types(32)
+    p = prompt(1024)
+    outs = []
+    for ub in (512, 256):
+        m = K.Model(LLAMA3_8B, types, max_ubatch=ub)
+        m.synth(1234)
+        outs.append(m.decode(p, 0))
+        m.close()
+    assert np.isfinite(outs[0]).all()
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
+def test_fullsize_graph_replay_and_decode_vs_prefill(K):
+    types = R.q4_k_m_types(32)
+    p = prompt(1100)
+    nxt = [17, 4242, 99, 100000]
+    m = K.Model(LLAMA3_8B, types)
+    m.synth(1234)
+    m.decode(p, 0, want_logits=False)
+    graphed = [m.decode([t], len(p) + i) for i, t in enumerate(nxt)]
+    m.set_graphs(False)
+    eager = [m.decode([t], len(p) + i) for i, t in enumerate(nxt)]      # same positions: overwrites the same KV rows
+    m.close()
+    for a, b in zip(graphed, eager):
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    hp2 = dict(LLAMA3_8B, n_layer=2)
+    t2 = R.q4_k_m_types(2)
+    res = []
+    for pre in (True, False):
+        r = K.Model(hp2, t2)
+        r.synth(1234)
+        if pre:
+            res.append(r.decode(p + nxt[:1], 0))
+        else:
+            r.decode(p, 0, want_logits=False)
+            res.append(r.decode(nxt[:1], len(p)))
+        r.close()
+    d = np.abs(res[0] - res[1])
+    assert d.max() < 0.15 and np.median(d) < 0.02, (d.max(), np.median(d))
+
+
+def test_fullsize_greedy_on_device_matches_host_loop(K):
+    types = R.q4_k_m_types(32)
+    p = prompt(300)
+    m = K.Model(LLAMA3_8B, types)
+    m.synth(1234)
+    lg = m.decode(p, 0)
+    dev = [m.argmax()]
+    n = len(p)
+    for _ in range(6):
+        dev.append(m.decode_greedy(n))
+        n += 1
+    m.close()
+    h = K.Model(LLAMA3_8B, types)
+    h.synth(1234)
+    lg2 = h.decode(p, 0)
+    host = [int(np.argmax(lg2))]
+    n = len(p)
+    for _ in range(6):
+        host.append(int(np.argmax(h.decode([host[-1]], n))))
+        n += 1
+    h.close()
+    assert int(np.argmax(lg)) == dev[0]
+    assert dev == host
