@@ -87,6 +87,7 @@ struct kcpp_model {
     float *hglu = nullptr;           // [ubatch][2 n_ff] fused gate|up GEMM output (prefill)
     uint16_t *q16 = nullptr;
     void *act = nullptr, *act2 = nullptr, *fa_ws = nullptr, *gemm_ws = nullptr;
+    void *gemm_ws2 = nullptr;               // prefill: attn_v GEMM on the side stream (q|k fused layers)
     size_t act_sz = 0, gemm_ws_sz = 0;
     int32_t *tok_dev = nullptr, *pos_dev = nullptr, *argmax_dev = nullptr;
     void *argmax_ws = nullptr;       // ARGMAX_BLOCKS (value, index) partials
@@ -371,7 +372,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     for (void *p : {(void *)m->moe_ids_h, (void *)m->moe_w_h, (void *)m->moe_rows_h, (void *)m->moe_rw_h})
         if (p) hipHostFree(p);
     F(m->x); F(m->qkv); F(m->attn); F(m->h); F(m->logits); F(m->q16); F(m->act); F(m->act2); F(m->fa_ws);
-    F(m->gemm_ws); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
+    F(m->gemm_ws); F(m->gemm_ws2); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
     F(m->kv_scratch); F(m->shift_cs);
     if (m->pin) hipHostFree(m->pin);
     if (m->logits_pin) hipHostFree(m->logits_pin);
@@ -694,8 +695,25 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             if (L.nqkv >= 2) {                       // q|k(|v) rows back to back: one GEMM
                 KTensor f = t[1];
                 f.N = E + (L.nqkv - 1) * EKV;
-                RC(matmul(m, f, nullptr, m->act, T, m->qkv, LQ, nullptr, 0, 0));
-                if (L.nqkv == 2) RC(matmul(m, t[3], nullptr, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0));
+                static const int side_env = getenv("KCPP_PREFILL_SIDE") ? atoi(getenv("KCPP_PREFILL_SIDE")) : 1;
+                if (L.nqkv == 2 && T > 8 && side_env && m->side) {
+                    // attn_v (another type: Q6_K on the more-bits layers) on the side stream with its own
+                    // workspace, concurrently with the q|k GEMM: its 64-workgroup grid alone leaves CUs idle
+                    if (!m->gemm_ws2) {
+                        const size_t sz = (size_t)kcpp_gemm_workspace_bytes(t[3].type, E, EKV, m->ub);
+                        RT_CHECK(hipMalloc(&m->gemm_ws2, sz));
+                    }
+                    RT_CHECK(hipEventRecord(m->ev_fork, s));
+                    RT_CHECK(hipStreamWaitEvent(m->side, m->ev_fork, 0));
+                    RC(kcpp_gemm(t[3].type, t[3].d, nullptr, E, EKV, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0,
+                                 m->gemm_ws2, m->side));
+                    RC(matmul(m, f, nullptr, m->act, T, m->qkv, LQ, nullptr, 0, 0));
+                    RT_CHECK(hipEventRecord(m->ev_join, m->side));
+                    RT_CHECK(hipStreamWaitEvent(s, m->ev_join, 0));
+                } else {
+                    RC(matmul(m, f, nullptr, m->act, T, m->qkv, LQ, nullptr, 0, 0));
+                    if (L.nqkv == 2) RC(matmul(m, t[3], nullptr, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0));
+                }
             } else {
                 RC(matmul(m, t[1], nullptr, m->act, T, m->qkv, LQ, nullptr, 0, 0));
                 RC(matmul(m, t[2], nullptr, m->act, T, m->qkv + E, LQ, nullptr, 0, 0));
