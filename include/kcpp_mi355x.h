@@ -118,6 +118,10 @@ int kcpp_fa_prefill_set_variant(int v);
  * sum 1; ids/weights [T][k] */
 int kcpp_moe_route(const float *x, int64_t ldx, const void *w_router, int wtype, int64_t K, int n_expert, int k,
                    int32_t *ids, float *weights, int T, void *stream);
+/* the router on rms_norm(x) * norm_w computed in the same launch (k_rms_norm's arithmetic; K <= 4096,
+ * n_expert <= 8); -3 when not covered */
+int kcpp_moe_route_norm(const float *x, int64_t ldx, const float *norm_w, float eps, const void *w_router, int wtype,
+                        int64_t K, int n_expert, int k, int32_t *ids, float *weights, int T, void *stream);
 /* MoE helpers: dst[i] = src[rows[i]] (row gather); dst[rows[i]] = w[i] * src[i] (weighted scatter into
  * the token's top-k slot row); combine: x[i] = ((slots[0][i] + slots[1][i]) + ...) + x[i] over k slots
  * spaced slot_stride floats (the ggml_add chain of llm_build_moe_ffn, src/llama.cpp:9500-9515) */

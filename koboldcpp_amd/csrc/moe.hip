@@ -18,17 +18,89 @@
 
 #define MOE_MAX_EXPERT 64
 
-template <int WT>
+// NORM: x is the residual stream and the router input is rms_norm(x) * nw computed here exactly as k_rms_norm
+// does for K <= 4096 (same thread -> element map, double partial sums in the same order), one launch less
+template <int WT, bool NORM = false>
 __global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, int64_t ldx, const void *__restrict__ w,
                                                    int K, int NE, int NU, int32_t *__restrict__ ids,
-                                                   float *__restrict__ wts) {
+                                                   float *__restrict__ wts, const float *__restrict__ nw = nullptr,
+                                                   float eps = 0.0f) {
     const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const float *xr = x + (int64_t)t * ldx;
     __shared__ float s_logit[MOE_MAX_EXPERT];
+    __shared__ float s_part[4][8];
+    if (NE <= 8) {
+        // all experts at once: thread tid owns elements 16 tid .. +15 of every 4096-element chunk, the loads of
+        // all NE router rows in flight together (one memory round trip per chunk)
+        float acc[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        float nscale = 1.0f;
+        if constexpr (NORM) {                            // K <= 4096: one chunk, elements 16 tid .. +15
+            double ss = 0.0;
+            if (16 * tid < K) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float4 f = *(const float4 *)(xr + 16 * tid + 4 * u);
+                    ss += (double)__fmul_rn(f.x, f.x); ss += (double)__fmul_rn(f.y, f.y);
+                    ss += (double)__fmul_rn(f.z, f.z); ss += (double)__fmul_rn(f.w, f.w);
+                }
+            }
+            ss = wave_sum(ss);
+            __shared__ double red[4];
+            if (lane == 0) red[wave] = ss;
+            __syncthreads();
+            double sum = 0.0;
+            for (int i = 0; i < 4; ++i) sum += red[i];
+            const float mean = (float)(sum / (double)K);
+            nscale = 1.0f / sqrtf(mean + eps);
+        }
+        for (int i0 = 16 * tid; i0 < K; i0 += 4096) {
+            float4 xv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                xv[u] = i0 + 4 * u < K ? *(const float4 *)(xr + i0 + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
+                if constexpr (NORM) {
+                    if (i0 + 4 * u < K) {
+                        const float4 g = *(const float4 *)(nw + i0 + 4 * u);
+                        xv[u] = make_float4(__fmul_rn(__fmul_rn(xv[u].x, nscale), g.x), __fmul_rn(__fmul_rn(xv[u].y, nscale), g.y),
+                                            __fmul_rn(__fmul_rn(xv[u].z, nscale), g.z), __fmul_rn(__fmul_rn(xv[u].w, nscale), g.w));
+                    }
+                }
+                if constexpr (WT == KT_F16)   // ggml converts src1 to the F16 vec_dot_type
+                    xv[u] = make_float4(h2f(f2h(xv[u].x)), h2f(f2h(xv[u].y)), h2f(f2h(xv[u].z)), h2f(f2h(xv[u].w)));
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                if (e >= NE) break;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = i0 + 4 * u;
+                    if (i >= K) break;
+                    float4 wv;
+                    if constexpr (WT == KT_F16) {
+                        const uint2 h = *(const uint2 *)((const uint16_t *)w + (int64_t)e * K + i);
+                        wv = make_float4(h2f(h.x & 0xFFFF), h2f(h.x >> 16), h2f(h.y & 0xFFFF), h2f(h.y >> 16));
+                    } else {
+                        wv = *(const float4 *)((const float *)w + (int64_t)e * K + i);
+                    }
+                    acc[e] = fmaf(xv[u].x, wv.x, acc[e]);
+                    acc[e] = fmaf(xv[u].y, wv.y, acc[e]);
+                    acc[e] = fmaf(xv[u].z, wv.z, acc[e]);
+                    acc[e] = fmaf(xv[u].w, wv.w, acc[e]);
+                }
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            if (e >= NE) break;
+            const float v = wave_sum(acc[e]);
+            if (lane == 0) s_part[wave][e] = v;
+        }
+        __syncthreads();
+        if (tid < NE) s_logit[tid] = (s_part[0][tid] + s_part[1][tid]) + (s_part[2][tid] + s_part[3][tid]);
+    } else {
     // wave w: experts w, w+4, ...; lane: 4 consecutive elements per 256-element step, 4 steps in flight
     for (int e = wave; e < NE; e += 4) {
         float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll 4
         for (int i0 = 4 * lane; i0 < K; i0 += 1024) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
@@ -53,8 +125,52 @@ __global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, 
         const float a = wave_sum((acc[0] + acc[1]) + (acc[2] + acc[3]));
         if (lane == 0) s_logit[e] = a;
     }
+    }
     __syncthreads();
     if (tid != 0) return;
+    if (NE <= 8) {
+        // the same steps on register arrays (constant indices after unrolling; the generic path below keeps
+        // p / idx in scratch, a chain of dependent private-memory loads that cost ~15 us per token and layer)
+        float p[8], pv[8];
+        int idx[8];
+        float mx = -INFINITY;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            p[e] = e < NE ? s_logit[e] : -INFINITY;
+            mx = fmaxf(mx, p[e]);
+        }
+        double sum = 0.0;                                // ggml_vec_soft_max_f32: ggml_float sum
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            if (e < NE) { p[e] = expf(p[e] - mx); sum += (double)p[e]; }
+        const float inv = (float)(1.0 / sum);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { p[e] *= inv; pv[e] = p[e]; idx[e] = e; }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {                    // argsort descending (exchange order), first NU
+            if (j >= NU) break;
+#pragma unroll
+            for (int k = j + 1; k < 8; ++k) {
+                if (k >= NE) break;
+                if (pv[j] < pv[k]) {
+                    const int ti = idx[j]; idx[j] = idx[k]; idx[k] = ti;
+                    const float tv = pv[j]; pv[j] = pv[k]; pv[k] = tv;
+                }
+            }
+        }
+        double ws = 0.0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j < NU) ws += (double)pv[j];
+        const float wsum = (float)ws;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j < NU) {
+                ids[t * NU + j] = idx[j];
+                wts[t * NU + j] = pv[j] / wsum;
+            }
+        return;
+    }
     float p[MOE_MAX_EXPERT];
     float mx = -INFINITY;
     for (int e = 0; e < NE; ++e) {
@@ -108,15 +224,31 @@ __global__ void k_moe_combine(float *__restrict__ x, const float *__restrict__ s
 
 extern "C" {
 
+int kcpp_moe_route_norm(const float *x, int64_t ldx, const float *norm_w, float eps, const void *w_router, int wtype,
+                        int64_t K, int n_expert, int k, int32_t *ids, float *weights, int T, void *stream) {
+    if (n_expert < 1 || n_expert > 8 || k < 1 || k > n_expert || K > 4096 || K % 16 || ldx % 4) return -3;
+    hipStream_t s = (hipStream_t)stream;
+    if (wtype == KT_F16)
+        hipLaunchKernelGGL((k_moe_route<KT_F16, true>), dim3(T), dim3(256), 0, s, x, ldx, w_router, (int)K, n_expert, k, ids,
+                           weights, norm_w, eps);
+    else if (wtype == KT_F32)
+        hipLaunchKernelGGL((k_moe_route<KT_F32, true>), dim3(T), dim3(256), 0, s, x, ldx, w_router, (int)K, n_expert, k, ids,
+                           weights, norm_w, eps);
+    else
+        return -3;
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
 int kcpp_moe_route(const float *x, int64_t ldx, const void *w_router, int wtype, int64_t K, int n_expert, int k,
                    int32_t *ids, float *weights, int T, void *stream) {
     if (n_expert < 1 || n_expert > MOE_MAX_EXPERT || k < 1 || k > n_expert) return -1;
     if (K % 4 || ldx % 4) return -1;                    // float4 / 4-half loads
     hipStream_t s = (hipStream_t)stream;
     if (wtype == KT_F16)
-        hipLaunchKernelGGL(k_moe_route<KT_F16>, dim3(T), dim3(256), 0, s, x, ldx, w_router, (int)K, n_expert, k, ids, weights);
+        hipLaunchKernelGGL((k_moe_route<KT_F16, false>), dim3(T), dim3(256), 0, s, x, ldx, w_router, (int)K, n_expert, k, ids, weights);
     else if (wtype == KT_F32)
-        hipLaunchKernelGGL(k_moe_route<KT_F32>, dim3(T), dim3(256), 0, s, x, ldx, w_router, (int)K, n_expert, k, ids, weights);
+        hipLaunchKernelGGL((k_moe_route<KT_F32, false>), dim3(T), dim3(256), 0, s, x, ldx, w_router, (int)K, n_expert, k, ids, weights);
     else
         return -3;
     KCPP_CHECK(hipGetLastError());

@@ -490,8 +490,11 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
     const int NU = hp.n_expert_used;
     const KTensor *t = L.t;
     hipStream_t s = m->stream;
-    RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, 1, hp.eps, s));
-    RC(kcpp_moe_route(m->attn, E, t[9].d, t[9].type, E, hp.n_expert, NU, m->moe_ids, m->moe_w, 1, s));
+    if (kcpp_moe_route_norm(m->x, E, (const float *)t[5].d, hp.eps, t[9].d, t[9].type, E, hp.n_expert, NU, m->moe_ids,
+                            m->moe_w, 1, s) != 0) {
+        RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, 1, hp.eps, s));
+        RC(kcpp_moe_route(m->attn, E, t[9].d, t[9].type, E, hp.n_expert, NU, m->moe_ids, m->moe_w, 1, s));
+    }
     for (int j = 0; j < NU; ++j) {
         if (t[6].type == t[7].type) {
             DecArgs a;

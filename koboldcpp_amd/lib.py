@@ -40,6 +40,7 @@ _SIGS = {
     "kcpp_rope_table": [P, I, I, Fl, Fl, P, Fl, Fl, Fl, Fl, I],
     "kcpp_rope_row": [P, I, I, Fl, Fl, Fl, Fl, Fl, Fl, I],
     "kcpp_kv_shift_rows": [P, P, P, P, I64, I, P, P],
+    "kcpp_moe_route_norm": [P, I64, P, Fl, P, I, I64, I, I, P, P, I, P],
     "kcpp_model_kv_shift": [P, I, I, I],
     "kcpp_rope_kv": [P, I64, P, P, P, P, I, I, I, I, I, P, P, P],
     "kcpp_flash_attn": [P, P, P, P, P, P, I, I, I, I, I, P, I, Fl, I, P],

@@ -244,3 +244,33 @@ def test_moe_mixtral_q5_k_m_policy_vs_oracle(env):
     orc32 = oracle_forced(types, prompt, forced, True, hp=hp)
     d = np.abs(got - orc32)
     assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_F32, (d.max(), np.median(d))
+
+
+@pytest.mark.parametrize("wtype", [R.F16, R.F32])
+@pytest.mark.parametrize("E", [4096, 512])
+def test_route_norm_fused_matches_norm_then_route(env, wtype, E):
+    """decode router with ffn_norm fused in (kcpp_moe_route_norm) == kcpp_rms_norm then kcpp_moe_route, bit for bit"""
+    torch, K = env
+    NE, k, T = 8, 2, 5
+    rng = np.random.default_rng(E + wtype)
+    x = (3 * rng.standard_normal((T, E))).astype(np.float32)
+    nw = (1 + 0.1 * rng.standard_normal(E)).astype(np.float32)
+    w = (0.05 * rng.standard_normal((NE, E))).astype(np.float16 if wtype == R.F16 else np.float32)
+    xd, nd = torch.from_numpy(x).cuda(), torch.from_numpy(nw).cuda()
+    wd = torch.from_numpy(w.view(np.uint8).copy()).cuda()
+    s = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for fused in (True, False):
+        ids = torch.full((T, k), -1, dtype=torch.int32, device="cuda")
+        wts = torch.zeros((T, k), device="cuda")
+        if fused:
+            K.call("kcpp_moe_route_norm", xd.data_ptr(), E, nd.data_ptr(), 1e-5, wd.data_ptr(), wtype, E, NE, k,
+                   ids.data_ptr(), wts.data_ptr(), T, s)
+        else:
+            xn = torch.empty_like(xd)
+            K.call("kcpp_rms_norm", xd.data_ptr(), E, nd.data_ptr(), xn.data_ptr(), E, None, E, T, 1e-5, s)
+            K.call("kcpp_moe_route", xn.data_ptr(), E, wd.data_ptr(), wtype, E, NE, k, ids.data_ptr(), wts.data_ptr(), T, s)
+        torch.cuda.synchronize()
+        outs.append((ids.cpu().numpy(), wts.cpu().numpy()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
