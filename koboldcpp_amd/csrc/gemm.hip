@@ -734,6 +734,11 @@ __global__ void k_act_frag3(const uint8_t *__restrict__ act, int64_t K, int64_t 
     }
 }
 
+#ifndef V3_PRIO_DEF
+#define V3_PRIO_DEF 1
+#endif
+constexpr bool V3_PRIO = V3_PRIO_DEF;
+
 template <int BMT> struct Q4v3Smem {
     h8v a[2][BMT][16 * 64];   // activation fragments [buf][token tile][step * 64 + lane]   (16 KiB per tile)
     h8v bs[2][BMT][64];       // Q8_K bsum fragments  [buf][token tile][lane]
@@ -870,8 +875,10 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
                 s1 = (int)((sdw >> (16 * (p & 1) + 8)) & 0xFF);
             }
             const h8v b = frag_q4v3(u4c(qc[p], st), (float)s0, (float)s1);
+            if constexpr (V3_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
             for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac[j], b, acc[j], 0, 0, 0);
+            if constexpr (V3_PRIO) __builtin_amdgcn_s_setprio(0);
         }
         // epilogue: tot -= dy * dmin * (sum_j m_j bsum_j), then tot += dy * (d * S)  (k_gemm_kq's order)
         h8v bm;                                   // mins of sub-blocks 4kg .. 4kg+3, each for its two 16-groups
