@@ -1106,6 +1106,10 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 #define Q80S_UNROLL 8
 
+static int q80s_version() {
+    static const int v = getenv("KCPP_Q80S_V") ? atoi(getenv("KCPP_Q80S_V")) : 2;
+    return v;
+}
 static int q80s_splits(int64_t K, int64_t N) {
     const int64_t nt = (N + 127) / 128, nb = K / 32;
     int64_t S = (384 + nt - 1) / nt;
@@ -1200,6 +1204,103 @@ __global__ void __launch_bounds__(256) k_gemm_q80s(const Q80Segs sg, int64_t K, 
     }
 }
 
+// v2 of the small-batch Q8_0 GEMM: the weight tile streams through LDS in row-contiguous pieces.  v1's direct
+// fragment loads touch 32 rows x 32 B per wave instruction (32 cache lines for 1 KiB); here every LDS-DMA wave
+// instruction reads 4 rows x 256 B (8 blocks of each row), 8 such per wave and chunk, into an XOR-swizzled
+// [row][256 B] image (16-B piece c of row n at slot c ^ (n & 15): the B-fragment reads of 32 rows at one piece
+// are conflict-free), double-buffered by 8-block chunks with the activation chunk beside it.  Same block math and
+// split-K partials as k_gemm_q80s (bit-identical partials).
+struct Q80s2Smem {
+    uint8_t w[2][128 * 256];     // weight chunk [buf][row][256 B] (swizzled 16-B pieces)
+    i32x4 a[2][8][64];           // activation fragments [buf][block][lane]
+};
+
+__global__ void __launch_bounds__(256) k_gemm_q80s2(const Q80Segs sg, int64_t K, int64_t N,
+                                                   const uint8_t *__restrict__ act, int64_t M, float *__restrict__ part) {
+    __shared__ Q80s2Smem S;
+    extern __shared__ __attribute__((aligned(16))) float q80_sdx2[];
+    float *sdx = q80_sdx2;                                       // [bps][32 tokens] (dynamic)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, kg = lane >> 5;
+    const int64_t nb = K / 32, S_ = gridDim.y;
+    const int64_t bps = (nb + S_ - 1) / S_, b0 = (int64_t)blockIdx.y * bps, b1 = std::min<int64_t>(nb, b0 + bps);
+    const int64_t nt0 = (int64_t)blockIdx.x * 128;
+    const int seg = (sg.nseg > 1 && nt0 >= sg.N[0]) ? ((sg.nseg > 2 && nt0 >= sg.N[0] + sg.N[1]) ? 2 : 1) : 0;
+    const int64_t soff = seg == 0 ? 0 : (seg == 1 ? sg.N[0] : sg.N[0] + sg.N[1]);
+    const int64_t Ns = seg == 0 ? sg.N[0] : (seg == 1 ? sg.N[1] : sg.N[2]);
+    const uint8_t *W = seg == 0 ? sg.W[0] : (seg == 1 ? sg.W[1] : sg.W[2]);
+    const uint16_t *dwp = (const uint16_t *)(W + Ns * nb * 32);
+    const int64_t trow = std::min<int64_t>(lr, M - 1);
+    const int8_t *qx = (const int8_t *)act + trow * K + 16 * kg;
+    const float *dx = (const float *)(act + M * K);
+    // weight LDS-DMA: wave instruction i covers rows 4i .. 4i+3 (16 lanes each, 16 B per lane); lane -> (row, slot)
+    const int wsub = lane >> 4, wslot = lane & 15;
+    auto stage = [&](int buf, int64_t cb) {                      // chunk = blocks [cb, cb + 8)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int rl = 4 * (8 * wave + i) + wsub;            // local row 0..127
+            const int64_t row = std::min<int64_t>(nt0 - soff + rl, Ns - 1);
+            const int piece = wslot ^ (rl & 15);                 // the 16-B piece this LDS slot holds
+            const int64_t blk = std::min<int64_t>(cb + (piece >> 1), b1 - 1);
+            glds16(W + (row * nb + blk) * 32 + 16 * (piece & 1), &S.w[buf][(8 * wave + i) * 1024]);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int bl = 2 * wave + u;
+            glds16(qx + std::min<int64_t>(cb + bl, b1 - 1) * 32, &S.a[buf][bl][0]);
+        }
+    };
+    for (int64_t i = tid; i < (b1 - b0) * 32; i += 256) {
+        const int64_t b = i >> 5, t = i & 31;
+        sdx[i] = t < M ? dx[t * nb + b0 + b] : 0.0f;
+    }
+    float tot[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tot[r] = 0.0f;
+    const int nl = 32 * wave + lr;                               // this lane's B row within the tile
+    const int64_t nrow = std::min<int64_t>(nt0 - soff + nl, Ns - 1);
+    stage(0, b0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int64_t cb = b0; cb < b1; cb += 8) {
+        const int buf = (int)(((cb - b0) >> 3) & 1);
+        if (cb + 8 < b1) stage(buf ^ 1, cb + 8);
+        float dwv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) dwv[u] = h2f(dwp[nrow * nb + std::min<int64_t>(cb + u, b1 - 1)]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (cb + u >= b1) break;
+            const int piece = 2 * u + kg;
+            const i32x4 wv = *(const i32x4 *)&S.w[buf][nl * 256 + ((piece ^ (nl & 15)) * 16)];
+            i32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0;
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(S.a[buf][u][lane], wv, acc, 0, 0, 0);
+            const float *sd = sdx + (cb + u - b0) * 32;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 d4 = *(const float4 *)(sd + 8 * q + 4 * kg);
+                const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    tot[4 * q + e] = __fadd_rn(tot[4 * q + e], __fmul_rn((float)acc[4 * q + e], __fmul_rn(dwv[u], dv[e])));
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    const int64_t n = nt0 + nl;
+    if (n >= N) return;
+    float *pp = part + (int64_t)blockIdx.y * 32 * N + n;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int t = (r & 3) + 8 * (r >> 2) + 4 * kg;
+        pp[(int64_t)t * N] = tot[r];
+    }
+}
+
 // Y[t][n] = sum_s part[s][t][n] (+ res), or silu(sum_s g) * (sum_s u) with u partials in part2
 __global__ void k_q80s_reduce(const float *__restrict__ part, const float *__restrict__ part2, int S, int64_t M,
                               int64_t N, float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr) {
@@ -1270,8 +1371,12 @@ int kcpp_gemm_q80_segs(const void *const *W, const int64_t *N, int nseg, int64_t
     const int S = q80s_splits(K, Ntot);
     const int64_t nb = K / 32, bps = (nb + S - 1) / S;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_gemm_q80s, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), (size_t)bps * 1152, s, sg, K,
-                       Ntot, (const uint8_t *)act, M, part);
+    if (q80s_version() == 2)
+        hipLaunchKernelGGL(k_gemm_q80s2, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), (size_t)bps * 128, s, sg,
+                           K, Ntot, (const uint8_t *)act, M, part);
+    else
+        hipLaunchKernelGGL(k_gemm_q80s, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), (size_t)bps * 1152, s, sg,
+                           K, Ntot, (const uint8_t *)act, M, part);
     KCPP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * Ntot + 255) / 256)), dim3(256), 0, s, part, nullptr, S, M, Ntot, Y, ldy,
                        nullptr, 0);
@@ -1305,11 +1410,17 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         const int64_t nb = K / 32, bps = (nb + S - 1) / S;
         const dim3 grid((unsigned)((N + 127) / 128), (unsigned)S);
         Q80Segs sg = {{(const uint8_t *)W, nullptr, nullptr}, {N, 0, 0}, 1};
-        hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 1152, s, sg, K, N, (const uint8_t *)act, M, part);
+        auto q80 = [&](float *pt) {
+            if (q80s_version() == 2)
+                hipLaunchKernelGGL(k_gemm_q80s2, grid, dim3(256), (size_t)bps * 128, s, sg, K, N, (const uint8_t *)act, M, pt);
+            else
+                hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 1152, s, sg, K, N, (const uint8_t *)act, M, pt);
+        };
+        q80(part);
         KCPP_CHECK(hipGetLastError());
         if (mode == 1) {
             sg.W[0] = (const uint8_t *)W2;
-            hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 1152, s, sg, K, N, (const uint8_t *)act, M, part2);
+            q80(part2);
             KCPP_CHECK(hipGetLastError());
         }
         hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, mode == 1 ? part2 : nullptr,
