@@ -1206,13 +1206,17 @@ __global__ void __launch_bounds__(256) k_gemm_q80s(const Q80Segs sg, int64_t K, 
 
 // v2 of the small-batch Q8_0 GEMM: the weight tile streams through LDS in row-contiguous pieces.  v1's direct
 // fragment loads touch 32 rows x 32 B per wave instruction (32 cache lines for 1 KiB); here every LDS-DMA wave
-// instruction reads 4 rows x 256 B (8 blocks of each row), 8 such per wave and chunk, into an XOR-swizzled
-// [row][256 B] image (16-B piece c of row n at slot c ^ (n & 15): the B-fragment reads of 32 rows at one piece
-// are conflict-free), double-buffered by 8-block chunks with the activation chunk beside it.  Same block math and
+// instruction reads 64 / (2 CH) rows x 32 CH bytes (CH blocks of each row) into an XOR-swizzled [row][32 CH B] image
+// (16-B piece c of row n at slot c ^ (n % 2CH)), double-buffered by CH-block chunks with the activation chunk beside
+// it; CH = 4 (40 KiB of LDS: three workgroups per CU keep more weight bytes in flight than CH = 8 at one).  Same block math and
 // split-K partials as k_gemm_q80s (bit-identical partials).
+// CH blocks per chunk (4: 40 KiB of LDS, three workgroups per CU)
+#ifndef Q80_CH
+#define Q80_CH 4
+#endif
 struct Q80s2Smem {
-    uint8_t w[2][128 * 256];     // weight chunk [buf][row][256 B] (swizzled 16-B pieces)
-    i32x4 a[2][8][64];           // activation fragments [buf][block][lane]
+    uint8_t w[2][128 * 32 * Q80_CH];  // weight chunk [buf][row][32 CH B] (swizzled 16-B pieces)
+    i32x4 a[2][Q80_CH][64];           // activation fragments [buf][block][lane]
 };
 
 __global__ void __launch_bounds__(256) k_gemm_q80s2(const Q80Segs sg, int64_t K, int64_t N,
@@ -1234,22 +1238,19 @@ __global__ void __launch_bounds__(256) k_gemm_q80s2(const Q80Segs sg, int64_t K,
     const int64_t trow = std::min<int64_t>(lr, M - 1);
     const int8_t *qx = (const int8_t *)act + trow * K + 16 * kg;
     const float *dx = (const float *)(act + M * K);
-    // weight LDS-DMA: wave instruction i covers rows 4i .. 4i+3 (16 lanes each, 16 B per lane); lane -> (row, slot)
-    const int wsub = lane >> 4, wslot = lane & 15;
-    auto stage = [&](int buf, int64_t cb) {                      // chunk = blocks [cb, cb + 8)
+    // weight LDS-DMA: a wave instruction covers RPI rows of 2 CH pieces (16 B per lane); lane -> (row, slot)
+    constexpr int PPR = 2 * Q80_CH, RPI = 64 / PPR, IPW = 128 / RPI / 4;   // pieces per row, rows / instr, instr / wave
+    const int wsub = lane / PPR, wslot = lane % PPR;
+    auto stage = [&](int buf, int64_t cb) {                      // chunk = blocks [cb, cb + CH)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int rl = 4 * (8 * wave + i) + wsub;            // local row 0..127
+        for (int i = 0; i < IPW; ++i) {
+            const int rl = RPI * (IPW * wave + i) + wsub;        // local row 0..127
             const int64_t row = std::min<int64_t>(nt0 - soff + rl, Ns - 1);
-            const int piece = wslot ^ (rl & 15);                 // the 16-B piece this LDS slot holds
+            const int piece = wslot ^ (rl % PPR);                // the 16-B piece this LDS slot holds
             const int64_t blk = std::min<int64_t>(cb + (piece >> 1), b1 - 1);
-            glds16(W + (row * nb + blk) * 32 + 16 * (piece & 1), &S.w[buf][(8 * wave + i) * 1024]);
+            glds16(W + (row * nb + blk) * 32 + 16 * (piece & 1), &S.w[buf][(IPW * wave + i) * 1024]);
         }
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int bl = 2 * wave + u;
-            glds16(qx + std::min<int64_t>(cb + bl, b1 - 1) * 32, &S.a[buf][bl][0]);
-        }
+        if (wave < Q80_CH) glds16(qx + std::min<int64_t>(cb + wave, b1 - 1) * 32, &S.a[buf][wave][0]);
     };
     for (int64_t i = tid; i < (b1 - b0) * 32; i += 256) {
         const int64_t b = i >> 5, t = i & 31;
@@ -1263,17 +1264,17 @@ __global__ void __launch_bounds__(256) k_gemm_q80s2(const Q80Segs sg, int64_t K,
     stage(0, b0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int64_t cb = b0; cb < b1; cb += 8) {
-        const int buf = (int)(((cb - b0) >> 3) & 1);
-        if (cb + 8 < b1) stage(buf ^ 1, cb + 8);
-        float dwv[8];
+    for (int64_t cb = b0; cb < b1; cb += Q80_CH) {
+        const int buf = (int)(((cb - b0) / Q80_CH) & 1);
+        if (cb + Q80_CH < b1) stage(buf ^ 1, cb + Q80_CH);
+        float dwv[Q80_CH];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) dwv[u] = h2f(dwp[nrow * nb + std::min<int64_t>(cb + u, b1 - 1)]);
+        for (int u = 0; u < Q80_CH; ++u) dwv[u] = h2f(dwp[nrow * nb + std::min<int64_t>(cb + u, b1 - 1)]);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < Q80_CH; ++u) {
             if (cb + u >= b1) break;
             const int piece = 2 * u + kg;
-            const i32x4 wv = *(const i32x4 *)&S.w[buf][nl * 256 + ((piece ^ (nl & 15)) * 16)];
+            const i32x4 wv = *(const i32x4 *)&S.w[buf][nl * 32 * Q80_CH + ((piece ^ (nl % PPR)) * 16)];
             i32x16 acc;
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[r] = 0;
