@@ -88,6 +88,9 @@ int kcpp_rs_supported(int type, int64_t K);
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,
                   int64_t nrows, float eps, void *stream);
+/* rms_norm * w quantized to Q8_0 in the same pass (= kcpp_rms_norm then kcpp_quantize_act(Q8_0), bit for bit) */
+int kcpp_rms_norm_q80(const float *x, int64_t ldx, const float *w, void *q80_out, int64_t ne0, int64_t nrows, float eps,
+                      void *stream);
 /* host-side table of (cos, sin) per [pos][D/2], exactly as ggml_rope_cache_init (ggml.c:14246) */
 int kcpp_rope_table(float *tab_host, int n_pos, int n_dims, float freq_base, float freq_scale, const float *freq_factors,
                     float ext_factor, float attn_factor, float beta_fast, float beta_slow, int n_ctx_orig);

@@ -15,7 +15,7 @@
 // group is exactly one Q8_K super-block, so the fused quantization needs only DPP steps.
 __global__ void __launch_bounds__(1024) k_rms_norm(const float *__restrict__ x, int64_t ldx, const float *__restrict__ w,
                                                    float *__restrict__ y, int64_t ldy, uint8_t *__restrict__ qout,
-                                                   int64_t ne0, int64_t nrows, float eps) {
+                                                   int64_t ne0, int64_t nrows, float eps, int q80 = 0) {
     const int64_t r = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (blockDim.x + 63) >> 6;
     const int64_t e0 = (int64_t)tid * 16;
@@ -58,7 +58,31 @@ __global__ void __launch_bounds__(1024) k_rms_norm(const float *__restrict__ x, 
 #pragma unroll
         for (int k = 0; k < 4; ++k) dst[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
     }
-    if (qout) {
+    if (qout && q80) {                                 // Q8_0 as k_quant_q80 (AVX2 semantics), a lane pair per block
+        const int64_t nb = ne0 / 32, ib = tid >> 1;
+        float am = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) am = fmaxf(am, fabsf(v[e]));
+        am = fmaxf(am, __shfl_xor(am, 1, 64));
+        const float dd = am / 127.f;
+        const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+        int qv[16], sq = 0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int iv = (int)rintf(__fmul_rn(v[e], id));
+            qv[e] = iv > 127 ? 127 : (iv < -128 ? -128 : iv);
+            sq += qv[e];
+        }
+        sq += __shfl_xor(sq, 1, 64);
+        int *qs = (int *)((int8_t *)qout + r * ne0 + e0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            qs[k] = (qv[4 * k] & 0xFF) | ((qv[4 * k + 1] & 0xFF) << 8) | ((qv[4 * k + 2] & 0xFF) << 16) | ((qv[4 * k + 3] & 0xFF) << 24);
+        if ((tid & 1) == 0) {
+            ((float *)(qout + nrows * ne0))[r * nb + ib] = h2f(f2h(dd));   // the dot uses GGML_FP16_TO_FP32(y.d)
+            ((int16_t *)(qout + nrows * ne0 + nrows * nb * 4))[r * nb + ib] = (int16_t)sq;
+        }
+    } else if (qout) {
         const int64_t nsb = ne0 / 256, sb = tid >> 4;
         int8_t *qs = (int8_t *)qout + r * ne0 + sb * 256;
         float *d = (float *)(qout + nrows * ne0) + r * nsb + sb;
@@ -143,6 +167,16 @@ int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t
     const unsigned nthr = (unsigned)(ne0 / 16 < 64 ? 64 : ne0 / 16);
     hipLaunchKernelGGL(k_rms_norm, dim3((unsigned)nrows), dim3(nthr), 0, (hipStream_t)stream, x, ldx, w, y,
                        ldy, (uint8_t *)q8k_out, ne0, nrows, eps);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_rms_norm_q80(const float *x, int64_t ldx, const float *w, void *q80_out, int64_t ne0, int64_t nrows, float eps,
+                      void *stream) {
+    if (ne0 % 256 || ne0 > 16384 || !q80_out) return -1;
+    const unsigned nthr = (unsigned)(ne0 / 16 < 64 ? 64 : ne0 / 16);
+    hipLaunchKernelGGL(k_rms_norm, dim3((unsigned)nrows), dim3(nthr), 0, (hipStream_t)stream, x, ldx, w, (float *)nullptr,
+                       (int64_t)0, (uint8_t *)q80_out, ne0, nrows, eps, 1);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

@@ -724,8 +724,7 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             }
         } else if (T > 8 && T <= 32 && t[1].type == KT_Q8_0 && t[2].type == KT_Q8_0 && t[3].type == KT_Q8_0 && E % 128 == 0 &&
                    EKV % 128 == 0) {                 // small-batch Q8_0: one quantization, one q|k|v launch
-            RC(kcpp_rms_norm(m->x, E, (const float *)t[0].d, m->attn, E, nullptr, E, T, hp.eps, s));
-            RC(kcpp_quantize_act(KT_Q8_0, m->attn, E, m->act, E, T, s));
+            RC(kcpp_rms_norm_q80(m->x, E, (const float *)t[0].d, m->act, E, T, hp.eps, s));
             const void *Wq[3] = {t[1].d, t[2].d, t[3].d};
             const int64_t Nq[3] = {E, EKV, EKV};
             RC(kcpp_gemm_q80_segs(Wq, Nq, 3, E, m->act, T, m->qkv, LQ, m->gemm_ws, s));
@@ -748,6 +747,8 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
         const bool gq = kcpp_vec_dot_type(t[6].type) == KT_Q8_K && kcpp_vec_dot_type(t[7].type) == KT_Q8_K;
         if (gq) {
             RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, nullptr, E, m->act, E, T, hp.eps, s));
+        } else if (kcpp_vec_dot_type(t[6].type) == KT_Q8_0 && kcpp_vec_dot_type(t[7].type) == KT_Q8_0) {
+            RC(kcpp_rms_norm_q80(m->x, E, (const float *)t[5].d, m->act, E, T, hp.eps, s));
         } else {
             RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, T, hp.eps, s));
             RC(kcpp_quantize_act(kcpp_vec_dot_type(t[6].type), m->attn, E, m->act, E, T, s));

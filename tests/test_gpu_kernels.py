@@ -406,6 +406,28 @@ def test_gemm_q8_0_small_batch(env, Kd, N, M):
     np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, mode=1, w2=w2), glu, rtol=1e-5, atol=tol)
 
 
+@pytest.mark.parametrize("ne0,nrows", [(4096, 9), (4096, 32), (256, 3), (14336, 5)])
+def test_rms_norm_q80_fused_bitwise(env, ne0, nrows):
+    """rms_norm with the Q8_0 quantization in its epilogue (config 3's norm -> Q8_0 step) must equal
+    kcpp_rms_norm followed by kcpp_quantize_act(Q8_0) byte for byte (qs, d, block sums)"""
+    torch, K = env
+    rng = np.random.default_rng(ne0 + nrows)
+    x = (rng.standard_normal((nrows, ne0)) * 3).astype(np.float32)
+    x[0, :32] = 0.0                                    # an all-zero block: d = 0, id = 0
+    w = rng.standard_normal(ne0).astype(np.float32)
+    xd, wd = dev(torch, x), dev(torch, w)
+    nb = ne0 // 32
+    nbytes = nrows * ne0 + nrows * nb * 4 + nrows * nb * 2
+    y = torch.empty((nrows, ne0), dtype=torch.float32, device="cuda")
+    qa = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    qb = torch.full((nbytes,), 0xA5, dtype=torch.uint8, device="cuda")
+    K.call("kcpp_rms_norm", xd.data_ptr(), ne0, wd.data_ptr(), y.data_ptr(), ne0, None, ne0, nrows, 1e-5, sptr(torch))
+    K.call("kcpp_quantize_act", R.Q8_0, y.data_ptr(), ne0, qa.data_ptr(), ne0, nrows, sptr(torch))
+    K.call("kcpp_rms_norm_q80", xd.data_ptr(), ne0, wd.data_ptr(), qb.data_ptr(), ne0, nrows, 1e-5, sptr(torch))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(host(torch, qb, np.uint8), host(torch, qa, np.uint8))
+
+
 @pytest.mark.parametrize("T,n_past", [(16, 0), (37, 0), (200, 60), (512, 300), (512, 3328), (70, 130)])
 def test_flash_attn_prefill_mfma_v2_bitwise(env, T, n_past):
     """MFMA prefill v2 (next-tile prefetch, V through ds_read_b64_tr_b16) keeps v1's key order and summation
