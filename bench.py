@@ -173,7 +173,7 @@ def other_config(args, K, torch):
         flops = 2 * sum(k * n for i, (k, n) in enumerate(shapes) if i >= 3 and n > 1) * ub
         return {"metric": "prefill tok/s at ubatch 32 (Llama-3-8B Q8_0)", "value": round(r["pre"], 1), "unit": "tok/s",
                 "n_gpus": 1, "higher_is_better": True,
-                "dtype": "q8_0 weights x q8_0 activations (exact int dot on f16 MFMA, f32 accum)", "data": "synthetic",
+                "dtype": "q8_0 weights x q8_0 activations (exact int8 block dots on i8 MFMA, f32 combination)", "data": "synthetic",
                 "config": {"workload": "llama3-8b-q8_0 prefill %d tokens in ubatches of %d" % (n_prompt, ub),
                            "model": "Llama-3-8B-shape Q8_0 random-init", "parallelism": "single GPU"},
                 "ms_per_ubatch": round(t_ub * 1e3, 3), "decode_tok_s": round(r["dec"], 2),
