@@ -63,6 +63,10 @@ int kcpp_gemm_set_variant(int v);
 /* Q8_0 at M <= 32 over nseg <= 3 weights whose outputs sit back to back in Y's columns (q|k|v of one layer,
  * one activation quantization and one launch instead of three); every N_i but the last a multiple of 128;
  * ws from kcpp_gemm_workspace_bytes(KT_Q8_0, K, sum N_i, M) */
+/* silu(W.x) * (W2.x) for Q8_0 weights at M <= 32, emitted directly as Q8_0 activations (the down projection's
+   input; = kcpp_gemm(mode 1) then kcpp_quantize_act(Q8_0), bit for bit).  ws as for kcpp_gemm(KT_Q8_0, K, N, M). */
+int kcpp_gemm_q80_glu_q80(const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, void *qout,
+                          void *ws, void *stream);
 int kcpp_gemm_q80_segs(const void *const *W, const int64_t *N, int nseg, int64_t K, const void *act, int64_t M, float *Y,
                        int64_t ldy, void *ws, void *stream);
 

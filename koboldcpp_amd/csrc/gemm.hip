@@ -1304,16 +1304,37 @@ __global__ void __launch_bounds__(256) k_gemm_q80s2(const Q80Segs sg, int64_t K,
 
 // Y[t][n] = sum_s part[s][t][n] (+ res), or silu(sum_s g) * (sum_s u) with u partials in part2
 __global__ void k_q80s_reduce(const float *__restrict__ part, const float *__restrict__ part2, int S, int64_t M,
-                              int64_t N, float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr) {
+                              int64_t N, float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr,
+                              uint8_t *__restrict__ qout = nullptr) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= M * N) return;
+    if (i >= M * N) return;                            // N % 32 == 0 with qout: whole 32-lane blocks retire together
     const int64_t t = i / N, n = i % N;
     float g = part[t * N + n];
     for (int s = 1; s < S; ++s) g = __fadd_rn(g, part[((int64_t)s * 32 + t) * N + n]);
     if (part2) {
         float u = part2[t * N + n];
         for (int s = 1; s < S; ++s) u = __fadd_rn(u, part2[((int64_t)s * 32 + t) * N + n]);
-        Y[t * ldy + n] = (g / (1.0f + expf(-g))) * u;
+        const float h = (g / (1.0f + expf(-g))) * u;
+        if (!qout) {
+            Y[t * ldy + n] = h;
+            return;
+        }
+        // h quantized to Q8_0 for the down projection, as k_quant_q80: one 32-lane group per block
+        float am = fabsf(h);
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) am = fmaxf(am, __shfl_xor(am, o, 32));
+        const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+        int q = (int)rintf(__fmul_rn(h, id));
+        q = q > 127 ? 127 : (q < -128 ? -128 : q);
+        int sq = q;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) sq += __shfl_xor(sq, o, 32);
+        const int64_t nb = N / 32, b = t * nb + n / 32;
+        ((int8_t *)qout)[t * N + n] = (int8_t)q;
+        if ((n & 31) == 0) {
+            ((float *)(qout + M * N))[b] = h2f(f2h(am / 127.f));
+            ((int16_t *)(qout + M * N + M * nb * 4))[b] = (int16_t)sq;
+        }
     } else {
         Y[t * ldy + n] = res ? __fadd_rn(g, res[t * ldr + n]) : g;
     }
@@ -1343,6 +1364,35 @@ static int g_gemm_variant = -1;
 static int gemm_variant() {
     if (g_gemm_variant < 0) g_gemm_variant = getenv("KCPP_GEMM_V") ? atoi(getenv("KCPP_GEMM_V")) : 0;
     return g_gemm_variant;
+}
+
+// BASELINE config 3's small-batch Q8_0 path: split-K int8-MFMA partials, then the ordered reduce (plain, + residual,
+// silu(g) * u, or silu(g) * u quantized straight to Q8_0 into qout for the next GEMM)
+static int gemm_q80_small(const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
+                          int64_t ldy, const float *res, int64_t ldr, int mode, uint8_t *qout, uint8_t *wsp, hipStream_t s) {
+    const int S = q80s_splits(K, N);
+    float *part = (float *)wsp;
+    float *part2 = part + (int64_t)S * 32 * N;
+    const int64_t nb = K / 32, bps = (nb + S - 1) / S;
+    const dim3 grid((unsigned)((N + 127) / 128), (unsigned)S);
+    Q80Segs sg = {{(const uint8_t *)W, nullptr, nullptr}, {N, 0, 0}, 1};
+    auto q80 = [&](float *pt) {
+        if (q80s_version() == 2)
+            hipLaunchKernelGGL(k_gemm_q80s2, grid, dim3(256), (size_t)bps * 128, s, sg, K, N, (const uint8_t *)act, M, pt);
+        else
+            hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 1152, s, sg, K, N, (const uint8_t *)act, M, pt);
+    };
+    q80(part);
+    KCPP_CHECK(hipGetLastError());
+    if (mode == 1) {
+        sg.W[0] = (const uint8_t *)W2;
+        q80(part2);
+        KCPP_CHECK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, mode == 1 ? part2 : nullptr,
+                       S, M, N, Y, ldy, mode == 1 ? nullptr : res, ldr, qout);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
 }
 
 extern "C" {
@@ -1390,6 +1440,15 @@ int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M) {
     return ws_layout(type, K, N, M, a, b, c, d);
 }
 
+int kcpp_gemm_q80_glu_q80(const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, void *qout,
+                          void *ws, void *stream) {
+    if (M < 1 || M > 32 || K % 32 || N % 32 || !ws || !qout) return -1;
+    int64_t o_a16, o_dy, o_bs, o_up;
+    ws_layout(KT_Q8_0, K, N, M, o_a16, o_dy, o_bs, o_up);
+    return gemm_q80_small(W, W2, K, N, act, M, nullptr, 0, nullptr, 0, 1, (uint8_t *)qout,
+                          (uint8_t *)ws + o_up + ((M * N * 4 + 255) & ~255LL), (hipStream_t)stream);
+}
+
 int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream) {
     hipStream_t s = (hipStream_t)stream;
@@ -1404,31 +1463,8 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     _Float16 *bs16 = (_Float16 *)(w8 + o_bs);
     float *up = (float *)(w8 + o_up);
     const int vt = vec_dot_type(type);
-    if (type == KT_Q8_0 && M <= 32 && K % 32 == 0) {
-        const int S = q80s_splits(K, N);
-        float *part = (float *)(w8 + o_up + ((M * N * 4 + 255) & ~255LL));
-        float *part2 = part + (int64_t)S * 32 * N;
-        const int64_t nb = K / 32, bps = (nb + S - 1) / S;
-        const dim3 grid((unsigned)((N + 127) / 128), (unsigned)S);
-        Q80Segs sg = {{(const uint8_t *)W, nullptr, nullptr}, {N, 0, 0}, 1};
-        auto q80 = [&](float *pt) {
-            if (q80s_version() == 2)
-                hipLaunchKernelGGL(k_gemm_q80s2, grid, dim3(256), (size_t)bps * 128, s, sg, K, N, (const uint8_t *)act, M, pt);
-            else
-                hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 1152, s, sg, K, N, (const uint8_t *)act, M, pt);
-        };
-        q80(part);
-        KCPP_CHECK(hipGetLastError());
-        if (mode == 1) {
-            sg.W[0] = (const uint8_t *)W2;
-            q80(part2);
-            KCPP_CHECK(hipGetLastError());
-        }
-        hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, mode == 1 ? part2 : nullptr,
-                           S, M, N, Y, ldy, mode == 1 ? nullptr : res, ldr);
-        KCPP_CHECK(hipGetLastError());
-        return 0;
-    }
+    if (type == KT_Q8_0 && M <= 32 && K % 32 == 0) return gemm_q80_small(W, W2, K, N, act, M, Y, ldy, res, ldr, mode, nullptr,
+                                                                        w8 + o_up + ((M * N * 4 + 255) & ~255LL), s);
     // v3: 128 tokens x 128 rows per workgroup when that gives >= 384 workgroups, else 64 x 128 (BMT = 2);
     // KCPP_GEMM_V / kcpp_gemm_set_variant: 2 forces v2, 3 forces v3
     const int gv = gemm_variant();

@@ -758,6 +758,9 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             f.N = 2 * F;                               // silu(g)*u fused into the Q8_K quantization
             RC(matmul(m, f, nullptr, m->act, T, m->hglu, 2 * F, nullptr, 0, 0));
             RC(kcpp_quantize_act_glu(m->hglu, 2 * F, F, m->act2, F, T, s));
+        } else if (T <= 32 && t[6].type == KT_Q8_0 && t[7].type == KT_Q8_0 && kcpp_vec_dot_type(t[8].type) == KT_Q8_0 &&
+                   F % 32 == 0) {
+            RC(kcpp_gemm_q80_glu_q80(t[6].d, t[7].d, E, F, m->act, T, m->act2, m->gemm_ws, s));   // Q8_0(silu(g) * u)
         } else {
             if (t[6].type == t[7].type) {
                 RC(matmul(m, t[6], &t[7], m->act, T, m->h, F, nullptr, 0, 1));          // h = silu(g) * u

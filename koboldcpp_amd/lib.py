@@ -38,6 +38,7 @@ _SIGS = {
     "kcpp_gemm": [I, P, P, I64, I64, P, I64, P, I64, P, I64, I, P, P],
     "kcpp_rms_norm": [P, I64, P, P, I64, P, I64, I64, Fl, P],
     "kcpp_rms_norm_q80": [P, I64, P, P, I64, I64, Fl, P],
+    "kcpp_gemm_q80_glu_q80": [P, P, I64, I64, P, I64, P, P, P],
     "kcpp_rope_table": [P, I, I, Fl, Fl, P, Fl, Fl, Fl, Fl, I],
     "kcpp_rope_row": [P, I, I, Fl, Fl, Fl, Fl, Fl, Fl, I],
     "kcpp_kv_shift_rows": [P, P, P, P, I64, I, P, P],

@@ -406,6 +406,33 @@ def test_gemm_q8_0_small_batch(env, Kd, N, M):
     np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, mode=1, w2=w2), glu, rtol=1e-5, atol=tol)
 
 
+@pytest.mark.parametrize("Kd,N,M", [(4096, 14336, 32), (4096, 1024, 9), (256, 96, 1)])
+def test_gemm_q80_glu_q80_bitwise(env, Kd, N, M):
+    """config 3's gate|up GEMM with the Q8_0 quantization of silu(g) * u in its reduce must equal kcpp_gemm(mode 1)
+    followed by kcpp_quantize_act(Q8_0) byte for byte"""
+    torch, K = env
+    t = R.Q8_0
+    rng = np.random.default_rng(Kd + N + M)
+    wd = upload_weight(torch, K, t, R.synth(t, 5, 710, Kd, N), Kd, N)
+    w2d = upload_weight(torch, K, t, R.synth(t, 5, 711, Kd, N), Kd, N)
+    xd = dev(torch, rng.standard_normal((M, Kd)).astype(np.float32))
+    act = empty(torch, K.act_bytes(t, Kd, M))
+    K.call("kcpp_quantize_act", K.vec_dot_type(t), xd.data_ptr(), Kd, act.data_ptr(), Kd, M, sptr(torch))
+    ws = empty(torch, K.raw().kcpp_gemm_workspace_bytes(t, Kd, N, M))
+    Y = torch.empty((M, N), dtype=torch.float32, device="cuda")
+    K.call("kcpp_gemm", t, wd.data_ptr(), w2d.data_ptr(), Kd, N, act.data_ptr(), M, Y.data_ptr(), N, None, N, 1,
+           ws.data_ptr(), sptr(torch))
+    nbytes = K.act_bytes(t, N, M)
+    qa = torch.zeros(nbytes, dtype=torch.uint8, device="cuda")
+    qb = torch.full((nbytes,), 0xA5, dtype=torch.uint8, device="cuda")
+    K.call("kcpp_quantize_act", K.vec_dot_type(t), Y.data_ptr(), N, qa.data_ptr(), N, M, sptr(torch))
+    K.call("kcpp_gemm_q80_glu_q80", wd.data_ptr(), w2d.data_ptr(), Kd, N, act.data_ptr(), M, qb.data_ptr(), ws.data_ptr(),
+           sptr(torch))
+    torch.cuda.synchronize()
+    used = M * N + M * (N // 32) * 6                   # qs, d (f32), block sums (i16)
+    np.testing.assert_array_equal(host(torch, qb, np.uint8)[:used], host(torch, qa, np.uint8)[:used])
+
+
 @pytest.mark.parametrize("ne0,nrows", [(4096, 9), (4096, 32), (256, 3), (14336, 5)])
 def test_rms_norm_q80_fused_bitwise(env, ne0, nrows):
     """rms_norm with the Q8_0 quantization in its epilogue (config 3's norm -> Q8_0 step) must equal
