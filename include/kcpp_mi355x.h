@@ -114,6 +114,15 @@ int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max);
 int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qout, void *ws,
                     int T, int H, int HKV, int D, int n_past, const int32_t *n_past_dev, int n_kv_max, float scale,
                     int force_path, void *stream);
+/* single-token decode attention with explicit cache strides in elements (key p of kv head hk at
+ * kc + p*kv_ld + hk*kv_hs); variant 0: 64-key chunks + combine, 1: splits with in-launch merge, 2: splits +
+ * combine (A/B measurement entry, tools/fa_dec_bench.py) */
+int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
+                      float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
+                      int n_kv_max, float scale, int variant, void *stream);
+/* diagnostic: per-workgroup phase stamps of the split-KV decode kernel (s_memrealtime, 8 per workgroup) into p
+ * (device, or NULL to disable); tools only */
+void kcpp_fa_set_stamps(void *p);
 /* the MFMA prefill kernel alone (koboldcpp_amd/csrc/attn_mfma.hip); -3 when the shape is not covered */
 int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, int T, int H,
                                  int HKV, int D, int n_past, float scale, void *stream);
@@ -240,6 +249,15 @@ int kcpp_model_set_graphs(kcpp_model *m, int enable);
 int kcpp_model_set_fused_decode(kcpp_model *m, int enable);
 int64_t kcpp_model_weight_bytes(kcpp_model *m);
 const char *kcpp_last_error(void);
+
+/* GGUF parse + tensor-table bounds validation alone (load_model's first step): 0 ok, -1 with the reason in err */
+int kcpp_gguf_check(const char *path, char *err, int err_len);
+/* generate()'s restated sampler chain (SampleLogits, gpttype_adapter.cpp:1338-1434) on caller logits, for the
+ * host-side parity test (koboldcpp_amd/csrc/expose.cpp documents fp / ip / restarts); returns the drawn token */
+int kcpp_sampler_probe(const float *logits, int n_vocab, int n_ctx, const float *fp, const int *ip, const int *order,
+                       int n_order, const int *ctx_toks, int n_ctx_toks, const int *last_n, int n_last,
+                       const int *restarts, int n_restart_ints, unsigned seed, float *mu, int *out_ids, float *out_p,
+                       int cap, int *out_n);
 
 #ifdef __cplusplus
 }

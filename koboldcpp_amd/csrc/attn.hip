@@ -17,6 +17,7 @@
 
 #define FA_CHUNK 64
 #define FA_MAXG 8
+#define FA_MAX_CHUNKS 2048          // k_fa_combine's chunk-weight table: 2048 x 64 = 131072 keys
 
 // K/V cache layout: [pos][HKV][D] f16, row stride EKV = HKV*D elements.
 // Query layout: q16 [T][H][D] f16.  Query t sits at absolute position n_past + t.
@@ -34,7 +35,7 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
                                                    float *__restrict__ out, uint8_t *__restrict__ qout, int T, int H,
                                                    int HKV, int n_past_arg, const int32_t *__restrict__ n_past_dev,
                                                    int n_chunks, float scale, const uint16_t *__restrict__ mask,
-                                                   int64_t mask_ld) {
+                                                   int64_t mask_ld, int64_t kv_ld, int64_t kv_hs) {
     static_assert(D == 128, "head dim 128");
     const int c = blockIdx.x, hk = blockIdx.y, t = blockIdx.z;
     const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
@@ -47,7 +48,6 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
     const int p0 = c * FA_CHUNK;
     const int p1 = min(p0 + FA_CHUNK, kend);              // exclusive
     const uint16_t *mrow = mask ? mask + (int64_t)t * mask_ld : nullptr;
-    const int64_t EKV = (int64_t)HKV * D;
     __shared__ float s_sc[G][FA_CHUNK];
     __shared__ float s_red[4][G][D];
     __shared__ float s_m[G], s_l[G];
@@ -67,7 +67,7 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
 #pragma unroll
     for (int i = 0; i < KPW / 4; ++i) {
         const int p = p0 + KPW * wave + 4 * i + kq;
-        kk[i] = p < p1 ? *(const uint4 *)(kc + (int64_t)p * EKV + hk * D + sub * 8) : make_uint4(0, 0, 0, 0);
+        kk[i] = p < p1 ? *(const uint4 *)(kc + (int64_t)p * kv_ld + hk * kv_hs + sub * 8) : make_uint4(0, 0, 0, 0);
     }
     uint32_t vv[KPW];
 #pragma unroll
@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
         const int p = p0 + KPW * wave + i;
         // masked keys are skipped like the CPU does (their V never enters the sum, even if not finite)
         const bool use = p < p1 && !(mrow && mrow[p] == 0xFC00);
-        vv[i] = use ? *(const uint32_t *)(vc + (int64_t)p * EKV + hk * D + 2 * lane) : 0u;
+        vv[i] = use ? *(const uint32_t *)(vc + (int64_t)p * kv_ld + hk * kv_hs + 2 * lane) : 0u;
     }
 #pragma unroll
     for (int i = 0; i < KPW / 4; ++i) {
@@ -236,8 +236,18 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
                                                  float2 *__restrict__ part_ml, unsigned *__restrict__ tickets,
                                                  float *__restrict__ out, uint8_t *__restrict__ qout, int H, int HKV,
                                                  int n_past_arg, const int32_t *__restrict__ n_past_dev, float scale,
-                                                 int probe) {
+                                                 int probe, int64_t kv_ld, int64_t kv_hs,
+                                                 unsigned long long *__restrict__ stamps) {
     constexpr int D = 128;
+    // diagnostic phase stamps (tools/fa_dec_bench.py): s_memrealtime (100 MHz, chip-wide) per workgroup,
+    // written by lane 0 of wave 0 with a vector store; stamps == nullptr in every product launch
+    const int wg_id = blockIdx.y * gridDim.x + blockIdx.x;
+#define FA_STAMP(ph)                                                                                   \
+    if (stamps && threadIdx.x == 0) {                                                                  \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
+        __hip_atomic_store(&stamps[wg_id * 8 + (ph)], t_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+    }
+    FA_STAMP(0);
     const int sp = blockIdx.x, NS = gridDim.x, hk = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int sub = lane & 15, kq = lane >> 4;
@@ -245,7 +255,6 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
     const int nkv = n_past + 1;
     const int per = ((nkv + NS - 1) / NS + 3) & ~3;
     const int p0 = min(sp * per, nkv), p1 = min(p0 + per, nkv);
-    const int64_t EKV = (int64_t)HKV * D;
     __shared__ float s_o[FA2_W][G][D];
     __shared__ float s_m[FA2_W][G], s_l[FA2_W][G];
     __shared__ int s_last;
@@ -258,6 +267,7 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
 #pragma unroll
         for (int i = 0; i < 4; ++i) { qv[g][2 * i] = h2f(w4[i] & 0xFFFF); qv[g][2 * i + 1] = h2f(w4[i] >> 16); }
     }
+    if (stamps) { if (qv[0][0] == 12345.0f) stamps[0] = 0; FA_STAMP(1); }
     float m[G], l[G], acc[G][8];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -265,18 +275,18 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[g][e] = 0.0f;
     }
-    const uint16_t *kb = kc + hk * D + sub * 8, *vb = vc + hk * D + sub * 8;
+    const uint16_t *kb = kc + hk * kv_hs + sub * 8, *vb = vc + hk * kv_hs + sub * 8;
     uint4 kk[4], vv[4];
     auto load_kv = [&](int c0, uint4 (&kr)[4], uint4 (&vr)[4]) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int p = c0 + 16 * wave + 4 * i + kq;
-            kr[i] = p < p1 ? *(const uint4 *)(kb + (int64_t)p * EKV) : make_uint4(0, 0, 0, 0);
+            kr[i] = p < p1 ? *(const uint4 *)(kb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int p = c0 + 16 * wave + 4 * i + kq;
-            vr[i] = p < p1 ? *(const uint4 *)(vb + (int64_t)p * EKV) : make_uint4(0, 0, 0, 0);
+            vr[i] = p < p1 ? *(const uint4 *)(vb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
         }
     };
     constexpr bool PF = true;                                       // register budget of the prefetch
@@ -334,6 +344,7 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
             for (int i = 0; i < 4; ++i) { kk[i] = kn[i]; vv[i] = vn[i]; }
         }
     }
+    FA_STAMP(2);
     // wave merge over its 4 key rows (kq): m is wave-uniform, l and acc are per row
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -383,8 +394,13 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
         }
         st_sc1_f2(pml + g, make_float2(M, L));
     }
-    if (tickets == nullptr) return;                                 // probe: partials only (tools/microbench.py)
+    FA_STAMP(3);
+    if (tickets == nullptr) {                                       // partials only (combine kernel follows)
+        if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(4); }
+        return;
+    }
     if (probe != 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    FA_STAMP(4);
     __syncthreads();
     if (tid == 0) {
         const unsigned prev = __hip_atomic_fetch_add(&tickets[hk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -392,6 +408,7 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
         if (s_last) __hip_atomic_store(&tickets[hk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    FA_STAMP(5);
     if (!s_last || probe == 3) return;
     // ---- last split of this kv head: merge the NS partials (sc1 loads only).  SS adjacent lanes share one
     // 4-dim quad of one head, each loading every SS-th split (16-B loads, all issued before use), then
@@ -438,6 +455,7 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
             }
         }
     }
+    FA_STAMP(6);
     if (qout == nullptr || G * D < 256) return;
     __syncthreads();
     const int nsbk = G * D / 256;
@@ -453,6 +471,8 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
         int16_t *bs = (int16_t *)(qout + E + nsb * 4) + sbg * 16;
         q8k_quant16(v, l16, qs, dp, bs);
     }
+    if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(7); }
+#undef FA_STAMP
 }
 
 // combine of k_fa_dec2's partials (decode v3 = k_fa_dec2 without tickets + this): one 256-thread workgroup
@@ -521,7 +541,7 @@ __global__ void __launch_bounds__(1024) k_fa_combine(const float *__restrict__ p
                                                      float *__restrict__ out, uint8_t *__restrict__ qout, int T, int H,
                                                      int D, int n_past_arg, const int32_t *__restrict__ n_past_dev,
                                                      int n_chunks_alloc, int masked) {
-    constexpr int MAXCH = 4096 / FA_CHUNK * 4;         // 16k context
+    constexpr int MAXCH = FA_MAX_CHUNKS;               // 128k context
     const int t = blockIdx.y;
     const int pair = blockIdx.x;                       // heads 2*pair, 2*pair+1
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -543,8 +563,10 @@ __global__ void __launch_bounds__(1024) k_fa_combine(const float *__restrict__ p
         const int c = cg + 4 * k;
         ov[k] = c < nch ? po[(int64_t)c * 128] : 0.0f;
     }
-    // M = max_c m_c per head: waves 0-7 hold head 0's chunks, 8-15 head 1's
-    float M = wave_max(mlv.x);
+    // M = max_c m_c per head: waves 0-7 hold head 0's chunks, 8-15 head 1's (chunks beyond 512: strided)
+    float mloc = mlv.x;
+    for (int c = r + 512; c < nch; c += 512) mloc = fmaxf(mloc, ml[c].x);
+    float M = wave_max(mloc);
     if (lane == 0) s_red[wave] = M;
     __syncthreads();
     M = s_red[8 * hl];
@@ -552,7 +574,14 @@ __global__ void __launch_bounds__(1024) k_fa_combine(const float *__restrict__ p
     for (int w = 1; w < 8; ++w) M = fmaxf(M, s_red[8 * hl + w]);
     const float wgt = mlv.x == -INFINITY ? 0.0f : expf(mlv.x - M);
     if (r < MAXCH) s_w[hl][r] = wgt;
-    float L = wave_sum(wgt * mlv.y);
+    float lsum = wgt * mlv.y;
+    for (int c = r + 512; c < nch; c += 512) {
+        const float2 v = ml[c];
+        const float w2 = v.x == -INFINITY ? 0.0f : expf(v.x - M);
+        s_w[hl][c] = w2;
+        lsum = fmaf(w2, v.y, lsum);
+    }
+    float L = wave_sum(lsum);
     __syncthreads();                                   // s_red reuse + s_w visible
     if (lane == 0) s_red[wave] = L;
     __syncthreads();
@@ -766,10 +795,10 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
         float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
         const dim3 grid(NS, HKV);
         switch (G0) {
-        case 1: hipLaunchKernelGGL(k_fa_dec2<1>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge); break;
-        case 2: hipLaunchKernelGGL(k_fa_dec2<2>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge); break;
-        case 4: hipLaunchKernelGGL(k_fa_dec2<4>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge); break;
-        default: hipLaunchKernelGGL(k_fa_dec2<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge); break;
+        case 1: hipLaunchKernelGGL(k_fa_dec2<1>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge, (int64_t)HKV * 128, (int64_t)128, nullptr); break;
+        case 2: hipLaunchKernelGGL(k_fa_dec2<2>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge, (int64_t)HKV * 128, (int64_t)128, nullptr); break;
+        case 4: hipLaunchKernelGGL(k_fa_dec2<4>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge, (int64_t)HKV * 128, (int64_t)128, nullptr); break;
+        default: hipLaunchKernelGGL(k_fa_dec2<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge, (int64_t)HKV * 128, (int64_t)128, nullptr); break;
         }
         KCPP_CHECK(hipGetLastError());
         if (v3) {
@@ -788,22 +817,24 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
         ws = (uint8_t *)ws + FA_WS_TICKETS;
         const int nkv = n_past_dev ? n_kv_max : n_past + T;
         const int nch = (nkv + FA_CHUNK - 1) / FA_CHUNK;
-        if (nch > 4096 / FA_CHUNK * 4) return -4;       // combine's chunk-weight table (16k context)
+        if (nch > FA_MAX_CHUNKS) return -4;              // combine's chunk-weight table (128k context)
         float *po = (float *)ws;
         float2 *pml = (float2 *)(po + (int64_t)T * H * nch * 128);
         const dim3 grid(nch, HKV, T);
         int *tickets = (int *)(pml + (int64_t)T * H * nch);
         const int G = H / HKV;
         static const int fuse_env = getenv("KCPP_FA_FUSED") ? atoi(getenv("KCPP_FA_FUSED")) : 0;
-        const bool fused = fuse_env && G >= 2;           // one kv head's outputs must fill Q8_K blocks
+        const bool fused = fuse_env && G >= 2 && nch <= 4096 / FA_CHUNK * 4;   // (its merge table: 16k keys)
 #define KCPP_FA_CASE(GG)                                                                                       \
     case GG:                                                                                                   \
         if (fused)                                                                                             \
             hipLaunchKernelGGL((k_fa_decode<128, GG, true>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, \
-                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale, nullptr, -1); \
+                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale, nullptr, -1,   \
+                               (int64_t)HKV * 128, (int64_t)128);                                          \
         else                                                                                                   \
             hipLaunchKernelGGL((k_fa_decode<128, GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, \
-                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale, nullptr, -1); \
+                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale, nullptr, -1,   \
+                               (int64_t)HKV * 128, (int64_t)128);                                          \
         break;
         switch (G) {
             KCPP_FA_CASE(1)
@@ -842,6 +873,65 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     return 0;
 }
 
+// single-token decode attention with explicit cache strides (elements): key p of kv head hk starts at
+// kc + p * kv_ld + hk * kv_hs.  Position-major ggml view: kv_ld = HKV*D, kv_hs = D; head-major: kv_ld = D,
+// kv_hs = n_ctx*D.  variant 0: 64-key chunks + k_fa_combine; 1: NS splits, last arriver merges in-launch;
+// 2: NS splits + k_fa_combine2.  (tools/fa_dec_bench.py)
+static void *g_fa_stamps = nullptr;
+void kcpp_fa_set_stamps(void *p) { g_fa_stamps = p; }     // diagnostic stamp buffer of k_fa_dec2 (tools only)
+int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
+                      float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
+                      int n_kv_max, float scale, int variant, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const int G = H / HKV;
+    if (H % HKV || !(G == 1 || G == 2 || G == 4 || G == 8) || (H % 2) || HKV > 64) return -1;
+    if (qout && G < 2) return -1;
+    const int nkv = n_past_dev ? n_kv_max : n_past + 1;
+    if (variant == 0) {
+        const int nch = (nkv + FA_CHUNK - 1) / FA_CHUNK;
+        if (nch > FA_MAX_CHUNKS) return -4;
+        float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
+        float2 *pml = (float2 *)(po + (int64_t)H * nch * 128);
+        const dim3 grid(nch, HKV, 1);
+#define KCPP_FA_CASE(GG)                                                                                         \
+    case GG:                                                                                                     \
+        hipLaunchKernelGGL((k_fa_decode<128, GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, nullptr, out, \
+                           (uint8_t *)qout, 1, H, HKV, n_past, n_past_dev, nch, scale, nullptr, -1, kv_ld, kv_hs); \
+        break;
+        switch (G) { KCPP_FA_CASE(1) KCPP_FA_CASE(2) KCPP_FA_CASE(4) KCPP_FA_CASE(8) }
+#undef KCPP_FA_CASE
+        KCPP_CHECK(hipGetLastError());
+        if (qout) hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, 1), dim3(1024), 0, s, po, pml, out, (uint8_t *)qout, 1, H, 128, n_past, n_past_dev, nch, 0);
+        else hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, 1), dim3(1024), 0, s, po, pml, out, (uint8_t *)nullptr, 1, H, 128, n_past, n_past_dev, nch, 0);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
+    const int NS = std::max(1, std::min(FA2_NS, (nkv + 127) / 128));
+    unsigned *tickets = variant == 1 ? (unsigned *)ws : nullptr;
+    float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
+    float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
+    const dim3 grid(NS, HKV);
+    const int probe = variant == 1 ? 0 : 1;
+    switch (G) {
+    case 1: hipLaunchKernelGGL(k_fa_dec2<1>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, probe, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
+    case 2: hipLaunchKernelGGL(k_fa_dec2<2>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, probe, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
+    case 4: hipLaunchKernelGGL(k_fa_dec2<4>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, probe, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
+    default: hipLaunchKernelGGL(k_fa_dec2<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, probe, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
+    }
+    KCPP_CHECK(hipGetLastError());
+    if (variant == 2) {
+#define KCPP_FA_C2(GG)                                                                                                     \
+    case GG:                                                                                                               \
+        if (qout) hipLaunchKernelGGL((k_fa_combine2<GG, true>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS); \
+        else hipLaunchKernelGGL((k_fa_combine2<GG, false>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS);    \
+        break;
+        switch (G) { KCPP_FA_C2(1) KCPP_FA_C2(2) KCPP_FA_C2(4) KCPP_FA_C2(8) }
+#undef KCPP_FA_C2
+        KCPP_CHECK(hipGetLastError());
+    }
+    return 0;
+}
+
 // GGML_OP_FLASH_ATTN_EXT as the ggml graph states it (the b1 backend path): q f32 [D][T][H] with byte
 // strides (q_nb1 between queries, q_nb2 between heads), K/V f16 cache views [n_kv][HKV][D] (row stride
 // HKV*D), mask f16 [T_pad][n_kv] (row stride mask_ld elements, 0 / -inf, may be null = no mask), out f32
@@ -869,7 +959,7 @@ int kcpp_flash_attn_ext(const float *q, int64_t q_nb1, int64_t q_nb2, const uint
     if (mask_ld < 0) mask_ld = 0;
     if (T <= 16) {
         const int nch = (n_kv + FA_CHUNK - 1) / FA_CHUNK;
-        if (nch > 4096 / FA_CHUNK * 4) return -4;
+        if (nch > FA_MAX_CHUNKS) return -4;
         float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
         float2 *pml = (float2 *)(po + (int64_t)T * H * nch * 128);
         int *tickets = (int *)(pml + (int64_t)T * H * nch);
@@ -877,7 +967,8 @@ int kcpp_flash_attn_ext(const float *q, int64_t q_nb1, int64_t q_nb2, const uint
 #define KCPP_FA_CASE(GG)                                                                                          \
     case GG:                                                                                                      \
         hipLaunchKernelGGL((k_fa_decode<128, GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, \
-                           (uint8_t *)nullptr, T, H, HKV, n_kv, nullptr, nch, scale, mask, mask_ld);              \
+                           (uint8_t *)nullptr, T, H, HKV, n_kv, nullptr, nch, scale, mask, mask_ld,                \
+                           (int64_t)HKV * 128, (int64_t)128);                                                     \
         break;
         switch (H / HKV) {
             KCPP_FA_CASE(1)

@@ -10,13 +10,16 @@
 //                  ("fast forward", gpttype_adapter.cpp:2929-2945), prefill in ubatches, sampling, streaming
 //                  text through new_token()/get_pending_output(), stop on EOS / stop sequences / max_length /
 //                  abort; last_process_time / last_eval_time in ms per token (gpttype_adapter.cpp:3513-3526).
-// Sampling is host code (as in the reference): repetition penalty over rep_pen_range, logit biases,
-// top-k, top-p, min-p, temperature, seeded mt19937; temperature <= 0 or top_k == 1 is greedy on the device.
+// Sampling is host code (as in the reference): the full SampleLogits chain restated in sampler.h (logit biases,
+// DRY, rep_pen, top-k/a/p, min-p, tfs, typical, temperature / dynatemp / smoothing, mirostat, XTC) over
+// the user's sampler_order and a seeded mt19937; when that chain reduces to argmax (greedy, no biases /
+// penalties / bans) the token comes from the on-device argmax instead of a logits copy.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <ctime>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -30,6 +33,7 @@
 #include "../../include/kcpp_mi355x.h"
 #include "../../include/kcpp_synth.h"
 #include "gguf.h"
+#include "sampler.h"
 #include "tokenizer.h"
 
 namespace {
@@ -55,6 +59,7 @@ std::string g_concat, g_result, g_pending;
 std::atomic<bool> g_finished{true}, g_abort{false};
 float g_last_eval = 0, g_last_process = 0;
 int g_last_count = 0, g_last_seed = 0, g_total_gens = 0;
+float g_mirostat_mu = 0.0f;
 int g_last_stop = KCPP_STOP_INVALID;
 std::vector<int> g_count_ids;
 
@@ -101,63 +106,132 @@ int forward(Engine &e, const int32_t *toks, int T, int n_past) {
     return 0;
 }
 
-int sample(Engine &e, const generation_inputs &in, const std::vector<int> &recent, std::mt19937 &rng, bool greedy) {
-    kcpp_model *last = e.stages.back();
-    if (greedy && in.rep_pen <= 1.0f) {
-        int32_t t = 0;
-        kcpp_model_argmax(last, &t);
-        return t;
-    }
-    // host sampling over the logits of the last position (the reference samples on the host too)
-    e.logits.resize(e.hp.n_vocab);
-    int32_t dummy;
-    (void)dummy;
-    {
-        // re-run nothing: copy the head output of the last decode
-        if (kcpp_model_read_logits(last, e.logits.data())) return e.tok.eos();
-    }
-    std::vector<float> &l = e.logits;
-    for (int k = 0; k < KCPP_LOGIT_BIAS_MAX; ++k) {
-        const logit_bias &b = in.logit_biases[k];
-        if (b.token_id > 0 && b.token_id < (int)l.size() && b.bias != 0.0f) l[b.token_id] += b.bias;
-    }
-    if (in.rep_pen > 1.0f) {
-        const int range = in.rep_pen_range > 0 ? in.rep_pen_range : (int)recent.size();
-        for (int k = std::max(0, (int)recent.size() - range); k < (int)recent.size(); ++k) {
-            float &v = l[recent[k]];
-            v = v > 0 ? v / in.rep_pen : v * in.rep_pen;
-        }
-    }
-    if (greedy) return (int)(std::max_element(l.begin(), l.end()) - l.begin());
-    std::vector<int> idx(l.size());
-    for (size_t k = 0; k < idx.size(); ++k) idx[k] = (int)k;
-    const int topk = in.top_k > 0 ? std::min<int>(in.top_k, (int)idx.size()) : (int)idx.size();
-    std::partial_sort(idx.begin(), idx.begin() + topk, idx.end(), [&](int a, int b) { return l[a] > l[b]; });
-    idx.resize(topk);
-    const float temp = in.temperature > 0 ? in.temperature : 1.0f;
-    std::vector<double> p(idx.size());
-    const double mx = l[idx[0]];
-    double sum = 0;
-    for (size_t k = 0; k < idx.size(); ++k) { p[k] = std::exp((l[idx[k]] - mx) / temp); sum += p[k]; }
-    for (auto &v : p) v /= sum;
-    size_t keep = p.size();
-    if (in.top_p > 0 && in.top_p < 1) {
-        double c = 0;
-        for (size_t k = 0; k < p.size(); ++k) { c += p[k]; if (c >= in.top_p) { keep = k + 1; break; } }
-    }
-    if (in.min_p > 0) {
-        size_t k2 = 0;
-        while (k2 < keep && p[k2] >= in.min_p * p[0]) ++k2;
-        keep = std::max<size_t>(1, k2);
-    }
-    double tot = 0;
-    for (size_t k = 0; k < keep; ++k) tot += p[k];
-    std::uniform_real_distribution<double> u(0.0, tot);
-    double r = u(rng);
-    for (size_t k = 0; k < keep; ++k) { r -= p[k]; if (r <= 0) return idx[k]; }
-    return idx[keep - 1];
+// per-generate sampler state: the reference's parameter clamps (gpttype_adapter.cpp:2576-2584, 2625-2735),
+// sampler order (:2957-2976), DRY restart sequences (:2650-2700), single-character token bans (:2518-2568)
+struct SamplerSetup {
+    ksamp::Params P;
+    std::vector<ksamp::LogitBias> biases;
+    ksamp::RestartSeqs restarts;
+    std::vector<int> banned;
+    int n_ctx = 0;
+    bool suppress_eos = false;
+};
+
+std::string lower(std::string s) {
+    for (char &c : s) c = (char)std::tolower((unsigned char)c);
+    return s;
 }
 
+// GetOverlappingTokenSequences, gpttype_adapter.cpp:348-408
+void overlapping_sequences(const Engine &e, const std::string &str, ksamp::RestartSeqs &seqs, int max_tail) {
+    bool ext = !str.empty();
+    for (unsigned char c : str) ext &= c > 127;
+    for (int v = 0; v < e.hp.n_vocab; ++v) {
+        const std::string word = e.tok.piece(v);
+        if (word.find(str) != std::string::npos) {
+            auto its = seqs.equal_range(v);
+            bool empty = false;
+            for (auto it = its.first; it != its.second; ++it) empty |= it->second.empty();
+            if (!empty) seqs.emplace(v, std::vector<int>());
+            continue;
+        }
+        const size_t wl = word.size(), sl = str.size();
+        size_t pos = (size_t)-1;
+        while ((pos = word.find(str[0], pos + 1)) != std::string::npos) {
+            bool match = true;
+            size_t i;
+            for (i = 1; i < sl && i + pos < wl; ++i)
+                if (word[pos + i] != str[i]) { match = false; break; }
+            if (match && !ext) {
+                std::vector<int> tail = e.tok.encode(str.substr(i), false);
+                if (max_tail >= 0 && (int)tail.size() > max_tail) tail.resize(max_tail);
+                auto its = seqs.equal_range(v);
+                bool found = false;
+                for (auto it = its.first; it != its.second; ++it) found |= it->second == tail;
+                if (!found) seqs.emplace(v, tail);
+            }
+        }
+    }
+}
+
+SamplerSetup make_sampler(const Engine &e, const generation_inputs &in, int n_ctx) {
+    SamplerSetup S;
+    ksamp::Params &P = S.P;
+    S.n_ctx = n_ctx;
+    const int nv = e.hp.n_vocab;
+    for (int k = 0; k < KCPP_LOGIT_BIAS_MAX; ++k) {
+        const logit_bias &b = in.logit_biases[k];
+        if (b.token_id >= 0 && b.token_id < nv && b.bias != 0) S.biases.push_back({b.token_id, b.bias});
+    }
+    P.top_k = (float)in.top_k; P.top_a = in.top_a; P.top_p = in.top_p; P.min_p = in.min_p; P.typical_p = in.typical_p;
+    P.tfs = in.tfs; P.temp = in.temperature; P.rep_pen = in.rep_pen; P.rep_pen_slope = in.rep_pen_slope;
+    P.presence_penalty = in.presence_penalty; P.mirostat = in.mirostat; P.mirostat_eta = in.mirostat_eta;
+    P.mirostat_tau = in.mirostat_tau; P.dry_multiplier = in.dry_multiplier; P.dry_base = in.dry_base;
+    P.dry_allowed_length = in.dry_allowed_length; P.dry_penalty_last_n = in.dry_penalty_last_n;
+    P.xtc_threshold = in.xtc_threshold; P.xtc_probability = in.xtc_probability; P.dynatemp_range = in.dynatemp_range;
+    P.dynatemp_exponent = in.dynatemp_exponent; P.smoothing_factor = in.smoothing_factor;
+    P.rep_pen_range = std::max(1, in.rep_pen_range);
+    if (P.rep_pen_slope > 1 || P.rep_pen_slope <= 0) P.rep_pen_slope = 1;
+    if (P.top_k < 1) P.top_k = (float)nv;
+    if (in.sampler_len <= 0)
+        P.order = {ksamp::S_REP_PEN, ksamp::S_TOP_K, ksamp::S_TOP_A, ksamp::S_TFS, ksamp::S_TYP, ksamp::S_TOP_P, ksamp::S_TEMP};
+    else
+        for (int i = 0; i < std::min(in.sampler_len, KCPP_SAMPLER_MAX); ++i) P.order.push_back(in.sampler_order[i]);
+    if (P.dry_multiplier > 0) {
+        for (int x = 0; x < KCPP_DRY_SEQ_BREAK_MAX; ++x) {
+            if (!in.dry_sequence_breakers[x] || !in.dry_sequence_breakers[x][0]) continue;
+            std::string w = in.dry_sequence_breakers[x];
+            if (w.size() > 40) w.resize(40);
+            overlapping_sequences(e, w, S.restarts, 20);
+        }
+    }
+    std::vector<std::string> single;
+    for (int x = 0; x < KCPP_BAN_TOKEN_MAX; ++x) {
+        if (!in.banned_tokens[x] || !in.banned_tokens[x][0]) continue;
+        const std::string w = lower(in.banned_tokens[x]);
+        if (e.tok.encode(w, false).size() == 1 && w.length() < 2) single.push_back(w);   // phrases (antislop): not provided
+    }
+    if (!single.empty())
+        for (int v = 0; v < nv; ++v) {
+            const std::string w = lower(e.tok.piece(v));
+            for (const std::string &b : single)
+                if (w.find(b) != std::string::npos) { S.banned.push_back(v); break; }
+        }
+    S.suppress_eos = !in.allow_eos_token && !in.bypass_eos_token;
+    return S;
+}
+
+// true when the reference chain reduces to argmax of the raw logits, so the on-device argmax is the same token
+bool chain_is_argmax(const SamplerSetup &S) {
+    const ksamp::Params &P = S.P;
+    if (!S.biases.empty() || !S.banned.empty() || P.mirostat == 1 || P.mirostat == 2) return false;
+    if (P.dry_multiplier > 0 && P.dry_base > 0) return false;
+    if (P.rep_pen != 1.0f || P.presence_penalty != 0) return false;
+    if (P.typical_p < 1.0f) return false;               // locally-typical sampling may drop the argmax
+    if (P.xtc_probability > 0 && P.xtc_threshold <= 0.5f) return false;
+    // greedy: temperature <= 0 (top-1 inside sample_temperature) or top_k == 1 anywhere in the order
+    bool has_temp = false, has_topk = false;
+    for (int s : P.order) { has_temp |= s == ksamp::S_TEMP; has_topk |= s == ksamp::S_TOP_K; }
+    return (has_topk && (int)P.top_k == 1) || (has_temp && P.temp <= 0 && P.dynatemp_range <= 0);
+}
+
+// one sampled token from the last stage's logits (gpttype_adapter.cpp:3182-3232); < 0 on a device error
+int sample(Engine &e, const SamplerSetup &S, const std::vector<int> &last_n, std::mt19937 &rng, float *mu) {
+    kcpp_model *last = e.stages.back();
+    const int eos = e.tok.eos();
+    if (chain_is_argmax(S)) {
+        int32_t t = 0;
+        if (kcpp_model_argmax(last, &t)) return -1;
+        if (!(S.suppress_eos && t == eos)) return t;
+    }
+    e.logits.resize(e.hp.n_vocab);
+    if (kcpp_model_read_logits(last, e.logits.data())) return -1;
+    float *l = e.logits.data();
+    const float low = ksamp::lowest_logit(l, e.logits.size());
+    if (S.suppress_eos && eos >= 0 && eos < e.hp.n_vocab) l[eos] = low;
+    for (int b : S.banned) l[b] = low;
+    return ksamp::sample_logits(l, S.n_ctx, e.hp.n_vocab, S.P, S.biases, S.restarts, e.ctx, last_n, rng, mu);
+}
 
 // ---- context shifting (restatement of model_adapter.cpp:337-430 and gpttype_adapter.cpp:1504-1571)
 bool arr_start_with(const std::vector<int> &t, const std::vector<int> &q) {
@@ -392,7 +466,8 @@ generation_outputs generate(const generation_inputs in) {
         std::vector<int> mem = e->tok.encode(in.memory, true);
         if (!bosv.empty() && !toks.empty() && toks[0] == bosv[0]) toks.erase(toks.begin());
         if ((int)mem.size() + max_len + 4 > max_ctx) {
-            mem.erase(mem.begin(), mem.begin() + ((int)mem.size() - max_ctx + max_len + 4));
+            const int cut = std::min((int)mem.size(), (int)mem.size() - max_ctx + max_len + 4);   // clamped (the
+            mem.erase(mem.begin(), mem.begin() + cut);                       // reference pre-resizes, :2840-2845)
             if (!bosv.empty() && !mem.empty()) mem[0] = bosv[0];
         }
         const int total = (int)(mem.size() + toks.size()) + max_len;
@@ -418,16 +493,27 @@ generation_outputs generate(const generation_inputs in) {
     }
     e->ctx.insert(e->ctx.end(), toks.begin() + keep, toks.end());
     const auto t1 = std::chrono::steady_clock::now();
-    std::mt19937 rng((uint32_t)(in.seed <= 0 ? (int)std::random_device{}() : in.seed));
-    g_last_seed = in.seed;
-    const bool greedy = in.temperature <= 0.0f || in.top_k == 1;
+    // seed as gpttype_adapter.cpp:2736-2740 (time-based when <= 0 or 0xFFFFFFFF)
+    uint32_t seed = (uint32_t)in.seed;
+    if (in.seed <= 0 || seed == 0xFFFFFFFFu) seed = (uint32_t)time(nullptr) % 1000000u;
+    std::mt19937 rng(seed);
+    g_last_seed = (int)seed;
+    const SamplerSetup S = make_sampler(*e, in, in.max_context_length > 0 ? in.max_context_length : max_ctx);
+    static bool mu_init = false;                 // SampleLogits' function-static mirostat_mu (:1369)
+    if (!mu_init) { g_mirostat_mu = 2.0f * S.P.mirostat_tau; mu_init = true; }
+    // last_n_tokens: repeat_last_n zeros, then every context token in order (:2892-2895, 3236-3243, 3420-3425)
+    std::vector<int> last_n(S.P.rep_pen_range, 0);
+    for (int t : e->ctx) { last_n.erase(last_n.begin()); last_n.push_back(t); }
     std::vector<std::string> stops;
     for (int k = 0; k < KCPP_STOP_TOKEN_MAX; ++k)
         if (in.stop_sequence[k] && in.stop_sequence[k][0]) stops.emplace_back(in.stop_sequence[k]);
     int n_gen = 0, stop = KCPP_STOP_OUT_OF_TOKENS;
     for (; n_gen < max_len; ++n_gen) {
         if (g_abort) { stop = KCPP_STOP_CUSTOM_STOPPER; break; }
-        const int t = sample(*e, in, e->ctx, rng, greedy);
+        const int t = sample(*e, S, last_n, rng, &g_mirostat_mu);
+        if (t < 0) { fprintf(stderr, "[kcpp] generate: sampling failed: %s\n", kcpp_last_error()); break; }
+        last_n.erase(last_n.begin());
+        last_n.push_back(t);
         if (t == e->tok.eos() && !in.bypass_eos_token) { stop = KCPP_STOP_EOS_TOKEN_HIT; break; }
         const std::string piece = e->tok.piece(t);
         bool hit = false;
@@ -464,6 +550,67 @@ generation_outputs generate(const generation_inputs in) {
     out.text = g_result.c_str();
     g_finished = true;
     return out;
+}
+
+// GGUF header / tensor-table validation alone (the first step of load_model): 0 when the file parses, else -1 with
+// the reason in err (tests/test_gguf_loader.py)
+int kcpp_gguf_check(const char *path, char *err, int err_len) {
+    gguf::File f;
+    std::string e;
+    const bool ok = path && f.open(path, e);
+    if (err && err_len > 0) snprintf(err, (size_t)err_len, "%s", ok ? "" : e.c_str());
+    return ok ? 0 : -1;
+}
+
+// test hook (tests/test_sampler.py): the restated SampleLogits chain on caller logits.  fp = {top_k, top_a, top_p,
+// min_p, typical_p, tfs, temp, rep_pen, rep_pen_slope, presence_penalty, mirostat_tau, mirostat_eta, dry_multiplier,
+// dry_base, xtc_threshold, xtc_probability, dynatemp_range, dynatemp_exponent, smoothing_factor}; ip = {rep_pen_range,
+// mirostat, dry_allowed_length, dry_penalty_last_n}; restarts: n_restart (head, tail length, tail...) records.
+// Writes up to cap candidates (id, p) left after the chain (before the draw; mirostat: after its own top-k) and
+// returns the drawn token, or -1 on bad arguments.
+int kcpp_sampler_probe(const float *logits, int n_vocab, int n_ctx, const float *fp, const int *ip, const int *order,
+                       int n_order, const int *ctx_toks, int n_ctx_toks, const int *last_n, int n_last,
+                       const int *restarts, int n_restart_ints, unsigned seed, float *mu, int *out_ids, float *out_p,
+                       int cap, int *out_n) {
+    if (!logits || n_vocab <= 0 || !fp || !ip) return -1;
+    ksamp::Params P;
+    P.top_k = fp[0]; P.top_a = fp[1]; P.top_p = fp[2]; P.min_p = fp[3]; P.typical_p = fp[4]; P.tfs = fp[5]; P.temp = fp[6];
+    P.rep_pen = fp[7]; P.rep_pen_slope = fp[8]; P.presence_penalty = fp[9]; P.mirostat_tau = fp[10]; P.mirostat_eta = fp[11];
+    P.dry_multiplier = fp[12]; P.dry_base = fp[13]; P.xtc_threshold = fp[14]; P.xtc_probability = fp[15];
+    P.dynatemp_range = fp[16]; P.dynatemp_exponent = fp[17]; P.smoothing_factor = fp[18];
+    P.rep_pen_range = ip[0]; P.mirostat = ip[1]; P.dry_allowed_length = ip[2]; P.dry_penalty_last_n = ip[3];
+    for (int i = 0; i < n_order; ++i) P.order.push_back(order[i]);
+    ksamp::RestartSeqs rs;
+    for (int i = 0; i + 1 < n_restart_ints;) {
+        const int head = restarts[i], len = restarts[i + 1];
+        if (len < 0 || i + 2 + len > n_restart_ints) return -1;
+        rs.emplace(head, std::vector<int>(restarts + i + 2, restarts + i + 2 + len));
+        i += 2 + len;
+    }
+    const std::vector<int> ctxv(ctx_toks, ctx_toks + n_ctx_toks), lastv(last_n, last_n + n_last);
+    std::mt19937 rng(seed);
+    std::vector<ksamp::TokData> cand;
+    int tok;
+    ksamp::Cands c;
+    if (P.mirostat == 1 || P.mirostat == 2) {
+        std::mt19937 rng2(seed);
+        float mu2 = *mu;
+        tok = ksamp::sample_logits(logits, n_ctx, n_vocab, P, {}, rs, ctxv, lastv, rng2, &mu2);
+        *mu = mu2;
+        c = ksamp::Cands{nullptr, 0, false};
+    } else {
+        c = ksamp::apply_chain(cand, logits, n_ctx, n_vocab, P, {}, rs, ctxv, lastv, rng, false);
+        ksamp::Cands c2 = c;
+        std::vector<ksamp::TokData> keep(c.data, c.data + c.size);
+        ksamp::Cands ck{keep.data(), keep.size(), c.sorted};
+        tok = ksamp::draw(&ck, rng);
+        (void)c2;
+        ksamp::softmax(&c);             // the probabilities the draw used
+    }
+    const int n = (int)std::min<size_t>(c.size, (size_t)std::max(cap, 0));
+    for (int i = 0; i < n; ++i) { out_ids[i] = c.data[i].id; out_p[i] = c.data[i].p; }
+    if (out_n) *out_n = (int)c.size;
+    return tok;
 }
 
 const char *new_token(int idx) {

@@ -9,6 +9,7 @@
 #include <unistd.h>
 
 #include <cstdint>
+#include <climits>
 #include <cstring>
 #include <map>
 #include <string>
@@ -34,7 +35,20 @@ struct Tensor {
     int64_t ne[4] = {1, 1, 1, 1};
     const uint8_t *data = nullptr;
     uint64_t offset = 0;
+    uint64_t nbytes = 0;
 };
+
+// (block elements, block bytes) of every ggml type id (ggml.h:363-398, block structs ggml-common.h:144-419);
+// {0, 0} for ids that do not exist
+inline void type_block(int t, uint64_t &be, uint64_t &bb) {
+    static const uint16_t tab[36][2] = {
+        {1, 4}, {1, 2}, {32, 18}, {32, 20}, {0, 0}, {0, 0}, {32, 22}, {32, 24}, {32, 34}, {32, 36},
+        {256, 84}, {256, 110}, {256, 144}, {256, 176}, {256, 210}, {256, 292}, {256, 66}, {256, 74}, {256, 98},
+        {256, 50}, {32, 18}, {256, 110}, {256, 82}, {256, 136}, {1, 1}, {1, 2}, {1, 4}, {1, 8}, {1, 8}, {256, 56},
+        {1, 2}, {32, 18}, {32, 18}, {32, 18}, {256, 54}, {256, 66}};
+    be = bb = 0;
+    if (t >= 0 && t < 36) { be = tab[t][0]; bb = tab[t][1]; }
+}
 
 class File {
 public:
@@ -63,6 +77,7 @@ public:
             uint64_t align = 32;
             auto it = kv.find("general.alignment");
             if (it != kv.end()) align = (uint64_t)it->second.i;
+            if (align == 0 || (align & (align - 1)) != 0) throw std::string("general.alignment must be a power of two");
             for (uint64_t t = 0; t < nt; ++t) {
                 Tensor tt;
                 tt.name = rds();
@@ -71,11 +86,24 @@ public:
                 for (uint32_t d = 0; d < nd; ++d) tt.ne[d] = (int64_t)rd<uint64_t>();
                 tt.type = (int)rd<uint32_t>();
                 tt.offset = rd<uint64_t>();
+                // byte size with overflow checks (llama.cpp:4379-4390 checks offset + size against the file)
+                uint64_t be, bb, nel = 1;
+                type_block(tt.type, be, bb);
+                if (!be) throw std::string("unknown tensor type in " + tt.name);
+                for (int d = 0; d < 4; ++d) {
+                    if (tt.ne[d] < 0) throw std::string("negative dimension in " + tt.name);
+                    if (tt.ne[d] && nel > UINT64_MAX / (uint64_t)tt.ne[d]) throw std::string("tensor too large: " + tt.name);
+                    nel *= (uint64_t)tt.ne[d];
+                }
+                if (tt.ne[0] % be) throw std::string("row not a whole number of blocks: " + tt.name);
+                if (nel / be > UINT64_MAX / bb) throw std::string("tensor too large: " + tt.name);
+                tt.nbytes = nel / be * bb;
                 tensors.push_back(tt);
             }
             const uint64_t data0 = (pos_ + align - 1) / align * align;
             for (auto &tt : tensors) {
-                if (data0 + tt.offset > size_) throw std::string("tensor offset past end of file: " + tt.name);
+                if (tt.offset > size_ || data0 > size_ - tt.offset || tt.nbytes > size_ - data0 - tt.offset)
+                    throw std::string("tensor data past end of file: " + tt.name);
                 tt.data = map_ + data0 + tt.offset;
                 by_name[tt.name] = &tt - &tensors[0];
             }
@@ -110,7 +138,7 @@ public:
 
 private:
     template <typename T> T rd() {
-        if (pos_ + sizeof(T) > size_) throw std::string("truncated");
+        if (sizeof(T) > size_ - pos_) throw std::string("truncated");
         T v;
         memcpy(&v, map_ + pos_, sizeof(T));
         pos_ += sizeof(T);
@@ -118,7 +146,7 @@ private:
     }
     std::string rds() {
         const uint64_t n = rd<uint64_t>();
-        if (pos_ + n > size_) throw std::string("truncated string");
+        if (n > size_ - pos_) throw std::string("truncated string");
         std::string s((const char *)map_ + pos_, (size_t)n);
         pos_ += n;
         return s;

@@ -240,6 +240,8 @@ extern "C" int kcpp_model_kv_shift(kcpp_model *m, int p0, int diff, int n_past) 
 extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *types, int device, int il0, int il1,
                                          int has_embed, int has_output, int max_ubatch) {
     if (hipSetDevice(device) != hipSuccess) { g_err = "hipSetDevice failed"; return nullptr; }
+    // the split-KV decode attention merges at most 2048 chunks of 64 keys (attn.hip FA_MAX_CHUNKS)
+    if (hp->n_ctx < 1 || hp->n_ctx > 131072) { g_err = "n_ctx must be in [1, 131072]"; return nullptr; }
     kcpp_model *m = new kcpp_model();
     m->hp = *hp;
     // on-device layout per tensor: dense Q4_K / Q6_K mat-mul weights whose K the RS kernels cover are held in

@@ -47,6 +47,9 @@ _SIGS = {
     "kcpp_rope_kv": [P, I64, P, P, P, P, I, I, I, I, I, P, P, P],
     "kcpp_flash_attn": [P, P, P, P, P, P, I, I, I, I, I, P, I, Fl, I, P],
     "kcpp_flash_attn_prefill_mfma": [P, P, P, P, I, I, I, I, I, Fl, P],
+    "kcpp_fa_decode_ex": [P, P, P, I64, I64, P, P, P, I, I, I, P, I, Fl, I, P],
+    "kcpp_fa_set_stamps": [P],
+    "kcpp_gguf_check": [ctypes.c_char_p, ctypes.c_char_p, I],
     "kcpp_add": [P, P, P, I64, P],
     "kcpp_silu_mul": [P, P, P, I64, P],
     "kcpp_moe_route": [P, I64, P, I, I64, I, I, P, P, I, P],
@@ -84,7 +87,7 @@ _SIGS = {
 }
 _RES = {"kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
         "kcpp_model_create": P, "kcpp_model_hidden": P, "kcpp_model_stream": P, "kcpp_model_weight_bytes": I64,
-        "kcpp_last_error": ctypes.c_char_p, "kcpp_model_free": None}
+        "kcpp_last_error": ctypes.c_char_p, "kcpp_model_free": None, "kcpp_fa_set_stamps": None}
 _L.kcpp_act_bytes.argtypes = [I, I64, I64]
 _L.kcpp_fa_workspace_bytes.argtypes = [I, I, I]
 _L.kcpp_fa_ext_workspace_bytes.argtypes = [I, I, I, I]

@@ -166,3 +166,48 @@ def test_moe_gguf_generate_matches_runtime(model, tmp_path, split):
         n += 1
     m.close()
     assert out.text == b"".join(piece(toks, ttypes, t) for t in want)
+
+
+def test_greedy_respects_logit_bias(model):
+    """Greedy with a logit bias: the reference adds biases before any sampler (gpttype_adapter.cpp:1349-1353),
+    token ids >= 0 accepted (:2576-2584), so banning the unbiased greedy token changes the first pick."""
+    h, X, toks, ttypes, _ = model
+    gi = X.generation_inputs()
+    gi.prompt = b"hello world"
+    gi.max_context_length = 248
+    gi.max_length = 1
+    gi.temperature = 0.0
+    gi.top_k = 1
+    gi.rep_pen = 1.0
+    gi.bypass_eos_token = True
+    gi.seed = 3
+    base = h.generate(gi).text
+    r = h.token_count(b"hello world", True)
+    ids = [r.ids[i] for i in range(r.count)]
+    first = [t for t in range(len(toks)) if piece(toks, ttypes, t) == base and base]
+    assert first, base
+    gi.logit_biases[0].token_id = first[0]
+    gi.logit_biases[0].bias = -1000.0
+    biased = h.generate(gi).text
+    assert biased != base
+    gi.logit_biases[0].token_id = 0                       # token 0 may be biased too (>= 0)
+    gi.logit_biases[0].bias = 1000.0
+    assert h.generate(gi).text == piece(toks, ttypes, 0)
+
+
+def test_long_context_decode_matches_short_context():
+    """n_ctx beyond 16384 keys (the combine's old chunk table) builds, graph-replays and gives the same logits as
+    a short-context model with the same weights (every decode failed at graph capture)."""
+    import koboldcpp_amd.lib as K
+    types = R.q4_k_m_types(R.TINY["n_layer"])
+    prompt = list(range(3, 40))
+    outs = []
+    for n_ctx in (256, 20008):
+        m = K.Model(dict(R.TINY, n_ctx=n_ctx), types)
+        m.synth(1234)
+        m.decode(prompt, 0, want_logits=False)
+        t = m.argmax()
+        lg = m.decode([t], len(prompt))
+        outs.append(lg)
+        m.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
