@@ -114,6 +114,11 @@ int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max);
 int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qout, void *ws,
                     int T, int H, int HKV, int D, int n_past, const int32_t *n_past_dev, int n_kv_max, float scale,
                     int force_path, void *stream);
+/* strict-parity attention: the reference CPU's order (ggml.c:15667-15875) with its f16 V accumulator, one serial
+ * chain per (query, head, dim) -- bit-for-bit the AVX2 build's arithmetic up to exp rounding (attn_exact.hip).
+ * Same layouts and causal window as kcpp_flash_attn; D = 128. */
+int kcpp_flash_attn_exact(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, int T, int H,
+                          int HKV, int D, int n_past, const int32_t *n_past_dev, float scale, void *stream);
 /* single-token decode attention with explicit cache strides in elements (key p of kv head hk at
  * kc + p*kv_ld + hk*kv_hs); variant 0: 64-key chunks + combine, 1: splits with in-launch merge, 2: splits +
  * combine (A/B measurement entry, tools/fa_dec_bench.py) */
@@ -247,6 +252,9 @@ int kcpp_model_kv_shift(kcpp_model *m, int p0, int diff, int n_past);
 int kcpp_model_set_graphs(kcpp_model *m, int enable);
 /* single-token decode through the fused mat-vec path (default on); off = one kernel per op */
 int kcpp_model_set_fused_decode(kcpp_model *m, int enable);
+/* 1: attention through kcpp_flash_attn_exact (reference order, f16 accumulation; strict-parity mode, slow);
+ * 0 (default, or KCPP_FA_EXACT=1 at creation): the split-KV / MFMA kernels */
+int kcpp_model_set_fa_exact(kcpp_model *m, int enable);
 int64_t kcpp_model_weight_bytes(kcpp_model *m);
 const char *kcpp_last_error(void);
 

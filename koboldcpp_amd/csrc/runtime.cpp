@@ -107,6 +107,7 @@ struct kcpp_model {
     float *logits_pin = nullptr;
     bool use_graphs = true;
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
+    bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
     hipGraphExec_t g_exec = nullptr;
     hipStream_t side = nullptr;             // second branch of the decode step (independent q|k|v launches)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -261,6 +262,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     types = m->types.data();
     m->device = device; m->il0 = il0; m->il1 = il1; m->has_embed = has_embed; m->has_output = has_output;
     m->ub = max_ubatch > 0 ? max_ubatch : 512;
+    m->fa_exact = getenv("KCPP_FA_EXACT") && atoi(getenv("KCPP_FA_EXACT")) != 0;
     auto fail = [&](const char *what) { g_err = what; kcpp_model_free(m); return (kcpp_model *)nullptr; };
     if (hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking) != hipSuccess) return fail("stream");
     if (hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
@@ -460,6 +462,11 @@ extern "C" int kcpp_model_set_graphs(kcpp_model *m, int enable) {
     m->use_graphs = enable != 0;
     return 0;
 }
+extern "C" int kcpp_model_set_fa_exact(kcpp_model *m, int enable) {
+    m->fa_exact = enable != 0;
+    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    return 0;
+}
 extern "C" int kcpp_model_set_fused_decode(kcpp_model *m, int enable) {
     m->fused_decode = enable != 0;
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
@@ -628,9 +635,12 @@ static int forward_layers_dec(kcpp_model *m) {
             for (int i = 0; i < nq; ++i) RC(kcpp_gemv_dec(qty[i], &qa[i], 2, 1, 2, s));
         }
         // --- attention over the cache, combine + Q8_K quantize for wo
-        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K;
-        RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, woq ? m->act : nullptr, m->fa_ws, 1, (int)H, (int)HKV, (int)D, 0,
-                           m->pos_dev, hp.n_ctx, kq_scale, 1, s));
+        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K && !m->fa_exact;
+        if (m->fa_exact)
+            RC(kcpp_flash_attn_exact(m->q16, L.kc, L.vc, m->attn, 1, (int)H, (int)HKV, (int)D, 0, m->pos_dev, kq_scale, s));
+        else
+            RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, woq ? m->act : nullptr, m->fa_ws, 1, (int)H, (int)HKV, (int)D,
+                               0, m->pos_dev, hp.n_ctx, kq_scale, 1, s));
         if (!woq) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, 1, s));
         {   // x += wo . attn
             DecArgs a;
@@ -739,10 +749,13 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             }
         }
         RC(kcpp_rope_kv(m->qkv, LQ, nullptr, m->q16, L.kc, L.vc, T, (int)H, (int)HKV, (int)D, n_past, posp, m->rope_tab, s));
-        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K;
+        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K && !m->fa_exact;
         static const int fa_force = getenv("KCPP_FA_PATH") ? atoi(getenv("KCPP_FA_PATH")) : 0;
-        RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, (woq && T <= 16) ? m->act : nullptr, m->fa_ws, T, (int)H,
-                           (int)HKV, (int)D, n_past, posp, hp.n_ctx, kq_scale, fa_force, s));
+        if (m->fa_exact)
+            RC(kcpp_flash_attn_exact(m->q16, L.kc, L.vc, m->attn, T, (int)H, (int)HKV, (int)D, n_past, posp, kq_scale, s));
+        else
+            RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, (woq && T <= 16) ? m->act : nullptr, m->fa_ws, T, (int)H,
+                               (int)HKV, (int)D, n_past, posp, hp.n_ctx, kq_scale, fa_force, s));
         if (!(woq && T <= 16)) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, T, s));
         RC(matmul(m, t[4], nullptr, m->act, T, m->x, E, m->x, E, 0));                    // x += wo . attn
         if (hp.n_expert > 0) { RC(T == 1 ? moe_dec(m, L) : moe_prefill(m, L, T)); continue; }   // T == 1: no host sync (graphs)

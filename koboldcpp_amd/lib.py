@@ -83,6 +83,8 @@ _SIGS = {
     "kcpp_model_decode_greedy": [P, I, P],
     "kcpp_model_set_graphs": [P, I],
     "kcpp_model_set_fused_decode": [P, I],
+    "kcpp_model_set_fa_exact": [P, I],
+    "kcpp_flash_attn_exact": [P, P, P, P, I, I, I, I, I, P, Fl, P],
     "kcpp_model_weight_bytes": [P],
 }
 _RES = {"kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
@@ -265,6 +267,10 @@ class Model:
 
     def set_fused_decode(self, on):
         _L.kcpp_model_set_fused_decode(self.m, int(on))
+
+    def set_fa_exact(self, on):
+        """strict-parity attention (reference order, f16 accumulation); see kcpp_flash_attn_exact"""
+        _chk(_L.kcpp_model_set_fa_exact(self.m, int(on)), "set_fa_exact")
 
     def set_graphs(self, on):
         _L.kcpp_model_set_graphs(self.m, int(on))

@@ -38,6 +38,9 @@ typedef struct {
     int n_prompt, n_gen, ubatch;
     int *prompt;
     char out[1024];
+    int n_forced;          /* optional: teacher-forced decode tokens (else the greedy argmax) */
+    int *forced;
+    char hidden_out[1024]; /* optional: per-layer residual stream of the prefill ubatch(es) */
 } cfg_t;
 
 static int read_cfg(const char *path, cfg_t *c) {
@@ -54,6 +57,12 @@ static int read_cfg(const char *path, cfg_t *c) {
     c->prompt = malloc(sizeof(int) * (c->n_prompt > 0 ? c->n_prompt : 1));
     for (int i = 0; i < c->n_prompt; ++i) if (fscanf(f, "%d", &c->prompt[i]) != 1) { fclose(f); return -5; }
     if (fscanf(f, "%1023s", c->out) != 1) { fclose(f); return -6; }
+    c->n_forced = 0; c->forced = NULL; c->hidden_out[0] = 0;
+    if (fscanf(f, "%d", &c->n_forced) == 1 && c->n_forced > 0) {
+        c->forced = malloc(sizeof(int) * c->n_forced);
+        for (int i = 0; i < c->n_forced; ++i) if (fscanf(f, "%d", &c->forced[i]) != 1) { fclose(f); return -7; }
+    }
+    if (fscanf(f, "%1023s", c->hidden_out) != 1) c->hidden_out[0] = 0;
     fclose(f);
     return 0;
 }
@@ -137,8 +146,10 @@ static int load_model(model_t *m) {
     return 0;
 }
 
-/* one llama_decode of T tokens at n_past; returns logits of the last token */
-static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits) {
+/* one llama_decode of T tokens at n_past; returns logits of the last token.  With hid != NULL the
+ * residual stream after every layer but the last ([n_layer-1][T][E]) is written there (layer outputs =
+ * the next layer's input; the last layer keeps only the last token, src/llama.cpp out_ids). */
+static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits, float *hid) {
     cfg_t *c = &m->c;
     const int E = c->n_embd, H = c->n_head, HKV = c->n_head_kv, D = E / H, EKV = HKV * D, F = c->n_ff;
     const int n_kv = n_past + T;
@@ -168,6 +179,7 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits)
 
     const float kq_scale = 1.0f / sqrtf((float)D);
     struct ggml_tensor *inpL = ggml_get_rows(ctx, m->w[0], inp_tokens);   /* llm_build_inp_embd */
+    struct ggml_tensor *lay_out[256];
     for (int il = 0; il < c->n_layer; ++il) {
         struct ggml_tensor **lw = m->w + 3 + (c->n_expert ? 10 : 9) * il;
         struct ggml_tensor *inpSA = inpL;
@@ -227,6 +239,8 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits)
             cur = ggml_mul_mat(ctx, lw[8], cur);
         }
         inpL = ggml_add(ctx, cur, ffn_inp);
+        lay_out[il] = inpL;
+        if (hid && il < c->n_layer - 1) ggml_build_forward_expand(gf, inpL);
     }
     struct ggml_tensor *cur = ggml_mul(ctx, ggml_rms_norm(ctx, inpL, c->eps), m->w[1]);
     cur = ggml_mul_mat(ctx, m->w[2], cur);
@@ -234,6 +248,9 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits)
     enum ggml_status st = ggml_graph_compute_with_ctx(ctx, gf, c->nthreads);
     if (st != GGML_STATUS_SUCCESS) { ggml_free(ctx); return -2; }
     memcpy(logits, cur->data, sizeof(float) * c->n_vocab);
+    if (hid)
+        for (int il = 0; il < c->n_layer - 1; ++il)
+            memcpy(hid + (size_t)il * T * E, lay_out[il]->data, sizeof(float) * (size_t)T * E);
     ggml_free(ctx);
     return 0;
 }
@@ -257,17 +274,22 @@ static int run_llama(const char *cfgpath) {
     float *logits = malloc(sizeof(float) * c->n_vocab);
     int n_past = 0;
     double tp0 = now_s();
+    FILE *hout = c->hidden_out[0] ? fopen(c->hidden_out, "wb") : NULL;
+    float *hid = hout ? malloc(sizeof(float) * (size_t)(c->n_layer > 1 ? c->n_layer - 1 : 1) * c->ubatch * c->n_embd) : NULL;
     for (int i = 0; i < c->n_prompt; i += c->ubatch) {
         int T = c->n_prompt - i < c->ubatch ? c->n_prompt - i : c->ubatch;
-        if (eval(&m, c->prompt + i, T, n_past, logits)) return 4;
+        if (eval(&m, c->prompt + i, T, n_past, logits, hid)) return 4;
+        if (hout) fwrite(hid, sizeof(float), (size_t)(c->n_layer - 1) * T * c->n_embd, hout);
         n_past += T;
     }
+    if (hout) { fclose(hout); free(hid); }
     double t_pp = now_s() - tp0;
     fwrite(logits, sizeof(float), c->n_vocab, out);
     int tok = argmax(logits, c->n_vocab);
     double tg0 = now_s();
     for (int g = 0; g < c->n_gen; ++g) {
-        if (eval(&m, &tok, 1, n_past, logits)) return 5;
+        if (g < c->n_forced) tok = c->forced[g];
+        if (eval(&m, &tok, 1, n_past, logits, NULL)) return 5;
         n_past += 1;
         fwrite(logits, sizeof(float), c->n_vocab, out);
         tok = argmax(logits, c->n_vocab);

@@ -11,6 +11,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
 REF_BIN = os.path.join(ROOT, "oracle", "_ref", "ref_llama")
+REF_BIN_SCALAR = os.path.join(ROOT, "oracle", "_ref", "scalar", "ref_llama")   # no-SIMD build (make ref_scalar)
 
 # ggml_type ids (ggml/include/ggml.h:364-399)
 F32, F16, Q4_0, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 8, 12, 13, 14, 15
@@ -187,12 +188,18 @@ def ref_available():
     return os.path.exists(REF_BIN)
 
 
-def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeout=600):
-    """Run the reference ggml graph; returns (logits [1+n_gen, V], info dict)."""
+def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeout=600, forced=None, hidden=False,
+                  binary=None):
+    """Run the reference ggml graph; returns (logits [1+n_gen, V], info dict).
+    forced: decode these tokens (teacher forcing) instead of the greedy argmax.
+    hidden: also return info["hidden"] = residual stream after layers 0..n_layer-2 of the prefill,
+            [n_layer-1][n_prompt][n_embd] (single-ubatch prompts).
+    binary: ref_llama build to run (default: the AVX2 build; REF_BIN_SCALAR for the scalar one)."""
     import json
     with tempfile.TemporaryDirectory() as td:
         cfg = os.path.join(td, "cfg.txt")
         out = os.path.join(td, "logits.bin")
+        hout = os.path.join(td, "hidden.bin")
         with open(cfg, "w") as f:
             f.write(" ".join(str(hp[n]) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")))
             f.write(" %r %r %r %d %d %d\n" % (float(hp["eps"]), float(hp["rope_base"]), float(hp.get("rope_freq_scale", 1.0)),
@@ -200,12 +207,18 @@ def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeou
             f.write(" ".join(map(str, types)) + "\n")
             f.write("%d %d %d %d\n" % (nthreads, len(prompt), n_gen, ubatch))
             f.write(" ".join(map(str, prompt)) + "\n" + out + "\n")
-        r = subprocess.run([REF_BIN, "llama", cfg], capture_output=True, text=True, timeout=timeout,
+            fl = [int(t) for t in (forced if forced is not None else [])]
+            f.write("%d %s\n" % (len(fl), " ".join(map(str, fl))))
+            if hidden:
+                f.write(hout + "\n")
+        r = subprocess.run([binary or REF_BIN, "llama", cfg], capture_output=True, text=True, timeout=timeout,
                            env=dict(os.environ, OMP_NUM_THREADS=str(nthreads)))
         if r.returncode != 0:
             raise RuntimeError("ref_llama failed: %s %s" % (r.returncode, r.stderr))
         info = json.loads(r.stdout.strip().splitlines()[-1])
         logits = np.fromfile(out, dtype=np.float32).reshape(-1, hp["n_vocab"])
+        if hidden:
+            info["hidden"] = np.fromfile(hout, dtype=np.float32).reshape(hp["n_layer"] - 1, len(prompt), hp["n_embd"])
         return logits, info
 
 

@@ -7,18 +7,21 @@ import refharness as R
 
 pytestmark = pytest.mark.gpu
 
-# Parity bar (DESIGN.md "parity bar"):
-#  * vs the C restatement with f32 V-accumulation in attention (same math as the HIP path): tight.
-#  * vs the reference itself: the reference CPU accumulates attention V in f16 (ggml.c:15788,
-#    ggml_vec_mad_f16), the HIP path in f32; on this tiny random model that alone moves logits by
-#    ~0.3% (median) -- measured identically between the restatement-f32 and the reference -- and the
-#    reference's own AVX2 vs scalar builds differ by up to ~0.02.  Teacher-forced comparison.
-#  * Even against the same math, a 1-ulp difference in any fp32 sum (e.g. flash-attention order)
-#    can flip one Q8_K/Q8_0 rounding downstream, and one flipped activation quantum in the FFN input
-#    moves every hidden element by ~1e-3 (measured: exact to 1e-7 until such a flip occurs).
-TOL_MAX = 0.05
-TOL_MEDIAN_REF = 6e-3
-TOL_MEDIAN_F32 = 5e-3
+# Parity bar, derived from the reference's own build-to-build spread (tests/golden/ref_spread.npz,
+# make_fullwidth.py: the reference sources built with AVX2/FMA/F16C vs without SIMD, same weights, prompt and
+# teacher-forced tokens).  Per fixture tag:
+#  * vs the reference golden: max and median |dlogit| per step <= 2 x the spread (max over steps).  One factor
+#    for the summation-order class (the GPU's order is a third one), and the production attention accumulates
+#    V*P in f32 where the CPU keeps an f16 accumulator (ggml.c:15788): the reference-pinned C restatement with
+#    f32 accumulation measures 1.9x (max) / 1.5x (median) of the spread on these fixtures.  The strict-parity
+#    mode (tests/test_gpu_fa_exact.py) is held to 1.5x.
+#  * vs the C restatement with f32 accumulation (same attention math as the HIP path): the same spread class.
+#  * HIP-vs-HIP self-consistency (ubatch split, fused vs unfused): 2x the largest spread.
+_SP = np.load(R.ROOT + "/tests/golden/ref_spread.npz")
+SPREAD_MAX = {t: float(_SP["tiny_%s_max" % t].max()) for t in ("q4km", "q8_0", "moe")}
+SPREAD_MED = {t: float(_SP["tiny_%s_median" % t].max()) for t in ("q4km", "q8_0", "moe")}
+TOL_MAX = 2 * max(SPREAD_MAX.values())
+TOL_MEDIAN_F32 = 2 * max(SPREAD_MED.values())
 
 
 @pytest.fixture(scope="module")
@@ -79,7 +82,8 @@ def test_e2e_vs_reference_golden(K, golden_e2e, tag):
     forced = golden_e2e[tag + "_tokens"][:-1]          # the reference's own greedy tokens
     got = run_gpu_forced(K, types, prompt, forced)
     d = np.abs(got - L)
-    assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_REF, (d.max(), np.median(d))
+    assert np.all(d.max(axis=1) <= 2 * SPREAD_MAX[tag]), d.max(axis=1)
+    assert np.all(np.median(d, axis=1) <= 2 * SPREAD_MED[tag]), np.median(d, axis=1)
     # the same comparison for the restatement with f32 attention accumulation shows the same spread
     orc32 = oracle_forced(types, prompt, forced, True)
     d32 = np.abs(orc32 - L)

@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 import refharness as R
-from test_gpu_model import TOL_MAX, TOL_MEDIAN_F32, TOL_MEDIAN_REF, oracle_forced, run_gpu, run_gpu_forced
+from test_gpu_model import SPREAD_MAX, SPREAD_MED, TOL_MAX, TOL_MEDIAN_F32, oracle_forced, run_gpu, run_gpu_forced
 
 pytestmark = pytest.mark.gpu
 
@@ -173,7 +173,8 @@ def golden_moe():
 
 
 def test_moe_e2e_vs_reference_golden(env, golden_moe):
-    """teacher-forced on the reference's own greedy tokens, same bar as the dense model"""
+    """teacher-forced on the reference's own greedy tokens; the dense model's bar (2 x the reference's own
+    AVX2-vs-scalar spread on this MoE fixture, tests/golden/ref_spread.npz tiny_moe_*)"""
     torch, K = env
     types = [int(t) for t in golden_moe["types"]]
     prompt = golden_moe["prompt"]
@@ -181,7 +182,8 @@ def test_moe_e2e_vs_reference_golden(env, golden_moe):
     forced = golden_moe["tokens"][:-1]
     got = run_gpu_forced(K, types, prompt, forced, hp=R.TINY_MOE)
     d = np.abs(got - L)
-    assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_REF, (d.max(), np.median(d))
+    assert np.all(d.max(axis=1) <= 2 * SPREAD_MAX["moe"]), d.max(axis=1)
+    assert np.all(np.median(d, axis=1) <= 2 * SPREAD_MED["moe"]), np.median(d, axis=1)
     orc32 = oracle_forced(types, prompt, forced, True, hp=R.TINY_MOE)
     e = np.abs(got - orc32)
     assert np.median(e) < TOL_MEDIAN_F32 and e.max() < TOL_MAX, (np.median(e), e.max())
