@@ -316,8 +316,7 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
 #pragma unroll
         for (int g = 0; g < G; ++g) {
             float cm = fmaxf(fmaxf(sc[g][0], sc[g][1]), fmaxf(sc[g][2], sc[g][3]));
-            cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
-            cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+            cm = xmax32(xmax16(cm));
             const float mn = fmaxf(m[g], cm);
             if (mn == -INFINITY) continue;                          // nothing valid yet (wave-uniform)
             const float alpha = m[g] == -INFINITY ? 0.0f : expf(m[g] - mn);
@@ -348,13 +347,9 @@ __global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restri
     // wave merge over its 4 key rows (kq): m is wave-uniform, l and acc are per row
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        l[g] += __shfl_xor(l[g], 16, 64);
-        l[g] += __shfl_xor(l[g], 32, 64);
+        l[g] = xsum32(xsum16(l[g]));
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            acc[g][e] += __shfl_xor(acc[g][e], 16, 64);
-            acc[g][e] += __shfl_xor(acc[g][e], 32, 64);
-        }
+        for (int e = 0; e < 8; ++e) acc[g][e] = xsum32(xsum16(acc[g][e]));
         if (kq == 0) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) s_o[wave][g][sub * 8 + e] = acc[g][e];

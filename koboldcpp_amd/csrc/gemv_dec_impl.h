@@ -26,9 +26,7 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
     v += dpp_f<0x4E>(v);
     v += dpp_f<0x141>(v);
     v += dpp_f<0x140>(v);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    return v;
+    return xsum32(xsum16(v));
 }
 
 // Q8_0 quantization (AVX2 quantize_row_q8_0, ggml-quants.c:940-1000) of 16 elements held by one lane,

@@ -174,21 +174,47 @@ __device__ __forceinline__ double dpp_d(double v) {
     const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// Cross-row exchanges on the gfx950 VALU (v_permlane16_swap / v_permlane32_swap): with both operands = v the
+// swap returns (row pair's even rows, odd rows) resp. (lower half, upper half), so lane l gets v[l] and
+// v[l ^ 16] (v[l ^ 32]) without an LDS round trip (__shfl_xor is a ds_bpermute).  a + b == b + a and
+// fmaxf(a, b) == fmaxf(b, a) bitwise, so these equal v (+|max) __shfl_xor(v, 16|32, 64) exactly.
+__device__ __forceinline__ float xsum16(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xsum32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xmax16(float v) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xmax32(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ double xsum16_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)(b & 0xFFFFFFFFll), (unsigned)(b & 0xFFFFFFFFll), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | lo[0]) + __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+__device__ __forceinline__ double xsum32_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)(b & 0xFFFFFFFFll), (unsigned)(b & 0xFFFFFFFFll), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false, false);
+    return __longlong_as_double(((long long)hi[0] << 32) | lo[0]) + __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
 __device__ __forceinline__ double wave_sum_d(double v) {
     v += dpp_d<0xB1>(v); v += dpp_d<0x4E>(v); v += dpp_d<0x141>(v); v += dpp_d<0x140>(v);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    return v;
+    return xsum32_d(xsum16_d(v));
 }
 __device__ __forceinline__ float wave_max_dpp(float v) {
     v = max16_f(v);
-    v = fmaxf(v, __shfl_xor(v, 16, 64));
-    v = fmaxf(v, __shfl_xor(v, 32, 64));
-    return v;
+    return xmax32(xmax16(v));
 }
 __device__ __forceinline__ float wave_sum_f(float v) {
     v += dpp_f<0xB1>(v); v += dpp_f<0x4E>(v); v += dpp_f<0x141>(v); v += dpp_f<0x140>(v);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    return v;
+    return xsum32(xsum16(v));
 }
