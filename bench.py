@@ -29,6 +29,7 @@ LLAMA3_8B = dict(n_vocab=128256, n_embd=4096, n_head=32, n_head_kv=8, n_layer=32
 MIXTRAL_8X7B = dict(n_vocab=32000, n_embd=4096, n_head=32, n_head_kv=8, n_layer=32, n_ff=14336, n_ctx=4096,
                     eps=1e-5, rope_base=1000000.0, n_expert=8, n_expert_used=2)
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
+MFMA_F16_PEAK_TFLOPS = 2500.0   # dense f16 MFMA peak (spec, no sparsity)
 
 
 def q4_k_m_types(n_layer):
@@ -55,7 +56,7 @@ def pmc_traffic():
     return d.get("traffic_bytes_per_launch"), os.path.relpath(fs[-1], ROOT)
 
 
-def measure_roofline(K, torch, iters=48):
+def measure_roofline(K, torch, iters=64, pairs=8):
     """Time the dominant decode kernel as the decode path launches it: the fused Q4_K gate|up
     mat-vec over the row-major decode layout with rms_norm+Q8_K prologue and SiLU-GLU epilogue
     (kcpp_gemv_dec(Q4_K_RS, mode 1, pro 1) -> k_gemv_rs, 4096 -> 2 x 14336), HIP events on the launch stream.  Algorithmic bytes per launch =
@@ -64,9 +65,9 @@ def measure_roofline(K, torch, iters=48):
     wbytes = Kd // 256 * 144 * N
     s = torch.cuda.current_stream()
     sp = s.cuda_stream
-    # 4 weight pairs (264 MB) so consecutive launches do not hit the 256 MiB Infinity Cache
+    # 8 weight pairs (8 x 66 MB = 504 MiB, twice the 256 MiB Infinity Cache) so no launch finds its weights cached
     ws = []
-    for i in range(4):
+    for i in range(pairs):
         a = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
         b = torch.empty(wbytes, dtype=torch.uint8, device="cuda")
         K.call("kcpp_weight_synth", K.Q4_K_RS, 1, 10 + 2 * i, a.data_ptr(), Kd, N, sp)
@@ -81,13 +82,13 @@ def measure_roofline(K, torch, iters=48):
         d.K, d.x, d.nw, d.eps, d.nseg = Kd, x.data_ptr(), nw.data_ptr(), 1e-5, 1
         d.W[0], d.W2, d.N[0], d.Y[0] = a.data_ptr(), b.data_ptr(), N, y.data_ptr()
         args.append(d)
-    for i in range(8):
-        assert K.gemv_dec(K.Q4_K_RS, args[i % 4], 1, 1, 1, sp) == 0
+    for i in range(2 * pairs):
+        assert K.gemv_dec(K.Q4_K_RS, args[i % pairs], 1, 1, 1, sp) == 0
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record(s)
     for i in range(iters):
-        K.gemv_dec(K.Q4_K_RS, args[i % 4], 1, 1, 1, sp)
+        K.gemv_dec(K.Q4_K_RS, args[i % pairs], 1, 1, 1, sp)
     e1.record(s)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / iters
@@ -100,7 +101,11 @@ def measure_roofline(K, torch, iters=48):
             "avg_us": round(ms * 1e3, 2)}
 
 
-def cpu_baseline(hp, types, threads, n_prompt=32, n_gen=4):
+def cpu_baseline(hp, types, threads, n_prompt=512, n_gen=16, threads2=8):
+    """The REFERENCE ggml CPU build on the same synthetic weights, koboldcpp --benchmark semantics, on a bounded
+    sample: a 512-token prompt (one ubatch) then 16 greedy tokens at context 512..527 (the GPU line decodes at
+    ~3.85k; the CPU cannot prefill 3840 tokens in a bounded run).  `threads` = the box's CPU share (16 on the GPU
+    box, OMP_NUM_THREADS), plus a second run at 8 threads for comparability."""
     import refharness as R
     if not R.ref_available():
         return None
@@ -108,6 +113,7 @@ def cpu_baseline(hp, types, threads, n_prompt=32, n_gen=4):
     hp2 = dict(hp)
     hp2["n_ctx"] = n_prompt + n_gen + 8
     _, info = R.run_ref_llama(hp2, types, 1234, prompt, n_gen, nthreads=threads, ubatch=512, timeout=900)
+    _, info2 = R.run_ref_llama(hp2, types, 1234, prompt, n_gen, nthreads=threads2, ubatch=512, timeout=900)
     cpu = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -118,8 +124,12 @@ def cpu_baseline(hp, types, threads, n_prompt=32, n_gen=4):
             "cpu_model": cpu, "host_cpus": os.cpu_count(),
             "kind": "reference",
             "prefill_tok_s": round(n_prompt / info["prefill_s"], 3),
-            "sample": "reference ggml CPU (oracle/_ref/ref_llama) on the same synthetic Llama-3-8B Q4_K_M: "
-                      "%d-token prefill + %d greedy decode tokens, %d threads" % (n_prompt, n_gen, threads)}
+            "context_depth": [n_prompt, n_prompt + n_gen],
+            "at_%d_threads" % threads2: {"decode_tok_s": round(n_gen / info2["decode_s"], 3),
+                                         "prefill_tok_s": round(n_prompt / info2["prefill_s"], 3)},
+            "sample": "reference ggml CPU (oracle/_ref/ref_llama, built from the reference sources) on the same "
+                      "synthetic Llama-3-8B Q4_K_M: %d-token prefill then %d greedy decode tokens at context %d-%d, "
+                      "%d threads (and %d)" % (n_prompt, n_gen, n_prompt, n_prompt + n_gen, threads, threads2)}
 
 
 def run_model(K, torch, hp, types, n_prompt, ubatch, steps, warmup):
@@ -245,9 +255,20 @@ def main():
     types = q4_k_m_types(hp["n_layer"])
     r = run_model(K, torch, hp, types, args.prompt, args.ubatch, args.steps, args.warmup)
     dec, pre, ms_step, steps, n_past, wb, t_pp = r["dec"], r["pre"], r["ms_step"], r["steps"], r["n_past"], r["wb"], r["t_pp"]
-    # decode roofline over the whole token: weights + KV at the mean position
+    # decode roofline over the whole token (B(p) = weights read per token + KV at the mean
+    # position; token_embd is a 1-row gather, not streamed, so it is excluded)
+    import refharness as R
+    embd_bytes = R.row_bytes(types[0], hp["n_embd"]) * hp["n_vocab"]
     kv_bytes = 2 * hp["n_layer"] * hp["n_head_kv"] * (hp["n_embd"] // hp["n_head"]) * 2 * (n_past - steps / 2)
-    token_gbs = (wb + kv_bytes) / (ms_step * 1e-3) / 1e9
+    token_gbs = (wb - embd_bytes + kv_bytes) / (ms_step * 1e-3) / 1e9
+    # prefill roofline: F(n) = 2 * (layer weight elements) * n + attention 2 * 2 * n_head * D
+    # * n(n+1)/2 per layer (causal QK^T and PV) + the output head once (only the last logits are computed)
+    shapes = R.weight_shapes(hp)
+    layer_elems = sum(k * n for i, (k, n) in enumerate(shapes) if i >= 3 and n > 1)
+    n = args.prompt
+    attn_flops = 4 * hp["n_layer"] * hp["n_embd"] * n * (n + 1) / 2
+    pre_flops = 2 * layer_elems * n + attn_flops + 2 * hp["n_embd"] * hp["n_vocab"]
+    pre_tflops = pre_flops / t_pp / 1e12
     roof = measure_roofline(K, torch)
     out = {
         "metric": "decode tok/s (Llama-3-8B Q4_K_M, 4k ctx); prefill tok/s in prefill_tok_s",
@@ -260,8 +281,12 @@ def main():
                    "parallelism": "single GPU"},
         "prefill_tok_s": round(pre, 1), "prefill_s": round(t_pp, 4),
         "decode_effective_GBps": round(token_gbs, 1), "decode_hbm_frac": round(token_gbs / HBM_PEAK_GBS, 4),
-        "weight_bytes": wb,
+        "decode_bytes_per_token": int(wb - embd_bytes + kv_bytes),
+        "weight_bytes_resident": wb,
         "roofline": roof,
+        "prefill_roofline": {"bound": "mfma", "achieved": round(pre_tflops, 1), "peak": MFMA_F16_PEAK_TFLOPS,
+                             "unit": "TFLOP/s", "frac": round(pre_tflops / MFMA_F16_PEAK_TFLOPS, 4),
+                             "flops": int(pre_flops), "scope": "whole prefill (all kernels), F(n) of SURVEY.md 8d"},
     }
     if not args.no_cpu_baseline:
         try:

@@ -119,6 +119,10 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
  * Same layouts and causal window as kcpp_flash_attn; D = 128. */
 int kcpp_flash_attn_exact(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, int T, int H,
                           int HKV, int D, int n_past, const int32_t *n_past_dev, float scale, void *stream);
+/* the same in the ggml op's graph form (arguments as kcpp_flash_attn_ext, no workspace): the b1 backend's strict mode */
+int kcpp_flash_attn_ext_exact(const float *q, int64_t q_nb1, int64_t q_nb2, const uint16_t *kc, const uint16_t *vc,
+                              const uint16_t *mask, int64_t mask_ld, float *out, int T, int H, int HKV, int D, int n_kv,
+                              float scale, void *stream);
 /* single-token decode attention with explicit cache strides in elements (key p of kv head hk at
  * kc + p*kv_ld + hk*kv_hs); variant 0: 64-key chunks + combine, 1: splits with in-launch merge, 2: splits +
  * combine (A/B measurement entry, tools/fa_dec_bench.py) */
@@ -184,7 +188,10 @@ int kcpp_ggml_sum_rows(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_
 /* dst[:, i10, i11, i12] = src[:, ids[i10, i11, i12], i11, i12] for KT_F32 / KT_F16 sources */
 int kcpp_ggml_get_rows(int stype, const void *src, const kcpp_tdesc *ts, const int32_t *ids, const kcpp_tdesc *ti,
                        void *dst, const kcpp_tdesc *td, void *stream);
-/* mul_mat with a KT_F16 (src1 rounded to f16, vec_dot_f16) or KT_F32 weight, any strides, batched */
+/* mul_mat with a KT_F16 (src1 rounded to f16, vec_dot_f16), KCPP_MM_F16_X32 (F16 weight x f32 src1 without
+ * rounding: the reference CPU's tinyBLAS route when built with AVX2/F16C, llamafile/sgemm.cpp:1094-1103) or KT_F32
+ * weight, any strides, batched */
+#define KCPP_MM_F16_X32 0x101
 int kcpp_ggml_mul_mat_f(int wtype, const void *w, const kcpp_tdesc *tw, const float *x, const kcpp_tdesc *tx, float *d,
                         const kcpp_tdesc *td, void *stream);
 /* GGML_OP_FLASH_ATTN_EXT in the graph's own form: q f32 (byte strides q_nb1 per query, q_nb2 per head), K/V f16

@@ -35,24 +35,34 @@ __device__ __forceinline__ uint16_t f2h_of_f32(float x) {
     return f2h(x);
 }
 
-__global__ void __launch_bounds__(EX_D) k_fa_exact(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
+// EXT = the ggml op's own form (the b1 backend): q f32 with byte strides (rounded to f16 here, q_to_vec_dot),
+// all n_kv keys of the K/V views under an explicit f16 mask row (-inf keys skipped, others s*scale + mask).
+// Otherwise the runtime's form: q16 f16 [T][H][D], implicit causal window [0, n_past + t].
+template <bool EXT>
+__global__ void __launch_bounds__(EX_D) k_fa_exact(const uint16_t *__restrict__ q16, const float *__restrict__ qf32,
+                                                   int64_t q_nb1, int64_t q_nb2, const uint16_t *__restrict__ kc,
                                                    const uint16_t *__restrict__ vc, float *__restrict__ out, int H,
                                                    int HKV, int n_past_arg, const int32_t *__restrict__ n_past_dev,
-                                                   float scale) {
+                                                   float scale, const uint16_t *__restrict__ mask, int64_t mask_ld) {
     const int h = blockIdx.x, t = blockIdx.y, d = threadIdx.x;
     const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
-    const int n_kv = n_past + t + 1;                 // causal: query t (position n_past + t) sees keys 0..n_past+t
+    // causal: query t (position n_past + t) sees keys 0..n_past+t; EXT: n_past_arg = n_kv, the mask decides
+    const int n_kv = EXT ? n_past_arg : n_past + t + 1;
+    const uint16_t *mrow = EXT && mask ? mask + (int64_t)t * mask_ld : nullptr;
     const int hk = h / (H / HKV);
     const int64_t ekv = (int64_t)HKV * EX_D;
     __shared__ float qf[EX_D];
     __shared__ float sc[EX_CH];
-    qf[d] = h2f(q16[((int64_t)t * H + h) * EX_D + d]);
+    if constexpr (EXT) qf[d] = h2f(f2h(((const float *)((const char *)qf32 + t * q_nb1 + h * q_nb2))[d]));
+    else qf[d] = h2f(q16[((int64_t)t * H + h) * EX_D + d]);
     __syncthreads();
     float M = -INFINITY, S = 0.0f;
     uint16_t vkq = 0;
     for (int c0 = 0; c0 < n_kv; c0 += EX_CH) {
         const int cnt = min(EX_CH, n_kv - c0);
         for (int j = d; j < cnt; j += EX_D) {
+            const float mv = mrow ? h2f(mrow[c0 + j]) : 0.0f;
+            if (mv == -INFINITY) { sc[j] = -INFINITY; continue; }      // the reference skips the key entirely
             const uint4 *kr = (const uint4 *)(kc + (int64_t)(c0 + j) * ekv + (int64_t)hk * EX_D);
             float acc[4][8];
 #pragma unroll
@@ -80,12 +90,13 @@ __global__ void __launch_bounds__(EX_D) k_fa_exact(const uint16_t *__restrict__ 
             const float t0 = acc[0][0] + acc[0][4], t1 = acc[0][1] + acc[0][5], t2 = acc[0][2] + acc[0][6],
                         t3 = acc[0][3] + acc[0][7];
             const float s = (t0 + t1) + (t2 + t3);
-            sc[j] = s * scale + 0.0f;                      // s*scale, then += mask (0 inside the window)
+            sc[j] = s * scale + mv;                        // s*scale, then += mask
         }
         __syncthreads();
         const uint16_t *vr = vc + (int64_t)c0 * ekv + (int64_t)hk * EX_D + d;
         for (int j = 0; j < cnt; ++j) {
             const float s = sc[j];
+            if (s == -INFINITY) continue;                  // masked key (a finite score plus a finite mask never is)
             const float v = h2f(vr[(int64_t)j * ekv]);
             float ms = 1.0f, vs = 1.0f;
             if (s > M) {
@@ -110,7 +121,18 @@ extern "C" int kcpp_flash_attn_exact(const uint16_t *q16, const uint16_t *kc, co
                                      int H, int HKV, int D, int n_past, const int32_t *n_past_dev, float scale,
                                      void *stream) {
     if (D != EX_D || T < 1 || HKV < 1 || H % HKV != 0 || (!n_past_dev && n_past < 0)) return -3;
-    hipLaunchKernelGGL(k_fa_exact, dim3(H, T), dim3(EX_D), 0, (hipStream_t)stream, q16, kc, vc, out, H, HKV, n_past,
-                       n_past_dev, scale);
+    hipLaunchKernelGGL(k_fa_exact<false>, dim3(H, T), dim3(EX_D), 0, (hipStream_t)stream, q16, nullptr, 0, 0, kc, vc, out,
+                       H, HKV, n_past, n_past_dev, scale, nullptr, 0);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// the graph form of GGML_OP_FLASH_ATTN_EXT (as kcpp_flash_attn_ext): q f32 [T][H][D] by byte strides, K/V views
+// [n_kv][HKV][D], optional f16 mask [T][n_kv] with row stride mask_ld (elements), out f32 [T][H][D]
+extern "C" int kcpp_flash_attn_ext_exact(const float *q, int64_t q_nb1, int64_t q_nb2, const uint16_t *kc,
+                                         const uint16_t *vc, const uint16_t *mask, int64_t mask_ld, float *out, int T,
+                                         int H, int HKV, int D, int n_kv, float scale, void *stream) {
+    if (D != EX_D || T < 1 || HKV < 1 || H % HKV != 0 || n_kv < 1) return -3;
+    hipLaunchKernelGGL(k_fa_exact<true>, dim3(H, T), dim3(EX_D), 0, (hipStream_t)stream, nullptr, q, q_nb1, q_nb2, kc, vc,
+                       out, H, HKV, n_kv, nullptr, scale, mask, mask_ld);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -1,0 +1,705 @@
+// ggml_backend.cpp -- the ggml backend plugin over this library's HIP kernels.
+//
+// What llama.cpp / ggml-backend.cpp see is the reference's ROCm backend interface (ggml/src/ggml-cuda.cu): a
+// registry "ROCm" with one device per GPU (GPU_FULL), per-device buffer types with 128-B alignment whose
+// get_alloc_size pads quantized rows to 512 elements and whose init_tensor zeroes that pad, a pinned host buffer
+// type, backends (one HIP stream each) with async tensor copies, events and graph_compute(ggml_cgraph *), and
+// the koboldcpp switch ggml_cuda_set_mul_mat_q.  The vtable types are the restated ones of
+// include/kcpp_ggml_backend.h (same layout as ggml-backend-impl.h).
+//
+// graph_compute walks the nodes in order (ggml_backend_cuda_graph_compute, ggml-cuda.cu:2508-2778 with CUDA
+// graphs off) and dispatches each to a kernel of this library:
+//   MUL_MAT      quantized weight: activation -> Q8_K/Q8_0 (kcpp_quantize_act), then the mat-vec (M <= 8) or the
+//                MFMA GEMM on a device-native image of the weight (row-major Q4_K_RS / Q6_K_RS planes, the
+//                structure-of-arrays Q4_0 / Q8_0 / Q6_K layouts), built once per weight on first use and kept until
+//                the weight's buffer is written again; F16 / F32 weight: kcpp_ggml_mul_mat_f
+//   GET_ROWS     quantized: kcpp_get_rows on the native image; F16 / F32: kcpp_ggml_get_rows
+//   FLASH_ATTN_EXT  kcpp_flash_attn_ext (graph-form Q view, F16 K/V cache views, F16 mask)
+//   RMS_NORM, ROPE (NORM / NEOX, YaRN), SOFT_MAX, ADD/SUB/MUL/DIV (broadcast), SCALE, UNARY (SILU/NEG/RELU),
+//   CPY/CONT/DUP (F32 <-> F16), ARGSORT, SUM_ROWS: the general-layout kernels of ggml_ops.hip
+//   NONE/RESHAPE/VIEW/PERMUTE/TRANSPOSE: nothing (views)
+// supports_op answers true for exactly these (placement decides the rest onto the CPU backend, as
+// ggml_backend_sched does with the reference's supports_op, ggml-cuda.cu:2959-3185).
+//
+// Errors: the reference aborts on a CUDA error (CUDA_CHECK, common.cuh:64-75); across this ABI nothing is
+// thrown -- graph_compute returns GGML_STATUS_FAILED with the reason in kcpp_ggml_backend_last_error().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "../../include/kcpp_ggml_backend.h"
+#include "../../include/kcpp_mi355x.h"
+#include "../../include/kcpp_synth.h"
+
+namespace {
+
+std::string g_last_error;
+int g_last_nodes = 0;
+bool g_mul_mat_q = true;
+
+// ggml type traits (ggml.c type_traits: blck_size, type_size, is_quantized) for every ggml_type id
+struct TypeTrait { int blck, size; bool quant; };
+const TypeTrait kTraits[KGGML_TYPE_COUNT] = {
+    {1, 4, false},     {1, 2, false},     {32, 18, true},    {32, 20, true},   {0, 0, false},    {0, 0, false},
+    {32, 22, true},    {32, 24, true},    {32, 34, true},    {32, 36, true},   {256, 84, true},  {256, 110, true},
+    {256, 144, true},  {256, 176, true},  {256, 210, true},  {256, 292, true}, {256, 66, true},  {256, 74, true},
+    {256, 98, true},   {256, 50, true},   {32, 18, true},    {256, 110, true}, {256, 82, true},  {256, 136, true},
+    {1, 1, false},     {1, 2, false},     {1, 4, false},     {1, 8, false},    {1, 8, false},    {256, 56, true},
+    {1, 2, false},     {32, 18, true},    {32, 18, true},    {32, 18, true},   {256, 54, true},  {256, 66, true},
+};
+
+bool type_ok(int t) { return t >= 0 && t < KGGML_TYPE_COUNT && kTraits[t].blck > 0; }
+bool is_quantized(int t) { return type_ok(t) && kTraits[t].quant; }
+size_t row_size(int t, int64_t ne) { return (size_t)kTraits[t].size * ne / kTraits[t].blck; }
+// ggml_nbytes (ggml.c)
+size_t nbytes(const kggml_tensor *t) {
+    const int b = kTraits[t->type].blck;
+    size_t n;
+    if (b == 1) {
+        n = kTraits[t->type].size;
+        for (int i = 0; i < KGGML_MAX_DIMS; ++i) n += (t->ne[i] - 1) * t->nb[i];
+    } else {
+        n = t->ne[0] * t->nb[0] / b;
+        for (int i = 1; i < KGGML_MAX_DIMS; ++i) n += (t->ne[i] - 1) * t->nb[i];
+    }
+    return n;
+}
+bool is_contiguous(const kggml_tensor *t) {   // ggml_is_contiguous
+    size_t next = kTraits[t->type].size;
+    if (t->ne[0] != kTraits[t->type].blck && t->nb[0] != next) return false;
+    next *= t->ne[0] / kTraits[t->type].blck;
+    for (int i = 1; i < KGGML_MAX_DIMS; ++i) {
+        if (t->ne[i] != 1) {
+            if (t->nb[i] != next) return false;
+            next *= t->ne[i];
+        }
+    }
+    return true;
+}
+int64_t nrows(const kggml_tensor *t) { return t->ne[1] * t->ne[2] * t->ne[3]; }
+kcpp_tdesc td_of(const kggml_tensor *t) {
+    kcpp_tdesc d;
+    for (int i = 0; i < 4; ++i) { d.ne[i] = t->ne[i]; d.nb[i] = (int64_t)t->nb[i]; }
+    return d;
+}
+float op_f(const kggml_tensor *t, int i) { float f; memcpy(&f, &t->op_params[i], 4); return f; }
+
+bool set_err(const std::string &s) { g_last_error = s; fprintf(stderr, "[kcpp ggml backend] %s\n", s.c_str()); return false; }
+
+// ------------------------------------------------------------------ buffers
+struct BufCtx {
+    int device;
+    void *dev_ptr;
+    std::string name;
+    unsigned gen = 0;          // bumped by every write through the buffer interface (native-image invalidation)
+};
+struct BuftCtx {
+    int device;
+    std::string name;
+};
+
+// device-native images of quantized weights, keyed by (device, data pointer, ggml type, K, N, target layout)
+struct Image { void *d; kggml_backend_buffer_t buf; unsigned gen; };
+std::mutex g_img_mu;
+std::map<std::tuple<int, const void *, int, int64_t, int64_t, int>, Image> g_images;
+
+void drop_images(kggml_backend_buffer_t buf) {
+    std::lock_guard<std::mutex> lk(g_img_mu);
+    for (auto it = g_images.begin(); it != g_images.end();) {
+        if (it->second.buf == buf) { hipFree(it->second.d); it = g_images.erase(it); }
+        else ++it;
+    }
+}
+
+const char *buf_get_name(kggml_backend_buffer_t b) { return ((BufCtx *)b->context)->name.c_str(); }
+bool buffer_is_ours(kggml_backend_buffer_t b) { return b && b->iface.get_name == buf_get_name; }
+void buf_free(kggml_backend_buffer_t b) {
+    BufCtx *c = (BufCtx *)b->context;
+    drop_images(b);
+    hipSetDevice(c->device);
+    hipFree(c->dev_ptr);
+    delete c;
+    // the host's ggml_backend_buffer_free deletes the struct (ggml-backend.cpp); ours when freed here directly
+}
+void *buf_get_base(kggml_backend_buffer_t b) { return ((BufCtx *)b->context)->dev_ptr; }
+
+size_t buft_get_alloc_size(kggml_backend_buffer_type_t, const kggml_tensor *t);
+
+// ggml_backend_cuda_buffer_init_tensor (ggml-cuda.cu:443-461): zero the row padding of quantized weights so the
+// kernels may read into it
+void buf_init_tensor(kggml_backend_buffer_t b, kggml_tensor *t) {
+    if (t->view_src != nullptr) return;
+    if (is_quantized(t->type) && b->usage != KGGML_BACKEND_BUFFER_USAGE_COMPUTE) {
+        const size_t orig = nbytes(t), padded = buft_get_alloc_size(b->buft, t);
+        if (padded > orig) {
+            hipSetDevice(((BufCtx *)b->context)->device);
+            hipMemset((char *)t->data + orig, 0, padded - orig);
+        }
+    }
+}
+void buf_memset_tensor(kggml_backend_buffer_t b, kggml_tensor *t, uint8_t v, size_t off, size_t size) {
+    BufCtx *c = (BufCtx *)b->context;
+    hipSetDevice(c->device);
+    ++c->gen;
+    hipMemsetAsync((char *)t->data + off, v, size, hipStreamPerThread);
+    hipStreamSynchronize(hipStreamPerThread);
+}
+void buf_set_tensor(kggml_backend_buffer_t b, kggml_tensor *t, const void *data, size_t off, size_t size) {
+    BufCtx *c = (BufCtx *)b->context;
+    hipSetDevice(c->device);
+    ++c->gen;
+    hipMemcpyAsync((char *)t->data + off, data, size, hipMemcpyHostToDevice, hipStreamPerThread);
+    hipStreamSynchronize(hipStreamPerThread);
+}
+void buf_get_tensor(kggml_backend_buffer_t b, const kggml_tensor *t, void *data, size_t off, size_t size) {
+    hipSetDevice(((BufCtx *)b->context)->device);
+    hipMemcpyAsync(data, (const char *)t->data + off, size, hipMemcpyDeviceToHost, hipStreamPerThread);
+    hipStreamSynchronize(hipStreamPerThread);
+}
+bool buf_cpy_tensor(kggml_backend_buffer_t b, const kggml_tensor *src, kggml_tensor *dst) {
+    if (!buffer_is_ours(src->buffer)) return false;
+    BufCtx *sc = (BufCtx *)src->buffer->context, *dc = (BufCtx *)dst->buffer->context;
+    ++dc->gen;
+    if (sc->device == dc->device) {
+        hipSetDevice(dc->device);
+        hipMemcpyAsync(dst->data, src->data, nbytes(src), hipMemcpyDeviceToDevice, hipStreamPerThread);
+    } else {
+        hipMemcpyPeerAsync(dst->data, dc->device, src->data, sc->device, nbytes(src), hipStreamPerThread);
+    }
+    hipStreamSynchronize(hipStreamPerThread);
+    return true;
+    (void)b;
+}
+void buf_clear(kggml_backend_buffer_t b, uint8_t v) {
+    BufCtx *c = (BufCtx *)b->context;
+    hipSetDevice(c->device);
+    ++c->gen;
+    hipDeviceSynchronize();
+    hipMemset(c->dev_ptr, v, b->size);
+    hipDeviceSynchronize();
+}
+const kggml_backend_buffer_i kBufIface = {buf_get_name, buf_free,      buf_get_base,   buf_init_tensor, buf_memset_tensor,
+                                          buf_set_tensor, buf_get_tensor, buf_cpy_tensor, buf_clear,       nullptr};
+
+const char *buft_get_name(kggml_backend_buffer_type_t bt) { return ((BuftCtx *)bt->context)->name.c_str(); }
+bool buft_is_ours(kggml_backend_buffer_type_t bt) { return bt && bt->iface.get_name == buft_get_name; }
+kggml_backend_buffer_t buft_alloc_buffer(kggml_backend_buffer_type_t bt, size_t size) {
+    BuftCtx *c = (BuftCtx *)bt->context;
+    hipSetDevice(c->device);
+    size = std::max<size_t>(size, 1);
+    void *p = nullptr;
+    if (hipMalloc(&p, size) != hipSuccess) {
+        (void)hipGetLastError();
+        set_err("alloc_buffer: hipMalloc of " + std::to_string(size) + " bytes failed on device " + std::to_string(c->device));
+        return nullptr;
+    }
+    BufCtx *bc = new BufCtx{c->device, p, KGGML_CUDA_NAME + std::to_string(c->device)};
+    // ggml_backend_buffer_init (ggml-backend.cpp): {iface, buft, context, size, usage ANY}
+    return new kggml_backend_buffer{kBufIface, bt, bc, size, KGGML_BACKEND_BUFFER_USAGE_ANY};
+}
+size_t buft_get_alignment(kggml_backend_buffer_type_t) { return 128; }   // ggml-cuda.cu:567-571
+// ggml-cuda.cu:573-586: quantized rows padded to a multiple of MATRIX_ROW_PADDING = 512 elements
+size_t buft_get_alloc_size(kggml_backend_buffer_type_t, const kggml_tensor *t) {
+    size_t size = nbytes(t);
+    const int64_t ne0 = t->ne[0];
+    if (is_quantized(t->type) && ne0 % 512 != 0) size += row_size(t->type, 512 - ne0 % 512);
+    return size;
+}
+const kggml_backend_buffer_type_i kBuftIface = {buft_get_name, buft_alloc_buffer, buft_get_alignment, nullptr,
+                                                buft_get_alloc_size, nullptr};
+
+// pinned host buffer type (ggml_backend_cuda_host_buffer_type): host-visible, hipHostMalloc'd
+struct HostBufCtx { void *p; };
+const char *hbuf_get_name(kggml_backend_buffer_t) { return KGGML_CUDA_NAME "_Host"; }
+void hbuf_free(kggml_backend_buffer_t b) { hipHostFree(((HostBufCtx *)b->context)->p); delete (HostBufCtx *)b->context; }
+void *hbuf_get_base(kggml_backend_buffer_t b) { return ((HostBufCtx *)b->context)->p; }
+void hbuf_memset(kggml_backend_buffer_t, kggml_tensor *t, uint8_t v, size_t off, size_t size) { memset((char *)t->data + off, v, size); }
+void hbuf_set(kggml_backend_buffer_t, kggml_tensor *t, const void *d, size_t off, size_t size) { memcpy((char *)t->data + off, d, size); }
+void hbuf_get(kggml_backend_buffer_t, const kggml_tensor *t, void *d, size_t off, size_t size) { memcpy(d, (const char *)t->data + off, size); }
+void hbuf_clear(kggml_backend_buffer_t b, uint8_t v) { memset(((HostBufCtx *)b->context)->p, v, b->size); }
+const kggml_backend_buffer_i kHostBufIface = {hbuf_get_name, hbuf_free, hbuf_get_base, nullptr, hbuf_memset,
+                                              hbuf_set,      hbuf_get,  nullptr,       hbuf_clear, nullptr};
+const char *hbuft_get_name(kggml_backend_buffer_type_t) { return KGGML_CUDA_NAME "_Host"; }
+kggml_backend_buffer_t hbuft_alloc(kggml_backend_buffer_type_t bt, size_t size) {
+    void *p = nullptr;
+    size = std::max<size_t>(size, 1);
+    if (hipHostMalloc(&p, size, hipHostMallocPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        set_err("host buffer: hipHostMalloc failed");
+        return nullptr;
+    }
+    return new kggml_backend_buffer{kHostBufIface, bt, new HostBufCtx{p}, size, KGGML_BACKEND_BUFFER_USAGE_ANY};
+}
+size_t hbuft_alignment(kggml_backend_buffer_type_t) { return 32; }    // TENSOR_ALIGNMENT of the CPU buffer type
+bool hbuft_is_host(kggml_backend_buffer_type_t) { return true; }
+const kggml_backend_buffer_type_i kHostBuftIface = {hbuft_get_name, hbuft_alloc, hbuft_alignment, nullptr, nullptr,
+                                                    hbuft_is_host};
+
+// ------------------------------------------------------------------ devices, registry
+struct DevCtx {
+    int device;
+    std::string name, description;
+};
+kggml_backend_reg g_reg;
+std::vector<kggml_backend_device> g_devs;
+std::vector<kggml_backend_buffer_type> g_bufts;
+kggml_backend_buffer_type g_host_buft = {kHostBuftIface, nullptr, nullptr};
+kggml_guid g_guid = {0x2c, 0xdd, 0xe8, 0x1c, 0x65, 0xb3, 0x65, 0x73, 0x6a, 0x12, 0x88, 0x61, 0x1c, 0xc9, 0xdc, 0x25};
+std::once_flag g_init_once;
+void init_registry();
+
+// ------------------------------------------------------------------ backend (one HIP stream)
+struct Scratch {
+    void *p = nullptr;
+    size_t sz = 0;
+    void *get(size_t n) {
+        if (n <= sz) return p;
+        if (p) hipFree(p);
+        p = nullptr;
+        sz = 0;
+        if (hipMalloc(&p, n) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+        sz = n;
+        return p;
+    }
+};
+struct BackendCtx {
+    int device;
+    std::string name;
+    hipStream_t stream;
+    Scratch act, ws, fa;
+    bool fa_exact = false;     // attention in the reference CPU's order with its f16 accumulator (attn_exact.hip)
+};
+
+// the native image of weight w for target layout `tt` (kcpp type id); w itself when the layouts coincide
+const void *native_image(BackendCtx *bc, const kggml_tensor *w, int tt) {
+    const int64_t K = w->ne[0], N = w->ne[1] * w->ne[2] * w->ne[3];
+    if (tt == w->type && (tt == KT_Q4_K || tt == KT_Q5_K)) return w->data;      // kcpp layout = ggml layout
+    kggml_backend_buffer_t buf = w->view_src ? w->view_src->buffer : w->buffer;
+    const unsigned gen = buffer_is_ours(buf) ? ((BufCtx *)buf->context)->gen : 0;
+    const auto key = std::make_tuple(bc->device, (const void *)w->data, w->type, K, N, tt);
+    std::lock_guard<std::mutex> lk(g_img_mu);
+    auto it = g_images.find(key);
+    if (it != g_images.end() && it->second.gen == gen) return it->second.d;
+    if (it != g_images.end()) { hipStreamSynchronize(bc->stream); hipFree(it->second.d); g_images.erase(it); }
+    void *d = nullptr;
+    if (hipMalloc(&d, row_size(w->type, K) * N) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
+    if (kcpp_weight_repack(tt, w->data, d, K, N, 0, bc->stream) != 0) { hipFree(d); return nullptr; }
+    g_images[key] = Image{d, buf, gen};
+    return d;
+}
+
+// decode-layout choice for mat-mul weights (as kcpp_model_create picks it)
+int matmul_layout(int t, int64_t K) {
+    if (t == KT_Q4_K && kcpp_rs_supported(KT_Q4_K_RS, K)) return KT_Q4_K_RS;
+    if (t == KT_Q6_K && kcpp_rs_supported(KT_Q6_K_RS, K)) return KT_Q6_K_RS;
+    return t;
+}
+bool matmul_quant_ok(int t) { return t == KT_Q4_0 || t == KT_Q8_0 || t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K; }
+
+bool supports(const kggml_tensor *op) {
+    auto f32 = [](const kggml_tensor *t) { return t && t->type == KGGML_TYPE_F32; };
+    switch (op->op) {
+    case KGGML_OP_NONE: case KGGML_OP_RESHAPE: case KGGML_OP_VIEW: case KGGML_OP_PERMUTE: case KGGML_OP_TRANSPOSE:
+        return true;
+    case KGGML_OP_ADD: case KGGML_OP_SUB: case KGGML_OP_MUL: case KGGML_OP_DIV:
+        return f32(op) && f32(op->src[0]) && f32(op->src[1]);
+    case KGGML_OP_SCALE: case KGGML_OP_RMS_NORM:
+        return f32(op) && f32(op->src[0]);
+    case KGGML_OP_UNARY: {
+        const int u = op->op_params[0];
+        return (u == KGGML_UNARY_OP_SILU || u == KGGML_UNARY_OP_NEG || u == KGGML_UNARY_OP_RELU) && f32(op) &&
+               f32(op->src[0]);
+    }
+    case KGGML_OP_CPY: case KGGML_OP_CONT: case KGGML_OP_DUP: {
+        const int s = op->src[0]->type, d = op->op == KGGML_OP_CPY ? op->src[1]->type : op->type;
+        return (s == KGGML_TYPE_F32 || s == KGGML_TYPE_F16) && (d == KGGML_TYPE_F32 || d == KGGML_TYPE_F16);
+    }
+    case KGGML_OP_ROPE: {
+        const int mode = op->op_params[2];
+        return f32(op) && f32(op->src[0]) && (mode == 0 || mode == 2) && op->src[0]->nb[0] == 4;
+    }
+    case KGGML_OP_SOFT_MAX:
+        return f32(op) && f32(op->src[0]) && op_f(op, 1) == 0.0f &&
+               (!op->src[1] || op->src[1]->type == KGGML_TYPE_F16 || op->src[1]->type == KGGML_TYPE_F32);
+    case KGGML_OP_ARGSORT:
+        return f32(op->src[0]) && op->type == KGGML_TYPE_I32;
+    case KGGML_OP_SUM_ROWS:
+        return f32(op) && f32(op->src[0]);
+    case KGGML_OP_GET_ROWS: {
+        const kggml_tensor *a = op->src[0], *ids = op->src[1];
+        if (!f32(op) || ids->type != KGGML_TYPE_I32) return false;
+        if (a->type == KGGML_TYPE_F32 || a->type == KGGML_TYPE_F16) return true;
+        return matmul_quant_ok(a->type) && a->ne[2] == 1 && a->ne[3] == 1 && is_contiguous(a) && is_contiguous(ids) &&
+               ids->ne[1] == 1 && ids->ne[2] == 1 && op->nb[0] == 4;
+    }
+    case KGGML_OP_MUL_MAT: {
+        const kggml_tensor *a = op->src[0], *b = op->src[1];
+        if (!f32(op) || !f32(b)) return false;
+        if (a->type == KGGML_TYPE_F32 || a->type == KGGML_TYPE_F16) return true;
+        return matmul_quant_ok(a->type) && a->ne[2] == 1 && a->ne[3] == 1 && is_contiguous(a) && b->nb[0] == 4 &&
+               b->ne[2] == 1 && b->ne[3] == 1 && is_contiguous(op) && a->ne[0] % 256 == 0;
+    }
+    case KGGML_OP_FLASH_ATTN_EXT: {
+        const kggml_tensor *q = op->src[0], *k = op->src[1], *v = op->src[2], *m = op->src[3];
+        if (!f32(op) || !f32(q) || k->type != KGGML_TYPE_F16 || v->type != KGGML_TYPE_F16) return false;
+        if (q->ne[0] != 128 || op_f(op, 1) != 0.0f || op_f(op, 2) != 0.0f || q->ne[3] != 1) return false;
+        const int64_t HKV = k->ne[2];
+        const bool kv_ok = k->nb[1] == (size_t)(HKV * 128 * 2) && k->nb[2] == 256 && v->nb[1] == k->nb[1] &&
+                           v->nb[2] == 256 && v->ne[1] == k->ne[1] && v->ne[2] == HKV;
+        return kv_ok && q->ne[2] % HKV == 0 && q->nb[0] == 4 && is_contiguous(op) &&
+               (!m || (m->type == KGGML_TYPE_F16 && m->nb[0] == 2));
+    }
+    default:
+        return false;
+    }
+}
+
+bool compute_node(BackendCtx *bc, kggml_tensor *n) {
+    hipStream_t s = bc->stream;
+    const kcpp_tdesc td = td_of(n);
+    kggml_tensor *a = n->src[0], *b = n->src[1];
+    auto chk = [&](int rc, const char *what) {
+        if (rc == 0) return true;
+        char msg[256];
+        snprintf(msg, sizeof msg, "%s failed rc=%d on node '%s' (%s)", what, rc, n->name, kcpp_last_error());
+        return set_err(msg);
+    };
+    switch (n->op) {
+    case KGGML_OP_NONE: case KGGML_OP_RESHAPE: case KGGML_OP_VIEW: case KGGML_OP_PERMUTE: case KGGML_OP_TRANSPOSE:
+        return true;
+    case KGGML_OP_ADD: case KGGML_OP_SUB: case KGGML_OP_MUL: case KGGML_OP_DIV: {
+        const int op = n->op == KGGML_OP_ADD ? KCPP_BIN_ADD : n->op == KGGML_OP_SUB ? KCPP_BIN_SUB
+                     : n->op == KGGML_OP_MUL ? KCPP_BIN_MUL : KCPP_BIN_DIV;
+        const kcpp_tdesc ta = td_of(a), tb = td_of(b);
+        return chk(kcpp_ggml_binary(op, a->data, &ta, b->data, &tb, n->data, &td, s), "binary");
+    }
+    case KGGML_OP_SCALE: {
+        const kcpp_tdesc ta = td_of(a);
+        return chk(kcpp_ggml_unary(KCPP_UN_SCALE, a->data, &ta, n->data, &td, op_f(n, 0), s), "scale");
+    }
+    case KGGML_OP_UNARY: {
+        const int u = n->op_params[0];
+        const int k = u == KGGML_UNARY_OP_SILU ? KCPP_UN_SILU : u == KGGML_UNARY_OP_NEG ? KCPP_UN_NEG : KCPP_UN_RELU;
+        const kcpp_tdesc ta = td_of(a);
+        return chk(kcpp_ggml_unary(k, a->data, &ta, n->data, &td, 0.0f, s), "unary");
+    }
+    case KGGML_OP_RMS_NORM: {
+        const kcpp_tdesc ta = td_of(a);
+        return chk(kcpp_ggml_rms_norm(a->data, &ta, n->data, &td, op_f(n, 0), s), "rms_norm");
+    }
+    case KGGML_OP_CPY: case KGGML_OP_CONT: case KGGML_OP_DUP: {
+        const kcpp_tdesc ta = td_of(a);
+        // GGML_OP_CPY's node is a view of src[1]: writing the node writes the destination
+        return chk(kcpp_ggml_cpy(a->type, a->data, &ta, n->type, n->data, &td, s), "cpy");
+    }
+    case KGGML_OP_ROPE: {
+        const kcpp_tdesc ta = td_of(a);
+        const kggml_tensor *ff = n->src[2];
+        return chk(kcpp_ggml_rope(a->data, &ta, n->data, &td, (const int32_t *)b->data, ff ? (const float *)ff->data : nullptr,
+                                  n->op_params[1], n->op_params[2], n->op_params[4], op_f(n, 5), op_f(n, 6), op_f(n, 7),
+                                  op_f(n, 8), op_f(n, 9), op_f(n, 10), s),
+                   "rope");
+    }
+    case KGGML_OP_SOFT_MAX: {
+        const kcpp_tdesc ta = td_of(a);
+        const kggml_tensor *m = b;
+        const int mt = m ? (m->type == KGGML_TYPE_F16 ? KT_F16 : KT_F32) : KT_F32;
+        const int64_t mld = m ? (int64_t)(m->nb[1] / kTraits[m->type].size) : 0;
+        return chk(kcpp_ggml_soft_max(a->data, &ta, m ? m->data : nullptr, mt, mld, m ? m->ne[1] : 1, n->data, &td,
+                                      op_f(n, 0), s),
+                   "soft_max");
+    }
+    case KGGML_OP_ARGSORT: {
+        const kcpp_tdesc ta = td_of(a);
+        return chk(kcpp_ggml_argsort(a->data, &ta, (int32_t *)n->data, (int64_t)(n->nb[1] / 4), n->op_params[0] == 1, s),
+                   "argsort");
+    }
+    case KGGML_OP_SUM_ROWS: {
+        const kcpp_tdesc ta = td_of(a);
+        return chk(kcpp_ggml_sum_rows(a->data, &ta, n->data, &td, s), "sum_rows");
+    }
+    case KGGML_OP_GET_ROWS: {
+        if (a->type == KGGML_TYPE_F32 || a->type == KGGML_TYPE_F16) {
+            const kcpp_tdesc ta = td_of(a), ti = td_of(b);
+            return chk(kcpp_ggml_get_rows(a->type, a->data, &ta, (const int32_t *)b->data, &ti, n->data, &td, s),
+                       "get_rows");
+        }
+        const void *img = native_image(bc, a, a->type);
+        if (!img) return set_err("get_rows: native image allocation failed");
+        return chk(kcpp_get_rows(a->type, img, a->ne[0], a->ne[1], (const int32_t *)b->data, b->ne[0], (float *)n->data,
+                                 (int64_t)(n->nb[1] / 4), s),
+                   "get_rows(quantized)");
+    }
+    case KGGML_OP_MUL_MAT: {
+        if (a->type == KGGML_TYPE_F32 || a->type == KGGML_TYPE_F16) {
+            const kcpp_tdesc ta = td_of(a), tb = td_of(b);
+            // F16 weights: the reference CPU (AVX2/F16C build) hands contiguous f32 src1 with K % 8 == 0 to
+            // tinyBLAS unrounded (llamafile/sgemm.cpp:1094-1103), otherwise rounds src1 to f16 (vec_dot_f16)
+            const int wt = a->type == KGGML_TYPE_F16 && is_contiguous(b) && a->ne[0] % 8 == 0 ? KCPP_MM_F16_X32 : a->type;
+            return chk(kcpp_ggml_mul_mat_f(wt, a->data, &ta, (const float *)b->data, &tb, (float *)n->data, &td, s),
+                       "mul_mat_f");
+        }
+        const int64_t K = a->ne[0], N = a->ne[1], M = b->ne[1];
+        const int tt = matmul_layout(a->type, K);
+        const void *W = native_image(bc, a, tt);
+        if (!W) return set_err("mul_mat: native image allocation failed");
+        void *act = bc->act.get((size_t)kcpp_act_bytes(a->type, K, M) + 256);
+        if (!act) return set_err("mul_mat: activation scratch allocation failed");
+        if (!chk(kcpp_quantize_act(kcpp_vec_dot_type(a->type), (const float *)b->data, (int64_t)(b->nb[1] / 4), act, K, M, s),
+                 "quantize_act"))
+            return false;
+        if (M <= 8)
+            return chk(kcpp_gemv(tt, W, nullptr, K, N, act, M, (float *)n->data, N, nullptr, 0, 0, s), "gemv");
+        void *ws = bc->ws.get((size_t)kcpp_gemm_workspace_bytes(tt, K, N, M) + 256);
+        if (!ws) return set_err("mul_mat: GEMM workspace allocation failed");
+        return chk(kcpp_gemm(tt, W, nullptr, K, N, act, M, (float *)n->data, N, nullptr, 0, 0, ws, s), "gemm");
+    }
+    case KGGML_OP_FLASH_ATTN_EXT: {
+        const kggml_tensor *q = a, *k = b, *v = n->src[2], *m = n->src[3];
+        const int T = (int)q->ne[1], H = (int)q->ne[2], HKV = (int)k->ne[2], n_kv = (int)k->ne[1];
+        if (bc->fa_exact)
+            return chk(kcpp_flash_attn_ext_exact((const float *)q->data, (int64_t)q->nb[1], (int64_t)q->nb[2],
+                                                 (const uint16_t *)k->data, (const uint16_t *)v->data,
+                                                 m ? (const uint16_t *)m->data : nullptr, m ? (int64_t)(m->nb[1] / 2) : 0,
+                                                 (float *)n->data, T, H, HKV, 128, n_kv, op_f(n, 0), s),
+                       "flash_attn_ext(exact)");
+        void *ws = bc->fa.get((size_t)kcpp_fa_ext_workspace_bytes(T, H, n_kv, 128));
+        if (!ws) return set_err("flash_attn_ext: workspace allocation failed");
+        return chk(kcpp_flash_attn_ext((const float *)q->data, (int64_t)q->nb[1], (int64_t)q->nb[2], (const uint16_t *)k->data,
+                                       (const uint16_t *)v->data, m ? (const uint16_t *)m->data : nullptr,
+                                       m ? (int64_t)(m->nb[1] / 2) : 0, (float *)n->data, ws, T, H, HKV, 128, n_kv,
+                                       op_f(n, 0), s),
+                   "flash_attn_ext");
+    }
+    default:
+        return set_err(std::string("unsupported op ") + std::to_string(n->op) + " on node '" + n->name + "'");
+    }
+}
+
+const char *be_get_name(kggml_backend_t be) { return ((BackendCtx *)be->context)->name.c_str(); }
+void be_free(kggml_backend_t be) {
+    BackendCtx *c = (BackendCtx *)be->context;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    for (Scratch *sc : {&c->act, &c->ws, &c->fa}) if (sc->p) hipFree(sc->p);
+    hipStreamDestroy(c->stream);
+    delete c;
+    delete be;
+}
+kggml_backend_buffer_type_t be_default_buft(kggml_backend_t be) {
+    return ggml_backend_cuda_buffer_type(((BackendCtx *)be->context)->device);
+}
+void be_set_async(kggml_backend_t be, kggml_tensor *t, const void *data, size_t off, size_t size) {
+    BackendCtx *c = (BackendCtx *)be->context;
+    kggml_backend_buffer_t buf = t->view_src ? t->view_src->buffer : t->buffer;
+    if (buffer_is_ours(buf)) ++((BufCtx *)buf->context)->gen;
+    hipSetDevice(c->device);
+    hipMemcpyAsync((char *)t->data + off, data, size, hipMemcpyHostToDevice, c->stream);
+}
+void be_get_async(kggml_backend_t be, const kggml_tensor *t, void *data, size_t off, size_t size) {
+    BackendCtx *c = (BackendCtx *)be->context;
+    hipSetDevice(c->device);
+    hipMemcpyAsync(data, (const char *)t->data + off, size, hipMemcpyDeviceToHost, c->stream);
+}
+// device-to-device between two of our backends, ordered on the source stream, then the destination waits
+// (ggml_backend_cuda_cpy_tensor_async, ggml-cuda.cu:2392-2445)
+bool be_cpy_async(kggml_backend_t src_be, kggml_backend_t dst_be, const kggml_tensor *src, kggml_tensor *dst) {
+    if (!ggml_backend_is_cuda(src_be) || !ggml_backend_is_cuda(dst_be)) return false;
+    kggml_backend_buffer_t sb = src->view_src ? src->view_src->buffer : src->buffer;
+    kggml_backend_buffer_t db = dst->view_src ? dst->view_src->buffer : dst->buffer;
+    if (!buffer_is_ours(sb) || !buffer_is_ours(db)) return false;
+    BackendCtx *sc = (BackendCtx *)src_be->context, *dc = (BackendCtx *)dst_be->context;
+    ++((BufCtx *)db->context)->gen;
+    hipSetDevice(sc->device);
+    if (sc->device == dc->device) {
+        hipMemcpyAsync(dst->data, src->data, nbytes(dst), hipMemcpyDeviceToDevice, sc->stream);
+    } else {
+        hipMemcpyPeerAsync(dst->data, dc->device, src->data, sc->device, nbytes(dst), sc->stream);
+    }
+    if (src_be != dst_be) {
+        hipEvent_t ev;
+        hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        hipEventRecord(ev, sc->stream);
+        hipSetDevice(dc->device);
+        hipStreamWaitEvent(dc->stream, ev, 0);
+        hipEventDestroy(ev);
+    }
+    return true;
+}
+void be_synchronize(kggml_backend_t be) {
+    BackendCtx *c = (BackendCtx *)be->context;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+}
+int be_graph_compute(kggml_backend_t be, kggml_cgraph *g) {
+    BackendCtx *c = (BackendCtx *)be->context;
+    hipSetDevice(c->device);
+    g_last_nodes = 0;
+    for (int i = 0; i < g->n_nodes; ++i) {
+        kggml_tensor *n = g->nodes[i];
+        if (n->ne[0] == 0 || n->ne[1] == 0 || n->ne[2] == 0 || n->ne[3] == 0) continue;   // ggml_is_empty
+        if (!supports(n)) { set_err(std::string("graph_compute: unsupported node '") + n->name + "'"); return KGGML_STATUS_FAILED; }
+        if (!compute_node(c, n)) return KGGML_STATUS_FAILED;
+        ++g_last_nodes;
+    }
+    if (hipGetLastError() != hipSuccess) { set_err("graph_compute: HIP launch error"); return KGGML_STATUS_FAILED; }
+    return KGGML_STATUS_SUCCESS;
+}
+void be_event_record(kggml_backend_t be, kggml_backend_event_t ev) {
+    hipEventRecord((hipEvent_t)ev->context, ((BackendCtx *)be->context)->stream);
+}
+void be_event_wait(kggml_backend_t be, kggml_backend_event_t ev) {
+    hipStreamWaitEvent(((BackendCtx *)be->context)->stream, (hipEvent_t)ev->context, 0);
+}
+const kggml_backend_i kBackendIface = {be_get_name,  be_free,        be_default_buft, be_set_async,    be_get_async,
+                                       be_cpy_async, be_synchronize, nullptr,         nullptr,         nullptr,
+                                       nullptr,      be_graph_compute, nullptr,       nullptr,         nullptr,
+                                       be_event_record, be_event_wait};
+
+const char *dev_get_name(kggml_backend_dev_t d) { return ((DevCtx *)d->context)->name.c_str(); }
+const char *dev_get_description(kggml_backend_dev_t d) { return ((DevCtx *)d->context)->description.c_str(); }
+void dev_get_memory(kggml_backend_dev_t d, size_t *free, size_t *total) {
+    hipSetDevice(((DevCtx *)d->context)->device);
+    hipMemGetInfo(free, total);
+}
+int dev_get_type(kggml_backend_dev_t) { return KGGML_BACKEND_DEVICE_TYPE_GPU_FULL; }
+void dev_get_props(kggml_backend_dev_t d, kggml_backend_dev_props *p) {
+    p->name = dev_get_name(d);
+    p->description = dev_get_description(d);
+    p->type = dev_get_type(d);
+    dev_get_memory(d, &p->memory_free, &p->memory_total);
+    p->caps = {true, getenv("GGML_CUDA_NO_PINNED") == nullptr, false, true};
+}
+kggml_backend_t dev_init_backend(kggml_backend_dev_t d, const char *) { return ggml_backend_cuda_init(((DevCtx *)d->context)->device); }
+kggml_backend_buffer_type_t dev_get_buft(kggml_backend_dev_t d) { return ggml_backend_cuda_buffer_type(((DevCtx *)d->context)->device); }
+kggml_backend_buffer_type_t dev_get_host_buft(kggml_backend_dev_t) { return ggml_backend_cuda_host_buffer_type(); }
+bool dev_supports_op(kggml_backend_dev_t, const kggml_tensor *op) { return supports(op); }
+bool dev_supports_buft(kggml_backend_dev_t d, kggml_backend_buffer_type_t bt) {
+    return buft_is_ours(bt) && ((BuftCtx *)bt->context)->device == ((DevCtx *)d->context)->device;
+}
+// ggml-cuda.cu:3201-3208: batches of >= 32 pull CPU-resident weights over
+bool dev_offload_op(kggml_backend_dev_t, const kggml_tensor *op) {
+    return (op->ne[1] >= 32 && op->op != KGGML_OP_GET_ROWS) || (op->ne[2] >= 32 && op->op == KGGML_OP_MUL_MAT_ID);
+}
+kggml_backend_event_t dev_event_new(kggml_backend_dev_t d) {
+    hipSetDevice(((DevCtx *)d->context)->device);
+    hipEvent_t ev;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return nullptr;
+    return new kggml_backend_event{d, ev};
+}
+void dev_event_free(kggml_backend_dev_t, kggml_backend_event_t ev) {
+    hipEventDestroy((hipEvent_t)ev->context);
+    delete ev;
+}
+void dev_event_sync(kggml_backend_dev_t, kggml_backend_event_t ev) { hipEventSynchronize((hipEvent_t)ev->context); }
+const kggml_backend_device_i kDevIface = {dev_get_name,    dev_get_description, dev_get_memory,  dev_get_type,
+                                          dev_get_props,   dev_init_backend,    dev_get_buft,    dev_get_host_buft,
+                                          nullptr,         dev_supports_op,     dev_supports_buft, dev_offload_op,
+                                          dev_event_new,   dev_event_free,      dev_event_sync};
+
+const char *reg_get_name(kggml_backend_reg_t) { return KGGML_CUDA_NAME; }
+size_t reg_get_device_count(kggml_backend_reg_t) { return g_devs.size(); }
+kggml_backend_dev_t reg_get_device(kggml_backend_reg_t, size_t i) { return i < g_devs.size() ? &g_devs[i] : nullptr; }
+void *reg_get_proc_address(kggml_backend_reg_t, const char *name) {
+    if (!strcmp(name, "ggml_backend_split_buffer_type")) return (void *)ggml_backend_cuda_split_buffer_type;
+    if (!strcmp(name, "ggml_backend_register_host_buffer")) return (void *)ggml_backend_cuda_register_host_buffer;
+    if (!strcmp(name, "ggml_backend_unregister_host_buffer")) return (void *)ggml_backend_cuda_unregister_host_buffer;
+    return nullptr;
+}
+const kggml_backend_reg_i kRegIface = {reg_get_name, reg_get_device_count, reg_get_device, reg_get_proc_address};
+
+void init_registry() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); n = 0; }
+    n = std::min(n, KGGML_CUDA_MAX_DEVICES);
+    g_reg = kggml_backend_reg{kRegIface, nullptr};
+    g_devs.resize(n);
+    g_bufts.resize(n);
+    for (int i = 0; i < n; ++i) {
+        hipDeviceProp_t prop;
+        std::string desc = "AMD GPU";
+        if (hipGetDeviceProperties(&prop, i) == hipSuccess) desc = prop.name;
+        g_devs[i] = kggml_backend_device{kDevIface, &g_reg, new DevCtx{i, KGGML_CUDA_NAME + std::to_string(i), desc}};
+        g_bufts[i] = kggml_backend_buffer_type{kBuftIface, &g_devs[i], new BuftCtx{i, KGGML_CUDA_NAME + std::to_string(i)}};
+    }
+    g_host_buft.device = n > 0 ? &g_devs[0] : nullptr;
+}
+
+}  // namespace
+
+extern "C" {
+
+kggml_backend_reg_t ggml_backend_cuda_reg(void) {
+    std::call_once(g_init_once, init_registry);
+    return &g_reg;
+}
+int ggml_backend_cuda_get_device_count(void) {
+    std::call_once(g_init_once, init_registry);
+    return (int)g_devs.size();
+}
+kggml_backend_buffer_type_t ggml_backend_cuda_buffer_type(int device) {
+    std::call_once(g_init_once, init_registry);
+    if (device < 0 || device >= (int)g_bufts.size()) return nullptr;
+    return &g_bufts[device];
+}
+kggml_backend_buffer_type_t ggml_backend_cuda_split_buffer_type(const float *) { return nullptr; }
+kggml_backend_buffer_type_t ggml_backend_cuda_host_buffer_type(void) {
+    std::call_once(g_init_once, init_registry);
+    return &g_host_buft;
+}
+kggml_backend_t ggml_backend_cuda_init(int device) {
+    std::call_once(g_init_once, init_registry);
+    if (device < 0 || device >= (int)g_devs.size()) { set_err("ggml_backend_cuda_init: invalid device"); return nullptr; }
+    hipSetDevice(device);
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) { set_err("stream create failed"); return nullptr; }
+    BackendCtx *c = new BackendCtx{device, KGGML_CUDA_NAME + std::to_string(device), s};
+    c->fa_exact = getenv("KCPP_FA_EXACT") && atoi(getenv("KCPP_FA_EXACT")) != 0;
+    return new kggml_backend{&g_guid, kBackendIface, &g_devs[device], c};
+}
+bool ggml_backend_is_cuda(kggml_backend_t be) {
+    return be != nullptr && be->guid != nullptr && memcmp(*be->guid, g_guid, sizeof(kggml_guid)) == 0;
+}
+void ggml_backend_cuda_get_device_description(int device, char *description, size_t description_size) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) { (void)hipGetLastError(); snprintf(description, description_size, "?"); return; }
+    snprintf(description, description_size, "%s", prop.name);
+}
+void ggml_backend_cuda_get_device_memory(int device, size_t *free, size_t *total) {
+    hipSetDevice(device);
+    hipMemGetInfo(free, total);
+}
+// ggml-cuda.cu: opt-in through GGML_CUDA_REGISTER_HOST, as the reference
+bool ggml_backend_cuda_register_host_buffer(void *buffer, size_t size) {
+    if (getenv("GGML_CUDA_REGISTER_HOST") == nullptr) return false;
+    if (hipHostRegister(buffer, size, hipHostRegisterPortable | hipHostRegisterReadOnly) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return true;
+}
+void ggml_backend_cuda_unregister_host_buffer(void *buffer) {
+    if (getenv("GGML_CUDA_REGISTER_HOST") == nullptr) return;
+    if (hipHostUnregister(buffer) != hipSuccess) (void)hipGetLastError();
+}
+// koboldcpp: MMQ (integer tiles) vs the hipBLAS dequantize+GEMM route.  Here every quantized mat-mul runs on the
+// exact-integer MFMA GEMM, which is the MMQ numerics; the switch is recorded and has no other effect.
+void ggml_cuda_set_mul_mat_q(bool mul_mat_q) { g_mul_mat_q = mul_mat_q; }
+
+int kcpp_ggml_backend_last_nodes(void) { return g_last_nodes; }
+int kcpp_ggml_backend_set_fa_exact(kggml_backend_t be, int on) {
+    if (!ggml_backend_is_cuda(be)) return -1;
+    ((BackendCtx *)be->context)->fa_exact = on != 0;
+    return 0;
+}
+const char *kcpp_ggml_backend_last_error(void) { return g_last_error.c_str(); }
+
+}  // extern "C"

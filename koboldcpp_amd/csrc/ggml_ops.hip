@@ -266,7 +266,7 @@ __global__ void k_get_rows_g(const char *__restrict__ s, TD ts, const char *__re
 
 // ---------------------------------------------------------------- mul_mat with F16 / F32 src0
 // one wave per dst element (n, m, batch); src0 broadcast over src1's dims 2/3 by ratio (ggml rule)
-template <bool F16>
+template <bool F16, bool ROUND_X = F16>
 __global__ void __launch_bounds__(256) k_mul_mat_f(const char *__restrict__ w, TD tw, const char *__restrict__ x, TD tx,
                                                    char *__restrict__ d, TD td) {
     const int lane = threadIdx.x & 63;
@@ -282,7 +282,7 @@ __global__ void __launch_bounds__(256) k_mul_mat_f(const char *__restrict__ w, T
     for (int64_t k = lane; k < tw.ne[0]; k += 64) {
         float xv = *(const float *)(xr + k * tx.nb[0]);
         float wv;
-        if (F16) { xv = h2f(f2h(xv)); wv = h2f(*(const uint16_t *)(wr + k * tw.nb[0])); }
+        if (F16) { if (ROUND_X) xv = h2f(f2h(xv)); wv = h2f(*(const uint16_t *)(wr + k * tw.nb[0])); }
         else wv = *(const float *)(wr + k * tw.nb[0]);
         acc = fmaf(xv, wv, acc);
     }
@@ -446,7 +446,10 @@ int kcpp_ggml_mul_mat_f(int wtype, const void *w, const kcpp_tdesc *tw, const fl
     if (tx->ne[2] % tw->ne[2] || tx->ne[3] % tw->ne[3] || tx->ne[1] > 65535) return -1;
     const dim3 g((unsigned)((td->ne[0] + 3) / 4), (unsigned)td->ne[1], (unsigned)(tx->ne[2] * tx->ne[3]));
     if (wtype == KT_F16)
-        hipLaunchKernelGGL(k_mul_mat_f<true>, g, dim3(256), 0, (hipStream_t)stream, (const char *)w, td_of(tw),
+        hipLaunchKernelGGL((k_mul_mat_f<true, true>), g, dim3(256), 0, (hipStream_t)stream, (const char *)w, td_of(tw),
+                           (const char *)x, td_of(tx), (char *)d, td_of(td));
+    else if (wtype == KCPP_MM_F16_X32)
+        hipLaunchKernelGGL((k_mul_mat_f<true, false>), g, dim3(256), 0, (hipStream_t)stream, (const char *)w, td_of(tw),
                            (const char *)x, td_of(tx), (char *)d, td_of(td));
     else if (wtype == KT_F32)
         hipLaunchKernelGGL(k_mul_mat_f<false>, g, dim3(256), 0, (hipStream_t)stream, (const char *)w, td_of(tw),

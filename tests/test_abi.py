@@ -12,7 +12,7 @@ LIB = os.path.join(ROOT, "koboldcpp_amd", "koboldcpp_hipblas.so")
 def declared(header):
     txt = open(header).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    names = set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", txt))
+    names = set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\((?!\s*\*)", txt))   # not "type (*member)(...)"
     keywords = {"if", "for", "while", "return", "sizeof", "defined"}
     return {n for n in names if n not in keywords and not n.startswith("__")}
 

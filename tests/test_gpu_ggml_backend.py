@@ -1,0 +1,323 @@
+"""The ggml backend plugin (include/kcpp_ggml_backend.h, csrc/ggml_backend.cpp) driven by the REFERENCE host.
+
+The graphs are built by the reference ggml library itself (oracle/_ref/libggml_ref.so: ggml.c graph builder,
+ggml-alloc.c allocator, ggml-backend.cpp dispatch), allocated by ggml_backend_alloc_ctx_tensors in OUR buffer
+type, filled by ggml_backend_tensor_set, computed by ggml_backend_graph_compute(our backend) and read back by
+ggml_backend_tensor_get -- every call crossing the plugin boundary through the vtables, as llama.cpp would.  The
+same graph computed by the reference CPU backend is the expected result.
+
+Bars: quantized and F16 mat-mul: exact integer dots, fp32 combination order only -> max |d| <= 3e-6 x max |ref|.
+Elementwise / norm / rope ops: 2e-6 relative.  A whole Llama layer (norm, q/k/v, rope, f16 KV-cache stores into
+cache views, masked flash attention over the cache, wo, residual, norm, gate/up/silu, down, residual): 2e-5
+with the strict-parity attention (kcpp_ggml_backend_set_fa_exact), 2e-2 with the production one (the reference
+accumulates attention in f16, ggml.c:15788, this backend in f32)."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import refharness as R
+
+pytestmark = pytest.mark.gpu
+
+REFLIB = os.path.join(R.ROOT, "oracle", "_ref", "libggml_ref.so")
+P, I, I64, F, SZ = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_size_t
+
+
+class InitParams(ctypes.Structure):
+    _fields_ = [("mem_size", SZ), ("mem_buffer", P), ("no_alloc", ctypes.c_bool)]
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+    assert torch.cuda.is_available()
+    if not os.path.exists(REFLIB):
+        pytest.skip("reference ggml build not shipped")
+    import koboldcpp_amd.lib as K
+    G = ctypes.CDLL(REFLIB)
+    sigs = {"ggml_init": ([InitParams], P), "ggml_free": ([P], None),
+            "ggml_new_tensor_1d": ([P, I, I64], P), "ggml_new_tensor_2d": ([P, I, I64, I64], P),
+            "ggml_new_tensor_3d": ([P, I, I64, I64, I64], P),
+            "ggml_mul_mat": ([P, P, P], P), "ggml_rms_norm": ([P, P, F], P), "ggml_mul": ([P, P, P], P),
+            "ggml_add": ([P, P, P], P), "ggml_silu": ([P, P], P), "ggml_scale": ([P, P, F], P),
+            "ggml_get_rows": ([P, P, P], P), "ggml_cpy": ([P, P, P], P),
+            "ggml_soft_max_ext": ([P, P, P, F, F], P),
+            "ggml_rope_ext": ([P, P, P, P, I, I, I, F, F, F, F, F, F], P),
+            "ggml_flash_attn_ext": ([P, P, P, P, P, F, F, F], P),
+            "ggml_view_1d": ([P, P, I64, SZ], P), "ggml_view_3d": ([P, P, I64, I64, I64, SZ, SZ, SZ], P),
+            "ggml_reshape_2d": ([P, P, I64, I64], P), "ggml_reshape_3d": ([P, P, I64, I64, I64], P),
+            "ggml_permute": ([P, P, I, I, I, I], P), "ggml_new_graph": ([P], P),
+            "ggml_build_forward_expand": ([P, P], None), "ggml_graph_compute_with_ctx": ([P, P, I], I),
+            "ggml_get_data": ([P], P), "ggml_nbytes": ([P], SZ), "ggml_row_size": ([I, I64], SZ),
+            "ggml_graph_n_nodes": ([P], I), "ggml_graph_node": ([P, I], P),
+            "ggml_backend_alloc_ctx_tensors": ([P, P], P), "ggml_backend_tensor_set": ([P, P, SZ, SZ], None),
+            "ggml_backend_tensor_get": ([P, P, SZ, SZ], None), "ggml_backend_graph_compute": ([P, P], I),
+            "ggml_backend_buffer_free": ([P], None), "ggml_backend_buft_get_alignment": ([P], SZ),
+            "ggml_backend_buft_get_alloc_size": ([P, P], SZ), "ggml_backend_buft_alloc_buffer": ([P, SZ], P),
+            "ggml_backend_buffer_clear": ([P, ctypes.c_uint8], None), "ggml_backend_buffer_get_base": ([P], P),
+            "ggml_backend_buffer_set_usage": ([P, I], None), "ggml_backend_tensor_alloc": ([P, P, P], None),
+            "ggml_backend_supports_op": ([P, P], ctypes.c_bool), "ggml_backend_name": ([P], ctypes.c_char_p),
+            "ggml_backend_dev_name": ([P], ctypes.c_char_p), "ggml_backend_get_device": ([P], P),
+            "ggml_backend_dev_type": ([P], I), "ggml_backend_free": ([P], None),
+            "ggml_backend_get_default_buffer_type": ([P], P)}
+    for n, (a, r) in sigs.items():
+        fn = getattr(G, n)
+        fn.argtypes, fn.restype = a, r
+    G.ggml_init(InitParams(1 << 20, None, False))      # fp16 tables
+    L = K.raw()
+    L.ggml_backend_cuda_init.argtypes, L.ggml_backend_cuda_init.restype = [I], P
+    L.ggml_backend_cuda_buffer_type.argtypes, L.ggml_backend_cuda_buffer_type.restype = [I], P
+    L.ggml_backend_cuda_reg.restype = P
+    L.kcpp_ggml_backend_last_error.restype = ctypes.c_char_p
+    be = L.ggml_backend_cuda_init(0)
+    assert be
+    yield G, L, be
+    G.ggml_backend_free(be)
+
+
+def run_both(G, be, build, inputs_fn, nthreads=8):
+    """build(ctx) -> (inputs [(tensor, np.ndarray)], out tensor); returns (ours, reference CPU)"""
+    outs = []
+    for on_gpu in (True, False):
+        ctx = G.ggml_init(InitParams(512 << 20, None, on_gpu))
+        ins, out = build(ctx)
+        g = G.ggml_new_graph(ctx)
+        G.ggml_build_forward_expand(g, out)
+        data = inputs_fn()
+        if on_gpu:
+            buf = G.ggml_backend_alloc_ctx_tensors(ctx, be)
+            assert buf
+            for t, arr in zip(ins, data):
+                a = np.ascontiguousarray(arr)
+                assert a.nbytes == G.ggml_nbytes(t)
+                G.ggml_backend_tensor_set(t, a.ctypes.data, 0, a.nbytes)
+            st = G.ggml_backend_graph_compute(be, g)
+            assert st == 0, st
+            res = np.empty(G.ggml_nbytes(out) // 4, np.float32)
+            G.ggml_backend_tensor_get(out, res.ctypes.data, 0, res.nbytes)
+            G.ggml_backend_buffer_free(buf)
+        else:
+            for t, arr in zip(ins, data):
+                a = np.ascontiguousarray(arr)
+                ctypes.memmove(G.ggml_get_data(t), a.ctypes.data, a.nbytes)
+            assert G.ggml_graph_compute_with_ctx(ctx, g, nthreads) == 0
+            res = np.ctypeslib.as_array((ctypes.c_float * (G.ggml_nbytes(out) // 4)).from_address(G.ggml_get_data(out))).copy()
+        G.ggml_free(ctx)
+        outs.append(res)
+    return outs
+
+
+# whole layer vs the reference CPU (relative to max |ref|): strict-parity attention reproduces the reference's
+# f16-accumulating order, leaving only the fp32 combination order of the quantized dots (measured 6.2e-6 max,
+# 3.6e-8 median); the production f32-accumulating attention differs by the reference's own f16 rounding
+# (measured 7.0e-3 max, 1.2e-3 median)
+LAYER_EXACT = 2e-5
+LAYER_PROD = 2e-2
+
+
+def rel(a, b):
+    return float(np.abs(a.astype(np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+
+
+def test_registry_device_and_buffer_rules(env):
+    """ROCm registry / GPU_FULL device through the reference accessors; alignment 128; quantized rows padded to
+    512 elements in get_alloc_size and the pad zeroed by init_tensor (not for compute buffers)
+    (ggml-cuda.cu:443-461, 567-586)"""
+    G, L, be = env
+    assert G.ggml_backend_name(be) == b"ROCm0"
+    dev = G.ggml_backend_get_device(be)
+    assert G.ggml_backend_dev_name(dev) == b"ROCm0" and G.ggml_backend_dev_type(dev) == 3   # GPU_FULL
+    buft = G.ggml_backend_get_default_buffer_type(be)
+    assert buft == L.ggml_backend_cuda_buffer_type(0)
+    assert G.ggml_backend_buft_get_alignment(buft) == 128
+    ctx = G.ggml_init(InitParams(1 << 20, None, True))
+    t = G.ggml_new_tensor_2d(ctx, R.Q4_K, 2304, 3)                # 9 super-blocks per row: 2304 % 512 = 256
+    nb = G.ggml_nbytes(t)
+    assert nb == 3 * 9 * 144
+    assert G.ggml_backend_buft_get_alloc_size(buft, t) == nb + G.ggml_row_size(R.Q4_K, 256)
+    f = G.ggml_new_tensor_2d(ctx, R.F32, 100, 3)
+    assert G.ggml_backend_buft_get_alloc_size(buft, f) == G.ggml_nbytes(f)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [P, P, SZ, I]
+    for usage, zeroed in ((1, True), (2, False)):                 # WEIGHTS, COMPUTE
+        buf = G.ggml_backend_buft_alloc_buffer(buft, 8192)
+        G.ggml_backend_buffer_set_usage(buf, usage)
+        G.ggml_backend_buffer_clear(buf, 0xFF)
+        base = G.ggml_backend_buffer_get_base(buf)
+        t = G.ggml_new_tensor_2d(ctx, R.Q4_K, 2304, 3)            # a fresh tensor: tensor_alloc asserts buffer == NULL
+        G.ggml_backend_tensor_alloc(buf, t, base)
+        host = np.empty(nb + 144, np.uint8)
+        assert hip.hipMemcpy(host.ctypes.data, base, host.nbytes, 2) == 0
+        assert np.all(host[:nb] == 0xFF)
+        assert np.all(host[nb:] == 0) if zeroed else np.all(host[nb:] == 0xFF)
+        G.ggml_backend_buffer_free(buf)
+    G.ggml_free(ctx)
+
+
+MM_CASES = [(R.Q4_K, 4096, 512, 1), (R.Q4_K, 4096, 384, 7), (R.Q4_K, 2048, 256, 40), (R.Q6_K, 4096, 256, 1),
+            (R.Q6_K, 2048, 256, 33), (R.Q5_K, 4096, 256, 1), (R.Q5_K, 2048, 128, 20), (R.Q8_0, 4096, 256, 1),
+            (R.Q8_0, 2048, 256, 24), (R.Q4_0, 4096, 256, 1), (R.Q4_0, 2048, 256, 40), (R.F16, 1024, 96, 5)]
+
+
+@pytest.mark.parametrize("case", MM_CASES, ids=lambda c: "t%d_%dx%d_m%d" % c)
+def test_mul_mat_vs_reference_cpu(env, case):
+    G, L, be = env
+    t, Kd, N, M = case
+    rng = np.random.default_rng(Kd + N + M + t)
+    w = R.synth(t, 5, 100 + t, Kd, N) if t != R.F16 else (rng.standard_normal((N, Kd)) * 0.05).astype(np.float16)
+    x = rng.standard_normal((M, Kd)).astype(np.float32)
+
+    def build(ctx):
+        W = G.ggml_new_tensor_2d(ctx, t, Kd, N)
+        X = G.ggml_new_tensor_2d(ctx, R.F32, Kd, M)
+        return [W, X], G.ggml_mul_mat(ctx, W, X)
+    ours, ref = run_both(G, be, build, lambda: [w, x])
+    assert rel(ours, ref) <= 3e-6, rel(ours, ref)
+    assert L.kcpp_ggml_backend_last_nodes() == 1
+
+
+def test_elementwise_ops_vs_reference_cpu(env):
+    """rms_norm * w + x, silu, scale, soft_max with an f16 mask, rope (NORM, base 500000) on a [128, 8, 6] view"""
+    G, L, be = env
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((6, 1024)).astype(np.float32)
+    w = (1 + 0.1 * rng.standard_normal(1024)).astype(np.float32)
+    msk = np.where(rng.random((6, 1024)) < 0.2, -np.inf, 0).astype(np.float16)
+    pos = np.arange(6, dtype=np.int32) * 37
+
+    def build(ctx):
+        X = G.ggml_new_tensor_2d(ctx, R.F32, 1024, 6)
+        Wt = G.ggml_new_tensor_1d(ctx, R.F32, 1024)
+        Mk = G.ggml_new_tensor_2d(ctx, R.F16, 1024, 6)
+        Pz = G.ggml_new_tensor_1d(ctx, 26, 6)                     # I32
+        h = G.ggml_add(ctx, G.ggml_mul(ctx, G.ggml_rms_norm(ctx, X, 1e-5), Wt), X)
+        h = G.ggml_scale(ctx, G.ggml_silu(ctx, h), 0.5)
+        h = G.ggml_soft_max_ext(ctx, h, Mk, 0.125, 0.0)
+        r = G.ggml_rope_ext(ctx, G.ggml_reshape_3d(ctx, X, 128, 8, 6), Pz, None, 128, 0, 4096, 500000.0, 1.0, 0.0,
+                            1.0, 32.0, 1.0)
+        out = G.ggml_add(ctx, G.ggml_reshape_2d(ctx, r, 1024, 6), h)
+        return [X, Wt, Mk, Pz], out
+    ours, ref = run_both(G, be, build, lambda: [x, w, msk, pos])
+    assert rel(ours, ref) <= 2e-6, rel(ours, ref)
+
+
+@pytest.mark.parametrize("t", [R.Q4_K, R.Q6_K, R.Q8_0, R.Q4_0, R.F16])
+def test_get_rows_vs_reference_cpu(env, t):
+    """token embedding gather (get_rows of a quantized or f16 table): dequantization is exact on both sides"""
+    G, L, be = env
+    Kd, N = 2048, 50
+    rng = np.random.default_rng(t)
+    tab = R.synth(t, 4, 40 + t, Kd, N) if t != R.F16 else rng.standard_normal((N, Kd)).astype(np.float16)
+    ids = rng.integers(0, N, size=9).astype(np.int32)
+
+    def build(ctx):
+        Tb = G.ggml_new_tensor_2d(ctx, t, Kd, N)
+        Ix = G.ggml_new_tensor_1d(ctx, 26, 9)
+        return [Tb, Ix], G.ggml_get_rows(ctx, Tb, Ix)
+    ours, ref = run_both(G, be, build, lambda: [tab, ids])
+    assert np.array_equal(ours.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("exact", [True, False], ids=["fa_exact", "production"])
+def test_llama_layer_vs_reference_cpu(env, exact):
+    """one build_llama layer (src/llama.cpp:10453-10620) at n_embd 1024, 8/2 heads x 128, n_ff 2816, Q4_K_M-like
+    weights, 5 new tokens after 37 cached positions"""
+    G, L, be = env
+    E, H, HKV, D, Fd, n_ctx, n_past, T = 1024, 8, 2, 128, 2816, 64, 37, 5
+    EKV = HKV * D
+    n_kv = n_past + T
+    rng = np.random.default_rng(11)
+    tys = [R.Q4_K, R.Q4_K, R.Q6_K, R.Q4_K, R.Q4_K, R.Q4_K, R.Q6_K]
+    shapes = [(E, E), (E, EKV), (E, EKV), (E, E), (E, Fd), (E, Fd), (Fd, E)]
+    ws = [R.synth(t, 9, 300 + i, k, n) for i, (t, (k, n)) in enumerate(zip(tys, shapes))]
+    nw1 = (1 + 0.05 * rng.standard_normal(E)).astype(np.float32)
+    nw2 = (1 + 0.05 * rng.standard_normal(E)).astype(np.float32)
+    x = rng.standard_normal((T, E)).astype(np.float32)
+    kc = (rng.standard_normal((n_ctx, EKV)) * 0.5).astype(np.float16)
+    vc = rng.standard_normal((n_ctx, EKV)).astype(np.float16)
+    pos = np.arange(n_past, n_past + T, dtype=np.int32)
+    T_pad = 32
+    mask = np.full((T_pad, n_kv), -np.inf, np.float16)
+    for t in range(T):
+        mask[t, :n_past + t + 1] = 0
+
+    def build(ctx):
+        W = [G.ggml_new_tensor_2d(ctx, t, k, n) for t, (k, n) in zip(tys, shapes)]
+        N1, N2 = G.ggml_new_tensor_1d(ctx, R.F32, E), G.ggml_new_tensor_1d(ctx, R.F32, E)
+        X = G.ggml_new_tensor_2d(ctx, R.F32, E, T)
+        KC, VC = G.ggml_new_tensor_1d(ctx, R.F16, n_ctx * EKV), G.ggml_new_tensor_1d(ctx, R.F16, n_ctx * EKV)
+        Pz = G.ggml_new_tensor_1d(ctx, 26, T)
+        Mk = G.ggml_new_tensor_2d(ctx, R.F16, n_kv, T_pad)
+        cur = G.ggml_mul(ctx, G.ggml_rms_norm(ctx, X, 1e-5), N1)
+        q = G.ggml_rope_ext(ctx, G.ggml_reshape_3d(ctx, G.ggml_mul_mat(ctx, W[0], cur), D, H, T), Pz, None, D, 0, n_ctx,
+                            500000.0, 1.0, 0.0, 1.0, 32.0, 1.0)
+        k = G.ggml_rope_ext(ctx, G.ggml_reshape_3d(ctx, G.ggml_mul_mat(ctx, W[1], cur), D, HKV, T), Pz, None, D, 0, n_ctx,
+                            500000.0, 1.0, 0.0, 1.0, 32.0, 1.0)
+        v = G.ggml_mul_mat(ctx, W[2], cur)
+        kv = G.ggml_view_1d(ctx, KC, T * EKV, n_past * EKV * 2)
+        vv = G.ggml_view_1d(ctx, VC, T * EKV, n_past * EKV * 2)
+        st_k = G.ggml_cpy(ctx, k, kv)
+        st_v = G.ggml_cpy(ctx, v, vv)
+        kview = G.ggml_view_3d(ctx, KC, D, n_kv, HKV, EKV * 2, D * 2, 0)
+        vview = G.ggml_view_3d(ctx, VC, D, n_kv, HKV, EKV * 2, D * 2, 0)
+        fa = G.ggml_flash_attn_ext(ctx, G.ggml_permute(ctx, q, 0, 2, 1, 3), kview, vview, Mk, 1.0 / np.sqrt(D), 0.0, 0.0)
+        att = G.ggml_mul_mat(ctx, W[3], G.ggml_reshape_2d(ctx, fa, E, T))
+        ffn_in = G.ggml_add(ctx, att, X)
+        h = G.ggml_mul(ctx, G.ggml_rms_norm(ctx, ffn_in, 1e-5), N2)
+        h = G.ggml_mul(ctx, G.ggml_silu(ctx, G.ggml_mul_mat(ctx, W[4], h)), G.ggml_mul_mat(ctx, W[5], h))
+        out = G.ggml_add(ctx, G.ggml_mul_mat(ctx, W[6], h), ffn_in)
+        # the cache stores must precede attention (llm_build_kv: ggml_build_forward_expand of the cpy nodes first)
+        build.pre = [st_k, st_v]
+        return W + [N1, N2, X, KC, VC, Pz, Mk], out
+
+    def inputs():
+        return ws + [nw1, nw2, x, kc, vc, pos, mask]
+
+    L.kcpp_ggml_backend_set_fa_exact(ctypes.c_void_p(be), int(exact))
+    outs = []
+    for on_gpu in (True, False):
+        ctx = G.ggml_init(InitParams(256 << 20, None, on_gpu))
+        ins, out = build(ctx)
+        g = G.ggml_new_graph(ctx)
+        for p_ in build.pre:
+            G.ggml_build_forward_expand(g, p_)
+        G.ggml_build_forward_expand(g, out)
+        if on_gpu:
+            for i in range(G.ggml_graph_n_nodes(g)):
+                assert G.ggml_backend_supports_op(be, G.ggml_graph_node(g, i))
+            buf = G.ggml_backend_alloc_ctx_tensors(ctx, be)
+            for t, a in zip(ins, inputs()):
+                a = np.ascontiguousarray(a)
+                G.ggml_backend_tensor_set(t, a.ctypes.data, 0, a.nbytes)
+            assert G.ggml_backend_graph_compute(be, g) == 0, L.kcpp_ggml_backend_last_error()
+            res = np.empty(T * E, np.float32)
+            G.ggml_backend_tensor_get(out, res.ctypes.data, 0, res.nbytes)
+            G.ggml_backend_buffer_free(buf)
+        else:
+            for t, a in zip(ins, inputs()):
+                a = np.ascontiguousarray(a)
+                ctypes.memmove(G.ggml_get_data(t), a.ctypes.data, a.nbytes)
+            assert G.ggml_graph_compute_with_ctx(ctx, g, 8) == 0
+            res = np.ctypeslib.as_array((ctypes.c_float * (T * E)).from_address(G.ggml_get_data(out))).copy()
+        G.ggml_free(ctx)
+        outs.append(res)
+    L.kcpp_ggml_backend_set_fa_exact(ctypes.c_void_p(be), 0)
+    e = rel(outs[0], outs[1])
+    med = float(np.median(np.abs(outs[0] - outs[1])) / np.abs(outs[1]).max())
+    print("layer exact=%d rel err max %.3g median %.3g" % (exact, e, med))
+    assert e <= (LAYER_EXACT if exact else LAYER_PROD), e
+
+
+def test_unsupported_ops_are_refused(env):
+    """placement: supports_op is false where this backend has no kernel (ggml-cuda.cu:2959-3185 decides placement;
+    ggml_backend_sched then keeps such nodes on the CPU backend)"""
+    G, L, be = env
+    ctx = G.ggml_init(InitParams(1 << 20, None, True))
+    w = G.ggml_new_tensor_2d(ctx, 3, 256, 4)                      # GGML_TYPE_Q4_1: no kernel here
+    x = G.ggml_new_tensor_2d(ctx, R.F32, 256, 2)
+    assert not G.ggml_backend_supports_op(be, G.ggml_mul_mat(ctx, w, x))
+    w2 = G.ggml_new_tensor_2d(ctx, R.Q4_K, 256, 4)
+    assert G.ggml_backend_supports_op(be, G.ggml_mul_mat(ctx, w2, x))
+    G.ggml_free(ctx)
