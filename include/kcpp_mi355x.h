@@ -157,7 +157,7 @@ int kcpp_moe_combine(float *x, const float *slots, int64_t slot_stride, int k, i
 int kcpp_add(float *y, const float *a, const float *b, int64_t n, void *stream);
 int kcpp_silu_mul(float *y, const float *g, const float *u, int64_t n, void *stream);
 
-/* ---------- 1b. general-layout ggml node kernels (the b1 backend, csrc/ggml_backend_kcpp.cpp) ----------
+/* ---------- 1b. general-layout ggml node kernels (the b1 backend, csrc/ggml_backend.cpp) ----------
  * A tensor is described by its ggml shape and byte strides (ggml_tensor.ne / .nb); data pointers are
  * device pointers.  Each entry follows the reference CPU op named in csrc/ggml_ops.hip. */
 typedef struct kcpp_tdesc {
@@ -229,6 +229,10 @@ void kcpp_model_free(kcpp_model *m);
  * must have been placed with kcpp_model_hidden_in.  If the stage has the output head, the last
  * token's logits are copied to logits_host (may be NULL). */
 int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, int n_past, float *logits_host);
+/* the same, enqueued on the stage's stream without any host synchronisation (pipeline driver: stages chained by
+ * events / RCCL, one host sync per step) */
+int kcpp_model_decode_async(kcpp_model *m, const int32_t *tokens, int T, int n_past);
+int kcpp_model_device(kcpp_model *m);
 /* device pointers of this stage's residual stream [max_ubatch][n_embd] f32 (pipeline handoff) */
 float *kcpp_model_hidden(kcpp_model *m);
 /* copy n floats of the residual stream starting at float offset (debug / pipeline host path) */

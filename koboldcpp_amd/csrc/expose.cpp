@@ -14,6 +14,7 @@
 // DRY, rep_pen, top-k/a/p, min-p, tfs, typical, temperature / dynatemp / smoothing, mirostat, XTC) over
 // the user's sampler_order and a seeded mt19937; when that chain reduces to argmax (greedy, no biases /
 // penalties / bans) the token comes from the on-device argmax instead of a logits copy.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -38,6 +39,34 @@
 
 namespace {
 
+// RCCL (librccl, loaded at run time so a one-GPU deployment does not need it): the entry points the stage
+// handoff uses, with ncclComm_t / ncclDataType_t / ncclResult_t as their ABI types (rccl.h)
+struct Rccl {
+    typedef int (*InitAllFn)(void **comms, int ndev, const int *devlist);
+    typedef int (*SendFn)(const void *buf, size_t count, int dtype, int peer, void *comm, hipStream_t stream);
+    typedef int (*RecvFn)(void *buf, size_t count, int dtype, int peer, void *comm, hipStream_t stream);
+    typedef int (*GroupFn)(void);
+    typedef int (*DestroyFn)(void *comm);
+    InitAllFn init_all = nullptr;
+    SendFn send = nullptr;
+    RecvFn recv = nullptr;
+    GroupFn group_start = nullptr, group_end = nullptr;
+    DestroyFn destroy = nullptr;
+    bool load() {
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return false;
+        init_all = (InitAllFn)dlsym(h, "ncclCommInitAll");
+        send = (SendFn)dlsym(h, "ncclSend");
+        recv = (RecvFn)dlsym(h, "ncclRecv");
+        group_start = (GroupFn)dlsym(h, "ncclGroupStart");
+        group_end = (GroupFn)dlsym(h, "ncclGroupEnd");
+        destroy = (DestroyFn)dlsym(h, "ncclCommDestroy");
+        return init_all && send && recv && group_start && group_end && destroy;
+    }
+};
+constexpr int kNcclFloat32 = 7;   // ncclFloat32 (rccl.h)
+
 struct Engine {
     gguf::File file;
     Tokenizer tok;
@@ -45,11 +74,26 @@ struct Engine {
     std::vector<int> types;
     std::vector<kcpp_model *> stages;
     std::vector<float *> hidden;            // per stage residual stream (device)
+    std::vector<int> devs;                  // per stage device
+    // stage handoff (replaces ggml_backend_sched_compute_splits' per-split input copies and events,
+    // ggml-backend.cpp:2108-2201): RCCL send/recv between the stage streams when every stage has its own GPU,
+    // otherwise a device copy ordered by events; never a host synchronisation between stages
+    Rccl rccl;
+    std::vector<void *> comms;              // rank s = stage s
+    std::vector<hipEvent_t> ev_done, ev_read;
     int ub = 512;
     bool use_contextshift = false;
     std::vector<int> ctx;                   // tokens whose K/V are in the caches
     std::vector<float> logits;
-    ~Engine() { for (auto *m : stages) kcpp_model_free(m); }
+    ~Engine() {
+        for (size_t s = 0; s < stages.size(); ++s) {
+            hipSetDevice(devs[s]);
+            if (s < ev_done.size() && ev_done[s]) hipEventDestroy(ev_done[s]);
+            if (s < ev_read.size() && ev_read[s]) hipEventDestroy(ev_read[s]);
+        }
+        for (void *c : comms) if (c && rccl.destroy) rccl.destroy(c);
+        for (auto *m : stages) kcpp_model_free(m);
+    }
 };
 
 std::unique_ptr<Engine> g_eng;
@@ -90,20 +134,70 @@ std::vector<int> split_layers(int n_layer, int n_dev, const float *ts) {
     return dev;   // dev[n_layer] = output head's device
 }
 
-// run tokens [i0, i0+T) through all stages (ubatch granularity); last stage leaves logits on device
+// stage s-1's residual stream (t tokens) -> stage s's input, on the two stages' streams
+int handoff(Engine &e, size_t s, int t) {
+    const size_t count = (size_t)t * e.hp.n_embd;
+    hipStream_t src = (hipStream_t)kcpp_model_stream(e.stages[s - 1]), dst = (hipStream_t)kcpp_model_stream(e.stages[s]);
+    if (!e.comms.empty()) {
+        if (e.rccl.group_start()) return -20;
+        const int r1 = e.rccl.send(e.hidden[s - 1], count, kNcclFloat32, (int)s, e.comms[s - 1], src);
+        const int r2 = e.rccl.recv(e.hidden[s], count, kNcclFloat32, (int)s - 1, e.comms[s], dst);
+        if (e.rccl.group_end() || r1 || r2) return -21;
+        return 0;
+    }
+    // dst waits for the producer, copies, and the producer's next write waits for the copy to have read
+    if (hipSetDevice(e.devs[s - 1]) || hipEventRecord(e.ev_done[s - 1], src)) return -22;
+    if (hipSetDevice(e.devs[s]) || hipStreamWaitEvent(dst, e.ev_done[s - 1], 0)) return -22;
+    const hipError_t ce = e.devs[s] == e.devs[s - 1]
+                              ? hipMemcpyAsync(e.hidden[s], e.hidden[s - 1], count * 4, hipMemcpyDeviceToDevice, dst)
+                              : hipMemcpyPeerAsync(e.hidden[s], e.devs[s], e.hidden[s - 1], e.devs[s - 1], count * 4, dst);
+    if (ce != hipSuccess || hipEventRecord(e.ev_read[s], dst)) return -23;
+    if (hipSetDevice(e.devs[s - 1]) || hipStreamWaitEvent(src, e.ev_read[s], 0)) return -22;
+    return 0;
+}
+
+// run tokens [i0, i0+T) through all stages, ubatch by ubatch, everything enqueued: stage s works on ubatch u while
+// stage s+1 works on ubatch u-1 (the pipeline the reference gets from n_copies = 4, ggml-backend.cpp:1372); the
+// caller's logits read on the last stage is the only host synchronisation
 int forward(Engine &e, const int32_t *toks, int T, int n_past) {
     for (int i = 0; i < T; i += e.ub) {
         const int t = std::min(e.ub, T - i);
         for (size_t s = 0; s < e.stages.size(); ++s) {
             if (s > 0) {
-                const int rc = kcpp_model_hidden_io(e.stages[s], e.hidden[s - 1], (int64_t)t * e.hp.n_embd, 0, 0);
+                const int rc = handoff(e, s, t);
                 if (rc) return rc;
             }
-            const int rc = kcpp_model_decode(e.stages[s], s == 0 ? toks + i : nullptr, t, n_past + i, nullptr);
+            const int rc = kcpp_model_decode_async(e.stages[s], s == 0 ? toks + i : nullptr, t, n_past + i);
             if (rc) return rc;
         }
     }
     return 0;
+}
+
+// events for the copy handoff, and an RCCL clique when every stage sits on its own device (RCCL refuses two
+// ranks on one GPU); KCPP_HANDOFF=copy forces the event-ordered copies
+bool init_handoff(Engine &e) {
+    const size_t S = e.stages.size();
+    e.ev_done.assign(S, nullptr);
+    e.ev_read.assign(S, nullptr);
+    for (size_t s = 0; s < S; ++s) {
+        hipSetDevice(e.devs[s]);
+        if (hipEventCreateWithFlags(&e.ev_done[s], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.ev_read[s], hipEventDisableTiming) != hipSuccess)
+            return false;
+    }
+    if (S < 2) return true;
+    std::vector<int> sorted = e.devs;
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    const char *mode = getenv("KCPP_HANDOFF");
+    if (!distinct || (mode && !strcmp(mode, "copy")) || !e.rccl.load()) return true;
+    e.comms.assign(S, nullptr);
+    if (e.rccl.init_all(e.comms.data(), (int)S, e.devs.data()) != 0) {
+        fprintf(stderr, "[kcpp] load_model: ncclCommInitAll failed, stage handoff by peer copies\n");
+        e.comms.clear();
+    }
+    return true;
 }
 
 // per-generate sampler state: the reference's parameter clamps (gpttype_adapter.cpp:2576-2584, 2625-2735),
@@ -401,31 +495,39 @@ bool load_model(const load_model_inputs inputs) {
     }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) { fprintf(stderr, "[kcpp] load_model: no GPU\n"); return false; }
+    // test hook: KCPP_VIRTUAL_DEVICES=n splits the layers as if n GPUs were visible, stage i on GPU i % ndev
+    const int nreal = ndev;
+    if (getenv("KCPP_VIRTUAL_DEVICES")) ndev = std::max(1, atoi(getenv("KCPP_VIRTUAL_DEVICES")));
     const std::vector<int> ldev = split_layers(hp.n_layer, std::min(ndev, KCPP_TENSOR_SPLIT_MAX), inputs.tensor_split);
     e->ub = inputs.blasbatchsize > 0 ? std::min(inputs.blasbatchsize, 512) : 512;
     e->use_contextshift = inputs.use_contextshift;
     int il = 0;
-    while (il < hp.n_layer || e->stages.empty()) {
-        const int d = il < hp.n_layer ? ldev[il] : ldev[hp.n_layer];
-        int il1 = il;
-        while (il1 < hp.n_layer && ldev[il1] == d) ++il1;
-        const bool last = il1 == hp.n_layer;
-        if (last && ldev[hp.n_layer] != d) {
-            fprintf(stderr, "[kcpp] load_model: output head must share the last layers' device\n");
-            return false;
-        }
-        kcpp_model *m = kcpp_model_create(&hp, e->types.data(), d, il, il1, e->stages.empty(), last, e->ub);
+    // stages of consecutive layers per device; the output head on its own device (upper_bound of
+    // (act - 1) / act, src/llama.cpp:7030-7033) -- a head-only stage when that is not the last layers' device
+    auto add_stage = [&](int d, int i0, int i1, bool out) {
+        const int gpu = d % nreal;
+        kcpp_model *m = kcpp_model_create(&hp, e->types.data(), gpu, i0, i1, e->stages.empty(), out, e->ub);
         if (!m) { fprintf(stderr, "[kcpp] load_model: %s\n", kcpp_last_error()); return false; }
         e->stages.push_back(m);
         e->hidden.push_back(kcpp_model_hidden(m));
-        if (e->stages.size() > 1) {
-            hipSetDevice(d);
-            hipDeviceEnablePeerAccess(ldev[std::max(0, il - 1)], 0);   // xGMI peer copies for the handoff
+        e->devs.push_back(gpu);
+        if (e->stages.size() > 1 && e->devs[e->devs.size() - 2] != gpu) {
+            hipSetDevice(gpu);
+            hipDeviceEnablePeerAccess(e->devs[e->devs.size() - 2], 0);   // xGMI peer copies for the handoff
             (void)hipGetLastError();
         }
+        return true;
+    };
+    while (il < hp.n_layer) {
+        const int d = ldev[il];
+        int il1 = il;
+        while (il1 < hp.n_layer && ldev[il1] == d) ++il1;
+        const bool last = il1 == hp.n_layer;
+        if (!add_stage(d, il, il1, last && ldev[hp.n_layer] == d)) return false;
+        if (last && ldev[hp.n_layer] != d && !add_stage(ldev[hp.n_layer], hp.n_layer, hp.n_layer, true)) return false;
         il = il1;
-        if (last) break;
     }
+    if (!init_handoff(*e)) { fprintf(stderr, "[kcpp] load_model: handoff events\n"); return false; }
     for (size_t k = 0; k < ts.size(); ++k) {
         for (kcpp_model *m : e->stages)
             if (kcpp_model_set_tensor(m, (int)k, ts[k].data, ts[k].bytes)) {

@@ -1,5 +1,5 @@
 // ggml_ops.hip -- general-layout (ne/nb strided) kernels for the ggml graph nodes the b1 backend
-// (ggml_backend_kcpp.cpp) executes outside the fused Llama runtime.  Each follows the CPU op of the
+// (csrc/ggml_backend.cpp) executes outside the fused Llama runtime.  Each follows the CPU op of the
 // reference (ggml/src/ggml.c) it replaces:
 //   binary add/sub/mul/div  ggml_compute_forward_add/mul/div_f32 (src1 broadcast by modulo)
 //   unary silu              ggml_vec_silu_f32 (x / (1 + exp(-x)))

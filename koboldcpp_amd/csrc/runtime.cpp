@@ -842,8 +842,9 @@ extern "C" int kcpp_model_forward_hidden(kcpp_model *m, int T, int n_past) {
     return forward_layers(m, T, n_past, false);
 }
 
-extern "C" int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, int n_past, float *logits_host) {
-    RT_CHECK(hipSetDevice(m->device));
+// enqueue one llama_decode of T tokens on the stage's stream (no host synchronisation): the pipeline driver
+// (expose.cpp) chains stages with events / RCCL and synchronises once per step
+static int decode_enqueue(kcpp_model *m, const int32_t *tokens, int T, int n_past) {
     const kcpp_hparams &hp = m->hp;
     if (T < 1 || n_past + T > hp.n_ctx) { g_err = "context overflow"; return -2; }
     if (m->has_embed && !tokens) { g_err = "decode: stage owns the embedding but tokens == NULL"; return -2; }
@@ -872,12 +873,24 @@ extern "C" int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, in
             if (m->has_output && i + t == T) RC(head(m, t));
         }
     }
+    return 0;
+}
+
+extern "C" int kcpp_model_decode_async(kcpp_model *m, const int32_t *tokens, int T, int n_past) {
+    RT_CHECK(hipSetDevice(m->device));
+    return decode_enqueue(m, tokens, T, n_past);
+}
+
+extern "C" int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, int n_past, float *logits_host) {
+    RT_CHECK(hipSetDevice(m->device));
+    RC(decode_enqueue(m, tokens, T, n_past));
     if (m->has_output && logits_host) {
-        RT_CHECK(hipMemcpyAsync(logits_host, m->logits, (size_t)hp.n_vocab * 4, hipMemcpyDeviceToHost, m->stream));
+        RT_CHECK(hipMemcpyAsync(logits_host, m->logits, (size_t)m->hp.n_vocab * 4, hipMemcpyDeviceToHost, m->stream));
     }
     RT_CHECK(hipStreamSynchronize(m->stream));
     return 0;
 }
+extern "C" int kcpp_model_device(kcpp_model *m) { return m->device; }
 
 // greedy argmax over the logits (first index wins ties, like the CPU sampler's top-1):
 // stage 1, ARGMAX_BLOCKS workgroups reduce strided slices to (value, index) pairs; stage 2, one

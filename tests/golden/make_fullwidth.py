@@ -73,6 +73,17 @@ def main():
     out["full_layer0_hidden_max"], out["full_layer0_hidden_median"] = dh.max(), np.median(dh)
     out["full_layer_logits_max"], out["full_layer_logits_median"] = spread(a2, b2)
     print("layer0 hidden spread max", dh.max(), "median", np.median(dh))
+    # ---- Llama-3-70B width (BASELINE config 4), one layer + head: the spread at that width, and the reference's
+    # greedy tokens for the 9-token prompt tests/test_gpu_config4.py teacher-forces
+    hp70 = dict(n_vocab=128256, n_embd=8192, n_head=64, n_head_kv=8, n_layer=1, n_ff=28672, n_ctx=64, eps=1e-5,
+                rope_base=500000.0)
+    p70 = [int(v) for v in np.random.default_rng(71).integers(1, hp70["n_vocab"], size=9)]
+    a70, _ = R.run_ref_llama(hp70, R.q4_k_m_types(1), SEED, p70, 2, nthreads=NTH)
+    f70 = np.argmax(a70, axis=1)[:-1].astype(np.int32)
+    b70, _ = R.run_ref_llama(hp70, R.q4_k_m_types(1), SEED, p70, 2, forced=f70, nthreads=NTH, binary=R.REF_BIN_SCALAR)
+    out["l70_max"], out["l70_median"] = spread(a70, b70)
+    out["l70_prompt"], out["l70_forced"] = np.array(p70, np.int32), f70
+    print("70B-width 1-layer spread max", out["l70_max"], "median", out["l70_median"])
     np.savez_compressed(os.path.join(HERE, "e2e_full.npz"), **full)
     np.savez_compressed(os.path.join(HERE, "ref_spread.npz"), **out)
     print("wrote e2e_full.npz, ref_spread.npz")

@@ -211,3 +211,53 @@ def test_long_context_decode_matches_short_context():
         outs.append(lg)
         m.close()
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def test_generate_layer_split_pipeline_matches_single_stage(model, tmp_path, monkeypatch):
+    """--tensorsplit through load_model: 3 stages (KCPP_VIRTUAL_DEVICES=3 puts them all on the one GPU of the
+    test box), prefill in 16-token ubatches pipelined across the stages, the residual stream handed stage to stage
+    on the stage streams with event ordering and no host synchronisation (RCCL send/recv when the stages sit on
+    distinct GPUs) -- greedy text equal to a single in-process stage with the same ubatch size.  Runs last: it
+    replaces the module's loaded model."""
+    import koboldcpp_amd.lib as K
+    h, X, _, _, _ = model
+    hp = dict(R.TINY, n_layer=5, n_ctx=256)
+    types = R.q4_k_m_types(hp["n_layer"])
+    path = str(tmp_path / "split.gguf")
+    toks = GW.llama_gguf(path, hp, types, 1234, WORDS)
+    monkeypatch.setenv("KCPP_VIRTUAL_DEVICES", "3")
+    li = X.load_model_inputs()
+    li.model_filename = path.encode()
+    li.max_context_length = 248
+    li.blasbatchsize = 16
+    li.gpulayers = 999
+    li.rope_freq_base = 10000.0
+    li.rope_freq_scale = 1.0
+    for i, v in enumerate((1.0, 2.0, 1.0)):
+        li.tensor_split[i] = v
+    assert h.load_model(li)
+    _, _, ttypes = GW.spm_vocab(hp["n_vocab"], WORDS)
+    prompt = b" ".join([b"hello world the a b of to"] * 6)
+    r = h.token_count(prompt, True)
+    ids = [r.ids[i] for i in range(r.count)]
+    assert len(ids) > 32                                       # at least three ubatches of 16
+    gi = X.generation_inputs()
+    gi.prompt = prompt
+    gi.max_context_length = 248
+    gi.max_length = 10
+    gi.temperature = 0.0
+    gi.top_k = 1
+    gi.rep_pen = 1.0
+    gi.bypass_eos_token = True
+    out = h.generate(gi)
+    assert out.status == 1
+    m = K.Model(hp, types, max_ubatch=16)
+    m.synth(1234)
+    m.decode(ids, 0, want_logits=False)
+    want = [m.argmax()]
+    n = len(ids)
+    for _ in range(9):
+        want.append(m.decode_greedy(n))
+        n += 1
+    m.close()
+    assert out.text == b"".join(piece(toks, ttypes, t) for t in want)
