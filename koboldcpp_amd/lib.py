@@ -72,6 +72,8 @@ _SIGS = {
     "kcpp_model_set_tensor": [P, I, P, I64],
     "kcpp_model_free": [P],
     "kcpp_model_decode": [P, P, I, I, P],
+    "kcpp_model_decode_async": [P, P, I, I],
+    "kcpp_model_device": [P],
     "kcpp_model_hidden": [P],
     "kcpp_model_read_hidden": [P, P, I64, I64],
     "kcpp_model_stream": [P],
@@ -231,6 +233,18 @@ class Model:
         _chk(_L.kcpp_model_decode(self.m, tok.ctypes.data_as(P) if tok is not None else None, T, n_past,
                                   logits.ctypes.data_as(P) if want_logits else None), "decode")
         return logits
+
+    def decode_async(self, tokens, n_past, n_tokens=None):
+        """enqueue the decode on the stage stream without a host sync (prefill ubatches of a pipeline); the
+        token array is copied before this returns"""
+        import numpy as np
+        if tokens is None:
+            tok, T = None, int(n_tokens)
+        else:
+            tok = np.ascontiguousarray(tokens, dtype=np.int32)
+            T = len(tok)
+        _chk(_L.kcpp_model_decode_async(self.m, tok.ctypes.data_as(P) if tok is not None else None, T, n_past),
+             "decode_async")
 
     def argmax(self):
         v = ctypes.c_int32(0)

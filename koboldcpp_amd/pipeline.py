@@ -78,7 +78,15 @@ class HipStage:
             self.m.synth(seed)
 
     def run(self, tokens, T, n_past):
-        self.m.decode(tokens if self.first else None, n_past, want_logits=False, n_tokens=T)
+        """enqueue the stage's layers for T tokens.  Prefill ubatches (T > 1, n_past passed by value) are only
+        enqueued, so a rank works on ubatch u + 1 while the next rank works on u; single-token steps read their
+        position from the stage's pinned word inside the replayed graph and stay synchronous, so the host can
+        never rewrite that word under a pending replay"""
+        tok = tokens if self.first else None
+        if T > 1:
+            self.m.decode_async(tok, n_past, n_tokens=T)
+        else:
+            self.m.decode(tok, n_past, want_logits=False, n_tokens=T)
 
     def argmax(self):
         return self.m.argmax()
