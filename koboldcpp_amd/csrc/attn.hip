@@ -628,11 +628,16 @@ __global__ void __launch_bounds__(1024) k_fa_combine(const float *__restrict__ p
 // S columns tx + 16*j (j<4) and O dims tx*8 .. tx*8+7 (8 dims).
 #define FP_BQ 64
 #define FP_BK 64
+// D = 128 or 64 (TinyLlama-class heads): thread tx owns DPT = D / 16 output dims; n_past from n_past_dev when given
+// (single-token decode replayed from a graph)
 template <int D>
 __global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
                                                     const uint16_t *__restrict__ vc, float *__restrict__ out, int T,
-                                                    int H, int HKV, int n_past, float scale,
-                                                    const uint16_t *__restrict__ mask, int64_t mask_ld, int n_kv) {
+                                                    int H, int HKV, int n_past_arg, float scale,
+                                                    const uint16_t *__restrict__ mask, int64_t mask_ld, int n_kv,
+                                                    const int32_t *__restrict__ n_past_dev) {
+    constexpr int DPT = D / 16;
+    const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
     const int qt = blockIdx.x, h = blockIdx.y;
     const int G = H / HKV, hk = h / G;
     const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
@@ -645,12 +650,12 @@ __global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__
         const int r = i / D, d = i % D;
         sQ[r][d] = (q0 + r < T) ? h2f(q16[((int64_t)(q0 + r) * H + h) * D + d]) : 0.0f;
     }
-    float m[4], l[4], o[4][8];
+    float m[4], l[4], o[4][DPT];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
         m[r] = -INFINITY; l[r] = 0.0f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[r][j] = 0.0f;
+        for (int j = 0; j < DPT; ++j) o[r][j] = 0.0f;
     }
     const int last_q = min(q0 + FP_BQ, T) - 1;
     const bool expl = mask_ld >= 0;                       // explicit ggml mask form (mask may be null)
@@ -726,21 +731,21 @@ __global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__
             l[r] = l[r] * alpha + ls;
             m[r] = mnew;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[r][j] *= alpha;
+            for (int j = 0; j < DPT; ++j) o[r][j] *= alpha;
         }
         // O += P V : P row r lives across the 16 tx-threads of the group (4 cols each)
         for (int src = 0; src < 16; ++src) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int kr = src + 16 * j;
-                float vr[8];
+                float vr[DPT];
 #pragma unroll
-                for (int e = 0; e < 8; ++e) vr[e] = sV[kr][tx * 8 + e];
+                for (int e = 0; e < DPT; ++e) vr[e] = sV[kr][tx * DPT + e];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const float pr = __shfl(s[r][j], ((16 * ty) & 63) + src, 64);
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) o[r][e] = fmaf(pr, vr[e], o[r][e]);
+                    for (int e = 0; e < DPT; ++e) o[r][e] = fmaf(pr, vr[e], o[r][e]);
                 }
             }
         }
@@ -751,7 +756,7 @@ __global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__
         if (qi < T) {
             const float inv = 1.0f / l[r];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) out[((int64_t)qi * H + h) * D + tx * 8 + e] = o[r][e] * inv;
+            for (int e = 0; e < DPT; ++e) out[((int64_t)qi * H + h) * D + tx * DPT + e] = o[r][e] * inv;
         }
     }
 }
@@ -774,7 +779,16 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
                     int T, int H, int HKV, int D, int n_past, const int32_t *n_past_dev, int n_kv_max, float scale,
                     int force_path, void *stream) {
     hipStream_t s = (hipStream_t)stream;
-    if (D != 128 || H % HKV || H / HKV > FA_MAXG || (H % 2)) return -1;
+    if ((D != 128 && D != 64) || H % HKV || (H % 2)) return -1;
+    if (D == 64) {       // 64-dim heads (TinyLlama class): the tiled kernel for decode and prefill alike
+        if (!out) return -2;
+        hipLaunchKernelGGL(k_fa_prefill<64>, dim3((T + FP_BQ - 1) / FP_BQ, H), dim3(256), 0, s, q16, kc, vc, out, T, H,
+                           HKV, n_past, scale, nullptr, -1, 0, n_past_dev);
+        KCPP_CHECK(hipGetLastError());
+        if (qout) return kcpp_quantize_act(KT_Q8_K, out, (int64_t)H * D, qout, (int64_t)H * D, T, stream);
+        return 0;
+    }
+    if (H / HKV > FA_MAXG) return -1;
     const bool use_decode = force_path == 1 || force_path == 4 || force_path == 5 || (force_path == 0 && T <= 16);
     static const int v2_env = getenv("KCPP_FA_V2") ? atoi(getenv("KCPP_FA_V2")) : 0;   // in-launch merge: slower end to end (422 vs 443 tok/s)
     const int G0 = H / HKV;
@@ -860,7 +874,7 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     if (rc == -3 && force_path == 3) return -3;
     if (rc == -3)
         hipLaunchKernelGGL(k_fa_prefill<128>, dim3((T + FP_BQ - 1) / FP_BQ, H), dim3(256), 0, s, q16, kc, vc, out, T, H, HKV,
-                           n_past, scale, nullptr, -1, 0);
+                           n_past, scale, nullptr, -1, 0, (const int32_t *)nullptr);
     else if (rc)
         return rc;
     KCPP_CHECK(hipGetLastError());
@@ -978,7 +992,7 @@ int kcpp_flash_attn_ext(const float *q, int64_t q_nb1, int64_t q_nb2, const uint
                            D, n_kv, nullptr, nch, 1);
     } else {
         hipLaunchKernelGGL(k_fa_prefill<128>, dim3((T + FP_BQ - 1) / FP_BQ, H), dim3(256), 0, s, q16, kc, vc, out, T, H,
-                           HKV, 0, scale, mask, mask_ld, n_kv);
+                           HKV, 0, scale, mask, mask_ld, n_kv, (const int32_t *)nullptr);
     }
     KCPP_CHECK(hipGetLastError());
     return 0;

@@ -427,8 +427,8 @@ bool load_model(const load_model_inputs inputs) {
     hp.rope_base = user_rope ? inputs.rope_freq_base : (float)f.get_f("llama.rope.freq_base", 10000.0);
     hp.rope_freq_scale = user_rope && inputs.rope_freq_scale > 0 ? inputs.rope_freq_scale : 1.0f;
     hp.n_ctx = inputs.max_context_length > 0 ? inputs.max_context_length + 8 : 2048 + 8;
-    if (hp.n_layer <= 0 || hp.n_head <= 0 || hp.n_embd / hp.n_head != 128) {
-        fprintf(stderr, "[kcpp] load_model: need head_dim 128 (got n_embd %d / n_head %d)\n", hp.n_embd, hp.n_head);
+    if (hp.n_layer <= 0 || hp.n_head <= 0 || (hp.n_embd / hp.n_head != 128 && hp.n_embd / hp.n_head != 64)) {
+        fprintf(stderr, "[kcpp] load_model: need head_dim 128 or 64 (got n_embd %d / n_head %d)\n", hp.n_embd, hp.n_head);
         return false;
     }
     // mixture of experts (llm_load_hparams / llm_load_tensors, src/llama.cpp:5444-5445, 7176-7215)

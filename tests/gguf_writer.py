@@ -8,6 +8,10 @@ import numpy as np
 
 U32, I32, F32, BOOL, STR, ARR, U64 = 4, 5, 6, 7, 8, 9, 10
 
+# SentencePiece merges only through pieces that exist: every word has its whole prefix chain
+WORDS = ["▁h", "▁he", "▁hel", "▁hell", "▁hello", "▁w", "▁wo", "▁wor", "▁worl", "▁world", "▁t", "▁th", "▁the",
+         "a", "b", "ab", "▁a", "▁b", "▁of", "▁to"]
+
 
 def _s(x):
     b = x.encode("utf-8")

@@ -1,0 +1,79 @@
+"""BASELINE config 1 through the drop-in ABI: a TinyLlama-1.1B-shape GGUF (d 2048, 22 layers, 32/4 heads of dim
+64, ff 5632, vocab 32000; Q4_0 weights, Q8_0 output head; synthetic weights) loaded by load_model() at 512
+context, a 448-token prompt and 64 greedy tokens from generate() -- against the reference ggml CPU build's own
+run of the same model (tests/golden/config1.npz, make_config1.py):
+
+* the prompt text tokenizes to the fixture's 448 ids (SentencePiece vocabulary of the GGUF);
+* generate()'s 64 tokens are the reference's 64 greedy tokens (the reference's smallest top-1/top-2 margin on this
+  run is 0.32 logits against a build-to-build spread of 0.003, so any correct implementation picks the same
+  tokens), and equal the in-process runtime's greedy decode;
+* the prompt's logits match the reference within 2x its build-to-build spread (measured: inside 1x)."""
+import os
+
+import numpy as np
+import pytest
+
+import gguf_writer as GW
+import refharness as R
+from test_gpu_expose import piece
+
+pytestmark = pytest.mark.gpu
+
+TINYLLAMA = dict(n_vocab=32000, n_embd=2048, n_head=32, n_head_kv=4, n_layer=22, n_ff=5632, n_ctx=520, eps=1e-5,
+                 rope_base=10000.0)
+
+
+def test_config1_tinyllama_q4_0_generate(tmp_path):
+    import torch
+    assert torch.cuda.is_available()
+    import koboldcpp_amd.lib as K
+    from koboldcpp_amd import expose as X
+    fx = np.load(os.path.join(R.ROOT, "tests", "golden", "config1.npz"))
+    hp = TINYLLAMA
+    types = R.uniform_types(hp["n_layer"], R.Q4_0, R.Q8_0)
+    path = str(tmp_path / "tinyllama-q4_0.gguf")
+    toks = GW.llama_gguf(path, hp, types, 1234, GW.WORDS)
+    _, _, ttypes = GW.spm_vocab(hp["n_vocab"], GW.WORDS)
+    h = X.init_library()
+    li = X.load_model_inputs()
+    li.model_filename = path.encode()
+    li.max_context_length = 512
+    li.blasbatchsize = 512
+    li.gpulayers = 999
+    li.rope_freq_base = 10000.0
+    li.rope_freq_scale = 1.0
+    assert h.load_model(li)
+    os.remove(path)
+    prompt = " ".join(["hello world the"] * 149).encode()
+    r = h.token_count(prompt, True)
+    assert [r.ids[i] for i in range(r.count)] == [int(t) for t in fx["prompt"]]
+    gi = X.generation_inputs()
+    gi.prompt = prompt
+    gi.memory = b""
+    gi.max_context_length = 512
+    gi.max_length = 64
+    gi.temperature = 0.0
+    gi.top_k = 1
+    gi.rep_pen = 1.0
+    gi.bypass_eos_token = True
+    gi.seed = 1
+    out = h.generate(gi)
+    assert out.status == 1 and h.get_last_token_count() == 64
+    want = [int(t) for t in fx["tokens"][:64]]
+    assert out.text == b"".join(piece(toks, ttypes, t) for t in want)
+    # the runtime in-process: same greedy tokens, and the prompt's logits vs the reference
+    m = K.Model(hp, types)
+    m.synth(1234)
+    lg = m.decode([int(t) for t in fx["prompt"]], 0)
+    got = [int(np.argmax(lg))]
+    n = len(fx["prompt"])
+    for _ in range(63):
+        got.append(m.decode_greedy(n))
+        n += 1
+    m.close()
+    assert got == want
+    d = np.abs(lg - fx["logits0"])
+    print("config 1 prompt logits vs reference: max %.4g median %.4g (spread max %.4g median %.4g)"
+          % (d.max(), np.median(d), fx["spread_max"].max(), fx["spread_median"].max()))
+    # measured 0.0022 max / 3.7e-4 median, inside the reference's own 0.0029 / 4.6e-4
+    assert d.max() <= 2 * fx["spread_max"].max() and np.median(d) <= 2 * fx["spread_median"].max()

@@ -13,8 +13,7 @@ import refharness as R
 pytestmark = pytest.mark.gpu
 
 # SentencePiece merges only through pieces that exist: give every word its whole prefix chain
-WORDS = ["▁h", "▁he", "▁hel", "▁hell", "▁hello", "▁w", "▁wo", "▁wor", "▁worl", "▁world", "▁t", "▁th", "▁the",
-         "a", "b", "ab", "▁a", "▁b", "▁of", "▁to"]
+WORDS = GW.WORDS
 
 
 def piece(toks, types, t):
