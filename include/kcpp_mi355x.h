@@ -123,6 +123,23 @@ int kcpp_flash_attn_exact(const uint16_t *q16, const uint16_t *kc, const uint16_
 int kcpp_flash_attn_ext_exact(const float *q, int64_t q_nb1, int64_t q_nb2, const uint16_t *kc, const uint16_t *vc,
                               const uint16_t *mask, int64_t mask_ld, float *out, int T, int H, int HKV, int D, int n_kv,
                               float scale, void *stream);
+/* quantized KV cache (koboldcpp --quantkv 1/2 = q8_0/q4_0 K and V, gpttype_adapter.cpp:1958-1959; attn_kvq.hip).
+ * Per-layer cache layout: Q8_0 = qs int8 [n_ctx][ekv] ++ d f16 [n_ctx][ekv/32]; Q4_0 = qs [n_ctx][ekv/2] (ggml
+ * nibble order per 32-block) ++ d f16 [n_ctx][ekv/32].  kcpp_kv_cache_bytes(KT_F16 / KT_Q8_0 / KT_Q4_0, ...). */
+int64_t kcpp_kv_cache_bytes(int type, int64_t n_ctx, int64_t ekv);
+/* RoPE (mode NORM, table as kcpp_rope_table) of the q and k heads in place in f32 q|k|v rows (stride ld) */
+int kcpp_rope_qk_inplace(float *qkv, int64_t ld, int T, int H, int HKV, int D, int n_past, const int32_t *pos_dev,
+                         const void *rope_tab, void *stream);
+/* K (column koff) and V (column voff) of T f32 rows into the quantized caches at n_past + t (pos_dev[0] + t when
+ * given): quantize_row_q8_0 (AVX2 rounding) / quantize_row_q4_0_ref, ggml-quants.c */
+int kcpp_kv_store_q(int tk, int tv, const float *qkv, int64_t ld, int64_t koff, int64_t voff, int T, int64_t ekv,
+                    void *kc, void *vc, int64_t n_ctx, int n_past, const int32_t *pos_dev, void *stream);
+/* causal attention of T f32 query rows (stride ldq, head h at h*D) over quantized caches, positions
+ * [0, n_past + t]: q quantized to Q8_0, s = sum_b d_k d_q (integer dot), V dequantized, f32 accumulation
+ * (ggml_compute_forward_flash_attn_ext_f16 with a quantized K/V, ggml.c:15750-15840); D = 64 or 128 */
+int kcpp_flash_attn_q(int tk, int tv, const float *q, int64_t ldq, const void *kc, const void *vc, float *out, int T,
+                      int H, int HKV, int D, int64_t n_ctx, int n_past, const int32_t *n_past_dev, float scale,
+                      void *stream);
 /* single-token decode attention with explicit cache strides in elements (key p of kv head hk at
  * kc + p*kv_ld + hk*kv_hs); variant 0: 64-key chunks + combine, 1: splits with in-launch merge, 2: splits +
  * combine (A/B measurement entry, tools/fa_dec_bench.py) */
@@ -266,6 +283,11 @@ int kcpp_model_set_fused_decode(kcpp_model *m, int enable);
 /* 1: attention through kcpp_flash_attn_exact (reference order, f16 accumulation; strict-parity mode, slow);
  * 0 (default, or KCPP_FA_EXACT=1 at creation): the split-KV / MFMA kernels */
 int kcpp_model_set_fa_exact(kcpp_model *m, int enable);
+/* K / V cache types (llama_context_params type_k / type_v): KT_F16 (default) or quantized KT_Q8_0 / KT_Q4_0 for
+ * both (koboldcpp --quantkv).  Reallocates and clears the caches; quantized caches run single-token decode
+ * through the unfused per-op path and refuse kcpp_model_kv_shift (koboldcpp turns context shift off with
+ * --quantkv, koboldcpp.py).  Returns -1 for other combinations. */
+int kcpp_model_set_kv_types(kcpp_model *m, int type_k, int type_v);
 int64_t kcpp_model_weight_bytes(kcpp_model *m);
 const char *kcpp_last_error(void);
 

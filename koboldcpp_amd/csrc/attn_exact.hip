@@ -30,10 +30,7 @@ __device__ __forceinline__ float ex_exp(float x) { return (float)exp((double)x);
 // f16(x) of an f32 value that must first be rounded to f32: without the register barrier the compiler folds
 // f2h(fmaf(a, b, h2f(c))) into one v_fma_mixlo_f16, which rounds the exact result straight to f16 (a single
 // rounding where the reference rounds twice, f32 then f16 -- a different result in rare double-rounding cases)
-__device__ __forceinline__ uint16_t f2h_of_f32(float x) {
-    asm volatile("" : "+v"(x));
-    return f2h(x);
-}
+__device__ __forceinline__ uint16_t f2h_of_f32(float x) { return f2h_rn(x); }
 
 // EXT = the ggml op's own form (the b1 backend): q f32 with byte strides (rounded to f16 here, q_to_vec_dot),
 // all n_kv keys of the K/V views under an explicit f16 mask row (-inf keys skipped, others s*scale + mask).

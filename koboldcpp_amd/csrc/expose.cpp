@@ -528,6 +528,20 @@ bool load_model(const load_model_inputs inputs) {
         il = il1;
     }
     if (!init_handoff(*e)) { fprintf(stderr, "[kcpp] load_model: handoff events\n"); return false; }
+    // KV cache types (gpttype_adapter.cpp:1958-1959: quant_k/v > 1 -> Q4_0, == 1 -> Q8_0, else F16).  Quantized
+    // caches imply flash attention and no context shift (koboldcpp.py's --quantkv handling); this runtime's
+    // attention is always the flash form.  K and V must both be F16 or both quantized.
+    const auto kvtype = [](int q) { return q > 1 ? KT_Q4_0 : (q == 1 ? KT_Q8_0 : KT_F16); };
+    const int tk = kvtype(inputs.quant_k), tv = kvtype(inputs.quant_v);
+    if (tk != KT_F16 || tv != KT_F16) {
+        for (kcpp_model *m : e->stages)
+            if (kcpp_model_set_kv_types(m, tk, tv)) {
+                fprintf(stderr, "[kcpp] load_model: quant_k %d / quant_v %d: %s\n", inputs.quant_k, inputs.quant_v,
+                        kcpp_last_error());
+                return false;
+            }
+        e->use_contextshift = false;
+    }
     for (size_t k = 0; k < ts.size(); ++k) {
         for (kcpp_model *m : e->stages)
             if (kcpp_model_set_tensor(m, (int)k, ts[k].data, ts[k].bytes)) {

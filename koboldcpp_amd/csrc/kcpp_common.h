@@ -44,6 +44,13 @@ __device__ __forceinline__ T group_sum(T v) {     // reduce over aligned groups 
 
 __device__ __forceinline__ float h2f(uint16_t h) { return __half2float(__ushort_as_half(h)); }
 __device__ __forceinline__ uint16_t f2h(float f) { return __half_as_ushort(__float2half_rn(f)); }
+// f32 -> f16 of an already-rounded f32 value.  Without the register barrier the backend folds f2h(a * b) into
+// v_fma_mixlo_f16(a, b, 0) -- ONE rounding of the exact product, and +0 for a -0 product -- which is not the
+// reference's GGML_FP32_TO_FP16(a * b) (two roundings, sign kept); -ffp-contract=off does not stop it.
+__device__ __forceinline__ uint16_t f2h_rn(float x) {
+    asm volatile("" : "+v"(x));
+    return f2h(x);
+}
 
 __device__ __forceinline__ int sdot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
 

@@ -66,7 +66,7 @@ __global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, 
                     }
                 }
                 if constexpr (WT == KT_F16)   // ggml converts src1 to the F16 vec_dot_type
-                    xv[u] = make_float4(h2f(f2h(xv[u].x)), h2f(f2h(xv[u].y)), h2f(f2h(xv[u].z)), h2f(f2h(xv[u].w)));
+                    xv[u] = make_float4(h2f(f2h_rn(xv[u].x)), h2f(f2h_rn(xv[u].y)), h2f(f2h_rn(xv[u].z)), h2f(f2h_rn(xv[u].w)));
             }
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, 
                 float4 wv;
                 if constexpr (WT == KT_F16) {
                     // ggml converts src1 to the F16 vec_dot_type
-                    xv = make_float4(h2f(f2h(xv.x)), h2f(f2h(xv.y)), h2f(f2h(xv.z)), h2f(f2h(xv.w)));
+                    xv = make_float4(h2f(f2h_rn(xv.x)), h2f(f2h_rn(xv.y)), h2f(f2h_rn(xv.z)), h2f(f2h_rn(xv.w)));
                     const uint2 h = *(const uint2 *)((const uint16_t *)w + (int64_t)e * K + i);
                     wv = make_float4(h2f(h.x & 0xFFFF), h2f(h.x >> 16), h2f(h.y & 0xFFFF), h2f(h.y >> 16));
                 } else {

@@ -108,6 +108,7 @@ struct kcpp_model {
     bool use_graphs = true;
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
+    int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
     hipGraphExec_t g_exec = nullptr;
     hipStream_t side = nullptr;             // second branch of the decode step (independent q|k|v launches)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -214,6 +215,7 @@ extern "C" int kcpp_rope_row(float *row, int p, int n_dims, float freq_base, flo
 // position-indexed here, so the rows move (through a scratch copy) instead of the cells being relabelled.
 extern "C" int kcpp_model_kv_shift(kcpp_model *m, int p0, int diff, int n_past) {
     if (!m || p0 < 0 || diff <= 0 || p0 + diff > n_past || n_past > m->hp.n_ctx) { g_err = "kv_shift: bad range"; return -1; }
+    if (m->kv_tk != KT_F16) { g_err = "kv_shift: quantized KV cache (context shift is off with --quantkv)"; return -1; }
     hipSetDevice(m->device);
     const int64_t E = m->hp.n_embd, H = m->hp.n_head, HKV = m->hp.n_head_kv, D = E / H, EKV = HKV * D;
     const int64_t count = n_past - p0 - diff;
@@ -464,6 +466,29 @@ extern "C" int kcpp_model_set_graphs(kcpp_model *m, int enable) {
 }
 extern "C" int kcpp_model_set_fa_exact(kcpp_model *m, int enable) {
     m->fa_exact = enable != 0;
+    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    return 0;
+}
+extern "C" int kcpp_model_set_kv_types(kcpp_model *m, int tk, int tv) {
+    const bool q = tk == KT_Q8_0 || tk == KT_Q4_0;
+    if (!((tk == KT_F16 && tv == KT_F16) || (q && (tv == KT_Q8_0 || tv == KT_Q4_0)))) {
+        g_err = "kv types: F16/F16 or Q8_0|Q4_0 for both";
+        return -1;
+    }
+    const int64_t E = m->hp.n_embd, H = m->hp.n_head, HKV = m->hp.n_head_kv, D = E / H, EKV = HKV * D;
+    if (q && D % 32) { g_err = "quantized kv: head dim must be a multiple of 32"; return -1; }
+    RT_CHECK(hipSetDevice(m->device));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    for (auto &L : m->layers) {
+        if (L.kc) RT_CHECK(hipFree(L.kc));
+        if (L.vc) RT_CHECK(hipFree(L.vc));
+        L.kc = L.vc = nullptr;
+        const size_t kb = (size_t)kcpp_kv_cache_bytes(tk, m->hp.n_ctx, EKV), vb = (size_t)kcpp_kv_cache_bytes(tv, m->hp.n_ctx, EKV);
+        if (hipMalloc(&L.kc, kb) != hipSuccess || hipMalloc(&L.vc, vb) != hipSuccess) { g_err = "kv alloc"; return -2; }
+        RT_CHECK(hipMemset(L.kc, 0, kb));
+        RT_CHECK(hipMemset(L.vc, 0, vb));
+    }
+    m->kv_tk = tk; m->kv_tv = tv;
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
     return 0;
 }
@@ -748,10 +773,19 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
                 RC(matmul(m, t[j], nullptr, m->act, T, m->qkv + off, LQ, nullptr, 0, 0));
             }
         }
-        RC(kcpp_rope_kv(m->qkv, LQ, nullptr, m->q16, L.kc, L.vc, T, (int)H, (int)HKV, (int)D, n_past, posp, m->rope_tab, s));
-        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K && !m->fa_exact;
+        const bool kvq = m->kv_tk != KT_F16;
+        if (kvq) {   // quantized cache: f32 rope in place, quantize K/V rows into the cache, Q8_0-dot attention
+            RC(kcpp_rope_qk_inplace(m->qkv, LQ, T, (int)H, (int)HKV, (int)D, n_past, posp, m->rope_tab, s));
+            RC(kcpp_kv_store_q(m->kv_tk, m->kv_tv, m->qkv, LQ, E, E + EKV, T, EKV, L.kc, L.vc, hp.n_ctx, n_past, posp, s));
+        } else {
+            RC(kcpp_rope_kv(m->qkv, LQ, nullptr, m->q16, L.kc, L.vc, T, (int)H, (int)HKV, (int)D, n_past, posp, m->rope_tab, s));
+        }
+        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K && !m->fa_exact && !kvq;
         static const int fa_force = getenv("KCPP_FA_PATH") ? atoi(getenv("KCPP_FA_PATH")) : 0;
-        if (m->fa_exact)
+        if (kvq)
+            RC(kcpp_flash_attn_q(m->kv_tk, m->kv_tv, m->qkv, LQ, L.kc, L.vc, m->attn, T, (int)H, (int)HKV, (int)D, hp.n_ctx,
+                                 n_past, posp, kq_scale, s));
+        else if (m->fa_exact)
             RC(kcpp_flash_attn_exact(m->q16, L.kc, L.vc, m->attn, T, (int)H, (int)HKV, (int)D, n_past, posp, kq_scale, s));
         else
             RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, (woq && T <= 16) ? m->act : nullptr, m->fa_ws, T, (int)H,
@@ -812,7 +846,7 @@ static int decode_step_dev(kcpp_model *m) {
     if (m->has_embed)
         RC(kcpp_get_rows(m->tok_embd.type, m->tok_embd.d, hp.n_embd, hp.n_vocab, m->tok_dev, 1, m->x, hp.n_embd,
                          m->stream));
-    if (m->fused_decode) {
+    if (m->fused_decode && m->kv_tk == KT_F16) {
         RC(forward_layers_dec(m));
         if (m->has_output) RC(head_dec(m));
     } else {

@@ -88,11 +88,17 @@ _SIGS = {
     "kcpp_model_set_fa_exact": [P, I],
     "kcpp_flash_attn_exact": [P, P, P, P, I, I, I, I, I, P, Fl, P],
     "kcpp_model_weight_bytes": [P],
+    "kcpp_model_set_kv_types": [P, I, I],
+    "kcpp_rope_qk_inplace": [P, I64, I, I, I, I, I, P, P, P],
+    "kcpp_kv_store_q": [I, I, P, I64, I64, I64, I, I64, P, P, I64, I, P, P],
+    "kcpp_flash_attn_q": [I, I, P, I64, P, P, P, I, I, I, I, I64, I, P, Fl, P],
 }
 _RES = {"kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
         "kcpp_model_create": P, "kcpp_model_hidden": P, "kcpp_model_stream": P, "kcpp_model_weight_bytes": I64,
         "kcpp_last_error": ctypes.c_char_p, "kcpp_model_free": None, "kcpp_fa_set_stamps": None}
 _L.kcpp_act_bytes.argtypes = [I, I64, I64]
+_L.kcpp_kv_cache_bytes.argtypes = [I, I64, I64]
+_L.kcpp_kv_cache_bytes.restype = I64
 _L.kcpp_fa_workspace_bytes.argtypes = [I, I, I]
 _L.kcpp_fa_ext_workspace_bytes.argtypes = [I, I, I, I]
 _L.kcpp_gemm_workspace_bytes.argtypes = [I, I64, I64, I64]
@@ -285,6 +291,10 @@ class Model:
     def set_fa_exact(self, on):
         """strict-parity attention (reference order, f16 accumulation); see kcpp_flash_attn_exact"""
         _chk(_L.kcpp_model_set_fa_exact(self.m, int(on)), "set_fa_exact")
+
+    def set_kv_types(self, type_k, type_v):
+        """K / V cache types: F16 (default) or Q8_0 / Q4_0 for both (koboldcpp --quantkv); clears the caches"""
+        _chk(_L.kcpp_model_set_kv_types(self.m, int(type_k), int(type_v)), "set_kv_types")
 
     def set_graphs(self, on):
         _L.kcpp_model_set_graphs(self.m, int(on))

@@ -192,8 +192,30 @@ void orc_quantize_row_q8_0(const float *x, void *vy, int64_t k) {
     }
 }
 
+/* quantize_row_q4_0_ref, ggml-quants.c:669-704 (quantize_row_q4_0 calls it, :707) */
+void orc_quantize_row_q4_0(const float *x, void *vy, int64_t k) {
+    blk_q4_0 *y = vy;
+    for (int64_t i = 0; i < k / 32; ++i) {
+        float amax = 0.0f, max = 0.0f;
+        for (int j = 0; j < 32; ++j) {
+            const float v = x[i * 32 + j];
+            if (amax < fabsf(v)) { amax = fabsf(v); max = v; }
+        }
+        const float d = max / -8;
+        const float id = d ? 1.0f / d : 0.0f;
+        y[i].d = F2H(d);
+        for (int j = 0; j < 16; ++j) {
+            const float x0 = x[i * 32 + j] * id, x1 = x[i * 32 + 16 + j] * id;
+            const int8_t a = (int8_t)(x0 + 8.5f), b = (int8_t)(x1 + 8.5f);
+            const uint8_t xi0 = a < 15 ? a : 15, xi1 = b < 15 ? b : 15;
+            y[i].qs[j] = xi0 | (uint8_t)(xi1 << 4);
+        }
+    }
+}
+
 void orc_quantize_row(int vtype, const float *x, void *y, int64_t k) {
     switch (vtype) {
+        case KT_Q4_0: orc_quantize_row_q4_0(x, y, k); break;
         case KT_Q8_K: orc_quantize_row_q8_K(x, y, k); break;
         case KT_Q8_0: orc_quantize_row_q8_0(x, y, k); break;
         case KT_F16: { uint16_t *h = y; for (int64_t i = 0; i < k; ++i) h[i] = F2H(x[i]); } break;
@@ -453,15 +475,68 @@ void orc_flash_attn_ext(const float *q, const uint16_t *k, const uint16_t *v, in
     }
 }
 
+/* ggml_compute_forward_flash_attn_ext_f16 with a QUANTIZED K and V (ggml.c:15748-15851): Q is converted to K's
+ * vec_dot_type (Q8_0) by its from_float, s = vec_dot(K row, Q_q), V rows dequantized (to_float) and accumulated in
+ * f32 (ggml_vec_scale_f32 / ggml_vec_mad_f32).  k / v: ggml block rows, position p of kv head hk at
+ * base + p*row_bytes + hk*orc_row_bytes(type, D). */
+void orc_flash_attn_ext_q(const float *q, const void *k, const void *v, int64_t k_row_bytes, int64_t v_row_bytes,
+                          int ktype, int vtype, const uint16_t *mask, float *out, int D, int n_q, int n_head,
+                          int n_kv, int n_head_kv, float scale, int nthreads) {
+    const int rk = n_head / n_head_kv;
+    const int64_t kh = orc_row_bytes(ktype, D), vh = orc_row_bytes(vtype, D);
+    const int qt = orc_vec_dot_type(ktype);
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+    #pragma omp parallel for num_threads(nthreads) schedule(dynamic, 1)
+    for (int ir = 0; ir < n_q * n_head; ++ir) {
+        const int iq1 = ir / n_head, h = ir % n_head;
+        const int hk = h / rk;
+        uint8_t qq[1024];
+        float vkq32[512], v32[512];
+        orc_quantize_row(qt, q + ((int64_t)iq1 * n_head + h) * D, qq, D);
+        for (int d = 0; d < D; ++d) vkq32[d] = 0.0f;
+        float S = 0.0f, M = -INFINITY;
+        for (int ic = 0; ic < n_kv; ++ic) {
+            const float mv = mask ? H2F(mask[(int64_t)iq1 * n_kv + ic]) : 0.0f;
+            if (mv == -INFINITY) continue;
+            float s = orc_vec_dot(ktype, D, (const uint8_t *)k + ic * k_row_bytes + hk * kh, qq);
+            s = s * scale;
+            s += mv;
+            const float Mold = M;
+            float ms = 1.0f, vs = 1.0f;
+            if (s > M) {
+                M = s;
+                ms = expf(Mold - M);
+                for (int d = 0; d < D; ++d) vkq32[d] *= ms;
+            } else {
+                vs = expf(s - M);
+            }
+            orc_dequantize_row(vtype, (const uint8_t *)v + ic * v_row_bytes + hk * vh, v32, D);
+            for (int d = 0; d < D; ++d) vkq32[d] = fmaf(v32[d], vs, vkq32[d]);
+            S = S * ms + vs;
+        }
+        const float S_inv = 1.0f / S;
+        float *po = out + ((int64_t)iq1 * n_head + h) * D;
+        for (int d = 0; d < D; ++d) po[d] = vkq32[d] * S_inv;
+    }
+}
+
 /* ======================= Llama forward (build_llama) ======================= */
 struct orc_llama {
     orc_hparams hp;
     const void *const *w;
     const int *t;
     int nthreads;
-    uint16_t *kc, *vc;     /* [n_layer][n_ctx][n_head_kv*D] f16 */
+    uint16_t *kc, *vc;     /* [n_layer][n_ctx][n_head_kv*D] f16, or ggml block rows of type tk / tv */
+    int tk, tv;            /* cache types (llama_context_params type_k / type_v): KT_F16, KT_Q8_0, KT_Q4_0 */
     float *last_hidden;
 };
+
+int orc_llama_set_kv_types(orc_llama *m, int tk, int tv) {
+    if ((tk != KT_F16 && tk != KT_Q8_0 && tk != KT_Q4_0) || (tv != KT_F16 && tv != KT_Q8_0 && tv != KT_Q4_0)) return -1;
+    if ((tk == KT_F16) != (tv == KT_F16)) return -1;    /* mixed F16 / quantized: not restated */
+    m->tk = tk; m->tv = tv;
+    return 0;
+}
 
 orc_llama *orc_llama_create(const orc_hparams *hp, const void *const *data, const int *types, int nthreads) {
     orc_llama *m = calloc(1, sizeof(*m));
@@ -475,8 +550,9 @@ orc_llama *orc_llama_create(const orc_hparams *hp, const void *const *data, cons
     m->nthreads = nthreads > 0 ? nthreads : omp_get_max_threads();
     const int64_t D = hp->n_embd / hp->n_head;
     const int64_t kvsz = (int64_t)hp->n_layer * hp->n_ctx * hp->n_head_kv * D;
-    m->kc = calloc(kvsz, 2);
+    m->kc = calloc(kvsz, 2);     /* f16 size bounds the quantized rows too (Q8_0 34/32, Q4_0 18/32 B per element) */
     m->vc = calloc(kvsz, 2);
+    m->tk = m->tv = KT_F16;
     m->last_hidden = calloc(hp->n_embd, 4);
     return m;
 }
@@ -566,12 +642,21 @@ int orc_llama_eval(orc_llama *m, const int32_t *tokens, int T, int n_past, float
         orc_rope(q, q, D, H, T, pos, D, hp->rope_base, hp->rope_freq_scale, NULL, 0.0f, 1.0f, 32.0f, 1.0f, hp->n_ctx);
         orc_rope(kk, kk, D, HKV, T, pos, D, hp->rope_base, hp->rope_freq_scale, NULL, 0.0f, 1.0f, 32.0f, 1.0f, hp->n_ctx);
         uint16_t *kl = m->kc + (int64_t)il * hp->n_ctx * EKV, *vl = m->vc + (int64_t)il * hp->n_ctx * EKV;
+        if (m->tk != KT_F16) {                           /* ggml_cpy f32 -> Q8_0 / Q4_0 (from_float) into the cache */
+            const int64_t kb = orc_row_bytes(m->tk, EKV), vb = orc_row_bytes(m->tv, EKV);
+            for (int t = 0; t < T; ++t) {
+                orc_quantize_row(m->tk, kk + (int64_t)t * EKV, (uint8_t *)kl + (n_past + t) * kb, EKV);
+                orc_quantize_row(m->tv, vv + (int64_t)t * EKV, (uint8_t *)vl + (n_past + t) * vb, EKV);
+            }
+            orc_flash_attn_ext_q(q, kl, vl, kb, vb, m->tk, m->tv, mask, attn, D, T, H, n_kv, HKV, kq_scale, NT);
+        } else {
         for (int t = 0; t < T; ++t)
             for (int i = 0; i < EKV; ++i) {           /* ggml_cpy f32 -> f16 into the cache */
                 kl[(int64_t)(n_past + t) * EKV + i] = F2H(kk[(int64_t)t * EKV + i]);
                 vl[(int64_t)(n_past + t) * EKV + i] = F2H(vv[(int64_t)t * EKV + i]);
             }
         orc_flash_attn_ext(q, kl, vl, EKV, mask, attn, D, T, H, n_kv, HKV, kq_scale, NT);
+        }
         orc_mul_mat(lt[4], lw[4], E, E, attn, T, tmp, NT);
         add_inplace(tmp, x, (int64_t)T * E);             /* ffn_inp = attn_out + inpSA */
         memcpy(x, tmp, sizeof(float) * T * E);

@@ -32,6 +32,7 @@ int  orc_vec_dot_type(int wtype);
 int64_t orc_row_bytes(int type, int64_t k);
 void orc_quantize_row_q8_K(const float *x, void *y, int64_t k);
 void orc_quantize_row_q8_0(const float *x, void *y, int64_t k);
+void orc_quantize_row_q4_0(const float *x, void *y, int64_t k);   /* quantize_row_q4_0_ref, ggml-quants.c:669 */
 void orc_quantize_row(int vtype, const float *x, void *y, int64_t k);
 
 /* ggml_vec_dot_<wtype>_<vec_dot_type> for one row (ggml-quants.c:3922,5519,7714,8282,8919) */
@@ -57,6 +58,13 @@ void orc_flash_attn_ext(const float *q, const uint16_t *k, const uint16_t *v, in
                         const uint16_t *mask, float *out, int D, int n_q, int n_head,
                         int n_kv, int n_head_kv, float scale, int nthreads);
 
+/* the same with a quantized K and V (Q8_0 / Q4_0 ggml block rows; ggml.c:15748-15851): Q quantized to Q8_0,
+ * integer-block dot, V dequantized and accumulated in f32.  Row p of kv head hk at base + p*row_bytes +
+ * hk*orc_row_bytes(type, D). */
+void orc_flash_attn_ext_q(const float *q, const void *k, const void *v, int64_t k_row_bytes, int64_t v_row_bytes,
+                          int ktype, int vtype, const uint16_t *mask, float *out, int D, int n_q, int n_head,
+                          int n_kv, int n_head_kv, float scale, int nthreads);
+
 /* diagnostic: 1 = accumulate V in f32 in orc_flash_attn_ext (NOT the reference's f16 VKQ16) */
 void orc_set_fa_f32_accum(int on);
 
@@ -75,6 +83,8 @@ typedef struct {
 typedef struct orc_llama orc_llama;
 orc_llama *orc_llama_create(const orc_hparams *hp, const void *const *data, const int *types, int nthreads);
 void       orc_llama_free(orc_llama *m);
+/* KV cache types (koboldcpp --quantkv): KT_F16 (default) or KT_Q8_0 / KT_Q4_0 for both; call before eval */
+int        orc_llama_set_kv_types(orc_llama *m, int type_k, int type_v);
 /* evaluate n_tokens at positions n_past.. ; writes last-token logits (n_vocab) */
 int        orc_llama_eval(orc_llama *m, const int32_t *tokens, int n_tokens, int n_past, float *logits);
 /* optional debug: copy hidden state of last token after last layer's ffn (n_embd) */

@@ -82,6 +82,10 @@ static void fill_tensor(struct ggml_tensor *t, int type, unsigned long long seed
     for (int64_t b = 0; b < nbl; ++b) ks_fill_block(type, seed, (uint64_t)tid, (uint64_t)b, p + b * bb);
 }
 
+/* KV cache types (koboldcpp --quantkv: gpttype_adapter.cpp:1958-1959 -> llama_kv_cache type_k / type_v):
+ * env REF_KV_TYPES="tk tv" with ggml type ids (1 = F16 default, 8 = Q8_0, 2 = Q4_0) */
+static int g_tk = GGML_TYPE_F16, g_tv = GGML_TYPE_F16;
+
 static int load_model(model_t *m) {
     cfg_t *c = &m->c;
     const int E = c->n_embd, D = E / c->n_head, EKV = c->n_head_kv * D, F = c->n_ff, V = c->n_vocab;
@@ -138,8 +142,8 @@ static int load_model(model_t *m) {
     m->kc = malloc(sizeof(*m->kc) * c->n_layer);
     m->vc = malloc(sizeof(*m->vc) * c->n_layer);
     for (int il = 0; il < c->n_layer; ++il) {
-        m->kc[il] = ggml_new_tensor_1d(m->wctx, GGML_TYPE_F16, (int64_t)EKV * c->n_ctx);
-        m->vc[il] = ggml_new_tensor_1d(m->wctx, GGML_TYPE_F16, (int64_t)EKV * c->n_ctx);
+        m->kc[il] = ggml_new_tensor_1d(m->wctx, (enum ggml_type)g_tk, (int64_t)EKV * c->n_ctx);
+        m->vc[il] = ggml_new_tensor_1d(m->wctx, (enum ggml_type)g_tv, (int64_t)EKV * c->n_ctx);
         memset(m->kc[il]->data, 0, ggml_nbytes(m->kc[il]));
         memset(m->vc[il]->data, 0, ggml_nbytes(m->vc[il]));
     }
@@ -192,16 +196,16 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits,
         Kcur = ggml_rope_ext(ctx, ggml_reshape_3d(ctx, Kcur, D, HKV, T), inp_pos, NULL, D, 0, c->n_ctx,
                              c->rope_base, c->rope_freq_scale, 0.0f, 1.0f, 32.0f, 1.0f);
         /* llm_build_kv_store (src/llama.cpp:9180-9202), FA => V not transposed */
-        struct ggml_tensor *kview = ggml_view_1d(ctx, m->kc[il], (int64_t)T * EKV, ggml_row_size(GGML_TYPE_F16, EKV) * n_past);
-        struct ggml_tensor *vview = ggml_view_1d(ctx, m->vc[il], (int64_t)T * EKV, ggml_row_size(GGML_TYPE_F16, EKV) * n_past);
+        struct ggml_tensor *kview = ggml_view_1d(ctx, m->kc[il], (int64_t)T * EKV, ggml_row_size((enum ggml_type)g_tk, EKV) * n_past);
+        struct ggml_tensor *vview = ggml_view_1d(ctx, m->vc[il], (int64_t)T * EKV, ggml_row_size((enum ggml_type)g_tv, EKV) * n_past);
         ggml_build_forward_expand(gf, ggml_cpy(ctx, Kcur, kview));
         ggml_build_forward_expand(gf, ggml_cpy(ctx, ggml_reshape_2d(ctx, Vcur, EKV, T), vview));
         /* llm_build_kqv, FA branch (src/llama.cpp:9517-9634) */
         struct ggml_tensor *q = ggml_permute(ctx, Qcur, 0, 2, 1, 3);
-        struct ggml_tensor *k = ggml_view_3d(ctx, m->kc[il], D, n_kv, HKV,
-                                             ggml_row_size(GGML_TYPE_F16, EKV), ggml_row_size(GGML_TYPE_F16, D), 0);
-        struct ggml_tensor *v = ggml_view_3d(ctx, m->vc[il], D, n_kv, HKV,
-                                             ggml_row_size(GGML_TYPE_F16, EKV), ggml_row_size(GGML_TYPE_F16, D), 0);
+        struct ggml_tensor *k = ggml_view_3d(ctx, m->kc[il], D, n_kv, HKV, ggml_row_size((enum ggml_type)g_tk, EKV),
+                                             ggml_row_size((enum ggml_type)g_tk, D), 0);
+        struct ggml_tensor *v = ggml_view_3d(ctx, m->vc[il], D, n_kv, HKV, ggml_row_size((enum ggml_type)g_tv, EKV),
+                                             ggml_row_size((enum ggml_type)g_tv, D), 0);
         cur = ggml_flash_attn_ext(ctx, q, k, v, kq_mask, kq_scale, 0.0f, 0.0f);
         ggml_flash_attn_ext_set_prec(cur, GGML_PREC_F32);
         cur = ggml_reshape_2d(ctx, cur, E, T);
@@ -355,6 +359,28 @@ static int run_op(int argc, char **argv) {
         struct ggml_tensor *kp = ggml_permute(ctx, k, 0, 2, 1, 3);
         struct ggml_tensor *vp = ggml_permute(ctx, v, 0, 2, 1, 3);
         res = ggml_flash_attn_ext(ctx, qp, kp, vp, mask, 1.0f / sqrtf((float)D), 0.0f, 0.0f);
+    } else if (!strcmp(op, "cpyq")) {            /* ggml_cpy f32 [R][N] -> type (the KV-cache store); out raw bytes */
+        int type = atoi(argv[5]), N = atoi(argv[6]), R = atoi(argv[7]);
+        struct ggml_tensor *x = ggml_new_tensor_2d(ctx, GGML_TYPE_F32, N, R);
+        memcpy(x->data, in, ggml_nbytes(x));
+        struct ggml_tensor *y = ggml_new_tensor_2d(ctx, (enum ggml_type)type, N, R);
+        res = ggml_cpy(ctx, x, y);
+    } else if (!strcmp(op, "fattnq")) {          /* fattn with K / V of types tk / tv ([n_kv][HKV*D] block rows) */
+        int D = atoi(argv[5]), T = atoi(argv[6]), H = atoi(argv[7]), HKV = atoi(argv[8]), NKV = atoi(argv[9]);
+        int tk = atoi(argv[10]), tv = atoi(argv[11]);
+        int T_pad = GGML_PAD(T, GGML_KQ_MASK_PAD);
+        struct ggml_tensor *q = ggml_new_tensor_3d(ctx, GGML_TYPE_F32, D, H, T);
+        struct ggml_tensor *k = ggml_new_tensor_3d(ctx, (enum ggml_type)tk, D, HKV, NKV);
+        struct ggml_tensor *v = ggml_new_tensor_3d(ctx, (enum ggml_type)tv, D, HKV, NKV);
+        struct ggml_tensor *mask = ggml_new_tensor_2d(ctx, GGML_TYPE_F16, NKV, T_pad);
+        size_t off = 0;
+        memcpy(q->data, in + off, ggml_nbytes(q)); off += ggml_nbytes(q);
+        memcpy(k->data, in + off, ggml_nbytes(k)); off += ggml_nbytes(k);
+        memcpy(v->data, in + off, ggml_nbytes(v)); off += ggml_nbytes(v);
+        memset(mask->data, 0, ggml_nbytes(mask));
+        memcpy(mask->data, in + off, (size_t)T * NKV * 2);
+        res = ggml_flash_attn_ext(ctx, ggml_permute(ctx, q, 0, 2, 1, 3), ggml_permute(ctx, k, 0, 2, 1, 3),
+                                  ggml_permute(ctx, v, 0, 2, 1, 3), mask, 1.0f / sqrtf((float)D), 0.0f, 0.0f);
     } else if (!strcmp(op, "mulmat")) {
         int type = atoi(argv[5]), K = atoi(argv[6]), N = atoi(argv[7]), M = atoi(argv[8]);
         struct ggml_tensor *w = ggml_new_tensor_2d(ctx, (enum ggml_type)type, K, N);
@@ -374,6 +400,7 @@ static int run_op(int argc, char **argv) {
 }
 
 int main(int argc, char **argv) {
+    if (getenv("REF_KV_TYPES") && sscanf(getenv("REF_KV_TYPES"), "%d %d", &g_tk, &g_tv) != 2) return 2;
     if (argc >= 3 && !strcmp(argv[1], "llama")) return run_llama(argv[2]);
     if (argc >= 5 && !strcmp(argv[1], "op")) return run_op(argc, argv);
     fprintf(stderr, "usage: ref_llama llama <cfg> | op <name> <in> <out> args...\n");

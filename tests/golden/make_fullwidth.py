@@ -84,6 +84,23 @@ def main():
     out["l70_max"], out["l70_median"] = spread(a70, b70)
     out["l70_prompt"], out["l70_forced"] = np.array(p70, np.int32), f70
     print("70B-width 1-layer spread max", out["l70_max"], "median", out["l70_median"])
+    # ---- quantized KV cache (koboldcpp --quantkv 1 / 2: q8_0 / q4_0 K and V, gpttype_adapter.cpp:1958-1959) on the
+    # tiny Q4_K_M fixture, teacher-forced on its f16 run's tokens: reference logits and the build spread
+    kvq = {}
+    g = np.load(os.path.join(HERE, "e2e_tiny.npz"))
+    types_t = [int(t) for t in g["q4km_types"]]
+    for tag, kv in (("q8_0", "8 8"), ("q4_0", "2 2")):
+        os.environ["REF_KV_TYPES"] = kv
+        try:
+            a, _ = R.run_ref_llama(R.TINY, types_t, SEED, g["q4km_prompt"], 8, forced=g["q4km_tokens"][:-1], nthreads=NTH)
+            b, _ = R.run_ref_llama(R.TINY, types_t, SEED, g["q4km_prompt"], 8, forced=g["q4km_tokens"][:-1], nthreads=NTH,
+                                   binary=R.REF_BIN_SCALAR)
+        finally:
+            del os.environ["REF_KV_TYPES"]
+        kvq[tag + "_logits"] = a
+        out["kv_%s_max" % tag], out["kv_%s_median" % tag] = spread(a, b)
+        print("kv", tag, "spread max", out["kv_%s_max" % tag].max())
+    np.savez_compressed(os.path.join(HERE, "e2e_kvq.npz"), **kvq)
     np.savez_compressed(os.path.join(HERE, "e2e_full.npz"), **full)
     np.savez_compressed(os.path.join(HERE, "ref_spread.npz"), **out)
     print("wrote e2e_full.npz, ref_spread.npz")

@@ -49,6 +49,8 @@ def lib():
         L.orc_llama_free.argtypes = [P]
         L.orc_llama_eval.argtypes = [P, P, I, I, P]
         L.orc_llama_last_hidden.argtypes = [P, P]
+        L.orc_llama_set_kv_types.argtypes = [P, I, I]
+        L.orc_flash_attn_ext_q.argtypes = [P, P, P, I64, I64, I, I, P, P, I, I, I, I, I, F, I]
         _lib = L
     return _lib
 
@@ -159,8 +161,23 @@ def synth_tensor(hp, t, seed, idx):
     return np.concatenate([synth(t, seed, idx * 256 + e, k, n) for e in range(ns)])
 
 
+def flash_attn_q(q, k, v, ktype, vtype, mask, nthreads=0):
+    """q [T][H][D] f32; k / v: uint8 [n_kv][row bytes] ggml block rows (Q8_0 / Q4_0) of HKV*D elements;
+    mask [T][n_kv] f16 or None"""
+    q = np.ascontiguousarray(q, dtype=np.float32)
+    T, H, D = q.shape
+    k, v = np.ascontiguousarray(k, dtype=np.uint8), np.ascontiguousarray(v, dtype=np.uint8)
+    n_kv = k.shape[0]
+    HKV = k.shape[1] // row_bytes(ktype, D)
+    out = np.empty_like(q)
+    m = ptr(np.ascontiguousarray(mask).view(np.uint16)) if mask is not None else None
+    lib().orc_flash_attn_ext_q(ptr(q), ptr(k), ptr(v), k.shape[1], v.shape[1], ktype, vtype, m, ptr(out), D, T, H,
+                               n_kv, HKV, np.float32(1) / np.sqrt(np.float32(D)), nthreads)
+    return out
+
+
 class OracleLlama:
-    def __init__(self, hp, types, seed, nthreads=0):
+    def __init__(self, hp, types, seed, nthreads=0, kv_types=None):
         self.hp = hp
         self.bufs = [synth_tensor(hp, t, seed, i) for i, t in enumerate(types)]
         arr = (ctypes.c_void_p * len(self.bufs))(*[b.ctypes.data for b in self.bufs])
@@ -170,6 +187,8 @@ class OracleLlama:
                     hp.get("n_expert_used", 0))
         self._arr, self._tarr, self._h = arr, tarr, h
         self.m = lib().orc_llama_create(ctypes.byref(h), arr, tarr, nthreads)
+        if kv_types is not None:
+            assert lib().orc_llama_set_kv_types(self.m, *kv_types) == 0
 
     def eval(self, tokens, n_past):
         tok = np.ascontiguousarray(tokens, dtype=np.int32)
@@ -222,7 +241,7 @@ def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeou
         return logits, info
 
 
-def run_ref_op(op, inp_bytes, out_count, args, nthreads=4):
+def run_ref_op(op, inp_bytes, out_count, args, nthreads=4, dtype=np.float32):
     with tempfile.TemporaryDirectory() as td:
         fi, fo = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
         with open(fi, "wb") as f:
@@ -231,7 +250,7 @@ def run_ref_op(op, inp_bytes, out_count, args, nthreads=4):
                            env=dict(os.environ, REF_THREADS=str(nthreads)))
         if r.returncode != 0:
             raise RuntimeError("ref op %s failed rc=%s %s" % (op, r.returncode, r.stderr))
-        return np.fromfile(fo, dtype=np.float32)[:out_count]
+        return np.fromfile(fo, dtype=dtype)[:out_count]
 
 
 TINY = dict(n_vocab=512, n_embd=512, n_head=4, n_head_kv=1, n_layer=2, n_ff=1024, n_ctx=256,
