@@ -17,7 +17,9 @@
 
 #define FA_CHUNK 64
 #define FA_MAXG 8
-#define FA_MAX_CHUNKS 2048          // k_fa_combine's chunk-weight table: 2048 x 64 = 131072 keys
+#define FA_WS_TICKETS 256
+#define FA_MAX_CHUNKS 2048
+static void *g_fa_stamps = nullptr;       // diagnostic stamp buffer (tools only; kcpp_fa_set_stamps)          // k_fa_combine's chunk-weight table: 2048 x 64 = 131072 keys
 
 // K/V cache layout: [pos][HKV][D] f16, row stride EKV = HKV*D elements.
 // Query layout: q16 [T][H][D] f16.  Query t sits at absolute position n_past + t.
@@ -527,6 +529,291 @@ __global__ void __launch_bounds__(256) k_fa_combine2(const float *__restrict__ p
     }
 }
 
+#define FA_STAMP(ph)                                                                                   \
+    if (stamps && threadIdx.x == 0) {                                                                  \
+        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
+        __hip_atomic_store(&stamps[wg_id * 8 + (ph)], t_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
+    }
+// ---------------------------------------------------------------- decode v4: streaming splits + wide combine
+// One token.  Grid (NS splits, kv head), 256 threads.  Split sp owns keys [sp*per, (sp+1)*per) of [0, n_past].
+// Wave w streams 16-key groups base = p0 + 16 w + 64 j: lane (kq = lane >> 4, sub = lane & 15) loads 16 B
+// (8 dims) of K and of V for keys base + 4 i + kq, i < 4 -- every load instruction 1 KiB contiguous per wave --
+// and the next group's 8 loads are issued before the current one is used.  Scores: 8-dim partial dot, 16-lane
+// DPP reduction; online softmax per wave (m, l wave-uniform); O: each lane accumulates its 8 dims over its
+// row's keys, rows summed once at the end (permlane swaps), waves merged in LDS.  Partials: O [H][NS][128],
+// (m, l) [H][NS] (m = -inf for an empty split).
+template <int G>
+__global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
+                                                 const uint16_t *__restrict__ vc, float *__restrict__ part_o,
+                                                 float2 *__restrict__ part_ml, int H, int n_past_arg,
+                                                 const int32_t *__restrict__ n_past_dev, int NS, float scale,
+                                                 int64_t kv_ld, int64_t kv_hs, unsigned long long *stamps) {
+    constexpr int D = 128;
+    const int sp = blockIdx.x, hk = blockIdx.y;
+    const int wg_id = blockIdx.y * gridDim.x + blockIdx.x;
+    FA_STAMP(0);
+    const int nkv = (n_past_dev ? n_past_dev[0] : n_past_arg) + 1;
+    const int per = (nkv + NS - 1) / NS;
+    const int p0 = sp * per, p1 = min(p0 + per, nkv);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = lane & 15, kq = lane >> 4;
+    __shared__ float s_o[4][G][D];
+    __shared__ float s_ml[4][G][2];
+    __shared__ float s_w[4][G], s_L[G];
+    // scores in the exp2 domain: s2 = (q . k) * scale * log2(e); partial m in the same domain
+    const float sc2 = scale * 1.4426950408889634f;
+    float qv[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint4 qq = *(const uint4 *)(q16 + (int64_t)(hk * G + g) * D + sub * 8);
+        const uint32_t w4[4] = {qq.x, qq.y, qq.z, qq.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { qv[g][2 * e] = h2f(w4[e] & 0xFFFF); qv[g][2 * e + 1] = h2f(w4[e] >> 16); }
+    }
+    if (stamps) { if (qv[0][0] == 12345.0f) stamps[0] = 0; FA_STAMP(1); }
+    const uint16_t *kb = kc + (int64_t)hk * kv_hs + sub * 8, *vb = vc + (int64_t)hk * kv_hs + sub * 8;
+    float m[G], l[G], acc[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        m[g] = -INFINITY; l[g] = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[g][e] = 0.0f;
+    }
+    uint4 ka[4], va[4], kn[4], vn[4];
+    auto issue = [&](int base, uint4 *kk, uint4 *vv) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int p = base + 4 * i + kq;
+            const bool ok = p < p1;
+            kk[i] = ok ? *(const uint4 *)(kb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
+            vv[i] = ok ? *(const uint4 *)(vb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
+        }
+    };
+    auto consume = [&](int base, const uint4 *kk, const uint4 *vv) {
+        float s[G][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t w4[4] = {kk[i].x, kk[i].y, kk[i].z, kk[i].w};
+            float kf[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { kf[2 * e] = h2f(w4[e] & 0xFFFF); kf[2 * e + 1] = h2f(w4[e] >> 16); }
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                float sc = 0.0f;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sc = fmaf(qv[g][e], kf[e], sc);
+                s[g][i] = sc;
+            }
+        }
+        // 16-lane row sums of all G x 4 partial dots, interleaved (independent DPP chains)
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s[g][i] += dpp_f<0xB1>(s[g][i]);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s[g][i] += dpp_f<0x4E>(s[g][i]);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s[g][i] += dpp_f<0x141>(s[g][i]);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                s[g][i] += dpp_f<0x140>(s[g][i]);
+                s[g][i] = base + 4 * i + kq < p1 ? s[g][i] * sc2 : -INFINITY;
+            }
+        float mx[G], al[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) mx[g] = fmaxf(fmaxf(s[g][0], s[g][1]), fmaxf(s[g][2], s[g][3]));
+#pragma unroll
+        for (int g = 0; g < G; ++g) mx[g] = xmax16(mx[g]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) mx[g] = xmax32(mx[g]);
+        float ls[G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float mn = fmaxf(m[g], mx[g]);           // finite: key base + kq (i = 0) of row 0 is valid
+            al[g] = __builtin_amdgcn_exp2f(m[g] - mn);     // m = -inf -> 0
+            ls[g] = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                s[g][i] = __builtin_amdgcn_exp2f(s[g][i] - mn);   // -inf -> 0
+                ls[g] += s[g][i];
+            }
+            m[g] = mn;
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) ls[g] = xsum16(ls[g]);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            l[g] = fmaf(l[g], al[g], xsum32(ls[g]));
+#pragma unroll
+            for (int e = 0; e < 8; ++e) acc[g][e] *= al[g];
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint32_t w4[4] = {vv[i].x, vv[i].y, vv[i].z, vv[i].w};
+            float vf[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) { vf[2 * e] = h2f(w4[e] & 0xFFFF); vf[2 * e + 1] = h2f(w4[e] >> 16); }
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(s[g][i], vf[e], acc[g][e]);
+        }
+    };
+    int base = p0 + 16 * wave;
+    if (base < p1) issue(base, ka, va);
+    for (; base < p1; base += 128) {
+        const int b1 = base + 64;
+        if (b1 < p1) issue(b1, kn, vn);
+        consume(base, ka, va);
+        if (stamps && base == p0 + 16 * wave) { if (acc[0][0] == 12345.0f) stamps[0] = 0; FA_STAMP(2); }
+        if (b1 >= p1) break;
+        if (b1 + 64 < p1) issue(b1 + 64, ka, va);
+        consume(b1, kn, vn);
+    }
+    FA_STAMP(3);
+    // rows (kq) hold disjoint keys: park every row's 8 dims in LDS, reduce rows and waves in one pass
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[g][e] = xsum16(acc[g][e]);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[g][e] = xsum32(acc[g][e]);
+    if (kq == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            *(float4 *)&s_o[wave][g][sub * 8] = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
+            *(float4 *)&s_o[wave][g][sub * 8 + 4] = make_float4(acc[g][4], acc[g][5], acc[g][6], acc[g][7]);
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) { s_ml[wave][g][0] = m[g]; s_ml[wave][g][1] = l[g]; }
+    }
+    __syncthreads();
+    if (tid < G) {                                        // per-head wave weights and the split's (M, L)
+        const int g = tid;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) M = fmaxf(M, s_ml[w][g][0]);
+        float L = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const float wt = M == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(s_ml[w][g][0] - M);
+            s_w[w][g] = wt;
+            L = fmaf(wt, s_ml[w][g][1], L);
+        }
+        s_L[g] = L;
+        part_ml[(int64_t)(hk * G + g) * NS + sp] = make_float2(M, L);
+    }
+    __syncthreads();
+    for (int i = tid; i < G * D; i += 256) {
+        const int g = i / D, d = i % D;
+        float O = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) O = fmaf(s_w[w][g], s_o[w][g][d], O);
+        part_o[((int64_t)(hk * G + g) * NS + sp) * D + d] = O;
+    }
+    FA_STAMP(4);
+    if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(5); }
+}
+
+// combine of k_fa_dec4's partials (m in the exp2 domain): grid (H / 2), 256 threads = 2 heads x 128 dims
+// (one Q8_K block of 256 when quantizing); thread (head, d) issues all NS partial loads of its dim (<= 64, in
+// flight together); one wave per head forms the split weights exp2(m_s - M) in LDS.
+template <bool QUANT>
+__global__ void __launch_bounds__(256) k_fa_comb4(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
+                                                  float *__restrict__ out, uint8_t *__restrict__ qout, int H, int NS,
+                                                  unsigned long long *stamps) {
+    constexpr int D = 128, MAXS = 64;
+    const int pair = blockIdx.x, tid = threadIdx.x;
+    const int wg_id = 2048 + blockIdx.x;
+    FA_STAMP(0);
+    const int hl = tid >> 7, d = tid & 127, h = 2 * pair + hl;
+    __shared__ float s_w[2][MAXS];
+    __shared__ float s_l[2];
+    __shared__ float s_res[2 * D];
+    const float *po = part_o + (int64_t)h * NS * D + d;
+    float ov[MAXS];
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) ov[s] = s < NS ? po[(int64_t)s * D] : 0.0f;
+    if (d < 64) {                                        // wave 0 / 2: split weights of head hl
+        const float2 v = d < NS ? part_ml[(int64_t)h * NS + d] : make_float2(-INFINITY, 0.0f);
+        const float M = wave_max_dpp(v.x);
+        const float wt = v.x == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(v.x - M);
+        s_w[hl][d] = wt;
+        const float L = wave_sum_f(wt * v.y);
+        if (d == 0) s_l[hl] = L;
+    }
+    __syncthreads();
+    FA_STAMP(1);
+    float O0 = 0.0f, O1 = 0.0f, O2 = 0.0f, O3 = 0.0f;
+#pragma unroll
+    for (int s = 0; s < MAXS; s += 4) {
+        O0 = fmaf(s_w[hl][s], ov[s], O0);
+        O1 = fmaf(s_w[hl][s + 1], ov[s + 1], O1);
+        O2 = fmaf(s_w[hl][s + 2], ov[s + 2], O2);
+        O3 = fmaf(s_w[hl][s + 3], ov[s + 3], O3);
+    }
+    const float res = ((O0 + O1) + (O2 + O3)) / s_l[hl];
+    FA_STAMP(2);
+    if (out) out[(int64_t)h * D + d] = res;
+    if constexpr (QUANT) {
+        s_res[tid] = res;
+        __syncthreads();
+        if (tid < 16) {
+            float v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = s_res[16 * tid + k];
+            const int64_t E = (int64_t)H * D, nsb = E / 256;
+            q8k_quant16(v, tid, (int8_t *)qout + pair * 256, (float *)(qout + E) + pair,
+                        (int16_t *)(qout + E + nsb * 4) + pair * 16);
+        }
+    }
+    if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(3); }
+}
+
+#undef FA_STAMP
+
+// split count of k_fa_dec4: one workgroup per CU (256 / HKV splits; measured at 3850 cached keys,
+// tools/fa_dec_bench.py: 7.8 us vs 8.7 at 512 workgroups).  Independent of the context size, so the key
+// partition -- and the result, bit for bit -- depends on the cached keys only (empty splits exit early).
+static int fa4_splits(int n_kv_max, int HKV) {
+    (void)n_kv_max;
+    static const int ns_env = getenv("KCPP_FA4_NS") ? atoi(getenv("KCPP_FA4_NS")) : 0;
+    const int ns = ns_env > 0 ? ns_env : 256 / HKV;
+    return std::max(1, std::min(ns, 64));
+}
+
+static int fa4_launch(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
+                      float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
+                      int n_kv_max, float scale, hipStream_t s) {
+    const int G = H / HKV;
+    const int NS = fa4_splits(n_kv_max, HKV);
+    float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
+    float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
+    const dim3 grid(NS, HKV);
+    switch (G) {
+    case 1: hipLaunchKernelGGL(k_fa_dec4<1>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
+    case 2: hipLaunchKernelGGL(k_fa_dec4<2>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
+    case 4: hipLaunchKernelGGL(k_fa_dec4<4>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
+    case 8: hipLaunchKernelGGL(k_fa_dec4<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
+    default: return -1;
+    }
+    KCPP_CHECK(hipGetLastError());
+    if (qout) hipLaunchKernelGGL(k_fa_comb4<true>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS, (unsigned long long *)g_fa_stamps);
+    else hipLaunchKernelGGL(k_fa_comb4<false>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, NS, (unsigned long long *)g_fa_stamps);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
 // combine split-KV partials; one 1024-thread workgroup covers two heads (= one Q8_K block of 256).
 // Latency-bound (a few hundred KB from L2), so it is built for memory-level parallelism: every
 // thread issues its 16 partial-O loads (4 threads per output dim split the chunks) together with
@@ -767,10 +1054,11 @@ extern "C" {
 // zero before first use (allocate zeroed); the merging workgroup resets its ticket.
 int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max) {
     const int64_t nch = (n_kv_max + FA_CHUNK - 1) / FA_CHUNK;
-    return 256 + (int64_t)T * H * nch * (128 * 4 + 8) + (int64_t)T * H * 4 + 256;
+    // partial slots: T x nch chunks (k_fa_decode), at least the 64 splits k_fa_dec4 may use
+    const int64_t slots = std::max<int64_t>((int64_t)T * nch, 64);
+    return 256 + (int64_t)H * slots * (128 * 4 + 8) + (int64_t)T * H * 4 + 256;
 }
 // the first 256 B of the workspace are the decode-v2 tickets (one per kv head, zero between launches)
-#define FA_WS_TICKETS 256
 
 // out f32 [T][H][D] (may be null), qout Q8_K act [T][H*D] (may be null), ws from kcpp_fa_workspace_bytes
 // n_past_dev (optional): device-resident n_past (graph-replayable decode); then n_kv_max
@@ -794,6 +1082,11 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     const int G0 = H / HKV;
     static const int v3_env = getenv("KCPP_FA_V3") ? atoi(getenv("KCPP_FA_V3")) : 0;
     const bool v3 = (v3_env || force_path == 5) && !(force_path == 4);
+    static const int fa4_env = getenv("KCPP_FA4") ? atoi(getenv("KCPP_FA4")) : 1;
+    if (use_decode && T == 1 && (force_path == 0 || force_path == 1) && fa4_env && !v2_env && !v3_env && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) &&
+        (qout == nullptr || G0 >= 2))
+        return fa4_launch(q16, kc, vc, (int64_t)HKV * 128, 128, out, qout, ws, H, HKV, n_past, n_past_dev,
+                          n_past_dev ? n_kv_max : n_past + 1, scale, s);
     if (use_decode && T == 1 && (v2_env || v3 || force_path == 4) && HKV <= 64 && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) && (qout == nullptr || G0 >= 2)) {
         const int nkv = n_past_dev ? n_kv_max : n_past + 1;
         const int NS = std::max(1, std::min(FA2_NS, (nkv + 127) / 128));   // >= 1 sub-chunk of 128 keys per split
@@ -886,7 +1179,7 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
 // kc + p * kv_ld + hk * kv_hs.  Position-major ggml view: kv_ld = HKV*D, kv_hs = D; head-major: kv_ld = D,
 // kv_hs = n_ctx*D.  variant 0: 64-key chunks + k_fa_combine; 1: NS splits, last arriver merges in-launch;
 // 2: NS splits + k_fa_combine2.  (tools/fa_dec_bench.py)
-static void *g_fa_stamps = nullptr;
+
 void kcpp_fa_set_stamps(void *p) { g_fa_stamps = p; }     // diagnostic stamp buffer of k_fa_dec2 (tools only)
 int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
                       float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
@@ -915,6 +1208,20 @@ int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *v
         KCPP_CHECK(hipGetLastError());
         return 0;
     }
+    if (variant >= 10 && variant <= 13) {         // timing probes (tools/fa_dec_bench.py): pieces of variant 3
+        const int NS = fa4_splits(nkv, HKV);
+        float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
+        float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
+        const int32_t *npd = variant == 12 ? nullptr : n_past_dev;
+        const int np = variant == 12 ? nkv - 1 : n_past;
+        if (variant != 11 && G == 4)
+            hipLaunchKernelGGL(k_fa_dec4<4>, dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, np, npd, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps);
+        if (variant == 11 || variant == 13)
+            hipLaunchKernelGGL(k_fa_comb4<true>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS, (unsigned long long *)g_fa_stamps);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
+    if (variant == 3) return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, nkv, scale, s);
     const int NS = std::max(1, std::min(FA2_NS, (nkv + 127) / 128));
     unsigned *tickets = variant == 1 ? (unsigned *)ws : nullptr;
     float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);

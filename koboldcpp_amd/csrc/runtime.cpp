@@ -659,20 +659,31 @@ static int forward_layers_dec(kcpp_model *m) {
         } else {
             for (int i = 0; i < nq; ++i) RC(kcpp_gemv_dec(qty[i], &qa[i], 2, 1, 2, s));
         }
-        // --- attention over the cache, combine + Q8_K quantize for wo
-        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K && !m->fa_exact;
+        // --- attention over the cache (f32 output); wo quantizes it in its own prologue (PRO 2: the Q8_K /
+        // Q8_0 conversion overlaps wo's first weight loads instead of ending the attention combine)
+        static const int wo_pro_env = getenv("KCPP_WO_PRO") ? atoi(getenv("KCPP_WO_PRO")) : 2;
+        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K && !m->fa_exact && wo_pro_env == 0;
         if (m->fa_exact)
             RC(kcpp_flash_attn_exact(m->q16, L.kc, L.vc, m->attn, 1, (int)H, (int)HKV, (int)D, 0, m->pos_dev, kq_scale, s));
         else
             RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, woq ? m->act : nullptr, m->fa_ws, 1, (int)H, (int)HKV, (int)D,
                                0, m->pos_dev, hp.n_ctx, kq_scale, 1, s));
-        if (!woq) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, 1, s));
         {   // x += wo . attn
             DecArgs a;
             memset(&a, 0, sizeof a);
-            a.K = E; a.act = (const uint8_t *)m->act; a.nseg = 1;
+            a.K = E; a.nseg = 1;
             a.W[0] = (const uint8_t *)t[4].d; a.N[0] = t[4].N; a.Y[0] = m->x; a.res = m->x;
-            RC(kcpp_gemv_dec(t[4].type, &a, 0, 0, rows_per_wave(t[4].N, 0), s));
+            int rc = -3;
+            if (!woq && wo_pro_env == 2) {
+                a.x = m->attn;
+                rc = kcpp_gemv_dec(t[4].type, &a, 0, 2, rows_per_wave(t[4].N, 0), s);
+            }
+            if (rc == -3) {
+                if (!woq) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, 1, s));
+                a.x = nullptr; a.act = (const uint8_t *)m->act;
+                rc = kcpp_gemv_dec(t[4].type, &a, 0, 0, rows_per_wave(t[4].N, 0), s);
+            }
+            RC(rc);
         }
         if (hp.n_expert > 0) { RC(moe_dec(m, L)); continue; }
         // --- ffn_norm + gate|up + silu*mul

@@ -36,7 +36,7 @@ def main():
     for n_past in npasts:
         pos.fill_(n_past)
         for lname, (ld, hs) in layouts.items():
-            for var in (0, 1, 2):
+            for var in [int(v) for v in os.environ.get('FA_VARIANTS', '0,1,2,3').split(',')]:
                 if var == 0 and n_past + 1 > 16384:
                     continue
 
@@ -71,8 +71,9 @@ def main():
 
 
 def stamps():
-    """phase stamps of k_fa_dec2 (variants 1: in-launch merge, 2: partials only) for the last of 32 graph-replayed
-    layers: per phase min / median / max over workgroups, microseconds after the earliest workgroup entry"""
+    """phase stamps (s_memrealtime, 100 MHz) for the last of 32 graph-replayed layers: per phase min / median /
+    max over workgroups, microseconds after the earliest workgroup entry.  FA_STAMP_VARIANTS: kcpp_fa_decode_ex
+    variants (1 / 2: k_fa_dec2; 3: k_fa_dec4 (workgroups < 2048) + k_fa_comb4 (2048+))"""
     n_ctx = 4176
     L2 = 32
     kc = (torch.randn(L2, n_ctx * HKV * D, device="cuda") * 0.5).half()
@@ -83,15 +84,17 @@ def stamps():
     ws = torch.zeros(K.fa_workspace_bytes(16, H, n_ctx), dtype=torch.uint8, device="cuda")
     pos = torch.zeros(1, dtype=torch.int32, device="cuda")
     st = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
-    names = ["entry", "q", "loop", "part_issued", "part_drained", "ticket", "merged", "quant_stored"]
+    variants = [int(v) for v in os.environ.get("FA_STAMP_VARIANTS", "1,2").split(",")]
     for n_past in (100, 3850):
         pos.fill_(n_past)
-        for var in (1, 2):
+        for var in variants:
+            lo, hi = (D, n_ctx * D) if var in (1, 2) else (HKV * D, D)
+
             def step():
                 sp = torch.cuda.current_stream().cuda_stream
                 for l in range(L2):
                     K.raw().kcpp_fa_set_stamps(st.data_ptr() if l == L2 - 1 else None)
-                    K.call("kcpp_fa_decode_ex", q[l].data_ptr(), kc[l].data_ptr(), vc[l].data_ptr(), D, n_ctx * D,
+                    K.call("kcpp_fa_decode_ex", q[l].data_ptr(), kc[l].data_ptr(), vc[l].data_ptr(), lo, hi,
                            out[l].data_ptr(), qout[l].data_ptr(), ws.data_ptr(), H, HKV, 0, pos.data_ptr(),
                            n_ctx, 1.0 / D ** 0.5, var, sp)
                 K.raw().kcpp_fa_set_stamps(None)
@@ -103,16 +106,19 @@ def stamps():
                 g.replay()
             torch.cuda.synchronize()
             a = st.view(-1, 8).cpu().numpy()
-            a = a[a[:, 0] > 0]
-            t0 = a[:, 0].min()
-            res = {}
-            for ph in range(8):
-                col = a[:, ph]
-                col = col[col > 0]
-                if len(col):
-                    d = (col - t0) / 100.0
-                    res[names[ph]] = [round(float(d.min()), 2), round(float(np.median(d)), 2), round(float(d.max()), 2), len(col)]
-            print(json.dumps({"n_past": n_past, "variant": var, "phases_us_min_med_max_n": res}), flush=True)
+            t0 = a[a[:, 0] > 0][:, 0].min()
+            for name, rows in (("dec", a[:2048]), ("comb", a[2048:])):
+                rows = rows[rows[:, 0] > 0]
+                if not len(rows):
+                    continue
+                res = {}
+                for ph in range(8):
+                    col = rows[:, ph]
+                    col = col[col > 0]
+                    if len(col):
+                        d = (col - t0) / 100.0
+                        res[ph] = [round(float(d.min()), 2), round(float(np.median(d)), 2), round(float(d.max()), 2), len(col)]
+                print(json.dumps({"n_past": n_past, "variant": var, "kernel": name, "phases_us_min_med_max_n": res}), flush=True)
 
 
 if __name__ == "__main__":
