@@ -542,12 +542,13 @@ __global__ void __launch_bounds__(256) k_fa_combine2(const float *__restrict__ p
 // DPP reduction; online softmax per wave (m, l wave-uniform); O: each lane accumulates its 8 dims over its
 // row's keys, rows summed once at the end (permlane swaps), waves merged in LDS.  Partials: O [H][NS][128],
 // (m, l) [H][NS] (m = -inf for an empty split).
-template <int G>
+template <int G, bool MERGE>
 __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
                                                  const uint16_t *__restrict__ vc, float *__restrict__ part_o,
                                                  float2 *__restrict__ part_ml, int H, int n_past_arg,
                                                  const int32_t *__restrict__ n_past_dev, int NS, float scale,
-                                                 int64_t kv_ld, int64_t kv_hs, unsigned long long *stamps) {
+                                                 int64_t kv_ld, int64_t kv_hs, unsigned long long *stamps,
+                                                 unsigned *__restrict__ tickets, float *__restrict__ out) {
     constexpr int D = 128;
     const int sp = blockIdx.x, hk = blockIdx.y;
     const int wg_id = blockIdx.y * gridDim.x + blockIdx.x;
@@ -723,6 +724,57 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
     }
     FA_STAMP(4);
     if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(5); }
+    if constexpr (MERGE) {
+        // the last split of this kv head to finish merges all NS partials (release / agent-scope ticket /
+        // acquire, as k_fa_decode's fused form) and writes the f32 attention output
+        __shared__ int s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned prev = __hip_atomic_fetch_add(&tickets[hk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = prev == (unsigned)(NS - 1);
+            if (s_last) {
+                __hip_atomic_store(&tickets[hk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+        if (!s_last) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        FA_STAMP(6);
+        // split weights: wave w forms exp2(m_s - M) of heads w, w + 4 in LDS (NS <= 64 = one lane each)
+        __shared__ float s_sw[G][64];
+        __shared__ float s_sl[G];
+        for (int g = wave; g < G; g += 4) {
+            const float2 v = lane < NS ? part_ml[(int64_t)(hk * G + g) * NS + lane] : make_float2(-INFINITY, 0.0f);
+            const float M = wave_max_dpp(v.x);
+            const float wt = v.x == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(v.x - M);
+            s_sw[g][lane] = wt;
+            const float L = wave_sum_f(wt * v.y);
+            if (lane == 0) s_sl[g] = L;
+        }
+        __syncthreads();
+        for (int i = tid; i < G * D; i += 256) {
+            const int g = i / D, d = i % D;
+            const float *po = part_o + (int64_t)(hk * G + g) * NS * D + d;
+            float ov[64];
+#pragma unroll
+            for (int s2 = 0; s2 < 64; ++s2) ov[s2] = s2 < NS ? po[(int64_t)s2 * D] : 0.0f;
+            float O0 = 0.0f, O1 = 0.0f, O2 = 0.0f, O3 = 0.0f;
+#pragma unroll
+            for (int s2 = 0; s2 < 64; s2 += 4) {
+                O0 = fmaf(s_sw[g][s2], ov[s2], O0);
+                O1 = fmaf(s_sw[g][s2 + 1], ov[s2 + 1], O1);
+                O2 = fmaf(s_sw[g][s2 + 2], ov[s2 + 2], O2);
+                O3 = fmaf(s_sw[g][s2 + 3], ov[s2 + 3], O3);
+            }
+            out[(int64_t)(hk * G + g) * D + d] = ((O0 + O1) + (O2 + O3)) / s_sl[g];
+        }
+        if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(7); }
+    }
 }
 
 // combine of k_fa_dec4's partials (m in the exp2 domain): grid (H / 2), 256 threads = 2 heads x 128 dims
@@ -800,14 +852,25 @@ static int fa4_launch(const uint16_t *q16, const uint16_t *kc, const uint16_t *v
     float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
     float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
     const dim3 grid(NS, HKV);
+    // in-launch merge by the last split of each kv head: opt-in only -- measured 17.9 vs 12.3 us per layer at 3850
+    // keys (tools/fa_dec_bench.py variant 4 vs 3: the agent-scope ticket lands ~5 us after the partial stores and
+    // the single merging workgroup per kv head reads its 64 KB of partials in ~4.6 us), the combine launch is cheaper
+    static const int merge_env = getenv("KCPP_FA4_MERGE") ? atoi(getenv("KCPP_FA4_MERGE")) : 0;
+    const bool merge = merge_env && qout == nullptr && out != nullptr && HKV * 4 <= FA_WS_TICKETS;
+    unsigned *tk = (unsigned *)ws;
+    unsigned long long *st = (unsigned long long *)g_fa_stamps;
+#define KCPP_FA4_CASE(GG)                                                                                               \
+    case GG:                                                                                                            \
+        if (merge) hipLaunchKernelGGL((k_fa_dec4<GG, true>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st, tk, out); \
+        else hipLaunchKernelGGL((k_fa_dec4<GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st, tk, out); \
+        break;
     switch (G) {
-    case 1: hipLaunchKernelGGL(k_fa_dec4<1>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
-    case 2: hipLaunchKernelGGL(k_fa_dec4<2>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
-    case 4: hipLaunchKernelGGL(k_fa_dec4<4>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
-    case 8: hipLaunchKernelGGL(k_fa_dec4<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
+        KCPP_FA4_CASE(1) KCPP_FA4_CASE(2) KCPP_FA4_CASE(4) KCPP_FA4_CASE(8)
     default: return -1;
     }
+#undef KCPP_FA4_CASE
     KCPP_CHECK(hipGetLastError());
+    if (merge) return 0;
     if (qout) hipLaunchKernelGGL(k_fa_comb4<true>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS, (unsigned long long *)g_fa_stamps);
     else hipLaunchKernelGGL(k_fa_comb4<false>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, NS, (unsigned long long *)g_fa_stamps);
     KCPP_CHECK(hipGetLastError());
@@ -1215,13 +1278,14 @@ int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *v
         const int32_t *npd = variant == 12 ? nullptr : n_past_dev;
         const int np = variant == 12 ? nkv - 1 : n_past;
         if (variant != 11 && G == 4)
-            hipLaunchKernelGGL(k_fa_dec4<4>, dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, np, npd, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps);
+            hipLaunchKernelGGL((k_fa_dec4<4, false>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, np, npd, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps, (unsigned *)ws, out);
         if (variant == 11 || variant == 13)
             hipLaunchKernelGGL(k_fa_comb4<true>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS, (unsigned long long *)g_fa_stamps);
         KCPP_CHECK(hipGetLastError());
         return 0;
     }
     if (variant == 3) return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, nkv, scale, s);
+    if (variant == 4) return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, nullptr, ws, H, HKV, n_past, n_past_dev, nkv, scale, s);
     const int NS = std::max(1, std::min(FA2_NS, (nkv + 127) / 128));
     unsigned *tickets = variant == 1 ? (unsigned *)ws : nullptr;
     float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);

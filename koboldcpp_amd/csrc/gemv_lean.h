@@ -36,8 +36,15 @@ struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_imp
             }
         }
     }
-    __device__ __forceinline__ void compute(const DecArgs &a, uint8_t *lds) {
+    __device__ __forceinline__ void compute(const DecArgs &a, uint8_t *lds, unsigned long long *st_ = nullptr) {
         const int tid = threadIdx.x;
+#ifdef KCPP_STAMPS
+#define LP_STAMP(ph) if (threadIdx.x == 0 && st_) __hip_atomic_store(&st_[(ph)], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+#define LP_STAMP(ph)
+#endif
+        if (v[0][0] == 12345.0f && st_) st_[15] = 1;
+        LP_STAMP(8);
         const int64_t K = a.K;
         const int nchunk = (int)(K / 16);
         if constexpr (PRO == 1) {
@@ -49,9 +56,11 @@ struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_imp
                     for (int e = 0; e < 16; ++e) ss += (double)__fmul_rn(v[i][e], v[i][e]);
                 }
             ss = wave_sum_d(ss);
+            LP_STAMP(9);
             __shared__ double red[4];
             if ((tid & 63) == 0) red[tid >> 6] = ss;
             __syncthreads();
+            LP_STAMP(10);
             const double sum = red[0] + red[1] + red[2] + red[3];
             const float scale = 1.0f / sqrtf((float)(sum / (double)K) + a.eps);   // ggml.c:12089
 #pragma unroll
@@ -62,12 +71,27 @@ struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_imp
         int8_t *qs = (int8_t *)lds;
         float *d = (float *)(lds + K);
         int16_t *bs = (int16_t *)(lds + K + K / 256 * 4);
+#ifndef KCPP_PROBE_NOQUANT
 #pragma unroll
         for (int i = 0; i < MAXC; ++i) {
             const int c = tid + 256 * i;
             if (c < nchunk) q8k_quant16(v[i], c & 15, qs + (c >> 4) * 256, d + (c >> 4), bs + (c >> 4) * 16);
         }
+#else   // timing probe only (wrong results, finite: an all-zero activation): the prologue without its quantization
+#pragma unroll
+        for (int i = 0; i < MAXC; ++i) {
+            const int c = tid + 256 * i;
+            if (c < nchunk) {
+                *(uint4 *)(qs + 16 * c) = make_uint4(v[i][0] == 1234.5f, 0, 0, 0);
+                if ((c & 15) == 0) d[c >> 4] = 0.0f;
+                bs[c] = 0;
+            }
+        }
+#endif
+        LP_STAMP(11);
         __syncthreads();
+        LP_STAMP(12);
+#undef LP_STAMP
     }
 };
 

@@ -25,6 +25,23 @@
 #include <algorithm>
 #include <cstdlib>
 
+#ifdef KCPP_STAMPS
+// phase stamps (tools/rs_stamps.py; instrumented A/B build only): per workgroup 8 words -- entry, activation
+// ready, first group reduced, streaming done, results stored, (grid << 32 | block), K | mode << 24, rows
+__device__ unsigned long long *g_rs_stamps;
+__device__ unsigned g_rs_slot;
+#define RS_STAMP(ph)                                                                                                  \
+    if (threadIdx.x == 0 && st_) __hip_atomic_store(&st_[(ph)], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,   \
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+extern "C" int kcpp_rs_set_stamps(void *p) {
+    unsigned z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_rs_stamps), &p, sizeof p) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_rs_slot), &z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#else
+#define RS_STAMP(ph)
+#endif
+
 namespace {
 
 // ---------------------------------------------------------------- Q4_K_RS
@@ -170,6 +187,21 @@ __global__ void __launch_bounds__(256) k_gemv_rs(const DecArgs a) {
     using T = RS<TYPE>;
     constexpr int RR = MODE == 1 ? 2 * R : R;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+#ifdef KCPP_STAMPS
+    __shared__ unsigned long long *st_s;
+    if (threadIdx.x == 0) {
+        unsigned long long *b = g_rs_stamps;   // every 8th workgroup records (one counter: ~88 adds per us)
+        st_s = (b && (blockIdx.x & 7) == 0) ? b + 16ull * (atomicAdd(&g_rs_slot, 1u) & 131071u) : nullptr;
+        if (st_s) {
+            st_s[5] = ((unsigned long long)gridDim.x << 32) | blockIdx.x;
+            st_s[6] = (unsigned long long)a.K | ((unsigned long long)MODE << 24) | ((unsigned long long)PRO << 28);
+            st_s[7] = (unsigned long long)(a.N[0] + (a.nseg > 1 ? a.N[1] : 0) + (a.nseg > 2 ? a.N[2] : 0));
+        }
+    }
+    __syncthreads();
+    unsigned long long *st_ = st_s;
+    RS_STAMP(0);
+#endif
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int K = (int)a.K, nsb = K / 256, RB = nsb * T::BYTES;
@@ -206,7 +238,11 @@ __global__ void __launch_bounds__(256) k_gemv_rs(const DecArgs a) {
         lean::ActPro<PRO, MC> pro;
         pro.load(a);
         issue(g0, ba);
+#ifdef KCPP_STAMPS
+        pro.compute(a, lds, st_);
+#else
         pro.compute(a, lds);
+#endif
     } else {
         lean::ActCopyCol cp;
         cp.load(a.act, K, a.act_mtot > 0 ? a.act_mtot : 1, a.act_col);
@@ -216,6 +252,7 @@ __global__ void __launch_bounds__(256) k_gemv_rs(const DecArgs a) {
     typename T::Act xr[NI];
 #pragma unroll
     for (int i = 0; i < NI; ++i) T::act(lds, K, min(T::sb_of(lane, i), nsb - 1), lc, xr[i]);
+    RS_STAMP(1);
 
     float slot[R];
 #pragma unroll
@@ -245,6 +282,9 @@ __global__ void __launch_bounds__(256) k_gemv_rs(const DecArgs a) {
             slot[r] = mine ? v : slot[r];
         }
         slot_g = mine ? g : slot_g;
+#ifdef KCPP_STAMPS
+        if (k == 0) { if (slot[0] == 12345.0f) st_[0] = 0; RS_STAMP(2); }
+#endif
     };
     int k = 0;
     if constexpr (PF) {
@@ -262,10 +302,15 @@ __global__ void __launch_bounds__(256) k_gemv_rs(const DecArgs a) {
             compute(g, ba, k);
         }
     }
+    RS_STAMP(3);
     if (slot_g < 0) return;
     int seg, row0;
     group_rows(slot_g, seg, row0);
     lean::store_group<R, MODE>(a, seg, row0, slot);
+#ifdef KCPP_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    RS_STAMP(4);
+#endif
 }
 
 namespace {

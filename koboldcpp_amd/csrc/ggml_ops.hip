@@ -254,7 +254,8 @@ __global__ void k_get_rows_g(const char *__restrict__ s, TD ts, const char *__re
     for (int64_t r = blockIdx.y; r < nrows; r += gridDim.y) {
         int64_t i10, i11, i12;
         row3(r, td.ne, i10, i11, i12);           // dst dims 1..3 = ids dims 0..2
-        const int64_t row = *(const int32_t *)(ids + i10 * ti.nb[0] + i11 * ti.nb[1] + i12 * ti.nb[2]);
+        const int64_t row = min(max((int64_t)*(const int32_t *)(ids + i10 * ti.nb[0] + i11 * ti.nb[1] + i12 * ti.nb[2]),
+                                    (int64_t)0), ts.ne[1] - 1);   // clamped: a bad id cannot fault the device
         const char *sr = s + row * ts.nb[1] + i11 * ts.nb[2] + i12 * ts.nb[3];
         char *dr = d + i10 * td.nb[1] + i11 * td.nb[2] + i12 * td.nb[3];
         for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < td.ne[0]; i0 += (int64_t)gridDim.x * blockDim.x) {

@@ -136,39 +136,55 @@ __device__ __forceinline__ void amax_step(float &a, int &i, float &x) {
 // quantize_row_q8_K_ref (ggml-quants.c:3786-3823) of one 256-element super-block held by an
 // aligned 16-lane group, lane j holding elements 16j..16j+15 (so bsums[j] is lane-local).
 // qs/d/bs point at the super-block's output; l16 = lane & 15.
+// VALU-lean form of the reference loop, same bytes:
+//  * amax = max |x|; the reference keeps the signed value of the FIRST element reaching it (`ax > amax`): the
+//    lane(s) whose own maximum equals amax scan for it, then the smallest index wins across the group;
+//  * nearest_int(iscale * x) (ggml-quants.c:1640, multiply not fused) = bits(iscale * x + 1.5 * 2^23) -
+//    0x4B400000, so the int8 code is the low byte of those float bits and the 16-element sum is the wrapped sum
+//    of the bits minus 16 * 0x4B400000; |iscale * x| <= 127, so the reference's MIN(127, .) never applies.
 __device__ __forceinline__ void q8k_quant16(const float (&v)[16], int l16, int8_t *qs, float *d, int16_t *bs) {
-    float am = -1.0f, mx = 0.0f;
-    int ai = 0;
+    float lm = 0.0f;
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-        const float a = fabsf(v[e]);
-        if (a > am) { am = a; ai = 16 * l16 + e; mx = v[e]; }
-    }
-    amax_step<0xB1>(am, ai, mx);
-    amax_step<0x4E>(am, ai, mx);
-    amax_step<0x141>(am, ai, mx);
-    amax_step<0x140>(am, ai, mx);
-    int q[16];
-    if (am == 0.0f) {
-#pragma unroll
-        for (int e = 0; e < 16; ++e) q[e] = 0;
+    for (int e = 0; e < 16; ++e) lm = fmaxf(lm, fabsf(v[e]));
+    const float am = max16_f(lm);
+    if (am == 0.0f) {                                  // uniform over the 16 lanes (one amax)
+        *(uint4 *)(qs + 16 * l16) = make_uint4(0, 0, 0, 0);
+        bs[l16] = 0;
         if (l16 == 0) *d = 0.0f;
-    } else {
-        const float iscale = -127.f / mx;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) { const int t = nearest_int_mul(iscale, v[e]); q[e] = t < 127 ? t : 127; }
-        if (l16 == 0) *d = 1.0f / iscale;
+        return;
     }
-    int s = 0;
-    uint32_t w[4];
+    int ai = 256;
+    float mx = 0.0f;
+    if (lm == am) {
+#pragma unroll
+        for (int e = 15; e >= 0; --e)
+            if (fabsf(v[e]) == am) { ai = 16 * l16 + e; mx = v[e]; }
+    }
+#define KCPP_Q8K_MIN_STEP(CTRL)                                                                  \
+    {                                                                                            \
+        const int a2 = dpp_i<CTRL>(ai);                                                          \
+        const float m2 = dpp_f<CTRL>(mx);                                                        \
+        if (a2 < ai) { ai = a2; mx = m2; }                                                       \
+    }
+    KCPP_Q8K_MIN_STEP(0xB1) KCPP_Q8K_MIN_STEP(0x4E) KCPP_Q8K_MIN_STEP(0x141) KCPP_Q8K_MIN_STEP(0x140)
+#undef KCPP_Q8K_MIN_STEP
+    const float iscale = -127.f / mx;
+    uint32_t w[4], sum = 0u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        w[k] = (uint32_t)(q[4 * k] & 0xFF) | ((uint32_t)(q[4 * k + 1] & 0xFF) << 8) |
-               ((uint32_t)(q[4 * k + 2] & 0xFF) << 16) | ((uint32_t)(q[4 * k + 3] & 0xFF) << 24);
-        s += q[4 * k] + q[4 * k + 1] + q[4 * k + 2] + q[4 * k + 3];
+        uint32_t bt[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            bt[j] = __float_as_uint(__fadd_rn(__fmul_rn(iscale, v[4 * k + j]), 12582912.f));
+            sum += bt[j];
+        }
+        const uint32_t lo = __builtin_amdgcn_perm(bt[1], bt[0], 0x0C0C0400u);   // byte0(bt0) | byte0(bt1) << 8
+        const uint32_t hi = __builtin_amdgcn_perm(bt[3], bt[2], 0x0C0C0400u);
+        w[k] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);                      // lo.b0 lo.b1 hi.b0 hi.b1
     }
     *(uint4 *)(qs + 16 * l16) = make_uint4(w[0], w[1], w[2], w[3]);
-    bs[l16] = (int16_t)s;
+    bs[l16] = (int16_t)(int32_t)(sum - 16u * 0x4B400000u);
+    if (l16 == 0) *d = 1.0f / iscale;
 }
 
 // 64-lane all-reduce of a double: DPP within rows of 16 (two 32-bit halves per step), then two

@@ -238,7 +238,8 @@ __device__ __forceinline__ float deq_elem(int type, const uint8_t *src, int64_t 
 __global__ void k_get_rows(int type, const uint8_t *__restrict__ src, int64_t K, int64_t N,
                            const int32_t *__restrict__ ids, float *__restrict__ y, int64_t ldy) {
     const int64_t t = blockIdx.y;
-    const int64_t r = ids[t];
+    // out-of-range ids (ggml asserts on the host) are clamped so a bad id cannot fault the device
+    const int64_t r = min(max((int64_t)ids[t], (int64_t)0), N - 1);
     const int be = ks_block_elems(type);
     const int64_t bpr = K / be, nb = bpr * N;
     for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < K; k += (int64_t)gridDim.x * blockDim.x)

@@ -964,6 +964,7 @@ __global__ void __launch_bounds__(256) k_argmax_final(const float2 *__restrict__
     const float2 p = part[threadIdx.x];
     float v = p.x; int i = __float_as_int(p.y);
     amax_block(v, i);
+    if (i == 0x7fffffff) i = 0;               // all-NaN logits: no comparison succeeded; keep the token id valid
     if (threadIdx.x == 0) { out[0] = i; if (tok) tok[0] = i; }
 }
 static int launch_argmax(kcpp_model *m) {

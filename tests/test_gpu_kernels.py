@@ -83,6 +83,14 @@ def _adversarial_acts(rng, n):
     blk[:] = np.float32(0.01)
     blk[0] = np.float32(127.0)
     blk[1:9] = np.array([0.5, 1.5, 2.5, -0.5, -1.5, 100.5, -126.5, 3.5], np.float32)
+    # |max| reached in several lanes of a block, the first occurrence negative, in a later lane and element
+    b2 = x[1536:1792]
+    b2[:] = (rng.standard_normal(256) * 0.1).astype(np.float32)
+    b2[37] = -7.0; b2[40] = 7.0; b2[200] = 7.0; b2[38] = -7.0
+    # and positive first, ties inside one lane only
+    b3 = x[2048:2304]
+    b3[:] = (rng.standard_normal(256) * 0.1).astype(np.float32)
+    b3[129] = 3.25; b3[130] = -3.25; b3[143] = 3.25
     return x
 
 
