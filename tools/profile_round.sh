@@ -13,6 +13,11 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o roof -- python3 bench.py --roofline-only > $OUT/write.log 2>&1 &&
 # 3: kernel-trace stats of the same command (average launch duration must agree with bench's HIP events)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o roof -- python3 bench.py --roofline-only > $OUT/trace.log 2>&1 &&
+# 5/6: memory-side bytes of the decode attention (k_fa_dec4 + k_fa_comb4 at 3850 cached keys, 32 layers' caches
+# rotated past the Infinity Cache), one counter per pass, and its kernel-trace stats
+FA_VARIANTS=3 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fa_fetch -o fa -- python3 tools/fa_dec_bench.py 3850 > $OUT/fa_fetch.log 2>&1 &&
+FA_VARIANTS=3 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/fa_write -o fa -- python3 tools/fa_dec_bench.py 3850 > $OUT/fa_write.log 2>&1 &&
+FA_VARIANTS=3 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/fa_trace -o fa -- python3 tools/fa_dec_bench.py 3850 > $OUT/fa_trace.log 2>&1 &&
 # 4: kernel-trace stats of a short full bench (prefill + decode), no CPU baseline
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench -o bench -- python3 bench.py --steps 32 --warmup 4 --no-cpu-baseline > $OUT/bench.log 2>&1
 rc=$?
