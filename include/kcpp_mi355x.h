@@ -87,6 +87,9 @@ int kcpp_gemv_q6k(const void *args, int mode, int pro, void *stream);
  * koboldcpp_amd/csrc/gemv_rs.hip); kcpp_gemv_dec dispatches these types here.  kcpp_rs_supported(type, K)
  * says whether a [K x N] weight of Q4_K / Q6_K (or its RS id) can be held in the RS layout. */
 int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
+/* q|k|v decode projection (mode 2, rms_norm + Q8_K prologue) with segments 0, 1 (q, k) in KT_Q4_K_RS and segment 2
+ * (v) in KT_Q6_K_RS -- the Q4_K_M "more bits" layers -- in one launch; -3 when the shape is not covered */
+int kcpp_gemv_rs_qkv_mixed(const void *args, void *stream);
 int kcpp_rs_supported(int type, int64_t K);
 
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */

@@ -367,6 +367,128 @@ int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
 }
 }  // namespace
 
+// ---------------------------------------------------------------- q|k (Q4_K_RS) + v (Q6_K_RS) in one launch
+// The Q4_K_M "more bits" layers keep attn_v in Q6_K: instead of a second launch for its 1024 rows (a latency-bound
+// kernel of its own: prologue, one group per wave, epilogue), segments 0 / 1 (q, k) run the Q4_K_RS path and
+// segment 2 (v) the Q6_K_RS path of one grid over the same LDS activation (rms_norm -> Q8_K prologue, both types'
+// vec_dot_type); groups are wave-uniform in type.  Mode 2 epilogue (RoPE + f16 q / K / V stores), R = 2.
+template <int NIA, int NIB, int MC>
+__global__ void __launch_bounds__(256) k_gemv_rs_qkv(const DecArgs a) {
+    using TA = RS<KT_Q4_K_RS>;
+    using TB = RS<KT_Q6_K_RS>;
+    constexpr int R = 2;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int K = (int)a.K, nsb = K / 256;
+    const int RBA = nsb * TA::BYTES, RBB = nsb * TB::BYTES;
+    const int npA = nsb * TA::PIECES_PER_SB, npB = nsb * TB::PIECES_PER_SB;
+    const int N0 = (int)a.N[0], N1 = (int)a.N[1], N2 = (int)a.N[2];
+    const int ngA = (N0 + N1) / R, ngroups = ngA + N2 / R;
+    const int nw = (int)gridDim.x * 4;
+    const int wid = (int)blockIdx.x * 4 + wave;
+    const typename TA::Lane lca = TA::lane_consts(lane);
+    const typename TB::Lane lcb = TB::lane_consts(lane);
+    auto group_rows = [&](int g, int &seg, int &row0) {
+        if (g < ngA) {
+            const int r = g * R;
+            seg = r < N0 ? 0 : 1;
+            row0 = seg == 0 ? r : r - N0;
+        } else {
+            seg = 2;
+            row0 = (g - ngA) * R;
+        }
+    };
+    struct BufA { typename TA::W w[NIA][R]; };
+    struct BufB { typename TB::W w[NIB][R]; };
+    auto issueA = [&](int g, BufA &b) {
+        int seg, row0;
+        group_rows(g, seg, row0);
+        const uint8_t *W = seg == 0 ? a.W[0] : a.W[1];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int i = 0; i < NIA; ++i) TA::load(W + (int64_t)(row0 + r) * RBA, nsb, min(lane + 64 * i, npA - 1), b.w[i][r]);
+    };
+    auto issueB = [&](int g, BufB &b) {
+        const int row0 = (g - ngA) * R;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int i = 0; i < NIB; ++i) TB::load(a.W[2] + (int64_t)(row0 + r) * RBB, nsb, min(lane + 64 * i, npB - 1), b.w[i][r]);
+    };
+    BufA ba;
+    BufB bb;
+    const int g0 = min(wid, ngroups - 1);
+    lean::ActPro<1, MC> pro;
+    pro.load(a);
+    if (g0 < ngA) issueA(g0, ba);
+    else issueB(g0, bb);
+    pro.compute(a, lds);
+    typename TA::Act xa[NIA];
+    typename TB::Act xb[NIB];
+#pragma unroll
+    for (int i = 0; i < NIA; ++i) TA::act(lds, K, min(TA::sb_of(lane, i), nsb - 1), lca, xa[i]);
+#pragma unroll
+    for (int i = 0; i < NIB; ++i) TB::act(lds, K, min(TB::sb_of(lane, i), nsb - 1), lcb, xb[i]);
+    float slot[R] = {0.0f, 0.0f};
+    int slot_g = -1;
+    int k = 0;
+    for (int g = wid; g < ngroups; g += nw, ++k) {
+        float acc[R] = {0.0f, 0.0f};
+        if (g < ngA) {
+            if (k) issueA(g, ba);
+#pragma unroll
+            for (int i = 0; i < NIA; ++i) {
+                const bool ok = (NIA * 64 == npA) || lane + 64 * i < npA;
+#pragma unroll
+                for (int r = 0; r < R; ++r) { const float p = TA::dot(ba.w[i][r], xa[i], lca); acc[r] += ok ? p : 0.0f; }
+            }
+        } else {
+            if (k) issueB(g, bb);
+#pragma unroll
+            for (int i = 0; i < NIB; ++i) {
+                const bool ok = (NIB * 64 == npB) || lane + 64 * i < npB;
+#pragma unroll
+                for (int r = 0; r < R; ++r) { const float p = TB::dot(bb.w[i][r], xb[i], lcb); acc[r] += ok ? p : 0.0f; }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_sum_f(acc[r]))));
+        const bool mine = lane == k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) slot[r] = mine ? acc[r] : slot[r];
+        slot_g = mine ? g : slot_g;
+    }
+    if (slot_g < 0) return;
+    int seg, row0;
+    group_rows(slot_g, seg, row0);
+    lean::store_group<R, 2>(a, seg, row0, slot);
+}
+
+// q|k|v decode projection with q, k in Q4_K_RS and v in Q6_K_RS (segments 0, 1, 2): one launch.  -3 when not covered.
+extern "C" int kcpp_gemv_rs_qkv_mixed(const void *args, void *stream) {
+    const DecArgs &a = *(const DecArgs *)args;
+    if (a.nseg != 3 || a.K % 256 || !kcpp_rs_supported(KT_Q4_K_RS, a.K) || !kcpp_rs_supported(KT_Q6_K_RS, a.K)) return -3;
+    if (a.N[0] % 2 || a.N[1] % 2 || a.N[2] % 2) return -5;
+    const int nsb = (int)(a.K / 256);
+    const int nia = (nsb * 8 + 63) / 64, nib = (nsb * 4 + 63) / 64, mc = (int)((a.K + 4095) / 4096);
+    const int64_t groups = (a.N[0] + a.N[1] + a.N[2]) / 2;
+    static const int b_env = getenv("KCPP_RS_QKV_BLOCKS") ? atoi(getenv("KCPP_RS_QKV_BLOCKS")) : 512;
+    int64_t nblk = std::min<int64_t>((groups + 3) / 4, b_env);
+    nblk = std::max<int64_t>(nblk, (groups + 255) / 256);
+    const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
+    hipStream_t s = (hipStream_t)stream;
+#define KCPP_QKVM(A_, B_, M_) hipLaunchKernelGGL((k_gemv_rs_qkv<A_, B_, M_>), dim3((unsigned)nblk), dim3(256), (size_t)abytes + 16, s, a)
+    if (nia == 2 && nib == 1 && mc == 1) KCPP_QKVM(2, 1, 1);          // n_embd 4096 (Llama-3-8B)
+    else if (nia == 4 && nib == 2 && mc == 2) KCPP_QKVM(4, 2, 2);     // n_embd 8192 (Llama-3-70B)
+    else if (nia == 1 && nib == 1 && mc == 1) KCPP_QKVM(1, 1, 1);
+    else return -3;
+#undef KCPP_QKVM
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
 // K coverage of the RS kernels (the runtime picks an RS layout only where this holds)
 extern "C" int kcpp_rs_supported(int type, int64_t K) {
     if (K % 256 || K < 256) return 0;

@@ -649,7 +649,18 @@ static int forward_layers_dec(kcpp_model *m) {
         }
         // measured: the forked graph replays slower than the serial one (453 vs 517 tok/s), so opt-in only
         static const int fork_env = getenv("KCPP_QKV_FORK") ? atoi(getenv("KCPP_QKV_FORK")) : 0;
-        if (nq == 2 && m->side && fork_env) {
+        static const int mixed_env = getenv("KCPP_QKV_MIXED") ? atoi(getenv("KCPP_QKV_MIXED")) : 1;
+        int mixed_rc = -3;
+        if (nq == 2 && mixed_env && qty[0] == KT_Q4_K_RS && qty[1] == KT_Q6_K_RS && qa[0].nseg == 2 && qa[1].nseg == 1 &&
+            qa[1].role[0] == 2) {
+            // q|k Q4_K + v Q6_K (Q4_K_M "more bits" layers): one launch (gemv_rs.hip k_gemv_rs_qkv)
+            DecArgs c = qa[0];
+            c.W[2] = qa[1].W[0]; c.N[2] = qa[1].N[0]; c.role[2] = 2; c.nseg = 3;
+            mixed_rc = kcpp_gemv_rs_qkv_mixed(&c, s);
+            if (mixed_rc != -3 && mixed_rc != -5) RC(mixed_rc);
+        }
+        if (mixed_rc == 0) {
+        } else if (nq == 2 && m->side && fork_env) {
             RT_CHECK(hipEventRecord(m->ev_fork, s));
             RT_CHECK(hipStreamWaitEvent(m->side, m->ev_fork, 0));
             RC(kcpp_gemv_dec(qty[1], &qa[1], 2, 1, 2, m->side));
