@@ -349,6 +349,10 @@ int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
     else if (mode == 2) { R = 2; B = 512; }
     else if (ntot > 16384) { R = 2; B = 512; }
     else if (a.K > 8192) { PF = TYPE == KT_Q4_K_RS; B = TYPE == KT_Q4_K_RS ? 256 : 512; }
+    else if (pro == 2) {                 // wo with its quantize prologue (every workgroup quantizes the input)
+        static const int wo_b = getenv("KCPP_RS_PRO2_BLOCKS") ? atoi(getenv("KCPP_RS_PRO2_BLOCKS")) : 512;
+        B = wo_b;
+    }
     if (r_env && mode == 0) R = r_env;
     if (pf_env >= 0) PF = pf_env;
     if (b_env) B = b_env;
