@@ -81,8 +81,6 @@ int kcpp_gemv_stream(int type, const void *args, int mode, int pro, void *stream
 /* the VALU-lean unit-per-lane Q4_K variant (koboldcpp_amd/csrc/gemv_q4k.hip), tried first for Q4_K;
  * -3 when not covered */
 int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream);
-/* the VALU-lean Q6_K variant (koboldcpp_amd/csrc/gemv_q6k.hip), tried first for Q6_K; -3 when not covered */
-int kcpp_gemv_q6k(const void *args, int mode, int pro, void *stream);
 /* single-token mat-vec over the row-major decode layouts KT_Q4_K_RS / KT_Q6_K_RS (type ids 112 / 114,
  * koboldcpp_amd/csrc/gemv_rs.hip); kcpp_gemv_dec dispatches these types here.  kcpp_rs_supported(type, K)
  * says whether a [K x N] weight of Q4_K / Q6_K (or its RS id) can be held in the RS layout. */
@@ -112,7 +110,8 @@ int kcpp_kv_shift_rows(const uint16_t *kc, const uint16_t *vc, uint16_t *ks, uin
 int kcpp_rope_kv(const float *qkv, int64_t ldqkv, float *q_out, uint16_t *q16, uint16_t *kc, uint16_t *vc, int T,
                  int H, int HKV, int D, int n_past, const int32_t *pos_dev, const void *rope_tab, void *stream);
 /* flash attention over the f16 cache (ggml_cuda_flash_attn_ext, fattn.cu:298-345) */
-/* force_path: 0 auto, 1 split-KV decode, 2 FMA-tiled prefill, 3 MFMA prefill (D = 128, H = 4 HKV) */
+/* force_path: 0 auto, 1 decode (T = 1: k_fa_dec4 splits + k_fa_comb4), 2 FMA-tiled prefill, 3 MFMA prefill
+ * (D = 128, H = 4 HKV), 6 decode through the 64-key chunked kernel even at T = 1 */
 int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max);
 int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qout, void *ws,
                     int T, int H, int HKV, int D, int n_past, const int32_t *n_past_dev, int n_kv_max, float scale,
@@ -144,8 +143,8 @@ int kcpp_flash_attn_q(int tk, int tv, const float *q, int64_t ldq, const void *k
                       int H, int HKV, int D, int64_t n_ctx, int n_past, const int32_t *n_past_dev, float scale,
                       void *stream);
 /* single-token decode attention with explicit cache strides in elements (key p of kv head hk at
- * kc + p*kv_ld + hk*kv_hs); variant 0: 64-key chunks + combine, 1: splits with in-launch merge, 2: splits +
- * combine (A/B measurement entry, tools/fa_dec_bench.py) */
+ * kc + p*kv_ld + hk*kv_hs); variant 0: 64-key chunks + combine, 3: the production k_fa_dec4 splits +
+ * k_fa_comb4 (A/B measurement entry, tools/fa_dec_bench.py) */
 int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
                       float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
                       int n_kv_max, float scale, int variant, void *stream);

@@ -18,23 +18,20 @@
 #define FA_CHUNK 64
 #define FA_MAXG 8
 #define FA_WS_TICKETS 256
-#define FA_MAX_CHUNKS 2048
-static void *g_fa_stamps = nullptr;       // diagnostic stamp buffer (tools only; kcpp_fa_set_stamps)          // k_fa_combine's chunk-weight table: 2048 x 64 = 131072 keys
+#define FA_MAX_CHUNKS 2048          // k_fa_combine's chunk-weight table: 2048 x 64 = 131072 keys
+static void *g_fa_stamps = nullptr;       // diagnostic stamp buffer (tools only; kcpp_fa_set_stamps)
 
 // K/V cache layout: [pos][HKV][D] f16, row stride EKV = HKV*D elements.
 // Query layout: q16 [T][H][D] f16.  Query t sits at absolute position n_past + t.
-// One workgroup = (128-key chunk, kv head, query); its G = H/HKV query heads share every K/V row
-// (GQA).  Wave w owns keys 32w..32w+31.  Scores: 16 lanes x 16 B per K row; P.V: lane owns two
-// dims and reads one dword of each V row (no cross-lane reduction).  The last workgroup of a
-// (query, kv head) to finish -- an agent-scope release/acquire ticket (cdna_hip_programming.md
-// Guideline 16) -- merges the chunk partials and, for G >= 2, quantizes the heads' output to
-// Q8_K for wo (replaces the reference's separate flash_attn_combine_results launch,
-// ggml/src/ggml-cuda/fattn-common.cuh:523).
-template <int D, int G, bool FUSED>
+// One workgroup = (64-key chunk, kv head, query); its G = H/HKV query heads share every K/V row
+// (GQA).  Scores: 16 lanes x 16 B per K row; P.V: lane owns two dims and reads one dword of each V
+// row (no cross-lane reduction).  Partials (O, m, l) per chunk, merged by k_fa_combine (the role of the
+// reference's flash_attn_combine_results, ggml/src/ggml-cuda/fattn-common.cuh:523).  Used for 2..16
+// queries (single-token decode runs k_fa_dec4) and by the ggml-op form.
+template <int D, int G>
 __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
                                                    const uint16_t *__restrict__ vc, float *__restrict__ part_o,
-                                                   float2 *__restrict__ part_ml, int *__restrict__ tickets,
-                                                   float *__restrict__ out, uint8_t *__restrict__ qout, int T, int H,
+                                                   float2 *__restrict__ part_ml, int T, int H,
                                                    int HKV, int n_past_arg, const int32_t *__restrict__ n_past_dev,
                                                    int n_chunks, float scale, const uint16_t *__restrict__ mask,
                                                    int64_t mask_ld, int64_t kv_ld, int64_t kv_hs) {
@@ -45,7 +42,6 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
     // (= n_past_arg) keys under the mask (none if mask is null)
     const int kend = mask_ld >= 0 ? n_past_arg : n_past + t + 1;   // exclusive
     if (c * FA_CHUNK >= kend) return;                    // chunk unused by this query (graph-static grid)
-    const int nused = (kend - 1) / FA_CHUNK + 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int p0 = c * FA_CHUNK;
     const int p1 = min(p0 + FA_CHUNK, kend);              // exclusive
@@ -53,7 +49,6 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
     __shared__ float s_sc[G][FA_CHUNK];
     __shared__ float s_red[4][G][D];
     __shared__ float s_m[G], s_l[G];
-    __shared__ int s_last;
 
     const int sub = lane & 15, kq = lane >> 4;
     float qv[G][8];
@@ -138,395 +133,6 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
         part_o[(((int64_t)t * H + hk * G + g) * n_chunks + c) * D + d] = o;
     }
     if (threadIdx.x < G) part_ml[((int64_t)t * H + hk * G + threadIdx.x) * n_chunks + c] = make_float2(s_m[threadIdx.x], s_l[threadIdx.x]);
-    if constexpr (!FUSED) return;
-    // ---- ticket: the last chunk of (t, hk) to finish merges the partials
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int prev = __hip_atomic_fetch_add(&tickets[t * HKV + hk], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == nused - 1;
-        if (s_last) {
-            __hip_atomic_store(&tickets[t * HKV + hk], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // chunk weights exp(m_c - M) per head; the denominators
-    __shared__ float s_w[G][4096 / FA_CHUNK * 4];
-    for (int g = wave; g < G; g += 4) {
-        const float2 *ml = part_ml + ((int64_t)t * H + hk * G + g) * n_chunks;
-        float M = -INFINITY;
-        for (int cc = lane; cc < nused; cc += 64) M = fmaxf(M, ml[cc].x);
-        M = wave_max_dpp(M);
-        float L = 0.0f;
-        for (int cc = lane; cc < nused; cc += 64) {
-            const float2 v = ml[cc];
-            const float wgt = v.x == -INFINITY ? 0.0f : expf(v.x - M);
-            s_w[g][cc] = wgt;
-            L = fmaf(wgt, v.y, L);
-        }
-        L = wave_sum_f(L);
-        if (lane == 0) s_l[g] = L;
-    }
-    __syncthreads();
-    float *s_out = &s_red[0][0][0];                        // reuse: G*D floats
-    for (int i = threadIdx.x; i < G * D; i += 256) {
-        const int g = i / D, d = i % D;
-        const float *po = part_o + ((int64_t)t * H + hk * G + g) * n_chunks * D + d;
-        float O0 = 0.0f, O1 = 0.0f, O2 = 0.0f, O3 = 0.0f;
-        int cc = 0;
-        for (; cc + 4 <= nused; cc += 4) {
-            O0 = fmaf(s_w[g][cc], po[(int64_t)cc * D], O0);
-            O1 = fmaf(s_w[g][cc + 1], po[(int64_t)(cc + 1) * D], O1);
-            O2 = fmaf(s_w[g][cc + 2], po[(int64_t)(cc + 2) * D], O2);
-            O3 = fmaf(s_w[g][cc + 3], po[(int64_t)(cc + 3) * D], O3);
-        }
-        for (; cc < nused; ++cc) O0 = fmaf(s_w[g][cc], po[(int64_t)cc * D], O0);
-        const float r = ((O0 + O1) + (O2 + O3)) / s_l[g];
-        s_out[i] = r;
-        if (out) out[(int64_t)t * H * D + (int64_t)(hk * G + g) * D + d] = r;
-    }
-    if (qout == nullptr || G * D < 256) return;
-    __syncthreads();
-    // quantize the G*D outputs (G*D/256 Q8_K super-blocks of this kv head's query heads)
-    const int nsbk = G * D / 256;
-    if ((int)threadIdx.x < nsbk * 16) {
-        const int sbl = threadIdx.x >> 4, l16 = threadIdx.x & 15;
-        float v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = s_out[sbl * 256 + 16 * l16 + k];
-        const int64_t E = (int64_t)H * D, nsb = E / 256;
-        const int64_t sbg = (int64_t)hk * nsbk + sbl;      // super-block index within the row
-        int8_t *qs = (int8_t *)qout + (int64_t)t * E + sbg * 256;
-        float *dp = (float *)(qout + (int64_t)T * E) + (int64_t)t * nsb + sbg;
-        int16_t *bs = (int16_t *)(qout + (int64_t)T * E + (int64_t)T * nsb * 4) + (int64_t)t * (E / 16) + sbg * 16;
-        q8k_quant16(v, l16, qs, dp, bs);
-    }
-}
-
-// ---------------------------------------------------------------- decode v2: split-KV + in-launch merge
-// One token (T = 1).  Grid (NS splits, kv head), 512 threads, one workgroup per CU at NS = 32 x 8 kv heads.
-// Split sp owns keys [p0, p1) of the causal window [0, n_past]; it streams them in 128-key sub-chunks, the
-// next one's loads issued before the current one is used (wave w: keys 16w + 4i + (lane >> 4), i < 4; a 16-lane row holds one K row and one V row, 8 dims per
-// lane), keeps an online softmax per wave, merges its 4 waves in LDS and publishes (m, l, O) of its G
-// heads WRITE-THROUGH (sc1 stores), then adds to the kv head's ticket.  The split whose add comes last
-// merges all NS partials with sc1 loads (MI355X_MICROARCH.md, visibility table row 1: one lane per storing
-// workgroup adds to one unsharded counter after every storing wave's vmcnt(0) + barrier; the last adder
-// loads), writes the f32 output and the Q8_K activation of wo, and resets the ticket.  Replaces the
-// reference's flash_attn_vec_ext + flash_attn_combine_results pair (fattn-vec-f16.cuh:4-299,
-// fattn-common.cuh:523) and this file's k_fa_decode + k_fa_combine pair (two launches, 1 MB of partials).
-typedef unsigned long long fa_u64;
-typedef unsigned int fa_v4u __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st_sc1_f2(float2 *p, float2 v) {
-    __hip_atomic_store((fa_u64 *)p, ((fa_u64)__float_as_uint(v.y) << 32) | __float_as_uint(v.x), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float2 ld_sc1_f2(const float2 *p) {
-    const fa_u64 x = __hip_atomic_load((fa_u64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return make_float2(__uint_as_float((uint32_t)x), __uint_as_float((uint32_t)(x >> 32)));
-}
-
-#define FA2_NS 32
-// FA2_W waves per workgroup (16 FA2_W-key sub-chunks): 8, or 4 at G = 8 (register budget)
-template <int G, int FA2_W = (G == 8 ? 4 : 8)>
-__global__ void __launch_bounds__(64 * FA2_W) k_fa_dec2(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
-                                                 const uint16_t *__restrict__ vc, float *__restrict__ part_o,
-                                                 float2 *__restrict__ part_ml, unsigned *__restrict__ tickets,
-                                                 float *__restrict__ out, uint8_t *__restrict__ qout, int H, int HKV,
-                                                 int n_past_arg, const int32_t *__restrict__ n_past_dev, float scale,
-                                                 int probe, int64_t kv_ld, int64_t kv_hs,
-                                                 unsigned long long *__restrict__ stamps) {
-    constexpr int D = 128;
-    // diagnostic phase stamps (tools/fa_dec_bench.py): s_memrealtime (100 MHz, chip-wide) per workgroup,
-    // written by lane 0 of wave 0 with a vector store; stamps == nullptr in every product launch
-    const int wg_id = blockIdx.y * gridDim.x + blockIdx.x;
-#define FA_STAMP(ph)                                                                                   \
-    if (stamps && threadIdx.x == 0) {                                                                  \
-        const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();                                \
-        __hip_atomic_store(&stamps[wg_id * 8 + (ph)], t_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); \
-    }
-    FA_STAMP(0);
-    const int sp = blockIdx.x, NS = gridDim.x, hk = blockIdx.y;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int sub = lane & 15, kq = lane >> 4;
-    const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
-    const int nkv = n_past + 1;
-    const int per = ((nkv + NS - 1) / NS + 3) & ~3;
-    const int p0 = min(sp * per, nkv), p1 = min(p0 + per, nkv);
-    __shared__ float s_o[FA2_W][G][D];
-    __shared__ float s_m[FA2_W][G], s_l[FA2_W][G];
-    __shared__ int s_last;
-
-    float qv[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const uint4 qq = *(const uint4 *)(q16 + (int64_t)(hk * G + g) * D + sub * 8);
-        const uint32_t w4[4] = {qq.x, qq.y, qq.z, qq.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) { qv[g][2 * i] = h2f(w4[i] & 0xFFFF); qv[g][2 * i + 1] = h2f(w4[i] >> 16); }
-    }
-    if (stamps) { if (qv[0][0] == 12345.0f) stamps[0] = 0; FA_STAMP(1); }
-    float m[G], l[G], acc[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        m[g] = -INFINITY; l[g] = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[g][e] = 0.0f;
-    }
-    const uint16_t *kb = kc + hk * kv_hs + sub * 8, *vb = vc + hk * kv_hs + sub * 8;
-    uint4 kk[4], vv[4];
-    auto load_kv = [&](int c0, uint4 (&kr)[4], uint4 (&vr)[4]) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int p = c0 + 16 * wave + 4 * i + kq;
-            kr[i] = p < p1 ? *(const uint4 *)(kb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int p = c0 + 16 * wave + 4 * i + kq;
-            vr[i] = p < p1 ? *(const uint4 *)(vb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
-        }
-    };
-    constexpr bool PF = true;                                       // register budget of the prefetch
-    if (PF && p0 < p1) load_kv(p0, kk, vv);
-    for (int c0 = p0; c0 < p1; c0 += 16 * FA2_W) {
-        uint4 kn[4], vn[4];
-        const bool nxt = PF && c0 + 16 * FA2_W < p1;
-        if (nxt) load_kv(c0 + 16 * FA2_W, kn, vn);
-        if (!PF) load_kv(c0, kk, vv);
-        float sc[G][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t w4[4] = {kk[i].x, kk[i].y, kk[i].z, kk[i].w};
-            float kf[8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { kf[2 * e] = h2f(w4[e] & 0xFFFF); kf[2 * e + 1] = h2f(w4[e] >> 16); }
-            const bool valid = c0 + 16 * wave + 4 * i + kq < p1;
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                float s = 0.0f;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) s = fmaf(qv[g][e], kf[e], s);
-                s += dpp_f<0xB1>(s); s += dpp_f<0x4E>(s); s += dpp_f<0x141>(s); s += dpp_f<0x140>(s);
-                sc[g][i] = valid ? s * scale : -INFINITY;
-            }
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            float cm = fmaxf(fmaxf(sc[g][0], sc[g][1]), fmaxf(sc[g][2], sc[g][3]));
-            cm = xmax32(xmax16(cm));
-            const float mn = fmaxf(m[g], cm);
-            if (mn == -INFINITY) continue;                          // nothing valid yet (wave-uniform)
-            const float alpha = m[g] == -INFINITY ? 0.0f : expf(m[g] - mn);
-            m[g] = mn;
-            float pr[4];
-            float ls = 0.0f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) { pr[i] = sc[g][i] == -INFINITY ? 0.0f : expf(sc[g][i] - mn); ls += pr[i]; }
-            l[g] = fmaf(l[g], alpha, ls);                           // lane-partial over its own keys
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[g][e] *= alpha;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t w4[4] = {vv[i].x, vv[i].y, vv[i].z, vv[i].w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    acc[g][2 * e] = fmaf(pr[i], h2f(w4[e] & 0xFFFF), acc[g][2 * e]);
-                    acc[g][2 * e + 1] = fmaf(pr[i], h2f(w4[e] >> 16), acc[g][2 * e + 1]);
-                }
-            }
-        }
-        if (nxt) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) { kk[i] = kn[i]; vv[i] = vn[i]; }
-        }
-    }
-    FA_STAMP(2);
-    // wave merge over its 4 key rows (kq): m is wave-uniform, l and acc are per row
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        l[g] = xsum32(xsum16(l[g]));
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[g][e] = xsum32(xsum16(acc[g][e]));
-        if (kq == 0) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) s_o[wave][g][sub * 8 + e] = acc[g][e];
-        }
-        if (lane == 0) { s_m[wave][g] = m[g]; s_l[wave][g] = l[g]; }
-    }
-    __syncthreads();
-    // workgroup merge of the waves -> this split's partial, published write-through (16-B sc1 stores)
-    float2 *pml = part_ml + ((int64_t)hk * NS + sp) * G;
-    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(part_o, 0, 0x7FFFFFFF, 0x00020000);
-    for (int j = tid; j < G * D / 4; j += 64 * FA2_W) {
-        const int g = (4 * j) / D, d = (4 * j) % D;
-        float M = s_m[0][g];
-#pragma unroll
-        for (int w = 1; w < FA2_W; ++w) M = fmaxf(M, s_m[w][g]);
-        float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (M != -INFINITY) {
-#pragma unroll
-            for (int w = 0; w < FA2_W; ++w) {
-                const float wt = s_m[w][g] == -INFINITY ? 0.0f : expf(s_m[w][g] - M);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = fmaf(wt, s_o[w][g][d + e], o[e]);
-            }
-        }
-        const fa_v4u v = {__float_as_uint(o[0]), __float_as_uint(o[1]), __float_as_uint(o[2]), __float_as_uint(o[3])};
-        __builtin_amdgcn_raw_buffer_store_b128(v, prs, (int)((((int64_t)hk * NS + sp) * G * D + g * D + d) * 4), 0, 16);
-    }
-    if (tid < G) {
-        const int g = tid;
-        float M = s_m[0][g];
-#pragma unroll
-        for (int w = 1; w < FA2_W; ++w) M = fmaxf(M, s_m[w][g]);
-        float L = 0.0f;
-        if (M != -INFINITY) {
-#pragma unroll
-            for (int w = 0; w < FA2_W; ++w) L = fmaf(s_m[w][g] == -INFINITY ? 0.0f : expf(s_m[w][g] - M), s_l[w][g], L);
-        }
-        st_sc1_f2(pml + g, make_float2(M, L));
-    }
-    FA_STAMP(3);
-    if (tickets == nullptr) {                                       // partials only (combine kernel follows)
-        if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(4); }
-        return;
-    }
-    if (probe != 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    FA_STAMP(4);
-    __syncthreads();
-    if (tid == 0) {
-        const unsigned prev = __hip_atomic_fetch_add(&tickets[hk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = prev == (unsigned)(NS - 1);
-        if (s_last) __hip_atomic_store(&tickets[hk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    FA_STAMP(5);
-    if (!s_last || probe == 3) return;
-    // ---- last split of this kv head: merge the NS partials (sc1 loads only).  SS adjacent lanes share one
-    // 4-dim quad of one head, each loading every SS-th split (16-B loads, all issued before use), then
-    // reduce over the SS lanes: every thread of the workgroup has <= PER partials in flight.
-    float *s_res = &s_o[0][0][0];                                  // reuse: G*D floats
-    {
-        constexpr int NQ = G * D / 4, NT = 64 * FA2_W;
-        constexpr int SS = NT / NQ >= 1 ? NT / NQ : 1, PER = (FA2_NS + SS - 1) / SS;
-        if (tid < NQ * SS) {
-            const int q = tid / SS, sub = tid % SS;
-            const int g = q / (D / 4), d = 4 * (q % (D / 4));
-            float2 ml[PER];
-            fa_v4u ov[PER];
-#pragma unroll
-            for (int k = 0; k < PER; ++k) {
-                const int s2 = sub + SS * k;
-                ml[k] = s2 < NS ? ld_sc1_f2(part_ml + ((int64_t)hk * NS + s2) * G + g) : make_float2(-INFINITY, 0.0f);
-                ov[k] = s2 < NS ? __builtin_amdgcn_raw_buffer_load_b128(prs, (int)((((int64_t)hk * NS + s2) * G * D + g * D + d) * 4), 0, 16)
-                                : fa_v4u{0u, 0u, 0u, 0u};
-            }
-            float M = -INFINITY;
-#pragma unroll
-            for (int k = 0; k < PER; ++k) M = fmaxf(M, ml[k].x);
-#pragma unroll
-            for (int o_ = 1; o_ < SS; o_ <<= 1) M = fmaxf(M, __shfl_xor(M, o_, 64));
-            float L = 0.0f, o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-            for (int k = 0; k < PER; ++k) {
-                const float wt = ml[k].x == -INFINITY ? 0.0f : expf(ml[k].x - M);
-                L = fmaf(wt, ml[k].y, L);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] = fmaf(wt, __uint_as_float(ov[k][e]), o[e]);
-            }
-#pragma unroll
-            for (int o_ = 1; o_ < SS; o_ <<= 1) {
-                L += __shfl_xor(L, o_, 64);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] += __shfl_xor(o[e], o_, 64);
-            }
-            if (sub == 0) {
-                const float4 r = make_float4(o[0] / L, o[1] / L, o[2] / L, o[3] / L);
-                *(float4 *)&s_res[g * D + d] = r;
-                if (out) *(float4 *)(out + (int64_t)(hk * G + g) * D + d) = r;
-            }
-        }
-    }
-    FA_STAMP(6);
-    if (qout == nullptr || G * D < 256) return;
-    __syncthreads();
-    const int nsbk = G * D / 256;
-    if (tid < nsbk * 16) {
-        const int sbl = tid >> 4, l16 = tid & 15;
-        float v[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) v[k] = s_res[sbl * 256 + 16 * l16 + k];
-        const int64_t E = (int64_t)H * D, nsb = E / 256;
-        const int64_t sbg = (int64_t)hk * nsbk + sbl;
-        int8_t *qs = (int8_t *)qout + sbg * 256;
-        float *dp = (float *)(qout + E) + sbg;
-        int16_t *bs = (int16_t *)(qout + E + nsb * 4) + sbg * 16;
-        q8k_quant16(v, l16, qs, dp, bs);
-    }
-    if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(7); }
-#undef FA_STAMP
-}
-
-// combine of k_fa_dec2's partials (decode v3 = k_fa_dec2 without tickets + this): one 256-thread workgroup
-// per head pair (= one Q8_K block of 256); 4 adjacent lanes share a 4-dim quad of one head and each loads
-// every 4th split (<= 8 x 16-B O loads + 8 x 8-B (m, l) loads per thread, all issued before use), then
-// reduce over the 4 lanes.  One barrier, before the Q8_K quantization of the pair's 256 outputs.
-template <int G, bool QUANT>
-__global__ void __launch_bounds__(256) k_fa_combine2(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
-                                                    float *__restrict__ out, uint8_t *__restrict__ qout, int H, int NS) {
-    constexpr int D = 128, SS = 4, PER = FA2_NS / SS;
-    const int pair = blockIdx.x, tid = threadIdx.x;
-    const int hl = tid >> 7, r = tid & 127, q = r >> 2, sub = r & 3;
-    const int h = 2 * pair + hl, hk = h / G, g = h % G, d = 4 * q;
-    __shared__ float s_res[2 * D];
-    float2 ml[PER];
-    float4 ov[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const int s2 = sub + SS * k;
-        ml[k] = s2 < NS ? part_ml[((int64_t)hk * NS + s2) * G + g] : make_float2(-INFINITY, 0.0f);
-        ov[k] = s2 < NS ? *(const float4 *)(part_o + (((int64_t)hk * NS + s2) * G + g) * D + d) : make_float4(0, 0, 0, 0);
-    }
-    float M = -INFINITY;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) M = fmaxf(M, ml[k].x);
-    M = fmaxf(M, __shfl_xor(M, 1, 64));
-    M = fmaxf(M, __shfl_xor(M, 2, 64));
-    float L = 0.0f, o0 = 0.0f, o1 = 0.0f, o2 = 0.0f, o3 = 0.0f;
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-        const float wt = ml[k].x == -INFINITY ? 0.0f : expf(ml[k].x - M);
-        L = fmaf(wt, ml[k].y, L);
-        o0 = fmaf(wt, ov[k].x, o0); o1 = fmaf(wt, ov[k].y, o1);
-        o2 = fmaf(wt, ov[k].z, o2); o3 = fmaf(wt, ov[k].w, o3);
-    }
-#pragma unroll
-    for (int x = 1; x <= 2; x <<= 1) {
-        L += __shfl_xor(L, x, 64);
-        o0 += __shfl_xor(o0, x, 64); o1 += __shfl_xor(o1, x, 64);
-        o2 += __shfl_xor(o2, x, 64); o3 += __shfl_xor(o3, x, 64);
-    }
-    if (sub == 0) {
-        const float4 res = make_float4(o0 / L, o1 / L, o2 / L, o3 / L);
-        *(float4 *)&s_res[hl * D + d] = res;
-        if (out) *(float4 *)(out + (int64_t)h * D + d) = res;
-    }
-    if constexpr (QUANT) {
-        __syncthreads();
-        if (tid < 16) {
-            float v[16];
-#pragma unroll
-            for (int k = 0; k < 16; ++k) v[k] = s_res[16 * tid + k];
-            const int64_t E = (int64_t)H * D, nsb = E / 256;
-            q8k_quant16(v, tid, (int8_t *)qout + pair * 256, (float *)(qout + E) + pair,
-                        (int16_t *)(qout + E + nsb * 4) + pair * 16);
-        }
-    }
 }
 
 #define FA_STAMP(ph)                                                                                   \
@@ -542,13 +148,12 @@ __global__ void __launch_bounds__(256) k_fa_combine2(const float *__restrict__ p
 // DPP reduction; online softmax per wave (m, l wave-uniform); O: each lane accumulates its 8 dims over its
 // row's keys, rows summed once at the end (permlane swaps), waves merged in LDS.  Partials: O [H][NS][128],
 // (m, l) [H][NS] (m = -inf for an empty split).
-template <int G, bool MERGE>
+template <int G>
 __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
                                                  const uint16_t *__restrict__ vc, float *__restrict__ part_o,
                                                  float2 *__restrict__ part_ml, int H, int n_past_arg,
                                                  const int32_t *__restrict__ n_past_dev, int NS, float scale,
-                                                 int64_t kv_ld, int64_t kv_hs, unsigned long long *stamps,
-                                                 unsigned *__restrict__ tickets, float *__restrict__ out) {
+                                                 int64_t kv_ld, int64_t kv_hs, unsigned long long *stamps) {
     constexpr int D = 128;
     const int sp = blockIdx.x, hk = blockIdx.y;
     const int wg_id = blockIdx.y * gridDim.x + blockIdx.x;
@@ -724,57 +329,6 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
     }
     FA_STAMP(4);
     if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(5); }
-    if constexpr (MERGE) {
-        // the last split of this kv head to finish merges all NS partials (release / agent-scope ticket /
-        // acquire, as k_fa_decode's fused form) and writes the f32 attention output
-        __shared__ int s_last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned prev = __hip_atomic_fetch_add(&tickets[hk], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = prev == (unsigned)(NS - 1);
-            if (s_last) {
-                __hip_atomic_store(&tickets[hk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
-        __syncthreads();
-        if (!s_last) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        FA_STAMP(6);
-        // split weights: wave w forms exp2(m_s - M) of heads w, w + 4 in LDS (NS <= 64 = one lane each)
-        __shared__ float s_sw[G][64];
-        __shared__ float s_sl[G];
-        for (int g = wave; g < G; g += 4) {
-            const float2 v = lane < NS ? part_ml[(int64_t)(hk * G + g) * NS + lane] : make_float2(-INFINITY, 0.0f);
-            const float M = wave_max_dpp(v.x);
-            const float wt = v.x == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(v.x - M);
-            s_sw[g][lane] = wt;
-            const float L = wave_sum_f(wt * v.y);
-            if (lane == 0) s_sl[g] = L;
-        }
-        __syncthreads();
-        for (int i = tid; i < G * D; i += 256) {
-            const int g = i / D, d = i % D;
-            const float *po = part_o + (int64_t)(hk * G + g) * NS * D + d;
-            float ov[64];
-#pragma unroll
-            for (int s2 = 0; s2 < 64; ++s2) ov[s2] = s2 < NS ? po[(int64_t)s2 * D] : 0.0f;
-            float O0 = 0.0f, O1 = 0.0f, O2 = 0.0f, O3 = 0.0f;
-#pragma unroll
-            for (int s2 = 0; s2 < 64; s2 += 4) {
-                O0 = fmaf(s_sw[g][s2], ov[s2], O0);
-                O1 = fmaf(s_sw[g][s2 + 1], ov[s2 + 1], O1);
-                O2 = fmaf(s_sw[g][s2 + 2], ov[s2 + 2], O2);
-                O3 = fmaf(s_sw[g][s2 + 3], ov[s2 + 3], O3);
-            }
-            out[(int64_t)(hk * G + g) * D + d] = ((O0 + O1) + (O2 + O3)) / s_sl[g];
-        }
-        if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(7); }
-    }
 }
 
 // combine of k_fa_dec4's partials (m in the exp2 domain): grid (H / 2), 256 threads = 2 heads x 128 dims
@@ -852,25 +406,18 @@ static int fa4_launch(const uint16_t *q16, const uint16_t *kc, const uint16_t *v
     float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
     float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
     const dim3 grid(NS, HKV);
-    // in-launch merge by the last split of each kv head: opt-in only -- measured 17.9 vs 12.3 us per layer at 3850
-    // keys (tools/fa_dec_bench.py variant 4 vs 3: the agent-scope ticket lands ~5 us after the partial stores and
-    // the single merging workgroup per kv head reads its 64 KB of partials in ~4.6 us), the combine launch is cheaper
-    static const int merge_env = getenv("KCPP_FA4_MERGE") ? atoi(getenv("KCPP_FA4_MERGE")) : 0;
-    const bool merge = merge_env && qout == nullptr && out != nullptr && HKV * 4 <= FA_WS_TICKETS;
-    unsigned *tk = (unsigned *)ws;
+    // (an in-launch merge by the last split of each kv head measured 17.9 vs 12.3 us per layer at 3850 keys: the
+    // agent-scope ticket lands ~5 us after the partial stores and one workgroup per kv head reads 64 KB of partials
+    // in ~4.6 us -- DESIGN.md §4; the combine launch is cheaper)
     unsigned long long *st = (unsigned long long *)g_fa_stamps;
-#define KCPP_FA4_CASE(GG)                                                                                               \
-    case GG:                                                                                                            \
-        if (merge) hipLaunchKernelGGL((k_fa_dec4<GG, true>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st, tk, out); \
-        else hipLaunchKernelGGL((k_fa_dec4<GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st, tk, out); \
-        break;
     switch (G) {
-        KCPP_FA4_CASE(1) KCPP_FA4_CASE(2) KCPP_FA4_CASE(4) KCPP_FA4_CASE(8)
+    case 1: hipLaunchKernelGGL(k_fa_dec4<1>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st); break;
+    case 2: hipLaunchKernelGGL(k_fa_dec4<2>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st); break;
+    case 4: hipLaunchKernelGGL(k_fa_dec4<4>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st); break;
+    case 8: hipLaunchKernelGGL(k_fa_dec4<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st); break;
     default: return -1;
     }
-#undef KCPP_FA4_CASE
     KCPP_CHECK(hipGetLastError());
-    if (merge) return 0;
     if (qout) hipLaunchKernelGGL(k_fa_comb4<true>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS, (unsigned long long *)g_fa_stamps);
     else hipLaunchKernelGGL(k_fa_comb4<false>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, NS, (unsigned long long *)g_fa_stamps);
     KCPP_CHECK(hipGetLastError());
@@ -1113,15 +660,13 @@ __global__ void __launch_bounds__(256) k_fa_prefill(const uint16_t *__restrict__
 
 extern "C" {
 
-// partial O + (m, l) per (query, head, chunk) + one ticket per (query, kv head).  The tickets must be
-// zero before first use (allocate zeroed); the merging workgroup resets its ticket.
+// partial O + (m, l) per (query, head, chunk / split) behind a 256-B header
 int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max) {
     const int64_t nch = (n_kv_max + FA_CHUNK - 1) / FA_CHUNK;
     // partial slots: T x nch chunks (k_fa_decode), at least the 64 splits k_fa_dec4 may use
     const int64_t slots = std::max<int64_t>((int64_t)T * nch, 64);
     return 256 + (int64_t)H * slots * (128 * 4 + 8) + (int64_t)T * H * 4 + 256;
 }
-// the first 256 B of the workspace are the decode-v2 tickets (one per kv head, zero between launches)
 
 // out f32 [T][H][D] (may be null), qout Q8_K act [T][H*D] (may be null), ws from kcpp_fa_workspace_bytes
 // n_past_dev (optional): device-resident n_past (graph-replayable decode); then n_kv_max
@@ -1140,44 +685,13 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
         return 0;
     }
     if (H / HKV > FA_MAXG) return -1;
-    const bool use_decode = force_path == 1 || force_path == 4 || force_path == 5 || (force_path == 0 && T <= 16);
-    static const int v2_env = getenv("KCPP_FA_V2") ? atoi(getenv("KCPP_FA_V2")) : 0;   // in-launch merge: slower end to end (422 vs 443 tok/s)
+    // force_path 0: auto (T <= 16 decode kernels, else prefill), 1: decode kernels, 2: tiled prefill, 3: MFMA
+    // prefill, 6: the 64-key-chunk decode kernel even for T = 1 (tests)
+    const bool use_decode = force_path == 1 || force_path == 6 || (force_path == 0 && T <= 16);
     const int G0 = H / HKV;
-    static const int v3_env = getenv("KCPP_FA_V3") ? atoi(getenv("KCPP_FA_V3")) : 0;
-    const bool v3 = (v3_env || force_path == 5) && !(force_path == 4);
-    static const int fa4_env = getenv("KCPP_FA4") ? atoi(getenv("KCPP_FA4")) : 1;
-    if (use_decode && T == 1 && (force_path == 0 || force_path == 1) && fa4_env && !v2_env && !v3_env && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) &&
-        (qout == nullptr || G0 >= 2))
+    if (use_decode && T == 1 && force_path != 6 && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) && (qout == nullptr || G0 >= 2))
         return fa4_launch(q16, kc, vc, (int64_t)HKV * 128, 128, out, qout, ws, H, HKV, n_past, n_past_dev,
                           n_past_dev ? n_kv_max : n_past + 1, scale, s);
-    if (use_decode && T == 1 && (v2_env || v3 || force_path == 4) && HKV <= 64 && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) && (qout == nullptr || G0 >= 2)) {
-        const int nkv = n_past_dev ? n_kv_max : n_past + 1;
-        const int NS = std::max(1, std::min(FA2_NS, (nkv + 127) / 128));   // >= 1 sub-chunk of 128 keys per split
-        static const int nomerge_env = getenv("KCPP_FA2_NOMERGE") ? atoi(getenv("KCPP_FA2_NOMERGE")) : 0;
-        const int nomerge = v3 ? 1 : nomerge_env;
-        unsigned *tickets = nomerge == 1 ? nullptr : (unsigned *)ws;
-        float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
-        float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
-        const dim3 grid(NS, HKV);
-        switch (G0) {
-        case 1: hipLaunchKernelGGL(k_fa_dec2<1>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge, (int64_t)HKV * 128, (int64_t)128, nullptr); break;
-        case 2: hipLaunchKernelGGL(k_fa_dec2<2>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge, (int64_t)HKV * 128, (int64_t)128, nullptr); break;
-        case 4: hipLaunchKernelGGL(k_fa_dec2<4>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge, (int64_t)HKV * 128, (int64_t)128, nullptr); break;
-        default: hipLaunchKernelGGL(k_fa_dec2<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, nomerge, (int64_t)HKV * 128, (int64_t)128, nullptr); break;
-        }
-        KCPP_CHECK(hipGetLastError());
-        if (v3) {
-#define KCPP_FA_C2(GG)                                                                                                     \
-    case GG:                                                                                                               \
-        if (qout) hipLaunchKernelGGL((k_fa_combine2<GG, true>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS); \
-        else hipLaunchKernelGGL((k_fa_combine2<GG, false>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS);    \
-        break;
-            switch (G0) { KCPP_FA_C2(1) KCPP_FA_C2(2) KCPP_FA_C2(4) KCPP_FA_C2(8) }
-#undef KCPP_FA_C2
-            KCPP_CHECK(hipGetLastError());
-        }
-        return 0;
-    }
     if (use_decode) {
         ws = (uint8_t *)ws + FA_WS_TICKETS;
         const int nkv = n_past_dev ? n_kv_max : n_past + T;
@@ -1186,22 +700,12 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
         float *po = (float *)ws;
         float2 *pml = (float2 *)(po + (int64_t)T * H * nch * 128);
         const dim3 grid(nch, HKV, T);
-        int *tickets = (int *)(pml + (int64_t)T * H * nch);
-        const int G = H / HKV;
-        static const int fuse_env = getenv("KCPP_FA_FUSED") ? atoi(getenv("KCPP_FA_FUSED")) : 0;
-        const bool fused = fuse_env && G >= 2 && nch <= 4096 / FA_CHUNK * 4;   // (its merge table: 16k keys)
 #define KCPP_FA_CASE(GG)                                                                                       \
     case GG:                                                                                                   \
-        if (fused)                                                                                             \
-            hipLaunchKernelGGL((k_fa_decode<128, GG, true>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, \
-                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale, nullptr, -1,   \
-                               (int64_t)HKV * 128, (int64_t)128);                                          \
-        else                                                                                                   \
-            hipLaunchKernelGGL((k_fa_decode<128, GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, \
-                               out, (uint8_t *)qout, T, H, HKV, n_past, n_past_dev, nch, scale, nullptr, -1,   \
-                               (int64_t)HKV * 128, (int64_t)128);                                          \
+        hipLaunchKernelGGL((k_fa_decode<128, GG>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, T, H, HKV,     \
+                           n_past, n_past_dev, nch, scale, nullptr, -1, (int64_t)HKV * 128, (int64_t)128);     \
         break;
-        switch (G) {
+        switch (G0) {
             KCPP_FA_CASE(1)
             KCPP_FA_CASE(2)
             KCPP_FA_CASE(4)
@@ -1210,14 +714,12 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
         }
 #undef KCPP_FA_CASE
         KCPP_CHECK(hipGetLastError());
-        if (!fused) {
-            if (qout)
-                hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, T), dim3(1024), 0, s, po, pml, out, (uint8_t *)qout, T,
-                                   H, D, n_past, n_past_dev, nch, 0);
-            else
-                hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, T), dim3(1024), 0, s, po, pml, out, (uint8_t *)nullptr,
-                                   T, H, D, n_past, n_past_dev, nch, 0);
-        }
+        if (qout)
+            hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, T), dim3(1024), 0, s, po, pml, out, (uint8_t *)qout, T,
+                               H, D, n_past, n_past_dev, nch, 0);
+        else
+            hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, T), dim3(1024), 0, s, po, pml, out, (uint8_t *)nullptr,
+                               T, H, D, n_past, n_past_dev, nch, 0);
         KCPP_CHECK(hipGetLastError());
         return 0;
     }
@@ -1240,10 +742,9 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
 
 // single-token decode attention with explicit cache strides (elements): key p of kv head hk starts at
 // kc + p * kv_ld + hk * kv_hs.  Position-major ggml view: kv_ld = HKV*D, kv_hs = D; head-major: kv_ld = D,
-// kv_hs = n_ctx*D.  variant 0: 64-key chunks + k_fa_combine; 1: NS splits, last arriver merges in-launch;
-// 2: NS splits + k_fa_combine2.  (tools/fa_dec_bench.py)
-
-void kcpp_fa_set_stamps(void *p) { g_fa_stamps = p; }     // diagnostic stamp buffer of k_fa_dec2 (tools only)
+// kv_hs = n_ctx*D.  variant 0: 64-key chunks + k_fa_combine; 3: k_fa_dec4 + k_fa_comb4 (the production kernel
+// pair).  A/B entry for tools/fa_dec_bench.py.
+void kcpp_fa_set_stamps(void *p) { g_fa_stamps = p; }     // diagnostic stamp buffer of k_fa_dec4 / k_fa_comb4 (tools only)
 int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
                       float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
                       int n_kv_max, float scale, int variant, void *stream) {
@@ -1252,63 +753,24 @@ int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *v
     if (H % HKV || !(G == 1 || G == 2 || G == 4 || G == 8) || (H % 2) || HKV > 64) return -1;
     if (qout && G < 2) return -1;
     const int nkv = n_past_dev ? n_kv_max : n_past + 1;
-    if (variant == 0) {
-        const int nch = (nkv + FA_CHUNK - 1) / FA_CHUNK;
-        if (nch > FA_MAX_CHUNKS) return -4;
-        float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
-        float2 *pml = (float2 *)(po + (int64_t)H * nch * 128);
-        const dim3 grid(nch, HKV, 1);
+    if (variant == 3) return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, nkv, scale, s);
+    if (variant != 0) return -1;
+    const int nch = (nkv + FA_CHUNK - 1) / FA_CHUNK;
+    if (nch > FA_MAX_CHUNKS) return -4;
+    float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
+    float2 *pml = (float2 *)(po + (int64_t)H * nch * 128);
+    const dim3 grid(nch, HKV, 1);
 #define KCPP_FA_CASE(GG)                                                                                         \
     case GG:                                                                                                     \
-        hipLaunchKernelGGL((k_fa_decode<128, GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, nullptr, out, \
-                           (uint8_t *)qout, 1, H, HKV, n_past, n_past_dev, nch, scale, nullptr, -1, kv_ld, kv_hs); \
+        hipLaunchKernelGGL((k_fa_decode<128, GG>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, 1, H, HKV, n_past, \
+                           n_past_dev, nch, scale, nullptr, -1, kv_ld, kv_hs);                                   \
         break;
-        switch (G) { KCPP_FA_CASE(1) KCPP_FA_CASE(2) KCPP_FA_CASE(4) KCPP_FA_CASE(8) }
+    switch (G) { KCPP_FA_CASE(1) KCPP_FA_CASE(2) KCPP_FA_CASE(4) KCPP_FA_CASE(8) }
 #undef KCPP_FA_CASE
-        KCPP_CHECK(hipGetLastError());
-        if (qout) hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, 1), dim3(1024), 0, s, po, pml, out, (uint8_t *)qout, 1, H, 128, n_past, n_past_dev, nch, 0);
-        else hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, 1), dim3(1024), 0, s, po, pml, out, (uint8_t *)nullptr, 1, H, 128, n_past, n_past_dev, nch, 0);
-        KCPP_CHECK(hipGetLastError());
-        return 0;
-    }
-    if (variant >= 10 && variant <= 13) {         // timing probes (tools/fa_dec_bench.py): pieces of variant 3
-        const int NS = fa4_splits(nkv, HKV);
-        float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
-        float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
-        const int32_t *npd = variant == 12 ? nullptr : n_past_dev;
-        const int np = variant == 12 ? nkv - 1 : n_past;
-        if (variant != 11 && G == 4)
-            hipLaunchKernelGGL((k_fa_dec4<4, false>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, np, npd, NS, scale, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps, (unsigned *)ws, out);
-        if (variant == 11 || variant == 13)
-            hipLaunchKernelGGL(k_fa_comb4<true>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS, (unsigned long long *)g_fa_stamps);
-        KCPP_CHECK(hipGetLastError());
-        return 0;
-    }
-    if (variant == 3) return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, nkv, scale, s);
-    if (variant == 4) return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, nullptr, ws, H, HKV, n_past, n_past_dev, nkv, scale, s);
-    const int NS = std::max(1, std::min(FA2_NS, (nkv + 127) / 128));
-    unsigned *tickets = variant == 1 ? (unsigned *)ws : nullptr;
-    float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
-    float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
-    const dim3 grid(NS, HKV);
-    const int probe = variant == 1 ? 0 : 1;
-    switch (G) {
-    case 1: hipLaunchKernelGGL(k_fa_dec2<1>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, probe, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
-    case 2: hipLaunchKernelGGL(k_fa_dec2<2>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, probe, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
-    case 4: hipLaunchKernelGGL(k_fa_dec2<4>, grid, dim3(512), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, probe, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
-    default: hipLaunchKernelGGL(k_fa_dec2<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, (uint8_t *)qout, H, HKV, n_past, n_past_dev, scale, probe, kv_ld, kv_hs, (unsigned long long *)g_fa_stamps); break;
-    }
     KCPP_CHECK(hipGetLastError());
-    if (variant == 2) {
-#define KCPP_FA_C2(GG)                                                                                                     \
-    case GG:                                                                                                               \
-        if (qout) hipLaunchKernelGGL((k_fa_combine2<GG, true>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS); \
-        else hipLaunchKernelGGL((k_fa_combine2<GG, false>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS);    \
-        break;
-        switch (G) { KCPP_FA_C2(1) KCPP_FA_C2(2) KCPP_FA_C2(4) KCPP_FA_C2(8) }
-#undef KCPP_FA_C2
-        KCPP_CHECK(hipGetLastError());
-    }
+    if (qout) hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, 1), dim3(1024), 0, s, po, pml, out, (uint8_t *)qout, 1, H, 128, n_past, n_past_dev, nch, 0);
+    else hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, 1), dim3(1024), 0, s, po, pml, out, (uint8_t *)nullptr, 1, H, 128, n_past, n_past_dev, nch, 0);
+    KCPP_CHECK(hipGetLastError());
     return 0;
 }
 
@@ -1342,13 +804,11 @@ int kcpp_flash_attn_ext(const float *q, int64_t q_nb1, int64_t q_nb2, const uint
         if (nch > FA_MAX_CHUNKS) return -4;
         float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
         float2 *pml = (float2 *)(po + (int64_t)T * H * nch * 128);
-        int *tickets = (int *)(pml + (int64_t)T * H * nch);
         const dim3 grid(nch, HKV, T);
 #define KCPP_FA_CASE(GG)                                                                                          \
     case GG:                                                                                                      \
-        hipLaunchKernelGGL((k_fa_decode<128, GG, false>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, tickets, out, \
-                           (uint8_t *)nullptr, T, H, HKV, n_kv, nullptr, nch, scale, mask, mask_ld,                \
-                           (int64_t)HKV * 128, (int64_t)128);                                                     \
+        hipLaunchKernelGGL((k_fa_decode<128, GG>), grid, dim3(256), 0, s, q16, kc, vc, po, pml, T, H, HKV, n_kv,   \
+                           nullptr, nch, scale, mask, mask_ld, (int64_t)HKV * 128, (int64_t)128);                 \
         break;
         switch (H / HKV) {
             KCPP_FA_CASE(1)

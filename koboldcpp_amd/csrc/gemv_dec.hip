@@ -17,11 +17,6 @@ extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int 
         const int rc = kcpp_gemv_q4k(args, mode, pro, stream);
         if (rc != -3) return rc;
     }
-    static const int use_q6k = getenv("KCPP_Q6K") ? atoi(getenv("KCPP_Q6K")) : 0;   // measured slower than gemv_dec_impl.h (head 125 vs 97 us)
-    if (use_q6k && type == KT_Q6_K) {
-        const int rc = kcpp_gemv_q6k(args, mode, pro, stream);
-        if (rc != -3) return rc;
-    }
     static const int use_stream = getenv("KCPP_STREAM") ? atoi(getenv("KCPP_STREAM")) : 1;
     if (use_stream) {
         const int rc = kcpp_gemv_stream(type, args, mode, pro, stream);

@@ -1,4 +1,4 @@
-// gemv_lean.h -- shared parts of the VALU-lean decode mat-vec kernels (gemv_q4k.hip, gemv_q6k.hip):
+// gemv_lean.h -- shared parts of the VALU-lean decode mat-vec kernels (gemv_q4k.hip, gemv_rs.hip):
 // the activation prologue (rms_norm * w -> Q8_K in LDS, or an already-quantized activation copied to
 // LDS) with its global loads issued before the first weight loads, and the epilogue that stores the
 // per-lane parked results (residual add / SiLU-GLU / RoPE + f16 K/V cache stores).

@@ -45,7 +45,6 @@ extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int 
 extern "C" int kcpp_gemv_stream(int type, const void *args, int mode, int pro, void *stream);
 // VALU-lean unit-per-lane Q4_K variant (gemv_q4k.hip); -3 = not covered
 extern "C" int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream);
-extern "C" int kcpp_gemv_q6k(const void *args, int mode, int pro, void *stream);
 
 
 // MFMA prefill flash attention (attn_mfma.hip); -3 = shape not covered (needs D = 128, H = 4 * HKV)

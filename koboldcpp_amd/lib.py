@@ -107,7 +107,6 @@ _L.kcpp_gemv_dec.argtypes = [I, P, I, I, I, P]
 _L.kcpp_gemv_dec_args_size.restype = I64
 _L.kcpp_gemv_stream.argtypes = [I, P, I, I, P]
 _L.kcpp_gemv_q4k.argtypes = [P, I, I, P]
-_L.kcpp_gemv_q6k.argtypes = [P, I, I, P]
 _L.kcpp_gemv_rs.argtypes = [I, P, I, I, P]
 _L.kcpp_rs_supported.argtypes = [I, I64]
 for _n, _a in _SIGS.items():
@@ -118,7 +117,7 @@ for _n, _r in _RES.items():
 
 def exported_symbols():
     return sorted(set(_SIGS) | set(_RES) | {"kcpp_vec_dot_type", "kcpp_gemv_dec", "kcpp_gemv_dec_args_size",
-                                             "kcpp_gemv_stream", "kcpp_gemv_q4k", "kcpp_gemv_q6k",
+                                             "kcpp_gemv_stream", "kcpp_gemv_q4k",
                                              "kcpp_gemv_rs", "kcpp_rs_supported"})
 
 

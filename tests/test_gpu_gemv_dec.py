@@ -71,7 +71,7 @@ CASES = [  # name, type, K, N, mode, pro
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
-@pytest.mark.parametrize("entry", ["dec", "stream", "q4k", "q6k"])
+@pytest.mark.parametrize("entry", ["dec", "stream", "q4k"])
 def test_gemv_dec_vs_unfused(env, case, entry):
     torch, K = env
     name, t, Kd, N, mode, pro = case
@@ -95,11 +95,10 @@ def test_gemv_dec_vs_unfused(env, case, entry):
         rc = int(K.raw().kcpp_gemv_stream(t, __import__("ctypes").byref(a), mode, pro, s))
         if rc == -3:
             pytest.skip("shape/type not covered by the streaming kernel")
-    elif entry in ("q4k", "q6k"):
-        if t != (R.Q4_K if entry == "q4k" else R.Q6_K):
+    elif entry == "q4k":
+        if t != R.Q4_K:
             pytest.skip("type-specific kernel")
-        fn = K.raw().kcpp_gemv_q4k if entry == "q4k" else K.raw().kcpp_gemv_q6k
-        rc = int(fn(__import__("ctypes").byref(a), mode, pro, s))
+        rc = int(K.raw().kcpp_gemv_q4k(__import__("ctypes").byref(a), mode, pro, s))
         if rc == -3:
             pytest.skip("shape not covered")
     else:

@@ -36,7 +36,7 @@ def main():
     for n_past in npasts:
         pos.fill_(n_past)
         for lname, (ld, hs) in layouts.items():
-            for var in [int(v) for v in os.environ.get('FA_VARIANTS', '0,1,2,3').split(',')]:
+            for var in [int(v) for v in os.environ.get('FA_VARIANTS', '0,3').split(',')]:
                 if var == 0 and n_past + 1 > 16384:
                     continue
 
@@ -73,7 +73,7 @@ def main():
 def stamps():
     """phase stamps (s_memrealtime, 100 MHz) for the last of 32 graph-replayed layers: per phase min / median /
     max over workgroups, microseconds after the earliest workgroup entry.  FA_STAMP_VARIANTS: kcpp_fa_decode_ex
-    variants (1 / 2: k_fa_dec2; 3: k_fa_dec4 (workgroups < 2048) + k_fa_comb4 (2048+))"""
+    variants (3: k_fa_dec4 (workgroups < 2048) + k_fa_comb4 (2048+))"""
     n_ctx = 4176
     L2 = 32
     kc = (torch.randn(L2, n_ctx * HKV * D, device="cuda") * 0.5).half()
@@ -84,11 +84,11 @@ def stamps():
     ws = torch.zeros(K.fa_workspace_bytes(16, H, n_ctx), dtype=torch.uint8, device="cuda")
     pos = torch.zeros(1, dtype=torch.int32, device="cuda")
     st = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
-    variants = [int(v) for v in os.environ.get("FA_STAMP_VARIANTS", "1,2").split(",")]
+    variants = [int(v) for v in os.environ.get("FA_STAMP_VARIANTS", "3").split(",")]
     for n_past in (100, 3850):
         pos.fill_(n_past)
         for var in variants:
-            lo, hi = (D, n_ctx * D) if var in (1, 2) else (HKV * D, D)
+            lo, hi = HKV * D, D
 
             def step():
                 sp = torch.cuda.current_stream().cuda_stream
