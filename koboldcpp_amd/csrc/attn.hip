@@ -334,9 +334,9 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
 // combine of k_fa_dec4's partials (m in the exp2 domain): grid (H / 2), 256 threads = 2 heads x 128 dims
 // (one Q8_K block of 256 when quantizing); thread (head, d) issues all NS partial loads of its dim (<= 64, in
 // flight together); one wave per head forms the split weights exp2(m_s - M) in LDS.
-template <bool QUANT>
+template <bool QUANT, int NS>
 __global__ void __launch_bounds__(256) k_fa_comb4(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
-                                                  float *__restrict__ out, uint8_t *__restrict__ qout, int H, int NS,
+                                                  float *__restrict__ out, uint8_t *__restrict__ qout, int H,
                                                   unsigned long long *stamps) {
     constexpr int D = 128, MAXS = 64;
     const int pair = blockIdx.x, tid = threadIdx.x;
@@ -347,9 +347,9 @@ __global__ void __launch_bounds__(256) k_fa_comb4(const float *__restrict__ part
     __shared__ float s_l[2];
     __shared__ float s_res[2 * D];
     const float *po = part_o + (int64_t)h * NS * D + d;
-    float ov[MAXS];
+    float ov[NS];
 #pragma unroll
-    for (int s = 0; s < MAXS; ++s) ov[s] = s < NS ? po[(int64_t)s * D] : 0.0f;
+    for (int s = 0; s < NS; ++s) ov[s] = po[(int64_t)s * D];
     if (d < 64) {                                        // wave 0 / 2: split weights of head hl
         const float2 v = d < NS ? part_ml[(int64_t)h * NS + d] : make_float2(-INFINITY, 0.0f);
         const float M = wave_max_dpp(v.x);
@@ -362,7 +362,7 @@ __global__ void __launch_bounds__(256) k_fa_comb4(const float *__restrict__ part
     FA_STAMP(1);
     float O0 = 0.0f, O1 = 0.0f, O2 = 0.0f, O3 = 0.0f;
 #pragma unroll
-    for (int s = 0; s < MAXS; s += 4) {
+    for (int s = 0; s < NS; s += 4) {
         O0 = fmaf(s_w[hl][s], ov[s], O0);
         O1 = fmaf(s_w[hl][s + 1], ov[s + 1], O1);
         O2 = fmaf(s_w[hl][s + 2], ov[s + 2], O2);
@@ -388,38 +388,62 @@ __global__ void __launch_bounds__(256) k_fa_comb4(const float *__restrict__ part
 
 #undef FA_STAMP
 
-// split count of k_fa_dec4: one workgroup per CU (256 / HKV splits; measured at 3850 cached keys,
-// tools/fa_dec_bench.py: 7.8 us vs 8.7 at 512 workgroups).  Independent of the context size, so the key
-// partition -- and the result, bit for bit -- depends on the cached keys only (empty splits exit early).
-static int fa4_splits(int n_kv_max, int HKV) {
-    (void)n_kv_max;
-    static const int ns_env = getenv("KCPP_FA4_NS") ? atoi(getenv("KCPP_FA4_NS")) : 0;
-    const int ns = ns_env > 0 ? ns_env : 256 / HKV;
-    return std::max(1, std::min(ns, 64));
+// split count of k_fa_dec4: one workgroup per CU (256 / HKV splits, rounded down to a power of two in [4, 64];
+// measured at 3850 cached keys, tools/fa_dec_bench.py: 7.8 us vs 8.7 at 512 workgroups).  Independent of the
+// context size, so the key partition -- and the result, bit for bit -- depends on the cached keys only.
+static int fa4_splits(int HKV) {
+    int ns = 4;
+    while (ns < 64 && 2 * ns * HKV <= 256) ns *= 2;
+    return ns;
 }
 
-static int fa4_launch(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
-                      float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
-                      int n_kv_max, float scale, hipStream_t s) {
-    const int G = H / HKV;
-    const int NS = fa4_splits(n_kv_max, HKV);
+template <int G, int NS>
+static void fa4_dispatch(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
+                         float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
+                         float scale, hipStream_t s) {
     float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
     float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
-    const dim3 grid(NS, HKV);
-    // (an in-launch merge by the last split of each kv head measured 17.9 vs 12.3 us per layer at 3850 keys: the
-    // agent-scope ticket lands ~5 us after the partial stores and one workgroup per kv head reads 64 KB of partials
-    // in ~4.6 us -- DESIGN.md §4; the combine launch is cheaper)
     unsigned long long *st = (unsigned long long *)g_fa_stamps;
-    switch (G) {
-    case 1: hipLaunchKernelGGL(k_fa_dec4<1>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st); break;
-    case 2: hipLaunchKernelGGL(k_fa_dec4<2>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st); break;
-    case 4: hipLaunchKernelGGL(k_fa_dec4<4>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st); break;
-    case 8: hipLaunchKernelGGL(k_fa_dec4<8>, grid, dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, st); break;
+    // (an in-launch merge -- write-through partials, a per-kv-head ticket, the last split merging -- measured
+    // 12.4 vs 10.6 us per layer at 3850 keys: draining the sc1 stores and the ticket round trip cost 1.5-3 us, more
+    // than this launch boundary)
+    hipLaunchKernelGGL((k_fa_dec4<G>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS,
+                       scale, kv_ld, kv_hs, st);
+    if (qout) hipLaunchKernelGGL((k_fa_comb4<true, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, st);
+    else hipLaunchKernelGGL((k_fa_comb4<false, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, st);
+}
+
+template <int G>
+static int fa4_dispatch_ns(int NS, const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld,
+                           int64_t kv_hs, float *out, void *qout, void *ws, int H, int HKV, int n_past,
+                           const int32_t *n_past_dev, float scale, hipStream_t s) {
+    switch (NS) {
+    case 4: fa4_dispatch<G, 4>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
+    case 8: fa4_dispatch<G, 8>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
+    case 16: fa4_dispatch<G, 16>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
+    case 32: fa4_dispatch<G, 32>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
+    case 64: fa4_dispatch<G, 64>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
     default: return -1;
     }
-    KCPP_CHECK(hipGetLastError());
-    if (qout) hipLaunchKernelGGL(k_fa_comb4<true>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, NS, (unsigned long long *)g_fa_stamps);
-    else hipLaunchKernelGGL(k_fa_comb4<false>, dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, NS, (unsigned long long *)g_fa_stamps);
+    return 0;
+}
+
+// single-token decode: k_fa_dec4 + k_fa_comb4; partials behind FA_WS_TICKETS in ws.
+static int fa4_launch(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
+                      float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
+                      float scale, hipStream_t s) {
+    const int G = H / HKV;
+    const int NS = fa4_splits(HKV);
+    if (!qout && !out) return -1;
+    int rc = -1;
+    switch (G) {
+    case 1: rc = fa4_dispatch_ns<1>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
+    case 2: rc = fa4_dispatch_ns<2>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
+    case 4: rc = fa4_dispatch_ns<4>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
+    case 8: rc = fa4_dispatch_ns<8>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
+    default: return -1;
+    }
+    if (rc) return rc;
     KCPP_CHECK(hipGetLastError());
     return 0;
 }
@@ -690,8 +714,7 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     const bool use_decode = force_path == 1 || force_path == 6 || (force_path == 0 && T <= 16);
     const int G0 = H / HKV;
     if (use_decode && T == 1 && force_path != 6 && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) && (qout == nullptr || G0 >= 2))
-        return fa4_launch(q16, kc, vc, (int64_t)HKV * 128, 128, out, qout, ws, H, HKV, n_past, n_past_dev,
-                          n_past_dev ? n_kv_max : n_past + 1, scale, s);
+        return fa4_launch(q16, kc, vc, (int64_t)HKV * 128, 128, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s);
     if (use_decode) {
         ws = (uint8_t *)ws + FA_WS_TICKETS;
         const int nkv = n_past_dev ? n_kv_max : n_past + T;
@@ -753,7 +776,7 @@ int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *v
     if (H % HKV || !(G == 1 || G == 2 || G == 4 || G == 8) || (H % 2) || HKV > 64) return -1;
     if (qout && G < 2) return -1;
     const int nkv = n_past_dev ? n_kv_max : n_past + 1;
-    if (variant == 3) return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, nkv, scale, s);
+    if (variant == 3) return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s);
     if (variant != 0) return -1;
     const int nch = (nkv + FA_CHUNK - 1) / FA_CHUNK;
     if (nch > FA_MAX_CHUNKS) return -4;

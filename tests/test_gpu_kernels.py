@@ -315,6 +315,39 @@ def test_flash_attn_vs_oracle_f32_accum(env, T, n_past, path):
         np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("H,HKV", [(32, 8), (32, 32), (64, 8), (16, 8), (32, 4), (8, 4), (64, 64)])
+def test_fa_dec4_split_counts(env, H, HKV):
+    """the production decode pair (k_fa_dec4 + k_fa_comb4, kcpp_fa_decode_ex variant 3) over split counts 4..64
+    (256 / HKV rounded down to a power of two) and GQA groups 1..8: back-to-back calls whose key counts differ
+    (empty, partial and full splits) are reproducible bit for bit and match the f32-accumulation oracle."""
+    torch, K = env
+    D, n_ctx = 128, 4200
+    rng = np.random.default_rng(H * 100 + HKV)
+    kcache = (rng.standard_normal((n_ctx, HKV, D)) * 0.5).astype(np.float16)
+    vcache = rng.standard_normal((n_ctx, HKV, D)).astype(np.float16)
+    kd, vd = dev(torch, kcache), dev(torch, vcache)
+    ws = torch.zeros(K.fa_workspace_bytes(16, H, n_ctx), dtype=torch.uint8, device="cuda")
+    npd = torch.zeros(1, dtype=torch.int32, device="cuda")
+    for n_past in (0, 5, 100, 3850, 7, 4095):
+        npd.fill_(n_past)
+        q = rng.standard_normal((1, H, D)).astype(np.float32)
+        q16 = dev(torch, q.astype(np.float16))
+        outs = []
+        for _ in range(2):
+            out = torch.full((1, H, D), float("nan"), dtype=torch.float32, device="cuda")
+            K.call("kcpp_fa_decode_ex", q16.data_ptr(), kd.data_ptr(), vd.data_ptr(), HKV * D, D, out.data_ptr(), None,
+                   ws.data_ptr(), H, HKV, 0, npd.data_ptr(), n_ctx, 1.0 / np.sqrt(D), 3, sptr(torch))
+            outs.append(host(torch, out, np.float32).reshape(1, H, D))
+        assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32)), f"n_past {n_past}"
+        n_kv = n_past + 1
+        R.lib().orc_set_fa_f32_accum(1)
+        try:
+            want = R.flash_attn(q, kcache[:n_kv], vcache[:n_kv], np.zeros((1, n_kv), np.float16))
+        finally:
+            R.lib().orc_set_fa_f32_accum(0)
+        np.testing.assert_allclose(outs[0], want, rtol=2e-5, atol=2e-6)
+
+
 @pytest.mark.parametrize("path", [1, 6])
 @pytest.mark.parametrize("n_past", [63, 2047, 4095])
 def test_flash_attn_decode_long_ctx(env, n_past, path):

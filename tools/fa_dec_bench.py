@@ -44,7 +44,7 @@ def main():
                     sp = torch.cuda.current_stream().cuda_stream     # the capture stream inside torch.cuda.graph
                     for l in range(L):
                         K.call("kcpp_fa_decode_ex", q[l].data_ptr(), kc[l].data_ptr(), vc[l].data_ptr(), ld, hs,
-                               out[l].data_ptr(), qout[l].data_ptr(), ws.data_ptr(), H, HKV, 0, pos.data_ptr(),
+                               out[l].data_ptr(), None, ws.data_ptr(), H, HKV, 0, pos.data_ptr(),
                                n_ctx, 1.0 / D ** 0.5, var, sp)
                 step()
                 torch.cuda.synchronize()
@@ -95,7 +95,7 @@ def stamps():
                 for l in range(L2):
                     K.raw().kcpp_fa_set_stamps(st.data_ptr() if l == L2 - 1 else None)
                     K.call("kcpp_fa_decode_ex", q[l].data_ptr(), kc[l].data_ptr(), vc[l].data_ptr(), lo, hi,
-                           out[l].data_ptr(), qout[l].data_ptr(), ws.data_ptr(), H, HKV, 0, pos.data_ptr(),
+                           out[l].data_ptr(), None, ws.data_ptr(), H, HKV, 0, pos.data_ptr(),
                            n_ctx, 1.0 / D ** 0.5, var, sp)
                 K.raw().kcpp_fa_set_stamps(None)
             st.zero_()
