@@ -43,7 +43,8 @@ def main():
                 def step():
                     sp = torch.cuda.current_stream().cuda_stream     # the capture stream inside torch.cuda.graph
                     for l in range(L):
-                        K.call("kcpp_fa_decode_ex", q[l].data_ptr(), kc[l].data_ptr(), vc[l].data_ptr(), ld, hs,
+                        lc = 0 if os.environ.get("FA_RESIDENT") else l     # one layer's K/V re-read: Infinity-Cache resident
+                        K.call("kcpp_fa_decode_ex", q[l].data_ptr(), kc[lc].data_ptr(), vc[lc].data_ptr(), ld, hs,
                                out[l].data_ptr(), None, ws.data_ptr(), H, HKV, 0, pos.data_ptr(),
                                n_ctx, 1.0 / D ** 0.5, var, sp)
                 step()

@@ -18,3 +18,8 @@ for k, v in sorted(d.items(), key=lambda kv: -sum(kv[1])):
     tot += sum(v) / ntok
 t0 = int(dec[0]['Start_Timestamp']); t1 = int(dec[-1]['End_Timestamp'])
 print('kernel sum per token %.1f us, wall per token %.1f us' % (tot, (t1 - t0) / 1e3 / ntok))
+# launch boundaries: gap from the previous kernel's end to each kernel's start, per kernel name
+gaps = collections.defaultdict(list)
+for a, b in zip(dec, dec[1:]):
+    gaps[b['Kernel_Name'].split('(')[0][:48]].append((int(b['Start_Timestamp']) - int(a['End_Timestamp'])) / 1e3)
+print('gaps before each kernel (us): ' + ', '.join('%s %.2f' % (k[:40], sum(v) / len(v)) for k, v in gaps.items()))
