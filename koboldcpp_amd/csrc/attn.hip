@@ -748,9 +748,8 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     }
     if (!out) return -2;
     // prefill: MFMA kernel (attn_mfma.hip) for GQA groups of 4 (force_path 3, or auto), else FMA tiles (2)
-    static const int mfma_env = getenv("KCPP_FA_MFMA") ? atoi(getenv("KCPP_FA_MFMA")) : 1;
     int rc = -3;
-    if (force_path == 3 || (force_path == 0 && mfma_env))
+    if (force_path == 3 || force_path == 0)
         rc = kcpp_flash_attn_prefill_mfma(q16, kc, vc, out, T, H, HKV, D, n_past, scale, stream);
     if (rc == -3 && force_path == 3) return -3;
     if (rc == -3)

@@ -294,8 +294,7 @@ extern "C" int kcpp_fa_prefill_set_variant(int v) {
 extern "C" int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out,
                                             int T, int H, int HKV, int D, int n_past, float scale, void *stream) {
     if (D != 128 || HKV <= 0 || H != 4 * HKV) return -3;
-    static const int v_env = getenv("KCPP_FA_MFMA_V") ? atoi(getenv("KCPP_FA_MFMA_V")) : 2;
-    const int v = g_fa_prefill_variant ? g_fa_prefill_variant : v_env;
+    const int v = g_fa_prefill_variant ? g_fa_prefill_variant : 2;
     if (v == 1)
         hipLaunchKernelGGL(k_fa_prefill_mfma, dim3((T + FM_Q - 1) / FM_Q, HKV), dim3(256), 0, (hipStream_t)stream, q16, kc,
                            vc, out, T, H, HKV, n_past, scale);

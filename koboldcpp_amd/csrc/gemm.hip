@@ -1106,10 +1106,6 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 #define Q80S_UNROLL 8
 
-static int q80s_version() {
-    static const int v = getenv("KCPP_Q80S_V") ? atoi(getenv("KCPP_Q80S_V")) : 2;
-    return v;
-}
 static int q80s_splits(int64_t K, int64_t N) {
     const int64_t nt = (N + 127) / 128, nb = K / 32;
     int64_t S = (384 + nt - 1) / nt;
@@ -1125,91 +1121,12 @@ struct Q80Segs {
     int nseg;
 };
 
-// grid (ceil(Ntot / 128), S), 256 threads; dynamic LDS bps * 1152 B: the K range's activation fragments + scales
-__global__ void __launch_bounds__(256) k_gemm_q80s(const Q80Segs sg, int64_t K, int64_t N,
-                                                  const uint8_t *__restrict__ act, int64_t M, float *__restrict__ part) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t q80_lds[];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int lr = lane & 31, kg = lane >> 5;
-    const int64_t nb = K / 32, S = gridDim.y;
-    const int64_t bps = (nb + S - 1) / S, b0 = (int64_t)blockIdx.y * bps, b1 = std::min<int64_t>(nb, b0 + bps);
-    const int64_t n = (int64_t)blockIdx.x * 128 + 32 * wave + lr;
-    // this tile's segment (uniform: boundaries are multiples of 128)
-    const int64_t nt0 = (int64_t)blockIdx.x * 128;
-    const int seg = (sg.nseg > 1 && nt0 >= sg.N[0]) ? ((sg.nseg > 2 && nt0 >= sg.N[0] + sg.N[1]) ? 2 : 1) : 0;
-    const int64_t soff = seg == 0 ? 0 : (seg == 1 ? sg.N[0] : sg.N[0] + sg.N[1]);
-    const int64_t Ns = seg == 0 ? sg.N[0] : (seg == 1 ? sg.N[1] : sg.N[2]);
-    const uint8_t *W = seg == 0 ? sg.W[0] : (seg == 1 ? sg.W[1] : sg.W[2]);
-    const int64_t nrow = std::min<int64_t>(n - soff, Ns - 1), trow = std::min<int64_t>(lr, M - 1);
-    const int8_t *qx = (const int8_t *)act + trow * K + 16 * kg;                 // A: token lr, bytes 16kg..+15
-    const float *dx = (const float *)(act + M * K);                               // [M][nb]
-    const uint8_t *qw = W + nrow * nb * 32 + 16 * kg;                             // B: row nrow
-    const uint16_t *dw = (const uint16_t *)(W + Ns * nb * 32) + nrow * nb;
-    // the workgroup's activation K range in LDS once (LDS-DMA, 1 KiB fragment image per block) + its scales
-    i32x4 *sA = (i32x4 *)q80_lds;                                                // [bps][64 lanes]
-    float *sdx = (float *)(q80_lds + bps * 1024);                                // [bps][32 tokens]
-    for (int64_t b = wave; b < b1 - b0; b += 4) glds16(qx + (b0 + b) * 32, &sA[b * 64]);
-    for (int64_t i = tid; i < (b1 - b0) * 32; i += 256) {
-        const int64_t b = i >> 5, t = i & 31;
-        sdx[i] = t < M ? dx[t * nb + b0 + b] : 0.0f;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    float tot[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tot[r] = 0.0f;
-    // weights: the next group of blocks is in flight while the current one is multiplied
-    i32x4 wn[Q80S_UNROLL];
-    float dn[Q80S_UNROLL];
-    auto loadw = [&](int64_t bb) {
-#pragma unroll
-        for (int u = 0; u < Q80S_UNROLL; ++u) {
-            const int64_t b = std::min<int64_t>(bb + u, b1 - 1);
-            wn[u] = *(const i32x4 *)(qw + b * 32);
-            dn[u] = h2f(dw[b]);
-        }
-    };
-    loadw(b0);
-    for (int64_t bb = b0; bb < b1; bb += Q80S_UNROLL) {
-        i32x4 wc[Q80S_UNROLL];
-        float dc[Q80S_UNROLL];
-#pragma unroll
-        for (int u = 0; u < Q80S_UNROLL; ++u) { wc[u] = wn[u]; dc[u] = dn[u]; }
-        if (bb + Q80S_UNROLL < b1) loadw(bb + Q80S_UNROLL);
-#pragma unroll
-        for (int u = 0; u < Q80S_UNROLL; ++u) {
-            if (bb + u >= b1) break;
-            i32x16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0;
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(sA[(bb + u - b0) * 64 + lane], wc[u], acc, 0, 0, 0);
-            const float *sd = sdx + (bb + u - b0) * 32;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float4 d4 = *(const float4 *)(sd + 8 * q + 4 * kg);
-                const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    tot[4 * q + e] = __fadd_rn(tot[4 * q + e], __fmul_rn((float)acc[4 * q + e], __fmul_rn(dc[u], dv[e])));
-            }
-        }
-    }
-    if (n >= N) return;
-    float *pp = part + (int64_t)blockIdx.y * 32 * N + n;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        const int t = (r & 3) + 8 * (r >> 2) + 4 * kg;
-        pp[(int64_t)t * N] = tot[r];
-    }
-}
-
-// v2 of the small-batch Q8_0 GEMM: the weight tile streams through LDS in row-contiguous pieces.  v1's direct
-// fragment loads touch 32 rows x 32 B per wave instruction (32 cache lines for 1 KiB); here every LDS-DMA wave
+// The small-batch Q8_0 GEMM: the weight tile streams through LDS in row-contiguous pieces (a first version's direct
+// fragment loads touched 32 rows x 32 B per wave instruction, 32 cache lines for 1 KiB; removed); every LDS-DMA wave
 // instruction reads 64 / (2 CH) rows x 32 CH bytes (CH blocks of each row) into an XOR-swizzled [row][32 CH B] image
 // (16-B piece c of row n at slot c ^ (n % 2CH)), double-buffered by CH-block chunks with the activation chunk beside
 // it; CH = 4 (40 KiB of LDS: three workgroups per CU keep more weight bytes in flight than CH = 8 at one).  Same block math and
-// split-K partials as k_gemm_q80s (bit-identical partials).
+// split-K partials.
 // CH blocks per chunk (4: 40 KiB of LDS, three workgroups per CU)
 #ifndef Q80_CH
 #define Q80_CH 4
@@ -1362,7 +1279,7 @@ static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a
 
 static int g_gemm_variant = -1;
 static int gemm_variant() {
-    if (g_gemm_variant < 0) g_gemm_variant = getenv("KCPP_GEMM_V") ? atoi(getenv("KCPP_GEMM_V")) : 0;
+    if (g_gemm_variant < 0) g_gemm_variant = 0;
     return g_gemm_variant;
 }
 
@@ -1377,10 +1294,7 @@ static int gemm_q80_small(const void *W, const void *W2, int64_t K, int64_t N, c
     const dim3 grid((unsigned)((N + 127) / 128), (unsigned)S);
     Q80Segs sg = {{(const uint8_t *)W, nullptr, nullptr}, {N, 0, 0}, 1};
     auto q80 = [&](float *pt) {
-        if (q80s_version() == 2)
-            hipLaunchKernelGGL(k_gemm_q80s2, grid, dim3(256), (size_t)bps * 128, s, sg, K, N, (const uint8_t *)act, M, pt);
-        else
-            hipLaunchKernelGGL(k_gemm_q80s, grid, dim3(256), (size_t)bps * 1152, s, sg, K, N, (const uint8_t *)act, M, pt);
+        hipLaunchKernelGGL(k_gemm_q80s2, grid, dim3(256), (size_t)bps * 128, s, sg, K, N, (const uint8_t *)act, M, pt);
     };
     q80(part);
     KCPP_CHECK(hipGetLastError());
@@ -1422,12 +1336,8 @@ int kcpp_gemm_q80_segs(const void *const *W, const int64_t *N, int nseg, int64_t
     const int S = q80s_splits(K, Ntot);
     const int64_t nb = K / 32, bps = (nb + S - 1) / S;
     hipStream_t s = (hipStream_t)stream;
-    if (q80s_version() == 2)
-        hipLaunchKernelGGL(k_gemm_q80s2, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), (size_t)bps * 128, s, sg,
-                           K, Ntot, (const uint8_t *)act, M, part);
-    else
-        hipLaunchKernelGGL(k_gemm_q80s, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), (size_t)bps * 1152, s, sg,
-                           K, Ntot, (const uint8_t *)act, M, part);
+    hipLaunchKernelGGL(k_gemm_q80s2, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), (size_t)bps * 128, s, sg,
+                       K, Ntot, (const uint8_t *)act, M, part);
     KCPP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * Ntot + 255) / 256)), dim3(256), 0, s, part, nullptr, S, M, Ntot, Y, ldy,
                        nullptr, 0);
@@ -1476,12 +1386,10 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         KCPP_CHECK(hipGetLastError());
         // measured at M = 512 (tools/gemm_ab.py): 128 x 128 tiles with 8 waves for gate|up (247 vs v2 301 us),
         // 64 x 128 tiles with 4 waves for the 128-192-tile shapes (wo 44.7 vs 46.7, down 131.5 vs 137.2 us)
-        static const int nw_env = getenv("KCPP_GEMM_V3_WAVES") ? atoi(getenv("KCPP_GEMM_V3_WAVES")) : 0;
-        static const int bmt_env = getenv("KCPP_GEMM_V3_BMT") ? atoi(getenv("KCPP_GEMM_V3_BMT")) : 0;
         const int64_t nt = (N + 127) / 128;
         const bool big = Mp / 128 * nt >= 384;
-        const int BMT = bmt_env ? bmt_env : (big ? 4 : 2);
-        const int NWv = nw_env ? nw_env : (big ? 8 : 4);
+        const int BMT = big ? 4 : 2;
+        const int NWv = big ? 8 : 4;
         const int MT = (int)(Mp / (32 * BMT));
         const unsigned nwg = (unsigned)(MT * nt);
         auto launch3 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
@@ -1508,12 +1416,10 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         hipLaunchKernelGGL(k_act_frag6, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
                            (h8v *)a16, dy);
         KCPP_CHECK(hipGetLastError());
-        static const int nw6_env = getenv("KCPP_GEMM_V3_WAVES") ? atoi(getenv("KCPP_GEMM_V3_WAVES")) : 0;
-        static const int bmt6_env = getenv("KCPP_GEMM_V3_BMT") ? atoi(getenv("KCPP_GEMM_V3_BMT")) : 0;
         const int64_t nt = (N + 127) / 128;
         const bool big = Mp / 128 * nt >= 384;
-        const int BMT = bmt6_env ? bmt6_env : (big ? 4 : 2);
-        const int NWv = nw6_env ? nw6_env : (big ? 8 : 4);
+        const int BMT = big ? 4 : 2;
+        const int NWv = big ? 8 : 4;
         const int MT = (int)(Mp / (32 * BMT));
         const unsigned nwg = (unsigned)(MT * nt);
         auto launch6 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
@@ -1533,15 +1439,13 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         KCPP_CHECK(hipGetLastError());
         return 0;
     }
-    static const int v1 = getenv("KCPP_GEMM_V1") ? atoi(getenv("KCPP_GEMM_V1")) : 0;
     const bool rs = type == KT_Q4_K_RS || type == KT_Q6_K_RS;       // decode layouts: v2 only
-    if (rs || (!v1 && (type == KT_Q4_K || type == KT_Q5_K || type == KT_Q6_K))) {
+    if (rs || type == KT_Q4_K || type == KT_Q5_K || type == KT_Q6_K) {
         const int64_t nth = Mp * K / 8 + (Mp / 32) * (K / 256) * 64 + Mp * (K / 256);
         hipLaunchKernelGGL(k_act_frag, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
                            (h8v *)a16, dy, (h8v *)bs16);
         KCPP_CHECK(hipGetLastError());
-        static const int tm_env = getenv("KCPP_GEMM_TM") ? atoi(getenv("KCPP_GEMM_TM")) : 0;
-        const int TMv = (type != KT_Q4_K && type != KT_Q4_K_RS) ? 1 : (tm_env ? tm_env : ((Mp % 256 == 0 && N >= 8192) ? 2 : 1));
+        const int TMv = (type != KT_Q4_K && type != KT_Q4_K_RS) ? 1 : ((Mp % 256 == 0 && N >= 8192) ? 2 : 1);
         if (TMv == 2 && Mp % 256) return -5;
         const int MT = (int)(Mp / (GB_M * TMv));
         const unsigned nwg = (unsigned)(MT * ((N + GB_N - 1) / GB_N));
@@ -1577,9 +1481,6 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     const dim3 grid((unsigned)((N + GB_N - 1) / GB_N), (unsigned)(Mp / GB_M));
     auto launch = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
         switch (type) {
-        case KT_Q4_K: hipLaunchKernelGGL(k_gemm<KT_Q4_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
-        case KT_Q5_K: hipLaunchKernelGGL(k_gemm<KT_Q5_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
-        case KT_Q6_K: hipLaunchKernelGGL(k_gemm<KT_Q6_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         case KT_Q4_0: hipLaunchKernelGGL(k_gemm<KT_Q4_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         case KT_Q8_0: hipLaunchKernelGGL(k_gemm<KT_Q8_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         default: return -3;

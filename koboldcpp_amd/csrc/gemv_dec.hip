@@ -12,13 +12,11 @@ extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int 
     // row-major decode layouts: only the RS kernels read them (gemv_rs.hip)
     if (type == KT_Q4_K_RS || type == KT_Q6_K_RS) return kcpp_gemv_rs(type, args, mode, pro, stream);
     // coalesced-streaming kernel where it covers the type/shape (gemv_stream.hip), else unit-per-lane
-    static const int use_q4k = getenv("KCPP_Q4K") ? atoi(getenv("KCPP_Q4K")) : 1;
-    if (use_q4k && type == KT_Q4_K) {
+    if (type == KT_Q4_K) {
         const int rc = kcpp_gemv_q4k(args, mode, pro, stream);
         if (rc != -3) return rc;
     }
-    static const int use_stream = getenv("KCPP_STREAM") ? atoi(getenv("KCPP_STREAM")) : 1;
-    if (use_stream) {
+    {
         const int rc = kcpp_gemv_stream(type, args, mode, pro, stream);
         if (rc != -3) return rc;
     }

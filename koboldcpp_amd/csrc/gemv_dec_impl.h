@@ -266,8 +266,7 @@ static int launch_dec_it(const DecArgs &a, hipStream_t s) {
     if (PRO != 0 && a.K > 4096 * MC) return -6;
     // 1024 workgroups for K = n_embd shapes (the output head prefers more), 512 for the K = n_ff
     // quantize-prologue shape (ffn_down: 20.6 vs 26.8 us measured)
-    static const int env_blocks = getenv("KCPP_DEC_BLOCKS") ? atoi(getenv("KCPP_DEC_BLOCKS")) : 0;
-    const int max_blocks = env_blocks ? env_blocks : (a.K > 4096 ? 512 : 1024);
+    const int max_blocks = a.K > 4096 ? 512 : 1024;
     const int64_t groups = ntot / R;
     const int64_t nblk = std::min<int64_t>((groups + 3) / 4, max_blocks);
     const int vt = (TYPE == KT_Q4_0 || TYPE == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;

@@ -178,21 +178,7 @@ __global__ void __launch_bounds__(256) k_gemv_q4k(const DecArgs a) {
         slot_g = mine ? g : slot_g;
     };
     int k = 0;
-    if constexpr (PF == 2) {                          // three buffers: two groups in flight while computing
-        Buf bc;
-        issue(min(wid + nw, ngroups - 1), bb);
-        for (int g = wid; g < ngroups; g += 3 * nw, k += 3) {
-            const int g1 = g + nw, g2 = g + 2 * nw, g3 = g + 3 * nw, g4 = g + 4 * nw;
-            issue(min(g2, ngroups - 1), bc);
-            compute(g, ba, k);
-            if (g1 >= ngroups) break;
-            issue(min(g3, ngroups - 1), ba);
-            compute(g1, bb, k + 1);
-            if (g2 >= ngroups) break;
-            issue(min(g4, ngroups - 1), bb);
-            compute(g2, bc, k + 2);
-        }
-    } else if constexpr (PF) {
+    if constexpr (PF) {
         for (int g = wid; g < ngroups; g += 2 * nw, k += 2) {
             const int g1 = g + nw, g2 = g + 2 * nw;
             issue(min(g1, ngroups - 1), bb);
@@ -225,12 +211,9 @@ int launch_q4k(const DecArgs &a, hipStream_t s) {
     const int64_t groups = ntot / R;
     // measured (tools/stream_probe.py sweep): 512 workgroups (2 per CU) for every shape, 256 for gate|up with
     // R = 2 -- fewer prologues (each workgroup re-derives the activation) and less queueing than 1024
-    static const int env_blocks = getenv("KCPP_Q4K_BLOCKS") ? atoi(getenv("KCPP_Q4K_BLOCKS")) : 0;
-    const int max_blocks = env_blocks ? env_blocks : (MODE == 1 && R == 2 ? 256 : 512);
-    static const int min_gpw = getenv("KCPP_Q4K_ONEPASS") ? atoi(getenv("KCPP_Q4K_ONEPASS")) : 0;
+    const int max_blocks = MODE == 1 && R == 2 ? 256 : 512;
     int64_t nblk = std::min<int64_t>((groups + 3) / 4, max_blocks);
     nblk = std::max<int64_t>(nblk, (groups + 255) / 256);    // <= 64 groups per wave (result slots)
-    if (min_gpw) nblk = (groups + 3) / 4;                     // experiment: one group per wave
     const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
     hipLaunchKernelGGL((k_gemv_q4k<IT, R, MODE, PRO, MC, PF>), dim3((unsigned)nblk), dim3(256), (size_t)abytes + 16, s, a);
     KCPP_CHECK(hipGetLastError());
@@ -243,37 +226,16 @@ extern "C" int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream) 
     const DecArgs &a = *(const DecArgs *)args;
     hipStream_t s = (hipStream_t)stream;
     if (a.nseg < 1 || a.nseg > 3) return -3;
-    static const int r_env = getenv("KCPP_Q4K_R") ? atoi(getenv("KCPP_Q4K_R")) : 0;
     // gate|up: R = 2 with prefetch at 256 workgroups (17.5 us vs 21.1 us for gemv_dec_impl.h)
-    static const int glu = getenv("KCPP_Q4K_GLU") ? atoi(getenv("KCPP_Q4K_GLU")) : 1;
     if (a.K == 4096) {
-        static const int pf_env = getenv("KCPP_Q4K_PF") ? atoi(getenv("KCPP_Q4K_PF")) : 1;
-        if (mode == 1 && pro == 1 && glu) {
-            if (!pf_env) return launch_q4k<1, 1, 1, 1, 1, 0>(a, s);
-            if (pf_env == 2) return launch_q4k<1, 2, 1, 1, 1, 2>(a, s);
-            return r_env == 1 ? launch_q4k<1, 1, 1, 1, 1, 1>(a, s) : launch_q4k<1, 2, 1, 1, 1, 1>(a, s);
-        }
+        if (mode == 1 && pro == 1) return launch_q4k<1, 2, 1, 1, 1, 1>(a, s);
         if (mode == 2 && pro == 1) return launch_q4k<1, 2, 2, 1, 1, 0>(a, s);
         if (mode == 0 && pro == 0) return launch_q4k<1, 1, 0, 0, 1, 0>(a, s);
         if (mode == 0 && pro == 1) return launch_q4k<1, 2, 0, 1, 1, 1>(a, s);
         return -3;
     }
-    static const int down_v = getenv("KCPP_Q4K_DOWN") ? atoi(getenv("KCPP_Q4K_DOWN")) : 0;
-    if (a.K == 14336 && mode == 0 && pro == 2) {
-        switch (down_v) {
-        case 1: return launch_q4k<4, 2, 0, 2, 4, 0>(a, s);
-        case 2: return launch_q4k<4, 1, 0, 2, 4, 1>(a, s);
-        case 3: return launch_q4k<4, 2, 0, 2, 4, 1>(a, s);
-        default: return launch_q4k<4, 1, 0, 2, 4, 0>(a, s);
-        }
-    }
-    if (a.K == 14336 && mode == 0 && pro == 0) {
-        switch (down_v) {
-        case 1: return launch_q4k<4, 2, 0, 0, 4, 0>(a, s);
-        case 2: return launch_q4k<4, 1, 0, 0, 4, 1>(a, s);
-        case 3: return launch_q4k<4, 2, 0, 0, 4, 1>(a, s);
-        default: return launch_q4k<4, 1, 0, 0, 4, 0>(a, s);
-        }
-    }
+    // ffn_down (K = 14336): R = 1 without prefetch (tools/probe_down sweep: R 2 / prefetch variants no faster)
+    if (a.K == 14336 && mode == 0 && pro == 2) return launch_q4k<4, 1, 0, 2, 4, 0>(a, s);
+    if (a.K == 14336 && mode == 0 && pro == 0) return launch_q4k<4, 1, 0, 0, 4, 0>(a, s);
     return -3;
 }

@@ -336,26 +336,17 @@ int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
 //   q|k|v (mode 2)    : R 2, 512                     7.0 us / 14 MB
 //   head (N > 16384)  : R 2, 512                    69.4 us / 431 MB (6.2 TB/s)
 //   down (K > 8192)   : R 1, PF, 256 (Q4_K) / 512 (Q6_K)   12.5 / 15.0 us
-//   other (wo, ...)   : R 1, 1024                    4.9 us / 9.4 MB
-// KCPP_RS_R / KCPP_RS_PF / KCPP_RS_BLOCKS override (sweeps)
+//   wo (quantize prologue, PRO 2): R 1, 512          (1024: every workgroup quantizes, more of them cost more)
+//   other             : R 1, 1024                    4.9 us / 9.4 MB
 template <int TYPE, int NI, int MC>
 int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
-    static const int r_env = getenv("KCPP_RS_R") ? atoi(getenv("KCPP_RS_R")) : 0;
-    static const int pf_env = getenv("KCPP_RS_PF") ? atoi(getenv("KCPP_RS_PF")) : -1;
-    static const int b_env = getenv("KCPP_RS_BLOCKS") ? atoi(getenv("KCPP_RS_BLOCKS")) : 0;
     const int64_t ntot = a.N[0] + (a.nseg > 1 ? a.N[1] : 0) + (a.nseg > 2 ? a.N[2] : 0);
     int R = 1, PF = 0, B = 1024;
     if (mode == 1) { PF = 1; B = 512; }
     else if (mode == 2) { R = 2; B = 512; }
     else if (ntot > 16384) { R = 2; B = 512; }
     else if (a.K > 8192) { PF = TYPE == KT_Q4_K_RS; B = TYPE == KT_Q4_K_RS ? 256 : 512; }
-    else if (pro == 2) {                 // wo with its quantize prologue (every workgroup quantizes the input)
-        static const int wo_b = getenv("KCPP_RS_PRO2_BLOCKS") ? atoi(getenv("KCPP_RS_PRO2_BLOCKS")) : 512;
-        B = wo_b;
-    }
-    if (r_env && mode == 0) R = r_env;
-    if (pf_env >= 0) PF = pf_env;
-    if (b_env) B = b_env;
+    else if (pro == 2) B = 512;          // wo with its quantize prologue (every workgroup quantizes the input)
 #define KCPP_RS_P(PRO_)                                                                                             \
     if (pro == PRO_) {                                                                                              \
         if (mode == 1) return PF ? launch_rs<TYPE, NI, 1, 1, PRO_, MC, 1>(a, B, s) : launch_rs<TYPE, NI, 1, 1, PRO_, MC, 0>(a, B, s); \
@@ -478,8 +469,7 @@ extern "C" int kcpp_gemv_rs_qkv_mixed(const void *args, void *stream) {
     const int nsb = (int)(a.K / 256);
     const int nia = (nsb * 8 + 63) / 64, nib = (nsb * 4 + 63) / 64, mc = (int)((a.K + 4095) / 4096);
     const int64_t groups = (a.N[0] + a.N[1] + a.N[2]) / 2;
-    static const int b_env = getenv("KCPP_RS_QKV_BLOCKS") ? atoi(getenv("KCPP_RS_QKV_BLOCKS")) : 512;
-    int64_t nblk = std::min<int64_t>((groups + 3) / 4, b_env);
+    int64_t nblk = std::min<int64_t>((groups + 3) / 4, 512);
     nblk = std::max<int64_t>(nblk, (groups + 255) / 256);
     const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
     hipStream_t s = (hipStream_t)stream;

@@ -305,8 +305,7 @@ int launch_stream(const DecArgs &a, hipStream_t s) {
         ntot += a.N[i];
     }
     const int64_t tiles = ntot / G;
-    static const int max_blocks = getenv("KCPP_STREAM_BLOCKS") ? atoi(getenv("KCPP_STREAM_BLOCKS")) : 1024;
-    int64_t nblk = std::min<int64_t>((tiles + 3) / 4, max_blocks);
+    int64_t nblk = std::min<int64_t>((tiles + 3) / 4, 1024);
     nblk = std::max<int64_t>(nblk, (tiles + 4 * LPR - 1) / (4 * LPR));   // <= LPR tiles per wave (slots)
     const int64_t abytes = K + nsb * 4 + (K / 16) * 2;
     const size_t lds = (size_t)((abytes + 15) & ~15) + (size_t)4 * (MODE == 1 ? 2 : 1) * G * nsb * (16 + 4);
@@ -322,24 +321,8 @@ extern "C" int kcpp_gemv_stream(int type, const void *args, int mode, int pro, v
     const DecArgs &a = *(const DecArgs *)args;
     hipStream_t s = (hipStream_t)stream;
     if (type != KT_Q4_K || a.K % 256 || a.nseg < 1 || a.nseg > 3 || a.eid) return -3;
-    static const int lpr_env = getenv("KCPP_STREAM_LPR") ? atoi(getenv("KCPP_STREAM_LPR")) : 0;
-    const int64_t K = a.K, NC = K / 256 * 9;
-    // measured (tools/stream_probe.py): only the K = 14336 quantize-prologue shape (ffn_down) beats the
-    // unit-per-lane kernel (20.3 vs 24.6 us); the K = 4096 shapes lose on VALU work per byte, so they
-    // are only reachable with KCPP_STREAM=2 (experiments)
-    static const int all_shapes = getenv("KCPP_STREAM") && atoi(getenv("KCPP_STREAM")) >= 2;
-    if (K == 4096 && all_shapes) {                    // NC = 144
-        const int lpr = lpr_env ? lpr_env : (mode == 0 ? 32 : 16);
-        if (mode == 1 && pro == 1) return lpr == 32 ? launch_stream<32, 5, 1, 1, 1>(a, s) : launch_stream<16, 9, 1, 1, 1>(a, s);
-        if (mode == 2 && pro == 1) return lpr == 16 ? launch_stream<16, 9, 2, 1, 1>(a, s) : launch_stream<32, 5, 2, 1, 1>(a, s);
-        if (mode == 0 && pro == 0) return lpr == 16 ? launch_stream<16, 9, 0, 0, 1>(a, s)
-                                        : (lpr == 64 ? launch_stream<64, 3, 0, 0, 1>(a, s) : launch_stream<32, 5, 0, 0, 1>(a, s));
-        if (mode == 0 && pro == 1) return launch_stream<32, 5, 0, 1, 1>(a, s);
-        return -3;
-    }
-    if (K == 14336 && mode == 0 && pro == 2) {        // NC = 504: one row per wave, 8 chunks per lane
-        (void)NC;
-        return launch_stream<64, 8, 0, 2, 4>(a, s);
-    }
+    // measured (tools/stream_probe.py): only the K = 14336 quantize-prologue shape (ffn_down in the kcpp Q4_K
+    // layout) beats the unit-per-lane kernel (20.3 vs 24.6 us); at K = 4096 it loses on VALU work per byte
+    if (a.K == 14336 && mode == 0 && pro == 2) return launch_stream<64, 8, 0, 2, 4>(a, s);   // one row per wave
     return -3;
 }

@@ -249,15 +249,14 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     m->hp = *hp;
     // on-device layout per tensor: dense Q4_K / Q6_K mat-mul weights whose K the RS kernels cover are held in
     // the row-major decode layouts (KT_Q4_K_RS / KT_Q6_K_RS, gemv_rs.hip); the token embedding (row
-    // gathers), expert slices and everything else keep the kcpp layout.  KCPP_RS=0 disables (A/B runs).
-    static const int rs_env = getenv("KCPP_RS") ? atoi(getenv("KCPP_RS")) : 1;
+    // gathers), expert slices and everything else keep the kcpp layout.
     m->types.resize(n_tensors(*hp));
     for (int idx = 0; idx < n_tensors(*hp); ++idx) {
         int t = types[idx];
         int64_t K, N;
         shape_of(*hp, idx, K, N);
         const bool dense = idx >= 2 && n_slices(*hp, idx) == 1 && N > 1 && (idx == 2 || (idx - 3) % per_layer(*hp) <= 8);
-        if (rs_env && dense && (t == KT_Q4_K || t == KT_Q6_K) && kcpp_rs_supported(t, K))
+        if (dense && (t == KT_Q4_K || t == KT_Q6_K) && kcpp_rs_supported(t, K))
             t = t == KT_Q4_K ? KT_Q4_K_RS : KT_Q6_K_RS;
         m->types[idx] = t;
     }
@@ -274,7 +273,6 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     const int64_t E = hp->n_embd, F = hp->n_ff, H = hp->n_head, HKV = hp->n_head_kv, D = E / H, EKV = HKV * D;
     const int64_t UB = m->ub;
     m->layers.resize(il1 - il0);
-    static const int fuse_env = getenv("KCPP_PREFILL_FUSE") ? atoi(getenv("KCPP_PREFILL_FUSE")) : 1;
     auto rowmajor = [](int t) { return t == KT_Q4_K || t == KT_Q5_K || t == KT_Q4_K_RS || t == KT_Q6_K_RS; };
     auto alloc_group = [&](void *&base, int idx0, int n) -> int {
         size_t tot = 0;
@@ -291,7 +289,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
         }
         return 0;
     };
-    for (int il = il0; il < il1 && fuse_env; ++il) {
+    for (int il = il0; il < il1; ++il) {
         KLayer &L = m->layers[il - il0];
         const int b = 3 + per_layer(*hp) * il;
         if (rowmajor(types[b + 1]) && types[b + 2] == types[b + 1]) {
@@ -507,10 +505,7 @@ static int matmul(kcpp_model *m, const KTensor &W, const KTensor *W2, const void
 }
 
 static int rows_per_wave(int64_t N, int mode) {
-    static const int r0 = getenv("KCPP_R0") ? atoi(getenv("KCPP_R0")) : 0;
-    static const int r1 = getenv("KCPP_R1") ? atoi(getenv("KCPP_R1")) : 0;
-    if (mode == 1) return r1 ? r1 : 1;
-    if (r0) return r0;
+    if (mode == 1) return 1;
     return N > 16384 ? 4 : (N > 4096 ? 2 : 1);
 }
 
@@ -629,9 +624,9 @@ static int forward_layers_dec(kcpp_model *m) {
     for (int il = m->il0; il < m->il1; ++il) {
         KLayer &L = m->layers[il - m->il0];
         const KTensor *t = L.t;
-        // --- attn_norm + q|k|v + rope + K/V cache store: one launch per quant type present; with mixed types
-        // (Q4_K_M: q|k Q4_K, v Q6_K on the more-bits layers) the launches are independent and can run as two
-        // branches (side stream, forked and joined by events -- also inside the captured hipGraph)
+        // --- attn_norm + q|k|v + rope + K/V cache store: one launch per quant type present; q|k Q4_K + v Q6_K (the
+        // Q4_K_M more-bits layers) in one launch.  (Two launches forked onto a side stream inside the graph
+        // replayed slower than in sequence, 453 vs 517 tok/s: removed.)
         DecArgs qa[3];
         int qty[3], nq = 0;
         for (int j = 1; j <= 3;) {
@@ -647,11 +642,8 @@ static int forward_layers_dec(kcpp_model *m) {
             }
             qty[nq++] = ty;
         }
-        // measured: the forked graph replays slower than the serial one (453 vs 517 tok/s), so opt-in only
-        static const int fork_env = getenv("KCPP_QKV_FORK") ? atoi(getenv("KCPP_QKV_FORK")) : 0;
-        static const int mixed_env = getenv("KCPP_QKV_MIXED") ? atoi(getenv("KCPP_QKV_MIXED")) : 1;
         int mixed_rc = -3;
-        if (nq == 2 && mixed_env && qty[0] == KT_Q4_K_RS && qty[1] == KT_Q6_K_RS && qa[0].nseg == 2 && qa[1].nseg == 1 &&
+        if (nq == 2 && qty[0] == KT_Q4_K_RS && qty[1] == KT_Q6_K_RS && qa[0].nseg == 2 && qa[1].nseg == 1 &&
             qa[1].role[0] == 2) {
             // q|k Q4_K + v Q6_K (Q4_K_M "more bits" layers): one launch (gemv_rs.hip k_gemv_rs_qkv)
             DecArgs c = qa[0];
@@ -659,38 +651,25 @@ static int forward_layers_dec(kcpp_model *m) {
             mixed_rc = kcpp_gemv_rs_qkv_mixed(&c, s);
             if (mixed_rc != -3 && mixed_rc != -5) RC(mixed_rc);
         }
-        if (mixed_rc == 0) {
-        } else if (nq == 2 && m->side && fork_env) {
-            RT_CHECK(hipEventRecord(m->ev_fork, s));
-            RT_CHECK(hipStreamWaitEvent(m->side, m->ev_fork, 0));
-            RC(kcpp_gemv_dec(qty[1], &qa[1], 2, 1, 2, m->side));
-            RC(kcpp_gemv_dec(qty[0], &qa[0], 2, 1, 2, s));
-            RT_CHECK(hipEventRecord(m->ev_join, m->side));
-            RT_CHECK(hipStreamWaitEvent(s, m->ev_join, 0));
-        } else {
+        if (mixed_rc != 0)
             for (int i = 0; i < nq; ++i) RC(kcpp_gemv_dec(qty[i], &qa[i], 2, 1, 2, s));
-        }
         // --- attention over the cache (f32 output); wo quantizes it in its own prologue (PRO 2: the Q8_K /
-        // Q8_0 conversion overlaps wo's first weight loads instead of ending the attention combine)
-        static const int wo_pro_env = getenv("KCPP_WO_PRO") ? atoi(getenv("KCPP_WO_PRO")) : 2;
-        const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K && !m->fa_exact && wo_pro_env == 0;
+        // Q8_0 conversion overlaps wo's first weight loads instead of ending the attention combine; measured
+        // against the combine quantizing and wo copying: 572 vs 575 tok/s, within noise)
         if (m->fa_exact)
             RC(kcpp_flash_attn_exact(m->q16, L.kc, L.vc, m->attn, 1, (int)H, (int)HKV, (int)D, 0, m->pos_dev, kq_scale, s));
         else
-            RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, woq ? m->act : nullptr, m->fa_ws, 1, (int)H, (int)HKV, (int)D,
-                               0, m->pos_dev, hp.n_ctx, kq_scale, 1, s));
+            RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, nullptr, m->fa_ws, 1, (int)H, (int)HKV, (int)D, 0, m->pos_dev,
+                               hp.n_ctx, kq_scale, 1, s));
         {   // x += wo . attn
             DecArgs a;
             memset(&a, 0, sizeof a);
             a.K = E; a.nseg = 1;
             a.W[0] = (const uint8_t *)t[4].d; a.N[0] = t[4].N; a.Y[0] = m->x; a.res = m->x;
-            int rc = -3;
-            if (!woq && wo_pro_env == 2) {
-                a.x = m->attn;
-                rc = kcpp_gemv_dec(t[4].type, &a, 0, 2, rows_per_wave(t[4].N, 0), s);
-            }
+            a.x = m->attn;
+            int rc = kcpp_gemv_dec(t[4].type, &a, 0, 2, rows_per_wave(t[4].N, 0), s);
             if (rc == -3) {
-                if (!woq) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, 1, s));
+                RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, 1, s));
                 a.x = nullptr; a.act = (const uint8_t *)m->act;
                 rc = kcpp_gemv_dec(t[4].type, &a, 0, 0, rows_per_wave(t[4].N, 0), s);
             }
@@ -757,8 +736,7 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             if (L.nqkv >= 2) {                       // q|k(|v) rows back to back: one GEMM
                 KTensor f = t[1];
                 f.N = E + (L.nqkv - 1) * EKV;
-                static const int side_env = getenv("KCPP_PREFILL_SIDE") ? atoi(getenv("KCPP_PREFILL_SIDE")) : 1;
-                if (L.nqkv == 2 && T > 8 && side_env && m->side) {
+                if (L.nqkv == 2 && T > 8 && m->side) {
                     // attn_v (another type: Q6_K on the more-bits layers) on the side stream with its own
                     // workspace, concurrently with the q|k GEMM: its 64-workgroup grid alone leaves CUs idle
                     if (!m->gemm_ws2) {
@@ -803,7 +781,6 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             RC(kcpp_rope_kv(m->qkv, LQ, nullptr, m->q16, L.kc, L.vc, T, (int)H, (int)HKV, (int)D, n_past, posp, m->rope_tab, s));
         }
         const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K && !m->fa_exact && !kvq;
-        static const int fa_force = getenv("KCPP_FA_PATH") ? atoi(getenv("KCPP_FA_PATH")) : 0;
         if (kvq)
             RC(kcpp_flash_attn_q(m->kv_tk, m->kv_tv, m->qkv, LQ, L.kc, L.vc, m->attn, T, (int)H, (int)HKV, (int)D, hp.n_ctx,
                                  n_past, posp, kq_scale, s));
@@ -811,7 +788,7 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             RC(kcpp_flash_attn_exact(m->q16, L.kc, L.vc, m->attn, T, (int)H, (int)HKV, (int)D, n_past, posp, kq_scale, s));
         else
             RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, (woq && T <= 16) ? m->act : nullptr, m->fa_ws, T, (int)H,
-                               (int)HKV, (int)D, n_past, posp, hp.n_ctx, kq_scale, fa_force, s));
+                               (int)HKV, (int)D, n_past, posp, hp.n_ctx, kq_scale, 0, s));
         if (!(woq && T <= 16)) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, T, s));
         RC(matmul(m, t[4], nullptr, m->act, T, m->x, E, m->x, E, 0));                    // x += wo . attn
         if (hp.n_expert > 0) { RC(T == 1 ? moe_dec(m, L) : moe_prefill(m, L, T)); continue; }   // T == 1: no host sync (graphs)

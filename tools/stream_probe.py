@@ -167,7 +167,7 @@ def dec():
             continue
         us = timed(lambda i, sp: K.gemv_dec(t, args[i % len(args)], mode, pro, rpw, sp), 40)
         print(json.dumps({"probe": "dec", "case": name, "bytes": wb * nmat, "us": round(us, 2),
-                          "GBps": round(wb * nmat / us / 1e3, 1), "blocks_env": os.environ.get("KCPP_DEC_BLOCKS")}))
+                          "GBps": round(wb * nmat / us / 1e3, 1)}))
         del ws, args
         torch.cuda.empty_cache()
 
