@@ -285,6 +285,9 @@ int kcpp_model_set_fused_decode(kcpp_model *m, int enable);
 /* 1: attention through kcpp_flash_attn_exact (reference order, f16 accumulation; strict-parity mode, slow);
  * 0 (default, or KCPP_FA_EXACT=1 at creation): the split-KV / MFMA kernels */
 int kcpp_model_set_fa_exact(kcpp_model *m, int enable);
+/* MoE: the expert ids the model's last MoE layer routed the last prefill's tokens to, n = T * n_expert_used
+ * int32 ([token][slot], the router's top-k order); diagnostics for routing-aware parity tests */
+int kcpp_model_moe_ids(kcpp_model *m, int32_t *out, int n);
 /* K / V cache types (llama_context_params type_k / type_v): KT_F16 (default) or quantized KT_Q8_0 / KT_Q4_0 for
  * both (koboldcpp --quantkv).  Reallocates and clears the caches; quantized caches run single-token decode
  * through the unfused per-op path and refuse kcpp_model_kv_shift (koboldcpp turns context shift off with

@@ -462,6 +462,14 @@ extern "C" int kcpp_model_set_graphs(kcpp_model *m, int enable) {
     m->use_graphs = enable != 0;
     return 0;
 }
+// the expert ids the last MoE prefill layer of this model (stage) routed its T tokens to, [T][n_expert_used]
+// (the host copy moe_prefill groups tokens by): diagnostics for routing-aware parity tests
+extern "C" int kcpp_model_moe_ids(kcpp_model *m, int32_t *out, int n) {
+    if (!m->moe_ids_h || n < 0 || n > m->ub * std::max(1, m->hp.n_expert_used)) { g_err = "moe ids"; return -1; }
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    memcpy(out, m->moe_ids_h, (size_t)n * 4);
+    return 0;
+}
 extern "C" int kcpp_model_set_fa_exact(kcpp_model *m, int enable) {
     m->fa_exact = enable != 0;
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }

@@ -86,6 +86,7 @@ _SIGS = {
     "kcpp_model_set_graphs": [P, I],
     "kcpp_model_set_fused_decode": [P, I],
     "kcpp_model_set_fa_exact": [P, I],
+    "kcpp_model_moe_ids": [P, P, I],
     "kcpp_flash_attn_exact": [P, P, P, P, I, I, I, I, I, P, Fl, P],
     "kcpp_model_weight_bytes": [P],
     "kcpp_model_set_kv_types": [P, I, I],
@@ -294,6 +295,12 @@ class Model:
     def set_kv_types(self, type_k, type_v):
         """K / V cache types: F16 (default) or Q8_0 / Q4_0 for both (koboldcpp --quantkv); clears the caches"""
         _chk(_L.kcpp_model_set_kv_types(self.m, int(type_k), int(type_v)), "set_kv_types")
+
+    def moe_ids(self, T, k):
+        import numpy as np
+        out = np.zeros((T, k), np.int32)
+        _chk(_L.kcpp_model_moe_ids(self.m, out.ctypes.data, T * k), "moe_ids")
+        return out
 
     def set_graphs(self, on):
         _L.kcpp_model_set_graphs(self.m, int(on))

@@ -150,9 +150,12 @@ static int load_model(model_t *m) {
     return 0;
 }
 
+static float *g_router = NULL;   /* MoE router logits of the hidden-dump layers (run_llama with a hidden file) */
+
 /* one llama_decode of T tokens at n_past; returns logits of the last token.  With hid != NULL the
  * residual stream after every layer but the last ([n_layer-1][T][E]) is written there (layer outputs =
- * the next layer's input; the last layer keeps only the last token, src/llama.cpp out_ids). */
+ * the next layer's input; the last layer keeps only the last token, src/llama.cpp out_ids), and with
+ * g_router the MoE router logits of those layers ([n_layer-1][T][n_expert]). */
 static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits, float *hid) {
     cfg_t *c = &m->c;
     const int E = c->n_embd, H = c->n_head, HKV = c->n_head_kv, D = E / H, EKV = HKV * D, F = c->n_ff;
@@ -183,7 +186,7 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits,
 
     const float kq_scale = 1.0f / sqrtf((float)D);
     struct ggml_tensor *inpL = ggml_get_rows(ctx, m->w[0], inp_tokens);   /* llm_build_inp_embd */
-    struct ggml_tensor *lay_out[256];
+    struct ggml_tensor *lay_out[256], *rlog[256];
     for (int il = 0; il < c->n_layer; ++il) {
         struct ggml_tensor **lw = m->w + 3 + (c->n_expert ? 10 : 9) * il;
         struct ggml_tensor *inpSA = inpL;
@@ -221,6 +224,8 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits,
             const int NE = c->n_expert, NU = c->n_expert_used;
             const int64_t T = cur->ne[1];                  /* 1 in the last layer (out_ids) */
             struct ggml_tensor *logits = ggml_mul_mat(ctx, lw[9], cur);                 /* [NE, T] */
+            rlog[il] = logits;
+            if (hid && g_router && il < c->n_layer - 1) ggml_build_forward_expand(gf, logits);
             struct ggml_tensor *probs = ggml_soft_max(ctx, logits);
             struct ggml_tensor *sel = ggml_top_k(ctx, probs, NU);                        /* [NU, T] */
             struct ggml_tensor *wts = ggml_get_rows(ctx, ggml_reshape_3d(ctx, probs, 1, NE, T), sel);
@@ -255,6 +260,9 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits,
     if (hid)
         for (int il = 0; il < c->n_layer - 1; ++il)
             memcpy(hid + (size_t)il * T * E, lay_out[il]->data, sizeof(float) * (size_t)T * E);
+    if (hid && g_router)      /* router logits of the same layers (MoE): [n_layer-1][T][n_expert] */
+        for (int il = 0; il < c->n_layer - 1; ++il)
+            memcpy(g_router + (size_t)il * T * c->n_expert, rlog[il]->data, sizeof(float) * (size_t)T * c->n_expert);
     ggml_free(ctx);
     return 0;
 }
@@ -280,13 +288,22 @@ static int run_llama(const char *cfgpath) {
     double tp0 = now_s();
     FILE *hout = c->hidden_out[0] ? fopen(c->hidden_out, "wb") : NULL;
     float *hid = hout ? malloc(sizeof(float) * (size_t)(c->n_layer > 1 ? c->n_layer - 1 : 1) * c->ubatch * c->n_embd) : NULL;
+    FILE *rout = NULL;
+    if (hout && c->n_expert) {  /* MoE: the router logits beside the hidden states, <hidden_out>.router */
+        char rp[1100];
+        snprintf(rp, sizeof rp, "%s.router", c->hidden_out);
+        rout = fopen(rp, "wb");
+        g_router = malloc(sizeof(float) * (size_t)(c->n_layer > 1 ? c->n_layer - 1 : 1) * c->ubatch * c->n_expert);
+    }
     for (int i = 0; i < c->n_prompt; i += c->ubatch) {
         int T = c->n_prompt - i < c->ubatch ? c->n_prompt - i : c->ubatch;
         if (eval(&m, c->prompt + i, T, n_past, logits, hid)) return 4;
         if (hout) fwrite(hid, sizeof(float), (size_t)(c->n_layer - 1) * T * c->n_embd, hout);
+        if (rout) fwrite(g_router, sizeof(float), (size_t)(c->n_layer - 1) * T * c->n_expert, rout);
         n_past += T;
     }
     if (hout) { fclose(hout); free(hid); }
+    if (rout) { fclose(rout); free(g_router); g_router = NULL; }
     double t_pp = now_s() - tp0;
     fwrite(logits, sizeof(float), c->n_vocab, out);
     int tok = argmax(logits, c->n_vocab);

@@ -212,7 +212,8 @@ def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeou
     """Run the reference ggml graph; returns (logits [1+n_gen, V], info dict).
     forced: decode these tokens (teacher forcing) instead of the greedy argmax.
     hidden: also return info["hidden"] = residual stream after layers 0..n_layer-2 of the prefill,
-            [n_layer-1][n_prompt][n_embd] (single-ubatch prompts).
+            [n_layer-1][n_prompt][n_embd] (single-ubatch prompts); MoE: info["router"] = those layers' router
+            logits [n_layer-1][n_prompt][n_expert].
     binary: ref_llama build to run (default: the AVX2 build; REF_BIN_SCALAR for the scalar one)."""
     import json
     with tempfile.TemporaryDirectory() as td:
@@ -238,6 +239,9 @@ def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeou
         logits = np.fromfile(out, dtype=np.float32).reshape(-1, hp["n_vocab"])
         if hidden:
             info["hidden"] = np.fromfile(hout, dtype=np.float32).reshape(hp["n_layer"] - 1, len(prompt), hp["n_embd"])
+            if hp.get("n_expert", 0):      # MoE: the router logits of the same layers
+                info["router"] = np.fromfile(hout + ".router", dtype=np.float32).reshape(
+                    hp["n_layer"] - 1, len(prompt), hp["n_expert"])
         return logits, info
 
 

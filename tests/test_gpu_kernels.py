@@ -397,10 +397,36 @@ def test_gemm_small_shapes(env, t, Kd, N, M):
     np.testing.assert_allclose(_gpu_mul_mat(torch, K, t, w, Kd, N, X, mode=1, w2=w2), glu, rtol=1e-5, atol=tol)
 
 
+@pytest.mark.parametrize("t", [R.Q5_K, R.Q6_K, R.Q4_K, R.Q8_0])
+@pytest.mark.parametrize("Kd,N", [(4096, 256), (14336, 128)])
+def test_mul_mat_every_batch_size(env, t, Kd, N):
+    """every token count 1..64 (the MoE prefill runs each expert's GEMMs on however many tokens the router sent
+    it) at the Mixtral expert widths, plain and GLU, vs the oracle"""
+    torch, K = env
+    rng = np.random.default_rng(Kd + N + t)
+    w = R.synth(t, 4, 700 + t, Kd, N)
+    w2 = R.synth(t, 4, 800 + t, Kd, N)
+    X = rng.standard_normal((64, Kd)).astype(np.float32)
+    a_all = R.mul_mat(t, w, Kd, N, X)
+    b_all = R.mul_mat(t, w2, Kd, N, X)
+    bad = []
+    for M in range(1, 65):
+        a, b = a_all[:M], b_all[:M]
+        tol = 3e-6 * max(1.0, np.abs(a).max())
+        g = _gpu_mul_mat(torch, K, t, w, Kd, N, X[:M])
+        if not np.allclose(g, a, rtol=0, atol=tol):
+            bad.append(("plain", M, float(np.abs(g - a).max())))
+        glu = (a / (1 + np.exp(-a))) * b
+        g = _gpu_mul_mat(torch, K, t, w, Kd, N, X[:M], mode=1, w2=w2)
+        if not np.allclose(g, glu, rtol=1e-5, atol=tol):
+            bad.append(("glu", M, float(np.abs(g - glu).max())))
+    assert not bad, bad
+
+
 @pytest.mark.parametrize("H,HKV", [(32, 8), (8, 8), (64, 8), (16, 8)])
 def test_flash_attn_decode_fused_quant(env, H, HKV):
-    """decode FA with the ticketed in-kernel combine (+Q8_K of the output) vs oracle and vs the
-    separate quantizer; repeated calls reuse the self-resetting tickets."""
+    """decode FA with the combine quantizing its output to Q8_K vs the oracle and vs the separate quantizer,
+    over repeated calls on one workspace."""
     torch, K = env
     D, n_ctx = 128, 1024
     rng = np.random.default_rng(H)

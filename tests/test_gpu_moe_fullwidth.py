@@ -1,0 +1,111 @@
+"""BASELINE config 5 (Mixtral 8x7B Q5_K_M) at full width against the reference ggml CPU build: n_embd 4096, 32/8
+heads, n_ff 14336, 8 experts top-2, vocab 32000, the Q5_K_M policy for 8 experts (Q8_0 attn_k / attn_v, Q6_K
+ffn_down_exps on the 'more bits' layer, F32 router), 2 layers, 64-token prompt + 3 teacher-forced decode steps
+(tests/golden/e2e_moe_full.npz, make_moe_full.py, with the reference's layer-0 residual stream and router logits).
+This exercises the full-width Q5_K expert mat-vecs and GEMMs, the Q8_0 k / v projections and the 8-way router.
+
+Top-k routing is discontinuous, and on these random weights its margins are tiny: the reference's own layer-0 top-2
+vs 3rd probability margin is below 0.01 on 27 of the 64 prompt tokens and 8.5e-5 at its smallest.  A perturbation
+well inside the reference's own AVX2-vs-scalar spread (here the f32-vs-f16 attention accumulation, or the GEMM's
+summation order) can flip such a choice and move that token's residual row by tens of units.  So the bars are
+routing-aware (the reference build pair did not flip on this prompt; measured here, production flips one layer-0
+token, the strict mode none at layer 0 and the last token at layer 1):
+  * layer 0: the GPU's expert choice (kcpp_model_moe_ids) equals the reference's wherever its margin is >= 1e-3
+    (production flips exactly the 8.5e-5 near-tie), every token routed like the reference has its residual row
+    within 1.5x (strict; measured 0.96x) / 2x (production, f32 attention accumulation; measured 1.64x) the
+    reference's spread max, the median over all rows within 1.5x (strict) / 20x (production, as
+    tests/test_gpu_fullwidth.py) of the spread median;
+  * layer 1 + head on the REFERENCE's layer-0 output: logits within 1.5x the spread (max and median);
+  * end to end: the decode steps' logits within 1.5x the spread, and the GPU's greedy token the reference's or
+    within 1.5x the spread of its top logit (the strict mode's step 1 picks a token 0.1 below the reference's);
+    the prompt step passes two routers and is covered by the per-layer checks."""
+import os
+
+import numpy as np
+import pytest
+
+import refharness as R
+
+pytestmark = pytest.mark.gpu
+
+MIXTRAL2 = dict(n_vocab=32000, n_embd=4096, n_head=32, n_head_kv=8, n_layer=2, n_ff=14336, n_ctx=128, eps=1e-5,
+                rope_base=1000000.0, n_expert=8, n_expert_used=2)
+FACTOR = 1.5
+PROD_MEDIAN_FACTOR = 20.0      # f32 attention accumulation vs the reference's f16 (tests/test_gpu_fullwidth.py)
+PROD_MAX_FACTOR = 2.0          # the same, per row: measured 1.64x on the equally routed layer-0 rows
+
+
+@pytest.fixture(scope="module")
+def K():
+    import torch
+    assert torch.cuda.is_available()
+    import koboldcpp_amd.lib as K
+    return K
+
+
+@pytest.mark.parametrize("exact", [False, True], ids=["production", "fa_exact"])
+@pytest.mark.parametrize("graphs", [True, False], ids=["graph", "eager"])
+def test_mixtral_width_vs_reference(K, graphs, exact):
+    f = np.load(os.path.join(R.ROOT, "tests", "golden", "e2e_moe_full.npz"))
+    types = [int(t) for t in f["types"]]
+    m = K.Model(MIXTRAL2, types)
+    m.set_graphs(graphs)
+    m.set_fa_exact(exact)
+    m.synth(1234)
+    out = [m.decode(f["prompt"], 0)]
+    n = len(f["prompt"])
+    for tok in f["forced"]:
+        out.append(m.decode([int(tok)], n))
+        n += 1
+    m.close()
+    out = np.array(out)
+    d = np.abs(out - f["logits"])
+    dmax, dmed = d.max(axis=1), np.median(d, axis=1)
+    print("gpu vs ref max", dmax, "median", dmed, "| ref spread max", f["spread_max"], "median", f["spread_median"])
+    assert np.all(dmax[1:] <= FACTOR * f["spread_max"].max()), dmax
+    assert np.all(dmed[1:] <= FACTOR * f["spread_median"].max()), dmed
+    # greedy choice: the GPU's top token is the reference's top token or within its spread of it (near-ties)
+    ref = f["logits"][1:]
+    g = np.argmax(out[1:], axis=1)
+    assert np.all(ref[np.arange(len(g)), g] >= ref.max(axis=1) - FACTOR * f["spread_max"].max()), g
+
+
+@pytest.mark.parametrize("exact", [False, True], ids=["production", "fa_exact"])
+def test_mixtral_width_per_layer(K, exact):
+    """layer 0 (embedding + layer 0) vs the reference's residual stream after it, and layer 1 + head run on the
+    REFERENCE's layer-0 output vs its logits (isolates each layer from the other's rounding)"""
+    f = np.load(os.path.join(R.ROOT, "tests", "golden", "e2e_moe_full.npz"))
+    types = [int(t) for t in f["types"]]
+    p = f["prompt"]
+    T, E = len(p), MIXTRAL2["n_embd"]
+    m0 = K.Model(MIXTRAL2, types, il0=0, il1=1, has_embed=True, has_output=False)
+    m0.set_fa_exact(exact)
+    m0.synth(1234)
+    m0.decode(p, 0, want_logits=False)
+    h0 = m0.read_hidden(T * E).reshape(T, E)
+    ids = m0.moe_ids(T, MIXTRAL2["n_expert_used"])
+    m0.close()
+    r = f["router0"].astype(np.float64)
+    pr = np.exp(r - r.max(axis=1, keepdims=True))
+    pr /= pr.sum(axis=1, keepdims=True)
+    order = np.argsort(-pr, axis=1, kind="stable")
+    margin = pr[np.arange(T), order[:, 1]] - pr[np.arange(T), order[:, 2]]
+    same = np.array([set(ids[t]) == set(order[t, :2]) for t in range(T)])
+    flipped = np.where(~same)[0]
+    print("layer0 routing: %d of %d tokens differ from the reference, margins %s" % (len(flipped), T, margin[flipped]))
+    assert np.all(margin[flipped] < 1e-3), (flipped, margin[flipped])
+    dh = np.abs(h0 - f["hidden0"])
+    m1 = K.Model(MIXTRAL2, types, il0=1, il1=2, has_embed=False, has_output=True)
+    m1.set_fa_exact(exact)
+    m1.synth(1234)
+    ref_in = np.ascontiguousarray(f["hidden0"], np.float32)
+    m1.hidden_io(ref_in.ctypes.data, T * E, 0, to_buf=False)
+    lg = m1.decode(None, 0, n_tokens=T)
+    m1.close()
+    d = np.abs(lg - f["logits"][0])
+    print("layer0 hidden max (same routing) %.4g median %.4g (ref spread %.4g %.4g) | layer1 logits max %.4g median %.4g"
+          % (dh[same].max(), np.median(dh), f["hidden0_spread_max"], f["hidden0_spread_median"], d.max(), np.median(d)))
+    assert dh[same].max() <= (FACTOR if exact else PROD_MAX_FACTOR) * f["hidden0_spread_max"]
+    assert np.median(dh) <= (FACTOR if exact else PROD_MEDIAN_FACTOR) * f["hidden0_spread_median"]
+    assert d.max() <= FACTOR * f["spread_max"].max()
+    assert np.median(d) <= FACTOR * f["spread_median"].max()
