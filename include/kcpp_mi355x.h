@@ -298,6 +298,12 @@ const char *kcpp_last_error(void);
 
 /* GGUF parse + tensor-table bounds validation alone (load_model's first step): 0 ok, -1 with the reason in err */
 int kcpp_gguf_check(const char *path, char *err, int err_len);
+/* host-only tokenizer probes (tests): the BPE pre-tokenizer of GGUF pre type `pre` (llm_tokenizer_bpe's
+ * regex_exprs, src/llama-vocab.cpp:597-712; custom splits src/unicode.cpp:248-492) -> byte end offsets of the
+ * words; and the GGUF vocabulary's full tokenization as generate() uses it (special tokens parsed,
+ * tokenizer_st_partition src/llama-vocab.cpp:1544).  Return the count, -1 on error. */
+int kcpp_pretokenize(const char *pre, const char *text, int64_t *ends, int cap);
+int kcpp_tokenize_probe(const char *gguf_path, const char *text, int add_bos, int32_t *out, int cap);
 /* generate()'s restated sampler chain (SampleLogits, gpttype_adapter.cpp:1338-1434) on caller logits, for the
  * host-side parity test (koboldcpp_amd/csrc/expose.cpp documents fp / ip / restarts); returns the drawn token */
 int kcpp_sampler_probe(const float *logits, int n_vocab, int n_ctx, const float *fp, const int *ip, const int *order,

@@ -670,6 +670,30 @@ generation_outputs generate(const generation_inputs in) {
 
 // GGUF header / tensor-table validation alone (the first step of load_model): 0 when the file parses, else -1 with
 // the reason in err (tests/test_gguf_loader.py)
+// the BPE pre-tokenizer alone (tests): byte end offsets of the words of text under pre-tokenizer type `pre` (the
+// GGUF tokenizer.ggml.pre value); returns the word count (at most cap offsets written)
+int kcpp_pretokenize(const char *pre, const char *text, int64_t *ends, int cap) {
+    if (!pre || !text) return -1;
+    const std::vector<size_t> e = Tokenizer::pretokenize_offsets(Tokenizer::pre_type(pre), std::string(text));
+    for (size_t i = 0; i < e.size() && (int)i < cap; ++i) ends[i] = (int64_t)e[i];
+    return (int)e.size();
+}
+
+// the GGUF's tokenizer alone (tests, host only): token ids of text (generate()'s tokenization: special tokens
+// parsed, BOS per the vocabulary when add_bos); returns the count (at most cap written), -1 on a load error
+int kcpp_tokenize_probe(const char *gguf_path, const char *text, int add_bos, int32_t *out, int cap) {
+    gguf::File f;
+    std::string err;
+    Tokenizer tk;
+    if (!gguf_path || !text || !f.open(gguf_path, err) || !tk.init(f, err)) {
+        if (!err.empty()) fprintf(stderr, "[kcpp] tokenize_probe: %s\n", err.c_str());
+        return -1;
+    }
+    const std::vector<int> ids = tk.encode(std::string(text), add_bos != 0);
+    for (size_t i = 0; i < ids.size() && (int)i < cap; ++i) out[i] = ids[i];
+    return (int)ids.size();
+}
+
 int kcpp_gguf_check(const char *path, char *err, int err_len) {
     gguf::File f;
     std::string e;

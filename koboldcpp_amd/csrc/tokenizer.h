@@ -1,9 +1,16 @@
 // tokenizer.h -- GGUF-vocabulary tokenizers for the drop-in generate() path.
 //   "llama" (SentencePiece BPE, llm_tokenizer_spm semantics, src/llama-vocab.cpp): "▁" for spaces, optional
 //     space prefix, greedy highest-score bigram merges over UTF-8 characters, <0xXX> byte fallback.
-//   "gpt2" (byte-level BPE, Llama-3): GPT-2 byte->unicode map, merges by rank; the pre-tokenizer follows the
-//     Llama-3 split regex with ASCII character classes (bytes >= 0x80 count as letters) -- exact for ASCII
-//     text, an approximation of \p{L}/\p{N} beyond it.
+//   "gpt2" (byte-level BPE, Llama-3): GPT-2 byte->unicode map, merges by rank (whole pre-token words found in the
+//     vocabulary taken as is for the Llama-3 pre-tokenizer: tokenizer_ignore_merges, src/llama-vocab.cpp:777); the
+//     pre-tokenizers are restated on code points with the Unicode classes \p{L} / \p{N} / \s of
+//     unicode_ranges.h: llama3 (unicode_regex_split_custom_llama3, src/unicode.cpp:355-492: "llama3", "llama-v3",
+//     "llama-bpe", "dbrx", "smaug-bpe", "chatglm-bpe"), qwen2 (the same with single-digit numbers: "qwen2",
+//     "stablelm2") and gpt2 (unicode_regex_split_custom_gpt2, :248-352: "gpt-2", "phi-2", "mpt", "olmo", "jais",
+//     "jina-*"; also every other pre type, for which the reference runs several std::regex passes -- an
+//     approximation there).  Invalid UTF-8 bytes become U+FFFD (the reference throws).
+// Special tokens (token types UNKNOWN / CONTROL / USER_DEFINED) are split out of the text first, longest first,
+// as tokenizer_st_partition with parse_special (src/llama-vocab.cpp:1544; koboldcpp's common_tokenize(..., true)).
 #pragma once
 #include <cstdint>
 #include <map>
@@ -13,6 +20,10 @@
 #include <vector>
 
 #include "gguf.h"
+#include "unicode_ranges.h"
+
+#include <algorithm>
+#include <cstring>
 
 class Tokenizer {
 public:
@@ -35,11 +46,24 @@ public:
             if (!m) { err = "BPE vocab without merges"; return false; }
             for (size_t i = 0; i < m->astr.size(); ++i) rank_.emplace(m->astr[i], (int)i);
             build_byte_map();
+            pre_ = pre_type(f.get_s("tokenizer.ggml.pre", "default"));
+            ignore_merges_ = pre_ == PRE_LLAMA3;
         } else if (model_ != "llama") {
             err = "unsupported tokenizer model " + model_;
             return false;
         }
+        for (size_t i = 0; i < vocab_.size(); ++i)     // cache_special_tokens (src/llama.cpp:6720-6733)
+            if ((ttype_[i] == 2 || ttype_[i] == 3 || ttype_[i] == 4) && !vocab_[i].empty()) special_.push_back((int)i);
+        std::stable_sort(special_.begin(), special_.end(),
+                         [&](int a, int b) { return vocab_[a].size() > vocab_[b].size(); });
         return true;
+    }
+    enum Pre { PRE_LLAMA3 = 0, PRE_QWEN2 = 1, PRE_GPT2 = 2 };
+    static Pre pre_type(const std::string &p) {
+        if (p == "llama3" || p == "llama-v3" || p == "llama-bpe" || p == "dbrx" || p == "smaug-bpe" || p == "chatglm-bpe")
+            return PRE_LLAMA3;
+        if (p == "qwen2" || p == "stablelm2") return PRE_QWEN2;
+        return PRE_GPT2;
     }
     int bos() const { return bos_; }
     int eos() const { return eos_; }
@@ -49,8 +73,44 @@ public:
         std::vector<int> out;
         if (add_bos && add_bos_) out.push_back(bos_);
         if (text.empty()) return out;
-        if (model_ == "llama") spm(text, out);
-        else bpe(text, out);
+        // fragments: raw text (id -1, byte range) and special tokens, in order
+        struct Frag { int id; size_t off, len; };
+        std::vector<Frag> fr{{-1, 0, text.size()}};
+        for (int sid : special_) {
+            const std::string &st = vocab_[sid];
+            std::vector<Frag> nx;
+            for (const Frag &g : fr) {
+                if (g.id >= 0) { nx.push_back(g); continue; }
+                size_t pos = g.off;
+                const size_t end = g.off + g.len;
+                while (true) {
+                    const size_t m = text.find(st, pos);
+                    if (m == std::string::npos || m + st.size() > end) break;
+                    if (m > pos) nx.push_back({-1, pos, m - pos});
+                    nx.push_back({sid, m, st.size()});
+                    pos = m + st.size();
+                }
+                if (pos < end) nx.push_back({-1, pos, end - pos});
+            }
+            fr.swap(nx);
+        }
+        bool prev_special = true;                      // SPM: space prefix at the start and after a special token
+        for (const Frag &g : fr) {
+            if (g.id >= 0) { out.push_back(g.id); prev_special = true; continue; }
+            const std::string raw = text.substr(g.off, g.len);
+            if (model_ == "llama") spm(raw, out, add_space_prefix_ && prev_special);
+            else bpe(raw, out);
+            prev_special = false;
+        }
+        return out;
+    }
+    // pre-tokenizer alone (tests): byte end offsets of the words of `text`
+    static std::vector<size_t> pretokenize_offsets(Pre pre, const std::string &text) {
+        std::vector<uint32_t> cp;
+        std::vector<size_t> bend;
+        decode_utf8(text, cp, bend);
+        std::vector<size_t> out;
+        for (size_t e : split_words(pre, cp)) out.push_back(bend[e - 1]);
         return out;
     }
     std::string piece(int id) const {            // text of one token (for streaming)
@@ -101,8 +161,8 @@ private:
     int find(const std::string &s) const { auto it = id_.find(s); return it == id_.end() ? -1 : it->second; }
 
     // ---- SentencePiece: highest-score adjacent merges (ties: leftmost)
-    void spm(const std::string &text, std::vector<int> &out) const {
-        std::string t = add_space_prefix_ ? " " + text : text;
+    void spm(const std::string &text, std::vector<int> &out, bool space_prefix) const {
+        std::string t = space_prefix ? " " + text : text;
         std::string n;
         for (char c : t) { if (c == ' ') n += "\xe2\x96\x81"; else n += c; }
         struct Sym { int prev, next; size_t off, len; };
@@ -164,60 +224,126 @@ private:
             u2b_[cp] = b;
         }
     }
-    static bool is_letter(unsigned char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c >= 0x80; }
-    static bool is_digit(unsigned char c) { return c >= '0' && c <= '9'; }
-    static bool is_space(unsigned char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f'; }
-    static bool is_nl(unsigned char c) { return c == '\n' || c == '\r'; }
-    std::vector<std::string> pretokenize(const std::string &s) const {
-        std::vector<std::string> w;
-        size_t i = 0, n = s.size();
-        auto lower = [](char c) { return (char)(c >= 'A' && c <= 'Z' ? c + 32 : c); };
-        while (i < n) {
+    // ---- pre-tokenizers over code points
+    static uint8_t cls(uint32_t c) {                   // 1 = \p{L}, 2 = \p{N}, 4 = \s
+        if (c < 0x80) {
+            if ((c | 0x20) >= 'a' && (c | 0x20) <= 'z') return 1;
+            if (c >= '0' && c <= '9') return 2;
+            return (c == ' ' || (c >= 9 && c <= 13)) ? 4 : 0;
+        }
+        int lo = 0, hi = ucd::kNumRanges - 1;
+        while (lo <= hi) {
+            const int mid = (lo + hi) / 2;
+            if (c < ucd::kRanges[mid].lo) hi = mid - 1;
+            else if (c > ucd::kRanges[mid].hi) lo = mid + 1;
+            else return ucd::kRanges[mid].f;
+        }
+        return 0;
+    }
+    // code points and each one's byte end offset; an invalid or truncated sequence is one U+FFFD per byte
+    static void decode_utf8(const std::string &s, std::vector<uint32_t> &cp, std::vector<size_t> &bend) {
+        for (size_t i = 0; i < s.size();) {
             const unsigned char c = (unsigned char)s[i];
-            if (c == '\'' && i + 1 < n) {              // contractions
-                static const char *cs[] = {"s", "t", "re", "ve", "m", "ll", "d"};
-                bool hit = false;
-                for (const char *x : cs) {
-                    const size_t L = strlen(x);
-                    if (i + 1 + L <= n) {
-                        bool ok = true;
-                        for (size_t k = 0; k < L; ++k) ok &= lower(s[i + 1 + k]) == x[k];
-                        if (ok) { w.push_back(s.substr(i, 1 + L)); i += 1 + L; hit = true; break; }
+            int n = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+            bool ok = n > 0 && i + n <= s.size();
+            for (int k = 1; ok && k < n; ++k) ok = ((unsigned char)s[i + k] >> 6) == 2;
+            if (!ok) { cp.push_back(0xFFFD); i += 1; bend.push_back(i); continue; }
+            uint32_t v = n == 1 ? c : c & (0xFF >> (n + 1));
+            for (int k = 1; k < n; ++k) v = (v << 6) | ((unsigned char)s[i + k] & 0x3F);
+            cp.push_back(v);
+            i += n;
+            bend.push_back(i);
+        }
+    }
+    static uint32_t lower_ascii(uint32_t c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
+    // word end positions (code point indices) -- llama3 / qwen2: unicode_regex_split_custom_llama3 semantics,
+    // gpt2: unicode_regex_split_custom_gpt2 (src/unicode.cpp)
+    static std::vector<size_t> split_words(Pre pre, const std::vector<uint32_t> &cp) {
+        std::vector<size_t> ends;
+        const size_t n = cp.size();
+        auto F = [&](size_t k) -> int { return k < n ? cls(cp[k]) : -1; };   // -1: past the end (no flags)
+        auto NL = [&](size_t k) { return k < n && (cp[k] == '\r' || cp[k] == '\n'); };
+        size_t pos = 0;
+        auto emit = [&](size_t e) { if (e > pos) ends.push_back(e); pos = e; };
+        while (pos < n) {
+            const uint32_t c = cp[pos];
+            const int f = F(pos);
+            if (c == '\'' && pos + 1 < n) {                // contractions (case-insensitive for llama3 / qwen2)
+                const uint32_t c1 = pre == PRE_GPT2 ? cp[pos + 1] : lower_ascii(cp[pos + 1]);
+                if (c1 == 's' || c1 == 't' || c1 == 'm' || c1 == 'd') { emit(pos + 2); continue; }
+                if (pos + 2 < n) {
+                    const uint32_t c2 = pre == PRE_GPT2 ? cp[pos + 2] : lower_ascii(cp[pos + 2]);
+                    if ((c1 == 'r' && c2 == 'e') || (c1 == 'v' && c2 == 'e') || (c1 == 'l' && c2 == 'l')) { emit(pos + 3); continue; }
+                }
+            }
+            if (pre == PRE_GPT2) {
+                const int f2 = c == ' ' ? F(pos + 1) : f;
+                if (f2 > 0 && (f2 & 1)) {                   //  ?\p{L}+
+                    size_t e = pos + (c == ' ');
+                    while (F(e) > 0 && (F(e) & 1)) ++e;
+                    emit(e); continue;
+                }
+                if (f2 > 0 && (f2 & 2)) {                   //  ?\p{N}+
+                    size_t e = pos + (c == ' ');
+                    while (F(e) > 0 && (F(e) & 2)) ++e;
+                    emit(e); continue;
+                }
+                if (f2 >= 0 && !(f2 & 7)) {                 //  ?[^\s\p{L}\p{N}]+
+                    size_t e = pos + (c == ' ');
+                    while (F(e) >= 0 && !(F(e) & 7)) ++e;
+                    emit(e); continue;
+                }
+            } else {
+                if (!(c == '\r' || c == '\n' || (f & 2))) {  // [^\r\n\p{L}\p{N}]?\p{L}+
+                    if ((f & 1) || (F(pos + 1) > 0 && (F(pos + 1) & 1))) {
+                        size_t e = pos + 1;
+                        while (F(e) > 0 && (F(e) & 1)) ++e;
+                        emit(e); continue;
                     }
                 }
-                if (hit) continue;
+                if (f & 2) {                                // \p{N}{1,3} (qwen2: \p{N})
+                    const size_t maxr = pre == PRE_QWEN2 ? 1 : 3;
+                    size_t e = pos;
+                    while (F(e) > 0 && (F(e) & 2) && e - pos < maxr) ++e;
+                    emit(e); continue;
+                }
+                const int f2 = c == ' ' ? F(pos + 1) : f;   //  ?[^\s\p{L}\p{N}]+[\r\n]*
+                if (f2 >= 0 && !(f2 & 7)) {
+                    size_t e = pos + (c == ' ');
+                    while (F(e) >= 0 && !(F(e) & 7)) ++e;
+                    while (NL(e)) ++e;
+                    emit(e); continue;
+                }
             }
-            if (is_letter(c) || (!is_nl(c) && !is_digit(c) && !is_letter(c) && i + 1 < n && is_letter((unsigned char)s[i + 1]) && !is_space(c))
-                || (c == ' ' && i + 1 < n && is_letter((unsigned char)s[i + 1]))) {
-                size_t j = is_letter(c) ? i : i + 1;
-                while (j < n && is_letter((unsigned char)s[j])) ++j;
-                w.push_back(s.substr(i, j - i)); i = j; continue;
+            size_t nws = 0, last_nl = 0;
+            while (F(pos + nws) > 0 && (F(pos + nws) & 4)) {
+                if (NL(pos + nws)) last_nl = pos + nws + 1;
+                ++nws;
             }
-            if (is_digit(c)) {
-                size_t j = i;
-                while (j < n && j < i + 3 && is_digit((unsigned char)s[j])) ++j;
-                w.push_back(s.substr(i, j - i)); i = j; continue;
-            }
-            if (!is_space(c) || (c == ' ' && i + 1 < n && !is_space((unsigned char)s[i + 1]) && !is_letter((unsigned char)s[i + 1]) && !is_digit((unsigned char)s[i + 1]))) {
-                size_t j = (c == ' ') ? i + 1 : i;
-                while (j < n && !is_space((unsigned char)s[j]) && !is_letter((unsigned char)s[j]) && !is_digit((unsigned char)s[j])) ++j;
-                while (j < n && is_nl((unsigned char)s[j])) ++j;
-                w.push_back(s.substr(i, j - i)); i = j; continue;
-            }
-            size_t j = i;                               // whitespace
-            while (j < n && is_space((unsigned char)s[j])) ++j;
-            size_t last_nl = std::string::npos;
-            for (size_t k = i; k < j; ++k) if (is_nl((unsigned char)s[k])) last_nl = k;
-            if (last_nl != std::string::npos) { w.push_back(s.substr(i, last_nl + 1 - i)); i = last_nl + 1; continue; }
-            if (j < n && j - i > 1) { w.push_back(s.substr(i, j - 1 - i)); i = j - 1; continue; }   // \s+(?!\S)
-            w.push_back(s.substr(i, j - i)); i = j;
+            if (pre != PRE_GPT2 && last_nl > 0) { emit(last_nl); continue; }   // \s*[\r\n]+
+            if (nws > 1 && pos + nws < n) { emit(pos + nws - 1); continue; }   // \s+(?!\S)
+            if (nws > 0) { emit(pos + nws); continue; }                       // \s+
+            emit(pos + 1);                                                    // no match
         }
-        return w;
+        return ends;
     }
     void bpe(const std::string &text, std::vector<int> &out) const {
-        for (const std::string &word : pretokenize(text)) {
+        std::vector<uint32_t> cp;
+        std::vector<size_t> bend;
+        decode_utf8(text, cp, bend);
+        size_t w0 = 0;
+        for (size_t e : split_words(pre_, cp)) {
+            std::string word;                           // the word's code points re-encoded (U+FFFD for bad bytes)
+            for (size_t k = w0; k < e; ++k) word += utf8_enc(cp[k]);
+            w0 = e;
             std::vector<std::string> parts;
             for (unsigned char c : word) parts.push_back(b2u_[c]);
+            if (ignore_merges_) {
+                std::string whole;
+                for (const std::string &p : parts) whole += p;
+                const int id = find(whole);
+                if (id >= 0) { out.push_back(id); continue; }
+            }
             while (parts.size() > 1) {
                 int best = -1, br = INT32_MAX;
                 for (size_t k = 0; k + 1 < parts.size(); ++k) {
@@ -236,6 +362,9 @@ private:
     }
 
     std::string model_;
+    Pre pre_ = PRE_LLAMA3;
+    bool ignore_merges_ = false;
+    std::vector<int> special_;
     std::vector<std::string> vocab_;
     std::unordered_map<std::string, int> id_;
     std::vector<float> scores_;

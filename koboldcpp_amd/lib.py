@@ -50,6 +50,8 @@ _SIGS = {
     "kcpp_fa_decode_ex": [P, P, P, I64, I64, P, P, P, I, I, I, P, I, Fl, I, P],
     "kcpp_fa_set_stamps": [P],
     "kcpp_gguf_check": [ctypes.c_char_p, ctypes.c_char_p, I],
+    "kcpp_pretokenize": [ctypes.c_char_p, ctypes.c_char_p, P, I],
+    "kcpp_tokenize_probe": [ctypes.c_char_p, ctypes.c_char_p, I, P, I],
     "kcpp_add": [P, P, P, I64, P],
     "kcpp_silu_mul": [P, P, P, I64, P],
     "kcpp_moe_route": [P, I64, P, I, I64, I, I, P, P, I, P],
