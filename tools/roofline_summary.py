@@ -48,7 +48,7 @@ res = {
     "bench_hip_event_avg_us": bench_line["roofline"]["avg_us"] if bench_line else None,
     "algorithmic_bytes_per_launch": bench_line["roofline"]["bytes_per_launch"] if bench_line else None,
     "note": "FETCH_SIZE doubled (gfx950: half the bytes of wide coalesced reads); includes the warm-up launches; "
-            "4 weight pairs rotated so the 256 MiB Infinity Cache cannot serve repeats",
+            "8 weight pairs (504 MiB) rotated so the 256 MiB Infinity Cache cannot serve repeats",
 }
 os.makedirs(os.path.join(root, "profiles"), exist_ok=True)
 with open(os.path.join(root, "profiles", tag + "_roofline_pmc.json"), "w") as f:
