@@ -774,7 +774,8 @@ template <int LAY, int NW, int BMT>
 __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                                          const h8v *__restrict__ af, const float *__restrict__ dyT,
                                                          const h8v *__restrict__ bsf, int64_t M, int64_t Mp, int MT,
-                                                         float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr) {
+                                                         float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr,
+                                                         int KS, float *__restrict__ part) {
     constexpr int TPW = 4 * BMT / NW;         // token tiles per wave
     constexpr int SPW = 16 * BMT / NW;        // A staging: LDS-DMA steps per wave and super-block
     static_assert(TPW >= 1 && SPW >= 1, "tile shape");
@@ -784,7 +785,10 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
     const int wr = wave & 3, wt = wave >> 2;
     const int lr = lane & 31, kg = lane >> 5;
     // XCD-aware tile order (as k_gemm_kq): ids with equal id % 8 share a token tile when MT divides 8
-    const int64_t id = blockIdx.x, nwg = gridDim.x;
+    // KS > 1: split-K -- the grid is KS copies of the tile grid, copy `split` covers super-blocks
+    // [split nsb / KS, (split + 1) nsb / KS) and writes its fp32 partial tile to part [KS][Mp][N]
+    const int64_t nwg = gridDim.x / KS, id = blockIdx.x % nwg;
+    const int split = (int)(blockIdx.x / nwg);
     int64_t mt, nt;
     if (8 % MT == 0 && nwg % 8 == 0) {
         const int64_t x = id & 7, j = id >> 3;
@@ -826,25 +830,26 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
         for (int p = 0; p < 4; ++p) qn[p] = ldg16(qp + QS * sb + 32 * p);
     };
 
+    const int64_t sbb = nsb * split / KS, sbe = nsb * (split + 1) / KS;
     f16acc tot[TPW];
 #pragma unroll
     for (int j = 0; j < TPW; ++j)
 #pragma unroll
         for (int i = 0; i < 16; ++i) tot[j][i] = 0.0f;
-    stage(0, 0);
-    load_raw(0);
+    stage(0, sbb);
+    load_raw(sbb);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    for (int64_t sb = 0; sb < nsb; ++sb) {
-        const int buf = (int)(sb & 1);
+    for (int64_t sb = sbb; sb < sbe; ++sb) {
+        const int buf = (int)((sb - sbb) & 1);
         const uint4 hc = hn;
         uint32_t sc_lo, sc_hi, m_lo, m_hi;
         k4_all(hc, sc_lo, sc_hi, m_lo, m_hi);
         uint4 qc[4];
 #pragma unroll
         for (int p = 0; p < 4; ++p) qc[p] = qn[p];
-        if (sb + 1 < nsb) {
+        if (sb + 1 < sbe) {
             stage(buf ^ 1, sb + 1);
             load_raw(sb + 1);
         }
@@ -918,8 +923,20 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int64_t t = m0 + 32 * (TPW * wt + j) + (r & 3) + 8 * (r >> 2) + 4 * kg;
-            if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
+            if (KS > 1) part[((int64_t)split * Mp + t) * N + n] = tot[j][r];
+            else if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
         }
+}
+
+// split-K partials [KS][Mp][N] summed in split order, then the residual (the unsplit kernel's tot + res)
+__global__ void k_splitk_reduce(const float *__restrict__ part, int KS, int64_t M, int64_t Mp, int64_t N,
+                                float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= M * N) return;
+    const int64_t t = i / N, n = i % N;
+    float g = part[t * N + n];
+    for (int k = 1; k < KS; ++k) g = __fadd_rn(g, part[((int64_t)k * Mp + t) * N + n]);
+    Y[t * ldy + n] = res ? __fadd_rn(g, res[t * ldr + n]) : g;
 }
 
 // ================================================================ Q6_K GEMM v3 (row-major decode layout Q6_K_RS)
@@ -965,7 +982,7 @@ template <int NW, int BMT>
 __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6v3(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                                          const h8v *__restrict__ af, const float *__restrict__ dyT,
                                                          int64_t M, int64_t Mp, int MT, float *__restrict__ Y, int64_t ldy,
-                                                         const float *res, int64_t ldr) {
+                                                         const float *res, int64_t ldr, int KS, float *__restrict__ part) {
     constexpr int TPW = 4 * BMT / NW;
     constexpr int SPW = 16 * BMT / NW;
     static_assert(TPW >= 1 && SPW >= 1, "tile shape");
@@ -974,7 +991,10 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6v3(const uint8_t *__restr
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave & 3, wt = wave >> 2;
     const int lr = lane & 31, kg = lane >> 5;
-    const int64_t id = blockIdx.x, nwg = gridDim.x;
+    // KS > 1: split-K -- the grid is KS copies of the tile grid, copy `split` covers super-blocks
+    // [split nsb / KS, (split + 1) nsb / KS) and writes its fp32 partial tile to part [KS][Mp][N]
+    const int64_t nwg = gridDim.x / KS, id = blockIdx.x % nwg;
+    const int split = (int)(blockIdx.x / nwg);
     int64_t mt, nt;
     if (8 % MT == 0 && nwg % 8 == 0) {
         const int64_t x = id & 7, j = id >> 3;
@@ -1014,24 +1034,25 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6v3(const uint8_t *__restr
         nd = pd[sb];
     };
 
+    const int64_t sbb = nsb * split / KS, sbe = nsb * (split + 1) / KS;
     f16acc tot[TPW];
 #pragma unroll
     for (int j = 0; j < TPW; ++j)
 #pragma unroll
         for (int i = 0; i < 16; ++i) tot[j][i] = 0.0f;
-    stage(0, 0);
-    load_raw(0);
+    stage(0, sbb);
+    load_raw(sbb);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    for (int64_t sb = 0; sb < nsb; ++sb) {
-        const int buf = (int)(sb & 1);
+    for (int64_t sb = sbb; sb < sbe; ++sb) {
+        const int buf = (int)((sb - sbb) & 1);
         uint2 clo[4], chi[4], cqh[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) { clo[u] = nlo[u]; chi[u] = nhi[u]; cqh[u] = nqh[u]; }
         const uint4 csc = nsc;
         const uint16_t cd = nd;
-        if (sb + 1 < nsb) {
+        if (sb + 1 < sbe) {
             stage(buf ^ 1, sb + 1);
             load_raw(sb + 1);
         }
@@ -1090,7 +1111,8 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6v3(const uint8_t *__restr
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int64_t t = m0 + 32 * (TPW * wt + j) + (r & 3) + 8 * (r >> 2) + 4 * kg;
-            if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
+            if (KS > 1) part[((int64_t)split * Mp + t) * N + n] = tot[j][r];
+            else if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
         }
 }
 
@@ -1274,6 +1296,7 @@ static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a
     o_bs = off; off += (Mp * (K / 16) * 2 + 255) & ~255LL;
     o_up = off; off += (M * N * 4 + 255) & ~255LL;
     if (type == KT_Q8_0) off += 2 * (int64_t)q80s_splits(K, N) * 32 * N * 4;   // small-M split-K partials (g, u)
+    if (type == KT_Q4_K || type == KT_Q4_K_RS || type == KT_Q6_K_RS) off += 2 * Mp * N * 4;   // v3 split-K partials
     return off;
 }
 
@@ -1375,10 +1398,19 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     const int vt = vec_dot_type(type);
     if (type == KT_Q8_0 && M <= 32 && K % 32 == 0) return gemm_q80_small(W, W2, K, N, act, M, Y, ldy, res, ldr, mode, nullptr,
                                                                         w8 + o_up + ((M * N * 4 + 255) & ~255LL), s);
-    // v3: 128 tokens x 128 rows per workgroup when that gives >= 384 workgroups, else 64 x 128 (BMT = 2);
-    // KCPP_GEMM_V / kcpp_gemm_set_variant: 2 forces v2, 3 forces v3
+    // v3: 128 tokens x 128 rows per workgroup when that gives >= 384 workgroups, else 64 x 128 (BMT = 2); on those
+    // small grids the K range is split in two (KS = 2: twice the workgroups, two per CU, partials summed in order by
+    // k_splitk_reduce) when the grid is tiny (< 128 workgroups) or K long (>= 32 super-blocks): measured at M = 512
+    // (tools/gemm_ab.py) down 14336 x 4096 122.9 -> 112.3 us, attn_v 4096 x 1024 (Q6_K) 56.7 -> 33.9 us, wo 4096 x 4096
+    // 43.3 -> 45.6 us (not split), gate|up (big grid) 236.8 -> 273.0 us (not split).
+    // kcpp_gemm_set_variant: 2 forces v2, 3 v3 without the split, 4 v3 with the split wherever the mode allows
     const int gv = gemm_variant();
-    const bool v3 = gv == 3 || gv == 0;
+    const bool v3 = gv == 3 || gv == 0 || gv == 4;
+    float *part = (float *)(w8 + o_up + ((M * N * 4 + 255) & ~255LL));
+    auto splitk = [&](bool big, int64_t tiles) {
+        if (mode != 0 || (K / 256) % 2) return 1;
+        return (gv == 4 || (gv == 0 && !big && (tiles < 128 || K / 256 >= 32))) ? 2 : 1;
+    };
     if ((type == KT_Q4_K || type == KT_Q4_K_RS) && v3) {
         const int64_t nth = Mp * K / 8 + (Mp / 32) * (K / 256) * 64 + Mp * (K / 256);
         hipLaunchKernelGGL(k_act_frag3, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
@@ -1391,17 +1423,23 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         const int BMT = big ? 4 : 2;
         const int NWv = big ? 8 : 4;
         const int MT = (int)(Mp / (32 * BMT));
-        const unsigned nwg = (unsigned)(MT * nt);
+        const int KS = splitk(big, MT * nt);
+        const unsigned nwg = (unsigned)(MT * nt * KS);
         auto launch3 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
 #define KCPP_V3(L_, NW_, B_)                                                                                                 \
     hipLaunchKernelGGL((k_gemm_q4v3<L_, NW_, B_>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, \
-                       dy, (const h8v *)bs16, M, Mp, MT, y, ly, r, lr)
+                       dy, (const h8v *)bs16, M, Mp, MT, y, ly, r, lr, KS, part)
 #define KCPP_V3B(L_, B_) { if (NWv == 4) KCPP_V3(L_, 4, B_); else KCPP_V3(L_, 8, B_); }
             if (type == KT_Q4_K_RS) { if (BMT == 2) KCPP_V3B(1, 2) else KCPP_V3B(1, 4) }
             else { if (BMT == 2) KCPP_V3B(0, 2) else KCPP_V3B(0, 4) }
 #undef KCPP_V3B
 #undef KCPP_V3
             KCPP_CHECK(hipGetLastError());
+            if (KS > 1) {
+                hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,
+                                   ly, r, lr);
+                KCPP_CHECK(hipGetLastError());
+            }
             return 0;
         };
         int rc = launch3(W, Y, ldy, mode == 1 ? nullptr : res, ldr);
@@ -1421,15 +1459,21 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         const int BMT = big ? 4 : 2;
         const int NWv = big ? 8 : 4;
         const int MT = (int)(Mp / (32 * BMT));
-        const unsigned nwg = (unsigned)(MT * nt);
+        const int KS = splitk(big, MT * nt);
+        const unsigned nwg = (unsigned)(MT * nt * KS);
         auto launch6 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
 #define KCPP_V6(NW_, B_)                                                                                                   \
     hipLaunchKernelGGL((k_gemm_q6v3<NW_, B_>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, \
-                       M, Mp, MT, y, ly, r, lr)
+                       M, Mp, MT, y, ly, r, lr, KS, part)
             if (BMT == 2) { if (NWv == 4) KCPP_V6(4, 2); else KCPP_V6(8, 2); }
             else { if (NWv == 4) KCPP_V6(4, 4); else KCPP_V6(8, 4); }
 #undef KCPP_V6
             KCPP_CHECK(hipGetLastError());
+            if (KS > 1) {
+                hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,
+                                   ly, r, lr);
+                KCPP_CHECK(hipGetLastError());
+            }
             return 0;
         };
         int rc = launch6(W, Y, ldy, mode == 1 ? nullptr : res, ldr);

@@ -179,6 +179,7 @@ def test_rs_columns_and_gemm(env, base, M):
     K.call("kcpp_quantize_act", K.vec_dot_type(base), X.data_ptr(), Kd, act.data_ptr(), Kd, M, s)
     res = torch.randn(M, N).cuda()
     ys = []
+    K.raw().kcpp_gemm_set_variant(3)       # the unsplit kernels: Q6_K's base layout runs v2, its RS layout v3
     for tt in (base, t):
         W, W2 = _synth(torch, K, tt, Kd, N, 8), _synth(torch, K, tt, Kd, N, 9)
         for mode in (0, 1):
@@ -193,6 +194,7 @@ def test_rs_columns_and_gemm(env, base, M):
                        ws.data_ptr(), s)
             torch.cuda.synchronize()
             ys.append(Y.cpu().numpy())
+    K.raw().kcpp_gemm_set_variant(0)
     for a_, b_ in zip(ys[:2], ys[2:]):
         if M > 8:
             assert np.array_equal(a_.view(np.uint32), b_.view(np.uint32))
@@ -232,3 +234,40 @@ def test_gemm_v3_matches_v2_bitwise(env, base, Kd, N, M):
     for mode in (0, 1):
         assert np.isfinite(outs[3, mode]).all()
         assert np.array_equal(outs[2, mode].view(np.uint32), outs[3, mode].view(np.uint32)), mode
+
+
+@pytest.mark.parametrize("base", [R.Q4_K, "rs", "rs6"])
+@pytest.mark.parametrize("Kd,N,M", [(4096, 512, 37), (14336, 256, 512), (2048, 384, 300)])
+def test_gemm_v3_split_k(env, base, Kd, N, M):
+    """v3 with the K range split in two (kcpp_gemm_set_variant(4); the default for grids under 384 workgroups):
+    each half's fp32 partial is the unsplit kernel's running sum over its super-blocks, added in split order and
+    then to the residual -- equal to the unsplit result up to that one re-association (<= 2e-6 of the output
+    scale) and to the oracle within the GEMM bar"""
+    torch, K = env
+    t = {"rs": RS[R.Q4_K], "rs6": RS[R.Q6_K]}.get(base, R.Q4_K)
+    bt = R.Q6_K if base == "rs6" else R.Q4_K
+    s = sptr(torch)
+    Xh = np.random.default_rng(M + Kd + 1).standard_normal((M, Kd)).astype(np.float32)
+    X = torch.from_numpy(Xh).cuda()
+    act = torch.zeros(K.act_bytes(R.Q4_K, Kd, M), dtype=torch.uint8, device="cuda")
+    K.call("kcpp_quantize_act", K.vec_dot_type(R.Q4_K), X.data_ptr(), Kd, act.data_ptr(), Kd, M, s)
+    resh = np.random.default_rng(M + N).standard_normal((M, N)).astype(np.float32)
+    res = torch.from_numpy(resh).cuda()
+    W = _synth(torch, K, t, Kd, N, 5)
+    ws = torch.empty(K.raw().kcpp_gemm_workspace_bytes(t, Kd, N, M), dtype=torch.uint8, device="cuda")
+    outs = {}
+    try:
+        for v in (3, 4):
+            K.raw().kcpp_gemm_set_variant(v)
+            Y = torch.full((M, N), float("nan"), device="cuda")
+            K.call("kcpp_gemm", t, W.data_ptr(), None, Kd, N, act.data_ptr(), M, Y.data_ptr(), N, res.data_ptr(), N, 0,
+                   ws.data_ptr(), s)
+            torch.cuda.synchronize()
+            outs[v] = Y.cpu().numpy()
+    finally:
+        K.raw().kcpp_gemm_set_variant(0)
+    assert np.isfinite(outs[4]).all()
+    scale = max(1.0, float(np.abs(outs[3]).max()))
+    assert np.abs(outs[4] - outs[3]).max() <= 2e-6 * scale
+    want = R.mul_mat(bt, R.synth(bt, 7, 5, Kd, N), Kd, N, Xh) + resh
+    assert np.abs(outs[4] - want).max() <= 3e-6 * max(1.0, float(np.abs(want).max())) + 1e-5
