@@ -127,6 +127,7 @@ template <int TYPE> struct GemmTraits {
 template <> struct GemmTraits<KT_Q4_K> { static constexpr int NB = 1; static constexpr bool MINS = true; static constexpr bool SB = true; };
 template <> struct GemmTraits<KT_Q5_K> { static constexpr int NB = 1; static constexpr bool MINS = true; static constexpr bool SB = true; };
 template <> struct GemmTraits<KT_Q6_K> { static constexpr int NB = 2; static constexpr bool MINS = false; static constexpr bool SB = true; };
+template <> struct GemmTraits<KT_Q3_K> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = true; };
 template <> struct GemmTraits<KT_Q4_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
 template <> struct GemmTraits<KT_Q8_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
 
@@ -202,6 +203,33 @@ __device__ __forceinline__ void stage_weights(SM &S, const uint8_t *__restrict__
             }
         }
         if (c == 0) S.wd[nl][0] = h2f(*(const uint16_t *)(W + nbt * 208 + b * 2));
+    } else if constexpr (TYPE == KT_Q3_K) {
+        // chunk c = quarter c of the super-block (half n = c >> 1, shifts j0 = 2 (c & 1), j0 + 1); weights
+        // (sc - 32) (v - 4) with v = 2 low bits | hmask bit << 2 -- exact f16 integers (|.| <= 128); SoA planes
+        // (quant.hip kl_store_block): hmask [nb][32], qs [nb][64], scales [nb][12], d [nb][2]
+        const int64_t b = n * bpr + sb;
+        const int hn = c >> 1, j0 = 2 * (c & 1);
+        const uint4 h0 = *(const uint4 *)(W + b * 32), h1 = *(const uint4 *)(W + b * 32 + 16);
+        const uint8_t *qp = W + nbt * 32 + b * 64 + 32 * hn;
+        const uint4 q0 = *(const uint4 *)qp, q1 = *(const uint4 *)(qp + 16);
+        const uint32_t *scp = (const uint32_t *)(W + nbt * 96 + b * 12);
+        const uint32_t a0 = scp[0], a1 = scp[1], a2 = scp[2];
+        const uint32_t k1 = 0x03030303u, k2 = 0x0f0f0f0fu;
+        const uint32_t sw = c == 0 ? (a0 & k2) | ((a2 & k1) << 4)
+                          : c == 1 ? (a1 & k2) | (((a2 >> 2) & k1) << 4)
+                          : c == 2 ? ((a0 >> 4) & k2) | (((a2 >> 4) & k1) << 4)
+                                   : ((a1 >> 4) & k2) | (((a2 >> 6) & k1) << 4);
+        const uint32_t qd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        const uint32_t hd[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = j0 + (i >> 2), w0 = 2 * (i & 3);            // elements l = 8 (i & 3) .. + 7
+            const uint32_t v0 = ((qd[w0] >> (2 * j)) & 0x03030303u) | (((hd[w0] >> (4 * hn + j)) & 0x01010101u) << 2);
+            const uint32_t v1 = ((qd[w0 + 1] >> (2 * j)) & 0x03030303u) | (((hd[w0 + 1] >> (4 * hn + j)) & 0x01010101u) << 2);
+            const int sc = (int)((sw >> (8 * (2 * (i >> 2) + ((i & 3) >> 1)))) & 0xFF) - 32;
+            S.bf[0][bslot(nl, 64 * c + 8 * i)] = frag8_sub(v0, v1, (float)sc, 4.0f);
+        }
+        if (c == 0) S.wd[nl][0] = h2f(*(const uint16_t *)(W + nbt * 108 + b * 2));
     } else if constexpr (TYPE == KT_Q4_0) {
         // this thread: 32-blocks 2c, 2c+1 of the 8 in the super-step
 #pragma unroll
@@ -1525,6 +1553,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     const dim3 grid((unsigned)((N + GB_N - 1) / GB_N), (unsigned)(Mp / GB_M));
     auto launch = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
         switch (type) {
+        case KT_Q3_K: hipLaunchKernelGGL(k_gemm<KT_Q3_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         case KT_Q4_0: hipLaunchKernelGGL(k_gemm<KT_Q4_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         case KT_Q8_0: hipLaunchKernelGGL(k_gemm<KT_Q8_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         default: return -3;

@@ -55,6 +55,27 @@ template <> struct Unit<KT_Q6_K> {
         d = *(const uint16_t *)(base + nb * 208 + b * 2);
     }
 };
+// ---- Q3_K (SoA planes, quant.hip kl_store_block): unit u = quarter qq = u & 3 of super-block u >> 2, i.e. the 64
+// elements of half n = qq >> 1, shifts j0 = 2 (qq & 1) and j0 + 1 (dequantize_row_q3_K, ggml-quants.c:2328):
+// qs bytes 32n..32n+31, all 32 hmask bytes (bits 4n + j), the scale word qq (scales 4qq..4qq+3), d
+template <> struct Unit<KT_Q3_K> {
+    static constexpr int ELEMS = 64;
+    uint4 q0, q1, h0, h1;
+    uint32_t s0, s1, s2;
+    uint16_t d;
+    __device__ __forceinline__ void load(const uint8_t *base, int64_t nb, int64_t b0, int u) {
+        const int64_t b = b0 + (u >> 2);
+        const int n = (u >> 1) & 1;
+        const uint8_t *q = base + nb * 32 + b * 64 + 32 * n;
+        q0 = ld_nt((const void *)q);
+        q1 = ld_nt((const void *)(q + 16));
+        h0 = *(const uint4 *)(base + b * 32);
+        h1 = *(const uint4 *)(base + b * 32 + 16);
+        const uint32_t *sc = (const uint32_t *)(base + nb * 96 + b * 12);
+        s0 = sc[0]; s1 = sc[1]; s2 = sc[2];
+        d = *(const uint16_t *)(base + nb * 108 + b * 2);
+    }
+};
 // ---- Q4_0 (SoA): unit = one 32-elem block: 16 B nibbles + fp16 d
 template <> struct Unit<KT_Q4_0> {
     static constexpr int ELEMS = 32;
@@ -220,6 +241,33 @@ __device__ __forceinline__ float unit_dot(const Unit<KT_Q6_K> &w, int u, const A
     return __fmul_rn(__fmul_rn(h2f(w.d), x.d), (float)sumi);
 }
 
+// Q3_K: v = low 2 bits | hmask bit << 2 (0..7) is the weight + 4, so each 16-group's dot is sum(v a) - 4 bsum;
+// scale word qq of the unpacked 16 (aux shuffle, ggml-quants.c:2346-2351) holds this unit's 4 scales
+__device__ __forceinline__ float unit_dot(const Unit<KT_Q3_K> &w, int u, const ActK &x) {
+    const int qq = u & 3, n = qq >> 1, j0 = 2 * (qq & 1);
+    const uint32_t k1 = 0x03030303u, k2 = 0x0f0f0f0fu;
+    const uint32_t sw = qq == 0 ? (w.s0 & k2) | ((w.s2 & k1) << 4)
+                      : qq == 1 ? (w.s1 & k2) | (((w.s2 >> 2) & k1) << 4)
+                      : qq == 2 ? ((w.s0 >> 4) & k2) | (((w.s2 >> 4) & k1) << 4)
+                                : ((w.s1 >> 4) & k2) | (((w.s2 >> 6) & k1) << 4);
+    int sumi = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int j = j0 + (g >> 1);
+        int dot = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int wi = 4 * (g & 1) + t;                  // qs / hmask dword: l = 4 wi .. 4 wi + 3
+            const uint32_t qd = wi < 4 ? u4(w.q0, wi) : u4(w.q1, wi - 4);
+            const uint32_t hd = wi < 4 ? u4(w.h0, wi) : u4(w.h1, wi - 4);
+            const uint32_t v = ((qd >> (2 * j)) & 0x03030303u) | (((hd >> (4 * n + j)) & 0x01010101u) << 2);
+            dot = sdot4((int)v, ai(x, 4 * g + t), dot);
+        }
+        sumi += ((int)((sw >> (8 * g)) & 0xFF) - 32) * (dot - 4 * x.bs[g]);
+    }
+    return __fmul_rn(__fmul_rn(h2f(w.d), x.d), (float)sumi);
+}
+
 __device__ __forceinline__ float unit_dot(const Unit<KT_Q4_0> &w, int, const Act0 &x) {
     int s = 0;
 #pragma unroll
@@ -247,7 +295,7 @@ template <int TYPE>
 __device__ __forceinline__ void load_unit(Unit<TYPE> &w, const uint8_t *W, int64_t nb, int64_t row, int64_t units_per_row, int u) {
     if constexpr (TYPE == KT_Q4_K) w.load(W + row * (units_per_row / 4) * 144, nb, u);
     else if constexpr (TYPE == KT_Q5_K) w.load(W + row * (units_per_row / 4) * 176, nb, u);
-    else if constexpr (TYPE == KT_Q6_K) w.load(W, nb, row * (units_per_row / 4), u);
+    else if constexpr (TYPE == KT_Q6_K || TYPE == KT_Q3_K) w.load(W, nb, row * (units_per_row / 4), u);
     else w.load(W, nb, row * units_per_row, u);
 }
 

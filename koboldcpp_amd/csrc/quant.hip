@@ -12,6 +12,13 @@
 __device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uint8_t *dst, int64_t b, int64_t nb,
                                                int64_t bpr) {
     switch (type) {
+    case KT_Q3_K: {   // SoA planes: hmask [nb][32] ++ qs [nb][64] ++ scales [nb][12] ++ d [nb][2] (16-B aligned loads)
+        uint8_t *hm = dst + b * 32, *q = dst + nb * 32 + b * 64, *sc = dst + nb * 96 + b * 12, *d = dst + nb * 108 + b * 2;
+        for (int i = 0; i < 32; ++i) hm[i] = src[i];
+        for (int i = 0; i < 64; ++i) q[i] = src[32 + i];
+        for (int i = 0; i < 12; ++i) sc[i] = src[96 + i];
+        d[0] = src[108]; d[1] = src[109];
+    } break;
     case KT_Q6_K: {
         uint8_t *q = dst + b * 192, *sc = dst + nb * 192 + b * 16, *d = dst + nb * 208 + b * 2;
         for (int i = 0; i < 192; ++i) q[i] = src[i];
@@ -58,6 +65,13 @@ __device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uin
 __device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint8_t *blk, int64_t b, int64_t nb,
                                               int64_t bpr) {
     switch (type) {
+    case KT_Q3_K: {
+        const uint8_t *hm = src + b * 32, *q = src + nb * 32 + b * 64, *sc = src + nb * 96 + b * 12, *d = src + nb * 108 + b * 2;
+        for (int i = 0; i < 32; ++i) blk[i] = hm[i];
+        for (int i = 0; i < 64; ++i) blk[32 + i] = q[i];
+        for (int i = 0; i < 12; ++i) blk[96 + i] = sc[i];
+        blk[108] = d[0]; blk[109] = d[1];
+    } break;
     case KT_Q6_K: {
         const uint8_t *q = src + b * 192, *sc = src + nb * 192 + b * 16, *d = src + nb * 208 + b * 2;
         for (int i = 0; i < 192; ++i) blk[i] = q[i];
@@ -133,6 +147,19 @@ __device__ __forceinline__ void scale_min_k4(int j, const uint8_t *q, int &d, in
     }
 }
 
+// the 16 biased 6-bit Q3_K scales from the 12 packed bytes (dequantize_row_q3_K, ggml-quants.c:2346-2351)
+__device__ __forceinline__ void q3k_scales(const uint8_t *s12, int8_t *sc) {
+    uint32_t a0 = s12[0] | (s12[1] << 8) | (s12[2] << 16) | ((uint32_t)s12[3] << 24);
+    uint32_t a1 = s12[4] | (s12[5] << 8) | (s12[6] << 16) | ((uint32_t)s12[7] << 24);
+    const uint32_t tmp = s12[8] | (s12[9] << 8) | (s12[10] << 16) | ((uint32_t)s12[11] << 24);
+    const uint32_t k1 = 0x03030303u, k2 = 0x0f0f0f0fu;
+    const uint32_t a2 = ((a0 >> 4) & k2) | (((tmp >> 4) & k1) << 4), a3 = ((a1 >> 4) & k2) | (((tmp >> 6) & k1) << 4);
+    a0 = (a0 & k2) | (((tmp >> 0) & k1) << 4);
+    a1 = (a1 & k2) | (((tmp >> 2) & k1) << 4);
+    const uint32_t a[4] = {a0, a1, a2, a3};
+    for (int i = 0; i < 16; ++i) sc[i] = (int8_t)((a[i >> 2] >> (8 * (i & 3))) & 0xFF);
+}
+
 // dequantize block b of a kcpp-layout tensor (nb blocks total) into o[0..block_elems)
 __device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t bpr, int64_t b, float *o) {
     uint8_t blk[256];
@@ -166,6 +193,17 @@ __device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t bpr,
                 o[64 * c + l] = __fsub_rn(__fmul_rn(d1, (float)lo), mm1);
                 o[64 * c + 32 + l] = __fsub_rn(__fmul_rn(d2, (float)hi), mm2);
             }
+        }
+    } break;
+    case KT_Q3_K: {                                   // ggml-quants.c:2328-2376 (exact: d (sc - 32) q3)
+        const float d = h2f(blk[108] | (blk[109] << 8));
+        int8_t sc[16];
+        q3k_scales(blk + 96, sc);
+        const uint8_t *hm = blk, *q = blk + 32;
+        for (int e = 0; e < 256; ++e) {
+            const int n = e >> 7, j = (e >> 5) & 3, l = e & 31;
+            const int v = ((q[32 * n + l] >> (2 * j)) & 3) - ((hm[l] >> (4 * n + j)) & 1 ? 0 : 4);
+            o[e] = __fmul_rn(__fmul_rn(d, (float)(sc[8 * n + 2 * j + (l >> 4)] - 32)), (float)v);
         }
     } break;
     case KT_Q6_K: {
@@ -222,6 +260,14 @@ __device__ __forceinline__ float deq_elem(int type, const uint8_t *src, int64_t 
         return __fsub_rn(__fmul_rn(d * sc, (float)q), mn * m);
     }
     case KT_Q4_K_RS: case KT_Q6_K_RS: return 0.0f;      // row gathers of decode layouts are not used
+    case KT_Q3_K: {
+        const float d = h2f(*(const uint16_t *)(src + nb * 108 + b * 2));
+        int8_t sc[16];
+        q3k_scales(src + nb * 96 + b * 12, sc);
+        const int n = e >> 7, j = (e >> 5) & 3, l = e & 31;
+        const int v = ((src[nb * 32 + b * 64 + 32 * n + l] >> (2 * j)) & 3) - ((src[b * 32 + l] >> (4 * n + j)) & 1 ? 0 : 4);
+        return __fmul_rn(__fmul_rn(d, (float)(sc[8 * n + 2 * j + (l >> 4)] - 32)), (float)v);
+    }
     case KT_Q6_K: {
         const uint8_t *q6 = src + b * 192;
         const int8_t *scp = (const int8_t *)(src + nb * 192 + b * 16);

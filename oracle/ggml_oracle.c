@@ -22,6 +22,7 @@ typedef struct { uint16_t d; int8_t qs[32]; } blk_q8_0;                   /* ggm
 typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qs[128]; } blk_q4_K;   /* :286 */
 typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qh[32]; uint8_t qs[128]; } blk_q5_K; /* :303 */
 typedef struct { uint8_t ql[128]; uint8_t qh[64]; int8_t scales[16]; uint16_t d; } blk_q6_K;       /* :321 */
+typedef struct { uint8_t hmask[32]; uint8_t qs[64]; uint8_t scales[12]; uint16_t d; } blk_q3_K;    /* :267 */
 typedef struct { float d; int8_t qs[256]; int16_t bsums[16]; } blk_q8_K;  /* :330 */
 
 _Static_assert(sizeof(blk_q4_0) == 18, "q4_0");
@@ -29,6 +30,7 @@ _Static_assert(sizeof(blk_q8_0) == 34, "q8_0");
 _Static_assert(sizeof(blk_q4_K) == 144, "q4_K");
 _Static_assert(sizeof(blk_q5_K) == 176, "q5_K");
 _Static_assert(sizeof(blk_q6_K) == 210, "q6_K");
+_Static_assert(sizeof(blk_q3_K) == 110, "q3_K");
 _Static_assert(sizeof(blk_q8_K) == 292, "q8_K");
 
 float orc_fp16_to_fp32(uint16_t h) { return _cvtsh_ss(h); }
@@ -47,6 +49,19 @@ static inline void scale_min_k4(int j, const uint8_t *q, uint8_t *d, uint8_t *m)
 
 int64_t orc_row_bytes(int type, int64_t k) {
     return k / ks_block_elems(type) * ks_block_bytes(type);
+}
+
+/* the 16 6-bit Q3_K scales (unsigned, biased by 32) from the 12 packed bytes (dequantize_row_q3_K's aux shuffle,
+ * ggml-quants.c:2346-2351) */
+static void q3k_scales(const uint8_t *s12, int8_t *sc) {
+    uint32_t aux[4];
+    memcpy(aux, s12, 12);
+    const uint32_t kmask1 = 0x03030303u, kmask2 = 0x0f0f0f0fu, tmp = aux[2];
+    aux[2] = ((aux[0] >> 4) & kmask2) | (((tmp >> 4) & kmask1) << 4);
+    aux[3] = ((aux[1] >> 4) & kmask2) | (((tmp >> 6) & kmask1) << 4);
+    aux[0] = (aux[0] & kmask2) | (((tmp >> 0) & kmask1) << 4);
+    aux[1] = (aux[1] & kmask2) | (((tmp >> 2) & kmask1) << 4);
+    memcpy(sc, aux, 16);
 }
 
 void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
@@ -104,6 +119,29 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
             }
         }
     } return;
+    case KT_Q3_K: {                                   /* ggml-quants.c:2328-2376 */
+        const blk_q3_K *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const float d_all = H2F(x[i].d);
+            int8_t sc[16];
+            q3k_scales(x[i].scales, sc);
+            const uint8_t *q = x[i].qs, *hm = x[i].hmask;
+            uint8_t m = 1;
+            int is = 0;
+            for (int n = 0; n < QK_K; n += 128) {
+                int shift = 0;
+                for (int j = 0; j < 4; ++j) {
+                    float dl = d_all * (sc[is++] - 32);
+                    for (int l = 0; l < 16; ++l) *y++ = dl * ((int8_t)((q[l] >> shift) & 3) - ((hm[l] & m) ? 0 : 4));
+                    dl = d_all * (sc[is++] - 32);
+                    for (int l = 0; l < 16; ++l) *y++ = dl * ((int8_t)((q[l + 16] >> shift) & 3) - ((hm[l + 16] & m) ? 0 : 4));
+                    shift += 2;
+                    m <<= 1;
+                }
+                q += 32;
+            }
+        }
+    } return;
     case KT_Q6_K: {                                   /* ggml-quants.c:2978-3006 */
         const blk_q6_K *x = vx;
         for (int64_t i = 0; i < k / QK_K; ++i) {
@@ -134,7 +172,7 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
 int orc_vec_dot_type(int wtype) {
     switch (wtype) {
         case KT_Q4_0: case KT_Q8_0: return KT_Q8_0;
-        case KT_Q4_K: case KT_Q5_K: case KT_Q6_K: return KT_Q8_K;
+        case KT_Q3_K: case KT_Q4_K: case KT_Q5_K: case KT_Q6_K: return KT_Q8_K;
         case KT_F16: return KT_F16;
         default: return KT_F32;
     }
@@ -299,6 +337,38 @@ static float dot_q6_K(int n, const blk_q6_K *x, const blk_q8_K *y) {       /* :8
     return sumf;
 }
 
+static float dot_q3_K(int n, const blk_q3_K *x, const blk_q8_K *y) {       /* :6933, scalar branch */
+    float sums[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < n / QK_K; ++i) {
+        int8_t a[QK_K], *pa = a;
+        const uint8_t *q3 = x[i].qs, *hm = x[i].hmask;
+        uint8_t m = 1;
+        for (int j = 0; j < QK_K; j += 128) {
+            for (int sh = 0; sh < 8; sh += 2) {
+                for (int l = 0; l < 32; ++l) pa[l] = (int8_t)(((q3[l] >> sh) & 3) - ((hm[l] & m) ? 0 : 4));
+                pa += 32;
+                m <<= 1;
+            }
+            q3 += 32;
+        }
+        int8_t sc[16];
+        q3k_scales(x[i].scales, sc);
+        int32_t aux32[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const int8_t *q8 = y[i].qs;
+        pa = a;
+        for (int j = 0; j < QK_K / 16; ++j)
+            for (int h = 0; h < 2; ++h) {
+                for (int l = 0; l < 8; ++l) aux32[l] += (sc[j] - 32) * (int16_t)(q8[l] * pa[l]);
+                q8 += 8; pa += 8;
+            }
+        const float d = H2F(x[i].d) * y[i].d;
+        for (int l = 0; l < 8; ++l) sums[l] += d * aux32[l];
+    }
+    float sumf = 0;
+    for (int l = 0; l < 8; ++l) sumf += sums[l];
+    return sumf;
+}
+
 static float dot_q4_0(int n, const blk_q4_0 *x, const blk_q8_0 *y) {       /* :3922, scalar tail */
     float sumf = 0;
     for (int ib = 0; ib < n / 32; ++ib) {
@@ -333,6 +403,7 @@ float orc_vec_dot(int wtype, int n, const void *w, const void *a) {
         case KT_Q4_K: return dot_q4_K(n, w, a);
         case KT_Q5_K: return dot_q5_K(n, w, a);
         case KT_Q6_K: return dot_q6_K(n, w, a);
+        case KT_Q3_K: return dot_q3_K(n, w, a);
         case KT_Q4_0: return dot_q4_0(n, w, a);
         case KT_Q8_0: return dot_q8_0(n, w, a);
         case KT_F16: return dot_f16(n, w, a);

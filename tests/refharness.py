@@ -14,8 +14,8 @@ REF_BIN = os.path.join(ROOT, "oracle", "_ref", "ref_llama")
 REF_BIN_SCALAR = os.path.join(ROOT, "oracle", "_ref", "scalar", "ref_llama")   # no-SIMD build (make ref_scalar)
 
 # ggml_type ids (ggml/include/ggml.h:364-399)
-F32, F16, Q4_0, Q8_0, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 8, 12, 13, 14, 15
-BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q8_0: (32, 34), Q4_K: (256, 144),
+F32, F16, Q4_0, Q8_0, Q3_K, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 8, 11, 12, 13, 14, 15
+BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q8_0: (32, 34), Q3_K: (256, 110), Q4_K: (256, 144),
          Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292)}
 
 
@@ -281,6 +281,19 @@ def mixtral_q5_k_m_types(n_layer):
         more = il < n_layer // 8 or il >= 7 * n_layer // 8 or (il - n_layer // 8) % 3 == 2
         ty += [F32, Q5_K, Q8_0, Q8_0, Q5_K, F32, Q5_K, Q5_K, Q6_K if more else Q5_K, F32]
     return ty
+
+
+def q3_k_m_types(n_layer):
+    """Q3_K_M per-tensor policy (llama_tensor_get_type, src/llama.cpp:17979-18208): Q3_K by default (token_embd
+    too), output Q6_K, attn_v Q5_K on the first two layers else Q4_K, attn_output Q4_K, ffn_down Q5_K below
+    n_layer / 16, Q4_K on the 'more bits' layers, else Q3_K"""
+    types = [Q3_K, F32, Q6_K]
+    for i in range(n_layer):
+        more = i < n_layer // 8 or i >= 7 * n_layer // 8 or (i - n_layer // 8) % 3 == 2
+        v = Q5_K if i < 2 else Q4_K
+        down = Q5_K if i < n_layer // 16 else (Q4_K if more else Q3_K)
+        types += [F32, Q3_K, Q3_K, v, Q4_K, F32, Q3_K, Q3_K, down]
+    return types
 
 
 def q4_k_m_types(n_layer, tok=Q4_K, out=Q6_K):
