@@ -4,7 +4,7 @@
  * There are no real Llama checkpoints on the build/GPU machines, so benchmarks and
  * parity tests use random-init weights *in the exact on-disk block formats* of
  * ggml (ggml/src/ggml-common.h:144-335 of the reference: block_q4_0, block_q8_0,
- * block_q3_K, block_q4_K, block_q5_K, block_q6_K).  Every byte is a pure function of
+ * block_q2_K, block_q3_K, block_q4_K, block_q5_K, block_q6_K).  Every byte is a pure function of
  * (seed, tensor id, block index), so the GPU runtime, the CPU oracle and the
  * reference-ggml harness all see bit-identical tensors without shipping files.
  *
@@ -89,6 +89,7 @@ KS_FN int ks_block_bytes(int type) {
         case KT_F16: return 2;
         case KT_Q4_0: return 18;
         case KT_Q8_0: return 34;
+        case KT_Q2_K: return 84;
         case KT_Q3_K: return 110;
         case KT_Q4_K: case KT_Q4_K_RS: return 144;
         case KT_Q5_K: return 176;
@@ -137,6 +138,10 @@ KS_FN void ks_fill_block(int type, uint64_t seed, uint64_t tid, uint64_t b, uint
             uint8_t *s = dst + 4;
             for (int j = 0; j < 4; ++j) { s[j] |= 0x10; s[j + 4] |= 0x10; }
             for (int j = 0; j < 4; ++j) { s[j + 8] = (uint8_t)(s[j + 8] | 0x11); }
+        } break;
+        case KT_Q2_K: {     /* w = d (sc & 15) q - dmin (sc >> 4), q in 0..3: std(sc q) ~12.7 */
+            h0 = ks_f32_to_f16(1.6e-3f * (0.75f + 0.5f * u0)); h1 = ks_f32_to_f16(2.4e-3f * (0.75f + 0.5f * u1));
+            memcpy(dst + 80, &h0, 2); memcpy(dst + 82, &h1, 2);
         } break;
         case KT_Q3_K: {     /* w = d (sc - 32) q3, sc 6-bit, q3 in -4..3: std(sc - 32) ~18.5, std(q3) ~2.3 */
             h0 = ks_f32_to_f16(4.6e-4f * (0.75f + 0.5f * u0));

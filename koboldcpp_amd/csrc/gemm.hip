@@ -128,6 +128,7 @@ template <> struct GemmTraits<KT_Q4_K> { static constexpr int NB = 1; static con
 template <> struct GemmTraits<KT_Q5_K> { static constexpr int NB = 1; static constexpr bool MINS = true; static constexpr bool SB = true; };
 template <> struct GemmTraits<KT_Q6_K> { static constexpr int NB = 2; static constexpr bool MINS = false; static constexpr bool SB = true; };
 template <> struct GemmTraits<KT_Q3_K> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = true; };
+template <> struct GemmTraits<KT_Q2_K> { static constexpr int NB = 1; static constexpr bool MINS = true; static constexpr bool SB = true; };
 template <> struct GemmTraits<KT_Q4_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
 template <> struct GemmTraits<KT_Q8_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
 
@@ -203,6 +204,30 @@ __device__ __forceinline__ void stage_weights(SM &S, const uint8_t *__restrict__
             }
         }
         if (c == 0) S.wd[nl][0] = h2f(*(const uint16_t *)(W + nbt * 208 + b * 2));
+    } else if constexpr (TYPE == KT_Q2_K) {
+        // chunk c = quarter c (half n = c >> 1, shifts 2 (c & 1), +1); weights (sc & 15) q exact (<= 45); mins
+        // (sc >> 4) per 16-group straight into the bsum fragment; SoA planes: scales [nb][16], qs [nb][64], d/dmin
+        const int64_t b = n * bpr + sb;
+        const int hn = c >> 1, j0 = 2 * (c & 1);
+        const uint8_t *qp = W + nbt * 16 + b * 64 + 32 * hn;
+        const uint4 q0 = *(const uint4 *)qp, q1 = *(const uint4 *)(qp + 16);
+        const uint32_t sw = *(const uint32_t *)(W + b * 16 + 4 * c);
+        const uint32_t qd[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int j = j0 + (i >> 2), w0 = 2 * (i & 3);
+            const int sc = (int)((sw >> (8 * (2 * (i >> 2) + ((i & 3) >> 1)))) & 0xF);
+            S.bf[0][bslot(nl, 64 * c + 8 * i)] = frag8((qd[w0] >> (2 * j)) & 0x03030303u, (qd[w0 + 1] >> (2 * j)) & 0x03030303u,
+                                                       (float)sc, 0.0f);
+        }
+        _Float16 *bm = (_Float16 *)&S.bm[(nl >> 5) * 64 + (c >> 1) * 32 + (nl & 31)] + 4 * (c & 1);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) bm[t] = (_Float16)(float)((sw >> (8 * t + 4)) & 0xF);
+        if (c == 0) {
+            const uint32_t dd = *(const uint32_t *)(W + nbt * 80 + b * 4);
+            S.wd[nl][0] = h2f((uint16_t)(dd & 0xFFFF));
+            S.wd[nl][1] = h2f((uint16_t)(dd >> 16));
+        }
     } else if constexpr (TYPE == KT_Q3_K) {
         // chunk c = quarter c of the super-block (half n = c >> 1, shifts j0 = 2 (c & 1), j0 + 1); weights
         // (sc - 32) (v - 4) with v = 2 low bits | hmask bit << 2 -- exact f16 integers (|.| <= 128); SoA planes
@@ -1553,6 +1578,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     const dim3 grid((unsigned)((N + GB_N - 1) / GB_N), (unsigned)(Mp / GB_M));
     auto launch = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
         switch (type) {
+        case KT_Q2_K: hipLaunchKernelGGL(k_gemm<KT_Q2_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         case KT_Q3_K: hipLaunchKernelGGL(k_gemm<KT_Q3_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         case KT_Q4_0: hipLaunchKernelGGL(k_gemm<KT_Q4_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         case KT_Q8_0: hipLaunchKernelGGL(k_gemm<KT_Q8_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;

@@ -128,6 +128,7 @@ int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         KCPP_T(KT_Q5_K)
         KCPP_T(KT_Q6_K)
         KCPP_T(KT_Q3_K)
+        KCPP_T(KT_Q2_K)
         KCPP_T(KT_Q4_0)
         KCPP_T(KT_Q8_0)
     default: return -3;

@@ -76,6 +76,23 @@ template <> struct Unit<KT_Q3_K> {
         d = *(const uint16_t *)(base + nb * 108 + b * 2);
     }
 };
+// ---- Q2_K (SoA planes, quant.hip kl_store_block): unit u = quarter qq = u & 3 of super-block u >> 2 (half
+// n = qq >> 1, shifts j0 = 2 (qq & 1), j0 + 1, as Q3_K): qs bytes 32n..32n+31, scale dword qq (scales 4qq..4qq+3:
+// low nibble scale, high nibble min), (d, dmin)
+template <> struct Unit<KT_Q2_K> {
+    static constexpr int ELEMS = 64;
+    uint4 q0, q1;
+    uint32_t sc, dd;
+    __device__ __forceinline__ void load(const uint8_t *base, int64_t nb, int64_t b0, int u) {
+        const int64_t b = b0 + (u >> 2);
+        const int qq = u & 3;
+        const uint8_t *q = base + nb * 16 + b * 64 + 32 * (qq >> 1);
+        q0 = ld_nt((const void *)q);
+        q1 = ld_nt((const void *)(q + 16));
+        sc = *(const uint32_t *)(base + b * 16 + 4 * qq);
+        dd = *(const uint32_t *)(base + nb * 80 + b * 4);
+    }
+};
 // ---- Q4_0 (SoA): unit = one 32-elem block: 16 B nibbles + fp16 d
 template <> struct Unit<KT_Q4_0> {
     static constexpr int ELEMS = 32;
@@ -268,6 +285,28 @@ __device__ __forceinline__ float unit_dot(const Unit<KT_Q3_K> &w, int u, const A
     return __fmul_rn(__fmul_rn(h2f(w.d), x.d), (float)sumi);
 }
 
+// Q2_K: d x.d sum_g (sc_g & 15) dot_g - dmin x.d sum_g (sc_g >> 4) bsum_g  (ggml_vec_dot_q2_K_q8_K)
+__device__ __forceinline__ float unit_dot(const Unit<KT_Q2_K> &w, int u, const ActK &x) {
+    const int j0 = 2 * (u & 1);
+    int sumi = 0, summ = 0;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int j = j0 + (g >> 1);
+        int dot = 0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int wi = 4 * (g & 1) + t;
+            const uint32_t qd = wi < 4 ? u4(w.q0, wi) : u4(w.q1, wi - 4);
+            dot = sdot4((int)((qd >> (2 * j)) & 0x03030303u), ai(x, 4 * g + t), dot);
+        }
+        const int s = (w.sc >> (8 * g)) & 0xFF;
+        sumi += (s & 0xF) * dot;
+        summ += (s >> 4) * x.bs[g];
+    }
+    const float dall = __fmul_rn(x.d, h2f((uint16_t)(w.dd & 0xFFFF))), dmin = __fmul_rn(x.d, h2f((uint16_t)(w.dd >> 16)));
+    return __fsub_rn(__fmul_rn(dall, (float)sumi), __fmul_rn(dmin, (float)summ));
+}
+
 __device__ __forceinline__ float unit_dot(const Unit<KT_Q4_0> &w, int, const Act0 &x) {
     int s = 0;
 #pragma unroll
@@ -295,7 +334,7 @@ template <int TYPE>
 __device__ __forceinline__ void load_unit(Unit<TYPE> &w, const uint8_t *W, int64_t nb, int64_t row, int64_t units_per_row, int u) {
     if constexpr (TYPE == KT_Q4_K) w.load(W + row * (units_per_row / 4) * 144, nb, u);
     else if constexpr (TYPE == KT_Q5_K) w.load(W + row * (units_per_row / 4) * 176, nb, u);
-    else if constexpr (TYPE == KT_Q6_K || TYPE == KT_Q3_K) w.load(W, nb, row * (units_per_row / 4), u);
+    else if constexpr (TYPE == KT_Q6_K || TYPE == KT_Q3_K || TYPE == KT_Q2_K) w.load(W, nb, row * (units_per_row / 4), u);
     else w.load(W, nb, row * units_per_row, u);
 }
 

@@ -12,6 +12,12 @@
 __device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uint8_t *dst, int64_t b, int64_t nb,
                                                int64_t bpr) {
     switch (type) {
+    case KT_Q2_K: {   // SoA planes: scales [nb][16] ++ qs [nb][64] ++ (d, dmin) [nb][4]
+        uint8_t *sc = dst + b * 16, *q = dst + nb * 16 + b * 64, *dd = dst + nb * 80 + b * 4;
+        for (int i = 0; i < 16; ++i) sc[i] = src[i];
+        for (int i = 0; i < 64; ++i) q[i] = src[16 + i];
+        for (int i = 0; i < 4; ++i) dd[i] = src[80 + i];
+    } break;
     case KT_Q3_K: {   // SoA planes: hmask [nb][32] ++ qs [nb][64] ++ scales [nb][12] ++ d [nb][2] (16-B aligned loads)
         uint8_t *hm = dst + b * 32, *q = dst + nb * 32 + b * 64, *sc = dst + nb * 96 + b * 12, *d = dst + nb * 108 + b * 2;
         for (int i = 0; i < 32; ++i) hm[i] = src[i];
@@ -65,6 +71,12 @@ __device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uin
 __device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint8_t *blk, int64_t b, int64_t nb,
                                               int64_t bpr) {
     switch (type) {
+    case KT_Q2_K: {
+        const uint8_t *sc = src + b * 16, *q = src + nb * 16 + b * 64, *dd = src + nb * 80 + b * 4;
+        for (int i = 0; i < 16; ++i) blk[i] = sc[i];
+        for (int i = 0; i < 64; ++i) blk[16 + i] = q[i];
+        for (int i = 0; i < 4; ++i) blk[80 + i] = dd[i];
+    } break;
     case KT_Q3_K: {
         const uint8_t *hm = src + b * 32, *q = src + nb * 32 + b * 64, *sc = src + nb * 96 + b * 12, *d = src + nb * 108 + b * 2;
         for (int i = 0; i < 32; ++i) blk[i] = hm[i];
@@ -195,6 +207,14 @@ __device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t bpr,
             }
         }
     } break;
+    case KT_Q2_K: {                                   // ggml-quants.c:2251-2282: (d (sc & 15)) q - dmin (sc >> 4)
+        const float d = h2f(blk[80] | (blk[81] << 8)), mn = h2f(blk[82] | (blk[83] << 8));
+        for (int e = 0; e < 256; ++e) {
+            const int n = e >> 7, j = (e >> 5) & 3, l = e & 31;
+            const int sc = blk[e >> 4], q = (blk[16 + 32 * n + l] >> (2 * j)) & 3;
+            o[e] = __fsub_rn(__fmul_rn(__fmul_rn(d, (float)(sc & 0xF)), (float)q), __fmul_rn(mn, (float)(sc >> 4)));
+        }
+    } break;
     case KT_Q3_K: {                                   // ggml-quants.c:2328-2376 (exact: d (sc - 32) q3)
         const float d = h2f(blk[108] | (blk[109] << 8));
         int8_t sc[16];
@@ -260,6 +280,12 @@ __device__ __forceinline__ float deq_elem(int type, const uint8_t *src, int64_t 
         return __fsub_rn(__fmul_rn(d * sc, (float)q), mn * m);
     }
     case KT_Q4_K_RS: case KT_Q6_K_RS: return 0.0f;      // row gathers of decode layouts are not used
+    case KT_Q2_K: {
+        const float d = h2f(*(const uint16_t *)(src + nb * 80 + b * 4)), mn = h2f(*(const uint16_t *)(src + nb * 80 + b * 4 + 2));
+        const int n = e >> 7, j = (e >> 5) & 3, l = e & 31;
+        const int sc = src[b * 16 + (e >> 4)], q = (src[nb * 16 + b * 64 + 32 * n + l] >> (2 * j)) & 3;
+        return __fsub_rn(__fmul_rn(__fmul_rn(d, (float)(sc & 0xF)), (float)q), __fmul_rn(mn, (float)(sc >> 4)));
+    }
     case KT_Q3_K: {
         const float d = h2f(*(const uint16_t *)(src + nb * 108 + b * 2));
         int8_t sc[16];

@@ -409,7 +409,7 @@ extern "C" int kcpp_model_set_tensor(kcpp_model *m, int idx, const void *src, in
     if (!t) return 0;                      // not on this stage
     if ((size_t)nbytes != t->bytes) { g_err = "set_tensor: size mismatch"; return -2; }
     RT_CHECK(hipSetDevice(m->device));
-    if (t->type == KT_Q6_K || t->type == KT_Q3_K || t->type == KT_Q4_0 || t->type == KT_Q8_0 || t->type == KT_Q4_K_RS ||
+    if (t->type == KT_Q6_K || t->type == KT_Q3_K || t->type == KT_Q2_K || t->type == KT_Q4_0 || t->type == KT_Q8_0 || t->type == KT_Q4_K_RS ||
         t->type == KT_Q6_K_RS) {
         void *stage = nullptr;
         RT_CHECK(hipMalloc(&stage, t->bytes));

@@ -23,6 +23,7 @@ typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qs[128]; } blk_q4
 typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qh[32]; uint8_t qs[128]; } blk_q5_K; /* :303 */
 typedef struct { uint8_t ql[128]; uint8_t qh[64]; int8_t scales[16]; uint16_t d; } blk_q6_K;       /* :321 */
 typedef struct { uint8_t hmask[32]; uint8_t qs[64]; uint8_t scales[12]; uint16_t d; } blk_q3_K;    /* :267 */
+typedef struct { uint8_t scales[16]; uint8_t qs[64]; uint16_t d, dmin; } blk_q2_K;                 /* :250 */
 typedef struct { float d; int8_t qs[256]; int16_t bsums[16]; } blk_q8_K;  /* :330 */
 
 _Static_assert(sizeof(blk_q4_0) == 18, "q4_0");
@@ -31,6 +32,7 @@ _Static_assert(sizeof(blk_q4_K) == 144, "q4_K");
 _Static_assert(sizeof(blk_q5_K) == 176, "q5_K");
 _Static_assert(sizeof(blk_q6_K) == 210, "q6_K");
 _Static_assert(sizeof(blk_q3_K) == 110, "q3_K");
+_Static_assert(sizeof(blk_q2_K) == 84, "q2_K");
 _Static_assert(sizeof(blk_q8_K) == 292, "q8_K");
 
 float orc_fp16_to_fp32(uint16_t h) { return _cvtsh_ss(h); }
@@ -119,6 +121,27 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
             }
         }
     } return;
+    case KT_Q2_K: {                                   /* ggml-quants.c:2251-2282 */
+        const blk_q2_K *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const float d = H2F(x[i].d), min = H2F(x[i].dmin);
+            const uint8_t *q = x[i].qs;
+            int is = 0;
+            for (int n = 0; n < QK_K; n += 128) {
+                int shift = 0;
+                for (int j = 0; j < 4; ++j) {
+                    uint8_t sc = x[i].scales[is++];
+                    float dl = d * (sc & 0xF), ml = min * (sc >> 4);
+                    for (int l = 0; l < 16; ++l) *y++ = dl * ((int8_t)((q[l] >> shift) & 3)) - ml;
+                    sc = x[i].scales[is++];
+                    dl = d * (sc & 0xF); ml = min * (sc >> 4);
+                    for (int l = 0; l < 16; ++l) *y++ = dl * ((int8_t)((q[l + 16] >> shift) & 3)) - ml;
+                    shift += 2;
+                }
+                q += 32;
+            }
+        }
+    } return;
     case KT_Q3_K: {                                   /* ggml-quants.c:2328-2376 */
         const blk_q3_K *x = vx;
         for (int64_t i = 0; i < k / QK_K; ++i) {
@@ -172,7 +195,7 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
 int orc_vec_dot_type(int wtype) {
     switch (wtype) {
         case KT_Q4_0: case KT_Q8_0: return KT_Q8_0;
-        case KT_Q3_K: case KT_Q4_K: case KT_Q5_K: case KT_Q6_K: return KT_Q8_K;
+        case KT_Q2_K: case KT_Q3_K: case KT_Q4_K: case KT_Q5_K: case KT_Q6_K: return KT_Q8_K;
         case KT_F16: return KT_F16;
         default: return KT_F32;
     }
@@ -337,6 +360,33 @@ static float dot_q6_K(int n, const blk_q6_K *x, const blk_q8_K *y) {       /* :8
     return sumf;
 }
 
+static float dot_q2_K(int n, const blk_q2_K *x, const blk_q8_K *y) {       /* :6448, scalar branch */
+    float sumf = 0;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const uint8_t *q2 = x[i].qs, *sc = x[i].scales;
+        const int8_t *q8 = y[i].qs;
+        int summs = 0;
+        for (int j = 0; j < 16; ++j) summs += y[i].bsums[j] * (sc[j] >> 4);
+        const float dall = y[i].d * H2F(x[i].d), dmin = y[i].d * H2F(x[i].dmin);
+        int isum = 0, is = 0;
+        for (int k = 0; k < QK_K / 128; ++k) {
+            for (int shift = 0; shift < 8; shift += 2) {
+                int d = sc[is++] & 0xF, isuml = 0;
+                for (int l = 0; l < 16; ++l) isuml += q8[l] * ((q2[l] >> shift) & 3);
+                isum += d * isuml;
+                d = sc[is++] & 0xF;
+                isuml = 0;
+                for (int l = 16; l < 32; ++l) isuml += q8[l] * ((q2[l] >> shift) & 3);
+                isum += d * isuml;
+                q8 += 32;
+            }
+            q2 += 32;
+        }
+        sumf += dall * isum - dmin * summs;
+    }
+    return sumf;
+}
+
 static float dot_q3_K(int n, const blk_q3_K *x, const blk_q8_K *y) {       /* :6933, scalar branch */
     float sums[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = 0; i < n / QK_K; ++i) {
@@ -404,6 +454,7 @@ float orc_vec_dot(int wtype, int n, const void *w, const void *a) {
         case KT_Q5_K: return dot_q5_K(n, w, a);
         case KT_Q6_K: return dot_q6_K(n, w, a);
         case KT_Q3_K: return dot_q3_K(n, w, a);
+        case KT_Q2_K: return dot_q2_K(n, w, a);
         case KT_Q4_0: return dot_q4_0(n, w, a);
         case KT_Q8_0: return dot_q8_0(n, w, a);
         case KT_F16: return dot_f16(n, w, a);
