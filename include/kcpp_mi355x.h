@@ -293,6 +293,15 @@ int kcpp_model_moe_ids(kcpp_model *m, int32_t *out, int n);
  * through the unfused per-op path and refuse kcpp_model_kv_shift (koboldcpp turns context shift off with
  * --quantkv, koboldcpp.py).  Returns -1 for other combinations. */
 int kcpp_model_set_kv_types(kcpp_model *m, int type_k, int type_v);
+/* row split (koboldcpp --rowsplit -> LLAMA_SPLIT_MODE_ROW, gpttype_adapter.cpp:1892; replaces the split buffer type
+ * ggml_backend_cuda_split_buffer_type, ggml-cuda.cu:659-955, and ggml_cuda_op_mul_mat's per-device row ranges,
+ * :1403-1700): the rows of every layer matrix and of the output matrix are spread over devices[0..n) by
+ * tensor_split (proportions; all zero = equal), bounds rounded to 128 rows; everything else stays on the stage's
+ * device.  n lanes may name the same GPU (each extra lane gets its own stream and buffers).  Call after create,
+ * before the weights are set.  Turns graph replay and the fused single-token path off; refuses MoE (-3). */
+int kcpp_model_set_row_split(kcpp_model *m, int n, const int *devices, const float *tensor_split);
+/* the row range [lo, hi) of an nrows matrix on device id of n (host only; get_row_split, ggml-cuda.cu:638-651) */
+int kcpp_row_split_range(int64_t nrows, int n, const float *tensor_split, int id, int64_t *lo, int64_t *hi);
 int64_t kcpp_model_weight_bytes(kcpp_model *m);
 const char *kcpp_last_error(void);
 

@@ -519,6 +519,24 @@ bool load_model(const load_model_inputs inputs) {
         }
         return true;
     };
+    if (inputs.use_rowsplit && std::min(ndev, KCPP_TENSOR_SPLIT_MAX) > 1) {
+        // LLAMA_SPLIT_MODE_ROW (gpttype_adapter.cpp:1892): one stage on the main device (cublas_info,
+        // gpttype_adapter.cpp:1708) owning every layer; the matrices' rows spread over the devices by tensor_split
+        const int nd = std::min(ndev, KCPP_TENSOR_SPLIT_MAX);
+        const int main_dev = std::min(inputs.cublas_info <= 0 ? 0 : inputs.cublas_info, nd - 1) % nreal;
+        std::vector<int> devs(nd);
+        for (int i = 0; i < nd; ++i) devs[i] = i % nreal;
+        kcpp_model *m = kcpp_model_create(&hp, e->types.data(), main_dev, 0, hp.n_layer, 1, 1, e->ub);
+        if (!m) { fprintf(stderr, "[kcpp] load_model: %s\n", kcpp_last_error()); return false; }
+        e->stages.push_back(m);
+        e->hidden.push_back(kcpp_model_hidden(m));
+        e->devs.push_back(main_dev);
+        if (kcpp_model_set_row_split(m, nd, devs.data(), inputs.tensor_split)) {
+            fprintf(stderr, "[kcpp] load_model: row split: %s\n", kcpp_last_error());
+            return false;
+        }
+        il = hp.n_layer;
+    }
     while (il < hp.n_layer) {
         const int d = ldev[il];
         int il1 = il;

@@ -143,11 +143,13 @@ __global__ void k_repack(int type, const uint8_t *__restrict__ src, uint8_t *__r
     }
 }
 
-__global__ void k_synth(int type, uint64_t seed, uint64_t tid, uint8_t *__restrict__ dst, int64_t nb, int64_t bpr) {
+// block b of the tensor gets the content of block b + boff of the synthetic stream (boff != 0: a row slice)
+__global__ void k_synth(int type, uint64_t seed, uint64_t tid, uint8_t *__restrict__ dst, int64_t nb, int64_t bpr,
+                        int64_t boff) {
     int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     uint8_t blk[256];
-    ks_fill_block(type, seed, tid, (uint64_t)b, blk);
+    ks_fill_block(type, seed, tid, (uint64_t)(b + boff), blk);
     kl_store_block(type, blk, dst, b, nb, bpr);
 }
 
@@ -402,12 +404,18 @@ int kcpp_weight_repack(int type, const void *src_ggml, void *dst_kcpp, int64_t K
     return 0;
 }
 
-int kcpp_weight_synth(int type, uint64_t seed, uint64_t tid, void *dst, int64_t K, int64_t N, void *stream) {
+int kcpp_weight_synth_rows(int type, uint64_t seed, uint64_t tid, void *dst, int64_t K, int64_t N, int64_t row0,
+                           void *stream) {
     const int64_t nb = kl_nblocks(type, K, N);
+    if (nb <= 0) return 0;
     hipLaunchKernelGGL(k_synth, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, (hipStream_t)stream, type, seed, tid,
-                       (uint8_t *)dst, nb, K / ks_block_elems(type));
+                       (uint8_t *)dst, nb, K / ks_block_elems(type), row0 * (K / ks_block_elems(type)));
     KCPP_CHECK(hipGetLastError());
     return 0;
+}
+
+int kcpp_weight_synth(int type, uint64_t seed, uint64_t tid, void *dst, int64_t K, int64_t N, void *stream) {
+    return kcpp_weight_synth_rows(type, seed, tid, dst, K, N, 0, stream);
 }
 
 int kcpp_dequantize(int type, const void *w, float *y, int64_t K, int64_t N, void *stream) {

@@ -54,6 +54,10 @@ extern "C" const char *kcpp_last_error(void) { return g_err.c_str(); }
         }                                                                                              \
     } while (0)
 
+// one device's rows of a row-split matrix (LLAMA_SPLIT_MODE_ROW, ggml_backend_cuda_split_buffer,
+// ggml-cuda.cu:659-955): rows [lo, hi) of the [K][N] tensor, stored as a [K][hi - lo] tensor in the device layout
+struct RowSlice { int lane = 0; int64_t lo = 0, hi = 0; void *d = nullptr; };
+
 struct KTensor {
     int type = KT_F32;
     int64_t K = 0, N = 0;
@@ -62,6 +66,19 @@ struct KTensor {
     bool owned = true;               // false: a slice of a fused group allocation
     int slices = 1;                  // MoE _exps tensors: n_expert consecutive [K][N] slices
     size_t slice_bytes = 0;
+    std::vector<RowSlice> rs;        // non-empty: row split, the rows live in these slices (d is null)
+};
+
+// a row-split execution lane: one device of the split.  The first lane on the stage's own device runs inline on
+// its stream and buffers; every other lane (other GPUs, or further lanes on the same GPU) has its own stream,
+// activation copy, output rows and GEMM workspace, fenced against the stage stream by events.
+struct Lane {
+    int dev = 0;
+    bool inline_main = false;
+    hipStream_t s = nullptr;
+    hipEvent_t done = nullptr;
+    void *act = nullptr, *ws = nullptr;
+    float *y = nullptr;
 };
 
 struct KLayer {
@@ -113,6 +130,8 @@ struct kcpp_model {
     hipStream_t side = nullptr;             // second branch of the decode step (independent q|k|v launches)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int64_t weight_bytes = 0;
+    std::vector<Lane> lanes;                // row split (kcpp_model_set_row_split); empty: every matrix whole here
+    hipEvent_t ev_in = nullptr;             // row split: the stage stream has produced a mat-mul's inputs
 };
 
 static int ensure_graph(kcpp_model *m);
@@ -367,9 +386,13 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     hipSetDevice(m->device);
     if (m->g_exec) hipGraphExecDestroy(m->g_exec);
     auto F = [](void *p) { if (p) hipFree(p); };
-    F(m->tok_embd.d); F(m->output_norm.d); F(m->output.d);
+    auto FS = [&](KTensor &t) {
+        for (auto &r : t.rs) { hipSetDevice(m->lanes[r.lane].dev); F(r.d); }
+        hipSetDevice(m->device);
+    };
+    F(m->tok_embd.d); F(m->output_norm.d); F(m->output.d); FS(m->output);
     for (auto &L : m->layers) {
-        for (auto &t : L.t) if (t.owned) F(t.d);
+        for (auto &t : L.t) { if (t.owned) F(t.d); FS(t); }
         F(L.qkv_base); F(L.glu_base); F(L.kc); F(L.vc);
     }
     F(m->hglu); F(m->moe_ids); F(m->moe_w); F(m->moe_rows); F(m->moe_rw); F(m->moe_slots);
@@ -384,6 +407,15 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     if (m->side) hipStreamDestroy(m->side);
     if (m->ev_fork) hipEventDestroy(m->ev_fork);
     if (m->ev_join) hipEventDestroy(m->ev_join);
+    if (m->ev_in) hipEventDestroy(m->ev_in);
+    for (auto &ln : m->lanes) {
+        if (ln.inline_main) continue;
+        hipSetDevice(ln.dev);
+        F(ln.act); F(ln.ws); F(ln.y);
+        if (ln.s) hipStreamDestroy(ln.s);
+        if (ln.done) hipEventDestroy(ln.done);
+    }
+    hipSetDevice(m->device);
     delete m;
 }
 
@@ -392,7 +424,16 @@ extern "C" int kcpp_model_synth_weights(kcpp_model *m, uint64_t seed) {
     for (int idx = 0; idx < n_tensors(m->hp); ++idx) {
         KTensor *t = tensor_at(m, idx);
         if (!t) continue;
-        if (t->slices == 1) {
+        if (!t->rs.empty()) {                  // row split: each slice holds its rows of the same tensor
+            for (const RowSlice &r : t->rs) {
+                const Lane &ln = m->lanes[r.lane];
+                RT_CHECK(hipSetDevice(ln.dev));
+                RC(kcpp_weight_synth_rows(t->type, seed, (uint64_t)idx, r.d, t->K, r.hi - r.lo, r.lo,
+                                          ln.inline_main ? m->stream : ln.s));
+                RT_CHECK(hipStreamSynchronize(ln.inline_main ? m->stream : ln.s));
+            }
+            RT_CHECK(hipSetDevice(m->device));
+        } else if (t->slices == 1) {
             RC(kcpp_weight_synth(t->type, seed, (uint64_t)idx, t->d, t->K, t->N, m->stream));
         } else {                               // expert e: tid = idx * 256 + e (tests/refharness.py)
             for (int e = 0; e < t->slices; ++e)
@@ -404,26 +445,44 @@ extern "C" int kcpp_model_synth_weights(kcpp_model *m, uint64_t seed) {
     return 0;
 }
 
+// host GGUF bytes of `slices` [K][N] tensors -> device layout at dst on device dev
+static int upload(int dev, hipStream_t s, int type, int64_t K, int64_t N, int slices, size_t slice_bytes,
+                  const void *src, void *dst) {
+    const size_t bytes = (size_t)tensor_bytes(type, K, N) * slices;
+    if (!slice_bytes) slice_bytes = bytes;
+    if (bytes == 0) return 0;
+    RT_CHECK(hipSetDevice(dev));
+    if (type == KT_Q6_K || type == KT_Q3_K || type == KT_Q2_K || type == KT_Q4_0 || type == KT_Q8_0 || type == KT_Q4_K_RS ||
+        type == KT_Q6_K_RS) {
+        void *stage = nullptr;
+        RT_CHECK(hipMalloc(&stage, bytes));
+        RT_CHECK(hipMemcpyAsync(stage, src, bytes, hipMemcpyHostToDevice, s));
+        for (int e = 0; e < slices; ++e)         // structure-of-arrays layout per expert slice
+            RC(kcpp_weight_repack(type, (uint8_t *)stage + e * slice_bytes, (uint8_t *)dst + e * slice_bytes, K, N, 0, s));
+        RT_CHECK(hipStreamSynchronize(s));
+        RT_CHECK(hipFree(stage));
+    } else {
+        RT_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+        RT_CHECK(hipStreamSynchronize(s));
+    }
+    return 0;
+}
+
 extern "C" int kcpp_model_set_tensor(kcpp_model *m, int idx, const void *src, int64_t nbytes) {
     KTensor *t = tensor_at(m, idx);
     if (!t) return 0;                      // not on this stage
     if ((size_t)nbytes != t->bytes) { g_err = "set_tensor: size mismatch"; return -2; }
-    RT_CHECK(hipSetDevice(m->device));
-    if (t->type == KT_Q6_K || t->type == KT_Q3_K || t->type == KT_Q2_K || t->type == KT_Q4_0 || t->type == KT_Q8_0 || t->type == KT_Q4_K_RS ||
-        t->type == KT_Q6_K_RS) {
-        void *stage = nullptr;
-        RT_CHECK(hipMalloc(&stage, t->bytes));
-        RT_CHECK(hipMemcpyAsync(stage, src, t->bytes, hipMemcpyHostToDevice, m->stream));
-        for (int e = 0; e < t->slices; ++e)         // structure-of-arrays layout per expert slice
-            RC(kcpp_weight_repack(t->type, (uint8_t *)stage + e * t->slice_bytes, (uint8_t *)t->d + e * t->slice_bytes,
-                                  t->K, t->N, 0, m->stream));
-        RT_CHECK(hipStreamSynchronize(m->stream));
-        RT_CHECK(hipFree(stage));
-    } else {
-        RT_CHECK(hipMemcpyAsync(t->d, src, t->bytes, hipMemcpyHostToDevice, m->stream));
-        RT_CHECK(hipStreamSynchronize(m->stream));
+    if (!t->rs.empty()) {                  // row split: GGUF rows are contiguous, each slice uploads its own
+        const size_t row_bytes = (size_t)tensor_bytes(t->type, t->K, 1);
+        for (const RowSlice &r : t->rs) {
+            const Lane &ln = m->lanes[r.lane];
+            RC(upload(ln.dev, ln.inline_main ? m->stream : ln.s, t->type, t->K, r.hi - r.lo, 1, 0,
+                      (const uint8_t *)src + r.lo * row_bytes, r.d));
+        }
+        RT_CHECK(hipSetDevice(m->device));
+        return 0;
     }
-    return 0;
+    return upload(m->device, m->stream, t->type, t->K, t->N, t->slices, t->slice_bytes, src, t->d);
 }
 
 extern "C" float *kcpp_model_hidden(kcpp_model *m) { return m->x; }
@@ -460,7 +519,108 @@ extern "C" int kcpp_model_read_logits(kcpp_model *m, float *host) {
 }
 extern "C" int64_t kcpp_model_weight_bytes(kcpp_model *m) { return m->weight_bytes; }
 extern "C" int kcpp_model_set_graphs(kcpp_model *m, int enable) {
-    m->use_graphs = enable != 0;
+    m->use_graphs = enable != 0 && m->lanes.empty();   // split buffers disable graphs (ggml-cuda.cu graph_compute)
+    return 0;
+}
+
+// rows [lo, hi) of an nrows matrix on device `id` of n under tensor_split (get_row_split / ggml_cuda_op_mul_mat,
+// ggml-cuda.cu:625-651,1445-1463): tensor_split is normalized to cumulative starts (ggml_backend_cuda_split_buffer_type,
+// all zero: equal shares), the bounds are rounded down to the MMQ tile height (get_row_rounding: 128 rows on CDNA)
+// unless they reach nrows, the last device ends at nrows
+extern "C" int kcpp_row_split_range(int64_t nrows, int n, const float *tensor_split, int id, int64_t *lo, int64_t *hi) {
+    if (n < 1 || n > 16 || id < 0 || id >= n) return -1;
+    float start[17];
+    float sum = 0.0f;
+    bool zero = true;
+    for (int i = 0; i < n; ++i) zero &= !tensor_split || tensor_split[i] == 0.0f;
+    for (int i = 0; i < n; ++i) { start[i] = sum; sum += zero ? 1.0f : tensor_split[i]; }
+    for (int i = 0; i < n; ++i) start[i] /= sum;
+    // get_row_rounding: the tile height of every device with a non-empty share
+    int64_t rounding = 0;
+    for (int i = 0; i < n; ++i)
+        if (start[i] < (i + 1 < n ? start[i + 1] : 1.0f)) rounding = 128;
+    if (!rounding) rounding = 128;
+    int64_t l = 0, h = nrows;
+    if (id != 0) {
+        l = (int64_t)(nrows * start[id]);
+        if (l < nrows) l -= l % rounding;
+    }
+    if (id != n - 1) {
+        h = (int64_t)(nrows * start[id + 1]);
+        if (h < nrows) h -= h % rounding;
+    }
+    *lo = l; *hi = h;
+    return 0;
+}
+
+// LLAMA_SPLIT_MODE_ROW (koboldcpp --rowsplit, gpttype_adapter.cpp:1892; llm_load_tensors' split_buft for the
+// repeating layers' matrices and the output matrix, src/llama.cpp:7038-7057): the stage keeps every non-matrix
+// op, the KV cache and the activations on its own device (main_gpu) and the rows of each dense matrix are spread
+// over `devices` by tensor_split.  Call after create and before the weights are set; the fused single-token
+// kernels (norm / RoPE / KV store inside the mat-vecs) and graph replay are off, as the reference's split
+// buffers turn CUDA graphs off.  MoE expert tensors cannot be split (ggml_cuda_op_mul_mat asserts ne02 == 1 for
+// split buffers, ggml-cuda.cu:1404): refused.
+extern "C" int kcpp_model_set_row_split(kcpp_model *m, int n, const int *devices, const float *tensor_split) {
+    if (!m->lanes.empty()) { g_err = "row split already set"; return -2; }
+    if (n < 1 || n > 16) { g_err = "row split: 1..16 devices"; return -2; }
+    if (m->hp.n_expert > 0) { g_err = "row split: MoE expert tensors cannot be split (ggml-cuda.cu:1404)"; return -3; }
+    RT_CHECK(hipSetDevice(m->device));
+    int ndev = 0;
+    RT_CHECK(hipGetDeviceCount(&ndev));
+    for (int i = 0; i < n; ++i)
+        if (!devices || devices[i] < 0 || devices[i] >= ndev) { g_err = "row split: bad device index"; return -2; }
+    m->lanes.resize(n);
+    bool have_inline = false;
+    for (int i = 0; i < n; ++i) {
+        m->lanes[i].dev = devices[i];
+        if (devices[i] == m->device && !have_inline) { m->lanes[i].inline_main = true; have_inline = true; }
+    }
+    // the split matrices: each layer's q, k, v, o, gate, up, down and the output head; the concatenated q|k|v and
+    // gate|up groups of the prefill fusion give way to per-device slices
+    std::vector<KTensor *> mats;
+    for (auto &L : m->layers) {
+        for (int j : {1, 2, 3, 4, 6, 7, 8}) mats.push_back(&L.t[j]);
+        if (L.qkv_base) { (void)hipFree(L.qkv_base); L.qkv_base = nullptr; }
+        if (L.glu_base) { (void)hipFree(L.glu_base); L.glu_base = nullptr; }
+        L.nqkv = 0; L.glu_fused = false;
+    }
+    if (m->has_output) mats.push_back(&m->output);
+    size_t ymax = 0;
+    for (KTensor *t : mats) {
+        if (t->owned && t->d) (void)hipFree(t->d);
+        t->d = nullptr; t->owned = false;
+        for (int i = 0; i < n; ++i) {
+            RowSlice r;
+            r.lane = i;
+            kcpp_row_split_range(t->N, n, tensor_split, i, &r.lo, &r.hi);
+            if (r.hi > r.lo) {
+                RT_CHECK(hipSetDevice(devices[i]));
+                RT_CHECK(hipMalloc(&r.d, ((size_t)tensor_bytes(t->type, t->K, r.hi - r.lo) + 255) & ~(size_t)255));
+                ymax = std::max(ymax, (size_t)(r.hi - r.lo) * (t == &m->output ? 1 : m->ub));
+            }
+            t->rs.push_back(r);
+        }
+    }
+    for (Lane &ln : m->lanes) {
+        if (ln.inline_main) continue;
+        RT_CHECK(hipSetDevice(ln.dev));
+        RT_CHECK(hipStreamCreateWithFlags(&ln.s, hipStreamNonBlocking));
+        RT_CHECK(hipEventCreateWithFlags(&ln.done, hipEventDisableTiming));
+        RT_CHECK(hipMalloc(&ln.act, m->act_sz));
+        RT_CHECK(hipMalloc((void **)&ln.y, std::max<size_t>(ymax, 1) * 4));
+        if (m->gemm_ws_sz) RT_CHECK(hipMalloc(&ln.ws, m->gemm_ws_sz));
+        if (ln.dev != m->device) {             // direct xGMI copies both ways
+            (void)hipDeviceEnablePeerAccess(m->device, 0);
+            RT_CHECK(hipSetDevice(m->device));
+            (void)hipDeviceEnablePeerAccess(ln.dev, 0);
+            (void)hipGetLastError();
+        }
+    }
+    RT_CHECK(hipSetDevice(m->device));
+    RT_CHECK(hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
+    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    m->use_graphs = false;
+    m->fused_decode = false;
     return 0;
 }
 // the expert ids the last MoE prefill layer of this model (stage) routed its T tokens to, [T][n_expert_used]
@@ -500,14 +660,57 @@ extern "C" int kcpp_model_set_kv_types(kcpp_model *m, int tk, int tv) {
     return 0;
 }
 extern "C" int kcpp_model_set_fused_decode(kcpp_model *m, int enable) {
-    m->fused_decode = enable != 0;
+    m->fused_decode = enable != 0 && m->lanes.empty();
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    return 0;
+}
+
+static int mm_launch(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
+                     int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, hipStream_t s) {
+    if (M <= 8) return kcpp_gemv(type, W, W2, K, N, act, M, Y, ldy, res, ldr, mode, s);
+    return kcpp_gemm(type, W, W2, K, N, act, M, Y, ldy, res, ldr, mode, ws, s);
+}
+
+// row split (ggml_cuda_op_mul_mat's split branch, ggml-cuda.cu:1403-1700): every lane computes its rows [lo, hi)
+// of Y.  A lane other than the inline one waits for the stage stream's ev_in, takes the activation block (and,
+// with a residual, its rows of the residual) by peer copies on its own stream, runs the same mat-vec / GEMM on
+// its slice into its own rows buffer and copies those rows into Y before its `done` event, which the stage
+// stream waits on.  Per row the arithmetic is the unsplit kernel's, so the split changes no row's result
+// beyond the GEMM's split-K grouping (which follows the slice's grid).
+static int matmul_rows(kcpp_model *m, const KTensor &W, const KTensor *W2, const void *act, int64_t M, float *Y,
+                       int64_t ldy, const float *res, int64_t ldr, int mode) {
+    const size_t abytes = (size_t)kcpp_act_bytes(W.type, W.K, M);
+    bool fenced = false;
+    for (size_t i = 0; i < W.rs.size(); ++i) {
+        const RowSlice &r = W.rs[i];
+        const int64_t n = r.hi - r.lo;
+        if (n <= 0) continue;
+        const void *w2 = W2 ? W2->rs[i].d : nullptr;
+        const Lane &ln = m->lanes[r.lane];
+        if (ln.inline_main) {
+            RC(mm_launch(W.type, r.d, w2, W.K, n, act, M, Y + r.lo, ldy, res ? res + r.lo : nullptr, ldr, mode, m->gemm_ws,
+                         m->stream));
+            continue;
+        }
+        if (!fenced) { RT_CHECK(hipEventRecord(m->ev_in, m->stream)); fenced = true; }
+        RT_CHECK(hipSetDevice(ln.dev));
+        RT_CHECK(hipStreamWaitEvent(ln.s, m->ev_in, 0));
+        RT_CHECK(hipMemcpyPeerAsync(ln.act, ln.dev, act, m->device, abytes, ln.s));
+        if (res)
+            RT_CHECK(hipMemcpy2DAsync(ln.y, n * 4, res + r.lo, ldr * 4, n * 4, M, hipMemcpyDefault, ln.s));
+        RC(mm_launch(W.type, r.d, w2, W.K, n, ln.act, M, ln.y, n, res ? ln.y : nullptr, n, mode, ln.ws, ln.s));
+        RT_CHECK(hipMemcpy2DAsync(Y + r.lo, ldy * 4, ln.y, n * 4, n * 4, M, hipMemcpyDefault, ln.s));
+        RT_CHECK(hipEventRecord(ln.done, ln.s));
+        RT_CHECK(hipSetDevice(m->device));
+        RT_CHECK(hipStreamWaitEvent(m->stream, ln.done, 0));
+    }
     return 0;
 }
 
 // y[c][n] = W . act  (+res) for M columns: mat-vec for M <= 8, MFMA GEMM above
 static int matmul(kcpp_model *m, const KTensor &W, const KTensor *W2, const void *act, int64_t M, float *Y, int64_t ldy,
                   const float *res, int64_t ldr, int mode) {
+    if (!W.rs.empty()) return matmul_rows(m, W, W2, act, M, Y, ldy, res, ldr, mode);
     if (M <= 8)
         return kcpp_gemv(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, m->stream);
     return kcpp_gemm(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, m->gemm_ws, m->stream);
@@ -768,7 +971,7 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
                 RC(matmul(m, t[2], nullptr, m->act, T, m->qkv + E, LQ, nullptr, 0, 0));
                 RC(matmul(m, t[3], nullptr, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0));
             }
-        } else if (T > 8 && T <= 32 && t[1].type == KT_Q8_0 && t[2].type == KT_Q8_0 && t[3].type == KT_Q8_0 && E % 128 == 0 &&
+        } else if (T > 8 && T <= 32 && m->lanes.empty() && t[1].type == KT_Q8_0 && t[2].type == KT_Q8_0 && t[3].type == KT_Q8_0 && E % 128 == 0 &&
                    EKV % 128 == 0) {                 // small-batch Q8_0: one quantization, one q|k|v launch
             RC(kcpp_rms_norm_q80(m->x, E, (const float *)t[0].d, m->act, E, T, hp.eps, s));
             const void *Wq[3] = {t[1].d, t[2].d, t[3].d};
@@ -815,7 +1018,7 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             f.N = 2 * F;                               // silu(g)*u fused into the Q8_K quantization
             RC(matmul(m, f, nullptr, m->act, T, m->hglu, 2 * F, nullptr, 0, 0));
             RC(kcpp_quantize_act_glu(m->hglu, 2 * F, F, m->act2, F, T, s));
-        } else if (T <= 32 && t[6].type == KT_Q8_0 && t[7].type == KT_Q8_0 && kcpp_vec_dot_type(t[8].type) == KT_Q8_0 &&
+        } else if (T <= 32 && m->lanes.empty() && t[6].type == KT_Q8_0 && t[7].type == KT_Q8_0 && kcpp_vec_dot_type(t[8].type) == KT_Q8_0 &&
                    F % 32 == 0) {
             RC(kcpp_gemm_q80_glu_q80(t[6].d, t[7].d, E, F, m->act, T, m->act2, m->gemm_ws, s));   // Q8_0(silu(g) * u)
         } else {
@@ -843,8 +1046,7 @@ static int head(kcpp_model *m, int T) {
         RC(kcpp_rms_norm(last, E, (const float *)m->output_norm.d, m->attn, E, nullptr, E, 1, hp.eps, m->stream));
         RC(kcpp_quantize_act(kcpp_vec_dot_type(m->output.type), m->attn, E, m->act, E, 1, m->stream));
     }
-    RC(kcpp_gemv(m->output.type, m->output.d, nullptr, E, hp.n_vocab, m->act, 1, m->logits, hp.n_vocab, nullptr, 0, 0,
-                 m->stream));
+    RC(matmul(m, m->output, nullptr, m->act, 1, m->logits, hp.n_vocab, nullptr, 0, 0));
     return 0;
 }
 

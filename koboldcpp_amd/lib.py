@@ -87,6 +87,8 @@ _SIGS = {
     "kcpp_model_decode_greedy": [P, I, P],
     "kcpp_model_set_graphs": [P, I],
     "kcpp_model_set_fused_decode": [P, I],
+    "kcpp_model_set_row_split": [P, I, P, P],
+    "kcpp_row_split_range": [I64, I, P, I, P, P],
     "kcpp_model_set_fa_exact": [P, I],
     "kcpp_model_moe_ids": [P, P, I],
     "kcpp_flash_attn_exact": [P, P, P, P, I, I, I, I, I, P, Fl, P],
@@ -307,6 +309,14 @@ class Model:
     def set_graphs(self, on):
         _L.kcpp_model_set_graphs(self.m, int(on))
 
+    def set_row_split(self, devices, tensor_split):
+        """LLAMA_SPLIT_MODE_ROW over `devices` (lanes may repeat a GPU); before synth / set_tensor"""
+        n = len(devices)
+        d = (ctypes.c_int * n)(*devices)
+        ts = (ctypes.c_float * n)(*tensor_split)
+        _chk(_L.kcpp_model_set_row_split(self.m, n, d, ts), "set_row_split")
+
+
     def weight_bytes(self):
         return int(_L.kcpp_model_weight_bytes(self.m))
 
@@ -317,3 +327,12 @@ class Model:
 
     def __del__(self):
         self.close()
+
+
+def row_split_range(nrows, tensor_split, i):
+    """(lo, hi) of device i's rows (kcpp_row_split_range)"""
+    n = len(tensor_split)
+    ts = (ctypes.c_float * n)(*tensor_split)
+    lo, hi = ctypes.c_int64(0), ctypes.c_int64(0)
+    _chk(_L.kcpp_row_split_range(int(nrows), n, ts, int(i), ctypes.byref(lo), ctypes.byref(hi)), "row_split_range")
+    return lo.value, hi.value

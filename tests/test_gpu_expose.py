@@ -260,3 +260,52 @@ def test_generate_layer_split_pipeline_matches_single_stage(model, tmp_path, mon
         n += 1
     m.close()
     assert out.text == b"".join(piece(toks, ttypes, t) for t in want)
+
+
+def test_generate_row_split_matches_in_process(model, tmp_path, monkeypatch):
+    """--rowsplit through load_model (use_rowsplit, tensor_split 1:2; KCPP_VIRTUAL_DEVICES=2 puts both row lanes on
+    the test box's GPU): one stage owning every layer, each matrix's rows split over the lanes -- greedy text equal
+    to the same row split built in-process"""
+    import koboldcpp_amd.lib as K
+    h, X, _, _, _ = model
+    hp = dict(R.TINY, n_layer=3, n_ctx=256)
+    types = R.q4_k_m_types(hp["n_layer"])
+    path = str(tmp_path / "rows.gguf")
+    toks = GW.llama_gguf(path, hp, types, 1234, WORDS)
+    monkeypatch.setenv("KCPP_VIRTUAL_DEVICES", "2")
+    li = X.load_model_inputs()
+    li.model_filename = path.encode()
+    li.max_context_length = 248
+    li.blasbatchsize = 512
+    li.gpulayers = 999
+    li.rope_freq_base = 10000.0
+    li.rope_freq_scale = 1.0
+    li.use_rowsplit = True
+    for i, v in enumerate((1.0, 2.0)):
+        li.tensor_split[i] = v
+    assert h.load_model(li)
+    _, _, ttypes = GW.spm_vocab(hp["n_vocab"], WORDS)
+    prompt = b" ".join([b"hello world the a b of to"] * 3)
+    r = h.token_count(prompt, True)
+    ids = [r.ids[i] for i in range(r.count)]
+    gi = X.generation_inputs()
+    gi.prompt = prompt
+    gi.max_context_length = 248
+    gi.max_length = 8
+    gi.temperature = 0.0
+    gi.top_k = 1
+    gi.rep_pen = 1.0
+    gi.bypass_eos_token = True
+    out = h.generate(gi)
+    assert out.status == 1
+    m = K.Model(hp, types)
+    m.set_row_split([0, 0], (1.0, 2.0))
+    m.synth(1234)
+    m.decode(ids, 0, want_logits=False)
+    want = [m.argmax()]
+    n = len(ids)
+    for _ in range(7):
+        want.append(m.decode_greedy(n))
+        n += 1
+    m.close()
+    assert out.text == b"".join(piece(toks, ttypes, t) for t in want)
