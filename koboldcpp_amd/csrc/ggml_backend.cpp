@@ -11,7 +11,7 @@
 // graphs off) and dispatches each to a kernel of this library:
 //   MUL_MAT      quantized weight: activation -> Q8_K/Q8_0 (kcpp_quantize_act), then the mat-vec (M <= 8) or the
 //                MFMA GEMM on a device-native image of the weight (row-major Q4_K_RS / Q6_K_RS planes, the
-//                structure-of-arrays Q4_0 / Q8_0 / Q6_K layouts), built once per weight on first use and kept until
+//                structure-of-arrays Q4_0 / Q8_0 / Q2_K / Q3_K / Q6_K layouts), built once per weight on first use and kept until
 //                the weight's buffer is written again; F16 / F32 weight: kcpp_ggml_mul_mat_f
 //   GET_ROWS     quantized: kcpp_get_rows on the native image; F16 / F32: kcpp_ggml_get_rows
 //   FLASH_ATTN_EXT  kcpp_flash_attn_ext (graph-form Q view, F16 K/V cache views, F16 mask)
@@ -302,7 +302,9 @@ int matmul_layout(int t, int64_t K) {
     if (t == KT_Q6_K && kcpp_rs_supported(KT_Q6_K_RS, K)) return KT_Q6_K_RS;
     return t;
 }
-bool matmul_quant_ok(int t) { return t == KT_Q4_0 || t == KT_Q8_0 || t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K; }
+bool matmul_quant_ok(int t) {
+    return t == KT_Q4_0 || t == KT_Q8_0 || t == KT_Q2_K || t == KT_Q3_K || t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K;
+}
 
 bool supports(const kggml_tensor *op) {
     auto f32 = [](const kggml_tensor *t) { return t && t->type == KGGML_TYPE_F32; };
