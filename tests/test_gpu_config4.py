@@ -32,20 +32,25 @@ def test_70b_stage_properties(K):
     """10-layer first stage (layers [0, 10) + embedding): no non-finite values; graph replay equals eager decode
     bit for bit; decode runs the K = 28672 down fallback in every layer.  Prefill in ubatches of 12 (attention by
     the split-KV kernel, T <= 16) vs one ubatch of 24 (MFMA flash attention, P rounded to f16) on the FIRST layer:
-    the two attention kernels' rounding only (across 10 random-weight layers such differences grow chaotically
-    -- the reference's own build-to-build spread does the same, tests/golden/ref_spread.npz)"""
+    with the strict-order attention (the same kernel for both splits) the last 12 rows are bit-identical; with the
+    production kernels they differ by the two attention kernels' rounding, which an activation quantization
+    (Q8_K before wo and the FFN) can turn into a flipped int8 rounding -- a discontinuity that moves a row by up to
+    ~1% of its scale (measured: 1-2 rows in 12, under either GEMM split policy) -- so most rows must agree to 1e-5 and
+    none may move beyond 2%.  (Across 10 random-weight layers such differences grow chaotically; the reference's
+    own build-to-build spread does the same, tests/golden/ref_spread.npz.)"""
     types = R.q4_k_m_types(L70["n_layer"])
     T, E = 24, L70["n_embd"]
     prompt = [int(v) for v in np.random.default_rng(70).integers(1, L70["n_vocab"], size=T)]
     res = {}
-    for mode in ("prefill24", "prefill12", "decode_graph", "decode_eager"):
+    for mode in ("prefill24", "prefill12", "prefill24x", "prefill12x", "decode_graph", "decode_eager"):
         m = K.Model(L70, types, il0=0, il1=1 if mode.startswith("prefill") else 10, has_embed=True, has_output=False,
-                    max_ubatch=12 if mode == "prefill12" else 24)
+                    max_ubatch=12 if mode.startswith("prefill12") else 24)
         m.synth(1234)
         if mode.startswith("prefill"):
+            m.set_fa_exact(mode.endswith("x"))
             m.decode(prompt, 0, want_logits=False)
-            rows = 12 if mode == "prefill12" else 24
-            res[mode] = m.read_hidden(rows * E).reshape(rows, E)[-1]
+            rows = 12 if mode.startswith("prefill12") else 24
+            res[mode] = m.read_hidden(rows * E).reshape(rows, E)[-12:]
         else:
             m.set_graphs(mode == "decode_graph")
             for i, t in enumerate(prompt):
@@ -55,10 +60,11 @@ def test_70b_stage_properties(K):
     for v in res.values():
         assert np.isfinite(v).all()
     assert np.array_equal(res["decode_graph"], res["decode_eager"])
+    assert np.array_equal(res["prefill12x"], res["prefill24x"])
     scale = np.abs(res["prefill24"]).max()
-    d = np.abs(res["prefill12"] - res["prefill24"])
-    print("70B layer 0, ubatch 12 vs 24: max %.3g median %.3g scale %.3g" % (d.max(), np.median(d), scale))
-    assert d.max() <= 1e-5 * scale and np.median(d) <= 1e-6 * scale, (d.max(), np.median(d), scale)   # measured 5.4e-7, 6.7e-8
+    d = np.abs(res["prefill12"] - res["prefill24"]).max(axis=1)          # per row
+    print("70B layer 0, ubatch 12 vs 24, per-row max:", " ".join("%.2g" % v for v in d), "scale %.3g" % scale)
+    assert np.median(d) <= 1e-5 * scale and np.mean(d <= 1e-5 * scale) >= 0.75 and d.max() <= 0.02 * scale, d
 
 
 def test_70b_width_one_layer_vs_oracle(K):
