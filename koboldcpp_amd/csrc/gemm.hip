@@ -130,6 +130,7 @@ template <> struct GemmTraits<KT_Q6_K> { static constexpr int NB = 2; static con
 template <> struct GemmTraits<KT_Q3_K> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = true; };
 template <> struct GemmTraits<KT_Q2_K> { static constexpr int NB = 1; static constexpr bool MINS = true; static constexpr bool SB = true; };
 template <> struct GemmTraits<KT_Q4_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
+template <> struct GemmTraits<KT_Q5_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
 template <> struct GemmTraits<KT_Q8_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
 
 template <int NB> struct GemmSmem {
@@ -268,6 +269,24 @@ __device__ __forceinline__ void stage_weights(SM &S, const uint8_t *__restrict__
             S.bf[0][bslot(nl, 32 * jb + 16)] = frag8((qd[0] >> 4) & 0x0F0F0F0Fu, (qd[1] >> 4) & 0x0F0F0F0Fu, 1.0f, 8.0f);
             S.bf[0][bslot(nl, 32 * jb + 24)] = frag8((qd[2] >> 4) & 0x0F0F0F0Fu, (qd[3] >> 4) & 0x0F0F0F0Fu, 1.0f, 8.0f);
             S.wd[nl][jb] = h2f(*(const uint16_t *)(W + nbt * 16 + b * 2));
+        }
+    } else if constexpr (TYPE == KT_Q5_0) {
+        // as Q4_0 with the fifth bit: (q | h << 4) - 16 in [-16, 15], exact in f16
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int jb = 2 * c + bb;
+            const int64_t b = n * bpr + sb * 8 + jb;
+            const uint4 qv = *(const uint4 *)(W + b * 16);
+            const uint32_t h = *(const uint32_t *)(W + nbt * 16 + b * 4);
+            const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
+            auto hb = [&](int sh) { return (((h >> sh) & 0xFu) * 0x00204081u & 0x01010101u) << 4; };
+            S.bf[0][bslot(nl, 32 * jb + 0)] = frag8((qd[0] & 0x0F0F0F0Fu) | hb(0), (qd[1] & 0x0F0F0F0Fu) | hb(4), 1.0f, 16.0f);
+            S.bf[0][bslot(nl, 32 * jb + 8)] = frag8((qd[2] & 0x0F0F0F0Fu) | hb(8), (qd[3] & 0x0F0F0F0Fu) | hb(12), 1.0f, 16.0f);
+            S.bf[0][bslot(nl, 32 * jb + 16)] = frag8(((qd[0] >> 4) & 0x0F0F0F0Fu) | hb(16), ((qd[1] >> 4) & 0x0F0F0F0Fu) | hb(20),
+                                                     1.0f, 16.0f);
+            S.bf[0][bslot(nl, 32 * jb + 24)] = frag8(((qd[2] >> 4) & 0x0F0F0F0Fu) | hb(24), ((qd[3] >> 4) & 0x0F0F0F0Fu) | hb(28),
+                                                     1.0f, 16.0f);
+            S.wd[nl][jb] = h2f(*(const uint16_t *)(W + nbt * 20 + b * 2));
         }
     } else {   // Q8_0: int8 -> (q ^ 0x80) = q + 128 as a byte
 #pragma unroll
@@ -1342,7 +1361,7 @@ __global__ void k_silu_mul_strided(float *__restrict__ y, int64_t ldy, const flo
 
 static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a16, int64_t &o_dy, int64_t &o_bs, int64_t &o_up) {
     const int64_t Mp = (M + GB_M - 1) / GB_M * GB_M;
-    const int64_t G = (type == KT_Q4_0 || type == KT_Q8_0) ? 32 : 256;
+    const int64_t G = (type == KT_Q4_0 || type == KT_Q5_0 || type == KT_Q8_0) ? 32 : 256;
     int64_t off = 0;
     o_a16 = off; off += (Mp * K * 2 + 255) & ~255LL;
     o_dy = off; off += (Mp * (K / G) * 4 + 255) & ~255LL;
@@ -1581,6 +1600,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         case KT_Q2_K: hipLaunchKernelGGL(k_gemm<KT_Q2_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         case KT_Q3_K: hipLaunchKernelGGL(k_gemm<KT_Q3_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         case KT_Q4_0: hipLaunchKernelGGL(k_gemm<KT_Q4_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
+        case KT_Q5_0: hipLaunchKernelGGL(k_gemm<KT_Q5_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         case KT_Q8_0: hipLaunchKernelGGL(k_gemm<KT_Q8_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
         default: return -3;
         }

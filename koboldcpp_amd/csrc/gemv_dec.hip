@@ -27,6 +27,7 @@ extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int 
     case KT_Q3_K: return dispatch_mode<KT_Q3_K>(a, mode, pro, rows_per_wave, s);
     case KT_Q2_K: return dispatch_mode<KT_Q2_K>(a, mode, pro, rows_per_wave, s);
     case KT_Q4_0: return dispatch_mode<KT_Q4_0>(a, mode, pro, rows_per_wave, s);
+    case KT_Q5_0: return dispatch_mode<KT_Q5_0>(a, mode, pro, rows_per_wave, s);
     case KT_Q8_0: return dispatch_mode<KT_Q8_0>(a, mode, pro, rows_per_wave, s);
     default: return -3;
     }

@@ -104,6 +104,19 @@ template <> struct Unit<KT_Q4_0> {
         d = *(const uint16_t *)(base + nb * 16 + b * 2);
     }
 };
+// ---- Q5_0 (SoA): unit = one 32-elem block: 16 B nibbles + 4 B high bits + fp16 d
+template <> struct Unit<KT_Q5_0> {
+    static constexpr int ELEMS = 32;
+    uint4 q;
+    uint32_t h;
+    uint16_t d;
+    __device__ __forceinline__ void load(const uint8_t *base, int64_t nb, int64_t b0, int u) {
+        const int64_t b = b0 + u;
+        q = ld_nt((const void *)(base + b * 16));
+        h = *(const uint32_t *)(base + nb * 16 + b * 4);
+        d = *(const uint16_t *)(base + nb * 20 + b * 2);
+    }
+};
 // ---- Q8_0 (SoA): unit = one 32-elem block: 32 B int8 + fp16 d
 template <> struct Unit<KT_Q8_0> {
     static constexpr int ELEMS = 32;
@@ -166,6 +179,7 @@ __device__ __forceinline__ void load_act0(const ActView &av, int u, Act0 &x) {
 
 template <int TYPE> struct ActOf { typedef ActK T; };
 template <> struct ActOf<KT_Q4_0> { typedef Act0 T; };
+template <> struct ActOf<KT_Q5_0> { typedef Act0 T; };
 template <> struct ActOf<KT_Q8_0> { typedef Act0 T; };
 
 __device__ __forceinline__ void load_act(const ActView &av, int u, ActK &x) { load_actk(av, u, x); }
@@ -316,6 +330,22 @@ __device__ __forceinline__ float unit_dot(const Unit<KT_Q4_0> &w, int, const Act
         s = sdot4((int)((q >> 4) & 0x0F0F0F0Fu), u4(*(const uint4 *)&x.a[1], i), s);
     }
     s -= 8 * x.s;
+    return __fmul_rn((float)s, __fmul_rn(h2f(w.d), x.d));
+}
+
+// 4 high bits (bits 0..3 of v) -> bit 4 of 4 bytes: the multiply places bit i at bit 8i + i, masked to bit 8i
+__device__ __forceinline__ uint32_t hbits4(uint32_t v) { return (((v & 0xFu) * 0x00204081u) & 0x01010101u) << 4; }
+
+// ggml_vec_dot_q5_0_q8_0 (ggml-quants.c:4790): x = (q | h << 4) - 16, so sum x a = sum (q | h << 4) a - 16 sum a
+__device__ __forceinline__ float unit_dot(const Unit<KT_Q5_0> &w, int, const Act0 &x) {
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t q = u4(w.q, i);
+        s = sdot4((int)((q & 0x0F0F0F0Fu) | hbits4(w.h >> (4 * i))), u4(*(const uint4 *)&x.a[0], i), s);
+        s = sdot4((int)(((q >> 4) & 0x0F0F0F0Fu) | hbits4(w.h >> (16 + 4 * i))), u4(*(const uint4 *)&x.a[1], i), s);
+    }
+    s -= 16 * x.s;
     return __fmul_rn((float)s, __fmul_rn(h2f(w.d), x.d));
 }
 

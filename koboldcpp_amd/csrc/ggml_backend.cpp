@@ -303,7 +303,7 @@ int matmul_layout(int t, int64_t K) {
     return t;
 }
 bool matmul_quant_ok(int t) {
-    return t == KT_Q4_0 || t == KT_Q8_0 || t == KT_Q2_K || t == KT_Q3_K || t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K;
+    return t == KT_Q4_0 || t == KT_Q5_0 || t == KT_Q8_0 || t == KT_Q2_K || t == KT_Q3_K || t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K;
 }
 
 bool supports(const kggml_tensor *op) {

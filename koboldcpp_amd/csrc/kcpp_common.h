@@ -101,7 +101,7 @@ __host__ __device__ inline ActView act_view(int vtype, const void *buf, int64_t 
     return a;
 }
 inline int vec_dot_type(int wtype) {
-    return (wtype == KT_Q4_0 || wtype == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;
+    return (wtype == KT_Q4_0 || wtype == KT_Q5_0 || wtype == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;
 }
 
 // ---------------------------------------------------------------------------------

@@ -36,6 +36,12 @@ __device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uin
         d[0] = src[0]; d[1] = src[1];
         for (int i = 0; i < 16; ++i) q[i] = src[2 + i];
     } break;
+    case KT_Q5_0: {   // SoA planes: qs [nb][16] ++ qh [nb][4] ++ d [nb][2]  (block_q5_0: d, qh[4], qs[16])
+        uint8_t *q = dst + b * 16, *h = dst + nb * 16 + b * 4, *d = dst + nb * 20 + b * 2;
+        d[0] = src[0]; d[1] = src[1];
+        for (int i = 0; i < 4; ++i) h[i] = src[2 + i];
+        for (int i = 0; i < 16; ++i) q[i] = src[6 + i];
+    } break;
     case KT_Q8_0: {
         uint8_t *q = dst + b * 32, *d = dst + nb * 32 + b * 2;
         d[0] = src[0]; d[1] = src[1];
@@ -94,6 +100,12 @@ __device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint
         const uint8_t *q = src + b * 16, *d = src + nb * 16 + b * 2;
         blk[0] = d[0]; blk[1] = d[1];
         for (int i = 0; i < 16; ++i) blk[2 + i] = q[i];
+    } break;
+    case KT_Q5_0: {
+        const uint8_t *q = src + b * 16, *h = src + nb * 16 + b * 4, *d = src + nb * 20 + b * 2;
+        blk[0] = d[0]; blk[1] = d[1];
+        for (int i = 0; i < 4; ++i) blk[2 + i] = h[i];
+        for (int i = 0; i < 16; ++i) blk[6 + i] = q[i];
     } break;
     case KT_Q8_0: {
         const uint8_t *q = src + b * 32, *d = src + nb * 32 + b * 2;
@@ -188,6 +200,14 @@ __device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t bpr,
             o[j + 16] = ((blk[2 + j] >> 4) - 8) * d;
         }
     } break;
+    case KT_Q5_0: {   // dequantize_row_q5_0, ggml-quants.c:1564-1588
+        const float d = h2f(blk[0] | (blk[1] << 8));
+        const uint32_t qh = blk[2] | (blk[3] << 8) | (blk[4] << 16) | ((uint32_t)blk[5] << 24);
+        for (int j = 0; j < 16; ++j) {
+            o[j] = (float)((int)((blk[6 + j] & 0x0F) | (((qh >> j) << 4) & 0x10)) - 16) * d;
+            o[j + 16] = (float)((int)((blk[6 + j] >> 4) | ((qh >> (j + 12)) & 0x10)) - 16) * d;
+        }
+    } break;
     case KT_Q8_0: {
         float d = h2f(blk[0] | (blk[1] << 8));
         for (int j = 0; j < 32; ++j) o[j] = (int8_t)blk[2 + j] * d;
@@ -267,6 +287,12 @@ __device__ __forceinline__ float deq_elem(int type, const uint8_t *src, int64_t 
         const float d = h2f(*(const uint16_t *)(src + nb * 16 + b * 2));
         const uint8_t q = src[b * 16 + (e & 15)];
         return ((e < 16 ? (q & 0xF) : (q >> 4)) - 8) * d;
+    }
+    case KT_Q5_0: {
+        const float d = h2f(*(const uint16_t *)(src + nb * 20 + b * 2));
+        const uint8_t q = src[b * 16 + (e & 15)];
+        const uint32_t qh = *(const uint32_t *)(src + nb * 16 + b * 4);
+        return (float)((int)((e < 16 ? (q & 0xF) : (q >> 4)) | (((qh >> e) & 1) << 4)) - 16) * d;
     }
     case KT_Q8_0: return (int8_t)src[b * 32 + e] * h2f(*(const uint16_t *)(src + nb * 32 + b * 2));
     case KT_Q4_K: case KT_Q5_K: {

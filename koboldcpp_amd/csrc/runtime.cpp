@@ -452,7 +452,7 @@ static int upload(int dev, hipStream_t s, int type, int64_t K, int64_t N, int sl
     if (!slice_bytes) slice_bytes = bytes;
     if (bytes == 0) return 0;
     RT_CHECK(hipSetDevice(dev));
-    if (type == KT_Q6_K || type == KT_Q3_K || type == KT_Q2_K || type == KT_Q4_0 || type == KT_Q8_0 || type == KT_Q4_K_RS ||
+    if (type == KT_Q6_K || type == KT_Q3_K || type == KT_Q2_K || type == KT_Q4_0 || type == KT_Q5_0 || type == KT_Q8_0 || type == KT_Q4_K_RS ||
         type == KT_Q6_K_RS) {
         void *stage = nullptr;
         RT_CHECK(hipMalloc(&stage, bytes));

@@ -18,6 +18,7 @@
 #define QK_K 256
 
 typedef struct { uint16_t d; uint8_t qs[16]; } blk_q4_0;                  /* ggml-common.h:144 */
+typedef struct { uint16_t d; uint8_t qh[4]; uint8_t qs[16]; } blk_q5_0;   /* ggml-common.h:161 */
 typedef struct { uint16_t d; int8_t qs[32]; } blk_q8_0;                   /* ggml-common.h:186 */
 typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qs[128]; } blk_q4_K;   /* :286 */
 typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qh[32]; uint8_t qs[128]; } blk_q5_K; /* :303 */
@@ -27,6 +28,7 @@ typedef struct { uint8_t scales[16]; uint8_t qs[64]; uint16_t d, dmin; } blk_q2_
 typedef struct { float d; int8_t qs[256]; int16_t bsums[16]; } blk_q8_K;  /* :330 */
 
 _Static_assert(sizeof(blk_q4_0) == 18, "q4_0");
+_Static_assert(sizeof(blk_q5_0) == 22, "q5_0");
 _Static_assert(sizeof(blk_q8_0) == 34, "q8_0");
 _Static_assert(sizeof(blk_q4_K) == 144, "q4_K");
 _Static_assert(sizeof(blk_q5_K) == 176, "q5_K");
@@ -77,6 +79,20 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
             for (int j = 0; j < 16; ++j) {
                 y[i * 32 + j] = ((x[i].qs[j] & 0x0F) - 8) * d;
                 y[i * 32 + j + 16] = ((x[i].qs[j] >> 4) - 8) * d;
+            }
+        }
+    } return;
+    case KT_Q5_0: {                                   /* ggml-quants.c:1564-1588 */
+        const blk_q5_0 *x = vx;
+        for (int64_t i = 0; i < k / 32; ++i) {
+            const float d = H2F(x[i].d);
+            uint32_t qh;
+            memcpy(&qh, x[i].qh, 4);
+            for (int j = 0; j < 16; ++j) {
+                const int x0 = ((x[i].qs[j] & 0x0F) | (((qh >> j) << 4) & 0x10)) - 16;
+                const int x1 = ((x[i].qs[j] >> 4) | ((qh >> (j + 12)) & 0x10)) - 16;
+                y[i * 32 + j] = x0 * d;
+                y[i * 32 + j + 16] = x1 * d;
             }
         }
     } return;
@@ -194,7 +210,7 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
 /* type_traits[..].vec_dot_type, ggml.c:793-959 */
 int orc_vec_dot_type(int wtype) {
     switch (wtype) {
-        case KT_Q4_0: case KT_Q8_0: return KT_Q8_0;
+        case KT_Q4_0: case KT_Q5_0: case KT_Q8_0: return KT_Q8_0;
         case KT_Q2_K: case KT_Q3_K: case KT_Q4_K: case KT_Q5_K: case KT_Q6_K: return KT_Q8_K;
         case KT_F16: return KT_F16;
         default: return KT_F32;
@@ -432,6 +448,23 @@ static float dot_q4_0(int n, const blk_q4_0 *x, const blk_q8_0 *y) {       /* :3
     return sumf;
 }
 
+static float dot_q5_0(int n, const blk_q5_0 *x, const blk_q8_0 *y) {       /* :4790, scalar tail */
+    float sumf = 0;
+    for (int ib = 0; ib < n / 32; ++ib) {
+        uint32_t qh;
+        memcpy(&qh, x[ib].qh, 4);
+        int s0 = 0, s1 = 0;
+        for (int j = 0; j < 16; ++j) {
+            const int x0 = ((x[ib].qs[j] & 0x0F) | (((qh >> j) << 4) & 0x10)) - 16;
+            const int x1 = ((x[ib].qs[j] >> 4) | ((qh >> (j + 12)) & 0x10)) - 16;
+            s0 += x0 * y[ib].qs[j];
+            s1 += x1 * y[ib].qs[j + 16];
+        }
+        sumf += (H2F(x[ib].d) * H2F(y[ib].d)) * (s0 + s1);
+    }
+    return sumf;
+}
+
 static float dot_q8_0(int n, const blk_q8_0 *x, const blk_q8_0 *y) {       /* :5519, scalar tail */
     float sumf = 0;
     for (int ib = 0; ib < n / 32; ++ib) {
@@ -456,6 +489,7 @@ float orc_vec_dot(int wtype, int n, const void *w, const void *a) {
         case KT_Q3_K: return dot_q3_K(n, w, a);
         case KT_Q2_K: return dot_q2_K(n, w, a);
         case KT_Q4_0: return dot_q4_0(n, w, a);
+        case KT_Q5_0: return dot_q5_0(n, w, a);
         case KT_Q8_0: return dot_q8_0(n, w, a);
         case KT_F16: return dot_f16(n, w, a);
         case KT_F32: { const float *x = w, *y = a; double s = 0; for (int i = 0; i < n; ++i) s += x[i] * y[i]; return (float)s; }

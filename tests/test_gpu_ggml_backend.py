@@ -159,7 +159,8 @@ def test_registry_device_and_buffer_rules(env):
 MM_CASES = [(R.Q4_K, 4096, 512, 1), (R.Q4_K, 4096, 384, 7), (R.Q4_K, 2048, 256, 40), (R.Q6_K, 4096, 256, 1),
             (R.Q6_K, 2048, 256, 33), (R.Q5_K, 4096, 256, 1), (R.Q5_K, 2048, 128, 20), (R.Q8_0, 4096, 256, 1),
             (R.Q8_0, 2048, 256, 24), (R.Q4_0, 4096, 256, 1), (R.Q4_0, 2048, 256, 40), (R.F16, 1024, 96, 5),
-            (R.Q2_K, 4096, 256, 1), (R.Q2_K, 2048, 256, 24), (R.Q3_K, 4096, 256, 1), (R.Q3_K, 2048, 384, 40)]
+            (R.Q2_K, 4096, 256, 1), (R.Q2_K, 2048, 256, 24), (R.Q3_K, 4096, 256, 1), (R.Q3_K, 2048, 384, 40),
+            (R.Q5_0, 4096, 256, 1), (R.Q5_0, 2048, 256, 24)]
 
 
 @pytest.mark.parametrize("case", MM_CASES, ids=lambda c: "t%d_%dx%d_m%d" % c)
@@ -204,7 +205,7 @@ def test_elementwise_ops_vs_reference_cpu(env):
     assert rel(ours, ref) <= 2e-6, rel(ours, ref)
 
 
-@pytest.mark.parametrize("t", [R.Q4_K, R.Q6_K, R.Q8_0, R.Q4_0, R.Q2_K, R.Q3_K, R.F16])
+@pytest.mark.parametrize("t", [R.Q4_K, R.Q6_K, R.Q8_0, R.Q4_0, R.Q5_0, R.Q2_K, R.Q3_K, R.F16])
 def test_get_rows_vs_reference_cpu(env, t):
     """token embedding gather (get_rows of a quantized or f16 table): dequantization is exact on both sides"""
     G, L, be = env

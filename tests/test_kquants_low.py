@@ -1,13 +1,13 @@
-"""Q2_K and Q3_K weights (Q2_K / Q3_K_S / Q3_K_M models; block_q2_K / block_q3_K, ggml-common.h:250,267): the CPU
-oracle and the HIP kernels against the reference builds' own outputs (tests/golden/q2k.npz / q3k.npz, make_q2k.py /
-make_q3k.py).
+"""Q2_K, Q3_K and Q5_0 weights (Q2_K / Q3_K_S / Q3_K_M / Q5_0 models; block_q2_K / block_q3_K / block_q5_0,
+ggml-common.h:250,267,161): the CPU oracle and the HIP kernels against the reference builds' own outputs
+(tests/golden/q2k.npz / q3k.npz / q50.npz, make_q2k.py / make_q3k.py / make_q50.py).
 
 * oracle (CPU): dequantize_row_q3_K bit-exact on synthetic and random-bit blocks; mul_mat at decode / small-batch /
   prefill shapes within 3e-6 of the output scale (a different fp32 summation order than ggml_vec_dot_q3_K_q8_K);
 * GPU: the SoA device layout round-trips and dequantizes bit-exactly; the generic mat-vec (kcpp_gemv), the fused
   decode mat-vec (kcpp_gemv_dec: plain + residual, SiLU-GLU, rms_norm prologue) and the MFMA GEMM (exact integer
-  f16 operands: Q3_K (sc - 32)(v - 4), Q2_K (sc & 15) q with the mins through the bsum MFMA) against the golden and
-  the oracle at 3e-6; a tiny Llama under the Q3_K_M / Q2_K policy end to end (prefill + teacher-forced decode, graph
+  f16 operands: Q3_K (sc - 32)(v - 4), Q2_K (sc & 15) q with the mins through the bsum MFMA, Q5_0 (q | h << 4) - 16) against the golden and
+  the oracle at 3e-6; a tiny Llama under the Q3_K_M / Q2_K / Q5_0 policy end to end (prefill + teacher-forced decode, graph
   and eager) within 1.5x the reference's AVX2-vs-scalar spread."""
 import os
 
@@ -16,7 +16,7 @@ import pytest
 
 import refharness as R
 
-KINDS = {"q3_k": (R.Q3_K, "q3k.npz"), "q2_k": (R.Q2_K, "q2k.npz")}
+KINDS = {"q3_k": (R.Q3_K, "q3k.npz"), "q2_k": (R.Q2_K, "q2k.npz"), "q5_0": (R.Q5_0, "q50.npz")}
 
 
 @pytest.fixture(scope="module", params=sorted(KINDS))
