@@ -79,7 +79,7 @@ KS_FN float ks_unit(uint64_t h) {            /* [0,1) */
 KS_FN int ks_block_elems(int type) {
     switch (type) {
         case KT_F32: case KT_F16: return 1;
-        case KT_Q4_0: case KT_Q5_0: case KT_Q8_0: return 32;
+        case KT_Q4_0: case KT_Q4_1: case KT_Q5_0: case KT_Q5_1: case KT_Q8_0: case KT_Q8_1: return 32;
         default: return 256;
     }
 }
@@ -88,7 +88,10 @@ KS_FN int ks_block_bytes(int type) {
         case KT_F32: return 4;
         case KT_F16: return 2;
         case KT_Q4_0: return 18;
+        case KT_Q4_1: return 20;
         case KT_Q5_0: return 22;
+        case KT_Q5_1: return 24;
+        case KT_Q8_1: return 36;
         case KT_Q8_0: return 34;
         case KT_Q2_K: return 84;
         case KT_Q3_K: return 110;
@@ -126,6 +129,12 @@ KS_FN void ks_fill_block(int type, uint64_t seed, uint64_t tid, uint64_t b, uint
             h0 = ks_f32_to_f16(0.0043f * (0.75f + 0.5f * u0));
             memcpy(dst, &h0, 2);
             break;
+        case KT_Q4_1: case KT_Q5_1: {   /* w = d q + m, q in 0..15 (0..31): mean -m/d-centred */
+            const float d = type == KT_Q4_1 ? 0.0043f : 0.00215f;
+            h0 = ks_f32_to_f16(d * (0.75f + 0.5f * u0));
+            h1 = ks_f32_to_f16(-(type == KT_Q4_1 ? 7.5f : 15.5f) * d * (0.9f + 0.2f * u1));
+            memcpy(dst, &h0, 2); memcpy(dst + 2, &h1, 2);
+        } break;
         case KT_Q5_0:       /* w = d ((q | h << 4) - 16), std ~9.2 d */
             h0 = ks_f32_to_f16(0.00215f * (0.75f + 0.5f * u0));
             memcpy(dst, &h0, 2);

@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(256) k_gemv(const uint8_t *__restrict__ W, con
     if (row0 >= N) return;
     const int64_t upr = K / E;
     const int64_t nb = K / ks_block_elems(TYPE) * N;
-    const int vt = (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;
+    const int vt = (TYPE == KT_Q4_1 || TYPE == KT_Q5_1) ? KT_Q8_1 : (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;
     constexpr int RR = MODE == 1 ? 2 : R;
     float acc[RR][NC];
 #pragma unroll
@@ -117,8 +117,8 @@ int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         }
         return 0;
     }
-    const int64_t E = (type == KT_Q4_0 || type == KT_Q5_0 || type == KT_Q8_0) ? 32 : 64;
-    if (K % (type == KT_Q4_0 || type == KT_Q5_0 || type == KT_Q8_0 ? 32 : 256) || K / E < 1) return -2;
+    const int64_t E = ks_block_elems(type) == 32 ? 32 : 64;
+    if (K % ks_block_elems(type) || K / E < 1) return -2;
 #define KCPP_T(T)                                                                   \
     case T:                                                                         \
         return mode == 1 ? launch_gemv_t<T, 1, 1>(W, W2, K, N, act, M, Mtot, c0, Y, ldy, res, ldr, s) \
@@ -131,6 +131,8 @@ int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         KCPP_T(KT_Q2_K)
         KCPP_T(KT_Q4_0)
         KCPP_T(KT_Q5_0)
+        KCPP_T(KT_Q4_1)
+        KCPP_T(KT_Q5_1)
         KCPP_T(KT_Q8_0)
     default: return -3;
     }

@@ -117,6 +117,28 @@ template <> struct Unit<KT_Q5_0> {
         d = *(const uint16_t *)(base + nb * 20 + b * 2);
     }
 };
+// ---- Q4_1 / Q5_1 (SoA): unit = one 32-elem block: 16 B nibbles (+ 4 B high bits) + fp16 (d, m)
+template <> struct Unit<KT_Q4_1> {
+    static constexpr int ELEMS = 32;
+    uint4 q;
+    uint32_t dm;
+    __device__ __forceinline__ void load(const uint8_t *base, int64_t nb, int64_t b0, int u) {
+        const int64_t b = b0 + u;
+        q = ld_nt((const void *)(base + b * 16));
+        dm = *(const uint32_t *)(base + nb * 16 + b * 4);
+    }
+};
+template <> struct Unit<KT_Q5_1> {
+    static constexpr int ELEMS = 32;
+    uint4 q;
+    uint32_t h, dm;
+    __device__ __forceinline__ void load(const uint8_t *base, int64_t nb, int64_t b0, int u) {
+        const int64_t b = b0 + u;
+        q = ld_nt((const void *)(base + b * 16));
+        h = *(const uint32_t *)(base + nb * 16 + b * 4);
+        dm = *(const uint32_t *)(base + nb * 20 + b * 4);
+    }
+};
 // ---- Q8_0 (SoA): unit = one 32-elem block: 32 B int8 + fp16 d
 template <> struct Unit<KT_Q8_0> {
     static constexpr int ELEMS = 32;
@@ -177,7 +199,18 @@ __device__ __forceinline__ void load_act0(const ActView &av, int u, Act0 &x) {
     x.s = av.bs[u];
 }
 
+// Activation unit for Q8_1 (Q4_1 / Q5_1 weights): the Q8_0 unit plus block_q8_1.s
+struct Act1 : Act0 {
+    float sf;
+};
+__device__ __forceinline__ void load_act(const ActView &av, int u, Act1 &x) {
+    load_act0(av, u, x);
+    x.sf = av.s[u];
+}
+
 template <int TYPE> struct ActOf { typedef ActK T; };
+template <> struct ActOf<KT_Q4_1> { typedef Act1 T; };
+template <> struct ActOf<KT_Q5_1> { typedef Act1 T; };
 template <> struct ActOf<KT_Q4_0> { typedef Act0 T; };
 template <> struct ActOf<KT_Q5_0> { typedef Act0 T; };
 template <> struct ActOf<KT_Q8_0> { typedef Act0 T; };
@@ -348,6 +381,20 @@ __device__ __forceinline__ float unit_dot(const Unit<KT_Q5_0> &w, int, const Act
     s -= 16 * x.s;
     return __fmul_rn((float)s, __fmul_rn(h2f(w.d), x.d));
 }
+
+// ggml_vec_dot_q4_1_q8_1 / _q5_1_q8_1 (ggml-quants.c:4503,5145): (d_w d_a) sum x a + m_w s_a, x = q (| h << 4)
+__device__ __forceinline__ float dot_q41(uint4 q, uint32_t h, uint32_t dm, const Act1 &x) {
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t v = u4(q, i);
+        s = sdot4((int)((v & 0x0F0F0F0Fu) | hbits4(h >> (4 * i))), u4(*(const uint4 *)&x.a[0], i), s);
+        s = sdot4((int)(((v >> 4) & 0x0F0F0F0Fu) | hbits4(h >> (16 + 4 * i))), u4(*(const uint4 *)&x.a[1], i), s);
+    }
+    return __fadd_rn(__fmul_rn(__fmul_rn(h2f((uint16_t)(dm & 0xFFFF)), x.d), (float)s), __fmul_rn(h2f((uint16_t)(dm >> 16)), x.sf));
+}
+__device__ __forceinline__ float unit_dot(const Unit<KT_Q4_1> &w, int, const Act1 &x) { return dot_q41(w.q, 0u, w.dm, x); }
+__device__ __forceinline__ float unit_dot(const Unit<KT_Q5_1> &w, int, const Act1 &x) { return dot_q41(w.q, w.h, w.dm, x); }
 
 __device__ __forceinline__ float unit_dot(const Unit<KT_Q8_0> &w, int, const Act0 &x) {
     int s = 0;

@@ -76,14 +76,17 @@ __host__ __device__ inline int64_t kl_nblocks(int type, int64_t K, int64_t N) {
 // Activation buffers (vec_dot_type of the weight; ggml.c:793-959):
 //   Q8_K act: qs int8 [M][K] ++ d f32 [M][K/256] ++ bsums int16 [M][K/16]
 //   Q8_0 act: qs int8 [M][K] ++ d f32 [M][K/32]  ++ asum  int16 [M][K/32]
+//   Q8_1 act: the Q8_0 act ++ s f32 [M][K/32] (block_q8_1.s = f16(d * sum qs), d before rounding; 4-B aligned)
 struct ActView {
     const int8_t *qs;
     const float *d;
     const int16_t *bs;
+    const float *s;
     int64_t K;
 };
 __host__ __device__ inline int64_t act_bytes(int vtype, int64_t K, int64_t M) {
     if (vtype == KT_Q8_K) return M * K + M * (K / 256) * 4 + M * (K / 16) * 2;
+    if (vtype == KT_Q8_1) return M * K + M * (K / 32) * 4 + ((M * (K / 32) * 2 + 3) & ~(int64_t)3) + M * (K / 32) * 4;
     return M * K + M * (K / 32) * 4 + M * (K / 32) * 2;
 }
 __host__ __device__ inline ActView act_view(int vtype, const void *buf, int64_t K, int64_t M, int64_t c) {
@@ -91,6 +94,9 @@ __host__ __device__ inline ActView act_view(int vtype, const void *buf, int64_t 
     ActView a;
     a.K = K;
     a.qs = base + c * K;
+    a.s = nullptr;
+    if (vtype == KT_Q8_1)
+        a.s = (const float *)(base + M * K + M * (K / 32) * 4 + ((M * (K / 32) * 2 + 3) & ~(int64_t)3)) + c * (K / 32);
     if (vtype == KT_Q8_K) {
         a.d = (const float *)(base + M * K) + c * (K / 256);
         a.bs = (const int16_t *)(base + M * K + M * (K / 256) * 4) + c * (K / 16);
@@ -101,6 +107,7 @@ __host__ __device__ inline ActView act_view(int vtype, const void *buf, int64_t 
     return a;
 }
 inline int vec_dot_type(int wtype) {
+    if (wtype == KT_Q4_1 || wtype == KT_Q5_1) return KT_Q8_1;
     return (wtype == KT_Q4_0 || wtype == KT_Q5_0 || wtype == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;
 }
 

@@ -36,6 +36,16 @@ __device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uin
         d[0] = src[0]; d[1] = src[1];
         for (int i = 0; i < 16; ++i) q[i] = src[2 + i];
     } break;
+    case KT_Q4_1: {   // SoA planes: qs [nb][16] ++ (d, m) [nb][4]  (block_q4_1: d, m, qs[16])
+        uint8_t *q = dst + b * 16, *dm = dst + nb * 16 + b * 4;
+        for (int i = 0; i < 4; ++i) dm[i] = src[i];
+        for (int i = 0; i < 16; ++i) q[i] = src[4 + i];
+    } break;
+    case KT_Q5_1: {   // SoA planes: qs [nb][16] ++ qh [nb][4] ++ (d, m) [nb][4]  (block_q5_1: d, m, qh[4], qs[16])
+        uint8_t *q = dst + b * 16, *h = dst + nb * 16 + b * 4, *dm = dst + nb * 20 + b * 4;
+        for (int i = 0; i < 4; ++i) { dm[i] = src[i]; h[i] = src[4 + i]; }
+        for (int i = 0; i < 16; ++i) q[i] = src[8 + i];
+    } break;
     case KT_Q5_0: {   // SoA planes: qs [nb][16] ++ qh [nb][4] ++ d [nb][2]  (block_q5_0: d, qh[4], qs[16])
         uint8_t *q = dst + b * 16, *h = dst + nb * 16 + b * 4, *d = dst + nb * 20 + b * 2;
         d[0] = src[0]; d[1] = src[1];
@@ -100,6 +110,16 @@ __device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint
         const uint8_t *q = src + b * 16, *d = src + nb * 16 + b * 2;
         blk[0] = d[0]; blk[1] = d[1];
         for (int i = 0; i < 16; ++i) blk[2 + i] = q[i];
+    } break;
+    case KT_Q4_1: {
+        const uint8_t *q = src + b * 16, *dm = src + nb * 16 + b * 4;
+        for (int i = 0; i < 4; ++i) blk[i] = dm[i];
+        for (int i = 0; i < 16; ++i) blk[4 + i] = q[i];
+    } break;
+    case KT_Q5_1: {
+        const uint8_t *q = src + b * 16, *h = src + nb * 16 + b * 4, *dm = src + nb * 20 + b * 4;
+        for (int i = 0; i < 4; ++i) { blk[i] = dm[i]; blk[4 + i] = h[i]; }
+        for (int i = 0; i < 16; ++i) blk[8 + i] = q[i];
     } break;
     case KT_Q5_0: {
         const uint8_t *q = src + b * 16, *h = src + nb * 16 + b * 4, *d = src + nb * 20 + b * 2;
@@ -200,6 +220,17 @@ __device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t bpr,
             o[j + 16] = ((blk[2 + j] >> 4) - 8) * d;
         }
     } break;
+    case KT_Q4_1: case KT_Q5_1: {   // dequantize_row_q4_1 / _q5_1, ggml-quants.c:1543-1616 (x d + m, two roundings)
+        const float d = h2f(blk[0] | (blk[1] << 8)), m = h2f(blk[2] | (blk[3] << 8));
+        const bool five = type == KT_Q5_1;
+        const uint32_t qh = five ? (blk[4] | (blk[5] << 8) | (blk[6] << 16) | ((uint32_t)blk[7] << 24)) : 0u;
+        const uint8_t *qs = blk + (five ? 8 : 4);
+        for (int j = 0; j < 16; ++j) {
+            const int x0 = (qs[j] & 0x0F) | (((qh >> j) << 4) & 0x10), x1 = (qs[j] >> 4) | ((qh >> (j + 12)) & 0x10);
+            o[j] = __fadd_rn(__fmul_rn((float)x0, d), m);
+            o[j + 16] = __fadd_rn(__fmul_rn((float)x1, d), m);
+        }
+    } break;
     case KT_Q5_0: {   // dequantize_row_q5_0, ggml-quants.c:1564-1588
         const float d = h2f(blk[0] | (blk[1] << 8));
         const uint32_t qh = blk[2] | (blk[3] << 8) | (blk[4] << 16) | ((uint32_t)blk[5] << 24);
@@ -287,6 +318,14 @@ __device__ __forceinline__ float deq_elem(int type, const uint8_t *src, int64_t 
         const float d = h2f(*(const uint16_t *)(src + nb * 16 + b * 2));
         const uint8_t q = src[b * 16 + (e & 15)];
         return ((e < 16 ? (q & 0xF) : (q >> 4)) - 8) * d;
+    }
+    case KT_Q4_1: case KT_Q5_1: {
+        const bool five = type == KT_Q5_1;
+        const uint32_t dm = *(const uint32_t *)(src + nb * (five ? 20 : 16) + b * 4);
+        const uint8_t q = src[b * 16 + (e & 15)];
+        const uint32_t qh = five ? *(const uint32_t *)(src + nb * 16 + b * 4) : 0u;
+        const int x = (int)((e < 16 ? (q & 0xF) : (q >> 4)) | (((qh >> e) & 1) << 4));
+        return __fadd_rn(__fmul_rn((float)x, h2f((uint16_t)(dm & 0xFFFF))), h2f((uint16_t)(dm >> 16)));
     }
     case KT_Q5_0: {
         const float d = h2f(*(const uint16_t *)(src + nb * 20 + b * 2));
@@ -383,6 +422,8 @@ __global__ void __launch_bounds__(256) k_quant_q8k(const float *__restrict__ x, 
 }
 
 // Q8_0 (AVX2 semantics): 8 lanes per 32-block, 4 elements per lane.
+// S1: Q8_1 (quantize_row_q8_1's AVX2 branch, ggml-quants.c:1280-1330): the same qs / d plus s = f16(d * sum qs)
+template <bool S1>
 __global__ void k_quant_q80(const float *__restrict__ x, int64_t ldx, uint8_t *__restrict__ out, int64_t K, int64_t M) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nb = K / 32;
@@ -415,6 +456,13 @@ __global__ void k_quant_q80(const float *__restrict__ x, int64_t ldx, uint8_t *_
     if (sub == 0) {
         ((float *)(out + M * K))[m * nb + ib] = h2f(f2h(d));        // the dot uses GGML_FP16_TO_FP32(y.d)
         ((int16_t *)(out + M * K + M * nb * 4))[m * nb + ib] = (int16_t)s;
+        if constexpr (S1) {
+            // the f32 product, rounded, THEN f16: without the barrier the compiler folds mul + cvt into one
+            // v_fma_mix (a single rounding of the exact product), which differs from the CPU on f16 ties
+            float p = __fmul_rn(d, (float)s);
+            asm volatile("" : "+v"(p));
+            ((float *)(out + M * K + M * nb * 4 + ((M * nb * 2 + 3) & ~(int64_t)3)))[m * nb + ib] = h2f(f2h(p));
+        }
     }
 }
 
@@ -461,7 +509,12 @@ int kcpp_quantize_act(int vtype, const float *x, int64_t ldx, void *out, int64_t
     } else if (vtype == KT_Q8_0) {
         if (K % 32) return -1;
         const int64_t nthreads = K / 32 * M * 8;
-        hipLaunchKernelGGL(k_quant_q80, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+        hipLaunchKernelGGL(k_quant_q80<false>, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
+                           ldx, (uint8_t *)out, K, M);
+    } else if (vtype == KT_Q8_1) {
+        if (K % 32) return -1;
+        const int64_t nthreads = K / 32 * M * 8;
+        hipLaunchKernelGGL(k_quant_q80<true>, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
                            ldx, (uint8_t *)out, K, M);
     } else {
         return -2;

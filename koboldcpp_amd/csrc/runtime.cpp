@@ -16,6 +16,7 @@
 // id are read from device memory, so one graph serves every position).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -124,6 +125,7 @@ struct kcpp_model {
     float *logits_pin = nullptr;
     bool use_graphs = true;
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
+    bool q81 = false;                // Q4_1 / Q5_1 weights (Q8_1 activations): single-token decode on the per-op path
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
     int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
     hipGraphExec_t g_exec = nullptr;
@@ -280,6 +282,8 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
         m->types[idx] = t;
     }
     types = m->types.data();
+    for (int idx = 0; idx < n_tensors(*hp); ++idx) m->q81 |= types[idx] == KT_Q4_1 || types[idx] == KT_Q5_1;
+    if (m->q81 && hp->n_expert > 0) { g_err = "Q4_1 / Q5_1 MoE models are not supported"; delete m; return nullptr; }
     m->device = device; m->il0 = il0; m->il1 = il1; m->has_embed = has_embed; m->has_output = has_output;
     m->ub = max_ubatch > 0 ? max_ubatch : 512;
     m->fa_exact = getenv("KCPP_FA_EXACT") && atoi(getenv("KCPP_FA_EXACT")) != 0;
@@ -333,7 +337,8 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
         hipMemset(L.kc, 0, kvb); hipMemset(L.vc, 0, kvb);
     }
     // activation buffers sized for the widest vec_dot input (K = F) at UB columns
-    m->act_sz = (size_t)std::max(kcpp_act_bytes(KT_Q4_K, std::max(E, F), UB), kcpp_act_bytes(KT_Q8_0, std::max(E, F), UB));
+    m->act_sz = (size_t)std::max({kcpp_act_bytes(KT_Q4_K, std::max(E, F), UB), kcpp_act_bytes(KT_Q8_0, std::max(E, F), UB),
+                                  kcpp_act_bytes(KT_Q4_1, std::max(E, F), UB)});
     m->gemm_ws_sz = 0;
     for (int idx = 0; idx < n_tensors(*hp); ++idx) {
         int64_t K, N; shape_of(*hp, idx, K, N);
@@ -452,7 +457,8 @@ static int upload(int dev, hipStream_t s, int type, int64_t K, int64_t N, int sl
     if (!slice_bytes) slice_bytes = bytes;
     if (bytes == 0) return 0;
     RT_CHECK(hipSetDevice(dev));
-    if (type == KT_Q6_K || type == KT_Q3_K || type == KT_Q2_K || type == KT_Q4_0 || type == KT_Q5_0 || type == KT_Q8_0 || type == KT_Q4_K_RS ||
+    if (type == KT_Q6_K || type == KT_Q3_K || type == KT_Q2_K || type == KT_Q4_0 || type == KT_Q4_1 || type == KT_Q5_0 || type == KT_Q5_1 || type == KT_Q8_0 ||
+        type == KT_Q4_K_RS ||
         type == KT_Q6_K_RS) {
         void *stage = nullptr;
         RT_CHECK(hipMalloc(&stage, bytes));
@@ -1056,7 +1062,7 @@ static int decode_step_dev(kcpp_model *m) {
     if (m->has_embed)
         RC(kcpp_get_rows(m->tok_embd.type, m->tok_embd.d, hp.n_embd, hp.n_vocab, m->tok_dev, 1, m->x, hp.n_embd,
                          m->stream));
-    if (m->fused_decode && m->kv_tk == KT_F16) {
+    if (m->fused_decode && m->kv_tk == KT_F16 && !m->q81) {
         RC(forward_layers_dec(m));
         if (m->has_output) RC(head_dec(m));
     } else {

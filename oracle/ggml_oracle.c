@@ -19,6 +19,9 @@
 
 typedef struct { uint16_t d; uint8_t qs[16]; } blk_q4_0;                  /* ggml-common.h:144 */
 typedef struct { uint16_t d; uint8_t qh[4]; uint8_t qs[16]; } blk_q5_0;   /* ggml-common.h:161 */
+typedef struct { uint16_t d, m; uint8_t qs[16]; } blk_q4_1;               /* ggml-common.h:149 */
+typedef struct { uint16_t d, m; uint8_t qh[4]; uint8_t qs[16]; } blk_q5_1; /* ggml-common.h:168 */
+typedef struct { uint16_t d, s; int8_t qs[32]; } blk_q8_1;                 /* ggml-common.h:193 */
 typedef struct { uint16_t d; int8_t qs[32]; } blk_q8_0;                   /* ggml-common.h:186 */
 typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qs[128]; } blk_q4_K;   /* :286 */
 typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qh[32]; uint8_t qs[128]; } blk_q5_K; /* :303 */
@@ -29,6 +32,7 @@ typedef struct { float d; int8_t qs[256]; int16_t bsums[16]; } blk_q8_K;  /* :33
 
 _Static_assert(sizeof(blk_q4_0) == 18, "q4_0");
 _Static_assert(sizeof(blk_q5_0) == 22, "q5_0");
+_Static_assert(sizeof(blk_q4_1) == 20 && sizeof(blk_q5_1) == 24 && sizeof(blk_q8_1) == 36, "q4_1 / q5_1 / q8_1");
 _Static_assert(sizeof(blk_q8_0) == 34, "q8_0");
 _Static_assert(sizeof(blk_q4_K) == 144, "q4_K");
 _Static_assert(sizeof(blk_q5_K) == 176, "q5_K");
@@ -79,6 +83,28 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
             for (int j = 0; j < 16; ++j) {
                 y[i * 32 + j] = ((x[i].qs[j] & 0x0F) - 8) * d;
                 y[i * 32 + j + 16] = ((x[i].qs[j] >> 4) - 8) * d;
+            }
+        }
+    } return;
+    case KT_Q4_1: {                                   /* ggml-quants.c:1543-1562 */
+        const blk_q4_1 *x = vx;
+        for (int64_t i = 0; i < k / 32; ++i) {
+            const float d = H2F(x[i].d), m = H2F(x[i].m);
+            for (int j = 0; j < 16; ++j) {
+                y[i * 32 + j] = (x[i].qs[j] & 0x0F) * d + m;
+                y[i * 32 + j + 16] = (x[i].qs[j] >> 4) * d + m;
+            }
+        }
+    } return;
+    case KT_Q5_1: {                                   /* ggml-quants.c:1590-1616 */
+        const blk_q5_1 *x = vx;
+        for (int64_t i = 0; i < k / 32; ++i) {
+            const float d = H2F(x[i].d), m = H2F(x[i].m);
+            uint32_t qh;
+            memcpy(&qh, x[i].qh, 4);
+            for (int j = 0; j < 16; ++j) {
+                y[i * 32 + j] = ((x[i].qs[j] & 0x0F) | (((qh >> j) << 4) & 0x10)) * d + m;
+                y[i * 32 + j + 16] = ((x[i].qs[j] >> 4) | ((qh >> (j + 12)) & 0x10)) * d + m;
             }
         }
     } return;
@@ -211,6 +237,7 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
 int orc_vec_dot_type(int wtype) {
     switch (wtype) {
         case KT_Q4_0: case KT_Q5_0: case KT_Q8_0: return KT_Q8_0;
+        case KT_Q4_1: case KT_Q5_1: return KT_Q8_1;
         case KT_Q2_K: case KT_Q3_K: case KT_Q4_K: case KT_Q5_K: case KT_Q6_K: return KT_Q8_K;
         case KT_F16: return KT_F16;
         default: return KT_F32;
@@ -269,6 +296,22 @@ void orc_quantize_row_q8_0(const float *x, void *vy, int64_t k) {
     }
 }
 
+/* quantize_row_q8_1 (AVX2 branch, ggml-quants.c:1280-1330): the Q8_0 quantization plus s = f16(d * sum qs), d unrounded */
+void orc_quantize_row_q8_1(const float *x, void *vy, int64_t k) {
+    blk_q8_1 *y = vy;
+    for (int64_t i = 0; i < k / 32; ++i) {
+        blk_q8_0 b;
+        orc_quantize_row_q8_0(x + i * 32, &b, 32);
+        float amax = 0;
+        for (int j = 0; j < 32; ++j) { float a = fabsf(x[i * 32 + j]); amax = a > amax ? a : amax; }
+        const float d = amax / 127.f;
+        int sum = 0;
+        for (int j = 0; j < 32; ++j) { y[i].qs[j] = b.qs[j]; sum += b.qs[j]; }
+        y[i].d = b.d;
+        y[i].s = F2H(d * (float)sum);
+    }
+}
+
 /* quantize_row_q4_0_ref, ggml-quants.c:669-704 (quantize_row_q4_0 calls it, :707) */
 void orc_quantize_row_q4_0(const float *x, void *vy, int64_t k) {
     blk_q4_0 *y = vy;
@@ -295,6 +338,7 @@ void orc_quantize_row(int vtype, const float *x, void *y, int64_t k) {
         case KT_Q4_0: orc_quantize_row_q4_0(x, y, k); break;
         case KT_Q8_K: orc_quantize_row_q8_K(x, y, k); break;
         case KT_Q8_0: orc_quantize_row_q8_0(x, y, k); break;
+        case KT_Q8_1: orc_quantize_row_q8_1(x, y, k); break;
         case KT_F16: { uint16_t *h = y; for (int64_t i = 0; i < k; ++i) h[i] = F2H(x[i]); } break;
         case KT_F32: memcpy(y, x, k * 4); break;
         default: abort();
@@ -465,6 +509,34 @@ static float dot_q5_0(int n, const blk_q5_0 *x, const blk_q8_0 *y) {       /* :4
     return sumf;
 }
 
+static float dot_q4_1(int n, const blk_q4_1 *x, const blk_q8_1 *y) {       /* :4503, scalar tail */
+    float sumf = 0;
+    for (int ib = 0; ib < n / 32; ++ib) {
+        int s0 = 0, s1 = 0;
+        for (int j = 0; j < 16; ++j) {
+            s0 += (x[ib].qs[j] & 0x0F) * y[ib].qs[j];
+            s1 += (x[ib].qs[j] >> 4) * y[ib].qs[j + 16];
+        }
+        sumf += (H2F(x[ib].d) * H2F(y[ib].d)) * (s0 + s1) + H2F(x[ib].m) * H2F(y[ib].s);
+    }
+    return sumf;
+}
+
+static float dot_q5_1(int n, const blk_q5_1 *x, const blk_q8_1 *y) {       /* :5145, scalar tail */
+    float sumf = 0;
+    for (int ib = 0; ib < n / 32; ++ib) {
+        uint32_t qh;
+        memcpy(&qh, x[ib].qh, 4);
+        int s0 = 0, s1 = 0;
+        for (int j = 0; j < 16; ++j) {
+            s0 += ((x[ib].qs[j] & 0x0F) | (((qh >> j) << 4) & 0x10)) * y[ib].qs[j];
+            s1 += ((x[ib].qs[j] >> 4) | ((qh >> (j + 12)) & 0x10)) * y[ib].qs[j + 16];
+        }
+        sumf += (H2F(x[ib].d) * H2F(y[ib].d)) * (s0 + s1) + H2F(x[ib].m) * H2F(y[ib].s);
+    }
+    return sumf;
+}
+
 static float dot_q8_0(int n, const blk_q8_0 *x, const blk_q8_0 *y) {       /* :5519, scalar tail */
     float sumf = 0;
     for (int ib = 0; ib < n / 32; ++ib) {
@@ -490,6 +562,8 @@ float orc_vec_dot(int wtype, int n, const void *w, const void *a) {
         case KT_Q2_K: return dot_q2_K(n, w, a);
         case KT_Q4_0: return dot_q4_0(n, w, a);
         case KT_Q5_0: return dot_q5_0(n, w, a);
+        case KT_Q4_1: return dot_q4_1(n, w, a);
+        case KT_Q5_1: return dot_q5_1(n, w, a);
         case KT_Q8_0: return dot_q8_0(n, w, a);
         case KT_F16: return dot_f16(n, w, a);
         case KT_F32: { const float *x = w, *y = a; double s = 0; for (int i = 0; i < n; ++i) s += x[i] * y[i]; return (float)s; }

@@ -14,8 +14,8 @@ REF_BIN = os.path.join(ROOT, "oracle", "_ref", "ref_llama")
 REF_BIN_SCALAR = os.path.join(ROOT, "oracle", "_ref", "scalar", "ref_llama")   # no-SIMD build (make ref_scalar)
 
 # ggml_type ids (ggml/include/ggml.h:364-399)
-F32, F16, Q4_0, Q5_0, Q8_0, Q2_K, Q3_K, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 6, 8, 10, 11, 12, 13, 14, 15
-BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q5_0: (32, 22), Q8_0: (32, 34), Q2_K: (256, 84), Q3_K: (256, 110), Q4_K: (256, 144),
+F32, F16, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q3_K, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 3, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15
+BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q4_1: (32, 20), Q5_0: (32, 22), Q5_1: (32, 24), Q8_0: (32, 34), Q8_1: (32, 36), Q2_K: (256, 84), Q3_K: (256, 110), Q4_K: (256, 144),
          Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292)}
 
 
@@ -296,6 +296,16 @@ def q5_0_types(n_layer):
     """LLAMA_FTYPE_MOSTLY_Q5_0 (llama_tensor_get_type, src/llama.cpp:17979-18208): Q5_0 everywhere (token_embd too),
     output Q6_K"""
     return uniform_types(n_layer, Q5_0, Q6_K)
+
+
+def q4_1_types(n_layer):
+    """LLAMA_FTYPE_MOSTLY_Q4_1: Q4_1 everywhere, output Q6_K"""
+    return uniform_types(n_layer, Q4_1, Q6_K)
+
+
+def q5_1_types(n_layer):
+    """LLAMA_FTYPE_MOSTLY_Q5_1: Q5_1 everywhere, output Q6_K"""
+    return uniform_types(n_layer, Q5_1, Q6_K)
 
 
 def q3_k_m_types(n_layer):
