@@ -101,19 +101,24 @@ def measure_roofline(K, torch, iters=64, pairs=8):
             "avg_us": round(ms * 1e3, 2)}
 
 
-def cpu_baseline(hp, types, threads, n_prompt=512, n_gen=16, threads2=8):
-    """The REFERENCE ggml CPU build on the same synthetic weights, koboldcpp --benchmark semantics, on a bounded
-    sample: a 512-token prompt (one ubatch) then 16 greedy tokens at context 512..527 (the GPU line decodes at
-    ~3.85k; the CPU cannot prefill 3840 tokens in a bounded run).  `threads` = the box's CPU share (16 on the GPU
-    box, OMP_NUM_THREADS), plus a second run at 8 threads for comparability."""
+def cpu_baseline(hp, types, threads, depth=3840, n_ub=512, n_gen=16, threads2=8):
+    """The REFERENCE ggml CPU build on the same synthetic weights, koboldcpp --benchmark semantics, on bounded samples:
+    (1) at the GPU line's context depth: the prompt's last ubatch (positions depth-512..depth-1, attending over the
+    whole prefix) and then n_gen greedy tokens at context depth..depth+n_gen; the earlier prompt positions are taken
+    as already cached (zeroed K/V, not computed: REF_SKIP_PREFIX in oracle/ref_llama.c) since a step's cost depends
+    on the cache length, not its contents; `threads` = the box's CPU share (16, OMP_NUM_THREADS);
+    (2) a 512-token prompt from position 0 and n_gen tokens at context 512..527 at 8 threads."""
     import refharness as R
     if not R.ref_available():
         return None
-    prompt = [16 + (i % 2) for i in range(n_prompt)]     # " 1" style repeated ids
+    prompt = [16 + (i % 2) for i in range(depth)]     # " 1" style repeated ids
     hp2 = dict(hp)
-    hp2["n_ctx"] = n_prompt + n_gen + 8
-    _, info = R.run_ref_llama(hp2, types, 1234, prompt, n_gen, nthreads=threads, ubatch=512, timeout=900)
-    _, info2 = R.run_ref_llama(hp2, types, 1234, prompt, n_gen, nthreads=threads2, ubatch=512, timeout=900)
+    hp2["n_ctx"] = depth + n_gen + 8
+    _, info = R.run_ref_llama(hp2, types, 1234, prompt, n_gen, nthreads=threads, ubatch=n_ub, timeout=900,
+                              skip_prefix=depth - n_ub)
+    hp3 = dict(hp)
+    hp3["n_ctx"] = n_ub + n_gen + 8
+    _, info2 = R.run_ref_llama(hp3, types, 1234, prompt[:n_ub], n_gen, nthreads=threads2, ubatch=n_ub, timeout=900)
     cpu = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -123,13 +128,15 @@ def cpu_baseline(hp, types, threads, n_prompt=512, n_gen=16, threads2=8):
     return {"value": round(n_gen / info["decode_s"], 3), "unit": "tok/s (decode)", "cores": threads,
             "cpu_model": cpu, "host_cpus": os.cpu_count(),
             "kind": "reference",
-            "prefill_tok_s": round(n_prompt / info["prefill_s"], 3),
-            "context_depth": [n_prompt, n_prompt + n_gen],
-            "at_%d_threads" % threads2: {"decode_tok_s": round(n_gen / info2["decode_s"], 3),
-                                         "prefill_tok_s": round(n_prompt / info2["prefill_s"], 3)},
-            "sample": "reference ggml CPU (oracle/_ref/ref_llama, built from the reference sources) on the same "
-                      "synthetic Llama-3-8B Q4_K_M: %d-token prefill then %d greedy decode tokens at context %d-%d, "
-                      "%d threads (and %d)" % (n_prompt, n_gen, n_prompt, n_prompt + n_gen, threads, threads2)}
+            "context_depth": [depth, depth + n_gen],
+            "prefill_tok_s_last_ubatch": round(n_ub / info["prefill_s"], 3),
+            "at_%d_threads_ctx_%d" % (threads2, n_ub): {"decode_tok_s": round(n_gen / info2["decode_s"], 3),
+                                                       "prefill_tok_s": round(n_ub / info2["prefill_s"], 3)},
+            "sample": "reference ggml CPU (oracle/_ref/ref_llama, built from the reference sources) on the same synthetic "
+                      "Llama-3-8B Q4_K_M: the prompt's last %d-token ubatch at positions %d-%d (prefix cached, not "
+                      "computed) then %d greedy decode tokens at context %d-%d, %d threads; and a %d-token prompt + %d "
+                      "tokens from position 0 at %d threads" % (n_ub, depth - n_ub, depth - 1, n_gen, depth, depth + n_gen,
+                                                                threads, n_ub, n_gen, threads2)}
 
 
 def run_model(K, torch, hp, types, n_prompt, ubatch, steps, warmup):
@@ -237,11 +244,25 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_dev = max(args.gpus, world)
+    if n_dev > 1 and torch.cuda.device_count() < n_dev:     # device_count does not initialise the GPU here
+        raise SystemExit("bench.py: --gpus %d but %d GPU(s) visible" % (n_dev, torch.cuda.device_count()))
     if world > 1:
-        from koboldcpp_amd import pipeline
-        return pipeline.bench_main(args, world, rank, local)
+        # launched by torchrun: the multi-GPU path is the in-process engine on rank 0 over all world GPUs (what
+        # load_model ships); the other ranks touch no GPU and only bracket the run with (gloo) barriers, so the
+        # max-over-ranks time is rank 0's
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        dist.barrier()
+        if rank == 0:
+            run_bench(args, K, torch, n_dev)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
+    run_bench(args, K, torch, n_dev)
 
+
+def run_bench(args, K, torch, n_dev):
     torch.cuda.set_device(0)
     if args.roofline_only:
         print(json.dumps({"roofline": measure_roofline(K, torch)}))
@@ -253,7 +274,23 @@ def main():
     if args.layers:
         hp["n_layer"] = args.layers
     types = q4_k_m_types(hp["n_layer"])
-    r = run_model(K, torch, hp, types, args.prompt, args.ubatch, args.steps, args.warmup)
+    if n_dev == 1:
+        r = run_model(K, torch, hp, types, args.prompt, args.ubatch, args.steps, args.warmup)
+        par = "single GPU"
+    else:
+        # the drop-in engine load_model ships (koboldcpp_amd/csrc/expose.cpp): n_dev layer-split stages in this one
+        # process, RCCL send/recv hand-off between the stage streams, pipelined prefill ubatches, generate()'s greedy
+        # loop (argmax on the last stage, token back to stage 0 through the host)
+        steps = min(args.steps, hp["n_ctx"] - args.prompt - args.warmup - 1)
+        e = K.engine_bench(hp, types, n_dev, args.prompt, args.ubatch, args.warmup, steps)
+        r = {"dec": steps / e["decode_s"], "pre": args.prompt / e["prefill_s"], "t_pp": e["prefill_s"],
+             "ms_step": e["decode_s"] / steps * 1e3, "steps": steps, "n_past": e["n_past"], "wb": weight_bytes(hp, types)}
+        par = "layer split over %d GPUs (tensor_split 1:...:1), %s hand-off, one process" % (
+            n_dev, "RCCL send/recv" if e["rccl"] else "event-ordered peer copy")
+    print(json.dumps(bench_line(args, K, torch, hp, types, r, n_dev, par)))
+
+
+def bench_line(args, K, torch, hp, types, r, n_dev, par):
     dec, pre, ms_step, steps, n_past, wb, t_pp = r["dec"], r["pre"], r["ms_step"], r["steps"], r["n_past"], r["wb"], r["t_pp"]
     # decode roofline over the whole token (B(p) = weights read per token + KV at the mean
     # position; token_embd is a 1-row gather, not streamed, so it is excluded)
@@ -272,28 +309,29 @@ def main():
     roof = measure_roofline(K, torch)
     out = {
         "metric": "decode tok/s (Llama-3-8B Q4_K_M, 4k ctx); prefill tok/s in prefill_tok_s",
-        "value": round(dec, 2), "unit": "tok/s", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
+        "value": round(dec, 2), "unit": "tok/s", "n_gpus": n_dev, "steps": steps, "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
         "dtype": "q4_K/q6_K weights x q8_K activations (int8 dot, f32 accum); f16 KV", "data": "synthetic",
         "config": {"workload": "llama3-8b-q4_k_m ctx4096: prefill %d (ubatch %d) + greedy decode" % (args.prompt, args.ubatch),
                    "model": "Llama-3-8B-shape Q4_K_M random-init", "n_layer": hp["n_layer"],
                    "prompt_tokens": args.prompt, "gen_positions": [args.prompt + args.warmup, n_past],
-                   "parallelism": "single GPU"},
+                   "parallelism": par},
         "prefill_tok_s": round(pre, 1), "prefill_s": round(t_pp, 4),
-        "decode_effective_GBps": round(token_gbs, 1), "decode_hbm_frac": round(token_gbs / HBM_PEAK_GBS, 4),
+        "decode_effective_GBps": round(token_gbs, 1), "decode_hbm_frac": round(token_gbs / HBM_PEAK_GBS, 4),   # one stage streams at a time
         "decode_bytes_per_token": int(wb - embd_bytes + kv_bytes),
         "weight_bytes_resident": wb,
         "roofline": roof,
-        "prefill_roofline": {"bound": "mfma", "achieved": round(pre_tflops, 1), "peak": MFMA_F16_PEAK_TFLOPS,
-                             "unit": "TFLOP/s", "frac": round(pre_tflops / MFMA_F16_PEAK_TFLOPS, 4),
-                             "flops": int(pre_flops), "scope": "whole prefill (all kernels), F(n) of SURVEY.md 8d"},
+        "prefill_roofline": {"bound": "mfma", "achieved": round(pre_tflops, 1), "peak": MFMA_F16_PEAK_TFLOPS * n_dev,
+                             "unit": "TFLOP/s", "frac": round(pre_tflops / MFMA_F16_PEAK_TFLOPS / n_dev, 4),
+                             "flops": int(pre_flops), "scope": "whole prefill (all kernels), F(n) of SURVEY.md 8d; "
+                                                               "peak = %d GPU(s)" % n_dev},
     }
     if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(hp, types, args.cpu_threads)
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"error": str(e)[:300]}
-    print(json.dumps(out))
+    return out
 
 
 if __name__ == "__main__":

@@ -303,6 +303,12 @@ int kcpp_model_set_row_split(kcpp_model *m, int n, const int *devices, const flo
 /* the row range [lo, hi) of an nrows matrix on device id of n (host only; get_row_split, ggml-cuda.cu:638-651) */
 int kcpp_row_split_range(int64_t nrows, int n, const float *tensor_split, int id, int64_t *lo, int64_t *hi);
 int64_t kcpp_model_weight_bytes(kcpp_model *m);
+/* bench.py --gpus N: the drop-in engine of load_model (layer-split stages over n_dev GPUs by tensor_split, RCCL or
+ * event-ordered hand-off, pipelined ubatches: koboldcpp_amd/csrc/expose.cpp) on synthetic weights: prefill n_prompt
+ * ids in ubatches of ub, then n_warm + n_steps greedy tokens as generate() runs them.  out = {prefill_s, decode_s of
+ * the n_steps tokens, n_past at the end, 1 if the hand-off ran on RCCL}.  0 ok, -1 fewer than n_dev GPUs visible. */
+int kcpp_engine_bench(const kcpp_hparams *hp, const int *types, int n_types, int n_dev, const float *tensor_split,
+                      uint64_t seed, int n_prompt, int ub, int n_warm, int n_steps, double *out);
 const char *kcpp_last_error(void);
 
 /* GGUF parse + tensor-table bounds validation alone (load_model's first step): 0 ok, -1 with the reason in err */
@@ -313,6 +319,9 @@ int kcpp_gguf_check(const char *path, char *err, int err_len);
  * tokenizer_st_partition src/llama-vocab.cpp:1544).  Return the count, -1 on error. */
 int kcpp_pretokenize(const char *pre, const char *text, int64_t *ends, int cap);
 int kcpp_tokenize_probe(const char *gguf_path, const char *text, int add_bos, int32_t *out, int cap);
+/* the vocabulary's special ids as generate() uses them: out = {bos, eos, eot} (eot -1 when the vocabulary has none;
+ * llm_load_vocab's EOT detection, src/llama.cpp:6606, 6642-6661).  0 ok, -1 on a load error */
+int kcpp_tokenizer_special_ids(const char *gguf_path, int32_t *out);
 /* generate()'s restated sampler chain (SampleLogits, gpttype_adapter.cpp:1338-1434) on caller logits, for the
  * host-side parity test (koboldcpp_amd/csrc/expose.cpp documents fp / ip / restarts); returns the drawn token */
 int kcpp_sampler_probe(const float *logits, int n_vocab, int n_ctx, const float *fp, const int *ip, const int *order,

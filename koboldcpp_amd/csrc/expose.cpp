@@ -201,6 +201,58 @@ bool init_handoff(Engine &e) {
     return true;
 }
 
+// the stages of a model over ndev (possibly virtual) devices, nreal of them real: layer split exactly as
+// llm_load_tensors (src/llama.cpp:7000-7036), or one row-split stage (LLAMA_SPLIT_MODE_ROW) on the main device
+bool build_stages(Engine &e, int ndev, int nreal, const float *tensor_split, bool rowsplit, int main_gpu) {
+    const kcpp_hparams &hp = e.hp;
+    const std::vector<int> ldev = split_layers(hp.n_layer, std::min(ndev, KCPP_TENSOR_SPLIT_MAX), tensor_split);
+    int il = 0;
+    // stages of consecutive layers per device; the output head on its own device (upper_bound of
+    // (act - 1) / act, src/llama.cpp:7030-7033) -- a head-only stage when that is not the last layers' device
+    auto add_stage = [&](int d, int i0, int i1, bool out) {
+        const int gpu = d % nreal;
+        kcpp_model *m = kcpp_model_create(&hp, e.types.data(), gpu, i0, i1, e.stages.empty(), out, e.ub);
+        if (!m) { fprintf(stderr, "[kcpp] load_model: %s\n", kcpp_last_error()); return false; }
+        e.stages.push_back(m);
+        e.hidden.push_back(kcpp_model_hidden(m));
+        e.devs.push_back(gpu);
+        if (e.stages.size() > 1 && e.devs[e.devs.size() - 2] != gpu) {
+            hipSetDevice(gpu);
+            hipDeviceEnablePeerAccess(e.devs[e.devs.size() - 2], 0);   // xGMI peer copies for the handoff
+            (void)hipGetLastError();
+        }
+        return true;
+    };
+    if (rowsplit && std::min(ndev, KCPP_TENSOR_SPLIT_MAX) > 1) {
+        // LLAMA_SPLIT_MODE_ROW (gpttype_adapter.cpp:1892): one stage on the main device (cublas_info,
+        // gpttype_adapter.cpp:1708) owning every layer; the matrices' rows spread over the devices by tensor_split
+        const int nd = std::min(ndev, KCPP_TENSOR_SPLIT_MAX);
+        const int main_dev = std::min(main_gpu <= 0 ? 0 : main_gpu, nd - 1) % nreal;
+        std::vector<int> devs(nd);
+        for (int i = 0; i < nd; ++i) devs[i] = i % nreal;
+        kcpp_model *m = kcpp_model_create(&hp, e.types.data(), main_dev, 0, hp.n_layer, 1, 1, e.ub);
+        if (!m) { fprintf(stderr, "[kcpp] load_model: %s\n", kcpp_last_error()); return false; }
+        e.stages.push_back(m);
+        e.hidden.push_back(kcpp_model_hidden(m));
+        e.devs.push_back(main_dev);
+        if (kcpp_model_set_row_split(m, nd, devs.data(), tensor_split)) {
+            fprintf(stderr, "[kcpp] load_model: row split: %s\n", kcpp_last_error());
+            return false;
+        }
+        il = hp.n_layer;
+    }
+    while (il < hp.n_layer) {
+        const int d = ldev[il];
+        int il1 = il;
+        while (il1 < hp.n_layer && ldev[il1] == d) ++il1;
+        const bool last = il1 == hp.n_layer;
+        if (!add_stage(d, il, il1, last && ldev[hp.n_layer] == d)) return false;
+        if (last && ldev[hp.n_layer] != d && !add_stage(ldev[hp.n_layer], hp.n_layer, hp.n_layer, true)) return false;
+        il = il1;
+    }
+    return true;
+}
+
 // per-generate sampler state: the reference's parameter clamps (gpttype_adapter.cpp:2576-2584, 2625-2735),
 // sampler order (:2957-2976), DRY restart sequences (:2650-2700), single-character token bans (:2518-2568)
 struct SamplerSetup {
@@ -313,17 +365,19 @@ bool chain_is_argmax(const SamplerSetup &S) {
 // one sampled token from the last stage's logits (gpttype_adapter.cpp:3182-3232); < 0 on a device error
 int sample(Engine &e, const SamplerSetup &S, const std::vector<int> &last_n, std::mt19937 &rng, float *mu) {
     kcpp_model *last = e.stages.back();
-    const int eos = e.tok.eos();
+    const int eos = e.tok.eos(), eot = e.tok.eot();
     if (chain_is_argmax(S)) {
         int32_t t = 0;
         if (kcpp_model_argmax(last, &t)) return -1;
-        if (!(S.suppress_eos && t == eos)) return t;
+        if (!(S.suppress_eos && (t == eos || (t == eot && eot != -1)))) return t;
     }
     e.logits.resize(e.hp.n_vocab);
     if (kcpp_model_read_logits(last, e.logits.data())) return -1;
     float *l = e.logits.data();
     const float low = ksamp::lowest_logit(l, e.logits.size());
+    // EOS and EOT both set to the lowest logit (gpttype_adapter.cpp:3198-3209)
     if (S.suppress_eos && eos >= 0 && eos < e.hp.n_vocab) l[eos] = low;
+    if (S.suppress_eos && eot >= 0 && eot < e.hp.n_vocab) l[eot] = low;
     for (int b : S.banned) l[b] = low;
     return ksamp::sample_logits(l, S.n_ctx, e.hp.n_vocab, S.P, S.biases, S.restarts, e.ctx, last_n, rng, mu);
 }
@@ -499,53 +553,9 @@ bool load_model(const load_model_inputs inputs) {
     // test hook: KCPP_VIRTUAL_DEVICES=n splits the layers as if n GPUs were visible, stage i on GPU i % ndev
     const int nreal = ndev;
     if (getenv("KCPP_VIRTUAL_DEVICES")) ndev = std::max(1, atoi(getenv("KCPP_VIRTUAL_DEVICES")));
-    const std::vector<int> ldev = split_layers(hp.n_layer, std::min(ndev, KCPP_TENSOR_SPLIT_MAX), inputs.tensor_split);
     e->ub = inputs.blasbatchsize > 0 ? std::min(inputs.blasbatchsize, 512) : 512;
     e->use_contextshift = inputs.use_contextshift;
-    int il = 0;
-    // stages of consecutive layers per device; the output head on its own device (upper_bound of
-    // (act - 1) / act, src/llama.cpp:7030-7033) -- a head-only stage when that is not the last layers' device
-    auto add_stage = [&](int d, int i0, int i1, bool out) {
-        const int gpu = d % nreal;
-        kcpp_model *m = kcpp_model_create(&hp, e->types.data(), gpu, i0, i1, e->stages.empty(), out, e->ub);
-        if (!m) { fprintf(stderr, "[kcpp] load_model: %s\n", kcpp_last_error()); return false; }
-        e->stages.push_back(m);
-        e->hidden.push_back(kcpp_model_hidden(m));
-        e->devs.push_back(gpu);
-        if (e->stages.size() > 1 && e->devs[e->devs.size() - 2] != gpu) {
-            hipSetDevice(gpu);
-            hipDeviceEnablePeerAccess(e->devs[e->devs.size() - 2], 0);   // xGMI peer copies for the handoff
-            (void)hipGetLastError();
-        }
-        return true;
-    };
-    if (inputs.use_rowsplit && std::min(ndev, KCPP_TENSOR_SPLIT_MAX) > 1) {
-        // LLAMA_SPLIT_MODE_ROW (gpttype_adapter.cpp:1892): one stage on the main device (cublas_info,
-        // gpttype_adapter.cpp:1708) owning every layer; the matrices' rows spread over the devices by tensor_split
-        const int nd = std::min(ndev, KCPP_TENSOR_SPLIT_MAX);
-        const int main_dev = std::min(inputs.cublas_info <= 0 ? 0 : inputs.cublas_info, nd - 1) % nreal;
-        std::vector<int> devs(nd);
-        for (int i = 0; i < nd; ++i) devs[i] = i % nreal;
-        kcpp_model *m = kcpp_model_create(&hp, e->types.data(), main_dev, 0, hp.n_layer, 1, 1, e->ub);
-        if (!m) { fprintf(stderr, "[kcpp] load_model: %s\n", kcpp_last_error()); return false; }
-        e->stages.push_back(m);
-        e->hidden.push_back(kcpp_model_hidden(m));
-        e->devs.push_back(main_dev);
-        if (kcpp_model_set_row_split(m, nd, devs.data(), inputs.tensor_split)) {
-            fprintf(stderr, "[kcpp] load_model: row split: %s\n", kcpp_last_error());
-            return false;
-        }
-        il = hp.n_layer;
-    }
-    while (il < hp.n_layer) {
-        const int d = ldev[il];
-        int il1 = il;
-        while (il1 < hp.n_layer && ldev[il1] == d) ++il1;
-        const bool last = il1 == hp.n_layer;
-        if (!add_stage(d, il, il1, last && ldev[hp.n_layer] == d)) return false;
-        if (last && ldev[hp.n_layer] != d && !add_stage(ldev[hp.n_layer], hp.n_layer, hp.n_layer, true)) return false;
-        il = il1;
-    }
+    if (!build_stages(*e, ndev, nreal, inputs.tensor_split, inputs.use_rowsplit, inputs.cublas_info)) return false;
     if (!init_handoff(*e)) { fprintf(stderr, "[kcpp] load_model: handoff events\n"); return false; }
     // KV cache types (gpttype_adapter.cpp:1958-1959: quant_k/v > 1 -> Q4_0, == 1 -> Q8_0, else F16).  Quantized
     // caches imply flash attention and no context shift (koboldcpp.py's --quantkv handling); this runtime's
@@ -627,15 +637,26 @@ generation_outputs generate(const generation_inputs in) {
         return out;
     }
     e->ctx.insert(e->ctx.end(), toks.begin() + keep, toks.end());
+    // forward() only enqueues: the prompt's time ends when the last stage's stream has drained (the reference's
+    // llama_decode returns after the graph ran, gpttype_adapter.cpp:3064, 3160-3164)
+    if (kcpp_model_sync(e->stages.back())) {
+        fprintf(stderr, "[kcpp] generate: prefill failed: %s\n", kcpp_last_error());
+        g_finished = true;
+        return out;
+    }
     const auto t1 = std::chrono::steady_clock::now();
     // seed as gpttype_adapter.cpp:2736-2740 (time-based when <= 0 or 0xFFFFFFFF)
     uint32_t seed = (uint32_t)in.seed;
     if (in.seed <= 0 || seed == 0xFFFFFFFFu) seed = (uint32_t)time(nullptr) % 1000000u;
     std::mt19937 rng(seed);
     g_last_seed = (int)seed;
+    // SampleLogits' n_ctx is kcpp_data->n_ctx, which generate() sets to the request's max_context_length
+    // (gpttype_adapter.cpp:2646, passed as nctx at :3227)
     const SamplerSetup S = make_sampler(*e, in, in.max_context_length > 0 ? in.max_context_length : max_ctx);
-    static bool mu_init = false;                 // SampleLogits' function-static mirostat_mu (:1369)
-    if (!mu_init) { g_mirostat_mu = 2.0f * S.P.mirostat_tau; mu_init = true; }
+    // SampleLogits' function-static mirostat_mu (:1369) is initialised by the first call that enters the
+    // mirostat branch, with that call's tau
+    static bool mu_init = false;
+    if (!mu_init && (S.P.mirostat == 1 || S.P.mirostat == 2)) { g_mirostat_mu = 2.0f * S.P.mirostat_tau; mu_init = true; }
     // last_n_tokens: repeat_last_n zeros, then every context token in order (:2892-2895, 3236-3243, 3420-3425)
     std::vector<int> last_n(S.P.rep_pen_range, 0);
     for (int t : e->ctx) { last_n.erase(last_n.begin()); last_n.push_back(t); }
@@ -649,7 +670,11 @@ generation_outputs generate(const generation_inputs in) {
         if (t < 0) { fprintf(stderr, "[kcpp] generate: sampling failed: %s\n", kcpp_last_error()); break; }
         last_n.erase(last_n.begin());
         last_n.push_back(t);
-        if (t == e->tok.eos() && !in.bypass_eos_token) { stop = KCPP_STOP_EOS_TOKEN_HIT; break; }
+        // EOS or EOT ends the generation when EOS is allowed (gpttype_adapter.cpp:3346)
+        if (!in.bypass_eos_token && in.allow_eos_token && (t == e->tok.eos() || (t == e->tok.eot() && t != -1))) {
+            stop = KCPP_STOP_EOS_TOKEN_HIT;
+            break;
+        }
         const std::string piece = e->tok.piece(t);
         bool hit = false;
         {
@@ -711,6 +736,64 @@ int kcpp_tokenize_probe(const char *gguf_path, const char *text, int add_bos, in
     const std::vector<int> ids = tk.encode(std::string(text), add_bos != 0);
     for (size_t i = 0; i < ids.size() && (int)i < cap; ++i) out[i] = ids[i];
     return (int)ids.size();
+}
+
+// bench.py --gpus N (N > 1): the drop-in engine over n_dev GPUs -- load_model's stages (build_stages), hand-off
+// (init_handoff: RCCL clique over distinct GPUs), forward() -- with synthetic weights instead of a GGUF.  Prefill of
+// n_prompt ids in ubatches of ub (timed to the last stage's drain), then n_warm + n_steps greedy tokens exactly as
+// generate() runs them: argmax on the last stage, the token back through the host, forward() over all stages.
+// out = {prefill_s, decode_s (the n_steps timed tokens), n_past at the end, 1 when the hand-off is RCCL}.
+int kcpp_engine_bench(const kcpp_hparams *hp, const int *types, int n_types, int n_dev, const float *tensor_split,
+                      uint64_t seed, int n_prompt, int ub, int n_warm, int n_steps, double *out) {
+    if (!hp || !types || !out || n_dev < 1 || n_prompt < 1 || n_prompt + n_warm + n_steps + 1 > hp->n_ctx) return -2;
+    int nreal = 0;                          // KCPP_VIRTUAL_DEVICES (tests): several stages per GPU, stage i on GPU i % nreal
+    if (hipGetDeviceCount(&nreal) != hipSuccess || nreal < 1 || (nreal < n_dev && !getenv("KCPP_VIRTUAL_DEVICES"))) {
+        fprintf(stderr, "[kcpp] engine_bench: %d GPUs requested, %d visible\n", n_dev, nreal);
+        return -1;
+    }
+    nreal = std::min(nreal, n_dev);
+    auto e = std::make_unique<Engine>();
+    e->hp = *hp;
+    e->types.assign(types, types + n_types);
+    e->ub = std::max(1, std::min(ub, 512));
+    float ts[KCPP_TENSOR_SPLIT_MAX] = {0};
+    for (int i = 0; i < n_dev && i < KCPP_TENSOR_SPLIT_MAX; ++i) ts[i] = tensor_split ? tensor_split[i] : 1.0f;
+    if (!build_stages(*e, n_dev, nreal, ts, false, 0) || !init_handoff(*e)) return -3;
+    for (kcpp_model *m : e->stages)
+        if (kcpp_model_synth_weights(m, seed)) return -4;
+    std::vector<int32_t> prompt(n_prompt);
+    for (int i = 0; i < n_prompt; ++i) prompt[i] = 16 + (i % 2);          // the " 1" pattern of bench.py
+    kcpp_model *last = e->stages.back();
+    // warm-up: a short prefill (first touch, graph capture on every stage)
+    if (forward(*e, prompt.data(), std::min(64, n_prompt), 0) || kcpp_model_sync(last)) return -5;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (forward(*e, prompt.data(), n_prompt, 0) || kcpp_model_sync(last)) return -5;
+    const auto t1 = std::chrono::steady_clock::now();
+    int n_past = n_prompt;
+    std::chrono::steady_clock::time_point t2 = t1;
+    for (int i = 0; i < n_warm + n_steps; ++i) {
+        if (i == n_warm) t2 = std::chrono::steady_clock::now();
+        int32_t tok = 0;
+        if (kcpp_model_argmax(last, &tok) || forward(*e, &tok, 1, n_past)) return -6;
+        ++n_past;
+    }
+    int32_t tok = 0;
+    if (kcpp_model_argmax(last, &tok)) return -6;                       // the last token's logits consumed
+    const auto t3 = std::chrono::steady_clock::now();
+    out[0] = std::chrono::duration<double>(t1 - t0).count();
+    out[1] = std::chrono::duration<double>(t3 - t2).count();
+    out[2] = n_past;
+    out[3] = e->comms.empty() ? 0.0 : 1.0;
+    return 0;
+}
+
+int kcpp_tokenizer_special_ids(const char *gguf_path, int32_t *out) {
+    gguf::File f;
+    std::string err;
+    Tokenizer tk;
+    if (!gguf_path || !out || !f.open(gguf_path, err) || !tk.init(f, err)) return -1;
+    out[0] = tk.bos(); out[1] = tk.eos(); out[2] = tk.eot();
+    return 0;
 }
 
 int kcpp_gguf_check(const char *path, char *err, int err_len) {

@@ -686,19 +686,18 @@ static int mm_launch(int type, const void *W, const void *W2, int64_t K, int64_t
 static int matmul_rows(kcpp_model *m, const KTensor &W, const KTensor *W2, const void *act, int64_t M, float *Y,
                        int64_t ldy, const float *res, int64_t ldr, int mode) {
     const size_t abytes = (size_t)kcpp_act_bytes(W.type, W.K, M);
+    // ev_in fences only the producers of act / res: it is recorded before the inline lane's launch, and every other
+    // lane is enqueued before it, so the lanes' mat-muls run concurrently with the main device's slice
     bool fenced = false;
+    int inl = -1;
     for (size_t i = 0; i < W.rs.size(); ++i) {
         const RowSlice &r = W.rs[i];
         const int64_t n = r.hi - r.lo;
         if (n <= 0) continue;
-        const void *w2 = W2 ? W2->rs[i].d : nullptr;
         const Lane &ln = m->lanes[r.lane];
-        if (ln.inline_main) {
-            RC(mm_launch(W.type, r.d, w2, W.K, n, act, M, Y + r.lo, ldy, res ? res + r.lo : nullptr, ldr, mode, m->gemm_ws,
-                         m->stream));
-            continue;
-        }
+        if (ln.inline_main) { inl = (int)i; continue; }
         if (!fenced) { RT_CHECK(hipEventRecord(m->ev_in, m->stream)); fenced = true; }
+        const void *w2 = W2 ? W2->rs[i].d : nullptr;
         RT_CHECK(hipSetDevice(ln.dev));
         RT_CHECK(hipStreamWaitEvent(ln.s, m->ev_in, 0));
         RT_CHECK(hipMemcpyPeerAsync(ln.act, ln.dev, act, m->device, abytes, ln.s));
@@ -708,7 +707,16 @@ static int matmul_rows(kcpp_model *m, const KTensor &W, const KTensor *W2, const
         RT_CHECK(hipMemcpy2DAsync(Y + r.lo, ldy * 4, ln.y, n * 4, n * 4, M, hipMemcpyDefault, ln.s));
         RT_CHECK(hipEventRecord(ln.done, ln.s));
         RT_CHECK(hipSetDevice(m->device));
-        RT_CHECK(hipStreamWaitEvent(m->stream, ln.done, 0));
+    }
+    if (inl >= 0) {
+        const RowSlice &r = W.rs[inl];
+        RC(mm_launch(W.type, r.d, W2 ? W2->rs[inl].d : nullptr, W.K, r.hi - r.lo, act, M, Y + r.lo, ldy,
+                     res ? res + r.lo : nullptr, ldr, mode, m->gemm_ws, m->stream));
+    }
+    for (size_t i = 0; fenced && i < W.rs.size(); ++i) {
+        const RowSlice &r = W.rs[i];
+        if (r.hi - r.lo <= 0 || (int)i == inl) continue;
+        RT_CHECK(hipStreamWaitEvent(m->stream, m->lanes[r.lane].done, 0));
     }
     return 0;
 }

@@ -52,6 +52,16 @@ public:
             err = "unsupported tokenizer model " + model_;
             return false;
         }
+        // EOT (llm_load_vocab, src/llama.cpp:6606, 6642-6661): tokenizer.ggml.eot_token_id, else the first token whose
+        // text is one of the known end-of-turn markers (the reference walks an unordered_map; here the lowest id wins)
+        eot_ = (int)f.get_i("tokenizer.ggml.eot_token_id", -1);
+        if (eot_ < 0 || eot_ >= (int)vocab_.size()) {
+            eot_ = -1;
+            static const char *marks[] = {"<|eot_id|>", "<|im_end|>", "<|end|>", "<end_of_turn>", "<|endoftext|>", "<EOT>"};
+            for (size_t i = 0; i < vocab_.size() && eot_ < 0; ++i)
+                for (const char *mk : marks)
+                    if (vocab_[i] == mk) { eot_ = (int)i; break; }
+        }
         for (size_t i = 0; i < vocab_.size(); ++i)     // cache_special_tokens (src/llama.cpp:6720-6733)
             if ((ttype_[i] == 2 || ttype_[i] == 3 || ttype_[i] == 4) && !vocab_[i].empty()) special_.push_back((int)i);
         std::stable_sort(special_.begin(), special_.end(),
@@ -67,6 +77,7 @@ public:
     }
     int bos() const { return bos_; }
     int eos() const { return eos_; }
+    int eot() const { return eot_; }
     int n_vocab() const { return (int)vocab_.size(); }
 
     std::vector<int> encode(const std::string &text, bool add_bos) const {
@@ -372,6 +383,6 @@ private:
     std::unordered_map<std::string, int> rank_;
     std::string b2u_[256];
     std::map<uint32_t, int> u2b_;
-    int bos_ = 1, eos_ = 2;
+    int bos_ = 1, eos_ = 2, eot_ = -1;
     bool add_bos_ = true, add_space_prefix_ = true;
 };

@@ -52,6 +52,8 @@ _SIGS = {
     "kcpp_gguf_check": [ctypes.c_char_p, ctypes.c_char_p, I],
     "kcpp_pretokenize": [ctypes.c_char_p, ctypes.c_char_p, P, I],
     "kcpp_tokenize_probe": [ctypes.c_char_p, ctypes.c_char_p, I, P, I],
+    "kcpp_tokenizer_special_ids": [ctypes.c_char_p, P],
+    "kcpp_engine_bench": [P, P, I, I, P, U64, I, I, I, I, P],
     "kcpp_add": [P, P, P, I64, P],
     "kcpp_silu_mul": [P, P, P, I64, P],
     "kcpp_moe_route": [P, I64, P, I, I64, I, I, P, P, I, P],
@@ -205,6 +207,18 @@ def hparams(hp):
     return HParams(*[int(hp[n]) for n in ("n_vocab", "n_embd", "n_head", "n_head_kv", "n_layer", "n_ff", "n_ctx")],
                    float(hp["eps"]), float(hp["rope_base"]), float(hp.get("rope_freq_scale", 1.0)),
                    int(hp.get("n_expert", 0)), int(hp.get("n_expert_used", 0)))
+
+
+def engine_bench(hp, types, n_dev, n_prompt, ubatch, n_warm, n_steps, seed=1234, tensor_split=None):
+    """the drop-in engine (load_model's layer-split stages over n_dev GPUs, RCCL / copy hand-off, generate()'s
+    greedy loop) on synthetic weights: {prefill_s, decode_s, n_past, rccl}"""
+    h = hparams(hp)
+    t = (ctypes.c_int * len(types))(*types)
+    ts = (ctypes.c_float * 16)(*((tensor_split or [1.0] * n_dev) + [0.0] * (16 - n_dev)))
+    out = (ctypes.c_double * 4)()
+    _chk(_L.kcpp_engine_bench(ctypes.byref(h), t, len(types), n_dev, ts, seed, n_prompt, ubatch, n_warm, n_steps, out),
+         "engine_bench")
+    return {"prefill_s": out[0], "decode_s": out[1], "n_past": int(out[2]), "rccl": bool(out[3])}
 
 
 class Model:

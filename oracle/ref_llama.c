@@ -285,6 +285,13 @@ static int run_llama(const char *cfgpath) {
     if (!out) return 3;
     float *logits = malloc(sizeof(float) * c->n_vocab);
     int n_past = 0;
+    /* REF_SKIP_PREFIX=n (bench.py's cpu_baseline at the GPU's context depth): the first n prompt positions are
+       taken as already in the (zeroed) KV cache, not computed -- a decode step's cost depends on the cache length,
+       not its contents -- so the timed work is the rest of the prompt at positions n.. and the decode after it */
+    const char *skip = getenv("REF_SKIP_PREFIX");
+    int p0 = skip ? atoi(skip) : 0;
+    if (p0 < 0 || p0 >= c->n_prompt) p0 = 0;
+    n_past = p0;
     double tp0 = now_s();
     FILE *hout = c->hidden_out[0] ? fopen(c->hidden_out, "wb") : NULL;
     float *hid = hout ? malloc(sizeof(float) * (size_t)(c->n_layer > 1 ? c->n_layer - 1 : 1) * c->ubatch * c->n_embd) : NULL;
@@ -295,7 +302,7 @@ static int run_llama(const char *cfgpath) {
         rout = fopen(rp, "wb");
         g_router = malloc(sizeof(float) * (size_t)(c->n_layer > 1 ? c->n_layer - 1 : 1) * c->ubatch * c->n_expert);
     }
-    for (int i = 0; i < c->n_prompt; i += c->ubatch) {
+    for (int i = p0; i < c->n_prompt; i += c->ubatch) {
         int T = c->n_prompt - i < c->ubatch ? c->n_prompt - i : c->ubatch;
         if (eval(&m, c->prompt + i, T, n_past, logits, hid)) return 4;
         if (hout) fwrite(hid, sizeof(float), (size_t)(c->n_layer - 1) * T * c->n_embd, hout);
@@ -317,8 +324,8 @@ static int run_llama(const char *cfgpath) {
     }
     double t_tg = now_s() - tg0;
     fclose(out);
-    printf("{\"load_s\": %.3f, \"prefill_s\": %.6f, \"decode_s\": %.6f, \"n_prompt\": %d, \"n_gen\": %d, \"threads\": %d}\n",
-           t_load, t_pp, t_tg, c->n_prompt, c->n_gen, c->nthreads);
+    printf("{\"load_s\": %.3f, \"prefill_s\": %.6f, \"decode_s\": %.6f, \"n_prompt\": %d, \"n_gen\": %d, \"threads\": %d, "
+           "\"skip_prefix\": %d}\n", t_load, t_pp, t_tg, c->n_prompt, c->n_gen, c->nthreads, p0);
     return 0;
 }
 

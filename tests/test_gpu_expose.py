@@ -309,3 +309,49 @@ def test_generate_row_split_matches_in_process(model, tmp_path, monkeypatch):
         n += 1
     m.close()
     assert out.text == b"".join(piece(toks, ttypes, t) for t in want)
+
+
+def test_engine_bench_virtual_stages(monkeypatch):
+    """bench.py --gpus N's path (kcpp_engine_bench): load_model's layer-split stages (3 on the one test GPU via
+    KCPP_VIRTUAL_DEVICES), event-ordered hand-off, pipelined prefill, generate()'s greedy loop -- runs and reports
+    the token count it decoded"""
+    import koboldcpp_amd.lib as K
+    monkeypatch.setenv("KCPP_VIRTUAL_DEVICES", "3")
+    hp = dict(R.TINY, n_layer=5, n_ctx=256)
+    types = R.q4_k_m_types(hp["n_layer"])
+    r = K.engine_bench(hp, types, 3, 64, 16, 2, 8)
+    assert r["n_past"] == 64 + 2 + 8 and not r["rccl"]
+    assert r["prefill_s"] > 0 and r["decode_s"] > 0
+
+
+def test_generate_process_time_includes_the_prefill(model):
+    """last_process_time covers the prompt's device time (the stream is drained before the clock stops): the
+    prompt's ms/token x tokens is at least a third of the same prompt's synchronous in-process decode"""
+    import time
+    import koboldcpp_amd.lib as K
+    h, X, _, _, types = model
+    prompt = b" ".join([b"hello world the a b of to"] * 12)
+    r = h.token_count(prompt, True)
+    ids = [r.ids[i] for i in range(r.count)]
+    gi = X.generation_inputs()
+    gi.prompt = prompt
+    gi.max_context_length = 248
+    gi.max_length = 2
+    gi.temperature = 0.0
+    gi.top_k = 1
+    gi.rep_pen = 1.0
+    gi.bypass_eos_token = True
+    h.generate(gi)                                   # warm (and fills the cache: the next call fast-forwards)
+    gi.prompt = b"the " + prompt                    # a different first token: the whole prompt is processed again
+    out = h.generate(gi)
+    assert out.status == 1
+    np_ = h.token_count(gi.prompt, True).count
+    t_proc = h.get_last_process_time() * np_ / 1e3
+    m = K.Model(dict(R.TINY, n_ctx=512), types, max_ubatch=512)
+    m.synth(1234)
+    m.decode(ids, 0, want_logits=False)
+    t0 = time.perf_counter()
+    m.decode(ids, 0, want_logits=False)
+    t_ref = time.perf_counter() - t0
+    m.close()
+    assert t_proc >= 0.3 * t_ref, (t_proc, t_ref)

@@ -150,3 +150,21 @@ def test_bpe_encode_matches_hf_tokenizers(lib, tmp_path):
     # BOS per the vocabulary
     out = (ctypes.c_int32 * 8)()
     assert lib.kcpp_tokenize_probe(path.encode(), b"hi", 1, out, 8) >= 1 and out[0] == 0
+
+
+@pytest.mark.parametrize("case", ["kv", "text", "none"])
+def test_special_ids_eot(lib, tmp_path, case):
+    """EOT as llm_load_vocab finds it (src/llama.cpp:6606, 6642-6661): the tokenizer.ggml.eot_token_id key, else a
+    token whose text is a known end-of-turn marker, else none (-1); generate() suppresses and stops on it like EOS"""
+    import gguf_writer as GW
+    toks = ["<unk>", "<s>", "</s>", "a", "b", "<|eot_id|>", "c"]
+    kv = {"general.architecture": "llama", "tokenizer.ggml.model": "llama",
+          "tokenizer.ggml.tokens": (GW.STR, toks if case != "none" else toks[:5] + ["x", "c"]),
+          "tokenizer.ggml.bos_token_id": 1, "tokenizer.ggml.eos_token_id": 2}
+    if case == "kv":
+        kv["tokenizer.ggml.eot_token_id"] = 6
+    path = str(tmp_path / "v.gguf")
+    GW.write(path, kv, [("token_embd.weight", 0, [8, len(toks)], np.zeros((len(toks), 8), np.float32))])
+    out = (ctypes.c_int32 * 3)()
+    assert lib.kcpp_tokenizer_special_ids(path.encode(), out) == 0
+    assert list(out) == [1, 2, {"kv": 6, "text": 5, "none": -1}[case]]
