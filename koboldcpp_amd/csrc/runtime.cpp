@@ -122,6 +122,7 @@ struct kcpp_model {
     void *kv_scratch = nullptr;             // context shift: moved K/V rows (n_ctx x EKV x 2 f16, lazily)
     float *shift_cs = nullptr;              // context shift: (cos, sin) pairs of the shift distance
     int32_t *pin = nullptr;          // pinned host {token, n_past}
+    int pos_val = -1;                // the value pos_dev holds once the enqueued work has run (-1: unknown)
     float *logits_pin = nullptr;
     bool use_graphs = true;
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
@@ -137,7 +138,8 @@ struct kcpp_model {
 };
 
 static int ensure_graph(kcpp_model *m);
-static int launch_argmax(kcpp_model *m);
+static int launch_argmax(kcpp_model *m, bool step_pos);
+static int launch_pos_step(kcpp_model *m);
 
 static int64_t tensor_bytes(int type, int64_t K, int64_t N) {
     return K / ks_block_elems(type) * N * ks_block_bytes(type);
@@ -1077,16 +1079,28 @@ static int decode_step_dev(kcpp_model *m) {
         RC(forward_layers(m, 1, 0, true));
         if (m->has_output) RC(head(m, 1));
     }
-    if (m->has_output) RC(launch_argmax(m));      // greedy token on device (tok_dev for the next step)
+    // greedy token on device (tok_dev for the next step); the device position steps to the next token's, so a
+    // replay needs no host-to-device copy when tokens follow each other (the graph holds no memcpy node)
+    if (m->has_output) RC(launch_argmax(m, true));
+    else RC(launch_pos_step(m));
     return 0;
 }
 
-// single-token graph: pos_dev <- pin[1] (read at replay time), embedding of tok_dev, layers, head, argmax
+// pos_dev <- n_past unless the device already holds it (the previous single-token step advanced it)
+static int set_pos(kcpp_model *m, int n_past) {
+    if (m->pos_val != n_past) {
+        m->pin[1] = n_past;
+        RT_CHECK(hipMemcpyAsync(m->pos_dev, &m->pin[1], 4, hipMemcpyHostToDevice, m->stream));
+    }
+    m->pos_val = n_past + 1;          // decode_step_dev advances it
+    return 0;
+}
+
+// single-token graph: embedding of tok_dev, layers at position pos_dev, head, argmax, pos_dev + 1
 static int ensure_graph(kcpp_model *m) {
     if (m->g_exec) return 0;
     hipGraph_t g;
     RT_CHECK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
-    hipMemcpyAsync(m->pos_dev, &m->pin[1], 4, hipMemcpyHostToDevice, m->stream);
     int rc = decode_step_dev(m);
     hipError_t e = hipStreamEndCapture(m->stream, &g);
     if (rc || e != hipSuccess) { g_err = "graph capture failed"; return rc ? rc : -3; }
@@ -1108,15 +1122,14 @@ static int decode_enqueue(kcpp_model *m, const int32_t *tokens, int T, int n_pas
     if (m->has_embed && !tokens) { g_err = "decode: stage owns the embedding but tokens == NULL"; return -2; }
     if (T == 1 && m->use_graphs) {
         m->pin[0] = m->has_embed ? tokens[0] : 0;
-        m->pin[1] = n_past;
         if (m->has_embed) RT_CHECK(hipMemcpyAsync(m->tok_dev, &m->pin[0], 4, hipMemcpyHostToDevice, m->stream));
         RC(ensure_graph(m));
+        RC(set_pos(m, n_past));
         RT_CHECK(hipGraphLaunch(m->g_exec, m->stream));
     } else if (T == 1) {
         m->pin[0] = m->has_embed ? tokens[0] : 0;
-        m->pin[1] = n_past;
         RT_CHECK(hipMemcpyAsync(m->tok_dev, &m->pin[0], 4, hipMemcpyHostToDevice, m->stream));
-        RT_CHECK(hipMemcpyAsync(m->pos_dev, &m->pin[1], 4, hipMemcpyHostToDevice, m->stream));
+        RC(set_pos(m, n_past));
         RC(decode_step_dev(m));
     } else {
         // split into ubatches (llama_decode_internal, src/llama.cpp:17187-17201)
@@ -1173,18 +1186,29 @@ __global__ void __launch_bounds__(256) k_argmax_part(const float *__restrict__ x
     amax_block(v, i);
     if (threadIdx.x == 0) part[blockIdx.x] = make_float2(v, __int_as_float(i));
 }
-__global__ void __launch_bounds__(256) k_argmax_final(const float2 *__restrict__ part, int32_t *out, int32_t *tok) {
+__global__ void __launch_bounds__(256) k_argmax_final(const float2 *__restrict__ part, int32_t *out, int32_t *tok,
+                                                      int32_t *pos) {
     const float2 p = part[threadIdx.x];
     float v = p.x; int i = __float_as_int(p.y);
     amax_block(v, i);
     if (i == 0x7fffffff) i = 0;               // all-NaN logits: no comparison succeeded; keep the token id valid
-    if (threadIdx.x == 0) { out[0] = i; if (tok) tok[0] = i; }
+    if (threadIdx.x == 0) {
+        out[0] = i;
+        if (tok) tok[0] = i;
+        if (pos) pos[0] += 1;                 // the next single-token step's position
+    }
 }
-static int launch_argmax(kcpp_model *m) {
+__global__ void k_pos_step(int32_t *pos) { pos[0] += 1; }
+static int launch_argmax(kcpp_model *m, bool step_pos) {
     hipLaunchKernelGGL(k_argmax_part, dim3(ARGMAX_BLOCKS), dim3(256), 0, m->stream, m->logits, m->hp.n_vocab,
                        (float2 *)m->argmax_ws);
     hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, m->stream, (const float2 *)m->argmax_ws, m->argmax_dev,
-                       m->has_embed ? m->tok_dev : nullptr);
+                       m->has_embed ? m->tok_dev : nullptr, step_pos ? m->pos_dev : nullptr);
+    RT_CHECK(hipGetLastError());
+    return 0;
+}
+static int launch_pos_step(kcpp_model *m) {
+    hipLaunchKernelGGL(k_pos_step, dim3(1), dim3(1), 0, m->stream, m->pos_dev);
     RT_CHECK(hipGetLastError());
     return 0;
 }
@@ -1192,7 +1216,7 @@ static int launch_argmax(kcpp_model *m) {
 extern "C" int kcpp_model_argmax(kcpp_model *m, int32_t *token_out) {
     if (!m->has_output) return -1;
     RT_CHECK(hipSetDevice(m->device));
-    RC(launch_argmax(m));
+    RC(launch_argmax(m, false));
     RT_CHECK(hipMemcpyAsync(&m->pin[2], m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
     RT_CHECK(hipStreamSynchronize(m->stream));
     *token_out = m->pin[2];
@@ -1205,12 +1229,12 @@ extern "C" int kcpp_model_decode_greedy(kcpp_model *m, int n_past, int32_t *toke
     if (!m->has_embed || !m->has_output) { g_err = "decode_greedy needs embedding and output on this stage"; return -2; }
     if (n_past + 1 > m->hp.n_ctx) { g_err = "context overflow"; return -2; }
     RT_CHECK(hipSetDevice(m->device));
-    m->pin[1] = n_past;
     if (m->use_graphs) {
         RC(ensure_graph(m));
+        RC(set_pos(m, n_past));
         RT_CHECK(hipGraphLaunch(m->g_exec, m->stream));
     } else {
-        RT_CHECK(hipMemcpyAsync(m->pos_dev, &m->pin[1], 4, hipMemcpyHostToDevice, m->stream));
+        RC(set_pos(m, n_past));
         RC(decode_step_dev(m));
     }
     RT_CHECK(hipMemcpyAsync(&m->pin[2], m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
