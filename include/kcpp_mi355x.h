@@ -89,6 +89,16 @@ int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
  * (v) in KT_Q6_K_RS -- the Q4_K_M "more bits" layers -- in one launch; -3 when the shape is not covered */
 int kcpp_gemv_rs_qkv_mixed(const void *args, void *stream);
 int kcpp_rs_supported(int type, int64_t K);
+/* single-token attn_norm -> q|k|v (+RoPE, K/V store) and the split-KV attention in one launch, then the combine into
+ * attn_out (koboldcpp_amd/csrc/dec_fused.hip; results equal kcpp_gemv_rs / kcpp_gemv_rs_qkv_mixed + kcpp_flash_attn
+ * bit for bit).  args: the mode-2 DecArgs (segments q, k, v in KT_Q4_K_RS, v in KT_Q6_K_RS with mixed = 1; pos =
+ * {position, epoch}); ws: the flash-attention workspace; gran: kcpp_dec_gran_bytes(H, HKV) zeroed once; il: the
+ * layer.  -3 when not covered. */
+int64_t kcpp_dec_gran_bytes(int H, int HKV);
+int kcpp_dec_qkv_att(int mixed, const void *args, void *ws, void *gran, int il, int H, int HKV, float scale,
+                     float *attn_out, void *stream);
+/* the fused launch's poll-timeout flag in gran (0: every wait completed), -1 on a copy error */
+int kcpp_dec_fused_error(void *gran, int H, int HKV);
 
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,
@@ -217,6 +227,10 @@ int kcpp_ggml_mul_mat_f(int wtype, const void *w, const kcpp_tdesc *tw, const fl
  * cache views [n_kv][HKV][128], optional f16 mask [T][n_kv] (row stride mask_ld; -inf keys skipped), out f32
  * [T][H][128]; ws of kcpp_fa_ext_workspace_bytes */
 int64_t kcpp_fa_ext_workspace_bytes(int T, int H, int n_kv, int D);
+/* f32 row moves (the MoE mat-mul's gather / scatter): dst row i <- src row i, K floats, each side addressed by byte
+ * offsets (offs != NULL) or by a byte stride (ld) */
+int kcpp_rows_move_f32(const void *src, const int64_t *soffs, int64_t sld, void *dst, const int64_t *doffs, int64_t dld,
+                       int64_t K, int n, void *stream);
 int kcpp_flash_attn_ext(const float *q, int64_t q_nb1, int64_t q_nb2, const uint16_t *kc, const uint16_t *vc,
                         const uint16_t *mask, int64_t mask_ld, float *out, void *ws, int T, int H, int HKV, int D,
                         int n_kv, float scale, void *stream);
@@ -282,6 +296,10 @@ int kcpp_model_kv_shift(kcpp_model *m, int p0, int diff, int n_past);
 int kcpp_model_set_graphs(kcpp_model *m, int enable);
 /* single-token decode through the fused mat-vec path (default on); off = one kernel per op */
 int kcpp_model_set_fused_decode(kcpp_model *m, int enable);
+/* single-token q|k|v + attention in one launch (kcpp_dec_qkv_att; default off: measured slower) */
+int kcpp_model_set_decode_fusion(kcpp_model *m, int enable);
+/* the fused launches' spin-timeout flag after the stream drains (0: none timed out) */
+int kcpp_model_fused_error(kcpp_model *m);
 /* 1: attention through kcpp_flash_attn_exact (reference order, f16 accumulation; strict-parity mode, slow);
  * 0 (default, or KCPP_FA_EXACT=1 at creation): the split-KV / MFMA kernels */
 int kcpp_model_set_fa_exact(kcpp_model *m, int enable);

@@ -9,6 +9,7 @@
 //   decode  : k_fa_decode  grid (chunks of 256 keys, kv-head, query) -> partial (O, m, l)
 //             k_fa_combine one 256-thread block per (query, head pair) -> f32 out (+Q8_K quant)
 //   prefill : k_fa_prefill tiled 64 queries x 64 keys per step, online softmax.
+#include "attn_dec.h"
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
@@ -17,7 +18,7 @@
 
 #define FA_CHUNK 64
 #define FA_MAXG 8
-#define FA_WS_TICKETS 256
+#define FA_WS_TICKETS KCPP_FA_WS_HEADER     // workspace header (kcpp_internal.h)
 #define FA_MAX_CHUNKS 2048          // k_fa_combine's chunk-weight table: 2048 x 64 = 131072 keys
 static void *g_fa_stamps = nullptr;       // diagnostic stamp buffer (tools only; kcpp_fa_set_stamps)
 
@@ -163,28 +164,15 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
     const int p0 = sp * per, p1 = min(p0 + per, nkv);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int sub = lane & 15, kq = lane >> 4;
-    __shared__ float s_o[4][G][D];
-    __shared__ float s_ml[4][G][2];
-    __shared__ float s_w[4][G], s_L[G];
+    __shared__ fadec::Smem<G> sm;
     // scores in the exp2 domain: s2 = (q . k) * scale * log2(e); partial m in the same domain
     const float sc2 = scale * 1.4426950408889634f;
-    float qv[G][8];
+    fadec::State<G> st;
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const uint4 qq = *(const uint4 *)(q16 + (int64_t)(hk * G + g) * D + sub * 8);
-        const uint32_t w4[4] = {qq.x, qq.y, qq.z, qq.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) { qv[g][2 * e] = h2f(w4[e] & 0xFFFF); qv[g][2 * e + 1] = h2f(w4[e] >> 16); }
-    }
-    if (stamps) { if (qv[0][0] == 12345.0f) stamps[0] = 0; FA_STAMP(1); }
+    for (int g = 0; g < G; ++g) fadec::set_q(st, g, *(const uint4 *)(q16 + (int64_t)(hk * G + g) * D + sub * 8));
+    if (stamps) { if (st.qv[0][0] == 12345.0f) stamps[0] = 0; FA_STAMP(1); }
     const uint16_t *kb = kc + (int64_t)hk * kv_hs + sub * 8, *vb = vc + (int64_t)hk * kv_hs + sub * 8;
-    float m[G], l[G], acc[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        m[g] = -INFINITY; l[g] = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[g][e] = 0.0f;
-    }
+    fadec::init(st);
     uint4 ka[4], va[4], kn[4], vn[4];
     auto issue = [&](int base, uint4 *kk, uint4 *vv) {
 #pragma unroll
@@ -195,138 +183,19 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
             vv[i] = ok ? *(const uint4 *)(vb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
         }
     };
-    auto consume = [&](int base, const uint4 *kk, const uint4 *vv) {
-        float s[G][4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t w4[4] = {kk[i].x, kk[i].y, kk[i].z, kk[i].w};
-            float kf[8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { kf[2 * e] = h2f(w4[e] & 0xFFFF); kf[2 * e + 1] = h2f(w4[e] >> 16); }
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                float sc = 0.0f;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) sc = fmaf(qv[g][e], kf[e], sc);
-                s[g][i] = sc;
-            }
-        }
-        // 16-lane row sums of all G x 4 partial dots, interleaved (independent DPP chains)
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) s[g][i] += dpp_f<0xB1>(s[g][i]);
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) s[g][i] += dpp_f<0x4E>(s[g][i]);
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) s[g][i] += dpp_f<0x141>(s[g][i]);
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                s[g][i] += dpp_f<0x140>(s[g][i]);
-                s[g][i] = base + 4 * i + kq < p1 ? s[g][i] * sc2 : -INFINITY;
-            }
-        float mx[G], al[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) mx[g] = fmaxf(fmaxf(s[g][0], s[g][1]), fmaxf(s[g][2], s[g][3]));
-#pragma unroll
-        for (int g = 0; g < G; ++g) mx[g] = xmax16(mx[g]);
-#pragma unroll
-        for (int g = 0; g < G; ++g) mx[g] = xmax32(mx[g]);
-        float ls[G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float mn = fmaxf(m[g], mx[g]);           // finite: key base + kq (i = 0) of row 0 is valid
-            al[g] = __builtin_amdgcn_exp2f(m[g] - mn);     // m = -inf -> 0
-            ls[g] = 0.0f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                s[g][i] = __builtin_amdgcn_exp2f(s[g][i] - mn);   // -inf -> 0
-                ls[g] += s[g][i];
-            }
-            m[g] = mn;
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) ls[g] = xsum16(ls[g]);
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            l[g] = fmaf(l[g], al[g], xsum32(ls[g]));
-#pragma unroll
-            for (int e = 0; e < 8; ++e) acc[g][e] *= al[g];
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint32_t w4[4] = {vv[i].x, vv[i].y, vv[i].z, vv[i].w};
-            float vf[8];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) { vf[2 * e] = h2f(w4[e] & 0xFFFF); vf[2 * e + 1] = h2f(w4[e] >> 16); }
-#pragma unroll
-            for (int g = 0; g < G; ++g)
-#pragma unroll
-                for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(s[g][i], vf[e], acc[g][e]);
-        }
-    };
     int base = p0 + 16 * wave;
     if (base < p1) issue(base, ka, va);
     for (; base < p1; base += 128) {
         const int b1 = base + 64;
         if (b1 < p1) issue(b1, kn, vn);
-        consume(base, ka, va);
-        if (stamps && base == p0 + 16 * wave) { if (acc[0][0] == 12345.0f) stamps[0] = 0; FA_STAMP(2); }
+        fadec::consume(st, base, p1, kq, sc2, ka, va);
+        if (stamps && base == p0 + 16 * wave) { if (st.acc[0][0] == 12345.0f) stamps[0] = 0; FA_STAMP(2); }
         if (b1 >= p1) break;
         if (b1 + 64 < p1) issue(b1 + 64, ka, va);
-        consume(b1, kn, vn);
+        fadec::consume(st, b1, p1, kq, sc2, kn, vn);
     }
     FA_STAMP(3);
-    // rows (kq) hold disjoint keys: park every row's 8 dims in LDS, reduce rows and waves in one pass
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[g][e] = xsum16(acc[g][e]);
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) acc[g][e] = xsum32(acc[g][e]);
-    if (kq == 0) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            *(float4 *)&s_o[wave][g][sub * 8] = make_float4(acc[g][0], acc[g][1], acc[g][2], acc[g][3]);
-            *(float4 *)&s_o[wave][g][sub * 8 + 4] = make_float4(acc[g][4], acc[g][5], acc[g][6], acc[g][7]);
-        }
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int g = 0; g < G; ++g) { s_ml[wave][g][0] = m[g]; s_ml[wave][g][1] = l[g]; }
-    }
-    __syncthreads();
-    if (tid < G) {                                        // per-head wave weights and the split's (M, L)
-        const int g = tid;
-        float M = -INFINITY;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) M = fmaxf(M, s_ml[w][g][0]);
-        float L = 0.0f;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {
-            const float wt = M == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(s_ml[w][g][0] - M);
-            s_w[w][g] = wt;
-            L = fmaf(wt, s_ml[w][g][1], L);
-        }
-        s_L[g] = L;
-        part_ml[(int64_t)(hk * G + g) * NS + sp] = make_float2(M, L);
-    }
-    __syncthreads();
-    for (int i = tid; i < G * D; i += 256) {
-        const int g = i / D, d = i % D;
-        float O = 0.0f;
-#pragma unroll
-        for (int w = 0; w < 4; ++w) O = fmaf(s_w[w][g], s_o[w][g][d], O);
-        part_o[((int64_t)(hk * G + g) * NS + sp) * D + d] = O;
-    }
+    fadec::finish(st, sm, hk, sp, NS, part_o, part_ml);
     FA_STAMP(4);
     if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(5); }
 }
@@ -337,9 +206,10 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
 template <bool QUANT, int NS>
 __global__ void __launch_bounds__(256) k_fa_comb4(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
                                                   float *__restrict__ out, uint8_t *__restrict__ qout, int H,
-                                                  unsigned long long *stamps) {
+                                                  unsigned long long *stamps, unsigned *reset) {
     constexpr int D = 128, MAXS = 64;
     const int pair = blockIdx.x, tid = threadIdx.x;
+    if (reset && pair == 0 && tid < 15) reset[32 * tid] = 0;   // (a caller's counters: reset once consumed)
     const int wg_id = 2048 + blockIdx.x;
     FA_STAMP(0);
     const int hl = tid >> 7, d = tid & 127, h = 2 * pair + hl;
@@ -409,8 +279,10 @@ static void fa4_dispatch(const uint16_t *q16, const uint16_t *kc, const uint16_t
     // than this launch boundary)
     hipLaunchKernelGGL((k_fa_dec4<G>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS,
                        scale, kv_ld, kv_hs, st);
-    if (qout) hipLaunchKernelGGL((k_fa_comb4<true, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, st);
-    else hipLaunchKernelGGL((k_fa_comb4<false, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, st);
+    if (qout) hipLaunchKernelGGL((k_fa_comb4<true, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, st,
+                                 (unsigned *)nullptr);
+    else hipLaunchKernelGGL((k_fa_comb4<false, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, st,
+                            (unsigned *)nullptr);
 }
 
 template <int G>
@@ -689,7 +561,7 @@ int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max) {
     const int64_t nch = (n_kv_max + FA_CHUNK - 1) / FA_CHUNK;
     // partial slots: T x nch chunks (k_fa_decode), at least the 64 splits k_fa_dec4 may use
     const int64_t slots = std::max<int64_t>((int64_t)T * nch, 64);
-    return 256 + (int64_t)H * slots * (128 * 4 + 8) + (int64_t)T * H * 4 + 256;
+    return FA_WS_TICKETS + (int64_t)H * slots * (128 * 4 + 8) + (int64_t)T * H * 4 + 256;
 }
 
 // out f32 [T][H][D] (may be null), qout Q8_K act [T][H*D] (may be null), ws from kcpp_fa_workspace_bytes
@@ -759,6 +631,28 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
         return rc;
     KCPP_CHECK(hipGetLastError());
     if (qout) return kcpp_quantize_act(KT_Q8_K, out, (int64_t)H * D, qout, (int64_t)H * D, T, stream);
+    return 0;
+}
+
+// the combine of the fused q|k|v + attention launch (dec_fused.hip): partials behind FA_WS_TICKETS in ws, split count
+// kcpp_fa_dec_splits(HKV)
+int kcpp_fa_dec_splits(int HKV) { return fa4_splits(HKV); }
+int kcpp_fa_comb_fused(void *ws, float *out, int H, int HKV, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const int NS = fa4_splits(HKV);
+    float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
+    float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
+    switch (NS) {
+#define KCPP_COMB(N_)                                                                                          \
+    case N_:                                                                                                   \
+        hipLaunchKernelGGL((k_fa_comb4<false, N_>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, \
+                           (unsigned long long *)nullptr, (unsigned *)nullptr);                                \
+        break;
+        KCPP_COMB(4) KCPP_COMB(8) KCPP_COMB(16) KCPP_COMB(32) KCPP_COMB(64)
+#undef KCPP_COMB
+    default: return -1;
+    }
+    KCPP_CHECK(hipGetLastError());
     return 0;
 }
 

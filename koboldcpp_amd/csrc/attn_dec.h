@@ -1,0 +1,178 @@
+// attn_dec.h -- the single-token split-KV attention body (one workgroup = one split of one kv head, 4 waves), shared
+// by the stand-alone decode kernel k_fa_dec4 (attn.hip) and the fused q|k|v + attention launch (dec_fused.hip).
+//
+// Split sp of NS owns keys [p0, p1) of [0, n_kv).  Wave w streams 16-key groups base = p0 + 16 w + 64 j: lane
+// (kq = lane >> 4, sub = lane & 15) holds 16 B (8 dims) of K and of V for keys base + 4 i + kq, i < 4 -- every load
+// instruction is 1 KiB contiguous per wave.  Scores: 8-dim partial dot, 16-lane DPP reduction; online softmax per
+// wave in the exp2 domain (m, l wave-uniform); O: each lane accumulates its 8 dims over its row's keys, rows summed
+// once at the end, waves merged in LDS.  Partials: O [H][NS][128], (m, l) [H][NS] (m = -inf for an empty split).
+#pragma once
+#include "kcpp_common.h"
+
+namespace fadec {
+
+constexpr int D = 128;
+
+template <int G>
+struct State {
+    float qv[G][8];
+    float m[G], l[G], acc[G][8];
+};
+
+template <int G>
+__device__ __forceinline__ void init(State<G> &st) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        st.m[g] = -INFINITY; st.l[g] = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) st.acc[g][e] = 0.0f;
+    }
+}
+
+// q of the G heads of kv head hk, dims sub*8 .. +7, from 16-B words (plain or write-through loads)
+template <int G>
+__device__ __forceinline__ void set_q(State<G> &st, int g, const uint4 qq) {
+    const uint32_t w4[4] = {qq.x, qq.y, qq.z, qq.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { st.qv[g][2 * e] = h2f(w4[e] & 0xFFFF); st.qv[g][2 * e + 1] = h2f(w4[e] >> 16); }
+}
+
+// one 16-key group (keys base + 4 i + kq, i < 4; keys >= p1 masked), sc2 = scale * log2(e)
+template <int G>
+__device__ __forceinline__ void consume(State<G> &st, int base, int p1, int kq, float sc2, const uint4 *kk, const uint4 *vv) {
+    float s[G][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t w4[4] = {kk[i].x, kk[i].y, kk[i].z, kk[i].w};
+        float kf[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { kf[2 * e] = h2f(w4[e] & 0xFFFF); kf[2 * e + 1] = h2f(w4[e] >> 16); }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            float sc = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sc = fmaf(st.qv[g][e], kf[e], sc);
+            s[g][i] = sc;
+        }
+    }
+    // 16-lane row sums of all G x 4 partial dots, interleaved (independent DPP chains)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[g][i] += dpp_f<0xB1>(s[g][i]);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[g][i] += dpp_f<0x4E>(s[g][i]);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) s[g][i] += dpp_f<0x141>(s[g][i]);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            s[g][i] += dpp_f<0x140>(s[g][i]);
+            s[g][i] = base + 4 * i + kq < p1 ? s[g][i] * sc2 : -INFINITY;
+        }
+    float mx[G], al[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) mx[g] = fmaxf(fmaxf(s[g][0], s[g][1]), fmaxf(s[g][2], s[g][3]));
+#pragma unroll
+    for (int g = 0; g < G; ++g) mx[g] = xmax16(mx[g]);
+#pragma unroll
+    for (int g = 0; g < G; ++g) mx[g] = xmax32(mx[g]);
+    float ls[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const float mn = fmaxf(st.m[g], mx[g]);           // finite: key base + kq (i = 0) of row 0 is valid
+        al[g] = __builtin_amdgcn_exp2f(st.m[g] - mn);     // m = -inf -> 0
+        ls[g] = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            s[g][i] = __builtin_amdgcn_exp2f(s[g][i] - mn);   // -inf -> 0
+            ls[g] += s[g][i];
+        }
+        st.m[g] = mn;
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) ls[g] = xsum16(ls[g]);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        st.l[g] = fmaf(st.l[g], al[g], xsum32(ls[g]));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) st.acc[g][e] *= al[g];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t w4[4] = {vv[i].x, vv[i].y, vv[i].z, vv[i].w};
+        float vf[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { vf[2 * e] = h2f(w4[e] & 0xFFFF); vf[2 * e + 1] = h2f(w4[e] >> 16); }
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) st.acc[g][e] = fmaf(s[g][i], vf[e], st.acc[g][e]);
+    }
+}
+
+template <int G>
+struct Smem {
+    float o[4][G][D];
+    float ml[4][G][2];
+    float w[4][G], L[G];
+};
+
+// rows (kq) hold disjoint keys: park every row's 8 dims in LDS, reduce rows and waves in one pass; write the split's
+// partial O and (M, L) of heads hk * G + g
+template <int G>
+__device__ __forceinline__ void finish(State<G> &st, Smem<G> &sm, int hk, int sp, int NS, float *__restrict__ part_o,
+                                       float2 *__restrict__ part_ml) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = lane & 15, kq = lane >> 4;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) st.acc[g][e] = xsum16(st.acc[g][e]);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) st.acc[g][e] = xsum32(st.acc[g][e]);
+    if (kq == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            *(float4 *)&sm.o[wave][g][sub * 8] = make_float4(st.acc[g][0], st.acc[g][1], st.acc[g][2], st.acc[g][3]);
+            *(float4 *)&sm.o[wave][g][sub * 8 + 4] = make_float4(st.acc[g][4], st.acc[g][5], st.acc[g][6], st.acc[g][7]);
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) { sm.ml[wave][g][0] = st.m[g]; sm.ml[wave][g][1] = st.l[g]; }
+    }
+    __syncthreads();
+    if (tid < G) {                                        // per-head wave weights and the split's (M, L)
+        const int g = tid;
+        float M = -INFINITY;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) M = fmaxf(M, sm.ml[w][g][0]);
+        float L = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            const float wt = M == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(sm.ml[w][g][0] - M);
+            sm.w[w][g] = wt;
+            L = fmaf(wt, sm.ml[w][g][1], L);
+        }
+        sm.L[g] = L;
+        part_ml[(int64_t)(hk * G + g) * NS + sp] = make_float2(M, L);
+    }
+    __syncthreads();
+    for (int i = tid; i < G * D; i += 256) {
+        const int g = i / D, d = i % D;
+        float O = 0.0f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) O = fmaf(sm.w[w][g], sm.o[w][g][d], O);
+        part_o[((int64_t)(hk * G + g) * NS + sp) * D + d] = O;
+    }
+}
+
+}  // namespace fadec

@@ -102,12 +102,18 @@ __global__ void k_rope_qk_inplace(float *__restrict__ qkv, int64_t ld, int H, in
 
 #define FQ_BQ 64
 #define FQ_BK 64
-// flash attention over quantized caches, causal window [0, n_past + t]; grid (ceil(T/64), H), 256 threads; thread
-// (ty, tx): query rows 4ty..4ty+3, key columns tx + 16j, output dims tx*DPT..; q f32 rows of the staging (ld)
-template <int D, int TK, int TV>
-__global__ void __launch_bounds__(256) k_fa_q(const float *__restrict__ q, int64_t ldq, const void *kc, const void *vc,
-                                              float *__restrict__ out, int T, int H, int HKV, int64_t n_ctx,
-                                              int n_past_arg, const int32_t *__restrict__ n_past_dev, float scale) {
+// flash attention over quantized caches; grid (ceil(T/64), H), 256 threads; thread (ty, tx): query rows 4ty..4ty+3,
+// key columns tx + 16j, output dims tx*DPT..; q f32 at byte strides q_nb1 (query) / q_nb2 (head).
+// GG = 0: the runtime's caches (layout above), causal window [0, n_past + t].
+// GG = 1: GGML_OP_FLASH_ATTN_EXT's own form (the b1 backend): K / V views of ggml blocks (block_q8_0 / block_q4_0: f16 d
+// then the quants) at byte strides nb1 (position) / nb2 (kv head), all n_kv = n_past_arg keys under an explicit f16
+// mask row (a -inf key is skipped, otherwise s * scale + mask, ggml.c:15780-15800); null mask = no mask.
+struct FqView { int64_t k_nb1, k_nb2, v_nb1, v_nb2; const uint16_t *mask; int64_t mask_ld; };
+template <int D, int TK, int TV, int GG>
+__global__ void __launch_bounds__(256) k_fa_q(const float *__restrict__ q, int64_t q_nb1, int64_t q_nb2, const void *kc,
+                                              const void *vc, float *__restrict__ out, int T, int H, int HKV, int64_t n_ctx,
+                                              int n_past_arg, const int32_t *__restrict__ n_past_dev, float scale,
+                                              const FqView gv) {
     constexpr int DPT = D / 16, NB = D / 32;
     const int n_past = n_past_dev ? n_past_dev[0] : n_past_arg;
     const int qt = blockIdx.x, h = blockIdx.y;
@@ -125,7 +131,8 @@ __global__ void __launch_bounds__(256) k_fa_q(const float *__restrict__ q, int64
         const int r = i / NB, b = i % NB;
         float x[32];
         const bool ok = q0 + r < T;
-        for (int e = 0; e < 32; ++e) x[e] = ok ? q[(int64_t)(q0 + r) * ldq + (int64_t)h * D + b * 32 + e] : 0.0f;
+        const float *qr = (const float *)((const char *)q + (int64_t)(q0 + r) * q_nb1 + (int64_t)h * q_nb2) + b * 32;
+        for (int e = 0; e < 32; ++e) x[e] = ok ? qr[e] : 0.0f;
         float am = 0.0f;
         for (int e = 0; e < 32; ++e) am = fmaxf(am, fabsf(x[e]));
         const float id = am != 0.0f ? 127.f / am : 0.0f;
@@ -144,7 +151,7 @@ __global__ void __launch_bounds__(256) k_fa_q(const float *__restrict__ q, int64
         for (int j = 0; j < DPT; ++j) o[r][j] = 0.0f;
     }
     const int last_q = min(q0 + FQ_BQ, T) - 1;
-    const int kend = n_past + last_q + 1;
+    const int kend = GG ? n_past_arg : n_past + last_q + 1;
     const uint16_t *kd = (const uint16_t *)((const uint8_t *)kc + (TK == KT_Q8_0 ? n_ctx * ekv : n_ctx * ekv / 2));
     const uint16_t *vd = (const uint16_t *)((const uint8_t *)vc + (TV == KT_Q8_0 ? n_ctx * ekv : n_ctx * ekv / 2));
     for (int k0 = 0; k0 < kend; k0 += FQ_BK) {
@@ -154,30 +161,33 @@ __global__ void __launch_bounds__(256) k_fa_q(const float *__restrict__ q, int64
             const int64_t p = k0 + r;
             const bool ok = p < kend;
             const int64_t blk = p * (ekv / 32) + (int64_t)hk * NB + b;   // block index within the cache
+            // GG: the ggml block at (position p, kv head hk, block b) of each view: {f16 d, quants}
+            const uint8_t *gk = (const uint8_t *)kc + (ok ? p : 0) * gv.k_nb1 + (int64_t)hk * gv.k_nb2 + b * (TK == KT_Q8_0 ? 34 : 18);
+            const uint8_t *gvb = (const uint8_t *)vc + (ok ? p : 0) * gv.v_nb1 + (int64_t)hk * gv.v_nb2 + b * (TV == KT_Q8_0 ? 34 : 18);
             float kv[32], vv[32];
             if (TK == KT_Q8_0) {
-                const int8_t *s8 = (const int8_t *)kc + blk * 32;
+                const int8_t *s8 = GG ? (const int8_t *)(gk + 2) : (const int8_t *)kc + blk * 32;
                 for (int e = 0; e < 32; ++e) kv[e] = ok ? (float)s8[e] : 0.0f;
             } else {
-                const uint8_t *s4 = (const uint8_t *)kc + blk * 16;
+                const uint8_t *s4 = GG ? gk + 2 : (const uint8_t *)kc + blk * 16;
                 for (int j = 0; j < 16; ++j) {
                     const int byte = ok ? s4[j] : 0x88;
                     kv[j] = (float)((byte & 0xF) - 8); kv[j + 16] = (float)((byte >> 4) - 8);
                 }
             }
-            const float dv = ok ? h2f(vd[blk]) : 0.0f;
+            const float dv = ok ? h2f(GG ? *(const uint16_t *)gvb : vd[blk]) : 0.0f;
             if (TV == KT_Q8_0) {
-                const int8_t *s8 = (const int8_t *)vc + blk * 32;
+                const int8_t *s8 = GG ? (const int8_t *)(gvb + 2) : (const int8_t *)vc + blk * 32;
                 for (int e = 0; e < 32; ++e) vv[e] = ok ? __fmul_rn(dv, (float)s8[e]) : 0.0f;
             } else {
-                const uint8_t *s4 = (const uint8_t *)vc + blk * 16;
+                const uint8_t *s4 = GG ? gvb + 2 : (const uint8_t *)vc + blk * 16;
                 for (int j = 0; j < 16; ++j) {
                     const int byte = ok ? s4[j] : 0x88;
                     vv[j] = __fmul_rn(dv, (float)((byte & 0xF) - 8)); vv[j + 16] = __fmul_rn(dv, (float)((byte >> 4) - 8));
                 }
             }
             for (int e = 0; e < 32; ++e) { sK[r][b * 32 + e] = kv[e]; sV[r][b * 32 + e] = vv[e]; }
-            sKd[r][b] = ok ? h2f(kd[blk]) : 0.0f;
+            sKd[r][b] = ok ? h2f(GG ? *(const uint16_t *)gk : kd[blk]) : 0.0f;
         }
         __syncthreads();
         float s[4][4];
@@ -217,7 +227,12 @@ __global__ void __launch_bounds__(256) k_fa_q(const float *__restrict__ q, int64
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int p = k0 + tx + 16 * j;
-                s[r][j] = (qi < T && p <= qpos) ? s[r][j] * scale : -INFINITY;
+                if constexpr (GG) {
+                    const float mv = (gv.mask && qi < T && p < kend) ? h2f(gv.mask[(int64_t)qi * gv.mask_ld + p]) : 0.0f;
+                    s[r][j] = (qi < T && p < kend && mv != -INFINITY) ? __fadd_rn(s[r][j] * scale, mv) : -INFINITY;
+                } else {
+                    s[r][j] = (qi < T && p <= qpos) ? s[r][j] * scale : -INFINITY;
+                }
                 mx = fmaxf(mx, s[r][j]);
             }
             mx = max16_f(mx);
@@ -306,7 +321,32 @@ int kcpp_flash_attn_q(int tk, int tv, const float *q, int64_t ldq, const void *k
     if (H % HKV || (D != 128 && D != 64)) return -1;
     const dim3 g((unsigned)((T + FQ_BQ - 1) / FQ_BQ), (unsigned)H);
     hipStream_t s = (hipStream_t)stream;
-#define FQ(DD, A, B) hipLaunchKernelGGL((k_fa_q<DD, A, B>), g, dim3(256), 0, s, q, ldq, kc, vc, out, T, H, HKV, n_ctx, n_past, n_past_dev, scale)
+    const FqView gv{0, 0, 0, 0, nullptr, 0};
+#define FQ(DD, A, B) hipLaunchKernelGGL((k_fa_q<DD, A, B, 0>), g, dim3(256), 0, s, q, ldq * 4, (int64_t)D * 4, kc, vc, out, T, H, HKV, n_ctx, n_past, n_past_dev, scale, gv)
+#define FQD(DD)                                                     \
+    if (tk == KT_Q8_0 && tv == KT_Q8_0) FQ(DD, KT_Q8_0, KT_Q8_0);   \
+    else if (tk == KT_Q8_0 && tv == KT_Q4_0) FQ(DD, KT_Q8_0, KT_Q4_0); \
+    else if (tk == KT_Q4_0 && tv == KT_Q8_0) FQ(DD, KT_Q4_0, KT_Q8_0); \
+    else if (tk == KT_Q4_0 && tv == KT_Q4_0) FQ(DD, KT_Q4_0, KT_Q4_0); \
+    else return -2;
+    if (D == 128) { FQD(128) } else { FQD(64) }
+#undef FQD
+#undef FQ
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// GGML_OP_FLASH_ATTN_EXT over quantized K / V views (the b1 backend): q f32 [T][H][D] at byte strides q_nb1 / q_nb2,
+// K / V views of ggml Q8_0 / Q4_0 blocks at byte strides nb1 (position) / nb2 (kv head), optional f16 mask [T][n_kv]
+// (row stride mask_ld elements), out f32 [T][H][D]
+int kcpp_flash_attn_ext_q(int tk, int tv, const float *q, int64_t q_nb1, int64_t q_nb2, const void *kc, int64_t k_nb1,
+                          int64_t k_nb2, const void *vc, int64_t v_nb1, int64_t v_nb2, const uint16_t *mask,
+                          int64_t mask_ld, float *out, int T, int H, int HKV, int D, int n_kv, float scale, void *stream) {
+    if (H % HKV || (D != 128 && D != 64) || n_kv < 1 || T < 1) return -1;
+    const dim3 g((unsigned)((T + FQ_BQ - 1) / FQ_BQ), (unsigned)H);
+    hipStream_t s = (hipStream_t)stream;
+    const FqView gv{k_nb1, k_nb2, v_nb1, v_nb2, mask, mask_ld};
+#define FQ(DD, A, B) hipLaunchKernelGGL((k_fa_q<DD, A, B, 1>), g, dim3(256), 0, s, q, q_nb1, q_nb2, kc, vc, out, T, H, HKV, (int64_t)0, n_kv, (const int32_t *)nullptr, scale, gv)
 #define FQD(DD)                                                     \
     if (tk == KT_Q8_0 && tv == KT_Q8_0) FQ(DD, KT_Q8_0, KT_Q8_0);   \
     else if (tk == KT_Q8_0 && tv == KT_Q4_0) FQ(DD, KT_Q8_0, KT_Q4_0); \

@@ -14,6 +14,8 @@
 //                structure-of-arrays Q4_0 / Q8_0 / Q2_K / Q3_K / Q6_K layouts), built once per weight on first use and kept until
 //                the weight's buffer is written again; F16 / F32 weight: kcpp_ggml_mul_mat_f
 //   GET_ROWS     quantized: kcpp_get_rows on the native image; F16 / F32: kcpp_ggml_get_rows
+//   MUL_MAT_ID   quantized experts: expert-indexed mat-vecs reading the ids on the device (few rows), else the ids
+//                on the host and one mat-vec / GEMM per expert over gathered columns (mul_mat_id below)
 //   FLASH_ATTN_EXT  kcpp_flash_attn_ext (graph-form Q view, F16 K/V cache views, F16 mask)
 //   RMS_NORM, ROPE (NORM / NEOX, YaRN), SOFT_MAX, ADD/SUB/MUL/DIV (broadcast), SCALE, UNARY (SILU/NEG/RELU),
 //   CPY/CONT/DUP (F32 <-> F16), ARGSORT, SUM_ROWS: the general-layout kernels of ggml_ops.hip
@@ -38,6 +40,7 @@
 #include "../../include/kcpp_ggml_backend.h"
 #include "../../include/kcpp_mi355x.h"
 #include "../../include/kcpp_synth.h"
+#include "kcpp_internal.h"
 
 namespace {
 
@@ -274,13 +277,14 @@ struct BackendCtx {
     int device;
     std::string name;
     hipStream_t stream;
-    Scratch act, ws, fa;
+    Scratch act, ws, fa, ids, xg, yg;
     bool fa_exact = false;     // attention in the reference CPU's order with its f16 accumulator (attn_exact.hip)
 };
 
 // the native image of weight w for target layout `tt` (kcpp type id); w itself when the layouts coincide
+// (a 3-D MUL_MAT_ID expert tensor is repacked slice by slice: expert e's image starts at e * nb[2], like its bytes)
 const void *native_image(BackendCtx *bc, const kggml_tensor *w, int tt) {
-    const int64_t K = w->ne[0], N = w->ne[1] * w->ne[2] * w->ne[3];
+    const int64_t K = w->ne[0], N = w->ne[1] * w->ne[2] * w->ne[3], NS = w->ne[2] * w->ne[3];
     if (tt == w->type && (tt == KT_Q4_K || tt == KT_Q5_K)) return w->data;      // kcpp layout = ggml layout
     kggml_backend_buffer_t buf = w->view_src ? w->view_src->buffer : w->buffer;
     const unsigned gen = buffer_is_ours(buf) ? ((BufCtx *)buf->context)->gen : 0;
@@ -291,7 +295,12 @@ const void *native_image(BackendCtx *bc, const kggml_tensor *w, int tt) {
     if (it != g_images.end()) { hipStreamSynchronize(bc->stream); hipFree(it->second.d); g_images.erase(it); }
     void *d = nullptr;
     if (hipMalloc(&d, row_size(w->type, K) * N) != hipSuccess) { (void)hipGetLastError(); return nullptr; }
-    if (kcpp_weight_repack(tt, w->data, d, K, N, 0, bc->stream) != 0) { hipFree(d); return nullptr; }
+    const int64_t N1 = N / NS, sb = (int64_t)row_size(w->type, K) * N1;
+    for (int64_t e = 0; e < NS; ++e)
+        if (kcpp_weight_repack(tt, (const char *)w->data + e * sb, (char *)d + e * sb, K, N1, 0, bc->stream) != 0) {
+            hipFree(d);
+            return nullptr;
+        }
     g_images[key] = Image{d, buf, gen};
     return d;
 }
@@ -349,6 +358,12 @@ bool supports(const kggml_tensor *op) {
         return matmul_quant_ok(a->type) && a->ne[2] == 1 && a->ne[3] == 1 && is_contiguous(a) && b->nb[0] == 4 &&
                b->ne[2] == 1 && b->ne[3] == 1 && is_contiguous(op) && a->ne[0] % 256 == 0;
     }
+    case KGGML_OP_MUL_MAT_ID: {             // ggml_cuda_mul_mat_id (ggml-cuda.cu:2003-2139): quantized experts
+        const kggml_tensor *a = op->src[0], *b = op->src[1], *ids = op->src[2];
+        return f32(op) && f32(b) && ids && ids->type == KGGML_TYPE_I32 && matmul_quant_ok(a->type) && a->ne[3] == 1 &&
+               is_contiguous(a) && a->ne[0] % 256 == 0 && b->nb[0] == 4 && op->nb[0] == 4 && ids->nb[0] == 4 &&
+               b->ne[3] == 1 && ids->ne[1] == b->ne[2] && op->ne[1] == ids->ne[0] && op->ne[2] == ids->ne[1];
+    }
     case KGGML_OP_FLASH_ATTN_EXT: {
         const kggml_tensor *q = op->src[0], *k = op->src[1], *v = op->src[2], *m = op->src[3];
         if (!f32(op) || !f32(q) || k->type != KGGML_TYPE_F16 || v->type != KGGML_TYPE_F16) return false;
@@ -362,6 +377,92 @@ bool supports(const kggml_tensor *op) {
     default:
         return false;
     }
+}
+
+// GGML_OP_MUL_MAT_ID (ggml_cuda_mul_mat_id, ggml-cuda.cu:2003-2139): dst[:, j, t] = as[:, :, ids[j, t]] . b[:, j % ne11, t].
+// A handful of rows (decode): one expert-indexed mat-vec per (j, t) that reads its expert id on the device
+// (DecArgs.eid) and quantizes its own column (prologue 2) -- no host synchronisation.  More rows (prefill): the ids
+// come to the host (the reference synchronises here too), the columns of each expert are gathered, quantized and
+// multiplied by one mat-vec / MFMA GEMM per expert, and the rows scattered back.
+bool mul_mat_id(BackendCtx *bc, kggml_tensor *n) {
+    hipStream_t s = bc->stream;
+    const kggml_tensor *as = n->src[0], *b = n->src[1], *ids = n->src[2];
+    const int64_t K = as->ne[0], N = as->ne[1], E = as->ne[2];
+    const int64_t n_ids = ids->ne[0], n_tok = ids->ne[1], ne11 = b->ne[1];
+    const int tt = matmul_layout(as->type, K);
+    const char *W = (const char *)native_image(bc, as, tt);
+    if (!W) return set_err("mul_mat_id: native image allocation failed");
+    const int64_t eb = (int64_t)as->nb[2];
+    auto chk = [&](int rc, const char *what) {
+        if (rc == 0) return true;
+        char msg[256];
+        snprintf(msg, sizeof msg, "mul_mat_id: %s failed rc=%d on node '%s' (%s)", what, rc, n->name, kcpp_last_error());
+        return set_err(msg);
+    };
+    if (n_ids * n_tok <= 16) {
+        int rc = 0;
+        for (int64_t t = 0; t < n_tok && rc == 0; ++t)
+            for (int64_t j = 0; j < n_ids && rc == 0; ++j) {
+                DecArgs d;
+                memset(&d, 0, sizeof d);
+                d.K = K; d.nseg = 1; d.W[0] = (const uint8_t *)W; d.N[0] = N;
+                d.Y[0] = (float *)((char *)n->data + j * n->nb[1] + t * n->nb[2]);
+                d.x = (const float *)((const char *)b->data + (j % ne11) * b->nb[1] + t * b->nb[2]);
+                d.eid = (const int32_t *)((const char *)ids->data + j * ids->nb[0] + t * ids->nb[1]);
+                d.ebytes = eb;
+                rc = kcpp_gemv_dec(tt, &d, 0, 2, 1, s);
+                if (rc != 0 && (t > 0 || j > 0)) return chk(rc, "expert mat-vec");
+            }
+        if (rc == 0) return true;
+        // rc on the first (j, t): this type / shape has no fused expert mat-vec; the grouped path below
+    }
+    std::vector<int32_t> idh((size_t)n_ids * n_tok);
+    if (hipStreamSynchronize(s) != hipSuccess) return set_err("mul_mat_id: stream error");
+    for (int64_t t = 0; t < n_tok; ++t)
+        if (hipMemcpy(idh.data() + t * n_ids, (const char *)ids->data + t * ids->nb[1], (size_t)n_ids * 4,
+                      hipMemcpyDeviceToHost) != hipSuccess)
+            return set_err("mul_mat_id: ids copy failed");
+    // per expert: the (source column, destination row) byte offsets of its (j, t), in (t, j) order
+    std::vector<std::vector<int64_t>> so(E), dof(E);
+    for (int64_t t = 0; t < n_tok; ++t)
+        for (int64_t j = 0; j < n_ids; ++j) {
+            const int32_t e = idh[t * n_ids + j];
+            if (e < 0 || e >= E) return set_err("mul_mat_id: expert id out of range");
+            so[e].push_back((j % ne11) * (int64_t)b->nb[1] + t * (int64_t)b->nb[2]);
+            dof[e].push_back(j * (int64_t)n->nb[1] + t * (int64_t)n->nb[2]);
+        }
+    const int64_t rows = n_ids * n_tok;
+    int64_t *offs = (int64_t *)bc->ids.get((size_t)rows * 16 + 256);
+    float *xg = (float *)bc->xg.get((size_t)rows * K * 4 + 256);
+    float *yg = (float *)bc->yg.get((size_t)rows * N * 4 + 256);
+    void *act = bc->act.get((size_t)kcpp_act_bytes(as->type, K, rows) + 256);
+    if (!offs || !xg || !yg || !act) return set_err("mul_mat_id: scratch allocation failed");
+    std::vector<int64_t> hoff;
+    hoff.reserve((size_t)rows * 2);
+    for (int64_t e = 0; e < E; ++e) hoff.insert(hoff.end(), so[e].begin(), so[e].end());
+    for (int64_t e = 0; e < E; ++e) hoff.insert(hoff.end(), dof[e].begin(), dof[e].end());
+    if (hipMemcpy(offs, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+        return set_err("mul_mat_id: offsets upload failed");
+    int64_t r0 = 0;
+    for (int64_t e = 0; e < E; ++e) {
+        const int64_t c = (int64_t)so[e].size();
+        if (c == 0) continue;
+        if (!chk(kcpp_rows_move_f32(b->data, offs + r0, 0, xg, nullptr, K * 4, K, (int)c, s), "gather") ||
+            !chk(kcpp_quantize_act(kcpp_vec_dot_type(as->type), xg, K, act, K, c, s), "quantize_act"))
+            return false;
+        const void *We = W + e * eb;
+        if (c <= 8) {
+            if (!chk(kcpp_gemv(tt, We, nullptr, K, N, act, c, yg, N, nullptr, 0, 0, s), "gemv")) return false;
+        } else {
+            void *ws = bc->ws.get((size_t)kcpp_gemm_workspace_bytes(tt, K, N, c) + 256);
+            if (!ws) return set_err("mul_mat_id: GEMM workspace allocation failed");
+            if (!chk(kcpp_gemm(tt, We, nullptr, K, N, act, c, yg, N, nullptr, 0, 0, ws, s), "gemm")) return false;
+        }
+        if (!chk(kcpp_rows_move_f32(yg, nullptr, N * 4, n->data, offs + rows + r0, 0, N, (int)c, s), "scatter"))
+            return false;
+        r0 += c;
+    }
+    return true;
 }
 
 bool compute_node(BackendCtx *bc, kggml_tensor *n) {
@@ -464,6 +565,8 @@ bool compute_node(BackendCtx *bc, kggml_tensor *n) {
         if (!ws) return set_err("mul_mat: GEMM workspace allocation failed");
         return chk(kcpp_gemm(tt, W, nullptr, K, N, act, M, (float *)n->data, N, nullptr, 0, 0, ws, s), "gemm");
     }
+    case KGGML_OP_MUL_MAT_ID:
+        return mul_mat_id(bc, n);
     case KGGML_OP_FLASH_ATTN_EXT: {
         const kggml_tensor *q = a, *k = b, *v = n->src[2], *m = n->src[3];
         const int T = (int)q->ne[1], H = (int)q->ne[2], HKV = (int)k->ne[2], n_kv = (int)k->ne[1];
@@ -491,7 +594,7 @@ void be_free(kggml_backend_t be) {
     BackendCtx *c = (BackendCtx *)be->context;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    for (Scratch *sc : {&c->act, &c->ws, &c->fa}) if (sc->p) hipFree(sc->p);
+    for (Scratch *sc : {&c->act, &c->ws, &c->fa, &c->ids, &c->xg, &c->yg}) if (sc->p) hipFree(sc->p);
     hipStreamDestroy(c->stream);
     delete c;
     delete be;

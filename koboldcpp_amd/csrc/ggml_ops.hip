@@ -291,6 +291,15 @@ __global__ void __launch_bounds__(256) k_mul_mat_f(const char *__restrict__ w, T
     if (lane == 0) *(float *)(d + n * td.nb[0] + m * td.nb[1] + i12 * td.nb[2] + i13 * td.nb[3]) = acc;
 }
 
+__global__ void k_rows_move(const char *__restrict__ src, const int64_t *__restrict__ soffs, int64_t sld,
+                            char *__restrict__ dst, const int64_t *__restrict__ doffs, int64_t dld, int64_t K) {
+    const int64_t i = blockIdx.y, e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= K) return;
+    const float *s = (const float *)(src + (soffs ? soffs[i] : i * sld));
+    float *d = (float *)(dst + (doffs ? doffs[i] : i * dld));
+    d[e] = s[e];
+}
+
 extern "C" {
 
 int kcpp_ggml_binary(int op, const void *a, const kcpp_tdesc *ta, const void *b, const kcpp_tdesc *tb, void *d,
@@ -457,6 +466,17 @@ int kcpp_ggml_mul_mat_f(int wtype, const void *w, const kcpp_tdesc *tw, const fl
                            (const char *)x, td_of(tx), (char *)d, td_of(td));
     else
         return -2;
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// row moves of the MoE mat-mul (ggml_cuda_mul_mat_id's k_copy_src1_to_contiguous / k_copy_dst_from_contiguous,
+// ggml-cuda.cu:1954-2001): dst row i = src row i, rows addressed by byte offsets (soffs / doffs) or by a stride
+int kcpp_rows_move_f32(const void *src, const int64_t *soffs, int64_t sld, void *dst, const int64_t *doffs, int64_t dld,
+                       int64_t K, int n, void *stream) {
+    if (n <= 0 || K <= 0) return 0;
+    hipLaunchKernelGGL(k_rows_move, dim3((unsigned)((K + 255) / 256), (unsigned)n), dim3(256), 0, (hipStream_t)stream,
+                       (const char *)src, soffs, sld, (char *)dst, doffs, dld, K);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

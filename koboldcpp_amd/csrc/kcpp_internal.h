@@ -2,6 +2,9 @@
 #pragma once
 #include <stdint.h>
 
+// bytes in front of the flash-attention workspace's partials (spare header words for in-launch hand-offs)
+#define KCPP_FA_WS_HEADER 2048
+
 extern "C" {
 int kcpp_weight_repack(int type, const void *src_ggml, void *dst_kcpp, int64_t K, int64_t N, int to_ggml, void *stream);
 int kcpp_weight_synth(int type, uint64_t seed, uint64_t tid, void *dst, int64_t K, int64_t N, void *stream);

@@ -107,7 +107,8 @@ struct kcpp_model {
     void *act = nullptr, *act2 = nullptr, *fa_ws = nullptr, *gemm_ws = nullptr;
     void *gemm_ws2 = nullptr;               // prefill: attn_v GEMM on the side stream (q|k fused layers)
     size_t act_sz = 0, gemm_ws_sz = 0;
-    int32_t *tok_dev = nullptr, *pos_dev = nullptr, *argmax_dev = nullptr;
+    int32_t *tok_dev = nullptr, *pos_dev = nullptr, *argmax_dev = nullptr;   // pos_dev = {position, epoch}
+    void *gran = nullptr;            // granules of the fused q|k|v + attention launch (dec_fused.hip)
     void *argmax_ws = nullptr;       // ARGMAX_BLOCKS (value, index) partials
     int32_t *moe_ids = nullptr;      // [ubatch][n_expert_used] selected experts (device)
     float *moe_w = nullptr;          // [ubatch][n_expert_used] normalized weights (device)
@@ -128,6 +129,7 @@ struct kcpp_model {
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
     bool q81 = false;                // Q4_1 / Q5_1 weights (Q8_1 activations): single-token decode on the per-op path
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
+    bool fuse_qkv_att = false;       // single-token q|k|v and attention partials in one launch (dec_fused.hip; opt-in, see DESIGN)
     int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
     hipGraphExec_t g_exec = nullptr;
     hipStream_t side = nullptr;             // second branch of the decode step (independent q|k|v launches)
@@ -376,6 +378,13 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     }
     // flash-attention tickets must start at zero (the merging workgroup resets its own)
     if (hipMemset(m->fa_ws, 0, kcpp_fa_workspace_bytes(16, H, hp->n_ctx)) != hipSuccess) return fail("fa ws memset");
+    {   // the epoch (pos_dev[1]) starts at 1 so that no zeroed granule carries a live tag
+        const int32_t pe[2] = {0, 1};
+        if (hipMalloc(&m->gran, kcpp_dec_gran_bytes(H, HKV)) != hipSuccess ||
+            hipMemset(m->gran, 0, kcpp_dec_gran_bytes(H, HKV)) != hipSuccess ||
+            hipMemcpy(m->pos_dev, pe, 8, hipMemcpyHostToDevice) != hipSuccess)
+            return fail("granule buffer");
+    }
     if (has_output) {
         if (hipMalloc(&m->logits, (size_t)hp->n_vocab * 4) != hipSuccess) return fail("logits alloc");
         if (hipHostMalloc((void **)&m->logits_pin, (size_t)hp->n_vocab * 4, hipHostMallocDefault) != hipSuccess)
@@ -406,7 +415,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     for (void *p : {(void *)m->moe_ids_h, (void *)m->moe_w_h, (void *)m->moe_rows_h, (void *)m->moe_rw_h})
         if (p) hipHostFree(p);
     F(m->x); F(m->qkv); F(m->attn); F(m->h); F(m->logits); F(m->q16); F(m->act); F(m->act2); F(m->fa_ws);
-    F(m->gemm_ws); F(m->gemm_ws2); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
+    F(m->gemm_ws); F(m->gemm_ws2); F(m->tok_dev); F(m->pos_dev); F(m->gran); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
     F(m->kv_scratch); F(m->shift_cs);
     if (m->pin) hipHostFree(m->pin);
     if (m->logits_pin) hipHostFree(m->logits_pin);
@@ -637,6 +646,16 @@ extern "C" int kcpp_model_moe_ids(kcpp_model *m, int32_t *out, int n) {
     if (!m->moe_ids_h || n < 0 || n > m->ub * std::max(1, m->hp.n_expert_used)) { g_err = "moe ids"; return -1; }
     RT_CHECK(hipStreamSynchronize(m->stream));
     memcpy(out, m->moe_ids_h, (size_t)n * 4);
+    return 0;
+}
+extern "C" int kcpp_model_fused_error(kcpp_model *m) {
+    RT_CHECK(hipSetDevice(m->device));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    return kcpp_dec_fused_error(m->gran, m->hp.n_head, m->hp.n_head_kv);
+}
+extern "C" int kcpp_model_set_decode_fusion(kcpp_model *m, int enable) {
+    m->fuse_qkv_att = enable != 0;
+    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
     return 0;
 }
 extern "C" int kcpp_model_set_fa_exact(kcpp_model *m, int enable) {
@@ -870,6 +889,20 @@ static int forward_layers_dec(kcpp_model *m) {
             }
             qty[nq++] = ty;
         }
+        // q|k|v + attention partials in one launch (dec_fused.hip), then the combine; -3: the two-kernel path below
+        int fused_rc = -3;
+        if (m->fuse_qkv_att && !m->fa_exact) {
+            if (nq == 2 && qty[0] == KT_Q4_K_RS && qty[1] == KT_Q6_K_RS && qa[0].nseg == 2 && qa[1].nseg == 1 &&
+                qa[1].role[0] == 2) {
+                DecArgs c = qa[0];
+                c.W[2] = qa[1].W[0]; c.N[2] = qa[1].N[0]; c.role[2] = 2; c.nseg = 3;
+                fused_rc = kcpp_dec_qkv_att(1, &c, m->fa_ws, m->gran, il, (int)H, (int)HKV, kq_scale, m->attn, s);
+            } else if (nq == 1 && qty[0] == KT_Q4_K_RS && qa[0].nseg == 3) {
+                fused_rc = kcpp_dec_qkv_att(0, &qa[0], m->fa_ws, m->gran, il, (int)H, (int)HKV, kq_scale, m->attn, s);
+            }
+            if (fused_rc != -3) RC(fused_rc);
+        }
+        if (fused_rc != 0) {
         int mixed_rc = -3;
         if (nq == 2 && qty[0] == KT_Q4_K_RS && qty[1] == KT_Q6_K_RS && qa[0].nseg == 2 && qa[1].nseg == 1 &&
             qa[1].role[0] == 2) {
@@ -889,6 +922,7 @@ static int forward_layers_dec(kcpp_model *m) {
         else
             RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, nullptr, m->fa_ws, 1, (int)H, (int)HKV, (int)D, 0, m->pos_dev,
                                hp.n_ctx, kq_scale, 1, s));
+        }
         {   // x += wo . attn
             DecArgs a;
             memset(&a, 0, sizeof a);
@@ -1195,10 +1229,10 @@ __global__ void __launch_bounds__(256) k_argmax_final(const float2 *__restrict__
     if (threadIdx.x == 0) {
         out[0] = i;
         if (tok) tok[0] = i;
-        if (pos) pos[0] += 1;                 // the next single-token step's position
+        if (pos) { pos[0] += 1; pos[1] += 1; }   // the next single-token step's position and epoch
     }
 }
-__global__ void k_pos_step(int32_t *pos) { pos[0] += 1; }
+__global__ void k_pos_step(int32_t *pos) { pos[0] += 1; pos[1] += 1; }
 static int launch_argmax(kcpp_model *m, bool step_pos) {
     hipLaunchKernelGGL(k_argmax_part, dim3(ARGMAX_BLOCKS), dim3(256), 0, m->stream, m->logits, m->hp.n_vocab,
                        (float2 *)m->argmax_ws);

@@ -92,6 +92,8 @@ _SIGS = {
     "kcpp_model_set_row_split": [P, I, P, P],
     "kcpp_row_split_range": [I64, I, P, I, P, P],
     "kcpp_model_set_fa_exact": [P, I],
+    "kcpp_model_set_decode_fusion": [P, I],
+    "kcpp_model_fused_error": [P],
     "kcpp_model_moe_ids": [P, P, I],
     "kcpp_flash_attn_exact": [P, P, P, P, I, I, I, I, I, P, Fl, P],
     "kcpp_model_weight_bytes": [P],
@@ -305,6 +307,13 @@ class Model:
 
     def set_fused_decode(self, on):
         _L.kcpp_model_set_fused_decode(self.m, int(on))
+
+    def set_decode_fusion(self, on):
+        """single-token q|k|v + attention in one launch (default on; kcpp_dec_qkv_att)"""
+        _chk(_L.kcpp_model_set_decode_fusion(self.m, int(on)), "set_decode_fusion")
+
+    def fused_error(self):
+        return int(_L.kcpp_model_fused_error(self.m))
 
     def set_fa_exact(self, on):
         """strict-parity attention (reference order, f16 accumulation); see kcpp_flash_attn_exact"""

@@ -323,3 +323,89 @@ def test_unsupported_ops_are_refused(env):
     w2 = G.ggml_new_tensor_2d(ctx, R.Q4_K, 256, 4)
     assert G.ggml_backend_supports_op(be, G.ggml_mul_mat(ctx, w2, x))
     G.ggml_free(ctx)
+
+
+def _moe_sigs(G):
+    for n, a in {"ggml_mul_mat_id": [P, P, P, P], "ggml_top_k": [P, P, I], "ggml_soft_max": [P, P],
+                 "ggml_sum_rows": [P, P], "ggml_div": [P, P, P], "ggml_view_2d": [P, P, I64, I64, SZ, SZ]}.items():
+        fn = getattr(G, n)
+        fn.argtypes, fn.restype = a, P
+
+
+MMID_CASES = [(R.Q4_K, 1), (R.Q4_K, 3), (R.Q4_K, 24), (R.Q5_K, 1), (R.Q5_K, 24), (R.Q6_K, 2), (R.Q6_K, 24),
+              (R.Q8_0, 1), (R.Q8_0, 24), (R.Q4_0, 3), (R.Q2_K, 1), (R.Q3_K, 24)]
+
+
+@pytest.mark.parametrize("case", MMID_CASES, ids=lambda c: "t%d_T%d" % c)
+def test_mul_mat_id_vs_reference_cpu(env, case):
+    """GGML_OP_MUL_MAT_ID (ggml_cuda_mul_mat_id, ggml-cuda.cu:2003-2139) with 8 experts, 2 used: src1 broadcast over
+    the used slots (ne11 = 1, the up / gate form) and one column per slot (ne11 = 2, the down form); T <= 8 runs the
+    device-routed expert mat-vecs, T = 24 the host-grouped per-expert GEMMs"""
+    G, L, be = env
+    _moe_sigs(G)
+    t, T = case
+    Kd, N, E, k = 1024, 512, 8, 2
+    rng = np.random.default_rng(t * 100 + T)
+    w = np.concatenate([R.synth(t, 6, 500 + e, Kd, N) for e in range(E)])
+    ids = np.stack([rng.permutation(E)[:k] for _ in range(T)]).astype(np.int32)       # [T][k]
+    for ne11 in (1, k):
+        x = rng.standard_normal((T, ne11, Kd)).astype(np.float32)
+
+        def build(ctx):
+            W = G.ggml_new_tensor_3d(ctx, t, Kd, N, E)
+            X = G.ggml_new_tensor_3d(ctx, R.F32, Kd, ne11, T)
+            Ix = G.ggml_new_tensor_2d(ctx, 26, k, T)
+            return [W, X, Ix], G.ggml_mul_mat_id(ctx, W, X, Ix)
+        ours, ref = run_both(G, be, build, lambda: [w, x, ids])
+        assert rel(ours, ref) <= 3e-6, (ne11, rel(ours, ref))
+
+
+@pytest.mark.parametrize("T", [1, 5, 40])
+def test_moe_ffn_graph_vs_reference_cpu(env, T):
+    """llm_build_moe_ffn (src/llama.cpp:9416-9514) at Mixtral's shape ratios (n_embd 1024, n_ff 1536, 8 experts,
+    top-2; Q5_K gate / up, Q6_K down, F32 router): router mul_mat, soft_max, top_k (argsort + view), get_rows of the
+    probabilities, sum_rows + div normalisation, MUL_MAT_ID x 3, silu, mul, weighting, slot views summed --
+    every node supported by this backend, the result equal to the reference CPU backend's"""
+    G, L, be = env
+    _moe_sigs(G)
+    E_, Fd, NE, k = 1024, 1536, 8, 2
+    rng = np.random.default_rng(T)
+    router = (rng.standard_normal((NE, E_)) * 0.05).astype(np.float32)
+    up = np.concatenate([R.synth(R.Q5_K, 7, 600 + e, E_, Fd) for e in range(NE)])
+    gate = np.concatenate([R.synth(R.Q5_K, 7, 700 + e, E_, Fd) for e in range(NE)])
+    down = np.concatenate([R.synth(R.Q6_K, 7, 800 + e, Fd, E_) for e in range(NE)])
+    x = rng.standard_normal((T, E_)).astype(np.float32)
+
+    def build(ctx):
+        Rt = G.ggml_new_tensor_2d(ctx, R.F32, E_, NE)
+        Up = G.ggml_new_tensor_3d(ctx, R.Q5_K, E_, Fd, NE)
+        Gt = G.ggml_new_tensor_3d(ctx, R.Q5_K, E_, Fd, NE)
+        Dn = G.ggml_new_tensor_3d(ctx, R.Q6_K, Fd, E_, NE)
+        X = G.ggml_new_tensor_2d(ctx, R.F32, E_, T)
+        logits = G.ggml_mul_mat(ctx, Rt, X)
+        probs = G.ggml_soft_max(ctx, logits)
+        sel = G.ggml_top_k(ctx, probs, k)
+        wts = G.ggml_get_rows(ctx, G.ggml_reshape_3d(ctx, probs, 1, NE, T), sel)
+        wts = G.ggml_reshape_2d(ctx, wts, k, T)
+        wts = G.ggml_div(ctx, wts, G.ggml_sum_rows(ctx, wts))
+        wts = G.ggml_reshape_3d(ctx, wts, 1, k, T)
+        cur = G.ggml_reshape_3d(ctx, X, E_, 1, T)
+        u = G.ggml_mul_mat_id(ctx, Up, cur, sel)
+        g = G.ggml_silu(ctx, G.ggml_mul_mat_id(ctx, Gt, cur, sel))
+        ex = G.ggml_mul(ctx, G.ggml_mul_mat_id(ctx, Dn, G.ggml_mul(ctx, u, g), sel), wts)
+        nb1 = E_ * 4
+        out = G.ggml_view_2d(ctx, ex, E_, T, nb1 * k, 0)
+        for i in range(1, k):
+            out = G.ggml_add(ctx, out, G.ggml_view_2d(ctx, ex, E_, T, nb1 * k, i * nb1))
+        build.graph_out = out
+        return [Rt, Up, Gt, Dn, X], out
+
+    ctx = G.ggml_init(InitParams(64 << 20, None, True))
+    _, out = build(ctx)
+    g = G.ggml_new_graph(ctx)
+    G.ggml_build_forward_expand(g, out)
+    unsupported = [i for i in range(G.ggml_graph_n_nodes(g)) if not G.ggml_backend_supports_op(be, G.ggml_graph_node(g, i))]
+    G.ggml_free(ctx)
+    assert not unsupported, unsupported
+    ours, ref = run_both(G, be, build, lambda: [router, up, gate, down, x])
+    assert rel(ours, ref) <= 2e-5, rel(ours, ref)
