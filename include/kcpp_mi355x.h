@@ -234,6 +234,15 @@ int kcpp_rows_move_f32(const void *src, const int64_t *soffs, int64_t sld, void 
 int kcpp_flash_attn_ext(const float *q, int64_t q_nb1, int64_t q_nb2, const uint16_t *kc, const uint16_t *vc,
                         const uint16_t *mask, int64_t mask_ld, float *out, void *ws, int T, int H, int HKV, int D,
                         int n_kv, float scale, void *stream);
+/* the same over quantized K / V views (--quantkv): tk / tv = KT_Q8_0 / KT_Q4_0, views of ggml blocks at byte strides
+ * nb1 (position) / nb2 (kv head); q quantized to Q8_0 per 32-block and integer block dots, V dequantized, f32
+ * accumulation (ggml_compute_forward_flash_attn_ext_f16's quantized branch, ggml.c:15748-15851); D 64 or 128 */
+/* GGML_OP_CPY f32 -> Q8_0 / Q4_0 (KT_ ids) of n contiguous values (n % 32 == 0) into ggml blocks: the reference's
+ * from_float (quantize_row_q8_0 AVX2 / quantize_row_q4_0_ref), byte for byte */
+int kcpp_cpy_f32_q(int type, const float *src, int64_t n, void *dst, void *stream);
+int kcpp_flash_attn_ext_q(int tk, int tv, const float *q, int64_t q_nb1, int64_t q_nb2, const void *kc, int64_t k_nb1,
+                          int64_t k_nb2, const void *vc, int64_t v_nb1, int64_t v_nb2, const uint16_t *mask,
+                          int64_t mask_ld, float *out, int T, int H, int HKV, int D, int n_kv, float scale, void *stream);
 
 /* ---------- 2. Llama runtime ---------- */
 typedef struct kcpp_hparams {

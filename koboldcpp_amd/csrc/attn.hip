@@ -710,11 +710,17 @@ int kcpp_flash_attn_ext(const float *q, int64_t q_nb1, int64_t q_nb2, const uint
                         const uint16_t *mask, int64_t mask_ld, float *out, void *ws, int T, int H, int HKV, int D,
                         int n_kv, float scale, void *stream) {
     hipStream_t s = (hipStream_t)stream;
-    if (D != 128 || H % HKV || H / HKV > FA_MAXG || (H % 2) || n_kv < 1) return -1;
+    if ((D != 128 && D != 64) || H % HKV || H / HKV > FA_MAXG || (H % 2) || n_kv < 1) return -1;
     uint16_t *q16 = (uint16_t *)((uint8_t *)ws + ((kcpp_fa_workspace_bytes(T, H, n_kv) + 255) & ~(int64_t)255));
     hipLaunchKernelGGL(k_q_to_f16, dim3(T, H), dim3(128), 0, s, (const char *)q, q_nb1, q_nb2, T, H, D, q16);
     KCPP_CHECK(hipGetLastError());
     if (mask_ld < 0) mask_ld = 0;
+    if (D == 64) {      // 64-dim heads (TinyLlama class): the tiled kernel for every T, under the explicit mask
+        hipLaunchKernelGGL(k_fa_prefill<64>, dim3((T + FP_BQ - 1) / FP_BQ, H), dim3(256), 0, s, q16, kc, vc, out, T, H, HKV,
+                           0, scale, mask, mask_ld, n_kv, (const int32_t *)nullptr);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
     if (T <= 16) {
         const int nch = (n_kv + FA_CHUNK - 1) / FA_CHUNK;
         if (nch > FA_MAX_CHUNKS) return -4;

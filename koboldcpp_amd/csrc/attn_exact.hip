@@ -12,7 +12,7 @@
 // Each f16 rounding depends on the previous one, so no key split reproduces it.  At full Llama-3-8B width
 // this f16 accumulation moves the residual stream by ~0.6% relative (tests/test_gpu_fullwidth.py), far
 // more than the reference's own build-to-build spread.  This kernel reproduces the order exactly:
-//   one workgroup per (query row, head), one lane per head dim (D = 128, two waves);
+//   one workgroup per (query row, head), one lane per head dim (D = 128: two waves; D = 64: one);
 //   phase 1: the chunk's scores, one lane per key, in the AVX2 lane/accumulator order of ggml_vec_dot_f16
 //            (4 accumulators x 8 lanes, FMA, then the GGML_F32x8_REDUCE tree), into LDS;
 //   phase 2: every lane walks the chunk's keys serially for its own dim (M and S are computed redundantly
@@ -23,7 +23,6 @@
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
-#define EX_D 128
 #define EX_CH 512
 
 __device__ __forceinline__ float ex_exp(float x) { return (float)exp((double)x); }
@@ -35,7 +34,7 @@ __device__ __forceinline__ uint16_t f2h_of_f32(float x) { return f2h_rn(x); }
 // EXT = the ggml op's own form (the b1 backend): q f32 with byte strides (rounded to f16 here, q_to_vec_dot),
 // all n_kv keys of the K/V views under an explicit f16 mask row (-inf keys skipped, others s*scale + mask).
 // Otherwise the runtime's form: q16 f16 [T][H][D], implicit causal window [0, n_past + t].
-template <bool EXT>
+template <bool EXT, int EX_D>
 __global__ void __launch_bounds__(EX_D) k_fa_exact(const uint16_t *__restrict__ q16, const float *__restrict__ qf32,
                                                    int64_t q_nb1, int64_t q_nb2, const uint16_t *__restrict__ kc,
                                                    const uint16_t *__restrict__ vc, float *__restrict__ out, int H,
@@ -117,9 +116,13 @@ __global__ void __launch_bounds__(EX_D) k_fa_exact(const uint16_t *__restrict__ 
 extern "C" int kcpp_flash_attn_exact(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, int T,
                                      int H, int HKV, int D, int n_past, const int32_t *n_past_dev, float scale,
                                      void *stream) {
-    if (D != EX_D || T < 1 || HKV < 1 || H % HKV != 0 || (!n_past_dev && n_past < 0)) return -3;
-    hipLaunchKernelGGL(k_fa_exact<false>, dim3(H, T), dim3(EX_D), 0, (hipStream_t)stream, q16, nullptr, 0, 0, kc, vc, out,
-                       H, HKV, n_past, n_past_dev, scale, nullptr, 0);
+    if ((D != 128 && D != 64) || T < 1 || HKV < 1 || H % HKV != 0 || (!n_past_dev && n_past < 0)) return -3;
+    if (D == 128)
+        hipLaunchKernelGGL((k_fa_exact<false, 128>), dim3(H, T), dim3(128), 0, (hipStream_t)stream, q16, nullptr, 0, 0, kc,
+                           vc, out, H, HKV, n_past, n_past_dev, scale, nullptr, 0);
+    else
+        hipLaunchKernelGGL((k_fa_exact<false, 64>), dim3(H, T), dim3(64), 0, (hipStream_t)stream, q16, nullptr, 0, 0, kc,
+                           vc, out, H, HKV, n_past, n_past_dev, scale, nullptr, 0);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -128,8 +131,12 @@ extern "C" int kcpp_flash_attn_exact(const uint16_t *q16, const uint16_t *kc, co
 extern "C" int kcpp_flash_attn_ext_exact(const float *q, int64_t q_nb1, int64_t q_nb2, const uint16_t *kc,
                                          const uint16_t *vc, const uint16_t *mask, int64_t mask_ld, float *out, int T,
                                          int H, int HKV, int D, int n_kv, float scale, void *stream) {
-    if (D != EX_D || T < 1 || HKV < 1 || H % HKV != 0 || n_kv < 1) return -3;
-    hipLaunchKernelGGL(k_fa_exact<true>, dim3(H, T), dim3(EX_D), 0, (hipStream_t)stream, nullptr, q, q_nb1, q_nb2, kc, vc,
-                       out, H, HKV, n_kv, nullptr, scale, mask, mask_ld);
+    if ((D != 128 && D != 64) || T < 1 || HKV < 1 || H % HKV != 0 || n_kv < 1) return -3;
+    if (D == 128)
+        hipLaunchKernelGGL((k_fa_exact<true, 128>), dim3(H, T), dim3(128), 0, (hipStream_t)stream, nullptr, q, q_nb1, q_nb2,
+                           kc, vc, out, H, HKV, n_kv, nullptr, scale, mask, mask_ld);
+    else
+        hipLaunchKernelGGL((k_fa_exact<true, 64>), dim3(H, T), dim3(64), 0, (hipStream_t)stream, nullptr, q, q_nb1, q_nb2,
+                           kc, vc, out, H, HKV, n_kv, nullptr, scale, mask, mask_ld);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

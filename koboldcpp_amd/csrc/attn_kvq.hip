@@ -22,17 +22,14 @@ __device__ __forceinline__ uint16_t *kv_d(void *c, int type, int64_t n_ctx, int6
     return (uint16_t *)((uint8_t *)c + (type == KT_Q8_0 ? n_ctx * ekv : n_ctx * ekv / 2));
 }
 
-// quantize 32 values into block b of row p (one thread per block)
+// quantize 32 values: Q8_0 -> 8 words of int8, Q4_0 -> 4 words of nibbles (byte j = elem j | elem j+16 << 4), d
 template <int TYPE>
-__device__ __forceinline__ void quant_block(const float *x, void *cache, int64_t n_ctx, int64_t ekv, int64_t p, int64_t b) {
-    uint16_t *dd = kv_d(cache, TYPE, n_ctx, ekv) + p * (ekv / 32) + b;
+__device__ __forceinline__ void quant32(const float *x, uint32_t *w, uint16_t &dh) {
     if constexpr (TYPE == KT_Q8_0) {
         float am = 0.0f;
         for (int e = 0; e < 32; ++e) am = fmaxf(am, fabsf(x[e]));
         const float d = am / 127.f;
         const float id = am != 0.0f ? 127.f / am : 0.0f;
-        int8_t *q = kv_qs(cache) + p * ekv + b * 32;
-        uint32_t w[8];
         for (int k = 0; k < 8; ++k) {
             uint32_t v = 0;
             for (int e = 0; e < 4; ++e) {
@@ -42,24 +39,50 @@ __device__ __forceinline__ void quant_block(const float *x, void *cache, int64_t
             }
             w[k] = v;
         }
-        for (int k = 0; k < 8; ++k) ((uint32_t *)q)[k] = w[k];
-        *dd = f2h_rn(d);
+        dh = f2h_rn(d);
     } else {
         float amax = 0.0f, mx = 0.0f;
         for (int e = 0; e < 32; ++e)
             if (amax < fabsf(x[e])) { amax = fabsf(x[e]); mx = x[e]; }
         const float d = mx / -8.0f;
         const float id = d != 0.0f ? 1.0f / d : 0.0f;
-        uint8_t *q = (uint8_t *)cache + p * (ekv / 2) + b * 16;
-        uint32_t w[4] = {0, 0, 0, 0};
+        for (int k = 0; k < 4; ++k) w[k] = 0;
         for (int j = 0; j < 16; ++j) {
             const float x0 = __fmul_rn(x[j], id), x1 = __fmul_rn(x[16 + j], id);
             const int xi0 = min(15, (int)(int8_t)__fadd_rn(x0, 8.5f)), xi1 = min(15, (int)(int8_t)__fadd_rn(x1, 8.5f));
             w[j >> 2] |= (uint32_t)(xi0 | (xi1 << 4)) << (8 * (j & 3));
         }
-        for (int k = 0; k < 4; ++k) ((uint32_t *)q)[k] = w[k];
-        *dd = f2h_rn(d);
+        dh = f2h_rn(d);
     }
+}
+
+// quantize 32 values into block b of row p of the runtime's cache layout (one thread per block)
+template <int TYPE>
+__device__ __forceinline__ void quant_block(const float *x, void *cache, int64_t n_ctx, int64_t ekv, int64_t p, int64_t b) {
+    uint32_t w[8];
+    uint16_t dh;
+    quant32<TYPE>(x, w, dh);
+    uint32_t *q = (uint32_t *)((uint8_t *)cache + (TYPE == KT_Q8_0 ? p * ekv + b * 32 : p * (ekv / 2) + b * 16));
+    for (int k = 0; k < (TYPE == KT_Q8_0 ? 8 : 4); ++k) q[k] = w[k];
+    kv_d(cache, TYPE, n_ctx, ekv)[p * (ekv / 32) + b] = dh;
+}
+
+// GGML_OP_CPY f32 -> Q8_0 / Q4_0 (ggml_cpy into a quantized cache view: the type's from_float, quantize_row_q8_0 /
+// quantize_row_q4_0_ref): n_blocks consecutive 32-blocks of a contiguous f32 source into ggml blocks {f16 d, quants}
+template <int TYPE>
+__global__ void k_cpy_f32_q(const float *__restrict__ src, int64_t n_blocks, uint8_t *__restrict__ dst) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n_blocks) return;
+    float x[32];
+    for (int e = 0; e < 32; ++e) x[e] = src[b * 32 + e];
+    uint32_t w[8];
+    uint16_t dh;
+    quant32<TYPE>(x, w, dh);
+    constexpr int BS = TYPE == KT_Q8_0 ? 34 : 18;
+    uint8_t *o = dst + b * BS;
+    *(uint16_t *)o = dh;
+    for (int k = 0; k < (TYPE == KT_Q8_0 ? 8 : 4); ++k)        // 2-B aligned block: 16-bit stores
+        for (int h = 0; h < 2; ++h) *(uint16_t *)(o + 2 + 4 * k + 2 * h) = (uint16_t)(w[k] >> (16 * h));
 }
 
 // K and V rows of T tokens (f32, from the q|k|v staging rows: k at column koff, v at voff, row stride ld) into the
@@ -356,6 +379,18 @@ int kcpp_flash_attn_ext_q(int tk, int tv, const float *q, int64_t q_nb1, int64_t
     if (D == 128) { FQD(128) } else { FQD(64) }
 #undef FQD
 #undef FQ
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_cpy_f32_q(int type, const float *src, int64_t n, void *dst, void *stream) {
+    if (n % 32) return -1;
+    const int64_t nb = n / 32;
+    if (nb == 0) return 0;
+    const dim3 g((unsigned)((nb + 255) / 256));
+    if (type == KT_Q8_0) hipLaunchKernelGGL(k_cpy_f32_q<KT_Q8_0>, g, dim3(256), 0, (hipStream_t)stream, src, nb, (uint8_t *)dst);
+    else if (type == KT_Q4_0) hipLaunchKernelGGL(k_cpy_f32_q<KT_Q4_0>, g, dim3(256), 0, (hipStream_t)stream, src, nb, (uint8_t *)dst);
+    else return -2;
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

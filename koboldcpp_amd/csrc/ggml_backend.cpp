@@ -16,9 +16,11 @@
 //   GET_ROWS     quantized: kcpp_get_rows on the native image; F16 / F32: kcpp_ggml_get_rows
 //   MUL_MAT_ID   quantized experts: expert-indexed mat-vecs reading the ids on the device (few rows), else the ids
 //                on the host and one mat-vec / GEMM per expert over gathered columns (mul_mat_id below)
-//   FLASH_ATTN_EXT  kcpp_flash_attn_ext (graph-form Q view, F16 K/V cache views, F16 mask)
+//   FLASH_ATTN_EXT  kcpp_flash_attn_ext (graph-form Q view, F16 K/V cache views, F16 mask; head dim 64 / 128) or
+//                kcpp_flash_attn_ext_q (Q8_0 / Q4_0 K/V views: --quantkv)
 //   RMS_NORM, ROPE (NORM / NEOX, YaRN), SOFT_MAX, ADD/SUB/MUL/DIV (broadcast), SCALE, UNARY (SILU/NEG/RELU),
-//   CPY/CONT/DUP (F32 <-> F16), ARGSORT, SUM_ROWS: the general-layout kernels of ggml_ops.hip
+//   CPY/CONT/DUP (F32 <-> F16; F32 -> Q8_0 / Q4_0 cache stores), ARGSORT, SUM_ROWS: the general-layout kernels of
+//   ggml_ops.hip / attn_kvq.hip
 //   NONE/RESHAPE/VIEW/PERMUTE/TRANSPOSE: nothing (views)
 // supports_op answers true for exactly these (placement decides the rest onto the CPU backend, as
 // ggml_backend_sched does with the reference's supports_op, ggml-cuda.cu:2959-3185).
@@ -312,7 +314,8 @@ int matmul_layout(int t, int64_t K) {
     return t;
 }
 bool matmul_quant_ok(int t) {
-    return t == KT_Q4_0 || t == KT_Q5_0 || t == KT_Q8_0 || t == KT_Q2_K || t == KT_Q3_K || t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K;
+    return t == KT_Q4_0 || t == KT_Q4_1 || t == KT_Q5_0 || t == KT_Q5_1 || t == KT_Q8_0 || t == KT_Q2_K || t == KT_Q3_K ||
+           t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K;
 }
 
 bool supports(const kggml_tensor *op) {
@@ -331,6 +334,8 @@ bool supports(const kggml_tensor *op) {
     }
     case KGGML_OP_CPY: case KGGML_OP_CONT: case KGGML_OP_DUP: {
         const int s = op->src[0]->type, d = op->op == KGGML_OP_CPY ? op->src[1]->type : op->type;
+        if (op->op == KGGML_OP_CPY && s == KGGML_TYPE_F32 && (d == KGGML_TYPE_Q8_0 || d == KGGML_TYPE_Q4_0))
+            return is_contiguous(op->src[0]) && is_contiguous(op->src[1]) && op->src[0]->ne[0] % 32 == 0;   // KV store
         return (s == KGGML_TYPE_F32 || s == KGGML_TYPE_F16) && (d == KGGML_TYPE_F32 || d == KGGML_TYPE_F16);
     }
     case KGGML_OP_ROPE: {
@@ -365,14 +370,24 @@ bool supports(const kggml_tensor *op) {
                b->ne[3] == 1 && ids->ne[1] == b->ne[2] && op->ne[1] == ids->ne[0] && op->ne[2] == ids->ne[1];
     }
     case KGGML_OP_FLASH_ATTN_EXT: {
+        // ggml_cuda_flash_attn_ext (fattn.cu:210-218, 298-345): head dim 64 or 128; K / V both F16 cache views
+        // [n_kv][HKV][D], or both quantized Q8_0 / Q4_0 (--quantkv) views of ggml blocks at any block-aligned strides
         const kggml_tensor *q = op->src[0], *k = op->src[1], *v = op->src[2], *m = op->src[3];
-        if (!f32(op) || !f32(q) || k->type != KGGML_TYPE_F16 || v->type != KGGML_TYPE_F16) return false;
-        if (q->ne[0] != 128 || op_f(op, 1) != 0.0f || op_f(op, 2) != 0.0f || q->ne[3] != 1) return false;
-        const int64_t HKV = k->ne[2];
-        const bool kv_ok = k->nb[1] == (size_t)(HKV * 128 * 2) && k->nb[2] == 256 && v->nb[1] == k->nb[1] &&
-                           v->nb[2] == 256 && v->ne[1] == k->ne[1] && v->ne[2] == HKV;
-        return kv_ok && q->ne[2] % HKV == 0 && q->nb[0] == 4 && is_contiguous(op) &&
-               (!m || (m->type == KGGML_TYPE_F16 && m->nb[0] == 2));
+        if (!f32(op) || !f32(q) || op_f(op, 1) != 0.0f || op_f(op, 2) != 0.0f || q->ne[3] != 1) return false;
+        const int64_t D = q->ne[0], HKV = k->ne[2];
+        if ((D != 64 && D != 128) || k->ne[0] != D || v->ne[0] != D) return false;
+        if (v->ne[1] != k->ne[1] || v->ne[2] != HKV || q->ne[2] % HKV || q->nb[0] != 4 || !is_contiguous(op) ||
+            (m && !(m->type == KGGML_TYPE_F16 && m->nb[0] == 2)))
+            return false;
+        const bool kq = k->type == KGGML_TYPE_Q8_0 || k->type == KGGML_TYPE_Q4_0;
+        const bool vq = v->type == KGGML_TYPE_Q8_0 || v->type == KGGML_TYPE_Q4_0;
+        if (kq && vq) {
+            const size_t kb = kTraits[k->type].size, vb = kTraits[v->type].size;
+            return k->nb[2] % kb == 0 && k->nb[1] % kb == 0 && v->nb[2] % vb == 0 && v->nb[1] % vb == 0 && k->nb[1] % 2 == 0;
+        }
+        if (k->type != KGGML_TYPE_F16 || v->type != KGGML_TYPE_F16) return false;
+        return k->nb[1] == (size_t)(HKV * D * 2) && k->nb[2] == (size_t)(D * 2) && v->nb[1] == k->nb[1] &&
+               v->nb[2] == (size_t)(D * 2);
     }
     default:
         return false;
@@ -500,6 +515,11 @@ bool compute_node(BackendCtx *bc, kggml_tensor *n) {
     }
     case KGGML_OP_CPY: case KGGML_OP_CONT: case KGGML_OP_DUP: {
         const kcpp_tdesc ta = td_of(a);
+        if (n->type == KGGML_TYPE_Q8_0 || n->type == KGGML_TYPE_Q4_0) {   // f32 -> quantized cache view (--quantkv)
+            const int64_t ne = a->ne[0] * a->ne[1] * a->ne[2] * a->ne[3];
+            return chk(kcpp_cpy_f32_q(n->type == KGGML_TYPE_Q8_0 ? KT_Q8_0 : KT_Q4_0, (const float *)a->data, ne, n->data, s),
+                       "cpy(f32 -> quantized)");
+        }
         // GGML_OP_CPY's node is a view of src[1]: writing the node writes the destination
         return chk(kcpp_ggml_cpy(a->type, a->data, &ta, n->type, n->data, &td, s), "cpy");
     }
@@ -569,18 +589,25 @@ bool compute_node(BackendCtx *bc, kggml_tensor *n) {
         return mul_mat_id(bc, n);
     case KGGML_OP_FLASH_ATTN_EXT: {
         const kggml_tensor *q = a, *k = b, *v = n->src[2], *m = n->src[3];
-        const int T = (int)q->ne[1], H = (int)q->ne[2], HKV = (int)k->ne[2], n_kv = (int)k->ne[1];
+        const int T = (int)q->ne[1], H = (int)q->ne[2], HKV = (int)k->ne[2], n_kv = (int)k->ne[1], D = (int)q->ne[0];
+        const uint16_t *mk = m ? (const uint16_t *)m->data : nullptr;
+        const int64_t mld = m ? (int64_t)(m->nb[1] / 2) : 0;
+        if (k->type != KGGML_TYPE_F16) {    // quantized K / V (the reference quantizes q to Q8_0, integer block dots)
+            const int tk = k->type == KGGML_TYPE_Q8_0 ? KT_Q8_0 : KT_Q4_0, tv = v->type == KGGML_TYPE_Q8_0 ? KT_Q8_0 : KT_Q4_0;
+            return chk(kcpp_flash_attn_ext_q(tk, tv, (const float *)q->data, (int64_t)q->nb[1], (int64_t)q->nb[2], k->data,
+                                             (int64_t)k->nb[1], (int64_t)k->nb[2], v->data, (int64_t)v->nb[1],
+                                             (int64_t)v->nb[2], mk, mld, (float *)n->data, T, H, HKV, D, n_kv, op_f(n, 0), s),
+                       "flash_attn_ext(quantized K/V)");
+        }
         if (bc->fa_exact)
             return chk(kcpp_flash_attn_ext_exact((const float *)q->data, (int64_t)q->nb[1], (int64_t)q->nb[2],
-                                                 (const uint16_t *)k->data, (const uint16_t *)v->data,
-                                                 m ? (const uint16_t *)m->data : nullptr, m ? (int64_t)(m->nb[1] / 2) : 0,
-                                                 (float *)n->data, T, H, HKV, 128, n_kv, op_f(n, 0), s),
+                                                 (const uint16_t *)k->data, (const uint16_t *)v->data, mk, mld,
+                                                 (float *)n->data, T, H, HKV, D, n_kv, op_f(n, 0), s),
                        "flash_attn_ext(exact)");
-        void *ws = bc->fa.get((size_t)kcpp_fa_ext_workspace_bytes(T, H, n_kv, 128));
+        void *ws = bc->fa.get((size_t)kcpp_fa_ext_workspace_bytes(T, H, n_kv, D));
         if (!ws) return set_err("flash_attn_ext: workspace allocation failed");
         return chk(kcpp_flash_attn_ext((const float *)q->data, (int64_t)q->nb[1], (int64_t)q->nb[2], (const uint16_t *)k->data,
-                                       (const uint16_t *)v->data, m ? (const uint16_t *)m->data : nullptr,
-                                       m ? (int64_t)(m->nb[1] / 2) : 0, (float *)n->data, ws, T, H, HKV, 128, n_kv,
+                                       (const uint16_t *)v->data, mk, mld, (float *)n->data, ws, T, H, HKV, D, n_kv,
                                        op_f(n, 0), s),
                    "flash_attn_ext");
     }

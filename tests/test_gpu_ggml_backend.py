@@ -160,7 +160,8 @@ MM_CASES = [(R.Q4_K, 4096, 512, 1), (R.Q4_K, 4096, 384, 7), (R.Q4_K, 2048, 256, 
             (R.Q6_K, 2048, 256, 33), (R.Q5_K, 4096, 256, 1), (R.Q5_K, 2048, 128, 20), (R.Q8_0, 4096, 256, 1),
             (R.Q8_0, 2048, 256, 24), (R.Q4_0, 4096, 256, 1), (R.Q4_0, 2048, 256, 40), (R.F16, 1024, 96, 5),
             (R.Q2_K, 4096, 256, 1), (R.Q2_K, 2048, 256, 24), (R.Q3_K, 4096, 256, 1), (R.Q3_K, 2048, 384, 40),
-            (R.Q5_0, 4096, 256, 1), (R.Q5_0, 2048, 256, 24)]
+            (R.Q5_0, 4096, 256, 1), (R.Q5_0, 2048, 256, 24), (R.Q4_1, 4096, 256, 1), (R.Q4_1, 2048, 256, 24),
+            (R.Q5_1, 4096, 256, 3), (R.Q5_1, 2048, 256, 40)]
 
 
 @pytest.mark.parametrize("case", MM_CASES, ids=lambda c: "t%d_%dx%d_m%d" % c)
@@ -205,7 +206,7 @@ def test_elementwise_ops_vs_reference_cpu(env):
     assert rel(ours, ref) <= 2e-6, rel(ours, ref)
 
 
-@pytest.mark.parametrize("t", [R.Q4_K, R.Q6_K, R.Q8_0, R.Q4_0, R.Q5_0, R.Q2_K, R.Q3_K, R.F16])
+@pytest.mark.parametrize("t", [R.Q4_K, R.Q6_K, R.Q8_0, R.Q4_0, R.Q5_0, R.Q2_K, R.Q3_K, R.Q4_1, R.Q5_1, R.F16])
 def test_get_rows_vs_reference_cpu(env, t):
     """token embedding gather (get_rows of a quantized or f16 table): dequantization is exact on both sides"""
     G, L, be = env
@@ -317,7 +318,7 @@ def test_unsupported_ops_are_refused(env):
     ggml_backend_sched then keeps such nodes on the CPU backend)"""
     G, L, be = env
     ctx = G.ggml_init(InitParams(1 << 20, None, True))
-    w = G.ggml_new_tensor_2d(ctx, 3, 256, 4)                      # GGML_TYPE_Q4_1: no kernel here
+    w = G.ggml_new_tensor_2d(ctx, 16, 256, 4)                     # GGML_TYPE_IQ2_XXS: no kernel here
     x = G.ggml_new_tensor_2d(ctx, R.F32, 256, 2)
     assert not G.ggml_backend_supports_op(be, G.ggml_mul_mat(ctx, w, x))
     w2 = G.ggml_new_tensor_2d(ctx, R.Q4_K, 256, 4)
@@ -333,7 +334,7 @@ def _moe_sigs(G):
 
 
 MMID_CASES = [(R.Q4_K, 1), (R.Q4_K, 3), (R.Q4_K, 24), (R.Q5_K, 1), (R.Q5_K, 24), (R.Q6_K, 2), (R.Q6_K, 24),
-              (R.Q8_0, 1), (R.Q8_0, 24), (R.Q4_0, 3), (R.Q2_K, 1), (R.Q3_K, 24)]
+              (R.Q8_0, 1), (R.Q8_0, 24), (R.Q4_0, 3), (R.Q2_K, 1), (R.Q3_K, 24), (R.Q4_1, 2), (R.Q5_1, 24)]
 
 
 @pytest.mark.parametrize("case", MMID_CASES, ids=lambda c: "t%d_T%d" % c)
@@ -409,3 +410,183 @@ def test_moe_ffn_graph_vs_reference_cpu(env, T):
     assert not unsupported, unsupported
     ours, ref = run_both(G, be, build, lambda: [router, up, gate, down, x])
     assert rel(ours, ref) <= 2e-5, rel(ours, ref)
+
+
+LAYER_CASES = [  # (name, n_embd, H, HKV, D, kv type, weight type, strict attention)
+    ("d64_f16_exact", 1024, 16, 4, 64, R.F16, R.Q4_0, True),
+    ("d64_f16_prod", 1024, 16, 4, 64, R.F16, R.Q4_0, False),
+    ("d128_kv_q8_0", 1024, 8, 2, 128, R.Q8_0, R.Q4_K, False),
+    ("d128_kv_q4_0", 1024, 8, 2, 128, R.Q4_0, R.Q4_K, False),
+    ("d64_kv_q8_0", 1024, 16, 4, 64, R.Q8_0, R.Q4_0, False),
+]
+
+
+@pytest.mark.parametrize("case", LAYER_CASES, ids=lambda c: c[0])
+def test_llama_layer_variants_vs_reference_cpu(env, case):
+    """one build_llama layer with 64-dim heads (TinyLlama class, BASELINE config 1) and with --quantkv caches (K / V
+    stored by ggml_cpy into Q8_0 / Q4_0 cache views, attention over the quantized views, fattn.cu:210-218): every
+    node supported by this backend, the output equal to the reference CPU backend's (F16 production attention: the
+    reference's f16 accumulation bound, as the 128-dim layer test)"""
+    G, L, be = env
+    name, E, H, HKV, D, kvt, wt, exact = case
+    Fd, n_ctx, n_past, T = 2816, 64, 37, 5
+    EKV = HKV * D
+    n_kv = n_past + T
+    rng = np.random.default_rng(len(name))
+    tys = [wt] * 7
+    shapes = [(E, E), (E, EKV), (E, EKV), (E, E), (E, Fd), (E, Fd), (Fd, E)]
+    ws = [R.synth(t, 9, 300 + i, k, n) for i, (t, (k, n)) in enumerate(zip(tys, shapes))]
+    nw1 = (1 + 0.05 * rng.standard_normal(E)).astype(np.float32)
+    nw2 = (1 + 0.05 * rng.standard_normal(E)).astype(np.float32)
+    x = rng.standard_normal((T, E)).astype(np.float32)
+    if kvt == R.F16:
+        kc = (rng.standard_normal((n_ctx, EKV)) * 0.5).astype(np.float16)
+        vc = rng.standard_normal((n_ctx, EKV)).astype(np.float16)
+    else:
+        kc, vc = R.synth(kvt, 3, 11, EKV, n_ctx), R.synth(kvt, 3, 12, EKV, n_ctx)
+    pos = np.arange(n_past, n_past + T, dtype=np.int32)
+    T_pad = 32
+    mask = np.full((T_pad, n_kv), -np.inf, np.float16)
+    for t in range(T):
+        mask[t, :n_past + t + 1] = 0
+    rs = G.ggml_row_size(kvt, EKV)
+
+    def build(ctx):
+        W = [G.ggml_new_tensor_2d(ctx, t, k, n) for t, (k, n) in zip(tys, shapes)]
+        N1, N2 = G.ggml_new_tensor_1d(ctx, R.F32, E), G.ggml_new_tensor_1d(ctx, R.F32, E)
+        X = G.ggml_new_tensor_2d(ctx, R.F32, E, T)
+        KC, VC = G.ggml_new_tensor_1d(ctx, kvt, n_ctx * EKV), G.ggml_new_tensor_1d(ctx, kvt, n_ctx * EKV)
+        Pz = G.ggml_new_tensor_1d(ctx, 26, T)
+        Mk = G.ggml_new_tensor_2d(ctx, R.F16, n_kv, T_pad)
+        cur = G.ggml_mul(ctx, G.ggml_rms_norm(ctx, X, 1e-5), N1)
+        q = G.ggml_rope_ext(ctx, G.ggml_reshape_3d(ctx, G.ggml_mul_mat(ctx, W[0], cur), D, H, T), Pz, None, D, 0, n_ctx,
+                            10000.0, 1.0, 0.0, 1.0, 32.0, 1.0)
+        k = G.ggml_rope_ext(ctx, G.ggml_reshape_3d(ctx, G.ggml_mul_mat(ctx, W[1], cur), D, HKV, T), Pz, None, D, 0, n_ctx,
+                            10000.0, 1.0, 0.0, 1.0, 32.0, 1.0)
+        v = G.ggml_mul_mat(ctx, W[2], cur)
+        st_k = G.ggml_cpy(ctx, k, G.ggml_view_1d(ctx, KC, T * EKV, n_past * rs))
+        st_v = G.ggml_cpy(ctx, v, G.ggml_view_1d(ctx, VC, T * EKV, n_past * rs))
+        kview = G.ggml_view_3d(ctx, KC, D, n_kv, HKV, rs, G.ggml_row_size(kvt, D), 0)
+        vview = G.ggml_view_3d(ctx, VC, D, n_kv, HKV, rs, G.ggml_row_size(kvt, D), 0)
+        fa = G.ggml_flash_attn_ext(ctx, G.ggml_permute(ctx, q, 0, 2, 1, 3), kview, vview, Mk, 1.0 / np.sqrt(D), 0.0, 0.0)
+        att = G.ggml_mul_mat(ctx, W[3], G.ggml_reshape_2d(ctx, fa, E, T))
+        ffn_in = G.ggml_add(ctx, att, X)
+        h = G.ggml_mul(ctx, G.ggml_rms_norm(ctx, ffn_in, 1e-5), N2)
+        h = G.ggml_mul(ctx, G.ggml_silu(ctx, G.ggml_mul_mat(ctx, W[4], h)), G.ggml_mul_mat(ctx, W[5], h))
+        out = G.ggml_add(ctx, G.ggml_mul_mat(ctx, W[6], h), ffn_in)
+        return W + [N1, N2, X, KC, VC, Pz, Mk], out, [st_k, st_v]
+
+    L.kcpp_ggml_backend_set_fa_exact(ctypes.c_void_p(be), int(exact))
+    outs = []
+    for on_gpu in (True, False):
+        ctx = G.ggml_init(InitParams(256 << 20, None, on_gpu))
+        ins, out, pre = build(ctx)
+        g = G.ggml_new_graph(ctx)
+        for p_ in pre:
+            G.ggml_build_forward_expand(g, p_)
+        G.ggml_build_forward_expand(g, out)
+        if on_gpu:
+            bad = [i for i in range(G.ggml_graph_n_nodes(g)) if not G.ggml_backend_supports_op(be, G.ggml_graph_node(g, i))]
+            assert not bad, bad
+            buf = G.ggml_backend_alloc_ctx_tensors(ctx, be)
+            for t, a in zip(ins, ws + [nw1, nw2, x, kc, vc, pos, mask]):
+                a = np.ascontiguousarray(a)
+                assert a.nbytes == G.ggml_nbytes(t)
+                G.ggml_backend_tensor_set(t, a.ctypes.data, 0, a.nbytes)
+            assert G.ggml_backend_graph_compute(be, g) == 0, L.kcpp_ggml_backend_last_error()
+            res = np.empty(T * E, np.float32)
+            G.ggml_backend_tensor_get(out, res.ctypes.data, 0, res.nbytes)
+            G.ggml_backend_buffer_free(buf)
+        else:
+            for t, a in zip(ins, ws + [nw1, nw2, x, kc, vc, pos, mask]):
+                a = np.ascontiguousarray(a)
+                ctypes.memmove(G.ggml_get_data(t), a.ctypes.data, a.nbytes)
+            assert G.ggml_graph_compute_with_ctx(ctx, g, 8) == 0
+            res = np.ctypeslib.as_array((ctypes.c_float * (T * E)).from_address(G.ggml_get_data(out))).copy()
+        G.ggml_free(ctx)
+        outs.append(res)
+    L.kcpp_ggml_backend_set_fa_exact(ctypes.c_void_p(be), 0)
+    e = rel(outs[0], outs[1])
+    print("%s rel err max %.3g" % (name, e))
+    # F16 caches: the attention bounds as in the 128-dim test.  Quantized caches: the cache store turns a 1-ulp
+    # difference of a k / v value (the q|k|v mat-mul's fp32 order) into a whole Q8_0 / Q4_0 quantum of that row
+    # (measured up to 4.9e-3 here; the per-op tests below pin the store and the attention exactly)
+    bar = LAYER_KVQ if kvt != R.F16 else (LAYER_EXACT if exact else LAYER_PROD)
+    assert e <= bar, e
+
+
+LAYER_KVQ = 1e-2
+
+
+@pytest.mark.parametrize("kvt", [R.Q8_0, R.Q4_0])
+def test_cpy_f32_to_quantized_cache_vs_reference_cpu(env, kvt):
+    """the --quantkv cache store (ggml_cpy f32 -> Q8_0 / Q4_0 view of the cache, quantize_row_q8_0 AVX2 /
+    quantize_row_q4_0_ref): the same bytes as the reference CPU's, including zero blocks and rounding ties"""
+    G, L, be = env
+    n_ctx, EKV, T, off = 16, 1024, 5, 7
+    rng = np.random.default_rng(kvt)
+    x = rng.standard_normal((T, EKV)).astype(np.float32)
+    x[0, :32] = 0.0                                               # an all-zero block
+    x[1, :32] = np.arange(32) - 15.5                              # exact .5 ties after scaling
+    cache = R.synth(kvt, 2, 5, EKV, n_ctx)
+    rs = G.ggml_row_size(kvt, EKV)
+
+    def build(ctx):
+        X = G.ggml_new_tensor_2d(ctx, R.F32, EKV, T)
+        C = G.ggml_new_tensor_1d(ctx, kvt, n_ctx * EKV)
+        st = G.ggml_cpy(ctx, X, G.ggml_view_1d(ctx, C, T * EKV, off * rs))
+        build.cache = C
+        return [X, C], st
+    outs = []
+    for on_gpu in (True, False):
+        ctx = G.ggml_init(InitParams(16 << 20, None, on_gpu))
+        ins, st = build(ctx)
+        g = G.ggml_new_graph(ctx)
+        G.ggml_build_forward_expand(g, st)
+        res = np.empty(n_ctx * rs, np.uint8)
+        if on_gpu:
+            assert G.ggml_backend_supports_op(be, G.ggml_graph_node(g, 0))
+            buf = G.ggml_backend_alloc_ctx_tensors(ctx, be)
+            for t, a in zip(ins, [x, cache]):
+                G.ggml_backend_tensor_set(t, np.ascontiguousarray(a).ctypes.data, 0, a.nbytes)
+            assert G.ggml_backend_graph_compute(be, g) == 0, L.kcpp_ggml_backend_last_error()
+            G.ggml_backend_tensor_get(build.cache, res.ctypes.data, 0, res.nbytes)
+            G.ggml_backend_buffer_free(buf)
+        else:
+            for t, a in zip(ins, [x, cache]):
+                ctypes.memmove(G.ggml_get_data(t), np.ascontiguousarray(a).ctypes.data, a.nbytes)
+            assert G.ggml_graph_compute_with_ctx(ctx, g, 4) == 0
+            ctypes.memmove(res.ctypes.data, G.ggml_get_data(build.cache), res.nbytes)
+        G.ggml_free(ctx)
+        outs.append(res)
+    assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("case", [(128, R.Q8_0, R.Q8_0, 1), (128, R.Q4_0, R.Q4_0, 7), (128, R.Q8_0, R.Q4_0, 3),
+                                  (64, R.Q8_0, R.Q8_0, 5), (64, R.Q4_0, R.Q8_0, 1)], ids=lambda c: "d%d_k%d_v%d_T%d" % c)
+def test_flash_attn_quantized_views_vs_reference_cpu(env, case):
+    """GGML_OP_FLASH_ATTN_EXT over Q8_0 / Q4_0 K and V cache views (fattn.cu:210-218) on identical inputs: q quantized
+    to Q8_0, exact integer block dots, V dequantized and accumulated in f32 as the reference CPU does"""
+    G, L, be = env
+    D, tk, tv, T = case
+    H, HKV, n_ctx, n_kv = 8, 2, 96, 70
+    EKV = HKV * D
+    rng = np.random.default_rng(D + T)
+    q = rng.standard_normal((T, H, D)).astype(np.float32)
+    kc, vc = R.synth(tk, 4, 21, EKV, n_ctx), R.synth(tv, 4, 22, EKV, n_ctx)
+    T_pad = 32
+    mask = np.full((T_pad, n_kv), -np.inf, np.float16)
+    for t in range(T):
+        mask[t, :n_kv - T + t + 1] = 0
+    mask[0, 3] = -np.inf                                          # a hole inside the window
+
+    def build(ctx):
+        Q = G.ggml_new_tensor_3d(ctx, R.F32, D, H, T)
+        KC, VC = G.ggml_new_tensor_1d(ctx, tk, n_ctx * EKV), G.ggml_new_tensor_1d(ctx, tv, n_ctx * EKV)
+        Mk = G.ggml_new_tensor_2d(ctx, R.F16, n_kv, T_pad)
+        kv = G.ggml_view_3d(ctx, KC, D, n_kv, HKV, G.ggml_row_size(tk, EKV), G.ggml_row_size(tk, D), 0)
+        vv = G.ggml_view_3d(ctx, VC, D, n_kv, HKV, G.ggml_row_size(tv, EKV), G.ggml_row_size(tv, D), 0)
+        fa = G.ggml_flash_attn_ext(ctx, G.ggml_permute(ctx, Q, 0, 2, 1, 3), kv, vv, Mk, 1.0 / np.sqrt(D), 0.0, 0.0)
+        return [Q, KC, VC, Mk], fa
+    ours, ref = run_both(G, be, build, lambda: [q, kc, vc, mask])
+    assert rel(ours, ref) <= 2e-6, rel(ours, ref)
