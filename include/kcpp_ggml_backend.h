@@ -262,6 +262,9 @@ void ggml_cuda_set_mul_mat_q(bool mul_mat_q);
 
 /* diagnostics (this backend only): nodes executed by the last graph_compute, and the last dispatch error */
 int kcpp_ggml_backend_last_nodes(void);
+/* device bytes held in separate native weight images (0 when every weight sits in a weight buffer: those are
+ * converted in place, one copy of the model) */
+int64_t kcpp_ggml_backend_image_bytes(void);
 /* strict-parity attention for this backend's FLASH_ATTN_EXT nodes (default from KCPP_FA_EXACT at init) */
 int kcpp_ggml_backend_set_fa_exact(kggml_backend_t backend, int on);
 const char *kcpp_ggml_backend_last_error(void);

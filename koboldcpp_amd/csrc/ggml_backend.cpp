@@ -100,11 +100,19 @@ float op_f(const kggml_tensor *t, int i) { float f; memcpy(&f, &t->op_params[i],
 bool set_err(const std::string &s) { g_last_error = s; fprintf(stderr, "[kcpp ggml backend] %s\n", s.c_str()); return false; }
 
 // ------------------------------------------------------------------ buffers
+// a weight held in its device-native layout IN PLACE of its ggml bytes (weight buffers only: one copy of the model)
+struct InPlace {
+    int tt;                    // native layout (kcpp type id)
+    int gtype;                 // ggml type
+    int64_t K, N1, NS;         // row length, rows per slice, slices (MUL_MAT_ID experts)
+};
 struct BufCtx {
     int device;
     void *dev_ptr;
     std::string name;
     unsigned gen = 0;          // bumped by every write through the buffer interface (native-image invalidation)
+    std::map<const void *, InPlace> native;   // tensors of this buffer converted in place, by data pointer
+    std::map<const void *, int> shared;       // tensors asked for in two layouts: separate images instead
 };
 struct BuftCtx {
     int device;
@@ -124,11 +132,48 @@ void drop_images(kggml_backend_buffer_t buf) {
     }
 }
 
+// ggml <-> native conversion of a whole in-place tensor through a transient device buffer (slice by slice for
+// expert tensors); synchronous on the caller's stream
+bool convert_inplace(void *data, const InPlace &ip, bool to_ggml, hipStream_t s) {
+    const size_t sb = row_size(ip.gtype, ip.K) * ip.N1, bytes = sb * ip.NS;
+    void *tmp = nullptr;
+    if (hipMalloc(&tmp, bytes) != hipSuccess) { (void)hipGetLastError(); return false; }
+    bool ok = true;
+    for (int64_t e = 0; e < ip.NS && ok; ++e)
+        ok = kcpp_weight_repack(ip.tt, (const char *)data + e * sb, (char *)tmp + e * sb, ip.K, ip.N1, to_ggml ? 1 : 0, s) == 0;
+    ok = ok && hipMemcpyAsync(data, tmp, bytes, hipMemcpyDeviceToDevice, s) == hipSuccess &&
+         hipStreamSynchronize(s) == hipSuccess;
+    hipFree(tmp);
+    return ok;
+}
+// the in-place tensor covering [p, p + n) of buffer c, or end()
+std::map<const void *, InPlace>::iterator inplace_at(BufCtx *c, const void *p, size_t n) {
+    for (auto it = c->native.begin(); it != c->native.end(); ++it) {
+        const size_t bytes = row_size(it->second.gtype, it->second.K) * it->second.N1 * it->second.NS;
+        const char *b = (const char *)it->first;
+        if ((const char *)p < b + bytes && (const char *)p + n > b) return it;
+    }
+    return c->native.end();
+}
+// back to ggml bytes before anything but this backend's mat-mul kernels touches [p, p + n)
+void restore_ggml(BufCtx *c, const void *p, size_t n) {
+    std::lock_guard<std::mutex> lk(g_img_mu);
+    for (auto it = inplace_at(c, p, n); it != c->native.end(); it = inplace_at(c, p, n)) {
+        hipSetDevice(c->device);
+        hipDeviceSynchronize();                       // pending kernels may still read the native bytes
+        if (!convert_inplace((void *)it->first, it->second, true, hipStreamPerThread))
+            fprintf(stderr, "[kcpp ggml backend] restoring a weight's ggml layout failed\n");
+        c->native.erase(it);
+    }
+}
+
 const char *buf_get_name(kggml_backend_buffer_t b) { return ((BufCtx *)b->context)->name.c_str(); }
 bool buffer_is_ours(kggml_backend_buffer_t b) { return b && b->iface.get_name == buf_get_name; }
 void buf_free(kggml_backend_buffer_t b) {
     BufCtx *c = (BufCtx *)b->context;
     drop_images(b);
+    hipSetDevice(c->device);
+    hipDeviceSynchronize();
     hipSetDevice(c->device);
     hipFree(c->dev_ptr);
     delete c;
@@ -152,6 +197,7 @@ void buf_init_tensor(kggml_backend_buffer_t b, kggml_tensor *t) {
 }
 void buf_memset_tensor(kggml_backend_buffer_t b, kggml_tensor *t, uint8_t v, size_t off, size_t size) {
     BufCtx *c = (BufCtx *)b->context;
+    restore_ggml(c, (char *)t->data + off, size);
     hipSetDevice(c->device);
     ++c->gen;
     hipMemsetAsync((char *)t->data + off, v, size, hipStreamPerThread);
@@ -159,12 +205,14 @@ void buf_memset_tensor(kggml_backend_buffer_t b, kggml_tensor *t, uint8_t v, siz
 }
 void buf_set_tensor(kggml_backend_buffer_t b, kggml_tensor *t, const void *data, size_t off, size_t size) {
     BufCtx *c = (BufCtx *)b->context;
+    restore_ggml(c, (char *)t->data + off, size);
     hipSetDevice(c->device);
     ++c->gen;
     hipMemcpyAsync((char *)t->data + off, data, size, hipMemcpyHostToDevice, hipStreamPerThread);
     hipStreamSynchronize(hipStreamPerThread);
 }
 void buf_get_tensor(kggml_backend_buffer_t b, const kggml_tensor *t, void *data, size_t off, size_t size) {
+    restore_ggml((BufCtx *)b->context, (const char *)t->data + off, size);
     hipSetDevice(((BufCtx *)b->context)->device);
     hipMemcpyAsync(data, (const char *)t->data + off, size, hipMemcpyDeviceToHost, hipStreamPerThread);
     hipStreamSynchronize(hipStreamPerThread);
@@ -172,6 +220,8 @@ void buf_get_tensor(kggml_backend_buffer_t b, const kggml_tensor *t, void *data,
 bool buf_cpy_tensor(kggml_backend_buffer_t b, const kggml_tensor *src, kggml_tensor *dst) {
     if (!buffer_is_ours(src->buffer)) return false;
     BufCtx *sc = (BufCtx *)src->buffer->context, *dc = (BufCtx *)dst->buffer->context;
+    restore_ggml(sc, src->data, nbytes(src));
+    restore_ggml(dc, dst->data, nbytes(dst));
     ++dc->gen;
     if (sc->device == dc->device) {
         hipSetDevice(dc->device);
@@ -188,6 +238,11 @@ void buf_clear(kggml_backend_buffer_t b, uint8_t v) {
     hipSetDevice(c->device);
     ++c->gen;
     hipDeviceSynchronize();
+    {
+        std::lock_guard<std::mutex> lk(g_img_mu);
+        c->native.clear();                            // every byte is overwritten: no layout to restore
+        c->shared.clear();
+    }
     hipMemset(c->dev_ptr, v, b->size);
     hipDeviceSynchronize();
 }
@@ -285,10 +340,30 @@ struct BackendCtx {
 
 // the native image of weight w for target layout `tt` (kcpp type id); w itself when the layouts coincide
 // (a 3-D MUL_MAT_ID expert tensor is repacked slice by slice: expert e's image starts at e * nb[2], like its bytes)
+// In a weight buffer (usage WEIGHTS, as llama.cpp marks its model buffers, src/llama.cpp:8982) the tensor is converted
+// IN PLACE on first use, so the model occupies its size once; every other access through the buffer interface
+// restores the ggml bytes first (restore_ggml).  Elsewhere a separate image is kept, invalidated by writes.
 const void *native_image(BackendCtx *bc, const kggml_tensor *w, int tt) {
     const int64_t K = w->ne[0], N = w->ne[1] * w->ne[2] * w->ne[3], NS = w->ne[2] * w->ne[3];
     if (tt == w->type && (tt == KT_Q4_K || tt == KT_Q5_K)) return w->data;      // kcpp layout = ggml layout
     kggml_backend_buffer_t buf = w->view_src ? w->view_src->buffer : w->buffer;
+    if (buffer_is_ours(buf) && buf->usage == KGGML_BACKEND_BUFFER_USAGE_WEIGHTS && w->view_src == nullptr) {
+        BufCtx *c = (BufCtx *)buf->context;
+        std::lock_guard<std::mutex> lk(g_img_mu);
+        auto it = c->native.find(w->data);
+        if (it != c->native.end() && it->second.tt == tt) return w->data;
+        if (it != c->native.end()) {                  // a second layout (e.g. tied embeddings): back to ggml bytes,
+            hipStreamSynchronize(bc->stream);         // separate images for both from now on
+            if (!convert_inplace(w->data, it->second, true, bc->stream)) return nullptr;
+            c->native.erase(it);
+            c->shared[w->data] = 1;
+        } else if (!c->shared.count(w->data)) {
+            const InPlace ip{tt, w->type, K, N / NS, NS};
+            if (!convert_inplace(w->data, ip, false, bc->stream)) return nullptr;
+            c->native[w->data] = ip;
+            return w->data;
+        }
+    }
     const unsigned gen = buffer_is_ours(buf) ? ((BufCtx *)buf->context)->gen : 0;
     const auto key = std::make_tuple(bc->device, (const void *)w->data, w->type, K, N, tt);
     std::lock_guard<std::mutex> lk(g_img_mu);
@@ -632,12 +707,17 @@ kggml_backend_buffer_type_t be_default_buft(kggml_backend_t be) {
 void be_set_async(kggml_backend_t be, kggml_tensor *t, const void *data, size_t off, size_t size) {
     BackendCtx *c = (BackendCtx *)be->context;
     kggml_backend_buffer_t buf = t->view_src ? t->view_src->buffer : t->buffer;
-    if (buffer_is_ours(buf)) ++((BufCtx *)buf->context)->gen;
+    if (buffer_is_ours(buf)) {
+        restore_ggml((BufCtx *)buf->context, (char *)t->data + off, size);
+        ++((BufCtx *)buf->context)->gen;
+    }
     hipSetDevice(c->device);
     hipMemcpyAsync((char *)t->data + off, data, size, hipMemcpyHostToDevice, c->stream);
 }
 void be_get_async(kggml_backend_t be, const kggml_tensor *t, void *data, size_t off, size_t size) {
     BackendCtx *c = (BackendCtx *)be->context;
+    kggml_backend_buffer_t buf = t->view_src ? t->view_src->buffer : t->buffer;
+    if (buffer_is_ours(buf)) restore_ggml((BufCtx *)buf->context, (const char *)t->data + off, size);
     hipSetDevice(c->device);
     hipMemcpyAsync(data, (const char *)t->data + off, size, hipMemcpyDeviceToHost, c->stream);
 }
@@ -649,6 +729,8 @@ bool be_cpy_async(kggml_backend_t src_be, kggml_backend_t dst_be, const kggml_te
     kggml_backend_buffer_t db = dst->view_src ? dst->view_src->buffer : dst->buffer;
     if (!buffer_is_ours(sb) || !buffer_is_ours(db)) return false;
     BackendCtx *sc = (BackendCtx *)src_be->context, *dc = (BackendCtx *)dst_be->context;
+    restore_ggml((BufCtx *)sb->context, src->data, nbytes(src));
+    restore_ggml((BufCtx *)db->context, dst->data, nbytes(dst));
     ++((BufCtx *)db->context)->gen;
     hipSetDevice(sc->device);
     if (sc->device == dc->device) {
@@ -827,6 +909,14 @@ void ggml_backend_cuda_unregister_host_buffer(void *buffer) {
 void ggml_cuda_set_mul_mat_q(bool mul_mat_q) { g_mul_mat_q = mul_mat_q; }
 
 int kcpp_ggml_backend_last_nodes(void) { return g_last_nodes; }
+// device bytes held by separate native images (weights outside weight buffers, or asked for in two layouts); the
+// weights of a weight buffer are converted in place and hold none
+int64_t kcpp_ggml_backend_image_bytes(void) {
+    std::lock_guard<std::mutex> lk(g_img_mu);
+    int64_t n = 0;
+    for (const auto &kv : g_images) n += (int64_t)row_size(std::get<2>(kv.first), std::get<3>(kv.first)) * std::get<4>(kv.first);
+    return n;
+}
 int kcpp_ggml_backend_set_fa_exact(kggml_backend_t be, int on) {
     if (!ggml_backend_is_cuda(be)) return -1;
     ((BackendCtx *)be->context)->fa_exact = on != 0;

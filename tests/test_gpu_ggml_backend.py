@@ -590,3 +590,63 @@ def test_flash_attn_quantized_views_vs_reference_cpu(env, case):
         return [Q, KC, VC, Mk], fa
     ours, ref = run_both(G, be, build, lambda: [q, kc, vc, mask])
     assert rel(ours, ref) <= 2e-6, rel(ours, ref)
+
+
+@pytest.mark.parametrize("t", [R.Q4_K, R.Q6_K, R.Q8_0, R.Q4_0, R.Q5_K])
+def test_weight_buffer_holds_one_copy(env, t):
+    """weights in a buffer marked WEIGHTS (llama.cpp's model buffers, src/llama.cpp:8982) are converted to the
+    device layout in place: no separate image is allocated, the mat-mul equals the reference CPU before and after,
+    and reading the tensor back through the buffer interface returns the original ggml bytes (the layout is restored
+    first); a later write is honoured"""
+    G, L, be = env
+    L.kcpp_ggml_backend_image_bytes.restype = I64
+    Kd, N, M = 2048, 384, 3
+    rng = np.random.default_rng(t)
+    w = R.synth(t, 8, 70 + t, Kd, N)
+    w2 = R.synth(t, 8, 71 + t, Kd, N)
+    x = rng.standard_normal((M, Kd)).astype(np.float32)
+    ctx_w = G.ggml_init(InitParams(1 << 20, None, True))
+    W = G.ggml_new_tensor_2d(ctx_w, t, Kd, N)
+    bw = G.ggml_backend_alloc_ctx_tensors(ctx_w, be)
+    G.ggml_backend_buffer_set_usage(bw, 1)                         # GGML_BACKEND_BUFFER_USAGE_WEIGHTS
+    G.ggml_backend_tensor_set(W, w.ctypes.data, 0, w.nbytes)
+    base = L.kcpp_ggml_backend_image_bytes()
+
+    def run(wbytes):
+        ctx = G.ggml_init(InitParams(1 << 20, None, True))
+        X = G.ggml_new_tensor_2d(ctx, R.F32, Kd, M)
+        out = G.ggml_mul_mat(ctx, W, X)
+        g = G.ggml_new_graph(ctx)
+        G.ggml_build_forward_expand(g, out)
+        bx = G.ggml_backend_alloc_ctx_tensors(ctx, be)
+        G.ggml_backend_tensor_set(X, x.ctypes.data, 0, x.nbytes)
+        assert G.ggml_backend_graph_compute(be, g) == 0, L.kcpp_ggml_backend_last_error()
+        res = np.empty(M * N, np.float32)
+        G.ggml_backend_tensor_get(out, res.ctypes.data, 0, res.nbytes)
+        G.ggml_backend_buffer_free(bx)
+        G.ggml_free(ctx)
+        # the reference CPU on the same bytes
+        cctx = G.ggml_init(InitParams(64 << 20, None, False))
+        Wc = G.ggml_new_tensor_2d(cctx, t, Kd, N)
+        Xc = G.ggml_new_tensor_2d(cctx, R.F32, Kd, M)
+        oc = G.ggml_mul_mat(cctx, Wc, Xc)
+        gc = G.ggml_new_graph(cctx)
+        G.ggml_build_forward_expand(gc, oc)
+        ctypes.memmove(G.ggml_get_data(Wc), wbytes.ctypes.data, wbytes.nbytes)
+        ctypes.memmove(G.ggml_get_data(Xc), x.ctypes.data, x.nbytes)
+        assert G.ggml_graph_compute_with_ctx(cctx, gc, 4) == 0
+        ref = np.ctypeslib.as_array((ctypes.c_float * (M * N)).from_address(G.ggml_get_data(oc))).copy()
+        G.ggml_free(cctx)
+        return res, ref
+    for _ in range(2):
+        ours, ref = run(w)
+        assert rel(ours, ref) <= 3e-6
+        assert L.kcpp_ggml_backend_image_bytes() == base           # no second copy of the weight
+    back = np.empty_like(w)
+    G.ggml_backend_tensor_get(W, back.ctypes.data, 0, back.nbytes)
+    assert np.array_equal(back, w)
+    G.ggml_backend_tensor_set(W, w2.ctypes.data, 0, w2.nbytes)
+    ours, ref = run(w2)
+    assert rel(ours, ref) <= 3e-6
+    G.ggml_backend_buffer_free(bw)
+    G.ggml_free(ctx_w)
