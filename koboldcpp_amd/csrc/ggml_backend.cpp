@@ -393,8 +393,170 @@ bool matmul_quant_ok(int t) {
            t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K;
 }
 
+// ------------------------------------------------------------------ split buffers (LLAMA_SPLIT_MODE_ROW)
+// ggml_backend_cuda_split_buffer_type (ggml-cuda.cu:625-955): a weight's rows are spread over the devices by
+// tensor_split (kcpp_row_split_range: cumulative normalised starts, bounds rounded down to 128 rows).  Each lane
+// (device) holds its rows as a [K][rows] tensor already in the device layout of the type (one copy, repacked at
+// set_tensor); tensor->extra points at the slices.  A MUL_MAT on such a weight runs on the main device's backend:
+// the activation is quantized there, every other lane takes it by a peer copy, multiplies its slice on its own
+// stream and copies its rows of the result back (ggml_cuda_op_mul_mat's split branch, ggml-cuda.cu:1403-1700).
+// KCPP_VIRTUAL_DEVICES=n (tests) splits over n lanes on the visible GPUs (lane i on GPU i % count).
+struct SplitExtra {
+    int n;                                   // lanes
+    int tt, gtype;                           // device layout, ggml type
+    int64_t K;
+    int64_t lo[KGGML_CUDA_MAX_DEVICES], hi[KGGML_CUDA_MAX_DEVICES];
+    void *d[KGGML_CUDA_MAX_DEVICES];
+};
+struct SplitBuftCtx { float split[KGGML_CUDA_MAX_DEVICES]; int n; };
+struct SplitBufCtx { std::vector<SplitExtra *> extras; };
+struct SplitLane {                           // a lane's stream and scratch for the split mat-mul
+    int dev = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t done = nullptr;
+    Scratch act, ws, y;
+};
+std::mutex g_split_mu;
+std::map<std::vector<float>, kggml_backend_buffer_type> g_split_bufts;
+SplitLane g_lanes[KGGML_CUDA_MAX_DEVICES];      // fixed slots: pointers to them stay valid
+
+int n_lanes() {
+    int n = (int)g_devs.size();
+    if (const char *v = getenv("KCPP_VIRTUAL_DEVICES")) n = std::max(1, atoi(v));
+    return std::min(n, (int)KGGML_CUDA_MAX_DEVICES);
+}
+int lane_device(int i) { return g_devs.empty() ? 0 : i % (int)g_devs.size(); }
+SplitLane *get_lane(int i) {
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    if (i < 0 || i >= (int)KGGML_CUDA_MAX_DEVICES) return nullptr;
+    SplitLane &l = g_lanes[i];
+    if (!l.s) {
+        l.dev = lane_device(i);
+        hipSetDevice(l.dev);
+        if (hipStreamCreateWithFlags(&l.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&l.done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        for (size_t j = 0; j < g_devs.size(); ++j)     // xGMI peer access both ways
+            if ((int)j != l.dev) {
+                hipDeviceEnablePeerAccess((int)j, 0);
+                (void)hipGetLastError();
+            }
+    }
+    return &l;
+}
+void split_rows(const SplitBuftCtx *c, int64_t nrows, int id, int64_t &lo, int64_t &hi) {
+    kcpp_row_split_range(nrows, c->n, c->split, id, &lo, &hi);
+}
+size_t split_pad(int type, int64_t ne0) {    // pad of the last row to 512 elements (ggml-cuda.cu:732-735)
+    return ne0 % 512 ? row_size(type, 512 - ne0 % 512) : 0;
+}
+
+const char *sbuf_get_name(kggml_backend_buffer_t) { return KGGML_CUDA_NAME "_Split"; }
+bool buffer_is_split(kggml_backend_buffer_t b) { return b && b->iface.get_name == sbuf_get_name; }
+void sbuf_free(kggml_backend_buffer_t b) {
+    SplitBufCtx *c = (SplitBufCtx *)b->context;
+    for (SplitExtra *x : c->extras) {
+        for (int i = 0; i < x->n; ++i)
+            if (x->d[i]) { hipSetDevice(lane_device(i)); hipFree(x->d[i]); }
+        delete x;
+    }
+    delete c;
+}
+void *sbuf_get_base(kggml_backend_buffer_t) { return (void *)0x1000; }    // never dereferenced (the extras hold the data)
+void sbuf_init_tensor(kggml_backend_buffer_t b, kggml_tensor *t) {
+    const SplitBuftCtx *bc = (const SplitBuftCtx *)b->buft->context;
+    SplitExtra *x = new SplitExtra{};
+    x->n = bc->n; x->gtype = t->type; x->K = t->ne[0];
+    x->tt = matmul_layout(t->type, t->ne[0]);
+    const int64_t nr = nrows(t);
+    for (int i = 0; i < x->n; ++i) {
+        split_rows(bc, nr, i, x->lo[i], x->hi[i]);
+        const int64_t n = x->hi[i] - x->lo[i];
+        if (n <= 0) continue;
+        const size_t sz = row_size(t->type, x->K) * n + split_pad(t->type, x->K);
+        hipSetDevice(lane_device(i));
+        if (hipMalloc(&x->d[i], sz) != hipSuccess) { (void)hipGetLastError(); x->d[i] = nullptr; set_err("split buffer: hipMalloc failed"); continue; }
+        hipMemset(x->d[i], 0, sz);
+    }
+    ((SplitBufCtx *)b->context)->extras.push_back(x);
+    t->extra = x;
+}
+// split tensors are written and read whole (ggml-cuda.cu:750-752, 795-797)
+void sbuf_set_tensor(kggml_backend_buffer_t, kggml_tensor *t, const void *data, size_t off, size_t size) {
+    SplitExtra *x = (SplitExtra *)t->extra;
+    if (!x || off != 0 || size != nbytes(t)) { set_err("split buffer: tensors are set whole"); return; }
+    const size_t rb = row_size(t->type, x->K);
+    for (int i = 0; i < x->n; ++i) {
+        const int64_t n = x->hi[i] - x->lo[i];
+        if (n <= 0 || !x->d[i]) continue;
+        hipSetDevice(lane_device(i));
+        void *tmp = nullptr;
+        if (hipMalloc(&tmp, rb * n) != hipSuccess) { (void)hipGetLastError(); set_err("split buffer: upload scratch"); return; }
+        hipMemcpy(tmp, (const char *)data + x->lo[i] * rb, rb * n, hipMemcpyHostToDevice);
+        kcpp_weight_repack(x->tt, tmp, x->d[i], x->K, n, 0, nullptr);
+        hipDeviceSynchronize();
+        hipFree(tmp);
+    }
+}
+void sbuf_get_tensor(kggml_backend_buffer_t, const kggml_tensor *t, void *data, size_t off, size_t size) {
+    const SplitExtra *x = (const SplitExtra *)t->extra;
+    if (!x || off != 0 || size != nbytes(t)) { set_err("split buffer: tensors are read whole"); return; }
+    const size_t rb = row_size(t->type, x->K);
+    for (int i = 0; i < x->n; ++i) {
+        const int64_t n = x->hi[i] - x->lo[i];
+        if (n <= 0 || !x->d[i]) continue;
+        hipSetDevice(lane_device(i));
+        void *tmp = nullptr;
+        if (hipMalloc(&tmp, rb * n) != hipSuccess) { (void)hipGetLastError(); set_err("split buffer: download scratch"); return; }
+        kcpp_weight_repack(x->tt, x->d[i], tmp, x->K, n, 1, nullptr);
+        hipMemcpy((char *)data + x->lo[i] * rb, tmp, rb * n, hipMemcpyDeviceToHost);
+        hipFree(tmp);
+    }
+}
+void sbuf_clear(kggml_backend_buffer_t b, uint8_t v) {
+    for (SplitExtra *x : ((SplitBufCtx *)b->context)->extras)
+        for (int i = 0; i < x->n; ++i)
+            if (x->d[i]) {
+                hipSetDevice(lane_device(i));
+                hipMemset(x->d[i], v, row_size(x->gtype, x->K) * (x->hi[i] - x->lo[i]));
+            }
+}
+const kggml_backend_buffer_i kSplitBufIface = {sbuf_get_name, sbuf_free,       sbuf_get_base, sbuf_init_tensor, nullptr,
+                                               sbuf_set_tensor, sbuf_get_tensor, nullptr,     sbuf_clear,       nullptr};
+const char *sbuft_get_name(kggml_backend_buffer_type_t) { return KGGML_CUDA_NAME "_Split"; }
+bool buft_is_split(kggml_backend_buffer_type_t bt) { return bt && bt->iface.get_name == sbuft_get_name; }
+kggml_backend_buffer_t sbuft_alloc(kggml_backend_buffer_type_t bt, size_t size) {
+    // the slices are allocated per tensor in init_tensor; size bounds their sum (ggml-cuda.cu:860-868)
+    return new kggml_backend_buffer{kSplitBufIface, bt, new SplitBufCtx, size, KGGML_BACKEND_BUFFER_USAGE_ANY};
+}
+size_t sbuft_alignment(kggml_backend_buffer_type_t) { return 128; }
+size_t sbuft_alloc_size(kggml_backend_buffer_type_t bt, const kggml_tensor *t) {
+    const SplitBuftCtx *c = (const SplitBuftCtx *)bt->context;
+    size_t total = 0;
+    for (int i = 0; i < c->n; ++i) {
+        int64_t lo, hi;
+        split_rows(c, nrows(t), i, lo, hi);
+        if (hi > lo) total += row_size(t->type, t->ne[0]) * (hi - lo) + split_pad(t->type, t->ne[0]);
+    }
+    return total;
+}
+bool sbuft_is_host(kggml_backend_buffer_type_t) { return false; }
+const kggml_backend_buffer_type_i kSplitBuftIface = {sbuft_get_name, sbuft_alloc, sbuft_alignment, nullptr,
+                                                     sbuft_alloc_size, sbuft_is_host};
+
 bool supports(const kggml_tensor *op) {
     auto f32 = [](const kggml_tensor *t) { return t && t->type == KGGML_TYPE_F32; };
+    for (int i = 0; i < KGGML_MAX_SRC; ++i) {     // a split weight feeds only a quantized MUL_MAT (src0)
+        const kggml_tensor *sr = op->src[i];
+        if (!sr || !sr->buffer || !buffer_is_split(sr->buffer)) continue;
+        if (op->op != KGGML_OP_MUL_MAT || i != 0 || !matmul_quant_ok(sr->type) || sr->ne[2] != 1 || sr->ne[3] != 1 ||
+            !f32(op->src[1]) || op->src[1]->nb[0] != 4 || op->src[1]->ne[2] != 1 || op->src[1]->ne[3] != 1 ||
+            !is_contiguous(op) || sr->ne[0] % 256 != 0)
+            return false;
+        return true;
+    }
     switch (op->op) {
     case KGGML_OP_NONE: case KGGML_OP_RESHAPE: case KGGML_OP_VIEW: case KGGML_OP_PERMUTE: case KGGML_OP_TRANSPOSE:
         return true;
@@ -555,6 +717,59 @@ bool mul_mat_id(BackendCtx *bc, kggml_tensor *n) {
     return true;
 }
 
+// MUL_MAT on a split weight (see the split buffers above)
+bool mul_mat_split(BackendCtx *bc, kggml_tensor *n) {
+    hipStream_t s = bc->stream;
+    const kggml_tensor *a = n->src[0], *b = n->src[1];
+    const SplitExtra *x = (const SplitExtra *)a->extra;
+    if (!x) return set_err("mul_mat: split weight without slices");
+    const int64_t K = a->ne[0], N = a->ne[1], M = b->ne[1];
+    const size_t abytes = (size_t)kcpp_act_bytes(a->type, K, M);
+    void *act = bc->act.get(abytes + 256);
+    if (!act) return set_err("mul_mat(split): activation scratch allocation failed");
+    if (kcpp_quantize_act(kcpp_vec_dot_type(a->type), (const float *)b->data, (int64_t)(b->nb[1] / 4), act, K, M, s))
+        return set_err("mul_mat(split): quantize_act failed");
+    auto mm = [&](const void *W, int64_t rows, const void *ac, float *Y, int64_t ldy, Scratch &ws, hipStream_t st) {
+        if (M <= 8) return kcpp_gemv(x->tt, W, nullptr, K, rows, ac, M, Y, ldy, nullptr, 0, 0, st);
+        void *w = ws.get((size_t)kcpp_gemm_workspace_bytes(x->tt, K, rows, M) + 256);
+        if (!w) return -100;
+        return kcpp_gemm(x->tt, W, nullptr, K, rows, ac, M, Y, ldy, nullptr, 0, 0, w, st);
+    };
+    hipEvent_t ev_in = nullptr;
+    int inl = -1;
+    std::vector<SplitLane *> used;
+    for (int i = 0; i < x->n; ++i) {
+        const int64_t rows = x->hi[i] - x->lo[i];
+        if (rows <= 0 || !x->d[i]) continue;
+        if (inl < 0 && lane_device(i) == bc->device) { inl = i; continue; }
+        SplitLane *l = get_lane(i);
+        if (!l) return set_err("mul_mat(split): lane setup failed");
+        if (!ev_in) {
+            hipEventCreateWithFlags(&ev_in, hipEventDisableTiming);
+            hipEventRecord(ev_in, s);
+        }
+        hipSetDevice(l->dev);
+        void *lact = l->act.get(abytes + 256);
+        float *ly = (float *)l->y.get((size_t)rows * M * 4 + 256);
+        if (!lact || !ly) return set_err("mul_mat(split): lane scratch allocation failed");
+        hipStreamWaitEvent(l->s, ev_in, 0);
+        hipMemcpyPeerAsync(lact, l->dev, act, bc->device, abytes, l->s);
+        const int rc = mm(x->d[i], rows, lact, ly, rows, l->ws, l->s);
+        if (rc) { hipSetDevice(bc->device); return set_err("mul_mat(split): lane mat-mul failed rc=" + std::to_string(rc)); }
+        hipMemcpy2DAsync((float *)n->data + x->lo[i], N * 4, ly, rows * 4, rows * 4, M, hipMemcpyDefault, l->s);
+        hipEventRecord(l->done, l->s);
+        used.push_back(l);
+        hipSetDevice(bc->device);
+    }
+    if (inl >= 0) {
+        const int rc = mm(x->d[inl], x->hi[inl] - x->lo[inl], act, (float *)n->data + x->lo[inl], N, bc->ws, s);
+        if (rc) return set_err("mul_mat(split): main-device slice failed rc=" + std::to_string(rc));
+    }
+    for (SplitLane *l : used) hipStreamWaitEvent(s, l->done, 0);
+    if (ev_in) hipEventDestroy(ev_in);
+    return true;
+}
+
 bool compute_node(BackendCtx *bc, kggml_tensor *n) {
     hipStream_t s = bc->stream;
     const kcpp_tdesc td = td_of(n);
@@ -637,6 +852,7 @@ bool compute_node(BackendCtx *bc, kggml_tensor *n) {
                    "get_rows(quantized)");
     }
     case KGGML_OP_MUL_MAT: {
+        if (a->buffer && buffer_is_split(a->buffer)) return mul_mat_split(bc, n);
         if (a->type == KGGML_TYPE_F32 || a->type == KGGML_TYPE_F16) {
             const kcpp_tdesc ta = td_of(a), tb = td_of(b);
             // F16 weights: the reference CPU (AVX2/F16C build) hands contiguous f32 src1 with K % 8 == 0 to
@@ -797,6 +1013,7 @@ kggml_backend_buffer_type_t dev_get_buft(kggml_backend_dev_t d) { return ggml_ba
 kggml_backend_buffer_type_t dev_get_host_buft(kggml_backend_dev_t) { return ggml_backend_cuda_host_buffer_type(); }
 bool dev_supports_op(kggml_backend_dev_t, const kggml_tensor *op) { return supports(op); }
 bool dev_supports_buft(kggml_backend_dev_t d, kggml_backend_buffer_type_t bt) {
+    if (buft_is_split(bt)) return true;                       // ggml-cuda.cu:3188-3190
     return buft_is_ours(bt) && ((BuftCtx *)bt->context)->device == ((DevCtx *)d->context)->device;
 }
 // ggml-cuda.cu:3201-3208: batches of >= 32 pull CPU-resident weights over
@@ -864,7 +1081,24 @@ kggml_backend_buffer_type_t ggml_backend_cuda_buffer_type(int device) {
     if (device < 0 || device >= (int)g_bufts.size()) return nullptr;
     return &g_bufts[device];
 }
-kggml_backend_buffer_type_t ggml_backend_cuda_split_buffer_type(const float *) { return nullptr; }
+// one buffer type per split (ggml-cuda.cu:918-955); all zero = an even split
+kggml_backend_buffer_type_t ggml_backend_cuda_split_buffer_type(const float *tensor_split) {
+    std::call_once(g_init_once, init_registry);
+    if (g_devs.empty()) return nullptr;
+    const int n = n_lanes();
+    std::vector<float> key(n, 0.0f);
+    bool zero = true;
+    for (int i = 0; i < n; ++i) zero &= !tensor_split || tensor_split[i] == 0.0f;
+    for (int i = 0; i < n; ++i) key[i] = zero ? 1.0f : tensor_split[i];
+    std::lock_guard<std::mutex> lk(g_split_mu);
+    auto it = g_split_bufts.find(key);
+    if (it != g_split_bufts.end()) return &it->second;
+    SplitBuftCtx *c = new SplitBuftCtx{};
+    c->n = n;
+    for (int i = 0; i < n; ++i) c->split[i] = key[i];
+    auto r = g_split_bufts.emplace(key, kggml_backend_buffer_type{kSplitBuftIface, &g_devs[0], c});
+    return &r.first->second;
+}
 kggml_backend_buffer_type_t ggml_backend_cuda_host_buffer_type(void) {
     std::call_once(g_init_once, init_registry);
     return &g_host_buft;

@@ -650,3 +650,62 @@ def test_weight_buffer_holds_one_copy(env, t):
     assert rel(ours, ref) <= 3e-6
     G.ggml_backend_buffer_free(bw)
     G.ggml_free(ctx_w)
+
+
+@pytest.mark.parametrize("case", [(R.Q4_K, 4096, 1024, 1), (R.Q6_K, 4096, 768, 5), (R.Q4_0, 2048, 640, 24),
+                                  (R.Q8_0, 2048, 512, 40), (R.Q4_K, 2048, 1280, 33)], ids=lambda c: "t%d_%dx%d_m%d" % c)
+def test_split_buffer_mul_mat_vs_reference_cpu(env, case, monkeypatch):
+    """ggml_backend_cuda_split_buffer_type (ggml-cuda.cu:625-955, llama.cpp's --rowsplit buffers): the weight's rows
+    spread over 3 lanes by tensor_split 1:2:1 (KCPP_VIRTUAL_DEVICES=3 puts the lanes on the one test GPU), each slice
+    held in the device layout; MUL_MAT on the main device's backend with peer copies of the activation and of the
+    result rows equals the reference CPU; the weight reads back byte-exact; only MUL_MAT may read a split tensor"""
+    G, L, be = env
+    monkeypatch.setenv("KCPP_VIRTUAL_DEVICES", "3")
+    t, Kd, N, M = case
+    for n, a in {"ggml_backend_alloc_ctx_tensors_from_buft": ([P, P], P)}.items():
+        fn = getattr(G, n)
+        fn.argtypes, fn.restype = a
+    L.ggml_backend_cuda_split_buffer_type.argtypes, L.ggml_backend_cuda_split_buffer_type.restype = [P], P
+    ts = (ctypes.c_float * 16)(1.0, 2.0, 1.0)
+    sbt = L.ggml_backend_cuda_split_buffer_type(ts)
+    assert sbt
+    rng = np.random.default_rng(N + M)
+    w = R.synth(t, 12, 90 + t, Kd, N)
+    x = rng.standard_normal((M, Kd)).astype(np.float32)
+    ctx_w = G.ggml_init(InitParams(1 << 20, None, True))
+    W = G.ggml_new_tensor_2d(ctx_w, t, Kd, N)
+    bw = G.ggml_backend_alloc_ctx_tensors_from_buft(ctx_w, sbt)
+    assert bw
+    G.ggml_backend_tensor_set(W, w.ctypes.data, 0, w.nbytes)
+    back = np.empty_like(w)
+    G.ggml_backend_tensor_get(W, back.ctypes.data, 0, back.nbytes)
+    assert np.array_equal(back, w)
+    ctx = G.ggml_init(InitParams(1 << 20, None, True))
+    X = G.ggml_new_tensor_2d(ctx, R.F32, Kd, M)
+    out = G.ggml_mul_mat(ctx, W, X)
+    assert G.ggml_backend_supports_op(be, out)
+    Ix = G.ggml_new_tensor_1d(ctx, 26, 2)
+    assert not G.ggml_backend_supports_op(be, G.ggml_get_rows(ctx, W, Ix))
+    g = G.ggml_new_graph(ctx)
+    G.ggml_build_forward_expand(g, out)
+    bx = G.ggml_backend_alloc_ctx_tensors(ctx, be)
+    G.ggml_backend_tensor_set(X, x.ctypes.data, 0, x.nbytes)
+    assert G.ggml_backend_graph_compute(be, g) == 0, L.kcpp_ggml_backend_last_error()
+    ours = np.empty(M * N, np.float32)
+    G.ggml_backend_tensor_get(out, ours.ctypes.data, 0, ours.nbytes)
+    G.ggml_backend_buffer_free(bx)
+    G.ggml_free(ctx)
+    G.ggml_backend_buffer_free(bw)
+    G.ggml_free(ctx_w)
+    cctx = G.ggml_init(InitParams(64 << 20, None, False))
+    Wc = G.ggml_new_tensor_2d(cctx, t, Kd, N)
+    Xc = G.ggml_new_tensor_2d(cctx, R.F32, Kd, M)
+    oc = G.ggml_mul_mat(cctx, Wc, Xc)
+    gc = G.ggml_new_graph(cctx)
+    G.ggml_build_forward_expand(gc, oc)
+    ctypes.memmove(G.ggml_get_data(Wc), w.ctypes.data, w.nbytes)
+    ctypes.memmove(G.ggml_get_data(Xc), x.ctypes.data, x.nbytes)
+    assert G.ggml_graph_compute_with_ctx(cctx, gc, 4) == 0
+    ref = np.ctypeslib.as_array((ctypes.c_float * (M * N)).from_address(G.ggml_get_data(oc))).copy()
+    G.ggml_free(cctx)
+    assert rel(ours, ref) <= 3e-6, rel(ours, ref)
