@@ -145,3 +145,30 @@ def test_generate_with_context_shift(tmp_path, capfd):
     assert err.count("Context Shifting: Erased") == 1, err
     assert outs[0][0] == outs[1][0]                  # first request: identical paths
     assert outs[0][1][:1] == outs[1][1][:1]          # after the shift: same next token
+
+
+def _kshift_fixture():
+    import os
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kshift.npz"))
+
+
+@pytest.mark.parametrize("base", [10000, 500000])
+@pytest.mark.parametrize("diff", [1, 37, 1000])
+def test_kv_shift_rows_vs_reference_k_shift(env, base, diff):
+    """the K-shift pinned to the reference: llama.cpp's build_k_shift graph (ggml_rope_ext_inplace on the F16 K-cache
+    view at position -diff, rope_f16, src/llama.cpp:10144-10190) run by the reference library
+    (tests/golden/make_kshift.py)  ==  kcpp_kv_shift_rows with the runtime's (cos, sin) row, bit for bit"""
+    torch, K = env
+    fx = _kshift_fixture()
+    k = fx["k_in"]
+    n, HKV, D = k.shape
+    cs = rope_row(K, -diff, D, float(base))
+    kd = torch.from_numpy(k.view(np.int16).copy()).cuda()
+    vd = torch.zeros_like(kd)
+    ks, vs = torch.empty_like(kd), torch.empty_like(vd)
+    csd = torch.from_numpy(cs).cuda()
+    K.call("kcpp_kv_shift_rows", kd.data_ptr(), vd.data_ptr(), ks.data_ptr(), vs.data_ptr(), n * HKV, D, csd.data_ptr(),
+           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = ks.cpu().numpy().astype(np.uint16)
+    assert np.array_equal(got, fx["k_shift_%d_%d" % (base, diff)])
