@@ -809,6 +809,9 @@ __global__ void k_act_frag3(const uint8_t *__restrict__ act, int64_t K, int64_t 
 #ifndef V3_PRIO_DEF
 #define V3_PRIO_DEF 1
 #endif
+#ifndef KCPP_GEMM_PROBE
+#define KCPP_GEMM_PROBE 0       // timing probes only (tools/gemm_ab.py with a PROBE_DEFS build): 1 no loads in the
+#endif                          // super-block loop, 2 no main-loop MFMAs, 3 no barrier, 4 no A staging, 5 no weight loads
 constexpr bool V3_PRIO = V3_PRIO_DEF;
 
 template <int BMT> struct Q4v3Smem {
@@ -842,12 +845,29 @@ __device__ __forceinline__ uint32_t u4c(const uint4 &v, int i) { return i == 0 ?
 // TPW = 4 BMT / NW token tiles [TPW (w / 4), +TPW): NW = 4 dequantizes every B fragment once per workgroup and
 // feeds it to TPW MFMAs; NW = 8 (two waves per SIMD, so one wave's LDS reads and dequantization hide under the
 // other's MFMAs) dequantizes each row twice.  BMT = 2 doubles the grid of small-N shapes (wo, q|k|v, down).
-template <int LAY, int NW, int BMT>
-__global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restrict__ W, int64_t K, int64_t N,
+// XCD-aware tile order: blocks b and b + 8 share an XCD (dealt round-robin).  XCD x serves token tiles
+// [G set, +G) (set = x % (MT / G)) against the row tiles of class x / (MT / G): the G token-tile workgroups of one
+// row tile run back to back on one XCD, so its weights come from HBM once and from that XCD's L2 G - 1 times,
+// while the XCD's L2 holds G token tiles of activations.  Falls back to plain order when the grid does not divide.
+__device__ __forceinline__ void xcd_tile(int64_t id, int64_t nwg, int MT, int64_t ntn, int G, int64_t &mt, int64_t &nt) {
+    const int nset = G > 0 && MT % G == 0 ? MT / G : 0;
+    const int xper = nset > 0 && 8 % nset == 0 ? 8 / nset : 0;
+    if (xper > 0 && nwg % 8 == 0 && ntn % xper == 0) {
+        const int64_t x = id & 7, j = id >> 3;
+        mt = (x % nset) * G + j % G;
+        nt = (j / G) * xper + x / nset;
+    } else {
+        mt = id % MT;
+        nt = id / MT;
+    }
+}
+
+template <int LAY, int NW, int BMT, int PF>
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) k_gemm_q4v3(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                                          const h8v *__restrict__ af, const float *__restrict__ dyT,
                                                          const h8v *__restrict__ bsf, int64_t M, int64_t Mp, int MT,
                                                          float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr,
-                                                         int KS, float *__restrict__ part) {
+                                                         int KS, float *__restrict__ part, int XG) {
     constexpr int TPW = 4 * BMT / NW;         // token tiles per wave
     constexpr int SPW = 16 * BMT / NW;        // A staging: LDS-DMA steps per wave and super-block
     static_assert(TPW >= 1 && SPW >= 1, "tile shape");
@@ -862,14 +882,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
     const int64_t nwg = gridDim.x / KS, id = blockIdx.x % nwg;
     const int split = (int)(blockIdx.x / nwg);
     int64_t mt, nt;
-    if (8 % MT == 0 && nwg % 8 == 0) {
-        const int64_t x = id & 7, j = id >> 3;
-        mt = x % MT;
-        nt = j * (8 / MT) + x / MT;
-    } else {
-        mt = id % MT;
-        nt = id / MT;
-    }
+    xcd_tile(id, nwg, MT, (N + 127) / 128, XG, mt, nt);
     const int64_t m0 = mt * 32 * BMT, n0 = nt * 128;
     const int64_t nsb = K / 256, bpr = nsb;
     // this lane's weight row; clamped at N (its results are not stored)
@@ -895,11 +908,13 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
         if (wave < BMT) glds16(bsrc + sb * 64, &S.bs[buf][stt][0]);
         if (wave == 0 && lane < 8 * BMT) glds16(dsrc + sb * Mp, &S.dy[buf][0]);
     };
-    uint4 hn, qn[4];
-    auto load_raw = [&](int64_t sb) {
-        hn = ldg16(hp + HS * sb);
+    // raw weight super-blocks are loaded PF ahead into register sets X / Y (PF = 2: ping-pong, the loop unrolled
+    // by two so each set stays in fixed registers); sb's set is copied out before it is refilled with sb + PF
+    uint4 hX, qX[4], hY, qY[4];
+    auto load_raw = [&](int64_t sb, uint4 &h, uint4 (&q)[4]) {
+        h = ldg16(hp + HS * sb);
 #pragma unroll
-        for (int p = 0; p < 4; ++p) qn[p] = ldg16(qp + QS * sb + 32 * p);
+        for (int p = 0; p < 4; ++p) q[p] = ldg16(qp + QS * sb + 32 * p);
     };
 
     const int64_t sbb = nsb * split / KS, sbe = nsb * (split + 1) / KS;
@@ -909,22 +924,24 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
 #pragma unroll
         for (int i = 0; i < 16; ++i) tot[j][i] = 0.0f;
     stage(0, sbb);
-    load_raw(sbb);
+    load_raw(sbb, hX, qX);
+    if (PF == 2 && sbb + 1 < sbe) load_raw(sbb + 1, hY, qY);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
-    for (int64_t sb = sbb; sb < sbe; ++sb) {
-        const int buf = (int)((sb - sbb) & 1);
-        const uint4 hc = hn;
+    auto body = [&](int64_t sb, int buf, uint4 &hs, uint4 (&qs)[4]) {
+        const uint4 hc = hs;
         uint32_t sc_lo, sc_hi, m_lo, m_hi;
         k4_all(hc, sc_lo, sc_hi, m_lo, m_hi);
         uint4 qc[4];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) qc[p] = qn[p];
-        if (sb + 1 < sbe) {
-            stage(buf ^ 1, sb + 1);
-            load_raw(sb + 1);
-        }
+        for (int p = 0; p < 4; ++p) qc[p] = qs[p];
+#if KCPP_GEMM_PROBE != 1 && KCPP_GEMM_PROBE != 4
+        if (sb + 1 < sbe) stage(buf ^ 1, sb + 1);
+#endif
+#if KCPP_GEMM_PROBE != 1 && KCPP_GEMM_PROBE != 5
+        if (sb + PF < sbe) load_raw(sb + PF, hs, qs);
+#endif
         f16acc acc[TPW];
 #pragma unroll
         for (int j = 0; j < TPW; ++j)
@@ -953,8 +970,13 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
             }
             const h8v b = frag_q4v3(u4c(qc[p], st), (float)s0, (float)s1);
             if constexpr (V3_PRIO) __builtin_amdgcn_s_setprio(1);
+#if KCPP_GEMM_PROBE == 2
+#pragma unroll
+            for (int j = 0; j < TPW; ++j) acc[j][0] += (float)ac[j][0] * (float)b[0];
+#else
 #pragma unroll
             for (int j = 0; j < TPW; ++j) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ac[j], b, acc[j], 0, 0, 0);
+#endif
             if constexpr (V3_PRIO) __builtin_amdgcn_s_setprio(0);
         }
         // epilogue: tot -= dy * dmin * (sum_j m_j bsum_j), then tot += dy * (d * S)  (k_gemm_kq's order)
@@ -985,8 +1007,25 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q4v3(const uint8_t *__restr
 #pragma unroll
             for (int r = 0; r < 16; ++r) tot[j][r] = fmaf(dyv[r], __fmul_rn(dw, acc[j][r]), tot[j][r]);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // the next super-block's A copy (and, PF = 2, its raw weights) must have landed; sb + 2's raw loads, issued
+        // last, may stay in flight (loads retire in order)
+        if (PF == 2 && sb + 2 < sbe) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if KCPP_GEMM_PROBE != 3
         __syncthreads();
+#endif
+    };
+    if constexpr (PF == 2) {
+        int64_t sb = sbb;
+        for (; sb + 1 < sbe; sb += 2) {
+            body(sb, 0, hX, qX);
+            __builtin_amdgcn_sched_barrier(0);
+            body(sb + 1, 1, hY, qY);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        if (sb < sbe) body(sb, 0, hX, qX);
+    } else {
+        for (int64_t sb = sbb; sb < sbe; ++sb) body(sb, (int)((sb - sbb) & 1), hX, qX);
     }
     const int64_t n = n0 + 32 * wr + lr;
     if (n >= N) return;
@@ -1372,6 +1411,221 @@ static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a
     return off;
 }
 
+
+// ================================================================ Q4_K GEMM v4 (int8 matrix cores)
+// v3 is bound by moving operands, not by the matrix cores (probes at M = 512, gate|up 4096 x 28672: 266 us, 142 us
+// with the in-loop loads removed, 216 us with the MFMAs removed): its f16 activation image is twice the Q8_K bytes
+// and every weight row is loaded by two waves one super-block ahead.  v4 multiplies the Q8_K bytes themselves on
+// v_mfma_i32_32x32x32_i8, one MFMA per 32-element sub-block and token tile, with an exact int32 accumulator:
+//   sum_k q*sc*a = 8 * sum_k (q*(sc>>3))*a + sum_k (q*(sc&7))*a,  q*(sc>>3), q*(sc&7) <= 105 (int8),
+// so each sub-block takes two MFMAs into acc_h / acc_l and isum = 8 acc_h + acc_l is the CPU's int32 sumi exactly
+// (v3 holds the same integer in fp32); the per-super-block epilogue is v3's, so the results are bit-identical.
+// Operands are staged with LDS-DMA straight from the Q8_K buffer (no fragment-image kernel): per super-block the
+// workgroup's 128 token rows x 256 B of int8, their bsums and scales, and its 128 weight rows' 144 B, the weights
+// in a 3-stage ring two super-blocks ahead (HBM latency), the activations double-buffered one ahead (L2 hits).
+// Workgroup = 128 tokens x 128 weight rows, 8 waves; wave w: weight rows 32 (w & 3) .. +32 x token tiles
+// 2 (w >> 2), +1.  Fragment k order: lane half g of token / weight row r holds bytes 16g .. 16g+15 of the
+// sub-block (any order common to both operands is exact); the Q4_K byte j of pair p holds element j of sub-block
+// 2p (low nibble) and 2p+1 (high nibble).
+struct Q4v4Smem {
+    i32x4 a[2][4][8][64];    // [buf][token tile][sub-block][lane]: 16 activation bytes
+    i32x4 bs[2][4][64];      // [buf][token tile][lane]: 8 bsums (int16) of the lane half's 128 elements
+    float dy[2][128];        // [buf][token]: Q8_K scale of the super-block
+    uint4 wh[3][4][32];      // [stage][row tile][row]: Q4_K header (d, dmin, 12 B scales / mins)
+    i32x4 wq[3][4][4][64];   // [stage][row tile][pair][lane]: qs bytes 32 p + 16 g .. +16 of the lane's row
+};
+
+// LDS-DMA issued from inline asm: the compiler does not track these writes, so it inserts no vmcnt(0) in front of
+// the LDS reads that follow (it cannot tell the ring stage being filled from the one being read, and a compiler-
+// visible DMA would drain every prefetch at the first read); the kernel orders them itself (s_waitcnt + barrier).
+// lds_base: wave-uniform LDS byte address; lane l writes lds_base + size * l.
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ void dma16(const void *g, const void *lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g),
+                 "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_base))) : "memory", "m0");
+}
+__device__ __forceinline__ void dma4(const void *g, const void *lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g),
+                 "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_base))) : "memory", "m0");
+}
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+// bytes of x (each <= 15) times s (<= 7), per byte: two 16-bit lanes, no carry out of a byte (v_pk_mul_lo_u16)
+__device__ __forceinline__ int mulb(uint32_t x, uint32_t s2) {
+    return (int)__builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, x) * __builtin_bit_cast(u16x2, s2));
+}
+
+template <int LAY>
+__global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict__ W, int64_t K, int64_t N,
+                                                     const uint8_t *__restrict__ act, int64_t M, int64_t Mp, int MT,
+                                                     float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr,
+                                                     int KS, float *__restrict__ part, int XG) {
+    __shared__ Q4v4Smem S;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave & 3, wt = wave >> 2;
+    const int lr = lane & 31, kg = lane >> 5;
+    const int64_t nwg = gridDim.x / KS, id = blockIdx.x % nwg;
+    const int split = (int)(blockIdx.x / nwg);
+    int64_t mt, nt;
+    xcd_tile(id, nwg, MT, (N + 127) / 128, XG, mt, nt);
+    const int64_t m0 = mt * 128, n0 = nt * 128;
+    const int64_t nsb = K / 256, bpr = nsb;
+    const int8_t *qs = (const int8_t *)act;
+    const float *dq = (const float *)(act + M * K);
+    const int16_t *bsq = (const int16_t *)(act + M * K + M * nsb * 4);
+    // DMA assignments (per super-block): A: token tile wave & 3, sub-blocks 4 (wave >> 2) .. +4; bsums: waves 0-3
+    // (tile = wave); dy: waves 4, 5 (tokens 64 (wave - 4) .. +64); weights: qs pairs 2 (wave >> 2), +1 of row tile
+    // wave & 3; headers: waves 0, 1 (row tiles 2 wave + (lane >> 5))
+    const int att = wave & 3, asub = 4 * (wave >> 2);
+    const int8_t *arow = qs + min(m0 + 32 * att + lr, M - 1) * K + 16 * kg;
+    const int16_t *bsrow = bsq + min(m0 + 32 * wave + lr, M - 1) * (K / 16) + 8 * kg;
+    const float *dyrow = dq + min(m0 + 64 * max(wave - 4, 0) + lane, M - 1) * nsb;
+    const int wrt = wave & 3, wp = 2 * (wave >> 2);
+    const int64_t wrow = min(n0 + 32 * wrt + lr, N - 1);
+    const int hrt = 2 * wave + kg;
+    const int64_t hrow = min(n0 + 32 * hrt + lr, N - 1);
+    constexpr int64_t HS = LAY == 1 ? 16 : 144, QS = LAY == 1 ? 128 : 144;
+    const uint8_t *wq0 = LAY == 1 ? W + wrow * 144 * bpr + 16 * bpr + 16 * kg : W + wrow * 144 * bpr + 16 + 16 * kg;
+    const uint8_t *wh0 = W + hrow * 144 * bpr;
+    auto stage_a = [&](int buf, int64_t sb) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dma16(arow + sb * 256 + 32 * (asub + u), &S.a[buf][att][asub + u][0]);
+        if (wave < 4) dma16(bsrow + sb * 16, &S.bs[buf][wave][0]);
+        else if (wave < 6) dma4(dyrow + sb, &S.dy[buf][64 * (wave - 4)]);
+    };
+    auto stage_w = [&](int st, int64_t sb) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) dma16(wq0 + QS * sb + 32 * (wp + u), &S.wq[st][wrt][wp + u][0]);
+        if (wave < 2) dma16(wh0 + HS * sb, &S.wh[st][2 * wave][0]);
+    };
+
+    const int64_t sbb = nsb * split / KS, sbe = nsb * (split + 1) / KS;
+    f16acc tot[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tot[j][i] = 0.0f;
+    stage_a(0, sbb);
+    stage_w(0, sbb);
+    if (sbb + 1 < sbe) stage_w(1, sbb + 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    int st = 0;
+    for (int64_t sb = sbb; sb < sbe; ++sb) {
+        const int buf = (int)((sb - sbb) & 1);
+        const bool w2 = sb + 2 < sbe && KCPP_GEMM_PROBE != 1 && KCPP_GEMM_PROBE != 5;
+#if KCPP_GEMM_PROBE != 1 && KCPP_GEMM_PROBE != 4
+        if (sb + 1 < sbe) stage_a(buf ^ 1, sb + 1);
+#endif
+        if (w2) stage_w(st == 0 ? 2 : st - 1, sb + 2);
+        const uint4 hc = S.wh[st][wr][lr];
+        uint32_t sc_lo, sc_hi, m_lo, m_hi;
+        k4_all(hc, sc_lo, sc_hi, m_lo, m_hi);
+        i32x16 ah[2], al[2];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            const i32x4 w4 = S.wq[st][wr][p][lane];
+            const uint32_t sdw = p < 2 ? sc_lo : sc_hi;
+            const uint32_t s0 = (sdw >> (16 * (p & 1))) & 0xFF, s1 = (sdw >> (16 * (p & 1) + 8)) & 0xFF;
+            const uint32_t h0 = (s0 >> 3) * 0x10001u, l0 = (s0 & 7) * 0x10001u;
+            const uint32_t h1 = (s1 >> 3) * 0x10001u, l1 = (s1 & 7) * 0x10001u;
+            i32x4 bh0, bl0, bh1, bl1;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t x = (uint32_t)w4[e];
+                const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
+                bh0[e] = mulb(lo, h0);
+                bl0[e] = mulb(lo, l0);
+                bh1[e] = mulb(hi, h1);
+                bl1[e] = mulb(hi, l1);
+            }
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int tt = 2 * wt + j;
+                const i32x4 a0 = S.a[buf][tt][2 * p][lane], a1 = S.a[buf][tt][2 * p + 1][lane];
+#if KCPP_GEMM_PROBE == 2
+                ah[j][0] += a0[0] * bh0[0] + a1[1] * bl1[1];
+                al[j][0] += a0[1] * bl0[0] + a1[0] * bh1[1];
+                continue;
+#endif
+                if (p == 0) {
+                    i32x16 z;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) z[i] = 0;
+                    ah[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bh0, z, 0, 0, 0);
+                    al[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bl0, z, 0, 0, 0);
+                } else {
+                    ah[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bh0, ah[j], 0, 0, 0);
+                    al[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bl0, al[j], 0, 0, 0);
+                }
+                ah[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bh1, ah[j], 0, 0, 0);
+                al[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bl1, al[j], 0, 0, 0);
+            }
+        }
+        // epilogue (v3's): tot -= dy * dmin * (sum_j m_j bsum_j), then tot += dy * (d * isum)
+        h8v bm;
+        const uint32_t mdw = kg ? m_hi : m_lo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const _Float16 mn = (_Float16)(float)((mdw >> (8 * e)) & 0xFF);
+            bm[2 * e] = mn;
+            bm[2 * e + 1] = mn;
+        }
+        const float dw = h2f((uint16_t)(hc.x & 0xFFFF)), dm = h2f((uint16_t)(hc.x >> 16));
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int tt = 2 * wt + j;
+            float dyv[16];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = *(const float4 *)&S.dy[buf][32 * tt + 8 * q + 4 * kg];
+                dyv[4 * q] = v.x; dyv[4 * q + 1] = v.y; dyv[4 * q + 2] = v.z; dyv[4 * q + 3] = v.w;
+            }
+            const i32x4 bsv = S.bs[buf][tt][lane];
+            h8v ab;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                ab[2 * e] = (_Float16)(int16_t)(bsv[e] & 0xFFFF);
+                ab[2 * e + 1] = (_Float16)(int16_t)((uint32_t)bsv[e] >> 16);
+            }
+            f16acc accm;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) accm[i] = 0.0f;
+            accm = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab, bm, accm, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) tot[j][r] = fmaf(-__fmul_rn(dyv[r], dm), accm[r], tot[j][r]);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float is = (float)(ah[j][r] * 8 + al[j][r]);
+                tot[j][r] = fmaf(dyv[r], __fmul_rn(dw, is), tot[j][r]);
+            }
+        }
+        // A (sb + 1) and W (sb + 1) must have landed; W (sb + 2), issued last, may stay in flight (in-order retire)
+        if (w2) {
+            if (wave < 2) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        st = st == 2 ? 0 : st + 1;
+    }
+    const int64_t n = n0 + 32 * wr + lr;
+    if (n >= N) return;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t t = m0 + 32 * (2 * wt + j) + (r & 3) + 8 * (r >> 2) + 4 * kg;
+            if (KS > 1) part[((int64_t)split * Mp + t) * N + n] = tot[j][r];
+            else if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
+        }
+}
+
 static int g_gemm_variant = -1;
 static int gemm_variant() {
     if (g_gemm_variant < 0) g_gemm_variant = 0;
@@ -1487,12 +1741,47 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     // 43.3 -> 45.6 us (not split), gate|up (big grid) 236.8 -> 273.0 us (not split).
     // kcpp_gemm_set_variant: 2 forces v2, 3 v3 without the split, 4 v3 with the split wherever the mode allows
     const int gv = gemm_variant();
-    const bool v3 = gv == 3 || gv == 0 || gv == 4;
+    const bool v3 = gv == 0 || (gv >= 3 && gv <= 13);
     float *part = (float *)(w8 + o_up + ((M * N * 4 + 255) & ~255LL));
     auto splitk = [&](bool big, int64_t tiles) {
         if (mode != 0 || (K / 256) % 2) return 1;
         return (gv == 4 || (gv == 0 && !big && (tiles < 128 || K / 256 >= 32))) ? 2 : 1;
     };
+    const bool bs_aligned = ((uintptr_t)((const uint8_t *)act + M * K + M * (K / 256) * 4) & 15) == 0;
+    // v4 where it measured faster (tools/gemm_ab.py, M = 512): the big grids (gate|up 28672 rows: 227-230 vs 234-242 us)
+    // and the long-K shapes with split-K (down 14336 -> 4096: 93-96 vs 115 us); v3's 64-token tiles stay ahead on the
+    // 4096-6144-row shapes (q|k|v 63.8 vs 69.5 us, wo even).  Variant 11 forces v4, 13 v4 unsplit, 3 / 4 force v3.
+    const bool v4_pick = gv == 0 && (Mp / 128 * ((N + 127) / 128) >= 384 || (K / 256 >= 32 && mode == 0));
+    if ((type == KT_Q4_K || type == KT_Q4_K_RS) && (gv == 11 || gv == 12 || gv == 13 || v4_pick) && bs_aligned && M > 32) {
+        // v4: int8 MFMA straight from the Q8_K buffer (no fragment image); 128 x 128 tiles, split-K when the tile
+        // grid is small
+        const int64_t nt = (N + 127) / 128;
+        const int MT = (int)(Mp / 128);
+        const int KS = (gv != 13 && mode == 0 && (K / 256) % 2 == 0 && MT * nt < 384) ? 2 : 1;
+        const unsigned nwg = (unsigned)(MT * nt * KS);
+        const int XG = gv == 12 ? 2 : 1;
+        auto launch4 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
+            if (type == KT_Q4_K_RS)
+                hipLaunchKernelGGL(k_gemm_q4v4<1>, dim3(nwg), dim3(512), 0, s, (const uint8_t *)w, K, N, (const uint8_t *)act,
+                                   M, Mp, MT, y, ly, r, lr, KS, part, XG);
+            else
+                hipLaunchKernelGGL(k_gemm_q4v4<0>, dim3(nwg), dim3(512), 0, s, (const uint8_t *)w, K, N, (const uint8_t *)act,
+                                   M, Mp, MT, y, ly, r, lr, KS, part, XG);
+            KCPP_CHECK(hipGetLastError());
+            if (KS > 1) {
+                hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,
+                                   ly, r, lr);
+                KCPP_CHECK(hipGetLastError());
+            }
+            return 0;
+        };
+        int rc = launch4(W, Y, ldy, mode == 1 ? nullptr : res, ldr);
+        if (rc || mode != 1) return rc;
+        if ((rc = launch4(W2, up, N, nullptr, 0))) return rc;
+        hipLaunchKernelGGL(k_silu_mul_strided, dim3((unsigned)((N * M + 255) / 256)), dim3(256), 0, s, Y, ldy, up, N, M);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
     if ((type == KT_Q4_K || type == KT_Q4_K_RS) && v3) {
         const int64_t nth = Mp * K / 8 + (Mp / 32) * (K / 256) * 64 + Mp * (K / 256);
         hipLaunchKernelGGL(k_act_frag3, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
@@ -1503,14 +1792,17 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         const int64_t nt = (N + 127) / 128;
         const bool big = Mp / 128 * nt >= 384;
         const int BMT = big ? 4 : 2;
-        const int NWv = big ? 8 : 4;
+        const int NWv = (gv == 6 || gv == 7) ? 4 : (big ? 8 : 4);
+        const int XG = gv == 8 ? 2 : (gv == 9 ? 4 : (gv == 10 ? 8 : 1));
         const int MT = (int)(Mp / (32 * BMT));
         const int KS = splitk(big, MT * nt);
         const unsigned nwg = (unsigned)(MT * nt * KS);
         auto launch3 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
 #define KCPP_V3(L_, NW_, B_)                                                                                                 \
-    hipLaunchKernelGGL((k_gemm_q4v3<L_, NW_, B_>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, \
-                       dy, (const h8v *)bs16, M, Mp, MT, y, ly, r, lr, KS, part)
+    if (gv == 5 || gv == 6) hipLaunchKernelGGL((k_gemm_q4v3<L_, NW_, B_, 2>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)w, K, N,      \
+                       (const h8v *)a16, dy, (const h8v *)bs16, M, Mp, MT, y, ly, r, lr, KS, part, XG);                      \
+    else hipLaunchKernelGGL((k_gemm_q4v3<L_, NW_, B_, 1>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, \
+                       dy, (const h8v *)bs16, M, Mp, MT, y, ly, r, lr, KS, part, XG)
 #define KCPP_V3B(L_, B_) { if (NWv == 4) KCPP_V3(L_, 4, B_); else KCPP_V3(L_, 8, B_); }
             if (type == KT_Q4_K_RS) { if (BMT == 2) KCPP_V3B(1, 2) else KCPP_V3B(1, 4) }
             else { if (BMT == 2) KCPP_V3B(0, 2) else KCPP_V3B(0, 4) }

@@ -271,3 +271,40 @@ def test_gemm_v3_split_k(env, base, Kd, N, M):
     assert np.abs(outs[4] - outs[3]).max() <= 2e-6 * scale
     want = R.mul_mat(bt, R.synth(bt, 7, 5, Kd, N), Kd, N, Xh) + resh
     assert np.abs(outs[4] - want).max() <= 3e-6 * max(1.0, float(np.abs(want).max())) + 1e-5
+
+
+@pytest.mark.parametrize("base", [R.Q4_K, "rs"])
+@pytest.mark.parametrize("Kd,N,M", [(4096, 512, 37), (4096, 640, 128), (2048, 1024, 300), (14336, 256, 512),
+                                    (4096, 384, 200)])
+def test_gemm_v4_int8_matches_v2_bitwise(env, base, Kd, N, M):
+    """Q4_K GEMM v4 (v_mfma_i32_32x32x32_i8 on the Q8_K bytes, isum = 8 acc(q*(sc>>3)) + acc(q*(sc&7)) in int32,
+    operands by LDS-DMA straight from the Q8_K buffer): the same integer sumi as v2's exact fp32 sums and the same
+    per-super-block epilogue, so bit-identical unsplit (kcpp_gemm_set_variant(13)), plain+residual and GLU, ragged M
+    (token rows past M clamp to M - 1 and are not stored) and N; the split-K default (11) within the GEMM bar"""
+    torch, K = env
+    t = RS[R.Q4_K] if base == "rs" else R.Q4_K
+    s = sptr(torch)
+    Xh = np.random.default_rng(M + Kd + 7).standard_normal((M, Kd)).astype(np.float32)
+    X = torch.from_numpy(Xh).cuda()
+    act = torch.zeros(K.act_bytes(R.Q4_K, Kd, M), dtype=torch.uint8, device="cuda")
+    K.call("kcpp_quantize_act", K.vec_dot_type(R.Q4_K), X.data_ptr(), Kd, act.data_ptr(), Kd, M, s)
+    res = torch.randn(M, N).cuda()
+    W, W2 = _synth(torch, K, t, Kd, N, 3), _synth(torch, K, t, Kd, N, 4)
+    ws = torch.empty(K.raw().kcpp_gemm_workspace_bytes(t, Kd, N, M), dtype=torch.uint8, device="cuda")
+    outs = {}
+    try:
+        for v in (2, 13, 11):
+            K.raw().kcpp_gemm_set_variant(v)
+            for mode in (0, 1):
+                Y = torch.full((M, N), float("nan"), device="cuda")
+                K.call("kcpp_gemm", t, W.data_ptr(), W2.data_ptr() if mode == 1 else None, Kd, N, act.data_ptr(), M,
+                       Y.data_ptr(), N, res.data_ptr() if mode == 0 else None, N, mode, ws.data_ptr(), s)
+                torch.cuda.synchronize()
+                outs[v, mode] = Y.cpu().numpy()
+    finally:
+        K.raw().kcpp_gemm_set_variant(0)
+    for mode in (0, 1):
+        assert np.isfinite(outs[13, mode]).all()
+        assert np.array_equal(outs[2, mode].view(np.uint32), outs[13, mode].view(np.uint32)), mode
+        scale = max(1.0, float(np.abs(outs[2, mode]).max()))
+        assert np.abs(outs[11, mode] - outs[2, mode]).max() <= 2e-6 * scale

@@ -32,6 +32,7 @@ def main():
         K.call("kcpp_quantize_act", K.vec_dot_type(12), X.data_ptr(), Kd, act.data_ptr(), Kd, M, sp)
         Y = torch.empty(M, N, device="cuda")
         ws = torch.empty(K.raw().kcpp_gemm_workspace_bytes(t, Kd, N, M), dtype=torch.uint8, device="cuda")
+        y0 = None
         for v in variants:
             K.raw().kcpp_gemm_set_variant(v)
             run = lambda i: K.call("kcpp_gemm", t, ws_[i % nrot].data_ptr(), ws_[(i + 1) % nrot].data_ptr() if mode else None,
@@ -47,9 +48,16 @@ def main():
             e1.record(s)
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) / it * 1e3
+            run(0)
+            torch.cuda.synchronize()
+            same = None
+            if y0 is None:
+                y0 = Y.clone()
+            else:
+                same = bool(torch.equal(Y, y0))
             fl = 2.0 * M * N * Kd * (2 if mode else 1)
             print(json.dumps({"shape": name, "type": t, "M": M, "K": Kd, "N": N, "variant": v, "us": round(us, 1),
-                              "TFLOPs": round(fl / us / 1e6, 1)}), flush=True)
+                              "TFLOPs": round(fl / us / 1e6, 1), "bitwise_equal_first": same}), flush=True)
     K.raw().kcpp_gemm_set_variant(0)
 
 
