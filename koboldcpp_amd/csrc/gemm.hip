@@ -1427,12 +1427,19 @@ static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a
 // 2 (w >> 2), +1.  Fragment k order: lane half g of token / weight row r holds bytes 16g .. 16g+15 of the
 // sub-block (any order common to both operands is exact); the Q4_K byte j of pair p holds element j of sub-block
 // 2p (low nibble) and 2p+1 (high nibble).
+// Swizzled LDS images: one LDS-DMA instruction (64 lanes x 16 B, lane-linear in LDS) fetches 8 rows x 8 chunks of
+// 16 B -- one 128-B line per row (a fragment-ordered fetch touches 32 lines per instruction) -- lane j: row
+// 8k + (j & 7), chunk 8h + (j >> 3), at slot 72 (4h + k) + j (72: rows 8 apart start 8 slots apart mod 16, so the
+// 16-lane groups of a fragment read hit 16 distinct bank quads: conflict-free).  Chunk c of row m of a 32-row tile:
+// slot 72 (4 (c >> 3) + (m >> 3)) + (m & 7) + 8 (c & 7).
+__device__ __forceinline__ int swz(int m, int c) { return 72 * (4 * (c >> 3) + (m >> 3)) + (m & 7) + 8 * (c & 7); }
+
 struct Q4v4Smem {
-    i32x4 a[2][4][8][64];    // [buf][token tile][sub-block][lane]: 16 activation bytes
+    i32x4 a[2][4][576];      // [buf][token tile][swz(row, chunk)]: 16 activation bytes, chunks 0..15 of the 256
     i32x4 bs[2][4][64];      // [buf][token tile][lane]: 8 bsums (int16) of the lane half's 128 elements
     float dy[2][128];        // [buf][token]: Q8_K scale of the super-block
     uint4 wh[3][4][32];      // [stage][row tile][row]: Q4_K header (d, dmin, 12 B scales / mins)
-    i32x4 wq[3][4][4][64];   // [stage][row tile][pair][lane]: qs bytes 32 p + 16 g .. +16 of the lane's row
+    i32x4 wq[3][4][288];     // [stage][row tile][swz(row, chunk)]: qs chunks 0..7 (pair p, half g: chunk 2p + g)
 };
 
 // LDS-DMA issued from inline asm: the compiler does not track these writes, so it inserts no vmcnt(0) in front of
@@ -1452,9 +1459,11 @@ __device__ __forceinline__ void dma4(const void *g, const void *lds_base) {
 }
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-// bytes of x (each <= 15) times s (<= 7), per byte: two 16-bit lanes, no carry out of a byte (v_pk_mul_lo_u16)
-__device__ __forceinline__ int mulb(uint32_t x, uint32_t s2) {
-    return (int)__builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, x) * __builtin_bit_cast(u16x2, s2));
+// bytes of x (each <= 15) times s (<= 7), per byte: two 16-bit lanes, no carry out of a byte (v_pk_mul_lo_u16;
+// the scalar factor is taken for both halves by op_sel)
+__device__ __forceinline__ int mulb(uint32_t x, uint32_t s) {
+    const u16x2 f = {(unsigned short)s, (unsigned short)s};
+    return (int)__builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, x) * f);
 }
 
 template <int LAY>
@@ -1479,26 +1488,31 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
     // DMA assignments (per super-block): A: token tile wave & 3, sub-blocks 4 (wave >> 2) .. +4; bsums: waves 0-3
     // (tile = wave); dy: waves 4, 5 (tokens 64 (wave - 4) .. +64); weights: qs pairs 2 (wave >> 2), +1 of row tile
     // wave & 3; headers: waves 0, 1 (row tiles 2 wave + (lane >> 5))
-    const int att = wave & 3, asub = 4 * (wave >> 2);
-    const int8_t *arow = qs + min(m0 + 32 * att + lr, M - 1) * K + 16 * kg;
+    // A: token tile wave & 3, chunk half wave >> 2, row groups 0..3; lane: row 8k + (lane & 7), chunk 8h + (lane >> 3)
+    const int att = wave & 3, ah8 = wave >> 2;
+    const int8_t *arow = qs + min(m0 + 32 * att + (lane & 7), M - 1) * K + 16 * (8 * ah8 + (lane >> 3));
     const int16_t *bsrow = bsq + min(m0 + 32 * wave + lr, M - 1) * (K / 16) + 8 * kg;
     const float *dyrow = dq + min(m0 + 64 * max(wave - 4, 0) + lane, M - 1) * nsb;
-    const int wrt = wave & 3, wp = 2 * (wave >> 2);
-    const int64_t wrow = min(n0 + 32 * wrt + lr, N - 1);
+    // W qs: row tile wave & 3, row groups 2 (wave >> 2), +1; lane: row 8k + (lane & 7), chunk lane >> 3
+    const int wrt = wave & 3, wk = 2 * (wave >> 2);
+    const int64_t wrow = min(n0 + 32 * wrt + 8 * wk + (lane & 7), N - 1);
     const int hrt = 2 * wave + kg;
     const int64_t hrow = min(n0 + 32 * hrt + lr, N - 1);
     constexpr int64_t HS = LAY == 1 ? 16 : 144, QS = LAY == 1 ? 128 : 144;
-    const uint8_t *wq0 = LAY == 1 ? W + wrow * 144 * bpr + 16 * bpr + 16 * kg : W + wrow * 144 * bpr + 16 + 16 * kg;
+    const uint8_t *wq0 = (LAY == 1 ? W + wrow * 144 * bpr + 16 * bpr : W + wrow * 144 * bpr + 16) + 16 * (lane >> 3);
+    const int64_t w8 = min<int64_t>(8, N - 1 - min(n0 + 32 * wrt + 8 * wk + (lane & 7), N - 1)) * 144 * bpr;   // next group
     const uint8_t *wh0 = W + hrow * 144 * bpr;
     auto stage_a = [&](int buf, int64_t sb) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) dma16(arow + sb * 256 + 32 * (asub + u), &S.a[buf][att][asub + u][0]);
+        for (int k = 0; k < 4; ++k)
+            dma16(arow + (int64_t)min(8 * k, (int)max<int64_t>(M - 1 - (m0 + 32 * att + (lane & 7)), 0)) * K + sb * 256,
+                  &S.a[buf][att][72 * (4 * ah8 + k)]);
         if (wave < 4) dma16(bsrow + sb * 16, &S.bs[buf][wave][0]);
         else if (wave < 6) dma4(dyrow + sb, &S.dy[buf][64 * (wave - 4)]);
     };
     auto stage_w = [&](int st, int64_t sb) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) dma16(wq0 + QS * sb + 32 * (wp + u), &S.wq[st][wrt][wp + u][0]);
+        for (int u = 0; u < 2; ++u) dma16(wq0 + QS * sb + (u ? w8 : 0), &S.wq[st][wrt][72 * (wk + u)]);
         if (wave < 2) dma16(wh0 + HS * sb, &S.wh[st][2 * wave][0]);
     };
 
@@ -1528,11 +1542,10 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
         i32x16 ah[2], al[2];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            const i32x4 w4 = S.wq[st][wr][p][lane];
+            const i32x4 w4 = S.wq[st][wr][swz(lr, 2 * p + kg)];
             const uint32_t sdw = p < 2 ? sc_lo : sc_hi;
             const uint32_t s0 = (sdw >> (16 * (p & 1))) & 0xFF, s1 = (sdw >> (16 * (p & 1) + 8)) & 0xFF;
-            const uint32_t h0 = (s0 >> 3) * 0x10001u, l0 = (s0 & 7) * 0x10001u;
-            const uint32_t h1 = (s1 >> 3) * 0x10001u, l1 = (s1 & 7) * 0x10001u;
+            const uint32_t h0 = s0 >> 3, l0 = s0 & 7, h1 = s1 >> 3, l1 = s1 & 7;
             i32x4 bh0, bl0, bh1, bl1;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -1546,7 +1559,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const int tt = 2 * wt + j;
-                const i32x4 a0 = S.a[buf][tt][2 * p][lane], a1 = S.a[buf][tt][2 * p + 1][lane];
+                const i32x4 a0 = S.a[buf][tt][swz(lr, 4 * p + kg)], a1 = S.a[buf][tt][swz(lr, 4 * p + 2 + kg)];
 #if KCPP_GEMM_PROBE == 2
                 ah[j][0] += a0[0] * bh0[0] + a1[1] * bl1[1];
                 al[j][0] += a0[1] * bl0[0] + a1[0] * bh1[1];
