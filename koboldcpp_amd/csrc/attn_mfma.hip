@@ -284,6 +284,246 @@ __global__ void __launch_bounds__(256) k_fa_prefill_mfma2(const uint16_t *__rest
         for (int r = 0; r < 4; ++r) op[16 * db + 4 * g + r] = o[db][r] * inv;
 }
 
+
+// v3: v2's work split and MFMA shapes with the tile movement and the softmax rebuilt (v2 spends ~5k cycles per 64-key
+// tile against 512 MFMA cycles):
+//   * K/V tiles arrive by LDS-DMA (inline asm, so the compiler drains nothing behind our back) into a 4-stage ring
+//     three tiles ahead -- no register staging, no ds_write; one DMA instruction = 4 key rows x 256 B (8 lines);
+//   * S = K Q^T of tile kt + 1 is issued before tile kt's softmax, so the matrix cores work under the exp2s;
+//   * XCD-aware block order: one kv head per XCD, so a head's K/V is read from that XCD's L2 by all its query
+//     blocks (v2's order had every XCD stream every head's K/V from the Infinity Cache: ~5 TB/s of re-reads);
+//     rows past the visible keys are clamped to the last visible key (finite data; their P is 0);
+//   * LDS image [key][16 chunks of 16 B] with chunk c stored at c ^ 2 (key & 7): the K fragment reads and the
+//     transposed V reads (ds_read_b64_tr_b16) are both conflict-free;
+//   * softmax in the exp2 domain (logits pre-scaled by scale * log2 e, one v_exp_f32 per element instead of expf),
+//     the causal / length mask only on tiles that cross the diagonal or the end.
+// Same key order and f16 rounding of P as v2; results differ from v2 only by exp2 vs expf rounding (<= 1 ulp of P).
+__device__ __forceinline__ uint32_t fa_lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ void fa_dma16(const void *g, const void *lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g),
+                 "s"(__builtin_amdgcn_readfirstlane(fa_lds_addr(lds_base))) : "memory", "m0");
+}
+__device__ __forceinline__ int fa_swz(int row, int c) { return row * 16 + (c ^ ((row & 7) << 1)); }
+
+// NW = 8: two waves per query head, wave w (head w & 3) takes key half hf = w >> 2 of every 64-key tile (its own
+// running max / sum / O over those keys; 2 waves per SIMD so one's softmax runs under the other's MFMAs); the two
+// halves' (m, l, O) are merged through LDS at the end -- exact online-softmax algebra, the summation split in two.
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t *__restrict__ q16,
+                                                                const uint16_t *__restrict__ kc,
+                                                                const uint16_t *__restrict__ vc, float *__restrict__ out,
+                                                                int T, int H, int HKV, int n_past, float scale) {
+    constexpr int D = 128, G = 4, NST = 4;
+    constexpr int NB = NW == 8 ? 2 : 4;               // 16-key blocks per wave and tile
+    __shared__ __attribute__((aligned(16))) uint4 sk[NST][FM_K * 16];
+    __shared__ __attribute__((aligned(16))) uint4 sv[NST][FM_K * 16];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hf = NW == 8 ? wave >> 2 : 0;
+    // 1-D grid, XCD-aware: blocks b and b + 8 share an XCD, so kv head = b % 8 (+ 8 (b / 8 % (HKV / 8))) keeps every
+    // query block of one head on one XCD -- its K/V (n_keys x 512 B) stays in that XCD's L2 instead of every XCD
+    // streaming all heads from the Infinity Cache
+    const int bid = blockIdx.x;
+    int hk, qb;
+    if (HKV % 8 == 0) {
+        const int j = bid >> 3;
+        hk = (bid & 7) + 8 * (j % (HKV / 8));
+        qb = j / (HKV / 8);
+    } else {
+        hk = bid % HKV;
+        qb = bid / HKV;
+    }
+    const int q0 = qb * FM_Q, h = hk * G + (wave & 3);
+    const int EKV = HKV * D;
+    const int ql = lane & 15, g = lane >> 4;
+    const int qi = q0 + ql;
+    const int qpos = n_past + qi;
+    const float sl2 = scale * 1.4426950408889634f;
+    h8 qf[4];
+    {
+        const int qc = min(qi, T - 1);
+        const uint16_t *qp = q16 + ((int64_t)qc * H + h) * D + 8 * g;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) qf[s] = *(const h8 *)(qp + 32 * s);
+    }
+    f4 o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = f4{0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY, l_run = 0.0f;
+    const int n_keys = n_past + min(q0 + FM_Q, T);
+    const int ntile = (n_keys + FM_K - 1) / FM_K;
+    const int qmin = n_past + q0;                         // smallest query position of the block
+    // DMA: wave w fetches key rows (64 / NW) w .. +64/NW of the tile (instructions of 4 rows) for K and for V;
+    // lane: row 4 i + (lane >> 4) of the instruction, chunk slot lane & 15 <- global chunk (slot ^ 2 (row & 7))
+    constexpr int RPW = FM_K / NW, IPW = RPW / 4;
+    const int drow = lane >> 4, dslot = lane & 15;
+    auto stage = [&](int kt) {
+        const int st = kt & (NST - 1);
+#pragma unroll
+        for (int i = 0; i < IPW; ++i) {
+            const int r = RPW * wave + 4 * i + drow;                // row in the tile
+            const int p = min(kt * FM_K + r, n_keys - 1);
+            const int c = dslot ^ ((r & 7) << 1);
+            const int64_t off = (int64_t)p * EKV + hk * D + 8 * c;
+            fa_dma16(kc + off, &sk[st][(RPW * wave + 4 * i) * 16]);
+            fa_dma16(vc + off, &sv[st][(RPW * wave + 4 * i) * 16]);
+        }
+    };
+    // lane-constant LDS byte offsets (swizzle folded in; the per-tile stage base and the row blocks are immediates):
+    // K fragment of step s: row 16 b + ql, chunk 4 s + g -> 4096 b + kofs[s];  V^T read of dim block db: rows
+    // 32 s2 + 4 g + trq (+ 16), chunk 2 db + (trp >> 1), half trp & 1 -> 8192 s2 (+ 4096) + vofs[db]
+    const int trq = ql >> 2, trp = ql & 3;
+    int kofs[4], vofs[8];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kofs[s] = 16 * (16 * ql + ((4 * s + g) ^ ((ql & 7) << 1)));
+    {
+        const int r0 = 4 * g + trq;
+#pragma unroll
+        for (int db = 0; db < 8; ++db) vofs[db] = 16 * (16 * r0 + ((2 * db + (trp >> 1)) ^ ((r0 & 7) << 1))) + 8 * (trp & 1);
+    }
+    const int b0 = NB * hf;                                   // this wave's first 16-key block
+    // S^T = K Q^T of the wave's key blocks of tile kt (keys x queries), MFMAs only: issued a tile ahead so they run
+    // under the softmax; all fragments of two steps read before their MFMAs, step-major (independent chains)
+    auto qk = [&](int kt, f4 (&sc)[NB]) {
+        const char *skb = (const char *)&sk[kt & (NST - 1)][0] + 4096 * b0;
+#pragma unroll
+        for (int b = 0; b < NB; ++b) sc[b] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int sp = 0; sp < 2; ++sp) {
+            h8 ka[2 * NB];
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int b = 0; b < NB; ++b) ka[NB * s + b] = *(const h8 *)(skb + 4096 * b + kofs[2 * sp + s]);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int b = 0; b < NB; ++b)
+                    sc[b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ka[NB * s + b], qf[2 * sp + s], sc[b], 0, 0, 0);
+        }
+    };
+    auto vread = [&](const char *svb, int s2, h8 (&va)[8]) {
+#pragma unroll
+        for (int db = 0; db < 8; ++db) {
+            const uint2 lo = ds_tr16((const uint16_t *)(svb + 8192 * s2 + vofs[db]));
+            const uint2 hi = ds_tr16((const uint16_t *)(svb + 8192 * s2 + 4096 + vofs[db]));
+            va[db] = __builtin_bit_cast(h8, make_uint4(lo.x, lo.y, hi.x, hi.y));
+        }
+    };
+    // ring of NST stages, NST - 1 tiles ahead: tile kt + 1's K is read at the top of iteration kt
+    for (int t = 0; t < NST - 1 && t < ntile; ++t) stage(t);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    f4 sc[NB], sn[NB];
+    qk(0, sc);
+    for (int kt = 0; kt < ntile; ++kt) {
+        const int p0 = kt * FM_K + 16 * b0;
+        const bool pre = kt + NST - 1 < ntile;
+        if (pre) stage(kt + NST - 1);
+        if (kt + 1 < ntile) qk(kt + 1, sn);
+        const char *svb = (const char *)&sv[kt & (NST - 1)][0];
+        h8 va[8];
+        vread(svb, NW == 8 ? hf : 0, va);             // V^T of the first 32 keys: independent of P, read under softmax
+        float mt = -INFINITY;
+        if (p0 + 16 * NB - 1 > qmin || p0 + 16 * NB > n_keys) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int p = p0 + 16 * b + 4 * g + r;
+                    const float v = (p <= qpos && p < n_keys) ? sc[b][r] * sl2 : -INFINITY;
+                    sc[b][r] = v;
+                    mt = fmaxf(mt, v);
+                }
+        } else {
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    sc[b][r] *= sl2;
+                    mt = fmaxf(mt, sc[b][r]);
+                }
+        }
+        mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+        mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        const float m_new = fmaxf(m_run, mt);
+        // m_new = -inf only when every key so far is masked (a half-tile wholly past the diagonal): keep alpha 1
+        const float alpha = m_new == -INFINITY ? 1.0f : __builtin_amdgcn_exp2f(m_run - m_new);
+        float ls = 0.0f;
+        h8 pb[NB / 2];
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float e = m_new == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(sc[b][r] - m_new);
+                ls += e;
+                pb[b >> 1][4 * (b & 1) + r] = (_Float16)e;
+            }
+        ls += __shfl_xor(ls, 16, 64);
+        ls += __shfl_xor(ls, 32, 64);
+        l_run = l_run * alpha + ls;
+        // the running maximum rarely moves after the first tiles: rescale only when some lane's did (alpha = 1
+        // leaves o unchanged bit for bit)
+        if (__builtin_amdgcn_ballot_w64(m_new != m_run)) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) o[i] *= alpha;
+        }
+        m_run = m_new;
+#pragma unroll
+        for (int db = 0; db < 8; ++db) o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[db], pb[0], o[db], 0, 0, 0);
+        if constexpr (NB == 4) {
+            vread(svb, 1, va);
+#pragma unroll
+            for (int db = 0; db < 8; ++db) o[db] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[db], pb[1], o[db], 0, 0, 0);
+        }
+#pragma unroll
+        for (int b = 0; b < NB; ++b) sc[b] = sn[b];
+        // tile kt + 2 must have landed before the next iteration reads its K (kt + 3's DMA instructions, issued
+        // last, may stay in flight)
+        if (pre) {
+            if constexpr (IPW == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
+    if constexpr (NW == 8) {
+        // merge the two key halves: wave hf = 1 publishes (m, l, O) in the (now idle) K ring, wave hf = 0 combines
+        float *xo = (float *)&sk[0][0] + (wave & 3) * (16 * 130);     // [16 queries][128 dims + m + l]
+        if (hf == 1) {
+#pragma unroll
+            for (int db = 0; db < 8; ++db)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) xo[ql * 130 + 16 * db + 4 * g + r] = o[db][r];
+            if (g == 0) {
+                xo[ql * 130 + 128] = m_run;
+                xo[ql * 130 + 129] = l_run;
+            }
+        }
+        __syncthreads();
+        if (hf == 1) return;
+        const float m1 = xo[ql * 130 + 128], l1 = xo[ql * 130 + 129];
+        const float m = fmaxf(m_run, m1);
+        const float a0 = m_run == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m_run - m);
+        const float a1 = m1 == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m1 - m);
+        l_run = l_run * a0 + l1 * a1;
+#pragma unroll
+        for (int db = 0; db < 8; ++db)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) o[db][r] = o[db][r] * a0 + xo[ql * 130 + 16 * db + 4 * g + r] * a1;
+    }
+    if (qi >= T) return;
+    const float inv = 1.0f / l_run;
+    float *op = out + ((int64_t)qi * H + h) * D;
+#pragma unroll
+    for (int db = 0; db < 8; ++db)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) op[16 * db + 4 * g + r] = o[db][r] * inv;
+}
+
 static int g_fa_prefill_variant = 0;
 extern "C" int kcpp_fa_prefill_set_variant(int v) {
     const int old = g_fa_prefill_variant;
@@ -294,8 +534,14 @@ extern "C" int kcpp_fa_prefill_set_variant(int v) {
 extern "C" int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out,
                                             int T, int H, int HKV, int D, int n_past, float scale, void *stream) {
     if (D != 128 || HKV <= 0 || H != 4 * HKV) return -3;
-    const int v = g_fa_prefill_variant ? g_fa_prefill_variant : 2;
-    if (v == 1)
+    const int v = g_fa_prefill_variant ? g_fa_prefill_variant : 4;
+    if (v == 3)
+        hipLaunchKernelGGL(k_fa_prefill_mfma3<4>, dim3((T + FM_Q - 1) / FM_Q * HKV), dim3(256), 0, (hipStream_t)stream, q16,
+                           kc, vc, out, T, H, HKV, n_past, scale);
+    else if (v == 4)
+        hipLaunchKernelGGL(k_fa_prefill_mfma3<8>, dim3((T + FM_Q - 1) / FM_Q * HKV), dim3(512), 0, (hipStream_t)stream, q16,
+                           kc, vc, out, T, H, HKV, n_past, scale);
+    else if (v == 1)
         hipLaunchKernelGGL(k_fa_prefill_mfma, dim3((T + FM_Q - 1) / FM_Q, HKV), dim3(256), 0, (hipStream_t)stream, q16, kc,
                            vc, out, T, H, HKV, n_past, scale);
     else

@@ -1,6 +1,6 @@
-"""Prefill flash-attention A/B (tools only): kcpp_flash_attn_prefill_mfma variants 1 vs 2 at the bench's
+"""Prefill flash-attention A/B (tools only): kcpp_flash_attn_prefill_mfma variants (default 2 vs 3) at the bench's
 ubatch-512 shapes (Llama-3-8B: 32 q heads, 8 kv heads, D 128), HIP-event timed.
-usage: python tools/fa_ab.py"""
+usage: python tools/fa_ab.py [variants...]"""
 import json
 import os
 import sys
@@ -20,8 +20,8 @@ def main():
     kc = (torch.randn(n_ctx, HKV, D, device="cuda") * 0.5).half()
     vc = torch.randn(n_ctx, HKV, D, device="cuda").half()
     out = torch.empty(T, H, D, device="cuda")
-    for n_past in (0, 1536, 3328):
-        for v in (1, 2):
+    for n_past in [int(x) for x in os.environ.get("FA_NPAST", "0,1536,3328").split(",")]:
+        for v in [int(a) for a in sys.argv[1:]] or [2, 3]:
             K.raw().kcpp_fa_prefill_set_variant(v)
             run = lambda: K.call("kcpp_flash_attn_prefill_mfma", q.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(),
                                  T, H, HKV, D, n_past, 1.0 / D ** 0.5, s.cuda_stream)
