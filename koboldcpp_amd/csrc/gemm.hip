@@ -1761,16 +1761,17 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         return (gv == 4 || (gv == 0 && !big && (tiles < 128 || K / 256 >= 32))) ? 2 : 1;
     };
     const bool bs_aligned = ((uintptr_t)((const uint8_t *)act + M * K + M * (K / 256) * 4) & 15) == 0;
-    // v4 where it measured faster (tools/gemm_ab.py, M = 512): the big grids (gate|up 28672 rows: 227-230 vs 234-242 us)
-    // and the long-K shapes with split-K (down 14336 -> 4096: 93-96 vs 115 us); v3's 64-token tiles stay ahead on the
-    // 4096-6144-row shapes (q|k|v 63.8 vs 69.5 us, wo even).  Variant 11 forces v4, 13 v4 unsplit, 3 / 4 force v3.
-    const bool v4_pick = gv == 0 && (Mp / 128 * ((N + 127) / 128) >= 384 || (K / 256 >= 32 && mode == 0));
+    // v4 for every Q4_K shape past the small-batch range (tools/gemm_ab.py, M = 512, v3 -> v4): gate|up 28672 rows
+    // 249 -> 216 us, down 14336 -> 4096 122 -> 101, q|k|v 6144 rows 59.4 -> 52.1 (unsplit), wo 4096 rows 43.1 -> 38.5
+    // (split-K); its tile grid is split in two along K when it has <= 128 tiles.  Variant 11 forces v4 (split rule),
+    // 13 v4 unsplit, 3 / 4 force v3.
+    const bool v4_pick = gv == 0;
     if ((type == KT_Q4_K || type == KT_Q4_K_RS) && (gv == 11 || gv == 12 || gv == 13 || v4_pick) && bs_aligned && M > 32) {
         // v4: int8 MFMA straight from the Q8_K buffer (no fragment image); 128 x 128 tiles, split-K when the tile
         // grid is small
         const int64_t nt = (N + 127) / 128;
         const int MT = (int)(Mp / 128);
-        const int KS = (gv != 13 && mode == 0 && (K / 256) % 2 == 0 && MT * nt < 384) ? 2 : 1;
+        const int KS = (gv != 13 && mode == 0 && (K / 256) % 2 == 0 && MT * nt <= 128) ? 2 : 1;
         const unsigned nwg = (unsigned)(MT * nt * KS);
         const int XG = gv == 12 ? 2 : 1;
         auto launch4 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
