@@ -29,7 +29,7 @@
 enum kcpp_type {
     KT_F32 = 0, KT_F16 = 1, KT_Q4_0 = 2, KT_Q4_1 = 3, KT_Q5_0 = 6, KT_Q5_1 = 7,
     KT_Q8_0 = 8, KT_Q8_1 = 9, KT_Q2_K = 10, KT_Q3_K = 11, KT_Q4_K = 12,
-    KT_Q5_K = 13, KT_Q6_K = 14, KT_Q8_K = 15, KT_BF16 = 30,
+    KT_Q5_K = 13, KT_Q6_K = 14, KT_Q8_K = 15, KT_IQ4_NL = 20, KT_IQ4_XS = 23, KT_BF16 = 30,
     /* GPU-internal row-major decode layouts of Q4_K / Q6_K (same bytes per row, re-arranged inside
        each row so the single-token mat-vec reads 1 KiB-contiguous wave loads; csrc/kcpp_common.h).
        Not ggml ids: they never leave the device library. */
@@ -79,7 +79,7 @@ KS_FN float ks_unit(uint64_t h) {            /* [0,1) */
 KS_FN int ks_block_elems(int type) {
     switch (type) {
         case KT_F32: case KT_F16: return 1;
-        case KT_Q4_0: case KT_Q4_1: case KT_Q5_0: case KT_Q5_1: case KT_Q8_0: case KT_Q8_1: return 32;
+        case KT_Q4_0: case KT_Q4_1: case KT_Q5_0: case KT_Q5_1: case KT_Q8_0: case KT_Q8_1: case KT_IQ4_NL: return 32;
         default: return 256;
     }
 }
@@ -87,8 +87,9 @@ KS_FN int ks_block_bytes(int type) {
     switch (type) {
         case KT_F32: return 4;
         case KT_F16: return 2;
-        case KT_Q4_0: return 18;
+        case KT_Q4_0: case KT_IQ4_NL: return 18;
         case KT_Q4_1: return 20;
+        case KT_IQ4_XS: return 136;
         case KT_Q5_0: return 22;
         case KT_Q5_1: return 24;
         case KT_Q8_1: return 36;
@@ -141,6 +142,14 @@ KS_FN void ks_fill_block(int type, uint64_t seed, uint64_t tid, uint64_t b, uint
             break;
         case KT_Q8_0:
             h0 = ks_f32_to_f16(0.00027f * (0.75f + 0.5f * u0));
+            memcpy(dst, &h0, 2);
+            break;
+        case KT_IQ4_NL:     /* w = d kvalues_iq4nl[q], std(kvalues) ~70 */
+            h0 = ks_f32_to_f16(2.8e-4f * (0.75f + 0.5f * u0));
+            memcpy(dst, &h0, 2);
+            break;
+        case KT_IQ4_XS:     /* w = d (ls - 32) kvalues_iq4nl[q], ls 6-bit: std(ls - 32) ~18.5 */
+            h0 = ks_f32_to_f16(1.6e-5f * (0.75f + 0.5f * u0));
             memcpy(dst, &h0, 2);
             break;
         case KT_Q4_K: case KT_Q5_K: {

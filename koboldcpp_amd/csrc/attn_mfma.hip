@@ -307,9 +307,9 @@ __device__ __forceinline__ void fa_dma16(const void *g, const void *lds_base) {
 }
 __device__ __forceinline__ int fa_swz(int row, int c) { return row * 16 + (c ^ ((row & 7) << 1)); }
 
-// NW = 8: two waves per query head, wave w (head w & 3) takes key half hf = w >> 2 of every 64-key tile (its own
-// running max / sum / O over those keys; 2 waves per SIMD so one's softmax runs under the other's MFMAs); the two
-// halves' (m, l, O) are merged through LDS at the end -- exact online-softmax algebra, the summation split in two.
+// NW = 8: two waves per query head, wave w (head w & 3) takes key half hf = w >> 2 of every 64-key tile (2 waves per
+// SIMD so one's softmax runs under the other's MFMAs); the halves share each tile's maximum through LDS, so P and the
+// running max are v3's, and their (l, O) partial sums are added at the end (only the f32 summation order differs).
 template <int NW>
 __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t *__restrict__ q16,
                                                                 const uint16_t *__restrict__ kc,
@@ -319,6 +319,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t 
     constexpr int NB = NW == 8 ? 2 : 4;               // 16-key blocks per wave and tile
     __shared__ __attribute__((aligned(16))) uint4 sk[NST][FM_K * 16];
     __shared__ __attribute__((aligned(16))) uint4 sv[NST][FM_K * 16];
+    __shared__ float s_mx[2][4][16];                  // NW = 8: per key half, head and query: the tile maximum
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int hf = NW == 8 ? wave >> 2 : 0;
@@ -448,6 +449,13 @@ __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t 
         }
         mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
         mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+        if constexpr (NW == 8) {
+            // both key halves take the whole tile's maximum (exchanged through LDS), so P, alpha and the running max
+            // are v3's exactly; only the f32 summation of O and l is split in two
+            if (g == 0) s_mx[hf][wave & 3][ql] = mt;
+            __syncthreads();
+            mt = fmaxf(mt, s_mx[hf ^ 1][wave & 3][ql]);
+        }
         const float m_new = fmaxf(m_run, mt);
         // m_new = -inf only when every key so far is masked (a half-tile wholly past the diagonal): keep alpha 1
         const float alpha = m_new == -INFINITY ? 1.0f : __builtin_amdgcn_exp2f(m_run - m_new);

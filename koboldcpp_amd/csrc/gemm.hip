@@ -1735,9 +1735,10 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     _Float16 *bs16 = (_Float16 *)(w8 + o_bs);
     float *up = (float *)(w8 + o_up);
     const int vt = vec_dot_type(type);
-    if (type == KT_Q4_1 || type == KT_Q5_1) {
-        // the legacy Q8_1-activation types (Q4_1 / Q5_1 files): the exact mat-vec over groups of 8 columns (each group
-        // one pass over the weights); their prefill is not on the BASELINE path
+    if (type == KT_Q4_1 || type == KT_Q5_1 || type == KT_IQ4_NL || type == KT_IQ4_XS) {
+        // the legacy Q8_1-activation types (Q4_1 / Q5_1 files) and the code-book types (IQ4_NL / IQ4_XS): the exact
+        // mat-vec over groups of 8 columns (each group one pass over the weights); their prefill is not on the
+        // BASELINE path
         for (int64_t c0 = 0; c0 < M; c0 += 8) {
             const int rc = gemv_cols(type, W, W2, K, N, act, std::min<int64_t>(8, M - c0), M, c0, Y, ldy, res, ldr, mode,
                                      stream);

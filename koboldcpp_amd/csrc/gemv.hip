@@ -32,7 +32,8 @@ __global__ void __launch_bounds__(256) k_gemv(const uint8_t *__restrict__ W, con
     if (row0 >= N) return;
     const int64_t upr = K / E;
     const int64_t nb = K / ks_block_elems(TYPE) * N;
-    const int vt = (TYPE == KT_Q4_1 || TYPE == KT_Q5_1) ? KT_Q8_1 : (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;
+    const int vt = (TYPE == KT_Q4_1 || TYPE == KT_Q5_1) ? KT_Q8_1
+                 : (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0 || TYPE == KT_IQ4_NL) ? KT_Q8_0 : KT_Q8_K;
     constexpr int RR = MODE == 1 ? 2 : R;
     float acc[RR][NC];
 #pragma unroll
@@ -133,6 +134,8 @@ int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         KCPP_T(KT_Q5_0)
         KCPP_T(KT_Q4_1)
         KCPP_T(KT_Q5_1)
+        KCPP_T(KT_IQ4_NL)
+        KCPP_T(KT_IQ4_XS)
         KCPP_T(KT_Q8_0)
     default: return -3;
     }

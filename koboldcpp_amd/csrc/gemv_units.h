@@ -139,6 +139,31 @@ template <> struct Unit<KT_Q5_1> {
         dm = *(const uint32_t *)(base + nb * 20 + b * 4);
     }
 };
+// ---- IQ4_NL (SoA as Q4_0): unit = one 32-elem block: 16 B of code-book indices + fp16 d
+template <> struct Unit<KT_IQ4_NL> {
+    static constexpr int ELEMS = 32;
+    uint4 q;
+    uint16_t d;
+    __device__ __forceinline__ void load(const uint8_t *base, int64_t nb, int64_t b0, int u) {
+        const int64_t b = b0 + u;
+        q = ld_nt((const void *)(base + b * 16));
+        d = *(const uint16_t *)(base + nb * 16 + b * 2);
+    }
+};
+// ---- IQ4_XS (SoA: qs [nb][128] ++ (d, scales_h, scales_l[4]) [nb][8]): unit u = sub-blocks 2j, 2j+1 (j = u & 3)
+// of super-block u >> 2: qs bytes 32j .. 32j+31 and the 8-byte header
+template <> struct Unit<KT_IQ4_XS> {
+    static constexpr int ELEMS = 64;
+    uint4 q0, q1;
+    uint2 h;
+    __device__ __forceinline__ void load(const uint8_t *base, int64_t nb, int64_t b0, int u) {
+        const int64_t b = b0 + (u >> 2);
+        const uint8_t *q = base + b * 128 + 32 * (u & 3);
+        q0 = ld_nt((const void *)q);
+        q1 = ld_nt((const void *)(q + 16));
+        h = *(const uint2 *)(base + nb * 128 + b * 8);
+    }
+};
 // ---- Q8_0 (SoA): unit = one 32-elem block: 32 B int8 + fp16 d
 template <> struct Unit<KT_Q8_0> {
     static constexpr int ELEMS = 32;
@@ -214,6 +239,7 @@ template <> struct ActOf<KT_Q5_1> { typedef Act1 T; };
 template <> struct ActOf<KT_Q4_0> { typedef Act0 T; };
 template <> struct ActOf<KT_Q5_0> { typedef Act0 T; };
 template <> struct ActOf<KT_Q8_0> { typedef Act0 T; };
+template <> struct ActOf<KT_IQ4_NL> { typedef Act0 T; };
 
 __device__ __forceinline__ void load_act(const ActView &av, int u, ActK &x) { load_actk(av, u, x); }
 __device__ __forceinline__ void load_act(const ActView &av, int u, Act0 &x) { load_act0(av, u, x); }
@@ -396,6 +422,38 @@ __device__ __forceinline__ float dot_q41(uint4 q, uint32_t h, uint32_t dm, const
 __device__ __forceinline__ float unit_dot(const Unit<KT_Q4_1> &w, int, const Act1 &x) { return dot_q41(w.q, 0u, w.dm, x); }
 __device__ __forceinline__ float unit_dot(const Unit<KT_Q5_1> &w, int, const Act1 &x) { return dot_q41(w.q, w.h, w.dm, x); }
 
+// ggml_vec_dot_iq4_nl_q8_0 (ggml-quants.c:12470; scalar :12660): (d_a d_w) sum kvalues[q] a over the block
+__device__ __forceinline__ float unit_dot(const Unit<KT_IQ4_NL> &w, int, const Act0 &x) {
+    int s = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t q = u4(w.q, i);
+        s = sdot4((int)iq4nl_lut4(q & 0x0F0F0F0Fu), u4(*(const uint4 *)&x.a[0], i), s);
+        s = sdot4((int)iq4nl_lut4((q >> 4) & 0x0F0F0F0Fu), u4(*(const uint4 *)&x.a[1], i), s);
+    }
+    return __fmul_rn((float)s, __fmul_rn(x.d, h2f(w.d)));
+}
+
+// ggml_vec_dot_iq4_xs_q8_K (ggml-quants.c:12672; AVX2 :12728): per 32-sub-block integer dot times (ls - 32), summed in
+// int32, then (d_w d_a) once -- the AVX2 branch's order
+__device__ __forceinline__ float unit_dot(const Unit<KT_IQ4_XS> &w, int u, const ActK &x) {
+    const int j = u & 3;
+    int s0 = 0, s1 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t qa = u4(w.q0, i), qb = u4(w.q1, i);
+        s0 = sdot4((int)iq4nl_lut4(qa & 0x0F0F0F0Fu), ai(x, i), s0);
+        s0 = sdot4((int)iq4nl_lut4((qa >> 4) & 0x0F0F0F0Fu), ai(x, 4 + i), s0);
+        s1 = sdot4((int)iq4nl_lut4(qb & 0x0F0F0F0Fu), ai(x, 8 + i), s1);
+        s1 = sdot4((int)iq4nl_lut4((qb >> 4) & 0x0F0F0F0Fu), ai(x, 12 + i), s1);
+    }
+    const uint32_t sh = w.h.x >> 16, sl = w.h.y;
+    const int ib0 = 2 * j, ib1 = 2 * j + 1;
+    const int ls0 = (int)(((sl >> (8 * (ib0 / 2))) & 0xF) | (((sh >> (2 * ib0)) & 3) << 4)) - 32;
+    const int ls1 = (int)(((sl >> (8 * (ib1 / 2) + 4)) & 0xF) | (((sh >> (2 * ib1)) & 3) << 4)) - 32;
+    return __fmul_rn(__fmul_rn(h2f((uint16_t)(w.h.x & 0xFFFF)), x.d), (float)(ls0 * s0 + ls1 * s1));
+}
+
 __device__ __forceinline__ float unit_dot(const Unit<KT_Q8_0> &w, int, const Act0 &x) {
     int s = 0;
 #pragma unroll
@@ -411,7 +469,8 @@ template <int TYPE>
 __device__ __forceinline__ void load_unit(Unit<TYPE> &w, const uint8_t *W, int64_t nb, int64_t row, int64_t units_per_row, int u) {
     if constexpr (TYPE == KT_Q4_K) w.load(W + row * (units_per_row / 4) * 144, nb, u);
     else if constexpr (TYPE == KT_Q5_K) w.load(W + row * (units_per_row / 4) * 176, nb, u);
-    else if constexpr (TYPE == KT_Q6_K || TYPE == KT_Q3_K || TYPE == KT_Q2_K) w.load(W, nb, row * (units_per_row / 4), u);
+    else if constexpr (TYPE == KT_Q6_K || TYPE == KT_Q3_K || TYPE == KT_Q2_K || TYPE == KT_IQ4_XS)
+        w.load(W, nb, row * (units_per_row / 4), u);
     else w.load(W, nb, row * units_per_row, u);
 }
 

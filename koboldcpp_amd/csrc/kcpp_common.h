@@ -43,6 +43,21 @@ __device__ __forceinline__ T group_sum(T v) {     // reduce over aligned groups 
 }
 
 __device__ __forceinline__ float h2f(uint16_t h) { return __half2float(__ushort_as_half(h)); }
+
+// IQ4_NL / IQ4_XS code book (kvalues_iq4nl, ggml-quants.c:3741) as four little-endian dwords
+__device__ __forceinline__ int kv_iq4nl(int q) {
+    const int8_t t[16] = {-127, -104, -83, -65, -49, -35, -22, -10, 1, 13, 25, 38, 53, 69, 89, 113};
+    return t[q & 15];
+}
+// four nibble codes (bytes of x, each 0..15) -> their four int8 code-book values: two v_perm_b32 byte lookups into the
+// 8-entry halves, picked per byte by the code's bit 3
+__device__ __forceinline__ uint32_t iq4nl_lut4(uint32_t x) {
+    constexpr uint32_t T0 = 0xBFAD9881u, T1 = 0xF6EADDCFu, T2 = 0x26190D01u, T3 = 0x71594535u;
+    const uint32_t sel = x & 0x07070707u;
+    const uint32_t lo = __builtin_amdgcn_perm(T1, T0, sel), hi = __builtin_amdgcn_perm(T3, T2, sel);
+    const uint32_t m = ((x >> 3) & 0x01010101u) * 0xFFu;
+    return (hi & m) | (lo & ~m);
+}
 __device__ __forceinline__ uint16_t f2h(float f) { return __half_as_ushort(__float2half_rn(f)); }
 // f32 -> f16 of an already-rounded f32 value.  Without the register barrier the backend folds f2h(a * b) into
 // v_fma_mixlo_f16(a, b, 0) -- ONE rounding of the exact product, and +0 for a -0 product -- which is not the
@@ -108,7 +123,7 @@ __host__ __device__ inline ActView act_view(int vtype, const void *buf, int64_t 
 }
 inline int vec_dot_type(int wtype) {
     if (wtype == KT_Q4_1 || wtype == KT_Q5_1) return KT_Q8_1;
-    return (wtype == KT_Q4_0 || wtype == KT_Q5_0 || wtype == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;
+    return (wtype == KT_Q4_0 || wtype == KT_Q5_0 || wtype == KT_Q8_0 || wtype == KT_IQ4_NL) ? KT_Q8_0 : KT_Q8_K;
 }
 
 // ---------------------------------------------------------------------------------

@@ -36,6 +36,16 @@ __device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uin
         d[0] = src[0]; d[1] = src[1];
         for (int i = 0; i < 16; ++i) q[i] = src[2 + i];
     } break;
+    case KT_IQ4_NL: { // SoA planes as Q4_0: qs [nb][16] ++ d [nb][2]  (block_iq4_nl: d, qs[16])
+        uint8_t *q = dst + b * 16, *d = dst + nb * 16 + b * 2;
+        d[0] = src[0]; d[1] = src[1];
+        for (int i = 0; i < 16; ++i) q[i] = src[2 + i];
+    } break;
+    case KT_IQ4_XS: { // SoA planes: qs [nb][128] ++ (d, scales_h, scales_l[4]) [nb][8]  (block_iq4_xs: d, sh, sl[4], qs[128])
+        uint8_t *q = dst + b * 128, *h = dst + nb * 128 + b * 8;
+        for (int i = 0; i < 8; ++i) h[i] = src[i];
+        for (int i = 0; i < 128; ++i) q[i] = src[8 + i];
+    } break;
     case KT_Q4_1: {   // SoA planes: qs [nb][16] ++ (d, m) [nb][4]  (block_q4_1: d, m, qs[16])
         uint8_t *q = dst + b * 16, *dm = dst + nb * 16 + b * 4;
         for (int i = 0; i < 4; ++i) dm[i] = src[i];
@@ -110,6 +120,16 @@ __device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint
         const uint8_t *q = src + b * 16, *d = src + nb * 16 + b * 2;
         blk[0] = d[0]; blk[1] = d[1];
         for (int i = 0; i < 16; ++i) blk[2 + i] = q[i];
+    } break;
+    case KT_IQ4_NL: {
+        const uint8_t *q = src + b * 16, *d = src + nb * 16 + b * 2;
+        blk[0] = d[0]; blk[1] = d[1];
+        for (int i = 0; i < 16; ++i) blk[2 + i] = q[i];
+    } break;
+    case KT_IQ4_XS: {
+        const uint8_t *q = src + b * 128, *h = src + nb * 128 + b * 8;
+        for (int i = 0; i < 8; ++i) blk[i] = h[i];
+        for (int i = 0; i < 128; ++i) blk[8 + i] = q[i];
     } break;
     case KT_Q4_1: {
         const uint8_t *q = src + b * 16, *dm = src + nb * 16 + b * 4;
@@ -243,6 +263,26 @@ __device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t bpr,
         float d = h2f(blk[0] | (blk[1] << 8));
         for (int j = 0; j < 32; ++j) o[j] = (int8_t)blk[2 + j] * d;
     } break;
+    case KT_IQ4_NL: {   // dequantize_row_iq4_nl, ggml-quants.c:3743-3759: d * kvalues[q] (one rounding)
+        const float d = h2f(blk[0] | (blk[1] << 8));
+        for (int j = 0; j < 16; ++j) {
+            o[j] = __fmul_rn(d, (float)kv_iq4nl(blk[2 + j] & 0xF));
+            o[j + 16] = __fmul_rn(d, (float)kv_iq4nl(blk[2 + j] >> 4));
+        }
+    } break;
+    case KT_IQ4_XS: {   // dequantize_row_iq4_xs, ggml-quants.c:3761-3782: (d (ls - 32)) * kvalues[q]
+        const float d = h2f(blk[0] | (blk[1] << 8));
+        const int sh = blk[2] | (blk[3] << 8);
+        for (int ib = 0; ib < 8; ++ib) {
+            const int ls = ((blk[4 + ib / 2] >> 4 * (ib % 2)) & 0xF) | (((sh >> 2 * ib) & 3) << 4);
+            const float dl = __fmul_rn(d, (float)(ls - 32));
+            const uint8_t *qs = blk + 8 + 16 * ib;
+            for (int j = 0; j < 16; ++j) {
+                o[32 * ib + j] = __fmul_rn(dl, (float)kv_iq4nl(qs[j] & 0xF));
+                o[32 * ib + j + 16] = __fmul_rn(dl, (float)kv_iq4nl(qs[j] >> 4));
+            }
+        }
+    } break;
     case KT_Q4_K: case KT_Q5_K: {
         const bool five = type == KT_Q5_K;
         const float d = h2f(blk[0] | (blk[1] << 8)), mn = h2f(blk[2] | (blk[3] << 8));
@@ -334,6 +374,18 @@ __device__ __forceinline__ float deq_elem(int type, const uint8_t *src, int64_t 
         return (float)((int)((e < 16 ? (q & 0xF) : (q >> 4)) | (((qh >> e) & 1) << 4)) - 16) * d;
     }
     case KT_Q8_0: return (int8_t)src[b * 32 + e] * h2f(*(const uint16_t *)(src + nb * 32 + b * 2));
+    case KT_IQ4_NL: {
+        const float d = h2f(*(const uint16_t *)(src + nb * 16 + b * 2));
+        const uint8_t q = src[b * 16 + (e & 15)];
+        return __fmul_rn(d, (float)kv_iq4nl(e < 16 ? (q & 0xF) : (q >> 4)));
+    }
+    case KT_IQ4_XS: {
+        const uint8_t *h = src + nb * 128 + b * 8;
+        const int ib = e >> 5, j = e & 31;
+        const int ls = ((h[4 + ib / 2] >> 4 * (ib % 2)) & 0xF) | ((((h[2] | (h[3] << 8)) >> 2 * ib) & 3) << 4);
+        const uint8_t q = src[b * 128 + 16 * ib + (j & 15)];
+        return __fmul_rn(__fmul_rn(h2f(h[0] | (h[1] << 8)), (float)(ls - 32)), (float)kv_iq4nl(j < 16 ? (q & 0xF) : (q >> 4)));
+    }
     case KT_Q4_K: case KT_Q5_K: {
         const bool five = type == KT_Q5_K;
         const uint8_t *blk = src + b * (five ? 176 : 144);

@@ -127,7 +127,7 @@ struct kcpp_model {
     float *logits_pin = nullptr;
     bool use_graphs = true;
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
-    bool q81 = false;                // Q4_1 / Q5_1 weights (Q8_1 activations): single-token decode on the per-op path
+    bool q81 = false;                // Q4_1 / Q5_1 (Q8_1 activations) or IQ4_NL / IQ4_XS weights: decode on the per-op path
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
     bool fuse_qkv_att = false;       // single-token q|k|v and attention partials in one launch (dec_fused.hip; opt-in, see DESIGN)
     int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
@@ -286,8 +286,9 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
         m->types[idx] = t;
     }
     types = m->types.data();
-    for (int idx = 0; idx < n_tensors(*hp); ++idx) m->q81 |= types[idx] == KT_Q4_1 || types[idx] == KT_Q5_1;
-    if (m->q81 && hp->n_expert > 0) { g_err = "Q4_1 / Q5_1 MoE models are not supported"; delete m; return nullptr; }
+    for (int idx = 0; idx < n_tensors(*hp); ++idx)
+        m->q81 |= types[idx] == KT_Q4_1 || types[idx] == KT_Q5_1 || types[idx] == KT_IQ4_NL || types[idx] == KT_IQ4_XS;
+    if (m->q81 && hp->n_expert > 0) { g_err = "Q4_1 / Q5_1 / IQ4 MoE models are not supported"; delete m; return nullptr; }
     m->device = device; m->il0 = il0; m->il1 = il1; m->has_embed = has_embed; m->has_output = has_output;
     m->ub = max_ubatch > 0 ? max_ubatch : 512;
     m->fa_exact = getenv("KCPP_FA_EXACT") && atoi(getenv("KCPP_FA_EXACT")) != 0;
@@ -469,6 +470,7 @@ static int upload(int dev, hipStream_t s, int type, int64_t K, int64_t N, int sl
     if (bytes == 0) return 0;
     RT_CHECK(hipSetDevice(dev));
     if (type == KT_Q6_K || type == KT_Q3_K || type == KT_Q2_K || type == KT_Q4_0 || type == KT_Q4_1 || type == KT_Q5_0 || type == KT_Q5_1 || type == KT_Q8_0 ||
+        type == KT_IQ4_NL || type == KT_IQ4_XS ||
         type == KT_Q4_K_RS ||
         type == KT_Q6_K_RS) {
         void *stage = nullptr;

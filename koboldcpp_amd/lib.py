@@ -11,10 +11,12 @@ import os
 from . import LIB_PATH
 
 F32, F16, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q3_K, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 3, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15
+IQ4_NL, IQ4_XS = 20, 23
 # device-internal row-major decode layouts of Q4_K / Q6_K (include/kcpp_synth.h; never ggml ids)
 Q4_K_RS, Q6_K_RS = 112, 114
 BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q4_1: (32, 20), Q5_0: (32, 22), Q5_1: (32, 24), Q8_0: (32, 34), Q8_1: (32, 36), Q2_K: (256, 84), Q3_K: (256, 110), Q4_K: (256, 144),
-         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292), Q4_K_RS: (256, 144), Q6_K_RS: (256, 210)}
+         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292), Q4_K_RS: (256, 144), Q6_K_RS: (256, 210),
+         IQ4_NL: (32, 18), IQ4_XS: (256, 136)}
 
 
 class KcppError(RuntimeError):

@@ -29,6 +29,11 @@ typedef struct { uint8_t ql[128]; uint8_t qh[64]; int8_t scales[16]; uint16_t d;
 typedef struct { uint8_t hmask[32]; uint8_t qs[64]; uint8_t scales[12]; uint16_t d; } blk_q3_K;    /* :267 */
 typedef struct { uint8_t scales[16]; uint8_t qs[64]; uint16_t d, dmin; } blk_q2_K;                 /* :250 */
 typedef struct { float d; int8_t qs[256]; int16_t bsums[16]; } blk_q8_K;  /* :330 */
+typedef struct { uint16_t d; uint8_t qs[16]; } blk_iq4_nl;                                            /* :407 */
+typedef struct { uint16_t d; uint16_t scales_h; uint8_t scales_l[4]; uint8_t qs[128]; } blk_iq4_xs;  /* :413 */
+
+/* the IQ4_NL / IQ4_XS non-linear code book, ggml-quants.c:3741 */
+static const int8_t kvalues_iq4nl[16] = {-127, -104, -83, -65, -49, -35, -22, -10, 1, 13, 25, 38, 53, 69, 89, 113};
 
 _Static_assert(sizeof(blk_q4_0) == 18, "q4_0");
 _Static_assert(sizeof(blk_q5_0) == 22, "q5_0");
@@ -40,6 +45,7 @@ _Static_assert(sizeof(blk_q6_K) == 210, "q6_K");
 _Static_assert(sizeof(blk_q3_K) == 110, "q3_K");
 _Static_assert(sizeof(blk_q2_K) == 84, "q2_K");
 _Static_assert(sizeof(blk_q8_K) == 292, "q8_K");
+_Static_assert(sizeof(blk_iq4_nl) == 18 && sizeof(blk_iq4_xs) == 136, "iq4_nl / iq4_xs");
 
 float orc_fp16_to_fp32(uint16_t h) { return _cvtsh_ss(h); }
 uint16_t orc_fp32_to_fp16(float f) { return _cvtss_sh(f, 0); }
@@ -119,6 +125,32 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
                 const int x1 = ((x[i].qs[j] >> 4) | ((qh >> (j + 12)) & 0x10)) - 16;
                 y[i * 32 + j] = x0 * d;
                 y[i * 32 + j + 16] = x1 * d;
+            }
+        }
+    } return;
+    case KT_IQ4_NL: {                                 /* dequantize_row_iq4_nl, ggml-quants.c:3743-3759 */
+        const blk_iq4_nl *x = vx;
+        for (int64_t i = 0; i < k / 32; ++i) {
+            const float d = H2F(x[i].d);
+            for (int j = 0; j < 16; ++j) {
+                y[i * 32 + j] = d * kvalues_iq4nl[x[i].qs[j] & 0xf];
+                y[i * 32 + j + 16] = d * kvalues_iq4nl[x[i].qs[j] >> 4];
+            }
+        }
+    } return;
+    case KT_IQ4_XS: {                                 /* dequantize_row_iq4_xs, ggml-quants.c:3761-3782 */
+        const blk_iq4_xs *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const float d = H2F(x[i].d);
+            const uint8_t *qs = x[i].qs;
+            for (int ib = 0; ib < QK_K / 32; ++ib) {
+                const int ls = ((x[i].scales_l[ib / 2] >> 4 * (ib % 2)) & 0xf) | (((x[i].scales_h >> 2 * ib) & 3) << 4);
+                const float dl = d * (ls - 32);
+                for (int j = 0; j < 16; ++j) {
+                    y[i * QK_K + 32 * ib + j] = dl * kvalues_iq4nl[qs[j] & 0xf];
+                    y[i * QK_K + 32 * ib + j + 16] = dl * kvalues_iq4nl[qs[j] >> 4];
+                }
+                qs += 16;
             }
         }
     } return;
@@ -236,7 +268,8 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
 /* type_traits[..].vec_dot_type, ggml.c:793-959 */
 int orc_vec_dot_type(int wtype) {
     switch (wtype) {
-        case KT_Q4_0: case KT_Q5_0: case KT_Q8_0: return KT_Q8_0;
+        case KT_Q4_0: case KT_Q5_0: case KT_Q8_0: case KT_IQ4_NL: return KT_Q8_0;   /* ggml.c:1053 */
+        case KT_IQ4_XS: return KT_Q8_K;                                             /* ggml.c:1065 */
         case KT_Q4_1: case KT_Q5_1: return KT_Q8_1;
         case KT_Q2_K: case KT_Q3_K: case KT_Q4_K: case KT_Q5_K: case KT_Q6_K: return KT_Q8_K;
         case KT_F16: return KT_F16;
@@ -547,6 +580,51 @@ static float dot_q8_0(int n, const blk_q8_0 *x, const blk_q8_0 *y) {       /* :5
     return sumf;
 }
 
+static float dot_iq4_nl(int n, const blk_iq4_nl *x, const blk_q8_0 *y) {   /* :12470, scalar tail :12660-12668 */
+    float sumf = 0;
+    for (int ib = 0; ib < n / 32; ++ib) {
+        const float d = H2F(y[ib].d) * H2F(x[ib].d);
+        int sumi1 = 0, sumi2 = 0;
+        for (int j = 0; j < 16; ++j) {
+            sumi1 += y[ib].qs[j] * kvalues_iq4nl[x[ib].qs[j] & 0xf];
+            sumi2 += y[ib].qs[j + 16] * kvalues_iq4nl[x[ib].qs[j] >> 4];
+        }
+        sumf += d * (sumi1 + sumi2);
+    }
+    return sumf;
+}
+
+static float dot_iq4_xs(int n, const blk_iq4_xs *x, const blk_q8_K *y) {   /* :12672, scalar branch :12974-13006 */
+    float sumf = 0;
+    for (int ibl = 0; ibl < n / QK_K; ++ibl) {
+        const float d4d8 = H2F(x[ibl].d) * y[ibl].d;
+        uint16_t h = x[ibl].scales_h;
+        const uint8_t *qs = x[ibl].qs;
+        const int8_t *q8 = y[ibl].qs;
+        for (int ib = 0; ib < QK_K / 32; ib += 2) {
+            const uint8_t ls1 = (x[ibl].scales_l[ib / 2] & 0xf) | ((h << 4) & 0x30);
+            const uint8_t ls2 = (x[ibl].scales_l[ib / 2] >> 4) | ((h << 2) & 0x30);
+            h >>= 4;
+            const float d1 = d4d8 * (ls1 - 32), d2 = d4d8 * (ls2 - 32);
+            int sumi1 = 0, sumi2 = 0;
+            for (int j = 0; j < 16; ++j) {
+                sumi1 += q8[j] * kvalues_iq4nl[qs[j] & 0xf];
+                sumi2 += q8[j + 16] * kvalues_iq4nl[qs[j] >> 4];
+            }
+            sumf += d1 * (sumi1 + sumi2);
+            qs += 16; q8 += 32;
+            sumi1 = sumi2 = 0;
+            for (int j = 0; j < 16; ++j) {
+                sumi1 += q8[j] * kvalues_iq4nl[qs[j] & 0xf];
+                sumi2 += q8[j + 16] * kvalues_iq4nl[qs[j] >> 4];
+            }
+            sumf += d2 * (sumi1 + sumi2);
+            qs += 16; q8 += 32;
+        }
+    }
+    return sumf;
+}
+
 static float dot_f16(int n, const uint16_t *x, const uint16_t *y) {        /* ggml.c:2258 */
     double s = 0;
     for (int i = 0; i < n; ++i) s += (double)(H2F(x[i]) * H2F(y[i]));
@@ -565,6 +643,8 @@ float orc_vec_dot(int wtype, int n, const void *w, const void *a) {
         case KT_Q4_1: return dot_q4_1(n, w, a);
         case KT_Q5_1: return dot_q5_1(n, w, a);
         case KT_Q8_0: return dot_q8_0(n, w, a);
+        case KT_IQ4_NL: return dot_iq4_nl(n, w, a);
+        case KT_IQ4_XS: return dot_iq4_xs(n, w, a);
         case KT_F16: return dot_f16(n, w, a);
         case KT_F32: { const float *x = w, *y = a; double s = 0; for (int i = 0; i < n; ++i) s += x[i] * y[i]; return (float)s; }
         default: abort();

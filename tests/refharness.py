@@ -15,8 +15,9 @@ REF_BIN_SCALAR = os.path.join(ROOT, "oracle", "_ref", "scalar", "ref_llama")   #
 
 # ggml_type ids (ggml/include/ggml.h:364-399)
 F32, F16, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q3_K, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 3, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15
+IQ4_NL, IQ4_XS = 20, 23
 BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q4_1: (32, 20), Q5_0: (32, 22), Q5_1: (32, 24), Q8_0: (32, 34), Q8_1: (32, 36), Q2_K: (256, 84), Q3_K: (256, 110), Q4_K: (256, 144),
-         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292)}
+         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292), IQ4_NL: (32, 18), IQ4_XS: (256, 136)}
 
 
 def row_bytes(t, k):
@@ -302,6 +303,16 @@ def q5_0_types(n_layer):
 def q4_1_types(n_layer):
     """LLAMA_FTYPE_MOSTLY_Q4_1: Q4_1 everywhere, output Q6_K"""
     return uniform_types(n_layer, Q4_1, Q6_K)
+
+
+def iq4_nl_types(n_layer):
+    """LLAMA_FTYPE_MOSTLY_IQ4_NL (src/llama.cpp llama_model_quantize_internal): IQ4_NL everywhere, output Q6_K"""
+    return uniform_types(n_layer, IQ4_NL, Q6_K)
+
+
+def iq4_xs_types(n_layer):
+    """LLAMA_FTYPE_MOSTLY_IQ4_XS: IQ4_XS everywhere, output Q6_K"""
+    return uniform_types(n_layer, IQ4_XS, Q6_K)
 
 
 def q5_1_types(n_layer):

@@ -1,7 +1,9 @@
-"""Q2_K, Q3_K, Q5_0, Q4_1 and Q5_1 weights (Q2_K / Q3_K_S / Q3_K_M / Q5_0 / Q4_1 / Q5_1 models; block_q2_K /
-block_q3_K / block_q5_0 / block_q4_1 / block_q5_1, ggml-common.h:250,267,161,149,168; Q4_1 / Q5_1 dot Q8_1
-activations, block_q8_1.s = f16(d * sum qs)): the CPU oracle and the HIP kernels against the reference builds' own outputs
-(tests/golden/q2k.npz / q3k.npz / q50.npz / q41.npz / q51.npz, make_q2k.py / make_q3k.py / make_legacy32.py).
+"""Q2_K, Q3_K, Q5_0, Q4_1, Q5_1, IQ4_NL and IQ4_XS weights (Q2_K / Q3_K_S / Q3_K_M / Q5_0 / Q4_1 / Q5_1 / IQ4_NL /
+IQ4_XS models; block_q2_K / block_q3_K / block_q5_0 / block_q4_1 / block_q5_1 / block_iq4_nl / block_iq4_xs,
+ggml-common.h:250,267,161,149,168,407,413; Q4_1 / Q5_1 dot Q8_1 activations, block_q8_1.s = f16(d * sum qs); IQ4_NL
+dot Q8_0, IQ4_XS dot Q8_K through the kvalues_iq4nl code book): the CPU oracle and the HIP kernels against the reference
+builds' own outputs (tests/golden/q2k.npz / q3k.npz / q50.npz / q41.npz / q51.npz / iq4nl.npz / iq4xs.npz,
+make_q2k.py / make_q3k.py / make_legacy32.py / make_iq4.py).
 
 * oracle (CPU): dequantize_row_q3_K bit-exact on synthetic and random-bit blocks; mul_mat at decode / small-batch /
   prefill shapes within 3e-6 of the output scale (a different fp32 summation order than ggml_vec_dot_q3_K_q8_K);
@@ -18,7 +20,8 @@ import pytest
 import refharness as R
 
 KINDS = {"q3_k": (R.Q3_K, "q3k.npz"), "q2_k": (R.Q2_K, "q2k.npz"), "q5_0": (R.Q5_0, "q50.npz"),
-         "q4_1": (R.Q4_1, "q41.npz"), "q5_1": (R.Q5_1, "q51.npz")}
+         "q4_1": (R.Q4_1, "q41.npz"), "q5_1": (R.Q5_1, "q51.npz"), "iq4_nl": (R.IQ4_NL, "iq4nl.npz"),
+         "iq4_xs": (R.IQ4_XS, "iq4xs.npz")}
 
 
 @pytest.fixture(scope="module", params=sorted(KINDS))
@@ -146,8 +149,8 @@ def test_gpu_fused_decode_matvec(env, kq, mode, pro):
     activation given (PRO 0) or quantized in the prologue (PRO 2), SiLU-GLU with the rms_norm prologue (PRO 1)"""
     torch, K = env
     T, _ = kq
-    if T in (R.Q4_1, R.Q5_1):
-        pytest.skip("Q8_1-activation types have no fused decode mat-vec: the runtime decodes them per op")
+    if T in (R.Q4_1, R.Q5_1, R.IQ4_NL, R.IQ4_XS):
+        pytest.skip("Q8_1-activation and code-book types have no fused decode mat-vec: the runtime decodes them per op")
     Kd, N = 4096, 512
     rng = np.random.default_rng(7 + mode + pro)
     x = rng.standard_normal(Kd).astype(np.float32)
