@@ -9,7 +9,7 @@ import glob
 import json
 import sys
 
-KERNELS = ["k_gemm_q4v3", "k_gemm_q6v3", "k_gemm_kq", "k_gemm_q80s2", "k_fa_prefill_mfma2", "k_fa_prefill_mfma",
+KERNELS = ["k_gemm_q4v4", "k_gemm_q4v3", "k_gemm_q6v3", "k_gemm_kq", "k_gemm_q80s2", "k_fa_prefill_mfma3", "k_fa_prefill_mfma2", "k_fa_prefill_mfma",
            "k_act_frag3", "k_act_frag6", "k_splitk_reduce"]
 
 
@@ -46,7 +46,8 @@ def main():
             e["trace_avg_us"] = round(sum(dur[k]) / len(dur[k]), 2)
         g = a.get("GRBM_GUI_ACTIVE")
         if g and "SQ_VALU_MFMA_BUSY_CYCLES" in a:
-            e["mfma_busy_frac"] = round(a["SQ_VALU_MFMA_BUSY_CYCLES"] / (g / 8 * 1024), 4)
+            # time-weighted over the kernel's dispatches (sums of both counters, same passes' dispatch sets)
+            e["mfma_busy_frac"] = round(sum(cs["SQ_VALU_MFMA_BUSY_CYCLES"]) / (sum(cs["GRBM_GUI_ACTIVE"]) / 8 * 1024), 4)
             if k in dur:
                 e["clock_ghz_est"] = round(g / 8 / (e["trace_avg_us"] * 1e3), 3)
         if "SQ_WAVE_CYCLES" in a:
