@@ -719,7 +719,7 @@ generation_outputs generate(const generation_inputs in) {
 // GGUF tokenizer.ggml.pre value); returns the word count (at most cap offsets written)
 int kcpp_pretokenize(const char *pre, const char *text, int64_t *ends, int cap) {
     if (!pre || !text) return -1;
-    const std::vector<size_t> e = Tokenizer::pretokenize_offsets(Tokenizer::pre_type(pre), std::string(text));
+    const std::vector<size_t> e = Tokenizer::pretokenize_offsets(std::string(pre), std::string(text));
     for (size_t i = 0; i < e.size() && (int)i < cap; ++i) ends[i] = (int64_t)e[i];
     return (int)e.size();
 }

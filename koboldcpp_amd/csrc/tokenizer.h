@@ -1,20 +1,29 @@
 // tokenizer.h -- GGUF-vocabulary tokenizers for the drop-in generate() path.
 //   "llama" (SentencePiece BPE, llm_tokenizer_spm semantics, src/llama-vocab.cpp): "▁" for spaces, optional
 //     space prefix, greedy highest-score bigram merges over UTF-8 characters, <0xXX> byte fallback.
-//   "gpt2" (byte-level BPE, Llama-3): GPT-2 byte->unicode map, merges by rank (whole pre-token words found in the
-//     vocabulary taken as is for the Llama-3 pre-tokenizer: tokenizer_ignore_merges, src/llama-vocab.cpp:777); the
-//     pre-tokenizers are restated on code points with the Unicode classes \p{L} / \p{N} / \s of
-//     unicode_ranges.h: llama3 (unicode_regex_split_custom_llama3, src/unicode.cpp:355-492: "llama3", "llama-v3",
-//     "llama-bpe", "dbrx", "smaug-bpe", "chatglm-bpe"), qwen2 (the same with single-digit numbers: "qwen2",
-//     "stablelm2") and gpt2 (unicode_regex_split_custom_gpt2, :248-352: "gpt-2", "phi-2", "mpt", "olmo", "jais",
-//     "jina-*"; also every other pre type, for which the reference runs several std::regex passes -- an
-//     approximation there).  Invalid UTF-8 bytes become U+FFFD (the reference throws).
+//   "gpt2" (byte-level BPE): GPT-2 byte->unicode map, merges by rank (whole pre-token words found in the
+//     vocabulary taken as is for the llama3 / tekken pre-tokenizers: tokenizer_ignore_merges, src/llama-vocab.cpp:777).
+//     The pre-tokenizer of every type llm_load_vocab accepts (src/llama.cpp:6338-6441) is its list of split passes
+//     (llm_tokenizer_bpe's regex_exprs, src/llama-vocab.cpp:597-712), applied in order, each splitting every current
+//     piece into its matches and the text between them (unicode_regex_split, src/unicode.cpp:663-830):
+//       - the passes the reference runs with hand-written matchers are restated on code points with the Unicode
+//         classes of unicode_ranges.h: llama3 (unicode_regex_split_custom_llama3, :355-492), gpt2
+//         (unicode_regex_split_custom_gpt2, :248-352), and qwen2's expression (llama3's with single digits);
+//       - every other pass runs on the C++ <regex> engines as the reference does: expressions that use \p{L} /
+//         \p{N} / \p{P} on a "collapsed" text (ASCII kept, other code points replaced by one byte per class:
+//         whitespace 0x0B, number 0xD1, letter 0xD2, punctuation 0xD3, anything else 0xD0) with each class
+//         rewritten as a bracket of its byte and its ASCII members; the others on the code points as wchar_t with
+//         non-ASCII whitespace replaced by 0x0B.
+//     Pinned to the reference tokenizer itself (oracle/_ref/ref_vocab, tests/test_tokenizer_ref.py).  Invalid UTF-8
+//     bytes become U+FFFD (the reference throws).
 // Special tokens (token types UNKNOWN / CONTROL / USER_DEFINED) are split out of the text first, longest first,
 // as tokenizer_st_partition with parse_special (src/llama-vocab.cpp:1544; koboldcpp's common_tokenize(..., true)).
 #pragma once
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <queue>
+#include <regex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -24,6 +33,11 @@
 
 #include <algorithm>
 #include <cstring>
+
+// deepseek-llm's letter and punctuation classes (src/llama-vocab.cpp:613-614), as universal character names
+static const char *const kDeepseekLetters =
+    "\\s?[A-Za-z\u00b5\u00c0-\u00d6\u00d8-\u00f6\u00f8-\u01ba\u01bc-\u01bf\u01c4-\u0293\u0295-\u02af\u0370-\u0373\u0376\u0377\u037b-\u037d\u037f\u0386\u0388-\u038a\u038c\u038e-\u03a1\u03a3-\u03f5\u03f7-\u0481\u048a-\u052f\u0531-\u0556\u10a0-\u10c5\u13a0-\u13f5\u13f8-\u13fd\u1c90-\u1cba\u1cbd-\u1cbf\u1d00-\u1d2b\u1d6b-\u1d77\u1d79-\u1d9a\u1e00-\u1f15\u1f18-\u1f1d\u1f20-\u1f45\u1f48-\u1f4d\u1f50-\u1f57\u1f59\u1f5b\u1f5d\u1f5f-\u1f7d\u1f80-\u1fb4\u1fb6-\u1fbc\u1fbe\u1fc2-\u1fc4\u1fc6-\u1fcc\u1fd0-\u1fd3\u1fd6-\u1fdb\u1fe0-\u1fec\u1ff2-\u1ff4\u1ff6-\u1ffc\u2102\u2107\u210a-\u2113\u2115\u2119-\u211d\u2124\u2126\u2128\u212a-\u212d\u212f-\u2134\u2139\u213c-\u213f\u2145-\u2149\u214e\u2183\u2184\u2c00-\u2c7b\u2c7e-\u2ce4\u2ceb-\u2cee\u2cf2\u2cf3\ua640-\ua66d\ua680-\ua69b\ua722-\ua76f\ua771-\ua787\ua78b-\ua78e\uab70-\uabbf\ufb00-\ufb06\ufb13-\ufb17\uff21-\uff3a\uff41-\uff5a\U00010400-\U0001044f\U000104b0-\U000104d3\U000104d8-\U000104fb\U00010c80-\U00010cb2\U00010cc0-\U00010cf2\U000118a0-\U000118df\U0001e900-\U0001e943]+";
+static const char *const kDeepseekPunct = "\\s?[!-/:-~\uff01-\uff0f\uff1a-\uff5e\u2018-\u201f\u3000-\u3002]+";
 
 class Tokenizer {
 public:
@@ -46,8 +60,10 @@ public:
             if (!m) { err = "BPE vocab without merges"; return false; }
             for (size_t i = 0; i < m->astr.size(); ++i) rank_.emplace(m->astr[i], (int)i);
             build_byte_map();
-            pre_ = pre_type(f.get_s("tokenizer.ggml.pre", "default"));
-            ignore_merges_ = pre_ == PRE_LLAMA3;
+            const std::string pre = f.get_s("tokenizer.ggml.pre", "default");
+            pre_ = pre_type(pre);
+            passes_ = make_passes(pre);
+            ignore_merges_ = pre_ == PRE_LLAMA3 || pre == "tekken";
         } else if (model_ != "llama") {
             err = "unsupported tokenizer model " + model_;
             return false;
@@ -68,12 +84,66 @@ public:
                          [&](int a, int b) { return vocab_[a].size() > vocab_[b].size(); });
         return true;
     }
-    enum Pre { PRE_LLAMA3 = 0, PRE_QWEN2 = 1, PRE_GPT2 = 2 };
+    enum Pre { PRE_LLAMA3 = 0, PRE_QWEN2 = 1, PRE_GPT2 = 2, PRE_STL = 3 };
     static Pre pre_type(const std::string &p) {
         if (p == "llama3" || p == "llama-v3" || p == "llama-bpe" || p == "dbrx" || p == "smaug-bpe" || p == "chatglm-bpe")
             return PRE_LLAMA3;
         if (p == "qwen2" || p == "stablelm2") return PRE_QWEN2;
         return PRE_GPT2;
+    }
+    // one split pass: a hand-written matcher (kind PRE_LLAMA3 / PRE_QWEN2 / PRE_GPT2) or a <regex> expression
+    // (PRE_STL: `wide` = run on the code points, else on the collapsed text with the class-rewritten expression)
+    struct Pass {
+        Pre kind;
+        bool wide = false;
+        std::shared_ptr<std::regex> rx;
+        std::shared_ptr<std::wregex> wrx;
+    };
+    static Pass custom(Pre k) { Pass p; p.kind = k; return p; }
+    static Pass stl(const std::string &expr) {
+        Pass p;
+        p.kind = PRE_STL;
+        const bool cats = expr.find("\\p{L}") != std::string::npos || expr.find("\\p{N}") != std::string::npos ||
+                          expr.find("\\p{P}") != std::string::npos;
+        if (cats) {
+            p.rx = std::make_shared<std::regex>(collapse_expr(expr));
+        } else {
+            p.wide = true;
+            std::vector<uint32_t> cp;
+            std::vector<size_t> bend;
+            decode_utf8(expr, cp, bend);
+            p.wrx = std::make_shared<std::wregex>(std::wstring(cp.begin(), cp.end()));
+        }
+        return p;
+    }
+    // the pass lists of llm_tokenizer_bpe (src/llama-vocab.cpp:597-712) by GGUF pre name (src/llama.cpp:6338-6441);
+    // the gpt2 / llama3 expressions are the reference's hand-matched ones
+    static std::vector<Pass> make_passes(const std::string &p) {
+        const Pass gpt2 = custom(PRE_GPT2);
+        const std::string finnish = " ?[^(\\s|.,!?\u2026\u3002\uff0c\u3001\u0964\u06d4\u060c)]+";
+        const std::string cjk = "[\u4e00-\u9fa5\u0800-\u4e00\uac00-\ud7ff]+";
+        if (pre_type(p) == PRE_LLAMA3) return {custom(PRE_LLAMA3)};
+        if (pre_type(p) == PRE_QWEN2) return {custom(PRE_QWEN2)};
+        if (p == "gpt-2" || p == "phi-2" || p.rfind("jina-", 0) == 0 || p == "mpt" || p == "olmo" || p == "jais") return {gpt2};
+        if (p == "deepseek-llm")
+            return {stl("[\r\n]"), stl(kDeepseekLetters), stl(kDeepseekPunct), stl("\\s+$"),
+                    stl(cjk), stl("\\p{N}+")};
+        if (p == "deepseek-coder")
+            return {stl("[\r\n]"), stl("\\s?\\p{L}+"), stl("\\s?\\p{P}+"), stl(cjk), stl("\\p{N}")};
+        if (p == "falcon") return {stl("[\\p{P}\\$\\+<=>\\^~\\|`]+"), gpt2, stl("[0-9][0-9][0-9]")};
+        if (p == "starcoder" || p == "refact" || p == "command-r" || p == "smollm" || p == "codeshell" || p == "exaone")
+            return {stl("\\p{N}"), gpt2};
+        if (p == "bloom" || p == "poro-chat" || p == "gpt3-finnish") return {stl(finnish)};
+        if (p == "viking") return {stl(finnish), stl("\\p{N}")};
+        if (p == "tekken")
+            return {stl("[^\\r\\n\\p{L}\\p{N}]?((?=[\\p{L}])([^a-z]))*((?=[\\p{L}])([^A-Z]))+|[^\\r\\n\\p{L}\\p{N}]?"
+                        "((?=[\\p{L}])([^a-z]))+((?=[\\p{L}])([^A-Z]))*|\\p{N}| ?[^\\s\\p{L}\\p{N}]+[\\r\\n/]*|\\s*[\\r\\n]+|"
+                        "\\s+(?!\\S)|\\s+")};
+        if (p == "chameleon")
+            return {stl("<sentinel:[0-9]+>"), stl("(IMGIMG)((A|B|C|D|E|F|G|H|I){1,4})Z"), stl("([\\t\\n]|    |  )"),
+                    stl("\\p{N}"), stl("[\\p{P}!-/:-@\\[-`{-~]"), gpt2};
+        // "default" and any other name (the reference rejects unknown names; its default list)
+        return {stl("[\\p{P}\\$\\+<=>\\^~\\|]+"), gpt2, stl("\\p{N}+"), stl("[0-9][0-9][0-9]")};
     }
     int bos() const { return bos_; }
     int eos() const { return eos_; }
@@ -116,12 +186,12 @@ public:
         return out;
     }
     // pre-tokenizer alone (tests): byte end offsets of the words of `text`
-    static std::vector<size_t> pretokenize_offsets(Pre pre, const std::string &text) {
+    static std::vector<size_t> pretokenize_offsets(const std::string &pre, const std::string &text) {
         std::vector<uint32_t> cp;
         std::vector<size_t> bend;
         decode_utf8(text, cp, bend);
         std::vector<size_t> out;
-        for (size_t e : split_words(pre, cp)) out.push_back(bend[e - 1]);
+        for (size_t e : split_passes(make_passes(pre), cp)) out.push_back(bend[e - 1]);
         return out;
     }
     std::string piece(int id) const {            // text of one token (for streaming)
@@ -235,6 +305,89 @@ private:
             u2b_[cp] = b;
         }
     }
+    // the collapsed form of an expression (src/unicode.cpp:757-795): \p{N} / \p{L} / \p{P} become a bracket of the
+    // class byte and its ASCII members (inside an existing bracket: just those members)
+    static std::string collapse_expr(const std::string &e) {
+        static const char *members[3] = {"\xD1\x30-\x39", "\xD2\x41-\x5A\x61-\x7A",
+                                         "\xD3\x21-\x23\x25-\x2A\x2C-\x2F\x3A-\x3B\x3F-\x40\\\x5B-\\\x5D\x5F\\\x7B\\\x7D"};
+        std::string out;
+        bool inside = false;
+        for (size_t i = 0; i < e.size(); ++i) {
+            if (e[i] == '[' && (i == 0 || e[i - 1] != '\\')) { out += '['; inside = true; continue; }
+            if (inside && e[i] == ']' && e[i - 1] != '\\') { out += ']'; inside = false; continue; }
+            if (e[i] == '\\' && i + 4 < e.size() && e[i + 1] == 'p' && e[i + 2] == '{' && e[i + 4] == '}') {
+                const int k = e[i + 3] == 'N' ? 0 : e[i + 3] == 'L' ? 1 : e[i + 3] == 'P' ? 2 : -1;
+                if (k >= 0) {
+                    if (!inside) out += '[';
+                    out += members[k];
+                    if (!inside) out += ']';
+                    i += 4;
+                    continue;
+                }
+            }
+            out += e[i];
+        }
+        return out;
+    }
+    // one byte per code point (src/unicode.cpp:697-723): ASCII as is; else whitespace 0x0B, N 0xD1, L 0xD2, P 0xD3,
+    // anything else 0xD0
+    static std::string collapse_text(const std::vector<uint32_t> &cp) {
+        std::string t(cp.size(), '\0');
+        for (size_t i = 0; i < cp.size(); ++i) {
+            const uint32_t c = cp[i];
+            if (c < 0x80) { t[i] = (char)c; continue; }
+            const uint8_t f = cls(c);
+            t[i] = (char)((f & 4) ? 0x0B : (f & 2) ? 0xD1 : (f & 1) ? 0xD2 : (f & 8) ? 0xD3 : 0xD0);
+        }
+        return t;
+    }
+    // word end positions (code point indices) after every pass; a pass splits each current piece into its matches
+    // and the text between them (unicode_regex_split_stl, src/unicode.cpp:496-553)
+    static std::vector<size_t> split_passes(const std::vector<Pass> &passes, const std::vector<uint32_t> &cp) {
+        std::vector<size_t> ends{cp.size()};
+        if (cp.empty()) return {};
+        std::string coll;
+        std::wstring wt;
+        for (const Pass &ps : passes) {
+            std::vector<size_t> nx;
+            size_t b = 0;
+            for (size_t e : ends) {
+                if (ps.kind != PRE_STL) {
+                    const std::vector<uint32_t> sub(cp.begin() + b, cp.begin() + e);
+                    for (size_t w : split_words(ps.kind, sub)) nx.push_back(b + w);
+                } else {
+                    size_t last = b;
+                    auto add = [&](size_t pos, size_t len) {
+                        if (pos > last) nx.push_back(pos);
+                        nx.push_back(pos + len);
+                        last = pos + len;
+                    };
+                    if (ps.wide) {
+                        if (wt.empty()) {
+                            wt.assign(cp.begin(), cp.end());
+                            for (auto &c : wt)
+                                if ((uint32_t)c > 0x7F && (cls((uint32_t)c) & 4)) c = 0x0B;
+                        }
+                        for (std::wcregex_iterator it(wt.data() + b, wt.data() + e, *ps.wrx), end; it != end; ++it)
+                            add(b + (size_t)it->position(), (size_t)it->length());
+                    } else {
+                        if (coll.empty()) coll = collapse_text(cp);
+                        for (std::cregex_iterator it(coll.data() + b, coll.data() + e, *ps.rx), end; it != end; ++it)
+                            add(b + (size_t)it->position(), (size_t)it->length());
+                    }
+                    if (last < e) nx.push_back(e);
+                }
+                b = e;
+            }
+            // empty matches leave zero-length pieces; the reference's BPE skips nothing for them either way
+            std::vector<size_t> clean;
+            size_t prev = 0;
+            for (size_t e : nx)
+                if (e > prev) { clean.push_back(e); prev = e; }
+            ends.swap(clean);
+        }
+        return ends;
+    }
     // ---- pre-tokenizers over code points
     static uint8_t cls(uint32_t c) {                   // 1 = \p{L}, 2 = \p{N}, 4 = \s
         if (c < 0x80) {
@@ -343,7 +496,7 @@ private:
         std::vector<size_t> bend;
         decode_utf8(text, cp, bend);
         size_t w0 = 0;
-        for (size_t e : split_words(pre_, cp)) {
+        for (size_t e : split_passes(passes_, cp)) {
             std::string word;                           // the word's code points re-encoded (U+FFFD for bad bytes)
             for (size_t k = w0; k < e; ++k) word += utf8_enc(cp[k]);
             w0 = e;
@@ -374,6 +527,7 @@ private:
 
     std::string model_;
     Pre pre_ = PRE_LLAMA3;
+    std::vector<Pass> passes_;
     bool ignore_merges_ = false;
     std::vector<int> special_;
     std::vector<std::string> vocab_;
