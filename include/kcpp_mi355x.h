@@ -346,6 +346,9 @@ int kcpp_gguf_check(const char *path, char *err, int err_len);
  * tokenizer_st_partition src/llama-vocab.cpp:1544).  Return the count, -1 on error. */
 int kcpp_pretokenize(const char *pre, const char *text, int64_t *ends, int cap);
 int kcpp_tokenize_probe(const char *gguf_path, const char *text, int add_bos, int32_t *out, int cap);
+/* every vocabulary id's streamed text (llama_token_to_piece_impl with special = false, src/llama-vocab.cpp:2007)
+ * concatenated into out (<= cap bytes), ends[i] = end offset of id i; returns n_vocab, -1 on a load error (host only) */
+int kcpp_pieces_probe(const char *gguf_path, char *out, int64_t cap, int64_t *ends, int n_ends);
 /* the vocabulary's special ids as generate() uses them: out = {bos, eos, eot} (eot -1 when the vocabulary has none;
  * llm_load_vocab's EOT detection, src/llama.cpp:6606, 6642-6661).  0 ok, -1 on a load error */
 int kcpp_tokenizer_special_ids(const char *gguf_path, int32_t *out);

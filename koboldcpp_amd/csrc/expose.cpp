@@ -739,6 +739,24 @@ int kcpp_tokenize_probe(const char *gguf_path, const char *text, int add_bos, in
     return (int)ids.size();
 }
 
+// the GGUF's tokenizer alone (tests, host only): every vocabulary id's streamed text (generate()'s piece rendering)
+// concatenated into out (at most cap bytes), ends[i] = end offset of id i's piece (at most n_ends written);
+// returns the vocabulary size, -1 on a load error
+int kcpp_pieces_probe(const char *gguf_path, char *out, int64_t cap, int64_t *ends, int n_ends) {
+    gguf::File f;
+    std::string err;
+    Tokenizer tk;
+    if (!gguf_path || !f.open(gguf_path, err) || !tk.init(f, err)) return -1;
+    int64_t o = 0;
+    for (int i = 0; i < tk.n_vocab(); ++i) {
+        const std::string p = tk.piece(i);
+        if (out && o + (int64_t)p.size() <= cap) memcpy(out + o, p.data(), p.size());
+        o += (int64_t)p.size();
+        if (ends && i < n_ends) ends[i] = o;
+    }
+    return tk.n_vocab();
+}
+
 // bench.py --gpus N (N > 1): the drop-in engine over n_dev GPUs -- load_model's stages (build_stages), hand-off
 // (init_handoff: RCCL clique over distinct GPUs), forward() -- with synthetic weights instead of a GGUF.  Prefill of
 // n_prompt ids in ubatches of ub (timed to the last stage's drain), then n_warm + n_steps greedy tokens exactly as

@@ -194,14 +194,20 @@ public:
         for (size_t e : split_passes(make_passes(pre), cp)) out.push_back(bend[e - 1]);
         return out;
     }
-    std::string piece(int id) const {            // text of one token (for streaming)
+    // text of one token as generate() streams it: llama_token_to_piece_impl with special = false
+    // (src/llama-vocab.cpp:2007-2077): unknown / control tokens render nothing, user-defined tokens their text,
+    // normal tokens unescaped (SPM: U+2581 -> space) or byte-decoded (BPE, llama_decode_text :1986-2004: a code
+    // point outside the byte map renders as "[UNK_BYTE_0x<its utf8>" + token text + "]"), SPM byte tokens their
+    // byte, every other type (undefined, unused, BPE byte) nothing
+    std::string piece(int id) const {
         if (id < 0 || id >= (int)vocab_.size()) return "";
         const int type = ttype_[id];
-        if (type == 3 || type == 4) return "";       // control / unused: not rendered
         const std::string &s = vocab_[id];
+        if (type == 2 || type == 3) return "";
+        if (type == 4) return s;
         if (model_ == "llama") {
-            if (type == 6 && s.size() == 6 && s.compare(0, 3, "<0x") == 0)        // byte token
-                return std::string(1, (char)strtol(s.substr(3, 2).c_str(), nullptr, 16));
+            if (type == 6) return s.size() >= 5 ? std::string(1, (char)strtol(s.substr(3, 2).c_str(), nullptr, 16)) : "";
+            if (type != 1) return "";
             std::string r;
             for (size_t i = 0; i < s.size();) {
                 if (s.compare(i, 3, "\xe2\x96\x81") == 0) { r += ' '; i += 3; }
@@ -209,12 +215,18 @@ public:
             }
             return r;
         }
+        if (type != 1) return "";
         std::string r;                                  // gpt2: unicode code points -> bytes
         for (size_t i = 0; i < s.size();) {
             uint32_t cp; int n = utf8_dec(s, i, cp);
             auto it = u2b_.find(cp);
             if (it != u2b_.end()) r += (char)it->second;
-            else r += s.substr(i, n);
+            else {
+                static const char hx[] = "0123456789abcdef";
+                r += "[UNK_BYTE_0x";
+                for (int k = 0; k < n; ++k) { r += hx[(unsigned char)s[i + k] >> 4]; r += hx[(unsigned char)s[i + k] & 15]; }
+                r += s + "]";
+            }
             i += n;
         }
         return r;

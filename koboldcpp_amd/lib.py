@@ -54,6 +54,7 @@ _SIGS = {
     "kcpp_gguf_check": [ctypes.c_char_p, ctypes.c_char_p, I],
     "kcpp_pretokenize": [ctypes.c_char_p, ctypes.c_char_p, P, I],
     "kcpp_tokenize_probe": [ctypes.c_char_p, ctypes.c_char_p, I, P, I],
+    "kcpp_pieces_probe": [ctypes.c_char_p, P, I64, P, I],
     "kcpp_tokenizer_special_ids": [ctypes.c_char_p, P],
     "kcpp_engine_bench": [P, P, I, I, P, U64, I, I, I, I, P],
     "kcpp_add": [P, P, P, I64, P],

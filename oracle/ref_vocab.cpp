@@ -12,7 +12,8 @@
 //   VOCAB: "bpe <pre-name>" | "spm"; then n; n lines "<hex text> <score> <type>" (GGUF token_type: 1 normal,
 //          2 unknown, 3 control, 4 user-defined, 6 byte); then m; m lines "<hex left> <hex right>" (BPE merges);
 //          then "bos eos unk add_bos" ids
-//   TEXTS: n; n lines of hex text;  OUT: one line of token ids per text (add_special false, parse_special true)
+//   TEXTS: n; n lines of hex text;  OUT: one line of token ids per text (add_special false, parse_special true),
+//   then one line per vocabulary id: its piece (llama_token_to_piece_impl, special = false) in hex, "-" if empty
 #include "llama-vocab.h"
 
 #include <algorithm>
@@ -139,6 +140,15 @@ int main(int argc, char **argv) {
         const auto ids = llama_tokenize_internal(v, unhex(h), false, true);
         for (size_t k = 0; k < ids.size(); ++k) fo << (k ? " " : "") << ids[k];
         fo << "\n";
+    }
+    // then every token's piece as koboldcpp streams it (llama_token_to_piece_impl, special = false), in hex
+    static const char hx[] = "0123456789abcdef";
+    for (size_t i = 0; i < n; ++i) {
+        char buf[1024];
+        const int32_t len = llama_token_to_piece_impl(v, (llama_token)i, buf, sizeof buf, 0, false);
+        std::string h;
+        for (int32_t k = 0; k < len; ++k) { h += hx[(unsigned char)buf[k] >> 4]; h += hx[(unsigned char)buf[k] & 15]; }
+        fo << (h.empty() ? "-" : h) << "\n";
     }
     return 0;
 }

@@ -3,7 +3,8 @@ the REFERENCE tokenizer itself: src/llama-vocab.cpp + src/unicode.cpp compiled f
 oracle/_ref/ref_vocab (oracle/ref_vocab.cpp fills llama_vocab as llm_load_vocab does and calls
 llama_tokenize_internal).  Both tokenize the same random Unicode texts with the same vocabulary (byte-level BPE
 trained with HF `tokenizers`, under every pre-tokenizer name llm_load_vocab accepts; a SentencePiece-style SPM
-vocabulary with byte fallback): the token ids must be equal.  Runs where the reference sources are (the build
+vocabulary with byte fallback): the token ids must be equal; and every vocabulary id's streamed piece
+(llama_token_to_piece_impl, special = false) must be equal byte for byte.  Runs where the reference sources are (the build
 container); skipped elsewhere."""
 import ctypes
 import json
@@ -39,7 +40,12 @@ def _hex(s):
     return b.hex() if b else "-"
 
 
-def ref_tokenize(ref_bin, tmp, kind, tokens, scores, ttypes, merges, texts, bos=-1, eos=-1, unk=-1, add_bos=-1):
+def ref_tokenize(*args, **kw):
+    return ref_run(*args, **kw)[0]
+
+
+def ref_run(ref_bin, tmp, kind, tokens, scores, ttypes, merges, texts, bos=-1, eos=-1, unk=-1, add_bos=-1):
+    """the reference's ids for each text and its piece (special = false) for each vocabulary id"""
     vp, tp, op = (os.path.join(tmp, n) for n in ("v.txt", "t.txt", "o.txt"))
     with open(vp, "w") as f:
         f.write(kind + "\n%d\n" % len(tokens))
@@ -55,7 +61,23 @@ def ref_tokenize(ref_bin, tmp, kind, tokens, scores, ttypes, merges, texts, bos=
             f.write(_hex(t) + "\n")
     subprocess.check_call([ref_bin, vp, tp, op])
     with open(op) as f:
-        return [[int(x) for x in line.split()] for line in f.read().split("\n")[:len(texts)]]
+        lines = f.read().split("\n")
+    ids = [[int(x) for x in line.split()] for line in lines[:len(texts)]]
+    pieces = [b"" if h == "-" else bytes.fromhex(h) for h in lines[len(texts):len(texts) + len(tokens)]]
+    assert len(pieces) == len(tokens)
+    return ids, pieces
+
+
+def ours_pieces(lib, path, n):
+    cap = 1 << 20
+    buf = ctypes.create_string_buffer(cap)
+    ends = (ctypes.c_int64 * n)()
+    assert lib.kcpp_pieces_probe(path.encode(), buf, cap, ends, n) == n and ends[n - 1] <= cap
+    raw, out, s = buf.raw, [], 0
+    for e in ends:
+        out.append(raw[s:e])
+        s = e
+    return out
 
 
 def ours_tokenize(lib, path, texts):
@@ -172,3 +194,45 @@ def test_spm_matches_reference_tokenizer(ref_bin, lib, tmp_path):
     got = ours_tokenize(lib, path, texts)
     bad = [(t, g, w) for t, g, w in zip(texts, got, want) if g != w]
     assert not bad, (len(bad), bad[:2])
+
+
+# token types as GGUF stores them (llama_token_type): 0 undefined, 1 normal, 2 unknown, 3 control, 4 user-defined,
+# 5 unused, 6 byte -- every one in both vocabularies, plus normal BPE tokens outside the byte map ("[UNK_BYTE_0x..]")
+EXTRA = [("中文", 1), ("a中b", 1), ("<user>", 4), ("<unused0>", 5), ("<undef>", 0), ("<bpe_byte>", 6),
+         ("<unk_t>", 2), ("▁x▁y", 1)]
+
+
+def test_pieces_match_reference(ref_bin, lib, bpe_vocab, tmp_path):
+    """detokenization pinned to the reference: every vocabulary id's streamed text (what generate() appends per
+    token: llama_token_to_piece_impl with special = false, src/llama-vocab.cpp:2007-2077) equal, byte for byte,
+    for a byte-level BPE and an SPM vocabulary holding every token type"""
+    import gguf_writer as GW
+    tokens, merges = bpe_vocab
+    tokens = tokens + [t for t, _ in EXTRA]
+    ttype = [3 if t in SPECIALS else 1 for t in bpe_vocab[0]] + [y for _, y in EXTRA]
+    kv = {"general.architecture": "llama", "tokenizer.ggml.model": "gpt2", "tokenizer.ggml.pre": "llama-bpe",
+          "tokenizer.ggml.tokens": (GW.STR, tokens), "tokenizer.ggml.token_type": (GW.I32, ttype),
+          "tokenizer.ggml.merges": (GW.STR, [a + " " + b for a, b in merges])}
+    path = str(tmp_path / "bpe.gguf")
+    GW.write(path, kv, [("token_embd.weight", 0, [8, len(tokens)], np.zeros((len(tokens), 8), np.float32))])
+    _, want = ref_run(ref_bin, str(tmp_path), "bpe llama-bpe", tokens, [0.0] * len(tokens), ttype, merges, [])
+    assert any(w.startswith(b"[UNK_BYTE_0x") for w in want) and want[tokens.index("<user>")] == b"<user>"
+    got = ours_pieces(lib, path, len(tokens))
+    bad = [(i, tokens[i], g, w) for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, (len(bad), bad[:4])
+
+    tokens, scores, ttype = _spm_vocab()
+    tokens = tokens + [t for t, _ in EXTRA]
+    ttype = ttype + [y for _, y in EXTRA]
+    scores = scores + [-1e4] * len(EXTRA)
+    kv = {"general.architecture": "llama", "tokenizer.ggml.model": "llama",
+          "tokenizer.ggml.tokens": (GW.STR, tokens), "tokenizer.ggml.scores": (GW.F32, scores),
+          "tokenizer.ggml.token_type": (GW.I32, ttype), "tokenizer.ggml.bos_token_id": 1,
+          "tokenizer.ggml.eos_token_id": 2, "tokenizer.ggml.unknown_token_id": 0}
+    path = str(tmp_path / "spm.gguf")
+    GW.write(path, kv, [("token_embd.weight", 0, [8, len(tokens)], np.zeros((len(tokens), 8), np.float32))])
+    _, want = ref_run(ref_bin, str(tmp_path), "spm", tokens, scores, ttype, [], [], bos=1, eos=2, unk=0)
+    assert want[3 + 0x41] == b"A" and want[tokens.index("\u2581x\u2581y")] == b" x y"
+    got = ours_pieces(lib, path, len(tokens))
+    bad = [(i, tokens[i], g, w) for i, (g, w) in enumerate(zip(got, want)) if g != w]
+    assert not bad, (len(bad), bad[:4])
