@@ -132,12 +132,20 @@ template <> struct GemmTraits<KT_Q2_K> { static constexpr int NB = 1; static con
 template <> struct GemmTraits<KT_Q4_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
 template <> struct GemmTraits<KT_Q5_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
 template <> struct GemmTraits<KT_Q8_0> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
+template <> struct GemmTraits<KT_Q4_1> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
+template <> struct GemmTraits<KT_Q5_1> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
+template <> struct GemmTraits<KT_IQ4_NL> { static constexpr int NB = 1; static constexpr bool MINS = false; static constexpr bool SB = false; };
+template <> struct GemmTraits<KT_IQ4_XS> { static constexpr int NB = 2; static constexpr bool MINS = false; static constexpr bool SB = true; };
+// Q8_1-activation types: the per-block m_w * s_a term (block_q8_1.s)
+template <int TYPE> constexpr bool kGemmM1 = TYPE == KT_Q4_1 || TYPE == KT_Q5_1;
 
 template <int NB> struct GemmSmem {
     h8v bf[NB][2 * 16 * 64];      // [plane][tile*16*64 + step*64 + lane]
     h8v bm[2 * 64];               // mins fragment [tile*64 + lane]
     float wd[GB_N][8];            // K-quants: [0]=d, [1]=dmin ; Q4_0/Q8_0: d per 32-block
     float dy[GB_M][8];            // K-quants: [0]=dy of this super-block ; Q4_0/Q8_0: per 32-block
+    float wm[GB_N][8];            // Q4_1 / Q5_1: m per 32-block
+    float sy[GB_M][8];            // Q4_1 / Q5_1: block_q8_1.s per 32-block
 };
 
 // dequantize the 64 x 256 weight tile of super-block `sb` into LDS (thread t: row t>>2, chunk t&3)
@@ -288,6 +296,65 @@ __device__ __forceinline__ void stage_weights(SM &S, const uint8_t *__restrict__
                                                      1.0f, 16.0f);
             S.wd[nl][jb] = h2f(*(const uint16_t *)(W + nbt * 20 + b * 2));
         }
+    } else if constexpr (TYPE == KT_Q4_1 || TYPE == KT_Q5_1) {
+        // q (| h << 4) in [0, 31] as is (s = 1, off = 0); d and m per block (SoA: qs [nb][16] (++ qh [nb][4]) ++ dm [nb][4])
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int jb = 2 * c + bb;
+            const int64_t b = n * bpr + sb * 8 + jb;
+            const uint4 qv = *(const uint4 *)(W + b * 16);
+            const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
+            uint32_t h = 0;
+            if constexpr (TYPE == KT_Q5_1) h = *(const uint32_t *)(W + nbt * 16 + b * 4);
+            auto hb = [&](int sh) { return (((h >> sh) & 0xFu) * 0x00204081u & 0x01010101u) << 4; };
+            S.bf[0][bslot(nl, 32 * jb + 0)] = frag8((qd[0] & 0x0F0F0F0Fu) | hb(0), (qd[1] & 0x0F0F0F0Fu) | hb(4), 1.0f, 0.0f);
+            S.bf[0][bslot(nl, 32 * jb + 8)] = frag8((qd[2] & 0x0F0F0F0Fu) | hb(8), (qd[3] & 0x0F0F0F0Fu) | hb(12), 1.0f, 0.0f);
+            S.bf[0][bslot(nl, 32 * jb + 16)] = frag8(((qd[0] >> 4) & 0x0F0F0F0Fu) | hb(16), ((qd[1] >> 4) & 0x0F0F0F0Fu) | hb(20),
+                                                     1.0f, 0.0f);
+            S.bf[0][bslot(nl, 32 * jb + 24)] = frag8(((qd[2] >> 4) & 0x0F0F0F0Fu) | hb(24), ((qd[3] >> 4) & 0x0F0F0F0Fu) | hb(28),
+                                                     1.0f, 0.0f);
+            const uint32_t dm = *(const uint32_t *)(W + nbt * (TYPE == KT_Q5_1 ? 20 : 16) + b * 4);
+            S.wd[nl][jb] = h2f((uint16_t)(dm & 0xFFFF));
+            S.wm[nl][jb] = h2f((uint16_t)(dm >> 16));
+        }
+    } else if constexpr (TYPE == KT_IQ4_NL) {
+        // code-book values kvalues_iq4nl[q] in [-127, 113] through v_perm (iq4nl_lut4), as Q8_0's biased bytes
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int jb = 2 * c + bb;
+            const int64_t b = n * bpr + sb * 8 + jb;
+            const uint4 qv = *(const uint4 *)(W + b * 16);
+            const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
+            auto lv = [&](uint32_t x) { return iq4nl_lut4(x & 0x0F0F0F0Fu) ^ 0x80808080u; };
+            S.bf[0][bslot(nl, 32 * jb + 0)] = frag8(lv(qd[0]), lv(qd[1]), 1.0f, 128.0f);
+            S.bf[0][bslot(nl, 32 * jb + 8)] = frag8(lv(qd[2]), lv(qd[3]), 1.0f, 128.0f);
+            S.bf[0][bslot(nl, 32 * jb + 16)] = frag8(lv(qd[0] >> 4), lv(qd[1] >> 4), 1.0f, 128.0f);
+            S.bf[0][bslot(nl, 32 * jb + 24)] = frag8(lv(qd[2] >> 4), lv(qd[3] >> 4), 1.0f, 128.0f);
+            S.wd[nl][jb] = h2f(*(const uint16_t *)(W + nbt * 16 + b * 2));
+        }
+    } else if constexpr (TYPE == KT_IQ4_XS) {
+        // sub-blocks 2c, 2c+1: (ls - 32) kv split as 8 (sc >> 3) kv + (sc & 7) kv over two planes (as Q6_K), both exact
+        // f16 integers; SoA: qs [nb][128] ++ (d, scales_h, scales_l[4]) [nb][8]
+        const int64_t b = n * bpr + sb;
+        const uint2 hv = *(const uint2 *)(W + nbt * 128 + b * 8);
+        const uint32_t shv = hv.x >> 16, slv = hv.y;
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int ib = 2 * c + bb;
+            const uint4 qv = *(const uint4 *)(W + b * 128 + 16 * ib);
+            const uint32_t qd[4] = {qv.x, qv.y, qv.z, qv.w};
+            const int sc = (int)(((slv >> (8 * (ib >> 1) + 4 * (ib & 1))) & 0xF) | (((shv >> (2 * ib)) & 3) << 4)) - 32;
+            const float shi = (float)(8 * (sc >> 3)), slo = (float)(sc & 7);
+            auto lv = [&](uint32_t x) { return iq4nl_lut4(x & 0x0F0F0F0Fu) ^ 0x80808080u; };
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int sh = i < 2 ? 0 : 4, w0 = 2 * (i & 1);
+                const uint32_t t0 = lv(qd[w0] >> sh), t1 = lv(qd[w0 + 1] >> sh);
+                S.bf[0][bslot(nl, 32 * ib + 8 * i)] = frag8_sub(t0, t1, shi, 128.0f);
+                S.bf[1][bslot(nl, 32 * ib + 8 * i)] = frag8_sub(t0, t1, slo, 128.0f);
+            }
+        }
+        if (c == 0) S.wd[nl][0] = h2f((uint16_t)(hv.x & 0xFFFF));
     } else {   // Q8_0: int8 -> (q ^ 0x80) = q + 128 as a byte
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
@@ -304,15 +371,19 @@ __device__ __forceinline__ void stage_weights(SM &S, const uint8_t *__restrict__
 }
 
 template <int TYPE>
-__global__ void __launch_bounds__(256) k_gemm(const uint8_t *__restrict__ W, int64_t K, int64_t N,
+__global__ void __launch_bounds__(256, 2) k_gemm(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                               const _Float16 *__restrict__ a16, const float *__restrict__ dyg,
                                               const _Float16 *__restrict__ bs16, int64_t M, float *__restrict__ Y,
-                                              int64_t ldy, const float *res, int64_t ldr) {
+                                              int64_t ldy, const float *res, int64_t ldr, const float *__restrict__ sg,
+                                              float *__restrict__ part, int64_t Mp) {
     using T = GemmTraits<TYPE>;
     __shared__ GemmSmem<T::NB> S;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t n0 = (int64_t)blockIdx.x * GB_N, m0 = (int64_t)blockIdx.y * GB_M;
-    const int64_t nsb = K / GB_K;
+    // split-K (gridDim.z > 1): this workgroup's super-block range; partials to part [z][Mp][N], summed in order by
+    // k_splitk_reduce
+    const int64_t nsb_all = K / GB_K, nsb_z = nsb_all / gridDim.z;
+    const int64_t sb0 = (int64_t)blockIdx.z * nsb_z, nsb = sb0 + nsb_z;
     const int64_t G = T::SB ? 256 : 32;
     const int lr = lane & 31, lh = lane >> 5;
     const int64_t arow = m0 + 32 * wave + lr;                  // token row this lane feeds into A
@@ -321,14 +392,26 @@ __global__ void __launch_bounds__(256) k_gemm(const uint8_t *__restrict__ W, int
 #pragma unroll
     for (int i = 0; i < 16; ++i) { tot[0][i] = 0.0f; tot[1][i] = 0.0f; }
 
-    for (int64_t sb = 0; sb < nsb; ++sb) {
+    for (int64_t sb = sb0; sb < nsb; ++sb) {
         __syncthreads();                                        // previous step done with LDS
         stage_weights<TYPE>(S, W, K, N, n0, sb);
+        // K-quants: the super-block's 16 A fragments, issued behind the weight loads (one latency per step, not one
+        // per MFMA pair); per-32 types load theirs per half super-block below (register pressure of 8 epilogues)
+        h8v av[16];
+        if constexpr (T::SB) {
+#pragma unroll
+            for (int s = 0; s < 16; ++s) av[s] = *(const h8v *)(ap + sb * GB_K + 16 * s);
+        }
         if (threadIdx.x < GB_M) {
             if constexpr (T::SB) S.dy[threadIdx.x][0] = dyg[(m0 + threadIdx.x) * (K / 256) + sb];
             else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) S.dy[threadIdx.x][j] = dyg[(m0 + threadIdx.x) * (K / 32) + sb * 8 + j];
+                if constexpr (kGemmM1<TYPE>) {
+                    const bool ok = m0 + threadIdx.x < M;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) S.sy[threadIdx.x][j] = ok ? sg[(m0 + threadIdx.x) * (K / 32) + sb * 8 + j] : 0.0f;
+                }
             }
         }
         __syncthreads();
@@ -336,9 +419,9 @@ __global__ void __launch_bounds__(256) k_gemm(const uint8_t *__restrict__ W, int
             f16acc acc[2], accm[2];
 #pragma unroll
             for (int i = 0; i < 16; ++i) { acc[0][i] = acc[1][i] = 0.0f; accm[0][i] = accm[1][i] = 0.0f; }
-#pragma unroll 4
+#pragma unroll
             for (int s = 0; s < 16; ++s) {
-                const h8v a = *(const h8v *)(ap + sb * GB_K + 16 * s);
+                const h8v a = av[s];
 #pragma unroll
                 for (int tl = 0; tl < 2; ++tl) {
                     acc[tl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, S.bf[0][(tl * 16 + s) * 64 + lane], acc[tl], 0, 0, 0);
@@ -367,15 +450,31 @@ __global__ void __launch_bounds__(256) k_gemm(const uint8_t *__restrict__ W, int
                 }
             }
         } else {
-#pragma unroll 2
-            for (int jb = 0; jb < 8; ++jb) {
+            // Q4_1 / Q5_1: + sum_j m_w[j] s_a[j] over the 8 blocks, an fp32 product of the [tokens x 8] s and
+            // [8 x rows] m tiles on the matrix cores (ggml_vec_dot_q4_1_q8_1 / _q5_1_q8_1, ggml-quants.c:4503,5145)
+            if constexpr (kGemmM1<TYPE>) {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) {
+                    const float a = S.sy[32 * wave + lr][2 * kk + lh];
+#pragma unroll
+                    for (int tl = 0; tl < 2; ++tl)
+                        tot[tl] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, S.wm[tl * 32 + lr][2 * kk + lh], tot[tl], 0, 0, 0);
+                }
+            }
+#pragma unroll 1
+            for (int hb = 0; hb < 2; ++hb) {
+#pragma unroll
+            for (int s = 0; s < 8; ++s) av[s] = *(const h8v *)(ap + sb * GB_K + 128 * hb + 16 * s);
+#pragma unroll
+            for (int jq = 0; jq < 4; ++jq) {
+                const int jb = 4 * hb + jq;
                 f16acc acc[2];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) acc[0][i] = acc[1][i] = 0.0f;
 #pragma unroll
                 for (int ss = 0; ss < 2; ++ss) {
                     const int s = 2 * jb + ss;
-                    const h8v a = *(const h8v *)(ap + sb * GB_K + 16 * s);
+                    const h8v a = av[2 * jq + ss];
 #pragma unroll
                     for (int tl = 0; tl < 2; ++tl)
                         acc[tl] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, S.bf[0][(tl * 16 + s) * 64 + lane], acc[tl], 0, 0, 0);
@@ -391,6 +490,7 @@ __global__ void __launch_bounds__(256) k_gemm(const uint8_t *__restrict__ W, int
                     }
                 }
             }
+            }
         }
     }
     // store (+ residual)
@@ -401,7 +501,8 @@ __global__ void __launch_bounds__(256) k_gemm(const uint8_t *__restrict__ W, int
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int64_t t = m0 + 32 * wave + (r & 3) + 8 * (r >> 2) + 4 * lh;
-            if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[tl][r], res[t * ldr + n]) : tot[tl][r];
+            if (gridDim.z > 1) { if (t < M) part[((int64_t)blockIdx.z * Mp + t) * N + n] = tot[tl][r]; }
+            else if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[tl][r], res[t * ldr + n]) : tot[tl][r];
         }
     }
 }
@@ -1400,7 +1501,8 @@ __global__ void k_silu_mul_strided(float *__restrict__ y, int64_t ldy, const flo
 
 static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a16, int64_t &o_dy, int64_t &o_bs, int64_t &o_up) {
     const int64_t Mp = (M + GB_M - 1) / GB_M * GB_M;
-    const int64_t G = (type == KT_Q4_0 || type == KT_Q5_0 || type == KT_Q8_0) ? 32 : 256;
+    const int64_t G = (type == KT_Q4_0 || type == KT_Q5_0 || type == KT_Q8_0 || type == KT_Q4_1 || type == KT_Q5_1 ||
+                       type == KT_IQ4_NL) ? 32 : 256;
     int64_t off = 0;
     o_a16 = off; off += (Mp * K * 2 + 255) & ~255LL;
     o_dy = off; off += (Mp * (K / G) * 4 + 255) & ~255LL;
@@ -1408,6 +1510,7 @@ static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a
     o_up = off; off += (M * N * 4 + 255) & ~255LL;
     if (type == KT_Q8_0) off += 2 * (int64_t)q80s_splits(K, N) * 32 * N * 4;   // small-M split-K partials (g, u)
     if (type == KT_Q4_K || type == KT_Q4_K_RS || type == KT_Q6_K_RS) off += 2 * Mp * N * 4;   // v3 split-K partials
+    else off += std::min<int64_t>(8 * Mp * N, 1024LL * GB_M * GB_N) * 4;                       // v1 split-K partials
     return off;
 }
 
@@ -1735,10 +1838,12 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     _Float16 *bs16 = (_Float16 *)(w8 + o_bs);
     float *up = (float *)(w8 + o_up);
     const int vt = vec_dot_type(type);
-    if (type == KT_Q4_1 || type == KT_Q5_1 || type == KT_IQ4_NL || type == KT_IQ4_XS) {
-        // the legacy Q8_1-activation types (Q4_1 / Q5_1 files) and the code-book types (IQ4_NL / IQ4_XS): the exact
-        // mat-vec over groups of 8 columns (each group one pass over the weights); their prefill is not on the
-        // BASELINE path
+    const int gv = gemm_variant();
+    if ((type == KT_Q4_1 || type == KT_Q5_1 || type == KT_IQ4_NL || type == KT_IQ4_XS) && (M <= 16 || gv == 20)) {
+        // the legacy Q8_1-activation types (Q4_1 / Q5_1 files) and the code-book types (IQ4_NL / IQ4_XS) at small
+        // batch: the exact mat-vec over groups of 8 columns (one pass over the weights each); past 16 columns the
+        // MFMA GEMM below is faster (tools/gemm_lowbit_ab.py: Q4_1 4096 x 14336 at 16 / 37 / 512 tokens: mat-vec
+        // 52 / 125 / 1592 us, GEMM 67 / 72 / 229 us)
         for (int64_t c0 = 0; c0 < M; c0 += 8) {
             const int rc = gemv_cols(type, W, W2, K, N, act, std::min<int64_t>(8, M - c0), M, c0, Y, ldy, res, ldr, mode,
                                      stream);
@@ -1754,7 +1859,6 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     // (tools/gemm_ab.py) down 14336 x 4096 122.9 -> 112.3 us, attn_v 4096 x 1024 (Q6_K) 56.7 -> 33.9 us, wo 4096 x 4096
     // 43.3 -> 45.6 us (not split), gate|up (big grid) 236.8 -> 273.0 us (not split).
     // kcpp_gemm_set_variant: 2 forces v2, 3 v3 without the split, 4 v3 with the split wherever the mode allows
-    const int gv = gemm_variant();
     const bool v3 = gv == 0 || (gv >= 3 && gv <= 13);
     float *part = (float *)(w8 + o_up + ((M * N * 4 + 255) & ~255LL));
     auto splitk = [&](bool big, int64_t tiles) {
@@ -1911,17 +2015,32 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     hipLaunchKernelGGL(k_act_to_f16, dim3((unsigned)((K + 1023) / 1024), (unsigned)Mp), dim3(256), 0, s,
                        (const uint8_t *)act, vt, K, M, Mp, a16, dy, bs16);
     KCPP_CHECK(hipGetLastError());
-    const dim3 grid((unsigned)((N + GB_N - 1) / GB_N), (unsigned)(Mp / GB_M));
+    // v1 split-K: on grids under 512 workgroups (two per CU) the K range is split (2 .. 8 ways, up to 1024 workgroups;
+    // partials summed in order by k_splitk_reduce): a lone workgroup otherwise walks all of K, one load latency a step
+    const int64_t nwg1 = (N + GB_N - 1) / GB_N * (Mp / GB_M);
+    int KS1 = 1;
+    while (gv != 21 && KS1 < 8 && nwg1 * KS1 * 2 <= 1024 && (K / GB_K) % (KS1 * 2) == 0) KS1 *= 2;
+    const dim3 grid((unsigned)((N + GB_N - 1) / GB_N), (unsigned)(Mp / GB_M), (unsigned)KS1);
+    const float *s81 = vt == KT_Q8_1 ? act_view(vt, act, K, M, 0).s : nullptr;      // block_q8_1.s [M][K/32]
     auto launch = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
         switch (type) {
-        case KT_Q2_K: hipLaunchKernelGGL(k_gemm<KT_Q2_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
-        case KT_Q3_K: hipLaunchKernelGGL(k_gemm<KT_Q3_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
-        case KT_Q4_0: hipLaunchKernelGGL(k_gemm<KT_Q4_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
-        case KT_Q5_0: hipLaunchKernelGGL(k_gemm<KT_Q5_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
-        case KT_Q8_0: hipLaunchKernelGGL(k_gemm<KT_Q8_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr); break;
+        case KT_Q2_K: hipLaunchKernelGGL(k_gemm<KT_Q2_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, nullptr, part, Mp); break;
+        case KT_Q3_K: hipLaunchKernelGGL(k_gemm<KT_Q3_K>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, nullptr, part, Mp); break;
+        case KT_Q4_0: hipLaunchKernelGGL(k_gemm<KT_Q4_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, nullptr, part, Mp); break;
+        case KT_Q5_0: hipLaunchKernelGGL(k_gemm<KT_Q5_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, nullptr, part, Mp); break;
+        case KT_Q8_0: hipLaunchKernelGGL(k_gemm<KT_Q8_0>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, nullptr, part, Mp); break;
+        case KT_Q4_1: hipLaunchKernelGGL(k_gemm<KT_Q4_1>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, s81, part, Mp); break;
+        case KT_Q5_1: hipLaunchKernelGGL(k_gemm<KT_Q5_1>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, s81, part, Mp); break;
+        case KT_IQ4_NL: hipLaunchKernelGGL(k_gemm<KT_IQ4_NL>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, nullptr, part, Mp); break;
+        case KT_IQ4_XS: hipLaunchKernelGGL(k_gemm<KT_IQ4_XS>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, nullptr, part, Mp); break;
         default: return -3;
         }
         KCPP_CHECK(hipGetLastError());
+        if (KS1 > 1) {
+            hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS1, M, Mp, N, y, ly,
+                               r, lr);
+            KCPP_CHECK(hipGetLastError());
+        }
         return 0;
     };
     int rc = launch(W, Y, ldy, mode == 1 ? nullptr : res, ldr);

@@ -9,7 +9,9 @@ make_q2k.py / make_q3k.py / make_legacy32.py / make_iq4.py).
   prefill shapes within 3e-6 of the output scale (a different fp32 summation order than ggml_vec_dot_q3_K_q8_K);
 * GPU: the SoA device layout round-trips and dequantizes bit-exactly; the generic mat-vec (kcpp_gemv), the fused
   decode mat-vec (kcpp_gemv_dec: plain + residual, SiLU-GLU, rms_norm prologue) and the MFMA GEMM (exact integer
-  f16 operands: Q3_K (sc - 32)(v - 4), Q2_K (sc & 15) q with the mins through the bsum MFMA, Q5_0 (q | h << 4) - 16) against the golden and
+  f16 operands: Q3_K (sc - 32)(v - 4), Q2_K (sc & 15) q with the mins through the bsum MFMA, Q5_0 (q | h << 4) - 16,
+  Q4_1 / Q5_1 q (| h << 4) with the m_w s_a term as an fp32 MFMA over the block scales, IQ4_NL code-book values, IQ4_XS
+  (ls - 32) kv split over two planes; past 16 tokens) against the golden and
   the oracle at 3e-6; a tiny Llama under the Q3_K_M / Q2_K / Q5_0 policy end to end (prefill + teacher-forced decode, graph
   and eager) within 1.5x the reference's AVX2-vs-scalar spread."""
 import os
