@@ -267,6 +267,37 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits,
     return 0;
 }
 
+/* context shift between the prompt and the decode (env REF_KSHIFT="p0 diff", koboldcpp PurgeMissingTokens,
+   gpttype_adapter.cpp:1504-1571): llama_kv_cache_seq_rm(p0, p0 + diff) + seq_add(p0 + diff, n_past, -diff), then
+   build_k_shift (src/llama.cpp:10144-10190): ggml_rope_ext_inplace on the F16 K cache of the moved cells with
+   position -diff.  The reference leaves the moved cells where they are and masks the erased ones; here the cells
+   are compacted (rows [p0 + diff, n_past) -> [p0, n_past - diff), K through the same rope op), which the
+   attention sees identically up to the order it visits keys.  F16 caches only. */
+static int kv_shift(model_t *m, int p0, int diff, int n_past) {
+    cfg_t *c = &m->c;
+    const int D = c->n_embd / c->n_head, HKV = c->n_head_kv, EKV = HKV * D, n = n_past - p0 - diff;
+    if (g_tk != GGML_TYPE_F16 || g_tv != GGML_TYPE_F16 || p0 < 0 || diff <= 0 || n < 0) return -1;
+    if (n == 0) return 0;
+    struct ggml_init_params ip = {(size_t)n * EKV * 16 + (1 << 20), NULL, false};
+    for (int il = 0; il < c->n_layer; ++il) {
+        struct ggml_context *ctx = ggml_init(ip);
+        struct ggml_tensor *k = ggml_new_tensor_3d(ctx, GGML_TYPE_F16, D, HKV, n);
+        struct ggml_tensor *pos = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, n);
+        memcpy(k->data, (const uint8_t *)m->kc[il]->data + (size_t)(p0 + diff) * EKV * 2, (size_t)n * EKV * 2);
+        for (int i = 0; i < n; ++i) ((int32_t *)pos->data)[i] = -diff;
+        struct ggml_tensor *r = ggml_rope_ext_inplace(ctx, k, pos, NULL, D, 0, c->n_ctx, c->rope_base, c->rope_freq_scale,
+                                                      0.0f, 1.0f, 32.0f, 1.0f);
+        struct ggml_cgraph *gf = ggml_new_graph(ctx);
+        ggml_build_forward_expand(gf, r);
+        if (ggml_graph_compute_with_ctx(ctx, gf, c->nthreads) != GGML_STATUS_SUCCESS) { ggml_free(ctx); return -2; }
+        memcpy((uint8_t *)m->kc[il]->data + (size_t)p0 * EKV * 2, r->data, (size_t)n * EKV * 2);
+        memmove((uint8_t *)m->vc[il]->data + (size_t)p0 * EKV * 2, (const uint8_t *)m->vc[il]->data + (size_t)(p0 + diff) * EKV * 2,
+                (size_t)n * EKV * 2);
+        ggml_free(ctx);
+    }
+    return 0;
+}
+
 static int argmax(const float *x, int n) {
     int b = 0;
     for (int i = 1; i < n; ++i) if (x[i] > x[b]) b = i;
@@ -314,6 +345,12 @@ static int run_llama(const char *cfgpath) {
     double t_pp = now_s() - tp0;
     fwrite(logits, sizeof(float), c->n_vocab, out);
     int tok = argmax(logits, c->n_vocab);
+    const char *ks = getenv("REF_KSHIFT");
+    if (ks && *ks) {
+        int sp0 = 0, sdiff = 0;
+        if (sscanf(ks, "%d %d", &sp0, &sdiff) != 2 || kv_shift(&m, sp0, sdiff, n_past)) return 6;
+        n_past -= sdiff;
+    }
     double tg0 = now_s();
     for (int g = 0; g < c->n_gen; ++g) {
         if (g < c->n_forced) tok = c->forced[g];

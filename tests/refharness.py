@@ -209,14 +209,16 @@ def ref_available():
 
 
 def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeout=600, forced=None, hidden=False,
-                  binary=None, skip_prefix=0):
+                  binary=None, skip_prefix=0, kshift=None):
     """Run the reference ggml graph; returns (logits [1+n_gen, V], info dict).
     forced: decode these tokens (teacher forcing) instead of the greedy argmax.
     hidden: also return info["hidden"] = residual stream after layers 0..n_layer-2 of the prefill,
             [n_layer-1][n_prompt][n_embd] (single-ubatch prompts); MoE: info["router"] = those layers' router
             logits [n_layer-1][n_prompt][n_expert].
     binary: ref_llama build to run (default: the AVX2 build; REF_BIN_SCALAR for the scalar one).
-    skip_prefix: the first skip_prefix prompt positions are taken as cached (zeroed K/V), not computed (timing only)."""
+    skip_prefix: the first skip_prefix prompt positions are taken as cached (zeroed K/V), not computed (timing only).
+    kshift: (p0, diff) -- context shift after the prompt (the reference's seq_rm / seq_add + build_k_shift), the
+            decode then continues at n_prompt - diff."""
     import json
     with tempfile.TemporaryDirectory() as td:
         cfg = os.path.join(td, "cfg.txt")
@@ -234,7 +236,8 @@ def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeou
             if hidden:
                 f.write(hout + "\n")
         r = subprocess.run([binary or REF_BIN, "llama", cfg], capture_output=True, text=True, timeout=timeout,
-                           env=dict(os.environ, OMP_NUM_THREADS=str(nthreads), REF_SKIP_PREFIX=str(skip_prefix)))
+                           env=dict(os.environ, OMP_NUM_THREADS=str(nthreads), REF_SKIP_PREFIX=str(skip_prefix),
+                                    REF_KSHIFT="%d %d" % tuple(kshift) if kshift else ""))
         if r.returncode != 0:
             raise RuntimeError("ref_llama failed: %s %s" % (r.returncode, r.stderr))
         info = json.loads(r.stdout.strip().splitlines()[-1])

@@ -5,7 +5,9 @@ their K is re-rotated by the shift distance (ggml_compute_forward_rope_f16, mode
 * kernel: kcpp_kv_shift_rows vs a numpy restatement of rope_f16 with the library's own (cos, sin) row -- bit-exact;
 * runtime (one layer, whose K/V rows depend only on their own tokens): prefill A, shift out a span, decode new
   tokens  vs  prefill the shortened context from scratch -- equal up to the K-shift's extra f16 rounding;
-* drop-in ABI: load_model(use_contextshift) + generate() with a prompt whose middle was cut runs the shift path."""
+* drop-in ABI: load_model(use_contextshift) + generate() with a prompt whose middle was cut runs the shift path;
+* against the reference: the K-shift kernel bit for bit vs build_k_shift's rope (tests/golden/kshift.npz), and a
+  2-layer model's decode on the shifted cache vs the reference's logits (tests/golden/kshift_e2e.npz)."""
 import ctypes
 
 import numpy as np
@@ -172,3 +174,38 @@ def test_kv_shift_rows_vs_reference_k_shift(env, base, diff):
     torch.cuda.synchronize()
     got = ks.cpu().numpy().astype(np.uint16)
     assert np.array_equal(got, fx["k_shift_%d_%d" % (base, diff)])
+
+
+@pytest.mark.parametrize("strict", [False, True], ids=["production", "strict"])
+def test_model_kv_shift_vs_reference_logits(env, strict):
+    """context shift end to end against the REFERENCE: a 2-layer tiny Llama (Q4_K_M policy) prefills 150 tokens,
+    45 cells after the first 20 are erased (kcpp_model_kv_shift  vs  the reference's seq_rm / seq_add +
+    build_k_shift, run by oracle/ref_llama.c on its own graph: tests/golden/make_kshift_e2e.py) and 8 teacher-forced
+    tokens are decoded on the shifted cache.  Bars: with the strict-parity attention every step
+    within 1.5x this fixture's AVX2-vs-scalar spread; with the production attention (f32 V*P accumulator) the tiny
+    e2e bar of test_gpu_model (TOL_MAX / TOL_MEDIAN_F32).  The shift moves the logits by up to 1.6, so a missing or
+    wrong shift fails either bar."""
+    import os
+    torch, K = env
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kshift_e2e.npz"))
+    p0, diff = (int(v) for v in g["shift"])
+    prompt = [int(v) for v in g["prompt"]]
+    m = K.Model(R.TINY, [int(t) for t in g["types"]])
+    m.synth(1234)
+    m.set_fa_exact(strict)
+    out = [m.decode(prompt, 0)]
+    m.kv_shift(p0, diff, len(prompt))
+    n = len(prompt) - diff
+    for tok in g["forced"]:
+        out.append(m.decode([int(tok)], n))
+        n += 1
+    m.close()
+    d = np.abs(np.array(out) - g["logits"])
+    print("gpu vs ref max", d.max(axis=1), "| spread", g["spread_max"])
+    if strict:
+        assert np.all(d.max(axis=1) <= 1.5 * g["spread_max"].max())
+        assert np.all(np.median(d, axis=1) <= 1.5 * g["spread_median"].max())
+    else:
+        assert np.all(d.max(axis=1) <= TOL_MAX) and np.all(np.median(d, axis=1) <= TOL_MEDIAN_F32)
+    # and not the unshifted continuation
+    assert np.abs(np.array(out)[1:] - g["noshift_logits"][1:]).max() > 10 * g["spread_max"].max()
