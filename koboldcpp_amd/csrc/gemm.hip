@@ -1861,9 +1861,11 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     // kcpp_gemm_set_variant: 2 forces v2, 3 v3 without the split, 4 v3 with the split wherever the mode allows
     const bool v3 = gv == 0 || (gv >= 3 && gv <= 13);
     float *part = (float *)(w8 + o_up + ((M * N * 4 + 255) & ~255LL));
-    auto splitk = [&](bool big, int64_t tiles) {
+    // (the rule reads the weight shape only -- "< 128 tiles" as counted at the 512-token ubatch, 64 x 128 tiles --
+    // so a prompt's bits do not depend on how it is cut into ubatches)
+    auto splitk = [&](bool big, int64_t) {
         if (mode != 0 || (K / 256) % 2) return 1;
-        return (gv == 4 || (gv == 0 && !big && (tiles < 128 || K / 256 >= 32))) ? 2 : 1;
+        return (gv == 4 || (gv == 0 && !big && ((N + 127) / 128 < 16 || K / 256 >= 32))) ? 2 : 1;
     };
     const bool bs_aligned = ((uintptr_t)((const uint8_t *)act + M * K + M * (K / 256) * 4) & 15) == 0;
     // v4 for every Q4_K shape past the small-batch range (tools/gemm_ab.py, M = 512, v3 -> v4): gate|up 28672 rows
@@ -1876,7 +1878,10 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         // grid is small
         const int64_t nt = (N + 127) / 128;
         const int MT = (int)(Mp / 128);
-        const int KS = (gv != 13 && mode == 0 && (K / 256) % 2 == 0 && MT * nt <= 128) ? 2 : 1;
+        // the split is chosen from the weight shape alone (<= 128 tiles at the 512-token ubatch, i.e. <= 32 row
+        // tiles), never from M: the split changes the f32 summation order, and a prompt must give the same bits
+        // however it is cut into ubatches (tests/test_gpu_fullsize.py)
+        const int KS = (gv != 13 && mode == 0 && (K / 256) % 2 == 0 && nt <= 32) ? 2 : 1;
         const unsigned nwg = (unsigned)(MT * nt * KS);
         const int XG = gv == 12 ? 2 : 1;
         auto launch4 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {

@@ -17,9 +17,13 @@ WORDS = GW.WORDS
 
 
 def piece(toks, types, t):
+    """llama_token_to_piece_impl with special=false (src/llama-vocab.cpp:2014-2064, SPM): UNKNOWN / CONTROL
+    are suppressed, UNUSED falls through to an empty piece, USER_DEFINED is copied raw."""
     s = toks[t]
-    if types[t] in (3, 4):
+    if types[t] in (2, 3, 5):
         return b""
+    if types[t] == 4:
+        return s.encode()
     if types[t] == 6:
         return bytes([int(s[3:5], 16)])
     return s.replace("▁", " ").encode()
@@ -169,7 +173,9 @@ def test_moe_gguf_generate_matches_runtime(model, tmp_path, split):
 
 def test_greedy_respects_logit_bias(model):
     """Greedy with a logit bias: the reference adds biases before any sampler (gpttype_adapter.cpp:1349-1353),
-    token ids >= 0 accepted (:2576-2584), so banning the unbiased greedy token changes the first pick."""
+    token ids >= 0 accepted (:2576-2584).  Checked on tokens with visible pieces (the random weights may pick an
+    unused token, whose piece is empty): a +1000 bias forces its token, a ban beside another +1000 moves the pick,
+    and token 0 (<unk>, empty piece) at +1000 beats a visible token at +999."""
     h, X, toks, ttypes, _ = model
     gi = X.generation_inputs()
     gi.prompt = b"hello world"
@@ -180,18 +186,19 @@ def test_greedy_respects_logit_bias(model):
     gi.rep_pen = 1.0
     gi.bypass_eos_token = True
     gi.seed = 3
-    base = h.generate(gi).text
-    r = h.token_count(b"hello world", True)
-    ids = [r.ids[i] for i in range(r.count)]
-    first = [t for t in range(len(toks)) if piece(toks, ttypes, t) == base and base]
-    assert first, base
-    gi.logit_biases[0].token_id = first[0]
+    vis = [t for t in range(len(toks)) if ttypes[t] == 1 and piece(toks, ttypes, t)]
+    v, w = vis[3], vis[7]
+    gi.logit_biases[0].token_id = v
+    gi.logit_biases[0].bias = 1000.0
+    assert h.generate(gi).text == piece(toks, ttypes, v)
     gi.logit_biases[0].bias = -1000.0
-    biased = h.generate(gi).text
-    assert biased != base
+    gi.logit_biases[1].token_id = w
+    gi.logit_biases[1].bias = 1000.0
+    assert h.generate(gi).text == piece(toks, ttypes, w)
     gi.logit_biases[0].token_id = 0                       # token 0 may be biased too (>= 0)
     gi.logit_biases[0].bias = 1000.0
-    assert h.generate(gi).text == piece(toks, ttypes, 0)
+    gi.logit_biases[1].bias = 999.0
+    assert h.generate(gi).text == piece(toks, ttypes, 0) == b""
 
 
 def test_long_context_decode_matches_short_context():
