@@ -11,7 +11,8 @@
 
 namespace lean {
 
-template <int PRO, int MAXC>
+// NT threads per workgroup (MAXC = 16-element chunks per thread: ceil(K / (16 NT)))
+template <int PRO, int MAXC, int NT = 256>
 struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_impl.h); loads first
     float v[MAXC][16];
     float w[PRO == 1 ? MAXC : 1][16];
@@ -19,7 +20,7 @@ struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_imp
         const int tid = threadIdx.x, nchunk = (int)(a.K / 16);
 #pragma unroll
         for (int i = 0; i < MAXC; ++i) {
-            const int c = min(tid + 256 * i, nchunk - 1);
+            const int c = min(tid + NT * i, nchunk - 1);
             const float4 *p = (const float4 *)(a.x + 16 * (int64_t)c);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -51,17 +52,19 @@ struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_imp
             double ss = 0.0;
 #pragma unroll
             for (int i = 0; i < MAXC; ++i)
-                if (tid + 256 * i < nchunk) {
+                if (tid + NT * i < nchunk) {
 #pragma unroll
                     for (int e = 0; e < 16; ++e) ss += (double)__fmul_rn(v[i][e], v[i][e]);
                 }
             ss = wave_sum_d(ss);
             LP_STAMP(9);
-            __shared__ double red[4];
+            __shared__ double red[NT / 64];
             if ((tid & 63) == 0) red[tid >> 6] = ss;
             __syncthreads();
             LP_STAMP(10);
-            const double sum = red[0] + red[1] + red[2] + red[3];
+            double sum = red[0] + red[1] + red[2] + red[3];
+#pragma unroll
+            for (int i = 4; i < NT / 64; i += 4) sum += red[i] + red[i + 1] + red[i + 2] + red[i + 3];
             const float scale = 1.0f / sqrtf((float)(sum / (double)K) + a.eps);   // ggml.c:12089
 #pragma unroll
             for (int i = 0; i < MAXC; ++i)
@@ -74,13 +77,13 @@ struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_imp
 #ifndef KCPP_PROBE_NOQUANT
 #pragma unroll
         for (int i = 0; i < MAXC; ++i) {
-            const int c = tid + 256 * i;
+            const int c = tid + NT * i;
             if (c < nchunk) q8k_quant16(v[i], c & 15, qs + (c >> 4) * 256, d + (c >> 4), bs + (c >> 4) * 16);
         }
 #else   // timing probe only (wrong results, finite: an all-zero activation): the prologue without its quantization
 #pragma unroll
         for (int i = 0; i < MAXC; ++i) {
-            const int c = tid + 256 * i;
+            const int c = tid + NT * i;
             if (c < nchunk) {
                 *(uint4 *)(qs + 16 * c) = make_uint4(v[i][0] == 1234.5f, 0, 0, 0);
                 if ((c & 15) == 0) d[c >> 4] = 0.0f;

@@ -49,8 +49,9 @@ using namespace rs;
 // NI = pieces per lane per row (ceil(nsb * PIECES_PER_SB / 64)); R rows per group (x2 for gate|up);
 // PRO 0: act copy, 1: rms_norm * w -> Q8_K, 2: quantize only; MC = ceil(K / 4096) prologue chunks;
 // PF: issue the next group's loads before reducing the current one.
-template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF>
-__global__ void __launch_bounds__(256) k_gemv_rs(const DecArgs a) {
+// NWV waves per workgroup (4, or 8: one activation prologue shared by twice the waves)
+template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4>
+__global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     using T = RS<TYPE>;
     constexpr int RR = MODE == 1 ? 2 * R : R;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -75,8 +76,8 @@ __global__ void __launch_bounds__(256) k_gemv_rs(const DecArgs a) {
     const int npieces = nsb * T::PIECES_PER_SB;
     const int N0 = (int)a.N[0], N1 = a.nseg > 1 ? (int)a.N[1] : 0, N2 = a.nseg > 2 ? (int)a.N[2] : 0;
     const int ngroups = (N0 + N1 + N2) / R;
-    const int nw = (int)gridDim.x * 4;
-    const int wid = (int)blockIdx.x * 4 + wave;
+    const int nw = (int)gridDim.x * NWV;
+    const int wid = (int)blockIdx.x * NWV + wave;
     const int64_t eoff = a.eid ? (int64_t)__builtin_amdgcn_readfirstlane(a.eid[0]) * a.ebytes : 0;   // MoE slice
     const int abytes = K + K / 256 * 4 + K / 16 * 2;
     const typename T::Lane lc = T::lane_consts(lane);
@@ -102,7 +103,7 @@ __global__ void __launch_bounds__(256) k_gemv_rs(const DecArgs a) {
     Buf ba, bb;
     const int g0 = min(wid, ngroups - 1);
     if constexpr (PRO != 0) {
-        lean::ActPro<PRO, MC> pro;
+        lean::ActPro<PRO, (MC * 4 + NWV - 1) / NWV, 64 * NWV> pro;
         pro.load(a);
         issue(g0, ba);
 #ifdef KCPP_STAMPS
@@ -181,7 +182,7 @@ __global__ void __launch_bounds__(256) k_gemv_rs(const DecArgs a) {
 }
 
 namespace {
-template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF>
+template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4>
 int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
     int64_t ntot = 0;
     for (int i = 0; i < a.nseg; ++i) {
@@ -189,11 +190,11 @@ int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
         ntot += a.N[i];
     }
     const int64_t groups = ntot / R;
-    int64_t nblk = std::min<int64_t>((groups + 3) / 4, max_blocks);
-    nblk = std::max<int64_t>(nblk, (groups + 255) / 256);    // <= 64 groups per wave (result slots)
+    int64_t nblk = std::min<int64_t>((groups + NWV - 1) / NWV, max_blocks);
+    nblk = std::max<int64_t>(nblk, (groups + 64 * NWV - 1) / (64 * NWV));    // <= 64 groups per wave (result slots)
     const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
-    hipLaunchKernelGGL((k_gemv_rs<TYPE, NI, R, MODE, PRO, MC, PF>), dim3((unsigned)nblk), dim3(256), (size_t)abytes + 16, s,
-                       a);
+    hipLaunchKernelGGL((k_gemv_rs<TYPE, NI, R, MODE, PRO, MC, PF, NWV>), dim3((unsigned)nblk), dim3(64 * NWV),
+                       (size_t)abytes + 16, s, a);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }
@@ -214,6 +215,13 @@ int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
     else if (ntot > 16384) { R = 2; B = 512; }
     else if (a.K > 8192) { PF = TYPE == KT_Q4_K_RS; B = TYPE == KT_Q4_K_RS ? 256 : 512; }
     else if (pro == 2) B = 512;          // wo with its quantize prologue (every workgroup quantizes the input)
+    // 8-wave workgroups, one per CU (one activation prologue shared by 8 waves instead of 4), measured per kernel in
+    // isolation (tools/stream_probe.py dec, weights rotated past the Infinity Cache): GLU 14.8 -> 14.1 us (PF),
+    // down Q4_K 11.3 -> 9.7 and Q6_K 13.6 -> 12.2 (no PF: two rows per wave, both in flight), wo 5.4 -> 4.7; in the
+    // bench's token graph down 12.0 / 13.7 -> 10.0 / 12.4 us, wo 5.3 -> 5.1, GLU unchanged: 577 -> 600 tok/s.  The
+    // q|k|v launches stay at 4 waves (8: 6.8 -> 7.4 us, 592 tok/s).
+    if (mode == 1 && pro == 1 && R == 1) return launch_rs<TYPE, NI, 1, 1, 1, MC, 1, 8>(a, 256, s);
+    if (mode == 0 && pro == 2 && R == 1 && ntot <= 16384) return launch_rs<TYPE, NI, 1, 0, 2, MC, 0, 8>(a, 256, s);
 #define KCPP_RS_P(PRO_)                                                                                             \
     if (pro == PRO_) {                                                                                              \
         if (mode == 1) return PF ? launch_rs<TYPE, NI, 1, 1, PRO_, MC, 1>(a, B, s) : launch_rs<TYPE, NI, 1, 1, PRO_, MC, 0>(a, B, s); \

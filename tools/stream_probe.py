@@ -107,6 +107,7 @@ def dec():
         ("wo q4k pro0 r4", 12, E, E, 0, 0, 4),
         ("down q4k pro0 r2", 12, F, E, 0, 0, 2),
         ("rs wo q4k pro0", 112, E, E, 0, 0, 1),
+        ("rs wo q4k pro2", 112, E, E, 0, 2, 1),
         ("rs qkv q4k pro1 rope", 112, E, E + 2048, 2, 1, 2),
         ("rs glu q4k pro1", 112, E, F, 1, 1, 1),
         ("rs down q4k pro2", 112, F, E, 0, 2, 1),
