@@ -97,7 +97,7 @@ def measure_roofline(K, torch, iters=64, pairs=8):
     traffic, tsrc = pmc_traffic()
     return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-            "kernel": "kcpp_gemv_dec -> k_gemv_rs<Q4_K_RS,NI2,R1,GLU,norm+quant prologue,PF> 4096x(2x14336)", "bytes_per_launch": alg,
+            "kernel": "kcpp_gemv_dec -> k_gemv_rs<Q4_K_RS,NI2,R1,GLU,norm+quant prologue,PF,8 waves> 4096x(2x14336)", "bytes_per_launch": alg,
             "avg_us": round(ms * 1e3, 2)}
 
 
