@@ -237,8 +237,12 @@ def main():
                     choices=["llama3-8b-q4_k_m", "llama3-8b-q8_0-b32", "mixtral-8x7b-q5_k_m"],
                     help="BASELINE configs[1] (default: the driver's line), configs[2], configs[4]")
     ap.add_argument("--layers", type=int, default=None, help="override n_layer (debug only; invalidates metric)")
+    ap.add_argument("--engine", type=int, default=None,
+                    help="1: single-token decode through the persistent engine (dec_engine.hip), 0: the launch chain")
     args = ap.parse_args()
 
+    if args.engine is not None:
+        os.environ["KCPP_ENGINE"] = str(args.engine)
     import torch
     import koboldcpp_amd.lib as K
 

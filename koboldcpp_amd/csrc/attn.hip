@@ -634,28 +634,6 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     return 0;
 }
 
-// the combine of the fused q|k|v + attention launch (dec_fused.hip): partials behind FA_WS_TICKETS in ws, split count
-// kcpp_fa_dec_splits(HKV)
-int kcpp_fa_dec_splits(int HKV) { return fa4_splits(HKV); }
-int kcpp_fa_comb_fused(void *ws, float *out, int H, int HKV, void *stream) {
-    hipStream_t s = (hipStream_t)stream;
-    const int NS = fa4_splits(HKV);
-    float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
-    float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
-    switch (NS) {
-#define KCPP_COMB(N_)                                                                                          \
-    case N_:                                                                                                   \
-        hipLaunchKernelGGL((k_fa_comb4<false, N_>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, \
-                           (unsigned long long *)nullptr, (unsigned *)nullptr);                                \
-        break;
-        KCPP_COMB(4) KCPP_COMB(8) KCPP_COMB(16) KCPP_COMB(32) KCPP_COMB(64)
-#undef KCPP_COMB
-    default: return -1;
-    }
-    KCPP_CHECK(hipGetLastError());
-    return 0;
-}
-
 // single-token decode attention with explicit cache strides (elements): key p of kv head hk starts at
 // kc + p * kv_ld + hk * kv_hs.  Position-major ggml view: kv_ld = HKV*D, kv_hs = D; head-major: kv_ld = D,
 // kv_hs = n_ctx*D.  variant 0: 64-key chunks + k_fa_combine; 3: k_fa_dec4 + k_fa_comb4 (the production kernel

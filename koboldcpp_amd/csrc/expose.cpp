@@ -20,6 +20,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <deque>
+#include <map>
 #include <ctime>
 #include <cmath>
 #include <cstdio>
@@ -118,6 +120,25 @@ bool supported_type(int t) {
            t == KT_IQ4_NL || t == KT_IQ4_XS ||
            t == KT_Q6_K;
 }
+
+}  // namespace
+
+// CalcGradientAIRopeFreqBase (gpttype_adapter.cpp:1598-1640): the RoPE base for a context beyond the trained one,
+// float arithmetic as the reference's (log10f / powf); solar = GGUFArch::ARCH_SOLAR (context x 8, positive offset)
+extern "C" float kcpp_gradient_ai_rope_base(float original_rope_base, int n_ctx_train, int n_ctx_desired, int solar) {
+    if (n_ctx_desired <= n_ctx_train || n_ctx_desired <= 2048) return original_rope_base;
+    const float ctx_multiplier = solar ? 8.0f : 1.0f;
+    const float chi_ctx_train_value = (n_ctx_train * ctx_multiplier) / 6.28318;
+    const float chi_ctx_value = (n_ctx_desired * ctx_multiplier) / 6.28318;
+    const float gradient_ai_rope_freq_base_value = powf(original_rope_base, log10f(chi_ctx_value) / log10f(chi_ctx_train_value));
+    if (!solar) return gradient_ai_rope_freq_base_value;
+    const float extended_rope_positive_offset_value =
+        1 + ((log10f(chi_ctx_value) - log10f(chi_ctx_train_value)) /
+             ((log10f(chi_ctx_value) * log10f(chi_ctx_train_value)) - (log10f(chi_ctx_value) + log10f(chi_ctx_train_value))));
+    return gradient_ai_rope_freq_base_value * extended_rope_positive_offset_value;
+}
+
+namespace {
 
 // layer -> device (src/llama.cpp:7010-7036, all layers offloaded)
 std::vector<int> split_layers(int n_layer, int n_dev, const float *ts) {
@@ -261,6 +282,8 @@ struct SamplerSetup {
     std::vector<ksamp::LogitBias> biases;
     ksamp::RestartSeqs restarts;
     std::vector<int> banned;
+    std::vector<std::string> phrases;      // antislop: banned multi-token phrases (lower case)
+    int delay = 0;                         // delayed_generated_tokens_limit: tokens held back before streaming
     int n_ctx = 0;
     bool suppress_eos = false;
 };
@@ -333,11 +356,20 @@ SamplerSetup make_sampler(const Engine &e, const generation_inputs &in, int n_ct
             overlapping_sequences(e, w, S.restarts, 20);
         }
     }
+    // token bans and antislop phrases (gpttype_adapter.cpp:2514-2545): a single-character entry that is one token bans
+    // every vocabulary entry containing it; anything longer is a phrase, caught after sampling by the delayed-output
+    // rewind in generate(); the output is held back by the longest phrase's token count + 3
     std::vector<std::string> single;
     for (int x = 0; x < KCPP_BAN_TOKEN_MAX; ++x) {
         if (!in.banned_tokens[x] || !in.banned_tokens[x][0]) continue;
         const std::string w = lower(in.banned_tokens[x]);
-        if (e.tok.encode(w, false).size() == 1 && w.length() < 2) single.push_back(w);   // phrases (antislop): not provided
+        const int tokcount = (int)e.tok.encode(w, false).size();
+        if (tokcount == 0) continue;
+        if (tokcount == 1 && w.length() < 2) single.push_back(w);
+        else {
+            S.delay = std::max(S.delay, tokcount + 3);
+            S.phrases.push_back(w);
+        }
     }
     if (!single.empty())
         for (int v = 0; v < nv; ++v) {
@@ -363,11 +395,13 @@ bool chain_is_argmax(const SamplerSetup &S) {
     return (has_topk && (int)P.top_k == 1) || (has_temp && P.temp <= 0 && P.dynatemp_range <= 0);
 }
 
-// one sampled token from the last stage's logits (gpttype_adapter.cpp:3182-3232); < 0 on a device error
-int sample(Engine &e, const SamplerSetup &S, const std::vector<int> &last_n, std::mt19937 &rng, float *mu) {
+// one sampled token from the last stage's logits (gpttype_adapter.cpp:3182-3232); < 0 on a device error.
+// slop: the antislop bans recorded for this position (set to the lowest logit like the token bans, :3219-3225)
+int sample(Engine &e, const SamplerSetup &S, const std::vector<int> &last_n, std::mt19937 &rng, float *mu,
+           const std::vector<int> *slop) {
     kcpp_model *last = e.stages.back();
     const int eos = e.tok.eos(), eot = e.tok.eot();
-    if (chain_is_argmax(S)) {
+    if (chain_is_argmax(S) && !slop) {
         int32_t t = 0;
         if (kcpp_model_argmax(last, &t)) return -1;
         if (!(S.suppress_eos && (t == eos || (t == eot && eot != -1)))) return t;
@@ -380,6 +414,9 @@ int sample(Engine &e, const SamplerSetup &S, const std::vector<int> &last_n, std
     if (S.suppress_eos && eos >= 0 && eos < e.hp.n_vocab) l[eos] = low;
     if (S.suppress_eos && eot >= 0 && eot < e.hp.n_vocab) l[eot] = low;
     for (int b : S.banned) l[b] = low;
+    if (slop)
+        for (int b : *slop)
+            if (b >= 0 && b < e.hp.n_vocab) l[b] = low;
     return ksamp::sample_logits(l, S.n_ctx, e.hp.n_vocab, S.P, S.biases, S.restarts, e.ctx, last_n, rng, mu);
 }
 
@@ -479,9 +516,30 @@ bool load_model(const load_model_inputs inputs) {
     hp.n_head = (int)f.get_i("llama.attention.head_count", 0);
     hp.n_head_kv = (int)f.get_i("llama.attention.head_count_kv", hp.n_head);
     hp.eps = (float)f.get_f("llama.attention.layer_norm_rms_epsilon", 1e-5);
-    const bool user_rope = inputs.rope_freq_base > 0 && (inputs.rope_freq_base != 10000.0f || inputs.rope_freq_scale != 1.0f);
-    hp.rope_base = user_rope ? inputs.rope_freq_base : (float)f.get_f("llama.rope.freq_base", 10000.0);
-    hp.rope_freq_scale = user_rope && inputs.rope_freq_scale > 0 ? inputs.rope_freq_scale : 1.0f;
+    // RoPE (gpttype_adapter.cpp:1677-1700, 1926-1950): a user --ropeconfig (rope_freq_scale > 0) wins; a model that
+    // sets its own RoPE (freq_base not 10000 / 500000, a linear scale, or YaRN) keeps its values; otherwise the base
+    // is auto-scaled for the requested context by the GradientAI rule (CalcGradientAIRopeFreqBase)
+    const float base_train = (float)f.get_f("llama.rope.freq_base", 10000.0);
+    float ropescale = (float)f.get_f("llama.rope.scaling.factor", 0.0);
+    if (ropescale == 0.0f) ropescale = (float)f.get_f("llama.rope.scale_linear", 0.0);
+    const float scale_train = ropescale == 0.0f ? 1.0f : 1.0f / ropescale;
+    if (f.get_s("llama.rope.scaling.type", "") == "yarn") {
+        fprintf(stderr, "[kcpp] load_model: YaRN rope scaling is not supported\n");
+        return false;
+    }
+    const int n_ctx_train = (int)f.get_i("llama.context_length", 2048);     // FileFormatExtraMeta default
+    // ARCH_SOLAR (model_adapter.cpp:309): llama, freq_base 10000, 435 or 611 tensors
+    const bool solar = base_train == 10000.0f && (f.tensors.size() == 435 || f.tensors.size() == 611);
+    if (inputs.rope_freq_scale > 0.0f) {
+        hp.rope_base = inputs.rope_freq_base;
+        hp.rope_freq_scale = inputs.rope_freq_scale;
+    } else if ((base_train != 10000.0f && base_train != 500000.0f) || scale_train != 1.0f) {
+        hp.rope_base = base_train;
+        hp.rope_freq_scale = scale_train;
+    } else {
+        hp.rope_base = kcpp_gradient_ai_rope_base(base_train, n_ctx_train, inputs.max_context_length, solar);
+        hp.rope_freq_scale = 1.0f;
+    }
     hp.n_ctx = inputs.max_context_length > 0 ? inputs.max_context_length + 8 : 2048 + 8;
     if (hp.n_layer <= 0 || hp.n_head <= 0 || (hp.n_embd / hp.n_head != 128 && hp.n_embd / hp.n_head != 64)) {
         fprintf(stderr, "[kcpp] load_model: need head_dim 128 or 64 (got n_embd %d / n_head %d)\n", hp.n_embd, hp.n_head);
@@ -549,6 +607,26 @@ bool load_model(const load_model_inputs inputs) {
         }
         e->types[k] = ts[k].type;
     }
+    // n_gpu_layers (src/llama.cpp:6977-7036: layers [0, n_layer - n_gpu_layers) stay on the CPU backend): this backend
+    // has no CPU compute path, so a partial offload is refused instead of silently becoming a full one; negative
+    // (koboldcpp's auto) and >= n_layer offload everything (the output head, which the reference keeps on the CPU
+    // for n_gpu_layers == n_layer, runs here on the last GPU)
+    if (inputs.gpulayers >= 0 && inputs.gpulayers < hp.n_layer) {
+        fprintf(stderr, "[kcpp] load_model: gpulayers %d < %d layers: partial offload (CPU layers) is not supported by "
+                        "this backend; use gpulayers >= %d (or -1)\n", inputs.gpulayers, hp.n_layer, hp.n_layer);
+        return false;
+    }
+    // rope_freqs.weight (Llama-3.1 / 3.2: src/llama.cpp:7171, one tensor shared by every layer's rope,
+    // build_rope_factors :10269), n_rot / 2 F32 frequency factors
+    std::vector<float> rope_ff;
+    if (const gguf::Tensor *rf = f.tensor("rope_freqs.weight")) {
+        const int nff = (hp.n_embd / hp.n_head) / 2;
+        if (rf->type != KT_F32 || rf->ne[0] != nff || rf->ne[1] * rf->ne[2] * rf->ne[3] != 1) {
+            fprintf(stderr, "[kcpp] load_model: rope_freqs.weight: expected %d F32 values\n", nff);
+            return false;
+        }
+        rope_ff.assign((const float *)rf->data, (const float *)rf->data + nff);
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) { fprintf(stderr, "[kcpp] load_model: no GPU\n"); return false; }
     // test hook: KCPP_VIRTUAL_DEVICES=n splits the layers as if n GPUs were visible, stage i on GPU i % ndev
@@ -572,6 +650,12 @@ bool load_model(const load_model_inputs inputs) {
             }
         e->use_contextshift = false;
     }
+    if (!rope_ff.empty())
+        for (kcpp_model *m : e->stages)
+            if (kcpp_model_set_rope_freqs(m, rope_ff.data(), (int)rope_ff.size())) {
+                fprintf(stderr, "[kcpp] load_model: rope_freqs: %s\n", kcpp_last_error());
+                return false;
+            }
     for (size_t k = 0; k < ts.size(); ++k) {
         for (kcpp_model *m : e->stages)
             if (kcpp_model_set_tensor(m, (int)k, ts[k].data, ts[k].bytes)) {
@@ -662,36 +746,96 @@ generation_outputs generate(const generation_inputs in) {
     std::vector<int> last_n(S.P.rep_pen_range, 0);
     for (int t : e->ctx) { last_n.erase(last_n.begin()); last_n.push_back(t); }
     std::vector<std::string> stops;
+    std::vector<int> special_stops;          // a stop string that is one special token without text (:2497-2510)
     for (int k = 0; k < KCPP_STOP_TOKEN_MAX; ++k)
-        if (in.stop_sequence[k] && in.stop_sequence[k][0]) stops.emplace_back(in.stop_sequence[k]);
+        if (in.stop_sequence[k] && in.stop_sequence[k][0]) {
+            stops.emplace_back(in.stop_sequence[k]);
+            const std::vector<int> st = e->tok.encode(in.stop_sequence[k], false);
+            if (st.size() == 1 && e->tok.piece(st[0]).empty()) special_stops.push_back(st[0]);
+        }
+    // generated text streams through a delay line of S.delay tokens (delayed_generated_tokens,
+    // gpttype_adapter.cpp:3251-3267); stop strings are matched on the streamed text only
+    std::deque<std::string> delayed;
+    std::map<int, std::vector<int>> slop;    // antislop bans: position -> token ids banned there (:3219, 3325-3331)
+    bool hit = false;
+    auto emit = [&](const std::string &piece) {
+        std::lock_guard<std::mutex> lk(g_out_mtx);
+        g_generated.push_back(piece);
+        g_concat += piece;
+        for (const std::string &st : stops) {
+            const size_t p = g_concat.find(st);
+            if (p != std::string::npos) { g_concat.resize(p); hit = true; break; }
+        }
+    };
     int n_gen = 0, stop = KCPP_STOP_OUT_OF_TOKENS;
     for (; n_gen < max_len; ++n_gen) {
         if (g_abort) { stop = KCPP_STOP_CUSTOM_STOPPER; break; }
-        const int t = sample(*e, S, last_n, rng, &g_mirostat_mu);
+        const auto sb = slop.find((int)e->ctx.size());
+        const int t = sample(*e, S, last_n, rng, &g_mirostat_mu, sb == slop.end() ? nullptr : &sb->second);
         if (t < 0) { fprintf(stderr, "[kcpp] generate: sampling failed: %s\n", kcpp_last_error()); break; }
         last_n.erase(last_n.begin());
         last_n.push_back(t);
-        // EOS or EOT ends the generation when EOS is allowed (gpttype_adapter.cpp:3346)
-        if (!in.bypass_eos_token && in.allow_eos_token && (t == e->tok.eos() || (t == e->tok.eot() && t != -1))) {
-            stop = KCPP_STOP_EOS_TOKEN_HIT;
-            break;
+        const bool eos_tok = t == e->tok.eos() || (t == e->tok.eot() && t != -1);
+        const bool special_stop = std::find(special_stops.begin(), special_stops.end(), t) != special_stops.end();
+        // rendered text (:3253-3257): special tokens as text with render_special, else EOS / EOT / special stops silent
+        std::string piece = e->tok.piece(t, in.render_special);
+        if (!in.render_special && (eos_tok || special_stop)) piece.clear();
+        delayed.push_back(piece);
+        while ((int)delayed.size() > S.delay && !delayed.empty()) {
+            emit(delayed.front());
+            delayed.pop_front();
         }
-        const std::string piece = e->tok.piece(t);
-        bool hit = false;
-        {
-            std::lock_guard<std::mutex> lk(g_out_mtx);
-            g_generated.push_back(piece);
-            g_concat += piece;
-            for (const std::string &s : stops) {
-                const size_t p = g_concat.find(s);
-                if (p != std::string::npos) { g_concat.resize(p); hit = true; break; }
+        // antislop (:3293-3341): a banned phrase in the held-back text rewinds the context to just before the
+        // shortest tail of tokens that contains it, and bans that tail's first token at that position
+        bool rewound = false;
+        if (!S.phrases.empty()) {
+            std::string scan;
+            for (const std::string &d : delayed) scan += d;
+            scan = lower(scan);
+            for (const std::string &ph : S.phrases) {
+                if (scan.find(ph) == std::string::npos) continue;
+                std::string check;
+                int rewind = 0;
+                for (int i = (int)delayed.size() - 1; i >= 0; --i) {
+                    check = delayed[i] + check;
+                    ++rewind;
+                    if (lower(check).find(ph) != std::string::npos) break;
+                }
+                const int cur = (int)e->ctx.size() + 1;            // current_context_tokens: the context + t
+                if (rewind > 0 && cur - rewind > 0) {
+                    const int last_tok = cur - rewind < (int)e->ctx.size() ? e->ctx[cur - rewind] : t;
+                    delayed.resize(delayed.size() - rewind);
+                    // ContextRewind (:424-480): last_n shrinks, the context drops `rewind` tokens, and the new last
+                    // context token is evaluated again (its cache row and every later one are rewritten)
+                    if (rewind >= (int)last_n.size()) last_n.clear();
+                    else last_n.resize(last_n.size() - rewind);
+                    e->ctx.resize(std::max(0, cur - rewind));
+                    const int32_t back = e->ctx.back();
+                    e->ctx.pop_back();
+                    if (forward(*e, &back, 1, (int)e->ctx.size())) {
+                        fprintf(stderr, "[kcpp] generate: decode failed\n");
+                        hit = true;
+                    }
+                    e->ctx.push_back(back);
+                    slop[(int)e->ctx.size()].push_back(last_tok);
+                    rewound = true;
+                    break;
+                }
             }
         }
+        // EOS (when allowed) or a special stop token ends the generation (:3344-3375), as does a stop string
+        if (!in.bypass_eos_token && in.allow_eos_token && eos_tok) { stop = KCPP_STOP_EOS_TOKEN_HIT; ++n_gen; break; }
+        if (special_stop) { stop = KCPP_STOP_EOS_TOKEN_HIT; ++n_gen; break; }
         if (hit) { stop = KCPP_STOP_CUSTOM_STOPPER; ++n_gen; break; }
-        if ((int)e->ctx.size() >= e->hp.n_ctx - 1) break;
+        if (rewound) continue;
+        if ((int)e->ctx.size() >= e->hp.n_ctx - 1) { ++n_gen; break; }
         const int32_t tt = t;
         if (forward(*e, &tt, 1, (int)e->ctx.size())) { fprintf(stderr, "[kcpp] generate: decode failed\n"); break; }
         e->ctx.push_back(t);
+    }
+    while (!delayed.empty()) {               // flush what the delay line still holds (:3497-3505)
+        if (!hit) emit(delayed.front());
+        delayed.pop_front();
     }
     const auto t2 = std::chrono::steady_clock::now();
     const double tp = std::chrono::duration<double, std::milli>(t1 - t0).count();

@@ -1499,6 +1499,16 @@ __global__ void k_silu_mul_strided(float *__restrict__ y, int64_t ldy, const flo
     y[m * ldy + n] = (g / (1.0f + expf(-g))) * u[i];
 }
 
+// v1 split-K factor, from the weight shape alone: on grids under 512 workgroups (two per CU) at a 512-token ubatch the
+// K range is split (2 .. 8 ways; partials summed in split order by k_splitk_reduce).  Chosen without M so that a
+// prompt gives the same bits however it is cut into ubatches (the f32 partial order depends only on the weight).
+static int ks1_of(int64_t K, int64_t N) {
+    const int64_t nwg = (N + GB_N - 1) / GB_N * (512 / GB_M);
+    int ks = 1;
+    while (ks < 8 && nwg * ks * 2 <= 1024 && (K / GB_K) % (ks * 2) == 0) ks *= 2;
+    return ks;
+}
+
 static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a16, int64_t &o_dy, int64_t &o_bs, int64_t &o_up) {
     const int64_t Mp = (M + GB_M - 1) / GB_M * GB_M;
     const int64_t G = (type == KT_Q4_0 || type == KT_Q5_0 || type == KT_Q8_0 || type == KT_Q4_1 || type == KT_Q5_1 ||
@@ -1510,7 +1520,7 @@ static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a
     o_up = off; off += (M * N * 4 + 255) & ~255LL;
     if (type == KT_Q8_0) off += 2 * (int64_t)q80s_splits(K, N) * 32 * N * 4;   // small-M split-K partials (g, u)
     if (type == KT_Q4_K || type == KT_Q4_K_RS || type == KT_Q6_K_RS) off += 2 * Mp * N * 4;   // v3 split-K partials
-    else off += std::min<int64_t>(8 * Mp * N, 1024LL * GB_M * GB_N) * 4;                       // v1 split-K partials
+    else off += (int64_t)ks1_of(K, N) * Mp * N * 4;                                             // v1 split-K partials
     return off;
 }
 
@@ -2020,11 +2030,8 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     hipLaunchKernelGGL(k_act_to_f16, dim3((unsigned)((K + 1023) / 1024), (unsigned)Mp), dim3(256), 0, s,
                        (const uint8_t *)act, vt, K, M, Mp, a16, dy, bs16);
     KCPP_CHECK(hipGetLastError());
-    // v1 split-K: on grids under 512 workgroups (two per CU) the K range is split (2 .. 8 ways, up to 1024 workgroups;
-    // partials summed in order by k_splitk_reduce): a lone workgroup otherwise walks all of K, one load latency a step
-    const int64_t nwg1 = (N + GB_N - 1) / GB_N * (Mp / GB_M);
-    int KS1 = 1;
-    while (gv != 21 && KS1 < 8 && nwg1 * KS1 * 2 <= 1024 && (K / GB_K) % (KS1 * 2) == 0) KS1 *= 2;
+    // v1 split-K (ks1_of: from the weight shape only): a lone workgroup otherwise walks all of K, one load latency a step
+    const int KS1 = gv == 21 ? 1 : ks1_of(K, N);
     const dim3 grid((unsigned)((N + GB_N - 1) / GB_N), (unsigned)(Mp / GB_M), (unsigned)KS1);
     const float *s81 = vt == KT_Q8_1 ? act_view(vt, act, K, M, 0).s : nullptr;      // block_q8_1.s [M][K/32]
     auto launch = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {

@@ -108,7 +108,11 @@ struct kcpp_model {
     void *gemm_ws2 = nullptr;               // prefill: attn_v GEMM on the side stream (q|k fused layers)
     size_t act_sz = 0, gemm_ws_sz = 0;
     int32_t *tok_dev = nullptr, *pos_dev = nullptr, *argmax_dev = nullptr;   // pos_dev = {position, epoch}
-    void *gran = nullptr;            // granules of the fused q|k|v + attention launch (dec_fused.hip)
+    void *eng_layers = nullptr;      // persistent decode engine (dec_engine.hip): device layer table
+    unsigned *eng_sync = nullptr;    // its edge counters (zeroed ahead of every launch) ++ error word
+    int eng_mode = 0;                // 1: single-token steps through the engine where covered; 0: the launch chain
+    int eng_ok = -1;                 // -1: not prepared yet; 0: not applicable; 1: ready
+    bool eng_used = false;           // the last enqueued single-token step ran the engine
     void *argmax_ws = nullptr;       // ARGMAX_BLOCKS (value, index) partials
     int32_t *moe_ids = nullptr;      // [ubatch][n_expert_used] selected experts (device)
     float *moe_w = nullptr;          // [ubatch][n_expert_used] normalized weights (device)
@@ -120,6 +124,7 @@ struct kcpp_model {
     int32_t *moe_rows_h = nullptr;
     float *moe_rw_h = nullptr;
     float2 *rope_tab = nullptr;
+    std::vector<float> rope_ff;             // rope frequency factors (rope_freqs.weight); empty: none
     void *kv_scratch = nullptr;             // context shift: moved K/V rows (n_ctx x EKV x 2 f16, lazily)
     float *shift_cs = nullptr;              // context shift: (cos, sin) pairs of the shift distance
     int32_t *pin = nullptr;          // pinned host {token, n_past}
@@ -129,7 +134,6 @@ struct kcpp_model {
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
     bool q81 = false;                // Q4_1 / Q5_1 (Q8_1 activations) or IQ4_NL / IQ4_XS weights: decode on the per-op path
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
-    bool fuse_qkv_att = false;       // single-token q|k|v and attention partials in one launch (dec_fused.hip; opt-in, see DESIGN)
     int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
     hipGraphExec_t g_exec = nullptr;
     hipStream_t side = nullptr;             // second branch of the decode step (independent q|k|v launches)
@@ -251,8 +255,8 @@ extern "C" int kcpp_model_kv_shift(kcpp_model *m, int p0, int diff, int n_past) 
     }
     if (!m->shift_cs && hipMalloc(&m->shift_cs, (size_t)D * 4) != hipSuccess) { g_err = "kv_shift cs"; return -2; }
     std::vector<float> row((size_t)D);
-    rope_row(row.data(), (float)-diff, (int)D, m->hp.rope_base, m->hp.rope_freq_scale, nullptr, 0.0f, 1.0f, 32.0f, 1.0f,
-             m->hp.n_ctx);
+    rope_row(row.data(), (float)-diff, (int)D, m->hp.rope_base, m->hp.rope_freq_scale,
+             m->rope_ff.empty() ? nullptr : m->rope_ff.data(), 0.0f, 1.0f, 32.0f, 1.0f, m->hp.n_ctx);
     RT_CHECK(hipMemcpyAsync(m->shift_cs, row.data(), (size_t)D * 4, hipMemcpyHostToDevice, m->stream));
     uint16_t *ks = (uint16_t *)m->kv_scratch, *vs = ks + (size_t)m->hp.n_ctx * EKV;
     for (auto &L : m->layers) {
@@ -262,6 +266,19 @@ extern "C" int kcpp_model_kv_shift(kcpp_model *m, int p0, int diff, int n_past) 
         RT_CHECK(hipMemcpyAsync(L.vc + p0 * EKV, vs, (size_t)count * EKV * 2, hipMemcpyDeviceToDevice, m->stream));
     }
     RT_CHECK(hipStreamSynchronize(m->stream));     // the host row above must outlive its copy
+    return 0;
+}
+
+extern "C" int kcpp_model_set_rope_freqs(kcpp_model *m, const float *ff, int n) {
+    const int64_t D = m->hp.n_embd / m->hp.n_head;
+    if (!ff || n != D / 2) { g_err = "rope_freqs: need head_dim / 2 values"; return -1; }
+    RT_CHECK(hipSetDevice(m->device));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    m->rope_ff.assign(ff, ff + n);
+    std::vector<float> tab((size_t)m->hp.n_ctx * D);
+    kcpp_rope_table(tab.data(), m->hp.n_ctx, (int)D, m->hp.rope_base, m->hp.rope_freq_scale, m->rope_ff.data(), 0.0f, 1.0f,
+                    32.0f, 1.0f, m->hp.n_ctx);
+    RT_CHECK(hipMemcpy(m->rope_tab, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -379,13 +396,11 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     }
     // flash-attention tickets must start at zero (the merging workgroup resets its own)
     if (hipMemset(m->fa_ws, 0, kcpp_fa_workspace_bytes(16, H, hp->n_ctx)) != hipSuccess) return fail("fa ws memset");
-    {   // the epoch (pos_dev[1]) starts at 1 so that no zeroed granule carries a live tag
+    {   // pos_dev = {position, step counter}
         const int32_t pe[2] = {0, 1};
-        if (hipMalloc(&m->gran, kcpp_dec_gran_bytes(H, HKV)) != hipSuccess ||
-            hipMemset(m->gran, 0, kcpp_dec_gran_bytes(H, HKV)) != hipSuccess ||
-            hipMemcpy(m->pos_dev, pe, 8, hipMemcpyHostToDevice) != hipSuccess)
-            return fail("granule buffer");
+        if (hipMemcpy(m->pos_dev, pe, 8, hipMemcpyHostToDevice) != hipSuccess) return fail("pos");
     }
+    if (getenv("KCPP_ENGINE")) m->eng_mode = atoi(getenv("KCPP_ENGINE")) != 0;
     if (has_output) {
         if (hipMalloc(&m->logits, (size_t)hp->n_vocab * 4) != hipSuccess) return fail("logits alloc");
         if (hipHostMalloc((void **)&m->logits_pin, (size_t)hp->n_vocab * 4, hipHostMallocDefault) != hipSuccess)
@@ -416,7 +431,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     for (void *p : {(void *)m->moe_ids_h, (void *)m->moe_w_h, (void *)m->moe_rows_h, (void *)m->moe_rw_h})
         if (p) hipHostFree(p);
     F(m->x); F(m->qkv); F(m->attn); F(m->h); F(m->logits); F(m->q16); F(m->act); F(m->act2); F(m->fa_ws);
-    F(m->gemm_ws); F(m->gemm_ws2); F(m->tok_dev); F(m->pos_dev); F(m->gran); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
+    F(m->gemm_ws); F(m->gemm_ws2); F(m->tok_dev); F(m->pos_dev); F(m->eng_layers); F(m->eng_sync); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
     F(m->kv_scratch); F(m->shift_cs);
     if (m->pin) hipHostFree(m->pin);
     if (m->logits_pin) hipHostFree(m->logits_pin);
@@ -650,16 +665,12 @@ extern "C" int kcpp_model_moe_ids(kcpp_model *m, int32_t *out, int n) {
     memcpy(out, m->moe_ids_h, (size_t)n * 4);
     return 0;
 }
-extern "C" int kcpp_model_fused_error(kcpp_model *m) {
-    RT_CHECK(hipSetDevice(m->device));
-    RT_CHECK(hipStreamSynchronize(m->stream));
-    return kcpp_dec_fused_error(m->gran, m->hp.n_head, m->hp.n_head_kv);
-}
-extern "C" int kcpp_model_set_decode_fusion(kcpp_model *m, int enable) {
-    m->fuse_qkv_att = enable != 0;
+extern "C" int kcpp_model_set_engine(kcpp_model *m, int enable) {
+    m->eng_mode = enable != 0;
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
     return 0;
 }
+extern "C" int kcpp_model_engine_active(kcpp_model *m) { return m->eng_used ? 1 : 0; }
 extern "C" int kcpp_model_set_fa_exact(kcpp_model *m, int enable) {
     m->fa_exact = enable != 0;
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
@@ -891,20 +902,6 @@ static int forward_layers_dec(kcpp_model *m) {
             }
             qty[nq++] = ty;
         }
-        // q|k|v + attention partials in one launch (dec_fused.hip), then the combine; -3: the two-kernel path below
-        int fused_rc = -3;
-        if (m->fuse_qkv_att && !m->fa_exact) {
-            if (nq == 2 && qty[0] == KT_Q4_K_RS && qty[1] == KT_Q6_K_RS && qa[0].nseg == 2 && qa[1].nseg == 1 &&
-                qa[1].role[0] == 2) {
-                DecArgs c = qa[0];
-                c.W[2] = qa[1].W[0]; c.N[2] = qa[1].N[0]; c.role[2] = 2; c.nseg = 3;
-                fused_rc = kcpp_dec_qkv_att(1, &c, m->fa_ws, m->gran, il, (int)H, (int)HKV, kq_scale, m->attn, s);
-            } else if (nq == 1 && qty[0] == KT_Q4_K_RS && qa[0].nseg == 3) {
-                fused_rc = kcpp_dec_qkv_att(0, &qa[0], m->fa_ws, m->gran, il, (int)H, (int)HKV, kq_scale, m->attn, s);
-            }
-            if (fused_rc != -3) RC(fused_rc);
-        }
-        if (fused_rc != 0) {
         int mixed_rc = -3;
         if (nq == 2 && qty[0] == KT_Q4_K_RS && qty[1] == KT_Q6_K_RS && qa[0].nseg == 2 && qa[1].nseg == 1 &&
             qa[1].role[0] == 2) {
@@ -924,7 +921,6 @@ static int forward_layers_dec(kcpp_model *m) {
         else
             RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, nullptr, m->fa_ws, 1, (int)H, (int)HKV, (int)D, 0, m->pos_dev,
                                hp.n_ctx, kq_scale, 1, s));
-        }
         {   // x += wo . attn
             DecArgs a;
             memset(&a, 0, sizeof a);
@@ -1102,13 +1098,89 @@ static int head(kcpp_model *m, int T) {
     return 0;
 }
 
+// Is the persistent decode engine (dec_engine.hip) applicable, and prepared?  Covered: F16 caches, no row split /
+// MoE / strict-parity attention, the compiled geometry, and the Q4_K_M layer types (q, k, wo, gate, up in Q4_K_RS;
+// attn_v and ffn_down in Q4_K_RS or Q6_K_RS).  Prepared outside any stream capture (allocations).
+static bool engine_on(const kcpp_model *m) {
+    return m->eng_mode && m->eng_ok == 1 && m->fused_decode && m->kv_tk == KT_F16 && !m->q81 && !m->fa_exact &&
+           m->lanes.empty();
+}
+static int engine_prepare(kcpp_model *m) {
+    if (m->eng_ok >= 0 || !m->eng_mode) return 0;
+    m->eng_ok = 0;
+    const kcpp_hparams &hp = m->hp;
+    const int64_t E = hp.n_embd, H = hp.n_head, D = E / H;
+    int ncu = 0;
+    RT_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device));
+    const int nl = m->il1 - m->il0;
+    if (nl < 1 || hp.n_expert > 0 || !kcpp_engine_supported((int)E, hp.n_ff, (int)H, hp.n_head_kv, (int)D, ncu)) return 0;
+    auto q4 = [](const KTensor &t) { return t.type == KT_Q4_K_RS && t.rs.empty(); };
+    auto q46 = [](const KTensor &t) { return (t.type == KT_Q4_K_RS || t.type == KT_Q6_K_RS) && t.rs.empty(); };
+    for (const auto &L : m->layers) {
+        const KTensor *t = L.t;
+        if (t[0].type != KT_F32 || t[5].type != KT_F32 || !q4(t[1]) || !q4(t[2]) || !q46(t[3]) || !q4(t[4]) ||
+            !q4(t[6]) || !q4(t[7]) || !q46(t[8]))
+            return 0;
+    }
+    const int rb = kcpp_engine_layer_bytes();
+    std::vector<uint8_t> tab((size_t)nl * rb);
+    for (int i = 0; i < nl; ++i) {
+        const KTensor *t = m->layers[i].t;
+        kcpp_engine_layer(tab.data() + (size_t)i * rb, t[1].d, t[2].d, t[3].d, t[4].d, t[6].d, t[7].d, t[8].d,
+                          (const float *)t[0].d, (const float *)t[5].d, m->layers[i].kc, m->layers[i].vc,
+                          t[3].type == KT_Q6_K_RS, t[8].type == KT_Q6_K_RS);
+    }
+    const size_t sb = (size_t)kcpp_engine_sync_bytes(nl);
+    RT_CHECK(hipMalloc(&m->eng_layers, tab.size()));
+    RT_CHECK(hipMemcpy(m->eng_layers, tab.data(), tab.size(), hipMemcpyHostToDevice));
+    RT_CHECK(hipMalloc((void **)&m->eng_sync, sb));
+    RT_CHECK(hipMemset(m->eng_sync, 0, sb));
+    m->eng_ok = 1;
+    return 0;
+}
+// after a synchronised engine step: a hand-off timeout (error word != 0) turns the engine off for this model
+static int engine_check(kcpp_model *m, unsigned err) {
+    if (!err) return 0;
+    const int nl = m->il1 - m->il0;
+    std::vector<unsigned> c((size_t)kcpp_engine_sync_bytes(nl) / 4);
+    if (hipMemcpy(c.data(), m->eng_sync, c.size() * 4, hipMemcpyDeviceToHost) == hipSuccess) {
+        const unsigned *e = c.data() + (size_t)nl * 48 * 32;
+        fprintf(stderr, "[kcpp] engine timeout: saw %u, waited for %u, workgroup %u\n", e[1], e[2], e[3]);
+        for (int l = 0; l < std::min(nl, 3); ++l) {
+            fprintf(stderr, "[kcpp]  layer %d:", l);
+            for (int k = 0; k < 48; ++k) fprintf(stderr, " %u", c[((size_t)l * 48 + k) * 32]);
+            fprintf(stderr, "\n");
+        }
+    }
+    (void)hipMemset(m->eng_sync, 0, (size_t)kcpp_engine_sync_bytes(nl));
+    char b[160];
+    snprintf(b, sizeof b, "decode engine: hand-off timeout (code %u); falling back to the launch chain", err);
+    g_err = b;
+    fprintf(stderr, "[kcpp] %s\n", b);
+    m->eng_ok = 0;
+    m->pos_val = -1;
+    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    return -7;
+}
+
 // full single-token step with the inputs read from device memory (graph-capturable)
 static int decode_step_dev(kcpp_model *m) {
     const kcpp_hparams &hp = m->hp;
     if (m->has_embed)
         RC(kcpp_get_rows(m->tok_embd.type, m->tok_embd.d, hp.n_embd, hp.n_vocab, m->tok_dev, 1, m->x, hp.n_embd,
                          m->stream));
-    if (m->fused_decode && m->kv_tk == KT_F16 && !m->q81) {
+    m->eng_used = false;
+    if (engine_on(m)) {
+        const int nl = m->il1 - m->il0;
+        const int64_t E = hp.n_embd, H = hp.n_head;
+        // the edge counters start at zero every launch (a memset node of the graph); the error word after them is kept
+        RT_CHECK(hipMemsetAsync(m->eng_sync, 0, (size_t)kcpp_engine_sync_bytes(nl) - 128, m->stream));
+        RC(kcpp_engine_decode(m->eng_layers, nl, m->x, m->q16, m->fa_ws, m->act, m->h, m->eng_sync, m->pos_dev,
+                              m->rope_tab, hp.eps, 1.0f / sqrtf((float)(E / H)), (int)E, hp.n_ff, (int)H, hp.n_head_kv,
+                              m->stream));
+        m->eng_used = true;
+        if (m->has_output) RC(head_dec(m));
+    } else if (m->fused_decode && m->kv_tk == KT_F16 && !m->q81) {
         RC(forward_layers_dec(m));
         if (m->has_output) RC(head_dec(m));
     } else {
@@ -1122,19 +1194,39 @@ static int decode_step_dev(kcpp_model *m) {
     return 0;
 }
 
-// pos_dev <- n_past unless the device already holds it (the previous single-token step advanced it)
+// pos_dev <- n_past unless the device already holds it (the previous single-token step advanced it).  The caller
+// records n_past + 1 in pos_val only once the step is enqueued (a failed enqueue leaves pos_val = -1).
 static int set_pos(kcpp_model *m, int n_past) {
     if (m->pos_val != n_past) {
+        m->pos_val = -1;
         m->pin[1] = n_past;
         RT_CHECK(hipMemcpyAsync(m->pos_dev, &m->pin[1], 4, hipMemcpyHostToDevice, m->stream));
     }
-    m->pos_val = n_past + 1;          // decode_step_dev advances it
+    return 0;
+}
+// one single-token step at n_past (tok_dev already set): graph replay or eager; advances pos_val on success
+static int step_one(kcpp_model *m, int n_past) {
+    m->pos_val = m->pos_val == n_past ? n_past : -1;
+    if (m->use_graphs) {
+        RC(ensure_graph(m));
+        RC(set_pos(m, n_past));
+        const hipError_t e = hipGraphLaunch(m->g_exec, m->stream);
+        if (e != hipSuccess) { m->pos_val = -1; RT_CHECK(e); }
+        m->eng_used = engine_on(m);
+    } else {
+        RC(engine_prepare(m));
+        RC(set_pos(m, n_past));
+        const int rc = decode_step_dev(m);
+        if (rc) { m->pos_val = -1; return rc; }
+    }
+    m->pos_val = n_past + 1;          // decode_step_dev advanced the device position
     return 0;
 }
 
 // single-token graph: embedding of tok_dev, layers at position pos_dev, head, argmax, pos_dev + 1
 static int ensure_graph(kcpp_model *m) {
     if (m->g_exec) return 0;
+    RC(engine_prepare(m));
     hipGraph_t g;
     RT_CHECK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
     int rc = decode_step_dev(m);
@@ -1156,18 +1248,12 @@ static int decode_enqueue(kcpp_model *m, const int32_t *tokens, int T, int n_pas
     const kcpp_hparams &hp = m->hp;
     if (T < 1 || n_past + T > hp.n_ctx) { g_err = "context overflow"; return -2; }
     if (m->has_embed && !tokens) { g_err = "decode: stage owns the embedding but tokens == NULL"; return -2; }
-    if (T == 1 && m->use_graphs) {
+    if (T == 1) {
         m->pin[0] = m->has_embed ? tokens[0] : 0;
         if (m->has_embed) RT_CHECK(hipMemcpyAsync(m->tok_dev, &m->pin[0], 4, hipMemcpyHostToDevice, m->stream));
-        RC(ensure_graph(m));
-        RC(set_pos(m, n_past));
-        RT_CHECK(hipGraphLaunch(m->g_exec, m->stream));
-    } else if (T == 1) {
-        m->pin[0] = m->has_embed ? tokens[0] : 0;
-        RT_CHECK(hipMemcpyAsync(m->tok_dev, &m->pin[0], 4, hipMemcpyHostToDevice, m->stream));
-        RC(set_pos(m, n_past));
-        RC(decode_step_dev(m));
+        RC(step_one(m, n_past));
     } else {
+        m->eng_used = false;
         // split into ubatches (llama_decode_internal, src/llama.cpp:17187-17201)
         for (int i = 0; i < T; i += m->ub) {
             const int t = std::min(m->ub, T - i);
@@ -1194,8 +1280,12 @@ extern "C" int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, in
     if (m->has_output && logits_host) {
         RT_CHECK(hipMemcpyAsync(logits_host, m->logits, (size_t)m->hp.n_vocab * 4, hipMemcpyDeviceToHost, m->stream));
     }
+    const bool eng = m->eng_used;
+    if (eng)
+        RT_CHECK(hipMemcpyAsync(&m->pin[3], m->eng_sync + (kcpp_engine_sync_bytes(m->il1 - m->il0) - 128) / 4, 4,
+                                hipMemcpyDeviceToHost, m->stream));
     RT_CHECK(hipStreamSynchronize(m->stream));
-    return 0;
+    return eng ? engine_check(m, (unsigned)m->pin[3]) : 0;
 }
 extern "C" int kcpp_model_device(kcpp_model *m) { return m->device; }
 
@@ -1265,16 +1355,13 @@ extern "C" int kcpp_model_decode_greedy(kcpp_model *m, int n_past, int32_t *toke
     if (!m->has_embed || !m->has_output) { g_err = "decode_greedy needs embedding and output on this stage"; return -2; }
     if (n_past + 1 > m->hp.n_ctx) { g_err = "context overflow"; return -2; }
     RT_CHECK(hipSetDevice(m->device));
-    if (m->use_graphs) {
-        RC(ensure_graph(m));
-        RC(set_pos(m, n_past));
-        RT_CHECK(hipGraphLaunch(m->g_exec, m->stream));
-    } else {
-        RC(set_pos(m, n_past));
-        RC(decode_step_dev(m));
-    }
+    RC(step_one(m, n_past));
     RT_CHECK(hipMemcpyAsync(&m->pin[2], m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
+    const bool eng = m->eng_used;
+    if (eng)
+        RT_CHECK(hipMemcpyAsync(&m->pin[3], m->eng_sync + (kcpp_engine_sync_bytes(m->il1 - m->il0) - 128) / 4, 4,
+                                hipMemcpyDeviceToHost, m->stream));
     RT_CHECK(hipStreamSynchronize(m->stream));
     *token_out = m->pin[2];
-    return 0;
+    return eng ? engine_check(m, (unsigned)m->pin[3]) : 0;
 }

@@ -199,11 +199,13 @@ public:
     // normal tokens unescaped (SPM: U+2581 -> space) or byte-decoded (BPE, llama_decode_text :1986-2004: a code
     // point outside the byte map renders as "[UNK_BYTE_0x<its utf8>" + token text + "]"), SPM byte tokens their
     // byte, every other type (undefined, unused, BPE byte) nothing
-    std::string piece(int id) const {
+    // llama_token_to_piece_impl (src/llama-vocab.cpp:2007-2077): special = false suppresses UNKNOWN / CONTROL tokens,
+    // special = true renders their raw text (koboldcpp's render_special)
+    std::string piece(int id, bool special = false) const {
         if (id < 0 || id >= (int)vocab_.size()) return "";
         const int type = ttype_[id];
         const std::string &s = vocab_[id];
-        if (type == 2 || type == 3) return "";
+        if (type == 2 || type == 3) return special ? s : "";
         if (type == 4) return s;
         if (model_ == "llama") {
             if (type == 6) return s.size() >= 5 ? std::string(1, (char)strtol(s.substr(3, 2).c_str(), nullptr, 16)) : "";

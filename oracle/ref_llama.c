@@ -85,6 +85,17 @@ static void fill_tensor(struct ggml_tensor *t, int type, unsigned long long seed
 /* KV cache types (koboldcpp --quantkv: gpttype_adapter.cpp:1958-1959 -> llama_kv_cache type_k / type_v):
  * env REF_KV_TYPES="tk tv" with ggml type ids (1 = F16 default, 8 = Q8_0, 2 = Q4_0) */
 static int g_tk = GGML_TYPE_F16, g_tv = GGML_TYPE_F16;
+/* optional rope frequency factors (env REF_ROPE_FREQS = path of D/2 f32 values): the model's rope_freqs.weight, fed
+   to every rope of build_llama (src/llama.cpp:7171 create_tensor, :10269 build_rope_factors, :10490 ggml_rope_ext)
+   and to the K-shift (build_k_shift) */
+static float *g_rope_ff = NULL;
+static int g_rope_nff = 0;
+static struct ggml_tensor *rope_factors(struct ggml_context *ctx) {
+    if (!g_rope_ff) return NULL;
+    struct ggml_tensor *t = ggml_new_tensor_1d(ctx, GGML_TYPE_F32, g_rope_nff);
+    memcpy(t->data, g_rope_ff, sizeof(float) * g_rope_nff);
+    return t;
+}
 
 static int load_model(model_t *m) {
     cfg_t *c = &m->c;
@@ -176,6 +187,7 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits,
     memcpy(inp_tokens->data, tokens, sizeof(int) * T);
     struct ggml_tensor *inp_pos = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, T);
     for (int t = 0; t < T; ++t) ((int32_t *)inp_pos->data)[t] = n_past + t;
+    struct ggml_tensor *rope_ff = rope_factors(ctx);
     struct ggml_tensor *kq_mask = ggml_new_tensor_2d(ctx, GGML_TYPE_F16, n_kv, T_pad);
     for (int t = 0; t < T_pad; ++t)
         for (int j = 0; j < n_kv; ++j)
@@ -194,9 +206,9 @@ static int eval(model_t *m, const int *tokens, int T, int n_past, float *logits,
         struct ggml_tensor *Qcur = ggml_mul_mat(ctx, lw[1], cur);
         struct ggml_tensor *Kcur = ggml_mul_mat(ctx, lw[2], cur);
         struct ggml_tensor *Vcur = ggml_mul_mat(ctx, lw[3], cur);
-        Qcur = ggml_rope_ext(ctx, ggml_reshape_3d(ctx, Qcur, D, H, T), inp_pos, NULL, D, 0, c->n_ctx,
+        Qcur = ggml_rope_ext(ctx, ggml_reshape_3d(ctx, Qcur, D, H, T), inp_pos, rope_ff, D, 0, c->n_ctx,
                              c->rope_base, c->rope_freq_scale, 0.0f, 1.0f, 32.0f, 1.0f);
-        Kcur = ggml_rope_ext(ctx, ggml_reshape_3d(ctx, Kcur, D, HKV, T), inp_pos, NULL, D, 0, c->n_ctx,
+        Kcur = ggml_rope_ext(ctx, ggml_reshape_3d(ctx, Kcur, D, HKV, T), inp_pos, rope_ff, D, 0, c->n_ctx,
                              c->rope_base, c->rope_freq_scale, 0.0f, 1.0f, 32.0f, 1.0f);
         /* llm_build_kv_store (src/llama.cpp:9180-9202), FA => V not transposed */
         struct ggml_tensor *kview = ggml_view_1d(ctx, m->kc[il], (int64_t)T * EKV, ggml_row_size((enum ggml_type)g_tk, EKV) * n_past);
@@ -285,7 +297,7 @@ static int kv_shift(model_t *m, int p0, int diff, int n_past) {
         struct ggml_tensor *pos = ggml_new_tensor_1d(ctx, GGML_TYPE_I32, n);
         memcpy(k->data, (const uint8_t *)m->kc[il]->data + (size_t)(p0 + diff) * EKV * 2, (size_t)n * EKV * 2);
         for (int i = 0; i < n; ++i) ((int32_t *)pos->data)[i] = -diff;
-        struct ggml_tensor *r = ggml_rope_ext_inplace(ctx, k, pos, NULL, D, 0, c->n_ctx, c->rope_base, c->rope_freq_scale,
+        struct ggml_tensor *r = ggml_rope_ext_inplace(ctx, k, pos, rope_factors(ctx), D, 0, c->n_ctx, c->rope_base, c->rope_freq_scale,
                                                       0.0f, 1.0f, 32.0f, 1.0f);
         struct ggml_cgraph *gf = ggml_new_graph(ctx);
         ggml_build_forward_expand(gf, r);
@@ -462,6 +474,12 @@ static int run_op(int argc, char **argv) {
 
 int main(int argc, char **argv) {
     if (getenv("REF_KV_TYPES") && sscanf(getenv("REF_KV_TYPES"), "%d %d", &g_tk, &g_tv) != 2) return 2;
+    if (getenv("REF_ROPE_FREQS") && getenv("REF_ROPE_FREQS")[0]) {
+        size_t n;
+        g_rope_ff = (float *)read_all(getenv("REF_ROPE_FREQS"), &n);
+        if (!g_rope_ff || n % 4) return 2;
+        g_rope_nff = (int)(n / 4);
+    }
     if (argc >= 3 && !strcmp(argv[1], "llama")) return run_llama(argv[2]);
     if (argc >= 5 && !strcmp(argv[1], "op")) return run_op(argc, argv);
     fprintf(stderr, "usage: ref_llama llama <cfg> | op <name> <in> <out> args...\n");

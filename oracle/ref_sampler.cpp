@@ -17,10 +17,20 @@
 #include "gpttype_adapter.cpp"
 
 #include <cstdio>
+#include <cstring>
 
 static bool rd(void *p, size_t n) { return fread(p, 1, n, stdin) == n; }
 
-int main() {
+int main(int argc, char **argv) {
+    // "rope" mode: lines "original_base n_ctx_train n_ctx_desired solar" -> the reference's
+    // CalcGradientAIRopeFreqBase (gpttype_adapter.cpp:1598) of them, printed exactly (%.9g)
+    if (argc > 1 && !strcmp(argv[1], "rope")) {
+        float base;
+        int train, want, solar;
+        while (scanf("%f %d %d %d", &base, &train, &want, &solar) == 4)
+            printf("%.9g\n", CalcGradientAIRopeFreqBase(base, train, want, solar ? GGUFArch::ARCH_SOLAR : GGUFArch::ARCH_DEFAULT));
+        return 0;
+    }
     for (;;) {
         int32_t h[6];
         uint32_t seed;

@@ -85,7 +85,7 @@ def spm_vocab(n_vocab, words):
 LAYER_NAMES = ["attn_norm", "attn_q", "attn_k", "attn_v", "attn_output", "ffn_norm", "ffn_gate", "ffn_up", "ffn_down"]
 
 
-def llama_gguf(path, hp, types, seed, words, split_experts=False):
+def llama_gguf(path, hp, types, seed, words, split_experts=False, kv_extra=None, rope_freqs=None):
     """Llama GGUF with the runtime's synthetic weights.  MoE (hp["n_expert"]): gate/up/down as 3-D
     blk.N.ffn_*_exps tensors [k, n, n_expert] plus blk.N.ffn_gate_inp, or with split_experts the older
     per-expert blk.N.ffn_gate.E tensors (both accepted by llm_load_tensors, src/llama.cpp:7176-7215)."""
@@ -109,6 +109,8 @@ def llama_gguf(path, hp, types, seed, words, split_experts=False):
         "tokenizer.ggml.bos_token_id": 1,
         "tokenizer.ggml.eos_token_id": 2,
     }
+    if kv_extra:
+        kv.update(kv_extra)
     ne_ = int(hp.get("n_expert", 0))
     if ne_:
         kv["llama.expert_count"] = ne_
@@ -136,5 +138,8 @@ def llama_gguf(path, hp, types, seed, words, split_experts=False):
         else:
             data = R.synth_tensor(hp, t, seed, idx)
             tensors.append((names[idx], t, [k, n, ns], np.ascontiguousarray(data).tobytes()))
+    if rope_freqs is not None:      # rope_freqs.weight (Llama-3.1 / 3.2), F32 [head_dim / 2]
+        rf = np.ascontiguousarray(rope_freqs, dtype=np.float32)
+        tensors.append(("rope_freqs.weight", R.F32, [len(rf)], rf.tobytes()))
     write(path, kv, tensors)
     return toks

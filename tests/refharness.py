@@ -209,7 +209,7 @@ def ref_available():
 
 
 def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeout=600, forced=None, hidden=False,
-                  binary=None, skip_prefix=0, kshift=None):
+                  binary=None, skip_prefix=0, kshift=None, rope_freqs=None):
     """Run the reference ggml graph; returns (logits [1+n_gen, V], info dict).
     forced: decode these tokens (teacher forcing) instead of the greedy argmax.
     hidden: also return info["hidden"] = residual stream after layers 0..n_layer-2 of the prefill,
@@ -218,7 +218,8 @@ def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeou
     binary: ref_llama build to run (default: the AVX2 build; REF_BIN_SCALAR for the scalar one).
     skip_prefix: the first skip_prefix prompt positions are taken as cached (zeroed K/V), not computed (timing only).
     kshift: (p0, diff) -- context shift after the prompt (the reference's seq_rm / seq_add + build_k_shift), the
-            decode then continues at n_prompt - diff."""
+            decode then continues at n_prompt - diff.
+    rope_freqs: head_dim / 2 frequency factors (the model's rope_freqs.weight) fed to every rope and the K-shift."""
     import json
     with tempfile.TemporaryDirectory() as td:
         cfg = os.path.join(td, "cfg.txt")
@@ -235,9 +236,13 @@ def run_ref_llama(hp, types, seed, prompt, n_gen, nthreads=4, ubatch=512, timeou
             f.write("%d %s\n" % (len(fl), " ".join(map(str, fl))))
             if hidden:
                 f.write(hout + "\n")
+        rff = ""
+        if rope_freqs is not None:
+            rff = os.path.join(td, "rope_freqs.bin")
+            np.ascontiguousarray(rope_freqs, dtype=np.float32).tofile(rff)
         r = subprocess.run([binary or REF_BIN, "llama", cfg], capture_output=True, text=True, timeout=timeout,
                            env=dict(os.environ, OMP_NUM_THREADS=str(nthreads), REF_SKIP_PREFIX=str(skip_prefix),
-                                    REF_KSHIFT="%d %d" % tuple(kshift) if kshift else ""))
+                                    REF_KSHIFT="%d %d" % tuple(kshift) if kshift else "", REF_ROPE_FREQS=rff))
         if r.returncode != 0:
             raise RuntimeError("ref_llama failed: %s %s" % (r.returncode, r.stderr))
         info = json.loads(r.stdout.strip().splitlines()[-1])
@@ -264,6 +269,27 @@ def run_ref_op(op, inp_bytes, out_count, args, nthreads=4, dtype=np.float32):
 
 TINY = dict(n_vocab=512, n_embd=512, n_head=4, n_head_kv=1, n_layer=2, n_ff=1024, n_ctx=256,
             eps=1e-5, rope_base=500000.0)
+
+
+def llama31_rope_freqs(base, dim, factor=8.0, low_freq_factor=1.0, high_freq_factor=4.0, old_context_len=8192):
+    """rope_freqs.weight as the reference's converter writes it for rope_type "llama3" (Llama-3.1 / 3.2;
+    convert_hf_to_gguf.py:1622-1650, generate_extra_tensors)"""
+    import math
+    freqs = 1.0 / (np.float32(base) ** (np.arange(0, dim, 2, dtype=np.float32) / np.float32(dim)))
+    low_wl, high_wl = old_context_len / low_freq_factor, old_context_len / high_freq_factor
+    out = []
+    for f in freqs.astype(np.float64):
+        wl = 2 * math.pi / f
+        if wl < high_wl:
+            out.append(1.0)
+        elif wl > low_wl:
+            out.append(factor)
+        else:
+            smooth = (old_context_len / wl - low_freq_factor) / (high_freq_factor - low_freq_factor)
+            out.append(1 / ((1 - smooth) / factor + smooth))
+    return np.array(out, np.float32)
+
+
 # Mixtral-style tiny MoE (4 experts, top-2): BASELINE config 5's structure at test size
 TINY_MOE = dict(TINY, n_expert=4, n_expert_used=2)
 

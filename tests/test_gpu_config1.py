@@ -41,7 +41,7 @@ def test_config1_tinyllama_q4_0_generate(tmp_path):
     li.blasbatchsize = 512
     li.gpulayers = 999
     li.rope_freq_base = 10000.0
-    li.rope_freq_scale = 1.0
+    li.rope_freq_scale = 0.0     # koboldcpp.py default --ropeconfig 0: automatic RoPE
     assert h.load_model(li)
     os.remove(path)
     prompt = " ".join(["hello world the"] * 149).encode()

@@ -122,7 +122,7 @@ def test_generate_with_context_shift(tmp_path, capfd):
         li.blasbatchsize = 512
         li.gpulayers = 999
         li.rope_freq_base = 10000.0
-        li.rope_freq_scale = 1.0
+        li.rope_freq_scale = 0.0     # koboldcpp.py default --ropeconfig 0: automatic RoPE
         li.use_contextshift = shift
         assert h.load_model(li)
         res = []

@@ -44,7 +44,7 @@ def model(tmp_path_factory):
     li.blasbatchsize = 512
     li.gpulayers = 999
     li.rope_freq_base = 10000.0
-    li.rope_freq_scale = 1.0
+    li.rope_freq_scale = 0.0     # koboldcpp.py default --ropeconfig 0: automatic RoPE
     assert h.load_model(li)
     _, _, ttypes = GW.spm_vocab(R.TINY["n_vocab"], WORDS)
     return h, X, toks, ttypes, types
@@ -143,7 +143,7 @@ def test_moe_gguf_generate_matches_runtime(model, tmp_path, split):
     li.blasbatchsize = 512
     li.gpulayers = 999
     li.rope_freq_base = 10000.0
-    li.rope_freq_scale = 1.0
+    li.rope_freq_scale = 0.0     # koboldcpp.py default --ropeconfig 0: automatic RoPE
     assert h.load_model(li)
     _, _, ttypes = GW.spm_vocab(hp["n_vocab"], WORDS)
     prompt = b"hello world the a b of to the"
@@ -238,7 +238,7 @@ def test_generate_layer_split_pipeline_matches_single_stage(model, tmp_path, mon
     li.blasbatchsize = 16
     li.gpulayers = 999
     li.rope_freq_base = 10000.0
-    li.rope_freq_scale = 1.0
+    li.rope_freq_scale = 0.0     # koboldcpp.py default --ropeconfig 0: automatic RoPE
     for i, v in enumerate((1.0, 2.0, 1.0)):
         li.tensor_split[i] = v
     assert h.load_model(li)
@@ -286,7 +286,7 @@ def test_generate_row_split_matches_in_process(model, tmp_path, monkeypatch):
     li.blasbatchsize = 512
     li.gpulayers = 999
     li.rope_freq_base = 10000.0
-    li.rope_freq_scale = 1.0
+    li.rope_freq_scale = 0.0     # koboldcpp.py default --ropeconfig 0: automatic RoPE
     li.use_rowsplit = True
     for i, v in enumerate((1.0, 2.0)):
         li.tensor_split[i] = v

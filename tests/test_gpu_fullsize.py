@@ -47,6 +47,23 @@ def test_fullsize_ubatch_invariance(K):
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
 
 
+@pytest.mark.parametrize("wt", ["Q4_0", "Q8_0"])
+def test_ubatch_invariance_legacy_types(K, wt):
+    """the v1 MFMA GEMM path (Q4_0 / Q8_0 / Q2_K / Q3_K / Q5_0 / Q4_1 / Q5_1 / IQ4): its split-K factor comes from the
+    weight shape only, so 1024 tokens as 2 x 512 or 4 x 256 give the same bits (4 layers of Llama-3-8B width)"""
+    hp = dict(LLAMA3_8B, n_layer=4)
+    types = R.uniform_types(4, getattr(R, wt), out=R.Q6_K)
+    p = prompt(1024)
+    outs = []
+    for ub in (512, 256):
+        m = K.Model(hp, types, max_ubatch=ub)
+        m.synth(99)
+        outs.append(m.decode(p, 0))
+        m.close()
+    assert np.isfinite(outs[0]).all()
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
 def test_fullsize_graph_replay_and_decode_vs_prefill(K):
     types = R.q4_k_m_types(32)
     p = prompt(1100)

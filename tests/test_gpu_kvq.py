@@ -225,7 +225,7 @@ def test_load_model_quantkv_generate(env, tmp_path):
     li.blasbatchsize = 512
     li.gpulayers = 999
     li.rope_freq_base = 10000.0
-    li.rope_freq_scale = 1.0
+    li.rope_freq_scale = 0.0     # koboldcpp.py default --ropeconfig 0: automatic RoPE
     li.flash_attention = True
     li.use_contextshift = True                        # turned off by the quantized cache
     li.quant_k = li.quant_v = 1
