@@ -41,6 +41,7 @@
 #include "gemv_rs.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 using namespace rs;
 
@@ -72,6 +73,7 @@ struct Args {
     const int32_t *pos;       // {position, epoch}
     const float2 *rope_tab;   // [n_ctx][64] (cos, sin)
     float eps, kq_scale;
+    int opt;                  // edge ordering per phase (2 bits each, Q O G D): 0 together, 1 store first, 2 arrive first
     float *dbg;               // diagnostics (tests only, null in the product): the merged attention rows in f32
     unsigned long long *stamps;   // diagnostics (tools/engine_stamps.py, null in the product): [NB][nl][32] clocks
 };
@@ -279,46 +281,36 @@ __device__ __forceinline__ void quant_lds(const float *xs, uint8_t *act, int tid
     }
 }
 
-// control wave: xs = rms_norm(x) * w (ggml_compute_forward_rms_norm_f32: f32 squares summed in double, ggml.c:12089).
-// Loads in batches of 4 per lane (the control wave's registers are allocated beside the compute waves' in-flight
-// weights at the same program point).
+// control wave: the rms_norm scale of the f32 row xs[E] gathered in LDS (ggml_compute_forward_rms_norm_f32: f32
+// squares summed in double, ggml.c:12089; lane order = the k_gemv_rs norm prologue's, so the bits agree)
 template <int E>
-__device__ __forceinline__ void ctl_norm(const float *x, const float *nw, float eps, float *xs, int lane) {
-    constexpr int NL = E / 256;                       // 16-B loads per lane
-    const auto rx = rsrc(x);
+__device__ __forceinline__ float ctl_scale(const float *xs, float eps, int lane) {
+    constexpr int NL = E / 256;                       // 16-B words per lane
     double ss = 0.0;
-#pragma unroll 1
-    for (int k0 = 0; k0 < NL; k0 += 4) {
-        uint4 u[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) u[k] = ld_sc1(rx, 16 * (lane + 64 * (k0 + k)));
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float4 v = make_float4(__uint_as_float(u[k].x), __uint_as_float(u[k].y), __uint_as_float(u[k].z),
-                                         __uint_as_float(u[k].w));
-            ss += (double)__fmul_rn(v.x, v.x) + (double)__fmul_rn(v.y, v.y) + (double)__fmul_rn(v.z, v.z) +
-                  (double)__fmul_rn(v.w, v.w);
-            *(float4 *)(xs + 4 * (lane + 64 * (k0 + k))) = v;
-        }
+    for (int k = 0; k < NL; ++k) {
+        const float4 v = *(const float4 *)(xs + 4 * (lane + 64 * k));
+        ss += (double)__fmul_rn(v.x, v.x) + (double)__fmul_rn(v.y, v.y) + (double)__fmul_rn(v.z, v.z) +
+              (double)__fmul_rn(v.w, v.w);
     }
     ss = wave_sum_d(ss);
-    const float scale = 1.0f / sqrtf((float)(ss / (double)E) + eps);
-#pragma unroll 1
-    for (int k0 = 0; k0 < NL; k0 += 4) {
-        float4 w[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w[k] = *(const float4 *)(nw + 4 * (lane + 64 * (k0 + k)));
+    return 1.0f / sqrtf((float)(ss / (double)E) + eps);
+}
+// Q8_K of rms_norm(xs) * w (w staged in LDS at nws) into the LDS image act (all 512 threads; 16 lanes per super-block)
+template <int K>
+__device__ __forceinline__ void quant_lds_norm(const float *xs, const float *nws, float scale, uint8_t *act, int tid) {
+    for (int c = tid; c < K / 16; c += NT) {
+        float v[16];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            float4 *p = (float4 *)(xs + 4 * (lane + 64 * (k0 + k)));
-            const float4 v = *p;
-            float4 o;
-            o.x = __fmul_rn(__fmul_rn(v.x, scale), w[k].x);
-            o.y = __fmul_rn(__fmul_rn(v.y, scale), w[k].y);
-            o.z = __fmul_rn(__fmul_rn(v.z, scale), w[k].z);
-            o.w = __fmul_rn(__fmul_rn(v.w, scale), w[k].w);
-            *p = o;
+            const float4 f = *(const float4 *)(xs + 16 * c + 4 * k), w = *(const float4 *)(nws + 16 * c + 4 * k);
+            v[4 * k] = __fmul_rn(__fmul_rn(f.x, scale), w.x);
+            v[4 * k + 1] = __fmul_rn(__fmul_rn(f.y, scale), w.y);
+            v[4 * k + 2] = __fmul_rn(__fmul_rn(f.z, scale), w.z);
+            v[4 * k + 3] = __fmul_rn(__fmul_rn(f.w, scale), w.w);
         }
+        q8k_quant16(v, c & 15, (int8_t *)act + (c >> 4) * 256, (float *)(act + K) + (c >> 4),
+                    (int16_t *)(act + K + K / 256 * 4) + (c >> 4) * 16);
     }
 }
 // control wave: n16 16-B words from a wave-uniform base into LDS by write-through (sc1) LDS-DMA (no registers), then
@@ -329,6 +321,36 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {
 __device__ __forceinline__ void dma16_sc1(const void *g, const void *lds_base) {
     asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(g),
                  "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_base))) : "memory", "m0");
+}
+__device__ __forceinline__ void dma16_plain(const void *g, const void *lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g),
+                 "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_base))) : "memory", "m0");
+}
+// control wave: issue (no wait) the LDS-DMA of n16 16-B words of read-only data (norm weights: cached)
+__device__ __forceinline__ void ctl_fetch(void *dst, const void *src, int n16, int lane) {
+    for (int k = 0; 64 * k < n16; ++k)
+        if (64 * k + lane < n16) dma16_plain((const uint8_t *)src + 16 * (64 * k + lane), (uint8_t *)dst + 1024 * k);
+}
+// control wave: a vector produced in 8 contiguous shards (shard s by the CUs [NB/8 s, NB/8 (s + 1)), whose arrivals
+// count on the s-th counter from c0) gathered into LDS by write-through LDS-DMA, each shard requested as soon as
+// its producers have arrived (the later shards' polls overlap the earlier shards' copies); drained at the end.
+// n16 / 8 is a multiple of 64 (host-checked shapes).  `wait` false: no polls (the launch's input).
+__device__ __forceinline__ void ctl_gather8(void *dst, const void *src, const unsigned *c0, int n16, unsigned per,
+                                            bool wait, unsigned *err, unsigned code, int lane) {
+    const int W = n16 / 8;
+    for (int sh = 0; sh < 8; ++sh) {
+        if (wait) poll(c0 + sh * 32, 1, per, err, code, lane);
+        for (int k = 0; 64 * k < W; ++k)
+            dma16_sc1((const uint8_t *)src + 16 * (sh * W + 64 * k + lane), (uint8_t *)dst + 16 * (sh * W + 64 * k));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+// control wave: issue the write-through LDS-DMA of n16 16-B words (no wait)
+__device__ __forceinline__ void ctl_copy_issue(void *dst, const void *src, int n16, int lane) {
+    for (int k = 0; 64 * k < n16; ++k) {
+        if (64 * k + lane < n16) dma16_sc1((const uint8_t *)src + 16 * (64 * k + lane), (uint8_t *)dst + 1024 * k);
+        if (k >= 56) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");      // (vmcnt counts to 63)
+    }
 }
 __device__ __forceinline__ void ctl_copy(void *dst, const void *src, int n16, int lane) {
 #ifdef ENG_REGCOPY
@@ -349,10 +371,7 @@ __device__ __forceinline__ void ctl_copy(void *dst, const void *src, int n16, in
     }
     return;
 #endif
-    for (int k = 0; 64 * k < n16; ++k) {
-        if (64 * k + lane < n16) dma16_sc1((const uint8_t *)src + 16 * (64 * k + lane), (uint8_t *)dst + 1024 * k);
-        if ((k & 31) == 31) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");     // (vmcnt counts to 63)
-    }
+    ctl_copy_issue(dst, src, n16, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -426,6 +445,8 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
     float *xs = (float *)(lds + GG::L_XS);
     uint8_t *act = lds + GG::L_ACT;
     float *res = (float *)(lds + GG::L_RES);
+    float *nws = xs + E;                                          // the norm weights, staged beside xs
+    float *sscale = (float *)(lds + GG::L_MISC);                  // the rms_norm scale
     uint16_t *sq = (uint16_t *)(lds + GG::L_Q), *snk = sq + G * D, *snv = snk + D;
 
     const int np = a.pos[0];
@@ -461,13 +482,15 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
         // ======================================================== Q: attn_norm -> q|k|v -> RoPE, f16 stores
         ESTAMP(0)
         if (ctl) {
-            if (l > 0) poll(counter(a.sync, l - 1, S_D), 8, GG::NB, err, 1u, lane);
+            ctl_fetch(nws, L.attn_norm, E / 4, lane);
+            ctl_gather8(xs, a.x, counter(a.sync, l > 0 ? l - 1 : 0, S_D), E / 4, GG::NB / 8, l > 0, err, 1u, lane);
             ESTAMP(1)
-            ctl_norm<E>(a.x, L.attn_norm, a.eps, xs, lane);
+            const float sc = ctl_scale<E>(xs, a.eps, lane);
+            if (lane == 0) *sscale = sc;
             ESTAMP(2)
         }
         __syncthreads();
-        quant_lds<E>(xs, act, tid);
+        quant_lds_norm<E>(xs, nws, *sscale, act, tid);
         __syncthreads();
         ESTAMP(3)
         if (!ctl) {
@@ -499,8 +522,11 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
         };
         __syncthreads();    // (behind the barrier: nothing of the q|k|v dots is live beside them)
         ESTAMP(4)
-        if (nch > 0) dma_chunk(k0, 0);
-        if (nch > 1) dma_chunk(k0 + 64, 1);
+        const int ordq = a.opt & 3;
+        if (ordq == 0) {
+            if (nch > 0) dma_chunk(k0, 0);
+            if (nch > 1) dma_chunk(k0 + 64, 1);
+        }
         if (ctl) {          // RoPE (NORM pairs, the rope table) + f16 q / K / V stores, write-through
             const int n = min(RQ, RG - jq * RQ);
             if (lane < n / 2) {
@@ -521,9 +547,15 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
                 }
                 st_sc1_u32(dst, pk);
             }
-            arrive(counter(a.sync, l, S_Q + hk), lane);
-            ESTAMP(5)
+            if (ordq != 1) arrive(counter(a.sync, l, S_Q + hk), lane);
         }
+        if (ordq != 0) {
+            __syncthreads();
+            if (nch > 0) dma_chunk(k0, 0);
+            if (nch > 1) dma_chunk(k0 + 64, 1);
+            if (ctl && ordq == 1) arrive(counter(a.sync, l, S_Q + hk), lane);
+        }
+        if (ctl) { ESTAMP(5) }
         // ======================================================== A: split jq of kv head hk
         if (ctl) {
             poll(counter(a.sync, l, S_Q + hk), 1, CG, err, 2u, lane);
@@ -652,6 +684,10 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
             float *cw = xs;                               // [2][NS] split weights
             float *cres = xs + 2 * NS;                    // [256] merged output
             float Lh;
+            // the two heads' partials [2][NS][D] into LDS by DMA (32 KB: no registers), issued first: the (m, l) loads
+            // below return behind them
+            float *cpo = xs + 1024;
+            ctl_copy_issue(cpo, a.part_o + (int64_t)(2 * u) * NS * D, 2 * NS * D / 4, lane);
             {
                 float2 ml = make_float2(-INFINITY, 0.0f);
                 if (c < NS) {
@@ -667,9 +703,7 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
                 t += dpp_f<0xB1>(t); t += dpp_f<0x4E>(t); t += dpp_f<0x141>(t); t += dpp_f<0x140>(t);
                 Lh = xsum16(t);
             }
-            // the two heads' partials [2][NS][D] into LDS by DMA (32 KB: no registers), then the weighted sums
-            float *cpo = xs + 1024;
-            ctl_copy(cpo, a.part_o + (int64_t)(2 * u) * NS * D, 2 * NS * D / 4, lane);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             float4 O0 = make_float4(0, 0, 0, 0), O1 = O0, O2 = O0, O3 = O0;
             auto fma4 = [](float w, float4 o, float4 &acc) {
                 acc.x = fmaf(w, o.x, acc.x); acc.y = fmaf(w, o.y, acc.y); acc.z = fmaf(w, o.z, acc.z); acc.w = fmaf(w, o.w, acc.w);
@@ -747,6 +781,15 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
         };
         __syncthreads();    // (issued behind the barrier: not live beside wo's rows and activation)
         ESTAMP(14)
+        const int ordo = (a.opt >> 2) & 3;
+        if (ctl) {
+            if (lane < RO && b * RO + lane < E) {
+                xres = __fadd_rn(res[lane], xres);
+                st_sc1_f32(a.x + b * RO + lane, xres);
+            }
+            if (ordo != 1) arrive(counter(a.sync, l, S_O + (b >> 5)), lane);
+        }
+        if (ordo != 0) __syncthreads();
 #pragma unroll
         for (int i = 0; i < GG::WG; ++i) {
             const int it = gs_ + i;
@@ -756,22 +799,20 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
             else zero_row<E>(wg[i]);
         }
         if (ctl) {
-            if (lane < RO && b * RO + lane < E) {
-                xres = __fadd_rn(res[lane], xres);
-                st_sc1_f32(a.x + b * RO + lane, xres);
-            }
-            arrive(counter(a.sync, l, S_O + (b & 7)), lane);
+            if (ordo == 1) arrive(counter(a.sync, l, S_O + (b >> 5)), lane);
             ESTAMP(15)
         }
         // ======================================================== G: ffn_norm -> gate|up -> silu(g) * u
         if (ctl) {
-            poll(counter(a.sync, l, S_O), 8, GG::NB, err, 5u, lane);
+            ctl_fetch(nws, L.ffn_norm, E / 4, lane);
+            ctl_gather8(xs, a.x, counter(a.sync, l, S_O), E / 4, GG::NB / 8, true, err, 5u, lane);
             ESTAMP(16)
-            ctl_norm<E>(a.x, L.ffn_norm, a.eps, xs, lane);
+            const float sc = ctl_scale<E>(xs, a.eps, lane);
+            if (lane == 0) *sscale = sc;
             ESTAMP(17)
         }
         __syncthreads();
-        quant_lds<E>(xs, act, tid);
+        quant_lds_norm<E>(xs, nws, *sscale, act, tid);
         __syncthreads();
         ESTAMP(18)
         if (!ctl) {
@@ -801,24 +842,28 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
         Row<F> wd[GG::WD];
         __syncthreads();
         ESTAMP(19)
-#pragma unroll
-        for (int i = 0; i < GG::WD; ++i)
-            if (ds_ + i < de_ && b * RO + ds_ + i < E) load_row<F>(wd[i], L.wd, b * RO + ds_ + i, d6, lane);
-            else zero_row<F>(wd[i]);
+        const int ordg = (a.opt >> 4) & 3;
         if (ctl) {
             const int n = min(RF, F - b * RF);
             if (lane < n) {
                 const float g = res[2 * lane], u = res[2 * lane + 1];
                 st_sc1_f32(a.h + b * RF + lane, (g / (1.0f + expf(-g))) * u);
             }
-            arrive(counter(a.sync, l, S_G + (b & 7)), lane);
+            if (ordg != 1) arrive(counter(a.sync, l, S_G + (b >> 5)), lane);
+        }
+        if (ordg != 0) __syncthreads();
+#pragma unroll
+        for (int i = 0; i < GG::WD; ++i)
+            if (ds_ + i < de_ && b * RO + ds_ + i < E) load_row<F>(wd[i], L.wd, b * RO + ds_ + i, d6, lane);
+            else zero_row<F>(wd[i]);
+        if (ctl) {
+            if (ordg == 1) arrive(counter(a.sync, l, S_G + (b >> 5)), lane);
             ESTAMP(20)
         }
         // ======================================================== D: x += down . Q8_K(h)
         if (ctl) {
-            poll(counter(a.sync, l, S_G), 8, GG::NB, err, 6u, lane);
+            ctl_gather8(xs, a.h, counter(a.sync, l, S_G), F / 4, GG::NB / 8, true, err, 6u, lane);
             ESTAMP(21)
-            ctl_copy(xs, a.h, F / 4, lane);
             ESTAMP(22)
         }
         __syncthreads();
@@ -839,16 +884,21 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
         }
         __syncthreads();
         ESTAMP(24)
-        if (l + 1 < a.nl) issue_qkv<E, GG>(wq, a.layers[l + 1], b, wave, lane);
-        else
-#pragma unroll
-            for (int i = 0; i < GG::MQ; ++i) zero_row<E>(wq[i]);
+        const int ordd = (a.opt >> 6) & 3;
         if (ctl) {
             if (lane < RO && b * RO + lane < E) {
                 xres = __fadd_rn(res[lane], xres);
                 st_sc1_f32(a.x + b * RO + lane, xres);
             }
-            arrive(counter(a.sync, l, S_D + (b & 7)), lane);
+            if (ordd != 1) arrive(counter(a.sync, l, S_D + (b >> 5)), lane);
+        }
+        if (ordd != 0) __syncthreads();
+        if (l + 1 < a.nl) issue_qkv<E, GG>(wq, a.layers[l + 1], b, wave, lane);
+        else
+#pragma unroll
+            for (int i = 0; i < GG::MQ; ++i) zero_row<E>(wq[i]);
+        if (ctl) {
+            if (ordd == 1) arrive(counter(a.sync, l, S_D + (b >> 5)), lane);
             ESTAMP(25)
         }
     }
@@ -904,6 +954,8 @@ extern "C" int kcpp_engine_decode(const void *layers_dev, int nl, float *x, uint
     a.kq_scale = kq_scale;
     a.dbg = g_dbg;
     a.stamps = g_stamps;
+    static const int opt = [] { const char *e = getenv("KCPP_ENGINE_OPT"); return e ? atoi(e) : 0; }();
+    a.opt = opt;
     hipLaunchKernelGGL((k_engine<4096, 14336, 32, 8>), dim3(GG::NB), dim3(NT), GG::LDS_REQ, (hipStream_t)stream, a);
     KCPP_CHECK(hipGetLastError());
     return 0;

@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(256) k_gemv_dec(const DecArgs a) {
     const int64_t nw = (int64_t)gridDim.x * 4;
     const int64_t wid = (int64_t)blockIdx.x * 4 + wave;
     // MoE: this launch's expert slice (index read on the device, wave-uniform)
-    const int64_t eoff = a.eid ? (int64_t)__builtin_amdgcn_readfirstlane(a.eid[0]) * a.ebytes : 0;
+    const int64_t eoff = dec_expert_offset(a);
     const float escale = a.escale ? a.escale[0] : 1.0f;
 
     auto group_rows = [&](int64_t g, int &seg, int64_t &row0) {

@@ -96,7 +96,7 @@ __global__ void __launch_bounds__(256) k_gemv_q4k(const DecArgs a) {
     const int ngroups = (N0 + N1 + N2) / R;
     const int nw = (int)gridDim.x * 4;
     const int wid = (int)blockIdx.x * 4 + wave;
-    const int64_t eoff = a.eid ? (int64_t)__builtin_amdgcn_readfirstlane(a.eid[0]) * a.ebytes : 0;   // MoE slice
+    const int64_t eoff = dec_expert_offset(a);   // MoE slice
     const int abytes = K + K / 256 * 4 + K / 16 * 2;
     const ScaleSel ss = scale_sel(lane & 3);
     // per-lane byte offsets of the unit (it) inside a row: super-block (u >> 2), chunk j = lane & 3

@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     const int ngroups = (N0 + N1 + N2) / R;
     const int nw = (int)gridDim.x * NWV;
     const int wid = (int)blockIdx.x * NWV + wave;
-    const int64_t eoff = a.eid ? (int64_t)__builtin_amdgcn_readfirstlane(a.eid[0]) * a.ebytes : 0;   // MoE slice
+    const int64_t eoff = dec_expert_offset(a);   // MoE slice
     const int abytes = K + K / 256 * 4 + K / 16 * 2;
     const typename T::Lane lc = T::lane_consts(lane);
 

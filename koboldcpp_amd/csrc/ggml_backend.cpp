@@ -347,6 +347,15 @@ const void *native_image(BackendCtx *bc, const kggml_tensor *w, int tt) {
     const int64_t K = w->ne[0], N = w->ne[1] * w->ne[2] * w->ne[3], NS = w->ne[2] * w->ne[3];
     if (tt == w->type && (tt == KT_Q4_K || tt == KT_Q5_K)) return w->data;      // kcpp layout = ggml layout
     kggml_backend_buffer_t buf = w->view_src ? w->view_src->buffer : w->buffer;
+    if (buffer_is_ours(buf) && buf->usage == KGGML_BACKEND_BUFFER_USAGE_WEIGHTS && w->view_src != nullptr) {
+        // a view of a weight: its separate image is packed from ggml bytes, so a root already converted in place goes
+        // back to the ggml layout and keeps separate images from now on (no in-place layout under a live view)
+        BufCtx *c = (BufCtx *)buf->context;
+        hipStreamSynchronize(bc->stream);
+        restore_ggml(c, w->data, nbytes(w));
+        std::lock_guard<std::mutex> lk(g_img_mu);
+        c->shared[w->view_src->data] = 1;
+    }
     if (buffer_is_ours(buf) && buf->usage == KGGML_BACKEND_BUFFER_USAGE_WEIGHTS && w->view_src == nullptr) {
         BufCtx *c = (BufCtx *)buf->context;
         std::lock_guard<std::mutex> lk(g_img_mu);
@@ -662,6 +671,7 @@ bool mul_mat_id(BackendCtx *bc, kggml_tensor *n) {
                 d.x = (const float *)((const char *)b->data + (j % ne11) * b->nb[1] + t * b->nb[2]);
                 d.eid = (const int32_t *)((const char *)ids->data + j * ids->nb[0] + t * ids->nb[1]);
                 d.ebytes = eb;
+                d.n_exp = E;
                 rc = kcpp_gemv_dec(tt, &d, 0, 2, 1, s);
                 if (rc != 0 && (t > 0 || j > 0)) return chk(rc, "expert mat-vec");
             }

@@ -48,7 +48,17 @@ struct DecArgs {
     const float *escale;
     // PRO 0 in the RS kernels: column act_col of an activation buffer holding act_mtot (0 = 1) columns
     int64_t act_mtot, act_col;
+    // MoE: the number of expert slices; an expert id read on the device is clamped to [0, n_exp) so that a bad
+    // router id cannot address past the tensor (the reference asserts, ggml-cuda.cu mul_mat_id); 0 = unchecked
+    int64_t n_exp;
 };
+// the expert slice offset of a DecArgs (0 without an expert id)
+__device__ __forceinline__ int64_t dec_expert_offset(const DecArgs &a) {
+    if (!a.eid) return 0;
+    int e = __builtin_amdgcn_readfirstlane(a.eid[0]);
+    if (a.n_exp > 0) e = e < 0 ? 0 : (e >= (int)a.n_exp ? (int)a.n_exp - 1 : e);
+    return (int64_t)e * a.ebytes;
+}
 extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int rows_per_wave, void *stream);
 // coalesced Q4_K variant (gemv_stream.hip); -3 = not covered
 extern "C" int kcpp_gemv_stream(int type, const void *args, int mode, int pro, void *stream);

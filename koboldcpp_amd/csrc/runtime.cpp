@@ -790,7 +790,7 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
             memset(&a, 0, sizeof a);
             a.K = E; a.x = m->x; a.nw = (const float *)t[5].d; a.eps = hp.eps; a.nseg = 1;
             a.W[0] = (const uint8_t *)t[6].d; a.W2 = (const uint8_t *)t[7].d; a.N[0] = F; a.Y[0] = m->h;
-            a.eid = m->moe_ids + j; a.ebytes = (int64_t)t[6].slice_bytes;
+            a.eid = m->moe_ids + j; a.n_exp = hp.n_expert; a.ebytes = (int64_t)t[6].slice_bytes;
             RC(kcpp_gemv_dec(t[6].type, &a, 1, 1, rows_per_wave(F, 1), s));
         } else {
             for (int i = 6; i <= 7; ++i) {
@@ -798,7 +798,7 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
                 memset(&a, 0, sizeof a);
                 a.K = E; a.x = m->x; a.nw = (const float *)t[5].d; a.eps = hp.eps; a.nseg = 1;
                 a.W[0] = (const uint8_t *)t[i].d; a.N[0] = F; a.Y[0] = i == 6 ? m->h : m->qkv;
-                a.eid = m->moe_ids + j; a.ebytes = (int64_t)t[i].slice_bytes;
+                a.eid = m->moe_ids + j; a.n_exp = hp.n_expert; a.ebytes = (int64_t)t[i].slice_bytes;
                 RC(kcpp_gemv_dec(t[i].type, &a, 0, 1, rows_per_wave(F, 0), s));
             }
             RC(kcpp_silu_mul(m->h, m->h, m->qkv, F, s));
@@ -807,7 +807,7 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
         memset(&a, 0, sizeof a);
         a.K = F; a.x = m->h; a.nseg = 1;
         a.W[0] = (const uint8_t *)t[8].d; a.N[0] = E; a.Y[0] = m->moe_slots + j * E;
-        a.eid = m->moe_ids + j; a.ebytes = (int64_t)t[8].slice_bytes; a.escale = m->moe_w + j;
+        a.eid = m->moe_ids + j; a.n_exp = hp.n_expert; a.ebytes = (int64_t)t[8].slice_bytes; a.escale = m->moe_w + j;
         const int rc = kcpp_gemv_dec(t[8].type, &a, 0, 2, rows_per_wave(E, 0), s);
         if (rc == -8) { g_err = "MoE down projection: n_ff beyond the fused mat-vec's K budget"; return rc; }
         RC(rc);

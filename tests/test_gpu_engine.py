@@ -148,8 +148,9 @@ def test_engine_phases_vs_kernels(K, v6, d6, NP):
     rc = K._L.kcpp_engine_decode(lay.data_ptr(), 1, A["x"].data_ptr(), A["q16"].data_ptr(), A["ws"].data_ptr(),
                                  A["act"].data_ptr(), A["h"].data_ptr(), sync.data_ptr(), pos.data_ptr(),
                                  rope.data_ptr(), 1e-5, scale, E_, F_, H_, HKV_, s)
-    assert rc == 0
     torch.cuda.synchronize()
+    K._L.kcpp_engine_set_debug(None)
+    assert rc == 0
     assert int(sync.view(torch.int32)[-32].item()) == 0, "hand-off timeout"
     # ---- the launch chain's kernels
     B = bufs()
@@ -181,16 +182,10 @@ def test_engine_phases_vs_kernels(K, v6, d6, NP):
         return po, pml
     poA, pmlA = parts(A["ws"])
     poB, pmlB = parts(B["ws"])
-    dm = np.abs(pmlA - pmlB)
-    fin = np.isfinite(pmlB[..., 0])
-    print("M diff", np.abs(pmlA[..., 0] - pmlB[..., 0])[fin].max(), "L rel", (np.abs(pmlA[..., 1] - pmlB[..., 1]) / pmlB[..., 1])[fin].max())
-    # O is unnormalised per split: compare O / L
-    oa = poA / pmlA[..., 1:2]
-    ob = poB / pmlB[..., 1:2]
-    do = np.abs(oa - ob)
-    print("O/L diff max", np.nanmax(do), "at", np.unravel_index(np.nanargmax(do), do.shape))
-
-    assert np.array_equal(poA.view(np.uint32), poB.view(np.uint32)) and np.array_equal(pmlA.view(np.uint32), pmlB.view(np.uint32))
+    assert np.array_equal(poA.view(np.uint32), poB.view(np.uint32)), "split partials O"
+    assert np.array_equal(pmlA.view(np.uint32), pmlB.view(np.uint32)), "split partials (m, l)"
+    dd = dbg.cpu().numpy()
+    attn_ref = B["attn"].cpu().numpy()
     assert np.array_equal(dd[:E_].view(np.uint32), attn_ref.view(np.uint32)), "merged attention"
     K.call("kcpp_quantize_act", 15, B["attn"].data_ptr(), E_, B["act"].data_ptr(), E_, 1, s)
     torch.cuda.synchronize()

@@ -56,6 +56,15 @@ def main():
             d = (a - b)[ok]
             print("  %-22s %7.2f  (p90 %7.2f)" % (NAMES[k], np.median(d), np.percentile(d, 90)))
             prev = k
+    # the critical path: each stamp against the layer's earliest top, median / max over workgroups
+    print("timeline since the layer's first top (us): median over layers of [median, max] over workgroups")
+    t0 = s[:, 1:, 0].min(axis=0)
+    for k in pts:
+        a = s[:, 1:, k]
+        ok = (a > 0).all(axis=0)
+        if ok.any():
+            r = a[:, ok] - t0[ok]
+            print("  %-22s %7.2f %7.2f" % (NAMES[k], np.median(np.median(r, axis=0)), np.median(r.max(axis=0))))
     tot = s[:, 1:, 25] - s[:, 1:, 0]
     lay = s[:, 2:, 0] - s[:, 1:-1, 0]
     print("layer (top to top): median %.2f us, max over workgroups per layer median %.2f us" %
