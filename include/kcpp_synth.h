@@ -29,12 +29,19 @@
 enum kcpp_type {
     KT_F32 = 0, KT_F16 = 1, KT_Q4_0 = 2, KT_Q4_1 = 3, KT_Q5_0 = 6, KT_Q5_1 = 7,
     KT_Q8_0 = 8, KT_Q8_1 = 9, KT_Q2_K = 10, KT_Q3_K = 11, KT_Q4_K = 12,
-    KT_Q5_K = 13, KT_Q6_K = 14, KT_Q8_K = 15, KT_IQ4_NL = 20, KT_IQ4_XS = 23, KT_BF16 = 30,
+    KT_Q5_K = 13, KT_Q6_K = 14, KT_Q8_K = 15, KT_IQ2_XXS = 16, KT_IQ2_XS = 17, KT_IQ3_XXS = 18, KT_IQ1_S = 19,
+    KT_IQ4_NL = 20, KT_IQ3_S = 21, KT_IQ2_S = 22, KT_IQ4_XS = 23, KT_IQ1_M = 29, KT_BF16 = 30,
     /* GPU-internal row-major decode layouts of Q4_K / Q6_K (same bytes per row, re-arranged inside
        each row so the single-token mat-vec reads 1 KiB-contiguous wave loads; csrc/kcpp_common.h).
        Not ggml ids: they never leave the device library. */
     KT_Q4_K_RS = 112, KT_Q6_K_RS = 114
 };
+
+/* the lattice-grid types (IQ1 / IQ2 / IQ3): ggml layout on the device, decoded through the code books */
+KS_FN int is_iq_grid_type(int t) {
+    return t == KT_IQ2_XXS || t == KT_IQ2_XS || t == KT_IQ2_S || t == KT_IQ3_XXS || t == KT_IQ3_S || t == KT_IQ1_S ||
+           t == KT_IQ1_M;
+}
 
 /* the ggml type whose blocks a layout holds */
 KS_FN int ks_base_type(int type) {
@@ -100,6 +107,13 @@ KS_FN int ks_block_bytes(int type) {
         case KT_Q5_K: return 176;
         case KT_Q6_K: case KT_Q6_K_RS: return 210;
         case KT_Q8_K: return 292;
+        case KT_IQ2_XXS: return 66;      /* block_iq2_xxs .. block_iq1_m, ggml-common.h:340-405 */
+        case KT_IQ2_XS: return 74;
+        case KT_IQ2_S: return 82;
+        case KT_IQ3_XXS: return 98;
+        case KT_IQ3_S: return 110;
+        case KT_IQ1_S: return 50;
+        case KT_IQ1_M: return 56;
         default: return 0;
     }
 }
@@ -152,6 +166,28 @@ KS_FN void ks_fill_block(int type, uint64_t seed, uint64_t tid, uint64_t b, uint
             h0 = ks_f32_to_f16(1.6e-5f * (0.75f + 0.5f * u0));
             memcpy(dst, &h0, 2);
             break;
+        /* the grid types (every index / sign / scale bit pattern is a valid code): d scaled for std ~0.02 */
+        case KT_IQ2_XXS: case KT_IQ2_XS: case KT_IQ2_S:   /* w = d (0.5 + ls) / 4 grid, grid in {8, 25, 43} */
+            h0 = ks_f32_to_f16(3.0e-4f * (0.75f + 0.5f * u0));
+            memcpy(dst, &h0, 2);
+            break;
+        case KT_IQ3_XXS:    /* w = d (0.5 + ls) / 2 grid, grid 4..62 */
+            h0 = ks_f32_to_f16(1.4e-4f * (0.75f + 0.5f * u0));
+            memcpy(dst, &h0, 2);
+            break;
+        case KT_IQ3_S:      /* w = d (1 + 2 ls) grid, grid 1..15 */
+            h0 = ks_f32_to_f16(1.3e-4f * (0.75f + 0.5f * u0));
+            memcpy(dst, &h0, 2);
+            break;
+        case KT_IQ1_S:      /* w = d (2 ls + 1) (grid +- 1/8), grid in {-1, 0, 1} */
+            h0 = ks_f32_to_f16(2.7e-3f * (0.75f + 0.5f * u0));
+            memcpy(dst, &h0, 2);
+            break;
+        case KT_IQ1_M: {    /* as IQ1_S; the f16 scale lives in the top nibbles of the four scale words */
+            h0 = ks_f32_to_f16(2.7e-3f * (0.75f + 0.5f * u0));
+            uint8_t *sc = dst + 48;
+            for (int j = 0; j < 4; ++j) sc[2 * j + 1] = (uint8_t)((sc[2 * j + 1] & 0x0F) | (((h0 >> (4 * j)) & 0xF) << 4));
+        } break;
         case KT_Q4_K: case KT_Q5_K: {
             float d = (type == KT_Q4_K ? 1.35e-4f : 6.7e-5f) * (0.75f + 0.5f * u0);
             float dm = (type == KT_Q4_K ? 1.0e-3f : 1.0e-3f) * (0.75f + 0.5f * u1);

@@ -338,10 +338,33 @@ __device__ __forceinline__ void ctl_fetch(void *dst, const void *src, int n16, i
 __device__ __forceinline__ void ctl_gather8(void *dst, const void *src, const unsigned *c0, int n16, unsigned per,
                                             bool wait, unsigned *err, unsigned code, int lane) {
     const int W = n16 / 8;
-    for (int sh = 0; sh < 8; ++sh) {
-        if (wait) poll(c0 + sh * 32, 1, per, err, code, lane);
-        for (int k = 0; 64 * k < W; ++k)
-            dma16_sc1((const uint8_t *)src + 16 * (sh * W + 64 * k + lane), (uint8_t *)dst + 16 * (sh * W + 64 * k));
+    unsigned done = wait ? 0u : 0xffu;
+    if (!wait)
+        for (int k = 0; 64 * k < n16; ++k)
+            dma16_sc1((const uint8_t *)src + 16 * (64 * k + lane), (uint8_t *)dst + 1024 * k);
+    for (unsigned it = 0; done != 0xffu; ++it) {
+        // one load of all 8 counters per round; the shards that completed since the last round are requested
+        const unsigned v = lane < 8 ? __hip_atomic_load(c0 + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        const unsigned ready = (unsigned)__ballot(lane < 8 && (int)(v - per) >= 0) & ~done & 0xffu;
+        for (unsigned m = ready; m; m &= m - 1) {
+            const int sh = __builtin_ctz(m);
+            for (int k = 0; 64 * k < W; ++k)
+                dma16_sc1((const uint8_t *)src + 16 * (sh * W + 64 * k + lane), (uint8_t *)dst + 16 * (sh * W + 64 * k));
+        }
+        done |= ready;
+        if (ready) continue;
+        if ((it & 31) == 31 &&
+            __builtin_amdgcn_readfirstlane(__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0u)
+            break;                                        // another workgroup gave up: drain
+        if (it > kSpinMax) {
+            if (lane == 0 && __hip_atomic_fetch_or(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                __hip_atomic_store(err + 1, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(err + 2, per, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(err + 3, (unsigned)blockIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -496,14 +519,17 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
         if (!ctl) {
             ActE<E> xa;
             load_act<E>(xa, act, lane, true, L.tv != 0);
-#pragma unroll
+            // (rolled, the row buffers rotating: the whole layer loop has to fit the instruction cache)
+#pragma unroll 1
             for (int i = 0; i < GG::MQ; ++i) {
                 const int gr = jq * RQ + qs_ + i;
                 if (qs_ + i < qe_ && gr < RG) {
                     const bool q6 = gr >= (G + 1) * D && L.tv != 0;
-                    const float v = dot_row<E>(wq[i], xa, q6, lane);
+                    const float v = dot_row<E>(wq[0], xa, q6, lane);
                     if (lane == 0) res[qs_ + i] = v;
                 }
+#pragma unroll
+                for (int j = 0; j + 1 < GG::MQ; ++j) wq[j] = wq[j + 1];
             }
         }
         // compute waves: the attention's cached keys (not this token's: this phase writes it) go in flight by LDS-DMA
@@ -818,19 +844,23 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
         if (!ctl) {
             ActE<E> xa;
             load_act<E>(xa, act, lane, true, false);
+            static_assert(GG::MG % GG::WG == 0, "gate|up ring");
+#pragma unroll 1
+            for (int i0 = 0; i0 < GG::MG; i0 += GG::WG) {
 #pragma unroll
-            for (int i = 0; i < GG::MG; ++i) {
-                const int it = gs_ + i;
-                const uint8_t *W; int row;
-                glu_item(it, W, row);
-                if (it < ge_ && row < F) {
-                    const float v = dot_row<E>(wg[i % GG::WG], xa, false, lane);
-                    if (lane == 0) res[it - 0] = v;
-                    const int it2 = it + GG::WG;
-                    const uint8_t *W2; int row2;
-                    glu_item(it2, W2, row2);
-                    if (i + GG::WG < GG::MG && it2 < ge_ && row2 < F) load_row<E>(wg[i % GG::WG], W2, row2, false, lane);
-                    else zero_row<E>(wg[i % GG::WG]);
+                for (int j = 0; j < GG::WG; ++j) {
+                    const int i = i0 + j, it = gs_ + i;
+                    const uint8_t *W; int row;
+                    glu_item(it, W, row);
+                    if (it < ge_ && row < F) {
+                        const float v = dot_row<E>(wg[j], xa, false, lane);
+                        if (lane == 0) res[it] = v;
+                        const int it2 = it + GG::WG;
+                        const uint8_t *W2; int row2;
+                        glu_item(it2, W2, row2);
+                        if (i + GG::WG < GG::MG && it2 < ge_ && row2 < F) load_row<E>(wg[j], W2, row2, false, lane);
+                        else zero_row<E>(wg[j]);
+                    }
                 }
             }
         }
@@ -871,15 +901,16 @@ __global__ void __launch_bounds__(512, 1) k_engine(const Args a) {
         __syncthreads();
         ESTAMP(23)
         if (!ctl) {
-#pragma unroll
+            static_assert(GG::WD == 1, "down: one row in flight per wave");
+#pragma unroll 1
             for (int i = 0; i < GG::MO; ++i)
                 if (ds_ + i < de_ && b * RO + ds_ + i < E) {
-                    const float v = dot_row_lds<F>(wd[i % GG::WD], act, d6, lane);
+                    const float v = dot_row_lds<F>(wd[0], act, d6, lane);
                     if (lane == 0) res[ds_ + i] = v;
-                    if (i + GG::WD < GG::MO && ds_ + i + GG::WD < de_ && b * RO + ds_ + i + GG::WD < E)
-                        load_row<F>(wd[i % GG::WD], L.wd, b * RO + ds_ + i + GG::WD, d6, lane);
+                    if (i + 1 < GG::MO && ds_ + i + 1 < de_ && b * RO + ds_ + i + 1 < E)
+                        load_row<F>(wd[0], L.wd, b * RO + ds_ + i + 1, d6, lane);
                     else
-                        zero_row<F>(wd[i % GG::WD]);
+                        zero_row<F>(wd[0]);
                 }
         }
         __syncthreads();

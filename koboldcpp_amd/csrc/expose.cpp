@@ -117,7 +117,7 @@ const char *tname(int il, int j) {
 
 bool supported_type(int t) {
     return t == KT_F32 || t == KT_F16 || t == KT_Q4_0 || t == KT_Q4_1 || t == KT_Q5_0 || t == KT_Q5_1 || t == KT_Q8_0 || t == KT_Q2_K || t == KT_Q3_K || t == KT_Q4_K || t == KT_Q5_K ||
-           t == KT_IQ4_NL || t == KT_IQ4_XS ||
+           t == KT_IQ4_NL || t == KT_IQ4_XS || t == KT_IQ2_XXS || t == KT_IQ2_XS || t == KT_IQ2_S || t == KT_IQ3_XXS || t == KT_IQ3_S || t == KT_IQ1_S || t == KT_IQ1_M ||
            t == KT_Q6_K;
 }
 

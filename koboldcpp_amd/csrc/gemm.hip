@@ -21,6 +21,7 @@
 // conflict-free); each wave owns 32 tokens x 64 rows (two 32x32 MFMA tiles).
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
+#include "iq_grid.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -355,6 +356,21 @@ __device__ __forceinline__ void stage_weights(SM &S, const uint8_t *__restrict__
             }
         }
         if (c == 0) S.wd[nl][0] = h2f((uint16_t)(hv.x & 0xFFFF));
+    } else if constexpr (kIqGrid<TYPE>) {
+        // the grid types (iq_grid.h, ggml layout): sub-blocks 2c, 2c+1; codes biased to bytes (+128), times the group's
+        // integer scale: exact f16 integers (|code ls| <= 62 x 31); d C per super-block
+        const uint8_t *blk = W + (n * bpr + sb) * ks_block_bytes(TYPE);
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+            const int ib = 2 * c + bb;
+            IqSub q;
+            iq_sub<TYPE>(blk, ib, q);
+#pragma unroll
+            for (int l = 0; l < 4; ++l)
+                S.bf[0][bslot(nl, 32 * ib + 8 * l)] = frag8(q.v[2 * l] ^ 0x80808080u, q.v[2 * l + 1] ^ 0x80808080u,
+                                                           (float)q.ls[l], 128.0f);
+        }
+        if (c == 0) S.wd[nl][0] = iq_d<TYPE>(blk) * iq_const<TYPE>();
     } else {   // Q8_0: int8 -> (q ^ 0x80) = q + 128 as a byte
 #pragma unroll
         for (int bb = 0; bb < 2; ++bb) {
@@ -1849,7 +1865,9 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     float *up = (float *)(w8 + o_up);
     const int vt = vec_dot_type(type);
     const int gv = gemm_variant();
-    if ((type == KT_Q4_1 || type == KT_Q5_1 || type == KT_IQ4_NL || type == KT_IQ4_XS) && (M <= 16 || gv == 20)) {
+    const bool iqg = type == KT_IQ2_XXS || type == KT_IQ2_XS || type == KT_IQ2_S || type == KT_IQ3_XXS ||
+                     type == KT_IQ3_S || type == KT_IQ1_S || type == KT_IQ1_M;
+    if ((type == KT_Q4_1 || type == KT_Q5_1 || type == KT_IQ4_NL || type == KT_IQ4_XS || iqg) && (M <= 16 || gv == 20)) {
         // the legacy Q8_1-activation types (Q4_1 / Q5_1 files) and the code-book types (IQ4_NL / IQ4_XS) at small
         // batch: the exact mat-vec over groups of 8 columns (one pass over the weights each); past 16 columns the
         // MFMA GEMM below is faster (tools/gemm_lowbit_ab.py: Q4_1 4096 x 14336 at 16 / 37 / 512 tokens: mat-vec
@@ -2045,6 +2063,10 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         case KT_Q5_1: hipLaunchKernelGGL(k_gemm<KT_Q5_1>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, s81, part, Mp); break;
         case KT_IQ4_NL: hipLaunchKernelGGL(k_gemm<KT_IQ4_NL>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, nullptr, part, Mp); break;
         case KT_IQ4_XS: hipLaunchKernelGGL(k_gemm<KT_IQ4_XS>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, nullptr, part, Mp); break;
+#define KCPP_IQ_GEMM(T) \
+        case T: hipLaunchKernelGGL(k_gemm<T>, grid, dim3(256), 0, s, (const uint8_t *)w, K, N, a16, dy, bs16, M, y, ly, r, lr, nullptr, part, Mp); break;
+        KCPP_IQ_CASES(KCPP_IQ_GEMM)
+#undef KCPP_IQ_GEMM
         default: return -3;
         }
         KCPP_CHECK(hipGetLastError());

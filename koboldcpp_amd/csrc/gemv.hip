@@ -137,6 +137,7 @@ int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         KCPP_T(KT_IQ4_NL)
         KCPP_T(KT_IQ4_XS)
         KCPP_T(KT_Q8_0)
+        KCPP_IQ_CASES(KCPP_T)
     default: return -3;
     }
 #undef KCPP_T

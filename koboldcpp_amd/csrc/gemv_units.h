@@ -3,6 +3,7 @@
 // ggml-quants.c:3922,5519,7714,8282,8919).  Shared by the mat-vec kernels.
 #pragma once
 #include "kcpp_common.h"
+#include "iq_grid.h"
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 // streamed-once weight loads: nontemporal (MI355X_MICROARCH.md "nt-weights")
@@ -176,6 +177,24 @@ template <> struct Unit<KT_Q8_0> {
         d = *(const uint16_t *)(base + nb * 32 + b * 2);
     }
 };
+
+// ---- the grid types (iq_grid.h, ggml layout): unit u = sub-blocks 2j, 2j+1 (j = u & 3) of super-block u >> 2,
+// decoded at load into signed int8 codes and integer group scales
+template <int T> struct UnitIQ {
+    static constexpr int ELEMS = 64;
+    IqSub s[2];
+    float dw;                                  // d_w * C
+    __device__ __forceinline__ void load(const uint8_t *row, int64_t, int u) {
+        const uint8_t *blk = row + (int64_t)(u >> 2) * ks_block_bytes(T);
+        const int j = u & 3;
+        iq_sub<T>(blk, 2 * j, s[0]);
+        iq_sub<T>(blk, 2 * j + 1, s[1]);
+        dw = iq_d<T>(blk) * iq_const<T>();     // (times a power of two: exact)
+    }
+};
+#define KCPP_IQ_UNIT(T) template <> struct Unit<T> : UnitIQ<T> {};
+KCPP_IQ_CASES(KCPP_IQ_UNIT)
+#undef KCPP_IQ_UNIT
 
 __device__ __forceinline__ int byte_of(uint32_t w, int k) { return (w >> (8 * k)) & 0xFF; }
 __device__ __forceinline__ uint32_t u4(const uint4 &v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w)); }
@@ -464,11 +483,33 @@ __device__ __forceinline__ float unit_dot(const Unit<KT_Q8_0> &w, int, const Act
     return __fmul_rn((float)s, __fmul_rn(h2f(w.d), x.d));
 }
 
+// the grid types against Q8_K (ggml_vec_dot_iq*_q8_K generic branches, ggml-quants.c:9606-12468): per group of 8 the
+// integer dot of codes and activation bytes, times the group's integer scale, summed in int32 over the unit, then
+// (d_w C) d_a once
+template <int T>
+__device__ __forceinline__ float iq_unit_dot(const UnitIQ<T> &w, const ActK &x) {
+    int tot = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int l = 0; l < 4; ++l) {
+            int p = sdot4((int)w.s[h].v[2 * l], ai(x, 8 * h + 2 * l), 0);
+            p = sdot4((int)w.s[h].v[2 * l + 1], ai(x, 8 * h + 2 * l + 1), p);
+            tot += w.s[h].ls[l] * p;
+        }
+    return __fmul_rn(__fmul_rn(w.dw, x.d), (float)tot);
+}
+#define KCPP_IQ_DOT(T) \
+    __device__ __forceinline__ float unit_dot(const Unit<T> &w, int, const ActK &x) { return iq_unit_dot<T>(w, x); }
+KCPP_IQ_CASES(KCPP_IQ_DOT)
+#undef KCPP_IQ_DOT
+
 // uniform unit loader: native-layout types index by row pointer, SoA types by block index
 template <int TYPE>
 __device__ __forceinline__ void load_unit(Unit<TYPE> &w, const uint8_t *W, int64_t nb, int64_t row, int64_t units_per_row, int u) {
     if constexpr (TYPE == KT_Q4_K) w.load(W + row * (units_per_row / 4) * 144, nb, u);
     else if constexpr (TYPE == KT_Q5_K) w.load(W + row * (units_per_row / 4) * 176, nb, u);
+    else if constexpr (kIqGrid<TYPE>) w.load(W + row * (units_per_row / 4) * ks_block_bytes(TYPE), nb, u);
     else if constexpr (TYPE == KT_Q6_K || TYPE == KT_Q3_K || TYPE == KT_Q2_K || TYPE == KT_IQ4_XS)
         w.load(W, nb, row * (units_per_row / 4), u);
     else w.load(W, nb, row * units_per_row, u);

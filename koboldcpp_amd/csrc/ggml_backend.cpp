@@ -399,7 +399,8 @@ int matmul_layout(int t, int64_t K) {
 }
 bool matmul_quant_ok(int t) {
     return t == KT_Q4_0 || t == KT_Q4_1 || t == KT_Q5_0 || t == KT_Q5_1 || t == KT_Q8_0 || t == KT_Q2_K || t == KT_Q3_K ||
-           t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K || t == KT_IQ4_NL || t == KT_IQ4_XS;
+           t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K || t == KT_IQ4_NL || t == KT_IQ4_XS ||
+           t == KT_IQ2_XXS || t == KT_IQ2_XS || t == KT_IQ2_S || t == KT_IQ3_XXS || t == KT_IQ3_S || t == KT_IQ1_S || t == KT_IQ1_M;
 }
 
 // ------------------------------------------------------------------ split buffers (LLAMA_SPLIT_MODE_ROW)

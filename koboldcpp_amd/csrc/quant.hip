@@ -6,6 +6,7 @@
 // Dequantization mirrors dequantize_row_* (ggml-quants.c:1523,1617,2556,2764,2978).
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
+#include "iq_grid.h"
 
 // ---------------------------------------------------------------- weight layout
 // place one ggml-layout block (src) into the kcpp GPU layout at block index b (bpr blocks per row)
@@ -347,6 +348,23 @@ __global__ void k_dequant(int type, const uint8_t *__restrict__ src, float *__re
     if (b >= nb) return;
     deq_block(type, src, nb, bpr, b, y + b * ks_block_elems(type));
 }
+// the grid types (ggml layout): one thread per 32-element sub-block
+template <int T>
+__global__ void k_dequant_iq(const uint8_t *__restrict__ src, float *__restrict__ y, int64_t nsub) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nsub) return;
+    iq_deq_sub<T>(src + (i >> 3) * ks_block_bytes(T), (int)(i & 7), y + 32 * i);
+}
+// get_rows of a grid type: one thread per sub-block of the selected row
+template <int T>
+__global__ void k_get_rows_iq(const uint8_t *__restrict__ src, int64_t K, int64_t N, const int32_t *__restrict__ ids,
+                              float *__restrict__ y, int64_t ldy) {
+    const int64_t t = blockIdx.y;
+    const int64_t r = min(max((int64_t)ids[t], (int64_t)0), N - 1);
+    const int64_t nsub = K / 32;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nsub; i += (int64_t)gridDim.x * blockDim.x)
+        iq_deq_sub<T>(src + (r * (K / 256) + (i >> 3)) * ks_block_bytes(T), (int)(i & 7), y + t * ldy + 32 * i);
+}
 
 // get_rows: one workgroup per token; thread i dequantizes element chunks of 8 of the selected row.
 // K-quant element e of super-block sb uses the same formulas as deq_block (ggml-quants.c:2556-3006).
@@ -546,6 +564,17 @@ int kcpp_weight_synth(int type, uint64_t seed, uint64_t tid, void *dst, int64_t 
 
 int kcpp_dequantize(int type, const void *w, float *y, int64_t K, int64_t N, void *stream) {
     const int64_t nb = kl_nblocks(type, K, N);
+    switch (type) {
+#define KCPP_IQ_DEQ(T)                                                                                             \
+    case T:                                                                                                        \
+        hipLaunchKernelGGL(k_dequant_iq<T>, dim3((unsigned)((8 * nb + 127) / 128)), dim3(128), 0, (hipStream_t)stream, \
+                           (const uint8_t *)w, y, 8 * nb);                                                         \
+        KCPP_CHECK(hipGetLastError());                                                                             \
+        return 0;
+        KCPP_IQ_CASES(KCPP_IQ_DEQ)
+#undef KCPP_IQ_DEQ
+    default: break;
+    }
     hipLaunchKernelGGL(k_dequant, dim3((unsigned)((nb + 127) / 128)), dim3(128), 0, (hipStream_t)stream, type,
                        (const uint8_t *)w, y, nb, K / ks_block_elems(type));
     KCPP_CHECK(hipGetLastError());
@@ -587,6 +616,18 @@ int kcpp_quantize_act_glu(const float *x, int64_t ldx, int64_t uoff, void *out, 
 int kcpp_get_rows(int type, const void *w, int64_t K, int64_t N, const int32_t *ids, int64_t T, float *y, int64_t ldy,
                   void *stream) {
     if (type == KT_Q4_K_RS || type == KT_Q6_K_RS) return -2;
+    switch (type) {
+#define KCPP_IQ_ROWS(TT)                                                                                            \
+    case TT:                                                                                                        \
+        if (K % 256) return -1;                                                                                    \
+        hipLaunchKernelGGL(k_get_rows_iq<TT>, dim3((unsigned)((K / 32 + 127) / 128), (unsigned)T), dim3(128), 0,    \
+                           (hipStream_t)stream, (const uint8_t *)w, K, N, ids, y, ldy);                            \
+        KCPP_CHECK(hipGetLastError());                                                                             \
+        return 0;
+        KCPP_IQ_CASES(KCPP_IQ_ROWS)
+#undef KCPP_IQ_ROWS
+    default: break;
+    }
     hipLaunchKernelGGL(k_get_rows, dim3((unsigned)((K + 255) / 256), (unsigned)T), dim3(256), 0, (hipStream_t)stream, type,
                        (const uint8_t *)w, K, N, ids, y, ldy);
     KCPP_CHECK(hipGetLastError());

@@ -304,8 +304,9 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     }
     types = m->types.data();
     for (int idx = 0; idx < n_tensors(*hp); ++idx)
-        m->q81 |= types[idx] == KT_Q4_1 || types[idx] == KT_Q5_1 || types[idx] == KT_IQ4_NL || types[idx] == KT_IQ4_XS;
-    if (m->q81 && hp->n_expert > 0) { g_err = "Q4_1 / Q5_1 / IQ4 MoE models are not supported"; delete m; return nullptr; }
+        m->q81 |= types[idx] == KT_Q4_1 || types[idx] == KT_Q5_1 || types[idx] == KT_IQ4_NL || types[idx] == KT_IQ4_XS ||
+                  is_iq_grid_type(types[idx]);
+    if (m->q81 && hp->n_expert > 0) { g_err = "Q4_1 / Q5_1 / IQ MoE models are not supported"; delete m; return nullptr; }
     m->device = device; m->il0 = il0; m->il1 = il1; m->has_embed = has_embed; m->has_output = has_output;
     m->ub = max_ubatch > 0 ? max_ubatch : 512;
     m->fa_exact = getenv("KCPP_FA_EXACT") && atoi(getenv("KCPP_FA_EXACT")) != 0;

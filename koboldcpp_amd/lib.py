@@ -17,6 +17,10 @@ Q4_K_RS, Q6_K_RS = 112, 114
 BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q4_1: (32, 20), Q5_0: (32, 22), Q5_1: (32, 24), Q8_0: (32, 34), Q8_1: (32, 36), Q2_K: (256, 84), Q3_K: (256, 110), Q4_K: (256, 144),
          Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292), Q4_K_RS: (256, 144), Q6_K_RS: (256, 210),
          IQ4_NL: (32, 18), IQ4_XS: (256, 136)}
+# the lattice-grid types (ggml-common.h:340-405), kept in the ggml layout on the device (csrc/iq_grid.h)
+IQ2_XXS, IQ2_XS, IQ3_XXS, IQ1_S, IQ3_S, IQ2_S, IQ1_M = 16, 17, 18, 19, 21, 22, 29
+BLOCK.update({IQ2_XXS: (256, 66), IQ2_XS: (256, 74), IQ2_S: (256, 82), IQ3_XXS: (256, 98), IQ3_S: (256, 110),
+              IQ1_S: (256, 50), IQ1_M: (256, 56)})
 
 
 class KcppError(RuntimeError):

@@ -32,6 +32,29 @@ typedef struct { float d; int8_t qs[256]; int16_t bsums[16]; } blk_q8_K;  /* :33
 typedef struct { uint16_t d; uint8_t qs[16]; } blk_iq4_nl;                                            /* :407 */
 typedef struct { uint16_t d; uint16_t scales_h; uint8_t scales_l[4]; uint8_t qs[128]; } blk_iq4_xs;  /* :413 */
 
+/* the IQ1/IQ2/IQ3 grid formats (ggml-common.h:340-405) */
+typedef struct { uint16_t d; uint16_t qs[32]; } blk_iq2_xxs;
+typedef struct { uint16_t d; uint16_t qs[32]; uint8_t scales[8]; } blk_iq2_xs;
+typedef struct { uint16_t d; uint8_t qs[64]; uint8_t qh[8]; uint8_t scales[8]; } blk_iq2_s;
+typedef struct { uint16_t d; uint8_t qs[96]; } blk_iq3_xxs;
+typedef struct { uint16_t d; uint8_t qs[64]; uint8_t qh[8]; uint8_t signs[32]; uint8_t scales[4]; } blk_iq3_s;
+typedef struct { uint16_t d; uint8_t qs[32]; uint16_t qh[8]; } blk_iq1_s;
+typedef struct { uint8_t qs[32]; uint8_t qh[16]; uint8_t scales[8]; } blk_iq1_m;
+_Static_assert(sizeof(blk_iq2_xxs) == 66 && sizeof(blk_iq2_xs) == 74 && sizeof(blk_iq2_s) == 82, "iq2");
+_Static_assert(sizeof(blk_iq3_xxs) == 98 && sizeof(blk_iq3_s) == 110, "iq3");
+_Static_assert(sizeof(blk_iq1_s) == 50 && sizeof(blk_iq1_m) == 56, "iq1");
+/* the code books, recovered from the reference's dequantization by tools/gen_iq_grids.py */
+#include "../koboldcpp_amd/csrc/iq_grids.h"
+#define G2XXS(i) ((const uint8_t *)(kcpp_iq2xxs_grid + 2 * (i)))
+#define G2XS(i) ((const uint8_t *)(kcpp_iq2xs_grid + 2 * (i)))
+#define G2S(i) ((const uint8_t *)(kcpp_iq2s_grid + 2 * (i)))
+#define G3XXS(i) ((const uint8_t *)(kcpp_iq3xxs_grid + (i)))
+#define G3S(i) ((const uint8_t *)(kcpp_iq3s_grid + (i)))
+#define G1S(i) ((const int8_t *)(kcpp_iq1s_grid + 2 * (i)))
+/* ksigns_iq2xs (ggml-common.h): 7 sign bits plus the even-parity 8th */
+static inline int ksign(int i) { return i | ((__builtin_popcount(i) & 1) << 7); }
+#define IQ1_DELTA 0.125f         /* IQ1S_DELTA / IQ1M_DELTA, ggml-common.h */
+
 /* the IQ4_NL / IQ4_XS non-linear code book, ggml-quants.c:3741 */
 static const int8_t kvalues_iq4nl[16] = {-127, -104, -83, -65, -49, -35, -22, -10, 1, 13, 25, 38, 53, 69, 89, 113};
 
@@ -154,6 +177,128 @@ void orc_dequantize_row(int type, const void *vx, float *y, int64_t k) {
             }
         }
     } return;
+    case KT_IQ2_XXS: {                                /* dequantize_row_iq2_xxs, ggml-quants.c:3504-3528 */
+        const blk_iq2_xxs *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const float d = H2F(x[i].d);
+            for (int ib = 0; ib < 8; ++ib) {
+                uint32_t a[2];
+                memcpy(a, x[i].qs + 4 * ib, 8);
+                const float db = d * (0.5f + (a[1] >> 28)) * 0.25f;
+                for (int l = 0; l < 4; ++l) {
+                    const uint8_t *g = G2XXS(((const uint8_t *)a)[l]);
+                    const int sg = ksign((a[1] >> 7 * l) & 127);
+                    for (int j = 0; j < 8; ++j) *y++ = db * g[j] * (sg & (1 << j) ? -1.f : 1.f);
+                }
+            }
+        }
+    } return;
+    case KT_IQ2_XS: {                                 /* dequantize_row_iq2_xs, ggml-quants.c:3532-3555 */
+        const blk_iq2_xs *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const float d = H2F(x[i].d);
+            for (int ib = 0; ib < 8; ++ib) {
+                const float db[2] = {d * (0.5f + (x[i].scales[ib] & 0xf)) * 0.25f, d * (0.5f + (x[i].scales[ib] >> 4)) * 0.25f};
+                for (int l = 0; l < 4; ++l) {
+                    const uint16_t q = x[i].qs[4 * ib + l];
+                    const uint8_t *g = G2XS(q & 511);
+                    const int sg = ksign(q >> 9);
+                    for (int j = 0; j < 8; ++j) *y++ = db[l / 2] * g[j] * (sg & (1 << j) ? -1.f : 1.f);
+                }
+            }
+        }
+    } return;
+    case KT_IQ2_S: {                                  /* dequantize_row_iq2_s, ggml-quants.c:3559-3587 */
+        const blk_iq2_s *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const float d = H2F(x[i].d);
+            for (int ib = 0; ib < 8; ++ib) {
+                const float db[2] = {d * (0.5f + (x[i].scales[ib] & 0xf)) * 0.25f, d * (0.5f + (x[i].scales[ib] >> 4)) * 0.25f};
+                for (int l = 0; l < 4; ++l) {
+                    const uint8_t *g = G2S(x[i].qs[4 * ib + l] | ((x[i].qh[ib] << (8 - 2 * l)) & 0x300));
+                    const int sg = x[i].qs[32 + 4 * ib + l];
+                    for (int j = 0; j < 8; ++j) *y++ = db[l / 2] * g[j] * (sg & (1 << j) ? -1.f : 1.f);
+                }
+            }
+        }
+    } return;
+    case KT_IQ3_XXS: {                                /* dequantize_row_iq3_xxs, ggml-quants.c:3591-3619 */
+        const blk_iq3_xxs *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const float d = H2F(x[i].d);
+            for (int ib = 0; ib < 8; ++ib) {
+                uint32_t a;
+                memcpy(&a, x[i].qs + 64 + 4 * ib, 4);
+                const float db = d * (0.5f + (a >> 28)) * 0.5f;
+                for (int l = 0; l < 4; ++l) {
+                    const int sg = ksign((a >> 7 * l) & 127);
+                    const uint8_t *g1 = G3XXS(x[i].qs[8 * ib + 2 * l]), *g2 = G3XXS(x[i].qs[8 * ib + 2 * l + 1]);
+                    for (int j = 0; j < 4; ++j) {
+                        y[j] = db * g1[j] * (sg & (1 << j) ? -1.f : 1.f);
+                        y[j + 4] = db * g2[j] * (sg & (1 << (j + 4)) ? -1.f : 1.f);
+                    }
+                    y += 8;
+                }
+            }
+        }
+    } return;
+    case KT_IQ3_S: {                                  /* dequantize_row_iq3_s, ggml-quants.c:3623-3662 */
+        const blk_iq3_s *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const float d = H2F(x[i].d);
+            for (int ib = 0; ib < 8; ++ib) {
+                const int sc = ib & 1 ? x[i].scales[ib / 2] >> 4 : x[i].scales[ib / 2] & 0xf;
+                const float db = d * (1 + 2 * sc);
+                const uint8_t *qs = x[i].qs + 8 * ib, *sg = x[i].signs + 4 * ib;
+                const int qh = x[i].qh[ib];
+                for (int l = 0; l < 4; ++l) {
+                    const uint8_t *g1 = G3S(qs[2 * l] | ((qh << (8 - 2 * l)) & 256));
+                    const uint8_t *g2 = G3S(qs[2 * l + 1] | ((qh << (7 - 2 * l)) & 256));
+                    for (int j = 0; j < 4; ++j) {
+                        y[j] = db * g1[j] * (sg[l] & (1 << j) ? -1.f : 1.f);
+                        y[j + 4] = db * g2[j] * (sg[l] & (1 << (j + 4)) ? -1.f : 1.f);
+                    }
+                    y += 8;
+                }
+            }
+        }
+    } return;
+    case KT_IQ1_S: {                                  /* dequantize_row_iq1_s, ggml-quants.c:3666-3689 */
+        const blk_iq1_s *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            const float d = H2F(x[i].d);
+            for (int ib = 0; ib < 8; ++ib) {
+                const int qh = x[i].qh[ib];
+                const float dl = d * (2 * ((qh >> 12) & 7) + 1);
+                const float delta = qh & 0x8000 ? -IQ1_DELTA : IQ1_DELTA;
+                for (int l = 0; l < 4; ++l) {
+                    const int8_t *g = G1S(x[i].qs[4 * ib + l] | (((qh >> 3 * l) & 7) << 8));
+                    for (int j = 0; j < 8; ++j) *y++ = dl * (g[j] + delta);
+                }
+            }
+        }
+    } return;
+    case KT_IQ1_M: {                                  /* dequantize_row_iq1_m, ggml-quants.c:3691-3739 */
+        const blk_iq1_m *x = vx;
+        for (int64_t i = 0; i < k / QK_K; ++i) {
+            uint16_t sc[4];
+            memcpy(sc, x[i].scales, 8);
+            const float d = H2F((uint16_t)((sc[0] >> 12) | ((sc[1] >> 8) & 0x00f0) | ((sc[2] >> 4) & 0x0f00) | (sc[3] & 0xf000)));
+            for (int ib = 0; ib < 8; ++ib) {
+                const uint8_t *qs = x[i].qs + 4 * ib, *qh = x[i].qh + 2 * ib;
+                const float dl1 = d * (2 * ((sc[ib / 2] >> (6 * (ib % 2) + 0)) & 7) + 1);
+                const float dl2 = d * (2 * ((sc[ib / 2] >> (6 * (ib % 2) + 3)) & 7) + 1);
+                const int idx[4] = {qs[0] | ((qh[0] << 8) & 0x700), qs[1] | ((qh[0] << 4) & 0x700),
+                                    qs[2] | ((qh[1] << 8) & 0x700), qs[3] | ((qh[1] << 4) & 0x700)};
+                const float delta[4] = {qh[0] & 0x08 ? -IQ1_DELTA : IQ1_DELTA, qh[0] & 0x80 ? -IQ1_DELTA : IQ1_DELTA,
+                                        qh[1] & 0x08 ? -IQ1_DELTA : IQ1_DELTA, qh[1] & 0x80 ? -IQ1_DELTA : IQ1_DELTA};
+                for (int l = 0; l < 4; ++l) {
+                    const int8_t *g = G1S(idx[l]);
+                    for (int j = 0; j < 8; ++j) *y++ = (l < 2 ? dl1 : dl2) * (g[j] + delta[l]);
+                }
+            }
+        }
+    } return;
     case KT_Q8_0: {                                   /* ggml-quants.c:1617-1631 */
         const blk_q8_0 *x = vx;
         for (int64_t i = 0; i < k / 32; ++i) {
@@ -270,6 +415,8 @@ int orc_vec_dot_type(int wtype) {
     switch (wtype) {
         case KT_Q4_0: case KT_Q5_0: case KT_Q8_0: case KT_IQ4_NL: return KT_Q8_0;   /* ggml.c:1053 */
         case KT_IQ4_XS: return KT_Q8_K;                                             /* ggml.c:1065 */
+        case KT_IQ2_XXS: case KT_IQ2_XS: case KT_IQ2_S: case KT_IQ3_XXS: case KT_IQ3_S:
+        case KT_IQ1_S: case KT_IQ1_M: return KT_Q8_K;                               /* ggml.c:985-1076 */
         case KT_Q4_1: case KT_Q5_1: return KT_Q8_1;
         case KT_Q2_K: case KT_Q3_K: case KT_Q4_K: case KT_Q5_K: case KT_Q6_K: return KT_Q8_K;
         case KT_F16: return KT_F16;
@@ -625,6 +772,174 @@ static float dot_iq4_xs(int n, const blk_iq4_xs *x, const blk_q8_K *y) {   /* :1
     return sumf;
 }
 
+/* the grid types against Q8_K: the reference's generic branches (integer sub-block dots times the sub-block scale,
+ * summed in int32 per super-block, then (d_w d_a) once per super-block, then the format's constant) */
+static float dot_iq2_xxs(int n, const blk_iq2_xxs *x, const blk_q8_K *y) {  /* ggml-quants.c:9606, generic :9886-9914 */
+    float sumf = 0.f;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const float d = H2F(x[i].d) * y[i].d;
+        const int8_t *q8 = y[i].qs;
+        int32_t bsum = 0;
+        for (int ib = 0; ib < 8; ++ib) {
+            uint32_t a[2];
+            memcpy(a, x[i].qs + 4 * ib, 8);
+            const int ls = 2 * (a[1] >> 28) + 1;
+            int32_t sumi = 0;
+            for (int l = 0; l < 4; ++l, q8 += 8) {
+                const uint8_t *g = G2XXS(((const uint8_t *)a)[l]);
+                const int sg = ksign((a[1] >> 7 * l) & 127);
+                for (int j = 0; j < 8; ++j) sumi += g[j] * q8[j] * (sg & (1 << j) ? -1 : 1);
+            }
+            bsum += sumi * ls;
+        }
+        sumf += d * bsum;
+    }
+    return 0.125f * sumf;
+}
+static float dot_iq2_xs(int n, const blk_iq2_xs *x, const blk_q8_K *y) {    /* :9917, generic branch */
+    float sumf = 0.f;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const float d = H2F(x[i].d) * y[i].d;
+        const int8_t *q8 = y[i].qs;
+        int32_t bsum = 0;
+        for (int ib = 0; ib < 8; ++ib) {
+            const int ls1 = 2 * (x[i].scales[ib] & 0xf) + 1, ls2 = 2 * (x[i].scales[ib] >> 4) + 1;
+            int32_t s1 = 0, s2 = 0;
+            for (int l = 0; l < 4; ++l, q8 += 8) {
+                const uint16_t q = x[i].qs[4 * ib + l];
+                const uint8_t *g = G2XS(q & 511);
+                const int sg = ksign(q >> 9);
+                int32_t t = 0;
+                for (int j = 0; j < 8; ++j) t += g[j] * q8[j] * (sg & (1 << j) ? -1 : 1);
+                if (l < 2) s1 += t; else s2 += t;
+            }
+            bsum += s1 * ls1 + s2 * ls2;
+        }
+        sumf += d * bsum;
+    }
+    return 0.125f * sumf;
+}
+static float dot_iq2_s(int n, const blk_iq2_s *x, const blk_q8_K *y) {      /* :10502, generic branch */
+    float sumf = 0.f;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const float d = H2F(x[i].d) * y[i].d;
+        const int8_t *q8 = y[i].qs;
+        int32_t bsum = 0;
+        for (int ib = 0; ib < 8; ++ib) {
+            const int ls1 = 1 + 2 * (x[i].scales[ib] & 0xf), ls2 = 1 + 2 * (x[i].scales[ib] >> 4);
+            int32_t s1 = 0, s2 = 0;
+            for (int l = 0; l < 4; ++l, q8 += 8) {
+                const uint8_t *g = G2S(x[i].qs[4 * ib + l] | ((x[i].qh[ib] << (8 - 2 * l)) & 0x300));
+                const int sg = x[i].qs[32 + 4 * ib + l];
+                int32_t t = 0;
+                for (int j = 0; j < 8; ++j) t += q8[j] * g[j] * (sg & (1 << j) ? -1 : 1);
+                if (l < 2) s1 += t; else s2 += t;
+            }
+            bsum += ls1 * s1 + ls2 * s2;
+        }
+        sumf += d * bsum;
+    }
+    return 0.125f * sumf;
+}
+static float dot_iq3_xxs(int n, const blk_iq3_xxs *x, const blk_q8_K *y) { /* :10980, generic branch */
+    float sumf = 0.f;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const float d = H2F(x[i].d) * y[i].d;
+        const int8_t *q8 = y[i].qs;
+        int32_t bsum = 0;
+        for (int ib = 0; ib < 8; ++ib) {
+            uint32_t a;
+            memcpy(&a, x[i].qs + 64 + 4 * ib, 4);
+            const int ls = 2 * (a >> 28) + 1;
+            int32_t sumi = 0;
+            for (int l = 0; l < 4; ++l, q8 += 8) {
+                const uint8_t *g1 = G3XXS(x[i].qs[8 * ib + 2 * l]), *g2 = G3XXS(x[i].qs[8 * ib + 2 * l + 1]);
+                const int sg = ksign((a >> 7 * l) & 127);
+                for (int j = 0; j < 4; ++j) {
+                    sumi += g1[j] * q8[j] * (sg & (1 << j) ? -1 : 1);
+                    sumi += g2[j] * q8[j + 4] * (sg & (1 << (j + 4)) ? -1 : 1);
+                }
+            }
+            bsum += sumi * ls;
+        }
+        sumf += d * bsum;
+    }
+    return 0.25f * sumf;
+}
+static float dot_iq3_s(int n, const blk_iq3_s *x, const blk_q8_K *y) {     /* :11303, generic branch */
+    float sumf = 0.f;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const float d = H2F(x[i].d) * y[i].d;
+        const int8_t *q8 = y[i].qs;
+        int32_t bsum = 0;
+        for (int ib = 0; ib < 8; ++ib) {
+            const int ls = 2 * (ib & 1 ? x[i].scales[ib / 2] >> 4 : x[i].scales[ib / 2] & 0xf) + 1;
+            const uint8_t *qs = x[i].qs + 8 * ib, *sg = x[i].signs + 4 * ib;
+            const int qh = x[i].qh[ib];
+            int32_t sumi = 0;
+            for (int l = 0; l < 4; ++l, q8 += 8) {
+                const uint8_t *g1 = G3S(qs[2 * l] | ((qh << (8 - 2 * l)) & 256));
+                const uint8_t *g2 = G3S(qs[2 * l + 1] | ((qh << (7 - 2 * l)) & 256));
+                for (int j = 0; j < 4; ++j) {
+                    sumi += g1[j] * q8[j] * (sg[l] & (1 << j) ? -1 : 1);
+                    sumi += g2[j] * q8[j + 4] * (sg[l] & (1 << (j + 4)) ? -1 : 1);
+                }
+            }
+            bsum += sumi * ls;
+        }
+        sumf += d * bsum;
+    }
+    return sumf;
+}
+static float dot_iq1_s(int n, const blk_iq1_s *x, const blk_q8_K *y) {     /* :11848, generic branch */
+    float sumf = 0;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const int8_t *q8 = y[i].qs;
+        int sumi = 0, sumi1 = 0;
+        for (int ib = 0; ib < 8; ++ib) {
+            const int qh = x[i].qh[ib];
+            const int ls = 2 * ((qh >> 12) & 7) + 1, delta = qh & 0x8000 ? -1 : 1;
+            int lsum = 0;
+            for (int l = 0; l < 4; ++l, q8 += 8) {
+                const int8_t *g = G1S(x[i].qs[4 * ib + l] | (((qh >> 3 * l) & 7) << 8));
+                for (int j = 0; j < 8; ++j) lsum += q8[j] * g[j];
+            }
+            sumi += ls * lsum;
+            sumi1 += ls * delta * (y[i].bsums[2 * ib] + y[i].bsums[2 * ib + 1]);
+        }
+        sumf += H2F(x[i].d) * y[i].d * (sumi + IQ1_DELTA * sumi1);
+    }
+    return sumf;
+}
+static float dot_iq1_m(int n, const blk_iq1_m *x, const blk_q8_K *y) {     /* :12179, generic branch */
+    float sumf = 0;
+    for (int i = 0; i < n / QK_K; ++i) {
+        const int8_t *q8 = y[i].qs;
+        uint16_t sc[4];
+        memcpy(sc, x[i].scales, 8);
+        const float d = H2F((uint16_t)((sc[0] >> 12) | ((sc[1] >> 8) & 0x00f0) | ((sc[2] >> 4) & 0x0f00) | (sc[3] & 0xf000)));
+        int sumi1 = 0, sumi2 = 0;
+        for (int ib = 0; ib < 8; ++ib) {
+            const uint8_t *qs = x[i].qs + 4 * ib, *qh = x[i].qh + 2 * ib;
+            int s1[2] = {0, 0}, s2[2] = {0, 0};
+            for (int l = 0; l < 4; ++l, q8 += 8) {
+                const int8_t *g = G1S(qs[l] | (((uint16_t)qh[l / 2] << (8 - 4 * (l % 2))) & 0x700));
+                const int delta = qh[l / 2] & (0x08 << 4 * (l % 2)) ? -1 : 1;
+                int a = 0, b = 0;
+                for (int j = 0; j < 8; ++j) { a += q8[j] * g[j]; b += q8[j]; }
+                s1[l / 2] += a;
+                s2[l / 2] += b * delta;
+            }
+            const int ls1 = 2 * ((sc[ib / 2] >> (6 * (ib % 2) + 0)) & 7) + 1;
+            const int ls2 = 2 * ((sc[ib / 2] >> (6 * (ib % 2) + 3)) & 7) + 1;
+            sumi1 += s1[0] * ls1 + s1[1] * ls2;
+            sumi2 += s2[0] * ls1 + s2[1] * ls2;
+        }
+        sumf += d * y[i].d * (sumi1 + IQ1_DELTA * sumi2);
+    }
+    return sumf;
+}
+
 static float dot_f16(int n, const uint16_t *x, const uint16_t *y) {        /* ggml.c:2258 */
     double s = 0;
     for (int i = 0; i < n; ++i) s += (double)(H2F(x[i]) * H2F(y[i]));
@@ -645,6 +960,13 @@ float orc_vec_dot(int wtype, int n, const void *w, const void *a) {
         case KT_Q8_0: return dot_q8_0(n, w, a);
         case KT_IQ4_NL: return dot_iq4_nl(n, w, a);
         case KT_IQ4_XS: return dot_iq4_xs(n, w, a);
+        case KT_IQ2_XXS: return dot_iq2_xxs(n, w, a);
+        case KT_IQ2_XS: return dot_iq2_xs(n, w, a);
+        case KT_IQ2_S: return dot_iq2_s(n, w, a);
+        case KT_IQ3_XXS: return dot_iq3_xxs(n, w, a);
+        case KT_IQ3_S: return dot_iq3_s(n, w, a);
+        case KT_IQ1_S: return dot_iq1_s(n, w, a);
+        case KT_IQ1_M: return dot_iq1_m(n, w, a);
         case KT_F16: return dot_f16(n, w, a);
         case KT_F32: { const float *x = w, *y = a; double s = 0; for (int i = 0; i < n; ++i) s += x[i] * y[i]; return (float)s; }
         default: abort();

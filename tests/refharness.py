@@ -16,8 +16,14 @@ REF_BIN_SCALAR = os.path.join(ROOT, "oracle", "_ref", "scalar", "ref_llama")   #
 # ggml_type ids (ggml/include/ggml.h:364-399)
 F32, F16, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q3_K, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 3, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15
 IQ4_NL, IQ4_XS = 20, 23
+IQ2_XXS, IQ2_XS, IQ3_XXS, IQ1_S, IQ3_S, IQ2_S, IQ1_M = 16, 17, 18, 19, 21, 22, 29
 BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q4_1: (32, 20), Q5_0: (32, 22), Q5_1: (32, 24), Q8_0: (32, 34), Q8_1: (32, 36), Q2_K: (256, 84), Q3_K: (256, 110), Q4_K: (256, 144),
-         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292), IQ4_NL: (32, 18), IQ4_XS: (256, 136)}
+         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292), IQ4_NL: (32, 18), IQ4_XS: (256, 136),
+         IQ2_XXS: (256, 66), IQ2_XS: (256, 74), IQ2_S: (256, 82), IQ3_XXS: (256, 98), IQ3_S: (256, 110),
+         IQ1_S: (256, 50), IQ1_M: (256, 56)}
+# the grid types (ggml-common.h:340-405): name -> type id
+IQ_GRID = {"iq2_xxs": IQ2_XXS, "iq2_xs": IQ2_XS, "iq2_s": IQ2_S, "iq3_xxs": IQ3_XXS, "iq3_s": IQ3_S,
+           "iq1_s": IQ1_S, "iq1_m": IQ1_M}
 
 
 def row_bytes(t, k):
@@ -342,6 +348,11 @@ def iq4_nl_types(n_layer):
 def iq4_xs_types(n_layer):
     """LLAMA_FTYPE_MOSTLY_IQ4_XS: IQ4_XS everywhere, output Q6_K"""
     return uniform_types(n_layer, IQ4_XS, Q6_K)
+
+
+def iq_grid_types(n_layer, t):
+    """a grid-type file (LLAMA_FTYPE_MOSTLY_IQ2_XXS .. IQ1_M): the type everywhere, output Q6_K"""
+    return uniform_types(n_layer, t, Q6_K)
 
 
 def q5_1_types(n_layer):

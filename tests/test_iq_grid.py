@@ -1,0 +1,186 @@
+"""The lattice-grid weight types IQ2_XXS / IQ2_XS / IQ2_S / IQ3_XXS / IQ3_S / IQ1_S / IQ1_M (block_iq2_xxs ..
+block_iq1_m, ggml-common.h:340-405; dot Q8_K through the code books, ggml_vec_dot_iq*_q8_K ggml-quants.c:9606-12468):
+the CPU oracle and the HIP kernels against the reference builds' own outputs (tests/golden/iq_grid.npz,
+make_iq_grid.py; the code books themselves are recovered from the reference's dequantization by
+tools/gen_iq_grids.py).
+
+* oracle (CPU): dequantize_row_iq* bit-exact on synthetic and random-bit blocks; mul_mat at decode / small-batch /
+  prefill shapes within 3e-6 of the output scale;
+* GPU: the (identity) device layout round-trips and dequantizes bit-exactly (kcpp_dequantize and get_rows); the
+  mat-vec (kcpp_gemv, M <= 8) and the MFMA GEMM (kcpp_gemm past 16 tokens: codes x integer group scales as exact f16
+  fragments) against the golden and the oracle at 3e-6; a tiny Llama with the type everywhere (output Q6_K) end to
+  end (prefill + teacher-forced decode, graph and eager) within 1.5x the reference's AVX2-vs-scalar spread, floored
+  at 1e-3 (for IQ2_S the two reference builds agree to 1.3e-6: the floor is the f32 summation-order class of the
+  other types)."""
+import os
+
+import numpy as np
+import pytest
+
+import refharness as R
+
+G = None
+
+
+def golden():
+    global G
+    if G is None:
+        G = np.load(os.path.join(R.ROOT, "tests", "golden", "iq_grid.npz"))
+    return G
+
+
+@pytest.fixture(scope="module", params=sorted(R.IQ_GRID))
+def kq(request):
+    return request.param, R.IQ_GRID[request.param], golden()
+
+
+def test_oracle_dequant_bit_exact(kq):
+    fn, T, g = kq
+    for tag in ("syn", "rnd"):
+        want = g["%s_deq_%s_out" % (fn, tag)]
+        got = R.dequant(T, g["%s_deq_%s_in" % (fn, tag)], want.size)
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), tag
+
+
+@pytest.mark.parametrize("shape", [(4096, 256, 1), (4096, 128, 8), (1024, 64, 40)])
+def test_oracle_mul_mat_vs_reference(kq, shape):
+    fn, T, g = kq
+    key = "%s_mm_%d_%d_%d" % ((fn,) + shape)
+    t, seed, tid, xseed, K, N, M = [int(v) for v in g[key + "_meta"]]
+    w = R.synth(t, seed, tid, K, N)
+    X = np.random.default_rng(xseed).standard_normal((M, K)).astype(np.float32)
+    want = g[key + "_y"]
+    np.testing.assert_allclose(R.mul_mat(t, w, K, N, X), want, rtol=0, atol=3e-6 * max(1.0, np.abs(want).max()))
+
+
+def test_code_books_generated():
+    """the generated header holds every table at its size (tools/gen_iq_grids.py)"""
+    src = open(os.path.join(R.ROOT, "koboldcpp_amd", "csrc", "iq_grids.h")).read()
+    for name, n in (("kcpp_iq2xxs_grid", 512), ("kcpp_iq2xs_grid", 1024), ("kcpp_iq2s_grid", 2048),
+                    ("kcpp_iq3xxs_grid", 256), ("kcpp_iq3s_grid", 512), ("kcpp_iq1s_grid", 4096)):
+        assert "KCPP_IQ_TABLE(%s, %d)" % (name, n) in src
+
+
+# ---------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def env():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    import koboldcpp_amd.lib as K
+    return torch, K
+
+
+def _sp(torch):
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _upload(torch, K, data, Kd, N, T):
+    src = torch.from_numpy(np.ascontiguousarray(data)).cuda()
+    dst = torch.empty_like(src)
+    K.call("kcpp_weight_repack", T, src.data_ptr(), dst.data_ptr(), Kd, N, 0, _sp(torch))
+    return dst
+
+
+@pytest.mark.gpu
+def test_gpu_layout_and_dequant(env, kq):
+    torch, K = env
+    fn, T, g = kq
+    for tag in ("syn", "rnd"):
+        data, want = g["%s_deq_%s_in" % (fn, tag)], g["%s_deq_%s_out" % (fn, tag)]
+        d = _upload(torch, K, data, want.size, 1, T)
+        back = torch.empty_like(d)
+        K.call("kcpp_weight_repack", T, d.data_ptr(), back.data_ptr(), want.size, 1, 1, _sp(torch))
+        y = torch.empty(want.size, dtype=torch.float32, device="cuda")
+        K.call("kcpp_dequantize", T, d.data_ptr(), y.data_ptr(), want.size, 1, _sp(torch))
+        # get_rows of row 0 of the same bytes seen as a [1][K] matrix
+        ids = torch.zeros(1, dtype=torch.int32, device="cuda")
+        yr = torch.empty(want.size, dtype=torch.float32, device="cuda")
+        K.call("kcpp_get_rows", T, d.data_ptr(), want.size, 1, ids.data_ptr(), 1, yr.data_ptr(), want.size, _sp(torch))
+        torch.cuda.synchronize()
+        assert np.array_equal(back.cpu().numpy(), data)
+        assert np.array_equal(y.cpu().numpy().view(np.uint32), want.view(np.uint32)), tag
+        assert np.array_equal(yr.cpu().numpy().view(np.uint32), want.view(np.uint32)), tag
+    Kd, N = 2048, 8
+    w = R.synth(T, 5, 77, Kd, N)
+    s = torch.empty(w.nbytes, dtype=torch.uint8, device="cuda")
+    K.call("kcpp_weight_synth", T, 5, 77, s.data_ptr(), Kd, N, _sp(torch))
+    torch.cuda.synchronize()
+    assert np.array_equal(s.cpu().numpy(), w)
+
+
+def _gpu_mul_mat(torch, K, T, w, Kd, N, X, mode=0, w2=None, res=None):
+    M = X.shape[0]
+    wd = _upload(torch, K, w, Kd, N, T)
+    w2d = _upload(torch, K, w2, Kd, N, T) if w2 is not None else None
+    xd = torch.from_numpy(np.ascontiguousarray(X, np.float32)).cuda()
+    act = torch.zeros(K.act_bytes(T, Kd, M), dtype=torch.uint8, device="cuda")
+    K.call("kcpp_quantize_act", K.vec_dot_type(T), xd.data_ptr(), Kd, act.data_ptr(), Kd, M, _sp(torch))
+    Y = torch.empty((M, N), dtype=torch.float32, device="cuda")
+    rd = torch.from_numpy(np.ascontiguousarray(res, np.float32)).cuda() if res is not None else None
+    w2p = w2d.data_ptr() if w2d is not None else None
+    rp = rd.data_ptr() if rd is not None else None
+    if M <= 8:
+        K.call("kcpp_gemv", T, wd.data_ptr(), w2p, Kd, N, act.data_ptr(), M, Y.data_ptr(), N, rp, N, mode, _sp(torch))
+    else:
+        ws = torch.empty(K.raw().kcpp_gemm_workspace_bytes(T, Kd, N, M), dtype=torch.uint8, device="cuda")
+        K.call("kcpp_gemm", T, wd.data_ptr(), w2p, Kd, N, act.data_ptr(), M, Y.data_ptr(), N, rp, N, mode,
+               ws.data_ptr(), _sp(torch))
+    torch.cuda.synchronize()
+    return Y.cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4096, 256, 1), (4096, 128, 8), (1024, 64, 40)])
+def test_gpu_mul_mat_vs_reference_golden(env, kq, shape):
+    torch, K = env
+    fn, T, g = kq
+    key = "%s_mm_%d_%d_%d" % ((fn,) + shape)
+    t, seed, tid, xseed, Kd, N, M = [int(v) for v in g[key + "_meta"]]
+    w = R.synth(t, seed, tid, Kd, N)
+    X = np.random.default_rng(xseed).standard_normal((M, Kd)).astype(np.float32)
+    want = g[key + "_y"]
+    np.testing.assert_allclose(_gpu_mul_mat(torch, K, T, w, Kd, N, X), want, rtol=0,
+                               atol=3e-6 * max(1.0, np.abs(want).max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 3, 17, 64, 300])
+def test_gpu_mul_mat_modes_vs_oracle(env, kq, M):
+    torch, K = env
+    fn, T, _ = kq
+    Kd, N = 2048, 96
+    rng = np.random.default_rng(M)
+    w, w2 = R.synth(T, 9, 1011, Kd, N), R.synth(T, 9, 2011, Kd, N)
+    X = rng.standard_normal((M, Kd)).astype(np.float32)
+    res = rng.standard_normal((M, N)).astype(np.float32)
+    a, b = R.mul_mat(T, w, Kd, N, X), R.mul_mat(T, w2, Kd, N, X)
+    tol = 3e-6 * max(1.0, np.abs(a).max())
+    np.testing.assert_allclose(_gpu_mul_mat(torch, K, T, w, Kd, N, X, res=res), a + res, rtol=0, atol=tol + 1e-6)
+    glu = (a / (1 + np.exp(-a))) * b
+    np.testing.assert_allclose(_gpu_mul_mat(torch, K, T, w, Kd, N, X, mode=1, w2=w2), glu, rtol=1e-5, atol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graphs", [True, False], ids=["graph", "eager"])
+def test_gpu_model_vs_reference(env, kq, graphs):
+    """tiny Llama with the grid type everywhere (output Q6_K): prefill + 8 teacher-forced decode steps vs the
+    reference logits, within 1.5x its own build spread (floored at 1e-3)"""
+    torch, K = env
+    fn, T, g = kq
+    types = [int(t) for t in g[fn + "_e2e_types"]]
+    m = K.Model(R.TINY, types)
+    m.set_graphs(graphs)
+    m.synth(1234)
+    prompt = g[fn + "_e2e_prompt"]
+    out = [m.decode(prompt, 0)]
+    n = len(prompt)
+    for tok in g[fn + "_e2e_forced"]:
+        out.append(m.decode([int(tok)], n))
+        n += 1
+    m.close()
+    d = np.abs(np.array(out) - g[fn + "_e2e_logits"])
+    tmax = max(1.5 * g[fn + "_e2e_spread_max"].max(), 1e-3)
+    tmed = max(1.5 * g[fn + "_e2e_spread_median"].max(), 2e-4)
+    print(fn, "gpu vs ref max", d.max(axis=1), "| spread", g[fn + "_e2e_spread_max"])
+    assert np.all(d.max(axis=1) <= tmax)
+    assert np.all(np.median(d, axis=1) <= tmed)
