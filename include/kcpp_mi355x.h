@@ -303,6 +303,16 @@ int kcpp_model_forward_hidden(kcpp_model *m, int T, int n_past);
 /* greedy argmax of the last logits on device (avoids the 0.5 MB logits copy); also becomes the
  * next decode_greedy step's input token */
 int kcpp_model_argmax(kcpp_model *m, int32_t *token_out);
+/* the same enqueued on the stage's stream (no host synchronisation): the token lands in kcpp_model_argmax_dev */
+int kcpp_model_argmax_async(kcpp_model *m);
+/* one single-token step at n_past whose input token is already in kcpp_model_token_dev (stage with the embedding;
+ * other stages take their hidden input as for decode_async); enqueued, no host synchronisation.  The stage with
+ * the output head computes the step's greedy token into kcpp_model_argmax_dev (and, when it also owns the
+ * embedding, into kcpp_model_token_dev: the next step's input).  Replaces the per-token host hop of the
+ * pipeline's greedy loop (the reference reads the token on the host: llama_sampling + llama_decode). */
+int kcpp_model_step_dev(kcpp_model *m, int n_past);
+int32_t *kcpp_model_token_dev(kcpp_model *m);
+int32_t *kcpp_model_argmax_dev(kcpp_model *m);
 /* one greedy generation step at n_past: input = the previous argmax (device-resident), the step's
  * own argmax computed in the same graph replay and returned (one host sync per token).
  * Requires a stage owning both the embedding and the output head. */
@@ -350,10 +360,17 @@ int kcpp_row_split_range(int64_t nrows, int n, const float *tensor_split, int id
 int64_t kcpp_model_weight_bytes(kcpp_model *m);
 /* bench.py --gpus N: the drop-in engine of load_model (layer-split stages over n_dev GPUs by tensor_split, RCCL or
  * event-ordered hand-off, pipelined ubatches: koboldcpp_amd/csrc/expose.cpp) on synthetic weights: prefill n_prompt
- * ids in ubatches of ub, then n_warm + n_steps greedy tokens as generate() runs them.  out = {prefill_s, decode_s of
- * the n_steps tokens, n_past at the end, 1 if the hand-off ran on RCCL}.  0 ok, -1 fewer than n_dev GPUs visible. */
+ * ids in ubatches of ub, then n_warm + n_steps greedy tokens with the token moved home on device (no host
+ * synchronisation inside a step).  out = {prefill_s, decode_s of the n_steps tokens, n_past at the end, 1 if the
+ * hand-off ran on RCCL}.  0 ok, -1 fewer than n_dev GPUs visible. */
 int kcpp_engine_bench(const kcpp_hparams *hp, const int *types, int n_types, int n_dev, const float *tensor_split,
                       uint64_t seed, int n_prompt, int ub, int n_warm, int n_steps, double *out);
+/* test hook: the pipeline schedule's enqueue order (prefill, argmax, token home, `steps` greedy steps) for n_stages
+ * stages, recorded by the schedule's trace backend into out (host only, no device calls) */
+int kcpp_pipeline_trace(int n_stages, int ub, int T, int n_past, int steps, char *out, int cap);
+/* test hook: load_model's layer placement (src/llama.cpp:7010-7036): out[i] = device of layer i, out[n_layer] =
+ * the output head's device */
+int kcpp_split_layers(int n_layer, int n_dev, const float *tensor_split, int *out);
 const char *kcpp_last_error(void);
 
 /* GGUF parse + tensor-table bounds validation alone (load_model's first step): 0 ok, -1 with the reason in err */

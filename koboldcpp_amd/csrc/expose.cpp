@@ -157,44 +157,126 @@ std::vector<int> split_layers(int n_layer, int n_dev, const float *ts) {
     return dev;   // dev[n_layer] = output head's device
 }
 
-// stage s-1's residual stream (t tokens) -> stage s's input, on the two stages' streams
-int handoff(Engine &e, size_t s, int t) {
-    const size_t count = (size_t)t * e.hp.n_embd;
-    hipStream_t src = (hipStream_t)kcpp_model_stream(e.stages[s - 1]), dst = (hipStream_t)kcpp_model_stream(e.stages[s]);
-    if (!e.comms.empty()) {
-        if (e.rccl.group_start()) return -20;
-        const int r1 = e.rccl.send(e.hidden[s - 1], count, kNcclFloat32, (int)s, e.comms[s - 1], src);
-        const int r2 = e.rccl.recv(e.hidden[s], count, kNcclFloat32, (int)s - 1, e.comms[s], dst);
-        if (e.rccl.group_end() || r1 || r2) return -21;
-        return 0;
-    }
-    // dst waits for the producer, copies, and the producer's next write waits for the copy to have read
-    if (hipSetDevice(e.devs[s - 1]) || hipEventRecord(e.ev_done[s - 1], src)) return -22;
-    if (hipSetDevice(e.devs[s]) || hipStreamWaitEvent(dst, e.ev_done[s - 1], 0)) return -22;
-    const hipError_t ce = e.devs[s] == e.devs[s - 1]
-                              ? hipMemcpyAsync(e.hidden[s], e.hidden[s - 1], count * 4, hipMemcpyDeviceToDevice, dst)
-                              : hipMemcpyPeerAsync(e.hidden[s], e.devs[s], e.hidden[s - 1], e.devs[s - 1], count * 4, dst);
-    if (ce != hipSuccess || hipEventRecord(e.ev_read[s], dst)) return -23;
-    if (hipSetDevice(e.devs[s - 1]) || hipStreamWaitEvent(src, e.ev_read[s], 0)) return -22;
-    return 0;
-}
+// The pipeline schedule is written against the stage operations below: HipOps drives the engine's stage streams
+// (RCCL send/recv or event-ordered peer copies) in the product, TraceOps records the enqueue order for the CPU test
+// hook kcpp_pipeline_trace (tests/test_pipeline.py).  Neither forward() nor greedy_step() synchronises the host.
+struct PipeOps {
+    virtual ~PipeOps() = default;
+    virtual size_t n_stages() const = 0;
+    virtual int ubatch() const = 0;
+    virtual int decode(size_t s, const int32_t *toks, int t, int n_past) = 0;   // enqueue t tokens (stage 0: the ids)
+    virtual int step_dev(size_t s, int n_past) = 0;       // one token whose input is already on the device
+    virtual int handoff(size_t s, int t) = 0;             // stage s-1's residual stream (t tokens) -> stage s
+    virtual int argmax_dev() = 0;                         // last stage: greedy token of its last logits, on device
+    virtual int token_home() = 0;                         // that token -> stage 0's input token (device copy)
+};
 
 // run tokens [i0, i0+T) through all stages, ubatch by ubatch, everything enqueued: stage s works on ubatch u while
 // stage s+1 works on ubatch u-1 (the pipeline the reference gets from n_copies = 4, ggml-backend.cpp:1372); the
 // caller's logits read on the last stage is the only host synchronisation
-int forward(Engine &e, const int32_t *toks, int T, int n_past) {
-    for (int i = 0; i < T; i += e.ub) {
-        const int t = std::min(e.ub, T - i);
-        for (size_t s = 0; s < e.stages.size(); ++s) {
+int forward(PipeOps &o, const int32_t *toks, int T, int n_past) {
+    const int ub = o.ubatch();
+    for (int i = 0; i < T; i += ub) {
+        const int t = std::min(ub, T - i);
+        for (size_t s = 0; s < o.n_stages(); ++s) {
             if (s > 0) {
-                const int rc = handoff(e, s, t);
+                const int rc = o.handoff(s, t);
                 if (rc) return rc;
             }
-            const int rc = kcpp_model_decode_async(e.stages[s], s == 0 ? toks + i : nullptr, t, n_past + i);
+            const int rc = o.decode(s, s == 0 ? toks + i : nullptr, t, n_past + i);
             if (rc) return rc;
         }
     }
     return 0;
+}
+
+// one greedy token through all stages without the host: stage 0 embeds the token the last stage's argmax left
+// (moved home by token_home), each later stage takes its predecessor's hand-off, the last stage's step computes
+// the next greedy token on device, which goes home for the next step
+int greedy_step(PipeOps &o, int n_past) {
+    for (size_t s = 0; s < o.n_stages(); ++s) {
+        if (s > 0) {
+            const int rc = o.handoff(s, 1);
+            if (rc) return rc;
+        }
+        const int rc = o.step_dev(s, n_past);
+        if (rc) return rc;
+    }
+    return o.token_home();
+}
+
+struct HipOps : PipeOps {
+    Engine &e;
+    explicit HipOps(Engine &en) : e(en) {}
+    size_t n_stages() const override { return e.stages.size(); }
+    int ubatch() const override { return e.ub; }
+    int decode(size_t s, const int32_t *toks, int t, int n_past) override {
+        return kcpp_model_decode_async(e.stages[s], toks, t, n_past);
+    }
+    int step_dev(size_t s, int n_past) override { return kcpp_model_step_dev(e.stages[s], n_past); }
+    int argmax_dev() override { return kcpp_model_argmax_async(e.stages.back()); }
+    // stage s-1's residual stream (t tokens) -> stage s's input, on the two stages' streams
+    int handoff(size_t s, int t) override {
+        const size_t count = (size_t)t * e.hp.n_embd;
+        hipStream_t src = (hipStream_t)kcpp_model_stream(e.stages[s - 1]), dst = (hipStream_t)kcpp_model_stream(e.stages[s]);
+        if (!e.comms.empty()) {
+            if (e.rccl.group_start()) return -20;
+            const int r1 = e.rccl.send(e.hidden[s - 1], count, kNcclFloat32, (int)s, e.comms[s - 1], src);
+            const int r2 = e.rccl.recv(e.hidden[s], count, kNcclFloat32, (int)s - 1, e.comms[s], dst);
+            if (e.rccl.group_end() || r1 || r2) return -21;
+            return 0;
+        }
+        // dst waits for the producer, copies, and the producer's next write waits for the copy to have read
+        if (hipSetDevice(e.devs[s - 1]) || hipEventRecord(e.ev_done[s - 1], src)) return -22;
+        if (hipSetDevice(e.devs[s]) || hipStreamWaitEvent(dst, e.ev_done[s - 1], 0)) return -22;
+        const hipError_t ce = e.devs[s] == e.devs[s - 1]
+                                  ? hipMemcpyAsync(e.hidden[s], e.hidden[s - 1], count * 4, hipMemcpyDeviceToDevice, dst)
+                                  : hipMemcpyPeerAsync(e.hidden[s], e.devs[s], e.hidden[s - 1], e.devs[s - 1], count * 4, dst);
+        if (ce != hipSuccess || hipEventRecord(e.ev_read[s], dst)) return -23;
+        if (hipSetDevice(e.devs[s - 1]) || hipStreamWaitEvent(src, e.ev_read[s], 0)) return -22;
+        return 0;
+    }
+    // the last stage's argmax (4 bytes) into stage 0's token input: stage 0's stream waits for the last stage's
+    // step, then a peer copy over xGMI (one stage: the argmax kernel already wrote the token input)
+    int token_home() override {
+        const size_t L = e.stages.size() - 1;
+        if (L == 0) return 0;
+        hipStream_t last = (hipStream_t)kcpp_model_stream(e.stages[L]), first = (hipStream_t)kcpp_model_stream(e.stages[0]);
+        if (hipSetDevice(e.devs[L]) || hipEventRecord(e.ev_done[L], last)) return -24;
+        if (hipSetDevice(e.devs[0]) || hipStreamWaitEvent(first, e.ev_done[L], 0)) return -24;
+        const hipError_t ce = e.devs[0] == e.devs[L]
+                                  ? hipMemcpyAsync(kcpp_model_token_dev(e.stages[0]), kcpp_model_argmax_dev(e.stages[L]), 4,
+                                                   hipMemcpyDeviceToDevice, first)
+                                  : hipMemcpyPeerAsync(kcpp_model_token_dev(e.stages[0]), e.devs[0],
+                                                       kcpp_model_argmax_dev(e.stages[L]), e.devs[L], 4, first);
+        return ce == hipSuccess ? 0 : -25;
+    }
+};
+
+// records the schedule: "d<s>:<t>@<n_past>" decode, "h<s>:<t>" hand-off into stage s, "s<s>@<n_past>" device-token
+// step, "a" last-stage argmax, "k" token home
+struct TraceOps : PipeOps {
+    size_t S;
+    int ub;
+    std::string log;
+    TraceOps(size_t s, int u) : S(s), ub(u) {}
+    size_t n_stages() const override { return S; }
+    int ubatch() const override { return ub; }
+    void put(const std::string &x) { log += (log.empty() ? "" : " ") + x; }
+    int decode(size_t s, const int32_t *toks, int t, int n_past) override {
+        if ((s == 0) != (toks != nullptr)) return -1;              // ids only into the embedding stage
+        put("d" + std::to_string(s) + ":" + std::to_string(t) + "@" + std::to_string(n_past));
+        return 0;
+    }
+    int step_dev(size_t s, int n_past) override { put("s" + std::to_string(s) + "@" + std::to_string(n_past)); return 0; }
+    int handoff(size_t s, int t) override { put("h" + std::to_string(s) + ":" + std::to_string(t)); return 0; }
+    int argmax_dev() override { put("a"); return 0; }
+    int token_home() override { put("k"); return 0; }
+};
+
+int forward(Engine &e, const int32_t *toks, int T, int n_past) {
+    HipOps o(e);
+    return forward(o, toks, T, n_past);
 }
 
 // events for the copy handoff, and an RCCL clique when every stage sits on its own device (RCCL refuses two
@@ -903,8 +985,9 @@ int kcpp_pieces_probe(const char *gguf_path, char *out, int64_t cap, int64_t *en
 
 // bench.py --gpus N (N > 1): the drop-in engine over n_dev GPUs -- load_model's stages (build_stages), hand-off
 // (init_handoff: RCCL clique over distinct GPUs), forward() -- with synthetic weights instead of a GGUF.  Prefill of
-// n_prompt ids in ubatches of ub (timed to the last stage's drain), then n_warm + n_steps greedy tokens exactly as
-// generate() runs them: argmax on the last stage, the token back through the host, forward() over all stages.
+// n_prompt ids in ubatches of ub (timed to the last stage's drain), then n_warm + n_steps greedy tokens by
+// greedy_step: argmax on the last stage, the token moved home to stage 0 on device, no host synchronisation inside
+// a step (generate() reads each token on the host: its samplers and stop checks run there, as the reference's).
 // out = {prefill_s, decode_s (the n_steps timed tokens), n_past at the end, 1 when the hand-off is RCCL}.
 int kcpp_engine_bench(const kcpp_hparams *hp, const int *types, int n_types, int n_dev, const float *tensor_split,
                       uint64_t seed, int n_prompt, int ub, int n_warm, int n_steps, double *out) {
@@ -927,27 +1010,59 @@ int kcpp_engine_bench(const kcpp_hparams *hp, const int *types, int n_types, int
     std::vector<int32_t> prompt(n_prompt);
     for (int i = 0; i < n_prompt; ++i) prompt[i] = 16 + (i % 2);          // the " 1" pattern of bench.py
     kcpp_model *last = e->stages.back();
+    HipOps o(*e);
+    auto sync_all = [&]() {
+        for (kcpp_model *m : e->stages)
+            if (kcpp_model_sync(m)) return -1;
+        return 0;
+    };
     // warm-up: a short prefill (first touch, graph capture on every stage)
-    if (forward(*e, prompt.data(), std::min(64, n_prompt), 0) || kcpp_model_sync(last)) return -5;
+    if (forward(o, prompt.data(), std::min(64, n_prompt), 0) || kcpp_model_sync(last)) return -5;
     const auto t0 = std::chrono::steady_clock::now();
-    if (forward(*e, prompt.data(), n_prompt, 0) || kcpp_model_sync(last)) return -5;
+    if (forward(o, prompt.data(), n_prompt, 0) || kcpp_model_sync(last)) return -5;
     const auto t1 = std::chrono::steady_clock::now();
     int n_past = n_prompt;
     std::chrono::steady_clock::time_point t2 = t1;
+    // greedy tokens without the host: the prefill's token goes home on device, then every step's token too
+    if (o.argmax_dev() || o.token_home()) return -6;
     for (int i = 0; i < n_warm + n_steps; ++i) {
-        if (i == n_warm) t2 = std::chrono::steady_clock::now();
-        int32_t tok = 0;
-        if (kcpp_model_argmax(last, &tok) || forward(*e, &tok, 1, n_past)) return -6;
+        if (i == n_warm) {
+            if (sync_all()) return -6;
+            t2 = std::chrono::steady_clock::now();
+        }
+        if (greedy_step(o, n_past)) return -6;
         ++n_past;
     }
-    int32_t tok = 0;
-    if (kcpp_model_argmax(last, &tok)) return -6;                       // the last token's logits consumed
+    if (sync_all()) return -6;                                         // the last token computed and home
     const auto t3 = std::chrono::steady_clock::now();
     out[0] = std::chrono::duration<double>(t1 - t0).count();
     out[1] = std::chrono::duration<double>(t3 - t2).count();
     out[2] = n_past;
     out[3] = e->comms.empty() ? 0.0 : 1.0;
     return 0;
+}
+
+// test hook (tests/test_pipeline.py): load_model's layer placement (split_layers): out[i] = device of layer i for
+// i < n_layer, out[n_layer] = the output head's device
+int kcpp_split_layers(int n_layer, int n_dev, const float *tensor_split, int *out) {
+    if (n_layer < 1 || n_dev < 1 || n_dev > KCPP_TENSOR_SPLIT_MAX || !tensor_split || !out) return -1;
+    const std::vector<int> d = split_layers(n_layer, n_dev, tensor_split);
+    for (int i = 0; i <= n_layer; ++i) out[i] = d[i];
+    return 0;
+}
+
+// test hook (tests/test_pipeline.py): the enqueue order of the pipeline schedule for n_stages stages -- a prefill of
+// T tokens at n_past in ubatches of ub, the last stage's argmax and its way home, then `steps` greedy steps -- as
+// TraceOps records it (space-separated into out).  Returns the length written, -1 on bad arguments.
+int kcpp_pipeline_trace(int n_stages, int ub, int T, int n_past, int steps, char *out, int cap) {
+    if (n_stages < 1 || ub < 1 || T < 1 || !out || cap < 1) return -1;
+    TraceOps o((size_t)n_stages, ub);
+    std::vector<int32_t> toks((size_t)T, 1);
+    if (forward(o, toks.data(), T, n_past) || o.argmax_dev() || o.token_home()) return -1;
+    for (int i = 0; i < steps; ++i)
+        if (greedy_step(o, n_past + T + i)) return -1;
+    snprintf(out, (size_t)cap, "%s", o.log.c_str());
+    return (int)std::min<size_t>(o.log.size(), (size_t)cap - 1);
 }
 
 int kcpp_tokenizer_special_ids(const char *gguf_path, int32_t *out) {

@@ -1340,6 +1340,21 @@ static int launch_pos_step(kcpp_model *m) {
     return 0;
 }
 
+// pipeline greedy steps without the host (expose.cpp greedy_step): the last stage's argmax on device, and a
+// single-token step whose input token (stage 0) is already in tok_dev
+extern "C" int kcpp_model_argmax_async(kcpp_model *m) {
+    if (!m->has_output) return -1;
+    RT_CHECK(hipSetDevice(m->device));
+    return launch_argmax(m, false);
+}
+extern "C" int kcpp_model_step_dev(kcpp_model *m, int n_past) {
+    if (n_past + 1 > m->hp.n_ctx) { g_err = "context overflow"; return -2; }
+    RT_CHECK(hipSetDevice(m->device));
+    return step_one(m, n_past);
+}
+extern "C" int32_t *kcpp_model_token_dev(kcpp_model *m) { return m->tok_dev; }
+extern "C" int32_t *kcpp_model_argmax_dev(kcpp_model *m) { return m->argmax_dev; }
+
 extern "C" int kcpp_model_argmax(kcpp_model *m, int32_t *token_out) {
     if (!m->has_output) return -1;
     RT_CHECK(hipSetDevice(m->device));

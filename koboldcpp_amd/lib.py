@@ -61,6 +61,10 @@ _SIGS = {
     "kcpp_pieces_probe": [ctypes.c_char_p, P, I64, P, I],
     "kcpp_tokenizer_special_ids": [ctypes.c_char_p, P],
     "kcpp_engine_bench": [P, P, I, I, P, U64, I, I, I, I, P],
+    "kcpp_pipeline_trace": [I, I, I, I, I, ctypes.c_char_p, I],
+    "kcpp_split_layers": [I, I, P, P],
+    "kcpp_model_argmax_async": [P],
+    "kcpp_model_step_dev": [P, I],
     "kcpp_add": [P, P, P, I64, P],
     "kcpp_silu_mul": [P, P, P, I64, P],
     "kcpp_moe_route": [P, I64, P, I, I64, I, I, P, P, I, P],
@@ -227,8 +231,8 @@ def hparams(hp):
 
 
 def engine_bench(hp, types, n_dev, n_prompt, ubatch, n_warm, n_steps, seed=1234, tensor_split=None):
-    """the drop-in engine (load_model's layer-split stages over n_dev GPUs, RCCL / copy hand-off, generate()'s
-    greedy loop) on synthetic weights: {prefill_s, decode_s, n_past, rccl}"""
+    """the drop-in engine (load_model's layer-split stages over n_dev GPUs, RCCL / copy hand-off, greedy tokens moved
+    home on device) on synthetic weights: {prefill_s, decode_s, n_past, rccl}"""
     h = hparams(hp)
     t = (ctypes.c_int * len(types))(*types)
     ts = (ctypes.c_float * 16)(*((tensor_split or [1.0] * n_dev) + [0.0] * (16 - n_dev)))
@@ -381,3 +385,21 @@ def row_split_range(nrows, tensor_split, i):
     lo, hi = ctypes.c_int64(0), ctypes.c_int64(0)
     _chk(_L.kcpp_row_split_range(int(nrows), n, ts, int(i), ctypes.byref(lo), ctypes.byref(hi)), "row_split_range")
     return lo.value, hi.value
+
+
+def pipeline_trace(n_stages, ubatch, T, n_past, steps):
+    """the pipeline schedule's enqueue order (expose.cpp forward / greedy_step over the trace backend): host only"""
+    buf = ctypes.create_string_buffer(1 << 16)
+    n = _L.kcpp_pipeline_trace(n_stages, ubatch, T, n_past, steps, buf, len(buf))
+    if n < 0:
+        raise KcppError("kcpp_pipeline_trace failed")
+    return buf.value.decode().split()
+
+
+def split_layers(n_layer, n_dev, tensor_split=None):
+    """load_model's layer placement: (device per layer, output head's device)"""
+    ts = (ctypes.c_float * 16)(*((list(tensor_split) if tensor_split else [1.0] * n_dev) + [0.0] * (16 - n_dev)))
+    out = (ctypes.c_int * (n_layer + 1))()
+    if _L.kcpp_split_layers(n_layer, n_dev, ts, out) != 0:
+        raise KcppError("kcpp_split_layers failed")
+    return list(out[:n_layer]), out[n_layer]

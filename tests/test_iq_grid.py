@@ -9,9 +9,8 @@ tools/gen_iq_grids.py).
 * GPU: the (identity) device layout round-trips and dequantizes bit-exactly (kcpp_dequantize and get_rows); the
   mat-vec (kcpp_gemv, M <= 8) and the MFMA GEMM (kcpp_gemm past 16 tokens: codes x integer group scales as exact f16
   fragments) against the golden and the oracle at 3e-6; a tiny Llama with the type everywhere (output Q6_K) end to
-  end (prefill + teacher-forced decode, graph and eager) within 1.5x the reference's AVX2-vs-scalar spread, floored
-  at 1e-3 (for IQ2_S the two reference builds agree to 1.3e-6: the floor is the f32 summation-order class of the
-  other types)."""
+  end (prefill + teacher-forced decode, graph and eager) within 2x the reference's AVX2-vs-scalar spread (the bar
+  of tests/test_gpu_model.py), and against the C restatement with the HIP path's f32 attention accumulation."""
 import os
 
 import numpy as np
@@ -160,27 +159,51 @@ def test_gpu_mul_mat_modes_vs_oracle(env, kq, M):
     np.testing.assert_allclose(_gpu_mul_mat(torch, K, T, w, Kd, N, X, mode=1, w2=w2), glu, rtol=1e-5, atol=tol)
 
 
+# the tiny-model parity bar of tests/test_gpu_model.py: the reference's own AVX2-vs-scalar spread (the larger of this
+# fixture's and the standard tiny fixtures', tests/golden/ref_spread.npz), x2 -- one factor for the GPU's summation
+# order, and the production attention accumulates V*P in f32 where the CPU keeps f16 (ggml.c:15788)
+_SP = np.load(os.path.join(R.ROOT, "tests", "golden", "ref_spread.npz"))
+SPREAD_MAX = max(float(_SP["tiny_%s_max" % t].max()) for t in ("q4km", "q8_0", "moe"))
+SPREAD_MED = max(float(_SP["tiny_%s_median" % t].max()) for t in ("q4km", "q8_0", "moe"))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("graphs", [True, False], ids=["graph", "eager"])
 def test_gpu_model_vs_reference(env, kq, graphs):
     """tiny Llama with the grid type everywhere (output Q6_K): prefill + 8 teacher-forced decode steps vs the
-    reference logits, within 1.5x its own build spread (floored at 1e-3)"""
+    reference logits within 2x the reference's build spread, and vs the C restatement with f32 attention
+    accumulation (the HIP path's math) within the same bar"""
     torch, K = env
     fn, T, g = kq
     types = [int(t) for t in g[fn + "_e2e_types"]]
     m = K.Model(R.TINY, types)
     m.set_graphs(graphs)
     m.synth(1234)
-    prompt = g[fn + "_e2e_prompt"]
+    prompt = [int(v) for v in g[fn + "_e2e_prompt"]]
+    forced = [int(t) for t in g[fn + "_e2e_forced"]]
     out = [m.decode(prompt, 0)]
     n = len(prompt)
-    for tok in g[fn + "_e2e_forced"]:
-        out.append(m.decode([int(tok)], n))
+    for tok in forced:
+        out.append(m.decode([tok], n))
         n += 1
     m.close()
-    d = np.abs(np.array(out) - g[fn + "_e2e_logits"])
-    tmax = max(1.5 * g[fn + "_e2e_spread_max"].max(), 1e-3)
-    tmed = max(1.5 * g[fn + "_e2e_spread_median"].max(), 2e-4)
+    got = np.array(out)
+    d = np.abs(got - g[fn + "_e2e_logits"])
+    tmax = 2 * max(float(g[fn + "_e2e_spread_max"].max()), SPREAD_MAX)
+    tmed = 2 * max(float(g[fn + "_e2e_spread_median"].max()), SPREAD_MED)
     print(fn, "gpu vs ref max", d.max(axis=1), "| spread", g[fn + "_e2e_spread_max"])
-    assert np.all(d.max(axis=1) <= tmax)
-    assert np.all(np.median(d, axis=1) <= tmed)
+    assert np.all(d.max(axis=1) <= tmax), d.max(axis=1)
+    assert np.all(np.median(d, axis=1) <= tmed), np.median(d, axis=1)
+    R.lib().orc_set_fa_f32_accum(1)
+    try:
+        o = R.OracleLlama(R.TINY, types, 1234)
+        ref32 = [o.eval(prompt, 0)]
+        n = len(prompt)
+        for tok in forced:
+            ref32.append(o.eval([tok], n))
+            n += 1
+    finally:
+        R.lib().orc_set_fa_f32_accum(0)
+    e = np.abs(got - np.array(ref32))
+    print(fn, "gpu vs oracle(f32 accumulation) max", e.max(), "median", np.median(e))
+    assert e.max() <= 2 * SPREAD_MAX and np.median(e) <= 2 * SPREAD_MED
