@@ -362,3 +362,127 @@ def test_generate_process_time_includes_the_prefill(model):
     t_ref = time.perf_counter() - t0
     m.close()
     assert t_proc >= 0.3 * t_ref, (t_proc, t_ref)
+
+
+def _antislop_script(m, prompt_ids, phrases, limit, max_len, piece_of):
+    """the reference's generation loop with antislop, restated from gpttype_adapter.cpp:3218-3341 + ContextRewind
+    (:424-480) for greedy sampling on the in-process model: the sampled token's piece enters a delay line of `limit`
+    entries; when the held-back text contains a banned phrase (lower case), the context is rewound to just before
+    the shortest tail holding it, that tail's first token is banned at that position, and the new last context
+    token is evaluated again.  Returns the streamed text and the number of sampled tokens."""
+    import numpy as np
+    ctx = list(prompt_ids)
+    logits = m.decode(ctx, 0)
+    delayed, out, slop, n_gen = [], [], {}, 0
+    while n_gen < max_len:
+        lg = logits.copy()
+        for b in slop.get(len(ctx), []):
+            lg[b] = -np.inf
+        t = int(np.argmax(lg))
+        n_gen += 1
+        delayed.append(piece_of(t))
+        while len(delayed) > limit:
+            out.append(delayed.pop(0))
+        scan = b"".join(delayed).lower()
+        rewound = False
+        for ph in phrases:
+            if ph not in scan:
+                continue
+            check, r = b"", 0
+            for d in reversed(delayed):
+                check = d + check
+                r += 1
+                if ph in check.lower():
+                    break
+            full = ctx + [t]
+            if r > 0 and len(full) - r > 0:
+                last_tok = full[len(full) - r]
+                delayed = delayed[:len(delayed) - r]
+                ctx = full[:len(full) - r]
+                logits = m.decode([ctx[-1]], len(ctx) - 1)
+                slop.setdefault(len(ctx), []).append(last_tok)
+                rewound = True
+                break
+        if rewound:
+            continue
+        logits = m.decode([t], len(ctx))
+        ctx.append(t)
+    return b"".join(out + delayed), n_gen
+
+
+def test_generate_antislop_phrase_ban(model):
+    """antislop phrase banning (gpttype_adapter.cpp:2514-2545 classification, :3218-3341 detection and rewind) against
+    the loop restated in Python on the in-process model (_antislop_script; parity unpinned: ref_sampler has no
+    generation loop, so these are scripted expectations derived from those lines): a phrase spanning two generated
+    tokens is never streamed, the text before it is unchanged, the result equals the script's, and the delay line
+    holds the text back only by the phrase's token count + 3."""
+    import koboldcpp_amd.lib as K
+    h, X, toks, ttypes, types = model
+    prompt = b"hello world the"
+    r = h.token_count(prompt, True)
+    ids = [r.ids[i] for i in range(r.count)]
+    gi = X.generation_inputs()
+    gi.prompt = prompt
+    gi.memory = b""
+    gi.max_context_length = 248
+    gi.max_length = 16
+    gi.temperature = 0.0
+    gi.top_k = 1
+    gi.rep_pen = 1.0
+    gi.bypass_eos_token = True
+    gi.seed = 7
+    base = h.generate(gi).text
+    hp = dict(R.TINY, n_ctx=256)
+    m = K.Model(hp, types)
+    m.synth(1234)
+    pf = lambda t: piece(toks, ttypes, t)
+    plain, _ = _antislop_script(m, ids, [], 0, 16, pf)
+    assert plain == base
+    # greedy tokens of the plain run; a phrase made of two consecutive visible pieces that first occurs there
+    m.decode(ids, 0, want_logits=False)
+    seq = [m.argmax()]
+    n = len(ids)
+    for _ in range(15):
+        seq.append(m.decode_greedy(n))
+        n += 1
+    phrase = None
+    for i in range(2, 12):
+        a, b = pf(seq[i]), pf(seq[i + 1])
+        cand = (a + b).lower()
+        if len(a) >= 1 and len(b) >= 1 and len(cand) >= 2 and cand not in b"".join(pf(t) for t in seq[:i + 1]).lower() \
+                and cand not in b.lower():
+            phrase = cand
+            break
+    if phrase is None:
+        pytest.skip("the synthetic model's greedy text has no two-piece phrase to ban")
+    gi.banned_tokens[0] = phrase
+    got = h.generate(gi)
+    ntok = h.token_count(phrase, False).count
+    want, n_sampled = _antislop_script(m, ids, [phrase], ntok + 3, 16, pf)
+    m.close()
+    assert phrase not in got.text.lower()
+    assert got.text == want
+    assert got.text[:base.lower().find(phrase)] == base[:base.lower().find(phrase)]
+    assert h.get_last_token_count() == n_sampled
+    gi.banned_tokens[0] = None
+
+
+def test_generate_render_special(model):
+    """render_special (gpttype_adapter.cpp:3253-3257): a forced EOS (bypassed, so generation continues) renders as
+    its text with render_special and as nothing without (the piece of a CONTROL token, llama_token_to_piece special)"""
+    h, X, toks, ttypes, _ = model
+    gi = X.generation_inputs()
+    gi.prompt = b"hello world"
+    gi.max_context_length = 248
+    gi.max_length = 1
+    gi.temperature = 0.0
+    gi.top_k = 1
+    gi.rep_pen = 1.0
+    gi.bypass_eos_token = True
+    gi.seed = 3
+    gi.logit_biases[0].token_id = 2                       # </s>
+    gi.logit_biases[0].bias = 1000.0
+    gi.render_special = False
+    assert h.generate(gi).text == b""
+    gi.render_special = True
+    assert h.generate(gi).text == b"</s>"
