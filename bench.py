@@ -127,6 +127,9 @@ def cpu_baseline(hp, types, threads, depth=3840, n_ub=512, n_gen=16, threads2=8)
         pass
     return {"value": round(n_gen / info["decode_s"], 3), "unit": "tok/s (decode)", "cores": threads,
             "cpu_model": cpu, "host_cpus": os.cpu_count(),
+            "cores_reason": "the GPU box grants this job a 16-CPU share (OMP_NUM_THREADS=16 there; nproc shows the whole "
+                            "host's CPUs, which other jobs use): more threads would time contention with them, not the "
+                            "reference; the 8-thread line is SURVEY.md 8d's setting",
             "kind": "reference",
             "context_depth": [depth, depth + n_gen],
             "prefill_tok_s_last_ubatch": round(n_ub / info["prefill_s"], 3),

@@ -826,7 +826,10 @@ generation_outputs generate(const generation_inputs in) {
     if (!mu_init && (S.P.mirostat == 1 || S.P.mirostat == 2)) { g_mirostat_mu = 2.0f * S.P.mirostat_tau; mu_init = true; }
     // last_n_tokens: repeat_last_n zeros, then every context token in order (:2892-2895, 3236-3243, 3420-3425)
     std::vector<int> last_n(S.P.rep_pen_range, 0);
-    for (int t : e->ctx) { last_n.erase(last_n.begin()); last_n.push_back(t); }
+    for (int t : e->ctx) {
+        if (!last_n.empty()) last_n.erase(last_n.begin());
+        last_n.push_back(t);
+    }
     std::vector<std::string> stops;
     std::vector<int> special_stops;          // a stop string that is one special token without text (:2497-2510)
     for (int k = 0; k < KCPP_STOP_TOKEN_MAX; ++k)
@@ -855,7 +858,7 @@ generation_outputs generate(const generation_inputs in) {
         const auto sb = slop.find((int)e->ctx.size());
         const int t = sample(*e, S, last_n, rng, &g_mirostat_mu, sb == slop.end() ? nullptr : &sb->second);
         if (t < 0) { fprintf(stderr, "[kcpp] generate: sampling failed: %s\n", kcpp_last_error()); break; }
-        last_n.erase(last_n.begin());
+        if (!last_n.empty()) last_n.erase(last_n.begin());     // (:3238: an antislop rewind may have emptied it)
         last_n.push_back(t);
         const bool eos_tok = t == e->tok.eos() || (t == e->tok.eot() && t != -1);
         const bool special_stop = std::find(special_stops.begin(), special_stops.end(), t) != special_stops.end();

@@ -436,6 +436,12 @@ def test_generate_antislop_phrase_ban(model):
     m = K.Model(hp, types)
     m.synth(1234)
     pf = lambda t: piece(toks, ttypes, t)
+    import numpy as np
+    lg = m.decode(ids, 0)
+    first = m.argmax()
+    lg1 = m.decode([first], len(ids))
+    second = m.argmax()
+    assert int(np.argmax(lg)) == first and int(np.argmax(lg1)) == second, (int(np.argmax(lg)), first, int(np.argmax(lg1)), second)
     plain, _ = _antislop_script(m, ids, [], 0, 16, pf)
     assert plain == base
     # greedy tokens of the plain run; a phrase made of two consecutive visible pieces that first occurs there
