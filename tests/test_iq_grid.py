@@ -207,3 +207,59 @@ def test_gpu_model_vs_reference(env, kq, graphs):
     e = np.abs(got - np.array(ref32))
     print(fn, "gpu vs oracle(f32 accumulation) max", e.max(), "median", np.median(e))
     assert e.max() <= 2 * SPREAD_MAX and np.median(e) <= 2 * SPREAD_MED
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fn", ["iq2_xxs", "iq1_m", "iq3_s"])
+def test_gpu_gguf_load_and_generate(env, tmp_path, fn):
+    """a GGUF file with the grid type (tests/gguf_writer.py; the same synthetic weights) through the drop-in ABI:
+    load_model accepts it and generate()'s greedy text equals the in-process model's greedy decode"""
+    torch, K = env
+    import gguf_writer as GW
+    from koboldcpp_amd import expose as X
+    T = R.IQ_GRID[fn]
+    types = R.iq_grid_types(R.TINY["n_layer"], T)
+    path = str(tmp_path / (fn + ".gguf"))
+    toks = GW.llama_gguf(path, R.TINY, types, 1234, GW.WORDS)
+    _, _, ttypes = GW.spm_vocab(R.TINY["n_vocab"], GW.WORDS)
+    h = X.init_library()
+    li = X.load_model_inputs()
+    li.model_filename = path.encode()
+    li.max_context_length = 248
+    li.blasbatchsize = 512
+    li.gpulayers = 999
+    li.rope_freq_base = 10000.0
+    li.rope_freq_scale = 0.0
+    assert h.load_model(li)
+    prompt = b"hello world the"
+    r = h.token_count(prompt, True)
+    ids = [r.ids[i] for i in range(r.count)]
+    gi = X.generation_inputs()
+    gi.prompt = prompt
+    gi.memory = b""
+    gi.max_context_length = 248
+    gi.max_length = 8
+    gi.temperature = 0.0
+    gi.top_k = 1
+    gi.rep_pen = 1.0
+    gi.bypass_eos_token = True
+    gi.seed = 7
+    out = h.generate(gi)
+    m = K.Model(dict(R.TINY, n_ctx=256), types)
+    m.synth(1234)
+    m.decode(ids, 0, want_logits=False)
+    want = [m.argmax()]
+    n = len(ids)
+    for _ in range(7):
+        want.append(m.decode_greedy(n))
+        n += 1
+    m.close()
+
+    def piece(t):
+        s = toks[t]
+        if ttypes[t] in (2, 3, 5):
+            return b""
+        if ttypes[t] == 6:
+            return bytes([int(s[3:5], 16)])
+        return s.replace("▁", " ").encode()
+    assert out.status == 1 and out.text == b"".join(piece(t) for t in want)
