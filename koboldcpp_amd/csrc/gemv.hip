@@ -19,12 +19,28 @@
 
 // ---------------------------------------------------------------- kernel
 // mode 0: Y[c][n] = dot (+ res[c][n] if res)      mode 1 (GLU): Y[c][n] = silu(dot(W,n)) * dot(W2,n)
+// ex (MoE, optional): the expert slice W + e * ebytes with e = ex.eid[0] read on the device (clamped to
+// [0, n_exp)), and mode 0's product scaled by ex.escale[0] (the router weight: llm_build_moe_ffn's ggml_mul)
+struct GemvExpert {
+    const int32_t *eid;
+    int64_t ebytes;
+    int n_exp;
+    const float *escale;
+};
 template <int TYPE, int R, int NC, int MODE>
 __global__ void __launch_bounds__(256) k_gemv(const uint8_t *__restrict__ W, const uint8_t *__restrict__ W2,
                                               int64_t K, int64_t N, const uint8_t *__restrict__ act, int64_t M,
                                               int64_t Mtot, int64_t c0,
-                                              float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr) {
+                                              float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr,
+                                              const GemvExpert ex) {
     using A = typename ActOf<TYPE>::T;
+    if (ex.eid) {
+        int e = __builtin_amdgcn_readfirstlane(ex.eid[0]);
+        e = e < 0 ? 0 : (e >= ex.n_exp ? ex.n_exp - 1 : e);
+        W += (int64_t)e * ex.ebytes;
+        if (W2) W2 += (int64_t)e * ex.ebytes;
+    }
+    const float esc = ex.escale ? ex.escale[0] : 1.0f;
     constexpr int E = Unit<TYPE>::ELEMS;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -77,7 +93,10 @@ __global__ void __launch_bounds__(256) k_gemv(const uint8_t *__restrict__ W, con
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     const int64_t n = row0 + r;
-                    if (n < N) Y[(c0 + c) * ldy + n] = acc[r][c] + (res ? res[(c0 + c) * ldr + n] : 0.0f);
+                    if (n < N) {
+                        const float v = ex.escale ? __fmul_rn(acc[r][c], esc) : acc[r][c];
+                        Y[(c0 + c) * ldy + n] = v + (res ? res[(c0 + c) * ldr + n] : 0.0f);
+                    }
                 }
             }
         }
@@ -86,12 +105,13 @@ __global__ void __launch_bounds__(256) k_gemv(const uint8_t *__restrict__ W, con
 
 template <int TYPE, int R, int MODE>
 static int launch_gemv_t(const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, int64_t Mtot,
-                         int64_t c0, float *Y, int64_t ldy, const float *res, int64_t ldr, hipStream_t s) {
+                         int64_t c0, float *Y, int64_t ldy, const float *res, int64_t ldr, hipStream_t s,
+                         const GemvExpert &ex) {
     const int rows_per_block = 4 * (MODE == 1 ? 1 : R);
     dim3 grid((unsigned)((N + rows_per_block - 1) / rows_per_block)), block(256);
 #define KCPP_GEMV_CASE(NCV)                                                                                    \
     hipLaunchKernelGGL((k_gemv<TYPE, R, NCV, MODE>), grid, block, 0, s, (const uint8_t *)W, (const uint8_t *)W2, K, N, \
-                       (const uint8_t *)act, M, Mtot, c0, Y, ldy, res, ldr)
+                       (const uint8_t *)act, M, Mtot, c0, Y, ldy, res, ldr, ex)
     if (M == 1) KCPP_GEMV_CASE(1);
     else if (M == 2) KCPP_GEMV_CASE(2);
     else if (M <= 4) KCPP_GEMV_CASE(4);
@@ -101,12 +121,15 @@ static int launch_gemv_t(const void *W, const void *W2, int64_t K, int64_t N, co
     return 0;
 }
 
-// columns [c0, c0+M) of an activation buffer holding Mtot columns
+// columns [c0, c0+M) of an activation buffer holding Mtot columns; eid != null: expert-indexed (see GemvExpert)
 int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, int64_t Mtot,
-              int64_t c0, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *stream) {
+              int64_t c0, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *stream,
+              const int32_t *eid, int64_t ebytes, int n_exp, const float *escale) {
     hipStream_t s = (hipStream_t)stream;
+    const GemvExpert ex{eid, ebytes, n_exp, escale};
     if (M < 1 || M > 8) return -1;
     if (type == KT_Q4_K_RS || type == KT_Q6_K_RS) {   // decode layouts: one RS mat-vec launch per column
+        if (eid) return -3;
         for (int64_t c = 0; c < M; ++c) {
             DecArgs a;
             memset(&a, 0, sizeof a);
@@ -122,8 +145,8 @@ int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     if (K % ks_block_elems(type) || K / E < 1) return -2;
 #define KCPP_T(T)                                                                   \
     case T:                                                                         \
-        return mode == 1 ? launch_gemv_t<T, 1, 1>(W, W2, K, N, act, M, Mtot, c0, Y, ldy, res, ldr, s) \
-                         : launch_gemv_t<T, 2, 0>(W, W2, K, N, act, M, Mtot, c0, Y, ldy, res, ldr, s);
+        return mode == 1 ? launch_gemv_t<T, 1, 1>(W, W2, K, N, act, M, Mtot, c0, Y, ldy, res, ldr, s, ex) \
+                         : launch_gemv_t<T, 2, 0>(W, W2, K, N, act, M, Mtot, c0, Y, ldy, res, ldr, s, ex);
     switch (type) {
         KCPP_T(KT_Q4_K)
         KCPP_T(KT_Q5_K)
@@ -150,6 +173,15 @@ extern "C" {
 int kcpp_gemv(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *stream) {
     return gemv_cols(type, W, W2, K, N, act, M, M, 0, Y, ldy, res, ldr, mode, stream);
+}
+
+// the same for one activation column with the weight slice of a device-resident expert id (MoE decode of the
+// types without a fused decode mat-vec: Q4_1 / Q5_1 / IQ*): W + e * ebytes, e = eid[0] clamped to [0, n_exp);
+// mode 0 scales the product by escale[0] when given
+int kcpp_gemv_expert(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, float *Y,
+                     const int32_t *eid, int64_t ebytes, int n_exp, const float *escale, int mode, void *stream) {
+    if (!eid || n_exp < 1) return -1;
+    return gemv_cols(type, W, W2, K, N, act, 1, 1, 0, Y, N, nullptr, 0, mode, stream, eid, ebytes, n_exp, escale);
 }
 
 }  // extern "C"

@@ -677,7 +677,23 @@ bool mul_mat_id(BackendCtx *bc, kggml_tensor *n) {
                 if (rc != 0 && (t > 0 || j > 0)) return chk(rc, "expert mat-vec");
             }
         if (rc == 0) return true;
-        // rc on the first (j, t): this type / shape has no fused expert mat-vec; the grouped path below
+        // rc on the first (j, t): this type / shape has no fused expert mat-vec (Q4_1 / Q5_1 / IQ*): per (j, t) the
+        // column quantized on its own, then the generic mat-vec on the expert slice its device-resident id selects
+        void *act1 = bc->act.get((size_t)kcpp_act_bytes(as->type, K, 1) + 256);
+        if (act1) {
+            rc = 0;
+            for (int64_t t = 0; t < n_tok && rc == 0; ++t)
+                for (int64_t j = 0; j < n_ids && rc == 0; ++j) {
+                    const float *x = (const float *)((const char *)b->data + (j % ne11) * b->nb[1] + t * b->nb[2]);
+                    float *y = (float *)((char *)n->data + j * n->nb[1] + t * n->nb[2]);
+                    const int32_t *eid = (const int32_t *)((const char *)ids->data + j * ids->nb[0] + t * ids->nb[1]);
+                    rc = kcpp_quantize_act(kcpp_vec_dot_type(as->type), x, K, act1, K, 1, s);
+                    if (rc == 0) rc = kcpp_gemv_expert(tt, W, nullptr, K, N, act1, y, eid, eb, (int)E, nullptr, 0, s);
+                }
+            if (rc == 0) return true;
+            return chk(rc, "expert mat-vec (generic)");
+        }
+        // otherwise the grouped path below
     }
     std::vector<int32_t> idh((size_t)n_ids * n_tok);
     if (hipStreamSynchronize(s) != hipSuccess) return set_err("mul_mat_id: stream error");

@@ -10,7 +10,10 @@ int kcpp_weight_repack(int type, const void *src_ggml, void *dst_kcpp, int64_t K
 int kcpp_weight_synth(int type, uint64_t seed, uint64_t tid, void *dst, int64_t K, int64_t N, void *stream);
 // columns [c0, c0 + M) (M <= 8) of an activation buffer of Mtot columns through the generic mat-vec (gemv.hip)
 int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, int64_t Mtot,
-              int64_t c0, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *stream);
+              int64_t c0, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *stream,
+              const int32_t *eid = nullptr, int64_t ebytes = 0, int n_exp = 0, const float *escale = nullptr);
+int kcpp_gemv_expert(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, float *Y,
+                     const int32_t *eid, int64_t ebytes, int n_exp, const float *escale, int mode, void *stream);
 // rows [row0, row0 + N) of the synthetic [K][N_full] tensor (a row-split slice)
 int kcpp_weight_synth_rows(int type, uint64_t seed, uint64_t tid, void *dst, int64_t K, int64_t N, int64_t row0,
                            void *stream);

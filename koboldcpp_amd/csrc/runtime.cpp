@@ -306,7 +306,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     for (int idx = 0; idx < n_tensors(*hp); ++idx)
         m->q81 |= types[idx] == KT_Q4_1 || types[idx] == KT_Q5_1 || types[idx] == KT_IQ4_NL || types[idx] == KT_IQ4_XS ||
                   is_iq_grid_type(types[idx]);
-    if (m->q81 && hp->n_expert > 0) { g_err = "Q4_1 / Q5_1 / IQ MoE models are not supported"; delete m; return nullptr; }
+
     m->device = device; m->il0 = il0; m->il1 = il1; m->has_embed = has_embed; m->has_output = has_output;
     m->ub = max_ubatch > 0 ? max_ubatch : 512;
     m->fa_exact = getenv("KCPP_FA_EXACT") && atoi(getenv("KCPP_FA_EXACT")) != 0;
@@ -784,6 +784,31 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
                             m->moe_w, 1, s) != 0) {
         RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, 1, hp.eps, s));
         RC(kcpp_moe_route(m->attn, E, t[9].d, t[9].type, E, hp.n_expert, NU, m->moe_ids, m->moe_w, 1, s));
+    }
+    if (m->q81) {
+        // types without a fused decode mat-vec (Q4_1 / Q5_1 / IQ*): ffn_norm + activation quantization once, then per
+        // slot the generic mat-vec on the expert slice its device-resident id selects (kcpp_gemv_expert)
+        const int vg = kcpp_vec_dot_type(t[6].type), vu = kcpp_vec_dot_type(t[7].type), vd = kcpp_vec_dot_type(t[8].type);
+        RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, 1, hp.eps, s));
+        RC(kcpp_quantize_act(vg, m->attn, E, m->act, E, 1, s));
+        if (vu != vg) RC(kcpp_quantize_act(vu, m->attn, E, m->act2, E, 1, s));
+        for (int j = 0; j < NU; ++j) {
+            const int32_t *id = m->moe_ids + j;
+            if (t[6].type == t[7].type) {
+                RC(kcpp_gemv_expert(t[6].type, t[6].d, t[7].d, E, F, m->act, m->h, id, (int64_t)t[6].slice_bytes,
+                                    hp.n_expert, nullptr, 1, s));
+            } else {
+                RC(kcpp_gemv_expert(t[6].type, t[6].d, nullptr, E, F, m->act, m->h, id, (int64_t)t[6].slice_bytes,
+                                    hp.n_expert, nullptr, 0, s));
+                RC(kcpp_gemv_expert(t[7].type, t[7].d, nullptr, E, F, vu != vg ? m->act2 : m->act, m->qkv, id,
+                                    (int64_t)t[7].slice_bytes, hp.n_expert, nullptr, 0, s));
+                RC(kcpp_silu_mul(m->h, m->h, m->qkv, F, s));
+            }
+            RC(kcpp_quantize_act(vd, m->h, F, m->act2, F, 1, s));
+            RC(kcpp_gemv_expert(t[8].type, t[8].d, nullptr, F, E, m->act2, m->moe_slots + j * E, id,
+                                (int64_t)t[8].slice_bytes, hp.n_expert, m->moe_w + j, 0, s));
+        }
+        return kcpp_moe_combine(m->x, m->moe_slots, E, NU, E, s);
     }
     for (int j = 0; j < NU; ++j) {
         if (t[6].type == t[7].type) {

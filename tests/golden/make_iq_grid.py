@@ -61,6 +61,20 @@ def main():
                     fn + "_e2e_spread_median": np.median(d, axis=1)})
         print(fn, "tiny spread max", d.max(axis=1).max(), "median", np.median(d, axis=1).max(),
               "logit std", a.std())
+    # Mixtral-shaped tiny MoE with expert weights of a grid type (and Q4_1: the other type without a fused decode
+    # mat-vec), through the reference's MUL_MAT_ID
+    for tag, T in (("moe_iq2_xxs", R.IQ2_XXS), ("moe_q4_1", R.Q4_1)):
+        rng = np.random.default_rng(20261018 + T)
+        types = R.moe_types(R.TINY_MOE["n_layer"], T)
+        prompt = [int(v) for v in rng.integers(1, R.TINY_MOE["n_vocab"], size=29)]
+        a, _ = R.run_ref_llama(R.TINY_MOE, types, 1234, prompt, 6)
+        forced = np.argmax(a, axis=1)[:-1].astype(np.int32)
+        b, _ = R.run_ref_llama(R.TINY_MOE, types, 1234, prompt, 6, forced=forced, binary=R.REF_BIN_SCALAR)
+        d = np.abs(a - b)
+        out.update({tag + "_e2e_types": np.array(types, np.int32), tag + "_e2e_prompt": np.array(prompt, np.int32),
+                    tag + "_e2e_logits": a, tag + "_e2e_forced": forced, tag + "_e2e_spread_max": d.max(axis=1),
+                    tag + "_e2e_spread_median": np.median(d, axis=1)})
+        print(tag, "tiny spread max", d.max(axis=1).max(), "median", np.median(d, axis=1).max())
     np.savez_compressed(os.path.join(HERE, "iq_grid.npz"), **out)
     print("wrote iq_grid.npz")
 
