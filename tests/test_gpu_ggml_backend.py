@@ -162,7 +162,9 @@ MM_CASES = [(R.Q4_K, 4096, 512, 1), (R.Q4_K, 4096, 384, 7), (R.Q4_K, 2048, 256, 
             (R.Q2_K, 4096, 256, 1), (R.Q2_K, 2048, 256, 24), (R.Q3_K, 4096, 256, 1), (R.Q3_K, 2048, 384, 40),
             (R.Q5_0, 4096, 256, 1), (R.Q5_0, 2048, 256, 24), (R.Q4_1, 4096, 256, 1), (R.Q4_1, 2048, 256, 24),
             (R.Q5_1, 4096, 256, 3), (R.Q5_1, 2048, 256, 40), (R.IQ4_NL, 4096, 256, 1), (R.IQ4_NL, 2048, 256, 24),
-            (R.IQ4_XS, 4096, 256, 1), (R.IQ4_XS, 2048, 256, 40)]
+            (R.IQ4_XS, 4096, 256, 1), (R.IQ4_XS, 2048, 256, 40),
+            (R.IQ2_XXS, 4096, 256, 1), (R.IQ2_XS, 2048, 256, 24), (R.IQ2_S, 4096, 256, 3), (R.IQ3_XXS, 2048, 256, 40),
+            (R.IQ3_S, 4096, 256, 1), (R.IQ1_S, 2048, 256, 24), (R.IQ1_M, 4096, 256, 2)]
 
 
 @pytest.mark.parametrize("case", MM_CASES, ids=lambda c: "t%d_%dx%d_m%d" % c)
@@ -208,7 +210,7 @@ def test_elementwise_ops_vs_reference_cpu(env):
 
 
 @pytest.mark.parametrize("t", [R.Q4_K, R.Q6_K, R.Q8_0, R.Q4_0, R.Q5_0, R.Q2_K, R.Q3_K, R.Q4_1, R.Q5_1, R.IQ4_NL, R.IQ4_XS,
-                               R.F16])
+                               R.IQ2_XXS, R.IQ2_XS, R.IQ2_S, R.IQ3_XXS, R.IQ3_S, R.IQ1_S, R.IQ1_M, R.F16])
 def test_get_rows_vs_reference_cpu(env, t):
     """token embedding gather (get_rows of a quantized or f16 table): dequantization is exact on both sides"""
     G, L, be = env
@@ -337,7 +339,7 @@ def _moe_sigs(G):
 
 MMID_CASES = [(R.Q4_K, 1), (R.Q4_K, 3), (R.Q4_K, 24), (R.Q5_K, 1), (R.Q5_K, 24), (R.Q6_K, 2), (R.Q6_K, 24),
               (R.Q8_0, 1), (R.Q8_0, 24), (R.Q4_0, 3), (R.Q2_K, 1), (R.Q3_K, 24), (R.Q4_1, 2), (R.Q5_1, 24),
-              (R.IQ4_NL, 2), (R.IQ4_XS, 24)]
+              (R.IQ4_NL, 2), (R.IQ4_XS, 24), (R.IQ2_XXS, 1), (R.IQ2_S, 24), (R.IQ3_XXS, 3), (R.IQ1_M, 2)]
 
 
 @pytest.mark.parametrize("case", MMID_CASES, ids=lambda c: "t%d_T%d" % c)
