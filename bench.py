@@ -101,7 +101,7 @@ def measure_roofline(K, torch, iters=64, pairs=8):
             "avg_us": round(ms * 1e3, 2)}
 
 
-def cpu_baseline(hp, types, threads, depth=3840, n_ub=512, n_gen=16, threads2=8):
+def cpu_baseline(hp, types, threads, depth=3840, n_ub=512, n_gen=32, threads2=8):
     """The REFERENCE ggml CPU build on the same synthetic weights, koboldcpp --benchmark semantics, on bounded samples:
     (1) at the GPU line's context depth: the prompt's last ubatch (positions depth-512..depth-1, attending over the
     whole prefix) and then n_gen greedy tokens at context depth..depth+n_gen; the earlier prompt positions are taken
