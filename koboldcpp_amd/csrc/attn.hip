@@ -12,6 +12,7 @@
 #include "attn_dec.h"
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
+#include "gemv_units.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -149,7 +150,7 @@ __global__ void __launch_bounds__(256) k_fa_decode(const uint16_t *__restrict__ 
 // DPP reduction; online softmax per wave (m, l wave-uniform); O: each lane accumulates its 8 dims over its
 // row's keys, rows summed once at the end (permlane swaps), waves merged in LDS.  Partials: O [H][NS][128],
 // (m, l) [H][NS] (m = -inf for an empty split).
-template <int G>
+template <int G, bool NT>
 __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
                                                  const uint16_t *__restrict__ vc, float *__restrict__ part_o,
                                                  float2 *__restrict__ part_ml, int H, int n_past_arg,
@@ -179,8 +180,13 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
         for (int i = 0; i < 4; ++i) {
             const int p = base + 4 * i + kq;
             const bool ok = p < p1;
-            kk[i] = ok ? *(const uint4 *)(kb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
-            vv[i] = ok ? *(const uint4 *)(vb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
+            if constexpr (NT) {      // K/V rows are read once per token: non-temporal (MI355X_MICROARCH.md nt-weights)
+                kk[i] = ok ? ld_nt(kb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
+                vv[i] = ok ? ld_nt(vb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
+            } else {
+                kk[i] = ok ? *(const uint4 *)(kb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
+                vv[i] = ok ? *(const uint4 *)(vb + (int64_t)p * kv_ld) : make_uint4(0, 0, 0, 0);
+            }
         }
     };
     int base = p0 + 16 * wave;
@@ -277,8 +283,13 @@ static void fa4_dispatch(const uint16_t *q16, const uint16_t *kc, const uint16_t
     // (an in-launch merge -- write-through partials, a per-kv-head ticket, the last split merging -- measured
     // 12.4 vs 10.6 us per layer at 3850 keys: draining the sc1 stores and the ticket round trip cost 1.5-3 us, more
     // than this launch boundary)
-    hipLaunchKernelGGL((k_fa_dec4<G>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past, n_past_dev, NS,
-                       scale, kv_ld, kv_hs, st);
+    static const bool nt = [] { const char *e = getenv("KCPP_FA_NT"); return e && atoi(e) != 0; }();
+    if (nt)
+        hipLaunchKernelGGL((k_fa_dec4<G, true>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past,
+                           n_past_dev, NS, scale, kv_ld, kv_hs, st);
+    else
+        hipLaunchKernelGGL((k_fa_dec4<G, false>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past,
+                           n_past_dev, NS, scale, kv_ld, kv_hs, st);
     if (qout) hipLaunchKernelGGL((k_fa_comb4<true, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, st,
                                  (unsigned *)nullptr);
     else hipLaunchKernelGGL((k_fa_comb4<false, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, st,
