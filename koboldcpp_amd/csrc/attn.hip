@@ -283,7 +283,9 @@ static void fa4_dispatch(const uint16_t *q16, const uint16_t *kc, const uint16_t
     // (an in-launch merge -- write-through partials, a per-kv-head ticket, the last split merging -- measured
     // 12.4 vs 10.6 us per layer at 3850 keys: draining the sc1 stores and the ticket round trip cost 1.5-3 us, more
     // than this launch boundary)
-    static const bool nt = [] { const char *e = getenv("KCPP_FA_NT"); return e && atoi(e) != 0; }();
+    // K/V rows are read once per token: non-temporal loads (MI355X_MICROARCH.md nt-weights) -- bench line 599.8 ->
+    // 632.5 tok/s; KCPP_FA_NT=0 restores the default policy
+    static const bool nt = [] { const char *e = getenv("KCPP_FA_NT"); return !e || atoi(e) != 0; }();
     if (nt)
         hipLaunchKernelGGL((k_fa_dec4<G, true>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past,
                            n_past_dev, NS, scale, kv_ld, kv_hs, st);

@@ -1563,12 +1563,15 @@ static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a
 // slot 72 (4 (c >> 3) + (m >> 3)) + (m & 7) + 8 (c & 7).
 __device__ __forceinline__ int swz(int m, int c) { return 72 * (4 * (c >> 3) + (m >> 3)) + (m & 7) + 8 * (c & 7); }
 
-struct Q4v4Smem {
-    i32x4 a[2][4][576];      // [buf][token tile][swz(row, chunk)]: 16 activation bytes, chunks 0..15 of the 256
+// TPW = 2 (v4): 4 row tiles (128 rows) x 2 token halves, 3 weight stages; TPW = 4 (v5): 8 row tiles (256 rows), every
+// wave against all 4 token tiles, so each dequantized weight fragment feeds twice the MFMAs; 2 weight stages (LDS).
+// Slot counts: the highest swizzled slot + 1 (activations 16 chunks: 568, weights 8 chunks: 280).
+template <int WR, int NST> struct Q4v4Smem {
+    i32x4 a[2][4][568];      // [buf][token tile][swz(row, chunk)]: 16 activation bytes, chunks 0..15 of the 256
     i32x4 bs[2][4][64];      // [buf][token tile][lane]: 8 bsums (int16) of the lane half's 128 elements
     float dy[2][128];        // [buf][token]: Q8_K scale of the super-block
-    uint4 wh[3][4][32];      // [stage][row tile][row]: Q4_K header (d, dmin, 12 B scales / mins)
-    i32x4 wq[3][4][288];     // [stage][row tile][swz(row, chunk)]: qs chunks 0..7 (pair p, half g: chunk 2p + g)
+    uint4 wh[NST][WR][32];   // [stage][row tile][row]: Q4_K header (d, dmin, 12 B scales / mins)
+    i32x4 wq[NST][WR][280];  // [stage][row tile][swz(row, chunk)]: qs chunks 0..7 (pair p, half g: chunk 2p + g)
 };
 
 // LDS-DMA issued from inline asm: the compiler does not track these writes, so it inserts no vmcnt(0) in front of
@@ -1595,41 +1598,44 @@ __device__ __forceinline__ int mulb(uint32_t x, uint32_t s) {
     return (int)__builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, x) * f);
 }
 
-template <int LAY>
+template <int LAY, int TPW>
 __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                                      const uint8_t *__restrict__ act, int64_t M, int64_t Mp, int MT,
                                                      float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr,
                                                      int KS, float *__restrict__ part, int XG) {
-    __shared__ Q4v4Smem S;
+    constexpr int WT = 4 / TPW, WR = 8 / WT, NR = 32 * WR, NST = TPW == 2 ? 3 : 2, NI = WR / 2;
+    __shared__ Q4v4Smem<WR, NST> S;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wr = wave & 3, wt = wave >> 2;
+    const int wr = wave % WR, wt = wave / WR;
     const int lr = lane & 31, kg = lane >> 5;
     const int64_t nwg = gridDim.x / KS, id = blockIdx.x % nwg;
     const int split = (int)(blockIdx.x / nwg);
     int64_t mt, nt;
-    xcd_tile(id, nwg, MT, (N + 127) / 128, XG, mt, nt);
-    const int64_t m0 = mt * 128, n0 = nt * 128;
+    xcd_tile(id, nwg, MT, (N + NR - 1) / NR, XG, mt, nt);
+    const int64_t m0 = mt * 128, n0 = nt * NR;
     const int64_t nsb = K / 256, bpr = nsb;
     const int8_t *qs = (const int8_t *)act;
     const float *dq = (const float *)(act + M * K);
     const int16_t *bsq = (const int16_t *)(act + M * K + M * nsb * 4);
     // DMA assignments (per super-block): A: token tile wave & 3, sub-blocks 4 (wave >> 2) .. +4; bsums: waves 0-3
-    // (tile = wave); dy: waves 4, 5 (tokens 64 (wave - 4) .. +64); weights: qs pairs 2 (wave >> 2), +1 of row tile
-    // wave & 3; headers: waves 0, 1 (row tiles 2 wave + (lane >> 5))
+    // (tile = wave); dy: waves 4, 5 (tokens 64 (wave - 4) .. +64); weights: NI groups of 8 rows, group i = 8u + wave
+    // (row tile i >> 2, rows 8 (i & 3) ..); headers: waves 0 .. NI - 1 (row tiles 2 wave + (lane >> 5))
     // A: token tile wave & 3, chunk half wave >> 2, row groups 0..3; lane: row 8k + (lane & 7), chunk 8h + (lane >> 3)
     const int att = wave & 3, ah8 = wave >> 2;
     const int8_t *arow = qs + min(m0 + 32 * att + (lane & 7), M - 1) * K + 16 * (8 * ah8 + (lane >> 3));
     const int16_t *bsrow = bsq + min(m0 + 32 * wave + lr, M - 1) * (K / 16) + 8 * kg;
     const float *dyrow = dq + min(m0 + 64 * max(wave - 4, 0) + lane, M - 1) * nsb;
-    // W qs: row tile wave & 3, row groups 2 (wave >> 2), +1; lane: row 8k + (lane & 7), chunk lane >> 3
-    const int wrt = wave & 3, wk = 2 * (wave >> 2);
-    const int64_t wrow = min(n0 + 32 * wrt + 8 * wk + (lane & 7), N - 1);
+    constexpr int64_t HS = LAY == 1 ? 16 : 144, QS = LAY == 1 ? 128 : 144;
+    const uint8_t *wq0[NI];
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        const int i = 8 * u + wave;
+        const int64_t row = min(n0 + 32 * (i >> 2) + 8 * (i & 3) + (lane & 7), N - 1);
+        wq0[u] = (LAY == 1 ? W + row * 144 * bpr + 16 * bpr : W + row * 144 * bpr + 16) + 16 * (lane >> 3);
+    }
     const int hrt = 2 * wave + kg;
     const int64_t hrow = min(n0 + 32 * hrt + lr, N - 1);
-    constexpr int64_t HS = LAY == 1 ? 16 : 144, QS = LAY == 1 ? 128 : 144;
-    const uint8_t *wq0 = (LAY == 1 ? W + wrow * 144 * bpr + 16 * bpr : W + wrow * 144 * bpr + 16) + 16 * (lane >> 3);
-    const int64_t w8 = min<int64_t>(8, N - 1 - min(n0 + 32 * wrt + 8 * wk + (lane & 7), N - 1)) * 144 * bpr;   // next group
     const uint8_t *wh0 = W + hrow * 144 * bpr;
     auto stage_a = [&](int buf, int64_t sb) {
 #pragma unroll
@@ -1641,74 +1647,57 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
     };
     auto stage_w = [&](int st, int64_t sb) {
 #pragma unroll
-        for (int u = 0; u < 2; ++u) dma16(wq0 + QS * sb + (u ? w8 : 0), &S.wq[st][wrt][72 * (wk + u)]);
-        if (wave < 2) dma16(wh0 + HS * sb, &S.wh[st][2 * wave][0]);
+        for (int u = 0; u < NI; ++u) {
+            const int i = 8 * u + wave;
+            dma16(wq0[u] + QS * sb, &S.wq[st][i >> 2][72 * (i & 3)]);
+        }
+        if (wave < NI) dma16(wh0 + HS * sb, &S.wh[st][2 * wave][0]);
     };
 
     const int64_t sbb = nsb * split / KS, sbe = nsb * (split + 1) / KS;
-    f16acc tot[2];
+    f16acc tot[TPW];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TPW; ++j)
 #pragma unroll
         for (int i = 0; i < 16; ++i) tot[j][i] = 0.0f;
     stage_a(0, sbb);
-    stage_w(0, sbb);
-    if (sbb + 1 < sbe) stage_w(1, sbb + 1);
+#pragma unroll
+    for (int q = 0; q < NST - 1; ++q)
+        if (sbb + q < sbe) stage_w(q, sbb + q);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
     int st = 0;
     for (int64_t sb = sbb; sb < sbe; ++sb) {
         const int buf = (int)((sb - sbb) & 1);
-        const bool w2 = sb + 2 < sbe && KCPP_GEMM_PROBE != 1 && KCPP_GEMM_PROBE != 5;
+        const bool wn = sb + NST - 1 < sbe && KCPP_GEMM_PROBE != 1 && KCPP_GEMM_PROBE != 5;
 #if KCPP_GEMM_PROBE != 1 && KCPP_GEMM_PROBE != 4
         if (sb + 1 < sbe) stage_a(buf ^ 1, sb + 1);
 #endif
-        if (w2) stage_w(st == 0 ? 2 : st - 1, sb + 2);
+        if (wn) stage_w(st == 0 ? NST - 1 : st - 1, sb + NST - 1);
         const uint4 hc = S.wh[st][wr][lr];
         uint32_t sc_lo, sc_hi, m_lo, m_hi;
         k4_all(hc, sc_lo, sc_hi, m_lo, m_hi);
-        i32x16 ah[2], al[2];
+        // the super-block's weight fragments dequantized once (bw[p]: q*(sc>>3), q*(sc&7) of sub-blocks 2p, 2p+1),
+        // then per token tile its 16 MFMAs and right behind them its epilogue (v3's: tot -= dy * dmin * (sum_j m_j
+        // bsum_j), then tot += dy * (d * isum)), so only one tile's integer accumulators are live
+        i32x4 bw[4][4];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const i32x4 w4 = S.wq[st][wr][swz(lr, 2 * p + kg)];
             const uint32_t sdw = p < 2 ? sc_lo : sc_hi;
             const uint32_t s0 = (sdw >> (16 * (p & 1))) & 0xFF, s1 = (sdw >> (16 * (p & 1) + 8)) & 0xFF;
             const uint32_t h0 = s0 >> 3, l0 = s0 & 7, h1 = s1 >> 3, l1 = s1 & 7;
-            i32x4 bh0, bl0, bh1, bl1;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 const uint32_t x = (uint32_t)w4[e];
                 const uint32_t lo = x & 0x0F0F0F0Fu, hi = (x >> 4) & 0x0F0F0F0Fu;
-                bh0[e] = mulb(lo, h0);
-                bl0[e] = mulb(lo, l0);
-                bh1[e] = mulb(hi, h1);
-                bl1[e] = mulb(hi, l1);
-            }
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                const int tt = 2 * wt + j;
-                const i32x4 a0 = S.a[buf][tt][swz(lr, 4 * p + kg)], a1 = S.a[buf][tt][swz(lr, 4 * p + 2 + kg)];
-#if KCPP_GEMM_PROBE == 2
-                ah[j][0] += a0[0] * bh0[0] + a1[1] * bl1[1];
-                al[j][0] += a0[1] * bl0[0] + a1[0] * bh1[1];
-                continue;
-#endif
-                if (p == 0) {
-                    i32x16 z;
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) z[i] = 0;
-                    ah[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bh0, z, 0, 0, 0);
-                    al[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bl0, z, 0, 0, 0);
-                } else {
-                    ah[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bh0, ah[j], 0, 0, 0);
-                    al[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bl0, al[j], 0, 0, 0);
-                }
-                ah[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bh1, ah[j], 0, 0, 0);
-                al[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bl1, al[j], 0, 0, 0);
+                bw[p][0][e] = mulb(lo, h0);
+                bw[p][1][e] = mulb(lo, l0);
+                bw[p][2][e] = mulb(hi, h1);
+                bw[p][3][e] = mulb(hi, l1);
             }
         }
-        // epilogue (v3's): tot -= dy * dmin * (sum_j m_j bsum_j), then tot += dy * (d * isum)
         h8v bm;
         const uint32_t mdw = kg ? m_hi : m_lo;
 #pragma unroll
@@ -1719,8 +1708,30 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
         }
         const float dw = h2f((uint16_t)(hc.x & 0xFFFF)), dm = h2f((uint16_t)(hc.x >> 16));
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int tt = 2 * wt + j;
+        for (int j = 0; j < TPW; ++j) {
+            const int tt = TPW * wt + j;
+            i32x16 ah, al;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const i32x4 a0 = S.a[buf][tt][swz(lr, 4 * p + kg)], a1 = S.a[buf][tt][swz(lr, 4 * p + 2 + kg)];
+#if KCPP_GEMM_PROBE == 2
+                ah[0] += a0[0] * bw[p][0][0] + a1[1] * bw[p][3][1];
+                al[0] += a0[1] * bw[p][1][0] + a1[0] * bw[p][2][1];
+                continue;
+#endif
+                if (p == 0) {
+                    i32x16 z;
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) z[i] = 0;
+                    ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bw[p][0], z, 0, 0, 0);
+                    al = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bw[p][1], z, 0, 0, 0);
+                } else {
+                    ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bw[p][0], ah, 0, 0, 0);
+                    al = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bw[p][1], al, 0, 0, 0);
+                }
+                ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bw[p][2], ah, 0, 0, 0);
+                al = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bw[p][3], al, 0, 0, 0);
+            }
             float dyv[16];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -1742,27 +1753,29 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
             for (int r = 0; r < 16; ++r) tot[j][r] = fmaf(-__fmul_rn(dyv[r], dm), accm[r], tot[j][r]);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float is = (float)(ah[j][r] * 8 + al[j][r]);
+                const float is = (float)(ah[r] * 8 + al[r]);
                 tot[j][r] = fmaf(dyv[r], __fmul_rn(dw, is), tot[j][r]);
             }
         }
-        // A (sb + 1) and W (sb + 1) must have landed; W (sb + 2), issued last, may stay in flight (in-order retire)
-        if (w2) {
-            if (wave < 2) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        // A (sb + 1) and W (sb + 1) must have landed; with three stages W (sb + 2), issued last, may stay in flight
+        // (in-order retire)
+        if (NST == 3 && wn) {
+            static_assert(NST != 3 || NI == 2, "vmcnt counts below assume two weight groups per wave");
+            if (wave < NI) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
-        st = st == 2 ? 0 : st + 1;
+        st = st == NST - 1 ? 0 : st + 1;
     }
     const int64_t n = n0 + 32 * wr + lr;
     if (n >= N) return;
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < TPW; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-            const int64_t t = m0 + 32 * (2 * wt + j) + (r & 3) + 8 * (r >> 2) + 4 * kg;
+            const int64_t t = m0 + 32 * (TPW * wt + j) + (r & 3) + 8 * (r >> 2) + 4 * kg;
             if (KS > 1) part[((int64_t)split * Mp + t) * N + n] = tot[j][r];
             else if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
         }
@@ -1901,7 +1914,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     // (split-K); its tile grid is split in two along K when it has <= 128 tiles.  Variant 11 forces v4 (split rule),
     // 13 v4 unsplit, 3 / 4 force v3.
     const bool v4_pick = gv == 0;
-    if ((type == KT_Q4_K || type == KT_Q4_K_RS) && (gv == 11 || gv == 12 || gv == 13 || v4_pick) && bs_aligned && M > 32) {
+    if ((type == KT_Q4_K || type == KT_Q4_K_RS) && (gv == 11 || gv == 12 || gv == 13 || gv == 14 || v4_pick) && bs_aligned && M > 32) {
         // v4: int8 MFMA straight from the Q8_K buffer (no fragment image); 128 x 128 tiles, split-K when the tile
         // grid is small
         const int64_t nt = (N + 127) / 128;
@@ -1910,15 +1923,20 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         // tiles), never from M: the split changes the f32 summation order, and a prompt must give the same bits
         // however it is cut into ubatches (tests/test_gpu_fullsize.py)
         const int KS = (gv != 13 && mode == 0 && (K / 256) % 2 == 0 && nt <= 32) ? 2 : 1;
-        const unsigned nwg = (unsigned)(MT * nt * KS);
+        // v5 (TPW = 4: 256-row tiles, each dequantized fragment feeding all 128 tokens' MFMAs) wherever its grid
+        // still covers ~7/8 of the CUs; same per-element arithmetic and order as v4 (and KS = 1 on both), so the
+        // choice never changes a bit (tools/gemm_ab.py, M = 512, v4 -> v5: gate|up 28672 rows 214.1 -> 188.6 us,
+        // gate + up 14336 rows 217.7 -> 201.0; q|k|v 6144 rows 52.3 -> 86.0 on its 96-workgroup grid, so not
+        // there).  Variant 14 forces v5.
+        const bool v5 = gv == 14 || (gv == 0 && KS == 1 && MT * ((N + 255) / 256) >= 224);
+        const int64_t ntw = v5 ? (N + 255) / 256 : nt;
+        const unsigned nwg = (unsigned)(MT * ntw * KS);
         const int XG = gv == 12 ? 2 : 1;
         auto launch4 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
-            if (type == KT_Q4_K_RS)
-                hipLaunchKernelGGL(k_gemm_q4v4<1>, dim3(nwg), dim3(512), 0, s, (const uint8_t *)w, K, N, (const uint8_t *)act,
-                                   M, Mp, MT, y, ly, r, lr, KS, part, XG);
-            else
-                hipLaunchKernelGGL(k_gemm_q4v4<0>, dim3(nwg), dim3(512), 0, s, (const uint8_t *)w, K, N, (const uint8_t *)act,
-                                   M, Mp, MT, y, ly, r, lr, KS, part, XG);
+            auto kern = type == KT_Q4_K_RS ? (v5 ? k_gemm_q4v4<1, 4> : k_gemm_q4v4<1, 2>)
+                                           : (v5 ? k_gemm_q4v4<0, 4> : k_gemm_q4v4<0, 2>);
+            hipLaunchKernelGGL(kern, dim3(nwg), dim3(512), 0, s, (const uint8_t *)w, K, N, (const uint8_t *)act, M, Mp, MT,
+                               y, ly, r, lr, KS, part, XG);
             KCPP_CHECK(hipGetLastError());
             if (KS > 1) {
                 hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,

@@ -46,8 +46,18 @@ def model(tmp_path_factory):
     li.rope_freq_base = 10000.0
     li.rope_freq_scale = 0.0     # koboldcpp.py default --ropeconfig 0: automatic RoPE
     assert h.load_model(li)
+    _TINY.update(li=li, path=path)
     _, _, ttypes = GW.spm_vocab(R.TINY["n_vocab"], WORDS)
     return h, X, toks, ttypes, types
+
+
+_TINY = {}
+
+
+def _reload_tiny(model):
+    """load the module's tiny GGUF again: the MoE / split tests above replace the loaded model"""
+    h = model[0]
+    assert h.load_model(_TINY["li"])
 
 
 def test_token_count_spm(model):
@@ -177,6 +187,7 @@ def test_greedy_respects_logit_bias(model):
     unused token, whose piece is empty): a +1000 bias forces its token, a ban beside another +1000 moves the pick,
     and token 0 (<unk>, empty piece) at +1000 beats a visible token at +999."""
     h, X, toks, ttypes, _ = model
+    _reload_tiny(model)
     gi = X.generation_inputs()
     gi.prompt = b"hello world"
     gi.max_context_length = 248
@@ -418,6 +429,7 @@ def test_generate_antislop_phrase_ban(model):
     holds the text back only by the phrase's token count + 3."""
     import koboldcpp_amd.lib as K
     h, X, toks, ttypes, types = model
+    _reload_tiny(model)
     prompt = b"hello world the"
     r = h.token_count(prompt, True)
     ids = [r.ids[i] for i in range(r.count)]
@@ -477,6 +489,7 @@ def test_generate_render_special(model):
     """render_special (gpttype_adapter.cpp:3253-3257): a forced EOS (bypassed, so generation continues) renders as
     its text with render_special and as nothing without (the piece of a CONTROL token, llama_token_to_piece special)"""
     h, X, toks, ttypes, _ = model
+    _reload_tiny(model)
     gi = X.generation_inputs()
     gi.prompt = b"hello world"
     gi.max_context_length = 248

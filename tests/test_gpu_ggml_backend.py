@@ -322,7 +322,7 @@ def test_unsupported_ops_are_refused(env):
     ggml_backend_sched then keeps such nodes on the CPU backend)"""
     G, L, be = env
     ctx = G.ggml_init(InitParams(1 << 20, None, True))
-    w = G.ggml_new_tensor_2d(ctx, 16, 256, 4)                     # GGML_TYPE_IQ2_XXS: no kernel here
+    w = G.ggml_new_tensor_2d(ctx, 15, 256, 4)                     # GGML_TYPE_Q8_K weights: no kernel here
     x = G.ggml_new_tensor_2d(ctx, R.F32, 256, 2)
     assert not G.ggml_backend_supports_op(be, G.ggml_mul_mat(ctx, w, x))
     w2 = G.ggml_new_tensor_2d(ctx, R.Q4_K, 256, 4)

@@ -1,8 +1,13 @@
 #!/bin/bash
-# round-4 GPU session: the whole GPU suite, the bench A/B of non-temporal K/V loads in decode attention, and the
-# engine variants + stamps.  Logs under gpurun_out/.
+# round-4 GPU session: the prefill GEMM A/B (v4 / v5, with and without SLP-packed f32), the whole GPU suite, the
+# bench A/B of non-temporal K/V loads in decode attention, and the engine variants + stamps.  Logs under gpurun_out/.
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out
+for lib in koboldcpp_hipblas koboldcpp_hipblas_noslp; do
+  [ -f koboldcpp_amd/$lib.so ] || continue
+  KCPP_LIB=$PWD/koboldcpp_amd/$lib.so timeout -k 10 240 python -u tools/gemm_ab.py 0 14 > gpurun_out/gemm_ab_$lib.log 2>&1 || exit $?
+  sed "s/^/$lib /" gpurun_out/gemm_ab_$lib.log
+done
 GPU_TEST_TIMEOUT=700 bash tools/gpu_tests.sh tests/
 rc=$?
 echo "tests rc=$rc"
