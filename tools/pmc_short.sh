@@ -7,7 +7,7 @@ out=${1:-gpurun_out/pmc_short}
 mkdir -p $out
 i=0
 for c in "rs wo q4k pro0" "rs qkv q4k pro1 rope" "rs down q4k pro2" "rs down q6k pro2"; do
-  i=$((i+1))
+  i=$((i+1)); mkdir -p $out/c$i
   for ctr in FETCH_SIZE WRITE_SIZE; do
     PROBE_CASE="$c" timeout -k 10 120 rocprofv3 --pmc $ctr --output-format csv -d $out/c$i/$ctr -o pmc -- python3 tools/stream_probe.py dec > $out/c$i/$ctr.log 2>&1 || exit $?
   done
