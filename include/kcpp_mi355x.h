@@ -343,6 +343,10 @@ int kcpp_model_set_fa_exact(kcpp_model *m, int enable);
 /* MoE: the expert ids the model's last MoE layer routed the last prefill's tokens to, n = T * n_expert_used
  * int32 ([token][slot], the router's top-k order); diagnostics for routing-aware parity tests */
 int kcpp_model_moe_ids(kcpp_model *m, int32_t *out, int n);
+/* MoE diagnostics: enable (1) / disable (0) a trace of single-token routing -- each MoE layer of the stage copies its
+ * top-k expert ids into [layer][n_expert_used] every decode step; _read returns the last step's n ids */
+int kcpp_model_moe_trace(kcpp_model *m, int enable);
+int kcpp_model_moe_trace_read(kcpp_model *m, int32_t *out, int n);
 /* K / V cache types (llama_context_params type_k / type_v): KT_F16 (default) or quantized KT_Q8_0 / KT_Q4_0 for
  * both (koboldcpp --quantkv).  Reallocates and clears the caches; quantized caches run single-token decode
  * through the unfused per-op path and refuse kcpp_model_kv_shift (koboldcpp turns context shift off with

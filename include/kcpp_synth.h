@@ -31,10 +31,10 @@ enum kcpp_type {
     KT_Q8_0 = 8, KT_Q8_1 = 9, KT_Q2_K = 10, KT_Q3_K = 11, KT_Q4_K = 12,
     KT_Q5_K = 13, KT_Q6_K = 14, KT_Q8_K = 15, KT_IQ2_XXS = 16, KT_IQ2_XS = 17, KT_IQ3_XXS = 18, KT_IQ1_S = 19,
     KT_IQ4_NL = 20, KT_IQ3_S = 21, KT_IQ2_S = 22, KT_IQ4_XS = 23, KT_IQ1_M = 29, KT_BF16 = 30,
-    /* GPU-internal row-major decode layouts of Q4_K / Q6_K (same bytes per row, re-arranged inside
+    /* GPU-internal row-major decode layouts of Q4_K / Q5_K / Q6_K (same bytes per row, re-arranged inside
        each row so the single-token mat-vec reads 1 KiB-contiguous wave loads; csrc/kcpp_common.h).
        Not ggml ids: they never leave the device library. */
-    KT_Q4_K_RS = 112, KT_Q6_K_RS = 114
+    KT_Q4_K_RS = 112, KT_Q5_K_RS = 113, KT_Q6_K_RS = 114
 };
 
 /* the lattice-grid types (IQ1 / IQ2 / IQ3): ggml layout on the device, decoded through the code books */
@@ -45,7 +45,7 @@ KS_FN int is_iq_grid_type(int t) {
 
 /* the ggml type whose blocks a layout holds */
 KS_FN int ks_base_type(int type) {
-    return type == KT_Q4_K_RS ? KT_Q4_K : (type == KT_Q6_K_RS ? KT_Q6_K : type);
+    return type == KT_Q4_K_RS ? KT_Q4_K : (type == KT_Q5_K_RS ? KT_Q5_K : (type == KT_Q6_K_RS ? KT_Q6_K : type));
 }
 
 KS_FN uint64_t ks_mix(uint64_t z) {          /* splitmix64 finalizer */
@@ -104,7 +104,7 @@ KS_FN int ks_block_bytes(int type) {
         case KT_Q2_K: return 84;
         case KT_Q3_K: return 110;
         case KT_Q4_K: case KT_Q4_K_RS: return 144;
-        case KT_Q5_K: return 176;
+        case KT_Q5_K: case KT_Q5_K_RS: return 176;
         case KT_Q6_K: case KT_Q6_K_RS: return 210;
         case KT_Q8_K: return 292;
         case KT_IQ2_XXS: return 66;      /* block_iq2_xxs .. block_iq1_m, ggml-common.h:340-405 */

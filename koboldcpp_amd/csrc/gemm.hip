@@ -581,7 +581,7 @@ template <> struct KqRaw<KT_Q5_K> { uint4 h, q0, q1, qh0, qh1; };
 template <> struct KqRaw<KT_Q6_K> { uint4 ql[4], qh[2]; uint32_t sc; uint32_t d; };
 
 // raw bytes of unit (row n, chunk c) of super-block sb; LAY 0: the kcpp layout, 1: the row-major decode
-// layouts KT_Q4_K_RS / KT_Q6_K_RS (kcpp_common.h; same raw unit, gathered from the row's planes)
+// layouts KT_Q4_K_RS / KT_Q5_K_RS / KT_Q6_K_RS (kcpp_common.h; same raw unit, gathered from the row's planes)
 template <int TYPE, int LAY>
 __device__ __forceinline__ void kq_load(KqRaw<TYPE> &r, const uint8_t *__restrict__ W, int64_t bpr, int64_t nbt,
                                         int64_t n, int c, int64_t sb) {
@@ -589,6 +589,13 @@ __device__ __forceinline__ void kq_load(KqRaw<TYPE> &r, const uint8_t *__restric
     if constexpr (LAY == 1 && TYPE == KT_Q4_K) {
         const uint8_t *row = W + n * 144 * bpr;
         r.h = ldg16(row + 16 * sb);
+        r.q0 = ldg16(row + 16 * bpr + 128 * sb + 32 * c);
+        r.q1 = ldg16(row + 16 * bpr + 128 * sb + 32 * c + 16);
+    } else if constexpr (LAY == 1 && TYPE == KT_Q5_K) {
+        const uint8_t *row = W + n * 176 * bpr;
+        r.h = ldg16(row + 16 * sb);
+        r.qh0 = ldg16(row + 144 * bpr + 32 * sb);
+        r.qh1 = ldg16(row + 144 * bpr + 32 * sb + 16);
         r.q0 = ldg16(row + 16 * bpr + 128 * sb + 32 * c);
         r.q1 = ldg16(row + 16 * bpr + 128 * sb + 32 * c + 16);
     } else if constexpr (LAY == 1 && TYPE == KT_Q6_K) {
@@ -2027,7 +2034,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         KCPP_CHECK(hipGetLastError());
         return 0;
     }
-    const bool rs = type == KT_Q4_K_RS || type == KT_Q6_K_RS;       // decode layouts: v2 only
+    const bool rs = type == KT_Q4_K_RS || type == KT_Q5_K_RS || type == KT_Q6_K_RS;       // decode layouts: v2 only
     if (rs || type == KT_Q4_K || type == KT_Q5_K || type == KT_Q6_K) {
         const int64_t nth = Mp * K / 8 + (Mp / 32) * (K / 256) * 64 + Mp * (K / 256);
         hipLaunchKernelGGL(k_act_frag, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
@@ -2048,6 +2055,8 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
                 break;
             case KT_Q4_K_RS: if (TMv == 2) hipLaunchKernelGGL((k_gemm_kq<KT_Q4_K, 2, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
                 else hipLaunchKernelGGL((k_gemm_kq<KT_Q4_K, 1, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
+                break;
+            case KT_Q5_K_RS: hipLaunchKernelGGL((k_gemm_kq<KT_Q5_K, 1, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
                 break;
             default: hipLaunchKernelGGL((k_gemm_kq<KT_Q6_K, 1, 1>), dim3(nwg), dim3(256), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, (const h8v *)bs16, M, MT, y, ly, r, lr);
                 break;

@@ -128,7 +128,7 @@ int gemv_cols(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     hipStream_t s = (hipStream_t)stream;
     const GemvExpert ex{eid, ebytes, n_exp, escale};
     if (M < 1 || M > 8) return -1;
-    if (type == KT_Q4_K_RS || type == KT_Q6_K_RS) {   // decode layouts: one RS mat-vec launch per column
+    if (type == KT_Q4_K_RS || type == KT_Q5_K_RS || type == KT_Q6_K_RS) {   // decode layouts: one RS mat-vec launch per column
         if (eid) return -3;
         for (int64_t c = 0; c < M; ++c) {
             DecArgs a;

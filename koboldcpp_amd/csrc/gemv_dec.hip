@@ -10,7 +10,7 @@ extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int 
     const DecArgs &a = *(const DecArgs *)args;
     hipStream_t s = (hipStream_t)stream;
     // row-major decode layouts: only the RS kernels read them (gemv_rs.hip)
-    if (type == KT_Q4_K_RS || type == KT_Q6_K_RS) return kcpp_gemv_rs(type, args, mode, pro, stream);
+    if (type == KT_Q4_K_RS || type == KT_Q5_K_RS || type == KT_Q6_K_RS) return kcpp_gemv_rs(type, args, mode, pro, stream);
     // coalesced-streaming kernel where it covers the type/shape (gemv_stream.hip), else unit-per-lane
     if (type == KT_Q4_K) {
         const int rc = kcpp_gemv_q4k(args, mode, pro, stream);

@@ -76,6 +76,60 @@ template <> struct RS<KT_Q4_K_RS> {
     }
 };
 
+// ---------------------------------------------------------------- Q5_K_RS
+// Q4_K_RS's pieces plus the fifth bits: row = [nsb][16] headers ++ [nsb][128] nibbles ++ [nsb][32] qh (ggml's qh bytes
+// of each super-block, dequantize_row_q5_K ggml-quants.c:2640: element 64 j + l (l < 32) takes bit 2 j of qh[l],
+// element 64 j + 32 + l bit 2 j + 1).  Piece (sb, j, hh) reads qh[16 hh .. 16 hh + 15] (the four pieces of a half
+// share those 16 B: one cache line, one HBM read); its bits are rotated onto bit 4 of each byte and or-ed onto the
+// nibbles, so the sdot4 operands are the 5-bit values themselves.
+template <> struct RS<KT_Q5_K_RS> {
+    static constexpr int BYTES = 176;
+    static constexpr int PIECES_PER_SB = 8;
+    using Act = RS<KT_Q4_K_RS>::Act;
+    struct W { uint4 h, q, qh; };
+    struct Lane { Q4Sel s; int j, hh, rlo, rhi; };
+    static __device__ __forceinline__ Lane lane_consts(int lane) {
+        Lane c;
+        c.j = (lane >> 1) & 3; c.hh = lane & 1; c.s = q4_sel(c.j);
+        c.rlo = (2 * c.j - 4) & 31;          // rotate right: bit 2j of each byte -> bit 4
+        c.rhi = (2 * c.j - 3) & 31;          //               bit 2j+1         -> bit 4
+        return c;
+    }
+    static __device__ __forceinline__ int sb_of(int lane, int i) { return (lane >> 3) + 8 * i; }
+    static __device__ __forceinline__ void act(const uint8_t *lds, int K, int sb, const Lane &c, Act &x) {
+        const int e0 = 256 * sb + 64 * c.j + 16 * c.hh;
+        x.lo = *(const int4 *)(lds + e0);
+        x.hi = *(const int4 *)(lds + e0 + 32);
+        x.d = ((const float *)(lds + K))[sb];
+        const int16_t *bs = (const int16_t *)(lds + K + (K / 256) * 4);
+        x.bslo = bs[e0 >> 4];
+        x.bshi = bs[(e0 >> 4) + 2];
+    }
+    static __device__ __forceinline__ void load(const uint8_t *rp, int nsb, int p, W &w) {
+        w.h = ld_nt(rp + 16 * (p >> 3));
+        w.q = ld_nt(rp + 16 * nsb + 16 * p);
+        w.qh = ld_nt(rp + 144 * nsb + 32 * (p >> 3) + 16 * (p & 1));
+    }
+    static __device__ __forceinline__ float dot(const W &w, const Act &x, const Lane &c) {
+        int sc0, m0, sc1, m1;
+        q4_scales(w.h, c.s, sc0, m0, sc1, m1);
+        const uint32_t q[4] = {w.q.x, w.q.y, w.q.z, w.q.w}, h[4] = {w.qh.x, w.qh.y, w.qh.z, w.qh.w};
+        const int al[4] = {x.lo.x, x.lo.y, x.lo.z, x.lo.w}, ah[4] = {x.hi.x, x.hi.y, x.hi.z, x.hi.w};
+        int dlo = 0, dhi = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t lo = (q[k] & 0x0F0F0F0Fu) | (__builtin_amdgcn_alignbit(h[k], h[k], c.rlo) & 0x10101010u);
+            const uint32_t hi = ((q[k] >> 4) & 0x0F0F0F0Fu) | (__builtin_amdgcn_alignbit(h[k], h[k], c.rhi) & 0x10101010u);
+            dlo = sdot4((int)lo, al[k], dlo);
+            dhi = sdot4((int)hi, ah[k], dhi);
+        }
+        const int sumi = __mul24(sc0, dlo) + __mul24(sc1, dhi);
+        const int summ = __mul24(m0, x.bslo) + __mul24(m1, x.bshi);
+        const float dw = h2f((uint16_t)(w.h.x & 0xFFFF)), dmw = h2f((uint16_t)(w.h.x >> 16));
+        return x.d * fmaf(dw, (float)sumi, -dmw * (float)summ);
+    }
+};
+
 // ---------------------------------------------------------------- Q6_K_RS
 // unit U = l + 64 i = 4 sb + u, u = (half h = u >> 1, 16-lane half lh = u & 1); its 64 elements are
 // 256 sb + 128 h + 16 lh + 32 g + 0..15 for g = 0..3 (dequantize_row_q6_K, ggml-quants.c:2978):

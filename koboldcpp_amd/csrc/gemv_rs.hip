@@ -1,4 +1,4 @@
-// gemv_rs.hip -- single-token mat-vec (decode) over the row-major decode layouts KT_Q4_K_RS / KT_Q6_K_RS.
+// gemv_rs.hip -- single-token mat-vec (decode) over the row-major decode layouts KT_Q4_K_RS / KT_Q5_K_RS / KT_Q6_K_RS.
 //
 // Why a layout of its own: in the ggml block order (block_q4_K, ggml-common.h:286: 16-B header + 128 B
 // of nibbles, repeated) a lane that owns a 64-element unit reads three 16-B pieces at a 144-B stride,
@@ -7,6 +7,7 @@
 // (tools/stream_probe.py).  The RS layouts keep each row's bytes together but split them into planes
 // (kcpp_common.h):
 //   Q4_K_RS row: [nsb][16] headers ++ [nsb][128] nibbles
+//   Q5_K_RS row: [nsb][16] headers ++ [nsb][128] nibbles ++ [nsb][32] qh
 //   Q6_K_RS row: [4 nsb][16] ql-lo ++ [4 nsb][16] ql-hi ++ [4 nsb][16] qh ++ [4 nsb][4] scales ++ [nsb] f16 d
 // so lane l's data piece i is the 16 B at plane + 16 (l + 64 i): one wave load = 1 KiB contiguous.
 //
@@ -362,7 +363,7 @@ extern "C" int kcpp_gemv_rs_qkv_mixed(const void *args, void *stream) {
 extern "C" int kcpp_rs_supported(int type, int64_t K) {
     if (K % 256 || K < 256) return 0;
     const int64_t nsb = K / 256;
-    if (type == KT_Q4_K_RS || type == KT_Q4_K) return nsb <= 56;
+    if (type == KT_Q4_K_RS || type == KT_Q4_K || type == KT_Q5_K_RS || type == KT_Q5_K) return nsb <= 56;
     if (type == KT_Q6_K_RS || type == KT_Q6_K) return nsb % 8 == 0 && nsb <= 64;
     return 0;
 }
@@ -384,6 +385,18 @@ extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void 
         case 5: return pick_rs<KT_Q4_K_RS, 5, 3>(a, mode, pro, s);
         case 6: return pick_rs<KT_Q4_K_RS, 6, 3>(a, mode, pro, s);
         default: return mc <= 4 ? pick_rs<KT_Q4_K_RS, 7, 4>(a, mode, pro, s) : -3;
+        }
+    }
+    if (type == KT_Q5_K_RS) {
+        const int ni = (nsb * 8 + 63) / 64, mc = (int)((a.K + 4095) / 4096);
+        switch (ni) {
+        case 1: return pick_rs<KT_Q5_K_RS, 1, 1>(a, mode, pro, s);
+        case 2: return pick_rs<KT_Q5_K_RS, 2, 1>(a, mode, pro, s);
+        case 3: return pick_rs<KT_Q5_K_RS, 3, 2>(a, mode, pro, s);
+        case 4: return pick_rs<KT_Q5_K_RS, 4, 2>(a, mode, pro, s);
+        case 5: return pick_rs<KT_Q5_K_RS, 5, 3>(a, mode, pro, s);
+        case 6: return pick_rs<KT_Q5_K_RS, 6, 3>(a, mode, pro, s);
+        default: return mc <= 4 ? pick_rs<KT_Q5_K_RS, 7, 4>(a, mode, pro, s) : -3;
         }
     }
     if (type == KT_Q6_K_RS) {

@@ -74,6 +74,13 @@ __device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uin
         for (int i = 0; i < 16; ++i) row[16 * sb + i] = src[i];
         for (int i = 0; i < 128; ++i) row[16 * bpr + 128 * sb + i] = src[16 + i];
     } break;
+    case KT_Q5_K_RS: {   // row: [nsb][16] headers (d, dmin, scales) ++ [nsb][128] nibbles ++ [nsb][32] qh
+        const int64_t n = b / bpr, sb = b % bpr;
+        uint8_t *row = dst + n * 176 * bpr;
+        for (int i = 0; i < 16; ++i) row[16 * sb + i] = src[i];
+        for (int i = 0; i < 128; ++i) row[16 * bpr + 128 * sb + i] = src[48 + i];
+        for (int i = 0; i < 32; ++i) row[144 * bpr + 32 * sb + i] = src[16 + i];
+    } break;
     case KT_Q6_K_RS: {
         const int64_t n = b / bpr, sb = b % bpr;
         uint8_t *row = dst + n * 210 * bpr;
@@ -158,6 +165,13 @@ __device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint
         const uint8_t *row = src + n * 144 * bpr;
         for (int i = 0; i < 16; ++i) blk[i] = row[16 * sb + i];
         for (int i = 0; i < 128; ++i) blk[16 + i] = row[16 * bpr + 128 * sb + i];
+    } break;
+    case KT_Q5_K_RS: {
+        const int64_t n = b / bpr, sb = b % bpr;
+        const uint8_t *row = src + n * 176 * bpr;
+        for (int i = 0; i < 16; ++i) blk[i] = row[16 * sb + i];
+        for (int i = 0; i < 128; ++i) blk[48 + i] = row[16 * bpr + 128 * sb + i];
+        for (int i = 0; i < 32; ++i) blk[16 + i] = row[144 * bpr + 32 * sb + i];
     } break;
     case KT_Q6_K_RS: {
         const int64_t n = b / bpr, sb = b % bpr;
@@ -285,7 +299,7 @@ __device__ void deq_block(int type, const uint8_t *src, int64_t nb, int64_t bpr,
         }
     } break;
     case KT_Q4_K: case KT_Q5_K: {
-        const bool five = type == KT_Q5_K;
+        const bool five = ks_base_type(type) == KT_Q5_K;
         const float d = h2f(blk[0] | (blk[1] << 8)), mn = h2f(blk[2] | (blk[3] << 8));
         const uint8_t *sc = blk + 4, *qh = blk + 16, *q = blk + (five ? 48 : 16);
         for (int c = 0; c < 4; ++c) {
@@ -416,7 +430,7 @@ __device__ __forceinline__ float deq_elem(int type, const uint8_t *src, int64_t 
         if (five) q += ((blk[16 + l] >> (2 * c + hi)) & 1) << 4;
         return __fsub_rn(__fmul_rn(d * sc, (float)q), mn * m);
     }
-    case KT_Q4_K_RS: case KT_Q6_K_RS: return 0.0f;      // row gathers of decode layouts are not used
+    case KT_Q4_K_RS: case KT_Q5_K_RS: case KT_Q6_K_RS: return 0.0f;      // row gathers of decode layouts are not used
     case KT_Q2_K: {
         const float d = h2f(*(const uint16_t *)(src + nb * 80 + b * 4)), mn = h2f(*(const uint16_t *)(src + nb * 80 + b * 4 + 2));
         const int n = e >> 7, j = (e >> 5) & 3, l = e & 31;
@@ -615,7 +629,7 @@ int kcpp_quantize_act_glu(const float *x, int64_t ldx, int64_t uoff, void *out, 
 
 int kcpp_get_rows(int type, const void *w, int64_t K, int64_t N, const int32_t *ids, int64_t T, float *y, int64_t ldy,
                   void *stream) {
-    if (type == KT_Q4_K_RS || type == KT_Q6_K_RS) return -2;
+    if (type == KT_Q4_K_RS || type == KT_Q5_K_RS || type == KT_Q6_K_RS) return -2;
     switch (type) {
 #define KCPP_IQ_ROWS(TT)                                                                                            \
     case TT:                                                                                                        \

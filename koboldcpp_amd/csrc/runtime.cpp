@@ -119,6 +119,7 @@ struct kcpp_model {
     int32_t *moe_rows = nullptr;     // prefill, grouped by expert: [ubatch*k] token rows ++ [ubatch*k] slot rows
     float *moe_rw = nullptr;         // [ubatch*k] routing weight of each grouped entry
     float *moe_slots = nullptr;      // [k][ubatch][n_embd] weighted expert outputs, summed in top-k order
+    int32_t *moe_trace = nullptr;    // [n_layer of the stage][n_expert_used] single-token routing (diagnostics)
     int32_t *moe_ids_h = nullptr;    // pinned host copies (prefill routing)
     float *moe_w_h = nullptr;
     int32_t *moe_rows_h = nullptr;
@@ -289,17 +290,18 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     if (hp->n_ctx < 1 || hp->n_ctx > 131072) { g_err = "n_ctx must be in [1, 131072]"; return nullptr; }
     kcpp_model *m = new kcpp_model();
     m->hp = *hp;
-    // on-device layout per tensor: dense Q4_K / Q6_K mat-mul weights whose K the RS kernels cover are held in
-    // the row-major decode layouts (KT_Q4_K_RS / KT_Q6_K_RS, gemv_rs.hip); the token embedding (row
-    // gathers), expert slices and everything else keep the kcpp layout.
+    // on-device layout per tensor: dense Q4_K / Q5_K / Q6_K mat-mul weights whose K the RS kernels cover are held in
+    // the row-major decode layouts (KT_Q4_K_RS / KT_Q5_K_RS / KT_Q6_K_RS, gemv_rs.hip), expert slices too (each slice
+    // its own RS tensor: the RS kernels take the device-resident expert index, the GEMMs read RS planes); the token
+    // embedding (row gathers), the router and everything else keep the kcpp layout.
     m->types.resize(n_tensors(*hp));
     for (int idx = 0; idx < n_tensors(*hp); ++idx) {
         int t = types[idx];
         int64_t K, N;
         shape_of(*hp, idx, K, N);
-        const bool dense = idx >= 2 && n_slices(*hp, idx) == 1 && N > 1 && (idx == 2 || (idx - 3) % per_layer(*hp) <= 8);
-        if (dense && (t == KT_Q4_K || t == KT_Q6_K) && kcpp_rs_supported(t, K))
-            t = t == KT_Q4_K ? KT_Q4_K_RS : KT_Q6_K_RS;
+        const bool dense = idx >= 2 && N > 1 && (idx == 2 || (idx - 3) % per_layer(*hp) <= 8);
+        if (dense && (t == KT_Q4_K || t == KT_Q5_K || t == KT_Q6_K) && kcpp_rs_supported(t, K))
+            t = t == KT_Q4_K ? KT_Q4_K_RS : (t == KT_Q5_K ? KT_Q5_K_RS : KT_Q6_K_RS);
         m->types[idx] = t;
     }
     types = m->types.data();
@@ -319,7 +321,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     const int64_t E = hp->n_embd, F = hp->n_ff, H = hp->n_head, HKV = hp->n_head_kv, D = E / H, EKV = HKV * D;
     const int64_t UB = m->ub;
     m->layers.resize(il1 - il0);
-    auto rowmajor = [](int t) { return t == KT_Q4_K || t == KT_Q5_K || t == KT_Q4_K_RS || t == KT_Q6_K_RS; };
+    auto rowmajor = [](int t) { return t == KT_Q4_K || t == KT_Q5_K || t == KT_Q4_K_RS || t == KT_Q5_K_RS || t == KT_Q6_K_RS; };
     auto alloc_group = [&](void *&base, int idx0, int n) -> int {
         size_t tot = 0;
         for (int j = 0; j < n; ++j) { int64_t K, N; shape_of(*hp, idx0 + j, K, N); tot += (size_t)tensor_bytes(types[idx0 + j], K, N); }
@@ -419,6 +421,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     hipSetDevice(m->device);
     if (m->g_exec) hipGraphExecDestroy(m->g_exec);
     auto F = [](void *p) { if (p) hipFree(p); };
+    F(m->moe_trace);
     auto FS = [&](KTensor &t) {
         for (auto &r : t.rs) { hipSetDevice(m->lanes[r.lane].dev); F(r.d); }
         hipSetDevice(m->device);
@@ -487,7 +490,7 @@ static int upload(int dev, hipStream_t s, int type, int64_t K, int64_t N, int sl
     RT_CHECK(hipSetDevice(dev));
     if (type == KT_Q6_K || type == KT_Q3_K || type == KT_Q2_K || type == KT_Q4_0 || type == KT_Q4_1 || type == KT_Q5_0 || type == KT_Q5_1 || type == KT_Q8_0 ||
         type == KT_IQ4_NL || type == KT_IQ4_XS ||
-        type == KT_Q4_K_RS ||
+        type == KT_Q4_K_RS || type == KT_Q5_K_RS ||
         type == KT_Q6_K_RS) {
         void *stage = nullptr;
         RT_CHECK(hipMalloc(&stage, bytes));
@@ -666,6 +669,28 @@ extern "C" int kcpp_model_moe_ids(kcpp_model *m, int32_t *out, int n) {
     memcpy(out, m->moe_ids_h, (size_t)n * 4);
     return 0;
 }
+// single-token routing trace (diagnostics): while enabled, every single-token MoE layer copies its top-k ids into
+// [layer][n_expert_used]; kcpp_model_moe_trace_read returns the last step's.  Toggling drops the captured graph.
+extern "C" int kcpp_model_moe_trace(kcpp_model *m, int enable) {
+    RT_CHECK(hipSetDevice(m->device));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    if (enable && !m->moe_trace && m->hp.n_expert > 0) {
+        const size_t n = m->layers.size() * (size_t)std::max(1, m->hp.n_expert_used);
+        RT_CHECK(hipMalloc(&m->moe_trace, n * 4));
+        RT_CHECK(hipMemset(m->moe_trace, 0xFF, n * 4));
+    } else if (!enable && m->moe_trace) {
+        RT_CHECK(hipFree(m->moe_trace));
+        m->moe_trace = nullptr;
+    }
+    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    return 0;
+}
+extern "C" int kcpp_model_moe_trace_read(kcpp_model *m, int32_t *out, int n) {
+    if (!m->moe_trace || n < 0 || n > (int)m->layers.size() * std::max(1, m->hp.n_expert_used)) { g_err = "moe trace"; return -1; }
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    RT_CHECK(hipMemcpy(out, m->moe_trace, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
 extern "C" int kcpp_model_set_engine(kcpp_model *m, int enable) {
     m->eng_mode = enable != 0;
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
@@ -785,6 +810,9 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
         RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, 1, hp.eps, s));
         RC(kcpp_moe_route(m->attn, E, t[9].d, t[9].type, E, hp.n_expert, NU, m->moe_ids, m->moe_w, 1, s));
     }
+    if (m->moe_trace)
+        RT_CHECK(hipMemcpyAsync(m->moe_trace + (&L - m->layers.data()) * NU, m->moe_ids, (size_t)NU * 4,
+                                hipMemcpyDeviceToDevice, s));
     if (m->q81) {
         // types without a fused decode mat-vec (Q4_1 / Q5_1 / IQ*): ffn_norm + activation quantization once, then per
         // slot the generic mat-vec on the expert slice its device-resident id selects (kcpp_gemv_expert)

@@ -13,9 +13,9 @@ from . import LIB_PATH
 F32, F16, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q3_K, Q4_K, Q5_K, Q6_K, Q8_K = 0, 1, 2, 3, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15
 IQ4_NL, IQ4_XS = 20, 23
 # device-internal row-major decode layouts of Q4_K / Q6_K (include/kcpp_synth.h; never ggml ids)
-Q4_K_RS, Q6_K_RS = 112, 114
+Q4_K_RS, Q5_K_RS, Q6_K_RS = 112, 113, 114
 BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q4_1: (32, 20), Q5_0: (32, 22), Q5_1: (32, 24), Q8_0: (32, 34), Q8_1: (32, 36), Q2_K: (256, 84), Q3_K: (256, 110), Q4_K: (256, 144),
-         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292), Q4_K_RS: (256, 144), Q6_K_RS: (256, 210),
+         Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292), Q4_K_RS: (256, 144), Q5_K_RS: (256, 176), Q6_K_RS: (256, 210),
          IQ4_NL: (32, 18), IQ4_XS: (256, 136)}
 # the lattice-grid types (ggml-common.h:340-405), kept in the ggml layout on the device (csrc/iq_grid.h)
 IQ2_XXS, IQ2_XS, IQ3_XXS, IQ1_S, IQ3_S, IQ2_S, IQ1_M = 16, 17, 18, 19, 21, 22, 29
@@ -114,6 +114,8 @@ _SIGS = {
     "kcpp_gradient_ai_rope_base": [Fl, I, I, I],
     "kcpp_model_engine_active": [P],
     "kcpp_model_moe_ids": [P, P, I],
+    "kcpp_model_moe_trace": [P, I],
+    "kcpp_model_moe_trace_read": [P, P, I],
     "kcpp_flash_attn_exact": [P, P, P, P, I, I, I, I, I, P, Fl, P],
     "kcpp_model_weight_bytes": [P],
     "kcpp_model_set_kv_types": [P, I, I],
@@ -353,6 +355,15 @@ class Model:
         import numpy as np
         out = np.zeros((T, k), np.int32)
         _chk(_L.kcpp_model_moe_ids(self.m, out.ctypes.data, T * k), "moe_ids")
+        return out
+
+    def moe_trace(self, on):
+        _chk(_L.kcpp_model_moe_trace(self.m, int(on)), "moe_trace")
+
+    def moe_trace_read(self, n_layer, k):
+        import numpy as np
+        out = np.zeros((n_layer, k), np.int32)
+        _chk(_L.kcpp_model_moe_trace_read(self.m, out.ctypes.data, n_layer * k), "moe_trace_read")
         return out
 
     def set_graphs(self, on):

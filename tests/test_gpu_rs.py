@@ -1,4 +1,4 @@
-"""Row-major decode layouts KT_Q4_K_RS / KT_Q6_K_RS (include/kcpp_synth.h, csrc/gemv_rs.hip).
+"""Row-major decode layouts KT_Q4_K_RS / KT_Q5_K_RS / KT_Q6_K_RS (include/kcpp_synth.h, csrc/gemv_rs.hip).
 
 * layout: ggml bytes -> RS -> ggml is the identity; the device synth and dequant of an RS tensor equal
   those of the base type (bit-exact);
@@ -16,7 +16,7 @@ import refharness as R
 
 pytestmark = pytest.mark.gpu
 
-RS = {R.Q4_K: 112, R.Q6_K: 114}
+RS = {R.Q4_K: 112, R.Q5_K: 113, R.Q6_K: 114}
 
 
 @pytest.fixture(scope="module")
@@ -44,7 +44,7 @@ def _close(a, b, rtol=1e-4):
     assert err < rtol, "max rel err %.3g" % err
 
 
-@pytest.mark.parametrize("base", [R.Q4_K, R.Q6_K])
+@pytest.mark.parametrize("base", [R.Q4_K, R.Q5_K, R.Q6_K])
 @pytest.mark.parametrize("Kd", [2048, 5632, 14336])
 def test_rs_layout_roundtrip_synth_dequant(env, base, Kd):
     torch, K = env
@@ -92,6 +92,12 @@ CASES = [  # name, base, K, N, mode, pro
     ("glu_q6k", R.Q6_K, 4096, 2048, 1, 1),
     ("head_q6k_big", R.Q6_K, 4096, 128256, 0, 1),
     ("k2048_q6k", R.Q6_K, 2048, 256, 0, 0),
+    ("wo_q5k", R.Q5_K, 4096, 4096, 0, 0),
+    ("glu_q5k", R.Q5_K, 4096, 14336, 1, 1),
+    ("down_q5k", R.Q5_K, 14336, 4096, 0, 2),
+    ("qkv_q5k", R.Q5_K, 4096, 6144, 0, 1),
+    ("k5632_q5k_masked", R.Q5_K, 5632, 2048, 0, 2),
+    ("head_q5k", R.Q5_K, 4096, 32768, 0, 1),
 ]
 
 
@@ -166,7 +172,7 @@ def test_gemv_rs_qkv_rope_kv(env, pos):
         _close(a_, b_, rtol=2e-3)
 
 
-@pytest.mark.parametrize("base", [R.Q4_K, R.Q6_K])
+@pytest.mark.parametrize("base", [R.Q4_K, R.Q5_K, R.Q6_K])
 @pytest.mark.parametrize("M", [3, 37])
 def test_rs_columns_and_gemm(env, base, M):
     """kcpp_gemv (M <= 8, one RS launch per column) and kcpp_gemm (MFMA, RS planes) vs the base layout"""
