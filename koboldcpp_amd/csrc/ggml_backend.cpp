@@ -10,7 +10,7 @@
 // graph_compute walks the nodes in order (ggml_backend_cuda_graph_compute, ggml-cuda.cu:2508-2778 with CUDA
 // graphs off) and dispatches each to a kernel of this library:
 //   MUL_MAT      quantized weight: activation -> Q8_K/Q8_0 (kcpp_quantize_act), then the mat-vec (M <= 8) or the
-//                MFMA GEMM on a device-native image of the weight (row-major Q4_K_RS / Q6_K_RS planes, the
+//                MFMA GEMM on a device-native image of the weight (row-major Q4_K_RS / Q5_K_RS / Q6_K_RS planes, the
 //                structure-of-arrays Q4_0 / Q8_0 / Q2_K / Q3_K / Q6_K layouts), built once per weight on first use and kept until
 //                the weight's buffer is written again; F16 / F32 weight: kcpp_ggml_mul_mat_f
 //   GET_ROWS     quantized: kcpp_get_rows on the native image; F16 / F32: kcpp_ggml_get_rows
@@ -394,6 +394,7 @@ const void *native_image(BackendCtx *bc, const kggml_tensor *w, int tt) {
 // decode-layout choice for mat-mul weights (as kcpp_model_create picks it)
 int matmul_layout(int t, int64_t K) {
     if (t == KT_Q4_K && kcpp_rs_supported(KT_Q4_K_RS, K)) return KT_Q4_K_RS;
+    if (t == KT_Q5_K && kcpp_rs_supported(KT_Q5_K_RS, K)) return KT_Q5_K_RS;
     if (t == KT_Q6_K && kcpp_rs_supported(KT_Q6_K_RS, K)) return KT_Q6_K_RS;
     return t;
 }
