@@ -156,7 +156,8 @@ __device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0,
         float *Y = seg == 0 ? a.Y[0] : (seg == 1 ? a.Y[1] : a.Y[2]);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const float v = (MODE == 0 && a.escale) ? __fmul_rn(slot[r], a.escale[0]) : slot[r];
+            float v = (MODE == 0 && a.escale) ? __fmul_rn(slot[r], a.escale[0]) : slot[r];
+            if (MODE == 0 && a.pre) v = __fadd_rn(a.pre[row0 + r], v);
             Y[row0 + r] = (MODE == 0 && a.res) ? __fadd_rn(v, a.res[row0 + r]) : v;
         }
     } else {

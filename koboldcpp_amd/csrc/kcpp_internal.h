@@ -54,6 +54,9 @@ struct DecArgs {
     // MoE: the number of expert slices; an expert id read on the device is clamped to [0, n_exp) so that a bad
     // router id cannot address past the tensor (the reference asserts, ggml-cuda.cu mul_mat_id); 0 = unchecked
     int64_t n_exp;
+    // MODE 0 in the RS kernels: added to the (scaled) product before the residual -- the MoE slot chain
+    // ((w0 o0 + w1 o1) + ...) + x of k_moe_combine, carried through the expert down projections
+    const float *pre;
 };
 // the expert slice offset of a DecArgs (0 without an expert id)
 __device__ __forceinline__ int64_t dec_expert_offset(const DecArgs &a) {

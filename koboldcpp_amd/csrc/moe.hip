@@ -34,6 +34,29 @@ __global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, 
         // all NE router rows in flight together (one memory round trip per chunk)
         float acc[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         float nscale = 1.0f;
+        // NORM (K <= 4096, one chunk): the router rows' loads go out first -- they do not wait for the norm -- so
+        // the weight and residual round trips overlap
+        float4 wpre[NORM ? 8 : 1][4], gpre[4];
+        if constexpr (NORM) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                gpre[u] = 16 * tid + 4 * u < K ? *(const float4 *)(nw + 16 * tid + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = 16 * tid + 4 * u;
+                    wpre[e][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (e < NE && i < K) {
+                        if constexpr (WT == KT_F16) {
+                            const uint2 h = *(const uint2 *)((const uint16_t *)w + (int64_t)e * K + i);
+                            wpre[e][u] = make_float4(h2f(h.x & 0xFFFF), h2f(h.x >> 16), h2f(h.y & 0xFFFF), h2f(h.y >> 16));
+                        } else {
+                            wpre[e][u] = *(const float4 *)((const float *)w + (int64_t)e * K + i);
+                        }
+                    }
+                }
+        }
         if constexpr (NORM) {                            // K <= 4096: one chunk, elements 16 tid .. +15
             double ss = 0.0;
             if (16 * tid < K) {
@@ -60,7 +83,7 @@ __global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, 
                 xv[u] = i0 + 4 * u < K ? *(const float4 *)(xr + i0 + 4 * u) : make_float4(0.f, 0.f, 0.f, 0.f);
                 if constexpr (NORM) {
                     if (i0 + 4 * u < K) {
-                        const float4 g = *(const float4 *)(nw + i0 + 4 * u);
+                        const float4 g = gpre[u];
                         xv[u] = make_float4(__fmul_rn(__fmul_rn(xv[u].x, nscale), g.x), __fmul_rn(__fmul_rn(xv[u].y, nscale), g.y),
                                             __fmul_rn(__fmul_rn(xv[u].z, nscale), g.z), __fmul_rn(__fmul_rn(xv[u].w, nscale), g.w));
                     }
@@ -76,7 +99,9 @@ __global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, 
                     const int i = i0 + 4 * u;
                     if (i >= K) break;
                     float4 wv;
-                    if constexpr (WT == KT_F16) {
+                    if constexpr (NORM) {
+                        wv = wpre[e][u];
+                    } else if constexpr (WT == KT_F16) {
                         const uint2 h = *(const uint2 *)((const uint16_t *)w + (int64_t)e * K + i);
                         wv = make_float4(h2f(h.x & 0xFFFF), h2f(h.x >> 16), h2f(h.y & 0xFFFF), h2f(h.y >> 16));
                     } else {

@@ -838,6 +838,9 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
         }
         return kcpp_moe_combine(m->x, m->moe_slots, E, NU, E, s);
     }
+    // RS down projections (MODE 0 store epilogue with DecArgs.pre): k_moe_combine's ((s0 + s1) + ...) + x in the
+    // same order, one launch per layer less
+    const bool chain = t[8].type == KT_Q4_K_RS || t[8].type == KT_Q5_K_RS || t[8].type == KT_Q6_K_RS;
     for (int j = 0; j < NU; ++j) {
         if (t[6].type == t[7].type) {
             DecArgs a;
@@ -862,11 +865,16 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
         a.K = F; a.x = m->h; a.nseg = 1;
         a.W[0] = (const uint8_t *)t[8].d; a.N[0] = E; a.Y[0] = m->moe_slots + j * E;
         a.eid = m->moe_ids + j; a.n_exp = hp.n_expert; a.ebytes = (int64_t)t[8].slice_bytes; a.escale = m->moe_w + j;
+        if (chain) {            // slot sum carried through the down projections, the last one adds the residual
+            a.Y[0] = j == NU - 1 ? m->x : m->moe_slots;
+            a.pre = j > 0 ? m->moe_slots : nullptr;
+            a.res = j == NU - 1 ? m->x : nullptr;
+        }
         const int rc = kcpp_gemv_dec(t[8].type, &a, 0, 2, rows_per_wave(E, 0), s);
         if (rc == -8) { g_err = "MoE down projection: n_ff beyond the fused mat-vec's K budget"; return rc; }
         RC(rc);
     }
-    return kcpp_moe_combine(m->x, m->moe_slots, E, NU, E, s);
+    return chain ? 0 : kcpp_moe_combine(m->x, m->moe_slots, E, NU, E, s);
 }
 
 // MoE FFN for a ubatch of T tokens: routing on the GPU, one host sync to group the tokens by expert
