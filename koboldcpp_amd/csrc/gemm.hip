@@ -1907,13 +1907,13 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     // (tools/gemm_ab.py) down 14336 x 4096 122.9 -> 112.3 us, attn_v 4096 x 1024 (Q6_K) 56.7 -> 33.9 us, wo 4096 x 4096
     // 43.3 -> 45.6 us (not split), gate|up (big grid) 236.8 -> 273.0 us (not split).
     // kcpp_gemm_set_variant: 2 forces v2, 3 v3 without the split, 4 v3 with the split wherever the mode allows
-    const bool v3 = gv == 0 || (gv >= 3 && gv <= 13);
+    const bool v3 = gv == 0 || (gv >= 3 && gv <= 13) || (gv >= 15 && gv <= 17);
     float *part = (float *)(w8 + o_up + ((M * N * 4 + 255) & ~255LL));
     // (the rule reads the weight shape only -- "< 128 tiles" as counted at the 512-token ubatch, 64 x 128 tiles --
     // so a prompt's bits do not depend on how it is cut into ubatches)
     auto splitk = [&](bool big, int64_t) {
         if (mode != 0 || (K / 256) % 2) return 1;
-        return (gv == 4 || (gv == 0 && !big && ((N + 127) / 128 < 16 || K / 256 >= 32))) ? 2 : 1;
+        return (gv == 4 || ((gv == 0 || (gv >= 15 && gv <= 17)) && !big && ((N + 127) / 128 < 16 || K / 256 >= 32))) ? 2 : 1;
     };
     const bool bs_aligned = ((uintptr_t)((const uint8_t *)act + M * K + M * (K / 256) * 4) & 15) == 0;
     // v4 for every Q4_K shape past the small-batch range (tools/gemm_ab.py, M = 512, v3 -> v4): gate|up 28672 rows
@@ -2007,8 +2007,13 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         KCPP_CHECK(hipGetLastError());
         const int64_t nt = (N + 127) / 128;
         const bool big = Mp / 128 * nt >= 384;
-        const int BMT = big ? 4 : 2;
-        const int NWv = big ? 8 : 4;
+        // long K (ffn_down, K/256 >= 32, split in two) also takes 128-token x 128-row tiles with 8 waves while that
+        // grid still has a workgroup per CU: tools/gemm_ab.py, M = 512, down 14336 x 4096 195.3 -> 171.5 us (v: 34.5
+        // stays on 64-token tiles, 49.8 / 53.9 on 128); the tile shape never changes a bit.  Variants 15 / 16 / 17
+        // force (BMT, NW) = (4, 4) / (4, 8) / (2, 8).
+        const bool longk = K / 256 >= 32 && mode == 0 && (K / 256) % 2 == 0 && Mp / 128 * nt * 2 >= 256;
+        const int BMT = gv == 15 || gv == 16 ? 4 : (gv == 17 ? 2 : (big || longk ? 4 : 2));
+        const int NWv = gv == 15 ? 4 : (gv == 16 || gv == 17 ? 8 : (big || longk ? 8 : 4));
         const int MT = (int)(Mp / (32 * BMT));
         const int KS = splitk(big, MT * nt);
         const unsigned nwg = (unsigned)(MT * nt * KS);

@@ -314,3 +314,35 @@ def test_gemm_v4_int8_matches_v2_bitwise(env, base, Kd, N, M):
         assert np.array_equal(outs[2, mode].view(np.uint32), outs[13, mode].view(np.uint32)), mode
         scale = max(1.0, float(np.abs(outs[2, mode]).max()))
         assert np.abs(outs[11, mode] - outs[2, mode]).max() <= 2e-6 * scale
+
+
+@pytest.mark.parametrize("Kd,N,M", [(4096, 28672, 512), (4096, 1000, 300), (2048, 512, 129), (14336, 4096, 256),
+                                    (4096, 14336, 64)])
+def test_gemm_v5_matches_v4_bitwise(env, Kd, N, M):
+    """Q4_K GEMM v5 (256-row tiles, every wave against all 128 tokens) against v4 (128-row tiles): the same
+    per-element integer MFMAs and f32 epilogue in the same order, and the same split-K rule, so the outputs must be
+    equal bit for bit -- RS layout, plain+residual and GLU modes, ragged M and N (a partial 256-row tile)"""
+    torch, K = env
+    t = RS[R.Q4_K]
+    s = sptr(torch)
+    X = torch.randn(M, Kd, generator=torch.Generator(device="cpu").manual_seed(M + N)).cuda()
+    act = torch.zeros(K.act_bytes(R.Q4_K, Kd, M), dtype=torch.uint8, device="cuda")
+    K.call("kcpp_quantize_act", K.vec_dot_type(R.Q4_K), X.data_ptr(), Kd, act.data_ptr(), Kd, M, s)
+    res = torch.randn(M, N).cuda()
+    W, W2 = _synth(torch, K, t, Kd, N, 13), _synth(torch, K, t, Kd, N, 14)
+    ws = torch.empty(K.raw().kcpp_gemm_workspace_bytes(t, Kd, N, M), dtype=torch.uint8, device="cuda")
+    outs = {}
+    try:
+        for v in (11, 14):
+            K.raw().kcpp_gemm_set_variant(v)
+            for mode in (0, 1):
+                Y = torch.full((M, N), float("nan"), device="cuda")
+                K.call("kcpp_gemm", t, W.data_ptr(), W2.data_ptr() if mode == 1 else None, Kd, N, act.data_ptr(), M,
+                       Y.data_ptr(), N, res.data_ptr() if mode == 0 else None, N, mode, ws.data_ptr(), s)
+                torch.cuda.synchronize()
+                outs[v, mode] = Y.cpu().numpy()
+    finally:
+        K.raw().kcpp_gemm_set_variant(0)
+    for mode in (0, 1):
+        assert np.isfinite(outs[14, mode]).all()
+        assert np.array_equal(outs[11, mode].view(np.uint32), outs[14, mode].view(np.uint32)), mode
