@@ -29,6 +29,15 @@ extern "C" int kcpp_gemv_dec(int type, const void *args, int mode, int pro, int 
     case KT_Q4_0: return dispatch_mode<KT_Q4_0>(a, mode, pro, rows_per_wave, s);
     case KT_Q5_0: return dispatch_mode<KT_Q5_0>(a, mode, pro, rows_per_wave, s);
     case KT_Q8_0: return dispatch_mode<KT_Q8_0>(a, mode, pro, rows_per_wave, s);
+    case KT_IQ4_NL: return dispatch_mode<KT_IQ4_NL>(a, mode, pro, rows_per_wave, s);
+    case KT_IQ4_XS: return dispatch_mode<KT_IQ4_XS>(a, mode, pro, rows_per_wave, s);
+    case KT_IQ2_XXS: return dispatch_mode<KT_IQ2_XXS>(a, mode, pro, rows_per_wave, s);
+    case KT_IQ2_XS: return dispatch_mode<KT_IQ2_XS>(a, mode, pro, rows_per_wave, s);
+    case KT_IQ2_S: return dispatch_mode<KT_IQ2_S>(a, mode, pro, rows_per_wave, s);
+    case KT_IQ3_XXS: return dispatch_mode<KT_IQ3_XXS>(a, mode, pro, rows_per_wave, s);
+    case KT_IQ3_S: return dispatch_mode<KT_IQ3_S>(a, mode, pro, rows_per_wave, s);
+    case KT_IQ1_S: return dispatch_mode<KT_IQ1_S>(a, mode, pro, rows_per_wave, s);
+    case KT_IQ1_M: return dispatch_mode<KT_IQ1_M>(a, mode, pro, rows_per_wave, s);
     default: return -3;
     }
 }

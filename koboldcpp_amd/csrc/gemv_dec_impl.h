@@ -143,7 +143,7 @@ template <int TYPE, int R, int MODE, int PRO, int MC, int IT>
 __global__ void __launch_bounds__(256) k_gemv_dec(const DecArgs a) {
     using A = typename ActOf<TYPE>::T;
     constexpr int E = Unit<TYPE>::ELEMS;
-    constexpr int VT = (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;
+    constexpr int VT = (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0 || TYPE == KT_IQ4_NL) ? KT_Q8_0 : KT_Q8_K;
     constexpr int RR = MODE == 1 ? 2 * R : R;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_act[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -269,7 +269,7 @@ static int launch_dec_it(const DecArgs &a, hipStream_t s) {
     const int max_blocks = a.K > 4096 ? 512 : 1024;
     const int64_t groups = ntot / R;
     const int64_t nblk = std::min<int64_t>((groups + 3) / 4, max_blocks);
-    const int vt = (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0) ? KT_Q8_0 : KT_Q8_K;
+    const int vt = (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0 || TYPE == KT_IQ4_NL) ? KT_Q8_0 : KT_Q8_K;
     const size_t lds = PRO ? (size_t)act_bytes(vt, a.K, 1) + 16 : 0;
     hipLaunchKernelGGL((k_gemv_dec<TYPE, R, MODE, PRO, MC, IT>), dim3((unsigned)nblk), dim3(256), lds, s, a);
     KCPP_CHECK(hipGetLastError());

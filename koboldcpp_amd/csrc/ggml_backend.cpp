@@ -678,7 +678,7 @@ bool mul_mat_id(BackendCtx *bc, kggml_tensor *n) {
                 if (rc != 0 && (t > 0 || j > 0)) return chk(rc, "expert mat-vec");
             }
         if (rc == 0) return true;
-        // rc on the first (j, t): this type / shape has no fused expert mat-vec (Q4_1 / Q5_1 / IQ*): per (j, t) the
+        // rc on the first (j, t): this type / shape has no fused expert mat-vec (Q4_1 / Q5_1): per (j, t) the
         // column quantized on its own, then the generic mat-vec on the expert slice its device-resident id selects
         void *act1 = bc->act.get((size_t)kcpp_act_bytes(as->type, K, 1) + 256);
         if (act1) {

@@ -133,7 +133,7 @@ struct kcpp_model {
     float *logits_pin = nullptr;
     bool use_graphs = true;
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
-    bool q81 = false;                // Q4_1 / Q5_1 (Q8_1 activations) or IQ4_NL / IQ4_XS weights: decode on the per-op path
+    bool q81 = false;                // Q4_1 / Q5_1 weights (Q8_1 activations): decode on the per-op path
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
     int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
     hipGraphExec_t g_exec = nullptr;
@@ -306,8 +306,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     }
     types = m->types.data();
     for (int idx = 0; idx < n_tensors(*hp); ++idx)
-        m->q81 |= types[idx] == KT_Q4_1 || types[idx] == KT_Q5_1 || types[idx] == KT_IQ4_NL || types[idx] == KT_IQ4_XS ||
-                  is_iq_grid_type(types[idx]);
+        m->q81 |= types[idx] == KT_Q4_1 || types[idx] == KT_Q5_1;
 
     m->device = device; m->il0 = il0; m->il1 = il1; m->has_embed = has_embed; m->has_output = has_output;
     m->ub = max_ubatch > 0 ? max_ubatch : 512;
@@ -814,7 +813,7 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
         RT_CHECK(hipMemcpyAsync(m->moe_trace + (&L - m->layers.data()) * NU, m->moe_ids, (size_t)NU * 4,
                                 hipMemcpyDeviceToDevice, s));
     if (m->q81) {
-        // types without a fused decode mat-vec (Q4_1 / Q5_1 / IQ*): ffn_norm + activation quantization once, then per
+        // types without a fused decode mat-vec (Q4_1 / Q5_1): ffn_norm + activation quantization once, then per
         // slot the generic mat-vec on the expert slice its device-resident id selects (kcpp_gemv_expert)
         const int vg = kcpp_vec_dot_type(t[6].type), vu = kcpp_vec_dot_type(t[7].type), vd = kcpp_vec_dot_type(t[8].type);
         RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, 1, hp.eps, s));
