@@ -80,6 +80,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     const int nw = (int)gridDim.x * NWV;
     const int wid = (int)blockIdx.x * NWV + wave;
     const int64_t eoff = dec_expert_offset(a);   // MoE slice
+    const int64_t eoff1 = a.eid1 ? dec_expert_offset(a, a.eid1) : eoff;   // segment 1's (two slots in one launch)
     const int abytes = K + K / 256 * 4 + K / 16 * 2;
     const typename T::Lane lc = T::lane_consts(lane);
 
@@ -92,10 +93,11 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     auto issue = [&](int g, Buf &b) {
         int seg, row0;
         group_rows(g, seg, row0);
-        const uint8_t *W = (seg == 0 ? a.W[0] : (seg == 1 ? a.W[1] : a.W[2])) + eoff;
+        const int64_t eo = seg == 1 ? eoff1 : eoff;
+        const uint8_t *W = (seg == 0 ? a.W[0] : (seg == 1 ? a.W[1] : a.W[2])) + eo;
 #pragma unroll
         for (int r = 0; r < RR; ++r) {
-            const uint8_t *rp = (MODE == 1 && r >= R ? a.W2 + eoff : W) + (int64_t)(row0 + (r % R)) * RB;
+            const uint8_t *rp = (MODE == 1 && r >= R ? a.W2 + eo : W) + (int64_t)(row0 + (r % R)) * RB;
 #pragma unroll
             for (int i = 0; i < NI; ++i) T::load(rp, nsb, min(lane + 64 * i, npieces - 1), b.w[i][r]);
         }
@@ -373,7 +375,7 @@ extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void 
     const DecArgs &a = *(const DecArgs *)args;
     hipStream_t s = (hipStream_t)stream;
     if (a.nseg < 1 || a.nseg > 3 || !kcpp_rs_supported(type, a.K)) return -3;
-    if (mode == 1 && a.nseg != 1) return -3;
+    if (mode == 1 && a.nseg != 1 && !(a.nseg == 2 && a.eid1)) return -3;   // GLU: one segment, or two MoE slots
     const int nsb = (int)(a.K / 256);
     if (type == KT_Q4_K_RS) {
         const int ni = (nsb * 8 + 63) / 64, mc = (int)((a.K + 4095) / 4096);

@@ -57,11 +57,15 @@ struct DecArgs {
     // MODE 0 in the RS kernels: added to the (scaled) product before the residual -- the MoE slot chain
     // ((w0 o0 + w1 o1) + ...) + x of k_moe_combine, carried through the expert down projections
     const float *pre;
+    // MoE, RS kernels: segment 1's expert index (two top-k slots' gate|up in one launch: segments 0 / 1 = slots 0 / 1
+    // over the same expert tensors, the same activation); null: every segment takes eid
+    const int32_t *eid1;
 };
-// the expert slice offset of a DecArgs (0 without an expert id)
-__device__ __forceinline__ int64_t dec_expert_offset(const DecArgs &a) {
-    if (!a.eid) return 0;
-    int e = __builtin_amdgcn_readfirstlane(a.eid[0]);
+// the expert slice offset of a DecArgs (0 without an expert id); `id` defaults to eid
+__device__ __forceinline__ int64_t dec_expert_offset(const DecArgs &a, const int32_t *id = nullptr) {
+    if (!id) id = a.eid;
+    if (!id) return 0;
+    int e = __builtin_amdgcn_readfirstlane(id[0]);
     if (a.n_exp > 0) e = e < 0 ? 0 : (e >= (int)a.n_exp ? (int)a.n_exp - 1 : e);
     return (int64_t)e * a.ebytes;
 }

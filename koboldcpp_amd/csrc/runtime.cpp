@@ -840,8 +840,23 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
     // RS down projections (MODE 0 store epilogue with DecArgs.pre): k_moe_combine's ((s0 + s1) + ...) + x in the
     // same order, one launch per layer less
     const bool chain = t[8].type == KT_Q4_K_RS || t[8].type == KT_Q5_K_RS || t[8].type == KT_Q6_K_RS;
+    // RS gate|up with two slots: both slots' GLU rows in one launch (segment j = slot j, its own expert index), one
+    // ramp instead of two; h of slot j at m->h + j F
+    const bool rs_gu = t[6].type == t[7].type &&
+                       (t[6].type == KT_Q4_K_RS || t[6].type == KT_Q5_K_RS || t[6].type == KT_Q6_K_RS);
+    const bool pair = rs_gu && NU == 2 && m->ub >= 2;
+    if (pair) {
+        DecArgs a;
+        memset(&a, 0, sizeof a);
+        a.K = E; a.x = m->x; a.nw = (const float *)t[5].d; a.eps = hp.eps; a.nseg = 2;
+        a.W[0] = a.W[1] = (const uint8_t *)t[6].d; a.W2 = (const uint8_t *)t[7].d; a.N[0] = a.N[1] = F;
+        a.Y[0] = m->h; a.Y[1] = m->h + F;
+        a.eid = m->moe_ids; a.eid1 = m->moe_ids + 1; a.n_exp = hp.n_expert; a.ebytes = (int64_t)t[6].slice_bytes;
+        RC(kcpp_gemv_dec(t[6].type, &a, 1, 1, rows_per_wave(F, 1), s));
+    }
     for (int j = 0; j < NU; ++j) {
-        if (t[6].type == t[7].type) {
+        if (pair) {
+        } else if (t[6].type == t[7].type) {
             DecArgs a;
             memset(&a, 0, sizeof a);
             a.K = E; a.x = m->x; a.nw = (const float *)t[5].d; a.eps = hp.eps; a.nseg = 1;
@@ -861,7 +876,7 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
         }
         DecArgs a;
         memset(&a, 0, sizeof a);
-        a.K = F; a.x = m->h; a.nseg = 1;
+        a.K = F; a.x = pair ? m->h + j * F : m->h; a.nseg = 1;
         a.W[0] = (const uint8_t *)t[8].d; a.N[0] = E; a.Y[0] = m->moe_slots + j * E;
         a.eid = m->moe_ids + j; a.n_exp = hp.n_expert; a.ebytes = (int64_t)t[8].slice_bytes; a.escale = m->moe_w + j;
         if (chain) {            // slot sum carried through the down projections, the last one adds the residual

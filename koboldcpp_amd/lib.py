@@ -208,7 +208,7 @@ class DecArgs(ctypes.Structure):
     _fields_ = [("W", P * 3), ("Y", P * 3), ("N", I64 * 3), ("role", I * 3), ("nseg", I), ("W2", P), ("K", I64),
                 ("act", P), ("x", P), ("nw", P), ("eps", Fl), ("res", P), ("q16", P), ("kc", P), ("vc", P),
                 ("ekv", I64), ("D", I), ("pos", P), ("rope_tab", P), ("eid", P), ("ebytes", I64), ("escale", P),
-                ("act_mtot", I64), ("act_col", I64), ("n_exp", I64), ("pre", P)]
+                ("act_mtot", I64), ("act_col", I64), ("n_exp", I64), ("pre", P), ("eid1", P)]
 
 
 if ctypes.sizeof(DecArgs) != _L.kcpp_gemv_dec_args_size():
