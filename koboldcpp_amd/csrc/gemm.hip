@@ -945,6 +945,22 @@ template <int BMT> struct Q4v3Smem {
 };
 
 // 16 B global -> LDS per lane (LDS address = wave-uniform base + 16 * lane)
+// LDS-DMA issued from inline asm: the compiler does not track these writes, so it inserts no vmcnt(0) in front of
+// the LDS reads that follow (it cannot tell the ring stage being filled from the one being read, and a compiler-
+// visible DMA would drain every prefetch at the first read); the kernel orders them itself (s_waitcnt + barrier).
+// lds_base: wave-uniform LDS byte address; lane l writes lds_base + size * l.
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+__device__ __forceinline__ void dma16(const void *g, const void *lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g),
+                 "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_base))) : "memory", "m0");
+}
+__device__ __forceinline__ void dma4(const void *g, const void *lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g),
+                 "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_base))) : "memory", "m0");
+}
+
 __device__ __forceinline__ void glds16(const void *g, void *lds_base) {
     __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(g),
                                      (__attribute__((address_space(3))) void *)(lds_base), 16, 0, 0);
@@ -1251,8 +1267,8 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6v3(const uint8_t *__restr
     const float *dsrc = dyT + m0 + 4 * lane;
     auto stage = [&](int buf, int64_t sb) {
 #pragma unroll
-        for (int st = 0; st < SPW; ++st) glds16(asrc + (16 * sb + st0 + st) * 64, &S.a[buf][stt][(st0 + st) * 64]);
-        if (wave == 0 && lane < 8 * BMT) glds16(dsrc + sb * Mp, &S.dy[buf][0]);
+        for (int st = 0; st < SPW; ++st) dma16(asrc + (16 * sb + st0 + st) * 64, &S.a[buf][stt][(st0 + st) * 64]);
+        if (wave == 0 && lane < 8 * BMT) dma16(dsrc + sb * Mp, &S.dy[buf][0]);
     };
     uint2 nlo[4], nhi[4], nqh[4];
     uint4 nsc;
@@ -1388,16 +1404,20 @@ struct Q80Segs {
 #ifndef Q80_CH
 #define Q80_CH 4
 #endif
+#ifndef Q80_ST
+#define Q80_ST 2
+#endif
 struct Q80s2Smem {
-    uint8_t w[2][128 * 32 * Q80_CH];  // weight chunk [buf][row][32 CH B] (swizzled 16-B pieces)
-    i32x4 a[2][Q80_CH][64];           // activation fragments [buf][block][lane]
+    uint8_t w[Q80_ST][128 * 32 * Q80_CH];  // weight chunk [stage][row][32 CH B] (swizzled 16-B pieces)
+    i32x4 a[Q80_ST][Q80_CH][64];           // activation fragments [stage][block][lane]
+    float dx[48 * 32];                     // token scales of the split's blocks [block][token] (q80s_splits: <= 48 blocks)
 };
 
 __global__ void __launch_bounds__(256) k_gemm_q80s2(const Q80Segs sg, int64_t K, int64_t N,
                                                    const uint8_t *__restrict__ act, int64_t M, float *__restrict__ part) {
     __shared__ Q80s2Smem S;
-    extern __shared__ __attribute__((aligned(16))) float q80_sdx2[];
-    float *sdx = q80_sdx2;                                       // [bps][32 tokens] (dynamic)
+    float *sdx = S.dx;        // static LDS: the compiler can tell it from the DMA targets (a dynamic array made it
+                              // wait for every outstanding LDS-DMA before each read of a token scale)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lr = lane & 31, kg = lane >> 5;
@@ -1422,9 +1442,9 @@ __global__ void __launch_bounds__(256) k_gemm_q80s2(const Q80Segs sg, int64_t K,
             const int64_t row = std::min<int64_t>(nt0 - soff + rl, Ns - 1);
             const int piece = wslot ^ (rl % PPR);                // the 16-B piece this LDS slot holds
             const int64_t blk = std::min<int64_t>(cb + (piece >> 1), b1 - 1);
-            glds16(W + (row * nb + blk) * 32 + 16 * (piece & 1), &S.w[buf][(IPW * wave + i) * 1024]);
+            dma16(W + (row * nb + blk) * 32 + 16 * (piece & 1), &S.w[buf][(IPW * wave + i) * 1024]);
         }
-        if (wave < Q80_CH) glds16(qx + std::min<int64_t>(cb + wave, b1 - 1) * 32, &S.a[buf][wave][0]);
+        if (wave < Q80_CH) dma16(qx + std::min<int64_t>(cb + wave, b1 - 1) * 32, &S.a[buf][wave][0]);
     };
     for (int64_t i = tid; i < (b1 - b0) * 32; i += 256) {
         const int64_t b = i >> 5, t = i & 31;
@@ -1435,15 +1455,25 @@ __global__ void __launch_bounds__(256) k_gemm_q80s2(const Q80Segs sg, int64_t K,
     for (int r = 0; r < 16; ++r) tot[r] = 0.0f;
     const int nl = 32 * wave + lr;                               // this lane's B row within the tile
     const int64_t nrow = std::min<int64_t>(nt0 - soff + nl, Ns - 1);
-    stage(0, b0);
+    // Q80_ST-stage ring: chunk i in stage i % Q80_ST, issued Q80_ST - 1 chunks ahead
+#pragma unroll
+    for (int q = 0; q < Q80_ST - 1; ++q)
+        if (b0 + q * Q80_CH < b1) stage(q, b0 + q * Q80_CH);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int64_t cb = b0; cb < b1; cb += Q80_CH) {
-        const int buf = (int)(((cb - b0) / Q80_CH) & 1);
-        if (cb + Q80_CH < b1) stage(buf ^ 1, cb + Q80_CH);
+        const int ci = (int)((cb - b0) / Q80_CH);
+        const int buf = ci % Q80_ST;
+        const bool ahead = cb + (Q80_ST - 1) * Q80_CH < b1;
+        // the weight block scales (plain global loads) are taken -- and waited for -- BEFORE the next chunk's LDS-DMA
+        // goes out: the compiler does not see the DMA, so the vmcnt it places in front of the first use of a scale
+        // would otherwise also wait for the whole prefetch and expose its latency every chunk
         float dwv[Q80_CH];
 #pragma unroll
         for (int u = 0; u < Q80_CH; ++u) dwv[u] = h2f(dwp[nrow * nb + std::min<int64_t>(cb + u, b1 - 1)]);
+#pragma unroll
+        for (int u = 0; u < Q80_CH; ++u) asm volatile("" ::"v"(dwv[u]));
+        if (ahead) stage((ci + Q80_ST - 1) % Q80_ST, cb + (Q80_ST - 1) * Q80_CH);
 #pragma unroll
         for (int u = 0; u < Q80_CH; ++u) {
             if (cb + u >= b1) break;
@@ -1463,7 +1493,13 @@ __global__ void __launch_bounds__(256) k_gemm_q80s2(const Q80Segs sg, int64_t K,
                     tot[4 * q + e] = __fadd_rn(tot[4 * q + e], __fmul_rn((float)acc[4 * q + e], __fmul_rn(dwv[u], dv[e])));
             }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // chunk ci + 1 must have landed; with three stages chunk ci + 2 (issued this iteration, last) may stay in flight
+        if (Q80_ST == 3 && ahead) {
+            static_assert(Q80_ST != 3 || (128 / (64 / (2 * Q80_CH)) / 4 == 4 && Q80_CH == 4), "vmcnt below: 4 + 1 per stage");
+            asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         __syncthreads();
     }
     const int64_t n = nt0 + nl;
@@ -1580,22 +1616,6 @@ template <int WR, int NST> struct Q4v4Smem {
     uint4 wh[NST][WR][32];   // [stage][row tile][row]: Q4_K header (d, dmin, 12 B scales / mins)
     i32x4 wq[NST][WR][280];  // [stage][row tile][swz(row, chunk)]: qs chunks 0..7 (pair p, half g: chunk 2p + g)
 };
-
-// LDS-DMA issued from inline asm: the compiler does not track these writes, so it inserts no vmcnt(0) in front of
-// the LDS reads that follow (it cannot tell the ring stage being filled from the one being read, and a compiler-
-// visible DMA would drain every prefetch at the first read); the kernel orders them itself (s_waitcnt + barrier).
-// lds_base: wave-uniform LDS byte address; lane l writes lds_base + size * l.
-__device__ __forceinline__ uint32_t lds_addr(const void *p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
-}
-__device__ __forceinline__ void dma16(const void *g, const void *lds_base) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g),
-                 "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_base))) : "memory", "m0");
-}
-__device__ __forceinline__ void dma4(const void *g, const void *lds_base) {
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(g),
-                 "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_base))) : "memory", "m0");
-}
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // bytes of x (each <= 15) times s (<= 7), per byte: two 16-bit lanes, no carry out of a byte (v_pk_mul_lo_u16;
@@ -1805,7 +1825,7 @@ static int gemm_q80_small(const void *W, const void *W2, int64_t K, int64_t N, c
     const dim3 grid((unsigned)((N + 127) / 128), (unsigned)S);
     Q80Segs sg = {{(const uint8_t *)W, nullptr, nullptr}, {N, 0, 0}, 1};
     auto q80 = [&](float *pt) {
-        hipLaunchKernelGGL(k_gemm_q80s2, grid, dim3(256), (size_t)bps * 128, s, sg, K, N, (const uint8_t *)act, M, pt);
+        hipLaunchKernelGGL(k_gemm_q80s2, grid, dim3(256), 0, s, sg, K, N, (const uint8_t *)act, M, pt);
     };
     q80(part);
     KCPP_CHECK(hipGetLastError());
@@ -1847,7 +1867,7 @@ int kcpp_gemm_q80_segs(const void *const *W, const int64_t *N, int nseg, int64_t
     const int S = q80s_splits(K, Ntot);
     const int64_t nb = K / 32, bps = (nb + S - 1) / S;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_gemm_q80s2, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), (size_t)bps * 128, s, sg,
+    hipLaunchKernelGGL(k_gemm_q80s2, dim3((unsigned)((Ntot + 127) / 128), (unsigned)S), dim3(256), 0, s, sg,
                        K, Ntot, (const uint8_t *)act, M, part);
     KCPP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * Ntot + 255) / 256)), dim3(256), 0, s, part, nullptr, S, M, Ntot, Y, ldy,
