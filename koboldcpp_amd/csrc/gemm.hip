@@ -961,10 +961,6 @@ __device__ __forceinline__ void dma4(const void *g, const void *lds_base) {
                  "s"(__builtin_amdgcn_readfirstlane(lds_addr(lds_base))) : "memory", "m0");
 }
 
-__device__ __forceinline__ void glds16(const void *g, void *lds_base) {
-    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void *)(g),
-                                     (__attribute__((address_space(3))) void *)(lds_base), 16, 0, 0);
-}
 
 // one qs dword (4 bytes of a sub-block pair) -> fragment: 4 low nibbles * s0, 4 high nibbles * s1 (exact)
 __device__ __forceinline__ h8v frag_q4v3(uint32_t w, float s0, float s1) {
@@ -1044,9 +1040,9 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) k_gemm_q4v3(const ui
     const float *dsrc = dyT + m0 + 4 * lane;
     auto stage = [&](int buf, int64_t sb) {
 #pragma unroll
-        for (int st = 0; st < SPW; ++st) glds16(asrc + (16 * sb + st0 + st) * 64, &S.a[buf][stt][(st0 + st) * 64]);
-        if (wave < BMT) glds16(bsrc + sb * 64, &S.bs[buf][stt][0]);
-        if (wave == 0 && lane < 8 * BMT) glds16(dsrc + sb * Mp, &S.dy[buf][0]);
+        for (int st = 0; st < SPW; ++st) dma16(asrc + (16 * sb + st0 + st) * 64, &S.a[buf][stt][(st0 + st) * 64]);
+        if (wave < BMT) dma16(bsrc + sb * 64, &S.bs[buf][stt][0]);
+        if (wave == 0 && lane < 8 * BMT) dma16(dsrc + sb * Mp, &S.dy[buf][0]);
     };
     // raw weight super-blocks are loaded PF ahead into register sets X / Y (PF = 2: ping-pong, the loop unrolled
     // by two so each set stays in fixed registers); sb's set is copied out before it is refilled with sb + PF
@@ -1405,7 +1401,7 @@ struct Q80Segs {
 #define Q80_CH 4
 #endif
 #ifndef Q80_ST
-#define Q80_ST 2
+#define Q80_ST 2        // ring depth; 3 measured slower on config 3 (6.51k vs 6.71k tok/s: 2 instead of 3 workgroups per CU)
 #endif
 struct Q80s2Smem {
     uint8_t w[Q80_ST][128 * 32 * Q80_CH];  // weight chunk [stage][row][32 CH B] (swizzled 16-B pieces)
