@@ -3,8 +3,10 @@
 Workload (BASELINE.json configs[1]): prompt of 3840 tokens prefilled in
 ubatches of 512, then greedy decode at positions 3840..4095.  A "step" is one decode token
 (one pass of the token-generation hot path); `value` = decode tokens/s.  Prefill tok/s is reported
-beside it.  Multi-GPU (N>1, torchrun): layer split across ranks (tensor_split 1,1,...), the hidden
-state handed off rank->rank with RCCL send/recv; value = tokens/s of the whole pipeline.
+beside it.  Multi-GPU (--gpus N > 1, with or without torchrun): rank 0 runs load_model's in-process
+engine over the N GPUs (layer split by tensor_split 1:...:1, stage streams handing the residual over
+by RCCL send/recv, the greedy token moved home to stage 0 by a device copy); the other ranks only
+bracket the run with barriers.  value = tokens/s of the whole pipeline.
 
 Adds:
   roofline     -- dominant decode kernel (Q4_K gate|up mat-vec, 4096 x 2*14336), HIP-event timed
@@ -240,12 +242,8 @@ def main():
                     choices=["llama3-8b-q4_k_m", "llama3-8b-q8_0-b32", "mixtral-8x7b-q5_k_m"],
                     help="BASELINE configs[1] (default: the driver's line), configs[2], configs[4]")
     ap.add_argument("--layers", type=int, default=None, help="override n_layer (debug only; invalidates metric)")
-    ap.add_argument("--engine", type=int, default=None,
-                    help="1: single-token decode through the persistent engine (dec_engine.hip), 0: the launch chain")
     args = ap.parse_args()
 
-    if args.engine is not None:
-        os.environ["KCPP_ENGINE"] = str(args.engine)
     import torch
     import koboldcpp_amd.lib as K
 
@@ -286,8 +284,9 @@ def run_bench(args, K, torch, n_dev):
         par = "single GPU"
     else:
         # the drop-in engine load_model ships (koboldcpp_amd/csrc/expose.cpp): n_dev layer-split stages in this one
-        # process, RCCL send/recv hand-off between the stage streams, pipelined prefill ubatches, generate()'s greedy
-        # loop (argmax on the last stage, token back to stage 0 through the host)
+        # process, RCCL send/recv hand-off between the stage streams, pipelined prefill ubatches, greedy steps with
+        # the argmax on the last stage and the token moved home to stage 0 by a 4-byte device copy (expose.cpp
+        # greedy_step / token_home: no host synchronisation inside a step)
         steps = min(args.steps, hp["n_ctx"] - args.prompt - args.warmup - 1)
         e = K.engine_bench(hp, types, n_dev, args.prompt, args.ubatch, args.warmup, steps)
         r = {"dec": steps / e["decode_s"], "pre": args.prompt / e["prefill_s"], "t_pp": e["prefill_s"],

@@ -89,26 +89,6 @@ int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
  * (v) in KT_Q6_K_RS -- the Q4_K_M "more bits" layers -- in one launch; -3 when the shape is not covered */
 int kcpp_gemv_rs_qkv_mixed(const void *args, void *stream);
 int kcpp_rs_supported(int type, int64_t K);
-/* Single-token decode of layers [0, nl) as ONE persistent launch (koboldcpp_amd/csrc/dec_engine.hip): one 512-thread
- * workgroup per CU, the q|k|v -> attention -> merge -> wo -> gate|up -> down edges handed over inside the launch by
- * write-through stores + device-scope counters, the next op's weights in flight while an edge resolves.  Replaces
- * the per-node launches of ggml_backend_cuda_graph_compute (ggml-cuda.cu:2654-2676) for a whole stage.
- * kcpp_engine_supported: 1 when the geometry is compiled (Llama-3-8B shapes, 256 CUs).  layers_dev: nl records of
- * kcpp_engine_layer_bytes() filled by kcpp_engine_layer (weights in KT_Q4_K_RS; attn_v / ffn_down KT_Q4_K_RS or
- * KT_Q6_K_RS).  sync: kcpp_engine_sync_bytes(nl) bytes; the nl * 48 counters (the first nl * 6144 bytes) must be zero
- * at every launch (a memset ahead of it), the error word after them is cleared by the caller.  -3: not covered. */
-int kcpp_engine_supported(int E, int F, int H, int HKV, int D, int ncu);
-int64_t kcpp_engine_sync_bytes(int nl);
-int kcpp_engine_layer_bytes(void);
-void kcpp_engine_layer(void *rec, const void *wq, const void *wk, const void *wv, const void *wo, const void *wg,
-                       const void *wu, const void *wd, const float *attn_norm, const float *ffn_norm, uint16_t *kc,
-                       uint16_t *vc, int v_q6, int down_q6);
-int kcpp_engine_decode(const void *layers_dev, int nl, float *x, uint16_t *q16, void *fa_ws, void *act, float *h,
-                       unsigned *sync, const int32_t *pos, const void *rope_tab, float eps, float kq_scale, int E,
-                       int F, int H, int HKV, void *stream);
-/* the engine's error word (0: every hand-off of every launch since it was cleared completed; else the code of the
- * first edge that timed out); synchronises the stream */
-int kcpp_engine_error(const unsigned *sync, int nl, void *stream);
 
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,
@@ -332,11 +312,6 @@ float kcpp_gradient_ai_rope_base(float original_rope_base, int n_ctx_train, int 
 int kcpp_model_set_graphs(kcpp_model *m, int enable);
 /* single-token decode through the fused mat-vec path (default on); off = one kernel per op */
 int kcpp_model_set_fused_decode(kcpp_model *m, int enable);
-/* single-token decode of the stage's layers as one persistent launch (kcpp_engine_decode) where the model is covered
- * (default on; KCPP_ENGINE=0 at creation turns it off); off = the fused launch chain (6 launches per layer) */
-int kcpp_model_set_engine(kcpp_model *m, int enable);
-/* 1 when the last single-token step ran the persistent engine, 0 when it ran the launch chain */
-int kcpp_model_engine_active(kcpp_model *m);
 /* 1: attention through kcpp_flash_attn_exact (reference order, f16 accumulation; strict-parity mode, slow);
  * 0 (default, or KCPP_FA_EXACT=1 at creation): the split-KV / MFMA kernels */
 int kcpp_model_set_fa_exact(kcpp_model *m, int enable);

@@ -1,5 +1,5 @@
-// attn_dec.h -- the single-token split-KV attention body (one workgroup = one split of one kv head, 4 waves), shared
-// by the stand-alone decode kernel k_fa_dec4 (attn.hip) and the persistent decode engine (dec_engine.hip).
+// attn_dec.h -- the single-token split-KV attention body (one workgroup = one split of one kv head, 4 waves), used
+// by the stand-alone decode kernel k_fa_dec4 (attn.hip).
 //
 // Split sp of NS owns keys [p0, p1) of [0, n_kv).  Wave w streams 16-key groups base = p0 + 16 w + 64 j: lane
 // (kq = lane >> 4, sub = lane & 15) holds 16 B (8 dims) of K and of V for keys base + 4 i + kq, i < 4 -- every load

@@ -605,8 +605,10 @@ bool load_model(const load_model_inputs inputs) {
     float ropescale = (float)f.get_f("llama.rope.scaling.factor", 0.0);
     if (ropescale == 0.0f) ropescale = (float)f.get_f("llama.rope.scale_linear", 0.0);
     const float scale_train = ropescale == 0.0f ? 1.0f : 1.0f / ropescale;
-    if (f.get_s("llama.rope.scaling.type", "") == "yarn") {
-        fprintf(stderr, "[kcpp] load_model: YaRN rope scaling is not supported\n");
+    // YaRN is refused only where the model's own RoPE values would be used: a user --ropeconfig replaces them and the
+    // reference then never reads the model's YaRN settings (gpttype_adapter.cpp:1681-1687, 1926-1930)
+    if (f.get_s("llama.rope.scaling.type", "") == "yarn" && !(inputs.rope_freq_scale > 0.0f)) {
+        fprintf(stderr, "[kcpp] load_model: YaRN rope scaling is not supported (pass --ropeconfig to override)\n");
         return false;
     }
     const int n_ctx_train = (int)f.get_i("llama.context_length", 2048);     // FileFormatExtraMeta default

@@ -1,6 +1,6 @@
 // gemv_rs.h -- the row-major decode layouts KT_Q4_K_RS / KT_Q6_K_RS as seen by one lane of a single-token mat-vec:
 // piece loads, the lane's Q8_K activation slices and the exact integer dot (gemv_rs.hip documents the layouts).
-// Shared by the stand-alone RS kernels (gemv_rs.hip) and the persistent decode engine (dec_engine.hip).
+// Used by the stand-alone RS kernels (gemv_rs.hip).
 #pragma once
 #include "gemv_lean.h"
 

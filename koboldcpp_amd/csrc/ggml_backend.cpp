@@ -350,11 +350,19 @@ const void *native_image(BackendCtx *bc, const kggml_tensor *w, int tt) {
     if (buffer_is_ours(buf) && buf->usage == KGGML_BACKEND_BUFFER_USAGE_WEIGHTS && w->view_src != nullptr) {
         // a view of a weight: its separate image is packed from ggml bytes, so a root already converted in place goes
         // back to the ggml layout and keeps separate images from now on (no in-place layout under a live view)
+        // (once the root is marked shared and nothing in place overlaps the view, there is nothing to restore: no host
+        // sync on every MUL_MAT against the view; restore_ggml synchronises the device itself when it converts)
         BufCtx *c = (BufCtx *)buf->context;
-        hipStreamSynchronize(bc->stream);
-        restore_ggml(c, w->data, nbytes(w));
-        std::lock_guard<std::mutex> lk(g_img_mu);
-        c->shared[w->view_src->data] = 1;
+        bool todo;
+        {
+            std::lock_guard<std::mutex> lk(g_img_mu);
+            todo = !c->shared.count(w->view_src->data) || inplace_at(c, w->data, nbytes(w)) != c->native.end();
+        }
+        if (todo) {
+            restore_ggml(c, w->data, nbytes(w));
+            std::lock_guard<std::mutex> lk(g_img_mu);
+            c->shared[w->view_src->data] = 1;
+        }
     }
     if (buffer_is_ours(buf) && buf->usage == KGGML_BACKEND_BUFFER_USAGE_WEIGHTS && w->view_src == nullptr) {
         BufCtx *c = (BufCtx *)buf->context;

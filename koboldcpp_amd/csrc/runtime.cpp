@@ -108,11 +108,6 @@ struct kcpp_model {
     void *gemm_ws2 = nullptr;               // prefill: attn_v GEMM on the side stream (q|k fused layers)
     size_t act_sz = 0, gemm_ws_sz = 0;
     int32_t *tok_dev = nullptr, *pos_dev = nullptr, *argmax_dev = nullptr;   // pos_dev = {position, epoch}
-    void *eng_layers = nullptr;      // persistent decode engine (dec_engine.hip): device layer table
-    unsigned *eng_sync = nullptr;    // its edge counters (zeroed ahead of every launch) ++ error word
-    int eng_mode = 0;                // 1: single-token steps through the engine where covered; 0: the launch chain
-    int eng_ok = -1;                 // -1: not prepared yet; 0: not applicable; 1: ready
-    bool eng_used = false;           // the last enqueued single-token step ran the engine
     void *argmax_ws = nullptr;       // ARGMAX_BLOCKS (value, index) partials
     int32_t *moe_ids = nullptr;      // [ubatch][n_expert_used] selected experts (device)
     float *moe_w = nullptr;          // [ubatch][n_expert_used] normalized weights (device)
@@ -402,7 +397,6 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
         const int32_t pe[2] = {0, 1};
         if (hipMemcpy(m->pos_dev, pe, 8, hipMemcpyHostToDevice) != hipSuccess) return fail("pos");
     }
-    if (getenv("KCPP_ENGINE")) m->eng_mode = atoi(getenv("KCPP_ENGINE")) != 0;
     if (has_output) {
         if (hipMalloc(&m->logits, (size_t)hp->n_vocab * 4) != hipSuccess) return fail("logits alloc");
         if (hipHostMalloc((void **)&m->logits_pin, (size_t)hp->n_vocab * 4, hipHostMallocDefault) != hipSuccess)
@@ -434,7 +428,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     for (void *p : {(void *)m->moe_ids_h, (void *)m->moe_w_h, (void *)m->moe_rows_h, (void *)m->moe_rw_h})
         if (p) hipHostFree(p);
     F(m->x); F(m->qkv); F(m->attn); F(m->h); F(m->logits); F(m->q16); F(m->act); F(m->act2); F(m->fa_ws);
-    F(m->gemm_ws); F(m->gemm_ws2); F(m->tok_dev); F(m->pos_dev); F(m->eng_layers); F(m->eng_sync); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
+    F(m->gemm_ws); F(m->gemm_ws2); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
     F(m->kv_scratch); F(m->shift_cs);
     if (m->pin) hipHostFree(m->pin);
     if (m->logits_pin) hipHostFree(m->logits_pin);
@@ -690,12 +684,6 @@ extern "C" int kcpp_model_moe_trace_read(kcpp_model *m, int32_t *out, int n) {
     RT_CHECK(hipMemcpy(out, m->moe_trace, (size_t)n * 4, hipMemcpyDeviceToHost));
     return 0;
 }
-extern "C" int kcpp_model_set_engine(kcpp_model *m, int enable) {
-    m->eng_mode = enable != 0;
-    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
-    return 0;
-}
-extern "C" int kcpp_model_engine_active(kcpp_model *m) { return m->eng_used ? 1 : 0; }
 extern "C" int kcpp_model_set_fa_exact(kcpp_model *m, int enable) {
     m->fa_exact = enable != 0;
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
@@ -812,8 +800,10 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
     if (m->moe_trace)
         RT_CHECK(hipMemcpyAsync(m->moe_trace + (&L - m->layers.data()) * NU, m->moe_ids, (size_t)NU * 4,
                                 hipMemcpyDeviceToDevice, s));
-    if (m->q81) {
-        // types without a fused decode mat-vec (Q4_1 / Q5_1): ffn_norm + activation quantization once, then per
+    auto is_q81 = [](int ty) { return ty == KT_Q4_1 || ty == KT_Q5_1; };
+    if (is_q81(t[6].type) || is_q81(t[7].type) || is_q81(t[8].type)) {
+        // expert types without a fused decode mat-vec (Q4_1 / Q5_1; chosen per layer from the expert tensors, not the
+        // model-wide flag: K-quant experts sit in the RS layouts, which the generic expert mat-vec does not read): ffn_norm + activation quantization once, then per
         // slot the generic mat-vec on the expert slice its device-resident id selects (kcpp_gemv_expert)
         const int vg = kcpp_vec_dot_type(t[6].type), vu = kcpp_vec_dot_type(t[7].type), vd = kcpp_vec_dot_type(t[8].type);
         RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, 1, hp.eps, s));
@@ -1174,89 +1164,13 @@ static int head(kcpp_model *m, int T) {
     return 0;
 }
 
-// Is the persistent decode engine (dec_engine.hip) applicable, and prepared?  Covered: F16 caches, no row split /
-// MoE / strict-parity attention, the compiled geometry, and the Q4_K_M layer types (q, k, wo, gate, up in Q4_K_RS;
-// attn_v and ffn_down in Q4_K_RS or Q6_K_RS).  Prepared outside any stream capture (allocations).
-static bool engine_on(const kcpp_model *m) {
-    return m->eng_mode && m->eng_ok == 1 && m->fused_decode && m->kv_tk == KT_F16 && !m->q81 && !m->fa_exact &&
-           m->lanes.empty();
-}
-static int engine_prepare(kcpp_model *m) {
-    if (m->eng_ok >= 0 || !m->eng_mode) return 0;
-    m->eng_ok = 0;
-    const kcpp_hparams &hp = m->hp;
-    const int64_t E = hp.n_embd, H = hp.n_head, D = E / H;
-    int ncu = 0;
-    RT_CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, m->device));
-    const int nl = m->il1 - m->il0;
-    if (nl < 1 || hp.n_expert > 0 || !kcpp_engine_supported((int)E, hp.n_ff, (int)H, hp.n_head_kv, (int)D, ncu)) return 0;
-    auto q4 = [](const KTensor &t) { return t.type == KT_Q4_K_RS && t.rs.empty(); };
-    auto q46 = [](const KTensor &t) { return (t.type == KT_Q4_K_RS || t.type == KT_Q6_K_RS) && t.rs.empty(); };
-    for (const auto &L : m->layers) {
-        const KTensor *t = L.t;
-        if (t[0].type != KT_F32 || t[5].type != KT_F32 || !q4(t[1]) || !q4(t[2]) || !q46(t[3]) || !q4(t[4]) ||
-            !q4(t[6]) || !q4(t[7]) || !q46(t[8]))
-            return 0;
-    }
-    const int rb = kcpp_engine_layer_bytes();
-    std::vector<uint8_t> tab((size_t)nl * rb);
-    for (int i = 0; i < nl; ++i) {
-        const KTensor *t = m->layers[i].t;
-        kcpp_engine_layer(tab.data() + (size_t)i * rb, t[1].d, t[2].d, t[3].d, t[4].d, t[6].d, t[7].d, t[8].d,
-                          (const float *)t[0].d, (const float *)t[5].d, m->layers[i].kc, m->layers[i].vc,
-                          t[3].type == KT_Q6_K_RS, t[8].type == KT_Q6_K_RS);
-    }
-    const size_t sb = (size_t)kcpp_engine_sync_bytes(nl);
-    RT_CHECK(hipMalloc(&m->eng_layers, tab.size()));
-    RT_CHECK(hipMemcpy(m->eng_layers, tab.data(), tab.size(), hipMemcpyHostToDevice));
-    RT_CHECK(hipMalloc((void **)&m->eng_sync, sb));
-    RT_CHECK(hipMemset(m->eng_sync, 0, sb));
-    m->eng_ok = 1;
-    return 0;
-}
-// after a synchronised engine step: a hand-off timeout (error word != 0) turns the engine off for this model
-static int engine_check(kcpp_model *m, unsigned err) {
-    if (!err) return 0;
-    const int nl = m->il1 - m->il0;
-    std::vector<unsigned> c((size_t)kcpp_engine_sync_bytes(nl) / 4);
-    if (hipMemcpy(c.data(), m->eng_sync, c.size() * 4, hipMemcpyDeviceToHost) == hipSuccess) {
-        const unsigned *e = c.data() + (size_t)nl * 48 * 32;
-        fprintf(stderr, "[kcpp] engine timeout: saw %u, waited for %u, workgroup %u\n", e[1], e[2], e[3]);
-        for (int l = 0; l < std::min(nl, 3); ++l) {
-            fprintf(stderr, "[kcpp]  layer %d:", l);
-            for (int k = 0; k < 48; ++k) fprintf(stderr, " %u", c[((size_t)l * 48 + k) * 32]);
-            fprintf(stderr, "\n");
-        }
-    }
-    (void)hipMemset(m->eng_sync, 0, (size_t)kcpp_engine_sync_bytes(nl));
-    char b[160];
-    snprintf(b, sizeof b, "decode engine: hand-off timeout (code %u); falling back to the launch chain", err);
-    g_err = b;
-    fprintf(stderr, "[kcpp] %s\n", b);
-    m->eng_ok = 0;
-    m->pos_val = -1;
-    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
-    return -7;
-}
-
 // full single-token step with the inputs read from device memory (graph-capturable)
 static int decode_step_dev(kcpp_model *m) {
     const kcpp_hparams &hp = m->hp;
     if (m->has_embed)
         RC(kcpp_get_rows(m->tok_embd.type, m->tok_embd.d, hp.n_embd, hp.n_vocab, m->tok_dev, 1, m->x, hp.n_embd,
                          m->stream));
-    m->eng_used = false;
-    if (engine_on(m)) {
-        const int nl = m->il1 - m->il0;
-        const int64_t E = hp.n_embd, H = hp.n_head;
-        // the edge counters start at zero every launch (a memset node of the graph); the error word after them is kept
-        RT_CHECK(hipMemsetAsync(m->eng_sync, 0, (size_t)kcpp_engine_sync_bytes(nl) - 128, m->stream));
-        RC(kcpp_engine_decode(m->eng_layers, nl, m->x, m->q16, m->fa_ws, m->act, m->h, m->eng_sync, m->pos_dev,
-                              m->rope_tab, hp.eps, 1.0f / sqrtf((float)(E / H)), (int)E, hp.n_ff, (int)H, hp.n_head_kv,
-                              m->stream));
-        m->eng_used = true;
-        if (m->has_output) RC(head_dec(m));
-    } else if (m->fused_decode && m->kv_tk == KT_F16 && !m->q81) {
+    if (m->fused_decode && m->kv_tk == KT_F16 && !m->q81) {
         RC(forward_layers_dec(m));
         if (m->has_output) RC(head_dec(m));
     } else {
@@ -1288,9 +1202,7 @@ static int step_one(kcpp_model *m, int n_past) {
         RC(set_pos(m, n_past));
         const hipError_t e = hipGraphLaunch(m->g_exec, m->stream);
         if (e != hipSuccess) { m->pos_val = -1; RT_CHECK(e); }
-        m->eng_used = engine_on(m);
     } else {
-        RC(engine_prepare(m));
         RC(set_pos(m, n_past));
         const int rc = decode_step_dev(m);
         if (rc) { m->pos_val = -1; return rc; }
@@ -1302,7 +1214,6 @@ static int step_one(kcpp_model *m, int n_past) {
 // single-token graph: embedding of tok_dev, layers at position pos_dev, head, argmax, pos_dev + 1
 static int ensure_graph(kcpp_model *m) {
     if (m->g_exec) return 0;
-    RC(engine_prepare(m));
     hipGraph_t g;
     RT_CHECK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
     int rc = decode_step_dev(m);
@@ -1329,7 +1240,6 @@ static int decode_enqueue(kcpp_model *m, const int32_t *tokens, int T, int n_pas
         if (m->has_embed) RT_CHECK(hipMemcpyAsync(m->tok_dev, &m->pin[0], 4, hipMemcpyHostToDevice, m->stream));
         RC(step_one(m, n_past));
     } else {
-        m->eng_used = false;
         // split into ubatches (llama_decode_internal, src/llama.cpp:17187-17201)
         for (int i = 0; i < T; i += m->ub) {
             const int t = std::min(m->ub, T - i);
@@ -1356,12 +1266,8 @@ extern "C" int kcpp_model_decode(kcpp_model *m, const int32_t *tokens, int T, in
     if (m->has_output && logits_host) {
         RT_CHECK(hipMemcpyAsync(logits_host, m->logits, (size_t)m->hp.n_vocab * 4, hipMemcpyDeviceToHost, m->stream));
     }
-    const bool eng = m->eng_used;
-    if (eng)
-        RT_CHECK(hipMemcpyAsync(&m->pin[3], m->eng_sync + (kcpp_engine_sync_bytes(m->il1 - m->il0) - 128) / 4, 4,
-                                hipMemcpyDeviceToHost, m->stream));
     RT_CHECK(hipStreamSynchronize(m->stream));
-    return eng ? engine_check(m, (unsigned)m->pin[3]) : 0;
+    return 0;
 }
 extern "C" int kcpp_model_device(kcpp_model *m) { return m->device; }
 
@@ -1448,11 +1354,7 @@ extern "C" int kcpp_model_decode_greedy(kcpp_model *m, int n_past, int32_t *toke
     RT_CHECK(hipSetDevice(m->device));
     RC(step_one(m, n_past));
     RT_CHECK(hipMemcpyAsync(&m->pin[2], m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
-    const bool eng = m->eng_used;
-    if (eng)
-        RT_CHECK(hipMemcpyAsync(&m->pin[3], m->eng_sync + (kcpp_engine_sync_bytes(m->il1 - m->il0) - 128) / 4, 4,
-                                hipMemcpyDeviceToHost, m->stream));
     RT_CHECK(hipStreamSynchronize(m->stream));
     *token_out = m->pin[2];
-    return eng ? engine_check(m, (unsigned)m->pin[3]) : 0;
+    return 0;
 }

@@ -103,16 +103,8 @@ _SIGS = {
     "kcpp_model_set_row_split": [P, I, P, P],
     "kcpp_row_split_range": [I64, I, P, I, P, P],
     "kcpp_model_set_fa_exact": [P, I],
-    "kcpp_model_set_engine": [P, I],
     "kcpp_model_set_rope_freqs": [P, P, I],
-    "kcpp_engine_supported": [I, I, I, I, I, I],
-    "kcpp_engine_sync_bytes": [I],
-    "kcpp_engine_layer_bytes": [],
-    "kcpp_engine_layer": [P, P, P, P, P, P, P, P, P, P, P, P, I, I],
-    "kcpp_engine_decode": [P, I, P, P, P, P, P, P, P, P, Fl, Fl, I, I, I, I, P],
-    "kcpp_engine_error": [P, I, P],
     "kcpp_gradient_ai_rope_base": [Fl, I, I, I],
-    "kcpp_model_engine_active": [P],
     "kcpp_model_moe_ids": [P, P, I],
     "kcpp_model_moe_trace": [P, I],
     "kcpp_model_moe_trace_read": [P, P, I],
@@ -123,7 +115,7 @@ _SIGS = {
     "kcpp_kv_store_q": [I, I, P, I64, I64, I64, I, I64, P, P, I64, I, P, P],
     "kcpp_flash_attn_q": [I, I, P, I64, P, P, P, I, I, I, I, I64, I, P, Fl, P],
 }
-_RES = {"kcpp_gradient_ai_rope_base": Fl, "kcpp_engine_sync_bytes": I64, "kcpp_engine_layer": None, "kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
+_RES = {"kcpp_gradient_ai_rope_base": Fl, "kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
         "kcpp_model_create": P, "kcpp_model_hidden": P, "kcpp_model_stream": P, "kcpp_model_weight_bytes": I64,
         "kcpp_last_error": ctypes.c_char_p, "kcpp_model_free": None, "kcpp_fa_set_stamps": None}
 _L.kcpp_act_bytes.argtypes = [I, I64, I64]
@@ -334,14 +326,6 @@ class Model:
         import numpy as np
         a = np.ascontiguousarray(ff, dtype=np.float32)
         _chk(_L.kcpp_model_set_rope_freqs(self.m, a.ctypes.data_as(P), len(a)), "set_rope_freqs")
-
-    def set_engine(self, on):
-        """single-token decode of all layers as one persistent launch (default on where covered; kcpp_engine_decode)"""
-        _chk(_L.kcpp_model_set_engine(self.m, int(on)), "set_engine")
-
-    def engine_active(self):
-        """1 when the last single-token step ran the persistent engine"""
-        return int(_L.kcpp_model_engine_active(self.m))
 
     def set_fa_exact(self, on):
         """strict-parity attention (reference order, f16 accumulation); see kcpp_flash_attn_exact"""
