@@ -65,7 +65,17 @@ def test_deep_logits_vs_reference(K, fx, exact):
           "| ratio max %.3f median %.3f" % (dmax.max() / smax.max(), dmed.max() / smed.max()))
     assert np.all(dmax <= FACTOR * smax.max()), dmax
     assert np.all(dmed <= FACTOR * smed.max()), dmed
-    assert np.array_equal(np.argmax(out, axis=1)[:-1], fx["forced"])
+    # greedy choice: equal to the reference's wherever its own top-2 margin exceeds the spread bar; at a near-tie
+    # (step 1 of this fixture: 5.8776 vs 5.8646, a 0.013 margin under the 0.10 build spread) the GPU's token must be
+    # one the reference scores within that bar of its maximum
+    bar = 2 * FACTOR * smax.max()
+    for i, ref in enumerate(fx["logits"]):
+        top2 = np.sort(ref)[-2:]
+        g = int(np.argmax(out[i]))
+        if top2[1] - top2[0] > bar:
+            assert g == int(np.argmax(ref)), (i, g)
+        else:
+            assert ref[g] >= top2[1] - bar, (i, g, ref[g], top2)
 
 
 @pytest.mark.parametrize("exact", [False, True], ids=["production", "fa_exact"])
