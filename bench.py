@@ -144,6 +144,57 @@ def cpu_baseline(hp, types, threads, depth=3840, n_ub=512, n_gen=32, threads2=8)
                                                                 threads, n_ub, n_gen, threads2)}
 
 
+def generate_path(hp, types, n_prompt, n_gen, ubatch, seed=1234):
+    """The drop-in number: koboldcpp --benchmark (koboldcpp.py:4274-4348) through the C ABI koboldcpp.py binds --
+    load_model() on a full-size Llama-3-8B Q4_K_M GGUF, then ONE generate() with the benchmark's sampler settings
+    (temperature 0.1, top_k 1, rep_pen 1, EOS banned), the prompt cut to max_context_length - max_length tokens, and
+    koboldcpp's own speeds from get_last_process_time / get_last_eval_time (ms per token, gpttype_adapter.cpp:
+    3513-3526).  generate() reads every token's logits on the host and samples there, as the reference does.  The GGUF
+    holds the real tensor directory with its data left as a sparse-file hole (no checkpoints exist offline); the
+    weights are the runtime's synthetic ones (kcpp_expose_synth_weights), as in the rest of this bench."""
+    import ctypes
+    import tempfile
+    import gguf_writer as GW
+    import koboldcpp_amd.lib as K
+    from koboldcpp_amd import expose as X
+    max_ctx = n_prompt + n_gen
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "llama3-8b-q4_k_m-synthetic.gguf")
+        GW.llama_gguf(path, dict(hp, n_ctx=8192), types, seed, GW.WORDS, sparse=True)
+        h = X.init_library()
+        li = X.load_model_inputs()
+        li.model_filename = path.encode()
+        li.max_context_length = max_ctx
+        li.blasbatchsize = ubatch
+        li.gpulayers = 999
+        li.flash_attention = True
+        li.rope_freq_base = 10000.0
+        li.rope_freq_scale = 0.0          # koboldcpp.py default --ropeconfig: the model's own RoPE
+        if not h.load_model(li):
+            raise RuntimeError("load_model failed")
+        if K.raw().kcpp_expose_synth_weights(ctypes.c_uint64(seed)) != 0:
+            raise RuntimeError("kcpp_expose_synth_weights failed")
+
+        def gen(prompt, n):
+            gi = X.generation_inputs()
+            gi.prompt, gi.memory = prompt, b""
+            gi.max_context_length, gi.max_length = max_ctx, n
+            gi.temperature, gi.top_k, gi.rep_pen, gi.bypass_eos_token, gi.seed = 0.1, 1, 1.0, True, 7
+            out = h.generate(gi)
+            if out.status != 1:
+                raise RuntimeError("generate failed")
+            return h.get_last_token_count()
+        gen(b"hello world", 8)                      # warm-up (first touch, graph capture); shares only BOS
+        # the benchmark prompt (" 1" repeated, koboldcpp.py:4300-4303), long enough to be cut to n_prompt tokens
+        n = gen(b" 1" * (n_prompt + 64), n_gen)
+        pt, et = h.get_last_process_time(), h.get_last_eval_time()
+    return {"decode_tok_s": round(1000.0 / et, 2), "prefill_tok_s": round(1000.0 / pt, 1), "gen_tokens": n,
+            "max_context_length": max_ctx,
+            "how": "koboldcpp --benchmark semantics through the C ABI: load_model (sparse full-size GGUF, synthetic "
+                   "weights) + one generate() (temperature 0.1, top_k 1, rep_pen 1, EOS banned; host sampling per "
+                   "token); speeds = 1000 / get_last_eval_time and 1000 / get_last_process_time (ms per token)"}
+
+
 def run_model(K, torch, hp, types, n_prompt, ubatch, steps, warmup):
     """koboldcpp --benchmark semantics on one GPU: prefill n_prompt ids (" 1" pattern) in ubatches, then
     greedy decode (graph replay + on-device argmax per token).  Weights and inputs resident before timing."""
@@ -224,7 +275,82 @@ def other_config(args, K, torch):
                            "model": "Mixtral-8x7B-shape Q5_K_M random-init", "parallelism": "single GPU"},
                 "prefill_tok_s": round(r["pre"], 1), "weight_bytes": r["wb"], "bytes_per_token": tok_bytes,
                 "decode_effective_GBps": round(gbs, 1), "decode_hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+    if args.config == "llama3-70b-stage":
+        return stage70b(args, K, torch)
     raise SystemExit("unknown --config %s" % args.config)
+
+
+LLAMA3_70B = dict(n_vocab=128256, n_embd=8192, n_head=64, n_head_kv=8, n_layer=80, n_ff=28672, n_ctx=4096,
+                  eps=1e-5, rope_base=500000.0)
+
+
+def stage70b(args, K, torch):
+    """BASELINE configs[3] (Llama-3-70B Q4_K_M, --tensorsplit over 8 GPUs) as one GPU can measure it: the first
+    pipeline stage exactly as load_model builds it for tensor_split 1:...:1 (layers [0, 10) + the embedding), 4k
+    context (prefill 3840 in ubatches of 512, then single-token steps at 3841..), its decode rate and HBM fraction;
+    and the per-boundary cost of the stage hand-off, from the 8B bench model run as 1 stage and as 8 stages on this
+    one GPU (KCPP_VIRTUAL_DEVICES: the event-ordered device-copy hand-off of expose.cpp, 7 hidden-state hops + the
+    token home per step).  The 8-GPU curve itself is the driver's (SCALE)."""
+    import refharness as R
+    hp = dict(LLAMA3_70B)
+    types = R.q4_k_m_types(hp["n_layer"])
+    il1 = hp["n_layer"] // 8
+    m = K.Model(hp, types, il0=0, il1=il1, has_embed=True, has_output=False, max_ubatch=args.ubatch)
+    m.synth(1234)
+    prompt = [16 + (i % 2) for i in range(args.prompt)]
+    m.decode(prompt[:64], 0, want_logits=False)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m.decode(prompt, 0, want_logits=False)
+    torch.cuda.synchronize()
+    t_pp = time.perf_counter() - t0
+    n = len(prompt)
+    m.decode([16], n, want_logits=False)        # the stage's single-token graph; its token stays in tok_dev
+    n += 1
+    L = K.raw()
+    for _ in range(args.warmup):
+        assert L.kcpp_model_step_dev(m.m, n) == 0
+        n += 1
+    steps = min(args.steps, hp["n_ctx"] - n)
+    m.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        assert L.kcpp_model_step_dev(m.m, n) == 0
+        n += 1
+    m.sync()
+    t_tg = time.perf_counter() - t0
+    wb = m.weight_bytes()
+    m.close()
+    embd = R.row_bytes(types[0], hp["n_embd"]) * hp["n_vocab"]
+    kv = 2 * il1 * hp["n_head_kv"] * (hp["n_embd"] // hp["n_head"]) * 2 * (n - steps / 2)
+    tok_bytes = wb - embd + kv
+    ms = t_tg / steps * 1e3
+    gbs = tok_bytes / (ms * 1e-3) / 1e9
+    # hand-off cost: the 8B bench model as 1 stage vs 8 stages on this GPU (same work, 8 hops more per step)
+    hp8, t8 = dict(LLAMA3_8B), q4_k_m_types(32)
+    hs = min(64, args.steps)
+    os.environ["KCPP_VIRTUAL_DEVICES"] = "1"
+    try:
+        one = K.engine_bench(hp8, t8, 1, 512, 512, 8, hs)
+        eight = K.engine_bench(hp8, t8, 8, 512, 512, 8, hs)
+    finally:
+        del os.environ["KCPP_VIRTUAL_DEVICES"]
+    per_hop_us = (eight["decode_s"] - one["decode_s"]) / hs / 8 * 1e6
+    return {"metric": "decode tok/s of one Llama-3-70B Q4_K_M pipeline stage (layers 0-9 + embedding, 4k ctx)",
+            "value": round(1e3 / ms, 2), "unit": "tok/s", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "dtype": "q4_K/q6_K weights x q8_K activations (int8 dot, f32 accum); f16 KV", "data": "synthetic",
+            "config": {"workload": "llama3-70b-q4_k_m stage [0,%d) of tensor_split 1:...:1 over 8 GPUs: prefill %d "
+                                   "(ubatch %d) + single-token steps" % (il1, args.prompt, args.ubatch),
+                       "model": "Llama-3-70B-shape Q4_K_M random-init", "parallelism": "one pipeline stage on one GPU"},
+            "prefill_tok_s": round(args.prompt / t_pp, 1), "stage_bytes_per_token": int(tok_bytes),
+            "decode_effective_GBps": round(gbs, 1), "decode_hbm_frac": round(gbs / HBM_PEAK_GBS, 4),
+            "handoff": {"per_hop_us": round(per_hop_us, 2), "hops_per_step": 8,
+                        "one_stage_ms_per_token": round(one["decode_s"] / hs * 1e3, 4),
+                        "eight_stages_ms_per_token": round(eight["decode_s"] / hs * 1e3, 4),
+                        "how": "Llama-3-8B bench model, 512-token prompt, %d greedy steps: 1 stage vs 8 stages on one GPU "
+                               "(KCPP_VIRTUAL_DEVICES, event-ordered device copies); (t8 - t1) / steps / 8 hops "
+                               "(7 hidden states + the token home)" % hs}}
 
 
 def main():
@@ -235,12 +361,14 @@ def main():
     ap.add_argument("--prompt", type=int, default=3840)
     ap.add_argument("--ubatch", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-generate-path", action="store_true",
+                    help="skip the generate() leg (koboldcpp --benchmark through the C ABI)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--roofline-only", action="store_true",
                     help="only the dominant-kernel timing (for the rocprofv3 --pmc passes in profiles/)")
     ap.add_argument("--config", default="llama3-8b-q4_k_m",
-                    choices=["llama3-8b-q4_k_m", "llama3-8b-q8_0-b32", "mixtral-8x7b-q5_k_m"],
-                    help="BASELINE configs[1] (default: the driver's line), configs[2], configs[4]")
+                    choices=["llama3-8b-q4_k_m", "llama3-8b-q8_0-b32", "mixtral-8x7b-q5_k_m", "llama3-70b-stage"],
+                    help="BASELINE configs[1] (default: the driver's line), configs[2], configs[4], configs[3]'s one-GPU stage")
     ap.add_argument("--layers", type=int, default=None, help="override n_layer (debug only; invalidates metric)")
     args = ap.parse_args()
 
@@ -332,6 +460,11 @@ def bench_line(args, K, torch, hp, types, r, n_dev, par):
                              "flops": int(pre_flops), "scope": "whole prefill (all kernels), F(n) of SURVEY.md 8d; "
                                                                "peak = %d GPU(s)" % n_dev},
     }
+    if n_dev == 1 and not args.no_generate_path:
+        try:
+            out["generate_path"] = generate_path(hp, types, args.prompt, 256, args.ubatch)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["generate_path"] = {"error": str(e)[:300]}
     if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(hp, types, args.cpu_threads)

@@ -344,6 +344,9 @@ int64_t kcpp_model_weight_bytes(kcpp_model *m);
  * hand-off ran on RCCL}.  0 ok, -1 fewer than n_dev GPUs visible. */
 int kcpp_engine_bench(const kcpp_hparams *hp, const int *types, int n_types, int n_dev, const float *tensor_split,
                       uint64_t seed, int n_prompt, int ub, int n_warm, int n_steps, double *out);
+/* bench / test hook: the model load_model() holds gets the runtime's synthetic weights (kcpp_model_synth_weights per
+ * stage; bench.py's generate() leg loads a sparse full-size GGUF, then this); 0 on success, -1 without a model */
+int kcpp_expose_synth_weights(uint64_t seed);
 /* test hook: the pipeline schedule's enqueue order (prefill, argmax, token home, `steps` greedy steps) for n_stages
  * stages, recorded by the schedule's trace backend into out (host only, no device calls) */
 int kcpp_pipeline_trace(int n_stages, int ub, int T, int n_past, int steps, char *out, int cap);

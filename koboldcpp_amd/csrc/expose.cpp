@@ -1047,6 +1047,18 @@ int kcpp_engine_bench(const kcpp_hparams *hp, const int *types, int n_types, int
     return 0;
 }
 
+// bench / test hook (not part of koboldcpp's ABI): replace the loaded model's weights by the runtime's synthetic weights
+// (kcpp_model_synth_weights on every stage).  bench.py's generate() leg loads a full-size GGUF whose tensor data is a
+// sparse-file hole (no checkpoints exist offline) and synthesizes the weights on the device; the context is dropped.
+int kcpp_expose_synth_weights(uint64_t seed) {
+    Engine *e = g_eng.get();
+    if (!e) return -1;
+    for (kcpp_model *m : e->stages)
+        if (kcpp_model_synth_weights(m, seed)) return -2;
+    e->ctx.clear();
+    return 0;
+}
+
 // test hook (tests/test_pipeline.py): load_model's layer placement (split_layers): out[i] = device of layer i for
 // i < n_layer, out[n_layer] = the output head's device
 int kcpp_split_layers(int n_layer, int n_dev, const float *tensor_split, int *out) {

@@ -51,7 +51,10 @@ using namespace rs;
 // PRO 0: act copy, 1: rms_norm * w -> Q8_K, 2: quantize only; MC = ceil(K / 4096) prologue chunks;
 // PF: issue the next group's loads before reducing the current one.
 // NWV waves per workgroup (4, or 8: one activation prologue shared by twice the waves)
-template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4>
+// XL (long K: 70B ffn_down K = 28672, MoE n_ff > 14336): the lane's activation slices are read from the LDS image per
+// piece instead of living in registers for the launch (NI up to 16 pieces per row would not fit beside the weights);
+// NI is then a ceiling, pieces past the row are masked (their loads clamped to the row's last piece)
+template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4, bool XL = false>
 __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     using T = RS<TYPE>;
     constexpr int RR = MODE == 1 ? 2 * R : R;
@@ -108,21 +111,24 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     if constexpr (PRO != 0) {
         lean::ActPro<PRO, (MC * 4 + NWV - 1) / NWV, 64 * NWV> pro;
         pro.load(a);
-        issue(g0, ba);
+        if constexpr (!XL) issue(g0, ba);     // XL: a row's pieces and the prologue's registers do not fit together
 #ifdef KCPP_STAMPS
         pro.compute(a, lds, st_);
 #else
         pro.compute(a, lds);
 #endif
+        if constexpr (XL) issue(g0, ba);
     } else {
         lean::ActCopyCol cp;
         cp.load(a.act, K, a.act_mtot > 0 ? a.act_mtot : 1, a.act_col);
         issue(g0, ba);
         cp.store(lds, K);
     }
-    typename T::Act xr[NI];
+    typename T::Act xr[XL ? 1 : NI];
+    if constexpr (!XL) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i) T::act(lds, K, min(T::sb_of(lane, i), nsb - 1), lc, xr[i]);
+        for (int i = 0; i < NI; ++i) T::act(lds, K, min(T::sb_of(lane, i), nsb - 1), lc, xr[i]);
+    }
     RS_STAMP(1);
 
     float slot[R];
@@ -136,11 +142,16 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
             const bool ok = (NI * 64 == npieces) || lane + 64 * i < npieces;
+            typename T::Act xl;
+            if constexpr (XL) T::act(lds, K, min(T::sb_of(lane, i), nsb - 1), lc, xl);
 #pragma unroll
             for (int r = 0; r < RR; ++r) {
-                const float p = T::dot(b.w[i][r], xr[i], lc);
+                const float p = T::dot(b.w[i][r], XL ? xl : xr[i], lc);
                 acc[r] += ok ? p : 0.0f;
             }
+            // XL: keep piece i + 1's LDS activation reads behind piece i's dot (hoisted, all NI of them would be live
+            // beside the row's NI in-flight weight pieces and spill)
+            if constexpr (XL) asm volatile("" ::: "memory");
         }
 #pragma unroll
         for (int r = 0; r < RR; ++r) acc[r] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_sum_f(acc[r]))));
@@ -185,7 +196,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
 }
 
 namespace {
-template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4>
+template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4, bool XL = false>
 int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
     int64_t ntot = 0;
     for (int i = 0; i < a.nseg; ++i) {
@@ -196,7 +207,7 @@ int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
     int64_t nblk = std::min<int64_t>((groups + NWV - 1) / NWV, max_blocks);
     nblk = std::max<int64_t>(nblk, (groups + 64 * NWV - 1) / (64 * NWV));    // <= 64 groups per wave (result slots)
     const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
-    hipLaunchKernelGGL((k_gemv_rs<TYPE, NI, R, MODE, PRO, MC, PF, NWV>), dim3((unsigned)nblk), dim3(64 * NWV),
+    hipLaunchKernelGGL((k_gemv_rs<TYPE, NI, R, MODE, PRO, MC, PF, NWV, XL>), dim3((unsigned)nblk), dim3(64 * NWV),
                        (size_t)abytes + 16, s, a);
     KCPP_CHECK(hipGetLastError());
     return 0;
@@ -237,6 +248,30 @@ int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
     KCPP_RS_P(2)
 #undef KCPP_RS_P
     return -3;
+}
+// long K (XL): mode 0 with a quantize / norm prologue only (the down projection of Llama-3-70B, K = 28672, and MoE
+// experts with n_ff past 14336), one row per group, 8-wave workgroups, no group prefetch: a row's NI pieces are already
+// 16 KB (Q4_K, K = 28672) in flight per wave, 128 KB per CU.  NI = the ceiling the shape rounds up to.
+template <int TYPE, int NI>
+int pick_rs_xl(const DecArgs &a, int mode, int pro, hipStream_t s) {
+    constexpr int MC = TYPE == KT_Q6_K_RS ? NI : NI / 2;        // ceil(K / 4096) at the ceiling
+    if (mode != 0) return -3;
+    if (pro == 2) return launch_rs<TYPE, NI, 1, 0, 2, MC, 0, 8, true>(a, 256, s);
+    if (pro == 1) return launch_rs<TYPE, NI, 1, 0, 1, MC, 0, 8, true>(a, 256, s);
+    return -3;
+}
+template <int TYPE>
+int dispatch_rs_xl(const DecArgs &a, int ni, int mode, int pro, hipStream_t s) {
+    if constexpr (TYPE == KT_Q6_K_RS) {
+        if (ni <= 6) return pick_rs_xl<TYPE, 6>(a, mode, pro, s);
+        return pick_rs_xl<TYPE, 8>(a, mode, pro, s);
+    } else if constexpr (TYPE == KT_Q5_K_RS) {         // 12 VGPRs per piece: spills past 10 pieces
+        return ni <= 10 ? pick_rs_xl<TYPE, 10>(a, mode, pro, s) : -3;
+    } else {
+        if (ni <= 10) return pick_rs_xl<TYPE, 10>(a, mode, pro, s);
+        if (ni <= 12) return pick_rs_xl<TYPE, 12>(a, mode, pro, s);
+        return ni <= 14 ? pick_rs_xl<TYPE, 14>(a, mode, pro, s) : -3;
+    }
 }
 }  // namespace
 
@@ -361,12 +396,15 @@ extern "C" int kcpp_gemv_rs_qkv_mixed(const void *args, void *stream) {
     return 0;
 }
 
-// K coverage of the RS kernels (the runtime picks an RS layout only where this holds)
+// K coverage of the RS kernels (the runtime picks an RS layout only where this holds): activation slices in registers
+// up to 56 (Q4_K / Q5_K) / 64 (Q6_K) super-blocks; read from LDS (XL, one row's pieces in flight per wave) up to the
+// register budget of a row: 112 (Q4_K: K 28672, Llama-3-70B's n_ff), 80 (Q5_K), 128 (Q6_K) super-blocks
 extern "C" int kcpp_rs_supported(int type, int64_t K) {
     if (K % 256 || K < 256) return 0;
     const int64_t nsb = K / 256;
-    if (type == KT_Q4_K_RS || type == KT_Q4_K || type == KT_Q5_K_RS || type == KT_Q5_K) return nsb <= 56;
-    if (type == KT_Q6_K_RS || type == KT_Q6_K) return nsb % 8 == 0 && nsb <= 64;
+    if (type == KT_Q4_K_RS || type == KT_Q4_K) return nsb <= 112;
+    if (type == KT_Q5_K_RS || type == KT_Q5_K) return nsb <= 80;
+    if (type == KT_Q6_K_RS || type == KT_Q6_K) return nsb % 8 == 0 && nsb <= 128;
     return 0;
 }
 
@@ -386,7 +424,8 @@ extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void 
         case 4: return pick_rs<KT_Q4_K_RS, 4, 2>(a, mode, pro, s);
         case 5: return pick_rs<KT_Q4_K_RS, 5, 3>(a, mode, pro, s);
         case 6: return pick_rs<KT_Q4_K_RS, 6, 3>(a, mode, pro, s);
-        default: return mc <= 4 ? pick_rs<KT_Q4_K_RS, 7, 4>(a, mode, pro, s) : -3;
+        case 7: return pick_rs<KT_Q4_K_RS, 7, 4>(a, mode, pro, s);
+        default: return dispatch_rs_xl<KT_Q4_K_RS>(a, ni, mode, pro, s);
         }
     }
     if (type == KT_Q5_K_RS) {
@@ -398,7 +437,8 @@ extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void 
         case 4: return pick_rs<KT_Q5_K_RS, 4, 2>(a, mode, pro, s);
         case 5: return pick_rs<KT_Q5_K_RS, 5, 3>(a, mode, pro, s);
         case 6: return pick_rs<KT_Q5_K_RS, 6, 3>(a, mode, pro, s);
-        default: return mc <= 4 ? pick_rs<KT_Q5_K_RS, 7, 4>(a, mode, pro, s) : -3;
+        case 7: return pick_rs<KT_Q5_K_RS, 7, 4>(a, mode, pro, s);
+        default: return dispatch_rs_xl<KT_Q5_K_RS>(a, ni, mode, pro, s);
         }
     }
     if (type == KT_Q6_K_RS) {
@@ -407,7 +447,8 @@ extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void 
         case 1: return pick_rs<KT_Q6_K_RS, 1, 1>(a, mode, pro, s);
         case 2: return pick_rs<KT_Q6_K_RS, 2, 2>(a, mode, pro, s);
         case 3: return pick_rs<KT_Q6_K_RS, 3, 3>(a, mode, pro, s);
-        default: return pick_rs<KT_Q6_K_RS, 4, 4>(a, mode, pro, s);
+        case 4: return pick_rs<KT_Q6_K_RS, 4, 4>(a, mode, pro, s);
+        default: return dispatch_rs_xl<KT_Q6_K_RS>(a, ni, mode, pro, s);
         }
     }
     return -3;

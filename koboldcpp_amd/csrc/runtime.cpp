@@ -875,7 +875,14 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
             a.res = j == NU - 1 ? m->x : nullptr;
         }
         const int rc = kcpp_gemv_dec(t[8].type, &a, 0, 2, rows_per_wave(E, 0), s);
-        if (rc == -8) { g_err = "MoE down projection: n_ff beyond the fused mat-vec's K budget"; return rc; }
+        if (rc == -8) {
+            // n_ff beyond the fused kernels' budget (no RS layout for it: chain is false, slots + combine): quantize the
+            // slot's h once, then the generic expert mat-vec (device-resident expert id, times the router weight)
+            RC(kcpp_quantize_act(kcpp_vec_dot_type(t[8].type), a.x, F, m->act2, F, 1, s));
+            RC(kcpp_gemv_expert(t[8].type, t[8].d, nullptr, F, E, m->act2, m->moe_slots + j * E, m->moe_ids + j,
+                                (int64_t)t[8].slice_bytes, hp.n_expert, m->moe_w + j, 0, s));
+            continue;
+        }
         RC(rc);
     }
     return chain ? 0 : kcpp_moe_combine(m->x, m->moe_slots, E, NU, E, s);

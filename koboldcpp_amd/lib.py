@@ -61,6 +61,7 @@ _SIGS = {
     "kcpp_pieces_probe": [ctypes.c_char_p, P, I64, P, I],
     "kcpp_tokenizer_special_ids": [ctypes.c_char_p, P],
     "kcpp_engine_bench": [P, P, I, I, P, U64, I, I, I, I, P],
+    "kcpp_expose_synth_weights": [U64],
     "kcpp_pipeline_trace": [I, I, I, I, I, ctypes.c_char_p, I],
     "kcpp_split_layers": [I, I, P, P],
     "kcpp_model_argmax_async": [P],

@@ -29,40 +29,51 @@ def _val(v):
         return struct.pack("<I", STR) + _s(v)
     if isinstance(v, tuple):                       # (elem_type, list)
         et, items = v
-        out = struct.pack("<I", ARR) + struct.pack("<IQ", et, len(items))
-        for it in items:
-            if et == STR:
-                out += _s(it)
-            elif et == F32:
-                out += struct.pack("<f", it)
-            elif et == I32:
-                out += struct.pack("<i", it)
-            else:
-                raise ValueError(et)
-        return out
+        out = [struct.pack("<I", ARR) + struct.pack("<IQ", et, len(items))]
+        if et == STR:
+            out += [_s(it) for it in items]
+        elif et == F32:
+            out.append(struct.pack("<%df" % len(items), *items))
+        elif et == I32:
+            out.append(struct.pack("<%di" % len(items), *items))
+        else:
+            raise ValueError(et)
+        return b"".join(out)
     raise ValueError(type(v))
+
+
+def _len(data):
+    return data if isinstance(data, int) else len(data)
 
 
 def write(path, kv, tensors, align=32):
     """kv: dict key -> value (int -> u32, float -> f32, str, bool, (type, list));
-    tensors: list of (name, ggml_type, ne list, bytes)"""
-    head = b"GGUF" + struct.pack("<IQQ", 3, len(tensors), len(kv))
+    tensors: list of (name, ggml_type, ne list, bytes -- or an int: that many zero bytes, left as a hole of a sparse
+    file, so a full-size model costs no disk and no write time)"""
+    parts = [b"GGUF" + struct.pack("<IQQ", 3, len(tensors), len(kv))]
     for k, v in kv.items():
-        head += _s(k) + _val(v)
+        parts.append(_s(k) + _val(v))
     off = 0
     offs = []
     for name, t, ne, data in tensors:
         offs.append(off)
-        off += (len(data) + align - 1) // align * align
+        off += (_len(data) + align - 1) // align * align
     for (name, t, ne, data), o in zip(tensors, offs):
-        head += _s(name) + struct.pack("<I", len(ne)) + b"".join(struct.pack("<Q", n) for n in ne)
-        head += struct.pack("<IQ", t, o)
+        parts.append(_s(name) + struct.pack("<I", len(ne)) + b"".join(struct.pack("<Q", n) for n in ne))
+        parts.append(struct.pack("<IQ", t, o))
+    head = b"".join(parts)
     pad = (-len(head)) % align
     with open(path, "wb") as f:
         f.write(head + b"\0" * pad)
+        base = f.tell()
         for (name, t, ne, data), o in zip(tensors, offs):
-            f.write(bytes(data))
-            f.write(b"\0" * ((-len(data)) % align))
+            if isinstance(data, int):
+                f.seek(base + o + (data + align - 1) // align * align)
+            else:
+                f.seek(base + o)
+                f.write(bytes(data))
+                f.write(b"\0" * ((-len(data)) % align))
+        f.truncate(base + off)
 
 
 def spm_vocab(n_vocab, words):
@@ -85,10 +96,12 @@ def spm_vocab(n_vocab, words):
 LAYER_NAMES = ["attn_norm", "attn_q", "attn_k", "attn_v", "attn_output", "ffn_norm", "ffn_gate", "ffn_up", "ffn_down"]
 
 
-def llama_gguf(path, hp, types, seed, words, split_experts=False, kv_extra=None, rope_freqs=None):
+def llama_gguf(path, hp, types, seed, words, split_experts=False, kv_extra=None, rope_freqs=None, sparse=False):
     """Llama GGUF with the runtime's synthetic weights.  MoE (hp["n_expert"]): gate/up/down as 3-D
     blk.N.ffn_*_exps tensors [k, n, n_expert] plus blk.N.ffn_gate_inp, or with split_experts the older
-    per-expert blk.N.ffn_gate.E tensors (both accepted by llm_load_tensors, src/llama.cpp:7176-7215)."""
+    per-expert blk.N.ffn_gate.E tensors (both accepted by llm_load_tensors, src/llama.cpp:7176-7215).
+    sparse: every tensor's data left as zeros in a sparse file (bench.py's full-size generate() leg: the weights are
+    then synthesized on the device, kcpp_expose_synth_weights)."""
     import refharness as R
     toks, scores, ttypes = spm_vocab(hp["n_vocab"], words)
     kv = {
@@ -126,6 +139,10 @@ def llama_gguf(path, hp, types, seed, words, split_experts=False, kv_extra=None,
     tensors = []
     for idx, ((k, n), t) in enumerate(zip(R.weight_shapes(hp), types)):
         ns = R.n_slices(hp, idx)
+        if sparse:
+            ne = [k] if n == 1 else ([k, n] if ns == 1 else [k, n, ns])
+            tensors.append((names[idx], t, ne, R.row_bytes(t, k) * n * ns))
+            continue
         if ns == 1:
             data = R.synth(t, seed, idx, k, n)
             ne = [k] if n == 1 else [k, n]

@@ -107,6 +107,27 @@ def test_down_residual(env, base):
     assert rel_err(y.cpu().numpy(), ref) < RTOL
 
 
+@pytest.mark.parametrize("base,Kd,N", [(R.Q4_K, 28672, 8192), (R.Q6_K, 28672, 8192), (R.Q5_K, 20480, 4096)],
+                         ids=["q4k-70b-down", "q6k-70b-down", "q5k-long"])
+def test_down_residual_long_k(env, base, Kd, N):
+    """x += down . Q8_K(h) beyond the register-resident activation budget: Llama-3-70B's ffn_down (K = n_ff = 28672,
+    Q4_K and the more-bits layers' Q6_K) and a long-K Q5_K (MoE experts with a large n_ff) on the XL variant of
+    k_gemv_rs (activation slices read from the LDS image per piece)"""
+    torch, K = env
+    rs = {R.Q4_K: 112, R.Q5_K: 113, R.Q6_K: 114}[base]
+    assert K.raw().kcpp_rs_supported(rs, Kd) == 1
+    h, _, res = vecs(Kd, N, 7)
+    W = dev_synth(torch, K, rs, Kd, N, 8)
+    hd, y = torch.from_numpy(h).cuda(), torch.from_numpy(res).cuda()
+    a = K.DecArgs()
+    a.K, a.nseg, a.x = Kd, 1, hd.data_ptr()
+    a.W[0], a.N[0], a.Y[0], a.res = W.data_ptr(), N, y.data_ptr(), y.data_ptr()
+    assert K.gemv_dec(rs, a, 0, 2, 1, sptr(torch)) == 0
+    torch.cuda.synchronize()
+    ref = R.mul_mat(base, R.synth(base, SEED, 8, Kd, N), Kd, N, h)[0] + res
+    assert rel_err(y.cpu().numpy(), ref) < RTOL
+
+
 def test_wo_residual(env):
     """x += wo . attn (attn already Q8_K, written by the flash-attention combine)"""
     torch, K = env
