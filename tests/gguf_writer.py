@@ -43,7 +43,7 @@ def _val(v):
 
 
 def _len(data):
-    return data if isinstance(data, int) else len(data)
+    return data if isinstance(data, int) else memoryview(data).nbytes
 
 
 def write(path, kv, tensors, align=32):
@@ -72,7 +72,7 @@ def write(path, kv, tensors, align=32):
             else:
                 f.seek(base + o)
                 f.write(bytes(data))
-                f.write(b"\0" * ((-len(data)) % align))
+                f.write(b"\0" * ((-_len(data)) % align))
         f.truncate(base + off)
 
 
