@@ -283,6 +283,9 @@ int kcpp_model_forward_hidden(kcpp_model *m, int T, int n_past);
 /* greedy argmax of the last logits on device (avoids the 0.5 MB logits copy); also becomes the
  * next decode_greedy step's input token */
 int kcpp_model_argmax(kcpp_model *m, int32_t *token_out);
+/* the greedy token the last single-token step computed on device (every step of the stage with the output head ends
+ * in its argmax): 4-byte read + stream sync, no launch */
+int kcpp_model_read_argmax(kcpp_model *m, int32_t *token_out);
 /* the same enqueued on the stage's stream (no host synchronisation): the token lands in kcpp_model_argmax_dev */
 int kcpp_model_argmax_async(kcpp_model *m);
 /* one single-token step at n_past whose input token is already in kcpp_model_token_dev (stage with the embedding;

@@ -87,6 +87,9 @@ struct Engine {
     bool use_contextshift = false;
     std::vector<int> ctx;                   // tokens whose K/V are in the caches
     std::vector<float> logits;
+    // the last stage's argmax_dev holds the greedy token of the current logits AND stage 0's token input holds the
+    // same token: true after a single-token step (its graph ends in the argmax) once the token is home
+    bool dev_tok = false;
     ~Engine() {
         for (size_t s = 0; s < stages.size(); ++s) {
             hipSetDevice(devs[s]);
@@ -479,14 +482,20 @@ bool chain_is_argmax(const SamplerSetup &S) {
 
 // one sampled token from the last stage's logits (gpttype_adapter.cpp:3182-3232); < 0 on a device error.
 // slop: the antislop bans recorded for this position (set to the lowest logit like the token bans, :3219-3225)
+// on_dev: the token is the device argmax (the next step can take it from the device, greedy_step)
 int sample(Engine &e, const SamplerSetup &S, const std::vector<int> &last_n, std::mt19937 &rng, float *mu,
-           const std::vector<int> *slop) {
+           const std::vector<int> *slop, bool *on_dev) {
     kcpp_model *last = e.stages.back();
     const int eos = e.tok.eos(), eot = e.tok.eot();
+    *on_dev = false;
     if (chain_is_argmax(S) && !slop) {
         int32_t t = 0;
-        if (kcpp_model_argmax(last, &t)) return -1;
-        if (!(S.suppress_eos && (t == eos || (t == eot && eot != -1)))) return t;
+        // after a single-token step the step's own argmax is already on the device: read it; after a prefill, run it
+        if (e.dev_tok ? kcpp_model_read_argmax(last, &t) : kcpp_model_argmax(last, &t)) return -1;
+        if (!(S.suppress_eos && (t == eos || (t == eot && eot != -1)))) {
+            *on_dev = true;
+            return t;
+        }
     }
     e.logits.resize(e.hp.n_vocab);
     if (kcpp_model_read_logits(last, e.logits.data())) return -1;
@@ -800,6 +809,7 @@ generation_outputs generate(const generation_inputs in) {
     if (keep == toks.size()) --keep;
     e->ctx.assign(toks.begin(), toks.begin() + keep);
     const auto t0 = std::chrono::steady_clock::now();
+    e->dev_tok = false;
     if (forward(*e, toks.data() + keep, (int)(toks.size() - keep), (int)keep)) {
         fprintf(stderr, "[kcpp] generate: prefill failed: %s\n", kcpp_last_error());
         g_finished = true;
@@ -858,7 +868,8 @@ generation_outputs generate(const generation_inputs in) {
     for (; n_gen < max_len; ++n_gen) {
         if (g_abort) { stop = KCPP_STOP_CUSTOM_STOPPER; break; }
         const auto sb = slop.find((int)e->ctx.size());
-        const int t = sample(*e, S, last_n, rng, &g_mirostat_mu, sb == slop.end() ? nullptr : &sb->second);
+        bool on_dev = false;
+        const int t = sample(*e, S, last_n, rng, &g_mirostat_mu, sb == slop.end() ? nullptr : &sb->second, &on_dev);
         if (t < 0) { fprintf(stderr, "[kcpp] generate: sampling failed: %s\n", kcpp_last_error()); break; }
         if (!last_n.empty()) last_n.erase(last_n.begin());     // (:3238: an antislop rewind may have emptied it)
         last_n.push_back(t);
@@ -899,6 +910,7 @@ generation_outputs generate(const generation_inputs in) {
                     e->ctx.resize(std::max(0, cur - rewind));
                     const int32_t back = e->ctx.back();
                     e->ctx.pop_back();
+                    e->dev_tok = false;
                     if (forward(*e, &back, 1, (int)e->ctx.size())) {
                         fprintf(stderr, "[kcpp] generate: decode failed\n");
                         hit = true;
@@ -917,7 +929,18 @@ generation_outputs generate(const generation_inputs in) {
         if (rewound) continue;
         if ((int)e->ctx.size() >= e->hp.n_ctx - 1) { ++n_gen; break; }
         const int32_t tt = t;
-        if (forward(*e, &tt, 1, (int)e->ctx.size())) { fprintf(stderr, "[kcpp] generate: decode failed\n"); break; }
+        int frc;
+        if (on_dev) {
+            // the greedy token is the device argmax: the step takes it from the device (no host-to-device copy, no
+            // second argmax launch -- the bench's decode_greedy loop, koboldcpp --benchmark's settings hit this)
+            HipOps o(*e);
+            frc = (!e->dev_tok && o.token_home()) ? -1 : greedy_step(o, (int)e->ctx.size());
+            e->dev_tok = frc == 0;
+        } else {
+            frc = forward(*e, &tt, 1, (int)e->ctx.size());
+            e->dev_tok = frc == 0 && e->stages.size() == 1;     // one stage: its argmax also wrote the token input
+        }
+        if (frc) { fprintf(stderr, "[kcpp] generate: decode failed\n"); break; }
         e->ctx.push_back(t);
     }
     while (!delayed.empty()) {               // flush what the delay line still holds (:3497-3505)

@@ -1343,6 +1343,16 @@ extern "C" int kcpp_model_step_dev(kcpp_model *m, int n_past) {
 extern "C" int32_t *kcpp_model_token_dev(kcpp_model *m) { return m->tok_dev; }
 extern "C" int32_t *kcpp_model_argmax_dev(kcpp_model *m) { return m->argmax_dev; }
 
+// the token the last single-token step's own argmax left in argmax_dev (decode_step_dev ends every step with it): a
+// 4-byte read, no kernel launch
+extern "C" int kcpp_model_read_argmax(kcpp_model *m, int32_t *token_out) {
+    if (!m->has_output) return -1;
+    RT_CHECK(hipSetDevice(m->device));
+    RT_CHECK(hipMemcpyAsync(&m->pin[2], m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    *token_out = m->pin[2];
+    return 0;
+}
 extern "C" int kcpp_model_argmax(kcpp_model *m, int32_t *token_out) {
     if (!m->has_output) return -1;
     RT_CHECK(hipSetDevice(m->device));
