@@ -176,10 +176,22 @@ def generate_path(hp, types, n_prompt, n_gen, ubatch, seed=1234):
             raise RuntimeError("kcpp_expose_synth_weights failed")
 
         def gen(prompt, n):
+            # the request koboldcpp.py's generate() builds for its --benchmark call (koboldcpp.py:870-1000): the
+            # benchmark's temperature 0.1 / top_k 1 / rep_pen 1 / ban_eos_token, every other field at its default
             gi = X.generation_inputs()
             gi.prompt, gi.memory = prompt, b""
             gi.max_context_length, gi.max_length = max_ctx, n
-            gi.temperature, gi.top_k, gi.rep_pen, gi.bypass_eos_token, gi.seed = 0.1, 1, 1.0, True, 7
+            gi.temperature, gi.top_k, gi.rep_pen, gi.seed = 0.1, 1, 1.0, 7
+            gi.top_a, gi.top_p, gi.min_p, gi.typical_p, gi.tfs = 0.0, 0.92, 0.0, 1.0, 1.0
+            gi.rep_pen_range, gi.rep_pen_slope, gi.presence_penalty = 320, 1.0, 0.0
+            gi.mirostat, gi.mirostat_tau, gi.mirostat_eta = 0, 5.0, 0.1
+            gi.dry_multiplier, gi.dry_base, gi.dry_allowed_length, gi.dry_penalty_last_n = 0.0, 1.75, 2, 320
+            gi.xtc_threshold, gi.xtc_probability = 0.2, 0.0
+            gi.dynatemp_range, gi.dynatemp_exponent, gi.smoothing_factor = 0.0, 1.0, 0.0
+            for i, v in enumerate([6, 0, 1, 3, 4, 2, 5]):
+                gi.sampler_order[i] = v
+            gi.sampler_len = 7
+            gi.allow_eos_token, gi.bypass_eos_token = False, False      # ban_eos_token = True
             out = h.generate(gi)
             if out.status != 1:
                 raise RuntimeError("generate failed")
@@ -191,8 +203,10 @@ def generate_path(hp, types, n_prompt, n_gen, ubatch, seed=1234):
     return {"decode_tok_s": round(1000.0 / et, 2), "prefill_tok_s": round(1000.0 / pt, 1), "gen_tokens": n,
             "max_context_length": max_ctx,
             "how": "koboldcpp --benchmark semantics through the C ABI: load_model (sparse full-size GGUF, synthetic "
-                   "weights) + one generate() (temperature 0.1, top_k 1, rep_pen 1, EOS banned; host sampling per "
-                   "token); speeds = 1000 / get_last_eval_time and 1000 / get_last_process_time (ms per token)"}
+                   "weights) + one generate() with the request koboldcpp.py builds (temperature 0.1, top_k 1, rep_pen 1, "
+                   "EOS banned, other samplers at their defaults: the chain reduces to the argmax, so each step's own "
+                   "device argmax is read back; the token returns to the host every step); speeds = 1000 / "
+                   "get_last_eval_time and 1000 / get_last_process_time (ms per token)"}
 
 
 def run_model(K, torch, hp, types, n_prompt, ubatch, steps, warmup):

@@ -865,11 +865,14 @@ generation_outputs generate(const generation_inputs in) {
         }
     };
     int n_gen = 0, stop = KCPP_STOP_OUT_OF_TOKENS;
+    double tm_sample = 0, tm_step = 0;     // host time in sample() / in the step's enqueue (KCPP_GEN_TIMING diagnostics)
     for (; n_gen < max_len; ++n_gen) {
         if (g_abort) { stop = KCPP_STOP_CUSTOM_STOPPER; break; }
         const auto sb = slop.find((int)e->ctx.size());
         bool on_dev = false;
+        const auto ts0 = std::chrono::steady_clock::now();
         const int t = sample(*e, S, last_n, rng, &g_mirostat_mu, sb == slop.end() ? nullptr : &sb->second, &on_dev);
+        tm_sample += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts0).count();
         if (t < 0) { fprintf(stderr, "[kcpp] generate: sampling failed: %s\n", kcpp_last_error()); break; }
         if (!last_n.empty()) last_n.erase(last_n.begin());     // (:3238: an antislop rewind may have emptied it)
         last_n.push_back(t);
@@ -930,6 +933,7 @@ generation_outputs generate(const generation_inputs in) {
         if ((int)e->ctx.size() >= e->hp.n_ctx - 1) { ++n_gen; break; }
         const int32_t tt = t;
         int frc;
+        const auto tf0 = std::chrono::steady_clock::now();
         if (on_dev) {
             // the greedy token is the device argmax: the step takes it from the device (no host-to-device copy, no
             // second argmax launch -- the bench's decode_greedy loop, koboldcpp --benchmark's settings hit this)
@@ -940,9 +944,13 @@ generation_outputs generate(const generation_inputs in) {
             frc = forward(*e, &tt, 1, (int)e->ctx.size());
             e->dev_tok = frc == 0 && e->stages.size() == 1;     // one stage: its argmax also wrote the token input
         }
+        tm_step += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tf0).count();
         if (frc) { fprintf(stderr, "[kcpp] generate: decode failed\n"); break; }
         e->ctx.push_back(t);
     }
+    if (getenv("KCPP_GEN_TIMING"))
+        fprintf(stderr, "[kcpp] generate timing: %d tokens, sample %.3f ms/token, step enqueue %.3f ms/token\n", n_gen,
+                tm_sample / std::max(1, n_gen), tm_step / std::max(1, n_gen));
     while (!delayed.empty()) {               // flush what the delay line still holds (:3497-3505)
         if (!hit) emit(delayed.front());
         delayed.pop_front();
