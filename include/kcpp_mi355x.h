@@ -96,6 +96,18 @@ int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t
 /* rms_norm * w quantized to Q8_0 in the same pass (= kcpp_rms_norm then kcpp_quantize_act(Q8_0), bit for bit) */
 int kcpp_rms_norm_q80(const float *x, int64_t ldx, const float *w, void *q80_out, int64_t ne0, int64_t nrows, float eps,
                       void *stream);
+/* the same quantized into the KT_Q8_0_TA activation layout of KT_Q8_0_T weights (kcpp_common.h) */
+int kcpp_rms_norm_q80t(const float *x, int64_t ldx, const float *w, void *q80t_out, int64_t ne0, int64_t nrows, float eps,
+                       void *stream);
+/* mat-mul of KT_Q8_0_T weights (Q8_0 in 32-row tile fragments, kcpp_common.h) with a KT_Q8_0_TA activation of M tokens
+ * (any M; replaces ggml_cuda_op_mul_mat's MMQ / MMVQ for Q8_0, ggml-cuda.cu:1882-1947): mode 0, up to 3 weight segments
+ * [K][Ns[i]] whose rows sit back to back in Y's columns, Y (+ res); mode 1 (one segment, W2 = up): h = silu(W act) *
+ * (W2 act) as f32 into Y, or, with qout, quantized to the KT_Q8_0_TA activation of h (K = Ns[0]).  ws:
+ * kcpp_gemm_workspace_bytes(KT_Q8_0_T, K, sum Ns, M) bytes, zero before its first use (split-K tickets). */
+int64_t kcpp_q80t_ws_bytes(int64_t K, int64_t N, int64_t M);
+int kcpp_gemm_q80t(const void *const *Ws, const int64_t *Ns, int nseg, const void *W2, int64_t K, const void *act,
+                   int64_t M, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *qout, void *ws,
+                   void *stream);
 /* host-side table of (cos, sin) per [pos][D/2], exactly as ggml_rope_cache_init (ggml.c:14246) */
 int kcpp_rope_table(float *tab_host, int n_pos, int n_dims, float freq_base, float freq_scale, const float *freq_factors,
                     float ext_factor, float attn_factor, float beta_fast, float beta_slow, int n_ctx_orig);

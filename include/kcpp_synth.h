@@ -34,7 +34,10 @@ enum kcpp_type {
     /* GPU-internal row-major decode layouts of Q4_K / Q5_K / Q6_K (same bytes per row, re-arranged inside
        each row so the single-token mat-vec reads 1 KiB-contiguous wave loads; csrc/kcpp_common.h).
        Not ggml ids: they never leave the device library. */
-    KT_Q4_K_RS = 112, KT_Q5_K_RS = 113, KT_Q6_K_RS = 114
+    KT_Q4_K_RS = 112, KT_Q5_K_RS = 113, KT_Q6_K_RS = 114,
+    /* GPU-internal tile layout of Q8_0 (32-row tiles, each block's 32 rows x 32 B one contiguous 1 KiB MFMA operand,
+       csrc/gemm_q80t.hip) and its activation layout (32-token groups in the same fragment order) */
+    KT_Q8_0_T = 115, KT_Q8_0_TA = 116
 };
 
 /* the lattice-grid types (IQ1 / IQ2 / IQ3): ggml layout on the device, decoded through the code books */
@@ -45,7 +48,8 @@ KS_FN int is_iq_grid_type(int t) {
 
 /* the ggml type whose blocks a layout holds */
 KS_FN int ks_base_type(int type) {
-    return type == KT_Q4_K_RS ? KT_Q4_K : (type == KT_Q5_K_RS ? KT_Q5_K : (type == KT_Q6_K_RS ? KT_Q6_K : type));
+    return type == KT_Q4_K_RS ? KT_Q4_K : (type == KT_Q5_K_RS ? KT_Q5_K : (type == KT_Q6_K_RS ? KT_Q6_K :
+           (type == KT_Q8_0_T ? KT_Q8_0 : type)));
 }
 
 KS_FN uint64_t ks_mix(uint64_t z) {          /* splitmix64 finalizer */
@@ -86,7 +90,7 @@ KS_FN float ks_unit(uint64_t h) {            /* [0,1) */
 KS_FN int ks_block_elems(int type) {
     switch (type) {
         case KT_F32: case KT_F16: return 1;
-        case KT_Q4_0: case KT_Q4_1: case KT_Q5_0: case KT_Q5_1: case KT_Q8_0: case KT_Q8_1: case KT_IQ4_NL: return 32;
+        case KT_Q4_0: case KT_Q4_1: case KT_Q5_0: case KT_Q5_1: case KT_Q8_0: case KT_Q8_1: case KT_IQ4_NL: case KT_Q8_0_T: return 32;
         default: return 256;
     }
 }
@@ -100,7 +104,7 @@ KS_FN int ks_block_bytes(int type) {
         case KT_Q5_0: return 22;
         case KT_Q5_1: return 24;
         case KT_Q8_1: return 36;
-        case KT_Q8_0: return 34;
+        case KT_Q8_0: case KT_Q8_0_T: return 34;
         case KT_Q2_K: return 84;
         case KT_Q3_K: return 110;
         case KT_Q4_K: case KT_Q4_K_RS: return 144;

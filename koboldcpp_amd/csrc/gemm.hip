@@ -1873,6 +1873,7 @@ int kcpp_gemm_q80_segs(const void *const *W, const int64_t *N, int nseg, int64_t
 }
 
 int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M) {
+    if (type == KT_Q8_0_T) return kcpp_q80t_ws_bytes(K, N, M);
     int64_t a, b, c, d;
     return ws_layout(type, K, N, M, a, b, c, d);
 }
@@ -1888,6 +1889,11 @@ int kcpp_gemm_q80_glu_q80(const void *W, const void *W2, int64_t K, int64_t N, c
 
 int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream) {
+    if (type == KT_Q8_0_T) {          // the tile layout (gemm_q80t.hip): every M, activation KT_Q8_0_TA
+        const void *Ws[1] = {W};
+        const int64_t Ns[1] = {N};
+        return kcpp_gemm_q80t(Ws, Ns, 1, W2, K, act, M, Y, ldy, res, ldr, mode, nullptr, ws, stream);
+    }
     hipStream_t s = (hipStream_t)stream;
     if (K % GB_K) return -1;
     if (!ws) return -2;

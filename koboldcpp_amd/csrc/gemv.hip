@@ -172,6 +172,7 @@ extern "C" {
 // mode 0: plain (+res), mode 1: GLU silu(W.x)*(W2.x)
 int kcpp_gemv(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *stream) {
+    if (type == KT_Q8_0_T) return -3;            // the tile layout runs through kcpp_gemm at every M (its workspace)
     return gemv_cols(type, W, W2, K, N, act, M, M, 0, Y, ldy, res, ldr, mode, stream);
 }
 

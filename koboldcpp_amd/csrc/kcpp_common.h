@@ -84,6 +84,10 @@ __device__ __forceinline__ int nearest_int_mul(float a, float b) {
 //   Q6_K : [nb][192] ql|qh  ++ [nb][16] scales ++ [nb] fp16 d
 //   Q4_0 : [nb][16] qs ++ [nb] fp16 d
 //   Q8_0 : [nb][32] qs ++ [nb] fp16 d
+//   Q8_0_T (KT_Q8_0_T, N % 32 == 0, K % 128 == 0): 32-row tiles; tile t, block b (nb = K / 32 blocks per row):
+//          qs at (t nb + b) * 1024: [half h][row r][16 B] = row 32 t + r, bytes 32 b + 16 h .. + 15  (the B operand of
+//          v_mfma_i32_32x32x32_i8 for lane 32 h + r, one contiguous 1 KiB wave load), then the d plane at N K:
+//          (t nb / 4 + b / 4) * 256 + r * 8 + (b % 4) * 2  (f16: four blocks of a row in one 8-B lane load)
 __host__ __device__ inline int64_t kl_nblocks(int type, int64_t K, int64_t N) {
     return K / ks_block_elems(type) * N;
 }
@@ -99,7 +103,11 @@ struct ActView {
     const float *s;
     int64_t K;
 };
+//   Q8_0_TA act (KT_Q8_0_T's vec_dot_type): the Q8_0 quantization of 32-token groups, G = ceil(M / 32):
+//          qs int8 [G][K / 32 blocks][half h][32 tokens][16 B] (the A operand of the MFMA, 1 KiB per block) ++
+//          d f32 [G][K / 32][32 tokens]; tokens past M are never read back
 __host__ __device__ inline int64_t act_bytes(int vtype, int64_t K, int64_t M) {
+    if (vtype == KT_Q8_0_TA) return (M + 31) / 32 * 32 * (K + K / 32 * 4);
     if (vtype == KT_Q8_K) return M * K + M * (K / 256) * 4 + M * (K / 16) * 2;
     if (vtype == KT_Q8_1) return M * K + M * (K / 32) * 4 + ((M * (K / 32) * 2 + 3) & ~(int64_t)3) + M * (K / 32) * 4;
     return M * K + M * (K / 32) * 4 + M * (K / 32) * 2;
@@ -123,6 +131,7 @@ __host__ __device__ inline ActView act_view(int vtype, const void *buf, int64_t 
 }
 inline int vec_dot_type(int wtype) {
     if (wtype == KT_Q4_1 || wtype == KT_Q5_1) return KT_Q8_1;
+    if (wtype == KT_Q8_0_T) return KT_Q8_0_TA;
     return (wtype == KT_Q4_0 || wtype == KT_Q5_0 || wtype == KT_Q8_0 || wtype == KT_IQ4_NL) ? KT_Q8_0 : KT_Q8_K;
 }
 

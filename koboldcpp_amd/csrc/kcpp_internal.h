@@ -83,3 +83,4 @@ extern "C" int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t 
 extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
 extern "C" int kcpp_rs_supported(int type, int64_t K);
 
+

@@ -74,10 +74,19 @@ __global__ void __launch_bounds__(1024) k_rms_norm(const float *__restrict__ x, 
             sq += qv[e];
         }
         sq += __shfl_xor(sq, 1, 64);
-        int *qs = (int *)((int8_t *)qout + r * ne0 + e0);
+        int pk[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            qs[k] = (qv[4 * k] & 0xFF) | ((qv[4 * k + 1] & 0xFF) << 8) | ((qv[4 * k + 2] & 0xFF) << 16) | ((qv[4 * k + 3] & 0xFF) << 24);
+            pk[k] = (qv[4 * k] & 0xFF) | ((qv[4 * k + 1] & 0xFF) << 8) | ((qv[4 * k + 2] & 0xFF) << 16) | ((qv[4 * k + 3] & 0xFF) << 24);
+        if (q80 == 2) {      // the tile layout's activation (KT_Q8_0_TA, kcpp_common.h): 32-token groups, fragment order
+            const int64_t g = r >> 5, tok = r & 31, ng = (nrows + 31) / 32;
+            *(int4 *)((int8_t *)qout + (g * nb + ib) * 1024 + (tid & 1) * 512 + tok * 16) = make_int4(pk[0], pk[1], pk[2], pk[3]);
+            if ((tid & 1) == 0) ((float *)(qout + ng * 32 * ne0))[(g * nb + ib) * 32 + tok] = h2f(f2h(dd));
+            return;
+        }
+        int *qs = (int *)((int8_t *)qout + r * ne0 + e0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) qs[k] = pk[k];
         if ((tid & 1) == 0) {
             ((float *)(qout + nrows * ne0))[r * nb + ib] = h2f(f2h(dd));   // the dot uses GGML_FP16_TO_FP32(y.d)
             ((int16_t *)(qout + nrows * ne0 + nrows * nb * 4))[r * nb + ib] = (int16_t)sq;
@@ -177,6 +186,17 @@ int kcpp_rms_norm_q80(const float *x, int64_t ldx, const float *w, void *q80_out
     const unsigned nthr = (unsigned)(ne0 / 16 < 64 ? 64 : ne0 / 16);
     hipLaunchKernelGGL(k_rms_norm, dim3((unsigned)nrows), dim3(nthr), 0, (hipStream_t)stream, x, ldx, w, (float *)nullptr,
                        (int64_t)0, (uint8_t *)q80_out, ne0, nrows, eps, 1);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// rms_norm * w -> the KT_Q8_0_TA activation of KT_Q8_0_T weights (same values as kcpp_rms_norm_q80)
+int kcpp_rms_norm_q80t(const float *x, int64_t ldx, const float *w, void *q80t_out, int64_t ne0, int64_t nrows, float eps,
+                       void *stream) {
+    if (ne0 % 256 || ne0 > 16384 || !q80t_out) return -1;
+    const unsigned nthr = (unsigned)(ne0 / 16 < 64 ? 64 : ne0 / 16);
+    hipLaunchKernelGGL(k_rms_norm, dim3((unsigned)nrows), dim3(nthr), 0, (hipStream_t)stream, x, ldx, w, (float *)nullptr,
+                       (int64_t)0, (uint8_t *)q80t_out, ne0, nrows, eps, 2);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

@@ -68,6 +68,14 @@ __device__ __forceinline__ void kl_store_block(int type, const uint8_t *src, uin
         d[0] = src[0]; d[1] = src[1];
         for (int i = 0; i < 32; ++i) q[i] = src[2 + i];
     } break;
+    case KT_Q8_0_T: {   // kcpp_common.h: 32-row tiles of [half][row][16 B] per block, d plane in groups of 4 blocks
+        const int64_t n = b / bpr, blk = b % bpr, t = n >> 5, r = n & 31;
+        uint8_t *q = dst + (t * bpr + blk) * 1024 + r * 16;
+        for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < 16; ++i) q[512 * h + i] = src[2 + 16 * h + i];
+        uint8_t *d = dst + nb * 32 + (t * (bpr / 4) + blk / 4) * 256 + r * 8 + (blk % 4) * 2;
+        d[0] = src[0]; d[1] = src[1];
+    } break;
     case KT_Q4_K_RS: {
         const int64_t n = b / bpr, sb = b % bpr;
         uint8_t *row = dst + n * 144 * bpr;
@@ -159,6 +167,14 @@ __device__ __forceinline__ void kl_load_block(int type, const uint8_t *src, uint
         const uint8_t *q = src + b * 32, *d = src + nb * 32 + b * 2;
         blk[0] = d[0]; blk[1] = d[1];
         for (int i = 0; i < 32; ++i) blk[2 + i] = q[i];
+    } break;
+    case KT_Q8_0_T: {
+        const int64_t n = b / bpr, bi = b % bpr, t = n >> 5, r = n & 31;
+        const uint8_t *q = src + (t * bpr + bi) * 1024 + r * 16;
+        for (int h = 0; h < 2; ++h)
+            for (int i = 0; i < 16; ++i) blk[2 + 16 * h + i] = q[512 * h + i];
+        const uint8_t *d = src + nb * 32 + (t * (bpr / 4) + bi / 4) * 256 + r * 8 + (bi % 4) * 2;
+        blk[0] = d[0]; blk[1] = d[1];
     } break;
     case KT_Q4_K_RS: {
         const int64_t n = b / bpr, sb = b % bpr;
@@ -430,7 +446,7 @@ __device__ __forceinline__ float deq_elem(int type, const uint8_t *src, int64_t 
         if (five) q += ((blk[16 + l] >> (2 * c + hi)) & 1) << 4;
         return __fsub_rn(__fmul_rn(d * sc, (float)q), mn * m);
     }
-    case KT_Q4_K_RS: case KT_Q5_K_RS: case KT_Q6_K_RS: return 0.0f;      // row gathers of decode layouts are not used
+    case KT_Q4_K_RS: case KT_Q5_K_RS: case KT_Q6_K_RS: case KT_Q8_0_T: return 0.0f;   // row gathers of decode layouts: unused
     case KT_Q2_K: {
         const float d = h2f(*(const uint16_t *)(src + nb * 80 + b * 4)), mn = h2f(*(const uint16_t *)(src + nb * 80 + b * 4 + 2));
         const int n = e >> 7, j = (e >> 5) & 3, l = e & 31;
@@ -507,7 +523,8 @@ __global__ void __launch_bounds__(256) k_quant_q8k(const float *__restrict__ x, 
 
 // Q8_0 (AVX2 semantics): 8 lanes per 32-block, 4 elements per lane.
 // S1: Q8_1 (quantize_row_q8_1's AVX2 branch, ggml-quants.c:1280-1330): the same qs / d plus s = f16(d * sum qs)
-template <bool S1>
+// TA: the KT_Q8_0_TA layout of the same values (the activation of KT_Q8_0_T weights)
+template <bool S1, bool TA = false>
 __global__ void k_quant_q80(const float *__restrict__ x, int64_t ldx, uint8_t *__restrict__ out, int64_t K, int64_t M) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t nb = K / 32;
@@ -535,6 +552,13 @@ __global__ void k_quant_q80(const float *__restrict__ x, int64_t ldx, uint8_t *_
     s += __shfl_xor(s, 2, 64);
     s += __shfl_xor(s, 4, 64);
     if (!valid) return;
+    if (TA) {          // KT_Q8_0_TA (kcpp_common.h): lane sub holds bytes 4 sub .. + 3 of the block = half sub / 4
+        const int64_t g = m >> 5, tok = m & 31, ng = (M + 31) / 32;
+        const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
+        *(int *)((int8_t *)out + (g * nb + ib) * 1024 + (sub >> 2) * 512 + tok * 16 + 4 * (sub & 3)) = packed;
+        if (sub == 0) ((float *)(out + ng * 32 * K))[(g * nb + ib) * 32 + tok] = h2f(f2h(d));
+        return;
+    }
     const int packed = (q[0] & 0xFF) | ((q[1] & 0xFF) << 8) | ((q[2] & 0xFF) << 16) | ((q[3] & 0xFF) << 24);
     ((int *)((int8_t *)out + m * K + ib * 32))[sub] = packed;
     if (sub == 0) {
@@ -606,6 +630,11 @@ int kcpp_quantize_act(int vtype, const float *x, int64_t ldx, void *out, int64_t
         const int64_t nthreads = K / 32 * M * 8;
         hipLaunchKernelGGL(k_quant_q80<false>, dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x,
                            ldx, (uint8_t *)out, K, M);
+    } else if (vtype == KT_Q8_0_TA) {
+        if (K % 32) return -1;
+        const int64_t nthreads = K / 32 * M * 8;
+        hipLaunchKernelGGL((k_quant_q80<false, true>), dim3((unsigned)((nthreads + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, x, ldx, (uint8_t *)out, K, M);
     } else if (vtype == KT_Q8_1) {
         if (K % 32) return -1;
         const int64_t nthreads = K / 32 * M * 8;
@@ -629,7 +658,7 @@ int kcpp_quantize_act_glu(const float *x, int64_t ldx, int64_t uoff, void *out, 
 
 int kcpp_get_rows(int type, const void *w, int64_t K, int64_t N, const int32_t *ids, int64_t T, float *y, int64_t ldy,
                   void *stream) {
-    if (type == KT_Q4_K_RS || type == KT_Q5_K_RS || type == KT_Q6_K_RS) return -2;
+    if (type == KT_Q4_K_RS || type == KT_Q5_K_RS || type == KT_Q6_K_RS || type == KT_Q8_0_T) return -2;
     switch (type) {
 #define KCPP_IQ_ROWS(TT)                                                                                            \
     case TT:                                                                                                        \

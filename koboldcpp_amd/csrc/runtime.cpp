@@ -129,6 +129,7 @@ struct kcpp_model {
     bool use_graphs = true;
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
     bool q81 = false;                // Q4_1 / Q5_1 weights (Q8_1 activations): decode on the per-op path
+    bool q80t = false;               // Q8_0 layer weights in the tile layout KT_Q8_0_T (gemm_q80t.hip) at every batch size
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
     int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
     hipGraphExec_t g_exec = nullptr;
@@ -299,6 +300,26 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
             t = t == KT_Q4_K ? KT_Q4_K_RS : (t == KT_Q5_K ? KT_Q5_K_RS : KT_Q6_K_RS);
         m->types[idx] = t;
     }
+    // an all-Q8_0 dense model (BASELINE config 3) holds its layer matrices (and a Q8_0 output head) in the tile layout
+    // KT_Q8_0_T: one int8 MFMA kernel at every batch size, 1 KiB-contiguous weight fragments (gemm_q80t.hip)
+    if (hp->n_expert == 0 && hp->n_layer > 0) {
+        bool all = true;
+        for (int il = 0; il < hp->n_layer && all; ++il)
+            for (int j : {1, 2, 3, 4, 6, 7, 8}) {
+                const int idx = 3 + per_layer(*hp) * il + j;
+                int64_t K, N;
+                shape_of(*hp, idx, K, N);
+                all = all && m->types[idx] == KT_Q8_0 && K % 128 == 0 && N % 32 == 0;
+            }
+        if (all) {
+            for (int il = 0; il < hp->n_layer; ++il)
+                for (int j : {1, 2, 3, 4, 6, 7, 8}) m->types[3 + per_layer(*hp) * il + j] = KT_Q8_0_T;
+            int64_t K, N;
+            shape_of(*hp, 2, K, N);
+            if (m->types[2] == KT_Q8_0 && K % 128 == 0 && N % 32 == 0) m->types[2] = KT_Q8_0_T;
+            m->q80t = true;
+        }
+    }
     types = m->types.data();
     for (int idx = 0; idx < n_tensors(*hp); ++idx)
         m->q81 |= types[idx] == KT_Q4_1 || types[idx] == KT_Q5_1;
@@ -357,7 +378,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     }
     // activation buffers sized for the widest vec_dot input (K = F) at UB columns
     m->act_sz = (size_t)std::max({kcpp_act_bytes(KT_Q4_K, std::max(E, F), UB), kcpp_act_bytes(KT_Q8_0, std::max(E, F), UB),
-                                  kcpp_act_bytes(KT_Q4_1, std::max(E, F), UB)});
+                                  kcpp_act_bytes(KT_Q4_1, std::max(E, F), UB), kcpp_act_bytes(KT_Q8_0_T, std::max(E, F), UB)});
     m->gemm_ws_sz = 0;
     for (int idx = 0; idx < n_tensors(*hp); ++idx) {
         int64_t K, N; shape_of(*hp, idx, K, N);
@@ -379,6 +400,8 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
               hipHostMalloc((void **)&m->pin, 64, hipHostMallocDefault) == hipSuccess &&
               (m->gemm_ws_sz == 0 || hipMalloc(&m->gemm_ws, m->gemm_ws_sz) == hipSuccess);
     if (!ok) return fail("workspace alloc");
+    // the KT_Q8_0_T GEMM's split-K tickets live in the workspace and must start at zero (each launch leaves them zero)
+    if (m->gemm_ws && hipMemset(m->gemm_ws, 0, m->gemm_ws_sz) != hipSuccess) return fail("gemm ws memset");
     if (hp->n_expert > 0) {
         const int NU = hp->n_expert_used;
         if (NU < 1 || NU > hp->n_expert || hp->n_expert > 64) return fail("bad n_expert / n_expert_used");
@@ -639,7 +662,10 @@ extern "C" int kcpp_model_set_row_split(kcpp_model *m, int n, const int *devices
         RT_CHECK(hipEventCreateWithFlags(&ln.done, hipEventDisableTiming));
         RT_CHECK(hipMalloc(&ln.act, m->act_sz));
         RT_CHECK(hipMalloc((void **)&ln.y, std::max<size_t>(ymax, 1) * 4));
-        if (m->gemm_ws_sz) RT_CHECK(hipMalloc(&ln.ws, m->gemm_ws_sz));
+        if (m->gemm_ws_sz) {
+            RT_CHECK(hipMalloc(&ln.ws, m->gemm_ws_sz));
+            RT_CHECK(hipMemset(ln.ws, 0, m->gemm_ws_sz));        // KT_Q8_0_T tickets
+        }
         if (ln.dev != m->device) {             // direct xGMI copies both ways
             (void)hipDeviceEnablePeerAccess(m->device, 0);
             RT_CHECK(hipSetDevice(m->device));
@@ -720,7 +746,7 @@ extern "C" int kcpp_model_set_fused_decode(kcpp_model *m, int enable) {
 
 static int mm_launch(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
                      int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, hipStream_t s) {
-    if (M <= 8) return kcpp_gemv(type, W, W2, K, N, act, M, Y, ldy, res, ldr, mode, s);
+    if (M <= 8 && type != KT_Q8_0_T) return kcpp_gemv(type, W, W2, K, N, act, M, Y, ldy, res, ldr, mode, s);
     return kcpp_gemm(type, W, W2, K, N, act, M, Y, ldy, res, ldr, mode, ws, s);
 }
 
@@ -772,7 +798,7 @@ static int matmul_rows(kcpp_model *m, const KTensor &W, const KTensor *W2, const
 static int matmul(kcpp_model *m, const KTensor &W, const KTensor *W2, const void *act, int64_t M, float *Y, int64_t ldy,
                   const float *res, int64_t ldr, int mode) {
     if (!W.rs.empty()) return matmul_rows(m, W, W2, act, M, Y, ldy, res, ldr, mode);
-    if (M <= 8)
+    if (M <= 8 && W.type != KT_Q8_0_T)
         return kcpp_gemv(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, m->stream);
     return kcpp_gemm(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, m->gemm_ws, m->stream);
 }
@@ -1092,6 +1118,16 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
                 RC(matmul(m, t[2], nullptr, m->act, T, m->qkv + E, LQ, nullptr, 0, 0));
                 RC(matmul(m, t[3], nullptr, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0));
             }
+        } else if (m->q80t) {                        // Q8_0 tile layout: norm + TA quantization, one q|k|v launch
+            RC(kcpp_rms_norm_q80t(m->x, E, (const float *)t[0].d, m->act, E, T, hp.eps, s));
+            if (m->lanes.empty()) {
+                const void *Wq[3] = {t[1].d, t[2].d, t[3].d};
+                const int64_t Nq[3] = {E, EKV, EKV};
+                RC(kcpp_gemm_q80t(Wq, Nq, 3, nullptr, E, m->act, T, m->qkv, LQ, nullptr, 0, 0, nullptr, m->gemm_ws, s));
+            } else {
+                for (int j = 1; j <= 3; ++j)
+                    RC(matmul(m, t[j], nullptr, m->act, T, m->qkv + (j == 1 ? 0 : (j == 2 ? E : E + EKV)), LQ, nullptr, 0, 0));
+            }
         } else if (T > 8 && T <= 32 && m->lanes.empty() && t[1].type == KT_Q8_0 && t[2].type == KT_Q8_0 && t[3].type == KT_Q8_0 && E % 128 == 0 &&
                    EKV % 128 == 0) {                 // small-batch Q8_0: one quantization, one q|k|v launch
             RC(kcpp_rms_norm_q80(m->x, E, (const float *)t[0].d, m->act, E, T, hp.eps, s));
@@ -1125,6 +1161,19 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
         if (!(woq && T <= 16)) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, T, s));
         RC(matmul(m, t[4], nullptr, m->act, T, m->x, E, m->x, E, 0));                    // x += wo . attn
         if (hp.n_expert > 0) { RC(T == 1 ? moe_dec(m, L) : moe_prefill(m, L, T)); continue; }   // T == 1: no host sync (graphs)
+        if (m->q80t) {
+            // ffn_norm -> TA quantization; gate|up with silu(g) u quantized to the TA activation of down in the GEMM's
+            // epilogue (one launch); down with the residual
+            RC(kcpp_rms_norm_q80t(m->x, E, (const float *)t[5].d, m->act, E, T, hp.eps, s));
+            if (m->lanes.empty()) {
+                RC(kcpp_gemm_q80t(&t[6].d, &F, 1, t[7].d, E, m->act, T, nullptr, 0, nullptr, 0, 1, m->act2, m->gemm_ws, s));
+            } else {
+                RC(matmul(m, t[6], &t[7], m->act, T, m->h, F, nullptr, 0, 1));          // h = silu(g) * u
+                RC(kcpp_quantize_act(KT_Q8_0_TA, m->h, F, m->act2, F, T, s));
+            }
+            RC(matmul(m, t[8], nullptr, m->act2, T, m->x, E, m->x, E, 0));               // x += down . h
+            continue;
+        }
         const bool gq = kcpp_vec_dot_type(t[6].type) == KT_Q8_K && kcpp_vec_dot_type(t[7].type) == KT_Q8_K;
         if (gq) {
             RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, nullptr, E, m->act, E, T, hp.eps, s));
@@ -1177,7 +1226,7 @@ static int decode_step_dev(kcpp_model *m) {
     if (m->has_embed)
         RC(kcpp_get_rows(m->tok_embd.type, m->tok_embd.d, hp.n_embd, hp.n_vocab, m->tok_dev, 1, m->x, hp.n_embd,
                          m->stream));
-    if (m->fused_decode && m->kv_tk == KT_F16 && !m->q81) {
+    if (m->fused_decode && m->kv_tk == KT_F16 && !m->q81 && !m->q80t) {
         RC(forward_layers_dec(m));
         if (m->has_output) RC(head_dec(m));
     } else {

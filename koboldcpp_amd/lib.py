@@ -14,9 +14,11 @@ F32, F16, Q4_0, Q4_1, Q5_0, Q5_1, Q8_0, Q8_1, Q2_K, Q3_K, Q4_K, Q5_K, Q6_K, Q8_K
 IQ4_NL, IQ4_XS = 20, 23
 # device-internal row-major decode layouts of Q4_K / Q6_K (include/kcpp_synth.h; never ggml ids)
 Q4_K_RS, Q5_K_RS, Q6_K_RS = 112, 113, 114
+# device-internal Q8_0 tile layout and its activation layout (kcpp_common.h, csrc/gemm_q80t.hip)
+Q8_0_T, Q8_0_TA = 115, 116
 BLOCK = {F32: (1, 4), F16: (1, 2), Q4_0: (32, 18), Q4_1: (32, 20), Q5_0: (32, 22), Q5_1: (32, 24), Q8_0: (32, 34), Q8_1: (32, 36), Q2_K: (256, 84), Q3_K: (256, 110), Q4_K: (256, 144),
          Q5_K: (256, 176), Q6_K: (256, 210), Q8_K: (256, 292), Q4_K_RS: (256, 144), Q5_K_RS: (256, 176), Q6_K_RS: (256, 210),
-         IQ4_NL: (32, 18), IQ4_XS: (256, 136)}
+         IQ4_NL: (32, 18), IQ4_XS: (256, 136), Q8_0_T: (32, 34)}
 # the lattice-grid types (ggml-common.h:340-405), kept in the ggml layout on the device (csrc/iq_grid.h)
 IQ2_XXS, IQ2_XS, IQ3_XXS, IQ1_S, IQ3_S, IQ2_S, IQ1_M = 16, 17, 18, 19, 21, 22, 29
 BLOCK.update({IQ2_XXS: (256, 66), IQ2_XS: (256, 74), IQ2_S: (256, 82), IQ3_XXS: (256, 98), IQ3_S: (256, 110),
@@ -62,6 +64,9 @@ _SIGS = {
     "kcpp_tokenizer_special_ids": [ctypes.c_char_p, P],
     "kcpp_engine_bench": [P, P, I, I, P, U64, I, I, I, I, P],
     "kcpp_expose_synth_weights": [U64],
+    "kcpp_gemm_q80t": [P, P, I, P, I64, P, I64, P, I64, P, I64, I, P, P, P],
+    "kcpp_rms_norm_q80t": [P, I64, P, P, I64, I64, Fl, P],
+    "kcpp_q80t_ws_bytes": [I64, I64, I64],
     "kcpp_pipeline_trace": [I, I, I, I, I, ctypes.c_char_p, I],
     "kcpp_split_layers": [I, I, P, P],
     "kcpp_model_argmax_async": [P],
@@ -116,7 +121,7 @@ _SIGS = {
     "kcpp_kv_store_q": [I, I, P, I64, I64, I64, I, I64, P, P, I64, I, P, P],
     "kcpp_flash_attn_q": [I, I, P, I64, P, P, P, I, I, I, I, I64, I, P, Fl, P],
 }
-_RES = {"kcpp_gradient_ai_rope_base": Fl, "kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
+_RES = {"kcpp_gradient_ai_rope_base": Fl, "kcpp_q80t_ws_bytes": I64, "kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
         "kcpp_model_create": P, "kcpp_model_hidden": P, "kcpp_model_stream": P, "kcpp_model_weight_bytes": I64,
         "kcpp_last_error": ctypes.c_char_p, "kcpp_model_free": None, "kcpp_fa_set_stamps": None}
 _L.kcpp_act_bytes.argtypes = [I, I64, I64]

@@ -61,6 +61,7 @@ def test_rowsplit_vs_reference_golden(K, golden_e2e, tag):
     (lambda n: R.q3_k_m_types(n), (0.25, 0.25, 0.5)),
     (lambda n: R.uniform_types(n, R.Q6_K, R.Q4_0), (2.0, 1.0)),
     (lambda n: R.uniform_types(n, R.Q5_K, R.Q8_0), (0.0, 0.0, 0.0, 0.0)),
+    (lambda n: R.uniform_types(n, R.Q8_0), (1.0, 1.0)),          # the Q8_0 tile layout (gemm_q80t.hip) sliced by rows
 ])
 def test_rowsplit_matches_whole_model(K, types_fn, split):
     """every device layout (row-major Q4_K/Q5_K, RS, SoA Q6_K/Q3_K/Q2_K, Q4_0/Q8_0 repacks) sliced by rows; a
