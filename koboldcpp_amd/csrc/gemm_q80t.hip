@@ -23,6 +23,13 @@
 
 #include <algorithm>
 
+#ifndef Q80T_FMA
+#define Q80T_FMA 1
+#endif
+#ifndef Q80T_GLU_WV
+#define Q80T_GLU_WV 4
+#endif
+
 namespace {
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -83,21 +90,17 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
     float *dxs = (float *)lds;                                       // token scales of the units [u0, u1): [block][32]
     float *red = dxs + (u1 - u0) * 128;                              // [WV][16][64] per-wave sums
     const int64_t ng = (a.M + 31) / 32;
-    {
-        const float4 *src = (const float4 *)(a.act + ng * 32 * K) + (z * nb + 4 * u0) * 8;
-        float4 *dst = (float4 *)dxs;
-        for (int64_t i = tid; i < (u1 - u0) * 32; i += 64 * WV) dst[i] = src[i];
-    }
-    __syncthreads();
     const uint8_t *wq = W + tl * nb * 1024 + lane * 16;              // block b at + b * 1024
     const uint8_t *wd = W + Ns * K + tl * nu * 256 + (lane & 31) * 8;   // unit u at + u * 256
     const uint8_t *aq = a.act + z * nb * 1024 + lane * 16;
+    // lanes of tokens past M read no activation (at M = 1 the wave fetches 32 B of it per block, not 1 KiB)
+    const bool xlive = z * 32 + (lane & 31) < a.M;
     struct Unit { i32x4 w[4], x[4]; uint2 d; };
     auto load = [&](int64_t u, Unit &U) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             U.w[i] = ld_frag_nt(wq + (4 * u + i) * 1024);
-            U.x[i] = *(const i32x4 *)(aq + (4 * u + i) * 1024);
+            U.x[i] = xlive ? *(const i32x4 *)(aq + (4 * u + i) * 1024) : i32x4{0, 0, 0, 0};
         }
         U.d = *(const uint2 *)(wd + u * 256);
     };
@@ -119,15 +122,27 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
                 const float4 d4 = *(const float4 *)(sd + 8 * c);
                 const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
+                for (int e = 0; e < 4; ++e) {
+#if Q80T_FMA
+                    tot[4 * c + e] = fmaf((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e]), tot[4 * c + e]);
+#else
                     tot[4 * c + e] = __fadd_rn(tot[4 * c + e], __fmul_rn((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e])));
+#endif
+                }
             }
         }
     };
     Unit ua, ub;
     if (wu0 < wu1) load(wu0, ua);
+    if (wu0 + 1 < wu1) load(wu0 + 1, ub);
+    {   // the token scales go to LDS while the first two units' fragments are in flight
+        const float4 *src = (const float4 *)(a.act + ng * 32 * K) + (z * nb + 4 * u0) * 8;
+        float4 *dst = (float4 *)dxs;
+        for (int64_t i = tid; i < (u1 - u0) * 32; i += 64 * WV) dst[i] = src[i];
+    }
+    __syncthreads();
     for (int64_t u = wu0; u < wu1; u += 2) {
-        if (u + 1 < wu1) load(u + 1, ub);
+        if (u > wu0 && u + 1 < wu1) load(u + 1, ub);
         comp(u, ua);
         if (u + 1 >= wu1) break;
         if (u + 2 < wu1) load(u + 2, ua);
@@ -216,8 +231,10 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
 
 // split / wave choice from the weight shape alone
 void q80t_shape(int mode, int64_t ntile, int64_t nu, int &S, int &WV) {
-    if (mode == 1) { S = 1; WV = 8; return; }
-    S = ntile < 256 && nu >= 16 ? 2 : 1;
+    if (mode == 1) { S = 1; WV = Q80T_GLU_WV; return; }
+    // tools/q80t_sweep.py (Llama-3-8B shapes, M = 1 and 32): q|k|v (192 tiles) S 1 x 8 waves 10.6 us vs 15.8 at S 2; wo /
+    // down (128 tiles) S 2 x 8 waves 9.0 / 16.9 us, the best of S 1-2 x 2-8 waves
+    S = ntile < 160 && nu >= 16 ? 2 : 1;
     WV = ntile * S >= 512 ? 4 : 8;
     while (WV > 1 && nu / S < WV) WV /= 2;
 }
@@ -266,7 +283,7 @@ int kcpp_gemm_q80t(const void *const *Ws, const int64_t *Ns, int nseg, const voi
     const int64_t nblk = (a.ntile + 7) / 8 * 8 * S * a.Z;
     hipStream_t s = (hipStream_t)stream;
 #define Q80T_L(MD, W_) hipLaunchKernelGGL((k_q80t<MD, W_>), dim3((unsigned)nblk), dim3(64 * W_), smem, s, a)
-    if (mode == 1) Q80T_L(1, 8);
+    if (mode == 1) Q80T_L(1, Q80T_GLU_WV);
     else if (WV == 8) Q80T_L(0, 8);
     else if (WV == 4) Q80T_L(0, 4);
     else if (WV == 2) Q80T_L(0, 2);
