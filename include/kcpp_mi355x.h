@@ -108,6 +108,13 @@ int64_t kcpp_q80t_ws_bytes(int64_t K, int64_t N, int64_t M);
 int kcpp_gemm_q80t(const void *const *Ws, const int64_t *Ns, int nseg, const void *W2, int64_t K, const void *act,
                    int64_t M, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *qout, void *ws,
                    void *stream);
+/* q|k|v (3 segments, Ns = {H D, HKV D, HKV D}) as kcpp_gemm_q80t mode 0 with kcpp_rope_kv fused into the epilogue
+ * (llama.cpp's ggml_rope_ext of Qcur/Kcur + the ggml_cpy of K/V into the cache, src/llama.cpp:9180-9202): rope(q) ->
+ * q16 [M][H D] f16, rope(k) and v -> kc / vc [pos][HKV D] f16 at pos_dev[t] (or n_past + t); bit-identical to the GEMM
+ * then kcpp_rope_kv. */
+int kcpp_gemm_q80t_qkv_rope(const void *const *Ws, const int64_t *Ns, int64_t K, const void *act, int64_t M,
+                            const void *rope_tab, int n_past, const int32_t *pos_dev, int head_dim, uint16_t *q16,
+                            uint16_t *kc, uint16_t *vc, void *ws, void *stream);
 /* host-side table of (cos, sin) per [pos][D/2], exactly as ggml_rope_cache_init (ggml.c:14246) */
 int kcpp_rope_table(float *tab_host, int n_pos, int n_dims, float freq_base, float freq_scale, const float *freq_factors,
                     float ext_factor, float attn_factor, float beta_fast, float beta_slow, int n_ctx_orig);
@@ -166,6 +173,12 @@ void kcpp_fa_set_stamps(void *p);
 /* the MFMA prefill kernel alone (koboldcpp_amd/csrc/attn_mfma.hip); -3 when the shape is not covered */
 int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, int T, int H,
                                  int HKV, int D, int n_past, float scale, void *stream);
+/* the same with, for T <= 64 and ws (kcpp_fa_workspace_bytes, zero before first use), the keys split over ~512
+ * workgroups merged in-launch by the last split; out (f32 [T][H D], may be NULL) and/or qta (the KT_Q8_0_TA
+ * activation of attn_output for KT_Q8_0_T weights, replacing kcpp_quantize_act; may be NULL).  -3 = not covered. */
+int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qta,
+                                    void *ws, int T, int H, int HKV, int D, int n_past, float scale, void *stream);
+int64_t kcpp_fa_split_ws_bytes(int H);
 /* MFMA prefill kernel generation: 2 (default; env KCPP_FA_MFMA_V) = next tile prefetched, V read through the
  * LDS transpose; 1 = the first version; 0 = the default.  Bit-identical outputs.  Returns the previous value. */
 int kcpp_fa_prefill_set_variant(int v);

@@ -574,7 +574,8 @@ int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max) {
     const int64_t nch = (n_kv_max + FA_CHUNK - 1) / FA_CHUNK;
     // partial slots: T x nch chunks (k_fa_decode), at least the 64 splits k_fa_dec4 may use
     const int64_t slots = std::max<int64_t>((int64_t)T * nch, 64);
-    return FA_WS_TICKETS + (int64_t)H * slots * (128 * 4 + 8) + (int64_t)T * H * 4 + 256;
+    return std::max<int64_t>(FA_WS_TICKETS + (int64_t)H * slots * (128 * 4 + 8) + (int64_t)T * H * 4 + 256,
+                             kcpp_fa_split_ws_bytes(H));      // the key-split prefill (attn_mfma.hip)
 }
 
 // out f32 [T][H][D] (may be null), qout Q8_K act [T][H*D] (may be null), ws from kcpp_fa_workspace_bytes

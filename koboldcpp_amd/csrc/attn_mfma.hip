@@ -18,6 +18,7 @@
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -310,11 +311,20 @@ __device__ __forceinline__ int fa_swz(int row, int c) { return row * 16 + (c ^ (
 // NW = 8: two waves per query head, wave w (head w & 3) takes key half hf = w >> 2 of every 64-key tile (2 waves per
 // SIMD so one's softmax runs under the other's MFMAs); the halves share each tile's maximum through LDS, so P and the
 // running max are v3's, and their (l, O) partial sums are added at the end (only the f32 summation order differs).
-template <int NW>
+//
+// SPL (short ubatches, BASELINE config 3's 32 tokens: (T / 16) x HKV workgroups alone leave most CUs idle): the grid
+// also splits the keys, ch tiles per workgroup; each split publishes its unnormalised (O, m, l) per query and head
+// (write-through stores, drained), takes a ticket per (query block, kv head), and the last arriver merges the nsp
+// splits in split order (deterministic whatever the arrival order) -- MI355X_MICROARCH.md hand-off table, row 1.
+// qta (optional): the output quantized straight to the KT_Q8_0_TA activation of attn_output (KT_Q8_0_T weights):
+// a head's 128 dims are 4 whole Q8_0 blocks, so no other workgroup's output is needed (k_quant_q80's rounding).
+template <int NW, bool SPL>
 __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t *__restrict__ q16,
                                                                 const uint16_t *__restrict__ kc,
                                                                 const uint16_t *__restrict__ vc, float *__restrict__ out,
-                                                                int T, int H, int HKV, int n_past, float scale) {
+                                                                int T, int H, int HKV, int n_past, float scale,
+                                                                float *__restrict__ part, unsigned *__restrict__ tick,
+                                                                int ch, int nsp_grid, uint8_t *__restrict__ qta) {
     constexpr int D = 128, G = 4, NST = 4;
     constexpr int NB = NW == 8 ? 2 : 4;               // 16-key blocks per wave and tile
     __shared__ __attribute__((aligned(16))) uint4 sk[NST][FM_K * 16];
@@ -326,7 +336,12 @@ __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t 
     // 1-D grid, XCD-aware: blocks b and b + 8 share an XCD, so kv head = b % 8 (+ 8 (b / 8 % (HKV / 8))) keeps every
     // query block of one head on one XCD -- its K/V (n_keys x 512 B) stays in that XCD's L2 instead of every XCD
     // streaming all heads from the Infinity Cache
-    const int bid = blockIdx.x;
+    int bid = blockIdx.x, sp = 0;
+    if constexpr (SPL) {
+        const int nb0 = (T + FM_Q - 1) / FM_Q * HKV;
+        sp = bid / nb0;
+        bid -= sp * nb0;                              // nb0 % 8 == 0 when HKV % 8 == 0: a head keeps its XCD
+    }
     int hk, qb;
     if (HKV % 8 == 0) {
         const int j = bid >> 3;
@@ -355,6 +370,12 @@ __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t 
     float m_run = -INFINITY, l_run = 0.0f;
     const int n_keys = n_past + min(q0 + FM_Q, T);
     const int ntile = (n_keys + FM_K - 1) / FM_K;
+    int kt0 = 0, kt1 = ntile;                             // this workgroup's key tiles
+    if constexpr (SPL) {
+        kt0 = sp * ch;
+        kt1 = min(kt0 + ch, ntile);
+        if (kt0 >= ntile) return;                         // past this query block's keys (whole workgroup)
+    }
     const int qmin = n_past + q0;                         // smallest query position of the block
     // DMA: wave w fetches key rows (64 / NW) w .. +64/NW of the tile (instructions of 4 rows) for K and for V;
     // lane: row 4 i + (lane >> 4) of the instruction, chunk slot lane & 15 <- global chunk (slot ^ 2 (row & 7))
@@ -414,16 +435,16 @@ __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t 
         }
     };
     // ring of NST stages, NST - 1 tiles ahead: tile kt + 1's K is read at the top of iteration kt
-    for (int t = 0; t < NST - 1 && t < ntile; ++t) stage(t);
+    for (int t = kt0; t < kt0 + NST - 1 && t < kt1; ++t) stage(t);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     f4 sc[NB], sn[NB];
-    qk(0, sc);
-    for (int kt = 0; kt < ntile; ++kt) {
+    qk(kt0, sc);
+    for (int kt = kt0; kt < kt1; ++kt) {
         const int p0 = kt * FM_K + 16 * b0;
-        const bool pre = kt + NST - 1 < ntile;
+        const bool pre = kt + NST - 1 < kt1;
         if (pre) stage(kt + NST - 1);
-        if (kt + 1 < ntile) qk(kt + 1, sn);
+        if (kt + 1 < kt1) qk(kt + 1, sn);
         const char *svb = (const char *)&sv[kt & (NST - 1)][0];
         h8 va[8];
         vread(svb, NW == 8 ? hf : 0, va);             // V^T of the first 32 keys: independent of P, read under softmax
@@ -512,24 +533,102 @@ __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t 
             }
         }
         __syncthreads();
-        if (hf == 1) return;
-        const float m1 = xo[ql * 130 + 128], l1 = xo[ql * 130 + 129];
-        const float m = fmaxf(m_run, m1);
-        const float a0 = m_run == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m_run - m);
-        const float a1 = m1 == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m1 - m);
-        l_run = l_run * a0 + l1 * a1;
+        if (!SPL && hf == 1) return;
+        if (hf == 0) {
+            const float m1 = xo[ql * 130 + 128], l1 = xo[ql * 130 + 129];
+            const float m = fmaxf(m_run, m1);
+            const float a0 = m_run == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m_run - m);
+            const float a1 = m1 == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(m1 - m);
+            l_run = l_run * a0 + l1 * a1;
+#pragma unroll
+            for (int db = 0; db < 8; ++db)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) o[db][r] = o[db][r] * a0 + xo[ql * 130 + 16 * db + 4 * g + r] * a1;
+            m_run = m;
+        }
+    }
+    if constexpr (SPL) {
+        constexpr int PS = 16 * 130;                      // one head's partial: [query][128 dims + m + l]
+        const int slot = qb * HKV + hk, nsp = (ntile + ch - 1) / ch;
+        float *pb = part + (int64_t)slot * nsp_grid * 4 * PS + (wave & 3) * PS + ql * 130;
+        if (hf == 0) {
+            float *pp = pb + (int64_t)sp * 4 * PS;
+#pragma unroll
+            for (int db = 0; db < 8; ++db)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    __hip_atomic_store(pp + 16 * db + 4 * g + r, o[db][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (g == 0) {
+                __hip_atomic_store(pp + 128, m_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(pp + 129, l_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        __shared__ unsigned s_old;
+        if (tid == 0) s_old = __hip_atomic_fetch_add(tick + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        if (s_old != (unsigned)(nsp - 1)) return;         // not the last split of this (query block, kv head)
+        if (tid == 0) __hip_atomic_store(tick + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (NW == 8 && hf == 1) return;
+        float mm = -INFINITY;
+        for (int k = 0; k < nsp; ++k)
+            mm = fmaxf(mm, __hip_atomic_load(pb + (int64_t)k * 4 * PS + 128, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        l_run = 0.0f;
+#pragma unroll
+        for (int db = 0; db < 8; ++db) o[db] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int k = 0; k < nsp; ++k) {                   // split order
+            const float *pk = pb + (int64_t)k * 4 * PS;
+            const float mk = __hip_atomic_load(pk + 128, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const float lk = __hip_atomic_load(pk + 129, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const float ak = mk == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(mk - mm);
+            l_run = l_run + lk * ak;
+#pragma unroll
+            for (int db = 0; db < 8; ++db)
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    o[db][r] = o[db][r] + __hip_atomic_load(pk + 16 * db + 4 * g + r, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT) * ak;
+        }
+    }
+    if (qi >= T) return;                                  // (all four lanes of a query leave together)
+    const float inv = 1.0f / l_run;
+    if (out) {
+        float *op = out + ((int64_t)qi * H + h) * D;
 #pragma unroll
         for (int db = 0; db < 8; ++db)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[db][r] = o[db][r] * a0 + xo[ql * 130 + 16 * db + 4 * g + r] * a1;
+            for (int r = 0; r < 4; ++r) op[16 * db + 4 * g + r] = o[db][r] * inv;
     }
-    if (qi >= T) return;
-    const float inv = 1.0f / l_run;
-    float *op = out + ((int64_t)qi * H + h) * D;
+    if (qta) {
+        // Q8_0 block k of this head = dims 32 k .. + 32 = o[2k], o[2k + 1] of the query's 4 lanes (g): element
+        // 16 (db - 2k) + 4 g + r -> half db - 2k, byte 4 g + r of the token's 16-byte row (kcpp_common.h KT_Q8_0_TA)
+        const int64_t E = (int64_t)H * D, nb = E / 32, ng = (T + 31) / 32, grp = qi >> 5, tok = qi & 31;
 #pragma unroll
-    for (int db = 0; db < 8; ++db)
+        for (int k = 0; k < 4; ++k) {
+            float v[8];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) op[16 * db + 4 * g + r] = o[db][r] * inv;
+            for (int r = 0; r < 4; ++r) { v[r] = o[2 * k][r] * inv; v[4 + r] = o[2 * k + 1][r] * inv; }
+            float am = 0.0f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(v[e]));
+            am = fmaxf(am, __shfl_xor(am, 16, 64));
+            am = fmaxf(am, __shfl_xor(am, 32, 64));
+            const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+            uint32_t pk[2] = {0u, 0u};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                int iv = (int)rintf(__fmul_rn(v[e], id));
+                iv = iv > 127 ? 127 : (iv < -128 ? -128 : iv);
+                pk[e >> 2] |= (uint32_t)(iv & 0xFF) << (8 * (e & 3));
+            }
+            const int64_t ib = (int64_t)h * 4 + k;
+            uint8_t *qb8 = qta + (grp * nb + ib) * 1024 + tok * 16 + 4 * g;
+            *(uint32_t *)qb8 = pk[0];
+            *(uint32_t *)(qb8 + 512) = pk[1];
+            if (g == 0) ((float *)(qta + ng * 32 * E))[(grp * nb + ib) * 32 + tok] = h2f(f2h(am / 127.f));
+        }
+    }
 }
 
 static int g_fa_prefill_variant = 0;
@@ -539,16 +638,57 @@ extern "C" int kcpp_fa_prefill_set_variant(int v) {
     return old;
 }
 
+// the key-split variant's workspace (kcpp_fa_workspace_bytes reserves it): tickets in the 2 KB header, then
+// [query block][kv head][split < FM_SPLITS][4 heads][16 queries][130] partials for T <= FM_SPLIT_T
+#define FM_SPLIT_T 64
+#define FM_SPLITS 32
+extern "C" int64_t kcpp_fa_split_ws_bytes(int H) {
+    return KCPP_FA_WS_HEADER + (int64_t)(FM_SPLIT_T / FM_Q) * (H / 4) * FM_SPLITS * 4 * 16 * 130 * 4;
+}
+
+extern "C" int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out,
+                                               void *qta, void *ws, int T, int H, int HKV, int D, int n_past, float scale,
+                                               void *stream) {
+    if (D != 128 || HKV <= 0 || H != 4 * HKV || (!out && !qta)) return -3;
+    const int v = g_fa_prefill_variant ? g_fa_prefill_variant : 4;
+    const int nqb = (T + FM_Q - 1) / FM_Q;
+    const int nb0 = nqb * HKV;
+    if (v == 4 && ws && T <= FM_SPLIT_T && nb0 <= 512) {
+        // keys split so that the grid has ~512 workgroups (at most FM_SPLITS splits of whole 64-key tiles)
+        const int ntile = (n_past + T + FM_K - 1) / FM_K;
+        const int want = std::min(FM_SPLITS, std::max(1, 512 / nb0));
+        const int ch = (ntile + want - 1) / want;
+        const int nsp = (ntile + ch - 1) / ch;
+        if (nsp > 1) {
+            hipLaunchKernelGGL((k_fa_prefill_mfma3<8, true>), dim3(nb0 * nsp), dim3(512), 0, (hipStream_t)stream, q16, kc,
+                               vc, out, T, H, HKV, n_past, scale, (float *)((uint8_t *)ws + KCPP_FA_WS_HEADER),
+                               (unsigned *)ws, ch, nsp, (uint8_t *)qta);
+            KCPP_CHECK(hipGetLastError());
+            return 0;
+        }
+    }
+    if (v == 4) {
+        hipLaunchKernelGGL((k_fa_prefill_mfma3<8, false>), dim3(nb0), dim3(512), 0, (hipStream_t)stream, q16, kc, vc, out,
+                           T, H, HKV, n_past, scale, (float *)nullptr, (unsigned *)nullptr, 0, 1, (uint8_t *)qta);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
+    if (!out) return -3;
+    return kcpp_flash_attn_prefill_mfma(q16, kc, vc, out, T, H, HKV, D, n_past, scale, stream);
+}
+
 extern "C" int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out,
                                             int T, int H, int HKV, int D, int n_past, float scale, void *stream) {
     if (D != 128 || HKV <= 0 || H != 4 * HKV) return -3;
     const int v = g_fa_prefill_variant ? g_fa_prefill_variant : 4;
     if (v == 3)
-        hipLaunchKernelGGL(k_fa_prefill_mfma3<4>, dim3((T + FM_Q - 1) / FM_Q * HKV), dim3(256), 0, (hipStream_t)stream, q16,
-                           kc, vc, out, T, H, HKV, n_past, scale);
+        hipLaunchKernelGGL((k_fa_prefill_mfma3<4, false>), dim3((T + FM_Q - 1) / FM_Q * HKV), dim3(256), 0,
+                           (hipStream_t)stream, q16, kc, vc, out, T, H, HKV, n_past, scale, (float *)nullptr,
+                           (unsigned *)nullptr, 0, 1, (uint8_t *)nullptr);
     else if (v == 4)
-        hipLaunchKernelGGL(k_fa_prefill_mfma3<8>, dim3((T + FM_Q - 1) / FM_Q * HKV), dim3(512), 0, (hipStream_t)stream, q16,
-                           kc, vc, out, T, H, HKV, n_past, scale);
+        hipLaunchKernelGGL((k_fa_prefill_mfma3<8, false>), dim3((T + FM_Q - 1) / FM_Q * HKV), dim3(512), 0,
+                           (hipStream_t)stream, q16, kc, vc, out, T, H, HKV, n_past, scale, (float *)nullptr,
+                           (unsigned *)nullptr, 0, 1, (uint8_t *)nullptr);
     else if (v == 1)
         hipLaunchKernelGGL(k_fa_prefill_mfma, dim3((T + FM_Q - 1) / FM_Q, HKV), dim3(256), 0, (hipStream_t)stream, q16, kc,
                            vc, out, T, H, HKV, n_past, scale);

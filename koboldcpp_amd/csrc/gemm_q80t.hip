@@ -26,6 +26,13 @@
 #ifndef Q80T_FMA
 #define Q80T_FMA 1
 #endif
+#ifndef Q80T_RING
+#define Q80T_RING 0              // 1: branch-free Q80T_P-deep weight ring (tools/q80t_sweep.py variants)
+#endif
+#ifndef Q80T_P
+#define Q80T_P 2                 // weight units in flight per wave (even: the x pair alternates with the ring slot)
+#endif
+#define Q80T_SMAX 8              // K ranges per tile at most (split-K tickets)
 #ifndef Q80T_GLU_WV
 #define Q80T_GLU_WV 4
 #endif
@@ -57,6 +64,13 @@ struct Q80TArgs {
     unsigned *tick;          // S = 2: [tile][group] arrival tickets, zero between launches (the second arriver resets)
     int64_t ntile;           // 32-row tiles (MODE 1: of the gate)
     int S, Z;                // K ranges per tile, 32-token groups
+    // MODE 0 q|k|v epilogue with rope_tab: rope(q) -> q16 [t][nq], rope(k) -> kc, v -> vc ([pos][nkv], f16) as
+    // ops.hip k_rope_kv stores them; Y is not written
+    const float2 *rope_tab;
+    uint16_t *q16, *kc, *vc;
+    const int32_t *pos;      // positions per token (graph replay), else n_past + t
+    int n_past, hd;
+    int64_t nq, nkv;
 };
 
 template <int MODE, int WV>
@@ -92,6 +106,89 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
     const int64_t ng = (a.M + 31) / 32;
     const uint8_t *wq = W + tl * nb * 1024 + lane * 16;              // block b at + b * 1024
     const uint8_t *wd = W + Ns * K + tl * nu * 256 + (lane & 31) * 8;   // unit u at + u * 256
+#if Q80T_RING
+    // lanes of tokens past M read their k-half's token-0 bytes (cache lines the live lanes fetch anyway: at M = 1 the
+    // wave moves 32 B of activation per block, not 1 KiB) and zero them
+    const bool xlive = z * 32 + (lane & 31) < a.M;
+    const uint8_t *aq = a.act + z * nb * 1024 + (xlive ? lane : (lane & 32)) * 16;
+    const int xm = xlive ? -1 : 0;
+    // weight fragments Q80T_P units (4 blocks each) ahead of the MFMA, activation fragments (L2-resident) one unit
+    // ahead; the loop body is branch-free (unit indices clamped to the wave's last unit, a clamped unit's scale zeroed)
+    // so the per-block MFMA + epilogue stays one scheduling region with one accumulator live
+    struct WUnit { i32x4 w[4]; uint2 d; };
+    struct XUnit { i32x4 x[4]; };
+    const int64_t ulast = wu1 - 1;
+    auto loadw = [&](int64_t u, WUnit &U) {
+        u = u < ulast ? u : ulast;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) U.w[i] = ld_frag_nt(wq + (4 * u + i) * 1024);
+        U.d = *(const uint2 *)(wd + u * 256);
+    };
+    auto loadx = [&](int64_t u, XUnit &X) {
+        u = u < ulast ? u : ulast;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) X.x[i] = *(const i32x4 *)(aq + (4 * u + i) * 1024) & xm;
+    };
+    float tot[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) tot[r] = 0.0f;
+    auto comp = [&](int64_t u, const WUnit &U, const XUnit &X) {
+        const bool live = u <= ulast;
+        u = live ? u : ulast;
+        const float dw[4] = {live ? h2f((uint16_t)(U.d.x & 0xFFFF)) : 0.0f, live ? h2f((uint16_t)(U.d.x >> 16)) : 0.0f,
+                             live ? h2f((uint16_t)(U.d.y & 0xFFFF)) : 0.0f, live ? h2f((uint16_t)(U.d.y >> 16)) : 0.0f};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            i32x16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[r] = 0;
+            i32x4 xv = X.x[i], wv = U.w[i];
+            asm volatile("" : "+v"(xv), "+v"(wv));   // block i's MFMA not hoisted above block i-1's epilogue
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(xv, wv, acc, 0, 0, 0);
+            const float *sd = dxs + ((u - u0) * 4 + i) * 32 + 4 * kg;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const float4 d4 = *(const float4 *)(sd + 8 * c);
+                const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+#if Q80T_FMA
+                    tot[4 * c + e] = fmaf((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e]), tot[4 * c + e]);
+#else
+                    tot[4 * c + e] = __fadd_rn(tot[4 * c + e], __fmul_rn((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e])));
+#endif
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(tot[r]));   // ... and its epilogue done here: one
+            asm volatile("" ::: "memory");                                   // accumulator live at a time
+        }
+    };
+    WUnit wr[Q80T_P];
+    XUnit xa, xb;
+    if (wu0 < wu1) {
+#pragma unroll
+        for (int i = 0; i < Q80T_P; ++i) loadw(wu0 + i, wr[i]);
+        loadx(wu0, xa);
+    }
+    {   // the token scales go to LDS while the first units' fragments are in flight
+        const float4 *src = (const float4 *)(a.act + ng * 32 * K) + (z * nb + 4 * u0) * 8;
+        float4 *dst = (float4 *)dxs;
+        for (int64_t i = tid; i < (u1 - u0) * 32; i += 64 * WV) dst[i] = src[i];
+    }
+    __syncthreads();
+    for (int64_t u = wu0; u < wu1; u += Q80T_P) {
+#pragma unroll
+        for (int i = 0; i < Q80T_P; ++i) {     // unrolled: ring slot i and the x pair are static registers
+            XUnit &xc = (i & 1) ? xb : xa, &xn = (i & 1) ? xa : xb;
+            loadx(u + i + 1, xn);
+            asm volatile("" ::: "memory");       // loads stay where they are issued (in flight across the compute)
+            comp(u + i, wr[i], xc);
+            loadw(u + i + Q80T_P, wr[i]);
+            asm volatile("" ::: "memory");
+        }
+    }
+#else
     const uint8_t *aq = a.act + z * nb * 1024 + lane * 16;
     // lanes of tokens past M read no activation (at M = 1 the wave fetches 32 B of it per block, not 1 KiB)
     const bool xlive = z * 32 + (lane & 31) < a.M;
@@ -148,6 +245,7 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
         if (u + 2 < wu1) load(u + 2, ua);
         comp(u + 1, ub);
     }
+#endif
     // waves summed in wave order: element (token t, row j) of lane l, r: t = (r & 3) + 8 (r >> 2) + 4 (l >> 5), j = l & 31
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = tot[r];
@@ -200,7 +298,7 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
         if (S > 1) {
             // publish this K range's partial (write-through stores, drained), then one agent-scope ticket per workgroup;
             // the second arriver adds the other partial (MI355X_MICROARCH.md hand-off table, row 1)
-            float *pp = a.part + ((tile * Z + z) * 2 + split) * 1024;
+            float *pp = a.part + ((tile * Z + z) * S + split) * 1024;
             for (int idx = tid; idx < 1024; idx += 64 * WV) {
                 float v = red[idx];
 #pragma unroll
@@ -212,26 +310,64 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
             unsigned *tk = a.tick + tile * 64 + z;
             if (tid == 0) s_old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __syncthreads();
-            if (s_old == 0) return;
+            if (s_old != (unsigned)(S - 1)) return;                   // the last arriver sums the S ranges
             if (tid == 0) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        const float *po = a.part + ((tile * Z + z) * 2 + (1 - split)) * 1024;
+        const float *po = a.part + (tile * Z + z) * S * 1024;
         for (int idx = tid; idx < 1024; idx += 64 * WV) {
             float v = red[idx];
 #pragma unroll
             for (int w = 1; w < WV; ++w) v = __fadd_rn(v, red[w * 1024 + idx]);
-            if (S > 1) v = __fadd_rn(v, __hip_atomic_load(po + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (S > 1) {     // in range order whichever workgroup arrived last (S = 2: a + b = b + a)
+                const float own = v;
+                v = split == 0 ? own : __hip_atomic_load(po + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (int k = 1; k < S; ++k)
+                    v = __fadd_rn(v, k == split ? own : __hip_atomic_load(po + k * 1024 + idx, __ATOMIC_RELAXED,
+                                                                          __HIP_MEMORY_SCOPE_AGENT));
+            }
             const int r = idx >> 6, l = idx & 63;
             const int64_t t = z * 32 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
             const int64_t n = coff + tl * 32 + (l & 31);
+            if (a.rope_tab) {
+                // k_rope_kv's rotation of the adjacent pair (n & ~1, n | 1): the partner is lane l ^ 1, same token
+                const float pv = __shfl_xor(v, 1, 64);
+                if (t < a.M) {
+                    const int64_t p = a.pos ? a.pos[t] : a.n_past + t;
+                    if (n < a.nq + a.nkv) {
+                        const int64_t nr = n < a.nq ? n : n - a.nq;
+                        const float2 cs = a.rope_tab[p * (a.hd / 2) + (nr % a.hd) / 2];
+                        const bool odd = n & 1;
+                        const float x0 = odd ? pv : v, x1 = odd ? v : pv;
+                        const float o = odd ? __fadd_rn(__fmul_rn(x0, cs.y), __fmul_rn(x1, cs.x))
+                                            : __fsub_rn(__fmul_rn(x0, cs.x), __fmul_rn(x1, cs.y));
+                        if (n < a.nq) a.q16[t * a.nq + n] = f2h_rn(o);
+                        else a.kc[p * a.nkv + nr] = f2h_rn(o);
+                    } else {
+                        a.vc[p * a.nkv + (n - a.nq - a.nkv)] = f2h_rn(v);
+                    }
+                }
+                continue;
+            }
             if (t < a.M) a.Y[t * a.ldy + n] = a.res ? __fadd_rn(v, a.res[t * a.ldr + n]) : v;
         }
     }
 }
 
-// split / wave choice from the weight shape alone
+// split / wave choice from the weight shape alone (KCPP_Q80T_SHAPE="S,WV" / KCPP_Q80T_GLU="WV": tools/q80t_sweep.py)
 void q80t_shape(int mode, int64_t ntile, int64_t nu, int &S, int &WV) {
-    if (mode == 1) { S = 1; WV = Q80T_GLU_WV; return; }
+    static int ov_s = -1, ov_wv = 0, ov_glu = 0;
+    if (ov_s < 0) {
+        ov_s = 0;
+        if (const char *e = getenv("KCPP_Q80T_SHAPE")) sscanf(e, "%d,%d", &ov_s, &ov_wv);
+        if (const char *e = getenv("KCPP_Q80T_GLU")) ov_glu = atoi(e);
+    }
+    if (mode == 1) { S = 1; WV = ov_glu == 4 || ov_glu == 8 ? ov_glu : Q80T_GLU_WV; return; }
+    if (ov_s >= 1 && ov_s <= Q80T_SMAX && (ov_wv == 1 || ov_wv == 2 || ov_wv == 4 || ov_wv == 8)) {
+        S = ntile <= 256 ? ov_s : 1;
+        WV = ov_wv;
+        while (WV > 1 && nu / S < WV) WV /= 2;
+        return;
+    }
     // tools/q80t_sweep.py (Llama-3-8B shapes, M = 1 and 32): q|k|v (192 tiles) S 1 x 8 waves 10.6 us vs 15.8 at S 2; wo /
     // down (128 tiles) S 2 x 8 waves 9.0 / 16.9 us, the best of S 1-2 x 2-8 waves
     S = ntile < 160 && nu >= 16 ? 2 : 1;
@@ -245,19 +381,20 @@ void q80t_shape(int mode, int64_t ntile, int64_t nu, int &S, int &WV) {
 // words, zero when the workspace is first used and left zero by every launch, whatever shape ran before), then the
 // partial tiles
 constexpr int64_t Q80T_TICK_BYTES = 256 * 64 * 4;
+static_assert(Q80T_SMAX <= 8, "partials sized for 8 ranges");
 extern "C" {
 int64_t kcpp_q80t_ws_bytes(int64_t K, int64_t N, int64_t M) {
     const int64_t ntile = N / 32, Z = (M + 31) / 32;
-    return Q80T_TICK_BYTES + ntile * Z * 2 * 4096;
+    int S, WV;
+    q80t_shape(0, ntile, K / 128, S, WV);
+    return Q80T_TICK_BYTES + ntile * Z * std::max(S, 2) * 4096;
 }
 
 // mode 0: Y = W act (+ res); mode 1: h = silu(W act) * (W2 act) as f32 (Y) or as the KT_Q8_0_TA activation (qout)
-int kcpp_gemm_q80t(const void *const *Ws, const int64_t *Ns, int nseg, const void *W2, int64_t K, const void *act,
-                   int64_t M, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *qout, void *ws,
-                   void *stream) {
+static int q80t_launch(Q80TArgs &a, const void *const *Ws, const int64_t *Ns, int nseg, const void *W2, int64_t K,
+                       const void *act, int64_t M, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode,
+                       void *qout, void *ws, void *stream) {
     if (nseg < 1 || nseg > 3 || K % 128 || M < 1 || (mode == 1 && (nseg != 1 || !W2))) return -1;
-    Q80TArgs a;
-    memset(&a, 0, sizeof a);
     int64_t ntot = 0;
     for (int i = 0; i < nseg; ++i) {
         if (Ns[i] % 32 || Ns[i] <= 0) return -1;
@@ -283,7 +420,8 @@ int kcpp_gemm_q80t(const void *const *Ws, const int64_t *Ns, int nseg, const voi
     const int64_t nblk = (a.ntile + 7) / 8 * 8 * S * a.Z;
     hipStream_t s = (hipStream_t)stream;
 #define Q80T_L(MD, W_) hipLaunchKernelGGL((k_q80t<MD, W_>), dim3((unsigned)nblk), dim3(64 * W_), smem, s, a)
-    if (mode == 1) Q80T_L(1, Q80T_GLU_WV);
+    if (mode == 1 && WV == 8) Q80T_L(1, 8);
+    else if (mode == 1) Q80T_L(1, 4);
     else if (WV == 8) Q80T_L(0, 8);
     else if (WV == 4) Q80T_L(0, 4);
     else if (WV == 2) Q80T_L(0, 2);
@@ -291,5 +429,29 @@ int kcpp_gemm_q80t(const void *const *Ws, const int64_t *Ns, int nseg, const voi
 #undef Q80T_L
     KCPP_CHECK(hipGetLastError());
     return 0;
+}
+
+int kcpp_gemm_q80t(const void *const *Ws, const int64_t *Ns, int nseg, const void *W2, int64_t K, const void *act,
+                   int64_t M, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *qout, void *ws,
+                   void *stream) {
+    Q80TArgs a;
+    memset(&a, 0, sizeof a);
+    return q80t_launch(a, Ws, Ns, nseg, W2, K, act, M, Y, ldy, res, ldr, mode, qout, ws, stream);
+}
+
+// q|k|v = W act with k_rope_kv fused into the epilogue: rope(q) -> q16 [M][H D], rope(k) / v -> the f16 caches at
+// positions pos[t] (or n_past + t); the f32 q|k|v rows are not written
+int kcpp_gemm_q80t_qkv_rope(const void *const *Ws, const int64_t *Ns, int64_t K, const void *act, int64_t M,
+                            const void *rope_tab, int n_past, const int32_t *pos_dev, int head_dim, uint16_t *q16,
+                            uint16_t *kc, uint16_t *vc, void *ws, void *stream) {
+    if (!rope_tab || !q16 || !kc || !vc || head_dim <= 0 || head_dim % 2 || Ns[0] % head_dim || Ns[1] % head_dim ||
+        Ns[1] != Ns[2])
+        return -1;
+    Q80TArgs a;
+    memset(&a, 0, sizeof a);
+    a.rope_tab = (const float2 *)rope_tab;
+    a.q16 = q16; a.kc = kc; a.vc = vc; a.pos = pos_dev; a.n_past = n_past; a.hd = head_dim;
+    a.nq = Ns[0]; a.nkv = Ns[1];
+    return q80t_launch(a, Ws, Ns, 3, nullptr, K, act, M, nullptr, 0, nullptr, 0, 0, nullptr, ws, stream);
 }
 }  // extern "C"

@@ -79,6 +79,10 @@ extern "C" int kcpp_gemv_q4k(const void *args, int mode, int pro, void *stream);
 // MFMA prefill flash attention (attn_mfma.hip); -3 = shape not covered (needs D = 128, H = 4 * HKV)
 extern "C" int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out,
                                             int T, int H, int HKV, int D, int n_past, float scale, void *stream);
+extern "C" int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out,
+                                               void *qta, void *ws, int T, int H, int HKV, int D, int n_past, float scale,
+                                               void *stream);
+extern "C" int64_t kcpp_fa_split_ws_bytes(int H);
 // decode mat-vec over the row-major RS layouts (gemv_rs.hip); -3 = not covered
 extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
 extern "C" int kcpp_rs_supported(int type, int64_t K);

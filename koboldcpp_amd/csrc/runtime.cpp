@@ -1089,6 +1089,7 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
         KLayer &L = m->layers[il - m->il0];
         const KTensor *t = L.t;
         const bool kq = kcpp_vec_dot_type(t[1].type) == KT_Q8_K;
+        bool roped = false;                          // q16 and this step's K/V rows already written
         // attn_norm -> act (Q8_K fused, or f32 then Q8_0)
         if (kq && kcpp_vec_dot_type(t[2].type) == KT_Q8_K && kcpp_vec_dot_type(t[3].type) == KT_Q8_K) {
             RC(kcpp_rms_norm(m->x, E, (const float *)t[0].d, nullptr, E, m->act, E, T, hp.eps, s));
@@ -1123,7 +1124,13 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             if (m->lanes.empty()) {
                 const void *Wq[3] = {t[1].d, t[2].d, t[3].d};
                 const int64_t Nq[3] = {E, EKV, EKV};
-                RC(kcpp_gemm_q80t(Wq, Nq, 3, nullptr, E, m->act, T, m->qkv, LQ, nullptr, 0, 0, nullptr, m->gemm_ws, s));
+                if (m->kv_tk == KT_F16) {          // rope + the f16 K/V stores in the GEMM's epilogue
+                    RC(kcpp_gemm_q80t_qkv_rope(Wq, Nq, E, m->act, T, m->rope_tab, n_past, posp, (int)D, m->q16, L.kc,
+                                               L.vc, m->gemm_ws, s));
+                    roped = true;
+                } else {
+                    RC(kcpp_gemm_q80t(Wq, Nq, 3, nullptr, E, m->act, T, m->qkv, LQ, nullptr, 0, 0, nullptr, m->gemm_ws, s));
+                }
             } else {
                 for (int j = 1; j <= 3; ++j)
                     RC(matmul(m, t[j], nullptr, m->act, T, m->qkv + (j == 1 ? 0 : (j == 2 ? E : E + EKV)), LQ, nullptr, 0, 0));
@@ -1146,11 +1153,21 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
         if (kvq) {   // quantized cache: f32 rope in place, quantize K/V rows into the cache, Q8_0-dot attention
             RC(kcpp_rope_qk_inplace(m->qkv, LQ, T, (int)H, (int)HKV, (int)D, n_past, posp, m->rope_tab, s));
             RC(kcpp_kv_store_q(m->kv_tk, m->kv_tv, m->qkv, LQ, E, E + EKV, T, EKV, L.kc, L.vc, hp.n_ctx, n_past, posp, s));
-        } else {
+        } else if (!roped) {
             RC(kcpp_rope_kv(m->qkv, LQ, nullptr, m->q16, L.kc, L.vc, T, (int)H, (int)HKV, (int)D, n_past, posp, m->rope_tab, s));
         }
         const bool woq = kcpp_vec_dot_type(t[4].type) == KT_Q8_K && !m->fa_exact && !kvq;
-        if (kvq)
+        // Q8_0 tile layout, ubatch > 16: attention writes attn_output's KT_Q8_0_TA activation itself (keys split
+        // over the grid for short ubatches)
+        bool attn_q = false;
+        if (m->q80t && m->lanes.empty() && !kvq && !m->fa_exact && !posp && T > 16 && t[4].type == KT_Q8_0_T) {
+            const int rc = kcpp_flash_attn_prefill_mfma_ex(m->q16, L.kc, L.vc, nullptr, m->act, m->fa_ws, T, (int)H,
+                                                           (int)HKV, (int)D, n_past, kq_scale, s);
+            if (rc != 0 && rc != -3) return rc;
+            attn_q = rc == 0;
+        }
+        if (attn_q) {
+        } else if (kvq)
             RC(kcpp_flash_attn_q(m->kv_tk, m->kv_tv, m->qkv, LQ, L.kc, L.vc, m->attn, T, (int)H, (int)HKV, (int)D, hp.n_ctx,
                                  n_past, posp, kq_scale, s));
         else if (m->fa_exact)
@@ -1158,7 +1175,7 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
         else
             RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, (woq && T <= 16) ? m->act : nullptr, m->fa_ws, T, (int)H,
                                (int)HKV, (int)D, n_past, posp, hp.n_ctx, kq_scale, 0, s));
-        if (!(woq && T <= 16)) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, T, s));
+        if (!(woq && T <= 16) && !attn_q) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, T, s));
         RC(matmul(m, t[4], nullptr, m->act, T, m->x, E, m->x, E, 0));                    // x += wo . attn
         if (hp.n_expert > 0) { RC(T == 1 ? moe_dec(m, L) : moe_prefill(m, L, T)); continue; }   // T == 1: no host sync (graphs)
         if (m->q80t) {

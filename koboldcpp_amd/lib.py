@@ -55,6 +55,8 @@ _SIGS = {
     "kcpp_rope_kv": [P, I64, P, P, P, P, I, I, I, I, I, P, P, P],
     "kcpp_flash_attn": [P, P, P, P, P, P, I, I, I, I, I, P, I, Fl, I, P],
     "kcpp_flash_attn_prefill_mfma": [P, P, P, P, I, I, I, I, I, Fl, P],
+    "kcpp_flash_attn_prefill_mfma_ex": [P, P, P, P, P, P, I, I, I, I, I, Fl, P],
+    "kcpp_fa_split_ws_bytes": [I],
     "kcpp_fa_decode_ex": [P, P, P, I64, I64, P, P, P, I, I, I, P, I, Fl, I, P],
     "kcpp_fa_set_stamps": [P],
     "kcpp_gguf_check": [ctypes.c_char_p, ctypes.c_char_p, I],
@@ -65,6 +67,7 @@ _SIGS = {
     "kcpp_engine_bench": [P, P, I, I, P, U64, I, I, I, I, P],
     "kcpp_expose_synth_weights": [U64],
     "kcpp_gemm_q80t": [P, P, I, P, I64, P, I64, P, I64, P, I64, I, P, P, P],
+    "kcpp_gemm_q80t_qkv_rope": [P, P, I64, P, I64, P, I, P, I, P, P, P, P, P],
     "kcpp_rms_norm_q80t": [P, I64, P, P, I64, I64, Fl, P],
     "kcpp_q80t_ws_bytes": [I64, I64, I64],
     "kcpp_pipeline_trace": [I, I, I, I, I, ctypes.c_char_p, I],
@@ -121,7 +124,7 @@ _SIGS = {
     "kcpp_kv_store_q": [I, I, P, I64, I64, I64, I, I64, P, P, I64, I, P, P],
     "kcpp_flash_attn_q": [I, I, P, I64, P, P, P, I, I, I, I, I64, I, P, Fl, P],
 }
-_RES = {"kcpp_gradient_ai_rope_base": Fl, "kcpp_q80t_ws_bytes": I64, "kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
+_RES = {"kcpp_gradient_ai_rope_base": Fl, "kcpp_fa_split_ws_bytes": I64, "kcpp_q80t_ws_bytes": I64, "kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
         "kcpp_model_create": P, "kcpp_model_hidden": P, "kcpp_model_stream": P, "kcpp_model_weight_bytes": I64,
         "kcpp_last_error": ctypes.c_char_p, "kcpp_model_free": None, "kcpp_fa_set_stamps": None}
 _L.kcpp_act_bytes.argtypes = [I, I64, I64]

@@ -166,15 +166,21 @@ def test_gemm_glu_vs_oracle_and_quantized_h(env, Kd, N, M):
 
 
 def test_qkv_segments(env):
-    """q|k|v as one launch over three segments equals the three mat-muls (bit for bit)"""
+    """q|k|v as one launch over three segments equals one matrix of the concatenated rows bit for bit (the split is a
+    function of the launch's total shape), and the three separate mat-muls (their own splits) to f32 summation-order
+    rounding"""
     torch, K = env
     Kd, Ns, M = 4096, [4096, 1024, 1024], 32
     X = np.random.default_rng(9).standard_normal((M, Kd)).astype(np.float32)
     Ws = [dev_t(torch, K, Kd, n, 30 + i) for i, n in enumerate(Ns)]
     act = quant_ta(torch, K, X)
     one = gemm(torch, K, Ws, Ns, Kd, act, M)
+    # KT_Q8_0_T of the stacked rows: the tile planes in order, then the scale planes in order
+    cat = torch.cat([w[:n * Kd] for w, n in zip(Ws, Ns)] + [w[n * Kd:] for w, n in zip(Ws, Ns)])
+    whole = gemm(torch, K, [cat], [sum(Ns)], Kd, act, M)
+    assert np.array_equal(one.view(np.uint32), whole.view(np.uint32))
     parts = np.concatenate([gemm(torch, K, [w], [n], Kd, act, M) for w, n in zip(Ws, Ns)], axis=1)
-    assert np.array_equal(one.view(np.uint32), parts.view(np.uint32))
+    assert np.abs(one - parts).max() <= 1e-5 * np.abs(parts).max()
 
 
 @pytest.mark.parametrize("Kd,N", [(4096, 4096), (14336, 4096), (4096, 14336)])
@@ -193,3 +199,43 @@ def test_batch_invariance_and_ticket_reset(env, Kd, N):
     for t in (0, 57, 99):
         one = gemm(torch, K, [W], [N], Kd, quant_ta(torch, K, X[t:t + 1]), 1, ws=ws)
         assert np.array_equal(one[0].view(np.uint32), full[t].view(np.uint32)), t
+
+
+@pytest.mark.parametrize("M,n_past,dev_pos", [(32, 1000, False), (7, 4000, False), (1, 3839, True), (45, 17, True)])
+def test_qkv_rope_epilogue(env, M, n_past, dev_pos):
+    """q|k|v with the rope + f16 K/V stores in the GEMM epilogue == the GEMM then kcpp_rope_kv, bit for bit (q16, the
+    cache rows at the positions, nothing else written)"""
+    torch, K = env
+    Kd, H, HKV, D, n_ctx = 4096, 32, 8, 128, 4096
+    Ns = [H * D, HKV * D, HKV * D]
+    X = np.random.default_rng(M).standard_normal((M, Kd)).astype(np.float32)
+    Ws = [dev_t(torch, K, Kd, n, 60 + i) for i, n in enumerate(Ns)]
+    act = quant_ta(torch, K, X)
+    tab = np.empty((n_ctx, D // 2, 2), np.float32)
+    K.call("kcpp_rope_table", tab.ctypes.data_as(ctypes.c_void_p), n_ctx, D, 500000.0, 1.0, None, 0.0, 1.0, 32.0, 1.0,
+           n_ctx)
+    tabd = torch.from_numpy(tab).cuda()
+    pos = np.arange(n_past, n_past + M, dtype=np.int32)
+    if dev_pos:
+        pos = np.random.default_rng(1).permutation(n_ctx)[:M].astype(np.int32)   # scattered positions
+    posd = torch.from_numpy(pos).cuda()
+    qkv = torch.from_numpy(gemm(torch, K, Ws, Ns, Kd, act, M)).cuda()
+    outs = []
+    for fused in (False, True):
+        q16 = torch.zeros((M, H * D), dtype=torch.int16, device="cuda")
+        kc = torch.zeros((n_ctx, HKV * D), dtype=torch.int16, device="cuda")
+        vc = torch.zeros((n_ctx, HKV * D), dtype=torch.int16, device="cuda")
+        if fused:
+            wp = (ctypes.c_void_p * 3)(*[w.data_ptr() for w in Ws])
+            np_ = (ctypes.c_int64 * 3)(*Ns)
+            K.call("kcpp_gemm_q80t_qkv_rope", wp, np_, Kd, act.data_ptr(), M, tabd.data_ptr(), n_past,
+                   posd.data_ptr() if dev_pos else None, D, q16.data_ptr(), kc.data_ptr(), vc.data_ptr(),
+                   ws_for(torch, K, Kd, sum(Ns), M).data_ptr(), sptr(torch))
+        else:
+            K.call("kcpp_rope_kv", qkv.data_ptr(), sum(Ns), None, q16.data_ptr(), kc.data_ptr(), vc.data_ptr(), M, H,
+                   HKV, D, n_past, posd.data_ptr() if dev_pos else None, tabd.data_ptr(), sptr(torch))
+        torch.cuda.synchronize()
+        outs.append([x.cpu().numpy() for x in (q16, kc, vc)])
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+    assert np.count_nonzero(outs[1][1].any(axis=1)) == M       # exactly the M positions' rows written

@@ -51,16 +51,21 @@ for i in range(it): launch(copies[i % 8])
 e1.record(); torch.cuda.synchronize()
 us = e0.elapsed_time(e1) * 1e3 / it
 b = sum(wbytes) * (2 if mode == 1 else 1)
-print(json.dumps({"shape": name, "M": M, "us": round(us, 2), "GBps": round(b / us / 1e3, 1), "ov": os.environ.get("KCPP_Q80T_SHAPE")}))
+print(json.dumps({"shape": name, "M": M, "us": round(us, 2), "GBps": round(b / us / 1e3, 1),
+                  "ov": os.environ.get("KCPP_Q80T_GLU" if mode == 1 else "KCPP_Q80T_SHAPE")}))
 '''
 
+FULL = "--full" in sys.argv          # the (S, WV) grid at M = 32; default: the built-in choice at M = 32 and 1
 for name, (Kd, Ns) in SHAPES.items():
     mode = 1 if name == "gate_up" else 0
-    for M in (32, 1):
-        for ov in [None]:
+    grid = [None]
+    if FULL:
+        grid = ["4", "8"] if mode == 1 else ["%d,%d" % (S, W) for S in (1, 2, 4, 8) for W in (2, 4, 8)]
+    for M in ((32,) if FULL else (32, 1)):
+        for ov in grid:
             env = dict(os.environ)
             if ov:
-                env["KCPP_Q80T_SHAPE"] = ov
+                env["KCPP_Q80T_GLU" if mode == 1 else "KCPP_Q80T_SHAPE"] = ov
             code = CHILD.replace("ROOT_", repr(ROOT)).replace("ARGS_", repr((name, Kd, Ns, M, mode)))
             r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
             print(r.stdout.strip().splitlines()[-1] if r.returncode == 0 else "FAIL %s %s %s" % (name, ov, r.stderr[-300:]),
