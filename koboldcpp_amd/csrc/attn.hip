@@ -209,7 +209,8 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
 // combine of k_fa_dec4's partials (m in the exp2 domain): grid (H / 2), 256 threads = 2 heads x 128 dims
 // (one Q8_K block of 256 when quantizing); thread (head, d) issues all NS partial loads of its dim (<= 64, in
 // flight together); one wave per head forms the split weights exp2(m_s - M) in LDS.
-template <bool QUANT, int NS>
+// QUANT 1: qout = the Q8_K activation; 2: the KT_Q8_0_TA activation of one token (8 Q8_0 blocks per head pair)
+template <int QUANT, int NS>
 __global__ void __launch_bounds__(256) k_fa_comb4(const float *__restrict__ part_o, const float2 *__restrict__ part_ml,
                                                   float *__restrict__ out, uint8_t *__restrict__ qout, int H,
                                                   unsigned long long *stamps, unsigned *reset) {
@@ -247,7 +248,30 @@ __global__ void __launch_bounds__(256) k_fa_comb4(const float *__restrict__ part
     const float res = ((O0 + O1) + (O2 + O3)) / s_l[hl];
     FA_STAMP(2);
     if (out) out[(int64_t)h * D + d] = res;
-    if constexpr (QUANT) {
+    if constexpr (QUANT == 2) {
+        s_res[tid] = res;
+        __syncthreads();
+        if (tid < 16) {                                  // half (tid & 1) of block tid >> 1: k_quant_q80's rounding
+            float v[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = s_res[16 * tid + k];
+            float am = 0.0f;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) am = fmaxf(am, fabsf(v[k]));
+            am = fmaxf(am, __shfl_xor(am, 1, 64));
+            const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+            uint32_t pk[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                int iv = (int)rintf(__fmul_rn(v[k], id));
+                iv = iv > 127 ? 127 : (iv < -128 ? -128 : iv);
+                pk[k >> 2] |= (uint32_t)(iv & 0xFF) << (8 * (k & 3));
+            }
+            const int64_t E = (int64_t)H * D, ib = (int64_t)pair * 8 + (tid >> 1);
+            *(uint4 *)(qout + ib * 1024 + (tid & 1) * 512) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+            if ((tid & 1) == 0) ((float *)(qout + 32 * E))[ib * 32] = h2f(f2h(am / 127.f));
+        }
+    } else if constexpr (QUANT == 1) {
         s_res[tid] = res;
         __syncthreads();
         if (tid < 16) {
@@ -276,7 +300,7 @@ static int fa4_splits(int HKV) {
 template <int G, int NS>
 static void fa4_dispatch(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
                          float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
-                         float scale, hipStream_t s) {
+                         float scale, hipStream_t s, int qkind) {
     float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
     float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
     unsigned long long *st = (unsigned long long *)g_fa_stamps;
@@ -292,22 +316,25 @@ static void fa4_dispatch(const uint16_t *q16, const uint16_t *kc, const uint16_t
     else
         hipLaunchKernelGGL((k_fa_dec4<G, false>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past,
                            n_past_dev, NS, scale, kv_ld, kv_hs, st);
-    if (qout) hipLaunchKernelGGL((k_fa_comb4<true, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, st,
-                                 (unsigned *)nullptr);
-    else hipLaunchKernelGGL((k_fa_comb4<false, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, st,
+    if (qout && qkind == 2)
+        hipLaunchKernelGGL((k_fa_comb4<2, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, st,
+                           (unsigned *)nullptr);
+    else if (qout) hipLaunchKernelGGL((k_fa_comb4<1, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, st,
+                                      (unsigned *)nullptr);
+    else hipLaunchKernelGGL((k_fa_comb4<0, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, st,
                             (unsigned *)nullptr);
 }
 
 template <int G>
 static int fa4_dispatch_ns(int NS, const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld,
                            int64_t kv_hs, float *out, void *qout, void *ws, int H, int HKV, int n_past,
-                           const int32_t *n_past_dev, float scale, hipStream_t s) {
+                           const int32_t *n_past_dev, float scale, hipStream_t s, int qkind) {
     switch (NS) {
-    case 4: fa4_dispatch<G, 4>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
-    case 8: fa4_dispatch<G, 8>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
-    case 16: fa4_dispatch<G, 16>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
-    case 32: fa4_dispatch<G, 32>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
-    case 64: fa4_dispatch<G, 64>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
+    case 4: fa4_dispatch<G, 4>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
+    case 8: fa4_dispatch<G, 8>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
+    case 16: fa4_dispatch<G, 16>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
+    case 32: fa4_dispatch<G, 32>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
+    case 64: fa4_dispatch<G, 64>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
     default: return -1;
     }
     return 0;
@@ -316,16 +343,16 @@ static int fa4_dispatch_ns(int NS, const uint16_t *q16, const uint16_t *kc, cons
 // single-token decode: k_fa_dec4 + k_fa_comb4; partials behind FA_WS_TICKETS in ws.
 static int fa4_launch(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
                       float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
-                      float scale, hipStream_t s) {
+                      float scale, hipStream_t s, int qkind = 1) {
     const int G = H / HKV;
     const int NS = fa4_splits(HKV);
     if (!qout && !out) return -1;
     int rc = -1;
     switch (G) {
-    case 1: rc = fa4_dispatch_ns<1>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
-    case 2: rc = fa4_dispatch_ns<2>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
-    case 4: rc = fa4_dispatch_ns<4>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
-    case 8: rc = fa4_dispatch_ns<8>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s); break;
+    case 1: rc = fa4_dispatch_ns<1>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
+    case 2: rc = fa4_dispatch_ns<2>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
+    case 4: rc = fa4_dispatch_ns<4>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
+    case 8: rc = fa4_dispatch_ns<8>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
     default: return -1;
     }
     if (rc) return rc;
@@ -576,6 +603,17 @@ int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max) {
     const int64_t slots = std::max<int64_t>((int64_t)T * nch, 64);
     return std::max<int64_t>(FA_WS_TICKETS + (int64_t)H * slots * (128 * 4 + 8) + (int64_t)T * H * 4 + 256,
                              kcpp_fa_split_ws_bytes(H));      // the key-split prefill (attn_mfma.hip)
+}
+
+// single-token decode attention (k_fa_dec4 + k_fa_comb4) whose combine writes the KT_Q8_0_TA activation of one token
+// (attn_output in the KT_Q8_0_T layout) instead of a separate kcpp_quantize_act; out f32 may be null.  -3: not covered
+int kcpp_flash_attn_dec_ta(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qta, void *ws,
+                           int H, int HKV, int D, int n_past, const int32_t *n_past_dev, float scale, void *stream) {
+    if (D != 128 || H % HKV || H % 2 || !qta) return -3;
+    const int G = H / HKV;
+    if (!(G == 2 || G == 4 || G == 8)) return -3;
+    return fa4_launch(q16, kc, vc, (int64_t)HKV * 128, 128, out, qta, ws, H, HKV, n_past, n_past_dev, scale,
+                      (hipStream_t)stream, 2);
 }
 
 // out f32 [T][H][D] (may be null), qout Q8_K act [T][H*D] (may be null), ws from kcpp_fa_workspace_bytes

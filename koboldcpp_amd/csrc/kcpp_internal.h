@@ -83,6 +83,9 @@ extern "C" int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16
                                                void *qta, void *ws, int T, int H, int HKV, int D, int n_past, float scale,
                                                void *stream);
 extern "C" int64_t kcpp_fa_split_ws_bytes(int H);
+extern "C" int kcpp_flash_attn_dec_ta(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qta,
+                                      void *ws, int H, int HKV, int D, int n_past, const int32_t *n_past_dev, float scale,
+                                      void *stream);
 // decode mat-vec over the row-major RS layouts (gemv_rs.hip); -3 = not covered
 extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
 extern "C" int kcpp_rs_supported(int type, int64_t K);

@@ -1160,9 +1160,11 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
         // Q8_0 tile layout, ubatch > 16: attention writes attn_output's KT_Q8_0_TA activation itself (keys split
         // over the grid for short ubatches)
         bool attn_q = false;
-        if (m->q80t && m->lanes.empty() && !kvq && !m->fa_exact && !posp && T > 16 && t[4].type == KT_Q8_0_T) {
-            const int rc = kcpp_flash_attn_prefill_mfma_ex(m->q16, L.kc, L.vc, nullptr, m->act, m->fa_ws, T, (int)H,
-                                                           (int)HKV, (int)D, n_past, kq_scale, s);
+        if (m->q80t && m->lanes.empty() && !kvq && !m->fa_exact && t[4].type == KT_Q8_0_T && (T == 1 || (T > 16 && !posp))) {
+            const int rc = T == 1 ? kcpp_flash_attn_dec_ta(m->q16, L.kc, L.vc, nullptr, m->act, m->fa_ws, (int)H, (int)HKV,
+                                                           (int)D, n_past, posp, kq_scale, s)
+                                  : kcpp_flash_attn_prefill_mfma_ex(m->q16, L.kc, L.vc, nullptr, m->act, m->fa_ws, T,
+                                                                    (int)H, (int)HKV, (int)D, n_past, kq_scale, s);
             if (rc != 0 && rc != -3) return rc;
             attn_q = rc == 0;
         }

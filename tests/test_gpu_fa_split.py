@@ -85,3 +85,31 @@ def test_unsplit_ta_epilogue(env):
            ws.data_ptr(), T, H, HKV, D, n_past, 0.088, sptr(torch))
     torch.cuda.synchronize()
     assert torch.equal(qta, want)
+
+
+@pytest.mark.parametrize("n_past,dev", [(3840, False), (100, True)])
+def test_decode_ta_combine(env, n_past, dev):
+    """single-token decode with the combine writing the KT_Q8_0_TA activation: out bit-identical to the plain pair,
+    TA bytes == kcpp_quantize_act(KT_Q8_0_TA) of that output"""
+    import ctypes
+    torch, K = env
+    H, HKV, D, n_ctx = 32, 8, 128, 4096
+    E = H * D
+    g = torch.Generator(device="cuda").manual_seed(n_past)
+    q16 = torch.randn(1, H, D, device="cuda", generator=g).half()
+    kc = torch.randn(n_ctx, HKV * D, device="cuda", generator=g).half()
+    vc = torch.randn(n_ctx, HKV * D, device="cuda", generator=g).half()
+    ws = torch.zeros(int(K.raw().kcpp_fa_workspace_bytes(16, H, n_ctx)), dtype=torch.uint8, device="cuda")
+    npd = torch.tensor([n_past], dtype=torch.int32, device="cuda")
+    ref = torch.empty(1, E, device="cuda")
+    K.call("kcpp_flash_attn", q16.data_ptr(), kc.data_ptr(), vc.data_ptr(), ref.data_ptr(), None, ws.data_ptr(), 1, H,
+           HKV, D, 0 if dev else n_past, npd.data_ptr() if dev else None, n_ctx, 0.088, 0, sptr(torch))
+    out = torch.empty(1, E, device="cuda")
+    qta = torch.zeros(K.act_bytes(K.Q8_0_T, E, 1), dtype=torch.uint8, device="cuda")
+    K.call("kcpp_flash_attn_dec_ta", q16.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(), qta.data_ptr(),
+           ws.data_ptr(), H, HKV, D, 0 if dev else n_past, npd.data_ptr() if dev else None, 0.088, sptr(torch))
+    want = torch.zeros_like(qta)
+    K.call("kcpp_quantize_act", K.Q8_0_TA, ref.data_ptr(), E, want.data_ptr(), E, 1, sptr(torch))
+    torch.cuda.synchronize()
+    assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+    assert torch.equal(qta, want)
