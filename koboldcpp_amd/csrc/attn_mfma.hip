@@ -26,6 +26,10 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 #define FM_Q 16          // queries per workgroup
 #define FM_K 64          // keys per tile
+#define FM_SPLIT_T 64    // key-split prefill (k_fa_prefill_mfma3<8, true>): ubatches up to this many tokens,
+#define FM_SPLITS 32     // at most this many key splits
+#define FM_PQ 132        // split partial of one (query, head): 128 dims, m, l, pad
+#define FM_PS (16 * FM_PQ)
 #define FM_KP 136        // K tile row pitch (halves): 128 + 8 -> rows 272 B apart (bank spread)
 #define FM_VP 72         // V^T tile row pitch (halves): 64 + 8
 
@@ -313,11 +317,13 @@ __device__ __forceinline__ int fa_swz(int row, int c) { return row * 16 + (c ^ (
 // running max are v3's, and their (l, O) partial sums are added at the end (only the f32 summation order differs).
 //
 // SPL (short ubatches, BASELINE config 3's 32 tokens: (T / 16) x HKV workgroups alone leave most CUs idle): the grid
-// also splits the keys, ch tiles per workgroup; each split publishes its unnormalised (O, m, l) per query and head
-// (write-through stores, drained), takes a ticket per (query block, kv head), and the last arriver merges the nsp
-// splits in split order (deterministic whatever the arrival order) -- MI355X_MICROARCH.md hand-off table, row 1.
-// qta (optional): the output quantized straight to the KT_Q8_0_TA activation of attn_output (KT_Q8_0_T weights):
-// a head's 128 dims are 4 whole Q8_0 blocks, so no other workgroup's output is needed (k_quant_q80's rounding).
+// also splits the keys, ch tiles per workgroup; each split stores its unnormalised (O, m, l) per query and head and
+// k_fa_split_merge (next launch) merges the splits in split order.  (An in-launch merge by the last-arriving split
+// -- write-through partials, a ticket, device-coherent loads -- measured 15-30 us per layer at 2-16 splits against
+// this pair's: every coherent round trip went through HBM.)
+// qta (optional, unsplit): the output quantized straight to the KT_Q8_0_TA activation of attn_output (KT_Q8_0_T
+// weights): a head's 128 dims are 4 whole Q8_0 blocks, so no other workgroup's output is needed (k_quant_q80's
+// rounding); split launches quantize in the merge.
 template <int NW, bool SPL>
 __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t *__restrict__ q16,
                                                                 const uint16_t *__restrict__ kc,
@@ -548,48 +554,14 @@ __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t 
         }
     }
     if constexpr (SPL) {
-        constexpr int PS = 16 * 130;                      // one head's partial: [query][128 dims + m + l]
-        const int slot = qb * HKV + hk, nsp = (ntile + ch - 1) / ch;
-        float *pb = part + (int64_t)slot * nsp_grid * 4 * PS + (wave & 3) * PS + ql * 130;
+        // publish this split's unnormalised (O, m, l) per query and head; k_fa_split_merge (the next launch) merges
         if (hf == 0) {
-            float *pp = pb + (int64_t)sp * 4 * PS;
+            float *pp = part + (((int64_t)(qb * HKV + hk) * nsp_grid + sp) * 4 + (wave & 3)) * FM_PS + ql * FM_PQ;
 #pragma unroll
-            for (int db = 0; db < 8; ++db)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    __hip_atomic_store(pp + 16 * db + 4 * g + r, o[db][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (g == 0) {
-                __hip_atomic_store(pp + 128, m_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(pp + 129, l_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            for (int db = 0; db < 8; ++db) *(float4 *)(pp + 16 * db + 4 * g) = make_float4(o[db][0], o[db][1], o[db][2], o[db][3]);
+            if (g == 0) *(float4 *)(pp + 128) = make_float4(m_run, l_run, 0.0f, 0.0f);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        __shared__ unsigned s_old;
-        if (tid == 0) s_old = __hip_atomic_fetch_add(tick + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        if (s_old != (unsigned)(nsp - 1)) return;         // not the last split of this (query block, kv head)
-        if (tid == 0) __hip_atomic_store(tick + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (NW == 8 && hf == 1) return;
-        float mm = -INFINITY;
-        for (int k = 0; k < nsp; ++k)
-            mm = fmaxf(mm, __hip_atomic_load(pb + (int64_t)k * 4 * PS + 128, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        l_run = 0.0f;
-#pragma unroll
-        for (int db = 0; db < 8; ++db) o[db] = f4{0.f, 0.f, 0.f, 0.f};
-        for (int k = 0; k < nsp; ++k) {                   // split order
-            const float *pk = pb + (int64_t)k * 4 * PS;
-            const float mk = __hip_atomic_load(pk + 128, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const float lk = __hip_atomic_load(pk + 129, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const float ak = mk == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(mk - mm);
-            l_run = l_run + lk * ak;
-#pragma unroll
-            for (int db = 0; db < 8; ++db)
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    o[db][r] = o[db][r] + __hip_atomic_load(pk + 16 * db + 4 * g + r, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT) * ak;
-        }
+        return;
     }
     if (qi >= T) return;                                  // (all four lanes of a query leave together)
     const float inv = 1.0f / l_run;
@@ -638,12 +610,99 @@ extern "C" int kcpp_fa_prefill_set_variant(int v) {
     return old;
 }
 
-// the key-split variant's workspace (kcpp_fa_workspace_bytes reserves it): tickets in the 2 KB header, then
-// [query block][kv head][split < FM_SPLITS][4 heads][16 queries][130] partials for T <= FM_SPLIT_T
-#define FM_SPLIT_T 64
-#define FM_SPLITS 32
+// merge of the key splits (SPL): one workgroup per (query block, kv head, head of the group), thread = (query,
+// 8-dim chunk); the splits' (m, l) and O chunks loaded together, weights exp2(m_s - max), summed in split order;
+// out f32 and / or the KT_Q8_0_TA activation (a Q8_0 block = 4 threads' 32 dims, k_quant_q80's rounding)
+__global__ void __launch_bounds__(256) k_fa_split_merge(const float *__restrict__ part, float *__restrict__ out,
+                                                        uint8_t *__restrict__ qta, int T, int H, int HKV, int n_past,
+                                                        int ch, int nsp_grid) {
+    constexpr int D = 128, G = 4;
+    const int slot = blockIdx.x >> 2, mh = blockIdx.x & 3, qb = slot / HKV, hk = slot % HKV;
+    const int tid = threadIdx.x, mq = tid >> 4, dc = tid & 15;
+    const int q0 = qb * FM_Q;
+    const int n_keys = n_past + min(q0 + FM_Q, T);
+    const int nsp = ((n_keys + FM_K - 1) / FM_K + ch - 1) / ch;
+    const float *pm = part + ((int64_t)slot * nsp_grid * 4 + mh) * FM_PS + mq * FM_PQ;
+    auto at = [&](int k) { return pm + (int64_t)min(k, nsp - 1) * 4 * FM_PS; };   // branch-free: clamped + weight 0
+    float mk[FM_SPLITS], lk[FM_SPLITS];
+#pragma unroll
+    for (int k = 0; k < FM_SPLITS; ++k) {
+        const float2 ml = *(const float2 *)(at(k) + 128);
+        mk[k] = k < nsp ? ml.x : -INFINITY;
+        lk[k] = k < nsp ? ml.y : 0.0f;
+    }
+    float4 v[8][2];
+    auto chunk = [&](int k0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) v[j][c] = *(const float4 *)(at(k0 + j) + 8 * dc + 4 * c);
+    };
+    chunk(0);
+    float mm = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < FM_SPLITS; ++k) mm = fmaxf(mm, mk[k]);
+    float lsum = 0.0f;
+#pragma unroll
+    for (int k = 0; k < FM_SPLITS; ++k) {
+        mk[k] = mk[k] == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(mk[k] - mm);
+        lsum = lsum + lk[k] * mk[k];
+    }
+    float ov[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ov[e] = 0.0f;
+#pragma unroll
+    for (int k0 = 0; k0 < FM_SPLITS; k0 += 8) {
+        if (k0 >= nsp) break;
+        if (k0 > 0) chunk(k0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const float w = mk[k0 + j];
+                ov[4 * c] = ov[4 * c] + v[j][c].x * w;
+                ov[4 * c + 1] = ov[4 * c + 1] + v[j][c].y * w;
+                ov[4 * c + 2] = ov[4 * c + 2] + v[j][c].z * w;
+                ov[4 * c + 3] = ov[4 * c + 3] + v[j][c].w * w;
+            }
+    }
+    const int qi = q0 + mq, h = hk * G + mh;
+    if (qi >= T) return;                                  // (a query's 16 threads leave together)
+    const float inv = 1.0f / lsum;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ov[e] = ov[e] * inv;
+    if (out) {
+        float4 *op = (float4 *)(out + ((int64_t)qi * H + h) * D + 8 * dc);
+        op[0] = make_float4(ov[0], ov[1], ov[2], ov[3]);
+        op[1] = make_float4(ov[4], ov[5], ov[6], ov[7]);
+    }
+    if (qta) {
+        const int64_t E = (int64_t)H * D, nb = E / 32, ng = (T + 31) / 32, grp = qi >> 5, tok = qi & 31;
+        float am = 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) am = fmaxf(am, fabsf(ov[e]));
+        am = fmaxf(am, __shfl_xor(am, 1, 64));
+        am = fmaxf(am, __shfl_xor(am, 2, 64));
+        const float id = (am != 0.0f) ? 127.f / am : 0.0f;
+        uint32_t pk[2] = {0u, 0u};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            int iv = (int)rintf(__fmul_rn(ov[e], id));
+            iv = iv > 127 ? 127 : (iv < -128 ? -128 : iv);
+            pk[e >> 2] |= (uint32_t)(iv & 0xFF) << (8 * (e & 3));
+        }
+        // dims 8 dc .. + 7 of the head = block 2 h*2.. : element 8 (dc & 3) + e of block dc >> 2 -> half (dc & 3) >> 1,
+        // bytes 8 (dc & 1) + e
+        const int64_t ib = (int64_t)h * 4 + (dc >> 2);
+        *(uint2 *)(qta + (grp * nb + ib) * 1024 + ((dc & 3) >> 1) * 512 + tok * 16 + 8 * (dc & 1)) = make_uint2(pk[0], pk[1]);
+        if ((dc & 3) == 0) ((float *)(qta + ng * 32 * E))[(grp * nb + ib) * 32 + tok] = h2f(f2h(am / 127.f));
+    }
+}
+
+// the key-split variant's workspace (kcpp_fa_workspace_bytes reserves it, after the 2 KB header):
+// [query block][kv head][split < FM_SPLITS][4 heads][16 queries][FM_PQ] partials for T <= FM_SPLIT_T
 extern "C" int64_t kcpp_fa_split_ws_bytes(int H) {
-    return KCPP_FA_WS_HEADER + (int64_t)(FM_SPLIT_T / FM_Q) * (H / 4) * FM_SPLITS * 4 * 16 * 130 * 4;
+    return KCPP_FA_WS_HEADER + (int64_t)(FM_SPLIT_T / FM_Q) * (H / 4) * FM_SPLITS * 4 * FM_PS * 4;
 }
 
 extern "C" int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out,
@@ -660,9 +719,12 @@ extern "C" int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16
         const int ch = (ntile + want - 1) / want;
         const int nsp = (ntile + ch - 1) / ch;
         if (nsp > 1) {
+            float *part = (float *)((uint8_t *)ws + KCPP_FA_WS_HEADER);
             hipLaunchKernelGGL((k_fa_prefill_mfma3<8, true>), dim3(nb0 * nsp), dim3(512), 0, (hipStream_t)stream, q16, kc,
-                               vc, out, T, H, HKV, n_past, scale, (float *)((uint8_t *)ws + KCPP_FA_WS_HEADER),
-                               (unsigned *)ws, ch, nsp, (uint8_t *)qta);
+                               vc, out, T, H, HKV, n_past, scale, part, (unsigned *)nullptr, ch, nsp, (uint8_t *)nullptr);
+            KCPP_CHECK(hipGetLastError());
+            hipLaunchKernelGGL(k_fa_split_merge, dim3(nb0 * 4), dim3(256), 0, (hipStream_t)stream, part, out, (uint8_t *)qta,
+                               T, H, HKV, n_past, ch, nsp);
             KCPP_CHECK(hipGetLastError());
             return 0;
         }

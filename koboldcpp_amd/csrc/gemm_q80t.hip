@@ -23,11 +23,8 @@
 
 #include <algorithm>
 
-#ifndef Q80T_FMA
-#define Q80T_FMA 1
-#endif
 #ifndef Q80T_RING
-#define Q80T_RING 0              // 1: branch-free Q80T_P-deep weight ring (tools/q80t_sweep.py variants)
+#define Q80T_RING 2              // loop per mode (bit MODE set: the branch-free Q80T_P-deep ring): tools/q80t_sweep.py
 #endif
 #ifndef Q80T_P
 #define Q80T_P 2                 // weight units in flight per wave (even: the x pair alternates with the ring slot)
@@ -73,7 +70,7 @@ struct Q80TArgs {
     int64_t nq, nkv;
 };
 
-template <int MODE, int WV>
+template <int MODE, int WV, bool RING = ((Q80T_RING >> MODE) & 1) != 0>
 __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int tid = threadIdx.x, lane = tid & 63, kg = lane >> 5;
@@ -106,146 +103,135 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
     const int64_t ng = (a.M + 31) / 32;
     const uint8_t *wq = W + tl * nb * 1024 + lane * 16;              // block b at + b * 1024
     const uint8_t *wd = W + Ns * K + tl * nu * 256 + (lane & 31) * 8;   // unit u at + u * 256
-#if Q80T_RING
-    // lanes of tokens past M read their k-half's token-0 bytes (cache lines the live lanes fetch anyway: at M = 1 the
-    // wave moves 32 B of activation per block, not 1 KiB) and zero them
-    const bool xlive = z * 32 + (lane & 31) < a.M;
-    const uint8_t *aq = a.act + z * nb * 1024 + (xlive ? lane : (lane & 32)) * 16;
-    const int xm = xlive ? -1 : 0;
-    // weight fragments Q80T_P units (4 blocks each) ahead of the MFMA, activation fragments (L2-resident) one unit
-    // ahead; the loop body is branch-free (unit indices clamped to the wave's last unit, a clamped unit's scale zeroed)
-    // so the per-block MFMA + epilogue stays one scheduling region with one accumulator live
-    struct WUnit { i32x4 w[4]; uint2 d; };
-    struct XUnit { i32x4 x[4]; };
-    const int64_t ulast = wu1 - 1;
-    auto loadw = [&](int64_t u, WUnit &U) {
-        u = u < ulast ? u : ulast;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) U.w[i] = ld_frag_nt(wq + (4 * u + i) * 1024);
-        U.d = *(const uint2 *)(wd + u * 256);
-    };
-    auto loadx = [&](int64_t u, XUnit &X) {
-        u = u < ulast ? u : ulast;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) X.x[i] = *(const i32x4 *)(aq + (4 * u + i) * 1024) & xm;
-    };
     float tot[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) tot[r] = 0.0f;
-    auto comp = [&](int64_t u, const WUnit &U, const XUnit &X) {
-        const bool live = u <= ulast;
-        u = live ? u : ulast;
-        const float dw[4] = {live ? h2f((uint16_t)(U.d.x & 0xFFFF)) : 0.0f, live ? h2f((uint16_t)(U.d.x >> 16)) : 0.0f,
-                             live ? h2f((uint16_t)(U.d.y & 0xFFFF)) : 0.0f, live ? h2f((uint16_t)(U.d.y >> 16)) : 0.0f};
+    if constexpr (RING) {
+        // lanes of tokens past M read their k-half's token-0 bytes (cache lines the live lanes fetch anyway: at M = 1 the
+        // wave moves 32 B of activation per block, not 1 KiB) and zero them
+        const bool xlive = z * 32 + (lane & 31) < a.M;
+        const uint8_t *aq = a.act + z * nb * 1024 + (xlive ? lane : (lane & 32)) * 16;
+        const int xm = xlive ? -1 : 0;
+        // weight fragments Q80T_P units (4 blocks each) ahead of the MFMA, activation fragments (L2-resident) one unit
+        // ahead; the loop body is branch-free (unit indices clamped to the wave's last unit, a clamped unit's scale zeroed)
+        // so the per-block MFMA + epilogue stays one scheduling region with one accumulator live
+        struct WUnit { i32x4 w[4]; uint2 d; };
+        struct XUnit { i32x4 x[4]; };
+        const int64_t ulast = wu1 - 1;
+        auto loadw = [&](int64_t u, WUnit &U) {
+            u = u < ulast ? u : ulast;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            i32x16 acc;
+            for (int i = 0; i < 4; ++i) U.w[i] = ld_frag_nt(wq + (4 * u + i) * 1024);
+            U.d = *(const uint2 *)(wd + u * 256);
+        };
+        auto loadx = [&](int64_t u, XUnit &X) {
+            u = u < ulast ? u : ulast;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0;
-            i32x4 xv = X.x[i], wv = U.w[i];
-            asm volatile("" : "+v"(xv), "+v"(wv));   // block i's MFMA not hoisted above block i-1's epilogue
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(xv, wv, acc, 0, 0, 0);
-            const float *sd = dxs + ((u - u0) * 4 + i) * 32 + 4 * kg;
+            for (int i = 0; i < 4; ++i) X.x[i] = *(const i32x4 *)(aq + (4 * u + i) * 1024) & xm;
+        };
+        auto comp = [&](int64_t u, const WUnit &U, const XUnit &X) {
+            const bool live = u <= ulast;
+            u = live ? u : ulast;
+            const float dw[4] = {live ? h2f((uint16_t)(U.d.x & 0xFFFF)) : 0.0f, live ? h2f((uint16_t)(U.d.x >> 16)) : 0.0f,
+                                 live ? h2f((uint16_t)(U.d.y & 0xFFFF)) : 0.0f, live ? h2f((uint16_t)(U.d.y >> 16)) : 0.0f};
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float4 d4 = *(const float4 *)(sd + 8 * c);
-                const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+            for (int i = 0; i < 4; ++i) {
+                i32x16 acc;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-#if Q80T_FMA
-                    tot[4 * c + e] = fmaf((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e]), tot[4 * c + e]);
-#else
-                    tot[4 * c + e] = __fadd_rn(tot[4 * c + e], __fmul_rn((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e])));
-#endif
+                for (int r = 0; r < 16; ++r) acc[r] = 0;
+                i32x4 xv = X.x[i], wv = U.w[i];
+                asm volatile("" : "+v"(xv), "+v"(wv));   // block i's MFMA not hoisted above block i-1's epilogue
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(xv, wv, acc, 0, 0, 0);
+                const float *sd = dxs + ((u - u0) * 4 + i) * 32 + 4 * kg;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 d4 = *(const float4 *)(sd + 8 * c);
+                    const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        tot[4 * c + e] = fmaf((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e]), tot[4 * c + e]);
+                    }
                 }
+#pragma unroll
+                for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(tot[r]));   // ... and its epilogue done here: one
+                asm volatile("" ::: "memory");                                   // accumulator live at a time
             }
+        };
+        WUnit wr[Q80T_P];
+        XUnit xa, xb;
+        if (wu0 < wu1) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(tot[r]));   // ... and its epilogue done here: one
-            asm volatile("" ::: "memory");                                   // accumulator live at a time
+            for (int i = 0; i < Q80T_P; ++i) loadw(wu0 + i, wr[i]);
+            loadx(wu0, xa);
         }
-    };
-    WUnit wr[Q80T_P];
-    XUnit xa, xb;
-    if (wu0 < wu1) {
-#pragma unroll
-        for (int i = 0; i < Q80T_P; ++i) loadw(wu0 + i, wr[i]);
-        loadx(wu0, xa);
-    }
-    {   // the token scales go to LDS while the first units' fragments are in flight
-        const float4 *src = (const float4 *)(a.act + ng * 32 * K) + (z * nb + 4 * u0) * 8;
-        float4 *dst = (float4 *)dxs;
-        for (int64_t i = tid; i < (u1 - u0) * 32; i += 64 * WV) dst[i] = src[i];
-    }
-    __syncthreads();
-    for (int64_t u = wu0; u < wu1; u += Q80T_P) {
-#pragma unroll
-        for (int i = 0; i < Q80T_P; ++i) {     // unrolled: ring slot i and the x pair are static registers
-            XUnit &xc = (i & 1) ? xb : xa, &xn = (i & 1) ? xa : xb;
-            loadx(u + i + 1, xn);
-            asm volatile("" ::: "memory");       // loads stay where they are issued (in flight across the compute)
-            comp(u + i, wr[i], xc);
-            loadw(u + i + Q80T_P, wr[i]);
-            asm volatile("" ::: "memory");
+        {   // the token scales go to LDS while the first units' fragments are in flight
+            const float4 *src = (const float4 *)(a.act + ng * 32 * K) + (z * nb + 4 * u0) * 8;
+            float4 *dst = (float4 *)dxs;
+            for (int64_t i = tid; i < (u1 - u0) * 32; i += 64 * WV) dst[i] = src[i];
         }
-    }
-#else
-    const uint8_t *aq = a.act + z * nb * 1024 + lane * 16;
-    // lanes of tokens past M read no activation (at M = 1 the wave fetches 32 B of it per block, not 1 KiB)
-    const bool xlive = z * 32 + (lane & 31) < a.M;
-    struct Unit { i32x4 w[4], x[4]; uint2 d; };
-    auto load = [&](int64_t u, Unit &U) {
+        __syncthreads();
+        for (int64_t u = wu0; u < wu1; u += Q80T_P) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            U.w[i] = ld_frag_nt(wq + (4 * u + i) * 1024);
-            U.x[i] = xlive ? *(const i32x4 *)(aq + (4 * u + i) * 1024) : i32x4{0, 0, 0, 0};
-        }
-        U.d = *(const uint2 *)(wd + u * 256);
-    };
-    float tot[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) tot[r] = 0.0f;
-    auto comp = [&](int64_t u, const Unit &U) {
-        const float dw[4] = {h2f((uint16_t)(U.d.x & 0xFFFF)), h2f((uint16_t)(U.d.x >> 16)), h2f((uint16_t)(U.d.y & 0xFFFF)),
-                             h2f((uint16_t)(U.d.y >> 16))};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            i32x16 acc;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[r] = 0;
-            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(U.x[i], U.w[i], acc, 0, 0, 0);
-            const float *sd = dxs + ((u - u0) * 4 + i) * 32 + 4 * kg;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float4 d4 = *(const float4 *)(sd + 8 * c);
-                const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-#if Q80T_FMA
-                    tot[4 * c + e] = fmaf((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e]), tot[4 * c + e]);
-#else
-                    tot[4 * c + e] = __fadd_rn(tot[4 * c + e], __fmul_rn((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e])));
-#endif
-                }
+            for (int i = 0; i < Q80T_P; ++i) {     // unrolled: ring slot i and the x pair are static registers
+                XUnit &xc = (i & 1) ? xb : xa, &xn = (i & 1) ? xa : xb;
+                loadx(u + i + 1, xn);
+                asm volatile("" ::: "memory");       // loads stay where they are issued (in flight across the compute)
+                comp(u + i, wr[i], xc);
+                loadw(u + i + Q80T_P, wr[i]);
+                asm volatile("" ::: "memory");
             }
         }
-    };
-    Unit ua, ub;
-    if (wu0 < wu1) load(wu0, ua);
-    if (wu0 + 1 < wu1) load(wu0 + 1, ub);
-    {   // the token scales go to LDS while the first two units' fragments are in flight
-        const float4 *src = (const float4 *)(a.act + ng * 32 * K) + (z * nb + 4 * u0) * 8;
-        float4 *dst = (float4 *)dxs;
-        for (int64_t i = tid; i < (u1 - u0) * 32; i += 64 * WV) dst[i] = src[i];
+    } else {
+        const uint8_t *aq = a.act + z * nb * 1024 + lane * 16;
+        // lanes of tokens past M read no activation (at M = 1 the wave fetches 32 B of it per block, not 1 KiB)
+        const bool xlive = z * 32 + (lane & 31) < a.M;
+        struct Unit { i32x4 w[4], x[4]; uint2 d; };
+        auto load = [&](int64_t u, Unit &U) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                U.w[i] = ld_frag_nt(wq + (4 * u + i) * 1024);
+                U.x[i] = xlive ? *(const i32x4 *)(aq + (4 * u + i) * 1024) : i32x4{0, 0, 0, 0};
+            }
+            U.d = *(const uint2 *)(wd + u * 256);
+        };
+        auto comp = [&](int64_t u, const Unit &U) {
+            const float dw[4] = {h2f((uint16_t)(U.d.x & 0xFFFF)), h2f((uint16_t)(U.d.x >> 16)), h2f((uint16_t)(U.d.y & 0xFFFF)),
+                                 h2f((uint16_t)(U.d.y >> 16))};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                i32x16 acc;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[r] = 0;
+                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(U.x[i], U.w[i], acc, 0, 0, 0);
+                const float *sd = dxs + ((u - u0) * 4 + i) * 32 + 4 * kg;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 d4 = *(const float4 *)(sd + 8 * c);
+                    const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        tot[4 * c + e] = fmaf((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e]), tot[4 * c + e]);
+                    }
+                }
+            }
+        };
+        Unit ua, ub;
+        if (wu0 < wu1) load(wu0, ua);
+        if (wu0 + 1 < wu1) load(wu0 + 1, ub);
+        {   // the token scales go to LDS while the first two units' fragments are in flight
+            const float4 *src = (const float4 *)(a.act + ng * 32 * K) + (z * nb + 4 * u0) * 8;
+            float4 *dst = (float4 *)dxs;
+            for (int64_t i = tid; i < (u1 - u0) * 32; i += 64 * WV) dst[i] = src[i];
+        }
+        __syncthreads();
+        for (int64_t u = wu0; u < wu1; u += 2) {
+            if (u > wu0 && u + 1 < wu1) load(u + 1, ub);
+            comp(u, ua);
+            if (u + 1 >= wu1) break;
+            if (u + 2 < wu1) load(u + 2, ua);
+            comp(u + 1, ub);
+        }
     }
-    __syncthreads();
-    for (int64_t u = wu0; u < wu1; u += 2) {
-        if (u > wu0 && u + 1 < wu1) load(u + 1, ub);
-        comp(u, ua);
-        if (u + 1 >= wu1) break;
-        if (u + 2 < wu1) load(u + 2, ua);
-        comp(u + 1, ub);
-    }
-#endif
     // waves summed in wave order: element (token t, row j) of lane l, r: t = (r & 3) + 8 (r >> 2) + 4 (l >> 5), j = l & 31
 #pragma unroll
     for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = tot[r];

@@ -59,6 +59,24 @@ __device__ __forceinline__ uint32_t iq4nl_lut4(uint32_t x) {
     return (hi & m) | (lo & ~m);
 }
 __device__ __forceinline__ uint16_t f2h(float f) { return __half_as_ushort(__float2half_rn(f)); }
+
+// In-launch hand-off payloads as 16-byte vector accesses with the agent-scope (sc1) policy that
+// __hip_atomic_{store,load}(..., __HIP_MEMORY_SCOPE_AGENT) puts on single dwords (write-through past the XCD's L2 /
+// read from the device-coherent level): one b128 instruction instead of four dword ones.  base must be
+// wave-uniform (a buffer resource), off in bytes (< 2 GiB).  MI355X_MICROARCH.md hand-off table, row 1.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t kcpp_rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 kcpp_ld_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+__device__ __forceinline__ void kcpp_st_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, float4 v) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 u = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+    __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 16);
+}
 // f32 -> f16 of an already-rounded f32 value.  Without the register barrier the backend folds f2h(a * b) into
 // v_fma_mixlo_f16(a, b, 0) -- ONE rounding of the exact product, and +0 for a -0 product -- which is not the
 // reference's GGML_FP32_TO_FP16(a * b) (two roundings, sign kept); -ffp-contract=off does not stop it.

@@ -1160,7 +1160,8 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
         // Q8_0 tile layout, ubatch > 16: attention writes attn_output's KT_Q8_0_TA activation itself (keys split
         // over the grid for short ubatches)
         bool attn_q = false;
-        if (m->q80t && m->lanes.empty() && !kvq && !m->fa_exact && t[4].type == KT_Q8_0_T && (T == 1 || (T > 16 && !posp))) {
+        // (row-split lanes too: attention is not split, and wo's lanes read the same activation)
+        if (m->q80t && !kvq && !m->fa_exact && t[4].type == KT_Q8_0_T && (T == 1 || (T > 16 && !posp))) {
             const int rc = T == 1 ? kcpp_flash_attn_dec_ta(m->q16, L.kc, L.vc, nullptr, m->act, m->fa_ws, (int)H, (int)HKV,
                                                            (int)D, n_past, posp, kq_scale, s)
                                   : kcpp_flash_attn_prefill_mfma_ex(m->q16, L.kc, L.vc, nullptr, m->act, m->fa_ws, T,

@@ -51,7 +51,7 @@ def test_split_prefill_vs_unsplit_and_ta(env, T, n_past):
         qtas.append(qta.cpu().numpy())
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
     assert np.array_equal(qtas[0], qtas[1])
-    assert not ws[:2048].any().item()                       # tickets back at zero
+    assert not ws[:2048].any().item()                       # header untouched
     r = ref.cpu().numpy()
     err = np.abs(outs[0] - r).max()
     print("T %d n_past %d: split vs unsplit max |d| %.3g (max |o| %.3g)" % (T, n_past, err, np.abs(r).max()))
