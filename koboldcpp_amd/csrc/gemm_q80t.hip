@@ -26,6 +26,9 @@
 #ifndef Q80T_RING
 #define Q80T_RING 2              // loop per mode (bit MODE set: the branch-free Q80T_P-deep ring): tools/q80t_sweep.py
 #endif
+#ifndef Q80T_PIPE
+#define Q80T_PIPE 0              // ring loop: the next block's MFMA issued before this block's epilogue
+#endif
 #ifndef Q80T_P
 #define Q80T_P 2                 // weight units in flight per wave (even: the x pair alternates with the ring slot)
 #endif
@@ -134,14 +137,26 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
             u = live ? u : ulast;
             const float dw[4] = {live ? h2f((uint16_t)(U.d.x & 0xFFFF)) : 0.0f, live ? h2f((uint16_t)(U.d.x >> 16)) : 0.0f,
                                  live ? h2f((uint16_t)(U.d.y & 0xFFFF)) : 0.0f, live ? h2f((uint16_t)(U.d.y >> 16)) : 0.0f};
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
+            auto mf = [&](int i) {
                 i32x16 acc;
 #pragma unroll
                 for (int r = 0; r < 16; ++r) acc[r] = 0;
                 i32x4 xv = X.x[i], wv = U.w[i];
-                asm volatile("" : "+v"(xv), "+v"(wv));   // block i's MFMA not hoisted above block i-1's epilogue
-                acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(xv, wv, acc, 0, 0, 0);
+                asm volatile("" : "+v"(xv), "+v"(wv));   // not hoisted above the previous block's epilogue
+                return __builtin_amdgcn_mfma_i32_32x32x32_i8(xv, wv, acc, 0, 0, 0);
+            };
+#if Q80T_PIPE
+            i32x16 accs[2];
+            accs[0] = mf(0);
+#endif
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+#if Q80T_PIPE
+                if (i < 3) accs[(i + 1) & 1] = mf(i + 1);   // block i + 1's MFMA runs under block i's epilogue
+                const i32x16 acc = accs[i & 1];
+#else
+                const i32x16 acc = mf(i);
+#endif
                 const float *sd = dxs + ((u - u0) * 4 + i) * 32 + 4 * kg;
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
