@@ -42,6 +42,7 @@ namespace {
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ i32x4 ld_frag_nt(const uint8_t *p) {   // weights: read once per launch (nt-weights)
     const v4u x = __builtin_nontemporal_load((const v4u *)p);
@@ -121,6 +122,9 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
         struct WUnit { i32x4 w[4]; uint2 d; };
         struct XUnit { i32x4 x[4]; };
         const int64_t ulast = wu1 - 1;
+        f2 tot2[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) tot2[r] = f2{0.0f, 0.0f};
         auto loadw = [&](int64_t u, WUnit &U) {
             u = u < ulast ? u : ulast;
 #pragma unroll
@@ -158,18 +162,18 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
                 const i32x16 acc = mf(i);
 #endif
                 const float *sd = dxs + ((u - u0) * 4 + i) * 32 + 4 * kg;
+                const f2 dw2 = {dw[i], dw[i]};
 #pragma unroll
-                for (int c = 0; c < 4; ++c) {
+                for (int c = 0; c < 4; ++c) {                // packed f32 pairs: v_pk_mul_f32 + v_pk_fma_f32
                     const float4 d4 = *(const float4 *)(sd + 8 * c);
-                    const float dv[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        tot[4 * c + e] = fmaf((float)acc[4 * c + e], __fmul_rn(dw[i], dv[e]), tot[4 * c + e]);
-                    }
+                    const f2 s0 = dw2 * f2{d4.x, d4.y}, s1 = dw2 * f2{d4.z, d4.w};
+                    tot2[2 * c] = __builtin_elementwise_fma(f2{(float)acc[4 * c], (float)acc[4 * c + 1]}, s0, tot2[2 * c]);
+                    tot2[2 * c + 1] =
+                        __builtin_elementwise_fma(f2{(float)acc[4 * c + 2], (float)acc[4 * c + 3]}, s1, tot2[2 * c + 1]);
                 }
 #pragma unroll
-                for (int r = 0; r < 16; ++r) asm volatile("" : "+v"(tot[r]));   // ... and its epilogue done here: one
-                asm volatile("" ::: "memory");                                   // accumulator live at a time
+                for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(tot2[r]));  // ... and its epilogue done here: one
+                asm volatile("" ::: "memory");                                  // accumulator live at a time
             }
         };
         WUnit wr[Q80T_P];
@@ -196,6 +200,8 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
                 asm volatile("" ::: "memory");
             }
         }
+#pragma unroll
+        for (int r = 0; r < 8; ++r) { tot[2 * r] = tot2[r].x; tot[2 * r + 1] = tot2[r].y; }
     } else {
         const uint8_t *aq = a.act + z * nb * 1024 + lane * 16;
         // lanes of tokens past M read no activation (at M = 1 the wave fetches 32 B of it per block, not 1 KiB)
