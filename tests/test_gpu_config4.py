@@ -2,8 +2,8 @@
 vocab 128256, Q4_K_M policy).  The 8-GPU run puts 10 of the 80 layers on each GPU (tensor_split 1,...,1,
 SURVEY.md 8d); this builds exactly such a stage -- layers [0, 10) with the embedding -- and a full-width
 one-layer model with the head, so every kernel shape of config 4 runs here, including the K = 28672 down
-projection (beyond the fused decode mat-vec's K budget: the quantize + kcpp_gemv fallback of
-forward_layers_dec).
+projection (the long-K "XL" variant of the fused decode mat-vec, gemv_rs.hip: the activation slices read from LDS
+per piece).
 
 * 10-layer stage: finite, graph replay == eager, prefill independent of the ubatch split;
 * 1-layer model with head: logits vs the C restatement of the reference CPU path (f32 attention accumulation,
@@ -30,7 +30,7 @@ def K():
 
 def test_70b_stage_properties(K):
     """10-layer first stage (layers [0, 10) + embedding): no non-finite values; graph replay equals eager decode
-    bit for bit; decode runs the K = 28672 down fallback in every layer.  Prefill in ubatches of 12 (attention by
+    bit for bit; decode runs the K = 28672 down projection on the XL mat-vec in every layer.  Prefill in ubatches of 12 (attention by
     the split-KV kernel, T <= 16) vs one ubatch of 24 (MFMA flash attention, P rounded to f16) on the FIRST layer:
     with the strict-order attention (the same kernel for both splits) the last 12 rows are bit-identical; with the
     production kernels they differ by the two attention kernels' rounding, which an activation quantization
