@@ -26,6 +26,9 @@
 #ifndef Q80T_RING
 #define Q80T_RING 2              // loop per mode (bit MODE set: the branch-free Q80T_P-deep ring): tools/q80t_sweep.py
 #endif
+#ifndef Q80T_NOXG
+#define Q80T_NOXG 0
+#endif
 #ifndef Q80T_PIPE
 #define Q80T_PIPE 0              // ring loop: the next block's MFMA issued before this block's epilogue
 #endif
@@ -134,7 +137,13 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
         auto loadx = [&](int64_t u, XUnit &X) {
             u = u < ulast ? u : ulast;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) X.x[i] = *(const i32x4 *)(aq + (4 * u + i) * 1024) & xm;
+            for (int i = 0; i < 4; ++i) {
+#if Q80T_NOXG      // timing probe only (wrong results): activation fragments from LDS instead of global memory
+                X.x[i] = *(const i32x4 *)(lds + (((4 * u + i) & 3) * 1024 + lane * 16)) & xm;
+#else
+                X.x[i] = *(const i32x4 *)(aq + (4 * u + i) * 1024) & xm;
+#endif
+            }
         };
         auto comp = [&](int64_t u, const WUnit &U, const XUnit &X) {
             const bool live = u <= ulast;

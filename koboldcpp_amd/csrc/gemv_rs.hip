@@ -54,7 +54,10 @@ using namespace rs;
 // XL (long K: 70B ffn_down K = 28672, MoE n_ff > 14336): the lane's activation slices are read from the LDS image per
 // piece instead of living in registers for the launch (NI up to 16 pieces per row would not fit beside the weights);
 // NI is then a ceiling, pieces past the row are masked (their loads clamped to the row's last piece)
-template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4, bool XL = false>
+// ROUTE (MoE two-slot GLU, PRO 1, K <= 4096): the router runs in every workgroup on the prologue's normalised row
+// (k_moe_route<WT, true>'s thread -> element map, fma order and wave / workgroup sums, so the ids and weights are
+// bit-identical), then the expert weights are issued; one launch per layer less
+template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4, bool XL = false, bool ROUTE = false>
 __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     using T = RS<TYPE>;
     constexpr int RR = MODE == 1 ? 2 * R : R;
@@ -82,8 +85,8 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     const int ngroups = (N0 + N1 + N2) / R;
     const int nw = (int)gridDim.x * NWV;
     const int wid = (int)blockIdx.x * NWV + wave;
-    const int64_t eoff = dec_expert_offset(a);   // MoE slice
-    const int64_t eoff1 = a.eid1 ? dec_expert_offset(a, a.eid1) : eoff;   // segment 1's (two slots in one launch)
+    int64_t eoff = ROUTE ? 0 : dec_expert_offset(a);   // MoE slice
+    int64_t eoff1 = ROUTE ? 0 : (a.eid1 ? dec_expert_offset(a, a.eid1) : eoff);   // segment 1's (two slots in one launch)
     const int abytes = K + K / 256 * 4 + K / 16 * 2;
     const typename T::Lane lc = T::lane_consts(lane);
 
@@ -111,13 +114,85 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     if constexpr (PRO != 0) {
         lean::ActPro<PRO, (MC * 4 + NWV - 1) / NWV, 64 * NWV> pro;
         pro.load(a);
-        if constexpr (!XL) issue(g0, ba);     // XL: a row's pieces and the prologue's registers do not fit together
+        float4 wpre[ROUTE ? 8 : 1][4];
+        const int tid = threadIdx.x;
+        if constexpr (ROUTE) {            // router rows first: they do not wait for the norm (k_moe_route's order)
+            const bool f16 = a.route_wt == KT_F16;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int i = 16 * tid + 4 * u;
+                    wpre[e][u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (e < a.route_ne && i < K) {
+                        if (f16) {
+                            const uint2 h = *(const uint2 *)((const uint16_t *)a.route_w + (int64_t)e * K + i);
+                            wpre[e][u] = make_float4(h2f(h.x & 0xFFFF), h2f(h.x >> 16), h2f(h.y & 0xFFFF), h2f(h.y >> 16));
+                        } else {
+                            wpre[e][u] = *(const float4 *)((const float *)a.route_w + (int64_t)e * K + i);
+                        }
+                    }
+                }
+        }
+        if constexpr (!XL && !ROUTE) issue(g0, ba);   // XL: a row's pieces and the prologue's registers do not fit together
 #ifdef KCPP_STAMPS
         pro.compute(a, lds, st_);
 #else
         pro.compute(a, lds);
 #endif
-        if constexpr (XL) issue(g0, ba);
+        if constexpr (ROUTE) {
+            // logits: thread tid's 16 elements (chunk tid, the prologue's row normalised in pro.v[0]), fma over the
+            // 4 float4 in order, wave sums, then ((w0 + w1) + (w2 + w3)) over the first four waves
+            __shared__ float r_part[4][8];
+            __shared__ int r_id[2];
+            __shared__ float r_w[2];
+            const bool f16 = a.route_wt == KT_F16;
+            float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (16 * tid < K) {
+                float xv[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) xv[q] = f16 ? h2f(f2h_rn(pro.v[0][q])) : pro.v[0][q];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if (e >= a.route_ne) break;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (16 * tid + 4 * u >= K) break;
+                        acc[e] = fmaf(xv[4 * u], wpre[e][u].x, acc[e]);
+                        acc[e] = fmaf(xv[4 * u + 1], wpre[e][u].y, acc[e]);
+                        acc[e] = fmaf(xv[4 * u + 2], wpre[e][u].z, acc[e]);
+                        acc[e] = fmaf(xv[4 * u + 3], wpre[e][u].w, acc[e]);
+                    }
+                }
+            }
+            if (wave < 4) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    if (e >= a.route_ne) break;
+                    const float v = wave_sum(acc[e]);
+                    if (lane == 0) r_part[wave][e] = v;
+                }
+            }
+            __syncthreads();
+            if (tid == 0) {
+                float logit[8];
+#pragma unroll
+                for (int e = 0; e < 8; ++e)
+                    logit[e] = e < a.route_ne ? (r_part[0][e] + r_part[1][e]) + (r_part[2][e] + r_part[3][e]) : 0.0f;
+                int id[2];
+                float w[2];
+                moe_topk8(logit, a.route_ne, 2, id, w);
+                r_id[0] = id[0]; r_id[1] = id[1]; r_w[0] = w[0]; r_w[1] = w[1];
+                if (blockIdx.x == 0) {
+                    a.route_ids[0] = id[0]; a.route_ids[1] = id[1];
+                    a.route_wts[0] = w[0]; a.route_wts[1] = w[1];
+                }
+            }
+            __syncthreads();
+            eoff = (int64_t)__builtin_amdgcn_readfirstlane(r_id[0]) * a.ebytes;
+            eoff1 = (int64_t)__builtin_amdgcn_readfirstlane(r_id[1]) * a.ebytes;
+        }
+        if constexpr (XL || ROUTE) issue(g0, ba);
     } else {
         lean::ActCopyCol cp;
         cp.load(a.act, K, a.act_mtot > 0 ? a.act_mtot : 1, a.act_col);
@@ -196,7 +271,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
 }
 
 namespace {
-template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4, bool XL = false>
+template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4, bool XL = false, bool ROUTE = false>
 int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
     int64_t ntot = 0;
     for (int i = 0; i < a.nseg; ++i) {
@@ -207,7 +282,7 @@ int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
     int64_t nblk = std::min<int64_t>((groups + NWV - 1) / NWV, max_blocks);
     nblk = std::max<int64_t>(nblk, (groups + 64 * NWV - 1) / (64 * NWV));    // <= 64 groups per wave (result slots)
     const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
-    hipLaunchKernelGGL((k_gemv_rs<TYPE, NI, R, MODE, PRO, MC, PF, NWV, XL>), dim3((unsigned)nblk), dim3(64 * NWV),
+    hipLaunchKernelGGL((k_gemv_rs<TYPE, NI, R, MODE, PRO, MC, PF, NWV, XL, ROUTE>), dim3((unsigned)nblk), dim3(64 * NWV),
                        (size_t)abytes + 16, s, a);
     KCPP_CHECK(hipGetLastError());
     return 0;
@@ -234,7 +309,17 @@ int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
     // down Q4_K 11.3 -> 9.7 and Q6_K 13.6 -> 12.2 (no PF: two rows per wave, both in flight), wo 5.4 -> 4.7; in the
     // bench's token graph down 12.0 / 13.7 -> 10.0 / 12.4 us, wo 5.3 -> 5.1, GLU unchanged: 577 -> 600 tok/s.  The
     // q|k|v launches stay at 4 waves (8: 6.8 -> 7.4 us, 592 tok/s).
-    if (mode == 1 && pro == 1 && R == 1) return launch_rs<TYPE, NI, 1, 1, 1, MC, 1, 8>(a, 256, s);
+    if (mode == 1 && pro == 1 && R == 1) {
+        if (a.route_w) {                  // routed two-slot GLU (MoE decode): K <= 4096 (one prologue chunk), NE <= 8
+            if constexpr (MC == 1) {
+                if (a.nseg == 2 && a.route_ne >= 2 && a.route_ne <= 8 && a.K <= 4096 && a.route_ids && a.route_wts &&
+                    (a.route_wt == KT_F32 || a.route_wt == KT_F16))
+                    return launch_rs<TYPE, NI, 1, 1, 1, MC, 1, 8, false, true>(a, 256, s);
+            }
+            return -3;
+        }
+        return launch_rs<TYPE, NI, 1, 1, 1, MC, 1, 8>(a, 256, s);
+    }
     if (mode == 0 && pro == 2 && R == 1 && ntot <= 16384) return launch_rs<TYPE, NI, 1, 0, 2, MC, 0, 8>(a, 256, s);
 #define KCPP_RS_P(PRO_)                                                                                             \
     if (pro == PRO_) {                                                                                              \

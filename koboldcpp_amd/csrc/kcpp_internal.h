@@ -60,7 +60,55 @@ struct DecArgs {
     // MoE, RS kernels: segment 1's expert index (two top-k slots' gate|up in one launch: segments 0 / 1 = slots 0 / 1
     // over the same expert tensors, the same activation); null: every segment takes eid
     const int32_t *eid1;
+    // MoE, RS GLU with two slots: route inside the launch (k_moe_route's math on the prologue's normalised row; NE <= 8,
+    // top-2, K <= 4096) instead of reading eid / eid1; workgroup 0 stores the ids and weights for the down projections
+    const void *route_w;      // ffn_gate_inp [NE][K], F32 or F16
+    int route_wt;             // KT_F32 / KT_F16
+    int route_ne;
+    int32_t *route_ids;
+    float *route_wts;
 };
+
+// top-NU of NE <= 8 router logits exactly as ggml's soft_max (ggml_float sum) + argsort (exchange order) + the
+// normalisation by the selected weights' sum (llm_build_moe_ffn, src/llama.cpp:9416-9470); shared by k_moe_route
+// (moe.hip) and the routed RS GLU launch (gemv_rs.hip) so both choose bit-identical experts and weights
+__device__ __forceinline__ void moe_topk8(const float *logit, int NE, int NU, int *idx_out, float *w_out) {
+    float p[8], pv[8];
+    int idx[8];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        p[e] = e < NE ? logit[e] : -INFINITY;
+        mx = fmaxf(mx, p[e]);
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+        if (e < NE) { p[e] = expf(p[e] - mx); sum += (double)p[e]; }
+    const float inv = (float)(1.0 / sum);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { p[e] *= inv; pv[e] = p[e]; idx[e] = e; }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        if (j >= NU) break;
+#pragma unroll
+        for (int k = j + 1; k < 8; ++k) {
+            if (k >= NE) break;
+            if (pv[j] < pv[k]) {
+                const int ti = idx[j]; idx[j] = idx[k]; idx[k] = ti;
+                const float tv = pv[j]; pv[j] = pv[k]; pv[k] = tv;
+            }
+        }
+    }
+    double ws = 0.0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (j < NU) ws += (double)pv[j];
+    const float wsum = (float)ws;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (j < NU) { idx_out[j] = idx[j]; w_out[j] = pv[j] / wsum; }
+}
 // the expert slice offset of a DecArgs (0 without an expert id); `id` defaults to eid
 __device__ __forceinline__ int64_t dec_expert_offset(const DecArgs &a, const int32_t *id = nullptr) {
     if (!id) id = a.eid;

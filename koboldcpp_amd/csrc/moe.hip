@@ -153,47 +153,8 @@ __global__ void __launch_bounds__(256) k_moe_route(const float *__restrict__ x, 
     }
     __syncthreads();
     if (tid != 0) return;
-    if (NE <= 8) {
-        // the same steps on register arrays (constant indices after unrolling; the generic path below keeps
-        // p / idx in scratch, a chain of dependent private-memory loads that cost ~15 us per token and layer)
-        float p[8], pv[8];
-        int idx[8];
-        float mx = -INFINITY;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            p[e] = e < NE ? s_logit[e] : -INFINITY;
-            mx = fmaxf(mx, p[e]);
-        }
-        double sum = 0.0;                                // ggml_vec_soft_max_f32: ggml_float sum
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-            if (e < NE) { p[e] = expf(p[e] - mx); sum += (double)p[e]; }
-        const float inv = (float)(1.0 / sum);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) { p[e] *= inv; pv[e] = p[e]; idx[e] = e; }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {                    // argsort descending (exchange order), first NU
-            if (j >= NU) break;
-#pragma unroll
-            for (int k = j + 1; k < 8; ++k) {
-                if (k >= NE) break;
-                if (pv[j] < pv[k]) {
-                    const int ti = idx[j]; idx[j] = idx[k]; idx[k] = ti;
-                    const float tv = pv[j]; pv[j] = pv[k]; pv[k] = tv;
-                }
-            }
-        }
-        double ws = 0.0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j < NU) ws += (double)pv[j];
-        const float wsum = (float)ws;
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j < NU) {
-                ids[t * NU + j] = idx[j];
-                wts[t * NU + j] = pv[j] / wsum;
-            }
+    if (NE <= 8) {      // register arrays (constant indices after unrolling; the generic path keeps p / idx in scratch)
+        moe_topk8(s_logit, NE, NU, ids + t * NU, wts + t * NU);
         return;
     }
     float p[MOE_MAX_EXPERT];

@@ -115,6 +115,7 @@ struct kcpp_model {
     float *moe_rw = nullptr;         // [ubatch*k] routing weight of each grouped entry
     float *moe_slots = nullptr;      // [k][ubatch][n_embd] weighted expert outputs, summed in top-k order
     int32_t *moe_trace = nullptr;    // [n_layer of the stage][n_expert_used] single-token routing (diagnostics)
+    bool no_fused_route = false;     // MoE decode: route in k_moe_route instead of inside the gate|up launch (A/B tests)
     int32_t *moe_ids_h = nullptr;    // pinned host copies (prefill routing)
     float *moe_w_h = nullptr;
     int32_t *moe_rows_h = nullptr;
@@ -704,6 +705,15 @@ extern "C" int kcpp_model_moe_trace(kcpp_model *m, int enable) {
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
     return 0;
 }
+// MoE single-token routing inside the two-slot gate|up launch (default) or in its own k_moe_route launch (0): the
+// two give bit-identical ids, weights and logits (tests/test_gpu_moe.py).  Drops the captured graph.
+extern "C" int kcpp_model_set_fused_route(kcpp_model *m, int on) {
+    RT_CHECK(hipSetDevice(m->device));
+    RT_CHECK(hipStreamSynchronize(m->stream));
+    m->no_fused_route = !on;
+    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    return 0;
+}
 extern "C" int kcpp_model_moe_trace_read(kcpp_model *m, int32_t *out, int n) {
     if (!m->moe_trace || n < 0 || n > (int)m->layers.size() * std::max(1, m->hp.n_expert_used)) { g_err = "moe trace"; return -1; }
     RT_CHECK(hipStreamSynchronize(m->stream));
@@ -818,7 +828,29 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
     const int NU = hp.n_expert_used;
     const KTensor *t = L.t;
     hipStream_t s = m->stream;
-    if (kcpp_moe_route_norm(m->x, E, (const float *)t[5].d, hp.eps, t[9].d, t[9].type, E, hp.n_expert, NU, m->moe_ids,
+    auto is_q81 = [](int ty) { return ty == KT_Q4_1 || ty == KT_Q5_1; };
+    // RS gate|up with two slots: both slots' GLU rows in one launch (segment j = slot j, its own expert index), one
+    // ramp instead of two; h of slot j at m->h + j F.  The router runs inside that launch where it can (top-2 of <= 8
+    // experts, K <= 4096: every workgroup routes on its prologue's normalised row, workgroup 0 stores ids / weights)
+    const bool rs_gu = t[6].type == t[7].type &&
+                       (t[6].type == KT_Q4_K_RS || t[6].type == KT_Q5_K_RS || t[6].type == KT_Q6_K_RS);
+    const bool pair = rs_gu && NU == 2 && m->ub >= 2;
+    bool routed = false;
+    if (pair && !m->no_fused_route && (t[9].type == KT_F32 || t[9].type == KT_F16) && hp.n_expert <= 8 && E <= 4096) {
+        DecArgs a;
+        memset(&a, 0, sizeof a);
+        a.K = E; a.x = m->x; a.nw = (const float *)t[5].d; a.eps = hp.eps; a.nseg = 2;
+        a.W[0] = a.W[1] = (const uint8_t *)t[6].d; a.W2 = (const uint8_t *)t[7].d; a.N[0] = a.N[1] = F;
+        a.Y[0] = m->h; a.Y[1] = m->h + F;
+        a.n_exp = hp.n_expert; a.ebytes = (int64_t)t[6].slice_bytes;
+        a.route_w = t[9].d; a.route_wt = t[9].type; a.route_ne = (int)hp.n_expert;
+        a.route_ids = m->moe_ids; a.route_wts = m->moe_w;
+        const int rc = kcpp_gemv_dec(t[6].type, &a, 1, 1, rows_per_wave(F, 1), s);
+        if (rc != 0 && rc != -3) return rc;
+        routed = rc == 0;
+    }
+    if (!routed &&
+        kcpp_moe_route_norm(m->x, E, (const float *)t[5].d, hp.eps, t[9].d, t[9].type, E, hp.n_expert, NU, m->moe_ids,
                             m->moe_w, 1, s) != 0) {
         RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, m->attn, E, nullptr, E, 1, hp.eps, s));
         RC(kcpp_moe_route(m->attn, E, t[9].d, t[9].type, E, hp.n_expert, NU, m->moe_ids, m->moe_w, 1, s));
@@ -826,7 +858,6 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
     if (m->moe_trace)
         RT_CHECK(hipMemcpyAsync(m->moe_trace + (&L - m->layers.data()) * NU, m->moe_ids, (size_t)NU * 4,
                                 hipMemcpyDeviceToDevice, s));
-    auto is_q81 = [](int ty) { return ty == KT_Q4_1 || ty == KT_Q5_1; };
     if (is_q81(t[6].type) || is_q81(t[7].type) || is_q81(t[8].type)) {
         // expert types without a fused decode mat-vec (Q4_1 / Q5_1; chosen per layer from the expert tensors, not the
         // model-wide flag: K-quant experts sit in the RS layouts, which the generic expert mat-vec does not read): ffn_norm + activation quantization once, then per
@@ -856,12 +887,7 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
     // RS down projections (MODE 0 store epilogue with DecArgs.pre): k_moe_combine's ((s0 + s1) + ...) + x in the
     // same order, one launch per layer less
     const bool chain = t[8].type == KT_Q4_K_RS || t[8].type == KT_Q5_K_RS || t[8].type == KT_Q6_K_RS;
-    // RS gate|up with two slots: both slots' GLU rows in one launch (segment j = slot j, its own expert index), one
-    // ramp instead of two; h of slot j at m->h + j F
-    const bool rs_gu = t[6].type == t[7].type &&
-                       (t[6].type == KT_Q4_K_RS || t[6].type == KT_Q5_K_RS || t[6].type == KT_Q6_K_RS);
-    const bool pair = rs_gu && NU == 2 && m->ub >= 2;
-    if (pair) {
+    if (pair && !routed) {
         DecArgs a;
         memset(&a, 0, sizeof a);
         a.K = E; a.x = m->x; a.nw = (const float *)t[5].d; a.eps = hp.eps; a.nseg = 2;

@@ -118,6 +118,7 @@ _SIGS = {
     "kcpp_model_moe_ids": [P, P, I],
     "kcpp_model_moe_trace": [P, I],
     "kcpp_model_moe_trace_read": [P, P, I],
+    "kcpp_model_set_fused_route": [P, I],
     "kcpp_flash_attn_exact": [P, P, P, P, I, I, I, I, I, P, Fl, P],
     "kcpp_model_weight_bytes": [P],
     "kcpp_model_set_kv_types": [P, I, I],
@@ -210,7 +211,8 @@ class DecArgs(ctypes.Structure):
     _fields_ = [("W", P * 3), ("Y", P * 3), ("N", I64 * 3), ("role", I * 3), ("nseg", I), ("W2", P), ("K", I64),
                 ("act", P), ("x", P), ("nw", P), ("eps", Fl), ("res", P), ("q16", P), ("kc", P), ("vc", P),
                 ("ekv", I64), ("D", I), ("pos", P), ("rope_tab", P), ("eid", P), ("ebytes", I64), ("escale", P),
-                ("act_mtot", I64), ("act_col", I64), ("n_exp", I64), ("pre", P), ("eid1", P)]
+                ("act_mtot", I64), ("act_col", I64), ("n_exp", I64), ("pre", P), ("eid1", P),
+                ("route_w", P), ("route_wt", I), ("route_ne", I), ("route_ids", P), ("route_wts", P)]
 
 
 if ctypes.sizeof(DecArgs) != _L.kcpp_gemv_dec_args_size():
@@ -353,6 +355,10 @@ class Model:
 
     def moe_trace(self, on):
         _chk(_L.kcpp_model_moe_trace(self.m, int(on)), "moe_trace")
+
+    def set_fused_route(self, on):
+        """MoE decode: route inside the two-slot gate|up launch (default) or by the separate router launch"""
+        _chk(_L.kcpp_model_set_fused_route(self.m, int(on)), "set_fused_route")
 
     def moe_trace_read(self, n_layer, k):
         import numpy as np

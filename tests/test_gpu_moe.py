@@ -276,3 +276,34 @@ def test_route_norm_fused_matches_norm_then_route(env, wtype, E):
         outs.append((ids.cpu().numpy(), wts.cpu().numpy()))
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+
+
+@pytest.mark.parametrize("policy", ["q5_k_f16_router", "mixtral_q5_k_m_f32_router"])
+@pytest.mark.parametrize("graphs", [True, False])
+def test_moe_routing_inside_glu_launch_bitwise(env, policy, graphs):
+    """single-token MoE decode with the router inside the two-slot gate|up launch (k_gemv_rs ROUTE: k_moe_route's
+    element map, fma order and sums on the prologue's normalised row) == the separate router launch: the same expert
+    ids every layer and step, logits bit for bit"""
+    torch, K = env
+    hp = R.TINY_MOE
+    types = R.moe_types(hp["n_layer"]) if policy.startswith("q5_k_f16") else R.mixtral_q5_k_m_types(hp["n_layer"])
+    prompt = [int(v) for v in np.random.default_rng(21).integers(1, 500, size=29)]
+    outs, traces = [], []
+    for fused in (True, False):
+        m = K.Model(hp, types)
+        m.set_graphs(graphs)
+        m.set_fused_route(fused)
+        m.synth(1234)
+        m.moe_trace(True)
+        lg = [m.decode(prompt, 0)]
+        tr = []
+        n = len(prompt)
+        for tok in (7, 100, 3, 250, 11, 42):
+            lg.append(m.decode([tok], n))
+            tr.append(m.moe_trace_read(hp["n_layer"], hp["n_expert_used"]))
+            n += 1
+        m.close()
+        outs.append(np.array(lg))
+        traces.append(np.array(tr))
+    assert np.array_equal(traces[0], traces[1])
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
