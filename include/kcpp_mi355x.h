@@ -354,8 +354,11 @@ int kcpp_model_moe_ids(kcpp_model *m, int32_t *out, int n);
  * top-k expert ids into [layer][n_expert_used] every decode step; _read returns the last step's n ids */
 int kcpp_model_moe_trace(kcpp_model *m, int enable);
 int kcpp_model_moe_trace_read(kcpp_model *m, int32_t *out, int n);
-/* MoE single-token decode: route inside the two-slot gate|up launch (1, default) or by k_moe_route (0); diagnostics */
+/* MoE single-token decode fusions (bit 0: route inside the two-slot gate|up launch, else k_moe_route; bit 1: both
+ * slots' down projections in one launch, else two chained launches; default 3); diagnostics */
 int kcpp_model_set_fused_route(kcpp_model *m, int on);
+/* enqueued so far (graph captures count once): routed gate|up launches (low 32 bits), two-slot down launches (high) */
+int64_t kcpp_model_fused_route_count(kcpp_model *m);
 /* K / V cache types (llama_context_params type_k / type_v): KT_F16 (default) or quantized KT_Q8_0 / KT_Q4_0 for
  * both (koboldcpp --quantkv).  Reallocates and clears the caches; quantized caches run single-token decode
  * through the unfused per-op path and refuse kcpp_model_kv_shift (koboldcpp turns context shift off with

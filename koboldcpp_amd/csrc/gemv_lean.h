@@ -158,7 +158,7 @@ __device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0,
         for (int r = 0; r < R; ++r) {
             float v = (MODE == 0 && a.escale) ? __fmul_rn(slot[r], a.escale[0]) : slot[r];
             if (MODE == 0 && a.pre) v = __fadd_rn(a.pre[row0 + r], v);
-            Y[row0 + r] = (MODE == 0 && a.res) ? __fadd_rn(v, a.res[row0 + r]) : v;
+            Y[row0 + r] = ((MODE == 0 || MODE == 3) && a.res) ? __fadd_rn(v, a.res[row0 + r]) : v;
         }
     } else {
         const int role = seg == 0 ? a.role[0] : (seg == 1 ? a.role[1] : a.role[2]);

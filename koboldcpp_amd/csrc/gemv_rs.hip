@@ -57,10 +57,14 @@ using namespace rs;
 // ROUTE (MoE two-slot GLU, PRO 1, K <= 4096): the router runs in every workgroup on the prologue's normalised row
 // (k_moe_route<WT, true>'s thread -> element map, fma order and wave / workgroup sums, so the ids and weights are
 // bit-identical), then the expert weights are issued; one launch per layer less
+// MODE 3 (MoE, both top-2 slots' down projections in one launch, NWV = 8, PRO 2): waves 0-3 stream expert eid's rows
+// against slot 0's h (x), waves 4-7 the same rows of expert eid1 against slot 1's h (x + K); the halves meet in LDS and
+// the row is ((w0 o0) + (w1 o1)) + res -- the two chained MODE 0 launches' result bit for bit
 template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4, bool XL = false, bool ROUTE = false>
 __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     using T = RS<TYPE>;
     constexpr int RR = MODE == 1 ? 2 * R : R;
+    static_assert(MODE != 3 || (NWV == 8 && PRO == 2 && !XL && !ROUTE), "MODE 3: 8 waves, quantize prologue");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
 #ifdef KCPP_STAMPS
     __shared__ unsigned long long *st_s;
@@ -83,11 +87,14 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     const int npieces = nsb * T::PIECES_PER_SB;
     const int N0 = (int)a.N[0], N1 = a.nseg > 1 ? (int)a.N[1] : 0, N2 = a.nseg > 2 ? (int)a.N[2] : 0;
     const int ngroups = (N0 + N1 + N2) / R;
-    const int nw = (int)gridDim.x * NWV;
-    const int wid = (int)blockIdx.x * NWV + wave;
+    constexpr int WPG = MODE == 3 ? NWV / 2 : NWV;     // waves per group set (MODE 3: per expert half)
+    const int hx = MODE == 3 ? wave / WPG : 0;          // MODE 3: which slot this wave serves
+    const int nw = (int)gridDim.x * WPG;
+    const int wid = (int)blockIdx.x * WPG + (MODE == 3 ? wave % WPG : wave);
     int64_t eoff = ROUTE ? 0 : dec_expert_offset(a);   // MoE slice
     int64_t eoff1 = ROUTE ? 0 : (a.eid1 ? dec_expert_offset(a, a.eid1) : eoff);   // segment 1's (two slots in one launch)
     const int abytes = K + K / 256 * 4 + K / 16 * 2;
+    const int aoff = MODE == 3 && hx ? (abytes + 15) & ~15 : 0;   // this wave's activation image in LDS
     const typename T::Lane lc = T::lane_consts(lane);
 
     auto group_rows = [&](int g, int &seg, int &row0) {
@@ -99,7 +106,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     auto issue = [&](int g, Buf &b) {
         int seg, row0;
         group_rows(g, seg, row0);
-        const int64_t eo = seg == 1 ? eoff1 : eoff;
+        const int64_t eo = (seg == 1 || hx) ? eoff1 : eoff;
         const uint8_t *W = (seg == 0 ? a.W[0] : (seg == 1 ? a.W[1] : a.W[2])) + eo;
 #pragma unroll
         for (int r = 0; r < RR; ++r) {
@@ -134,12 +141,19 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
                     }
                 }
         }
-        if constexpr (!XL && !ROUTE) issue(g0, ba);   // XL: a row's pieces and the prologue's registers do not fit together
+        if constexpr (!XL && !ROUTE && MODE != 3) issue(g0, ba);   // XL: a row's pieces and the prologue's registers do not fit together
 #ifdef KCPP_STAMPS
         pro.compute(a, lds, st_);
 #else
         pro.compute(a, lds);
 #endif
+        if constexpr (MODE == 3) {          // slot 1's h follows slot 0's: its Q8_K image behind the first
+            DecArgs a1 = a;
+            a1.x = a.x + a.K;
+            lean::ActPro<PRO, (MC * 4 + NWV - 1) / NWV, 64 * NWV> pro1;
+            pro1.load(a1);
+            pro1.compute(a1, lds + ((abytes + 15) & ~15));
+        }
         if constexpr (ROUTE) {
             // logits: thread tid's 16 elements (chunk tid, the prologue's row normalised in pro.v[0]), fma over the
             // 4 float4 in order, wave sums, then ((w0 + w1) + (w2 + w3)) over the first four waves
@@ -192,7 +206,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
             eoff = (int64_t)__builtin_amdgcn_readfirstlane(r_id[0]) * a.ebytes;
             eoff1 = (int64_t)__builtin_amdgcn_readfirstlane(r_id[1]) * a.ebytes;
         }
-        if constexpr (XL || ROUTE) issue(g0, ba);
+        if constexpr (XL || ROUTE || MODE == 3) issue(g0, ba);
     } else {
         lean::ActCopyCol cp;
         cp.load(a.act, K, a.act_mtot > 0 ? a.act_mtot : 1, a.act_col);
@@ -202,7 +216,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     typename T::Act xr[XL ? 1 : NI];
     if constexpr (!XL) {
 #pragma unroll
-        for (int i = 0; i < NI; ++i) T::act(lds, K, min(T::sb_of(lane, i), nsb - 1), lc, xr[i]);
+        for (int i = 0; i < NI; ++i) T::act(lds + aoff, K, min(T::sb_of(lane, i), nsb - 1), lc, xr[i]);
     }
     RS_STAMP(1);
 
@@ -260,6 +274,17 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
         }
     }
     RS_STAMP(3);
+    if constexpr (MODE == 3) {
+        // the halves meet: lane k of wave w (k-th group of the wave) -> xs[half][w % 4][r][k]; half 0 combines
+        __shared__ float xs[2][4][R][64];
+#pragma unroll
+        for (int r = 0; r < R; ++r) xs[hx][wave % WPG][r][lane] = slot[r];
+        __syncthreads();
+        if (hx) return;
+        const float e0 = a.escale[0], e1 = a.escale[1];
+#pragma unroll
+        for (int r = 0; r < R; ++r) slot[r] = __fadd_rn(__fmul_rn(slot[r], e0), __fmul_rn(xs[1][wave][r][lane], e1));
+    }
     if (slot_g < 0) return;
     int seg, row0;
     group_rows(slot_g, seg, row0);
@@ -279,11 +304,13 @@ int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
         ntot += a.N[i];
     }
     const int64_t groups = ntot / R;
-    int64_t nblk = std::min<int64_t>((groups + NWV - 1) / NWV, max_blocks);
-    nblk = std::max<int64_t>(nblk, (groups + 64 * NWV - 1) / (64 * NWV));    // <= 64 groups per wave (result slots)
+    constexpr int WPG = MODE == 3 ? NWV / 2 : NWV;
+    int64_t nblk = std::min<int64_t>((groups + WPG - 1) / WPG, max_blocks);
+    nblk = std::max<int64_t>(nblk, (groups + 64 * WPG - 1) / (64 * WPG));    // <= 64 groups per wave (result slots)
     const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
+    const int64_t lbytes = MODE == 3 ? 2 * ((abytes + 15) & ~(int64_t)15) : abytes;
     hipLaunchKernelGGL((k_gemv_rs<TYPE, NI, R, MODE, PRO, MC, PF, NWV, XL, ROUTE>), dim3((unsigned)nblk), dim3(64 * NWV),
-                       (size_t)abytes + 16, s, a);
+                       (size_t)lbytes + 16, s, a);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }
@@ -493,12 +520,22 @@ extern "C" int kcpp_rs_supported(int type, int64_t K) {
     return 0;
 }
 
+// MODE 3 (both MoE slots' down projections): the shapes of the Mixtral class (n_ff 14336: 56 super-blocks)
+static int pick_rs_pair(int type, const DecArgs &a, hipStream_t s) {
+    if (a.nseg != 1 || !a.eid || !a.eid1 || !a.escale || a.K != 14336) return -3;
+    if (type == KT_Q4_K_RS) return launch_rs<KT_Q4_K_RS, 7, 1, 3, 2, 4, 0, 8>(a, 256, s);
+    if (type == KT_Q5_K_RS) return launch_rs<KT_Q5_K_RS, 7, 1, 3, 2, 4, 0, 8>(a, 256, s);
+    if (type == KT_Q6_K_RS) return launch_rs<KT_Q6_K_RS, 4, 1, 3, 2, 4, 0, 8>(a, 256, s);
+    return -3;
+}
+
 // -3 = not covered
 extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream) {
     const DecArgs &a = *(const DecArgs *)args;
     hipStream_t s = (hipStream_t)stream;
+    if (mode == 3) return pro == 2 && kcpp_rs_supported(type, a.K) ? pick_rs_pair(type, a, s) : -3;
     if (a.nseg < 1 || a.nseg > 3 || !kcpp_rs_supported(type, a.K)) return -3;
-    if (mode == 1 && a.nseg != 1 && !(a.nseg == 2 && a.eid1)) return -3;   // GLU: one segment, or two MoE slots
+    if (mode == 1 && a.nseg != 1 && !(a.nseg == 2 && (a.eid1 || a.route_w))) return -3;   // GLU: one segment, or two MoE slots
     const int nsb = (int)(a.K / 256);
     if (type == KT_Q4_K_RS) {
         const int ni = (nsb * 8 + 63) / 64, mc = (int)((a.K + 4095) / 4096);

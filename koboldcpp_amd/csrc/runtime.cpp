@@ -116,6 +116,9 @@ struct kcpp_model {
     float *moe_slots = nullptr;      // [k][ubatch][n_embd] weighted expert outputs, summed in top-k order
     int32_t *moe_trace = nullptr;    // [n_layer of the stage][n_expert_used] single-token routing (diagnostics)
     bool no_fused_route = false;     // MoE decode: route in k_moe_route instead of inside the gate|up launch (A/B tests)
+    int64_t n_fused_route = 0;       // routed gate|up launches enqueued (tests: the fused path really ran)
+    bool no_pair_down = false;       // MoE decode: the two slots' down projections as two chained launches (A/B tests)
+    int64_t n_pair_down = 0;         // two-slot down launches enqueued
     int32_t *moe_ids_h = nullptr;    // pinned host copies (prefill routing)
     float *moe_w_h = nullptr;
     int32_t *moe_rows_h = nullptr;
@@ -705,15 +708,18 @@ extern "C" int kcpp_model_moe_trace(kcpp_model *m, int enable) {
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
     return 0;
 }
-// MoE single-token routing inside the two-slot gate|up launch (default) or in its own k_moe_route launch (0): the
-// two give bit-identical ids, weights and logits (tests/test_gpu_moe.py).  Drops the captured graph.
+// MoE single-token decode fusions: bit 0 routes inside the two-slot gate|up launch (else k_moe_route), bit 1 runs
+// both slots' down projections in one launch (else two chained launches); every combination gives bit-identical ids,
+// weights and logits (tests/test_gpu_moe.py).  Drops the captured graph.
 extern "C" int kcpp_model_set_fused_route(kcpp_model *m, int on) {
     RT_CHECK(hipSetDevice(m->device));
     RT_CHECK(hipStreamSynchronize(m->stream));
-    m->no_fused_route = !on;
+    m->no_fused_route = !(on & 1);
+    m->no_pair_down = !(on & 2);
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
     return 0;
 }
+extern "C" int64_t kcpp_model_fused_route_count(kcpp_model *m) { return m->n_fused_route + (m->n_pair_down << 32); }
 extern "C" int kcpp_model_moe_trace_read(kcpp_model *m, int32_t *out, int n) {
     if (!m->moe_trace || n < 0 || n > (int)m->layers.size() * std::max(1, m->hp.n_expert_used)) { g_err = "moe trace"; return -1; }
     RT_CHECK(hipStreamSynchronize(m->stream));
@@ -848,6 +854,7 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
         const int rc = kcpp_gemv_dec(t[6].type, &a, 1, 1, rows_per_wave(F, 1), s);
         if (rc != 0 && rc != -3) return rc;
         routed = rc == 0;
+        m->n_fused_route += routed;
     }
     if (!routed &&
         kcpp_moe_route_norm(m->x, E, (const float *)t[5].d, hp.eps, t[9].d, t[9].type, E, hp.n_expert, NU, m->moe_ids,
@@ -895,6 +902,19 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
         a.Y[0] = m->h; a.Y[1] = m->h + F;
         a.eid = m->moe_ids; a.eid1 = m->moe_ids + 1; a.n_exp = hp.n_expert; a.ebytes = (int64_t)t[6].slice_bytes;
         RC(kcpp_gemv_dec(t[6].type, &a, 1, 1, rows_per_wave(F, 1), s));
+    }
+    // RS down projections of both slots in one launch (k_gemv_rs MODE 3: half the waves per slot, met in LDS):
+    // ((w0 o0) + (w1 o1)) + x, the two chained launches' result bit for bit
+    if (pair && chain && !m->no_pair_down) {
+        DecArgs a;
+        memset(&a, 0, sizeof a);
+        a.K = F; a.x = m->h; a.nseg = 1;
+        a.W[0] = a.W[1] = (const uint8_t *)t[8].d; a.N[0] = E; a.Y[0] = m->x; a.res = m->x;
+        a.eid = m->moe_ids; a.eid1 = m->moe_ids + 1; a.n_exp = hp.n_expert; a.ebytes = (int64_t)t[8].slice_bytes;
+        a.escale = m->moe_w;
+        const int rc = kcpp_gemv_dec(t[8].type, &a, 3, 2, rows_per_wave(E, 0), s);
+        if (rc == 0) { m->n_pair_down++; return 0; }
+        if (rc != -3) return rc;
     }
     for (int j = 0; j < NU; ++j) {
         if (pair) {

@@ -119,6 +119,7 @@ _SIGS = {
     "kcpp_model_moe_trace": [P, I],
     "kcpp_model_moe_trace_read": [P, P, I],
     "kcpp_model_set_fused_route": [P, I],
+    "kcpp_model_fused_route_count": [P],
     "kcpp_flash_attn_exact": [P, P, P, P, I, I, I, I, I, P, Fl, P],
     "kcpp_model_weight_bytes": [P],
     "kcpp_model_set_kv_types": [P, I, I],
@@ -126,7 +127,7 @@ _SIGS = {
     "kcpp_kv_store_q": [I, I, P, I64, I64, I64, I, I64, P, P, I64, I, P, P],
     "kcpp_flash_attn_q": [I, I, P, I64, P, P, P, I, I, I, I, I64, I, P, Fl, P],
 }
-_RES = {"kcpp_gradient_ai_rope_base": Fl, "kcpp_fa_split_ws_bytes": I64, "kcpp_q80t_ws_bytes": I64, "kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
+_RES = {"kcpp_gradient_ai_rope_base": Fl, "kcpp_model_fused_route_count": I64, "kcpp_fa_split_ws_bytes": I64, "kcpp_q80t_ws_bytes": I64, "kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
         "kcpp_model_create": P, "kcpp_model_hidden": P, "kcpp_model_stream": P, "kcpp_model_weight_bytes": I64,
         "kcpp_last_error": ctypes.c_char_p, "kcpp_model_free": None, "kcpp_fa_set_stamps": None}
 _L.kcpp_act_bytes.argtypes = [I, I64, I64]
@@ -356,9 +357,16 @@ class Model:
     def moe_trace(self, on):
         _chk(_L.kcpp_model_moe_trace(self.m, int(on)), "moe_trace")
 
-    def set_fused_route(self, on):
-        """MoE decode: route inside the two-slot gate|up launch (default) or by the separate router launch"""
-        _chk(_L.kcpp_model_set_fused_route(self.m, int(on)), "set_fused_route")
+    def set_fused_route(self, on, pair_down=None):
+        """MoE decode fusions (default on): the router inside the two-slot gate|up launch, and (pair_down, default =
+        on) both slots' down projections in one launch; off = the separate router launch / two chained launches"""
+        pd = on if pair_down is None else pair_down
+        _chk(_L.kcpp_model_set_fused_route(self.m, int(bool(on)) | (2 * int(bool(pd)))), "set_fused_route")
+
+    def fused_route_count(self):
+        """(routed gate|up launches, two-slot down launches) enqueued so far"""
+        v = int(_L.kcpp_model_fused_route_count(self.m))
+        return v & 0xFFFFFFFF, v >> 32
 
     def moe_trace_read(self, n_layer, k):
         import numpy as np

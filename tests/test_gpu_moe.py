@@ -282,10 +282,11 @@ def test_route_norm_fused_matches_norm_then_route(env, wtype, E):
 @pytest.mark.parametrize("graphs", [True, False])
 def test_moe_routing_inside_glu_launch_bitwise(env, policy, graphs):
     """single-token MoE decode with the router inside the two-slot gate|up launch (k_gemv_rs ROUTE: k_moe_route's
-    element map, fma order and sums on the prologue's normalised row) == the separate router launch: the same expert
-    ids every layer and step, logits bit for bit"""
+    element map, fma order and sums on the prologue's normalised row) and both slots' down projections in one launch
+    (MODE 3, at n_ff 14336) == the separate router launch + two chained down launches: the same expert ids every
+    layer and step, logits bit for bit"""
     torch, K = env
-    hp = R.TINY_MOE
+    hp = dict(R.TINY_MOE, n_ff=14336)       # the two-slot down launch covers the Mixtral class (n_ff 14336)
     types = R.moe_types(hp["n_layer"]) if policy.startswith("q5_k_f16") else R.mixtral_q5_k_m_types(hp["n_layer"])
     prompt = [int(v) for v in np.random.default_rng(21).integers(1, 500, size=29)]
     outs, traces = [], []
@@ -302,6 +303,8 @@ def test_moe_routing_inside_glu_launch_bitwise(env, policy, graphs):
             lg.append(m.decode([tok], n))
             tr.append(m.moe_trace_read(hp["n_layer"], hp["n_expert_used"]))
             n += 1
+        routed, paired = m.fused_route_count()
+        assert (routed > 0) == fused and (paired > 0) == fused     # the fused launches really ran (only when asked)
         m.close()
         outs.append(np.array(lg))
         traces.append(np.array(tr))
