@@ -16,12 +16,12 @@ template <int PRO, int MAXC, int NT = 256>
 struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_impl.h); loads first
     float v[MAXC][16];
     float w[PRO == 1 ? MAXC : 1][16];
-    __device__ __forceinline__ void load(const DecArgs &a) {
+    __device__ __forceinline__ void load(const DecArgs &a, int64_t xoff = 0) {   // input row a.x + xoff
         const int tid = threadIdx.x, nchunk = (int)(a.K / 16);
 #pragma unroll
         for (int i = 0; i < MAXC; ++i) {
             const int c = min(tid + NT * i, nchunk - 1);
-            const float4 *p = (const float4 *)(a.x + 16 * (int64_t)c);
+            const float4 *p = (const float4 *)(a.x + xoff + 16 * (int64_t)c);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float4 f = p[k];

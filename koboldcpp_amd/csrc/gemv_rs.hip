@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     const int N0 = (int)a.N[0], N1 = a.nseg > 1 ? (int)a.N[1] : 0, N2 = a.nseg > 2 ? (int)a.N[2] : 0;
     const int ngroups = (N0 + N1 + N2) / R;
     constexpr int WPG = MODE == 3 ? NWV / 2 : NWV;     // waves per group set (MODE 3: per expert half)
-    const int hx = MODE == 3 ? wave / WPG : 0;          // MODE 3: which slot this wave serves
+    const int hx = MODE == 3 ? __builtin_amdgcn_readfirstlane(wave / WPG) : 0;   // MODE 3: which slot this wave serves
     const int nw = (int)gridDim.x * WPG;
     const int wid = (int)blockIdx.x * WPG + (MODE == 3 ? wave % WPG : wave);
     int64_t eoff = ROUTE ? 0 : dec_expert_offset(a);   // MoE slice
@@ -106,7 +106,10 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     auto issue = [&](int g, Buf &b) {
         int seg, row0;
         group_rows(g, seg, row0);
-        const int64_t eo = (seg == 1 || hx) ? eoff1 : eoff;
+        int64_t eo = seg == 1 ? eoff1 : eoff;
+        if constexpr (MODE == 3) {          // the wave's slot (wave-uniform; a select of the two would go to scratch)
+            if (hx) eo = eoff1;
+        }
         const uint8_t *W = (seg == 0 ? a.W[0] : (seg == 1 ? a.W[1] : a.W[2])) + eo;
 #pragma unroll
         for (int r = 0; r < RR; ++r) {
@@ -148,11 +151,9 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
         pro.compute(a, lds);
 #endif
         if constexpr (MODE == 3) {          // slot 1's h follows slot 0's: its Q8_K image behind the first
-            DecArgs a1 = a;
-            a1.x = a.x + a.K;
             lean::ActPro<PRO, (MC * 4 + NWV - 1) / NWV, 64 * NWV> pro1;
-            pro1.load(a1);
-            pro1.compute(a1, lds + ((abytes + 15) & ~15));
+            pro1.load(a, a.K);
+            pro1.compute(a, lds + ((abytes + 15) & ~15));
         }
         if constexpr (ROUTE) {
             // logits: thread tid's 16 elements (chunk tid, the prologue's row normalised in pro.v[0]), fma over the
