@@ -64,7 +64,7 @@ template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 
 __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     using T = RS<TYPE>;
     constexpr int RR = MODE == 1 ? 2 * R : R;
-    static_assert(MODE != 3 || (NWV == 8 && PRO == 2 && !XL && !ROUTE), "MODE 3: 8 waves, quantize prologue");
+    static_assert(MODE != 3 || (NWV == 8 && PRO == 2 && !ROUTE), "MODE 3: 8 waves, quantize prologue");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
 #ifdef KCPP_STAMPS
     __shared__ unsigned long long *st_s;
@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
         for (int i = 0; i < NI; ++i) {
             const bool ok = (NI * 64 == npieces) || lane + 64 * i < npieces;
             typename T::Act xl;
-            if constexpr (XL) T::act(lds, K, min(T::sb_of(lane, i), nsb - 1), lc, xl);
+            if constexpr (XL) T::act(lds + aoff, K, min(T::sb_of(lane, i), nsb - 1), lc, xl);
 #pragma unroll
             for (int r = 0; r < RR; ++r) {
                 const float p = T::dot(b.w[i][r], XL ? xl : xr[i], lc);
@@ -521,12 +521,18 @@ extern "C" int kcpp_rs_supported(int type, int64_t K) {
     return 0;
 }
 
+#ifndef Q_PF
+#define Q_PF 0               // MODE 3 group prefetch: measured no faster (23.2 / 21.7 vs 23.2 / 21.0 us), more registers
+#endif
+#ifndef Q_XL
+#define Q_XL false
+#endif
 // MODE 3 (both MoE slots' down projections): the shapes of the Mixtral class (n_ff 14336: 56 super-blocks)
 static int pick_rs_pair(int type, const DecArgs &a, hipStream_t s) {
     if (a.nseg != 1 || !a.eid || !a.eid1 || !a.escale || a.K != 14336) return -3;
-    if (type == KT_Q4_K_RS) return launch_rs<KT_Q4_K_RS, 7, 1, 3, 2, 4, 0, 8>(a, 256, s);
-    if (type == KT_Q5_K_RS) return launch_rs<KT_Q5_K_RS, 7, 1, 3, 2, 4, 0, 8>(a, 256, s);
-    if (type == KT_Q6_K_RS) return launch_rs<KT_Q6_K_RS, 4, 1, 3, 2, 4, 0, 8>(a, 256, s);
+    if (type == KT_Q4_K_RS) return launch_rs<KT_Q4_K_RS, 7, 1, 3, 2, 4, Q_PF, 8, Q_XL>(a, 256, s);
+    if (type == KT_Q5_K_RS) return launch_rs<KT_Q5_K_RS, 7, 1, 3, 2, 4, Q_PF, 8, Q_XL>(a, 256, s);
+    if (type == KT_Q6_K_RS) return launch_rs<KT_Q6_K_RS, 4, 1, 3, 2, 4, Q_PF, 8, Q_XL>(a, 256, s);
     return -3;
 }
 
