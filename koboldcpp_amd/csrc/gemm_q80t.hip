@@ -26,12 +26,6 @@
 #ifndef Q80T_RING
 #define Q80T_RING 2              // loop per mode (bit MODE set: the branch-free Q80T_P-deep ring): tools/q80t_sweep.py
 #endif
-#ifndef Q80T_NOXG
-#define Q80T_NOXG 0
-#endif
-#ifndef Q80T_PIPE
-#define Q80T_PIPE 0              // ring loop: the next block's MFMA issued before this block's epilogue
-#endif
 #ifndef Q80T_P
 #define Q80T_P 2                 // weight units in flight per wave (even: the x pair alternates with the ring slot)
 #endif
@@ -137,13 +131,7 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
         auto loadx = [&](int64_t u, XUnit &X) {
             u = u < ulast ? u : ulast;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-#if Q80T_NOXG      // timing probe only (wrong results): activation fragments from LDS instead of global memory
-                X.x[i] = *(const i32x4 *)(lds + (((4 * u + i) & 3) * 1024 + lane * 16)) & xm;
-#else
-                X.x[i] = *(const i32x4 *)(aq + (4 * u + i) * 1024) & xm;
-#endif
-            }
+            for (int i = 0; i < 4; ++i) X.x[i] = *(const i32x4 *)(aq + (4 * u + i) * 1024) & xm;
         };
         auto comp = [&](int64_t u, const WUnit &U, const XUnit &X) {
             const bool live = u <= ulast;
@@ -158,18 +146,9 @@ __global__ void __launch_bounds__(64 * WV) k_q80t(const Q80TArgs a) {
                 asm volatile("" : "+v"(xv), "+v"(wv));   // not hoisted above the previous block's epilogue
                 return __builtin_amdgcn_mfma_i32_32x32x32_i8(xv, wv, acc, 0, 0, 0);
             };
-#if Q80T_PIPE
-            i32x16 accs[2];
-            accs[0] = mf(0);
-#endif
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-#if Q80T_PIPE
-                if (i < 3) accs[(i + 1) & 1] = mf(i + 1);   // block i + 1's MFMA runs under block i's epilogue
-                const i32x16 acc = accs[i & 1];
-#else
                 const i32x16 acc = mf(i);
-#endif
                 const float *sd = dxs + ((u - u0) * 4 + i) * 32 + 4 * kg;
                 const f2 dw2 = {dw[i], dw[i]};
 #pragma unroll
