@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
@@ -1575,6 +1576,7 @@ static int64_t ws_layout(int type, int64_t K, int64_t N, int64_t M, int64_t &o_a
     o_up = off; off += (M * N * 4 + 255) & ~255LL;
     if (type == KT_Q8_0) off += 2 * (int64_t)q80s_splits(K, N) * 32 * N * 4;   // small-M split-K partials (g, u)
     if (type == KT_Q4_K || type == KT_Q4_K_RS || type == KT_Q6_K_RS) off += 2 * Mp * N * 4;   // v3 split-K partials
+    else if (type == KT_Q5_K || type == KT_Q5_K_RS) off += (int64_t)std::max(2, ks1_of(K, N)) * Mp * N * 4;   // v4 / v1
     else off += (int64_t)ks1_of(K, N) * Mp * N * 4;                                             // v1 split-K partials
     return off;
 }
@@ -1612,6 +1614,10 @@ template <int WR, int NST> struct Q4v4Smem {
     uint4 wh[NST][WR][32];   // [stage][row tile][row]: Q4_K header (d, dmin, 12 B scales / mins)
     i32x4 wq[NST][WR][280];  // [stage][row tile][swz(row, chunk)]: qs chunks 0..7 (pair p, half g: chunk 2p + g)
 };
+// Q5_K adds the fifth bits: qh bytes 16 g .. 16 g + 15 of row r (bit j = sub-block j) at slot 32 g + r
+template <int WR, int NST> struct Q5v4Smem : Q4v4Smem<WR, NST> {
+    i32x4 wqh[NST][WR][64];  // [stage][row tile][32 g + row]
+};
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 // bytes of x (each <= 15) times s (<= 7), per byte: two 16-bit lanes, no carry out of a byte (v_pk_mul_lo_u16;
@@ -1621,13 +1627,19 @@ __device__ __forceinline__ int mulb(uint32_t x, uint32_t s) {
     return (int)__builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, x) * f);
 }
 
-template <int LAY, int TPW>
+// Q5_K (TYPE = KT_Q5_K, TPW = 2 only -- the qh stages do not fit v5's LDS): q = lo + 16 hb, lo <= 15, hb <= 1, so
+//   sum_k q*sc*a = 8 (sum_k (lo*(sc>>3))*a + sum_k (hb*2sc)*a) + sum_k (lo*(sc&7))*a,  hb*2sc <= 126,
+// a third MFMA per sub-block, into acc_h; isum = 8 acc_h + acc_l is again the CPU's exact int32 sumi
+// (ggml_vec_dot_q5_K_q8_K, ggml-quants.c), and the epilogue is unchanged.
+template <int TYPE, int LAY, int TPW>
 __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                                      const uint8_t *__restrict__ act, int64_t M, int64_t Mp, int MT,
                                                      float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr,
                                                      int KS, float *__restrict__ part, int XG) {
     constexpr int WT = 4 / TPW, WR = 8 / WT, NR = 32 * WR, NST = TPW == 2 ? 3 : 2, NI = WR / 2;
-    __shared__ Q4v4Smem<WR, NST> S;
+    constexpr bool Q5 = TYPE == KT_Q5_K;
+    static_assert(TYPE == KT_Q4_K || (Q5 && TPW == 2), "v4 int8 GEMM: Q4_K (TPW 2 / 4) or Q5_K (TPW 2)");
+    __shared__ std::conditional_t<Q5, Q5v4Smem<WR, NST>, Q4v4Smem<WR, NST>> S;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave % WR, wt = wave / WR;
@@ -1649,17 +1661,23 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
     const int8_t *arow = qs + min(m0 + 32 * att + (lane & 7), M - 1) * K + 16 * (8 * ah8 + (lane >> 3));
     const int16_t *bsrow = bsq + min(m0 + 32 * wave + lr, M - 1) * (K / 16) + 8 * kg;
     const float *dyrow = dq + min(m0 + 64 * max(wave - 4, 0) + lane, M - 1) * nsb;
-    constexpr int64_t HS = LAY == 1 ? 16 : 144, QS = LAY == 1 ? 128 : 144;
+    // bytes per super-block and row: Q4_K 144 (header 16, qs 128), Q5_K 176 (header 16, qh 32, qs 128); LAY 1 keeps
+    // each row's headers, qs and (Q5_K) qh as planes: [nsb][16] ++ [nsb][128] ++ [nsb][32]
+    constexpr int64_t BPB = Q5 ? 176 : 144;
+    constexpr int64_t HS = LAY == 1 ? 16 : BPB, QS = LAY == 1 ? 128 : BPB, QHS = LAY == 1 ? 32 : BPB;
+    const int64_t qoff = LAY == 1 ? 16 * bpr : (Q5 ? 48 : 16), qhoff = LAY == 1 ? 144 * bpr : 16;
     const uint8_t *wq0[NI];
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
         const int i = 8 * u + wave;
         const int64_t row = min(n0 + 32 * (i >> 2) + 8 * (i & 3) + (lane & 7), N - 1);
-        wq0[u] = (LAY == 1 ? W + row * 144 * bpr + 16 * bpr : W + row * 144 * bpr + 16) + 16 * (lane >> 3);
+        wq0[u] = W + row * BPB * bpr + qoff + 16 * (lane >> 3);
     }
     const int hrt = 2 * wave + kg;
     const int64_t hrow = min(n0 + 32 * hrt + lr, N - 1);
-    const uint8_t *wh0 = W + hrow * 144 * bpr;
+    const uint8_t *wh0 = W + hrow * BPB * bpr;
+    // qh (Q5_K): waves 4 .. 7, row tile wave - 4, lane = 32 g + row
+    const uint8_t *wqh0 = W + min(n0 + 32 * max(wave - 4, 0) + lr, N - 1) * BPB * bpr + qhoff + 16 * kg;
     auto stage_a = [&](int buf, int64_t sb) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
@@ -1675,6 +1693,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
             dma16(wq0[u] + QS * sb, &S.wq[st][i >> 2][72 * (i & 3)]);
         }
         if (wave < NI) dma16(wh0 + HS * sb, &S.wh[st][2 * wave][0]);
+        if constexpr (Q5)
+            if (wave >= 4) dma16(wqh0 + QHS * sb, &S.wqh[st][wave - 4][0]);
     };
 
     const int64_t sbb = nsb * split / KS, sbe = nsb * (split + 1) / KS;
@@ -1705,6 +1725,8 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
         // then per token tile its 16 MFMAs and right behind them its epilogue (v3's: tot -= dy * dmin * (sum_j m_j
         // bsum_j), then tot += dy * (d * isum)), so only one tile's integer accumulators are live
         i32x4 bw[4][4];
+        i32x4 qhv;
+        if constexpr (Q5) qhv = S.wqh[st][wr][32 * kg + lr];
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             const i32x4 w4 = S.wq[st][wr][swz(lr, 2 * p + kg)];
@@ -1737,6 +1759,18 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
                 const i32x4 a0 = S.a[buf][tt][swz(lr, 4 * p + kg)], a1 = S.a[buf][tt][swz(lr, 4 * p + 2 + kg)];
+                // Q5_K: hb*sc of sub-blocks 2p, 2p+1, made per token tile (held for all four pairs they spill)
+                i32x4 bh0, bh1;
+                if constexpr (Q5) {
+                    const uint32_t sdw = p < 2 ? sc_lo : sc_hi;
+                    const uint32_t s0 = (sdw >> (16 * (p & 1))) & 0xFF, s1 = (sdw >> (16 * (p & 1) + 8)) & 0xFF;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {     // hb * 2sc
+                        const uint32_t hx = (uint32_t)qhv[e];
+                        bh0[e] = mulb((hx >> (2 * p)) & 0x01010101u, 2 * s0);
+                        bh1[e] = mulb((hx >> (2 * p + 1)) & 0x01010101u, 2 * s1);
+                    }
+                }
 #if KCPP_GEMM_PROBE == 2
                 ah[0] += a0[0] * bw[p][0][0] + a1[1] * bw[p][3][1];
                 al[0] += a0[1] * bw[p][1][0] + a1[0] * bw[p][2][1];
@@ -1748,12 +1782,15 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
                     for (int i = 0; i < 16; ++i) z[i] = 0;
                     ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bw[p][0], z, 0, 0, 0);
                     al = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bw[p][1], z, 0, 0, 0);
+                    if constexpr (Q5) ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bh0, ah, 0, 0, 0);
                 } else {
                     ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bw[p][0], ah, 0, 0, 0);
                     al = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bw[p][1], al, 0, 0, 0);
+                    if constexpr (Q5) ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0, bh0, ah, 0, 0, 0);
                 }
                 ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bw[p][2], ah, 0, 0, 0);
                 al = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bw[p][3], al, 0, 0, 0);
+                if constexpr (Q5) ah = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1, bh1, ah, 0, 0, 0);
             }
             float dyv[16];
 #pragma unroll
@@ -1784,7 +1821,7 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
         // (in-order retire)
         if (NST == 3 && wn) {
             static_assert(NST != 3 || NI == 2, "vmcnt counts below assume two weight groups per wave");
-            if (wave < NI) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            if (wave < NI || (Q5 && wave >= 4)) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");   // 3 weight DMAs
             else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1943,7 +1980,13 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     // (split-K); its tile grid is split in two along K when it has <= 128 tiles.  Variant 11 forces v4 (split rule),
     // 13 v4 unsplit, 3 / 4 force v3.
     const bool v4_pick = gv == 0;
-    if ((type == KT_Q4_K || type == KT_Q4_K_RS) && (gv == 11 || gv == 12 || gv == 13 || gv == 14 || v4_pick) && bs_aligned && M > 32) {
+    // Q5_K: v4 with the fifth-bit MFMA (TPW 2 only), by default for the plain / residual projections only
+    // (tools/gemm_ab.py, v2 -> v4, Mixtral expert shapes: down 14336 -> 4096 (split-K) M = 128 134.3 -> 96.3 us,
+    // M = 512 151.4 -> 124.6; GLU 4096 -> 2 x 14336 M = 128 93.9 -> 125.9 (112 workgroups), M = 512 276.4 -> 281.5,
+    // so GLU stays on v2; variants 11 / 13 force v4 there too)
+    const bool q5 = (type == KT_Q5_K || type == KT_Q5_K_RS) && (mode == 0 || gv != 0);
+    if ((type == KT_Q4_K || type == KT_Q4_K_RS || q5) && (gv == 11 || gv == 12 || gv == 13 || gv == 14 || v4_pick) && bs_aligned &&
+        M > 32) {
         // v4: int8 MFMA straight from the Q8_K buffer (no fragment image); 128 x 128 tiles, split-K when the tile
         // grid is small
         const int64_t nt = (N + 127) / 128;
@@ -1957,13 +2000,15 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         // choice never changes a bit (tools/gemm_ab.py, M = 512, v4 -> v5: gate|up 28672 rows 214.1 -> 188.6 us,
         // gate + up 14336 rows 217.7 -> 201.0; q|k|v 6144 rows 52.3 -> 86.0 on its 96-workgroup grid, so not
         // there).  Variant 14 forces v5.
-        const bool v5 = gv == 14 || (gv == 0 && KS == 1 && MT * ((N + 255) / 256) >= 224);
+        const bool v5 = !q5 && (gv == 14 || (gv == 0 && KS == 1 && MT * ((N + 255) / 256) >= 224));
         const int64_t ntw = v5 ? (N + 255) / 256 : nt;
         const unsigned nwg = (unsigned)(MT * ntw * KS);
         const int XG = gv == 12 ? 2 : 1;
         auto launch4 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
-            auto kern = type == KT_Q4_K_RS ? (v5 ? k_gemm_q4v4<1, 4> : k_gemm_q4v4<1, 2>)
-                                           : (v5 ? k_gemm_q4v4<0, 4> : k_gemm_q4v4<0, 2>);
+            auto kern = type == KT_Q5_K_RS ? k_gemm_q4v4<KT_Q5_K, 1, 2>
+                        : type == KT_Q5_K  ? k_gemm_q4v4<KT_Q5_K, 0, 2>
+                        : type == KT_Q4_K_RS ? (v5 ? k_gemm_q4v4<KT_Q4_K, 1, 4> : k_gemm_q4v4<KT_Q4_K, 1, 2>)
+                                             : (v5 ? k_gemm_q4v4<KT_Q4_K, 0, 4> : k_gemm_q4v4<KT_Q4_K, 0, 2>);
             hipLaunchKernelGGL(kern, dim3(nwg), dim3(512), 0, s, (const uint8_t *)w, K, N, (const uint8_t *)act, M, Mp, MT,
                                y, ly, r, lr, KS, part, XG);
             KCPP_CHECK(hipGetLastError());

@@ -279,16 +279,17 @@ def test_gemm_v3_split_k(env, base, Kd, N, M):
     assert np.abs(outs[4] - want).max() <= 3e-6 * max(1.0, float(np.abs(want).max())) + 1e-5
 
 
-@pytest.mark.parametrize("base", [R.Q4_K, "rs"])
+@pytest.mark.parametrize("base", [R.Q4_K, "rs", R.Q5_K, "rs5"])
 @pytest.mark.parametrize("Kd,N,M", [(4096, 512, 37), (4096, 640, 128), (2048, 1024, 300), (14336, 256, 512),
                                     (4096, 384, 200)])
 def test_gemm_v4_int8_matches_v2_bitwise(env, base, Kd, N, M):
     """Q4_K GEMM v4 (v_mfma_i32_32x32x32_i8 on the Q8_K bytes, isum = 8 acc(q*(sc>>3)) + acc(q*(sc&7)) in int32,
     operands by LDS-DMA straight from the Q8_K buffer): the same integer sumi as v2's exact fp32 sums and the same
     per-super-block epilogue, so bit-identical unsplit (kcpp_gemm_set_variant(13)), plain+residual and GLU, ragged M
-    (token rows past M clamp to M - 1 and are not stored) and N; the split-K default (11) within the GEMM bar"""
+    (token rows past M clamp to M - 1 and are not stored) and N; the split-K default (11) within the GEMM bar.
+    Q5_K (base and RS layouts): the fifth bit as a third MFMA, hb*2sc into acc_h -- the same exact sumi"""
     torch, K = env
-    t = RS[R.Q4_K] if base == "rs" else R.Q4_K
+    t = {"rs": RS[R.Q4_K], "rs5": RS[R.Q5_K]}.get(base, base)
     s = sptr(torch)
     Xh = np.random.default_rng(M + Kd + 7).standard_normal((M, Kd)).astype(np.float32)
     X = torch.from_numpy(Xh).cuda()

@@ -1,5 +1,6 @@
-"""Prefill GEMM A/B (tools only): kcpp_gemm Q4_K_RS at the Llama-3-8B ubatch-512 shapes, kernel variant
-2 vs 3 (kcpp_gemm_set_variant), HIP-event timed over weights rotated past the Infinity Cache.
+"""Prefill GEMM A/B (tools only): kcpp_gemm Q4_K_RS / Q6_K_RS at the Llama-3-8B ubatch-512 shapes and Q5_K at the
+Mixtral expert shapes (GEMM_M tokens, GEMM_ONLY one shape): kernel variants (kcpp_gemm_set_variant, default 2 vs 3),
+HIP-event timed over weights rotated past the Infinity Cache.
 usage: python tools/gemm_ab.py [variants...]"""
 import json
 import os
@@ -20,7 +21,9 @@ def main():
     for name, t, Kd, N, mode in [("gate|up", K.Q4_K_RS, 4096, 28672, 0), ("qkv", K.Q4_K_RS, 4096, 6144, 0),
                                  ("wo", K.Q4_K_RS, 4096, 4096, 0), ("down", K.Q4_K_RS, 14336, 4096, 0),
                                  ("glu2", K.Q4_K_RS, 4096, 14336, 1), ("down6", K.Q6_K_RS, 14336, 4096, 0),
-                                 ("v6", K.Q6_K_RS, 4096, 1024, 0)]:
+                                 ("v6", K.Q6_K_RS, 4096, 1024, 0), ("glu5", K.Q5_K, 4096, 14336, 1),
+                                 ("down5", K.Q5_K, 14336, 4096, 0), ("glu5rs", K.Q5_K_RS, 4096, 14336, 1),
+                                 ("wo5", K.Q5_K, 4096, 4096, 0)]:
         if os.environ.get("GEMM_ONLY") and name != os.environ["GEMM_ONLY"]:
             continue
         nrot = 3
