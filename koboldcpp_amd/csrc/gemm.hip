@@ -1632,10 +1632,13 @@ __device__ __forceinline__ int mulb(uint32_t x, uint32_t s) {
 // a third MFMA per sub-block, into acc_h; isum = 8 acc_h + acc_l is again the CPU's exact int32 sumi
 // (ggml_vec_dot_q5_K_q8_K, ggml-quants.c), and the epilogue is unchanged.
 template <int TYPE, int LAY, int TPW>
+// GLU: W2 / Y2 set -- the grid's second half computes the up matrix into Y2 (one launch for both: twice the
+// workgroups on the small expert grids, no second ramp; every tile's arithmetic unchanged)
 __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                                      const uint8_t *__restrict__ act, int64_t M, int64_t Mp, int MT,
                                                      float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr,
-                                                     int KS, float *__restrict__ part, int XG) {
+                                                     int KS, float *__restrict__ part, int XG, const uint8_t *W2,
+                                                     float *Y2, int64_t ldy2) {
     constexpr int WT = 4 / TPW, WR = 8 / WT, NR = 32 * WR, NST = TPW == 2 ? 3 : 2, NI = WR / 2;
     constexpr bool Q5 = TYPE == KT_Q5_K;
     static_assert(TYPE == KT_Q4_K || (Q5 && TPW == 2), "v4 int8 GEMM: Q4_K (TPW 2 / 4) or Q5_K (TPW 2)");
@@ -1644,8 +1647,12 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave % WR, wt = wave / WR;
     const int lr = lane & 31, kg = lane >> 5;
-    const int64_t nwg = gridDim.x / KS, id = blockIdx.x % nwg;
-    const int split = (int)(blockIdx.x / nwg);
+    const int64_t per = W2 ? gridDim.x / 2 : gridDim.x;       // workgroups per matrix
+    const bool second = blockIdx.x >= per;
+    const int64_t bid = second ? blockIdx.x - per : blockIdx.x;
+    if (second) { W = W2; Y = Y2; ldy = ldy2; res = nullptr; }
+    const int64_t nwg = per / KS, id = bid % nwg;
+    const int split = (int)(bid / nwg);
     int64_t mt, nt;
     xcd_tile(id, nwg, MT, (N + NR - 1) / NR, XG, mt, nt);
     const int64_t m0 = mt * 128, n0 = nt * NR;
@@ -1980,11 +1987,12 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     // (split-K); its tile grid is split in two along K when it has <= 128 tiles.  Variant 11 forces v4 (split rule),
     // 13 v4 unsplit, 3 / 4 force v3.
     const bool v4_pick = gv == 0;
-    // Q5_K: v4 with the fifth-bit MFMA (TPW 2 only), by default for the plain / residual projections only
-    // (tools/gemm_ab.py, v2 -> v4, Mixtral expert shapes: down 14336 -> 4096 (split-K) M = 128 134.3 -> 96.3 us,
-    // M = 512 151.4 -> 124.6; GLU 4096 -> 2 x 14336 M = 128 93.9 -> 125.9 (112 workgroups), M = 512 276.4 -> 281.5,
-    // so GLU stays on v2; variants 11 / 13 force v4 there too)
-    const bool q5 = (type == KT_Q5_K || type == KT_Q5_K_RS) && (mode == 0 || gv != 0);
+    // Q5_K: v4 with the fifth-bit MFMA (TPW 2 only) for the plain / residual projections (tools/gemm_ab.py, v2 -> v4,
+    // Mixtral expert shapes: down 14336 -> 4096 (split-K) M = 128 134.3 -> 96.3 us, M = 512 151.4 -> 124.6) and for
+    // GLU (gate + up in one launch) up to 256 tokens: 4096 -> 2 x 14336 M = 128 93.9 -> 73.1, but M = 512 ~270 ->
+    // ~305, so v2 there.  GLU is unsplit on both kernels and bitwise equal (test_gemm_v4_int8_matches_v2_bitwise), so
+    // the token-count rule does not change a bit.  Variants 11 / 13 force v4.
+    const bool q5 = (type == KT_Q5_K || type == KT_Q5_K_RS) && (mode == 0 || gv != 0 || Mp <= 256);
     if ((type == KT_Q4_K || type == KT_Q4_K_RS || q5) && (gv == 11 || gv == 12 || gv == 13 || gv == 14 || v4_pick) && bs_aligned &&
         M > 32) {
         // v4: int8 MFMA straight from the Q8_K buffer (no fragment image); 128 x 128 tiles, split-K when the tile
@@ -2004,13 +2012,13 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         const int64_t ntw = v5 ? (N + 255) / 256 : nt;
         const unsigned nwg = (unsigned)(MT * ntw * KS);
         const int XG = gv == 12 ? 2 : 1;
-        auto launch4 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
+        auto launch4 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr, const void *w2, float *y2) -> int {
             auto kern = type == KT_Q5_K_RS ? k_gemm_q4v4<KT_Q5_K, 1, 2>
                         : type == KT_Q5_K  ? k_gemm_q4v4<KT_Q5_K, 0, 2>
                         : type == KT_Q4_K_RS ? (v5 ? k_gemm_q4v4<KT_Q4_K, 1, 4> : k_gemm_q4v4<KT_Q4_K, 1, 2>)
                                              : (v5 ? k_gemm_q4v4<KT_Q4_K, 0, 4> : k_gemm_q4v4<KT_Q4_K, 0, 2>);
-            hipLaunchKernelGGL(kern, dim3(nwg), dim3(512), 0, s, (const uint8_t *)w, K, N, (const uint8_t *)act, M, Mp, MT,
-                               y, ly, r, lr, KS, part, XG);
+            hipLaunchKernelGGL(kern, dim3(nwg * (w2 ? 2 : 1)), dim3(512), 0, s, (const uint8_t *)w, K, N, (const uint8_t *)act,
+                               M, Mp, MT, y, ly, r, lr, KS, part, XG, (const uint8_t *)w2, y2, (int64_t)N);
             KCPP_CHECK(hipGetLastError());
             if (KS > 1) {
                 hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,
@@ -2019,9 +2027,9 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
             }
             return 0;
         };
-        int rc = launch4(W, Y, ldy, mode == 1 ? nullptr : res, ldr);
+        // GLU (KS = 1): gate and up in one launch
+        int rc = launch4(W, Y, ldy, mode == 1 ? nullptr : res, ldr, mode == 1 ? W2 : nullptr, up);
         if (rc || mode != 1) return rc;
-        if ((rc = launch4(W2, up, N, nullptr, 0))) return rc;
         hipLaunchKernelGGL(k_silu_mul_strided, dim3((unsigned)((N * M + 255) / 256)), dim3(256), 0, s, Y, ldy, up, N, M);
         KCPP_CHECK(hipGetLastError());
         return 0;
