@@ -56,6 +56,13 @@ int kcpp_gemv(int type, const void *W, const void *W2, int64_t K, int64_t N, con
 int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M);
 int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream);
+/* Grouped expert GEMM for MoE prefill (replaces ggml_cuda_mul_mat_id's per-expert loop, ggml-cuda.cu:2003-2139):
+ * ng groups of cnt_host[e] rows (act: Q8_K of all M rows, grouped back to back; cnt_dev the same counts on the
+ * device), group e against W + e*wstride (and W2 + e*wstride); mode 0 plain, 1 silu(g)*u with up [M][N] scratch.
+ * Q4_K / Q5_K and their RS layouts; Y is [M][N]. */
+int kcpp_gemm_grouped(int type, const void *W, const void *W2, int64_t wstride, int64_t K, int64_t N, const void *act,
+                      int64_t M, const int32_t *cnt_host, const int32_t *cnt_dev, int ng, float *Y, float *up, int mode,
+                      void *stream);
 /* Q4_K GEMM kernel generation for later kcpp_gemm calls: 3 (= 0, the default; env KCPP_GEMM_V) = 128(64) x 128
  * tiles, LDS-DMA activation, register-dequantized weights; 2 = 128(256) x 64 tiles, LDS weights.  Same results
  * bit for bit.  Returns the previous value. */
@@ -359,6 +366,10 @@ int kcpp_model_moe_trace_read(kcpp_model *m, int32_t *out, int n);
 int kcpp_model_set_fused_route(kcpp_model *m, int on);
 /* enqueued so far (graph captures count once): routed gate|up launches (low 32 bits), two-slot down launches (high) */
 int64_t kcpp_model_fused_route_count(kcpp_model *m);
+/* MoE prefill: grouped expert GEMMs (1, default) or the per-expert loop (0); returns the previous setting.
+ * kcpp_model_moe_grouped_count: grouped layers run so far (diagnostics) */
+int kcpp_model_set_moe_grouped(kcpp_model *m, int on);
+int64_t kcpp_model_moe_grouped_count(kcpp_model *m);
 /* K / V cache types (llama_context_params type_k / type_v): KT_F16 (default) or quantized KT_Q8_0 / KT_Q4_0 for
  * both (koboldcpp --quantkv).  Reallocates and clears the caches; quantized caches run single-token decode
  * through the unfused per-op path and refuse kcpp_model_kv_shift (koboldcpp turns context shift off with

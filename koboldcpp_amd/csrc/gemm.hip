@@ -1633,12 +1633,16 @@ __device__ __forceinline__ int mulb(uint32_t x, uint32_t s) {
 // (ggml_vec_dot_q5_K_q8_K, ggml-quants.c), and the epilogue is unchanged.
 template <int TYPE, int LAY, int TPW>
 // GLU: W2 / Y2 set -- the grid's second half computes the up matrix into Y2 (one launch for both: twice the
-// workgroups on the small expert grids, no second ramp; every tile's arithmetic unchanged)
+// workgroups on the small expert grids, no second ramp; every tile's arithmetic unchanged).
+// Grouped (MoE prefill, gcnt set, KS = 1): act holds gne groups of token rows back to back (Q8_K planes of M rows in
+// all), group e = gcnt[e] rows against weight matrix W + e wstride; the grid is every group's tile grid in order,
+// each group's outputs at its first row of Y (and Y2).
 __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                                      const uint8_t *__restrict__ act, int64_t M, int64_t Mp, int MT,
                                                      float *__restrict__ Y, int64_t ldy, const float *res, int64_t ldr,
                                                      int KS, float *__restrict__ part, int XG, const uint8_t *W2,
-                                                     float *Y2, int64_t ldy2) {
+                                                     float *Y2, int64_t ldy2, const int32_t *gcnt, int gne,
+                                                     int64_t wstride) {
     constexpr int WT = 4 / TPW, WR = 8 / WT, NR = 32 * WR, NST = TPW == 2 ? 3 : 2, NI = WR / 2;
     constexpr bool Q5 = TYPE == KT_Q5_K;
     static_assert(TYPE == KT_Q4_K || (Q5 && TPW == 2), "v4 int8 GEMM: Q4_K (TPW 2 / 4) or Q5_K (TPW 2)");
@@ -1649,17 +1653,39 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
     const int lr = lane & 31, kg = lane >> 5;
     const int64_t per = W2 ? gridDim.x / 2 : gridDim.x;       // workgroups per matrix
     const bool second = blockIdx.x >= per;
-    const int64_t bid = second ? blockIdx.x - per : blockIdx.x;
+    int64_t bid = second ? blockIdx.x - per : blockIdx.x;
     if (second) { W = W2; Y = Y2; ldy = ldy2; res = nullptr; }
-    const int64_t nwg = per / KS, id = bid % nwg;
-    const int split = (int)(bid / nwg);
-    int64_t mt, nt;
-    xcd_tile(id, nwg, MT, (N + NR - 1) / NR, XG, mt, nt);
-    const int64_t m0 = mt * 128, n0 = nt * NR;
     const int64_t nsb = K / 256, bpr = nsb;
     const int8_t *qs = (const int8_t *)act;
     const float *dq = (const float *)(act + M * K);
     const int16_t *bsq = (const int16_t *)(act + M * K + M * nsb * 4);
+    int64_t nwg = per / KS;
+    if (gcnt) {                 // uniform scan for this workgroup's group (<= 64 groups)
+        const int64_t ntn = (N + NR - 1) / NR;
+        int64_t t0 = 0, r0 = 0;
+        int e = 0;
+        for (; e < gne; ++e) {
+            const int64_t te = (gcnt[e] + 127) / 128 * ntn;
+            if (bid < t0 + te) break;
+            t0 += te;
+            r0 += gcnt[e];
+        }
+        if (e >= gne) return;
+        bid -= t0;
+        W += e * wstride;
+        Y += r0 * ldy;
+        qs += r0 * K;
+        dq += r0 * nsb;
+        bsq += r0 * (K / 16);
+        M = gcnt[e];
+        MT = (int)((M + 127) / 128);
+        nwg = MT * ntn;
+    }
+    const int64_t id = bid % nwg;
+    const int split = (int)(bid / nwg);
+    int64_t mt, nt;
+    xcd_tile(id, nwg, MT, (N + NR - 1) / NR, XG, mt, nt);
+    const int64_t m0 = mt * 128, n0 = nt * NR;
     // DMA assignments (per super-block): A: token tile wave & 3, sub-blocks 4 (wave >> 2) .. +4; bsums: waves 0-3
     // (tile = wave); dy: waves 4, 5 (tokens 64 (wave - 4) .. +64); weights: NI groups of 8 rows, group i = 8u + wave
     // (row tile i >> 2, rows 8 (i & 3) ..); headers: waves 0 .. NI - 1 (row tiles 2 wave + (lane >> 5))
@@ -1931,6 +1957,42 @@ int kcpp_gemm_q80_glu_q80(const void *W, const void *W2, int64_t K, int64_t N, c
                           (uint8_t *)ws + o_up + ((M * N * 4 + 255) & ~255LL), (hipStream_t)stream);
 }
 
+// grouped expert GEMM (MoE prefill): ng groups of cnt_host[e] token rows (act: Q8_K of all M = sum rows, grouped
+// back to back), group e against W + e wstride (and W2 + e wstride); mode 0: Y = X W^T, mode 1: Y = silu(X W^T) *
+// (X W2^T) with up [M][N] as scratch.  cnt_dev: the same counts on the device (read by the kernel); Q4_K / Q5_K
+// (+ RS) only, K a multiple of 256.  One launch per mode (+ the GLU product); every row's arithmetic is v4's unsplit
+// (bitwise the single-expert kcpp_gemm result wherever that runs unsplit)
+int kcpp_gemm_grouped(int type, const void *W, const void *W2, int64_t wstride, int64_t K, int64_t N, const void *act,
+                      int64_t M, const int32_t *cnt_host, const int32_t *cnt_dev, int ng, float *Y, float *up, int mode,
+                      void *stream) {
+    if (type != KT_Q4_K && type != KT_Q4_K_RS && type != KT_Q5_K && type != KT_Q5_K_RS) return -1;
+    if (K % 256 || ng < 1 || ng > 64 || !cnt_dev || !cnt_host || (mode == 1 && (!W2 || !up)) || mode < 0 || mode > 1)
+        return -1;
+    if (((uintptr_t)((const uint8_t *)act + M * K + M * (K / 256) * 4) & 15) != 0) return -3;
+    int64_t tiles = 0, rows = 0;
+    const int64_t ntn = (N + 127) / 128;
+    for (int e = 0; e < ng; ++e) {
+        if (cnt_host[e] < 0) return -1;
+        tiles += (cnt_host[e] + 127) / 128 * ntn;
+        rows += cnt_host[e];
+    }
+    if (rows != M) return -1;
+    if (!tiles) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    auto kern = type == KT_Q5_K_RS ? k_gemm_q4v4<KT_Q5_K, 1, 2>
+                : type == KT_Q5_K  ? k_gemm_q4v4<KT_Q5_K, 0, 2>
+                : type == KT_Q4_K_RS ? k_gemm_q4v4<KT_Q4_K, 1, 2> : k_gemm_q4v4<KT_Q4_K, 0, 2>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(tiles * (mode == 1 ? 2 : 1))), dim3(512), 0, s, (const uint8_t *)W, K, N,
+                       (const uint8_t *)act, M, M, 1, Y, N, (const float *)nullptr, (int64_t)0, 1, (float *)nullptr, 1,
+                       (const uint8_t *)(mode == 1 ? W2 : nullptr), up, N, cnt_dev, ng, wstride);
+    KCPP_CHECK(hipGetLastError());
+    if (mode == 1) {
+        hipLaunchKernelGGL(k_silu_mul_strided, dim3((unsigned)((N * M + 255) / 256)), dim3(256), 0, s, Y, N, up, N, M);
+        KCPP_CHECK(hipGetLastError());
+    }
+    return 0;
+}
+
 int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream) {
     if (type == KT_Q8_0_T) {          // the tile layout (gemm_q80t.hip): every M, activation KT_Q8_0_TA
@@ -2018,7 +2080,8 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
                         : type == KT_Q4_K_RS ? (v5 ? k_gemm_q4v4<KT_Q4_K, 1, 4> : k_gemm_q4v4<KT_Q4_K, 1, 2>)
                                              : (v5 ? k_gemm_q4v4<KT_Q4_K, 0, 4> : k_gemm_q4v4<KT_Q4_K, 0, 2>);
             hipLaunchKernelGGL(kern, dim3(nwg * (w2 ? 2 : 1)), dim3(512), 0, s, (const uint8_t *)w, K, N, (const uint8_t *)act,
-                               M, Mp, MT, y, ly, r, lr, KS, part, XG, (const uint8_t *)w2, y2, (int64_t)N);
+                               M, Mp, MT, y, ly, r, lr, KS, part, XG, (const uint8_t *)w2, y2, (int64_t)N,
+                               (const int32_t *)nullptr, 0, (int64_t)0);
             KCPP_CHECK(hipGetLastError());
             if (KS > 1) {
                 hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,

@@ -119,6 +119,11 @@ struct kcpp_model {
     int64_t n_fused_route = 0;       // routed gate|up launches enqueued (tests: the fused path really ran)
     bool no_pair_down = false;       // MoE decode: the two slots' down projections as two chained launches (A/B tests)
     int64_t n_pair_down = 0;         // two-slot down launches enqueued
+    bool no_moe_grouped = false;     // MoE prefill: per-expert GEMM loop instead of the grouped launches (A/B tests)
+    int64_t n_moe_grouped = 0;       // grouped MoE prefill layers run
+    float *moe_gx = nullptr, *moe_gh = nullptr, *moe_gup = nullptr, *moe_geo = nullptr;   // grouped prefill: [ubatch*k]
+    void *moe_gact = nullptr;        // rows (gathered input, GLU output, up scratch, down output), their Q8_K
+    int32_t *moe_gcnt = nullptr, *moe_gcnt_h = nullptr;   // per-expert row counts (device, pinned host)
     int32_t *moe_ids_h = nullptr;    // pinned host copies (prefill routing)
     float *moe_w_h = nullptr;
     int32_t *moe_rows_h = nullptr;
@@ -452,7 +457,9 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
         F(L.qkv_base); F(L.glu_base); F(L.kc); F(L.vc);
     }
     F(m->hglu); F(m->moe_ids); F(m->moe_w); F(m->moe_rows); F(m->moe_rw); F(m->moe_slots);
-    for (void *p : {(void *)m->moe_ids_h, (void *)m->moe_w_h, (void *)m->moe_rows_h, (void *)m->moe_rw_h})
+    F(m->moe_gx); F(m->moe_gh); F(m->moe_gup); F(m->moe_geo); F(m->moe_gact); F(m->moe_gcnt);
+    for (void *p : {(void *)m->moe_ids_h, (void *)m->moe_w_h, (void *)m->moe_rows_h, (void *)m->moe_rw_h,
+                    (void *)m->moe_gcnt_h})
         if (p) hipHostFree(p);
     F(m->x); F(m->qkv); F(m->attn); F(m->h); F(m->logits); F(m->q16); F(m->act); F(m->act2); F(m->fa_ws);
     F(m->gemm_ws); F(m->gemm_ws2); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
@@ -720,6 +727,14 @@ extern "C" int kcpp_model_set_fused_route(kcpp_model *m, int on) {
     return 0;
 }
 extern "C" int64_t kcpp_model_fused_route_count(kcpp_model *m) { return m->n_fused_route + (m->n_pair_down << 32); }
+// MoE prefill: grouped expert GEMMs (one launch for every expert's gate|up, one for every down; default) or the
+// per-expert loop; returns the previous setting.  kcpp_model_moe_grouped_count: grouped layers run so far.
+extern "C" int kcpp_model_set_moe_grouped(kcpp_model *m, int on) {
+    const int old = !m->no_moe_grouped;
+    m->no_moe_grouped = !on;
+    return old;
+}
+extern "C" int64_t kcpp_model_moe_grouped_count(kcpp_model *m) { return m->n_moe_grouped; }
 extern "C" int kcpp_model_moe_trace_read(kcpp_model *m, int32_t *out, int n) {
     if (!m->moe_trace || n < 0 || n > (int)m->layers.size() * std::max(1, m->hp.n_expert_used)) { g_err = "moe trace"; return -1; }
     RT_CHECK(hipStreamSynchronize(m->stream));
@@ -963,6 +978,56 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
 // MoE FFN for a ubatch of T tokens: routing on the GPU, one host sync to group the tokens by expert
 // (ggml_cuda_mul_mat_id does the same, ggml-cuda.cu:2003-2139), then per expert with tokens: gather
 // the normalized rows, gate|up GEMM with silu*up, down GEMM, weighted scatter into the top-k slots.
+static bool grouped_type(int t) { return t == KT_Q4_K || t == KT_Q4_K_RS || t == KT_Q5_K || t == KT_Q5_K_RS; }
+
+// grouped MoE prefill (after routing): every routed row gathered in expert order, one Q8_K quantization, the gate|up
+// GEMMs of all experts in one launch (kcpp_gemm_grouped), the down GEMMs likewise (or per expert for a type the
+// grouped kernel lacks, e.g. Q6_K), one scatter -- 5-6 launches per layer instead of 6 per active expert, and grids
+// that fill the GPU at ~ubatch*k/n_expert rows per expert.  Per row the arithmetic is the per-expert path's v4
+// (unsplit), so gate|up is bitwise that path's and down within its split-K re-association.
+static int moe_prefill_grouped(kcpp_model *m, const KLayer &L, int T, const int *cnt, const int *off) {
+    const kcpp_hparams &hp = m->hp;
+    const int64_t E = hp.n_embd, F = hp.n_ff, UB = m->ub;
+    const int NU = hp.n_expert_used, NE = hp.n_expert;
+    const KTensor *t = L.t;
+    hipStream_t s = m->stream;
+    const int64_t R = (int64_t)T * NU;
+    if (!m->moe_gx) {
+        const int64_t RM = UB * NU;
+        if (hipMalloc(&m->moe_gx, RM * E * 4) != hipSuccess || hipMalloc(&m->moe_gh, RM * F * 4) != hipSuccess ||
+            hipMalloc(&m->moe_gup, RM * F * 4) != hipSuccess || hipMalloc(&m->moe_geo, RM * E * 4) != hipSuccess ||
+            hipMalloc(&m->moe_gact, kcpp_act_bytes(KT_Q4_K, std::max(E, F), RM)) != hipSuccess ||
+            hipMalloc(&m->moe_gcnt, 64 * 4) != hipSuccess ||
+            hipHostMalloc((void **)&m->moe_gcnt_h, 64 * 4, hipHostMallocDefault) != hipSuccess) {
+            g_err = "grouped MoE buffers";
+            return -2;
+        }
+    }
+    memcpy(m->moe_gcnt_h, cnt, (size_t)NE * 4);        // the previous layer's copy is done (moe_prefill synchronized)
+    RT_CHECK(hipMemcpyAsync(m->moe_gcnt, m->moe_gcnt_h, (size_t)NE * 4, hipMemcpyHostToDevice, s));
+    RC(kcpp_moe_gather(m->attn, E, m->moe_rows, (int)R, E, m->moe_gx, s));
+    RC(kcpp_quantize_act(kcpp_vec_dot_type(t[6].type), m->moe_gx, E, m->moe_gact, E, R, s));
+    RC(kcpp_gemm_grouped(t[6].type, t[6].d, t[7].d, t[6].slice_bytes, E, F, m->moe_gact, R, cnt, m->moe_gcnt, NE,
+                         m->moe_gh, m->moe_gup, 1, s));
+    if (grouped_type(t[8].type) && kcpp_vec_dot_type(t[8].type) == KT_Q8_K) {
+        RC(kcpp_quantize_act(KT_Q8_K, m->moe_gh, F, m->moe_gact, F, R, s));
+        RC(kcpp_gemm_grouped(t[8].type, t[8].d, nullptr, t[8].slice_bytes, F, E, m->moe_gact, R, cnt, m->moe_gcnt, NE,
+                             m->moe_geo, nullptr, 0, s));
+    } else {
+        for (int e = 0; e < NE; ++e) {
+            const int n = cnt[e];
+            if (!n) continue;
+            KTensor d = t[8];
+            d.d = (uint8_t *)t[8].d + e * t[8].slice_bytes;
+            RC(kcpp_quantize_act(kcpp_vec_dot_type(d.type), m->moe_gh + (int64_t)off[e] * F, F, m->act2, F, n, s));
+            RC(matmul(m, d, nullptr, m->act2, n, m->moe_geo + (int64_t)off[e] * E, E, nullptr, 0, 0));
+        }
+    }
+    RC(kcpp_moe_scatter(m->moe_slots, E, m->moe_geo, m->moe_rows + UB * NU, m->moe_rw, (int)R, E, s));
+    m->n_moe_grouped++;
+    return kcpp_moe_combine(m->x, m->moe_slots, (int64_t)T * E, NU, (int64_t)T * E, s);
+}
+
 static int moe_prefill(kcpp_model *m, const KLayer &L, int T) {
     const kcpp_hparams &hp = m->hp;
     const int64_t E = hp.n_embd, F = hp.n_ff, UB = m->ub;
@@ -994,6 +1059,9 @@ static int moe_prefill(kcpp_model *m, const KLayer &L, int T) {
         }
     RT_CHECK(hipMemcpyAsync(m->moe_rows, m->moe_rows_h, (size_t)2 * UB * NU * 4, hipMemcpyHostToDevice, s));
     RT_CHECK(hipMemcpyAsync(m->moe_rw, m->moe_rw_h, (size_t)T * NU * 4, hipMemcpyHostToDevice, s));
+    if (!m->no_moe_grouped && t[6].type == t[7].type && grouped_type(t[6].type) && E % 256 == 0 && F % 256 == 0 &&
+        NE <= 64)
+        return moe_prefill_grouped(m, L, T, cnt, off);
     float *xg = m->qkv, *eo = m->hglu;
     for (int e = 0; e < NE; ++e) {
         const int n = cnt[e];

@@ -310,3 +310,77 @@ def test_moe_routing_inside_glu_launch_bitwise(env, policy, graphs):
         traces.append(np.array(tr))
     assert np.array_equal(traces[0], traces[1])
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
+@pytest.mark.parametrize("t", [R.Q4_K, R.Q5_K, 113])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_gemm_grouped_matches_per_expert_bitwise(env, t, mode):
+    """kcpp_gemm_grouped (every expert's GEMM in one launch: the MoE prefill of ggml_cuda_mul_mat_id,
+    ggml-cuda.cu:2003-2139) == kcpp_gemm on each expert's own rows with the unsplit kernels
+    (kcpp_gemm_set_variant(13)), bit for bit, plain and GLU, over ragged counts (empty experts, 1 row, > 256 rows)"""
+    torch, K = env
+    s = torch.cuda.current_stream().cuda_stream
+    Kd, N = 2048, 640
+    cnt = [37, 0, 1, 129, 300, 31, 64, 5]
+    NE, M = len(cnt), sum(cnt)
+    rb = K.row_bytes(t, Kd) * N
+    W = torch.empty(NE * rb, dtype=torch.uint8, device="cuda")
+    W2 = torch.empty(NE * rb, dtype=torch.uint8, device="cuda")
+    for e in range(NE):
+        K.call("kcpp_weight_synth", t, 1, 50 + e, W.data_ptr() + e * rb, Kd, N, s)
+        K.call("kcpp_weight_synth", t, 1, 80 + e, W2.data_ptr() + e * rb, Kd, N, s)
+    X = torch.randn(M, Kd, generator=torch.Generator(device="cpu").manual_seed(M + t + mode)).cuda()
+    vt = K.vec_dot_type(R.Q4_K)
+    act = torch.zeros(K.act_bytes(R.Q4_K, Kd, M), dtype=torch.uint8, device="cuda")
+    K.call("kcpp_quantize_act", vt, X.data_ptr(), Kd, act.data_ptr(), Kd, M, s)
+    cnt_dev = torch.tensor(cnt, dtype=torch.int32, device="cuda")
+    cnt_host = (ctypes.c_int32 * NE)(*cnt)
+    Y = torch.full((M, N), float("nan"), device="cuda")
+    up = torch.empty(M, N, device="cuda")
+    K.call("kcpp_gemm_grouped", t, W.data_ptr(), W2.data_ptr() if mode else None, rb, Kd, N, act.data_ptr(), M,
+           cnt_host, cnt_dev.data_ptr(), NE, Y.data_ptr(), up.data_ptr() if mode else None, mode, s)
+    torch.cuda.synchronize()
+    got = Y.cpu().numpy()
+    bad = []
+    try:
+        K.raw().kcpp_gemm_set_variant(13)
+        r0 = 0
+        for e, n in enumerate(cnt):
+            if n:
+                ae = torch.zeros(K.act_bytes(R.Q4_K, Kd, n), dtype=torch.uint8, device="cuda")
+                K.call("kcpp_quantize_act", vt, X[r0:r0 + n].contiguous().data_ptr(), Kd, ae.data_ptr(), Kd, n, s)
+                ws = torch.empty(K.raw().kcpp_gemm_workspace_bytes(t, Kd, N, n), dtype=torch.uint8, device="cuda")
+                Ye = torch.empty(n, N, device="cuda")
+                K.call("kcpp_gemm", t, W.data_ptr() + e * rb, W2.data_ptr() + e * rb if mode else None, Kd, N,
+                       ae.data_ptr(), n, Ye.data_ptr(), N, None, N, mode, ws.data_ptr(), s)
+                torch.cuda.synchronize()
+                want = Ye.cpu().numpy()
+                if not np.array_equal(got[r0:r0 + n].view(np.uint32), want.view(np.uint32)):
+                    bad.append((e, n, float(np.nanmax(np.abs(got[r0:r0 + n] - want)))))
+            r0 += n
+    finally:
+        K.raw().kcpp_gemm_set_variant(0)
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("policy", ["q5_k_f16router", "mixtral_q5_k_m"])
+def test_moe_grouped_prefill_matches_per_expert(env, policy):
+    """MoE prefill with the grouped expert GEMMs (default) vs the per-expert loop: gate|up bitwise (unsplit v4 on
+    both), down within split-K re-association, so logits within the GEMM bar; the grouped path really ran (and the
+    Q6_K down of the 'more bits' layers took its per-expert fallback)"""
+    torch, K = env
+    hp = R.TINY_MOE
+    types = R.moe_types(hp["n_layer"]) if policy.startswith("q5_k") else R.mixtral_q5_k_m_types(hp["n_layer"])
+    prompt = [int(v) for v in np.random.default_rng(5).integers(1, 500, size=150)]
+    outs = []
+    for grouped in (True, False):
+        m = K.Model(hp, types)
+        m.set_moe_grouped(grouped)
+        m.synth(77)
+        lg = [m.decode(prompt, 0), m.decode([9], len(prompt))]
+        assert (m.moe_grouped_count() > 0) == grouped
+        m.close()
+        outs.append(np.array(lg))
+    assert np.isfinite(outs[0]).all()
+    d = np.abs(outs[0] - outs[1]).max()
+    assert d < TOL_MAX, d
