@@ -59,10 +59,12 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
 /* Grouped expert GEMM for MoE prefill (replaces ggml_cuda_mul_mat_id's per-expert loop, ggml-cuda.cu:2003-2139):
  * ng groups of cnt_host[e] rows (act: Q8_K of all M rows, grouped back to back; cnt_dev the same counts on the
  * device), group e against W + e*wstride (and W2 + e*wstride); mode 0 plain, 1 silu(g)*u with up [M][N] scratch.
- * Q4_K / Q5_K and their RS layouts; Y is [M][N]. */
+ * Q4_K / Q5_K and their RS layouts; Q6_K_RS in mode 0 with ws of kcpp_gemm_grouped_ws_bytes (else ws unused,
+ * may be NULL); Y is [M][N]. */
+int64_t kcpp_gemm_grouped_ws_bytes(int type, int64_t K, int64_t M, int ng);
 int kcpp_gemm_grouped(int type, const void *W, const void *W2, int64_t wstride, int64_t K, int64_t N, const void *act,
                       int64_t M, const int32_t *cnt_host, const int32_t *cnt_dev, int ng, float *Y, float *up, int mode,
-                      void *stream);
+                      void *ws, void *stream);
 /* Q4_K GEMM kernel generation for later kcpp_gemm calls: 3 (= 0, the default; env KCPP_GEMM_V) = 128(64) x 128
  * tiles, LDS-DMA activation, register-dequantized weights; 2 = 128(256) x 64 tiles, LDS weights.  Same results
  * bit for bit.  Returns the previous value. */

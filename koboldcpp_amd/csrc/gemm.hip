@@ -1193,20 +1193,42 @@ __global__ void k_splitk_reduce(const float *__restrict__ part, int KS, int64_t 
 // k order: MFMA step s = 4u + g (u = RS unit (h = u >> 1, lh = u & 1), g = 0..3), lane half kg, half e:
 //   k = 128 h + 16 lh + 32 g + 8 kg + e    -- one 16-element sub-block per fragment (one scale), the lane's
 // bytes 8kg..8kg+7 of the unit's ql-lo / ql-hi / qh planes (dequantize_row_q6_K, ggml-quants.c:2978).
+// grouped layouts (MoE prefill): group e's gcnt[e] real rows sit at virtual rows [P_e, P_e + 128 ceil(n_e / 128)),
+// P_e = the padded sizes before it; vrow -> (group, its virtual base, its real first row, its count)
+__device__ __forceinline__ int grp_find(const int32_t *gcnt, int gne, int64_t v, int64_t &P, int64_t &r0, int64_t &n) {
+    P = 0;
+    r0 = 0;
+    for (int e = 0; e < gne; ++e) {
+        const int64_t c = gcnt[e], pe = (c + 127) / 128 * 128;
+        if (v < P + pe) { n = c; return e; }
+        P += pe;
+        r0 += c;
+    }
+    n = 0;
+    return -1;
+}
+
+// gcnt set: the image has Mp virtual rows of the grouped layout (grp_find), real rows from the M-row Q8_K act
 __global__ void k_act_frag6(const uint8_t *__restrict__ act, int64_t K, int64_t M, int64_t Mp, h8v *__restrict__ af,
-                            float *__restrict__ dyT) {
+                            float *__restrict__ dyT, const int32_t *gcnt, int gne) {
     const int64_t nA = Mp * K / 8, nD = Mp * (K / 256);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int8_t *qs = (const int8_t *)act;
     const float *d = (const float *)(act + M * K);
+    auto real = [&](int64_t vm) -> int64_t {          // virtual row -> real row, or -1
+        if (!gcnt) return vm < M ? vm : -1;
+        int64_t P, r0, n;
+        if (grp_find(gcnt, gne, vm, P, r0, n) < 0) return -1;
+        return vm - P < n ? r0 + (vm - P) : -1;
+    };
     if (i < nA) {
         const int lane = (int)(i & 63), kg = lane >> 5;
         const int64_t s16 = (i >> 6) % (K / 16), mt = (i >> 6) / (K / 16);
-        const int64_t m = 32 * mt + (lane & 31);
+        const int64_t m = real(32 * mt + (lane & 31));
         const int u = (int)((s16 >> 2) & 3), g = (int)(s16 & 3);
         const int64_t k0 = 256 * (s16 >> 4) + 128 * (u >> 1) + 16 * (u & 1) + 32 * g + 8 * kg;
         uint2 v = make_uint2(0, 0);
-        if (m < M) v = *(const uint2 *)(qs + m * K + k0);
+        if (m >= 0) v = *(const uint2 *)(qs + m * K + k0);
         h8v r;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1216,8 +1238,8 @@ __global__ void k_act_frag6(const uint8_t *__restrict__ act, int64_t K, int64_t 
         af[i] = r;
     } else if (i < nA + nD) {
         const int64_t j = i - nA;
-        const int64_t sb = j / Mp, m = j % Mp;
-        dyT[j] = m < M ? d[m * (K / 256) + sb] : 0.0f;
+        const int64_t sb = j / Mp, m = real(j % Mp);
+        dyT[j] = m >= 0 ? d[m * (K / 256) + sb] : 0.0f;
     }
 }
 
@@ -1230,7 +1252,8 @@ template <int NW, int BMT>
 __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6v3(const uint8_t *__restrict__ W, int64_t K, int64_t N,
                                                          const h8v *__restrict__ af, const float *__restrict__ dyT,
                                                          int64_t M, int64_t Mp, int MT, float *__restrict__ Y, int64_t ldy,
-                                                         const float *res, int64_t ldr, int KS, float *__restrict__ part) {
+                                                         const float *res, int64_t ldr, int KS, float *__restrict__ part,
+                                                         const int32_t *gcnt, int gne, int64_t wstride) {
     constexpr int TPW = 4 * BMT / NW;
     constexpr int SPW = 16 * BMT / NW;
     static_assert(TPW >= 1 && SPW >= 1, "tile shape");
@@ -1254,6 +1277,13 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6v3(const uint8_t *__restr
     }
     const int64_t m0 = mt * 32 * BMT, n0 = nt * 128;
     const int64_t nsb = K / 256, bpr = nsb;
+    // grouped (KS = 1, 32 BMT divides 128): the tile's group -> its weights; rows stored back at real positions
+    int64_t gP = 0, gr0 = 0, gn = 0;
+    if (gcnt) {
+        const int e = grp_find(gcnt, gne, m0, gP, gr0, gn);
+        if (e < 0) return;
+        W += e * wstride;
+    }
     const int64_t nrow = min(n0 + 32 * wr + lr, N - 1);
     const uint8_t *row = W + nrow * 210 * bpr;
     const uint8_t *plo = row + 8 * kg, *phi = row + 64 * bpr + 8 * kg, *pqh = row + 128 * bpr + 8 * kg;
@@ -1359,7 +1389,9 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6v3(const uint8_t *__restr
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int64_t t = m0 + 32 * (TPW * wt + j) + (r & 3) + 8 * (r >> 2) + 4 * kg;
-            if (KS > 1) part[((int64_t)split * Mp + t) * N + n] = tot[j][r];
+            if (gcnt) {
+                if (t - gP < gn) Y[(gr0 + t - gP) * ldy + n] = tot[j][r];
+            } else if (KS > 1) part[((int64_t)split * Mp + t) * N + n] = tot[j][r];
             else if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
         }
 }
@@ -1962,12 +1994,44 @@ int kcpp_gemm_q80_glu_q80(const void *W, const void *W2, int64_t K, int64_t N, c
 // (X W2^T) with up [M][N] as scratch.  cnt_dev: the same counts on the device (read by the kernel); Q4_K / Q5_K
 // (+ RS) only, K a multiple of 256.  One launch per mode (+ the GLU product); every row's arithmetic is v4's unsplit
 // (bitwise the single-expert kcpp_gemm result wherever that runs unsplit)
+int64_t kcpp_gemm_grouped_ws_bytes(int type, int64_t K, int64_t M, int ng) {
+    if (type != KT_Q6_K_RS) return 0;
+    const int64_t Pv = M + 128LL * ng;                  // >= the padded virtual rows
+    return ((Pv * K * 2 + 255) & ~255LL) + Pv * (K / 256) * 4;
+}
+
 int kcpp_gemm_grouped(int type, const void *W, const void *W2, int64_t wstride, int64_t K, int64_t N, const void *act,
                       int64_t M, const int32_t *cnt_host, const int32_t *cnt_dev, int ng, float *Y, float *up, int mode,
-                      void *stream) {
-    if (type != KT_Q4_K && type != KT_Q4_K_RS && type != KT_Q5_K && type != KT_Q5_K_RS) return -1;
+                      void *ws, void *stream) {
+    if (type != KT_Q4_K && type != KT_Q4_K_RS && type != KT_Q5_K && type != KT_Q5_K_RS && type != KT_Q6_K_RS) return -1;
     if (K % 256 || ng < 1 || ng > 64 || !cnt_dev || !cnt_host || (mode == 1 && (!W2 || !up)) || mode < 0 || mode > 1)
         return -1;
+    if (type == KT_Q6_K_RS) {
+        // Q6_K (RS layout): k_gemm_q6v3 over a 128-row-padded virtual layout (the f16 fragment image of every
+        // group, padding rows zero), 128 x 128 tiles, 8 waves, unsplit; plain mode only
+        if (mode != 0 || !ws) return -1;
+        int64_t Pv = 0, rows = 0;
+        for (int e = 0; e < ng; ++e) {
+            if (cnt_host[e] < 0) return -1;
+            Pv += (cnt_host[e] + 127) / 128 * 128;
+            rows += cnt_host[e];
+        }
+        if (rows != M) return -1;
+        if (!Pv) return 0;
+        hipStream_t s = (hipStream_t)stream;
+        h8v *a16 = (h8v *)ws;
+        float *dyT = (float *)((uint8_t *)ws + ((Pv * K * 2 + 255) & ~255LL));
+        const int64_t nth = Pv * K / 8 + Pv * (K / 256);
+        hipLaunchKernelGGL(k_act_frag6, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Pv,
+                           a16, dyT, cnt_dev, ng);
+        KCPP_CHECK(hipGetLastError());
+        const int MT = (int)(Pv / 128);
+        const unsigned nwg = (unsigned)(MT * ((N + 127) / 128));
+        hipLaunchKernelGGL((k_gemm_q6v3<8, 4>), dim3(nwg), dim3(512), 0, s, (const uint8_t *)W, K, N, (const h8v *)a16, dyT,
+                           Pv, Pv, MT, Y, N, (const float *)nullptr, (int64_t)0, 1, (float *)nullptr, cnt_dev, ng, wstride);
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
     if (((uintptr_t)((const uint8_t *)act + M * K + M * (K / 256) * 4) & 15) != 0) return -3;
     int64_t tiles = 0, rows = 0;
     const int64_t ntn = (N + 127) / 128;
@@ -2141,7 +2205,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     if (type == KT_Q6_K_RS && v3) {
         const int64_t nth = Mp * K / 8 + Mp * (K / 256);
         hipLaunchKernelGGL(k_act_frag6, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Mp,
-                           (h8v *)a16, dy);
+                           (h8v *)a16, dy, (const int32_t *)nullptr, 0);
         KCPP_CHECK(hipGetLastError());
         const int64_t nt = (N + 127) / 128;
         const bool big = Mp / 128 * nt >= 384;
@@ -2158,7 +2222,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         auto launch6 = [&](const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
 #define KCPP_V6(NW_, B_)                                                                                                   \
     hipLaunchKernelGGL((k_gemm_q6v3<NW_, B_>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)w, K, N, (const h8v *)a16, dy, \
-                       M, Mp, MT, y, ly, r, lr, KS, part)
+                       M, Mp, MT, y, ly, r, lr, KS, part, (const int32_t *)nullptr, 0, (int64_t)0)
             if (BMT == 2) { if (NWv == 4) KCPP_V6(4, 2); else KCPP_V6(8, 2); }
             else { if (NWv == 4) KCPP_V6(4, 4); else KCPP_V6(8, 4); }
 #undef KCPP_V6

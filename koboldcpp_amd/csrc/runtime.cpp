@@ -123,6 +123,7 @@ struct kcpp_model {
     int64_t n_moe_grouped = 0;       // grouped MoE prefill layers run
     float *moe_gx = nullptr, *moe_gh = nullptr, *moe_gup = nullptr, *moe_geo = nullptr;   // grouped prefill: [ubatch*k]
     void *moe_gact = nullptr;        // rows (gathered input, GLU output, up scratch, down output), their Q8_K
+    void *moe_gws = nullptr;         // grouped Q6_K down: fragment image of the padded layout
     int32_t *moe_gcnt = nullptr, *moe_gcnt_h = nullptr;   // per-expert row counts (device, pinned host)
     int32_t *moe_ids_h = nullptr;    // pinned host copies (prefill routing)
     float *moe_w_h = nullptr;
@@ -457,7 +458,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
         F(L.qkv_base); F(L.glu_base); F(L.kc); F(L.vc);
     }
     F(m->hglu); F(m->moe_ids); F(m->moe_w); F(m->moe_rows); F(m->moe_rw); F(m->moe_slots);
-    F(m->moe_gx); F(m->moe_gh); F(m->moe_gup); F(m->moe_geo); F(m->moe_gact); F(m->moe_gcnt);
+    F(m->moe_gx); F(m->moe_gh); F(m->moe_gup); F(m->moe_geo); F(m->moe_gact); F(m->moe_gcnt); F(m->moe_gws);
     for (void *p : {(void *)m->moe_ids_h, (void *)m->moe_w_h, (void *)m->moe_rows_h, (void *)m->moe_rw_h,
                     (void *)m->moe_gcnt_h})
         if (p) hipHostFree(p);
@@ -1008,11 +1009,19 @@ static int moe_prefill_grouped(kcpp_model *m, const KLayer &L, int T, const int 
     RC(kcpp_moe_gather(m->attn, E, m->moe_rows, (int)R, E, m->moe_gx, s));
     RC(kcpp_quantize_act(kcpp_vec_dot_type(t[6].type), m->moe_gx, E, m->moe_gact, E, R, s));
     RC(kcpp_gemm_grouped(t[6].type, t[6].d, t[7].d, t[6].slice_bytes, E, F, m->moe_gact, R, cnt, m->moe_gcnt, NE,
-                         m->moe_gh, m->moe_gup, 1, s));
-    if (grouped_type(t[8].type) && kcpp_vec_dot_type(t[8].type) == KT_Q8_K) {
+                         m->moe_gh, m->moe_gup, 1, nullptr, s));
+    if ((grouped_type(t[8].type) || t[8].type == KT_Q6_K_RS) && kcpp_vec_dot_type(t[8].type) == KT_Q8_K) {
+        void *gws = nullptr;
+        if (t[8].type == KT_Q6_K_RS) {          // the f16 fragment image of the padded layout (lazily, once)
+            if (!m->moe_gws && hipMalloc(&m->moe_gws, kcpp_gemm_grouped_ws_bytes(KT_Q6_K_RS, F, UB * NU, NE)) != hipSuccess) {
+                g_err = "grouped MoE workspace";
+                return -2;
+            }
+            gws = m->moe_gws;
+        }
         RC(kcpp_quantize_act(KT_Q8_K, m->moe_gh, F, m->moe_gact, F, R, s));
         RC(kcpp_gemm_grouped(t[8].type, t[8].d, nullptr, t[8].slice_bytes, F, E, m->moe_gact, R, cnt, m->moe_gcnt, NE,
-                             m->moe_geo, nullptr, 0, s));
+                             m->moe_geo, nullptr, 0, gws, s));
     } else {
         for (int e = 0; e < NE; ++e) {
             const int n = cnt[e];

@@ -312,12 +312,12 @@ def test_moe_routing_inside_glu_launch_bitwise(env, policy, graphs):
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
 
 
-@pytest.mark.parametrize("t", [R.Q4_K, R.Q5_K, 113])
-@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("t,mode", [(R.Q4_K, 0), (R.Q5_K, 0), (113, 0), (R.Q4_K, 1), (R.Q5_K, 1), (113, 1), (114, 0)])
 def test_gemm_grouped_matches_per_expert_bitwise(env, t, mode):
     """kcpp_gemm_grouped (every expert's GEMM in one launch: the MoE prefill of ggml_cuda_mul_mat_id,
     ggml-cuda.cu:2003-2139) == kcpp_gemm on each expert's own rows with the unsplit kernels
-    (kcpp_gemm_set_variant(13)), bit for bit, plain and GLU, over ragged counts (empty experts, 1 row, > 256 rows)"""
+    (kcpp_gemm_set_variant(13)), bit for bit, plain and GLU, over ragged counts (empty experts, 1 row, > 256 rows);
+    Q6_K (RS layout, plain) through its 128-row-padded virtual layout"""
     torch, K = env
     s = torch.cuda.current_stream().cuda_stream
     Kd, N = 2048, 640
@@ -337,8 +337,9 @@ def test_gemm_grouped_matches_per_expert_bitwise(env, t, mode):
     cnt_host = (ctypes.c_int32 * NE)(*cnt)
     Y = torch.full((M, N), float("nan"), device="cuda")
     up = torch.empty(M, N, device="cuda")
+    gws = torch.empty(max(1, int(K.raw().kcpp_gemm_grouped_ws_bytes(t, Kd, M, NE))), dtype=torch.uint8, device="cuda")
     K.call("kcpp_gemm_grouped", t, W.data_ptr(), W2.data_ptr() if mode else None, rb, Kd, N, act.data_ptr(), M,
-           cnt_host, cnt_dev.data_ptr(), NE, Y.data_ptr(), up.data_ptr() if mode else None, mode, s)
+           cnt_host, cnt_dev.data_ptr(), NE, Y.data_ptr(), up.data_ptr() if mode else None, mode, gws.data_ptr(), s)
     torch.cuda.synchronize()
     got = Y.cpu().numpy()
     bad = []
