@@ -2025,10 +2025,18 @@ int kcpp_gemm_grouped(int type, const void *W, const void *W2, int64_t wstride, 
         hipLaunchKernelGGL(k_act_frag6, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, s, (const uint8_t *)act, K, M, Pv,
                            a16, dyT, cnt_dev, ng);
         KCPP_CHECK(hipGetLastError());
-        const int MT = (int)(Pv / 128);
+        // tile shape (never changes a bit): 128 x 128, 8 waves; variants 15 / 17 force (BMT, NW) = (4, 4) / (2, 8)
+        const int gv = gemm_variant();
+        const int BMT = gv == 17 ? 2 : 4, NWv = gv == 15 ? 4 : 8;
+        const int MT = (int)(Pv / (32 * BMT));
         const unsigned nwg = (unsigned)(MT * ((N + 127) / 128));
-        hipLaunchKernelGGL((k_gemm_q6v3<8, 4>), dim3(nwg), dim3(512), 0, s, (const uint8_t *)W, K, N, (const h8v *)a16, dyT,
-                           Pv, Pv, MT, Y, N, (const float *)nullptr, (int64_t)0, 1, (float *)nullptr, cnt_dev, ng, wstride);
+#define KCPP_G6(NW_, B_)                                                                                                   \
+    hipLaunchKernelGGL((k_gemm_q6v3<NW_, B_>), dim3(nwg), dim3(64 * NW_), 0, s, (const uint8_t *)W, K, N, (const h8v *)a16, \
+                       dyT, Pv, Pv, MT, Y, N, (const float *)nullptr, (int64_t)0, 1, (float *)nullptr, cnt_dev, ng, wstride)
+        if (BMT == 2) KCPP_G6(8, 2);
+        else if (NWv == 4) KCPP_G6(4, 4);
+        else KCPP_G6(8, 4);
+#undef KCPP_G6
         KCPP_CHECK(hipGetLastError());
         return 0;
     }
