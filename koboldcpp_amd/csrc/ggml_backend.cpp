@@ -15,7 +15,8 @@
 //                the weight's buffer is written again; F16 / F32 weight: kcpp_ggml_mul_mat_f
 //   GET_ROWS     quantized: kcpp_get_rows on the native image; F16 / F32: kcpp_ggml_get_rows
 //   MUL_MAT_ID   quantized experts: expert-indexed mat-vecs reading the ids on the device (few rows), else the ids
-//                on the host and one mat-vec / GEMM per expert over gathered columns (mul_mat_id below)
+//                on the host and the gathered columns of all experts in one grouped GEMM (Q4_K / Q5_K / Q6_K) or
+//                one mat-vec / GEMM per expert (mul_mat_id below)
 //   FLASH_ATTN_EXT  kcpp_flash_attn_ext (graph-form Q view, F16 K/V cache views, F16 mask; head dim 64 / 128) or
 //                kcpp_flash_attn_ext_q (Q8_0 / Q4_0 K/V views: --quantkv)
 //   RMS_NORM, ROPE (NORM / NEOX, YaRN), SOFT_MAX, ADD/SUB/MUL/DIV (broadcast), SCALE, UNARY (SILU/NEG/RELU),
@@ -334,7 +335,7 @@ struct BackendCtx {
     int device;
     std::string name;
     hipStream_t stream;
-    Scratch act, ws, fa, ids, xg, yg;
+    Scratch act, ws, fa, ids, xg, yg, gcnt;
     bool fa_exact = false;     // attention in the reference CPU's order with its f16 accumulator (attn_exact.hip)
 };
 
@@ -654,7 +655,8 @@ bool supports(const kggml_tensor *op) {
 // A handful of rows (decode): one expert-indexed mat-vec per (j, t) that reads its expert id on the device
 // (DecArgs.eid) and quantizes its own column (prologue 2) -- no host synchronisation.  More rows (prefill): the ids
 // come to the host (the reference synchronises here too), the columns of each expert are gathered, quantized and
-// multiplied by one mat-vec / MFMA GEMM per expert, and the rows scattered back.
+// multiplied by one grouped MFMA GEMM over all experts (kcpp_gemm_grouped; other types: one mat-vec / GEMM per
+// expert), and the rows scattered back.
 bool mul_mat_id(BackendCtx *bc, kggml_tensor *n) {
     hipStream_t s = bc->stream;
     const kggml_tensor *as = n->src[0], *b = n->src[1], *ids = n->src[2];
@@ -731,6 +733,25 @@ bool mul_mat_id(BackendCtx *bc, kggml_tensor *n) {
     for (int64_t e = 0; e < E; ++e) hoff.insert(hoff.end(), dof[e].begin(), dof[e].end());
     if (hipMemcpy(offs, hoff.data(), hoff.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
         return set_err("mul_mat_id: offsets upload failed");
+    // Q4_K / Q5_K / Q6_K (RS) experts: every expert's GEMM in one launch (kcpp_gemm_grouped) -- one gather, one
+    // quantization, one scatter, grids over all experts' rows
+    const bool grouped = (tt == KT_Q4_K || tt == KT_Q4_K_RS || tt == KT_Q5_K || tt == KT_Q5_K_RS || tt == KT_Q6_K_RS) &&
+                         K % 256 == 0 && E <= 64 && rows > 16;
+    if (grouped) {
+        std::vector<int32_t> cnt((size_t)E);
+        for (int64_t e = 0; e < E; ++e) cnt[e] = (int32_t)so[e].size();
+        int32_t *cnt_dev = (int32_t *)bc->gcnt.get(256);
+        const int64_t gwb = kcpp_gemm_grouped_ws_bytes(tt, K, rows, (int)E);
+        void *gws = gwb > 0 ? bc->ws.get((size_t)gwb + 256) : nullptr;
+        if (!cnt_dev || (gwb > 0 && !gws)) return set_err("mul_mat_id: grouped scratch allocation failed");
+        if (hipMemcpy(cnt_dev, cnt.data(), (size_t)E * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return set_err("mul_mat_id: counts upload failed");
+        return chk(kcpp_rows_move_f32(b->data, offs, 0, xg, nullptr, K * 4, K, (int)rows, s), "gather") &&
+               chk(kcpp_quantize_act(kcpp_vec_dot_type(as->type), xg, K, act, K, rows, s), "quantize_act") &&
+               chk(kcpp_gemm_grouped(tt, W, nullptr, eb, K, N, act, rows, cnt.data(), cnt_dev, (int)E, yg, nullptr, 0,
+                                     gws, s), "grouped gemm") &&
+               chk(kcpp_rows_move_f32(yg, nullptr, N * 4, n->data, offs + rows, 0, N, (int)rows, s), "scatter");
+    }
     int64_t r0 = 0;
     for (int64_t e = 0; e < E; ++e) {
         const int64_t c = (int64_t)so[e].size();
@@ -948,7 +969,7 @@ void be_free(kggml_backend_t be) {
     BackendCtx *c = (BackendCtx *)be->context;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    for (Scratch *sc : {&c->act, &c->ws, &c->fa, &c->ids, &c->xg, &c->yg}) if (sc->p) hipFree(sc->p);
+    for (Scratch *sc : {&c->act, &c->ws, &c->fa, &c->ids, &c->xg, &c->yg, &c->gcnt}) if (sc->p) hipFree(sc->p);
     hipStreamDestroy(c->stream);
     delete c;
     delete be;
