@@ -346,7 +346,8 @@ MMID_CASES = [(R.Q4_K, 1), (R.Q4_K, 3), (R.Q4_K, 24), (R.Q5_K, 1), (R.Q5_K, 24),
 def test_mul_mat_id_vs_reference_cpu(env, case):
     """GGML_OP_MUL_MAT_ID (ggml_cuda_mul_mat_id, ggml-cuda.cu:2003-2139) with 8 experts, 2 used: src1 broadcast over
     the used slots (ne11 = 1, the up / gate form) and one column per slot (ne11 = 2, the down form); T <= 8 runs the
-    device-routed expert mat-vecs, T = 24 the host-grouped per-expert GEMMs"""
+    device-routed expert mat-vecs, T = 24 the host-grouped GEMMs (one kcpp_gemm_grouped launch over all experts for
+    Q4_K / Q5_K / Q6_K, one GEMM per expert for the other types)"""
     G, L, be = env
     _moe_sigs(G)
     t, T = case
