@@ -2121,12 +2121,16 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
     // (split-K); its tile grid is split in two along K when it has <= 128 tiles.  Variant 11 forces v4 (split rule),
     // 13 v4 unsplit, 3 / 4 force v3.
     const bool v4_pick = gv == 0;
-    // Q5_K: v4 with the fifth-bit MFMA (TPW 2 only) for the plain / residual projections (tools/gemm_ab.py, v2 -> v4,
-    // Mixtral expert shapes: down 14336 -> 4096 (split-K) M = 128 134.3 -> 96.3 us, M = 512 151.4 -> 124.6) and for
-    // GLU (gate + up in one launch) up to 256 tokens: 4096 -> 2 x 14336 M = 128 93.9 -> 73.1, but M = 512 ~270 ->
-    // ~305, so v2 there.  GLU is unsplit on both kernels and bitwise equal (test_gemm_v4_int8_matches_v2_bitwise), so
-    // the token-count rule does not change a bit.  Variants 11 / 13 force v4.
-    const bool q5 = (type == KT_Q5_K || type == KT_Q5_K_RS) && (mode == 0 || gv != 0 || Mp <= 256);
+    // Q5_K: v4 with the fifth-bit MFMA (TPW 2 only) for the plain / residual projections it splits along K (<= 32
+    // row tiles; tools/gemm_ab.py, v2 -> v4: Mixtral expert down 14336 -> 4096 M = 128 134.3 -> 96.3 us, M = 512
+    // 151.4 -> 124.6; wo 4096^2 42.6 -> 34.6 / 49.1 -> 45.4) -- a weight-shape rule, as the split changes bits -- and
+    // for GLU (gate + up in one launch) up to 256 tokens: 4096 -> 2 x 14336 M = 128 93.9 -> 73.1.  Unsplit shapes
+    // stay on v2 (`profiles/r05_q5k_v4_gemm_ab.jsonl`: GLU M = 512 ~270 vs ~305; dense gate|up 4096 -> 28672 M = 512
+    // ~240 vs ~271; q|k|v 6144 rows M = 128 43.6 vs 55.7); unsplit v4 and v2 are bitwise equal
+    // (test_gemm_v4_int8_matches_v2_bitwise), so the GLU token-count rule does not change a bit.  Variants 11 / 13
+    // force v4.
+    const bool q5split = mode == 0 && (K / 256) % 2 == 0 && (N + 127) / 128 <= 32;
+    const bool q5 = (type == KT_Q5_K || type == KT_Q5_K_RS) && (gv != 0 || q5split || (mode == 1 && Mp <= 256));
     if ((type == KT_Q4_K || type == KT_Q4_K_RS || q5) && (gv == 11 || gv == 12 || gv == 13 || gv == 14 || v4_pick) && bs_aligned &&
         M > 32) {
         // v4: int8 MFMA straight from the Q8_K buffer (no fragment image); 128 x 128 tiles, split-K when the tile

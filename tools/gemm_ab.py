@@ -23,7 +23,8 @@ def main():
                                  ("glu2", K.Q4_K_RS, 4096, 14336, 1), ("down6", K.Q6_K_RS, 14336, 4096, 0),
                                  ("v6", K.Q6_K_RS, 4096, 1024, 0), ("glu5", K.Q5_K, 4096, 14336, 1),
                                  ("down5", K.Q5_K, 14336, 4096, 0), ("glu5rs", K.Q5_K_RS, 4096, 14336, 1),
-                                 ("wo5", K.Q5_K, 4096, 4096, 0)]:
+                                 ("wo5", K.Q5_K, 4096, 4096, 0), ("gu5", K.Q5_K_RS, 4096, 28672, 0),
+                                 ("qkv5", K.Q5_K_RS, 4096, 6144, 0)]:
         if os.environ.get("GEMM_ONLY") and name != os.environ["GEMM_ONLY"]:
             continue
         nrot = 3
