@@ -374,7 +374,7 @@ void q80t_shape(int mode, int64_t ntile, int64_t nu, int &S, int &WV) {
 
 // workspace of kcpp_gemm for KT_Q8_0_T: the S = 2 tickets at a FIXED place (the first 64 KB: [tile < 256][group < 64]
 // words, zero when the workspace is first used and left zero by every launch, whatever shape ran before), then the
-// partial tiles
+// partial tiles of a split shape
 constexpr int64_t Q80T_TICK_BYTES = 256 * 64 * 4;
 static_assert(Q80T_SMAX <= 8, "partials sized for 8 ranges");
 extern "C" {
@@ -382,7 +382,9 @@ int64_t kcpp_q80t_ws_bytes(int64_t K, int64_t N, int64_t M) {
     const int64_t ntile = N / 32, Z = (M + 31) / 32;
     int S, WV;
     q80t_shape(0, ntile, K / 128, S, WV);
-    return Q80T_TICK_BYTES + ntile * Z * std::max(S, 2) * 4096;
+    // partial tiles only where the shape splits K (S > 1; GLU, mode 1, never splits): the output head (4008 tiles) and
+    // the fused gate|up need none, so the workspace is the tickets plus the split projections' partials
+    return Q80T_TICK_BYTES + (S > 1 ? ntile * Z * S * 4096 : 0);
 }
 
 // mode 0: Y = W act (+ res); mode 1: h = silu(W act) * (W2 act) as f32 (Y) or as the KT_Q8_0_TA activation (qout)

@@ -120,31 +120,33 @@ struct ActCopy {
 };
 
 // column c of a Q8_K activation buffer with Mt columns (qs [Mt][K] ++ d [Mt][K/256] ++ bsums [Mt][K/16]) ->
-// the single-column LDS image qs[K] ++ d[K/256] ++ bsums[K/16]; K <= 16384
+// the single-column LDS image qs[K] ++ d[K/256] ++ bsums[K/16]; NT threads, K <= NT * QPT * 16 (and the
+// K / 256 + K / 32 scale words <= NT * SPT): 256 threads x (4, 2) cover K 16384, 512 x (4, 3) K 32768 (XL)
+template <int NT = 256, int QPT = 4, int SPT = 2>
 struct ActCopyCol {
-    uint4 q[4];
-    uint32_t s[2];
+    uint4 q[QPT];
+    uint32_t s[SPT];
     __device__ __forceinline__ void load(const uint8_t *act, int K, int64_t Mt, int64_t c) {
         const int tid = threadIdx.x, nq = K / 16, ns = K / 256 + K / 32;
         const uint8_t *qs = act + c * K;
         const uint32_t *d = (const uint32_t *)(act + Mt * K) + c * (K / 256);
         const uint32_t *bs = (const uint32_t *)(act + Mt * K + Mt * (K / 256) * 4) + c * (K / 32);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) q[i] = *(const uint4 *)(qs + 16 * min(tid + 256 * i, nq - 1));
+        for (int i = 0; i < QPT; ++i) q[i] = *(const uint4 *)(qs + 16 * min(tid + NT * i, nq - 1));
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int j = min(tid + 256 * i, ns - 1);
+        for (int i = 0; i < SPT; ++i) {
+            const int j = min(tid + NT * i, ns - 1);
             s[i] = j < K / 256 ? d[j] : bs[j - K / 256];
         }
     }
     __device__ __forceinline__ void store(uint8_t *lds, int K) {
         const int tid = threadIdx.x, nq = K / 16, ns = K / 256 + K / 32;
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-            if (tid + 256 * i < nq) *(uint4 *)(lds + 16 * (tid + 256 * i)) = q[i];
+        for (int i = 0; i < QPT; ++i)
+            if (tid + NT * i < nq) *(uint4 *)(lds + 16 * (tid + NT * i)) = q[i];
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-            if (tid + 256 * i < ns) ((uint32_t *)(lds + K))[tid + 256 * i] = s[i];
+        for (int i = 0; i < SPT; ++i)
+            if (tid + NT * i < ns) ((uint32_t *)(lds + K))[tid + NT * i] = s[i];
         __syncthreads();
     }
 };

@@ -209,7 +209,8 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
         }
         if constexpr (XL || ROUTE || MODE == 3) issue(g0, ba);
     } else {
-        lean::ActCopyCol cp;
+        // the column copy covers K <= 16384 at 256 threads; XL's 512 threads x (4, 3) cover K <= 32768
+        lean::ActCopyCol<64 * NWV, XL ? 4 : (16384 / 16 + 64 * NWV - 1) / (64 * NWV), XL ? 3 : (16384 / 256 + 16384 / 32 + 64 * NWV - 1) / (64 * NWV)> cp;
         cp.load(a.act, K, a.act_mtot > 0 ? a.act_mtot : 1, a.act_col);
         issue(g0, ba);
         cp.store(lds, K);
@@ -362,15 +363,26 @@ int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
 #undef KCPP_RS_P
     return -3;
 }
-// long K (XL): mode 0 with a quantize / norm prologue only (the down projection of Llama-3-70B, K = 28672, and MoE
-// experts with n_ff past 14336), one row per group, 8-wave workgroups, no group prefetch: a row's NI pieces are already
-// 16 KB (Q4_K, K = 28672) in flight per wave, 128 KB per CU.  NI = the ceiling the shape rounds up to.
+// long K (XL): the down projection of Llama-3-70B (K = 28672) and MoE experts with n_ff past 14336 (mode 0, quantize
+// or norm prologue), the same tensors read column by column from a quantized activation (pro 0: the M <= 8 prefill
+// tail and the ggml plugin's few-row MUL_MAT, gemv_cols), and the projections of models with n_embd past 14336 (GLU
+// mode 1, q|k|v mode 2 with the norm prologue).  One row per group (two for mode 2), 8-wave workgroups, no group
+// prefetch: a row's NI pieces are already 16 KB (Q4_K, K = 28672) in flight per wave, 128 KB per CU.  NI = the ceiling
+// the shape rounds up to.
 template <int TYPE, int NI>
 int pick_rs_xl(const DecArgs &a, int mode, int pro, hipStream_t s) {
     constexpr int MC = TYPE == KT_Q6_K_RS ? NI : NI / 2;        // ceil(K / 4096) at the ceiling
-    if (mode != 0) return -3;
-    if (pro == 2) return launch_rs<TYPE, NI, 1, 0, 2, MC, 0, 8, true>(a, 256, s);
-    if (pro == 1) return launch_rs<TYPE, NI, 1, 0, 1, MC, 0, 8, true>(a, 256, s);
+    if (mode == 0) {
+        if (pro == 2) return launch_rs<TYPE, NI, 1, 0, 2, MC, 0, 8, true>(a, 256, s);
+        if (pro == 1) return launch_rs<TYPE, NI, 1, 0, 1, MC, 0, 8, true>(a, 256, s);
+        if (pro == 0) return launch_rs<TYPE, NI, 1, 0, 0, MC, 0, 8, true>(a, 256, s);
+    } else if (mode == 1) {
+        if (a.route_w || (a.nseg != 1 && !a.eid1)) return -3;
+        if (pro == 1) return launch_rs<TYPE, NI, 1, 1, 1, MC, 0, 8, true>(a, 256, s);
+        if (pro == 0) return launch_rs<TYPE, NI, 1, 1, 0, MC, 0, 8, true>(a, 256, s);
+    } else if (mode == 2) {
+        if (pro == 1) return launch_rs<TYPE, NI, 2, 2, 1, MC, 0, 8, true>(a, 256, s);
+    }
     return -3;
 }
 template <int TYPE>

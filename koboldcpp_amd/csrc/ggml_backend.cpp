@@ -735,7 +735,10 @@ bool mul_mat_id(BackendCtx *bc, kggml_tensor *n) {
         return set_err("mul_mat_id: offsets upload failed");
     // Q4_K / Q5_K / Q6_K (RS) experts: every expert's GEMM in one launch (kcpp_gemm_grouped) -- one gather, one
     // quantization, one scatter, grids over all experts' rows
-    const bool grouped = (tt == KT_Q4_K || tt == KT_Q4_K_RS || tt == KT_Q5_K || tt == KT_Q5_K_RS || tt == KT_Q6_K_RS) &&
+    // (the int8 kernel's 16-B DMA of the Q8_K bsums plane needs rows * (K / 256) % 4 == 0, e.g. not K 11008 / 6400 at an
+    // odd row count: those take the per-expert loop; the Q6_K kernel reads an f16 fragment image instead)
+    const bool grouped = (((tt == KT_Q4_K || tt == KT_Q4_K_RS || tt == KT_Q5_K || tt == KT_Q5_K_RS) &&
+                           (rows * (K / 256)) % 4 == 0) || tt == KT_Q6_K_RS) &&
                          K % 256 == 0 && E <= 64 && rows > 16;
     if (grouped) {
         std::vector<int32_t> cnt((size_t)E);

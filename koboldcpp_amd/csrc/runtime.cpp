@@ -980,13 +980,17 @@ static int moe_dec(kcpp_model *m, const KLayer &L) {
 // (ggml_cuda_mul_mat_id does the same, ggml-cuda.cu:2003-2139), then per expert with tokens: gather
 // the normalized rows, gate|up GEMM with silu*up, down GEMM, weighted scatter into the top-k slots.
 static bool grouped_type(int t) { return t == KT_Q4_K || t == KT_Q4_K_RS || t == KT_Q5_K || t == KT_Q5_K_RS; }
+// the grouped int8 GEMM streams the Q8_K bsums plane of its M-row activation by 16-B DMA: M * (K / 256) * 4 bytes of d
+// in front of it must keep it 16-B aligned (kcpp_gemm_grouped returns -3 otherwise, e.g. K 11008 or 6400 with an odd
+// routed-row count); such layers take the per-expert path
+static bool grouped_act_aligned(int64_t M, int64_t K) { return (M * (K / 256)) % 4 == 0; }
 
 // grouped MoE prefill (after routing): every routed row gathered in expert order, one Q8_K quantization, the gate|up
 // GEMMs of all experts in one launch (kcpp_gemm_grouped), the down GEMMs likewise (or per expert for a type the
 // grouped kernel lacks, e.g. Q6_K), one scatter -- 5-6 launches per layer instead of 6 per active expert, and grids
 // that fill the GPU at ~ubatch*k/n_expert rows per expert.  Per row the arithmetic is the per-expert path's v4
 // (unsplit), so gate|up is bitwise that path's and down within its split-K re-association.
-static int moe_prefill_grouped(kcpp_model *m, const KLayer &L, int T, const int *cnt, const int *off) {
+static int moe_prefill_grouped(kcpp_model *m, const KLayer &L, int T, const int *cnt, const int *off, bool down_grouped) {
     const kcpp_hparams &hp = m->hp;
     const int64_t E = hp.n_embd, F = hp.n_ff, UB = m->ub;
     const int NU = hp.n_expert_used, NE = hp.n_expert;
@@ -1010,7 +1014,7 @@ static int moe_prefill_grouped(kcpp_model *m, const KLayer &L, int T, const int 
     RC(kcpp_quantize_act(kcpp_vec_dot_type(t[6].type), m->moe_gx, E, m->moe_gact, E, R, s));
     RC(kcpp_gemm_grouped(t[6].type, t[6].d, t[7].d, t[6].slice_bytes, E, F, m->moe_gact, R, cnt, m->moe_gcnt, NE,
                          m->moe_gh, m->moe_gup, 1, nullptr, s));
-    if ((grouped_type(t[8].type) || t[8].type == KT_Q6_K_RS) && kcpp_vec_dot_type(t[8].type) == KT_Q8_K) {
+    if (down_grouped && kcpp_vec_dot_type(t[8].type) == KT_Q8_K) {
         void *gws = nullptr;
         if (t[8].type == KT_Q6_K_RS) {          // the f16 fragment image of the padded layout (lazily, once)
             if (!m->moe_gws && hipMalloc(&m->moe_gws, kcpp_gemm_grouped_ws_bytes(KT_Q6_K_RS, F, UB * NU, NE)) != hipSuccess) {
@@ -1068,9 +1072,11 @@ static int moe_prefill(kcpp_model *m, const KLayer &L, int T) {
         }
     RT_CHECK(hipMemcpyAsync(m->moe_rows, m->moe_rows_h, (size_t)2 * UB * NU * 4, hipMemcpyHostToDevice, s));
     RT_CHECK(hipMemcpyAsync(m->moe_rw, m->moe_rw_h, (size_t)T * NU * 4, hipMemcpyHostToDevice, s));
+    const int64_t RR = (int64_t)T * NU;
+    const bool down_grouped = (grouped_type(t[8].type) && grouped_act_aligned(RR, F)) || t[8].type == KT_Q6_K_RS;
     if (!m->no_moe_grouped && t[6].type == t[7].type && grouped_type(t[6].type) && E % 256 == 0 && F % 256 == 0 &&
-        NE <= 64)
-        return moe_prefill_grouped(m, L, T, cnt, off);
+        NE <= 64 && grouped_act_aligned(RR, E))
+        return moe_prefill_grouped(m, L, T, cnt, off, down_grouped);
     float *xg = m->qkv, *eo = m->hglu;
     for (int e = 0; e < NE; ++e) {
         const int n = cnt[e];

@@ -90,3 +90,25 @@ def test_70b_width_one_layer_vs_oracle(K):
     print("70B-width 1 layer vs restatement: max", d.max(axis=1), "median", np.median(d, axis=1))
     assert np.all(d.max(axis=1) <= 2 * sp["l70_max"].max())
     assert np.all(np.median(d, axis=1) <= 2 * sp["l70_median"].max())
+
+
+@pytest.mark.parametrize("T", [2, 5, 8])
+def test_70b_width_short_prompt_vs_oracle(K, T):
+    """a 2-8 token prompt (a prompt tail after context reuse) at Llama-3-70B width: M <= 8 runs the column mat-vec
+    (kcpp_gemv) on every projection, including the K = 28672 ffn_down in its long-K RS layout (the XL variant with the
+    activation-copy prologue); logits vs the pinned C restatement within 2x the reference's own spread at this width"""
+    import os
+    sp = np.load(os.path.join(R.ROOT, "tests", "golden", "ref_spread.npz"))
+    hp = dict(L70, n_layer=1, n_ctx=64)
+    types = R.q4_k_m_types(1)
+    prompt = [int(t) for t in sp["l70_prompt"]][:T]
+    m = K.Model(hp, types)
+    m.synth(1234)
+    got = m.decode(prompt, 0)
+    m.close()
+    ref = oracle_forced(types, prompt, [], True, hp=hp)
+    d = np.abs(np.asarray(got) - ref[0])
+    print("70B-width 1 layer, %d-token prompt vs restatement: max %.3g median %.3g" % (T, d.max(), np.median(d)))
+    assert np.isfinite(got).all()
+    assert d.max() <= 2 * sp["l70_max"].max()
+    assert np.median(d) <= 2 * sp["l70_median"].max()

@@ -385,3 +385,26 @@ def test_moe_grouped_prefill_matches_per_expert(env, policy):
     assert np.isfinite(outs[0]).all()
     d = np.abs(outs[0] - outs[1]).max()
     assert d < TOL_MAX, d
+
+
+def test_moe_grouped_prefill_unaligned_bsums_falls_back(env):
+    """n_ff with an odd super-block count (768 = 3 x 256, as K 11008 / 6400 of real MoE merges) and an odd prompt: the
+    routed rows x (F / 256) is not a multiple of 4, so the grouped int8 GEMM cannot stream the down projection's Q8_K
+    bsums plane (kcpp_gemm_grouped: -3); that layer's down runs per expert while gate|up (K = 512) stays grouped.
+    Prefill succeeds and matches the all-per-expert path within the GEMM bar"""
+    torch, K = env
+    hp = dict(R.TINY_MOE, n_ff=768)
+    types = R.moe_types(hp["n_layer"])
+    prompt = [int(v) for v in np.random.default_rng(6).integers(1, 500, size=151)]
+    outs = []
+    for grouped in (True, False):
+        m = K.Model(hp, types)
+        m.set_moe_grouped(grouped)
+        m.synth(78)
+        lg = [m.decode(prompt, 0), m.decode([9], len(prompt))]
+        assert (m.moe_grouped_count() > 0) == grouped
+        m.close()
+        outs.append(np.array(lg))
+    assert np.isfinite(outs[0]).all()
+    d = np.abs(outs[0] - outs[1]).max()
+    assert d < TOL_MAX, d

@@ -98,6 +98,15 @@ CASES = [  # name, base, K, N, mode, pro
     ("qkv_q5k", R.Q5_K, 4096, 6144, 0, 1),
     ("k5632_q5k_masked", R.Q5_K, 5632, 2048, 0, 2),
     ("head_q5k", R.Q5_K, 4096, 32768, 0, 1),
+    # long K (the XL variants: activation slices read from LDS per piece): every prologue of mode 0 -- 0 is the column
+    # path (kcpp_gemv / the ggml plugin's few-row MUL_MAT) on the 70B ffn_down --, GLU for n_embd past 14336
+    ("down70_pro0", R.Q4_K, 28672, 512, 0, 0),
+    ("down70_pro2", R.Q4_K, 28672, 512, 0, 2),
+    ("glu_xl", R.Q4_K, 16384, 256, 1, 1),
+    ("glu_xl_pro0", R.Q4_K, 16384, 256, 1, 0),
+    ("down_q5k_xl_pro0", R.Q5_K, 20480, 256, 0, 0),
+    ("down_q6k_xl_pro0", R.Q6_K, 32768, 256, 0, 0),
+    ("glu_q6k_xl", R.Q6_K, 16384, 128, 1, 1),
 ]
 
 
@@ -172,6 +181,58 @@ def test_gemv_rs_qkv_rope_kv(env, pos):
         _close(a_, b_, rtol=2e-3)
 
 
+def test_gemv_rs_qkv_rope_kv_xl(env):
+    """mode 2 at n_embd 16384 (past the register-resident activation: the XL variant) on Q4_K_RS, against the per-op
+    path on the base layout: rms_norm, Q8_K, the column mat-vec, then NORM RoPE of q / k from the same table (adjacent
+    pairs, ggml_rope_cache_init's cos / sin) and f16 rounding"""
+    torch, K = env
+    E, EKV, D, n_ctx, pos = 16384, 4096, 128, 256, 77
+    s = sptr(torch)
+    g = torch.Generator(device="cpu").manual_seed(6)
+    x = torch.randn(E, generator=g).cuda()
+    nw = (1 + 0.01 * torch.randn(E, generator=g)).cuda()
+    tab = np.empty(n_ctx * D, np.float32)
+    K.call("kcpp_rope_table", tab.ctypes.data_as(ctypes.c_void_p), n_ctx, D, 500000.0, 1.0, None, 0.0, 1.0, 32.0, 1.0,
+           n_ctx)
+    tab_d = torch.from_numpy(tab).cuda()
+    posd = torch.tensor([pos], dtype=torch.int32, device="cuda")
+    Ns = (E, EKV, EKV)
+    Wr = [_synth(torch, K, 112, E, n, 3 + i) for i, n in enumerate(Ns)]
+    Wb = [_synth(torch, K, R.Q4_K, E, n, 3 + i) for i, n in enumerate(Ns)]
+    q16 = torch.zeros(E, dtype=torch.int16, device="cuda")
+    kc = torch.zeros(n_ctx * EKV, dtype=torch.int16, device="cuda")
+    vc = torch.zeros(n_ctx * EKV, dtype=torch.int16, device="cuda")
+    a = K.DecArgs()
+    a.K, a.nseg, a.x, a.nw, a.eps = E, 3, x.data_ptr(), nw.data_ptr(), 1e-5
+    for i, (w, n) in enumerate(zip(Wr, Ns)):
+        a.W[i], a.N[i], a.role[i] = w.data_ptr(), n, i
+    a.q16, a.kc, a.vc, a.ekv, a.D, a.pos, a.rope_tab = (q16.data_ptr(), kc.data_ptr(), vc.data_ptr(), EKV, D,
+                                                       posd.data_ptr(), tab_d.data_ptr())
+    assert K.gemv_dec(112, a, 2, 1, 2, s) == 0
+    y1 = torch.empty(E, device="cuda")
+    K.call("kcpp_rms_norm", x.data_ptr(), E, nw.data_ptr(), y1.data_ptr(), E, None, E, 1, 1e-5, s)
+    act = torch.zeros(K.act_bytes(R.Q4_K, E, 1) + 64, dtype=torch.uint8, device="cuda")
+    K.call("kcpp_quantize_act", K.vec_dot_type(R.Q4_K), y1.data_ptr(), E, act.data_ptr(), E, 1, s)
+    ref = []
+    for w, n in zip(Wb, Ns):
+        y = torch.empty(n, device="cuda")
+        K.call("kcpp_gemv", R.Q4_K, w.data_ptr(), None, E, n, act.data_ptr(), 1, y.data_ptr(), n, None, n, 0, s)
+        ref.append(y)
+    torch.cuda.synchronize()
+    cs = tab.reshape(n_ctx, D // 2, 2)[pos]
+
+    def rope(v):
+        p = v.reshape(-1, D // 2, 2)
+        c, sn = cs[None, :, 0], cs[None, :, 1]
+        return np.stack([p[..., 0] * c - p[..., 1] * sn, p[..., 0] * sn + p[..., 1] * c], -1).reshape(-1)
+    want = [rope(ref[0].cpu().numpy()), rope(ref[1].cpu().numpy()), ref[2].cpu().numpy()]
+    f = lambda z: z.cpu().numpy().view(np.float16).astype(np.float32)
+    sl = slice(pos * EKV, (pos + 1) * EKV)
+    for got, w_ in zip((f(q16), f(kc[sl]), f(vc[sl])), want):
+        assert np.isfinite(got).all()
+        _close(got, w_, rtol=2e-3)
+
+
 @pytest.mark.parametrize("base", [R.Q4_K, R.Q5_K, R.Q6_K])
 @pytest.mark.parametrize("M", [3, 37])
 def test_rs_columns_and_gemm(env, base, M):
@@ -207,6 +268,34 @@ def test_rs_columns_and_gemm(env, base, M):
         else:
             _close(b_, a_)
 
+
+@pytest.mark.parametrize("base,Kd", [(R.Q4_K, 28672), (R.Q5_K, 20480), (R.Q6_K, 32768)])
+@pytest.mark.parametrize("M", [1, 2, 5, 8])
+def test_rs_columns_long_k(env, base, Kd, M):
+    """kcpp_gemv at M <= 8 on a long-K RS tensor (Llama-3-70B ffn_down K = 28672: a 2-8 token prompt tail, the ggml
+    plugin's few-row MUL_MAT): one XL launch per column with the activation-copy prologue, vs the base layout's
+    column mat-vec -- plain + residual and GLU"""
+    torch, K = env
+    t = RS[base]
+    assert K.raw().kcpp_rs_supported(t, Kd)
+    N = 384
+    s = sptr(torch)
+    X = torch.randn(M, Kd, generator=torch.Generator(device="cpu").manual_seed(M + Kd)).cuda()
+    act = torch.zeros(K.act_bytes(base, Kd, M), dtype=torch.uint8, device="cuda")
+    K.call("kcpp_quantize_act", K.vec_dot_type(base), X.data_ptr(), Kd, act.data_ptr(), Kd, M, s)
+    res = torch.randn(M, N).cuda()
+    ys = []
+    for tt in (base, t):
+        W, W2 = _synth(torch, K, tt, Kd, N, 21), _synth(torch, K, tt, Kd, N, 22)
+        for mode in (0, 1):
+            Y = torch.full((M, N), float("nan"), device="cuda")
+            K.call("kcpp_gemv", tt, W.data_ptr(), W2.data_ptr() if mode == 1 else None, Kd, N, act.data_ptr(), M,
+                   Y.data_ptr(), N, res.data_ptr() if mode == 0 else None, N, mode, s)
+            torch.cuda.synchronize()
+            ys.append(Y.cpu().numpy())
+    for a_, b_ in zip(ys[:2], ys[2:]):
+        assert np.isfinite(b_).all()
+        _close(b_, a_)
 
 
 @pytest.mark.parametrize("base", [R.Q4_K, "rs", "rs6"])
