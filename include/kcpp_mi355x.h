@@ -188,10 +188,12 @@ int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t *kc, const 
 int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qta,
                                     void *ws, int T, int H, int HKV, int D, int n_past, float scale, void *stream);
 int64_t kcpp_fa_split_ws_bytes(int H);
-/* single-token decode attention (the k_fa_dec4 + k_fa_comb4 pair) with the combine writing the KT_Q8_0_TA activation of
- * the token (qta) -- bit-identical to kcpp_quantize_act(KT_Q8_0_TA) of its f32 output; -3 = not covered */
+/* single-token decode attention (the k_fa_dec5 + k_fa_comb4 pair) with the combine writing the KT_Q8_0_TA activation of
+ * the token (qta) -- bit-identical to kcpp_quantize_act(KT_Q8_0_TA) of its f32 output; n_kv_max = the caches' row count
+ * when n_past_dev is given (the graph-replayable form); -3 = not covered */
 int kcpp_flash_attn_dec_ta(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qta, void *ws,
-                           int H, int HKV, int D, int n_past, const int32_t *n_past_dev, float scale, void *stream);
+                           int H, int HKV, int D, int n_past, const int32_t *n_past_dev, int n_kv_max, float scale,
+                           void *stream);
 /* MFMA prefill kernel generation: 2 (default; env KCPP_FA_MFMA_V) = next tile prefetched, V read through the
  * LDS transpose; 1 = the first version; 0 = the default.  Bit-identical outputs.  Returns the previous value. */
 int kcpp_fa_prefill_set_variant(int v);

@@ -206,6 +206,68 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
     if (stamps) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); FA_STAMP(5); }
 }
 
+// ---------------------------------------------------------------- decode v5: every K/V load in flight from entry
+// k_fa_dec4 issued its first 16-key group only after the n_past word arrived (the split range depends on it), and its
+// loads sat in lane-conditional branches, so the compiler could not count them: the q conversion waited for nearly
+// all of the first group and the second group went out only after the first had landed -- two dependent HBM round
+// trips per wave plus the n_past one in front.  Here the key partition does not depend on n_past: 64-key chunks,
+// chunk c on split c % NS (chunks sp, sp + NS, ...), wave w owning keys 64 c + 16 w .. + 15 of each, so split sp's
+// first chunk is issued at entry beside q (rows clamped to the cache's n_rows), its second as soon as n_past is
+// known (rows clamped to n_past), and every load is unconditional (rows past the keys clamp to a valid row and are
+// masked by their score), which keeps the compiler's vmcnt accounting exact: two chunks per wave in flight, q waited
+// for alone.  Partials as k_fa_dec4 (O [H][NS][128], (m, l) [H][NS], m = -inf for a split without keys); the merge
+// is k_fa_comb4.
+template <int G, bool NT, int NW = 4>
+__global__ void __launch_bounds__(64 * NW) k_fa_dec5(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
+                                                     const uint16_t *__restrict__ vc, float *__restrict__ part_o,
+                                                     float2 *__restrict__ part_ml, int H, int n_past_arg,
+                                                     const int32_t *__restrict__ n_past_dev, int NS, float scale,
+                                                     int64_t kv_ld, int64_t kv_hs, int n_rows) {
+    constexpr int D = 128, CK = 16 * NW;              // keys per chunk: 16 per wave
+    const int sp = blockIdx.x, hk = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int sub = lane & 15, kq = lane >> 4;
+    __shared__ fadec::Smem<G, NW> sm;
+    const float sc2 = scale * 1.4426950408889634f;    // scores in the exp2 domain
+    uint4 qraw[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) qraw[g] = *(const uint4 *)(q16 + (int64_t)(hk * G + g) * D + sub * 8);
+    const uint16_t *kb = kc + (int64_t)hk * kv_hs + sub * 8, *vb = vc + (int64_t)hk * kv_hs + sub * 8;
+    uint4 ka[4], va[4], kn[4], vn[4];
+    auto issue = [&](int base, int lim, uint4 *kk, uint4 *vv) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t p = min(base + 4 * i + kq, lim);
+            if constexpr (NT) {
+                kk[i] = ld_nt(kb + p * kv_ld);
+                vv[i] = ld_nt(vb + p * kv_ld);
+            } else {
+                kk[i] = *(const uint4 *)(kb + p * kv_ld);
+                vv[i] = *(const uint4 *)(vb + p * kv_ld);
+            }
+        }
+    };
+    issue(CK * sp + 16 * wave, n_rows - 1, ka, va);
+    const int nkv = (n_past_dev ? n_past_dev[0] : n_past_arg) + 1;
+    const int lim = nkv - 1;
+    issue(CK * (sp + NS) + 16 * wave, lim, kn, vn);
+    fadec::State<G> st;
+#pragma unroll
+    for (int g = 0; g < G; ++g) fadec::set_q(st, g, qraw[g]);
+    fadec::init(st);
+    const int nch = (nkv + CK - 1) / CK;
+    for (int c = sp; c < nch; c += 2 * NS) {
+        const int b0 = CK * c + 16 * wave;
+        if (b0 < nkv) fadec::consume(st, b0, nkv, kq, sc2, ka, va);
+        issue(CK * (c + 2 * NS) + 16 * wave, lim, ka, va);
+        if (c + NS >= nch) break;
+        const int b1 = CK * (c + NS) + 16 * wave;
+        if (b1 < nkv) fadec::consume(st, b1, nkv, kq, sc2, kn, vn);
+        issue(CK * (c + 3 * NS) + 16 * wave, lim, kn, vn);
+    }
+    fadec::finish(st, sm, hk, sp, NS, part_o, part_ml);
+}
+
 // combine of k_fa_dec4's partials (m in the exp2 domain): grid (H / 2), 256 threads = 2 heads x 128 dims
 // (one Q8_K block of 256 when quantizing); thread (head, d) issues all NS partial loads of its dim (<= 64, in
 // flight together); one wave per head forms the split weights exp2(m_s - M) in LDS.
@@ -300,22 +362,25 @@ static int fa4_splits(int HKV) {
 template <int G, int NS>
 static void fa4_dispatch(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
                          float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
-                         float scale, hipStream_t s, int qkind) {
+                         float scale, hipStream_t s, int qkind, int n_rows, bool v5) {
     float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
     float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
     unsigned long long *st = (unsigned long long *)g_fa_stamps;
-    // (an in-launch merge -- write-through partials, a per-kv-head ticket, the last split merging -- measured
-    // 12.4 vs 10.6 us per layer at 3850 keys: draining the sc1 stores and the ticket round trip cost 1.5-3 us, more
-    // than this launch boundary)
-    // K/V rows are read once per token: non-temporal loads (MI355X_MICROARCH.md nt-weights) -- bench line 599.8 ->
-    // 632.5 tok/s; KCPP_FA_NT=0 restores the default policy
     static const bool nt = [] { const char *e = getenv("KCPP_FA_NT"); return !e || atoi(e) != 0; }();
-    if (nt)
+    if (v5 && n_rows > 0) {
+        if (nt)
+            hipLaunchKernelGGL((k_fa_dec5<G, true>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past,
+                               n_past_dev, NS, scale, kv_ld, kv_hs, n_rows);
+        else
+            hipLaunchKernelGGL((k_fa_dec5<G, false>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past,
+                               n_past_dev, NS, scale, kv_ld, kv_hs, n_rows);
+    } else if (nt) {
         hipLaunchKernelGGL((k_fa_dec4<G, true>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past,
                            n_past_dev, NS, scale, kv_ld, kv_hs, st);
-    else
+    } else {
         hipLaunchKernelGGL((k_fa_dec4<G, false>), dim3(NS, HKV), dim3(256), 0, s, q16, kc, vc, po, pml, H, n_past,
                            n_past_dev, NS, scale, kv_ld, kv_hs, st);
+    }
     if (qout && qkind == 2)
         hipLaunchKernelGGL((k_fa_comb4<2, NS>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)qout, H, st,
                            (unsigned *)nullptr);
@@ -328,31 +393,36 @@ static void fa4_dispatch(const uint16_t *q16, const uint16_t *kc, const uint16_t
 template <int G>
 static int fa4_dispatch_ns(int NS, const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld,
                            int64_t kv_hs, float *out, void *qout, void *ws, int H, int HKV, int n_past,
-                           const int32_t *n_past_dev, float scale, hipStream_t s, int qkind) {
+                           const int32_t *n_past_dev, float scale, hipStream_t s, int qkind, int n_rows, bool v5) {
     switch (NS) {
-    case 4: fa4_dispatch<G, 4>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
-    case 8: fa4_dispatch<G, 8>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
-    case 16: fa4_dispatch<G, 16>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
-    case 32: fa4_dispatch<G, 32>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
-    case 64: fa4_dispatch<G, 64>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
+    case 4: fa4_dispatch<G, 4>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind, n_rows, v5); break;
+    case 8: fa4_dispatch<G, 8>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind, n_rows, v5); break;
+    case 16: fa4_dispatch<G, 16>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind, n_rows, v5); break;
+    case 32: fa4_dispatch<G, 32>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind, n_rows, v5); break;
+    case 64: fa4_dispatch<G, 64>(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind, n_rows, v5); break;
     default: return -1;
     }
     return 0;
 }
 
-// single-token decode: k_fa_dec4 + k_fa_comb4; partials behind FA_WS_TICKETS in ws.
+// single-token decode: k_fa_dec5 (k_fa_dec4 when the cache's row count n_rows is not known, or for A/B with v5 off) +
+// k_fa_comb4; partials behind FA_WS_TICKETS in ws.  n_rows: rows the K/V views hold (n_ctx), >= n_past + 1.
+static bool fa_dec5_default() {
+    static const bool on = [] { const char *e = getenv("KCPP_FA_DEC"); return !e || atoi(e) != 4; }();
+    return on;
+}
 static int fa4_launch(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
                       float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
-                      float scale, hipStream_t s, int qkind = 1) {
+                      float scale, hipStream_t s, int qkind, int n_rows, bool v5) {
     const int G = H / HKV;
     const int NS = fa4_splits(HKV);
     if (!qout && !out) return -1;
     int rc = -1;
     switch (G) {
-    case 1: rc = fa4_dispatch_ns<1>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
-    case 2: rc = fa4_dispatch_ns<2>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
-    case 4: rc = fa4_dispatch_ns<4>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
-    case 8: rc = fa4_dispatch_ns<8>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind); break;
+    case 1: rc = fa4_dispatch_ns<1>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind, n_rows, v5); break;
+    case 2: rc = fa4_dispatch_ns<2>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind, n_rows, v5); break;
+    case 4: rc = fa4_dispatch_ns<4>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind, n_rows, v5); break;
+    case 8: rc = fa4_dispatch_ns<8>(NS, q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, qkind, n_rows, v5); break;
     default: return -1;
     }
     if (rc) return rc;
@@ -608,12 +678,13 @@ int64_t kcpp_fa_workspace_bytes(int T, int H, int n_kv_max) {
 // single-token decode attention (k_fa_dec4 + k_fa_comb4) whose combine writes the KT_Q8_0_TA activation of one token
 // (attn_output in the KT_Q8_0_T layout) instead of a separate kcpp_quantize_act; out f32 may be null.  -3: not covered
 int kcpp_flash_attn_dec_ta(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qta, void *ws,
-                           int H, int HKV, int D, int n_past, const int32_t *n_past_dev, float scale, void *stream) {
+                           int H, int HKV, int D, int n_past, const int32_t *n_past_dev, int n_kv_max, float scale,
+                           void *stream) {
     if (D != 128 || H % HKV || H % 2 || !qta) return -3;
     const int G = H / HKV;
     if (!(G == 2 || G == 4 || G == 8)) return -3;
     return fa4_launch(q16, kc, vc, (int64_t)HKV * 128, 128, out, qta, ws, H, HKV, n_past, n_past_dev, scale,
-                      (hipStream_t)stream, 2);
+                      (hipStream_t)stream, 2, n_past_dev ? n_kv_max : n_past + 1, fa_dec5_default());
 }
 
 // out f32 [T][H][D] (may be null), qout Q8_K act [T][H*D] (may be null), ws from kcpp_fa_workspace_bytes
@@ -638,7 +709,8 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     const bool use_decode = force_path == 1 || force_path == 6 || (force_path == 0 && T <= 16);
     const int G0 = H / HKV;
     if (use_decode && T == 1 && force_path != 6 && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) && (qout == nullptr || G0 >= 2))
-        return fa4_launch(q16, kc, vc, (int64_t)HKV * 128, 128, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s);
+        return fa4_launch(q16, kc, vc, (int64_t)HKV * 128, 128, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, 1,
+                          n_past_dev ? n_kv_max : n_past + 1, fa_dec5_default());
     if (use_decode) {
         ws = (uint8_t *)ws + FA_WS_TICKETS;
         const int nkv = n_past_dev ? n_kv_max : n_past + T;
@@ -688,8 +760,8 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
 
 // single-token decode attention with explicit cache strides (elements): key p of kv head hk starts at
 // kc + p * kv_ld + hk * kv_hs.  Position-major ggml view: kv_ld = HKV*D, kv_hs = D; head-major: kv_ld = D,
-// kv_hs = n_ctx*D.  variant 0: 64-key chunks + k_fa_combine; 3: k_fa_dec4 + k_fa_comb4 (the production kernel
-// pair).  A/B entry for tools/fa_dec_bench.py.
+// kv_hs = n_ctx*D.  variant 0: 64-key chunks + k_fa_combine; 3: k_fa_dec4 + k_fa_comb4 (round 5's production pair);
+// 5: k_fa_dec5 + k_fa_comb4 (the production pair; n_kv_max = the views' row count).  A/B entry for tools/fa_dec_bench.py.
 void kcpp_fa_set_stamps(void *p) { g_fa_stamps = p; }     // diagnostic stamp buffer of k_fa_dec4 / k_fa_comb4 (tools only)
 int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
                       float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
@@ -699,7 +771,34 @@ int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *v
     if (H % HKV || !(G == 1 || G == 2 || G == 4 || G == 8) || (H % 2) || HKV > 64) return -1;
     if (qout && G < 2) return -1;
     const int nkv = n_past_dev ? n_kv_max : n_past + 1;
-    if (variant == 3) return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s);
+    if (variant == 3 || variant == 5)
+        return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, 1, nkv,
+                          variant == 5);
+    if (variant == 6 || variant == 7) {     // A/B (tools/fa_dec_bench.py): k_fa_dec5 at NS splits (KCPP_FA_NS) x NW waves
+        // (KCPP_FA_NW), G = 4; 7: without the combine (the split kernel alone)
+        const int NS = getenv("KCPP_FA_NS") ? atoi(getenv("KCPP_FA_NS")) : 32;
+        const int NW = getenv("KCPP_FA_NW") ? atoi(getenv("KCPP_FA_NW")) : 4;
+        if (G != 4 || !out) return -1;
+        float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
+        float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
+#define KCPP_D6(NW_) hipLaunchKernelGGL((k_fa_dec5<4, true, NW_>), dim3(NS, HKV), dim3(64 * NW_), 0, s, q16, kc, vc, po, pml, \
+                                        H, n_past, n_past_dev, NS, scale, kv_ld, kv_hs, nkv)
+        if (NW == 4) KCPP_D6(4);
+        else if (NW == 8) KCPP_D6(8);
+        else if (NW == 16) KCPP_D6(16);
+        else return -1;
+#undef KCPP_D6
+        if (variant == 6) {
+            switch (NS) {
+            case 8: hipLaunchKernelGGL((k_fa_comb4<0, 8>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, (unsigned long long *)nullptr, (unsigned *)nullptr); break;
+            case 16: hipLaunchKernelGGL((k_fa_comb4<0, 16>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, (unsigned long long *)nullptr, (unsigned *)nullptr); break;
+            case 32: hipLaunchKernelGGL((k_fa_comb4<0, 32>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, H, (unsigned long long *)nullptr, (unsigned *)nullptr); break;
+            default: return -1;
+            }
+        }
+        KCPP_CHECK(hipGetLastError());
+        return 0;
+    }
     if (variant != 0) return -1;
     const int nch = (nkv + FA_CHUNK - 1) / FA_CHUNK;
     if (nch > FA_MAX_CHUNKS) return -4;

@@ -105,7 +105,10 @@ __device__ __forceinline__ void consume(State<G> &st, int base, int p1, int kq, 
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const uint32_t w4[4] = {vv[i].x, vv[i].y, vv[i].z, vv[i].w};
+        // keys >= p1 carry weight exp2(-inf) = 0; their V words (clamped or stale rows) are zeroed so a non-finite
+        // value there cannot turn 0 * v into NaN
+        const bool vok = base + 4 * i + kq < p1;
+        const uint32_t w4[4] = {vok ? vv[i].x : 0u, vok ? vv[i].y : 0u, vok ? vv[i].z : 0u, vok ? vv[i].w : 0u};
         float vf[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) { vf[2 * e] = h2f(w4[e] & 0xFFFF); vf[2 * e + 1] = h2f(w4[e] >> 16); }
@@ -116,17 +119,17 @@ __device__ __forceinline__ void consume(State<G> &st, int base, int p1, int kq, 
     }
 }
 
-template <int G>
+template <int G, int NW = 4>
 struct Smem {
-    float o[4][G][D];
-    float ml[4][G][2];
-    float w[4][G], L[G];
+    float o[NW][G][D];
+    float ml[NW][G][2];
+    float w[NW][G], L[G];
 };
 
-// rows (kq) hold disjoint keys: park every row's 8 dims in LDS, reduce rows and waves in one pass; write the split's
-// partial O and (M, L) of heads hk * G + g
-template <int G>
-__device__ __forceinline__ void finish(State<G> &st, Smem<G> &sm, int hk, int sp, int NS, float *__restrict__ part_o,
+// rows (kq) hold disjoint keys: park every row's 8 dims in LDS, reduce rows and the NW waves in one pass; write the
+// split's partial O and (M, L) of heads hk * G + g
+template <int G, int NW = 4>
+__device__ __forceinline__ void finish(State<G> &st, Smem<G, NW> &sm, int hk, int sp, int NS, float *__restrict__ part_o,
                                        float2 *__restrict__ part_ml) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int sub = lane & 15, kq = lane >> 4;
@@ -154,10 +157,10 @@ __device__ __forceinline__ void finish(State<G> &st, Smem<G> &sm, int hk, int sp
         const int g = tid;
         float M = -INFINITY;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) M = fmaxf(M, sm.ml[w][g][0]);
+        for (int w = 0; w < NW; ++w) M = fmaxf(M, sm.ml[w][g][0]);
         float L = 0.0f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < NW; ++w) {
             const float wt = M == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(sm.ml[w][g][0] - M);
             sm.w[w][g] = wt;
             L = fmaf(wt, sm.ml[w][g][1], L);
@@ -166,11 +169,11 @@ __device__ __forceinline__ void finish(State<G> &st, Smem<G> &sm, int hk, int sp
         part_ml[(int64_t)(hk * G + g) * NS + sp] = make_float2(M, L);
     }
     __syncthreads();
-    for (int i = tid; i < G * D; i += 256) {
+    for (int i = tid; i < G * D; i += 64 * NW) {
         const int g = i / D, d = i % D;
         float O = 0.0f;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) O = fmaf(sm.w[w][g], sm.o[w][g][d], O);
+        for (int w = 0; w < NW; ++w) O = fmaf(sm.w[w][g], sm.o[w][g][d], O);
         part_o[((int64_t)(hk * G + g) * NS + sp) * D + d] = O;
     }
 }

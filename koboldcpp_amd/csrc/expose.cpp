@@ -36,6 +36,7 @@
 #include "../../include/kcpp_mi355x.h"
 #include "../../include/kcpp_synth.h"
 #include "gguf.h"
+#include "kcpp_internal.h"
 #include "sampler.h"
 #include "tokenizer.h"
 
@@ -83,6 +84,11 @@ struct Engine {
     Rccl rccl;
     std::vector<void *> comms;              // rank s = stage s
     std::vector<hipEvent_t> ev_done, ev_read;
+    // greedy single-token steps: the hand-off inside each stage's graph (link.hip: the consumer's first kernel pulls the
+    // producer's row once its flag is up, the producer's last kernel raises it) -- no event, copy or host call between
+    // stages; prefill ubatches keep the RCCL / event-ordered copies above
+    bool linked = false;
+    std::vector<void *> link_blk;           // per stage: 256 B of flag words on the stage's device
     int ub = 512;
     bool use_contextshift = false;
     std::vector<int> ctx;                   // tokens whose K/V are in the caches
@@ -98,6 +104,8 @@ struct Engine {
         }
         for (void *c : comms) if (c && rccl.destroy) rccl.destroy(c);
         for (auto *m : stages) kcpp_model_free(m);
+        for (size_t s = 0; s < link_blk.size(); ++s)
+            if (link_blk[s]) { hipSetDevice(devs[s]); hipFree(link_blk[s]); }
     }
 };
 
@@ -172,6 +180,7 @@ struct PipeOps {
     virtual int handoff(size_t s, int t) = 0;             // stage s-1's residual stream (t tokens) -> stage s
     virtual int argmax_dev() = 0;                         // last stage: greedy token of its last logits, on device
     virtual int token_home() = 0;                         // that token -> stage 0's input token (device copy)
+    bool in_greedy = false;                               // inside greedy_step
 };
 
 // run tokens [i0, i0+T) through all stages, ubatch by ubatch, everything enqueued: stage s works on ubatch u while
@@ -195,17 +204,18 @@ int forward(PipeOps &o, const int32_t *toks, int T, int n_past) {
 
 // one greedy token through all stages without the host: stage 0 embeds the token the last stage's argmax left
 // (moved home by token_home), each later stage takes its predecessor's hand-off, the last stage's step computes
-// the next greedy token on device, which goes home for the next step
+// the next greedy token on device, which goes home for the next step.  (HipOps with linked stages: the hand-offs
+// and the token's way home happen inside the stage steps, link.hip.)
 int greedy_step(PipeOps &o, int n_past) {
-    for (size_t s = 0; s < o.n_stages(); ++s) {
-        if (s > 0) {
-            const int rc = o.handoff(s, 1);
-            if (rc) return rc;
-        }
-        const int rc = o.step_dev(s, n_past);
-        if (rc) return rc;
+    o.in_greedy = true;
+    int rc = 0;
+    for (size_t s = 0; s < o.n_stages() && !rc; ++s) {
+        if (s > 0) rc = o.handoff(s, 1);
+        if (!rc) rc = o.step_dev(s, n_past);
     }
-    return o.token_home();
+    if (!rc) rc = o.token_home();
+    o.in_greedy = false;
+    return rc;
 }
 
 struct HipOps : PipeOps {
@@ -216,10 +226,13 @@ struct HipOps : PipeOps {
     int decode(size_t s, const int32_t *toks, int t, int n_past) override {
         return kcpp_model_decode_async(e.stages[s], toks, t, n_past);
     }
-    int step_dev(size_t s, int n_past) override { return kcpp_model_step_dev(e.stages[s], n_past); }
+    int step_dev(size_t s, int n_past) override {
+        return e.linked ? kcpp_model_step_linked(e.stages[s], n_past) : kcpp_model_step_dev(e.stages[s], n_past);
+    }
     int argmax_dev() override { return kcpp_model_argmax_async(e.stages.back()); }
     // stage s-1's residual stream (t tokens) -> stage s's input, on the two stages' streams
     int handoff(size_t s, int t) override {
+        if (in_greedy && e.linked) return 0;                       // pulled by stage s's own graph (link.hip)
         const size_t count = (size_t)t * e.hp.n_embd;
         hipStream_t src = (hipStream_t)kcpp_model_stream(e.stages[s - 1]), dst = (hipStream_t)kcpp_model_stream(e.stages[s]);
         if (!e.comms.empty()) {
@@ -243,7 +256,8 @@ struct HipOps : PipeOps {
     // step, then a peer copy over xGMI (one stage: the argmax kernel already wrote the token input)
     int token_home() override {
         const size_t L = e.stages.size() - 1;
-        if (L == 0) return 0;
+        if (L == 0 || (in_greedy && e.linked)) return 0;           // linked: stage 0's graph pulls the token
+        
         hipStream_t last = (hipStream_t)kcpp_model_stream(e.stages[L]), first = (hipStream_t)kcpp_model_stream(e.stages[0]);
         if (hipSetDevice(e.devs[L]) || hipEventRecord(e.ev_done[L], last)) return -24;
         if (hipSetDevice(e.devs[0]) || hipStreamWaitEvent(first, e.ev_done[L], 0)) return -24;
@@ -282,6 +296,58 @@ int forward(Engine &e, const int32_t *toks, int T, int n_past) {
     return forward(o, toks, T, n_past);
 }
 
+// the linked single-token hand-off (link.hip) when every stage replays graphs and each pair of neighbouring stages
+// (and the last and the first) can reach each other's memory; KCPP_HANDOFF=copy / rccl keep the single-token hops on
+// the event-ordered copies / RCCL
+static void init_links(Engine &e) {
+    const size_t S = e.stages.size();
+    const char *mode = getenv("KCPP_HANDOFF");
+    if (S < 2 || (mode && (!strcmp(mode, "copy") || !strcmp(mode, "rccl")))) return;
+    auto reach = [&](int a, int b) {            // device a's kernels may access device b's memory
+        if (a == b) return true;
+        int ok = 0;
+        if (hipDeviceCanAccessPeer(&ok, a, b) != hipSuccess || !ok) return false;
+        hipSetDevice(a);
+        const hipError_t r = hipDeviceEnablePeerAccess(b, 0);
+        (void)hipGetLastError();
+        return r == hipSuccess || r == hipErrorPeerAccessAlreadyEnabled;
+    };
+    for (size_t s = 0; s < S; ++s) {
+        const size_t p = (s + S - 1) % S, c = (s + 1) % S;
+        if (!reach(e.devs[s], e.devs[p]) || !reach(e.devs[s], e.devs[c])) return;
+    }
+    e.link_blk.assign(S, nullptr);
+    for (size_t s = 0; s < S; ++s) {
+        hipSetDevice(e.devs[s]);
+        if (hipMalloc(&e.link_blk[s], 256) != hipSuccess || hipMemset(e.link_blk[s], 0, 256) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess)
+            return;
+    }
+    // words of stage s's block: [0] step counter, [16] ready_in, [32] copied_out
+    auto word = [&](size_t s, int i) { return (unsigned *)e.link_blk[s] + i; };
+    for (size_t s = 0; s < S; ++s) {
+        const size_t p = (s + S - 1) % S, c = (s + 1) % S;
+        KLink L{};
+        L.stepctr = word(s, 0);
+        L.ready_in = word(s, 16);
+        L.copied_out = word(s, 32);
+        L.ready_out = word(c, 16);
+        L.copied_report = word(p, 32);
+        if (s == 0) {
+            L.src_tok = kcpp_model_argmax_dev(e.stages[S - 1]);
+            L.dst_tok = kcpp_model_token_dev(e.stages[0]);
+            L.in_lag = 1;
+        } else {
+            L.src_x = e.hidden[s - 1];
+            L.dst_x = e.hidden[s];
+            L.n = e.hp.n_embd;
+        }
+        L.out_lag = s == S - 1 ? 0 : 1;
+        if (kcpp_model_set_link(e.stages[s], &L)) return;
+    }
+    e.linked = true;
+}
+
 // events for the copy handoff, and an RCCL clique when every stage sits on its own device (RCCL refuses two
 // ranks on one GPU); KCPP_HANDOFF=copy forces the event-ordered copies
 bool init_handoff(Engine &e) {
@@ -295,6 +361,7 @@ bool init_handoff(Engine &e) {
             return false;
     }
     if (S < 2) return true;
+    init_links(e);
     std::vector<int> sorted = e.devs;
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
@@ -1061,6 +1128,7 @@ int kcpp_engine_bench(const kcpp_hparams *hp, const int *types, int n_types, int
     std::chrono::steady_clock::time_point t2 = t1;
     // greedy tokens without the host: the prefill's token goes home on device, then every step's token too
     if (o.argmax_dev() || o.token_home()) return -6;
+    std::chrono::steady_clock::time_point te = t1;
     for (int i = 0; i < n_warm + n_steps; ++i) {
         if (i == n_warm) {
             if (sync_all()) return -6;
@@ -1069,8 +1137,13 @@ int kcpp_engine_bench(const kcpp_hparams *hp, const int *types, int n_types, int
         if (greedy_step(o, n_past)) return -6;
         ++n_past;
     }
+    te = std::chrono::steady_clock::now();                             // host: every step enqueued
     if (sync_all()) return -6;                                         // the last token computed and home
     const auto t3 = std::chrono::steady_clock::now();
+    if (getenv("KCPP_ENGINE_HOST_TIMING"))
+        fprintf(stderr, "[kcpp] engine_bench: %zu stages, host enqueue %.1f us/token, wall %.1f us/token\n",
+                e->stages.size(), std::chrono::duration<double>(te - t2).count() * 1e6 / n_steps,
+                std::chrono::duration<double>(t3 - t2).count() * 1e6 / n_steps);
     out[0] = std::chrono::duration<double>(t1 - t0).count();
     out[1] = std::chrono::duration<double>(t3 - t2).count();
     out[2] = n_past;

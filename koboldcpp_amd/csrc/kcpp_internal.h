@@ -132,10 +132,33 @@ extern "C" int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16
                                                void *stream);
 extern "C" int64_t kcpp_fa_split_ws_bytes(int H);
 extern "C" int kcpp_flash_attn_dec_ta(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, float *out, void *qta,
-                                      void *ws, int H, int HKV, int D, int n_past, const int32_t *n_past_dev, float scale,
-                                      void *stream);
+                                      void *ws, int H, int HKV, int D, int n_past, const int32_t *n_past_dev,
+                                      int n_kv_max, float scale, void *stream);
 // decode mat-vec over the row-major RS layouts (gemv_rs.hip); -3 = not covered
 extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
 extern "C" int kcpp_rs_supported(int type, int64_t K);
 
 
+
+struct kcpp_model;
+// single-token stage hand-off by the stages' own kernels (link.hip; the layer-split engine in expose.cpp): this stage's
+// wait / pull / report words and the peers it writes (peer memory on another GPU).  in_lag: 1 on stage 0 (its input is
+// the previous step's token), else 0; out_lag: 0 on the last stage (stage 0 pulls its token in the same step), else 1.
+struct KLink {
+    unsigned *stepctr;            // this stage's linked-step counter (local)
+    const unsigned *ready_in;     // local: the producer's published step
+    const unsigned *copied_out;   // local: the step the consumer has pulled this stage's output for
+    unsigned *ready_out;          // the consumer's ready_in
+    unsigned *copied_report;      // the producer's copied_out
+    const float *src_x;           // stage >= 1: the producer's residual row, n floats
+    float *dst_x;
+    int n;
+    const int32_t *src_tok;       // stage 0: the last stage's greedy token
+    int32_t *dst_tok;
+    int in_lag, out_lag;
+};
+int kcpp_link_wait(const KLink &L, hipStream_t s);
+int kcpp_link_publish(const KLink &L, hipStream_t s);
+// the stage's single-token graph bracketed by the link kernels (runtime.cpp); -3 when graphs are off (row split)
+int kcpp_model_set_link(kcpp_model *m, const KLink *L);
+int kcpp_model_step_linked(kcpp_model *m, int n_past);

@@ -143,6 +143,10 @@ struct kcpp_model {
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
     int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
     hipGraphExec_t g_exec = nullptr;
+    // layer-split engine: the single-token graph bracketed by the stage hand-off kernels (link.hip), captured lazily
+    KLink link{};
+    bool has_link = false;
+    hipGraphExec_t g_link = nullptr;
     hipStream_t side = nullptr;             // second branch of the decode step (independent q|k|v launches)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int64_t weight_bytes = 0;
@@ -446,6 +450,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     if (!m) return;
     hipSetDevice(m->device);
     if (m->g_exec) hipGraphExecDestroy(m->g_exec);
+    if (m->g_link) hipGraphExecDestroy(m->g_link);
     auto F = [](void *p) { if (p) hipFree(p); };
     F(m->moe_trace);
     auto FS = [&](KTensor &t) {
@@ -688,6 +693,7 @@ extern "C" int kcpp_model_set_row_split(kcpp_model *m, int n, const int *devices
     RT_CHECK(hipSetDevice(m->device));
     RT_CHECK(hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
     m->use_graphs = false;
     m->fused_decode = false;
     return 0;
@@ -714,6 +720,7 @@ extern "C" int kcpp_model_moe_trace(kcpp_model *m, int enable) {
         m->moe_trace = nullptr;
     }
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
     return 0;
 }
 // MoE single-token decode fusions: bit 0 routes inside the two-slot gate|up launch (else k_moe_route), bit 1 runs
@@ -725,6 +732,7 @@ extern "C" int kcpp_model_set_fused_route(kcpp_model *m, int on) {
     m->no_fused_route = !(on & 1);
     m->no_pair_down = !(on & 2);
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
     return 0;
 }
 extern "C" int64_t kcpp_model_fused_route_count(kcpp_model *m) { return m->n_fused_route + (m->n_pair_down << 32); }
@@ -745,6 +753,7 @@ extern "C" int kcpp_model_moe_trace_read(kcpp_model *m, int32_t *out, int n) {
 extern "C" int kcpp_model_set_fa_exact(kcpp_model *m, int enable) {
     m->fa_exact = enable != 0;
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
     return 0;
 }
 extern "C" int kcpp_model_set_kv_types(kcpp_model *m, int tk, int tv) {
@@ -768,11 +777,13 @@ extern "C" int kcpp_model_set_kv_types(kcpp_model *m, int tk, int tv) {
     }
     m->kv_tk = tk; m->kv_tv = tv;
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
     return 0;
 }
 extern "C" int kcpp_model_set_fused_decode(kcpp_model *m, int enable) {
     m->fused_decode = enable != 0 && m->lanes.empty();
     if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
+    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
     return 0;
 }
 
@@ -1292,7 +1303,7 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
         // (row-split lanes too: attention is not split, and wo's lanes read the same activation)
         if (m->q80t && !kvq && !m->fa_exact && t[4].type == KT_Q8_0_T && (T == 1 || (T > 16 && !posp))) {
             const int rc = T == 1 ? kcpp_flash_attn_dec_ta(m->q16, L.kc, L.vc, nullptr, m->act, m->fa_ws, (int)H, (int)HKV,
-                                                           (int)D, n_past, posp, kq_scale, s)
+                                                           (int)D, n_past, posp, hp.n_ctx, kq_scale, s)
                                   : kcpp_flash_attn_prefill_mfma_ex(m->q16, L.kc, L.vc, nullptr, m->act, m->fa_ws, T,
                                                                     (int)H, (int)HKV, (int)D, n_past, kq_scale, s);
             if (rc != 0 && rc != -3) return rc;
@@ -1426,6 +1437,42 @@ static int ensure_graph(kcpp_model *m) {
     if (rc || e != hipSuccess) { g_err = "graph capture failed"; return rc ? rc : -3; }
     RT_CHECK(hipGraphInstantiate(&m->g_exec, g, nullptr, nullptr, 0));
     hipGraphDestroy(g);
+    return 0;
+}
+
+// the linked single-token step (layer-split engine, expose.cpp): k_link_wait (pull this stage's input from the
+// producer stage, device-side), the step, k_link_publish -- one graph replay, no host call between stages
+int kcpp_model_set_link(kcpp_model *m, const KLink *L) {
+    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
+    m->has_link = L != nullptr;
+    if (L) m->link = *L;
+    return 0;
+}
+
+static int ensure_graph_linked(kcpp_model *m) {
+    if (m->g_link) return 0;
+    hipGraph_t g;
+    RT_CHECK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
+    int rc = kcpp_link_wait(m->link, m->stream);
+    if (!rc) rc = decode_step_dev(m);
+    if (!rc) rc = kcpp_link_publish(m->link, m->stream);
+    hipError_t e = hipStreamEndCapture(m->stream, &g);
+    if (rc || e != hipSuccess) { g_err = "linked graph capture failed"; return rc ? rc : -3; }
+    RT_CHECK(hipGraphInstantiate(&m->g_link, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
+    return 0;
+}
+
+int kcpp_model_step_linked(kcpp_model *m, int n_past) {
+    if (!m->has_link || !m->use_graphs) { g_err = "linked step: no link or graphs off"; return -3; }
+    if (n_past + 1 > m->hp.n_ctx) { g_err = "context overflow"; return -2; }
+    RT_CHECK(hipSetDevice(m->device));
+    m->pos_val = m->pos_val == n_past ? n_past : -1;
+    RC(ensure_graph_linked(m));
+    RC(set_pos(m, n_past));
+    const hipError_t e = hipGraphLaunch(m->g_link, m->stream);
+    if (e != hipSuccess) { m->pos_val = -1; RT_CHECK(e); }
+    m->pos_val = n_past + 1;
     return 0;
 }
 

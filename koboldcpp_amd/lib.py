@@ -57,7 +57,7 @@ _SIGS = {
     "kcpp_flash_attn_prefill_mfma": [P, P, P, P, I, I, I, I, I, Fl, P],
     "kcpp_flash_attn_prefill_mfma_ex": [P, P, P, P, P, P, I, I, I, I, I, Fl, P],
     "kcpp_fa_split_ws_bytes": [I],
-    "kcpp_flash_attn_dec_ta": [P, P, P, P, P, P, I, I, I, I, P, Fl, P],
+    "kcpp_flash_attn_dec_ta": [P, P, P, P, P, P, I, I, I, I, P, I, Fl, P],
     "kcpp_fa_decode_ex": [P, P, P, I64, I64, P, P, P, I, I, I, P, I, Fl, I, P],
     "kcpp_fa_set_stamps": [P],
     "kcpp_gguf_check": [ctypes.c_char_p, ctypes.c_char_p, I],

@@ -230,19 +230,25 @@ def test_long_context_decode_matches_short_context():
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
-def test_generate_layer_split_pipeline_matches_single_stage(model, tmp_path, monkeypatch):
-    """--tensorsplit through load_model: 3 stages (KCPP_VIRTUAL_DEVICES=3 puts them all on the one GPU of the
+@pytest.mark.parametrize("handoff,split", [("linked", (1.0, 2.0, 1.0)), ("copy", (1.0, 2.0, 1.0)),
+                                           ("linked", (1.0, 1.0, 3.0, 1.0, 1.0))])
+def test_generate_layer_split_pipeline_matches_single_stage(model, tmp_path, monkeypatch, handoff, split):
+    """--tensorsplit through load_model: 3 or 5 stages (KCPP_VIRTUAL_DEVICES puts them all on the one GPU of the
     test box), prefill in 16-token ubatches pipelined across the stages, the residual stream handed stage to stage
     on the stage streams with event ordering and no host synchronisation (RCCL send/recv when the stages sit on
-    distinct GPUs) -- greedy text equal to a single in-process stage with the same ubatch size.  Runs last: it
-    replaces the module's loaded model."""
+    distinct GPUs); greedy decode steps with the hand-off inside the stage graphs (link.hip: each stage's first
+    kernel pulls its input once the producer's flag is up, stage 0 pulls the last stage's token; KCPP_HANDOFF=copy:
+    the event-ordered copies, as in prefill), uneven stages -- greedy text equal to a single in-process stage with
+    the same ubatch size.  Runs last: it replaces the module's loaded model."""
     import koboldcpp_amd.lib as K
     h, X, _, _, _ = model
     hp = dict(R.TINY, n_layer=5, n_ctx=256)
     types = R.q4_k_m_types(hp["n_layer"])
     path = str(tmp_path / "split.gguf")
     toks = GW.llama_gguf(path, hp, types, 1234, WORDS)
-    monkeypatch.setenv("KCPP_VIRTUAL_DEVICES", "3")
+    monkeypatch.setenv("KCPP_VIRTUAL_DEVICES", str(len(split)))
+    if handoff == "copy":
+        monkeypatch.setenv("KCPP_HANDOFF", "copy")
     li = X.load_model_inputs()
     li.model_filename = path.encode()
     li.max_context_length = 248
@@ -250,7 +256,7 @@ def test_generate_layer_split_pipeline_matches_single_stage(model, tmp_path, mon
     li.gpulayers = 999
     li.rope_freq_base = 10000.0
     li.rope_freq_scale = 0.0     # koboldcpp.py default --ropeconfig 0: automatic RoPE
-    for i, v in enumerate((1.0, 2.0, 1.0)):
+    for i, v in enumerate(split):
         li.tensor_split[i] = v
     assert h.load_model(li)
     _, _, ttypes = GW.spm_vocab(hp["n_vocab"], WORDS)
@@ -261,7 +267,7 @@ def test_generate_layer_split_pipeline_matches_single_stage(model, tmp_path, mon
     gi = X.generation_inputs()
     gi.prompt = prompt
     gi.max_context_length = 248
-    gi.max_length = 10
+    gi.max_length = 24
     gi.temperature = 0.0
     gi.top_k = 1
     gi.rep_pen = 1.0
@@ -273,7 +279,7 @@ def test_generate_layer_split_pipeline_matches_single_stage(model, tmp_path, mon
     m.decode(ids, 0, want_logits=False)
     want = [m.argmax()]
     n = len(ids)
-    for _ in range(9):
+    for _ in range(23):
         want.append(m.decode_greedy(n))
         n += 1
     m.close()
@@ -340,6 +346,11 @@ def test_engine_bench_virtual_stages(monkeypatch):
     r = K.engine_bench(hp, types, 3, 64, 16, 2, 8)
     assert r["n_past"] == 64 + 2 + 8 and not r["rccl"]
     assert r["prefill_s"] > 0 and r["decode_s"] > 0
+    # the linked single-token steps: 200 of them back to back on 8 stages (every hand-off flag reused 200 times)
+    monkeypatch.setenv("KCPP_VIRTUAL_DEVICES", "8")
+    hp8 = dict(R.TINY, n_layer=8, n_ctx=300)
+    r = K.engine_bench(hp8, R.q4_k_m_types(8), 8, 32, 16, 4, 200)
+    assert r["n_past"] == 32 + 4 + 200 and r["decode_s"] > 0
 
 
 def test_generate_process_time_includes_the_prefill(model):

@@ -107,7 +107,7 @@ def test_decode_ta_combine(env, n_past, dev):
     out = torch.empty(1, E, device="cuda")
     qta = torch.zeros(K.act_bytes(K.Q8_0_T, E, 1), dtype=torch.uint8, device="cuda")
     K.call("kcpp_flash_attn_dec_ta", q16.data_ptr(), kc.data_ptr(), vc.data_ptr(), out.data_ptr(), qta.data_ptr(),
-           ws.data_ptr(), H, HKV, D, 0 if dev else n_past, npd.data_ptr() if dev else None, 0.088, sptr(torch))
+           ws.data_ptr(), H, HKV, D, 0 if dev else n_past, npd.data_ptr() if dev else None, n_ctx, 0.088, sptr(torch))
     want = torch.zeros_like(qta)
     K.call("kcpp_quantize_act", K.Q8_0_TA, ref.data_ptr(), E, want.data_ptr(), E, 1, sptr(torch))
     torch.cuda.synchronize()

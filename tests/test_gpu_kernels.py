@@ -315,11 +315,14 @@ def test_flash_attn_vs_oracle_f32_accum(env, T, n_past, path):
         np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
 
 
+@pytest.mark.parametrize("variant", [3, 5])
 @pytest.mark.parametrize("H,HKV", [(32, 8), (32, 32), (64, 8), (16, 8), (32, 4), (8, 4), (64, 64)])
-def test_fa_dec4_split_counts(env, H, HKV):
-    """the production decode pair (k_fa_dec4 + k_fa_comb4, kcpp_fa_decode_ex variant 3) over split counts 4..64
-    (256 / HKV rounded down to a power of two) and GQA groups 1..8: back-to-back calls whose key counts differ
-    (empty, partial and full splits) are reproducible bit for bit and match the f32-accumulation oracle."""
+def test_fa_dec4_split_counts(env, H, HKV, variant):
+    """the decode pairs (5: k_fa_dec5 + k_fa_comb4, production: 64-key chunks dealt round-robin over the splits, rows
+    clamped to the cache; 3: round 5's k_fa_dec4, contiguous key ranges) over split counts 4..64 (256 / HKV rounded down
+    to a power of two) and GQA groups 1..8: back-to-back calls whose key counts differ (empty, partial and full splits,
+    a cache whose rows past the keys hold NaN / inf, which must not leak into the result) are reproducible bit for bit
+    and match the f32-accumulation oracle."""
     torch, K = env
     D, n_ctx = 128, 4200
     rng = np.random.default_rng(H * 100 + HKV)
@@ -330,13 +333,18 @@ def test_fa_dec4_split_counts(env, H, HKV):
     npd = torch.zeros(1, dtype=torch.int32, device="cuda")
     for n_past in (0, 5, 100, 3850, 7, 4095):
         npd.fill_(n_past)
+        # rows past the keys: stale cache contents may be anything (v5 loads them, masked by score)
+        kd.copy_(dev(torch, kcache))
+        vd.copy_(dev(torch, vcache))
+        kd.view(n_ctx, HKV, D)[n_past + 1:] = float("nan")
+        vd.view(n_ctx, HKV, D)[n_past + 1:] = float("inf")
         q = rng.standard_normal((1, H, D)).astype(np.float32)
         q16 = dev(torch, q.astype(np.float16))
         outs = []
         for _ in range(2):
             out = torch.full((1, H, D), float("nan"), dtype=torch.float32, device="cuda")
             K.call("kcpp_fa_decode_ex", q16.data_ptr(), kd.data_ptr(), vd.data_ptr(), HKV * D, D, out.data_ptr(), None,
-                   ws.data_ptr(), H, HKV, 0, npd.data_ptr(), n_ctx, 1.0 / np.sqrt(D), 3, sptr(torch))
+                   ws.data_ptr(), H, HKV, 0, npd.data_ptr(), n_ctx, 1.0 / np.sqrt(D), variant, sptr(torch))
             outs.append(host(torch, out, np.float32).reshape(1, H, D))
         assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32)), f"n_past {n_past}"
         n_kv = n_past + 1
