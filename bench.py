@@ -229,12 +229,17 @@ def run_model(K, torch, hp, types, n_prompt, ubatch, steps, warmup):
         n_past += 1
     steps = min(steps, hp["n_ctx"] - n_past)
     torch.cuda.synchronize()
+    # every token comes back to the host, one step behind the device (the next step is queued while the host reads
+    # the previous token: kcpp_model_decode_greedy_lagged); the timed region ends when the last token is on the host
+    toks = []
     t0 = time.perf_counter()
     for _ in range(steps):
-        m.decode_greedy(n_past)
+        toks.append(m.decode_greedy_lagged(n_past))
         n_past += 1
+    toks.append(m.greedy_drain())
     torch.cuda.synchronize()
     t_tg = time.perf_counter() - t0
+    assert toks[0] == -1 and min(toks[1:]) >= 0 and len(toks) == steps + 1
     wb = m.weight_bytes()
     m.close()
     return {"dec": steps / t_tg, "pre": n_prompt / t_pp, "t_pp": t_pp, "ms_step": t_tg / steps * 1e3, "steps": steps,

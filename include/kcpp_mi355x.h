@@ -340,6 +340,11 @@ int32_t *kcpp_model_argmax_dev(kcpp_model *m);
  * own argmax computed in the same graph replay and returned (one host sync per token).
  * Requires a stage owning both the embedding and the output head. */
 int kcpp_model_decode_greedy(kcpp_model *m, int n_past, int32_t *token_out);
+/* the same step with the host one token behind the device: returns the PREVIOUS step's token (-1 on the first call
+ * after a drain) once its 4-byte read has landed, while this step is already queued; kcpp_model_greedy_drain returns
+ * the last step's token and resets the readback ring */
+int kcpp_model_decode_greedy_lagged(kcpp_model *m, int n_past, int32_t *token_out);
+int kcpp_model_greedy_drain(kcpp_model *m, int32_t *token_out);
 /* context shift (koboldcpp PurgeMissingTokens, gpttype_adapter.cpp:1504-1571: llama_kv_cache_seq_rm(p0, p0+diff)
  * + seq_add(p0+diff, n_past, -diff) + the K-shift of build_k_shift): cache rows [p0+diff, n_past) move to
  * [p0, n_past-diff) and K is re-rotated by position -diff (rope f16, mode NORM).  Synchronous. */

@@ -217,27 +217,42 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
 // masked by their score), which keeps the compiler's vmcnt accounting exact: two chunks per wave in flight, q waited
 // for alone.  Partials as k_fa_dec4 (O [H][NS][128], (m, l) [H][NS], m = -inf for a split without keys); the merge
 // is k_fa_comb4.
-template <int G, bool NT, int NW = 4>
+// GRAPH (the ggml plugin's FLASH_ATTN_EXT with one query, kcpp_flash_attn_ext_dec): q f32 at qf (head stride qf_hs
+// floats), rounded to f16 in the kernel; the f16 mask row added to the scores, -inf keys skipped.
+template <int G, bool NT, int NW = 4, bool GRAPH = false>
 __global__ void __launch_bounds__(64 * NW) k_fa_dec5(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
                                                      const uint16_t *__restrict__ vc, float *__restrict__ part_o,
                                                      float2 *__restrict__ part_ml, int H, int n_past_arg,
                                                      const int32_t *__restrict__ n_past_dev, int NS, float scale,
-                                                     int64_t kv_ld, int64_t kv_hs, int n_rows) {
+                                                     int64_t kv_ld, int64_t kv_hs, int n_rows,
+                                                     const float *__restrict__ qf = nullptr, int64_t qf_hs = 0,
+                                                     const uint16_t *__restrict__ mask = nullptr) {
     constexpr int D = 128, CK = 16 * NW;              // keys per chunk: 16 per wave
     const int sp = blockIdx.x, hk = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int sub = lane & 15, kq = lane >> 4;
     __shared__ fadec::Smem<G, NW> sm;
     const float sc2 = scale * 1.4426950408889634f;    // scores in the exp2 domain
-    uint4 qraw[G];
+    uint4 qraw[GRAPH ? 1 : G];
+    float4 qfa[GRAPH ? G : 1], qfb[GRAPH ? G : 1];
 #pragma unroll
-    for (int g = 0; g < G; ++g) qraw[g] = *(const uint4 *)(q16 + (int64_t)(hk * G + g) * D + sub * 8);
+    for (int g = 0; g < G; ++g) {
+        if constexpr (GRAPH) {
+            const float4 *qp = (const float4 *)(qf + (int64_t)(hk * G + g) * qf_hs + sub * 8);
+            qfa[g] = qp[0];
+            qfb[g] = qp[1];
+        } else {
+            qraw[g] = *(const uint4 *)(q16 + (int64_t)(hk * G + g) * D + sub * 8);
+        }
+    }
     const uint16_t *kb = kc + (int64_t)hk * kv_hs + sub * 8, *vb = vc + (int64_t)hk * kv_hs + sub * 8;
     uint4 ka[4], va[4], kn[4], vn[4];
-    auto issue = [&](int base, int lim, uint4 *kk, uint4 *vv) {
+    uint32_t ma[GRAPH ? 4 : 1], mb[GRAPH ? 4 : 1];      // mask words (f16) of the group's keys
+    auto issue = [&](int base, int lim, uint4 *kk, uint4 *vv, uint32_t *mm) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int64_t p = min(base + 4 * i + kq, lim);
+            if constexpr (GRAPH) mm[i] = mask[p];
             if constexpr (NT) {
                 kk[i] = ld_nt(kb + p * kv_ld);
                 vv[i] = ld_nt(vb + p * kv_ld);
@@ -247,23 +262,34 @@ __global__ void __launch_bounds__(64 * NW) k_fa_dec5(const uint16_t *__restrict_
             }
         }
     };
-    issue(CK * sp + 16 * wave, n_rows - 1, ka, va);
+    issue(CK * sp + 16 * wave, n_rows - 1, ka, va, ma);
     const int nkv = (n_past_dev ? n_past_dev[0] : n_past_arg) + 1;
     const int lim = nkv - 1;
-    issue(CK * (sp + NS) + 16 * wave, lim, kn, vn);
+    issue(CK * (sp + NS) + 16 * wave, lim, kn, vn, mb);
     fadec::State<G> st;
 #pragma unroll
-    for (int g = 0; g < G; ++g) fadec::set_q(st, g, qraw[g]);
+    for (int g = 0; g < G; ++g) {
+        if constexpr (GRAPH) fadec::set_q_f32(st, g, qfa[g], qfb[g]);
+        else fadec::set_q(st, g, qraw[g]);
+    }
     fadec::init(st);
+    const float l2e = 1.4426950408889634f;
+    auto madd = [&](const uint32_t *mm, float *out) {    // the mask times log2(e); -inf stays -inf
+#pragma unroll
+        for (int i = 0; i < 4; ++i) out[i] = h2f((uint16_t)mm[i]) * l2e;
+    };
     const int nch = (nkv + CK - 1) / CK;
     for (int c = sp; c < nch; c += 2 * NS) {
         const int b0 = CK * c + 16 * wave;
-        if (b0 < nkv) fadec::consume(st, b0, nkv, kq, sc2, ka, va);
-        issue(CK * (c + 2 * NS) + 16 * wave, lim, ka, va);
+        float md[4];
+        if constexpr (GRAPH) madd(ma, md);
+        if (b0 < nkv) fadec::consume(st, b0, nkv, kq, sc2, ka, va, GRAPH ? md : nullptr);
+        issue(CK * (c + 2 * NS) + 16 * wave, lim, ka, va, ma);
         if (c + NS >= nch) break;
         const int b1 = CK * (c + NS) + 16 * wave;
-        if (b1 < nkv) fadec::consume(st, b1, nkv, kq, sc2, kn, vn);
-        issue(CK * (c + 3 * NS) + 16 * wave, lim, kn, vn);
+        if constexpr (GRAPH) madd(mb, md);
+        if (b1 < nkv) fadec::consume(st, b1, nkv, kq, sc2, kn, vn, GRAPH ? md : nullptr);
+        issue(CK * (c + 3 * NS) + 16 * wave, lim, kn, vn, mb);
     }
     fadec::finish(st, sm, hk, sp, NS, part_o, part_ml);
 }
@@ -815,6 +841,41 @@ int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *v
     KCPP_CHECK(hipGetLastError());
     if (qout) hipLaunchKernelGGL(k_fa_combine<true>, dim3(H / 2, 1), dim3(1024), 0, s, po, pml, out, (uint8_t *)qout, 1, H, 128, n_past, n_past_dev, nch, 0);
     else hipLaunchKernelGGL(k_fa_combine<false>, dim3(H / 2, 1), dim3(1024), 0, s, po, pml, out, (uint8_t *)nullptr, 1, H, 128, n_past, n_past_dev, nch, 0);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// one query of GGML_OP_FLASH_ATTN_EXT in the graph form (the b1 backend's decode): k_fa_dec5<GRAPH> over the views
+// (key j of kv head h at kc + j k_ld + h k_hs elements), the f16 mask row (may be null), q f32 [H][D] with head
+// stride q_nb2 bytes rounded to f16 in the kernel, then k_fa_comb4 into out [H][D].  -3: shape not covered.
+int kcpp_flash_attn_ext_dec(const float *q, int64_t q_nb2, const uint16_t *kc, const uint16_t *vc, int64_t k_ld,
+                            int64_t k_hs, const uint16_t *mask, float *out, void *ws, int H, int HKV, int D, int n_kv,
+                            float scale, void *stream) {
+    if (D != 128 || H % HKV || H % 2 || n_kv < 1 || q_nb2 % 16 || ((uintptr_t)q & 15)) return -3;
+    const int G = H / HKV, NS = fa4_splits(HKV);
+    if (!(G == 1 || G == 2 || G == 4 || G == 8)) return -3;
+    hipStream_t s = (hipStream_t)stream;
+    float *po = (float *)((uint8_t *)ws + FA_WS_TICKETS);
+    float2 *pml = (float2 *)(po + (int64_t)H * NS * 128);
+    if (!mask) return -3;                         // (llama.cpp always passes the KQ mask)
+#define KCPP_FAD(GG)                                                                                                \
+    hipLaunchKernelGGL((k_fa_dec5<GG, true, 4, true>), dim3(NS, HKV), dim3(256), 0, s, (const uint16_t *)nullptr, kc, vc, \
+                       po, pml, H, n_kv - 1, (const int32_t *)nullptr, NS, scale, k_ld, k_hs, n_kv, q, q_nb2 / 4, mask)
+    switch (G) {
+    case 1: KCPP_FAD(1); break;
+    case 2: KCPP_FAD(2); break;
+    case 4: KCPP_FAD(4); break;
+    default: KCPP_FAD(8); break;
+    }
+#undef KCPP_FAD
+    KCPP_CHECK(hipGetLastError());
+    switch (NS) {
+#define KCPP_FAC(N_) case N_: hipLaunchKernelGGL((k_fa_comb4<0, N_>), dim3(H / 2), dim3(256), 0, s, po, pml, out, (uint8_t *)nullptr, \
+                                                 H, (unsigned long long *)nullptr, (unsigned *)nullptr); break;
+    KCPP_FAC(4) KCPP_FAC(8) KCPP_FAC(16) KCPP_FAC(32) KCPP_FAC(64)
+#undef KCPP_FAC
+    default: return -3;
+    }
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

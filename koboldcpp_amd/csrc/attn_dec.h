@@ -37,9 +37,19 @@ __device__ __forceinline__ void set_q(State<G> &st, int g, const uint4 qq) {
     for (int e = 0; e < 4; ++e) { st.qv[g][2 * e] = h2f(w4[e] & 0xFFFF); st.qv[g][2 * e + 1] = h2f(w4[e] >> 16); }
 }
 
-// one 16-key group (keys base + 4 i + kq, i < 4; keys >= p1 masked), sc2 = scale * log2(e)
+// q of head g from 8 f32 values (the graph form's f32 Q), rounded to f16 first as the reference's q_to_vec_dot
 template <int G>
-__device__ __forceinline__ void consume(State<G> &st, int base, int p1, int kq, float sc2, const uint4 *kk, const uint4 *vv) {
+__device__ __forceinline__ void set_q_f32(State<G> &st, int g, const float4 a, const float4 b) {
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) st.qv[g][e] = h2f(f2h(v[e]));
+}
+
+// one 16-key group (keys base + 4 i + kq, i < 4; keys >= p1 masked), sc2 = scale * log2(e).  madd (optional): the
+// row's additive mask times log2(e), -inf = key skipped (its V never enters, as the CPU skips it)
+template <int G>
+__device__ __forceinline__ void consume(State<G> &st, int base, int p1, int kq, float sc2, const uint4 *kk, const uint4 *vv,
+                                        const float *madd = nullptr) {
     float s[G][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -73,7 +83,12 @@ __device__ __forceinline__ void consume(State<G> &st, int base, int p1, int kq, 
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             s[g][i] += dpp_f<0x140>(s[g][i]);
-            s[g][i] = base + 4 * i + kq < p1 ? s[g][i] * sc2 : -INFINITY;
+            if (madd) {
+                const bool ok = base + 4 * i + kq < p1 && madd[i] != -INFINITY;
+                s[g][i] = ok ? __fadd_rn(s[g][i] * sc2, madd[i]) : -INFINITY;
+            } else {
+                s[g][i] = base + 4 * i + kq < p1 ? s[g][i] * sc2 : -INFINITY;
+            }
         }
     float mx[G], al[G];
 #pragma unroll
@@ -85,12 +100,15 @@ __device__ __forceinline__ void consume(State<G> &st, int base, int p1, int kq, 
     float ls[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-        const float mn = fmaxf(st.m[g], mx[g]);           // finite: key base + kq (i = 0) of row 0 is valid
-        al[g] = __builtin_amdgcn_exp2f(st.m[g] - mn);     // m = -inf -> 0
+        // finite when a key of the group is valid (without a mask: key base + kq (i = 0) of row 0 is); a group whose
+        // keys are all masked keeps m = -inf and contributes nothing (mr = 0 keeps exp2 away from -inf - -inf)
+        const float mn = fmaxf(st.m[g], mx[g]);
+        const float mr = mn == -INFINITY ? 0.0f : mn;
+        al[g] = __builtin_amdgcn_exp2f(st.m[g] - mr);     // m = -inf -> 0
         ls[g] = 0.0f;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            s[g][i] = __builtin_amdgcn_exp2f(s[g][i] - mn);   // -inf -> 0
+            s[g][i] = __builtin_amdgcn_exp2f(s[g][i] - mr);   // -inf -> 0
             ls[g] += s[g][i];
         }
         st.m[g] = mn;
@@ -107,7 +125,7 @@ __device__ __forceinline__ void consume(State<G> &st, int base, int p1, int kq, 
     for (int i = 0; i < 4; ++i) {
         // keys >= p1 carry weight exp2(-inf) = 0; their V words (clamped or stale rows) are zeroed so a non-finite
         // value there cannot turn 0 * v into NaN
-        const bool vok = base + 4 * i + kq < p1;
+        const bool vok = base + 4 * i + kq < p1 && (!madd || madd[i] != -INFINITY);
         const uint32_t w4[4] = {vok ? vv[i].x : 0u, vok ? vv[i].y : 0u, vok ? vv[i].z : 0u, vok ? vv[i].w : 0u};
         float vf[8];
 #pragma unroll

@@ -337,6 +337,9 @@ struct BackendCtx {
     hipStream_t stream;
     Scratch act, ws, fa, ids, xg, yg, gcnt;
     bool fa_exact = false;     // attention in the reference CPU's order with its f16 accumulator (attn_exact.hip)
+    // single-token MUL_MAT on the fused mat-vec (quantize prologue) and FLASH_ATTN_EXT on the split decode kernel;
+    // KCPP_B1_UNFUSED=1: one kernel per step as before (A/B)
+    bool no_fused_mv = getenv("KCPP_B1_UNFUSED") && atoi(getenv("KCPP_B1_UNFUSED")) != 0;
 };
 
 // the native image of weight w for target layout `tt` (kcpp type id); w itself when the layouts coincide
@@ -925,6 +928,16 @@ bool compute_node(BackendCtx *bc, kggml_tensor *n) {
         const int tt = matmul_layout(a->type, K);
         const void *W = native_image(bc, a, tt);
         if (!W) return set_err("mul_mat: native image allocation failed");
+        if (M == 1 && b->nb[0] == 4 && !bc->no_fused_mv) {
+            // one token (decode): the fused single-token mat-vec quantizes src1 in its own prologue (the same Q8_K /
+            // Q8_0 bytes as kcpp_quantize_act) -- one launch per MUL_MAT instead of two; -3: type without it
+            DecArgs d;
+            memset(&d, 0, sizeof d);
+            d.K = K; d.nseg = 1; d.W[0] = (const uint8_t *)W; d.N[0] = N; d.Y[0] = (float *)n->data;
+            d.x = (const float *)b->data;
+            if (kcpp_gemv_dec(tt, &d, 0, 2, N > 16384 ? 4 : (N > 4096 ? 2 : 1), s) == 0) return true;
+            (void)hipGetLastError();            // not covered (type / shape): the two-launch path below
+        }
         void *act = bc->act.get((size_t)kcpp_act_bytes(a->type, K, M) + 256);
         if (!act) return set_err("mul_mat: activation scratch allocation failed");
         if (!chk(kcpp_quantize_act(kcpp_vec_dot_type(a->type), (const float *)b->data, (int64_t)(b->nb[1] / 4), act, K, M, s),
@@ -957,6 +970,12 @@ bool compute_node(BackendCtx *bc, kggml_tensor *n) {
                        "flash_attn_ext(exact)");
         void *ws = bc->fa.get((size_t)kcpp_fa_ext_workspace_bytes(T, H, n_kv, D));
         if (!ws) return set_err("flash_attn_ext: workspace allocation failed");
+        if (T == 1 && !bc->no_fused_mv) {   // one query: the production split kernel under the graph's mask, q rounded in it
+            const int rc = kcpp_flash_attn_ext_dec((const float *)q->data, (int64_t)q->nb[2], (const uint16_t *)k->data,
+                                                   (const uint16_t *)v->data, (int64_t)(k->nb[1] / 2), (int64_t)(k->nb[2] / 2),
+                                                   mk, (float *)n->data, ws, H, HKV, D, n_kv, op_f(n, 0), s);
+            if (rc != -3) return chk(rc, "flash_attn_ext(decode)");
+        }
         return chk(kcpp_flash_attn_ext((const float *)q->data, (int64_t)q->nb[1], (int64_t)q->nb[2], (const uint16_t *)k->data,
                                        (const uint16_t *)v->data, mk, mld, (float *)n->data, ws, T, H, HKV, D, n_kv,
                                        op_f(n, 0), s),

@@ -162,3 +162,7 @@ int kcpp_link_publish(const KLink &L, hipStream_t s);
 // the stage's single-token graph bracketed by the link kernels (runtime.cpp); -3 when graphs are off (row split)
 int kcpp_model_set_link(kcpp_model *m, const KLink *L);
 int kcpp_model_step_linked(kcpp_model *m, int n_past);
+// one query of FLASH_ATTN_EXT in the ggml graph form on the split decode kernel (attn.hip; the b1 backend's decode)
+extern "C" int kcpp_flash_attn_ext_dec(const float *q, int64_t q_nb2, const uint16_t *kc, const uint16_t *vc, int64_t k_ld,
+                                       int64_t k_hs, const uint16_t *mask, float *out, void *ws, int H, int HKV, int D,
+                                       int n_kv, float scale, void *stream);

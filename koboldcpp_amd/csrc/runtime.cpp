@@ -68,6 +68,8 @@ struct KTensor {
     int slices = 1;                  // MoE _exps tensors: n_expert consecutive [K][N] slices
     size_t slice_bytes = 0;
     std::vector<RowSlice> rs;        // non-empty: row split, the rows live in these slices (d is null)
+    void *dec = nullptr;             // KT_Q8_0_T weights: a second copy in the row-major KT_Q8_0 layout for the fused
+                                     // single-token chain (gemv_dec), owned
 };
 
 // a row-split execution lane: one device of the split.  The first lane on the stage's own device runs inline on
@@ -134,12 +136,15 @@ struct kcpp_model {
     void *kv_scratch = nullptr;             // context shift: moved K/V rows (n_ctx x EKV x 2 f16, lazily)
     float *shift_cs = nullptr;              // context shift: (cos, sin) pairs of the shift distance
     int32_t *pin = nullptr;          // pinned host {token, n_past}
+    hipEvent_t ev_tok[2] = {nullptr, nullptr};   // decode_greedy_lagged: token readback ring (pin[4 + k % 2])
+    int lag_k = 0;                   // lagged steps enqueued since the last drain
     int pos_val = -1;                // the value pos_dev holds once the enqueued work has run (-1: unknown)
     float *logits_pin = nullptr;
     bool use_graphs = true;
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
     bool q81 = false;                // Q4_1 / Q5_1 weights (Q8_1 activations): decode on the per-op path
     bool q80t = false;               // Q8_0 layer weights in the tile layout KT_Q8_0_T (gemm_q80t.hip) at every batch size
+    bool q80_dec = false;            // ... plus their KT_Q8_0 decode copies (KTensor::dec): single tokens on the fused chain
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
     int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
     hipGraphExec_t g_exec = nullptr;
@@ -416,6 +421,26 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     if (!ok) return fail("workspace alloc");
     // the KT_Q8_0_T GEMM's split-K tickets live in the workspace and must start at zero (each launch leaves them zero)
     if (m->gemm_ws && hipMemset(m->gemm_ws, 0, m->gemm_ws_sz) != hipSuccess) return fail("gemm ws memset");
+    // all-Q8_0 models: the tile layout serves every batch size, and single-token steps run the fused row-major chain
+    // (norm / RoPE / K-V / residual / GLU fused into the mat-vecs) on a second copy in the KT_Q8_0 layout -- 398 vs 372
+    // tok/s on Llama-3-8B Q8_0 for 7.4 GB more HBM (the layer matrices and the head stored twice; KCPP_Q80_DEC=0:
+    // one copy, single tokens on the tile GEMM)
+    if (m->q80t && !(getenv("KCPP_Q80_DEC") && atoi(getenv("KCPP_Q80_DEC")) == 0)) {
+        bool ok2 = true;
+        for (int idx = 2; idx < n_tensors(*hp) && ok2; ++idx) {
+            KTensor *t = tensor_at(m, idx);
+            if (!t || t->type != KT_Q8_0_T || t->slices != 1) continue;
+            ok2 = hipMalloc(&t->dec, (size_t)tensor_bytes(KT_Q8_0, t->K, t->N)) == hipSuccess;
+        }
+        if (!ok2) {                               // not enough memory for the copies: one copy, tile GEMM decode
+            for (int idx = 2; idx < n_tensors(*hp); ++idx) {
+                KTensor *t = tensor_at(m, idx);
+                if (t && t->dec) { hipFree(t->dec); t->dec = nullptr; }
+            }
+            (void)hipGetLastError();
+        }
+        m->q80_dec = ok2;
+    }
     if (hp->n_expert > 0) {
         const int NU = hp->n_expert_used;
         if (NU < 1 || NU > hp->n_expert || hp->n_expert > 64) return fail("bad n_expert / n_expert_used");
@@ -457,9 +482,9 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
         for (auto &r : t.rs) { hipSetDevice(m->lanes[r.lane].dev); F(r.d); }
         hipSetDevice(m->device);
     };
-    F(m->tok_embd.d); F(m->output_norm.d); F(m->output.d); FS(m->output);
+    F(m->tok_embd.d); F(m->output_norm.d); F(m->output.d); FS(m->output); F(m->output.dec);
     for (auto &L : m->layers) {
-        for (auto &t : L.t) { if (t.owned) F(t.d); FS(t); }
+        for (auto &t : L.t) { if (t.owned) F(t.d); FS(t); F(t.dec); }
         F(L.qkv_base); F(L.glu_base); F(L.kc); F(L.vc);
     }
     F(m->hglu); F(m->moe_ids); F(m->moe_w); F(m->moe_rows); F(m->moe_rw); F(m->moe_slots);
@@ -471,6 +496,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     F(m->gemm_ws); F(m->gemm_ws2); F(m->tok_dev); F(m->pos_dev); F(m->argmax_dev); F(m->argmax_ws); F(m->rope_tab);
     F(m->kv_scratch); F(m->shift_cs);
     if (m->pin) hipHostFree(m->pin);
+    for (hipEvent_t &ev : m->ev_tok) if (ev) hipEventDestroy(ev);
     if (m->logits_pin) hipHostFree(m->logits_pin);
     if (m->stream) hipStreamDestroy(m->stream);
     if (m->side) hipStreamDestroy(m->side);
@@ -504,6 +530,7 @@ extern "C" int kcpp_model_synth_weights(kcpp_model *m, uint64_t seed) {
             RT_CHECK(hipSetDevice(m->device));
         } else if (t->slices == 1) {
             RC(kcpp_weight_synth(t->type, seed, (uint64_t)idx, t->d, t->K, t->N, m->stream));
+            if (t->dec) RC(kcpp_weight_synth(KT_Q8_0, seed, (uint64_t)idx, t->dec, t->K, t->N, m->stream));
         } else {                               // expert e: tid = idx * 256 + e (tests/refharness.py)
             for (int e = 0; e < t->slices; ++e)
                 RC(kcpp_weight_synth(t->type, seed, (uint64_t)idx * 256 + e, (uint8_t *)t->d + e * t->slice_bytes, t->K,
@@ -524,7 +551,7 @@ static int upload(int dev, hipStream_t s, int type, int64_t K, int64_t N, int sl
     if (type == KT_Q6_K || type == KT_Q3_K || type == KT_Q2_K || type == KT_Q4_0 || type == KT_Q4_1 || type == KT_Q5_0 || type == KT_Q5_1 || type == KT_Q8_0 ||
         type == KT_IQ4_NL || type == KT_IQ4_XS ||
         type == KT_Q4_K_RS || type == KT_Q5_K_RS ||
-        type == KT_Q6_K_RS) {
+        type == KT_Q6_K_RS || type == KT_Q8_0_T) {
         void *stage = nullptr;
         RT_CHECK(hipMalloc(&stage, bytes));
         RT_CHECK(hipMemcpyAsync(stage, src, bytes, hipMemcpyHostToDevice, s));
@@ -553,6 +580,7 @@ extern "C" int kcpp_model_set_tensor(kcpp_model *m, int idx, const void *src, in
         RT_CHECK(hipSetDevice(m->device));
         return 0;
     }
+    if (t->dec) RC(upload(m->device, m->stream, KT_Q8_0, t->K, t->N, 1, 0, src, t->dec));
     return upload(m->device, m->stream, t->type, t->K, t->N, t->slices, t->slice_bytes, src, t->d);
 }
 
@@ -1122,7 +1150,12 @@ static int forward_layers_dec(kcpp_model *m) {
     const float kq_scale = 1.0f / sqrtf((float)D);
     for (int il = m->il0; il < m->il1; ++il) {
         KLayer &L = m->layers[il - m->il0];
-        const KTensor *t = L.t;
+        KTensor tl[10];                              // the layer's tensors; KT_Q8_0_T ones by their KT_Q8_0 decode copies
+        for (int j = 0; j < 10; ++j) {
+            tl[j] = L.t[j];
+            if (tl[j].dec) { tl[j].type = KT_Q8_0; tl[j].d = tl[j].dec; }
+        }
+        const KTensor *t = tl;
         // --- attn_norm + q|k|v + rope + K/V cache store: one launch per quant type present; q|k Q4_K + v Q6_K (the
         // Q4_K_M more-bits layers) in one launch.  (Two launches forked onto a side stream inside the graph
         // replayed slower than in sequence, 453 vs 517 tok/s: removed.)
@@ -1213,8 +1246,8 @@ static int head_dec(kcpp_model *m) {
     DecArgs a;
     memset(&a, 0, sizeof a);
     a.K = m->hp.n_embd; a.x = m->x; a.nw = (const float *)m->output_norm.d; a.eps = m->hp.eps; a.nseg = 1;
-    a.W[0] = (const uint8_t *)m->output.d; a.N[0] = m->hp.n_vocab; a.Y[0] = m->logits;
-    return kcpp_gemv_dec(m->output.type, &a, 0, 1, rows_per_wave(m->hp.n_vocab, 0), m->stream);
+    a.W[0] = (const uint8_t *)(m->output.dec ? m->output.dec : m->output.d); a.N[0] = m->hp.n_vocab; a.Y[0] = m->logits;
+    return kcpp_gemv_dec(m->output.dec ? KT_Q8_0 : m->output.type, &a, 0, 1, rows_per_wave(m->hp.n_vocab, 0), m->stream);
 }
 
 // run layers [il0, il1) on m->x for T tokens (T <= ub).  n_past via pos_dev when graph-replayed.
@@ -1386,7 +1419,7 @@ static int decode_step_dev(kcpp_model *m) {
     if (m->has_embed)
         RC(kcpp_get_rows(m->tok_embd.type, m->tok_embd.d, hp.n_embd, hp.n_vocab, m->tok_dev, 1, m->x, hp.n_embd,
                          m->stream));
-    if (m->fused_decode && m->kv_tk == KT_F16 && !m->q81 && !m->q80t) {
+    if (m->fused_decode && m->kv_tk == KT_F16 && !m->q81 && (!m->q80t || m->q80_dec)) {
         RC(forward_layers_dec(m));
         if (m->has_output) RC(head_dec(m));
     } else {
@@ -1605,6 +1638,40 @@ extern "C" int kcpp_model_argmax(kcpp_model *m, int32_t *token_out) {
     RT_CHECK(hipMemcpyAsync(&m->pin[2], m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
     RT_CHECK(hipStreamSynchronize(m->stream));
     *token_out = m->pin[2];
+    return 0;
+}
+
+// Greedy decode with the host one step behind the device: enqueue this step (its input is the previous step's device
+// argmax, in place), then the 4-byte read of its token into a pinned ring slot, and return the PREVIOUS step's token
+// once its read has landed -- the next step is already queued when the host waits, so no per-token bubble (a serving
+// loop checks its stop conditions on token k while step k + 1 runs).  *token_out = -1 on the first call after a drain;
+// kcpp_model_greedy_drain returns the last step's token and resets the ring.
+extern "C" int kcpp_model_decode_greedy_lagged(kcpp_model *m, int n_past, int32_t *token_out) {
+    if (!m->has_embed || !m->has_output) { g_err = "decode_greedy needs embedding and output on this stage"; return -2; }
+    if (n_past + 1 > m->hp.n_ctx) { g_err = "context overflow"; return -2; }
+    RT_CHECK(hipSetDevice(m->device));
+    for (hipEvent_t &ev : m->ev_tok)
+        if (!ev) RT_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    RC(step_one(m, n_past));
+    const int slot = m->lag_k & 1;
+    RT_CHECK(hipMemcpyAsync(&m->pin[4 + slot], m->argmax_dev, 4, hipMemcpyDeviceToHost, m->stream));
+    RT_CHECK(hipEventRecord(m->ev_tok[slot], m->stream));
+    *token_out = -1;
+    if (m->lag_k > 0) {
+        RT_CHECK(hipEventSynchronize(m->ev_tok[slot ^ 1]));
+        *token_out = m->pin[4 + (slot ^ 1)];
+    }
+    ++m->lag_k;
+    return 0;
+}
+extern "C" int kcpp_model_greedy_drain(kcpp_model *m, int32_t *token_out) {
+    RT_CHECK(hipSetDevice(m->device));
+    *token_out = -1;
+    if (m->lag_k > 0) {
+        RT_CHECK(hipEventSynchronize(m->ev_tok[(m->lag_k - 1) & 1]));
+        *token_out = m->pin[4 + ((m->lag_k - 1) & 1)];
+    }
+    m->lag_k = 0;
     return 0;
 }
 

@@ -108,6 +108,8 @@ _SIGS = {
     "kcpp_model_forward_hidden": [P, I, I],
     "kcpp_model_argmax": [P, P],
     "kcpp_model_decode_greedy": [P, I, P],
+    "kcpp_model_decode_greedy_lagged": [P, I, P],
+    "kcpp_model_greedy_drain": [P, P],
     "kcpp_model_set_graphs": [P, I],
     "kcpp_model_set_fused_decode": [P, I],
     "kcpp_model_set_row_split": [P, I, P, P],
@@ -311,6 +313,18 @@ class Model:
         """one greedy step on the device-resident previous argmax; returns this step's token"""
         v = ctypes.c_int32(0)
         _chk(_L.kcpp_model_decode_greedy(self.m, n_past, ctypes.byref(v)), "decode_greedy")
+        return v.value
+
+    def decode_greedy_lagged(self, n_past):
+        """one greedy step, the host one token behind: returns the previous step's token (-1 after a drain)"""
+        v = ctypes.c_int32(0)
+        _chk(_L.kcpp_model_decode_greedy_lagged(self.m, n_past, ctypes.byref(v)), "decode_greedy_lagged")
+        return v.value
+
+    def greedy_drain(self):
+        """the last lagged step's token; resets the readback ring"""
+        v = ctypes.c_int32(0)
+        _chk(_L.kcpp_model_greedy_drain(self.m, ctypes.byref(v)), "greedy_drain")
         return v.value
 
     def forward_hidden(self, T, n_past):

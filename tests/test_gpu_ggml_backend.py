@@ -227,14 +227,20 @@ def test_get_rows_vs_reference_cpu(env, t):
     assert np.array_equal(ours.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("exact", [True, False], ids=["fa_exact", "production"])
-def test_llama_layer_vs_reference_cpu(env, exact):
+@pytest.mark.parametrize("exact,n_past,T,n_ctx,pad", [(True, 37, 5, 64, 0), (False, 37, 5, 64, 0), (False, 37, 1, 64, 0),
+                                                     (True, 37, 1, 64, 0), (False, 700, 1, 1024, 256),
+                                                     (True, 700, 1, 1024, 256)],
+                         ids=["fa_exact", "production", "decode", "decode_exact", "decode_ctx700_pad256",
+                              "decode_ctx700_exact"])
+def test_llama_layer_vs_reference_cpu(env, exact, n_past, T, n_ctx, pad):
     """one build_llama layer (src/llama.cpp:10453-10620) at n_embd 1024, 8/2 heads x 128, n_ff 2816, Q4_K_M-like
-    weights, 5 new tokens after 37 cached positions"""
+    weights, 5 new tokens after 37 cached positions; and single tokens (decode: MUL_MAT on the fused mat-vec with its
+    quantize prologue, FLASH_ATTN_EXT on the split decode kernel under the graph's mask), also with the KV view padded
+    to 256 cells as llama_kv_cache does for flash attention (masked cells past n_past hold NaN, never read into V)"""
     G, L, be = env
-    E, H, HKV, D, Fd, n_ctx, n_past, T = 1024, 8, 2, 128, 2816, 64, 37, 5
+    E, H, HKV, D, Fd = 1024, 8, 2, 128, 2816
     EKV = HKV * D
-    n_kv = n_past + T
+    n_kv = n_past + T if not pad else (n_past + T + pad - 1) // pad * pad
     rng = np.random.default_rng(11)
     tys = [R.Q4_K, R.Q4_K, R.Q6_K, R.Q4_K, R.Q4_K, R.Q4_K, R.Q6_K]
     shapes = [(E, E), (E, EKV), (E, EKV), (E, E), (E, Fd), (E, Fd), (Fd, E)]
@@ -244,6 +250,9 @@ def test_llama_layer_vs_reference_cpu(env, exact):
     x = rng.standard_normal((T, E)).astype(np.float32)
     kc = (rng.standard_normal((n_ctx, EKV)) * 0.5).astype(np.float16)
     vc = rng.standard_normal((n_ctx, EKV)).astype(np.float16)
+    if pad:
+        kc[n_past + T:] = np.nan
+        vc[n_past + T:] = np.nan
     pos = np.arange(n_past, n_past + T, dtype=np.int32)
     T_pad = 32
     mask = np.full((T_pad, n_kv), -np.inf, np.float16)
@@ -314,7 +323,10 @@ def test_llama_layer_vs_reference_cpu(env, exact):
     e = rel(outs[0], outs[1])
     med = float(np.median(np.abs(outs[0] - outs[1])) / np.abs(outs[1]).max())
     print("layer exact=%d rel err max %.3g median %.3g" % (exact, e, med))
-    assert e <= (LAYER_EXACT if exact else LAYER_PROD), e
+    # (the strict-order attention matches a layer to 2e-5 over tens of keys; over 700 keys its result drifts to 4e-3 of
+    # the reference's -- measured the same with and without this round's single-token paths -- so that case only
+    # proves the masked NaN cells stay out; the strict mode is pinned end to end at 3840 keys by test_gpu_deep.py)
+    assert e <= (LAYER_EXACT if exact and n_past < 100 else LAYER_PROD), e
 
 
 def test_unsupported_ops_are_refused(env):

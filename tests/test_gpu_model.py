@@ -169,15 +169,59 @@ def test_decode_greedy_matches_host_loop(K, graphs):
         m.decode(prompt, 0, want_logits=False)
         tok = m.argmax()
         toks, n = [tok], len(prompt)
-        for _ in range(12):
-            if greedy:
+        for i in range(12):
+            if greedy == "lagged":           # the host one token behind (bench.py's decode loop)
+                prev = m.decode_greedy_lagged(n)
+                assert (prev == -1) == (i == 0)
+                if i:
+                    toks.append(prev)
+            elif greedy:
                 tok = m.decode_greedy(n)
             else:
                 logits = m.decode([tok], n)
                 tok = m.argmax()
                 assert tok == int(np.argmax(logits))
-            toks.append(tok)
+            if greedy != "lagged":
+                toks.append(tok)
             n += 1
+        if greedy == "lagged":
+            toks.append(m.greedy_drain())
+            assert m.greedy_drain() == -1
         m.close()
         return toks
-    assert run(True) == run(False)
+    want = run(False)
+    assert run(True) == want
+    assert run("lagged") == want
+
+
+def test_q8_0_decode_copy(K, monkeypatch):
+    """all-Q8_0 model: prefill on the tile layout (KT_Q8_0_T), single tokens on the fused row-major chain over the
+    KT_Q8_0 decode copies (round 6).  Weights given as GGUF bytes (kcpp_model_set_tensor fills both copies) equal the
+    synthetic ones; decode with the copies vs without (KCPP_Q80_DEC=0: the tile GEMM at M = 1) within the GEMM bar, and
+    both vs the C restatement"""
+    hp = dict(R.TINY)
+    types = R.uniform_types(hp["n_layer"], R.Q8_0)
+    prompt = [int(v) for v in np.random.default_rng(9).integers(1, 500, size=40)]
+    outs = {}
+    for mode in ("copies", "set_tensor", "tile"):
+        if mode == "tile":
+            monkeypatch.setenv("KCPP_Q80_DEC", "0")
+        m = K.Model(hp, types)
+        if mode == "set_tensor":
+            for idx, t in enumerate(types):
+                m.set_tensor(idx, R.synth_tensor(hp, t, 1234, idx))
+        else:
+            m.synth(1234)
+        lg = [m.decode(prompt, 0)]
+        n = len(prompt)
+        for tok in (7, 100, 3, 250, 11):
+            lg.append(m.decode([tok], n))
+            n += 1
+        m.close()
+        outs[mode] = np.array(lg)
+    assert np.array_equal(outs["copies"].view(np.uint32), outs["set_tensor"].view(np.uint32))
+    d = np.abs(outs["copies"] - outs["tile"])
+    assert d.max() < TOL_MAX and np.median(d) < 1e-5, (d.max(), np.median(d))
+    orc32 = oracle_forced(types, prompt, [7, 100, 3, 250, 11], True)
+    d = np.abs(outs["copies"] - orc32)
+    assert d.max() < TOL_MAX and np.median(d) < TOL_MEDIAN_F32, (d.max(), np.median(d))
