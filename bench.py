@@ -32,6 +32,7 @@ MIXTRAL_8X7B = dict(n_vocab=32000, n_embd=4096, n_head=32, n_head_kv=8, n_layer=
                     eps=1e-5, rope_base=1000000.0, n_expert=8, n_expert_used=2)
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md chip table (spec)
 MFMA_F16_PEAK_TFLOPS = 2500.0   # dense f16 MFMA peak (spec, no sparsity)
+MFMA_I8_PEAK_TOPS = 5000.0      # dense i8 MFMA peak: 2x the f16 rate per clock (MI355X_MICROARCH.md, Matrix cores: I8 row)
 
 
 def q4_k_m_types(n_layer):
@@ -476,8 +477,13 @@ def bench_line(args, K, torch, hp, types, r, n_dev, par):
         "roofline": roof,
         "prefill_roofline": {"bound": "mfma", "achieved": round(pre_tflops, 1), "peak": MFMA_F16_PEAK_TFLOPS * n_dev,
                              "unit": "TFLOP/s", "frac": round(pre_tflops / MFMA_F16_PEAK_TFLOPS / n_dev, 4),
+                             # the Q4_K / Q5_K GEMMs run v_mfma_i32_32x32x32_i8 (2x the f16 rate per clock,
+                             # MI355X_MICROARCH.md: Matrix cores), so against that peak the same work is half the fraction
+                             "peak_i8": MFMA_I8_PEAK_TOPS * n_dev,
+                             "frac_i8": round(pre_tflops / MFMA_I8_PEAK_TOPS / n_dev, 4),
                              "flops": int(pre_flops), "scope": "whole prefill (all kernels), F(n) of SURVEY.md 8d; "
-                                                               "peak = %d GPU(s)" % n_dev},
+                                                               "peak = %d GPU(s); frac vs the dense f16 peak, frac_i8 "
+                                                               "vs the dense i8 peak" % n_dev},
     }
     if n_dev == 1 and not args.no_generate_path:
         try:
