@@ -249,8 +249,10 @@ kggml_backend_reg_t ggml_backend_cuda_reg(void);
 kggml_backend_t ggml_backend_cuda_init(int device);
 bool ggml_backend_is_cuda(kggml_backend_t backend);
 kggml_backend_buffer_type_t ggml_backend_cuda_buffer_type(int device);
-/* row split across devices (ggml-cuda.cu:659-955): not provided -- returns NULL, and the device supports_buft
- * refuses foreign types, so llama.cpp's LLAMA_SPLIT_MODE_ROW is unavailable with this backend */
+/* row split across devices (ggml-cuda.cu:625-955, LLAMA_SPLIT_MODE_ROW): one buffer type per tensor_split (all
+ * zero or NULL = an even split); each weight's rows are spread over the devices, already in the device layout of
+ * its type, and a MUL_MAT on it runs on the main device with every other device multiplying its own rows
+ * (ggml_backend.cpp, "split buffers").  NULL only when no device is present. */
 kggml_backend_buffer_type_t ggml_backend_cuda_split_buffer_type(const float *tensor_split);
 kggml_backend_buffer_type_t ggml_backend_cuda_host_buffer_type(void);
 int ggml_backend_cuda_get_device_count(void);
