@@ -56,6 +56,13 @@ int kcpp_gemv(int type, const void *W, const void *W2, int64_t K, int64_t N, con
 int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M);
 int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
               int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream);
+/* Q6_K prefill image (same MUL_MAT role as kcpp_gemm on KT_Q6_K_RS, int8 matrix cores): the exact weight integers
+ * sc*(q-32) of a Q6_K_RS matrix as two int8 planes, N*K*2 bytes (0 = shape not covered: N % 128, K % 256).
+ * kcpp_gemm_q6p gives kcpp_gemm(KT_Q6_K_RS, ...)'s results bit for bit (M > 32; ws of kcpp_gemm_workspace_bytes). */
+int64_t kcpp_q6p_image_bytes(int64_t K, int64_t N);
+int kcpp_q6p_build(const void *W, int64_t K, int64_t N, void *img, void *stream);
+int kcpp_gemm_q6p(const void *img, const void *W, const void *img2, const void *W2, int64_t K, int64_t N, const void *act,
+                  int64_t M, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream);
 /* Grouped expert GEMM for MoE prefill (replaces ggml_cuda_mul_mat_id's per-expert loop, ggml-cuda.cu:2003-2139):
  * ng groups of cnt_host[e] rows (act: Q8_K of all M rows, grouped back to back; cnt_dev the same counts on the
  * device), group e against W + e*wstride (and W2 + e*wstride); mode 0 plain, 1 silu(g)*u with up [M][N] scratch.

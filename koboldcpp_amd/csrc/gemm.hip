@@ -1906,6 +1906,183 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
         }
 }
 
+// ================================================================ Q6_K GEMM on int8 matrix cores (prefill image)
+// q6v3 spends two f16 MFMAs per 16 k (sc*(q-32) needs 13 bits) plus the dequantization VALU of every fragment.  The
+// prefill image keeps each weight's exact integer v = sc*(q-32) in [-4096, 4064] as two int8 planes,
+//   v = 64 A + C,  A = floor((v + 32) / 64) in [-64, 64],  C = v - 64 A in [-32, 31],
+// so one super-block row is 2 x 256 bytes and the sub-block scales are already inside: per 32 k two
+// v_mfma_i32_32x32x32_i8 (int32 accumulators acc_A, acc_C) and no dequantization at all; isum = 64 acc_A + acc_C is
+// the CPU's int32 sumi of the super-block (ggml_vec_dot_q6_K_q8_K, ggml-quants.c:8919) exactly, and the epilogue is
+// q6v3's (tot = fma(dy, d * isum, tot)), so the results are q6v3's bit for bit wherever q6v3's fp32 accumulator holds
+// its integer exactly (|sumi| < 2^24), and the CPU's exact integer always.
+// Image: per 32-row tile rt and super-block sb, 16 blocks of 1 KiB (k-block kb = 0..7, plane p = 0 (A) / 1 (C)) at
+// ((rt nsb + sb) 16 + 2 kb + p) KiB; lane l of a block = row 32 rt + (l & 31), k = 256 sb + 32 kb + 16 (l >> 5) + e,
+// e = 0..15 -- exactly one v_mfma B operand, one contiguous 1 KiB wave load.  The row scale d stays in the Q6_K_RS
+// weights (read beside the image).  Prefill only: decode keeps the 0.82 B / weight RS layout.
+__device__ __forceinline__ int64_t q6p_off(int64_t n, int64_t k, int64_t nsb, int p) {
+    const int64_t rt = n >> 5, sb = k >> 8;
+    const int kk = (int)(k & 255), kb = kk >> 5, kg = (kk >> 4) & 1, e = kk & 15;
+    return ((rt * nsb + sb) * 16 + 2 * kb + p) * 1024 + 16 * ((int)(n & 31) + 32 * kg) + e;
+}
+
+// one thread = (row n, super-block sb, RS unit u, byte j): the four elements g = 0..3 of that byte position
+// (q6v3's unit decoding: k = 128 h + 16 lh + 32 g + j, sub-block 8 h + lh + 2 g, scale byte 4 u + g)
+__global__ void k_q6p_build(const uint8_t *__restrict__ W, int64_t K, int64_t N, int64_t Np, uint8_t *__restrict__ img) {
+    const int64_t nsb = K / 256;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Np * nsb * 64) return;
+    const int j = (int)(i & 15), u = (int)((i >> 4) & 3);
+    const int64_t sb = (i >> 6) % nsb, n = (i >> 6) / nsb;
+    const int h = u >> 1, lh = u & 1;
+    int8_t A[4], C[4];
+    if (n < N) {
+        const uint8_t *row = W + n * 210 * nsb;
+        const int64_t U = 4 * sb + u;
+        const uint8_t lo = row[16 * U + j], hi = row[64 * nsb + 16 * U + j], qh = row[128 * nsb + 16 * U + j];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int ql = ((g & 1) ? hi : lo) >> (4 * (g >> 1)) & 0xF;
+            const int q = ql | (((qh >> (2 * g)) & 3) << 4);
+            const int sc = (int8_t)row[192 * nsb + 4 * U + g];
+            const int v = sc * (q - 32);
+            const int a = (v + 32) >> 6;            // arithmetic shift: floor
+            A[g] = (int8_t)a;
+            C[g] = (int8_t)(v - 64 * a);
+        }
+    } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) A[g] = C[g] = 0;
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const int64_t k = 256 * sb + 128 * h + 16 * lh + 32 * g + j;
+        img[q6p_off(n, k, nsb, 0)] = (uint8_t)A[g];
+        img[q6p_off(n, k, nsb, 1)] = (uint8_t)C[g];
+    }
+}
+
+struct Q6pSmem {
+    i32x4 a[2][4][568];      // [buf][token tile][swz(row, chunk)]: 16 activation bytes, chunks 0..15 of the 256
+    float dy[2][128];        // [buf][token]: Q8_K scale of the super-block
+};
+
+// grid: MT * (N / 128) * KS workgroups (KS copies of the tile grid along K, as q6v3), 256 threads, one workgroup per
+// CU.  Workgroup = 128 tokens x 128 weight rows; wave w owns rows [32 w, +32) against all four 32-token tiles (every
+// B fragment feeds four MFMAs).  B fragments go global -> registers one super-block ahead (two register sets, the
+// loop unrolled by two so no set is copied while its loads are in flight); A (Q8_K bytes) and dy by LDS-DMA, double
+// buffered, in q4v4's swizzled image.  XG = token tiles per XCD group (xcd_tile): MT keeps a row tile's four token
+// tiles on one XCD, so its image comes from HBM once and from that XCD's L2 three times.
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6p(const i32x4 *__restrict__ img, const uint8_t *__restrict__ Wrs,
+                                                    int64_t K, int64_t N, const uint8_t *__restrict__ act, int64_t M,
+                                                    int64_t Mp, int MT, float *__restrict__ Y, int64_t ldy,
+                                                    const float *res, int64_t ldr, int KS, float *__restrict__ part,
+                                                    int XG) {
+    constexpr int TPW = 16 / NW;                     // token tiles per wave: 4 (4 waves) or 2 (8 waves)
+    __shared__ Q6pSmem S;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int lr = lane & 31, kg = lane >> 5;
+    const int64_t nsb = K / 256;
+    const int8_t *qs = (const int8_t *)act;
+    const float *dq = (const float *)(act + M * K);
+    const int64_t ntn = N / 128, nwg = (int64_t)gridDim.x / KS;
+    const int64_t id = blockIdx.x % nwg;
+    const int split = (int)(blockIdx.x / nwg);
+    int64_t mt, nt;
+    xcd_tile(id, nwg, MT, ntn, XG, mt, nt);
+    // wave w: rows [32 (w & 3), +32) of the tile against token tiles TPW (w >> 2) .. + TPW
+    const int wr = wave & 3, jt0 = TPW * (wave >> 2);
+    const int64_t m0 = mt * 128, rt = nt * 4 + wr;
+    // A: token tile (wave & 3), chunk halves h (all, or wave >> 2 with 8 waves), row groups 0..3; lane: row
+    // 8k + (lane & 7), chunk 8h + (lane >> 3).  dy: waves 0, 1 (tokens 64 wave + lane)
+    const int att = wave & 3;
+    const int64_t arow0 = m0 + 32 * att + (lane & 7);
+    const int8_t *arow = qs + min(arow0, M - 1) * K + 16 * (lane >> 3);
+    const float *dyrow = dq + min(m0 + 64 * min(wave, 1) + lane, M - 1) * nsb;
+    auto stage_a = [&](int buf, int64_t sb) {
+#pragma unroll
+        for (int hh = 0; hh < 8 / NW; ++hh) {
+            const int h = NW == 8 ? (wave >> 2) : hh;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                dma16(arow + (int64_t)min(8 * k, (int)max<int64_t>(M - 1 - arow0, 0)) * K + 128 * h + sb * 256,
+                      &S.a[buf][att][72 * (4 * h + k)]);
+        }
+        if (wave < 2) dma4(dyrow + sb, &S.dy[buf][64 * wave]);
+    };
+    const i32x4 *wsrc = img + rt * nsb * 16 * 64 + lane;
+    const uint16_t *pd = (const uint16_t *)(Wrs + (32 * rt + lr) * 210 * nsb + 208 * nsb);
+
+    const int64_t sbb = nsb * split / KS, sbe = nsb * (split + 1) / KS;
+    f16acc tot[TPW];
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tot[j][i] = 0.0f;
+
+    // one register set: fragment pair kb of super-block sb + 1 is loaded into the registers of pair kb of sb right
+    // after their last MFMA, so every load has one super-block of MFMAs to land in
+    i32x4 b[16];
+    stage_a(0, sbb);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) b[q] = wsrc[(sbb * 16 + q) * 64];
+    uint16_t d = pd[sbb];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int64_t sb = sbb; sb < sbe; ++sb) {
+        const int buf = (int)((sb - sbb) & 1);
+        const bool nx = sb + 1 < sbe;
+        if (nx) stage_a(buf ^ 1, sb + 1);
+        const float dw = h2f(d);
+        if (nx) d = pd[sb + 1];
+        // k-block outer, token tile inner: eight independent accumulators, one A fragment live at a time
+        i32x16 aa[TPW], ac[TPW];
+#pragma unroll
+        for (int j = 0; j < TPW; ++j)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) aa[j][i] = ac[j][i] = 0;
+#pragma unroll
+        for (int kb = 0; kb < 8; ++kb) {
+#pragma unroll
+            for (int j = 0; j < TPW; ++j) {
+                const i32x4 a = S.a[buf][jt0 + j][swz(lr, 2 * kb + kg)];
+                aa[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b[2 * kb], aa[j], 0, 0, 0);
+                ac[j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b[2 * kb + 1], ac[j], 0, 0, 0);
+            }
+            if (nx) {
+                b[2 * kb] = wsrc[((sb + 1) * 16 + 2 * kb) * 64];
+                b[2 * kb + 1] = wsrc[((sb + 1) * 16 + 2 * kb + 1) * 64];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < TPW; ++j) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const float4 v = *(const float4 *)&S.dy[buf][32 * (jt0 + j) + 8 * q + 4 * kg];
+                const float dv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int r = 4 * q + e;
+                    tot[j][r] = fmaf(dv[e], __fmul_rn(dw, (float)(aa[j][r] * 64 + ac[j][r])), tot[j][r]);
+                }
+            }
+        }
+        // A (sb + 1) landed (the d and 16 B loads issued after it may stay in flight); everyone is done with buf
+        if (nx) asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+        __syncthreads();
+    }
+    const int64_t n = 32 * rt + lr;
+#pragma unroll
+    for (int j = 0; j < TPW; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int64_t t = m0 + 32 * (jt0 + j) + (r & 3) + 8 * (r >> 2) + 4 * kg;
+            if (KS > 1) part[((int64_t)split * Mp + t) * N + n] = tot[j][r];
+            else if (t < M) Y[t * ldy + n] = res ? __fadd_rn(tot[j][r], res[t * ldr + n]) : tot[j][r];
+        }
+}
+
 static int g_gemm_variant = -1;
 static int gemm_variant() {
     if (g_gemm_variant < 0) g_gemm_variant = 0;
@@ -1970,6 +2147,65 @@ int kcpp_gemm_q80_segs(const void *const *W, const int64_t *N, int nseg, int64_t
     KCPP_CHECK(hipGetLastError());
     hipLaunchKernelGGL(k_q80s_reduce, dim3((unsigned)((M * Ntot + 255) / 256)), dim3(256), 0, s, part, nullptr, S, M, Ntot, Y, ldy,
                        nullptr, 0);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// Q6_K prefill image (k_q6p_build / k_gemm_q6p): N % 128 == 0, K % 256 == 0
+int64_t kcpp_q6p_image_bytes(int64_t K, int64_t N) {
+    if (K <= 0 || N <= 0 || K % 256 || N % 128) return 0;
+    return N * K * 2;
+}
+
+int kcpp_q6p_build(const void *W, int64_t K, int64_t N, void *img, void *stream) {
+    if (!W || !img || !kcpp_q6p_image_bytes(K, N)) return -1;
+    const int64_t nth = N * (K / 256) * 64;
+    hipLaunchKernelGGL(k_q6p_build, dim3((unsigned)((nth + 255) / 256)), dim3(256), 0, (hipStream_t)stream, (const uint8_t *)W,
+                       K, N, N, (uint8_t *)img);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// kcpp_gemm(KT_Q6_K_RS, ...) with the prefill image(s) beside the RS weights: the same results bit for bit (same
+// K split rule, same epilogue order), int8 matrix cores.  M > 32; mode 0 (res optional) or 1 (silu(g) * u, W2 / img2);
+// ws from kcpp_gemm_workspace_bytes(KT_Q6_K_RS, K, N, M).  Returns -3 for shapes the image does not cover.
+int kcpp_gemm_q6p(const void *img, const void *W, const void *img2, const void *W2, int64_t K, int64_t N, const void *act,
+                  int64_t M, float *Y, int64_t ldy, const float *res, int64_t ldr, int mode, void *ws, void *stream) {
+    if (!img || !W || !act || !Y || !ws || M < 1 || (mode == 1 && (!img2 || !W2)) || mode < 0 || mode > 1) return -1;
+    if (!kcpp_q6p_image_bytes(K, N)) return -3;
+    hipStream_t s = (hipStream_t)stream;
+    int64_t o_a16, o_dy, o_bs, o_up;
+    ws_layout(KT_Q6_K_RS, K, N, M, o_a16, o_dy, o_bs, o_up);
+    uint8_t *w8 = (uint8_t *)ws;
+    float *up = (float *)(w8 + o_up);
+    float *part = (float *)(w8 + o_up + ((M * N * 4 + 255) & ~255LL));
+    const int64_t Mp = (M + 127) / 128 * 128, nsb = K / 256, nt = N / 128;
+    const int MT = (int)(Mp / 128);
+    // q6v3's split rule (kcpp_gemm, variant 0), so the f32 summation order -- and every bit -- is the same
+    const bool big = Mp / 128 * nt >= 384;
+    const int KS = (mode == 0 && nsb % 2 == 0 && !big && (nt < 16 || nsb >= 32)) ? 2 : 1;
+    const int XG = 8 % MT == 0 ? MT : 1;
+    static const int NWq = [] { const char *e = getenv("KCPP_Q6P_NW"); return e && atoi(e) == 4 ? 4 : 8; }();
+    const unsigned nwg = (unsigned)(MT * nt * KS);
+    auto launch = [&](const void *im, const void *w, float *y, int64_t ly, const float *r, int64_t lr) -> int {
+        if (NWq == 8)
+            hipLaunchKernelGGL(k_gemm_q6p<8>, dim3(nwg), dim3(512), 0, s, (const i32x4 *)im, (const uint8_t *)w, K, N,
+                               (const uint8_t *)act, M, Mp, MT, y, ly, r, lr, KS, part, XG);
+        else
+            hipLaunchKernelGGL(k_gemm_q6p<4>, dim3(nwg), dim3(256), 0, s, (const i32x4 *)im, (const uint8_t *)w, K, N,
+                               (const uint8_t *)act, M, Mp, MT, y, ly, r, lr, KS, part, XG);
+        KCPP_CHECK(hipGetLastError());
+        if (KS > 1) {
+            hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,
+                               ly, r, lr);
+            KCPP_CHECK(hipGetLastError());
+        }
+        return 0;
+    };
+    int rc = launch(img, W, Y, ldy, mode == 1 ? nullptr : res, ldr);
+    if (rc || mode != 1) return rc;
+    if ((rc = launch(img2, W2, up, N, nullptr, 0))) return rc;
+    hipLaunchKernelGGL(k_silu_mul_strided, dim3((unsigned)((N * M + 255) / 256)), dim3(256), 0, s, Y, ldy, up, N, M);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

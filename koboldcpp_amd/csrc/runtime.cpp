@@ -70,6 +70,8 @@ struct KTensor {
     std::vector<RowSlice> rs;        // non-empty: row split, the rows live in these slices (d is null)
     void *dec = nullptr;             // KT_Q8_0_T weights: a second copy in the row-major KT_Q8_0 layout for the fused
                                      // single-token chain (gemv_dec), owned
+    void *pre = nullptr;             // KT_Q6_K_RS layer weights: the int8 two-plane prefill image (kcpp_q6p_build)
+    bool pre_owned = false;          // false: a slice of the layer's q|k|v or gate|up image group
 };
 
 // a row-split execution lane: one device of the split.  The first lane on the stage's own device runs inline on
@@ -441,6 +443,46 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
         }
         m->q80_dec = ok2;
     }
+    // Q6_K layer matrices: the int8 prefill image beside the RS weights (k_gemm_q6p: int8 matrix cores, q6v3's bits;
+    // 2 B per weight more, e.g. +1.9 GB on Llama-3-8B Q4_K_M).  Fused q|k|v / gate|up groups get one image each, so
+    // the group's GEMM reads one contiguous image.  KCPP_Q6P=0: no images (q6v3).
+    if (!(getenv("KCPP_Q6P") && atoi(getenv("KCPP_Q6P")) == 0)) {
+        bool ok3 = true;
+        auto img_group = [&](KTensor *ts, const int *js, int n) {
+            size_t tot = 0;
+            for (int i = 0; i < n; ++i) {
+                const KTensor &t = ts[js[i]];
+                if (t.type != KT_Q6_K_RS || t.slices != 1 || !t.d || !kcpp_q6p_image_bytes(t.K, t.N)) return;
+                tot += (size_t)kcpp_q6p_image_bytes(t.K, t.N);
+            }
+            void *base = nullptr;
+            if (hipMalloc(&base, tot) != hipSuccess) { ok3 = false; return; }
+            size_t off = 0;
+            for (int i = 0; i < n; ++i) {
+                KTensor &t = ts[js[i]];
+                t.pre = (uint8_t *)base + off; t.pre_owned = i == 0;
+                off += (size_t)kcpp_q6p_image_bytes(t.K, t.N);
+            }
+        };
+        for (auto &L : m->layers) {
+            static const int qkv[3] = {1, 2, 3}, glu[2] = {6, 7};
+            if (L.nqkv >= 2) img_group(L.t, qkv, L.nqkv);
+            if (L.glu_fused) img_group(L.t, glu, 2);
+            for (int j = 1; j <= 8 && ok3; ++j) {
+                if (j == 5 || L.t[j].pre) continue;
+                const int one[1] = {j};
+                img_group(L.t, one, 1);
+            }
+        }
+        if (!ok3) {                               // not enough memory: no images anywhere
+            for (auto &L : m->layers)
+                for (auto &t : L.t) {
+                    if (t.pre && t.pre_owned) hipFree(t.pre);
+                    t.pre = nullptr; t.pre_owned = false;
+                }
+            (void)hipGetLastError();
+        }
+    }
     if (hp->n_expert > 0) {
         const int NU = hp->n_expert_used;
         if (NU < 1 || NU > hp->n_expert || hp->n_expert > 64) return fail("bad n_expert / n_expert_used");
@@ -484,7 +526,7 @@ extern "C" void kcpp_model_free(kcpp_model *m) {
     };
     F(m->tok_embd.d); F(m->output_norm.d); F(m->output.d); FS(m->output); F(m->output.dec);
     for (auto &L : m->layers) {
-        for (auto &t : L.t) { if (t.owned) F(t.d); FS(t); F(t.dec); }
+        for (auto &t : L.t) { if (t.owned) F(t.d); FS(t); F(t.dec); if (t.pre_owned) F(t.pre); }
         F(L.qkv_base); F(L.glu_base); F(L.kc); F(L.vc);
     }
     F(m->hglu); F(m->moe_ids); F(m->moe_w); F(m->moe_rows); F(m->moe_rw); F(m->moe_slots);
@@ -531,6 +573,7 @@ extern "C" int kcpp_model_synth_weights(kcpp_model *m, uint64_t seed) {
         } else if (t->slices == 1) {
             RC(kcpp_weight_synth(t->type, seed, (uint64_t)idx, t->d, t->K, t->N, m->stream));
             if (t->dec) RC(kcpp_weight_synth(KT_Q8_0, seed, (uint64_t)idx, t->dec, t->K, t->N, m->stream));
+            if (t->pre) RC(kcpp_q6p_build(t->d, t->K, t->N, t->pre, m->stream));
         } else {                               // expert e: tid = idx * 256 + e (tests/refharness.py)
             for (int e = 0; e < t->slices; ++e)
                 RC(kcpp_weight_synth(t->type, seed, (uint64_t)idx * 256 + e, (uint8_t *)t->d + e * t->slice_bytes, t->K,
@@ -581,7 +624,12 @@ extern "C" int kcpp_model_set_tensor(kcpp_model *m, int idx, const void *src, in
         return 0;
     }
     if (t->dec) RC(upload(m->device, m->stream, KT_Q8_0, t->K, t->N, 1, 0, src, t->dec));
-    return upload(m->device, m->stream, t->type, t->K, t->N, t->slices, t->slice_bytes, src, t->d);
+    RC(upload(m->device, m->stream, t->type, t->K, t->N, t->slices, t->slice_bytes, src, t->d));
+    if (t->pre) {
+        RC(kcpp_q6p_build(t->d, t->K, t->N, t->pre, m->stream));
+        RT_CHECK(hipStreamSynchronize(m->stream));
+    }
+    return 0;
 }
 
 extern "C" float *kcpp_model_hidden(kcpp_model *m) { return m->x; }
@@ -688,6 +736,8 @@ extern "C" int kcpp_model_set_row_split(kcpp_model *m, int n, const int *devices
     for (KTensor *t : mats) {
         if (t->owned && t->d) (void)hipFree(t->d);
         t->d = nullptr; t->owned = false;
+        if (t->pre && t->pre_owned) (void)hipFree(t->pre);       // row slices run q6v3 (no per-slice images)
+        t->pre = nullptr; t->pre_owned = false;
         for (int i = 0; i < n; ++i) {
             RowSlice r;
             r.lane = i;
@@ -866,12 +916,23 @@ static int matmul_rows(kcpp_model *m, const KTensor &W, const KTensor *W2, const
 }
 
 // y[c][n] = W . act  (+res) for M columns: mat-vec for M <= 8, MFMA GEMM above
+// the batched GEMM of one weight (M > 8): Q6_K with a prefill image on the int8 kernel (kcpp_gemm's bits), else kcpp_gemm
+static int gemm_w(const KTensor &W, const KTensor *W2, const void *act, int64_t M, float *Y, int64_t ldy, const float *res,
+                  int64_t ldr, int mode, void *ws, hipStream_t s) {
+    if (W.pre && (!W2 || W2->pre)) {
+        const int rc = kcpp_gemm_q6p(W.pre, W.d, W2 ? W2->pre : nullptr, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy,
+                                     res, ldr, mode, ws, s);
+        if (rc != -3) return rc;
+    }
+    return kcpp_gemm(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, ws, s);
+}
+
 static int matmul(kcpp_model *m, const KTensor &W, const KTensor *W2, const void *act, int64_t M, float *Y, int64_t ldy,
                   const float *res, int64_t ldr, int mode) {
     if (!W.rs.empty()) return matmul_rows(m, W, W2, act, M, Y, ldy, res, ldr, mode);
     if (M <= 8 && W.type != KT_Q8_0_T)
         return kcpp_gemv(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, m->stream);
-    return kcpp_gemm(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, m->gemm_ws, m->stream);
+    return gemm_w(W, W2, act, M, Y, ldy, res, ldr, mode, m->gemm_ws, m->stream);
 }
 
 static int rows_per_wave(int64_t N, int mode) {
@@ -1278,8 +1339,7 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
                     }
                     RT_CHECK(hipEventRecord(m->ev_fork, s));
                     RT_CHECK(hipStreamWaitEvent(m->side, m->ev_fork, 0));
-                    RC(kcpp_gemm(t[3].type, t[3].d, nullptr, E, EKV, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0,
-                                 m->gemm_ws2, m->side));
+                    RC(gemm_w(t[3], nullptr, m->act, T, m->qkv + E + EKV, LQ, nullptr, 0, 0, m->gemm_ws2, m->side));
                     RC(matmul(m, f, nullptr, m->act, T, m->qkv, LQ, nullptr, 0, 0));
                     RT_CHECK(hipEventRecord(m->ev_join, m->side));
                     RT_CHECK(hipStreamWaitEvent(s, m->ev_join, 0));

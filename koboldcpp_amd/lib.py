@@ -44,6 +44,9 @@ _SIGS = {
     "kcpp_quantize_act_glu": [P, I64, I64, P, I64, I64, P],
     "kcpp_gemv": [I, P, P, I64, I64, P, I64, P, I64, P, I64, I, P],
     "kcpp_gemm": [I, P, P, I64, I64, P, I64, P, I64, P, I64, I, P, P],
+    "kcpp_q6p_image_bytes": [I64, I64],
+    "kcpp_q6p_build": [P, I64, I64, P, P],
+    "kcpp_gemm_q6p": [P, P, P, P, I64, I64, P, I64, P, I64, P, I64, I, P, P],
     "kcpp_rms_norm": [P, I64, P, P, I64, P, I64, I64, Fl, P],
     "kcpp_rms_norm_q80": [P, I64, P, P, I64, I64, Fl, P],
     "kcpp_gemm_q80_glu_q80": [P, P, I64, I64, P, I64, P, P, P],
@@ -133,7 +136,7 @@ _SIGS = {
     "kcpp_kv_store_q": [I, I, P, I64, I64, I64, I, I64, P, P, I64, I, P, P],
     "kcpp_flash_attn_q": [I, I, P, I64, P, P, P, I, I, I, I, I64, I, P, Fl, P],
 }
-_RES = {"kcpp_gradient_ai_rope_base": Fl, "kcpp_model_fused_route_count": I64, "kcpp_model_moe_grouped_count": I64, "kcpp_gemm_grouped_ws_bytes": I64, "kcpp_fa_split_ws_bytes": I64, "kcpp_q80t_ws_bytes": I64, "kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
+_RES = {"kcpp_gradient_ai_rope_base": Fl, "kcpp_q6p_image_bytes": I64, "kcpp_model_fused_route_count": I64, "kcpp_model_moe_grouped_count": I64, "kcpp_gemm_grouped_ws_bytes": I64, "kcpp_fa_split_ws_bytes": I64, "kcpp_q80t_ws_bytes": I64, "kcpp_act_bytes": I64, "kcpp_fa_ext_workspace_bytes": I64, "kcpp_fa_workspace_bytes": I64, "kcpp_gemm_workspace_bytes": I64,
         "kcpp_model_create": P, "kcpp_model_hidden": P, "kcpp_model_stream": P, "kcpp_model_weight_bytes": I64,
         "kcpp_last_error": ctypes.c_char_p, "kcpp_model_free": None, "kcpp_fa_set_stamps": None}
 _L.kcpp_act_bytes.argtypes = [I, I64, I64]
