@@ -109,6 +109,17 @@ int kcpp_rs_supported(int type, int64_t K);
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */
 int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t ldy, void *q8k_out, int64_t ne0,
                   int64_t nrows, float eps, void *stream);
+/* split-K partials [KS][Mp][ne0] summed in split order (+ res) into x, then kcpp_rms_norm(x, w, -> q8k_out): one
+ * launch, bit for bit the reduce followed by the norm (the residual GEMM's reduce and the next ggml RMS_NORM + MUL) */
+int kcpp_reduce_rms_norm(const float *part, int KS, int64_t Mp, const float *res, int64_t ldr, float *x, int64_t ldx,
+                         const float *w, void *q8k_out, int64_t ne0, int64_t nrows, float eps, void *stream);
+/* kcpp_gemm (mode 0) / kcpp_gemm_q6p followed by kcpp_rms_norm(Y, norm_w, -> q8k_out), the norm folded into the
+ * GEMM's split-K reduce when it splits (results identical to the two calls) */
+int kcpp_gemm_rms_norm(int type, const void *W, int64_t K, int64_t N, const void *act, int64_t M, float *Y, int64_t ldy,
+                       const float *res, int64_t ldr, void *ws, void *stream, const float *norm_w, float eps, void *q8k_out);
+int kcpp_gemm_q6p_rms_norm(const void *img, const void *W, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
+                           int64_t ldy, const float *res, int64_t ldr, void *ws, void *stream, const float *norm_w, float eps,
+                           void *q8k_out);
 /* rms_norm * w quantized to Q8_0 in the same pass (= kcpp_rms_norm then kcpp_quantize_act(Q8_0), bit for bit) */
 int kcpp_rms_norm_q80(const float *x, int64_t ldx, const float *w, void *q80_out, int64_t ne0, int64_t nrows, float eps,
                       void *stream);

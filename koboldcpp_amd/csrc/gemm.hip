@@ -1187,6 +1187,21 @@ __global__ void k_splitk_reduce(const float *__restrict__ part, int KS, int64_t 
     Y[t * ldy + n] = res ? __fadd_rn(g, res[t * ldr + n]) : g;
 }
 
+// kcpp_gemm_rms_norm / kcpp_gemm_q6p_rms_norm: the residual GEMM's split-K reduce also forms the next rms_norm's
+// Q8_K activation (ops.hip k_rms_norm with partials; bit for bit the reduce followed by kcpp_rms_norm)
+struct NormHook { const float *w; void *qout; float eps; bool used; };
+static thread_local NormHook *g_norm_hook = nullptr;
+static void splitk_finish(const float *part, int KS, int64_t M, int64_t Mp, int64_t N, float *y, int64_t ly,
+                          const float *r, int64_t lr, hipStream_t s) {
+    if (g_norm_hook && !g_norm_hook->used && ly == N &&
+        kcpp_reduce_rms_norm(part, KS, Mp, r, lr, y, ly, g_norm_hook->w, g_norm_hook->qout, N, M, g_norm_hook->eps, s) == 0) {
+        g_norm_hook->used = true;
+        return;
+    }
+    hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y, ly,
+                       r, lr);
+}
+
 // ================================================================ Q6_K GEMM v3 (row-major decode layout Q6_K_RS)
 // k_gemm_q4v3's structure for Q6_K: activation by LDS-DMA, each wave dequantizes its own 32 rows into MFMA
 // fragments, exact integer weights sc*(q-32) split as 8*(sc>>3)*(q-32) + (sc&7)*(q-32) into two MFMAs (as v2).
@@ -2196,8 +2211,7 @@ int kcpp_gemm_q6p(const void *img, const void *W, const void *img2, const void *
                                (const uint8_t *)act, M, Mp, MT, y, ly, r, lr, KS, part, XG);
         KCPP_CHECK(hipGetLastError());
         if (KS > 1) {
-            hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,
-                               ly, r, lr);
+            splitk_finish(part, KS, M, Mp, N, y, ly, r, lr, s);
             KCPP_CHECK(hipGetLastError());
         }
         return 0;
@@ -2208,6 +2222,42 @@ int kcpp_gemm_q6p(const void *img, const void *W, const void *img2, const void *
     hipLaunchKernelGGL(k_silu_mul_strided, dim3((unsigned)((N * M + 255) / 256)), dim3(256), 0, s, Y, ldy, up, N, M);
     KCPP_CHECK(hipGetLastError());
     return 0;
+}
+
+// kcpp_gemm / kcpp_gemm_q6p (mode 0) followed by kcpp_rms_norm(Y, ldy, norm_w, -> q8k_out): when the GEMM splits K, its
+// reduce forms the norm's Q8_K activation in the same launch; the results are those of the two calls bit for bit
+static int gemm_then_norm(int rc_gemm_call(void *), void *ctx, float *Y, int64_t ldy, int64_t N, int64_t M,
+                          const float *norm_w, float eps, void *q8k_out, void *stream) {
+    NormHook h{norm_w, q8k_out, eps, false};
+    g_norm_hook = &h;
+    const int rc = rc_gemm_call(ctx);
+    g_norm_hook = nullptr;
+    if (rc) return rc;
+    if (h.used) return 0;
+    return kcpp_rms_norm(Y, ldy, norm_w, nullptr, 0, q8k_out, N, M, eps, stream);
+}
+
+int kcpp_gemm_rms_norm(int type, const void *W, int64_t K, int64_t N, const void *act, int64_t M, float *Y, int64_t ldy,
+                       const float *res, int64_t ldr, void *ws, void *stream, const float *norm_w, float eps, void *q8k_out) {
+    if (!norm_w || !q8k_out) return -1;
+    struct C { int type; const void *W; int64_t K, N; const void *act; int64_t M; float *Y; int64_t ldy; const float *res;
+               int64_t ldr; void *ws, *stream; } c{type, W, K, N, act, M, Y, ldy, res, ldr, ws, stream};
+    return gemm_then_norm([](void *p) {
+        const C &c = *(const C *)p;
+        return kcpp_gemm(c.type, c.W, nullptr, c.K, c.N, c.act, c.M, c.Y, c.ldy, c.res, c.ldr, 0, c.ws, c.stream);
+    }, &c, Y, ldy, N, M, norm_w, eps, q8k_out, stream);
+}
+
+int kcpp_gemm_q6p_rms_norm(const void *img, const void *W, int64_t K, int64_t N, const void *act, int64_t M, float *Y,
+                           int64_t ldy, const float *res, int64_t ldr, void *ws, void *stream, const float *norm_w, float eps,
+                           void *q8k_out) {
+    if (!norm_w || !q8k_out) return -1;
+    struct C { const void *img, *W; int64_t K, N; const void *act; int64_t M; float *Y; int64_t ldy; const float *res;
+               int64_t ldr; void *ws, *stream; } c{img, W, K, N, act, M, Y, ldy, res, ldr, ws, stream};
+    return gemm_then_norm([](void *p) {
+        const C &c = *(const C *)p;
+        return kcpp_gemm_q6p(c.img, c.W, nullptr, nullptr, c.K, c.N, c.act, c.M, c.Y, c.ldy, c.res, c.ldr, 0, c.ws, c.stream);
+    }, &c, Y, ldy, N, M, norm_w, eps, q8k_out, stream);
 }
 
 int64_t kcpp_gemm_workspace_bytes(int type, int64_t K, int64_t N, int64_t M) {
@@ -2396,8 +2446,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
                                (const int32_t *)nullptr, 0, (int64_t)0);
             KCPP_CHECK(hipGetLastError());
             if (KS > 1) {
-                hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,
-                                   ly, r, lr);
+                splitk_finish(part, KS, M, Mp, N, y, ly, r, lr, s);
                 KCPP_CHECK(hipGetLastError());
             }
             return 0;
@@ -2437,8 +2486,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
 #undef KCPP_V3
             KCPP_CHECK(hipGetLastError());
             if (KS > 1) {
-                hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,
-                                   ly, r, lr);
+                splitk_finish(part, KS, M, Mp, N, y, ly, r, lr, s);
                 KCPP_CHECK(hipGetLastError());
             }
             return 0;
@@ -2476,8 +2524,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
 #undef KCPP_V6
             KCPP_CHECK(hipGetLastError());
             if (KS > 1) {
-                hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS, M, Mp, N, y,
-                                   ly, r, lr);
+                splitk_finish(part, KS, M, Mp, N, y, ly, r, lr, s);
                 KCPP_CHECK(hipGetLastError());
             }
             return 0;
@@ -2553,8 +2600,7 @@ int kcpp_gemm(int type, const void *W, const void *W2, int64_t K, int64_t N, con
         }
         KCPP_CHECK(hipGetLastError());
         if (KS1 > 1) {
-            hipLaunchKernelGGL(k_splitk_reduce, dim3((unsigned)((M * N + 255) / 256)), dim3(256), 0, s, part, KS1, M, Mp, N, y, ly,
-                               r, lr);
+            splitk_finish(part, KS1, M, Mp, N, y, ly, r, lr, s);
             KCPP_CHECK(hipGetLastError());
         }
         return 0;

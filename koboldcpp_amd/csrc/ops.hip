@@ -13,19 +13,42 @@
 // ---------------------------------------------------------------- rms_norm (+ weight, + quantize)
 // One workgroup per row, ne0/16 threads, 16 consecutive elements per thread: an aligned 16-lane
 // group is exactly one Q8_K super-block, so the fused quantization needs only DPP steps.
+// part (optional): x is first formed from KS split-K partials [KS][Mp][ne0] summed in split order plus res, exactly as
+// gemm.hip k_splitk_reduce does, and stored at xout -- the reduce and the norm of the next layer step in one launch
 __global__ void __launch_bounds__(1024) k_rms_norm(const float *__restrict__ x, int64_t ldx, const float *__restrict__ w,
                                                    float *__restrict__ y, int64_t ldy, uint8_t *__restrict__ qout,
-                                                   int64_t ne0, int64_t nrows, float eps, int q80 = 0) {
+                                                   int64_t ne0, int64_t nrows, float eps, int q80 = 0,
+                                                   const float *__restrict__ part = nullptr, int KS = 1, int64_t Mp = 0,
+                                                   float *__restrict__ xout = nullptr, const float *__restrict__ res = nullptr,
+                                                   int64_t ldr = 0) {
     const int64_t r = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = (blockDim.x + 63) >> 6;
     const int64_t e0 = (int64_t)tid * 16;
     const bool active = e0 < ne0;                    // block is >= 64 threads even for small rows
     float v[16];
-    const float4 *src = (const float4 *)(x + r * ldx + e0);
+    if (part) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float4 f = active ? src[k] : make_float4(0, 0, 0, 0);
-        v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
+        for (int k = 0; k < 4; ++k) {
+            float4 g = active ? *(const float4 *)(part + r * ne0 + e0 + 4 * k) : make_float4(0, 0, 0, 0);
+            for (int sp = 1; sp < KS; ++sp) {
+                const float4 h = active ? *(const float4 *)(part + ((int64_t)sp * Mp + r) * ne0 + e0 + 4 * k)
+                                        : make_float4(0, 0, 0, 0);
+                g = make_float4(__fadd_rn(g.x, h.x), __fadd_rn(g.y, h.y), __fadd_rn(g.z, h.z), __fadd_rn(g.w, h.w));
+            }
+            if (res && active) {
+                const float4 h = *(const float4 *)(res + r * ldr + e0 + 4 * k);
+                g = make_float4(__fadd_rn(g.x, h.x), __fadd_rn(g.y, h.y), __fadd_rn(g.z, h.z), __fadd_rn(g.w, h.w));
+            }
+            if (active) *(float4 *)(xout + r * ldx + e0 + 4 * k) = g;
+            v[4 * k] = g.x; v[4 * k + 1] = g.y; v[4 * k + 2] = g.z; v[4 * k + 3] = g.w;
+        }
+    } else {
+        const float4 *src = (const float4 *)(x + r * ldx + e0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 f = active ? src[k] : make_float4(0, 0, 0, 0);
+            v[4 * k] = f.x; v[4 * k + 1] = f.y; v[4 * k + 2] = f.z; v[4 * k + 3] = f.w;
+        }
     }
     double ss = 0.0;
 #pragma unroll
@@ -176,6 +199,18 @@ int kcpp_rms_norm(const float *x, int64_t ldx, const float *w, float *y, int64_t
     const unsigned nthr = (unsigned)(ne0 / 16 < 64 ? 64 : ne0 / 16);
     hipLaunchKernelGGL(k_rms_norm, dim3((unsigned)nrows), dim3(nthr), 0, (hipStream_t)stream, x, ldx, w, y,
                        ldy, (uint8_t *)q8k_out, ne0, nrows, eps);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// split-K partials [KS][Mp][ne0] (+ res) -> x (stored at x, row stride ldx) -> rms_norm * w -> the Q8_K activation:
+// k_splitk_reduce followed by kcpp_rms_norm(x, ..., q8k_out), bit for bit, in one launch
+int kcpp_reduce_rms_norm(const float *part, int KS, int64_t Mp, const float *res, int64_t ldr, float *x, int64_t ldx,
+                         const float *w, void *q8k_out, int64_t ne0, int64_t nrows, float eps, void *stream) {
+    if (ne0 % 256 || ne0 > 16384 || !part || KS < 1 || !x || !q8k_out) return -1;
+    const unsigned nthr = (unsigned)(ne0 / 16 < 64 ? 64 : ne0 / 16);
+    hipLaunchKernelGGL(k_rms_norm, dim3((unsigned)nrows), dim3(nthr), 0, (hipStream_t)stream, (const float *)x, ldx, w,
+                       (float *)nullptr, (int64_t)0, (uint8_t *)q8k_out, ne0, nrows, eps, 0, part, KS, Mp, x, res, ldr);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

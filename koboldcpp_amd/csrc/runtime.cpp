@@ -146,6 +146,7 @@ struct kcpp_model {
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
     bool q81 = false;                // Q4_1 / Q5_1 weights (Q8_1 activations): decode on the per-op path
     bool q80t = false;               // Q8_0 layer weights in the tile layout KT_Q8_0_T (gemm_q80t.hip) at every batch size
+    bool no_norm_fold = false;       // KCPP_NORM_FOLD=0: the residual GEMMs never carry the next rms_norm (A/B)
     bool q80_dec = false;            // ... plus their KT_Q8_0 decode copies (KTensor::dec): single tokens on the fused chain
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
     int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
@@ -446,6 +447,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     // Q6_K layer matrices: the int8 prefill image beside the RS weights (k_gemm_q6p: int8 matrix cores, q6v3's bits;
     // 2 B per weight more, e.g. +1.9 GB on Llama-3-8B Q4_K_M).  Fused q|k|v / gate|up groups get one image each, so
     // the group's GEMM reads one contiguous image.  KCPP_Q6P=0: no images (q6v3).
+    m->no_norm_fold = getenv("KCPP_NORM_FOLD") && atoi(getenv("KCPP_NORM_FOLD")) == 0;
     if (!(getenv("KCPP_Q6P") && atoi(getenv("KCPP_Q6P")) == 0)) {
         bool ok3 = true;
         auto img_group = [&](KTensor *ts, const int *js, int n) {
@@ -927,6 +929,21 @@ static int gemm_w(const KTensor &W, const KTensor *W2, const void *act, int64_t 
     return kcpp_gemm(W.type, W.d, W2 ? W2->d : nullptr, W.K, W.N, act, M, Y, ldy, res, ldr, mode, ws, s);
 }
 
+// the residual GEMM (M > 8) followed by the next rms_norm's Q8_K activation: the norm folded into the GEMM's split-K
+// reduce where it splits (kcpp_gemm_rms_norm), the two steps' bits either way
+static int gemm_w_norm(const KTensor &W, const void *act, int64_t M, float *Y, int64_t ldy, const float *res, int64_t ldr,
+                       void *ws, hipStream_t s, const float *nw, float eps, void *qout) {
+    if (W.pre) {
+        const int rc = kcpp_gemm_q6p_rms_norm(W.pre, W.d, W.K, W.N, act, M, Y, ldy, res, ldr, ws, s, nw, eps, qout);
+        if (rc != -3) return rc;
+    }
+    return kcpp_gemm_rms_norm(W.type, W.d, W.K, W.N, act, M, Y, ldy, res, ldr, ws, s, nw, eps, qout);
+}
+// may the residual GEMM of W at T tokens carry the following rms_norm -> Q8_K (gemm_w_norm)?
+static bool norm_foldable(const kcpp_model *m, const KTensor &W, int T) {
+    return T > 8 && W.rs.empty() && W.type != KT_Q8_0_T && m->lanes.empty() && !m->no_norm_fold;
+}
+
 static int matmul(kcpp_model *m, const KTensor &W, const KTensor *W2, const void *act, int64_t M, float *Y, int64_t ldy,
                   const float *res, int64_t ldr, int mode) {
     if (!W.rs.empty()) return matmul_rows(m, W, W2, act, M, Y, ldy, res, ldr, mode);
@@ -1319,14 +1336,22 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
     hipStream_t s = m->stream;
     const float kq_scale = 1.0f / sqrtf((float)D);
     const int32_t *posp = dev_pos ? m->pos_dev : nullptr;
+    // a layer's attn_norm Q8_K activation already formed by the previous layer's down GEMM (gemm_w_norm)
+    auto qkv_q8k = [](const KTensor *t) {
+        return kcpp_vec_dot_type(t[1].type) == KT_Q8_K && kcpp_vec_dot_type(t[2].type) == KT_Q8_K &&
+               kcpp_vec_dot_type(t[3].type) == KT_Q8_K;
+    };
+    bool pre_normed = false;
     for (int il = m->il0; il < m->il1; ++il) {
         KLayer &L = m->layers[il - m->il0];
         const KTensor *t = L.t;
         const bool kq = kcpp_vec_dot_type(t[1].type) == KT_Q8_K;
         bool roped = false;                          // q16 and this step's K/V rows already written
+        const bool normed = pre_normed;
+        pre_normed = false;
         // attn_norm -> act (Q8_K fused, or f32 then Q8_0)
-        if (kq && kcpp_vec_dot_type(t[2].type) == KT_Q8_K && kcpp_vec_dot_type(t[3].type) == KT_Q8_K) {
-            RC(kcpp_rms_norm(m->x, E, (const float *)t[0].d, nullptr, E, m->act, E, T, hp.eps, s));
+        if (qkv_q8k(t)) {
+            if (!normed) RC(kcpp_rms_norm(m->x, E, (const float *)t[0].d, nullptr, E, m->act, E, T, hp.eps, s));
             if (L.nqkv >= 2) {                       // q|k(|v) rows back to back: one GEMM
                 KTensor f = t[1];
                 f.N = E + (L.nqkv - 1) * EKV;
@@ -1412,7 +1437,13 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, (woq && T <= 16) ? m->act : nullptr, m->fa_ws, T, (int)H,
                                (int)HKV, (int)D, n_past, posp, hp.n_ctx, kq_scale, 0, s));
         if (!(woq && T <= 16) && !attn_q) RC(kcpp_quantize_act(kcpp_vec_dot_type(t[4].type), m->attn, E, m->act, E, T, s));
-        RC(matmul(m, t[4], nullptr, m->act, T, m->x, E, m->x, E, 0));                    // x += wo . attn
+        const bool gq = kcpp_vec_dot_type(t[6].type) == KT_Q8_K && kcpp_vec_dot_type(t[7].type) == KT_Q8_K;
+        // x += wo . attn; dense Q8_K FFNs: ffn_norm's activation formed with it (in wo's split-K reduce)
+        const bool wo_norm = hp.n_expert <= 0 && !m->q80t && gq && norm_foldable(m, t[4], T);
+        if (wo_norm)
+            RC(gemm_w_norm(t[4], m->act, T, m->x, E, m->x, E, m->gemm_ws, s, (const float *)t[5].d, hp.eps, m->act));
+        else
+            RC(matmul(m, t[4], nullptr, m->act, T, m->x, E, m->x, E, 0));
         if (hp.n_expert > 0) { RC(T == 1 ? moe_dec(m, L) : moe_prefill(m, L, T)); continue; }   // T == 1: no host sync (graphs)
         if (m->q80t) {
             // ffn_norm -> TA quantization; gate|up with silu(g) u quantized to the TA activation of down in the GEMM's
@@ -1427,9 +1458,8 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             RC(matmul(m, t[8], nullptr, m->act2, T, m->x, E, m->x, E, 0));               // x += down . h
             continue;
         }
-        const bool gq = kcpp_vec_dot_type(t[6].type) == KT_Q8_K && kcpp_vec_dot_type(t[7].type) == KT_Q8_K;
         if (gq) {
-            RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, nullptr, E, m->act, E, T, hp.eps, s));
+            if (!wo_norm) RC(kcpp_rms_norm(m->x, E, (const float *)t[5].d, nullptr, E, m->act, E, T, hp.eps, s));
         } else if (kcpp_vec_dot_type(t[6].type) == KT_Q8_0 && kcpp_vec_dot_type(t[7].type) == KT_Q8_0) {
             RC(kcpp_rms_norm_q80(m->x, E, (const float *)t[5].d, m->act, E, T, hp.eps, s));
         } else {
@@ -1454,7 +1484,14 @@ static int forward_layers(kcpp_model *m, int T, int n_past, bool dev_pos) {
             }
             RC(kcpp_quantize_act(kcpp_vec_dot_type(t[8].type), m->h, F, m->act2, F, T, s));
         }
-        RC(matmul(m, t[8], nullptr, m->act2, T, m->x, E, m->x, E, 0));                   // x += down . h
+        // x += down . h; the next layer's attn_norm activation formed with it when that layer takes Q8_K
+        const KTensor *tn = il + 1 < m->il1 ? m->layers[il + 1 - m->il0].t : nullptr;
+        if (tn && qkv_q8k(tn) && norm_foldable(m, t[8], T)) {
+            RC(gemm_w_norm(t[8], m->act2, T, m->x, E, m->x, E, m->gemm_ws, s, (const float *)tn[0].d, hp.eps, m->act));
+            pre_normed = true;
+        } else {
+            RC(matmul(m, t[8], nullptr, m->act2, T, m->x, E, m->x, E, 0));
+        }
     }
     return 0;
 }

@@ -45,6 +45,9 @@ _SIGS = {
     "kcpp_gemv": [I, P, P, I64, I64, P, I64, P, I64, P, I64, I, P],
     "kcpp_gemm": [I, P, P, I64, I64, P, I64, P, I64, P, I64, I, P, P],
     "kcpp_q6p_image_bytes": [I64, I64],
+    "kcpp_gemm_rms_norm": [I, P, I64, I64, P, I64, P, I64, P, I64, P, P, P, Fl, P],
+    "kcpp_gemm_q6p_rms_norm": [P, P, I64, I64, P, I64, P, I64, P, I64, P, P, P, Fl, P],
+    "kcpp_reduce_rms_norm": [P, I, I64, P, I64, P, I64, P, P, I64, I64, Fl, P],
     "kcpp_q6p_build": [P, I64, I64, P, P],
     "kcpp_gemm_q6p": [P, P, P, P, I64, I64, P, I64, P, I64, P, I64, I, P, P],
     "kcpp_rms_norm": [P, I64, P, P, I64, P, I64, I64, Fl, P],

@@ -9,7 +9,7 @@ import glob
 import json
 import sys
 
-KERNELS = ["k_gemm_q4v4", "k_gemm_q4v3", "k_gemm_q6v3", "k_gemm_kq", "k_gemm_q80s2", "k_fa_prefill_mfma3", "k_fa_prefill_mfma2", "k_fa_prefill_mfma",
+KERNELS = ["k_gemm_q6p", "k_gemm_q4v4", "k_gemm_q4v3", "k_gemm_q6v3", "k_gemm_kq", "k_gemm_q80s2", "k_fa_prefill_mfma3", "k_fa_prefill_mfma2", "k_fa_prefill_mfma",
            "k_act_frag3", "k_act_frag6", "k_splitk_reduce"]
 
 

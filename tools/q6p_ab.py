@@ -15,7 +15,10 @@ Q6_K_RS = 114
 
 def main():
     s = torch.cuda.current_stream().cuda_stream
-    for Kd, N, M in [(14336, 4096, 512), (4096, 1024, 512), (4096, 4096, 512), (4096, 28672, 512), (14336, 4096, 128)]:
+    shapes = [(14336, 4096, 512), (4096, 1024, 512), (4096, 4096, 512), (4096, 28672, 512), (14336, 4096, 128)]
+    if os.environ.get("Q6P_AB_SHAPES"):          # e.g. "0" or "0,3": a subset (PMC passes)
+        shapes = [shapes[int(i)] for i in os.environ["Q6P_AB_SHAPES"].split(",")]
+    for Kd, N, M in shapes:
         w = torch.empty(N * Kd // 256 * 210, dtype=torch.uint8, device="cuda")
         K.call("kcpp_weight_synth", Q6_K_RS, 7, 1, w.data_ptr(), Kd, N, s)
         img = torch.empty(int(K.raw().kcpp_q6p_image_bytes(Kd, N)), dtype=torch.uint8, device="cuda")
