@@ -104,6 +104,10 @@ int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
 /* q|k|v decode projection (mode 2, rms_norm + Q8_K prologue) with segments 0, 1 (q, k) in KT_Q4_K_RS and segment 2
  * (v) in KT_Q6_K_RS -- the Q4_K_M "more bits" layers -- in one launch; -3 when the shape is not covered */
 int kcpp_gemv_rs_qkv_mixed(const void *args, void *stream);
+/* decode q|k|v with q in an RS layout (Q4_K / Q5_K / Q6_K, qargs) and k|v in Q8_0 (kvargs) -- Mixtral's Q5_K_M
+ * policy -- as one grid holding both mat-vec launches' workgroups (mode 2 each, results identical to the two
+ * kcpp_gemv_dec calls); -3 when not covered */
+int kcpp_gemv_qkv_dual(const void *qargs, int qtype, const void *kvargs, void *stream);
 int kcpp_rs_supported(int type, int64_t K);
 
 /* rms_norm (ggml.c:12059) * w, optionally quantized to Q8_K in the same pass (q8k_out) */

@@ -219,7 +219,9 @@ __global__ void __launch_bounds__(256) k_fa_dec4(const uint16_t *__restrict__ q1
 // is k_fa_comb4.
 // GRAPH (the ggml plugin's FLASH_ATTN_EXT with one query, kcpp_flash_attn_ext_dec): q f32 at qf (head stride qf_hs
 // floats), rounded to f16 in the kernel; the f16 mask row added to the scores, -inf keys skipped.
-template <int G, bool NT, int NW = 4, bool GRAPH = false>
+// FINAL (short contexts, NS = 1, kcpp_flash_attn force_path 7): one workgroup per kv head walks every key and writes
+// the attention output itself (part_o = out [H][128]) -- no combine launch
+template <int G, bool NT, int NW = 4, bool GRAPH = false, bool FINAL = false>
 __global__ void __launch_bounds__(64 * NW) k_fa_dec5(const uint16_t *__restrict__ q16, const uint16_t *__restrict__ kc,
                                                      const uint16_t *__restrict__ vc, float *__restrict__ part_o,
                                                      float2 *__restrict__ part_ml, int H, int n_past_arg,
@@ -291,7 +293,7 @@ __global__ void __launch_bounds__(64 * NW) k_fa_dec5(const uint16_t *__restrict_
         if (b1 < nkv) fadec::consume(st, b1, nkv, kq, sc2, kn, vn, GRAPH ? md : nullptr);
         issue(CK * (c + 3 * NS) + 16 * wave, lim, kn, vn, mb);
     }
-    fadec::finish(st, sm, hk, sp, NS, part_o, part_ml);
+    fadec::finish<G, NW, FINAL>(st, sm, hk, sp, NS, part_o, part_ml);
 }
 
 // combine of k_fa_dec4's partials (m in the exp2 domain): grid (H / 2), 256 threads = 2 heads x 128 dims
@@ -437,6 +439,29 @@ static bool fa_dec5_default() {
     static const bool on = [] { const char *e = getenv("KCPP_FA_DEC"); return !e || atoi(e) != 4; }();
     return on;
 }
+// short contexts (n_kv <= KCPP_FA_SHORT_MAX): k_fa_dec5<FINAL> on one 8-wave workgroup per kv head, the output written
+// directly (one launch instead of split + combine; at a few hundred keys the split grid mostly holds empty splits and
+// the combine is a whole dependent launch).  The caller decides by the host-known position (graphs per regime).
+static int fa_short_launch(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
+                           float *out, int H, int HKV, int n_past, const int32_t *n_past_dev, float scale, hipStream_t s,
+                           int n_rows) {
+    const int G = H / HKV;
+#define KCPP_FS(G_)                                                                                                   \
+    hipLaunchKernelGGL((k_fa_dec5<G_, true, 8, false, true>), dim3(1, HKV), dim3(512), 0, s, q16, kc, vc, out,         \
+                       (float2 *)nullptr, H, n_past, n_past_dev, 1, scale, kv_ld, kv_hs, n_rows, (const float *)nullptr, \
+                       (int64_t)0, (const uint16_t *)nullptr)
+    switch (G) {
+    case 1: KCPP_FS(1); break;
+    case 2: KCPP_FS(2); break;
+    case 4: KCPP_FS(4); break;
+    case 8: KCPP_FS(8); break;
+    default: return -3;
+    }
+#undef KCPP_FS
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
 static int fa4_launch(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
                       float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
                       float scale, hipStream_t s, int qkind, int n_rows, bool v5) {
@@ -734,6 +759,11 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
     // prefill, 6: the 64-key-chunk decode kernel even for T = 1 (tests)
     const bool use_decode = force_path == 1 || force_path == 6 || (force_path == 0 && T <= 16);
     const int G0 = H / HKV;
+    if (force_path == 7) {       // single-pass decode (short contexts: the caller keeps n_kv <= KCPP_FA_SHORT_MAX)
+        if (T != 1 || !out || qout) return -1;
+        return fa_short_launch(q16, kc, vc, (int64_t)HKV * 128, 128, out, H, HKV, n_past, n_past_dev, scale, s,
+                               n_past_dev ? n_kv_max : n_past + 1);
+    }
     if (use_decode && T == 1 && force_path != 6 && (G0 == 1 || G0 == 2 || G0 == 4 || G0 == 8) && (qout == nullptr || G0 >= 2))
         return fa4_launch(q16, kc, vc, (int64_t)HKV * 128, 128, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, 1,
                           n_past_dev ? n_kv_max : n_past + 1, fa_dec5_default());
@@ -787,7 +817,8 @@ int kcpp_flash_attn(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc,
 // single-token decode attention with explicit cache strides (elements): key p of kv head hk starts at
 // kc + p * kv_ld + hk * kv_hs.  Position-major ggml view: kv_ld = HKV*D, kv_hs = D; head-major: kv_ld = D,
 // kv_hs = n_ctx*D.  variant 0: 64-key chunks + k_fa_combine; 3: k_fa_dec4 + k_fa_comb4 (round 5's production pair);
-// 5: k_fa_dec5 + k_fa_comb4 (the production pair; n_kv_max = the views' row count).  A/B entry for tools/fa_dec_bench.py.
+// 5: k_fa_dec5 + k_fa_comb4 (the production pair; n_kv_max = the views' row count); 8: the short-context single launch
+// (one workgroup per kv head, no combine).  A/B entry for tools/fa_dec_bench.py.
 void kcpp_fa_set_stamps(void *p) { g_fa_stamps = p; }     // diagnostic stamp buffer of k_fa_dec4 / k_fa_comb4 (tools only)
 int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *vc, int64_t kv_ld, int64_t kv_hs,
                       float *out, void *qout, void *ws, int H, int HKV, int n_past, const int32_t *n_past_dev,
@@ -800,6 +831,10 @@ int kcpp_fa_decode_ex(const uint16_t *q16, const uint16_t *kc, const uint16_t *v
     if (variant == 3 || variant == 5)
         return fa4_launch(q16, kc, vc, kv_ld, kv_hs, out, qout, ws, H, HKV, n_past, n_past_dev, scale, s, 1, nkv,
                           variant == 5);
+    if (variant == 8) {                     // the short-context single launch (kcpp_flash_attn force_path 7)
+        if (qout || !out) return -1;
+        return fa_short_launch(q16, kc, vc, kv_ld, kv_hs, out, H, HKV, n_past, n_past_dev, scale, s, nkv);
+    }
     if (variant == 6 || variant == 7) {     // A/B (tools/fa_dec_bench.py): k_fa_dec5 at NS splits (KCPP_FA_NS) x NW waves
         // (KCPP_FA_NW), G = 4; 7: without the combine (the split kernel alone)
         const int NS = getenv("KCPP_FA_NS") ? atoi(getenv("KCPP_FA_NS")) : 32;

@@ -145,8 +145,9 @@ struct Smem {
 };
 
 // rows (kq) hold disjoint keys: park every row's 8 dims in LDS, reduce rows and the NW waves in one pass; write the
-// split's partial O and (M, L) of heads hk * G + g
-template <int G, int NW = 4>
+// split's partial O and (M, L) of heads hk * G + g.  FINAL (one split holds every key): write O / L to part_o as the
+// attention output [H][128] instead -- what k_fa_comb4 makes of a lone split, bit for bit (weight exp2(0) = 1)
+template <int G, int NW = 4, bool FINAL = false>
 __device__ __forceinline__ void finish(State<G> &st, Smem<G, NW> &sm, int hk, int sp, int NS, float *__restrict__ part_o,
                                        float2 *__restrict__ part_ml) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -184,7 +185,7 @@ __device__ __forceinline__ void finish(State<G> &st, Smem<G, NW> &sm, int hk, in
             L = fmaf(wt, sm.ml[w][g][1], L);
         }
         sm.L[g] = L;
-        part_ml[(int64_t)(hk * G + g) * NS + sp] = make_float2(M, L);
+        if (!FINAL) part_ml[(int64_t)(hk * G + g) * NS + sp] = make_float2(M, L);
     }
     __syncthreads();
     for (int i = tid; i < G * D; i += 64 * NW) {
@@ -192,7 +193,8 @@ __device__ __forceinline__ void finish(State<G> &st, Smem<G, NW> &sm, int hk, in
         float O = 0.0f;
 #pragma unroll
         for (int w = 0; w < NW; ++w) O = fmaf(sm.w[w][g], sm.o[w][g][d], O);
-        part_o[((int64_t)(hk * G + g) * NS + sp) * D + d] = O;
+        if (FINAL) part_o[(int64_t)(hk * G + g) * D + d] = O / sm.L[g];
+        else part_o[((int64_t)(hk * G + g) * NS + sp) * D + d] = O;
     }
 }
 

@@ -141,119 +141,23 @@ __device__ __forceinline__ void act_to_lds(const uint8_t *__restrict__ act, uint
 // 2 x IT x R units (48-80 B each per lane) in flight.
 template <int TYPE, int R, int MODE, int PRO, int MC, int IT>
 __global__ void __launch_bounds__(256) k_gemv_dec(const DecArgs a) {
-    using A = typename ActOf<TYPE>::T;
-    constexpr int E = Unit<TYPE>::ELEMS;
-    constexpr int VT = (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0 || TYPE == KT_IQ4_NL) ? KT_Q8_0 : KT_Q8_K;
-    constexpr int RR = MODE == 1 ? 2 * R : R;
     extern __shared__ __attribute__((aligned(16))) uint8_t lds_act[];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t K = a.K;
-    const int upr = (int)(K / E);
+    const int KB_BID = (int)blockIdx.x, KB_NBLK = (int)gridDim.x;
+#define KB_ARGS a
+#include "gemv_dec_body.inc"
+#undef KB_ARGS
+}
+
+// grid and LDS of k_gemv_dec<TYPE, R, MODE, PRO, ...> for a (launch_dec_it's rule)
+template <int TYPE, int R, int PRO>
+static int64_t dec_grid(const DecArgs &a, size_t &lds) {
     int64_t ntot = 0;
     for (int i = 0; i < a.nseg; ++i) ntot += a.N[i];
-    const int64_t ngroups = ntot / R;
-    const int64_t nw = (int64_t)gridDim.x * 4;
-    const int64_t wid = (int64_t)blockIdx.x * 4 + wave;
-    // MoE: this launch's expert slice (index read on the device, wave-uniform)
-    const int64_t eoff = dec_expert_offset(a);
-    const float escale = a.escale ? a.escale[0] : 1.0f;
-
-    auto group_rows = [&](int64_t g, int &seg, int64_t &row0) {
-        int64_t r = g * R;
-        seg = 0;
-        while (seg < a.nseg - 1 && r >= a.N[seg]) { r -= a.N[seg]; ++seg; }
-        row0 = r;
-    };
-    auto issue = [&](int64_t g, Unit<TYPE>(&w)[IT][RR]) {
-        int seg; int64_t row0;
-        group_rows(g, seg, row0);
-        const int64_t N = a.N[seg];
-        const int64_t nb = K / ks_block_elems(TYPE) * N;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int u = lane + 64 * it;
-            if (u < upr) {
-#pragma unroll
-                for (int r = 0; r < RR; ++r) {
-                    if constexpr (MODE == 1) load_unit<TYPE>(w[it][r], (r < R ? a.W[seg] : a.W2) + eoff, nb, row0 + (r % R), upr, u);
-                    else load_unit<TYPE>(w[it][r], a.W[seg] + eoff, nb, row0 + r, upr, u);
-                }
-            }
-        }
-    };
-    auto finish = [&](int64_t g, float (&acc)[RR]) {
-        int seg; int64_t row0;
-        group_rows(g, seg, row0);
-#pragma unroll
-        for (int r = 0; r < RR; ++r) acc[r] = wave_sum_dpp(acc[r]);
-        if (lane != 0) return;
-        float *Y = a.Y[seg];
-        if constexpr (MODE == 0) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const float v = a.escale ? __fmul_rn(acc[r], escale) : acc[r];
-                Y[row0 + r] = a.res ? __fadd_rn(v, a.res[row0 + r]) : v;
-            }
-        } else if constexpr (MODE == 1) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const float gt = acc[r], up = acc[R + r];
-                Y[row0 + r] = (gt / (1.0f + expf(-gt))) * up;
-            }
-        } else {
-            const int role = a.role[seg];
-            const int p = a.pos[0];
-            if (role == 2) {
-#pragma unroll
-                for (int r = 0; r < R; ++r) a.vc[(int64_t)p * a.ekv + row0 + r] = f2h(acc[r]);
-            } else {
-                const int hd = a.D / 2;
-#pragma unroll
-                for (int r = 0; r < R; r += 2) {      // rows (2i, 2i+1): a RoPE pair (NORM mode)
-                    const int64_t row = row0 + r;
-                    const float2 cs = a.rope_tab[(int64_t)p * hd + (int)((row % a.D) / 2)];
-                    const float x0 = acc[r], x1 = acc[r + 1];
-                    const float o0 = __fsub_rn(__fmul_rn(x0, cs.x), __fmul_rn(x1, cs.y));
-                    const float o1 = __fadd_rn(__fmul_rn(x0, cs.y), __fmul_rn(x1, cs.x));
-                    if (role == 0) { a.q16[row] = f2h(o0); a.q16[row + 1] = f2h(o1); }
-                    else {
-                        a.kc[(int64_t)p * a.ekv + row] = f2h(o0);
-                        a.kc[(int64_t)p * a.ekv + row + 1] = f2h(o1);
-                    }
-                }
-            }
-        }
-    };
-    auto compute = [&](const Unit<TYPE>(&w)[IT][RR], const ActView &av, float (&acc)[RR]) {
-#pragma unroll
-        for (int r = 0; r < RR; ++r) acc[r] = 0.0f;
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-            const int u = lane + 64 * it;
-            if (u < upr) {
-                A x;
-                load_act(av, u, x);
-#pragma unroll
-                for (int r = 0; r < RR; ++r) acc[r] += unit_dot(w[it][r], u, x);
-            }
-        }
-    };
-
-    Unit<TYPE> wa[IT][RR], wb[IT][RR];
-    if (wid < ngroups) issue(wid, wa);
-    if constexpr (PRO != 0) prologue<VT, PRO, MC>(a, lds_act);
-    const ActView av = act_view(VT, PRO != 0 ? (const uint8_t *)lds_act : a.act, K, 1, 0);
-    float acc[RR];
-    for (int64_t g = wid; g < ngroups; g += 2 * nw) {
-        const int64_t g1 = g + nw, g2 = g + 2 * nw;
-        if (g1 < ngroups) issue(g1, wb);
-        compute(wa, av, acc);
-        finish(g, acc);
-        if (g1 >= ngroups) break;
-        if (g2 < ngroups) issue(g2, wa);
-        compute(wb, av, acc);
-        finish(g1, acc);
-    }
+    const int max_blocks = a.K > 4096 ? 512 : 1024;
+    const int64_t groups = ntot / R;
+    const int vt = (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0 || TYPE == KT_IQ4_NL) ? KT_Q8_0 : KT_Q8_K;
+    lds = PRO ? (size_t)act_bytes(vt, a.K, 1) + 16 : 0;
+    return std::min<int64_t>((groups + 3) / 4, max_blocks);
 }
 
 template <int TYPE, int R, int MODE, int PRO, int MC, int IT>
@@ -266,11 +170,8 @@ static int launch_dec_it(const DecArgs &a, hipStream_t s) {
     if (PRO != 0 && a.K > 4096 * MC) return -6;
     // 1024 workgroups for K = n_embd shapes (the output head prefers more), 512 for the K = n_ff
     // quantize-prologue shape (ffn_down: 20.6 vs 26.8 us measured)
-    const int max_blocks = a.K > 4096 ? 512 : 1024;
-    const int64_t groups = ntot / R;
-    const int64_t nblk = std::min<int64_t>((groups + 3) / 4, max_blocks);
-    const int vt = (TYPE == KT_Q4_0 || TYPE == KT_Q5_0 || TYPE == KT_Q8_0 || TYPE == KT_IQ4_NL) ? KT_Q8_0 : KT_Q8_K;
-    const size_t lds = PRO ? (size_t)act_bytes(vt, a.K, 1) + 16 : 0;
+    size_t lds = 0;
+    const int64_t nblk = dec_grid<TYPE, R, PRO>(a, lds);
     hipLaunchKernelGGL((k_gemv_dec<TYPE, R, MODE, PRO, MC, IT>), dim3((unsigned)nblk), dim3(256), lds, s, a);
     KCPP_CHECK(hipGetLastError());
     return 0;

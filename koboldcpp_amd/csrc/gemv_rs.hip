@@ -44,6 +44,7 @@ extern "C" int kcpp_rs_set_stamps(void *p) {
 #endif
 
 #include "gemv_rs.h"
+#include "gemv_dec_impl.h"
 using namespace rs;
 
 
@@ -62,239 +63,9 @@ using namespace rs;
 // the row is ((w0 o0) + (w1 o1)) + res -- the two chained MODE 0 launches' result bit for bit
 template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4, bool XL = false, bool ROUTE = false>
 __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
-    using T = RS<TYPE>;
-    constexpr int RR = MODE == 1 ? 2 * R : R;
-    static_assert(MODE != 3 || (NWV == 8 && PRO == 2 && !ROUTE), "MODE 3: 8 waves, quantize prologue");
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-#ifdef KCPP_STAMPS
-    __shared__ unsigned long long *st_s;
-    if (threadIdx.x == 0) {
-        unsigned long long *b = g_rs_stamps;   // every 8th workgroup records (one counter: ~88 adds per us)
-        st_s = (b && (blockIdx.x & 7) == 0) ? b + 16ull * (atomicAdd(&g_rs_slot, 1u) & 131071u) : nullptr;
-        if (st_s) {
-            st_s[5] = ((unsigned long long)gridDim.x << 32) | blockIdx.x;
-            st_s[6] = (unsigned long long)a.K | ((unsigned long long)MODE << 24) | ((unsigned long long)PRO << 28);
-            st_s[7] = (unsigned long long)(a.N[0] + (a.nseg > 1 ? a.N[1] : 0) + (a.nseg > 2 ? a.N[2] : 0));
-        }
-    }
-    __syncthreads();
-    unsigned long long *st_ = st_s;
-    RS_STAMP(0);
-#endif
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int K = (int)a.K, nsb = K / 256, RB = nsb * T::BYTES;
-    const int npieces = nsb * T::PIECES_PER_SB;
-    const int N0 = (int)a.N[0], N1 = a.nseg > 1 ? (int)a.N[1] : 0, N2 = a.nseg > 2 ? (int)a.N[2] : 0;
-    const int ngroups = (N0 + N1 + N2) / R;
-    constexpr int WPG = MODE == 3 ? NWV / 2 : NWV;     // waves per group set (MODE 3: per expert half)
-    const int hx = MODE == 3 ? __builtin_amdgcn_readfirstlane(wave / WPG) : 0;   // MODE 3: which slot this wave serves
-    const int nw = (int)gridDim.x * WPG;
-    const int wid = (int)blockIdx.x * WPG + (MODE == 3 ? wave % WPG : wave);
-    int64_t eoff = ROUTE ? 0 : dec_expert_offset(a);   // MoE slice
-    int64_t eoff1 = ROUTE ? 0 : (a.eid1 ? dec_expert_offset(a, a.eid1) : eoff);   // segment 1's (two slots in one launch)
-    const int abytes = K + K / 256 * 4 + K / 16 * 2;
-    const int aoff = MODE == 3 && hx ? (abytes + 15) & ~15 : 0;   // this wave's activation image in LDS
-    const typename T::Lane lc = T::lane_consts(lane);
-
-    auto group_rows = [&](int g, int &seg, int &row0) {
-        const int r = g * R;
-        seg = r < N0 ? 0 : (r < N0 + N1 ? 1 : 2);
-        row0 = seg == 0 ? r : (seg == 1 ? r - N0 : r - N0 - N1);
-    };
-    struct Buf { typename T::W w[NI][RR]; };
-    auto issue = [&](int g, Buf &b) {
-        int seg, row0;
-        group_rows(g, seg, row0);
-        int64_t eo = seg == 1 ? eoff1 : eoff;
-        if constexpr (MODE == 3) {          // the wave's slot (wave-uniform; a select of the two would go to scratch)
-            if (hx) eo = eoff1;
-        }
-        const uint8_t *W = (seg == 0 ? a.W[0] : (seg == 1 ? a.W[1] : a.W[2])) + eo;
-#pragma unroll
-        for (int r = 0; r < RR; ++r) {
-            const uint8_t *rp = (MODE == 1 && r >= R ? a.W2 + eo : W) + (int64_t)(row0 + (r % R)) * RB;
-#pragma unroll
-            for (int i = 0; i < NI; ++i) T::load(rp, nsb, min(lane + 64 * i, npieces - 1), b.w[i][r]);
-        }
-    };
-
-    Buf ba, bb;
-    const int g0 = min(wid, ngroups - 1);
-    if constexpr (PRO != 0) {
-        lean::ActPro<PRO, (MC * 4 + NWV - 1) / NWV, 64 * NWV> pro;
-        pro.load(a);
-        float4 wpre[ROUTE ? 8 : 1][4];
-        const int tid = threadIdx.x;
-        if constexpr (ROUTE) {            // router rows first: they do not wait for the norm (k_moe_route's order)
-            const bool f16 = a.route_wt == KT_F16;
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int i = 16 * tid + 4 * u;
-                    wpre[e][u] = make_float4(0.f, 0.f, 0.f, 0.f);
-                    if (e < a.route_ne && i < K) {
-                        if (f16) {
-                            const uint2 h = *(const uint2 *)((const uint16_t *)a.route_w + (int64_t)e * K + i);
-                            wpre[e][u] = make_float4(h2f(h.x & 0xFFFF), h2f(h.x >> 16), h2f(h.y & 0xFFFF), h2f(h.y >> 16));
-                        } else {
-                            wpre[e][u] = *(const float4 *)((const float *)a.route_w + (int64_t)e * K + i);
-                        }
-                    }
-                }
-        }
-        if constexpr (!XL && !ROUTE && MODE != 3) issue(g0, ba);   // XL: a row's pieces and the prologue's registers do not fit together
-#ifdef KCPP_STAMPS
-        pro.compute(a, lds, st_);
-#else
-        pro.compute(a, lds);
-#endif
-        if constexpr (MODE == 3) {          // slot 1's h follows slot 0's: its Q8_K image behind the first
-            lean::ActPro<PRO, (MC * 4 + NWV - 1) / NWV, 64 * NWV> pro1;
-            pro1.load(a, a.K);
-            pro1.compute(a, lds + ((abytes + 15) & ~15));
-        }
-        if constexpr (ROUTE) {
-            // logits: thread tid's 16 elements (chunk tid, the prologue's row normalised in pro.v[0]), fma over the
-            // 4 float4 in order, wave sums, then ((w0 + w1) + (w2 + w3)) over the first four waves
-            __shared__ float r_part[4][8];
-            __shared__ int r_id[2];
-            __shared__ float r_w[2];
-            const bool f16 = a.route_wt == KT_F16;
-            float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-            if (16 * tid < K) {
-                float xv[16];
-#pragma unroll
-                for (int q = 0; q < 16; ++q) xv[q] = f16 ? h2f(f2h_rn(pro.v[0][q])) : pro.v[0][q];
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    if (e >= a.route_ne) break;
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        if (16 * tid + 4 * u >= K) break;
-                        acc[e] = fmaf(xv[4 * u], wpre[e][u].x, acc[e]);
-                        acc[e] = fmaf(xv[4 * u + 1], wpre[e][u].y, acc[e]);
-                        acc[e] = fmaf(xv[4 * u + 2], wpre[e][u].z, acc[e]);
-                        acc[e] = fmaf(xv[4 * u + 3], wpre[e][u].w, acc[e]);
-                    }
-                }
-            }
-            if (wave < 4) {
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    if (e >= a.route_ne) break;
-                    const float v = wave_sum(acc[e]);
-                    if (lane == 0) r_part[wave][e] = v;
-                }
-            }
-            __syncthreads();
-            if (tid == 0) {
-                float logit[8];
-#pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    logit[e] = e < a.route_ne ? (r_part[0][e] + r_part[1][e]) + (r_part[2][e] + r_part[3][e]) : 0.0f;
-                int id[2];
-                float w[2];
-                moe_topk8(logit, a.route_ne, 2, id, w);
-                r_id[0] = id[0]; r_id[1] = id[1]; r_w[0] = w[0]; r_w[1] = w[1];
-                if (blockIdx.x == 0) {
-                    a.route_ids[0] = id[0]; a.route_ids[1] = id[1];
-                    a.route_wts[0] = w[0]; a.route_wts[1] = w[1];
-                }
-            }
-            __syncthreads();
-            eoff = (int64_t)__builtin_amdgcn_readfirstlane(r_id[0]) * a.ebytes;
-            eoff1 = (int64_t)__builtin_amdgcn_readfirstlane(r_id[1]) * a.ebytes;
-        }
-        if constexpr (XL || ROUTE || MODE == 3) issue(g0, ba);
-    } else {
-        // the column copy covers K <= 16384 at 256 threads; XL's 512 threads x (4, 3) cover K <= 32768
-        lean::ActCopyCol<64 * NWV, XL ? 4 : (16384 / 16 + 64 * NWV - 1) / (64 * NWV), XL ? 3 : (16384 / 256 + 16384 / 32 + 64 * NWV - 1) / (64 * NWV)> cp;
-        cp.load(a.act, K, a.act_mtot > 0 ? a.act_mtot : 1, a.act_col);
-        issue(g0, ba);
-        cp.store(lds, K);
-    }
-    typename T::Act xr[XL ? 1 : NI];
-    if constexpr (!XL) {
-#pragma unroll
-        for (int i = 0; i < NI; ++i) T::act(lds + aoff, K, min(T::sb_of(lane, i), nsb - 1), lc, xr[i]);
-    }
-    RS_STAMP(1);
-
-    float slot[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) slot[r] = 0.0f;
-    int slot_g = -1;
-    auto compute = [&](int g, const Buf &b, int k) {
-        float acc[RR];
-#pragma unroll
-        for (int r = 0; r < RR; ++r) acc[r] = 0.0f;
-#pragma unroll
-        for (int i = 0; i < NI; ++i) {
-            const bool ok = (NI * 64 == npieces) || lane + 64 * i < npieces;
-            typename T::Act xl;
-            if constexpr (XL) T::act(lds + aoff, K, min(T::sb_of(lane, i), nsb - 1), lc, xl);
-#pragma unroll
-            for (int r = 0; r < RR; ++r) {
-                const float p = T::dot(b.w[i][r], XL ? xl : xr[i], lc);
-                acc[r] += ok ? p : 0.0f;
-            }
-            // XL: keep piece i + 1's LDS activation reads behind piece i's dot (hoisted, all NI of them would be live
-            // beside the row's NI in-flight weight pieces and spill)
-            if constexpr (XL) asm volatile("" ::: "memory");
-        }
-#pragma unroll
-        for (int r = 0; r < RR; ++r) acc[r] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_sum_f(acc[r]))));
-        const bool mine = lane == k;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            float v;
-            if constexpr (MODE == 1) v = (acc[r] / (1.0f + expf(-acc[r]))) * acc[R + r];
-            else v = acc[r];
-            slot[r] = mine ? v : slot[r];
-        }
-        slot_g = mine ? g : slot_g;
-#ifdef KCPP_STAMPS
-        if (k == 0) { if (slot[0] == 12345.0f) st_[0] = 0; RS_STAMP(2); }
-#endif
-    };
-    int k = 0;
-    if constexpr (PF) {
-        for (int g = wid; g < ngroups; g += 2 * nw, k += 2) {
-            const int g1 = g + nw, g2 = g + 2 * nw;
-            issue(min(g1, ngroups - 1), bb);
-            compute(g, ba, k);
-            if (g1 >= ngroups) break;
-            issue(min(g2, ngroups - 1), ba);
-            compute(g1, bb, k + 1);
-        }
-    } else {
-        for (int g = wid; g < ngroups; g += nw, ++k) {
-            if (k) issue(g, ba);
-            compute(g, ba, k);
-        }
-    }
-    RS_STAMP(3);
-    if constexpr (MODE == 3) {
-        // the halves meet: lane k of wave w (k-th group of the wave) -> xs[half][w % 4][r][k]; half 0 combines
-        __shared__ float xs[2][4][R][64];
-#pragma unroll
-        for (int r = 0; r < R; ++r) xs[hx][wave % WPG][r][lane] = slot[r];
-        __syncthreads();
-        if (hx) return;
-        const float e0 = a.escale[0], e1 = a.escale[1];
-#pragma unroll
-        for (int r = 0; r < R; ++r) slot[r] = __fadd_rn(__fmul_rn(slot[r], e0), __fmul_rn(xs[1][wave][r][lane], e1));
-    }
-    if (slot_g < 0) return;
-    int seg, row0;
-    group_rows(slot_g, seg, row0);
-    lean::store_group<R, MODE>(a, seg, row0, slot);
-#ifdef KCPP_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    RS_STAMP(4);
-#endif
+    const int KB_BID = (int)blockIdx.x, KB_NBLK = (int)gridDim.x;
+#include "gemv_rs_body.inc"
 }
 
 namespace {
@@ -517,6 +288,71 @@ extern "C" int kcpp_gemv_rs_qkv_mixed(const void *args, void *stream) {
     else if (nia == 1 && nib == 1 && mc == 1) KCPP_QKVM(1, 1, 1);
     else return -3;
 #undef KCPP_QKVM
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// ---------------------------------------------------------------- q (RS layout) + k|v (Q8_0) in one launch
+// Mixtral's Q5_K_M policy keeps attn_k / attn_v in Q8_0 (n_expert == 8) and attn_q in Q5_K, so its q|k|v decode step
+// was two dependent launches of short latency-bound kernels.  Here one grid runs both unchanged: workgroups [0, nA) are
+// the RS q launch (k_gemv_rs's body, mode 2: RoPE + f16 q), [nA, nA + nB) the Q8_0 k|v launch (k_gemv_dec's body,
+// mode 2: RoPE of k + the f16 K / V cache stores), each with its own prologue (Q8_K / Q8_0 activation of the same
+// normalised row) and its own grid size, so every row's arithmetic -- and result -- is the separate launches'.  The
+// bodies are included textually (gemv_rs_body.inc, gemv_dec_body.inc) so that each reads its DecArgs kernel parameter
+// directly (through a reference the parameter is copied to scratch memory and every load goes through it).
+template <int TA, int NIA, int MCA, int ITB>
+__global__ void __launch_bounds__(256) k_gemv_qkv_dual(const DecArgs a, const DecArgs b, int nA) {
+    if ((int)blockIdx.x < nA) {
+        constexpr int TYPE = TA, NI = NIA, R = 2, MODE = 2, PRO = 1, MC = MCA, PF = 0, NWV = 4;
+        constexpr bool XL = false, ROUTE = false;
+        extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+        const int KB_BID = (int)blockIdx.x, KB_NBLK = nA;
+#include "gemv_rs_body.inc"
+    } else {
+        constexpr int TYPE = KT_Q8_0, R = 2, MODE = 2, PRO = 1, MC = 1, IT = ITB;
+        extern __shared__ __attribute__((aligned(16))) uint8_t lds_act[];
+        const int KB_BID = (int)blockIdx.x - nA, KB_NBLK = (int)gridDim.x - nA;
+#define KB_ARGS b
+#include "gemv_dec_body.inc"
+#undef KB_ARGS
+    }
+}
+
+// qa: the RS-layout segments (mode 2, rms_norm prologue) -- pick_rs's launch for them; kv: Q8_0 segments (mode 2) --
+// dispatch_mode<KT_Q8_0>'s.  -3 when the pair is not covered (the caller launches them separately).
+extern "C" int kcpp_gemv_qkv_dual(const void *qargs, int qtype, const void *kvargs, void *stream) {
+    const DecArgs &a = *(const DecArgs *)qargs;
+    const DecArgs &b = *(const DecArgs *)kvargs;
+    if (qtype != KT_Q4_K_RS && qtype != KT_Q5_K_RS && qtype != KT_Q6_K_RS) return -3;
+    if (a.K != b.K || a.K % 256 || a.K > 4096 || !kcpp_rs_supported(qtype, a.K) || a.route_w) return -3;
+    int64_t na_rows = 0;
+    for (int i = 0; i < a.nseg; ++i) {
+        if (a.N[i] % 2) return -5;
+        na_rows += a.N[i];
+    }
+    for (int i = 0; i < b.nseg; ++i)
+        if (b.N[i] % 2) return -5;
+    // RS side: launch_rs<.., R 2, mode 2, PRO 1, .., NWV 4>(a, 512)
+    const int64_t groups = na_rows / 2;
+    int64_t nA = std::min<int64_t>((groups + 3) / 4, 512);
+    nA = std::max<int64_t>(nA, (groups + 255) / 256);
+    const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
+    // Q8_0 side: launch_dec_it<KT_Q8_0, 2, 2, 1, 1, IT>
+    size_t ldsB = 0;
+    const int64_t nB = dec_grid<KT_Q8_0, 2, 1>(b, ldsB);
+    const int64_t upr = b.K / Unit<KT_Q8_0>::ELEMS, itb = (upr + 63) / 64;
+    const size_t lds = std::max<size_t>((size_t)abytes + 16, ldsB);
+    const int nsb = (int)(a.K / 256);
+    const int ppsb = qtype == KT_Q6_K_RS ? 4 : 8;
+    const int nia = (nsb * ppsb + 63) / 64;
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid((unsigned)(nA + nB));
+#define KCPP_DUAL(TA_, NIA_, ITB_) hipLaunchKernelGGL((k_gemv_qkv_dual<TA_, NIA_, 1, ITB_>), grid, dim3(256), lds, s, a, b, (int)nA)
+    if (itb == 2 && nia == 2 && qtype == KT_Q5_K_RS) KCPP_DUAL(KT_Q5_K_RS, 2, 2);      // Mixtral: K 4096
+    else if (itb == 2 && nia == 2 && qtype == KT_Q4_K_RS) KCPP_DUAL(KT_Q4_K_RS, 2, 2);
+    else if (itb == 2 && nia == 1 && qtype == KT_Q6_K_RS) KCPP_DUAL(KT_Q6_K_RS, 1, 2);
+    else return -3;
+#undef KCPP_DUAL
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

@@ -146,15 +146,20 @@ struct kcpp_model {
     bool fused_decode = true;        // single-token path through gemv_dec (norm/rope/KV fused)
     bool q81 = false;                // Q4_1 / Q5_1 weights (Q8_1 activations): decode on the per-op path
     bool q80t = false;               // Q8_0 layer weights in the tile layout KT_Q8_0_T (gemm_q80t.hip) at every batch size
+    bool no_dual_qkv = false;        // KCPP_DUAL_QKV=0: q (RS) and k|v (Q8_0) as two launches (A/B)
     bool no_norm_fold = false;       // KCPP_NORM_FOLD=0: the residual GEMMs never carry the next rms_norm (A/B)
     bool q80_dec = false;            // ... plus their KT_Q8_0 decode copies (KTensor::dec): single tokens on the fused chain
     bool fa_exact = false;           // attention in the reference CPU's order with f16 accumulation (attn_exact.hip)
     int kv_tk = KT_F16, kv_tv = KT_F16;   // cache types (--quantkv: Q8_0 / Q4_0, attn_kvq.hip)
-    hipGraphExec_t g_exec = nullptr;
+    hipGraphExec_t g_exec[2] = {nullptr, nullptr};   // single-token graph per attention regime (dec_short)
     // layer-split engine: the single-token graph bracketed by the stage hand-off kernels (link.hip), captured lazily
     KLink link{};
     bool has_link = false;
-    hipGraphExec_t g_link = nullptr;
+    hipGraphExec_t g_link[2] = {nullptr, nullptr};
+    // single-token attention regime: contexts up to short_max keys take the one-launch kernel (kcpp_flash_attn
+    // force_path 7, no combine); chosen per step from the host-known position, each regime its own graph
+    bool dec_short = false;
+    int short_max = 0;
     hipStream_t side = nullptr;             // second branch of the decode step (independent q|k|v launches)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int64_t weight_bytes = 0;
@@ -163,6 +168,12 @@ struct kcpp_model {
 };
 
 static int ensure_graph(kcpp_model *m);
+static void drop_graphs(kcpp_model *m) {
+    for (int r = 0; r < 2; ++r) {
+        if (m->g_exec[r]) { (void)hipGraphExecDestroy(m->g_exec[r]); m->g_exec[r] = nullptr; }
+        if (m->g_link[r]) { (void)hipGraphExecDestroy(m->g_link[r]); m->g_link[r] = nullptr; }
+    }
+}
 static int launch_argmax(kcpp_model *m, bool step_pos);
 static int launch_pos_step(kcpp_model *m);
 
@@ -448,6 +459,8 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
     // 2 B per weight more, e.g. +1.9 GB on Llama-3-8B Q4_K_M).  Fused q|k|v / gate|up groups get one image each, so
     // the group's GEMM reads one contiguous image.  KCPP_Q6P=0: no images (q6v3).
     m->no_norm_fold = getenv("KCPP_NORM_FOLD") && atoi(getenv("KCPP_NORM_FOLD")) == 0;
+    m->no_dual_qkv = getenv("KCPP_DUAL_QKV") && atoi(getenv("KCPP_DUAL_QKV")) == 0;
+    m->short_max = getenv("KCPP_FA_SHORT") ? atoi(getenv("KCPP_FA_SHORT")) : KCPP_FA_SHORT_MAX;
     if (!(getenv("KCPP_Q6P") && atoi(getenv("KCPP_Q6P")) == 0)) {
         bool ok3 = true;
         auto img_group = [&](KTensor *ts, const int *js, int n) {
@@ -518,8 +531,7 @@ extern "C" kcpp_model *kcpp_model_create(const kcpp_hparams *hp, const int *type
 extern "C" void kcpp_model_free(kcpp_model *m) {
     if (!m) return;
     hipSetDevice(m->device);
-    if (m->g_exec) hipGraphExecDestroy(m->g_exec);
-    if (m->g_link) hipGraphExecDestroy(m->g_link);
+    drop_graphs(m);
     auto F = [](void *p) { if (p) hipFree(p); };
     F(m->moe_trace);
     auto FS = [&](KTensor &t) {
@@ -772,8 +784,7 @@ extern "C" int kcpp_model_set_row_split(kcpp_model *m, int n, const int *devices
     }
     RT_CHECK(hipSetDevice(m->device));
     RT_CHECK(hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
-    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
-    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
+    drop_graphs(m);
     m->use_graphs = false;
     m->fused_decode = false;
     return 0;
@@ -799,8 +810,7 @@ extern "C" int kcpp_model_moe_trace(kcpp_model *m, int enable) {
         RT_CHECK(hipFree(m->moe_trace));
         m->moe_trace = nullptr;
     }
-    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
-    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
+    drop_graphs(m);
     return 0;
 }
 // MoE single-token decode fusions: bit 0 routes inside the two-slot gate|up launch (else k_moe_route), bit 1 runs
@@ -811,8 +821,7 @@ extern "C" int kcpp_model_set_fused_route(kcpp_model *m, int on) {
     RT_CHECK(hipStreamSynchronize(m->stream));
     m->no_fused_route = !(on & 1);
     m->no_pair_down = !(on & 2);
-    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
-    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
+    drop_graphs(m);
     return 0;
 }
 extern "C" int64_t kcpp_model_fused_route_count(kcpp_model *m) { return m->n_fused_route + (m->n_pair_down << 32); }
@@ -832,8 +841,7 @@ extern "C" int kcpp_model_moe_trace_read(kcpp_model *m, int32_t *out, int n) {
 }
 extern "C" int kcpp_model_set_fa_exact(kcpp_model *m, int enable) {
     m->fa_exact = enable != 0;
-    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
-    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
+    drop_graphs(m);
     return 0;
 }
 extern "C" int kcpp_model_set_kv_types(kcpp_model *m, int tk, int tv) {
@@ -856,14 +864,12 @@ extern "C" int kcpp_model_set_kv_types(kcpp_model *m, int tk, int tv) {
         RT_CHECK(hipMemset(L.vc, 0, vb));
     }
     m->kv_tk = tk; m->kv_tv = tv;
-    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
-    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
+    drop_graphs(m);
     return 0;
 }
 extern "C" int kcpp_model_set_fused_decode(kcpp_model *m, int enable) {
     m->fused_decode = enable != 0 && m->lanes.empty();
-    if (m->g_exec) { (void)hipGraphExecDestroy(m->g_exec); m->g_exec = nullptr; }
-    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
+    drop_graphs(m);
     return 0;
 }
 
@@ -1261,6 +1267,11 @@ static int forward_layers_dec(kcpp_model *m) {
             mixed_rc = kcpp_gemv_rs_qkv_mixed(&c, s);
             if (mixed_rc != -3 && mixed_rc != -5) RC(mixed_rc);
         }
+        if (mixed_rc != 0 && nq == 2 && qty[1] == KT_Q8_0 && !m->no_dual_qkv) {
+            // q in an RS layout + k|v in Q8_0 (Mixtral's Q5_K_M policy): both launches' workgroups in one grid
+            mixed_rc = kcpp_gemv_qkv_dual(&qa[0], qty[0], &qa[1], s);
+            if (mixed_rc != -3 && mixed_rc != -5) RC(mixed_rc);
+        }
         if (mixed_rc != 0)
             for (int i = 0; i < nq; ++i) RC(kcpp_gemv_dec(qty[i], &qa[i], 2, 1, 2, s));
         // --- attention over the cache (f32 output); wo quantizes it in its own prologue (PRO 2: the Q8_K /
@@ -1270,7 +1281,7 @@ static int forward_layers_dec(kcpp_model *m) {
             RC(kcpp_flash_attn_exact(m->q16, L.kc, L.vc, m->attn, 1, (int)H, (int)HKV, (int)D, 0, m->pos_dev, kq_scale, s));
         else
             RC(kcpp_flash_attn(m->q16, L.kc, L.vc, m->attn, nullptr, m->fa_ws, 1, (int)H, (int)HKV, (int)D, 0, m->pos_dev,
-                               hp.n_ctx, kq_scale, 1, s));
+                               hp.n_ctx, kq_scale, m->dec_short && D == 128 ? 7 : 1, s));
         {   // x += wo . attn
             DecArgs a;
             memset(&a, 0, sizeof a);
@@ -1543,10 +1554,11 @@ static int set_pos(kcpp_model *m, int n_past) {
 // one single-token step at n_past (tok_dev already set): graph replay or eager; advances pos_val on success
 static int step_one(kcpp_model *m, int n_past) {
     m->pos_val = m->pos_val == n_past ? n_past : -1;
+    m->dec_short = n_past + 1 <= m->short_max;
     if (m->use_graphs) {
         RC(ensure_graph(m));
         RC(set_pos(m, n_past));
-        const hipError_t e = hipGraphLaunch(m->g_exec, m->stream);
+        const hipError_t e = hipGraphLaunch(m->g_exec[m->dec_short], m->stream);
         if (e != hipSuccess) { m->pos_val = -1; RT_CHECK(e); }
     } else {
         RC(set_pos(m, n_past));
@@ -1559,13 +1571,13 @@ static int step_one(kcpp_model *m, int n_past) {
 
 // single-token graph: embedding of tok_dev, layers at position pos_dev, head, argmax, pos_dev + 1
 static int ensure_graph(kcpp_model *m) {
-    if (m->g_exec) return 0;
+    if (m->g_exec[m->dec_short]) return 0;
     hipGraph_t g;
     RT_CHECK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
     int rc = decode_step_dev(m);
     hipError_t e = hipStreamEndCapture(m->stream, &g);
     if (rc || e != hipSuccess) { g_err = "graph capture failed"; return rc ? rc : -3; }
-    RT_CHECK(hipGraphInstantiate(&m->g_exec, g, nullptr, nullptr, 0));
+    RT_CHECK(hipGraphInstantiate(&m->g_exec[m->dec_short], g, nullptr, nullptr, 0));
     hipGraphDestroy(g);
     return 0;
 }
@@ -1573,14 +1585,15 @@ static int ensure_graph(kcpp_model *m) {
 // the linked single-token step (layer-split engine, expose.cpp): k_link_wait (pull this stage's input from the
 // producer stage, device-side), the step, k_link_publish -- one graph replay, no host call between stages
 int kcpp_model_set_link(kcpp_model *m, const KLink *L) {
-    if (m->g_link) { (void)hipGraphExecDestroy(m->g_link); m->g_link = nullptr; }
+    for (auto &gx : m->g_link)
+        if (gx) { (void)hipGraphExecDestroy(gx); gx = nullptr; }
     m->has_link = L != nullptr;
     if (L) m->link = *L;
     return 0;
 }
 
 static int ensure_graph_linked(kcpp_model *m) {
-    if (m->g_link) return 0;
+    if (m->g_link[m->dec_short]) return 0;
     hipGraph_t g;
     RT_CHECK(hipStreamBeginCapture(m->stream, hipStreamCaptureModeThreadLocal));
     int rc = kcpp_link_wait(m->link, m->stream);
@@ -1588,7 +1601,7 @@ static int ensure_graph_linked(kcpp_model *m) {
     if (!rc) rc = kcpp_link_publish(m->link, m->stream);
     hipError_t e = hipStreamEndCapture(m->stream, &g);
     if (rc || e != hipSuccess) { g_err = "linked graph capture failed"; return rc ? rc : -3; }
-    RT_CHECK(hipGraphInstantiate(&m->g_link, g, nullptr, nullptr, 0));
+    RT_CHECK(hipGraphInstantiate(&m->g_link[m->dec_short], g, nullptr, nullptr, 0));
     hipGraphDestroy(g);
     return 0;
 }
@@ -1598,9 +1611,10 @@ int kcpp_model_step_linked(kcpp_model *m, int n_past) {
     if (n_past + 1 > m->hp.n_ctx) { g_err = "context overflow"; return -2; }
     RT_CHECK(hipSetDevice(m->device));
     m->pos_val = m->pos_val == n_past ? n_past : -1;
+    m->dec_short = n_past + 1 <= m->short_max;
     RC(ensure_graph_linked(m));
     RC(set_pos(m, n_past));
-    const hipError_t e = hipGraphLaunch(m->g_link, m->stream);
+    const hipError_t e = hipGraphLaunch(m->g_link[m->dec_short], m->stream);
     if (e != hipSuccess) { m->pos_val = -1; RT_CHECK(e); }
     m->pos_val = n_past + 1;
     return 0;

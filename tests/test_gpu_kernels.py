@@ -315,11 +315,12 @@ def test_flash_attn_vs_oracle_f32_accum(env, T, n_past, path):
         np.testing.assert_allclose(got, want, rtol=2e-5, atol=2e-6)
 
 
-@pytest.mark.parametrize("variant", [3, 5])
+@pytest.mark.parametrize("variant", [3, 5, 8])
 @pytest.mark.parametrize("H,HKV", [(32, 8), (32, 32), (64, 8), (16, 8), (32, 4), (8, 4), (64, 64)])
 def test_fa_dec4_split_counts(env, H, HKV, variant):
     """the decode pairs (5: k_fa_dec5 + k_fa_comb4, production: 64-key chunks dealt round-robin over the splits, rows
-    clamped to the cache; 3: round 5's k_fa_dec4, contiguous key ranges) over split counts 4..64 (256 / HKV rounded down
+    clamped to the cache; 3: round 5's k_fa_dec4, contiguous key ranges; 8: the short-context single launch, one
+    workgroup per kv head over every key) over split counts 4..64 (256 / HKV rounded down
     to a power of two) and GQA groups 1..8: back-to-back calls whose key counts differ (empty, partial and full splits,
     a cache whose rows past the keys hold NaN / inf, which must not leak into the result) are reproducible bit for bit
     and match the f32-accumulation oracle."""
