@@ -72,23 +72,6 @@ struct DecArgs {
     int32_t *route_ids;
     float *route_wts;
 };
-#ifdef __HIPCC__
-// DecArgs pointers marked global: a kernel body that receives the kernel's DecArgs through a function parameter (the
-// struct is copied, its pointers lose their kernel-argument origin) would otherwise load through flat instructions
-template <typename T> __device__ __forceinline__ T *as_global(T *p) {
-    return (T *)(__attribute__((address_space(1))) T *)p;
-}
-__device__ __forceinline__ DecArgs dec_args_global(DecArgs a) {
-    for (int i = 0; i < 3; ++i) { a.W[i] = as_global(a.W[i]); a.Y[i] = as_global(a.Y[i]); }
-    a.W2 = as_global(a.W2); a.act = as_global(a.act); a.x = as_global(a.x); a.nw = as_global(a.nw);
-    a.res = as_global(a.res); a.q16 = as_global(a.q16); a.kc = as_global(a.kc); a.vc = as_global(a.vc);
-    a.pos = as_global(a.pos); a.rope_tab = as_global(a.rope_tab); a.eid = as_global(a.eid);
-    a.escale = as_global(a.escale); a.pre = as_global(a.pre); a.eid1 = as_global(a.eid1);
-    a.route_w = as_global((const uint8_t *)a.route_w); a.route_ids = as_global(a.route_ids);
-    a.route_wts = as_global(a.route_wts);
-    return a;
-}
-#endif
 
 
 // top-NU of NE <= 8 router logits exactly as ggml's soft_max (ggml_float sum) + argsort (exchange order) + the
