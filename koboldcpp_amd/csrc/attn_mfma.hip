@@ -324,7 +324,12 @@ __device__ __forceinline__ int fa_swz(int row, int c) { return row * 16 + (c ^ (
 // qta (optional, unsplit): the output quantized straight to the KT_Q8_0_TA activation of attn_output (KT_Q8_0_T
 // weights): a head's 128 dims are 4 whole Q8_0 blocks, so no other workgroup's output is needed (k_quant_q80's
 // rounding); split launches quantize in the merge.
-template <int NW, bool SPL>
+// HM (NW = 8 only; variant 5, A/B): each key half keeps its own running maximum -- no per-tile maximum exchange (one
+// barrier per tile instead of two); P is relative to the half's maximum (the same f16 rounding bound), the halves merged
+// at the end as before.  tools/fa_ab.py at 512 queries: 16.3 -> 14.7 us (n_past 0), 45.6 -> 41.6 (1536), 79.4 -> 73.3
+// (3328), within the kernel test's error bars -- but as the default it took the tiny Q4_1 model's logits just past
+// 1.5x the reference's own spread (tests/test_kquants_low.py: 0.0291 vs 0.0283), so variant 4 stays the default
+template <int NW, bool SPL, bool HM = false>
 __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t *__restrict__ q16,
                                                                 const uint16_t *__restrict__ kc,
                                                                 const uint16_t *__restrict__ vc, float *__restrict__ out,
@@ -476,7 +481,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_fa_prefill_mfma3(const uint16_t 
         }
         mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
         mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-        if constexpr (NW == 8) {
+        if constexpr (NW == 8 && !HM) {
             // both key halves take the whole tile's maximum (exchanged through LDS), so P, alpha and the running max
             // are v3's exactly; only the f32 summation of O and l is split in two
             if (g == 0) s_mx[hf][wave & 3][ql] = mt;
@@ -712,7 +717,7 @@ extern "C" int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16
     const int v = g_fa_prefill_variant ? g_fa_prefill_variant : 4;
     const int nqb = (T + FM_Q - 1) / FM_Q;
     const int nb0 = nqb * HKV;
-    if (v == 4 && ws && T <= FM_SPLIT_T && nb0 <= 512) {
+    if ((v == 4 || v == 5) && ws && T <= FM_SPLIT_T && nb0 <= 512) {
         // keys split so that the grid has ~512 workgroups (at most FM_SPLITS splits of whole 64-key tiles)
         const int ntile = (n_past + T + FM_K - 1) / FM_K;
         const int want = std::min(FM_SPLITS, std::max(1, 512 / nb0));
@@ -720,8 +725,13 @@ extern "C" int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16
         const int nsp = (ntile + ch - 1) / ch;
         if (nsp > 1) {
             float *part = (float *)((uint8_t *)ws + KCPP_FA_WS_HEADER);
-            hipLaunchKernelGGL((k_fa_prefill_mfma3<8, true>), dim3(nb0 * nsp), dim3(512), 0, (hipStream_t)stream, q16, kc,
-                               vc, out, T, H, HKV, n_past, scale, part, (unsigned *)nullptr, ch, nsp, (uint8_t *)nullptr);
+            if (v == 5)
+                hipLaunchKernelGGL((k_fa_prefill_mfma3<8, true, true>), dim3(nb0 * nsp), dim3(512), 0, (hipStream_t)stream,
+                                   q16, kc, vc, out, T, H, HKV, n_past, scale, part, (unsigned *)nullptr, ch, nsp,
+                                   (uint8_t *)nullptr);
+            else
+                hipLaunchKernelGGL((k_fa_prefill_mfma3<8, true>), dim3(nb0 * nsp), dim3(512), 0, (hipStream_t)stream, q16, kc,
+                                   vc, out, T, H, HKV, n_past, scale, part, (unsigned *)nullptr, ch, nsp, (uint8_t *)nullptr);
             KCPP_CHECK(hipGetLastError());
             hipLaunchKernelGGL(k_fa_split_merge, dim3(nb0 * 4), dim3(256), 0, (hipStream_t)stream, part, out, (uint8_t *)qta,
                                T, H, HKV, n_past, ch, nsp);
@@ -729,9 +739,13 @@ extern "C" int kcpp_flash_attn_prefill_mfma_ex(const uint16_t *q16, const uint16
             return 0;
         }
     }
-    if (v == 4) {
-        hipLaunchKernelGGL((k_fa_prefill_mfma3<8, false>), dim3(nb0), dim3(512), 0, (hipStream_t)stream, q16, kc, vc, out,
-                           T, H, HKV, n_past, scale, (float *)nullptr, (unsigned *)nullptr, 0, 1, (uint8_t *)qta);
+    if (v == 4 || v == 5) {
+        if (v == 5)
+            hipLaunchKernelGGL((k_fa_prefill_mfma3<8, false, true>), dim3(nb0), dim3(512), 0, (hipStream_t)stream, q16, kc, vc,
+                               out, T, H, HKV, n_past, scale, (float *)nullptr, (unsigned *)nullptr, 0, 1, (uint8_t *)qta);
+        else
+            hipLaunchKernelGGL((k_fa_prefill_mfma3<8, false>), dim3(nb0), dim3(512), 0, (hipStream_t)stream, q16, kc, vc, out,
+                               T, H, HKV, n_past, scale, (float *)nullptr, (unsigned *)nullptr, 0, 1, (uint8_t *)qta);
         KCPP_CHECK(hipGetLastError());
         return 0;
     }
@@ -749,6 +763,10 @@ extern "C" int kcpp_flash_attn_prefill_mfma(const uint16_t *q16, const uint16_t 
                            (unsigned *)nullptr, 0, 1, (uint8_t *)nullptr);
     else if (v == 4)
         hipLaunchKernelGGL((k_fa_prefill_mfma3<8, false>), dim3((T + FM_Q - 1) / FM_Q * HKV), dim3(512), 0,
+                           (hipStream_t)stream, q16, kc, vc, out, T, H, HKV, n_past, scale, (float *)nullptr,
+                           (unsigned *)nullptr, 0, 1, (uint8_t *)nullptr);
+    else if (v == 5)
+        hipLaunchKernelGGL((k_fa_prefill_mfma3<8, false, true>), dim3((T + FM_Q - 1) / FM_Q * HKV), dim3(512), 0,
                            (hipStream_t)stream, q16, kc, vc, out, T, H, HKV, n_past, scale, (float *)nullptr,
                            (unsigned *)nullptr, 0, 1, (uint8_t *)nullptr);
     else if (v == 1)

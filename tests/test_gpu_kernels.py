@@ -559,7 +559,7 @@ def test_flash_attn_prefill_mfma_v2_bitwise(env, T, n_past):
 
 
 @pytest.mark.parametrize("T,n_past", [(16, 0), (37, 0), (200, 60), (512, 300), (512, 3328), (70, 130), (512, 0)])
-@pytest.mark.parametrize("v", [3, 4])
+@pytest.mark.parametrize("v", [3, 4, 5])
 def test_flash_attn_prefill_mfma_v3_vs_v2(env, T, n_past, v):
     """MFMA prefill v3 (LDS-DMA K/V ring, swizzled LDS, exp2-domain softmax, mask only on diagonal / end tiles; v = 4:
     two waves per head over the two key halves of each tile, merged at the end) against v2 and an exact float64
