@@ -316,14 +316,20 @@ static void init_links(Engine &e) {
         const size_t p = (s + S - 1) % S, c = (s + 1) % S;
         if (!reach(e.devs[s], e.devs[p]) || !reach(e.devs[s], e.devs[c])) return;
     }
+    // flag blocks in fine-grained device memory: a peer GPU's flag stores are visible to the polling kernel without a
+    // kernel boundary (coarse-grained lines may sit in the owner's L2 until one); stages sharing one GPU could do with
+    // coarse-grained memory, but one rule keeps the multi-GPU path the one the tests exercise
     e.link_blk.assign(S, nullptr);
     for (size_t s = 0; s < S; ++s) {
         hipSetDevice(e.devs[s]);
-        if (hipMalloc(&e.link_blk[s], 256) != hipSuccess || hipMemset(e.link_blk[s], 0, 256) != hipSuccess ||
-            hipDeviceSynchronize() != hipSuccess)
-            return;
+        if (hipExtMallocWithFlags(&e.link_blk[s], 256, hipDeviceMallocFinegrained) != hipSuccess) {
+            (void)hipGetLastError();
+            e.link_blk[s] = nullptr;
+            return;                               // no fine-grained memory: the event-ordered hand-offs
+        }
+        if (hipMemset(e.link_blk[s], 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return;
     }
-    // words of stage s's block: [0] step counter, [16] ready_in, [32] copied_out
+    // words of stage s's block: [0] step counter, [16] ready_in, [32] copied_out, [48] error (a wait that gave up)
     auto word = [&](size_t s, int i) { return (unsigned *)e.link_blk[s] + i; };
     for (size_t s = 0; s < S; ++s) {
         const size_t p = (s + S - 1) % S, c = (s + 1) % S;
@@ -343,9 +349,27 @@ static void init_links(Engine &e) {
             L.n = e.hp.n_embd;
         }
         L.out_lag = s == S - 1 ? 0 : 1;
+        L.err = word(s, 48);
         if (kcpp_model_set_link(e.stages[s], &L)) return;
     }
     e.linked = true;
+}
+
+// after a sync: did any linked wait give up (k_link_wait's bounded poll)?  Reported once, cleared.
+static bool link_errors(Engine &e) {
+    if (!e.linked) return false;
+    bool bad = false;
+    for (size_t s = 0; s < e.link_blk.size(); ++s) {
+        unsigned w = 0;
+        hipSetDevice(e.devs[s]);
+        if (hipMemcpy(&w, (unsigned *)e.link_blk[s] + 48, 4, hipMemcpyDeviceToHost) != hipSuccess || w) {
+            fprintf(stderr, "[kcpp] linked hand-off: stage %zu gave up waiting at step %u\n", s, w);
+            const unsigned z = 0;
+            (void)hipMemcpy((unsigned *)e.link_blk[s] + 48, &z, 4, hipMemcpyHostToDevice);
+            bad = true;
+        }
+    }
+    return bad;
 }
 
 // events for the copy handoff, and an RCCL clique when every stage sits on its own device (RCCL refuses two
@@ -1015,6 +1039,7 @@ generation_outputs generate(const generation_inputs in) {
         if (frc) { fprintf(stderr, "[kcpp] generate: decode failed\n"); break; }
         e->ctx.push_back(t);
     }
+    if (link_errors(*e)) fprintf(stderr, "[kcpp] generate: a linked hand-off timed out; the tokens after it are invalid\n");
     if (getenv("KCPP_GEN_TIMING"))
         fprintf(stderr, "[kcpp] generate timing: %d tokens, sample %.3f ms/token, step enqueue %.3f ms/token\n", n_gen,
                 tm_sample / std::max(1, n_gen), tm_step / std::max(1, n_gen));
@@ -1139,6 +1164,7 @@ int kcpp_engine_bench(const kcpp_hparams *hp, const int *types, int n_types, int
     }
     te = std::chrono::steady_clock::now();                             // host: every step enqueued
     if (sync_all()) return -6;                                         // the last token computed and home
+    if (link_errors(*e)) return -7;
     const auto t3 = std::chrono::steady_clock::now();
     if (getenv("KCPP_ENGINE_HOST_TIMING"))
         fprintf(stderr, "[kcpp] engine_bench: %zu stages, host enqueue %.1f us/token, wall %.1f us/token\n",

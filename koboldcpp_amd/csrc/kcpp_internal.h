@@ -161,6 +161,7 @@ struct KLink {
     const int32_t *src_tok;       // stage 0: the last stage's greedy token
     int32_t *dst_tok;
     int in_lag, out_lag;
+    unsigned *err;                // local: set when a wait gave up (bounded poll); the host checks it after a sync
 };
 int kcpp_link_wait(const KLink &L, hipStream_t s);
 int kcpp_link_publish(const KLink &L, hipStream_t s);

@@ -17,9 +17,14 @@
 //
 // Every wait is on a word that an EARLIER enqueued kernel sets (the host enqueues stages in pipeline order), so
 // in-order queues never hold a waiter in front of what it waits for.  Flags are polled with system-scope relaxed
-// loads (cross-device words over xGMI) with s_sleep between polls, by one lane.
+// loads (cross-device words over xGMI) with s_sleep between polls, by one lane; the flag blocks are fine-grained
+// device memory (expose.cpp init_links), so a peer's stores are seen without waiting for a kernel boundary.  A wait
+// gives up after ~2 s (LINK_POLL_MAX polls), sets the stage's error word and lets the step run: a lost flag then
+// costs a wrong step the host reports (expose.cpp link_errors), never a GPU that spins forever.
 #include "kcpp_common.h"
 #include "kcpp_internal.h"
+
+#define LINK_POLL_MAX (1u << 24)     // x s_sleep(2) (~128 clocks): ~1-2 s
 
 __global__ void __launch_bounds__(256) k_link_wait(const KLink L) {
     __shared__ unsigned s_step;
@@ -27,10 +32,14 @@ __global__ void __launch_bounds__(256) k_link_wait(const KLink L) {
     if (tid == 0) {
         const unsigned step = __hip_atomic_load(L.stepctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
         __hip_atomic_store(L.stepctr, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (__hip_atomic_load(L.ready_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + (unsigned)L.in_lag < step)
+        unsigned polls = 0;
+        while (__hip_atomic_load(L.ready_in, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + (unsigned)L.in_lag < step &&
+               ++polls < LINK_POLL_MAX)
             __builtin_amdgcn_s_sleep(2);
-        while (__hip_atomic_load(L.copied_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + (unsigned)L.out_lag < step)
+        while (__hip_atomic_load(L.copied_out, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + (unsigned)L.out_lag < step &&
+               ++polls < LINK_POLL_MAX)
             __builtin_amdgcn_s_sleep(2);
+        if (polls >= LINK_POLL_MAX && L.err) __hip_atomic_store(L.err, step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         s_step = step;
     }
