@@ -264,11 +264,16 @@ void ggml_cuda_set_mul_mat_q(bool mul_mat_q);
 
 /* diagnostics (this backend only): nodes executed by the last graph_compute, and the last dispatch error */
 int kcpp_ggml_backend_last_nodes(void);
+/* of those, the nodes that ran inside a fused launch (RMS_NORM+MUL, MUL_MAT+ADD, the SiLU GLU; 0 with KCPP_B1_UNFUSED=1) */
+int kcpp_ggml_backend_last_fused(void);
 /* device bytes held in separate native weight images (0 when every weight sits in a weight buffer: those are
  * converted in place, one copy of the model) */
 int64_t kcpp_ggml_backend_image_bytes(void);
 /* strict-parity attention for this backend's FLASH_ATTN_EXT nodes (default from KCPP_FA_EXACT at init) */
 int kcpp_ggml_backend_set_fa_exact(kggml_backend_t backend, int on);
+/* node fusion (RMS_NORM+MUL, MUL_MAT+ADD, the SiLU GLU at one token) on / off for this backend (default on; off with
+ * KCPP_B1_UNFUSED=1 or KCPP_B1_NOFUSE=1 at init) */
+int kcpp_ggml_backend_set_fusion(kggml_backend_t backend, int on);
 const char *kcpp_ggml_backend_last_error(void);
 
 #ifdef __cplusplus

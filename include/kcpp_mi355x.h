@@ -257,6 +257,10 @@ int kcpp_ggml_unary(int op, const void *a, const kcpp_tdesc *ta, void *d, const 
 int kcpp_ggml_cpy(int stype, const void *src, const kcpp_tdesc *ts, int dtype, void *dst, const kcpp_tdesc *td,
                   void *stream);
 int kcpp_ggml_rms_norm(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdesc *ty, float eps, void *stream);
+/* b1 fusion: rms_norm then MUL by the broadcast weight w (build_norm), one launch writing both outputs: r = the norm
+ * node's tensor, y = the MUL node's; each element the two nodes' bits.  Rows contiguous (nb[0] = 4), else -2 */
+int kcpp_ggml_rms_norm_mul(const void *x, const kcpp_tdesc *tx, void *r, const kcpp_tdesc *tr, void *y,
+                           const kcpp_tdesc *ty, const float *w, const kcpp_tdesc *tw, float eps, void *stream);
 /* GGML_OP_ROPE f32, mode 0 (NORM) or 2 (NEOX); pos int32 [ne2]; freq_factors may be null */
 int kcpp_ggml_rope(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdesc *ty, const int32_t *pos,
                    const float *freq_factors, int n_dims, int mode, int n_ctx_orig, float freq_base, float freq_scale,

@@ -152,15 +152,22 @@ struct ActCopyCol {
 };
 
 // store R parked results of group slot_g (rows row0.. of segment seg)
-template <int R, int MODE>
-__device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0, const float (&slot)[R]) {
+template <int R, int MODE, bool AUX = false>
+__device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0, const float (&slot)[R],
+                                            float *aux0 = nullptr) {
     if constexpr (MODE != 2) {
         float *Y = seg == 0 ? a.Y[0] : (seg == 1 ? a.Y[1] : a.Y[2]);
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             float v = (MODE == 0 && a.escale) ? __fmul_rn(slot[r], a.escale[0]) : slot[r];
             if (MODE == 0 && a.pre) v = __fadd_rn(a.pre[row0 + r], v);
-            Y[row0 + r] = ((MODE == 0 || MODE == 3) && a.res) ? __fadd_rn(v, a.res[row0 + r]) : v;
+            if constexpr (AUX && MODE == 0) {      // the ggml plugin's MUL_MAT -> ADD: the product node's tensor too
+                const float rv = a.res ? a.res[row0 + r] : 0.0f;
+                aux0[row0 + r] = v;
+                Y[row0 + r] = a.res ? __fadd_rn(v, rv) : v;
+            } else {
+                Y[row0 + r] = ((MODE == 0 || MODE == 3) && a.res) ? __fadd_rn(v, a.res[row0 + r]) : v;
+            }
         }
     } else {
         const int role = seg == 0 ? a.role[0] : (seg == 1 ? a.role[1] : a.role[2]);

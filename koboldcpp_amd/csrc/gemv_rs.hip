@@ -65,11 +65,27 @@ template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 
 __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const int KB_BID = (int)blockIdx.x, KB_NBLK = (int)gridDim.x;
+    constexpr bool AUX = false;
+    float *const aux0 = nullptr, *const aux1 = nullptr, *const aux2 = nullptr;
+#include "gemv_rs_body.inc"
+}
+// the ggml plugin's fused nodes (AuxOut): the same body storing the intermediate nodes' tensors too -- MODE 0 the
+// product before the residual, MODE 1 gate, silu(gate) and up beside the GLU product
+template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV>
+__global__ void __launch_bounds__(64 * NWV) k_gemv_rs_aux(const DecArgs a, const AuxOut o) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const int KB_BID = (int)blockIdx.x, KB_NBLK = (int)gridDim.x;
+    constexpr bool XL = false, ROUTE = false, AUX = true;
+    float *const aux0 = o.p0, *const aux1 = o.p1, *const aux2 = o.p2;
 #include "gemv_rs_body.inc"
 }
 
 namespace {
-template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4, bool XL = false, bool ROUTE = false>
+// the ggml plugin's AuxOut for the launches below (kcpp_gemv_rs_aux; null: the runtime's plain launches)
+thread_local const AuxOut *g_rs_aux = nullptr;
+
+template <int TYPE, int NI, int R, int MODE, int PRO, int MC, int PF, int NWV = 4, bool XL = false, bool ROUTE = false,
+          bool AUX = false>
 int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
     int64_t ntot = 0;
     for (int i = 0; i < a.nseg; ++i) {
@@ -82,8 +98,14 @@ int launch_rs(const DecArgs &a, int max_blocks, hipStream_t s) {
     nblk = std::max<int64_t>(nblk, (groups + 64 * WPG - 1) / (64 * WPG));    // <= 64 groups per wave (result slots)
     const int64_t abytes = a.K + a.K / 256 * 4 + a.K / 16 * 2;
     const int64_t lbytes = MODE == 3 ? 2 * ((abytes + 15) & ~(int64_t)15) : abytes;
-    hipLaunchKernelGGL((k_gemv_rs<TYPE, NI, R, MODE, PRO, MC, PF, NWV, XL, ROUTE>), dim3((unsigned)nblk), dim3(64 * NWV),
-                       (size_t)lbytes + 16, s, a);
+    if constexpr (AUX) {
+        static_assert(!XL && !ROUTE, "AUX instances: plain single-token launches");
+        hipLaunchKernelGGL((k_gemv_rs_aux<TYPE, NI, R, MODE, PRO, MC, PF, NWV>), dim3((unsigned)nblk), dim3(64 * NWV),
+                           (size_t)lbytes + 16, s, a, *g_rs_aux);
+    } else {
+        hipLaunchKernelGGL((k_gemv_rs<TYPE, NI, R, MODE, PRO, MC, PF, NWV, XL, ROUTE>), dim3((unsigned)nblk), dim3(64 * NWV),
+                           (size_t)lbytes + 16, s, a);
+    }
     KCPP_CHECK(hipGetLastError());
     return 0;
 }
@@ -109,6 +131,15 @@ int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
     // down Q4_K 11.3 -> 9.7 and Q6_K 13.6 -> 12.2 (no PF: two rows per wave, both in flight), wo 5.4 -> 4.7; in the
     // bench's token graph down 12.0 / 13.7 -> 10.0 / 12.4 us, wo 5.3 -> 5.1, GLU unchanged: 577 -> 600 tok/s.  The
     // q|k|v launches stay at 4 waves (8: 6.8 -> 7.4 us, 592 tok/s).
+    // the ggml plugin's fused nodes (aux: the intermediate nodes' tensors stored too), separate instances so the
+    // runtime's launches carry none of it: MUL_MAT -> ADD as the plain single-token launch below (quantize prologue,
+    // 8 waves), the SiLU GLU as KCPP_RS_P(2)'s mode 1
+    if (g_rs_aux) {
+        if (mode == 0 && pro == 2 && ntot <= 16384) return launch_rs<TYPE, NI, 1, 0, 2, MC, 0, 8, false, false, true>(a, 256, s);
+        if (mode == 1 && pro == 2 && a.nseg == 1 && !a.eid && !a.route_w)
+            return launch_rs<TYPE, NI, 1, 1, 2, MC, 1, 4, false, false, true>(a, 512, s);
+        return -3;
+    }
     if (mode == 1 && pro == 1 && R == 1) {
         if (a.route_w) {                  // routed two-slot GLU (MoE decode): K <= 4096 (one prologue chunk), NE <= 8
             if constexpr (MC == 1) {
@@ -142,6 +173,7 @@ int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
 // the shape rounds up to.
 template <int TYPE, int NI>
 int pick_rs_xl(const DecArgs &a, int mode, int pro, hipStream_t s) {
+    if (g_rs_aux) return -3;
     constexpr int MC = TYPE == KT_Q6_K_RS ? NI : NI / 2;        // ceil(K / 4096) at the ceiling
     if (mode == 0) {
         if (pro == 2) return launch_rs<TYPE, NI, 1, 0, 2, MC, 0, 8, true>(a, 256, s);
@@ -304,7 +336,8 @@ template <int TA, int NIA, int MCA, int ITB>
 __global__ void __launch_bounds__(256) k_gemv_qkv_dual(const DecArgs a, const DecArgs b, int nA) {
     if ((int)blockIdx.x < nA) {
         constexpr int TYPE = TA, NI = NIA, R = 2, MODE = 2, PRO = 1, MC = MCA, PF = 0, NWV = 4;
-        constexpr bool XL = false, ROUTE = false;
+        constexpr bool XL = false, ROUTE = false, AUX = false;
+        float *const aux0 = nullptr, *const aux1 = nullptr, *const aux2 = nullptr;
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
         const int KB_BID = (int)blockIdx.x, KB_NBLK = nA;
 #include "gemv_rs_body.inc"
@@ -429,4 +462,14 @@ extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void 
         }
     }
     return -3;
+}
+
+// the ggml plugin's fused nodes: kcpp_gemv_rs's launch (modes 0 and 1, quantize prologue, one segment) through the AUX
+// instances, which also store the intermediate nodes' tensors (AuxOut); -3 where no AUX instance covers the shape
+extern "C" int kcpp_gemv_rs_aux(int type, const void *args, int mode, const AuxOut *aux, void *stream) {
+    if (!aux || !aux->p0 || (mode == 1 && (!aux->p1 || !aux->p2)) || (mode != 0 && mode != 1)) return -3;
+    g_rs_aux = aux;
+    const int rc = kcpp_gemv_rs(type, args, mode, 2, stream);
+    g_rs_aux = nullptr;
+    return rc;
 }

@@ -49,6 +49,7 @@ namespace {
 
 std::string g_last_error;
 int g_last_nodes = 0;
+int g_last_fused = 0;     // of those, nodes that ran inside a fused launch (fuse_at)
 bool g_mul_mat_q = true;
 
 // ggml type traits (ggml.c type_traits: blck_size, type_size, is_quantized) for every ggml_type id
@@ -340,6 +341,8 @@ struct BackendCtx {
     // single-token MUL_MAT on the fused mat-vec (quantize prologue) and FLASH_ATTN_EXT on the split decode kernel;
     // KCPP_B1_UNFUSED=1: one kernel per step as before (A/B)
     bool no_fused_mv = getenv("KCPP_B1_UNFUSED") && atoi(getenv("KCPP_B1_UNFUSED")) != 0;
+    // node fusion (fuse_at): off with KCPP_B1_UNFUSED or KCPP_B1_NOFUSE, or kcpp_ggml_backend_set_fusion(be, 0)
+    bool no_fuse = no_fused_mv || (getenv("KCPP_B1_NOFUSE") && atoi(getenv("KCPP_B1_NOFUSE")) != 0);
 };
 
 // the native image of weight w for target layout `tt` (kcpp type id); w itself when the layouts coincide
@@ -986,6 +989,144 @@ bool compute_node(BackendCtx *bc, kggml_tensor *n) {
     }
 }
 
+// ------------------------------------------------------------------ node fusion (decode)
+// Three node sequences of every llama-family token graph (build_norm, the residual ADD after wo / ffn_down, build_ffn's
+// parallel SiLU GLU) run as one launch each.  A fused launch still writes EVERY node's output tensor, per element in
+// node order, so the graph's tensors hold afterwards exactly what the node-by-node sequence leaves: no use counting is
+// needed (a split view -- ggml_graph_view, ggml.c:19059 -- cannot see consumers in other splits, and an OUTPUT-flagged
+// intermediate stays materialised).  What the fusion does need: the nodes consecutive in the graph, every output a
+// plain contiguous f32 vector of one shape, and no output overlapping an input that other workgroups still read (the
+// allocator may hand a dead input's bytes to a later node); outputs may coincide exactly with each other or with an
+// element-wise input (ggml-alloc's in-place reuse).  Anything else runs node by node.  KCPP_B1_UNFUSED=1 disables it.
+namespace {
+bool mem_overlap(const kggml_tensor *a, const kggml_tensor *b) {
+    const char *pa = (const char *)a->data, *pb = (const char *)b->data;
+    return pa < pb + nbytes(b) && pb < pa + nbytes(a);
+}
+bool same_bytes(const kggml_tensor *a, const kggml_tensor *b) {
+    return a->data == b->data && nbytes(a) == nbytes(b) && a->nb[1] == b->nb[1];
+}
+bool exact_or_disjoint(const kggml_tensor *a, const kggml_tensor *b) { return same_bytes(a, b) || !mem_overlap(a, b); }
+bool f32_vec(const kggml_tensor *t, int64_t n) {   // a contiguous f32 [n, 1, 1, 1]
+    return t && t->type == KGGML_TYPE_F32 && t->ne[0] == n && t->ne[1] == 1 && t->ne[2] == 1 && t->ne[3] == 1 &&
+           t->nb[0] == 4 && t->data;
+}
+bool same_shape(const kggml_tensor *a, const kggml_tensor *b) {
+    return a->ne[0] == b->ne[0] && a->ne[1] == b->ne[1] && a->ne[2] == b->ne[2] && a->ne[3] == b->ne[3];
+}
+// a single-token quantized MUL_MAT the fused mat-vec (compute_node's M == 1 path) runs
+bool mv_node(const kggml_tensor *m) {
+    const kggml_tensor *a = m->src[0], *b = m->src[1];
+    return m->op == KGGML_OP_MUL_MAT && supports(m) && a && b && is_quantized(a->type) &&
+           !(a->buffer && buffer_is_split(a->buffer)) && f32_vec(m, a->ne[1]) && f32_vec(b, a->ne[0]) && a->data;
+}
+
+// RMS_NORM -> MUL(norm, w): kcpp_ggml_rms_norm_mul writes the norm row, then the product row
+int fuse_norm_mul(BackendCtx *bc, kggml_cgraph *g, int i) {
+    if (i + 1 >= g->n_nodes) return 0;
+    kggml_tensor *nn = g->nodes[i], *m = g->nodes[i + 1];
+    if (nn->op != KGGML_OP_RMS_NORM || m->op != KGGML_OP_MUL || m->src[0] != nn || !supports(nn) || !supports(m)) return 0;
+    kggml_tensor *x = nn->src[0], *w = m->src[1];
+    if (!x || !w || w->type != KGGML_TYPE_F32 || !same_shape(x, nn) || !same_shape(nn, m)) return 0;
+    if (x->nb[0] != 4 || nn->nb[0] != 4 || m->nb[0] != 4 || w->nb[0] != 4) return 0;
+    for (int d = 0; d < 4; ++d)
+        if (w->ne[d] <= 0 || m->ne[d] % w->ne[d] != 0) return 0;           // ggml_can_repeat
+    if (!exact_or_disjoint(nn, m) || !exact_or_disjoint(x, nn) || !exact_or_disjoint(x, m) || mem_overlap(w, nn) ||
+        mem_overlap(w, m))
+        return 0;
+    const kcpp_tdesc tx = td_of(x), tr = td_of(nn), ty = td_of(m), tw = td_of(w);
+    if (kcpp_ggml_rms_norm_mul(x->data, &tx, nn->data, &tr, m->data, &ty, (const float *)w->data, &tw, op_f(nn, 0),
+                               bc->stream) != 0) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return 2;
+}
+
+// MUL_MAT(W, x) -> ADD(product, r): the mat-vec with the residual in its epilogue (aux[0] = the product node's output;
+// the RS kernels' AUX instances -- other layouts return -3 and the two nodes run one by one)
+int fuse_mv_add(BackendCtx *bc, kggml_cgraph *g, int i) {
+    if (i + 1 >= g->n_nodes) return 0;
+    kggml_tensor *mm = g->nodes[i], *ad = g->nodes[i + 1];
+    if (ad->op != KGGML_OP_ADD || !supports(ad) || !mv_node(mm)) return 0;
+    kggml_tensor *r = ad->src[0] == mm ? ad->src[1] : (ad->src[1] == mm ? ad->src[0] : nullptr);
+    const int64_t N = mm->ne[0];
+    kggml_tensor *x = mm->src[1];
+    if (!r || r == mm || !f32_vec(r, N) || !f32_vec(ad, N)) return 0;
+    kggml_tensor *a = mm->src[0];
+    const int tt = matmul_layout(a->type, a->ne[0]);
+    if (tt != KT_Q4_K_RS && tt != KT_Q5_K_RS && tt != KT_Q6_K_RS) return 0;
+    if (mem_overlap(mm, x) || mem_overlap(ad, x) || !exact_or_disjoint(mm, ad) || !exact_or_disjoint(r, ad) ||
+        !exact_or_disjoint(r, mm))
+        return 0;
+    const void *W = native_image(bc, a, tt);
+    if (!W) return 0;
+    DecArgs d;
+    memset(&d, 0, sizeof d);
+    d.K = a->ne[0]; d.nseg = 1; d.W[0] = (const uint8_t *)W; d.N[0] = N; d.Y[0] = (float *)ad->data;
+    d.x = (const float *)x->data; d.res = (const float *)r->data;
+    const AuxOut o{(float *)mm->data, nullptr, nullptr};
+    if (kcpp_gemv_rs_aux(tt, &d, 0, &o, bc->stream) != 0) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return 2;
+}
+
+// build_ffn's LLM_FFN_SILU + LLM_FFN_PAR: gate = MUL_MAT(Wg, x), s = SILU(gate), up = MUL_MAT(Wu, x), MUL(s, up), in
+// either evaluation order of the two mat-vecs: the GLU mat-vec (mode 1, quantize prologue) writing gate, s, up, then
+// the product (RS layouts; -3 elsewhere and the nodes run one by one)
+int fuse_glu(BackendCtx *bc, kggml_cgraph *g, int i) {
+    if (i + 3 >= g->n_nodes) return 0;
+    kggml_tensor *p[3] = {g->nodes[i], g->nodes[i + 1], g->nodes[i + 2]}, *mu = g->nodes[i + 3];
+    if (mu->op != KGGML_OP_MUL || !supports(mu)) return 0;
+    auto in_window = [&](const kggml_tensor *t) { return t == p[0] || t == p[1] || t == p[2]; };
+    auto is_silu = [](const kggml_tensor *t) {
+        return t && t->op == KGGML_OP_UNARY && t->op_params[0] == KGGML_UNARY_OP_SILU && supports(t);
+    };
+    kggml_tensor *s = is_silu(mu->src[0]) ? mu->src[0] : (is_silu(mu->src[1]) ? mu->src[1] : nullptr);
+    if (!s || !in_window(s)) return 0;
+    kggml_tensor *up = mu->src[0] == s ? mu->src[1] : mu->src[0], *gate = s->src[0];
+    if (!gate || !up || gate == up || !in_window(gate) || !in_window(up) || !mv_node(gate) || !mv_node(up)) return 0;
+    kggml_tensor *x = gate->src[1], *wg = gate->src[0], *wu = up->src[0];
+    if (up->src[1] != x || wg->type != wu->type || !same_shape(wg, wu)) return 0;
+    const int64_t N = gate->ne[0];
+    if (!f32_vec(s, N) || !f32_vec(mu, N)) return 0;
+    kggml_tensor *outs[4] = {gate, s, up, mu};
+    for (int j = 0; j < 4; ++j) {
+        if (mem_overlap(outs[j], x)) return 0;
+        for (int k = j + 1; k < 4; ++k)
+            if (!exact_or_disjoint(outs[j], outs[k])) return 0;
+    }
+    const int tt = matmul_layout(wg->type, wg->ne[0]);
+    if (tt != KT_Q4_K_RS && tt != KT_Q5_K_RS && tt != KT_Q6_K_RS) return 0;
+    const void *Wg = native_image(bc, wg, tt), *Wu = native_image(bc, wu, tt);
+    if (!Wg || !Wu) return 0;
+    DecArgs d;
+    memset(&d, 0, sizeof d);
+    d.K = wg->ne[0]; d.nseg = 1; d.W[0] = (const uint8_t *)Wg; d.W2 = (const uint8_t *)Wu; d.N[0] = N;
+    d.Y[0] = (float *)mu->data; d.x = (const float *)x->data;
+    const AuxOut o{(float *)gate->data, (float *)s->data, (float *)up->data};
+    if (kcpp_gemv_rs_aux(tt, &d, 1, &o, bc->stream) != 0) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return 4;
+}
+
+// the number of nodes node i starts a fused launch for (0: none)
+int fuse_at(BackendCtx *bc, kggml_cgraph *g, int i) {
+    switch (g->nodes[i]->op) {
+    case KGGML_OP_RMS_NORM: return fuse_norm_mul(bc, g, i);
+    case KGGML_OP_MUL_MAT: {
+        const int k = fuse_glu(bc, g, i);
+        return k ? k : fuse_mv_add(bc, g, i);
+    }
+    default: return 0;
+    }
+}
+}  // namespace
+
 const char *be_get_name(kggml_backend_t be) { return ((BackendCtx *)be->context)->name.c_str(); }
 void be_free(kggml_backend_t be) {
     BackendCtx *c = (BackendCtx *)be->context;
@@ -1052,10 +1193,20 @@ int be_graph_compute(kggml_backend_t be, kggml_cgraph *g) {
     BackendCtx *c = (BackendCtx *)be->context;
     hipSetDevice(c->device);
     g_last_nodes = 0;
+    g_last_fused = 0;
     for (int i = 0; i < g->n_nodes; ++i) {
         kggml_tensor *n = g->nodes[i];
         if (n->ne[0] == 0 || n->ne[1] == 0 || n->ne[2] == 0 || n->ne[3] == 0) continue;   // ggml_is_empty
         if (!supports(n)) { set_err(std::string("graph_compute: unsupported node '") + n->name + "'"); return KGGML_STATUS_FAILED; }
+        if (!c->no_fuse) {
+            const int k = fuse_at(c, g, i);
+            if (k) {
+                g_last_nodes += k;
+                g_last_fused += k;
+                i += k - 1;
+                continue;
+            }
+        }
         if (!compute_node(c, n)) return KGGML_STATUS_FAILED;
         ++g_last_nodes;
     }
@@ -1222,6 +1373,7 @@ void ggml_backend_cuda_unregister_host_buffer(void *buffer) {
 void ggml_cuda_set_mul_mat_q(bool mul_mat_q) { g_mul_mat_q = mul_mat_q; }
 
 int kcpp_ggml_backend_last_nodes(void) { return g_last_nodes; }
+int kcpp_ggml_backend_last_fused(void) { return g_last_fused; }
 // device bytes held by separate native images (weights outside weight buffers, or asked for in two layouts); the
 // weights of a weight buffer are converted in place and hold none
 int64_t kcpp_ggml_backend_image_bytes(void) {
@@ -1233,6 +1385,11 @@ int64_t kcpp_ggml_backend_image_bytes(void) {
 int kcpp_ggml_backend_set_fa_exact(kggml_backend_t be, int on) {
     if (!ggml_backend_is_cuda(be)) return -1;
     ((BackendCtx *)be->context)->fa_exact = on != 0;
+    return 0;
+}
+int kcpp_ggml_backend_set_fusion(kggml_backend_t be, int on) {
+    if (!ggml_backend_is_cuda(be)) return -1;
+    ((BackendCtx *)be->context)->no_fuse = on == 0;
     return 0;
 }
 const char *kcpp_ggml_backend_last_error(void) { return g_last_error.c_str(); }

@@ -136,6 +136,39 @@ __global__ void __launch_bounds__(256) k_rms_norm_g(const char *__restrict__ x, 
     }
 }
 
+// rms_norm and the MUL by a broadcast weight that follows it (build_norm, src/llama.cpp: ggml_mul(ggml_rms_norm(x),
+// w)) in one launch: both nodes' outputs are written, each element the unfused pair's bits (r = x * scale rounded,
+// then y = r * w rounded, the norm row before the product row per element -- an in-place y over r ends the same).
+// Rows of x, r, y, w contiguous (nb[0] = 4); w broadcast over rows by modulo as k_bin.
+__global__ void __launch_bounds__(256) k_rms_norm_mul_g(const char *__restrict__ x, TD tx, char *r, TD tr, char *y, TD ty,
+                                                        const char *__restrict__ w, TD tw, float eps, int64_t nrows) {
+    for (int64_t row = blockIdx.x; row < nrows; row += gridDim.x) {
+        int64_t i1, i2, i3;
+        row3(row, tx.ne, i1, i2, i3);
+        const float *xr = (const float *)(x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3]);
+        float *rr = (float *)(r + i1 * tr.nb[1] + i2 * tr.nb[2] + i3 * tr.nb[3]);
+        float *yr = (float *)(y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
+        const float *wr = (const float *)(w + (i1 % tw.ne[1]) * tw.nb[1] + (i2 % tw.ne[2]) * tw.nb[2] + (i3 % tw.ne[3]) * tw.nb[3]);
+        const bool wfull = tw.ne[0] == ty.ne[0];
+        double ss = 0.0;
+        for (int64_t i = threadIdx.x; i < tx.ne[0]; i += 256) ss += (double)__fmul_rn(xr[i], xr[i]);
+        ss = wave_sum(ss);
+        __shared__ double red[4];
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+        __syncthreads();
+        const double sum = (red[0] + red[1]) + (red[2] + red[3]);
+        __syncthreads();
+        const float mean = (float)(sum / (double)tx.ne[0]);
+        const float scale = 1.0f / sqrtf(mean + eps);
+        for (int64_t i = threadIdx.x; i < tx.ne[0]; i += 256) {
+            const float v = __fmul_rn(xr[i], scale);
+            const float wv = wr[wfull ? i : i % tw.ne[0]];
+            rr[i] = v;
+            yr[i] = __fmul_rn(v, wv);
+        }
+    }
+}
+
 // ---------------------------------------------------------------- rope
 // thread = one pair (i0 = 2 ip); theta iterated from the position exactly as ggml_rope_cache_init,
 // cos / sin correctly rounded through double (the CPU's glibc cosf / sinf are within 1 ulp of that).
@@ -370,6 +403,18 @@ int kcpp_ggml_rms_norm(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_
     if (nr == 0) return 0;
     hipLaunchKernelGGL(k_rms_norm_g, dim3((unsigned)std::min<int64_t>(nr, 65535)), dim3(256), 0, (hipStream_t)stream,
                        (const char *)x, td_of(tx), (char *)y, td_of(ty), eps, nr);
+    KCPP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int kcpp_ggml_rms_norm_mul(const void *x, const kcpp_tdesc *tx, void *r, const kcpp_tdesc *tr, void *y,
+                           const kcpp_tdesc *ty, const float *w, const kcpp_tdesc *tw, float eps, void *stream) {
+    const int64_t nr = nrows_of(tx);
+    if (nr == 0) return 0;
+    if (tx->nb[0] != 4 || tr->nb[0] != 4 || ty->nb[0] != 4 || tw->nb[0] != 4) return -2;
+    hipLaunchKernelGGL(k_rms_norm_mul_g, dim3((unsigned)std::min<int64_t>(nr, 65535)), dim3(256), 0, (hipStream_t)stream,
+                       (const char *)x, td_of(tx), (char *)r, td_of(tr), (char *)y, td_of(ty), (const char *)w, td_of(tw),
+                       eps, nr);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

@@ -72,6 +72,13 @@ struct DecArgs {
     int32_t *route_ids;
     float *route_wts;
 };
+// the ggml plugin's fused nodes (ggml_backend.cpp fuse_*): the intermediate nodes' outputs, written beside Y so that
+// the graph's every tensor holds what the unfused node sequence leaves.  MODE 0: p0 = the product before the residual
+// (the MUL_MAT node under an ADD).  MODE 1: p0 = gate, p1 = silu(gate), p2 = up.  A separate kernel parameter of the
+// RS kernels' AUX instances (kcpp_gemv_rs_aux), so the runtime's launches and their DecArgs carry none of it.
+struct AuxOut {
+    float *p0, *p1, *p2;
+};
 
 
 // top-NU of NE <= 8 router logits exactly as ggml's soft_max (ggml_float sum) + argsort (exchange order) + the
@@ -141,6 +148,8 @@ extern "C" int kcpp_flash_attn_dec_ta(const uint16_t *q16, const uint16_t *kc, c
                                       int n_kv_max, float scale, void *stream);
 // decode mat-vec over the row-major RS layouts (gemv_rs.hip); -3 = not covered
 extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
+// the same single-token launch (mode 0 / 1, quantize prologue) storing the intermediate nodes' tensors too (AuxOut)
+extern "C" int kcpp_gemv_rs_aux(int type, const void *args, int mode, const AuxOut *aux, void *stream);
 extern "C" int kcpp_rs_supported(int type, int64_t K);
 
 

@@ -727,3 +727,114 @@ def test_split_buffer_mul_mat_vs_reference_cpu(env, case, monkeypatch):
     ref = np.ctypeslib.as_array((ctypes.c_float * (M * N)).from_address(G.ggml_get_data(oc))).copy()
     G.ggml_free(cctx)
     assert rel(ours, ref) <= 3e-6, rel(ours, ref)
+
+
+FUSION_CASES = [("q4k_q6k", R.Q4_K, R.Q6_K, "ctx"), ("q4k_q6k_gallocr", R.Q4_K, R.Q6_K, "gallocr"),
+                ("q8_0", R.Q8_0, R.Q8_0, "ctx"), ("q5k_gallocr", R.Q5_K, R.Q5_K, "gallocr")]
+
+
+@pytest.mark.parametrize("case", FUSION_CASES, ids=lambda c: c[0])
+def test_decode_node_fusion_matches_node_by_node(env, case):
+    """the plugin's decode node fusion (ggml_backend.cpp fuse_at: RMS_NORM+MUL, MUL_MAT+ADD, the SiLU GLU quadruple)
+    against the same graph run node by node (kcpp_ggml_backend_set_fusion(be, 0)) on one token of a build_llama
+    layer: bit for bit on the layer output, and -- each tensor in its own allocation (ggml_backend_alloc_ctx_tensors)
+    -- on EVERY node's output, the fused launches writing the intermediate nodes' tensors too.  Allocated by
+    ggml_gallocr (ggml-alloc.c, the allocator llama.cpp's scheduler uses) the intermediates share bytes in place, which
+    the fusion must leave as the node sequence does.  The mat-vec fusions need an RS layout (Q4_K / Q5_K / Q6_K): the
+    Q8_0 case fuses the norms only."""
+    G, L, be = env
+    name, wt, wdown, alloc = case
+    for n, (a, r) in {"ggml_gallocr_new": ([P], P), "ggml_gallocr_alloc_graph": ([P, P], ctypes.c_bool),
+                      "ggml_gallocr_free": ([P], None), "ggml_set_input": ([P], None),
+                      "ggml_set_output": ([P], None)}.items():
+        fn = getattr(G, n)
+        fn.argtypes, fn.restype = a, r
+    L.kcpp_ggml_backend_set_fusion.argtypes = [P, I]
+    E, H, HKV, D, Fd, n_ctx, n_past, T = 1024, 8, 2, 128, 2816, 64, 37, 1
+    EKV, n_kv = HKV * D, n_past + T
+    rng = np.random.default_rng(5)
+    tys = [wt] * 6 + [wdown]
+    shapes = [(E, E), (E, EKV), (E, EKV), (E, E), (E, Fd), (E, Fd), (Fd, E)]
+    ws = [R.synth(t, 9, 400 + i, k, n) for i, (t, (k, n)) in enumerate(zip(tys, shapes))]
+    nw1 = (1 + 0.05 * rng.standard_normal(E)).astype(np.float32)
+    nw2 = (1 + 0.05 * rng.standard_normal(E)).astype(np.float32)
+    x = rng.standard_normal((T, E)).astype(np.float32)
+    kc = (rng.standard_normal((n_ctx, EKV)) * 0.5).astype(np.float16)
+    vc = rng.standard_normal((n_ctx, EKV)).astype(np.float16)
+    pos = np.array([n_past], np.int32)
+    mask = np.full((32, n_kv), -np.inf, np.float16)
+    mask[0, :n_kv] = 0
+    data = ws + [nw1, nw2, x, kc, vc, pos, mask]
+
+    ctx = G.ggml_init(InitParams(256 << 20, None, True))
+    W = [G.ggml_new_tensor_2d(ctx, t, k, n) for t, (k, n) in zip(tys, shapes)]
+    N1, N2 = G.ggml_new_tensor_1d(ctx, R.F32, E), G.ggml_new_tensor_1d(ctx, R.F32, E)
+    X = G.ggml_new_tensor_2d(ctx, R.F32, E, T)
+    KC, VC = G.ggml_new_tensor_1d(ctx, R.F16, n_ctx * EKV), G.ggml_new_tensor_1d(ctx, R.F16, n_ctx * EKV)
+    Pz = G.ggml_new_tensor_1d(ctx, 26, T)
+    Mk = G.ggml_new_tensor_2d(ctx, R.F16, n_kv, 32)
+    ins = W + [N1, N2, X, KC, VC, Pz, Mk]
+    for t in ins:
+        G.ggml_set_input(t)
+    cur = G.ggml_mul(ctx, G.ggml_rms_norm(ctx, X, 1e-5), N1)
+    q = G.ggml_rope_ext(ctx, G.ggml_reshape_3d(ctx, G.ggml_mul_mat(ctx, W[0], cur), D, H, T), Pz, None, D, 0, n_ctx,
+                        500000.0, 1.0, 0.0, 1.0, 32.0, 1.0)
+    k = G.ggml_rope_ext(ctx, G.ggml_reshape_3d(ctx, G.ggml_mul_mat(ctx, W[1], cur), D, HKV, T), Pz, None, D, 0, n_ctx,
+                        500000.0, 1.0, 0.0, 1.0, 32.0, 1.0)
+    v = G.ggml_mul_mat(ctx, W[2], cur)
+    st_k = G.ggml_cpy(ctx, k, G.ggml_view_1d(ctx, KC, T * EKV, n_past * EKV * 2))
+    st_v = G.ggml_cpy(ctx, v, G.ggml_view_1d(ctx, VC, T * EKV, n_past * EKV * 2))
+    kview = G.ggml_view_3d(ctx, KC, D, n_kv, HKV, EKV * 2, D * 2, 0)
+    vview = G.ggml_view_3d(ctx, VC, D, n_kv, HKV, EKV * 2, D * 2, 0)
+    fa = G.ggml_flash_attn_ext(ctx, G.ggml_permute(ctx, q, 0, 2, 1, 3), kview, vview, Mk, 1.0 / np.sqrt(D), 0.0, 0.0)
+    att = G.ggml_mul_mat(ctx, W[3], G.ggml_reshape_2d(ctx, fa, E, T))
+    ffn_in = G.ggml_add(ctx, att, X)
+    h = G.ggml_mul(ctx, G.ggml_rms_norm(ctx, ffn_in, 1e-5), N2)
+    h = G.ggml_mul(ctx, G.ggml_silu(ctx, G.ggml_mul_mat(ctx, W[4], h)), G.ggml_mul_mat(ctx, W[5], h))
+    out = G.ggml_add(ctx, G.ggml_mul_mat(ctx, W[6], h), ffn_in)
+    G.ggml_set_output(out)
+    g = G.ggml_new_graph(ctx)
+    G.ggml_build_forward_expand(g, st_k)
+    G.ggml_build_forward_expand(g, st_v)
+    G.ggml_build_forward_expand(g, out)
+    nodes = [G.ggml_graph_node(g, i) for i in range(G.ggml_graph_n_nodes(g))]
+    assert all(G.ggml_backend_supports_op(be, n) for n in nodes)
+    if alloc == "ctx":
+        buf, galloc = G.ggml_backend_alloc_ctx_tensors(ctx, be), None
+        assert buf
+    else:
+        galloc = G.ggml_gallocr_new(L.ggml_backend_cuda_buffer_type(0))
+        assert G.ggml_gallocr_alloc_graph(galloc, g)
+    # every node with its own bytes (ctx allocation): the F32 node outputs compared too
+    probe = [n for n in nodes if alloc == "ctx" and ctypes.c_int.from_address(n).value == R.F32]
+    runs = []
+    try:
+        for fused in (1, 0):
+            assert L.kcpp_ggml_backend_set_fusion(ctypes.c_void_p(be), fused) == 0
+            for t, a in zip(ins, data):
+                a = np.ascontiguousarray(a)
+                G.ggml_backend_tensor_set(t, a.ctypes.data, 0, a.nbytes)
+            assert G.ggml_backend_graph_compute(be, g) == 0, L.kcpp_ggml_backend_last_error()
+            nf = L.kcpp_ggml_backend_last_fused()
+            got = []
+            for t in [out] + probe:
+                r = np.empty(G.ggml_nbytes(t) // 4, np.float32)
+                G.ggml_backend_tensor_get(t, r.ctypes.data, 0, r.nbytes)
+                got.append(r)
+            runs.append((nf, got))
+    finally:
+        L.kcpp_ggml_backend_set_fusion(ctypes.c_void_p(be), 1)
+        if galloc:
+            G.ggml_gallocr_free(galloc)
+        else:
+            G.ggml_backend_buffer_free(buf)
+        G.ggml_free(ctx)
+    (nf1, a), (nf0, b) = runs
+    L.kcpp_rs_supported.argtypes = [I, I64]
+    rs = [bool(L.kcpp_rs_supported(t, k)) for t, (k, n) in zip(tys, shapes)]      # ggml type ids = KT_ codes
+    want = 2 * 2 + 2 * rs[3] + 4 * rs[4] + 2 * rs[6]     # 2 norms; wo + ADD, the GLU, down + ADD on RS layouts
+    print("%s: %d nodes fused of %d (expected %d)" % (name, nf1, len(nodes), want))
+    assert nf0 == 0 and nf1 == want, (nf1, want)
+    assert rs[4] == (wt != R.Q8_0)
+    for i, (u, w_) in enumerate(zip(a, b)):
+        assert np.array_equal(u.view(np.uint32), w_.view(np.uint32)), (i, rel(u, w_))
