@@ -57,6 +57,9 @@ def main():
             same = None
             if y0 is None:
                 y0 = Y.clone()
+                if os.environ.get("GEMM_DUMP"):      # the first variant's output, for a cross-build bitwise check
+                    os.makedirs(os.environ["GEMM_DUMP"], exist_ok=True)
+                    Y.cpu().numpy().tofile(os.path.join(os.environ["GEMM_DUMP"], name.replace("|", "_") + ".f32"))
             else:
                 same = bool(torch.equal(Y, y0))
             fl = 2.0 * M * N * Kd * (2 if mode else 1)

@@ -18,6 +18,12 @@ struct Big { long long v[32]; };
 
 __global__ void k_empty(int *p) { if (p && threadIdx.x == 1023) p[0] = 1; }
 __global__ void k_big(Big b, int *p) { if (threadIdx.x == 1023) p[0] = (int)b.v[31]; }
+template <int NB> struct Arg { long long v[NB / 8]; };
+// a 256-WG kernel reading its first and last argument words (the kernarg size sweep: DecArgs is 296 B)
+template <int NB>
+__global__ void k_arg(Arg<NB> b, int *p) {
+    if (threadIdx.x == 1023) p[0] = (int)(b.v[0] + b.v[NB / 8 - 1]);
+}
 __global__ void k_dep(const int *in, int *out) {
     const int v = in[blockIdx.x & 255];
     if (threadIdx.x == 0) out[blockIdx.x & 255] = v + 1;
@@ -66,6 +72,11 @@ int main() {
             hipLaunchKernelGGL(k_dep, dim3(256), dim3(256), 0, s, buf + (i & 1) * 4096, buf + ((i + 1) & 1) * 4096);
         });
     }
+    // kernarg size sweep, 256-launch chains
+#define KA(NB) { Arg<NB> a{}; time_chain("arg" #NB, 256, s, [&](int) { hipLaunchKernelGGL(k_arg<NB>, dim3(256), dim3(256), 0, s, a, buf); }); }
+    KA(16) KA(64) KA(128) KA(192) KA(248) KA(256) KA(264) KA(296) KA(320) KA(384) KA(512) KA(1024)
+    KA(16) KA(296) KA(320)
+#undef KA
     // eager (no graph) for comparison
     {
         hipEvent_t a, b;
