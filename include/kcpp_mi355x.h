@@ -262,6 +262,11 @@ int kcpp_ggml_rms_norm(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_
 int kcpp_ggml_rms_norm_mul(const void *x, const kcpp_tdesc *tx, void *r, const kcpp_tdesc *tr, void *y,
                            const kcpp_tdesc *ty, const float *w, const kcpp_tdesc *tw, float eps, void *stream);
 /* GGML_OP_ROPE f32, mode 0 (NORM) or 2 (NEOX); pos int32 [ne2]; freq_factors may be null */
+/* b1 fusion: the same ROPE also storing each value as f16 at its linear element index in y16 (the CPY of the roped
+ * tensor into a contiguous F16 cache view that follows it); y must be contiguous */
+int kcpp_ggml_rope_f16(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdesc *ty, void *y16, const int32_t *pos,
+                       const float *freq_factors, int n_dims, int mode, int n_ctx_orig, float freq_base, float freq_scale,
+                       float ext_factor, float attn_factor, float beta_fast, float beta_slow, void *stream);
 int kcpp_ggml_rope(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdesc *ty, const int32_t *pos,
                    const float *freq_factors, int n_dims, int mode, int n_ctx_orig, float freq_base, float freq_scale,
                    float ext_factor, float attn_factor, float beta_fast, float beta_slow, void *stream);

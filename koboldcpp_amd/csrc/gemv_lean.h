@@ -154,7 +154,7 @@ struct ActCopyCol {
 // store R parked results of group slot_g (rows row0.. of segment seg)
 template <int R, int MODE, bool AUX = false>
 __device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0, const float (&slot)[R],
-                                            float *aux0 = nullptr) {
+                                            float *aux0 = nullptr, uint16_t *auxh = nullptr) {
     if constexpr (MODE != 2) {
         float *Y = seg == 0 ? a.Y[0] : (seg == 1 ? a.Y[1] : a.Y[2]);
 #pragma unroll
@@ -163,7 +163,8 @@ __device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0,
             if (MODE == 0 && a.pre) v = __fadd_rn(a.pre[row0 + r], v);
             if constexpr (AUX && MODE == 0) {      // the ggml plugin's MUL_MAT -> ADD: the product node's tensor too
                 const float rv = a.res ? a.res[row0 + r] : 0.0f;
-                aux0[row0 + r] = v;
+                if (aux0) aux0[row0 + r] = v;
+                if (auxh) auxh[row0 + r] = f2h(v);
                 Y[row0 + r] = a.res ? __fadd_rn(v, rv) : v;
             } else {
                 Y[row0 + r] = ((MODE == 0 || MODE == 3) && a.res) ? __fadd_rn(v, a.res[row0 + r]) : v;

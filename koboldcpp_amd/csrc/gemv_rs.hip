@@ -67,6 +67,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     const int KB_BID = (int)blockIdx.x, KB_NBLK = (int)gridDim.x;
     constexpr bool AUX = false;
     float *const aux0 = nullptr, *const aux1 = nullptr, *const aux2 = nullptr;
+    uint16_t *const auxh = nullptr;
 #include "gemv_rs_body.inc"
 }
 // the ggml plugin's fused nodes (AuxOut): the same body storing the intermediate nodes' tensors too -- MODE 0 the
@@ -77,6 +78,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs_aux(const DecArgs a, const
     const int KB_BID = (int)blockIdx.x, KB_NBLK = (int)gridDim.x;
     constexpr bool XL = false, ROUTE = false, AUX = true;
     float *const aux0 = o.p0, *const aux1 = o.p1, *const aux2 = o.p2;
+    uint16_t *const auxh = o.h0;
 #include "gemv_rs_body.inc"
 }
 
@@ -338,6 +340,7 @@ __global__ void __launch_bounds__(256) k_gemv_qkv_dual(const DecArgs a, const De
         constexpr int TYPE = TA, NI = NIA, R = 2, MODE = 2, PRO = 1, MC = MCA, PF = 0, NWV = 4;
         constexpr bool XL = false, ROUTE = false, AUX = false;
         float *const aux0 = nullptr, *const aux1 = nullptr, *const aux2 = nullptr;
+        uint16_t *const auxh = nullptr;
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
         const int KB_BID = (int)blockIdx.x, KB_NBLK = nA;
 #include "gemv_rs_body.inc"
@@ -467,7 +470,9 @@ extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void 
 // the ggml plugin's fused nodes: kcpp_gemv_rs's launch (modes 0 and 1, quantize prologue, one segment) through the AUX
 // instances, which also store the intermediate nodes' tensors (AuxOut); -3 where no AUX instance covers the shape
 extern "C" int kcpp_gemv_rs_aux(int type, const void *args, int mode, const AuxOut *aux, void *stream) {
-    if (!aux || !aux->p0 || (mode == 1 && (!aux->p1 || !aux->p2)) || (mode != 0 && mode != 1)) return -3;
+    if (!aux || (mode == 0 && !aux->p0 && !aux->h0) || (mode == 1 && (!aux->p0 || !aux->p1 || !aux->p2)) ||
+        (mode != 0 && mode != 1))
+        return -3;
     g_rs_aux = aux;
     const int rc = kcpp_gemv_rs(type, args, mode, 2, stream);
     g_rs_aux = nullptr;

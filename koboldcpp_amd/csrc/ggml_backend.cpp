@@ -1065,7 +1065,7 @@ int fuse_mv_add(BackendCtx *bc, kggml_cgraph *g, int i) {
     memset(&d, 0, sizeof d);
     d.K = a->ne[0]; d.nseg = 1; d.W[0] = (const uint8_t *)W; d.N[0] = N; d.Y[0] = (float *)ad->data;
     d.x = (const float *)x->data; d.res = (const float *)r->data;
-    const AuxOut o{(float *)mm->data, nullptr, nullptr};
+    const AuxOut o{(float *)mm->data, nullptr, nullptr, nullptr};
     if (kcpp_gemv_rs_aux(tt, &d, 0, &o, bc->stream) != 0) {
         (void)hipGetLastError();
         return 0;
@@ -1106,7 +1106,7 @@ int fuse_glu(BackendCtx *bc, kggml_cgraph *g, int i) {
     memset(&d, 0, sizeof d);
     d.K = wg->ne[0]; d.nseg = 1; d.W[0] = (const uint8_t *)Wg; d.W2 = (const uint8_t *)Wu; d.N[0] = N;
     d.Y[0] = (float *)mu->data; d.x = (const float *)x->data;
-    const AuxOut o{(float *)gate->data, (float *)s->data, (float *)up->data};
+    const AuxOut o{(float *)gate->data, (float *)s->data, (float *)up->data, nullptr};
     if (kcpp_gemv_rs_aux(tt, &d, 1, &o, bc->stream) != 0) {
         (void)hipGetLastError();
         return 0;
@@ -1114,13 +1114,82 @@ int fuse_glu(BackendCtx *bc, kggml_cgraph *g, int i) {
     return 4;
 }
 
+// node i's output stored into an F16 cache slot right after: view-only nodes (no work here), then a CPY whose source
+// holds node i's bytes (node i itself or a reshape of it: same data, both contiguous, same element count) and whose
+// destination is a contiguous F16 view (llm_build_kv_store: ggml_cpy(k_cur / v_cur, ggml_view_1d(k_l / v_l, ...))).
+// Returns the CPY's index (0: no such CPY).
+int cpy16_after(kggml_cgraph *g, int i) {
+    kggml_tensor *src = g->nodes[i];
+    for (int j = i + 1; j < g->n_nodes && j <= i + 3; ++j) {
+        kggml_tensor *n = g->nodes[j];
+        if (n->op == KGGML_OP_NONE || n->op == KGGML_OP_RESHAPE || n->op == KGGML_OP_VIEW || n->op == KGGML_OP_PERMUTE ||
+            n->op == KGGML_OP_TRANSPOSE)
+            continue;
+        if (n->op != KGGML_OP_CPY || !supports(n)) return 0;
+        kggml_tensor *a = n->src[0], *d = n->src[1];
+        if (!a || !d || a->type != KGGML_TYPE_F32 || d->type != KGGML_TYPE_F16 || !is_contiguous(a) || !is_contiguous(d) ||
+            !is_contiguous(src) || a->data != src->data || nbytes(a) != nbytes(src))
+            return 0;
+        const int64_t ne = src->ne[0] * src->ne[1] * src->ne[2] * src->ne[3];
+        if (d->ne[0] * d->ne[1] * d->ne[2] * d->ne[3] != ne || n->data != d->data) return 0;
+        return j;
+    }
+    return 0;
+}
+
+// ROPE -> CPY into the F16 cache: the rope kernel stores each value as f16 too (kcpp_ggml_rope_f16)
+int fuse_rope_cpy(BackendCtx *bc, kggml_cgraph *g, int i) {
+    kggml_tensor *n = g->nodes[i];
+    if (n->op != KGGML_OP_ROPE || !supports(n)) return 0;
+    const int j = cpy16_after(g, i);
+    if (!j) return 0;
+    kggml_tensor *x = n->src[0], *d = g->nodes[j]->src[1];
+    if (mem_overlap(d, n) || mem_overlap(d, x) || (n->src[1] && mem_overlap(d, n->src[1]))) return 0;
+    const int mode = n->op_params[2];
+    const kcpp_tdesc ta = td_of(x), td = td_of(n);
+    const float *ff = n->src[2] ? (const float *)n->src[2]->data : nullptr;
+    if (kcpp_ggml_rope_f16(x->data, &ta, n->data, &td, d->data, (const int32_t *)n->src[1]->data, ff, n->op_params[1],
+                           mode, n->op_params[4], op_f(n, 5), op_f(n, 6), op_f(n, 7), op_f(n, 8), op_f(n, 9), op_f(n, 10),
+                           bc->stream) != 0) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return j - i + 1;
+}
+
+// single-token MUL_MAT -> CPY into the F16 cache (the V store): the mat-vec also stores the product as f16 (AuxOut h0)
+int fuse_mv_cpy(BackendCtx *bc, kggml_cgraph *g, int i) {
+    kggml_tensor *mm = g->nodes[i];
+    if (!mv_node(mm)) return 0;
+    const int j = cpy16_after(g, i);
+    if (!j) return 0;
+    kggml_tensor *a = mm->src[0], *x = mm->src[1], *d = g->nodes[j]->src[1];
+    const int tt = matmul_layout(a->type, a->ne[0]);
+    if (tt != KT_Q4_K_RS && tt != KT_Q5_K_RS && tt != KT_Q6_K_RS) return 0;
+    if (mem_overlap(mm, x) || mem_overlap(d, x) || mem_overlap(d, mm)) return 0;
+    const void *W = native_image(bc, a, tt);
+    if (!W) return 0;
+    DecArgs dd;
+    memset(&dd, 0, sizeof dd);
+    dd.K = a->ne[0]; dd.nseg = 1; dd.W[0] = (const uint8_t *)W; dd.N[0] = mm->ne[0]; dd.Y[0] = (float *)mm->data;
+    dd.x = (const float *)x->data;
+    const AuxOut o{nullptr, nullptr, nullptr, (uint16_t *)d->data};
+    if (kcpp_gemv_rs_aux(tt, &dd, 0, &o, bc->stream) != 0) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return j - i + 1;
+}
+
 // the number of nodes node i starts a fused launch for (0: none)
 int fuse_at(BackendCtx *bc, kggml_cgraph *g, int i) {
     switch (g->nodes[i]->op) {
     case KGGML_OP_RMS_NORM: return fuse_norm_mul(bc, g, i);
+    case KGGML_OP_ROPE: return fuse_rope_cpy(bc, g, i);
     case KGGML_OP_MUL_MAT: {
-        const int k = fuse_glu(bc, g, i);
-        return k ? k : fuse_mv_add(bc, g, i);
+        int k = fuse_glu(bc, g, i);
+        if (!k) k = fuse_mv_add(bc, g, i);
+        return k ? k : fuse_mv_cpy(bc, g, i);
     }
     default: return 0;
     }

@@ -115,6 +115,32 @@ __global__ void k_cpy(const char *__restrict__ s, TD ts, char *__restrict__ d, T
 }
 
 // ---------------------------------------------------------------- rms_norm (any row length)
+// sum over a row of (double)(x*x): thread t accumulates elements t, t + 256, ... in ascending order (16 loads in
+// flight, not one dependent load per step -- a single-row norm is one workgroup's latency chain), then the wave sums
+// and ((w0 + w1) + (w2 + w3)).  256 threads; rows of nb0 bytes per element (4: contiguous).
+__device__ __forceinline__ double row_sumsq(const float *xr, int64_t ne0, int64_t nb0) {
+    const char *xb = (const char *)xr;
+    double ss = 0.0;
+    for (int64_t i0 = threadIdx.x; i0 < ne0; i0 += 256 * 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int64_t i = i0 + 256 * u;
+            v[u] = i < ne0 ? *(const float *)(xb + i * nb0) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            if (i0 + 256 * u < ne0) ss += (double)__fmul_rn(v[u], v[u]);
+    }
+    ss = wave_sum(ss);
+    __shared__ double red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    const double sum = (red[0] + red[1]) + (red[2] + red[3]);
+    __syncthreads();
+    return sum;
+}
+
 __global__ void __launch_bounds__(256) k_rms_norm_g(const char *__restrict__ x, TD tx, char *__restrict__ y, TD ty,
                                                     float eps, int64_t nrows) {
     for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
@@ -122,14 +148,7 @@ __global__ void __launch_bounds__(256) k_rms_norm_g(const char *__restrict__ x, 
         row3(r, tx.ne, i1, i2, i3);
         const float *xr = (const float *)(x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3]);
         float *yr = (float *)(y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
-        double ss = 0.0;
-        for (int64_t i = threadIdx.x; i < tx.ne[0]; i += 256) ss += (double)__fmul_rn(xr[i], xr[i]);
-        ss = wave_sum(ss);
-        __shared__ double red[4];
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-        __syncthreads();
-        const double sum = (red[0] + red[1]) + (red[2] + red[3]);
-        __syncthreads();
+        const double sum = row_sumsq(xr, tx.ne[0], 4);
         const float mean = (float)(sum / (double)tx.ne[0]);
         const float scale = 1.0f / sqrtf(mean + eps);
         for (int64_t i = threadIdx.x; i < tx.ne[0]; i += 256) yr[i] = __fmul_rn(xr[i], scale);
@@ -150,21 +169,57 @@ __global__ void __launch_bounds__(256) k_rms_norm_mul_g(const char *__restrict__
         float *yr = (float *)(y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
         const float *wr = (const float *)(w + (i1 % tw.ne[1]) * tw.nb[1] + (i2 % tw.ne[2]) * tw.nb[2] + (i3 % tw.ne[3]) * tw.nb[3]);
         const bool wfull = tw.ne[0] == ty.ne[0];
-        double ss = 0.0;
-        for (int64_t i = threadIdx.x; i < tx.ne[0]; i += 256) ss += (double)__fmul_rn(xr[i], xr[i]);
-        ss = wave_sum(ss);
-        __shared__ double red[4];
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
-        __syncthreads();
-        const double sum = (red[0] + red[1]) + (red[2] + red[3]);
-        __syncthreads();
+        if (tx.ne[0] <= 256 * 16) {
+            // one pass (rows up to 4096): x and w loaded once, up front; the same sums in the same order as below
+            float xv[16], wv[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int64_t i = threadIdx.x + 256 * u;
+                xv[u] = i < tx.ne[0] ? xr[i] : 0.0f;
+                wv[u] = i < tx.ne[0] ? wr[wfull ? i : i % tw.ne[0]] : 0.0f;
+            }
+            double ss = 0.0;
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                if (threadIdx.x + 256 * u < tx.ne[0]) ss += (double)__fmul_rn(xv[u], xv[u]);
+            ss = wave_sum(ss);
+            __shared__ double red1[4];
+            if ((threadIdx.x & 63) == 0) red1[threadIdx.x >> 6] = ss;
+            __syncthreads();
+            const double sum1 = (red1[0] + red1[1]) + (red1[2] + red1[3]);
+            __syncthreads();
+            const float scale1 = 1.0f / sqrtf((float)(sum1 / (double)tx.ne[0]) + eps);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const int64_t i = threadIdx.x + 256 * u;
+                if (i >= tx.ne[0]) break;
+                const float v = __fmul_rn(xv[u], scale1);
+                rr[i] = v;
+                yr[i] = __fmul_rn(v, wv[u]);
+            }
+            continue;
+        }
+        const double sum = row_sumsq(xr, tx.ne[0], 4);
         const float mean = (float)(sum / (double)tx.ne[0]);
         const float scale = 1.0f / sqrtf(mean + eps);
-        for (int64_t i = threadIdx.x; i < tx.ne[0]; i += 256) {
-            const float v = __fmul_rn(xr[i], scale);
-            const float wv = wr[wfull ? i : i % tw.ne[0]];
-            rr[i] = v;
-            yr[i] = __fmul_rn(v, wv);
+        // 8 elements per thread in flight (x and w loaded before the stores; an in-place r / y over x reads each
+        // element before its own thread writes it)
+        for (int64_t i0 = threadIdx.x; i0 < tx.ne[0]; i0 += 256 * 8) {
+            float xv[8], wv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t i = i0 + 256 * u;
+                xv[u] = i < tx.ne[0] ? xr[i] : 0.0f;
+                wv[u] = i < tx.ne[0] ? wr[wfull ? i : i % tw.ne[0]] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t i = i0 + 256 * u;
+                if (i >= tx.ne[0]) break;
+                const float v = __fmul_rn(xv[u], scale);
+                rr[i] = v;
+                yr[i] = __fmul_rn(v, wv[u]);
+            }
         }
     }
 }
@@ -174,7 +229,9 @@ __global__ void __launch_bounds__(256) k_rms_norm_mul_g(const char *__restrict__
 // cos / sin correctly rounded through double (the CPU's glibc cosf / sinf are within 1 ulp of that).
 __global__ void k_rope(const char *__restrict__ x, TD tx, char *__restrict__ y, TD ty, const int32_t *__restrict__ pos,
                        const float *__restrict__ ff, int n_dims, int neox, float freq_scale, float ext_factor,
-                       float attn_factor, float mscale_ext, float corr0, float corr1, float theta_scale, int64_t nrows) {
+                       float attn_factor, float mscale_ext, float corr0, float corr1, float theta_scale, int64_t nrows,
+                       uint16_t *__restrict__ h16 = nullptr) {
+    // h16 (the ggml plugin's ROPE -> CPY fusion): y contiguous, each value also stored as f16 at its linear index
     for (int64_t r = blockIdx.y; r < nrows; r += gridDim.y) {
         int64_t i1, i2, i3;
         row3(r, tx.ne, i1, i2, i3);
@@ -184,8 +241,10 @@ __global__ void k_rope(const char *__restrict__ x, TD tx, char *__restrict__ y, 
         for (int64_t ip = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; ip < tx.ne[0] / 2; ip += (int64_t)gridDim.x * blockDim.x) {
             const int64_t i0 = 2 * ip;
             if (i0 >= n_dims) {                            // tail beyond n_dims: copied
-                *(float *)(yr + i0 * ty.nb[0]) = *(const float *)(xr + i0 * tx.nb[0]);
-                *(float *)(yr + (i0 + 1) * ty.nb[0]) = *(const float *)(xr + (i0 + 1) * tx.nb[0]);
+                const float t0 = *(const float *)(xr + i0 * tx.nb[0]), t1 = *(const float *)(xr + (i0 + 1) * tx.nb[0]);
+                *(float *)(yr + i0 * ty.nb[0]) = t0;
+                *(float *)(yr + (i0 + 1) * ty.nb[0]) = t1;
+                if (h16) { h16[r * tx.ne[0] + i0] = f2h(t0); h16[r * tx.ne[0] + i0 + 1] = f2h(t1); }
                 continue;
             }
             float theta = p;
@@ -202,8 +261,10 @@ __global__ void k_rope(const char *__restrict__ x, TD tx, char *__restrict__ y, 
             const float c = (float)cos((double)th) * mscale, s = (float)sin((double)th) * mscale;
             const int64_t ia = neox ? ip : i0, ib = neox ? ip + n_dims / 2 : i0 + 1;
             const float x0 = *(const float *)(xr + ia * tx.nb[0]), x1 = *(const float *)(xr + ib * tx.nb[0]);
-            *(float *)(yr + ia * ty.nb[0]) = __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s));
-            *(float *)(yr + ib * ty.nb[0]) = __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c));
+            const float o0 = __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s)), o1 = __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c));
+            *(float *)(yr + ia * ty.nb[0]) = o0;
+            *(float *)(yr + ib * ty.nb[0]) = o1;
+            if (h16) { h16[r * tx.ne[0] + ia] = f2h(o0); h16[r * tx.ne[0] + ib] = f2h(o1); }
         }
     }
 }
@@ -422,6 +483,13 @@ int kcpp_ggml_rms_norm_mul(const void *x, const kcpp_tdesc *tx, void *r, const k
 int kcpp_ggml_rope(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdesc *ty, const int32_t *pos,
                    const float *freq_factors, int n_dims, int mode, int n_ctx_orig, float freq_base, float freq_scale,
                    float ext_factor, float attn_factor, float beta_fast, float beta_slow, void *stream) {
+    return kcpp_ggml_rope_f16(x, tx, y, ty, nullptr, pos, freq_factors, n_dims, mode, n_ctx_orig, freq_base, freq_scale,
+                              ext_factor, attn_factor, beta_fast, beta_slow, stream);
+}
+
+int kcpp_ggml_rope_f16(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdesc *ty, void *y16, const int32_t *pos,
+                       const float *freq_factors, int n_dims, int mode, int n_ctx_orig, float freq_base, float freq_scale,
+                       float ext_factor, float attn_factor, float beta_fast, float beta_slow, void *stream) {
     const int64_t nr = nrows_of(tx);
     if (nr == 0) return 0;
     if (n_dims > tx->ne[0] || n_dims % 2 || tx->nb[0] != 4) return -1;
@@ -437,7 +505,7 @@ int kcpp_ggml_rope(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdes
     const dim3 g = row_grid(tx->ne[0] / 2, nr, 64);
     hipLaunchKernelGGL(k_rope, g, dim3(64), 0, (hipStream_t)stream, (const char *)x, td_of(tx), (char *)y, td_of(ty), pos,
                        freq_factors, n_dims, mode == 2 ? 1 : 0, freq_scale, ext_factor, attn_factor, mscale_ext, corr0,
-                       corr1, theta_scale, nr);
+                       corr1, theta_scale, nr, (uint16_t *)y16);
     KCPP_CHECK(hipGetLastError());
     return 0;
 }

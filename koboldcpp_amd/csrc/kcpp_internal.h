@@ -74,10 +74,12 @@ struct DecArgs {
 };
 // the ggml plugin's fused nodes (ggml_backend.cpp fuse_*): the intermediate nodes' outputs, written beside Y so that
 // the graph's every tensor holds what the unfused node sequence leaves.  MODE 0: p0 = the product before the residual
-// (the MUL_MAT node under an ADD).  MODE 1: p0 = gate, p1 = silu(gate), p2 = up.  A separate kernel parameter of the
-// RS kernels' AUX instances (kcpp_gemv_rs_aux), so the runtime's launches and their DecArgs carry none of it.
+// (the MUL_MAT node under an ADD; null without one), h0 = the product as f16 (a CPY into a contiguous F16 cache view;
+// null without one).  MODE 1: p0 = gate, p1 = silu(gate), p2 = up.  A separate kernel parameter of the RS kernels'
+// AUX instances (kcpp_gemv_rs_aux), so the runtime's launches and their DecArgs carry none of it.
 struct AuxOut {
     float *p0, *p1, *p2;
+    uint16_t *h0;
 };
 
 

@@ -93,6 +93,7 @@ _SIGS = {
     "kcpp_ggml_rms_norm": [P, P, P, P, Fl, P],
     "kcpp_ggml_rms_norm_mul": [P, P, P, P, P, P, P, P, Fl, P],
     "kcpp_ggml_rope": [P, P, P, P, P, P, I, I, I, Fl, Fl, Fl, Fl, Fl, Fl, P],
+    "kcpp_ggml_rope_f16": [P, P, P, P, P, P, P, I, I, I, Fl, Fl, Fl, Fl, Fl, Fl, P],
     "kcpp_ggml_soft_max": [P, P, P, I, I64, I64, P, P, Fl, P],
     "kcpp_ggml_argsort": [P, P, P, I64, I, P],
     "kcpp_ggml_sum_rows": [P, P, P, P, P],
