@@ -102,7 +102,7 @@ int main(int argc, char **argv) {
     uint8_t *cbuf = malloc(cmem);
     float *logits = malloc(sizeof(float) * NV);
     int tok = 16, n_nodes = 0, n_splits = 0;
-    double t_tg = 0.0;
+    double t_tg = 0.0, t_build = 0.0, t_alloc = 0.0, t_in = 0.0, t_comp = 0.0, t_out = 0.0;   /* per-phase host time */
     const float kq_scale = 1.0f / sqrtf((float)D);
     for (int step = -2; step < n_steps; ++step) {           /* two untimed warm-up steps */
         const int n_past = n_past0 + (step < 0 ? 0 : step);
@@ -153,8 +153,10 @@ int main(int argc, char **argv) {
         struct ggml_tensor *out = ggml_mul_mat(ctx, w[2], ggml_mul(ctx, ggml_rms_norm(ctx, inpL, 1e-5f), w[1]));
         ggml_set_output(out);
         ggml_build_forward_expand(gf, out);
+        const double t1 = now_s();
         ggml_backend_sched_reset(sched);
         if (!ggml_backend_sched_alloc_graph(sched, gf)) { fprintf(stderr, "sched alloc failed\n"); return 5; }
+        const double t2 = now_s();
         const int32_t pos = n_past;
         ggml_backend_tensor_set(inp_tokens, &tok, 0, 4);
         ggml_backend_tensor_set(inp_pos, &pos, 0, 4);
@@ -164,7 +166,10 @@ int main(int argc, char **argv) {
                 mask[(size_t)r * n_kv + j] = ggml_fp32_to_fp16((r == 0 && j <= n_past) ? 0.0f : -INFINITY);
         ggml_backend_tensor_set(kq_mask, mask, 0, sizeof(ggml_fp16_t) * n_kv * GGML_KQ_MASK_PAD);
         free(mask);
+        const double t3 = now_s();
         if (ggml_backend_sched_graph_compute(sched, gf) != GGML_STATUS_SUCCESS) { fprintf(stderr, "compute failed\n"); return 6; }
+        ggml_backend_sched_synchronize(sched);
+        const double t4 = now_s();
         ggml_backend_tensor_get(out, logits, 0, sizeof(float) * NV);
         int b = 0;
         for (int i = 1; i < NV; ++i) if (logits[i] > logits[b]) b = i;
@@ -172,11 +177,18 @@ int main(int argc, char **argv) {
         n_nodes = ggml_graph_n_nodes(gf);
         n_splits = ggml_backend_sched_get_n_splits(sched);
         ggml_free(ctx);
-        if (step >= 0) t_tg += now_s() - ts;
+        if (step >= 0) {
+            const double t5 = now_s();
+            t_tg += t5 - ts;
+            t_build += t1 - ts; t_alloc += t2 - t1; t_in += t3 - t2; t_comp += t4 - t3; t_out += t5 - t4;
+        }
     }
     printf("{\"b1_decode_tok_s\": %.2f, \"ms_per_token\": %.4f, \"n_layer\": %d, \"n_past\": %d, \"steps\": %d, "
-           "\"graph_nodes\": %d, \"sched_splits\": %d, \"load_s\": %.1f, \"last_token\": %d}\n",
-           n_steps / t_tg, t_tg / n_steps * 1e3, n_layer, n_past0, n_steps, n_nodes, n_splits, t_load, tok);
+           "\"graph_nodes\": %d, \"sched_splits\": %d, \"load_s\": %.1f, \"last_token\": %d, \"ms_build\": %.4f, "
+           "\"ms_sched_alloc\": %.4f, \"ms_inputs\": %.4f, \"ms_compute_sync\": %.4f, \"ms_logits_argmax\": %.4f}\n",
+           n_steps / t_tg, t_tg / n_steps * 1e3, n_layer, n_past0, n_steps, n_nodes, n_splits, t_load, tok,
+           t_build / n_steps * 1e3, t_alloc / n_steps * 1e3, t_in / n_steps * 1e3, t_comp / n_steps * 1e3,
+           t_out / n_steps * 1e3);
     ggml_backend_sched_free(sched);
     ggml_backend_buffer_free(wbuf);
     ggml_free(wctx);
