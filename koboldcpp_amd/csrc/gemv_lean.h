@@ -154,7 +154,7 @@ struct ActCopyCol {
 // store R parked results of group slot_g (rows row0.. of segment seg)
 template <int R, int MODE, bool AUX = false>
 __device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0, const float (&slot)[R],
-                                            float *aux0 = nullptr, uint16_t *auxh = nullptr) {
+                                            float *aux0 = nullptr, uint16_t *auxh = nullptr, RopeP rp = RopeP{}) {
     if constexpr (MODE != 2) {
         float *Y = seg == 0 ? a.Y[0] : (seg == 1 ? a.Y[1] : a.Y[2]);
 #pragma unroll
@@ -164,8 +164,22 @@ __device__ __forceinline__ void store_group(const DecArgs &a, int seg, int row0,
             if constexpr (AUX && MODE == 0) {      // the ggml plugin's MUL_MAT -> ADD: the product node's tensor too
                 const float rv = a.res ? a.res[row0 + r] : 0.0f;
                 if (aux0) aux0[row0 + r] = v;
-                if (auxh) auxh[row0 + r] = f2h(v);
+                if (auxh && !rp.out) auxh[row0 + r] = f2h_rn(v);
                 Y[row0 + r] = a.res ? __fadd_rn(v, rv) : v;
+                if constexpr (R % 2 == 0) {
+                    if (rp.out && (r & 1)) {          // MUL_MAT -> ROPE (-> CPY): the pair (row0 + r - 1, row0 + r)
+                        const int row = row0 + r - 1;
+                        float c, s;
+                        ggml_rope_cs((float)rp.pos[0], (int64_t)((row % rp.D) / 2), rp.ff, rp.theta_scale, rp.freq_scale,
+                                     rp.ext_factor, rp.attn_factor, rp.mscale_ext, rp.corr0, rp.corr1, c, s);
+                        const float x0 = slot[r - 1], x1 = v;
+                        const float o0 = __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s));
+                        const float o1 = __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c));
+                        rp.out[row] = o0;
+                        rp.out[row + 1] = o1;
+                        if (auxh) { auxh[row] = f2h_rn(o0); auxh[row + 1] = f2h_rn(o1); }
+                    }
+                }
             } else {
                 Y[row0 + r] = ((MODE == 0 || MODE == 3) && a.res) ? __fadd_rn(v, a.res[row0 + r]) : v;
             }

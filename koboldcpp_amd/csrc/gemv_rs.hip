@@ -68,6 +68,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     constexpr bool AUX = false;
     float *const aux0 = nullptr, *const aux1 = nullptr, *const aux2 = nullptr;
     uint16_t *const auxh = nullptr;
+    const RopeP rp{};
 #include "gemv_rs_body.inc"
 }
 // the ggml plugin's fused nodes (AuxOut): the same body storing the intermediate nodes' tensors too -- MODE 0 the
@@ -79,6 +80,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs_aux(const DecArgs a, const
     constexpr bool XL = false, ROUTE = false, AUX = true;
     float *const aux0 = o.p0, *const aux1 = o.p1, *const aux2 = o.p2;
     uint16_t *const auxh = o.h0;
+    const RopeP rp = o.rope;
 #include "gemv_rs_body.inc"
 }
 
@@ -137,6 +139,10 @@ int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
     // runtime's launches carry none of it: MUL_MAT -> ADD as the plain single-token launch below (quantize prologue,
     // 8 waves), the SiLU GLU as KCPP_RS_P(2)'s mode 1
     if (g_rs_aux) {
+        // with a ROPE behind the product: two rows per group (a rope pair in one lane), as the runtime's q|k|v launch
+        if (g_rs_aux->rope.out)
+            return mode == 0 && pro == 2 && ntot <= 16384 && ntot % 2 == 0
+                       ? launch_rs<TYPE, NI, 2, 0, 2, MC, 0, 4, false, false, true>(a, 512, s) : -3;
         if (mode == 0 && pro == 2 && ntot <= 16384) return launch_rs<TYPE, NI, 1, 0, 2, MC, 0, 8, false, false, true>(a, 256, s);
         if (mode == 1 && pro == 2 && a.nseg == 1 && !a.eid && !a.route_w)
             return launch_rs<TYPE, NI, 1, 1, 2, MC, 1, 4, false, false, true>(a, 512, s);
@@ -341,6 +347,7 @@ __global__ void __launch_bounds__(256) k_gemv_qkv_dual(const DecArgs a, const De
         constexpr bool XL = false, ROUTE = false, AUX = false;
         float *const aux0 = nullptr, *const aux1 = nullptr, *const aux2 = nullptr;
         uint16_t *const auxh = nullptr;
+        const RopeP rp{};
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
         const int KB_BID = (int)blockIdx.x, KB_NBLK = nA;
 #include "gemv_rs_body.inc"
@@ -470,8 +477,8 @@ extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void 
 // the ggml plugin's fused nodes: kcpp_gemv_rs's launch (modes 0 and 1, quantize prologue, one segment) through the AUX
 // instances, which also store the intermediate nodes' tensors (AuxOut); -3 where no AUX instance covers the shape
 extern "C" int kcpp_gemv_rs_aux(int type, const void *args, int mode, const AuxOut *aux, void *stream) {
-    if (!aux || (mode == 0 && !aux->p0 && !aux->h0) || (mode == 1 && (!aux->p0 || !aux->p1 || !aux->p2)) ||
-        (mode != 0 && mode != 1))
+    if (!aux || (mode == 0 && !aux->p0 && !aux->h0 && !aux->rope.out) || (mode == 1 && (!aux->p0 || !aux->p1 || !aux->p2)) ||
+        (mode != 0 && mode != 1) || (aux->rope.out && (mode != 0 || !aux->rope.pos || aux->rope.D < 2 || aux->rope.D % 2)))
         return -3;
     g_rs_aux = aux;
     const int rc = kcpp_gemv_rs(type, args, mode, 2, stream);

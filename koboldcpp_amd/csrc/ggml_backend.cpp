@@ -1003,8 +1003,9 @@ bool mem_overlap(const kggml_tensor *a, const kggml_tensor *b) {
     const char *pa = (const char *)a->data, *pb = (const char *)b->data;
     return pa < pb + nbytes(b) && pb < pa + nbytes(a);
 }
+// the same bytes element for element: same start and size, both contiguous (a reshape of the other counts)
 bool same_bytes(const kggml_tensor *a, const kggml_tensor *b) {
-    return a->data == b->data && nbytes(a) == nbytes(b) && a->nb[1] == b->nb[1];
+    return a->data == b->data && nbytes(a) == nbytes(b) && a->type == b->type && is_contiguous(a) && is_contiguous(b);
 }
 bool exact_or_disjoint(const kggml_tensor *a, const kggml_tensor *b) { return same_bytes(a, b) || !mem_overlap(a, b); }
 bool f32_vec(const kggml_tensor *t, int64_t n) {   // a contiguous f32 [n, 1, 1, 1]
@@ -1065,7 +1066,8 @@ int fuse_mv_add(BackendCtx *bc, kggml_cgraph *g, int i) {
     memset(&d, 0, sizeof d);
     d.K = a->ne[0]; d.nseg = 1; d.W[0] = (const uint8_t *)W; d.N[0] = N; d.Y[0] = (float *)ad->data;
     d.x = (const float *)x->data; d.res = (const float *)r->data;
-    const AuxOut o{(float *)mm->data, nullptr, nullptr, nullptr};
+    AuxOut o{};
+    o.p0 = (float *)mm->data;
     if (kcpp_gemv_rs_aux(tt, &d, 0, &o, bc->stream) != 0) {
         (void)hipGetLastError();
         return 0;
@@ -1106,7 +1108,8 @@ int fuse_glu(BackendCtx *bc, kggml_cgraph *g, int i) {
     memset(&d, 0, sizeof d);
     d.K = wg->ne[0]; d.nseg = 1; d.W[0] = (const uint8_t *)Wg; d.W2 = (const uint8_t *)Wu; d.N[0] = N;
     d.Y[0] = (float *)mu->data; d.x = (const float *)x->data;
-    const AuxOut o{(float *)gate->data, (float *)s->data, (float *)up->data, nullptr};
+    AuxOut o{};
+    o.p0 = (float *)gate->data; o.p1 = (float *)s->data; o.p2 = (float *)up->data;
     if (kcpp_gemv_rs_aux(tt, &d, 1, &o, bc->stream) != 0) {
         (void)hipGetLastError();
         return 0;
@@ -1173,12 +1176,63 @@ int fuse_mv_cpy(BackendCtx *bc, kggml_cgraph *g, int i) {
     memset(&dd, 0, sizeof dd);
     dd.K = a->ne[0]; dd.nseg = 1; dd.W[0] = (const uint8_t *)W; dd.N[0] = mm->ne[0]; dd.Y[0] = (float *)mm->data;
     dd.x = (const float *)x->data;
-    const AuxOut o{nullptr, nullptr, nullptr, (uint16_t *)d->data};
+    AuxOut o{};
+    o.h0 = (uint16_t *)d->data;
     if (kcpp_gemv_rs_aux(tt, &dd, 0, &o, bc->stream) != 0) {
         (void)hipGetLastError();
         return 0;
     }
     return j - i + 1;
+}
+
+// single-token MUL_MAT -> RESHAPE -> ROPE (NORM, n_dims = head size) [-> CPY into the F16 cache]: the q / k path of
+// build_llama; the mat-vec stores the product, the roped values (two rows per group: a pair per lane, ggml_rope_cs --
+// the ROPE kernel's own code) and their f16 copy
+int fuse_mv_rope(BackendCtx *bc, kggml_cgraph *g, int i) {
+    kggml_tensor *mm = g->nodes[i];
+    if (!mv_node(mm)) return 0;
+    int k = i + 1;
+    while (k < g->n_nodes && k <= i + 2 && (g->nodes[k]->op == KGGML_OP_RESHAPE || g->nodes[k]->op == KGGML_OP_VIEW)) ++k;
+    if (k >= g->n_nodes) return 0;
+    kggml_tensor *rp = g->nodes[k];
+    if (rp->op != KGGML_OP_ROPE || !supports(rp)) return 0;
+    kggml_tensor *rx = rp->src[0], *pos = rp->src[1];
+    const int n_dims = rp->op_params[1], mode = rp->op_params[2];
+    if (!rx || !pos || pos->type != KGGML_TYPE_I32 || mode != 0 || rx->data != mm->data || !is_contiguous(rx) ||
+        nbytes(rx) != nbytes(mm) || n_dims != rx->ne[0] || rx->ne[0] % 2 || rx->ne[2] != 1 || rx->ne[3] != 1 ||
+        !is_contiguous(rp) || !same_shape(rp, rx) || rp->type != KGGML_TYPE_F32)
+        return 0;
+    if (rp->src[2] && rp->src[2]->type != KGGML_TYPE_F32) return 0;
+    kggml_tensor *a = mm->src[0], *x = mm->src[1];
+    const int tt = matmul_layout(a->type, a->ne[0]);
+    if (tt != KT_Q4_K_RS && tt != KT_Q5_K_RS && tt != KT_Q6_K_RS) return 0;
+    const int j = cpy16_after(g, k);
+    kggml_tensor *d = j ? g->nodes[j]->src[1] : nullptr;
+    if (mem_overlap(mm, x) || mem_overlap(rp, x) || !exact_or_disjoint(mm, rp) || mem_overlap(pos, rp) ||
+        mem_overlap(pos, mm))
+        return 0;
+    if (d && (mem_overlap(d, x) || mem_overlap(d, mm) || mem_overlap(d, rp))) return 0;
+    const void *W = native_image(bc, a, tt);
+    if (!W) return 0;
+    DecArgs dd;
+    memset(&dd, 0, sizeof dd);
+    dd.K = a->ne[0]; dd.nseg = 1; dd.W[0] = (const uint8_t *)W; dd.N[0] = mm->ne[0]; dd.Y[0] = (float *)mm->data;
+    dd.x = (const float *)x->data;
+    AuxOut o{};
+    o.h0 = d ? (uint16_t *)d->data : nullptr;
+    float cst[4];
+    kcpp_ggml_rope_consts(n_dims, rp->op_params[4], op_f(rp, 5), op_f(rp, 6), op_f(rp, 8), op_f(rp, 9), op_f(rp, 10), cst);
+    o.rope.out = (float *)rp->data;
+    o.rope.pos = (const int32_t *)pos->data;
+    o.rope.ff = rp->src[2] ? (const float *)rp->src[2]->data : nullptr;
+    o.rope.D = (int)rx->ne[0];
+    o.rope.theta_scale = cst[0]; o.rope.corr0 = cst[1]; o.rope.corr1 = cst[2]; o.rope.mscale_ext = cst[3];
+    o.rope.freq_scale = op_f(rp, 6); o.rope.ext_factor = op_f(rp, 7); o.rope.attn_factor = op_f(rp, 8);
+    if (kcpp_gemv_rs_aux(tt, &dd, 0, &o, bc->stream) != 0) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return (j ? j : k) - i + 1;
 }
 
 // the number of nodes node i starts a fused launch for (0: none)
@@ -1189,6 +1243,7 @@ int fuse_at(BackendCtx *bc, kggml_cgraph *g, int i) {
     case KGGML_OP_MUL_MAT: {
         int k = fuse_glu(bc, g, i);
         if (!k) k = fuse_mv_add(bc, g, i);
+        if (!k) k = fuse_mv_rope(bc, g, i);
         return k ? k : fuse_mv_cpy(bc, g, i);
     }
     default: return 0;

@@ -244,27 +244,17 @@ __global__ void k_rope(const char *__restrict__ x, TD tx, char *__restrict__ y, 
                 const float t0 = *(const float *)(xr + i0 * tx.nb[0]), t1 = *(const float *)(xr + (i0 + 1) * tx.nb[0]);
                 *(float *)(yr + i0 * ty.nb[0]) = t0;
                 *(float *)(yr + (i0 + 1) * ty.nb[0]) = t1;
-                if (h16) { h16[r * tx.ne[0] + i0] = f2h(t0); h16[r * tx.ne[0] + i0 + 1] = f2h(t1); }
+                if (h16) { h16[r * tx.ne[0] + i0] = f2h_rn(t0); h16[r * tx.ne[0] + i0 + 1] = f2h_rn(t1); }
                 continue;
             }
-            float theta = p;
-            for (int64_t k = 0; k < ip; ++k) theta *= theta_scale;
-            const float theta_extrap = theta / (ff ? ff[ip] : 1.0f);
-            const float theta_interp = freq_scale * theta_extrap;
-            float th = theta_interp, mscale = attn_factor;
-            if (ext_factor != 0.0f) {
-                const float yy = (ip - corr0) / fmaxf(0.001f, corr1 - corr0);
-                const float ramp_mix = (1.0f - fminf(1.0f, fmaxf(0.0f, yy))) * ext_factor;
-                th = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
-                mscale = mscale_ext;
-            }
-            const float c = (float)cos((double)th) * mscale, s = (float)sin((double)th) * mscale;
+            float c, s;
+            ggml_rope_cs(p, ip, ff, theta_scale, freq_scale, ext_factor, attn_factor, mscale_ext, corr0, corr1, c, s);
             const int64_t ia = neox ? ip : i0, ib = neox ? ip + n_dims / 2 : i0 + 1;
             const float x0 = *(const float *)(xr + ia * tx.nb[0]), x1 = *(const float *)(xr + ib * tx.nb[0]);
             const float o0 = __fsub_rn(__fmul_rn(x0, c), __fmul_rn(x1, s)), o1 = __fadd_rn(__fmul_rn(x0, s), __fmul_rn(x1, c));
             *(float *)(yr + ia * ty.nb[0]) = o0;
             *(float *)(yr + ib * ty.nb[0]) = o1;
-            if (h16) { h16[r * tx.ne[0] + ia] = f2h(o0); h16[r * tx.ne[0] + ib] = f2h(o1); }
+            if (h16) { h16[r * tx.ne[0] + ia] = f2h_rn(o0); h16[r * tx.ne[0] + ib] = f2h_rn(o1); }
         }
     }
 }
@@ -480,6 +470,21 @@ int kcpp_ggml_rms_norm_mul(const void *x, const kcpp_tdesc *tx, void *r, const k
     return 0;
 }
 
+// host-side constants exactly as the CPU op computes them (ggml.c:14321-14324, rope_yarn :14223):
+// out = {theta_scale, corr0, corr1, mscale_ext}
+void kcpp_ggml_rope_consts(int n_dims, int n_ctx_orig, float freq_base, float freq_scale, float attn_factor,
+                           float beta_fast, float beta_slow, float *out) {
+    const float theta_scale = powf(freq_base, -2.0f / n_dims);
+    auto corr_dim = [&](float n_rot) {
+        return n_dims * logf(n_ctx_orig / (n_rot * 2 * (float)M_PI)) / (2 * logf(freq_base));
+    };
+    const float start = floorf(corr_dim(beta_fast)), end = ceilf(corr_dim(beta_slow));
+    out[0] = theta_scale;
+    out[1] = fmaxf(0.0f, start);
+    out[2] = fminf((float)(n_dims - 1), end);
+    out[3] = attn_factor * (1.0f + 0.1f * logf(1.0f / freq_scale));
+}
+
 int kcpp_ggml_rope(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_tdesc *ty, const int32_t *pos,
                    const float *freq_factors, int n_dims, int mode, int n_ctx_orig, float freq_base, float freq_scale,
                    float ext_factor, float attn_factor, float beta_fast, float beta_slow, void *stream) {
@@ -494,14 +499,9 @@ int kcpp_ggml_rope_f16(const void *x, const kcpp_tdesc *tx, void *y, const kcpp_
     if (nr == 0) return 0;
     if (n_dims > tx->ne[0] || n_dims % 2 || tx->nb[0] != 4) return -1;
     if (mode != 0 && mode != 2) return -2;
-    // host-side constants exactly as the CPU op computes them (ggml.c:14321-14324, rope_yarn :14223)
-    const float theta_scale = powf(freq_base, -2.0f / n_dims);
-    auto corr_dim = [&](float n_rot) {
-        return n_dims * logf(n_ctx_orig / (n_rot * 2 * (float)M_PI)) / (2 * logf(freq_base));
-    };
-    const float start = floorf(corr_dim(beta_fast)), end = ceilf(corr_dim(beta_slow));
-    const float corr0 = fmaxf(0.0f, start), corr1 = fminf((float)(n_dims - 1), end);
-    const float mscale_ext = attn_factor * (1.0f + 0.1f * logf(1.0f / freq_scale));
+    float cst[4];
+    kcpp_ggml_rope_consts(n_dims, n_ctx_orig, freq_base, freq_scale, attn_factor, beta_fast, beta_slow, cst);
+    const float theta_scale = cst[0], corr0 = cst[1], corr1 = cst[2], mscale_ext = cst[3];
     const dim3 g = row_grid(tx->ne[0] / 2, nr, 64);
     hipLaunchKernelGGL(k_rope, g, dim3(64), 0, (hipStream_t)stream, (const char *)x, td_of(tx), (char *)y, td_of(ty), pos,
                        freq_factors, n_dims, mode == 2 ? 1 : 0, freq_scale, ext_factor, attn_factor, mscale_ext, corr0,

@@ -87,6 +87,29 @@ __device__ __forceinline__ uint16_t f2h_rn(float x) {
 
 __device__ __forceinline__ int sdot4(int a, int b, int c) { return __builtin_amdgcn_sdot4(a, b, c, false); }
 
+// (cos, sin) of rope pair ip at position p, as ggml_compute_forward_rope_f32 (ggml.c:14272) with
+// ggml_rope_cache_init (:14246) and rope_yarn (:14223): theta iterated from the position by theta_scale, the YaRN
+// ramp when ext_factor != 0, cos / sin correctly rounded through double (the CPU's glibc cosf / sinf are within 1 ulp
+// of that), times mscale.  Shared by the ggml plugin's ROPE kernel and the mat-vec epilogue it is fused into, so both
+// give the same bits.
+__device__ __forceinline__ void ggml_rope_cs(float p, int64_t ip, const float *ff, float theta_scale, float freq_scale,
+                                             float ext_factor, float attn_factor, float mscale_ext, float corr0,
+                                             float corr1, float &c, float &s) {
+    float theta = p;
+    for (int64_t k = 0; k < ip; ++k) theta *= theta_scale;
+    const float theta_extrap = theta / (ff ? ff[ip] : 1.0f);
+    const float theta_interp = freq_scale * theta_extrap;
+    float th = theta_interp, mscale = attn_factor;
+    if (ext_factor != 0.0f) {
+        const float yy = (ip - corr0) / fmaxf(0.001f, corr1 - corr0);
+        const float ramp_mix = (1.0f - fminf(1.0f, fmaxf(0.0f, yy))) * ext_factor;
+        th = theta_interp * (1 - ramp_mix) + theta_extrap * ramp_mix;
+        mscale = mscale_ext;
+    }
+    c = (float)cos((double)th) * mscale;
+    s = (float)sin((double)th) * mscale;
+}
+
 // nearest_int() of ggml-quants.c:1640 with the multiply NOT fused (the reference is built
 // -std=c11, i.e. -ffp-contract=off).
 __device__ __forceinline__ int nearest_int_mul(float a, float b) {

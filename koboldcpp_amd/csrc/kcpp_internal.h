@@ -77,9 +77,20 @@ struct DecArgs {
 // (the MUL_MAT node under an ADD; null without one), h0 = the product as f16 (a CPY into a contiguous F16 cache view;
 // null without one).  MODE 1: p0 = gate, p1 = silu(gate), p2 = up.  A separate kernel parameter of the RS kernels'
 // AUX instances (kcpp_gemv_rs_aux), so the runtime's launches and their DecArgs carry none of it.
+// RopeP (MODE 0, pairs of rows): the ROPE node (mode NORM, n_dims = D) that follows the product -- out = its f32
+// output, rows (2i, 2i+1) of each D-row head rotated by pair (i mod D/2) at position pos[0] (ggml_rope_cs); h0 then
+// holds the roped values as f16 (the CPY of the ROPE into the cache)
+struct RopeP {
+    float *out;
+    const int32_t *pos;
+    const float *ff;
+    int D;
+    float theta_scale, freq_scale, ext_factor, attn_factor, mscale_ext, corr0, corr1;
+};
 struct AuxOut {
     float *p0, *p1, *p2;
     uint16_t *h0;
+    RopeP rope;
 };
 
 
@@ -150,6 +161,9 @@ extern "C" int kcpp_flash_attn_dec_ta(const uint16_t *q16, const uint16_t *kc, c
                                       int n_kv_max, float scale, void *stream);
 // decode mat-vec over the row-major RS layouts (gemv_rs.hip); -3 = not covered
 extern "C" int kcpp_gemv_rs(int type, const void *args, int mode, int pro, void *stream);
+// ROPE's host constants {theta_scale, corr0, corr1, mscale_ext} (ggml_ops.hip; the CPU op's own expressions)
+extern "C" void kcpp_ggml_rope_consts(int n_dims, int n_ctx_orig, float freq_base, float freq_scale, float attn_factor,
+                                      float beta_fast, float beta_slow, float *out);
 // the same single-token launch (mode 0 / 1, quantize prologue) storing the intermediate nodes' tensors too (AuxOut)
 extern "C" int kcpp_gemv_rs_aux(int type, const void *args, int mode, const AuxOut *aux, void *stream);
 extern "C" int kcpp_rs_supported(int type, int64_t K);

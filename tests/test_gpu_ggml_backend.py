@@ -736,7 +736,7 @@ FUSION_CASES = [("q4k_q6k", R.Q4_K, R.Q6_K, "ctx"), ("q4k_q6k_gallocr", R.Q4_K, 
 @pytest.mark.parametrize("case", FUSION_CASES, ids=lambda c: c[0])
 def test_decode_node_fusion_matches_node_by_node(env, case):
     """the plugin's decode node fusion (ggml_backend.cpp fuse_at: RMS_NORM+MUL, MUL_MAT+ADD, the SiLU GLU quadruple,
-    ROPE / MUL_MAT + CPY into the F16 cache)
+    MUL_MAT + ROPE, ROPE / MUL_MAT + CPY into the F16 cache)
     against the same graph run node by node (kcpp_ggml_backend_set_fusion(be, 0)) on one token of a build_llama
     layer: bit for bit on the layer output, and -- each tensor in its own allocation (ggml_backend_alloc_ctx_tensors)
     -- on EVERY node's output, the fused launches writing the intermediate nodes' tensors too.  Allocated by
@@ -833,9 +833,9 @@ def test_decode_node_fusion_matches_node_by_node(env, case):
     (nf1, a), (nf0, b) = runs
     L.kcpp_rs_supported.argtypes = [I, I64]
     rs = [bool(L.kcpp_rs_supported(t, k)) for t, (k, n) in zip(tys, shapes)]      # ggml type ids = KT_ codes
-    # 2 norms (+ MUL); k's ROPE + VIEW + CPY into the cache; on RS layouts v's MUL_MAT + VIEW + CPY, wo + ADD, the
-    # GLU quadruple, down + ADD
-    want = 2 * 2 + 3 + 3 * rs[2] + 2 * rs[3] + 4 * rs[4] + 2 * rs[6]
+    # 2 norms (+ MUL); on RS layouts q's MUL_MAT + RESHAPE + ROPE, k's MUL_MAT + RESHAPE + ROPE + VIEW + CPY into the
+    # cache (otherwise its ROPE + VIEW + CPY), v's MUL_MAT + VIEW + CPY, wo + ADD, the GLU quadruple, down + ADD
+    want = 2 * 2 + 3 * rs[0] + (5 if rs[1] else 3) + 3 * rs[2] + 2 * rs[3] + 4 * rs[4] + 2 * rs[6]
     print("%s: %d nodes fused of %d (expected %d)" % (name, nf1, len(nodes), want))
     assert nf0 == 0 and nf1 == want, (nf1, want)
     assert rs[4] == (wt != R.Q8_0)
