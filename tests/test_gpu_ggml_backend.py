@@ -841,3 +841,89 @@ def test_decode_node_fusion_matches_node_by_node(env, case):
     assert rs[4] == (wt != R.Q8_0)
     for i, (u, w_) in enumerate(zip(a, b)):
         assert np.array_equal(u.view(np.uint32), w_.view(np.uint32)), (i, rel(u, w_))
+
+
+@pytest.mark.parametrize("wt,mode,ext,ff", [(R.Q4_K, 0, 0.0, False), (R.Q4_K, 0, 1.0, True), (R.Q4_K, 2, 0.0, False),
+                                            (R.Q6_K, 0, 1.0, False), (R.Q8_0, 0, 0.0, True)],
+                         ids=["q4k_norm", "q4k_norm_yarn_ff", "q4k_neox", "q6k_norm_yarn", "q8_0_norm_ff"])
+def test_mv_rope_cpy_fusion(env, wt, mode, ext, ff):
+    """the k path of a token graph -- MUL_MAT -> RESHAPE -> ROPE -> VIEW -> CPY into an F16 cache view -- fused
+    (NORM rope on RS layouts: one mat-vec launch with the rope pairs in its epilogue; NEOX rope or other layouts: the
+    ROPE + CPY pair) against node by node, bitwise on the product, the roped tensor and the cache bytes, with YaRN
+    (ext_factor, freq_scale 0.25) and freq factors; and the fused result against the reference CPU backend"""
+    G, L, be = env
+    L.kcpp_ggml_backend_set_fusion.argtypes = [P, I]
+    Kd, D, HKV, n_ctx, n_past = 4096, 128, 8, 64, 21
+    EKV = D * HKV
+    w = R.synth(wt, 9, 77, Kd, EKV)
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal(Kd).astype(np.float32)
+    kc = (rng.standard_normal((n_ctx, EKV)) * 0.5).astype(np.float16)
+    pos = np.array([n_past], np.int32)
+    fq = (1.0 + 0.5 * rng.random(D // 2)).astype(np.float32)
+    fscale = 0.25 if ext else 1.0
+
+    def build(ctx):
+        Wt = G.ggml_new_tensor_2d(ctx, wt, Kd, EKV)
+        X = G.ggml_new_tensor_2d(ctx, R.F32, Kd, 1)
+        KC = G.ggml_new_tensor_1d(ctx, R.F16, n_ctx * EKV)
+        Pz = G.ggml_new_tensor_1d(ctx, 26, 1)
+        FF = G.ggml_new_tensor_1d(ctx, R.F32, D // 2) if ff else None
+        mm = G.ggml_mul_mat(ctx, Wt, X)
+        k = G.ggml_rope_ext(ctx, G.ggml_reshape_3d(ctx, mm, D, HKV, 1), Pz, FF, D, mode, 4096, 500000.0, fscale, ext,
+                            1.0, 32.0, 1.0)
+        st = G.ggml_cpy(ctx, k, G.ggml_view_1d(ctx, KC, EKV, n_past * EKV * 2))
+        ins = [Wt, X, KC, Pz] + ([FF] if ff else [])
+        return ins, [mm, k], st, KC
+
+    data = [w, x, kc, pos] + ([fq] if ff else [])
+    outs = {}
+    for tag in ("fused", "nodes", "cpu"):
+        ctx = G.ggml_init(InitParams(64 << 20, None, tag != "cpu"))
+        ins, probes, st, KC = build(ctx)
+        g = G.ggml_new_graph(ctx)
+        G.ggml_build_forward_expand(g, st)
+        if tag != "cpu":
+            assert L.kcpp_ggml_backend_set_fusion(ctypes.c_void_p(be), int(tag == "fused")) == 0
+            buf = G.ggml_backend_alloc_ctx_tensors(ctx, be)
+            for t, a in zip(ins, data):
+                a = np.ascontiguousarray(a)
+                G.ggml_backend_tensor_set(t, a.ctypes.data, 0, a.nbytes)
+            try:
+                assert G.ggml_backend_graph_compute(be, g) == 0, L.kcpp_ggml_backend_last_error()
+                nf = L.kcpp_ggml_backend_last_fused()
+            finally:
+                L.kcpp_ggml_backend_set_fusion(ctypes.c_void_p(be), 1)
+            got = []
+            for t in probes:
+                r = np.empty(G.ggml_nbytes(t) // 4, np.float32)
+                G.ggml_backend_tensor_get(t, r.ctypes.data, 0, r.nbytes)
+                got.append(r)
+            c = np.empty(n_ctx * EKV, np.float16)
+            G.ggml_backend_tensor_get(KC, c.ctypes.data, 0, c.nbytes)
+            got.append(c)
+            G.ggml_backend_buffer_free(buf)
+            outs[tag] = (nf, got)
+        else:
+            for t, a in zip(ins, data):
+                a = np.ascontiguousarray(a)
+                ctypes.memmove(G.ggml_get_data(t), a.ctypes.data, a.nbytes)
+            assert G.ggml_graph_compute_with_ctx(ctx, g, 8) == 0
+            got = [np.ctypeslib.as_array((ctypes.c_float * (G.ggml_nbytes(t) // 4)).from_address(G.ggml_get_data(t))).copy()
+                   for t in probes]
+            got.append(np.ctypeslib.as_array((ctypes.c_uint16 * (n_ctx * EKV)).from_address(G.ggml_get_data(KC))).copy()
+                       .view(np.float16))
+            outs[tag] = (0, got)
+        G.ggml_free(ctx)
+    L.kcpp_rs_supported.argtypes = [I, I64]
+    rs = bool(L.kcpp_rs_supported(wt, Kd))
+    (nf1, a), (nf0, b), (_, c) = outs["fused"], outs["nodes"], outs["cpu"]
+    assert nf0 == 0 and nf1 == (5 if rs and mode == 0 else 3), nf1
+    for u, v in zip(a, b):
+        assert np.array_equal(u.view(np.uint16 if u.dtype == np.float16 else np.uint32),
+                              v.view(np.uint16 if v.dtype == np.float16 else np.uint32))
+    assert rel(a[0], c[0]) <= 3e-6, rel(a[0], c[0])                  # the product: exact dots, fp32 order
+    assert rel(a[1], c[1]) <= 1e-5, rel(a[1], c[1])                  # roped
+    kcache = a[2].astype(np.float32).reshape(n_ctx, EKV)
+    assert np.array_equal(kcache[:n_past], c[2].astype(np.float32).reshape(n_ctx, EKV)[:n_past])   # untouched rows
+    assert np.abs(kcache[n_past] - a[1]).max() <= np.abs(a[1]).max() * 2e-3       # the stored row: f16 of the roped
