@@ -1791,6 +1791,10 @@ __global__ void __launch_bounds__(512, 1) k_gemm_q4v4(const uint8_t *__restrict_
     __syncthreads();
 
     int st = 0;
+    // waves 4-7 (the later-dispatched half, each sharing a SIMD with one of waves 0-3 running the same program) at
+    // static priority 1: the arbitration loser otherwise (MI355X_MICROARCH.md, two waves per SIMD, item 4); bitwise
+    // the same results.  tools/gemm_ab.py: q|k|v 53.3 -> 50.5 us, bench prefill 34.16k -> 34.56k tok/s
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
     for (int64_t sb = sbb; sb < sbe; ++sb) {
         const int buf = (int)((sb - sbb) & 1);
         const bool wn = sb + NST - 1 < sbe && KCPP_GEMM_PROBE != 1 && KCPP_GEMM_PROBE != 5;
@@ -2045,6 +2049,7 @@ __global__ void __launch_bounds__(64 * NW, 1) k_gemm_q6p(const i32x4 *__restrict
     uint16_t d = pd[sbb];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);      // as k_gemm_q4v4 (q6p down 114.1 -> 113.1 us)
     for (int64_t sb = sbb; sb < sbe; ++sb) {
         const int buf = (int)((sb - sbb) & 1);
         const bool nx = sb + 1 < sbe;
