@@ -266,6 +266,8 @@ void ggml_cuda_set_mul_mat_q(bool mul_mat_q);
 int kcpp_ggml_backend_last_nodes(void);
 /* of those, the nodes that ran inside a fused launch (RMS_NORM+MUL, MUL_MAT+ADD, the SiLU GLU; 0 with KCPP_B1_UNFUSED=1) */
 int kcpp_ggml_backend_last_fused(void);
+/* and the number of fused launches they ran as */
+int kcpp_ggml_backend_last_fused_launches(void);
 /* device bytes held in separate native weight images (0 when every weight sits in a weight buffer: those are
  * converted in place, one copy of the model) */
 int64_t kcpp_ggml_backend_image_bytes(void);

@@ -12,7 +12,9 @@
 namespace lean {
 
 // NT threads per workgroup (MAXC = 16-element chunks per thread: ceil(K / (16 NT)))
-template <int PRO, int MAXC, int NT = 256>
+// STORE (the ggml plugin's RMS_NORM -> MUL fused into the first consumer, AUX instances): compute() also stores the
+// normalised row r = x * scale and the product y = r * w (the two nodes' tensors) where given
+template <int PRO, int MAXC, int NT = 256, bool STORE = false>
 struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_impl.h); loads first
     float v[MAXC][16];
     float w[PRO == 1 ? MAXC : 1][16];
@@ -37,7 +39,8 @@ struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_imp
             }
         }
     }
-    __device__ __forceinline__ void compute(const DecArgs &a, uint8_t *lds, unsigned long long *st_ = nullptr) {
+    __device__ __forceinline__ void compute(const DecArgs &a, uint8_t *lds, unsigned long long *st_ = nullptr,
+                                            float *rout = nullptr, float *yout = nullptr) {
         const int tid = threadIdx.x;
 #ifdef KCPP_STAMPS
 #define LP_STAMP(ph) if (threadIdx.x == 0 && st_) __hip_atomic_store(&st_[(ph)], __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -66,10 +69,37 @@ struct ActPro {               // rms_norm * w -> Q8_K into LDS (see gemv_dec_imp
 #pragma unroll
             for (int i = 4; i < NT / 64; i += 4) sum += red[i] + red[i + 1] + red[i + 2] + red[i + 3];
             const float scale = 1.0f / sqrtf((float)(sum / (double)K) + a.eps);   // ggml.c:12089
+            if constexpr (STORE) {
+                if (rout || yout) {
 #pragma unroll
-            for (int i = 0; i < MAXC; ++i)
+                    for (int i = 0; i < MAXC; ++i) {
+                        const int c = tid + NT * i;
+                        float r16[16];
 #pragma unroll
-                for (int e = 0; e < 16; ++e) v[i][e] = __fmul_rn(__fmul_rn(v[i][e], scale), w[i][e]);
+                        for (int e = 0; e < 16; ++e) {
+                            r16[e] = __fmul_rn(v[i][e], scale);
+                            v[i][e] = __fmul_rn(r16[e], w[i][e]);
+                        }
+                        if (c < nchunk) {
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                if (rout) ((float4 *)(rout + 16 * (int64_t)c))[k] = make_float4(r16[4 * k], r16[4 * k + 1], r16[4 * k + 2], r16[4 * k + 3]);
+                                if (yout) ((float4 *)(yout + 16 * (int64_t)c))[k] = make_float4(v[i][4 * k], v[i][4 * k + 1], v[i][4 * k + 2], v[i][4 * k + 3]);
+                            }
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < MAXC; ++i)
+#pragma unroll
+                        for (int e = 0; e < 16; ++e) v[i][e] = __fmul_rn(__fmul_rn(v[i][e], scale), w[i][e]);
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < MAXC; ++i)
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) v[i][e] = __fmul_rn(__fmul_rn(v[i][e], scale), w[i][e]);
+            }
         }
         int8_t *qs = (int8_t *)lds;
         float *d = (float *)(lds + K);

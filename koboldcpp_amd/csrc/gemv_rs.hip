@@ -69,6 +69,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs(const DecArgs a) {
     float *const aux0 = nullptr, *const aux1 = nullptr, *const aux2 = nullptr;
     uint16_t *const auxh = nullptr;
     const RopeP rp{};
+    float *const auxrn = nullptr, *const auxyn = nullptr;
 #include "gemv_rs_body.inc"
 }
 // the ggml plugin's fused nodes (AuxOut): the same body storing the intermediate nodes' tensors too -- MODE 0 the
@@ -81,6 +82,7 @@ __global__ void __launch_bounds__(64 * NWV) k_gemv_rs_aux(const DecArgs a, const
     float *const aux0 = o.p0, *const aux1 = o.p1, *const aux2 = o.p2;
     uint16_t *const auxh = o.h0;
     const RopeP rp = o.rope;
+    float *const auxrn = o.rn, *const auxyn = o.yn;
 #include "gemv_rs_body.inc"
 }
 
@@ -140,12 +142,18 @@ int pick_rs(const DecArgs &a, int mode, int pro, hipStream_t s) {
     // 8 waves), the SiLU GLU as KCPP_RS_P(2)'s mode 1
     if (g_rs_aux) {
         // with a ROPE behind the product: two rows per group (a rope pair in one lane), as the runtime's q|k|v launch
-        if (g_rs_aux->rope.out)
-            return mode == 0 && pro == 2 && ntot <= 16384 && ntot % 2 == 0
-                       ? launch_rs<TYPE, NI, 2, 0, 2, MC, 0, 4, false, false, true>(a, 512, s) : -3;
+        if (g_rs_aux->rope.out) {
+            if (mode != 0 || ntot > 16384 || ntot % 2) return -3;
+            if (pro == 2) return launch_rs<TYPE, NI, 2, 0, 2, MC, 0, 4, false, false, true>(a, 512, s);
+            if (pro == 1 && MC == 1) return launch_rs<TYPE, NI, 2, 0, 1, MC, 0, 4, false, false, true>(a, 512, s);
+            return -3;
+        }
         if (mode == 0 && pro == 2 && ntot <= 16384) return launch_rs<TYPE, NI, 1, 0, 2, MC, 0, 8, false, false, true>(a, 256, s);
-        if (mode == 1 && pro == 2 && a.nseg == 1 && !a.eid && !a.route_w)
-            return launch_rs<TYPE, NI, 1, 1, 2, MC, 1, 4, false, false, true>(a, 512, s);
+        if (mode == 1 && a.nseg == 1 && !a.eid && !a.route_w) {
+            if (pro == 2) return launch_rs<TYPE, NI, 1, 1, 2, MC, 1, 4, false, false, true>(a, 512, s);
+            // the norm in the prologue (the runtime's GLU shape: 8 waves, group prefetch)
+            if (pro == 1 && MC == 1) return launch_rs<TYPE, NI, 1, 1, 1, MC, 1, 8, false, false, true>(a, 256, s);
+        }
         return -3;
     }
     if (mode == 1 && pro == 1 && R == 1) {
@@ -348,6 +356,7 @@ __global__ void __launch_bounds__(256) k_gemv_qkv_dual(const DecArgs a, const De
         float *const aux0 = nullptr, *const aux1 = nullptr, *const aux2 = nullptr;
         uint16_t *const auxh = nullptr;
         const RopeP rp{};
+        float *const auxrn = nullptr, *const auxyn = nullptr;
         extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
         const int KB_BID = (int)blockIdx.x, KB_NBLK = nA;
 #include "gemv_rs_body.inc"
@@ -480,8 +489,13 @@ extern "C" int kcpp_gemv_rs_aux(int type, const void *args, int mode, const AuxO
     if (!aux || (mode == 0 && !aux->p0 && !aux->h0 && !aux->rope.out) || (mode == 1 && (!aux->p0 || !aux->p1 || !aux->p2)) ||
         (mode != 0 && mode != 1) || (aux->rope.out && (mode != 0 || !aux->rope.pos || aux->rope.D < 2 || aux->rope.D % 2)))
         return -3;
+    // the norm prologue (rn / yn given): x = the norm's input, nw = the MUL's weight, K <= 4096 (one chunk per thread,
+    // so the prologue's sum order is the plugin's norm kernels' -- ggml_ops.hip row_sumsq16)
+    const DecArgs &da = *(const DecArgs *)args;
+    const bool pro1 = da.nw != nullptr;       // (only the plugin's norm-in launches set nw here)
+    if (pro1 && (da.K > 4096 || da.K % 256)) return -3;
     g_rs_aux = aux;
-    const int rc = kcpp_gemv_rs(type, args, mode, 2, stream);
+    const int rc = kcpp_gemv_rs(type, args, mode, pro1 ? 1 : 2, stream);
     g_rs_aux = nullptr;
     return rc;
 }

@@ -34,6 +34,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <map>
 #include <mutex>
 #include <string>
@@ -50,6 +51,7 @@ namespace {
 std::string g_last_error;
 int g_last_nodes = 0;
 int g_last_fused = 0;     // of those, nodes that ran inside a fused launch (fuse_at)
+int g_last_fused_launches = 0;   // and the fused launches they took
 bool g_mul_mat_q = true;
 
 // ggml type traits (ggml.c type_traits: blck_size, type_size, is_quantized) for every ggml_type id
@@ -1023,6 +1025,42 @@ bool mv_node(const kggml_tensor *m) {
 }
 
 // RMS_NORM -> MUL(norm, w): kcpp_ggml_rms_norm_mul writes the norm row, then the product row
+// an RMS_NORM -> MUL(w) pair run inside the prologue of the mat-vec that consumes it (x, w: the norm's input and
+// weight; r, y: the two nodes' tensors, stored by that launch's workgroup 0; eps: the norm's)
+struct NormIn {
+    kggml_tensor *x, *w, *r, *y;
+    float eps;
+    mutable bool write_r, write_y;
+};
+// the launch reads x (every workgroup) instead of y, so no output of it may touch x or w.  When ggml-alloc has already
+// handed r's or y's bytes to an output of this launch, that tensor is dead (the allocator reuses only freed bytes:
+// r's one consumer is the MUL, y's may all be inside this launch, as the GLU's gate and up) and the node sequence
+// leaves the output there, so it is not written (r == y exactly: r, then y, in one thread).
+bool fuse_dbg() { static const bool on = getenv("KCPP_B1_FUSE_DEBUG") != nullptr; return on; }
+bool normin_ok(const NormIn *ni, std::initializer_list<const kggml_tensor *> outs) {
+    if (!ni) return true;
+    ni->write_r = ni->write_y = true;
+    for (const kggml_tensor *o : outs) {
+        if (!o) continue;
+        if (mem_overlap(o, ni->x) || mem_overlap(o, ni->w)) {
+            if (fuse_dbg()) fprintf(stderr, "[fuse] norm-in: output '%s' overlaps the norm input / weight\n", o->name);
+            return false;
+        }
+        if (mem_overlap(o, ni->r)) ni->write_r = false;
+        if (mem_overlap(o, ni->y)) ni->write_y = false;
+    }
+    return !mem_overlap(ni->r, ni->x) && !mem_overlap(ni->y, ni->x) && !mem_overlap(ni->r, ni->w) &&
+           !mem_overlap(ni->y, ni->w) && exact_or_disjoint(ni->r, ni->y);
+}
+void normin_args(const NormIn *ni, DecArgs &d, AuxOut &o) {
+    if (!ni) return;
+    d.x = (const float *)ni->x->data;
+    d.nw = (const float *)ni->w->data;
+    d.eps = ni->eps;
+    o.rn = ni->write_r ? (float *)ni->r->data : nullptr;
+    o.yn = ni->write_y ? (float *)ni->y->data : nullptr;
+}
+
 int fuse_norm_mul(BackendCtx *bc, kggml_cgraph *g, int i) {
     if (i + 1 >= g->n_nodes) return 0;
     kggml_tensor *nn = g->nodes[i], *m = g->nodes[i + 1];
@@ -1078,7 +1116,7 @@ int fuse_mv_add(BackendCtx *bc, kggml_cgraph *g, int i) {
 // build_ffn's LLM_FFN_SILU + LLM_FFN_PAR: gate = MUL_MAT(Wg, x), s = SILU(gate), up = MUL_MAT(Wu, x), MUL(s, up), in
 // either evaluation order of the two mat-vecs: the GLU mat-vec (mode 1, quantize prologue) writing gate, s, up, then
 // the product (RS layouts; -3 elsewhere and the nodes run one by one)
-int fuse_glu(BackendCtx *bc, kggml_cgraph *g, int i) {
+int fuse_glu(BackendCtx *bc, kggml_cgraph *g, int i, const NormIn *ni = nullptr) {
     if (i + 3 >= g->n_nodes) return 0;
     kggml_tensor *p[3] = {g->nodes[i], g->nodes[i + 1], g->nodes[i + 2]}, *mu = g->nodes[i + 3];
     if (mu->op != KGGML_OP_MUL || !supports(mu)) return 0;
@@ -1092,11 +1130,12 @@ int fuse_glu(BackendCtx *bc, kggml_cgraph *g, int i) {
     if (!gate || !up || gate == up || !in_window(gate) || !in_window(up) || !mv_node(gate) || !mv_node(up)) return 0;
     kggml_tensor *x = gate->src[1], *wg = gate->src[0], *wu = up->src[0];
     if (up->src[1] != x || wg->type != wu->type || !same_shape(wg, wu)) return 0;
+    if (ni && (x != ni->y || !normin_ok(ni, {gate, s, up, mu}))) return 0;
     const int64_t N = gate->ne[0];
     if (!f32_vec(s, N) || !f32_vec(mu, N)) return 0;
     kggml_tensor *outs[4] = {gate, s, up, mu};
     for (int j = 0; j < 4; ++j) {
-        if (mem_overlap(outs[j], x)) return 0;
+        if (mem_overlap(outs[j], ni ? ni->x : x)) return 0;   // the row every workgroup reads
         for (int k = j + 1; k < 4; ++k)
             if (!exact_or_disjoint(outs[j], outs[k])) return 0;
     }
@@ -1110,6 +1149,7 @@ int fuse_glu(BackendCtx *bc, kggml_cgraph *g, int i) {
     d.Y[0] = (float *)mu->data; d.x = (const float *)x->data;
     AuxOut o{};
     o.p0 = (float *)gate->data; o.p1 = (float *)s->data; o.p2 = (float *)up->data;
+    normin_args(ni, d, o);
     if (kcpp_gemv_rs_aux(tt, &d, 1, &o, bc->stream) != 0) {
         (void)hipGetLastError();
         return 0;
@@ -1188,7 +1228,7 @@ int fuse_mv_cpy(BackendCtx *bc, kggml_cgraph *g, int i) {
 // single-token MUL_MAT -> RESHAPE -> ROPE (NORM, n_dims = head size) [-> CPY into the F16 cache]: the q / k path of
 // build_llama; the mat-vec stores the product, the roped values (two rows per group: a pair per lane, ggml_rope_cs --
 // the ROPE kernel's own code) and their f16 copy
-int fuse_mv_rope(BackendCtx *bc, kggml_cgraph *g, int i) {
+int fuse_mv_rope(BackendCtx *bc, kggml_cgraph *g, int i, const NormIn *ni = nullptr) {
     kggml_tensor *mm = g->nodes[i];
     if (!mv_node(mm)) return 0;
     int k = i + 1;
@@ -1208,10 +1248,12 @@ int fuse_mv_rope(BackendCtx *bc, kggml_cgraph *g, int i) {
     if (tt != KT_Q4_K_RS && tt != KT_Q5_K_RS && tt != KT_Q6_K_RS) return 0;
     const int j = cpy16_after(g, k);
     kggml_tensor *d = j ? g->nodes[j]->src[1] : nullptr;
-    if (mem_overlap(mm, x) || mem_overlap(rp, x) || !exact_or_disjoint(mm, rp) || mem_overlap(pos, rp) ||
+    const kggml_tensor *xin = ni ? ni->x : x;   // the row every workgroup reads
+    if (mem_overlap(mm, xin) || mem_overlap(rp, xin) || !exact_or_disjoint(mm, rp) || mem_overlap(pos, rp) ||
         mem_overlap(pos, mm))
         return 0;
-    if (d && (mem_overlap(d, x) || mem_overlap(d, mm) || mem_overlap(d, rp))) return 0;
+    if (d && (mem_overlap(d, xin) || mem_overlap(d, mm) || mem_overlap(d, rp))) return 0;
+    if (ni && (x != ni->y || !normin_ok(ni, {mm, rp, d}))) return 0;
     const void *W = native_image(bc, a, tt);
     if (!W) return 0;
     DecArgs dd;
@@ -1228,6 +1270,7 @@ int fuse_mv_rope(BackendCtx *bc, kggml_cgraph *g, int i) {
     o.rope.D = (int)rx->ne[0];
     o.rope.theta_scale = cst[0]; o.rope.corr0 = cst[1]; o.rope.corr1 = cst[2]; o.rope.mscale_ext = cst[3];
     o.rope.freq_scale = op_f(rp, 6); o.rope.ext_factor = op_f(rp, 7); o.rope.attn_factor = op_f(rp, 8);
+    normin_args(ni, dd, o);
     if (kcpp_gemv_rs_aux(tt, &dd, 0, &o, bc->stream) != 0) {
         (void)hipGetLastError();
         return 0;
@@ -1235,10 +1278,32 @@ int fuse_mv_rope(BackendCtx *bc, kggml_cgraph *g, int i) {
     return (j ? j : k) - i + 1;
 }
 
+// RMS_NORM -> MUL(w) -> its first consumer as one launch: the consumer mat-vec (the GLU quadruple or a MUL_MAT ->
+// ROPE chain) normalises x in its prologue -- the plugin's norm kernels sum in that prologue's order for rows up to
+// 4096 (ggml_ops.hip row_sumsq16), so r, y and the consumer's result are the node sequence's bits -- and its
+// workgroup 0 stores r and y for the later consumers
+int fuse_norm_into(BackendCtx *bc, kggml_cgraph *g, int i) {
+    if (i + 2 >= g->n_nodes) return 0;
+    kggml_tensor *nn = g->nodes[i], *m = g->nodes[i + 1];
+    if (nn->op != KGGML_OP_RMS_NORM || m->op != KGGML_OP_MUL || m->src[0] != nn || !supports(nn) || !supports(m)) return 0;
+    kggml_tensor *x = nn->src[0], *w = m->src[1];
+    const int64_t K = nn->ne[0];
+    if (!x || !w || K > 4096 || K % 256 || !f32_vec(x, K) || !f32_vec(nn, K) || !f32_vec(m, K) || !f32_vec(w, K)) return 0;
+    const NormIn ni{x, w, nn, m, op_f(nn, 0), true, true};
+    if (g->nodes[i + 2]->op != KGGML_OP_MUL_MAT) return 0;
+    int k = fuse_glu(bc, g, i + 2, &ni);
+    if (!k) k = fuse_mv_rope(bc, g, i + 2, &ni);
+    if (!k && fuse_dbg()) fprintf(stderr, "[fuse] norm-in: no consumer pattern at '%s' after '%s'\n", g->nodes[i + 2]->name, nn->name);
+    return k ? k + 2 : 0;
+}
+
 // the number of nodes node i starts a fused launch for (0: none)
 int fuse_at(BackendCtx *bc, kggml_cgraph *g, int i) {
     switch (g->nodes[i]->op) {
-    case KGGML_OP_RMS_NORM: return fuse_norm_mul(bc, g, i);
+    case KGGML_OP_RMS_NORM: {
+        const int k = fuse_norm_into(bc, g, i);
+        return k ? k : fuse_norm_mul(bc, g, i);
+    }
     case KGGML_OP_ROPE: return fuse_rope_cpy(bc, g, i);
     case KGGML_OP_MUL_MAT: {
         int k = fuse_glu(bc, g, i);
@@ -1318,6 +1383,7 @@ int be_graph_compute(kggml_backend_t be, kggml_cgraph *g) {
     hipSetDevice(c->device);
     g_last_nodes = 0;
     g_last_fused = 0;
+    g_last_fused_launches = 0;
     for (int i = 0; i < g->n_nodes; ++i) {
         kggml_tensor *n = g->nodes[i];
         if (n->ne[0] == 0 || n->ne[1] == 0 || n->ne[2] == 0 || n->ne[3] == 0) continue;   // ggml_is_empty
@@ -1327,6 +1393,7 @@ int be_graph_compute(kggml_backend_t be, kggml_cgraph *g) {
             if (k) {
                 g_last_nodes += k;
                 g_last_fused += k;
+                ++g_last_fused_launches;
                 i += k - 1;
                 continue;
             }
@@ -1498,6 +1565,7 @@ void ggml_cuda_set_mul_mat_q(bool mul_mat_q) { g_mul_mat_q = mul_mat_q; }
 
 int kcpp_ggml_backend_last_nodes(void) { return g_last_nodes; }
 int kcpp_ggml_backend_last_fused(void) { return g_last_fused; }
+int kcpp_ggml_backend_last_fused_launches(void) { return g_last_fused_launches; }
 // device bytes held by separate native images (weights outside weight buffers, or asked for in two layouts); the
 // weights of a weight buffer are converted in place and hold none
 int64_t kcpp_ggml_backend_image_bytes(void) {

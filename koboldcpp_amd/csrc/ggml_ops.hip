@@ -141,6 +141,28 @@ __device__ __forceinline__ double row_sumsq(const float *xr, int64_t ne0, int64_
     return sum;
 }
 
+// rows of up to 4096 (a multiple of 16): the decode mat-vec prologue's own order (lean::ActPro, PRO 1) -- thread t
+// sums chunk t (elements 16t .. 16t + 15) in order, wave_sum_d, then ((w0 + w1) + w2) + w3 -- so a norm fused into
+// the consumer's prologue gives these kernels' bits (ggml_backend.cpp fuse_norm_into)
+__device__ __forceinline__ double row_sumsq16(const float *xr, int64_t ne0, float (&v)[16]) {
+    const int tid = threadIdx.x;
+    const bool live = tid < ne0 / 16;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) v[e] = live ? xr[16 * tid + e] : 0.0f;
+    double ss = 0.0;
+    if (live) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) ss += (double)__fmul_rn(v[e], v[e]);
+    }
+    ss = wave_sum_d(ss);
+    __shared__ double red16[4];
+    if ((tid & 63) == 0) red16[tid >> 6] = ss;
+    __syncthreads();
+    const double sum = red16[0] + red16[1] + red16[2] + red16[3];
+    __syncthreads();
+    return sum;
+}
+
 __global__ void __launch_bounds__(256) k_rms_norm_g(const char *__restrict__ x, TD tx, char *__restrict__ y, TD ty,
                                                     float eps, int64_t nrows) {
     for (int64_t r = blockIdx.x; r < nrows; r += gridDim.x) {
@@ -148,6 +170,16 @@ __global__ void __launch_bounds__(256) k_rms_norm_g(const char *__restrict__ x, 
         row3(r, tx.ne, i1, i2, i3);
         const float *xr = (const float *)(x + i1 * tx.nb[1] + i2 * tx.nb[2] + i3 * tx.nb[3]);
         float *yr = (float *)(y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
+        if (tx.ne[0] % 16 == 0 && tx.ne[0] <= 4096) {
+            float v[16];
+            const double sum = row_sumsq16(xr, tx.ne[0], v);
+            const float scale = 1.0f / sqrtf((float)(sum / (double)tx.ne[0]) + eps);
+            if (threadIdx.x < tx.ne[0] / 16) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) yr[16 * threadIdx.x + e] = __fmul_rn(v[e], scale);
+            }
+            continue;
+        }
         const double sum = row_sumsq(xr, tx.ne[0], 4);
         const float mean = (float)(sum / (double)tx.ne[0]);
         const float scale = 1.0f / sqrtf(mean + eps);
@@ -169,6 +201,27 @@ __global__ void __launch_bounds__(256) k_rms_norm_mul_g(const char *__restrict__
         float *yr = (float *)(y + i1 * ty.nb[1] + i2 * ty.nb[2] + i3 * ty.nb[3]);
         const float *wr = (const float *)(w + (i1 % tw.ne[1]) * tw.nb[1] + (i2 % tw.ne[2]) * tw.nb[2] + (i3 % tw.ne[3]) * tw.nb[3]);
         const bool wfull = tw.ne[0] == ty.ne[0];
+        if (tx.ne[0] % 16 == 0 && tx.ne[0] <= 4096) {      // the mat-vec prologue's order (row_sumsq16)
+            float v[16], wv[16];
+            const bool live = threadIdx.x < tx.ne[0] / 16;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int64_t i = 16 * threadIdx.x + e;
+                wv[e] = live ? wr[wfull ? i : i % tw.ne[0]] : 0.0f;
+            }
+            const double sum = row_sumsq16(xr, tx.ne[0], v);
+            const float scale = 1.0f / sqrtf((float)(sum / (double)tx.ne[0]) + eps);
+            if (live) {
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int64_t i = 16 * threadIdx.x + e;
+                    const float rv = __fmul_rn(v[e], scale);
+                    rr[i] = rv;
+                    yr[i] = __fmul_rn(rv, wv[e]);
+                }
+            }
+            continue;
+        }
         if (tx.ne[0] <= 256 * 16) {
             // one pass (rows up to 4096): x and w loaded once, up front; the same sums in the same order as below
             float xv[16], wv[16];

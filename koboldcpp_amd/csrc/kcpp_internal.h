@@ -87,10 +87,13 @@ struct RopeP {
     int D;
     float theta_scale, freq_scale, ext_factor, attn_factor, mscale_ext, corr0, corr1;
 };
+// yn / rn (PRO 1 launches; rn may be null): the RMS_NORM and MUL nodes in front of this, stored by workgroup 0 from
+// the prologue's normalised row (r = x * scale, y = r * w: the nodes' own bits)
 struct AuxOut {
     float *p0, *p1, *p2;
     uint16_t *h0;
     RopeP rope;
+    float *rn, *yn;
 };
 
 

@@ -816,7 +816,7 @@ def test_decode_node_fusion_matches_node_by_node(env, case):
                 a = np.ascontiguousarray(a)
                 G.ggml_backend_tensor_set(t, a.ctypes.data, 0, a.nbytes)
             assert G.ggml_backend_graph_compute(be, g) == 0, L.kcpp_ggml_backend_last_error()
-            nf = L.kcpp_ggml_backend_last_fused()
+            nf = (L.kcpp_ggml_backend_last_fused(), L.kcpp_ggml_backend_last_fused_launches())
             got = []
             for t in [out] + probe:
                 r = np.empty(G.ggml_nbytes(t) // 4, np.float32)
@@ -830,14 +830,21 @@ def test_decode_node_fusion_matches_node_by_node(env, case):
         else:
             G.ggml_backend_buffer_free(buf)
         G.ggml_free(ctx)
-    (nf1, a), (nf0, b) = runs
+    ((nf1, nl1), a), ((nf0, nl0), b) = runs
     L.kcpp_rs_supported.argtypes = [I, I64]
     rs = [bool(L.kcpp_rs_supported(t, k)) for t, (k, n) in zip(tys, shapes)]      # ggml type ids = KT_ codes
     # 2 norms (+ MUL); on RS layouts q's MUL_MAT + RESHAPE + ROPE, k's MUL_MAT + RESHAPE + ROPE + VIEW + CPY into the
     # cache (otherwise its ROPE + VIEW + CPY), v's MUL_MAT + VIEW + CPY, wo + ADD, the GLU quadruple, down + ADD
     want = 2 * 2 + 3 * rs[0] + (5 if rs[1] else 3) + 3 * rs[2] + 2 * rs[3] + 4 * rs[4] + 2 * rs[6]
-    print("%s: %d nodes fused of %d (expected %d)" % (name, nf1, len(nodes), want))
+    # launches: the attention norm inside k's chain (RS k; otherwise its own launch and k's ROPE + CPY), q's chain, v,
+    # wo + ADD, the ffn norm inside the GLU (RS gate / up; otherwise its own launch), down + ADD
+    want_l = (1 if rs[1] else 2) + rs[0] + rs[2] + rs[3] + 1 + rs[6]
+    print("%s: %d nodes fused of %d in %d launches (expected %d in %d)" % (name, nf1, len(nodes), nl1, want, want_l))
     assert nf0 == 0 and nf1 == want, (nf1, want)
+    # (under ggml_gallocr the norm weights are graph tensors whose bytes the allocator may hand to a mat-vec output
+    # once the MUL has read them; a norm fused into that mat-vec's prologue would race with it, so the norm then runs
+    # as its own launch -- llama.cpp keeps the weights in their own buffer)
+    assert nl1 == want_l if alloc == "ctx" else want_l <= nl1 <= want_l + 2, (nl1, want_l)
     assert rs[4] == (wt != R.Q8_0)
     for i, (u, w_) in enumerate(zip(a, b)):
         assert np.array_equal(u.view(np.uint32), w_.view(np.uint32)), (i, rel(u, w_))
