@@ -1289,6 +1289,8 @@ int fuse_norm_into(BackendCtx *bc, kggml_cgraph *g, int i) {
     kggml_tensor *x = nn->src[0], *w = m->src[1];
     const int64_t K = nn->ne[0];
     if (!x || !w || K > 4096 || K % 256 || !f32_vec(x, K) || !f32_vec(nn, K) || !f32_vec(m, K) || !f32_vec(w, K)) return 0;
+    for (const kggml_tensor *t : {x, w, nn, m})     // the prologue moves 16 B per access
+        if ((uintptr_t)t->data % 16) return 0;
     const NormIn ni{x, w, nn, m, op_f(nn, 0), true, true};
     if (g->nodes[i + 2]->op != KGGML_OP_MUL_MAT) return 0;
     int k = fuse_glu(bc, g, i + 2, &ni);
