@@ -933,7 +933,7 @@ bool compute_node(BackendCtx *bc, kggml_tensor *n) {
         const int tt = matmul_layout(a->type, K);
         const void *W = native_image(bc, a, tt);
         if (!W) return set_err("mul_mat: native image allocation failed");
-        if (M == 1 && b->nb[0] == 4 && !bc->no_fused_mv) {
+        if (M == 1 && b->nb[0] == 4 && (uintptr_t)b->data % 16 == 0 && !bc->no_fused_mv) {
             // one token (decode): the fused single-token mat-vec quantizes src1 in its own prologue (the same Q8_K /
             // Q8_0 bytes as kcpp_quantize_act) -- one launch per MUL_MAT instead of two; -3: type without it
             DecArgs d;
@@ -1021,7 +1021,8 @@ bool same_shape(const kggml_tensor *a, const kggml_tensor *b) {
 bool mv_node(const kggml_tensor *m) {
     const kggml_tensor *a = m->src[0], *b = m->src[1];
     return m->op == KGGML_OP_MUL_MAT && supports(m) && a && b && is_quantized(a->type) &&
-           !(a->buffer && buffer_is_split(a->buffer)) && f32_vec(m, a->ne[1]) && f32_vec(b, a->ne[0]) && a->data;
+           !(a->buffer && buffer_is_split(a->buffer)) && f32_vec(m, a->ne[1]) && f32_vec(b, a->ne[0]) && a->data &&
+           (uintptr_t)b->data % 16 == 0;          // the quantize prologue reads the row 16 B at a time
 }
 
 // RMS_NORM -> MUL(norm, w): kcpp_ggml_rms_norm_mul writes the norm row, then the product row
